@@ -1,0 +1,266 @@
+/*
+ * pt_api.h — C ABI of the MI355X wavefront path tracer (libpt_hip.so).
+ *
+ * This is the drop-in boundary for the reference's per-sample loop
+ * (marko176/PathTracing).  The reference's `Integrator` interface
+ * (Integrators.hpp:10-23: Render(threadCount), Li(Ray)) sits on top of it: a
+ * host-side `HipPathIntegrator` flattens the already-built Scene (TLAS4/BLAS4
+ * cluster arrays BVH.hpp:1214-1216, primitives, materials, lights, light
+ * sampler, camera, film filter) into a pt_scene_desc once, then every
+ * Render() becomes one pt_render().  Scene build, model loading and image
+ * output stay on the host.  See INTEGRATION.md.
+ *
+ * Plain pointers and sizes only; no C++ or torch types.  Every call returns a
+ * pt_status (0 = OK, < 0 = error, message via pt_last_error); nothing aborts.
+ * All host arrays are read during the call and copied to device memory; no
+ * pointer is retained after return.
+ */
+#ifndef PT_API_H
+#define PT_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_API_VERSION 1
+
+typedef int32_t pt_status;
+#define PT_OK 0
+#define PT_ERR_ARG (-1)     /* invalid argument / inconsistent scene       */
+#define PT_ERR_HIP (-2)     /* HIP runtime error                            */
+#define PT_ERR_OOM (-3)     /* device allocation failed                     */
+#define PT_ERR_STATE (-4)   /* call order (e.g. render before upload)       */
+#define PT_ERR_NODEV (-5)   /* no HIP device                                */
+
+/* ------------------------------------------------------------------------ */
+/* Reference-form BVH4 (BVH.hpp:38-60), byte-identical to BVH4_NODE /        */
+/* BVH4_CLUSTER.  pt_bvh4_build reproduces BVHBase::BuildBaseThreaded        */
+/* (BVH.hpp:290-390) + BVH4::buildBVH4 (788-1017).                            */
+/* ------------------------------------------------------------------------ */
+typedef struct pt_ref_bvh4_node {
+    uint8_t count;        /* leaf: primitive count (u8, as the reference)     */
+    uint8_t active;       /* 0 => leaf                                        */
+    uint8_t perm;         /* topology/axis code, index into the octant LUT    */
+    uint8_t pad;
+    uint32_t cluster_idx; /* leaf: first primitive, else cluster index        */
+} pt_ref_bvh4_node;
+
+typedef struct pt_ref_bvh4_cluster {
+    float xmin[4], xmax[4];
+    float ymin[4], ymax[4];
+    float zmin[4], zmax[4];
+    pt_ref_bvh4_node children[4];
+} pt_ref_bvh4_cluster; /* 128 bytes */
+
+/* boxes: n x {minx,miny,minz,maxx,maxy,maxz}.  clusters must hold >= max(n,1)
+ * entries.  prim_order[i] = input index of the i-th primitive in leaf order.
+ * bbox (optional, 6 floats) receives the root box. */
+pt_status pt_bvh4_build(const float* boxes, uint32_t n, pt_ref_bvh4_cluster* clusters, uint32_t* n_clusters,
+                        pt_ref_bvh4_node* root, uint32_t* prim_order, float* bbox);
+
+/* The octant traversal order byte for (ray-sign octant, perm) exactly as
+ * BVH4::LUT / PermToIndexLUT (BVH.hpp:10-24, 562-718): 2-bit child slots,
+ * most significant = nearest.  out: 8*135 bytes. */
+pt_status pt_bvh4_order_table(uint8_t* out);
+
+/* ------------------------------------------------------------------------ */
+/* Flat scene                                                                */
+/* ------------------------------------------------------------------------ */
+enum { PT_PRIM_TRIANGLE = 0, PT_PRIM_QUAD = 1, PT_PRIM_SPHERE = 2, PT_PRIM_BLAS = 3 };
+
+/* One GeometricPrimitive (Primitive.hpp:17-31) or a nested BLAS (a Model,
+ * Model.hpp:25-31), indexed by its global leaf-order slot. */
+typedef struct pt_prim {
+    uint32_t kind;     /* PT_PRIM_*                                              */
+    uint32_t index;    /* TRIANGLE: triangle id; QUAD: quad id; SPHERE: sphere id;
+                          BLAS: index into pt_scene_desc.bvhs                    */
+    int32_t material;  /* -1 = none: medium boundary, rays pass through         */
+    int32_t light;     /* area light id or -1                                    */
+    int32_t medium;    /* medium id or -1 (carried, unused by Path/SimplePath)   */
+} pt_prim;
+
+typedef struct pt_bvh_desc {
+    const pt_ref_bvh4_cluster* clusters;
+    uint32_t n_clusters;
+    pt_ref_bvh4_node root;
+    uint32_t prim_base;  /* global slot of this BVH's primitive 0 (leaf order) */
+    uint32_t n_prims;
+} pt_bvh_desc;
+
+/* QuadShape (Shape.hpp:118-171) with its ctor-derived fields. */
+typedef struct pt_quad {
+    float Q[3], u[3], v[3], normal[3], D, w[3];
+} pt_quad;
+
+typedef struct pt_sphere {
+    float center[3], radius;
+} pt_sphere;
+
+enum { PT_TEX_SOLID = 0, PT_TEX_IMAGE = 1, PT_TEX_CHECKER = 2 };
+/* SolidColor / ImageTexture / CheckerTexture (Texture.hpp:122-213). */
+typedef struct pt_texture {
+    uint32_t kind;
+    float scale[3];      /* colorScale                                     */
+    float value[3];      /* SOLID: albedo                                  */
+    int32_t a, b;        /* CHECKER: children                              */
+    float inv_scale[2];  /* CHECKER: 1/uvscale                             */
+    int32_t image;       /* IMAGE: image id                                */
+} pt_texture;
+
+typedef struct pt_image {
+    uint64_t offset;     /* byte offset into pt_scene_desc.texels          */
+    int32_t width, height, channels;
+    int32_t pad;
+} pt_image;
+
+enum { PT_MAT_DIFFUSE = 0, PT_MAT_DIELECTRIC = 1, PT_MAT_THIN = 2, PT_MAT_CONDUCTOR = 3 };
+enum { PT_ALPHA_OPAQUE = 0, PT_ALPHA_BLEND = 1, PT_ALPHA_MASK = 2 };
+/* MicrofacetDiffuse / MicrofacetDielectric / ThinDielectric / SpecularConductor
+ * (Material.hpp:200-673).  Texture ids -1 = absent. */
+typedef struct pt_material {
+    uint32_t kind;
+    int32_t tex, norm, rough, metal, alpha;
+    uint32_t alpha_mode; /* effective AlphaTester mode (Material.hpp:176-198) */
+    float alpha_cutoff;
+    float ri;            /* DIELECTRIC / THIN                               */
+    float albedo[3];     /* CONDUCTOR                                       */
+} pt_material;
+
+enum { PT_LIGHT_AREA = 0, PT_LIGHT_UNIFORM_INF = 1, PT_LIGHT_SKY_INF = 2, PT_LIGHT_DISTANT = 3, PT_LIGHT_POINT = 4 };
+/* AreaLight / UniformInfiniteLight / FunctionInfiniteLight (sky gradient of
+ * main.cpp:292-295, parameterised) / DistantLight / PointLight (Light.cpp). */
+typedef struct pt_light {
+    uint32_t kind;
+    int32_t prim;        /* AREA: global prim slot of its shape             */
+    int32_t tex;         /* AREA: emissive texture                          */
+    uint32_t one_sided;
+    float power;         /* Light::Power() after PreProcess                 */
+    float pmf;           /* LightSampler::PMF(light)                        */
+    float color[3];      /* UNIFORM/DISTANT/POINT colour; SKY: horizon c0   */
+    float vec[3];        /* DISTANT dir; POINT position; SKY: zenith c1     */
+    float scale;         /* SKY scale                                       */
+} pt_light;
+
+enum { PT_LS_UNIFORM = 0, PT_LS_POWER = 1 };
+
+typedef struct pt_scene_desc {
+    /* triangle meshes, global arrays */
+    const float* positions;      /* 3 * n_vertices */
+    const float* normals;        /* 3 * n_vertices */
+    const float* uvs;            /* 2 * n_vertices */
+    const float* tangents;       /* 3 * n_vertices (zeros where a mesh has none) */
+    uint32_t n_vertices;
+    const uint32_t* tri_vidx;    /* 3 * n_triangles */
+    const uint32_t* tri_flags;   /* n_triangles: bit0 = mesh has tangents */
+    uint32_t n_triangles;
+    const pt_quad* quads;
+    uint32_t n_quads;
+    const pt_sphere* spheres;
+    uint32_t n_spheres;
+    /* primitives in global leaf-order slots; bvhs[0] is the TLAS */
+    const pt_prim* prims;
+    uint32_t n_prims;
+    const pt_bvh_desc* bvhs;
+    uint32_t n_bvhs;
+    /* appearance */
+    const pt_material* materials;
+    uint32_t n_materials;
+    const pt_texture* textures;
+    uint32_t n_textures;
+    const pt_image* images;
+    uint32_t n_images;
+    const uint8_t* texels;
+    uint64_t n_texel_bytes;
+    /* lights */
+    const pt_light* lights;
+    uint32_t n_lights;
+    uint32_t light_sampler;          /* PT_LS_*                                 */
+    const uint32_t* sampler_lights;  /* lights the sampler draws from, in order */
+    uint32_t n_sampler_lights;
+    const uint32_t* infinite_lights; /* Scene::infiniteLights, in order         */
+    uint32_t n_infinite_lights;
+} pt_scene_desc;
+
+/* Camera (Camera.hpp:7-35) after its ctor. */
+typedef struct pt_camera_desc {
+    float origin[3];
+    float u[3], v[3], w[3];
+    float half_width, half_height;
+    float defocus_radius, focus_distance, focus_angle;
+    int32_t width, height;
+} pt_camera_desc;
+
+enum { PT_INTEGRATOR_PATH = 0, PT_INTEGRATOR_SIMPLE = 1 };
+enum { PT_FILTER_MITCHELL = 0, PT_FILTER_BOX = 1, PT_FILTER_GAUSSIAN = 2 };
+#define PT_RENDER_COUNT_NODES 0x1u  /* instrumented traversal: node/tri counts */
+#define PT_RENDER_TIMING 0x2u       /* per-kernel HIP-event timing into stats   */
+
+typedef struct pt_render_desc {
+    uint32_t integrator;       /* PT_INTEGRATOR_*                               */
+    uint32_t spp;              /* samples per pixel of the whole frame          */
+    uint32_t max_depth;
+    uint32_t seed;             /* sample-stream base seed                       */
+    uint32_t filter;           /* PT_FILTER_*                                   */
+    float filter_radius[2];
+    double filter_params[2];   /* Mitchell b,c | Gaussian sigma                  */
+    uint32_t shard_index;      /* this call renders samples s with             */
+    uint32_t shard_count;      /*   s % shard_count == shard_index              */
+    uint32_t flags;            /* PT_RENDER_*                                   */
+    uint32_t paths_in_flight;  /* wavefront size; 0 = library default           */
+    uint32_t pixel_begin;      /* render pixels [pixel_begin, pixel_end) only;  */
+    uint32_t pixel_end;        /*   0,0 = whole film                            */
+} pt_render_desc;
+
+typedef struct pt_stats {
+    uint64_t paths;            /* camera samples traced                         */
+    uint64_t rays_closest;     /* Scene::Intersect calls                        */
+    uint64_t rays_any;         /* Scene::IntersectPred calls                    */
+    uint64_t nodes_closest, tris_closest, nodes_any, tris_any; /* COUNT_NODES   */
+    uint64_t shade_hits;       /* closest hits shaded                           */
+    double ms_total;           /* host wall time of pt_render                   */
+    double ms_closest;         /* TIMING: summed closest-hit kernel time        */
+    double ms_any;             /* TIMING: summed any-hit kernel time            */
+    double ms_shade;           /* TIMING: summed shade kernel time              */
+    uint64_t launches_closest;
+    uint64_t launches_any;
+} pt_stats;
+
+/* Rays for the pt_trace test hook (Scene::Intersect / IntersectPred). */
+typedef struct pt_ray {
+    float o[3], d[3], tmax;
+} pt_ray;
+
+typedef struct pt_hit {
+    float t, b1, b2;           /* t; barycentrics (tri) or quad alpha/beta     */
+    int32_t prim;              /* global slot or -1 (any-hit: 1/0 in prim)     */
+} pt_hit;
+
+typedef struct pt_ctx pt_ctx;
+
+int pt_version(void);
+pt_status pt_create(pt_ctx** ctx, int device);
+void pt_destroy(pt_ctx* ctx);
+const char* pt_last_error(const pt_ctx* ctx);   /* ctx may be NULL          */
+pt_status pt_set_stream(pt_ctx* ctx, void* hip_stream); /* NULL = ctx stream */
+pt_status pt_scene_upload(pt_ctx* ctx, const pt_scene_desc* scene);
+/* Accumulates W*H*4 doubles {sum R*w, sum G*w, sum B*w, sum w} (Film.hpp:227-253)
+ * into film_accum, a host or a device pointer (detected). */
+pt_status pt_render(pt_ctx* ctx, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_accum,
+                    pt_stats* stats);
+/* Per-sample radiance of pixels [pixel_begin, pixel_end) (0,0 = all), samples
+ * [0, spp): out_L[((pix - pixel_begin) * spp + s) * 3] (host pointer).  The
+ * unfiltered Integrator::Li values behind pt_render; for parity tests. */
+pt_status pt_render_samples(pt_ctx* ctx, const pt_camera_desc* cam, const pt_render_desc* rd, float* out_L,
+                            pt_stats* stats);
+/* Test hook: rays and hits are host or device pointers (detected). */
+pt_status pt_trace(pt_ctx* ctx, const pt_ray* rays, uint32_t n, int any_hit, pt_hit* hits, pt_stats* stats);
+/* Device bytes held by the uploaded scene. */
+uint64_t pt_scene_device_bytes(const pt_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PT_API_H */

@@ -1,0 +1,1531 @@
+/*
+ * pt_oracle.c — TEST INFRASTRUCTURE ONLY (see pt_oracle.h).
+ *
+ * A scalar C restatement of marko176/PathTracing's per-sample hot path over
+ * the flat scene of include/pt_api.h.  Each function cites the reference
+ * file:line it follows.  Float expressions keep the reference's operand order;
+ * the build uses -ffp-contract=fast like the reference's GCC gnu++20 build.
+ */
+#define _GNU_SOURCE
+#include "pt_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define EPS_SHADOW 0.00001f /* shadowEpsilon (AABB.hpp:6) */
+#define FLT_EPS 1.19209290e-07f
+#define PI_F 3.14159265358979323846f
+#define INV_PI_F 0.318309886183790671538f
+
+int oracle_version(void) { return 1; }
+
+/* ------------------------------------------------------------------ vec3 */
+typedef struct { float x, y, z; } v3;
+static inline v3 V(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static inline v3 vl(const float* p) { return V(p[0], p[1], p[2]); }
+static inline v3 add(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline v3 sub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline v3 mul(v3 a, v3 b) { return V(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline v3 muls(v3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
+static inline v3 smul(float s, v3 a) { return V(s * a.x, s * a.y, s * a.z); }
+static inline v3 divs(v3 a, float s) { return V(a.x / s, a.y / s, a.z / s); }
+static inline v3 neg(v3 a) { return V(-a.x, -a.y, -a.z); }
+/* glm::dot: tmp = a*b; tmp.x + tmp.y + tmp.z (func_geometric.inl) */
+static inline float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline v3 cross(v3 a, v3 b) {
+    return V(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
+}
+static inline float length3(v3 a) { return sqrtf(dot(a, a)); }
+/* glm::normalize = v * inversesqrt(dot(v,v)), inversesqrt = 1/sqrt */
+static inline v3 normalize(v3 a) { return muls(a, 1.0f / sqrtf(dot(a, a))); }
+static inline int is_zero(v3 a) { return a.x == 0.0f && a.y == 0.0f && a.z == 0.0f; }
+static inline v3 reflect(v3 I, v3 N) { return sub(I, muls(muls(N, dot(N, I)), 2.0f)); }
+static inline v3 refract(v3 I, v3 N, float eta) {
+    float d = dot(N, I);
+    float k = 1.0f - eta * eta * (1.0f - d * d);
+    if (k >= 0.0f) return sub(smul(eta, I), smul(eta * d + sqrtf(k), N));
+    return V(0, 0, 0);
+}
+static inline float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+static inline float fmaxf_(float a, float b) { return a < b ? b : a; } /* std::max */
+
+/* ------------------------------------------------------------------ RNG */
+/* The sample stream (DESIGN.md "Sample stream"): PCG-RXS-M-XS hash. */
+static inline uint32_t pcg_hash(uint32_t v) {
+    uint32_t state = v * 747796405u + 2891336453u;
+    uint32_t word = ((state >> ((state >> 28u) + 4u)) ^ state) * 277803737u;
+    return (word >> 22u) ^ word;
+}
+static inline uint32_t stream_key(uint32_t seed, uint32_t pixel, uint32_t sample) {
+    return pcg_hash(pcg_hash(seed ^ pcg_hash(pixel)) + sample);
+}
+typedef struct { uint32_t key, dim; } rng_t;
+static inline float next1(rng_t* r) {
+    return (float)(pcg_hash(r->key + 0x9E3779B9u * r->dim++) >> 8) * (1.0f / 16777216.0f);
+}
+/* Alpha Blend draws random_float() (Material.hpp:189) from a nondeterministic
+ * thread-local generator; parity is waived there: we draw a hash of the ray. */
+static inline uint32_t fbits(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return u;
+}
+static inline float blend_random(v3 o, v3 d, int prim) {
+    uint32_t h = pcg_hash(fbits(o.x) ^ pcg_hash(fbits(d.y) ^ pcg_hash((uint32_t)prim)));
+    return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+
+/* ------------------------------------------------------------------ ray / interaction */
+typedef struct { v3 o, inv, d; } ray_t;
+static inline ray_t mkray(v3 o, v3 d) {
+    /* Ray ctor (Ray.hpp:32-35) */
+    ray_t r;
+    r.o = o;
+    r.d = d;
+    r.inv.x = fabsf(d.x) < 1e-32f ? 1e32f : 1.0f / d.x;
+    r.inv.y = fabsf(d.y) < 1e-32f ? 1e32f : 1.0f / d.y;
+    r.inv.z = fabsf(d.z) < 1e-32f ? 1e32f : 1.0f / d.z;
+    return r;
+}
+static inline v3 at(const ray_t* r, float t) { return add(r->o, smul(t, r->d)); }
+
+typedef struct {
+    v3 p, n, ns, tangent;
+    float uv[2], t;
+    int prim, mat, light, medium;
+} si_t;
+
+/* ------------------------------------------------------------------ scene view */
+typedef struct {
+    const pt_scene_desc* s;
+    uint8_t lut[8][135];
+} scene_t;
+
+/* BVH4::LUT (BVH.hpp:562-718) composed with PermToIndexLUT (10-17): the
+ * permutation byte P(a,b,c,d), a = child visited first. */
+static int is_perm(unsigned p) {
+    unsigned seen = 0;
+    for (int s = 0; s < 4; s++) seen |= 1u << ((p >> (2 * s)) & 3);
+    return p < 256 && seen == 0xF;
+}
+static void build_lut(uint8_t lut[8][135]) {
+    for (unsigned rs = 0; rs < 8; rs++) {
+        unsigned sg[3] = {rs & 1u, (rs >> 1) & 1u, rs >> 2};
+        for (unsigned code = 0; code < 135; code++) {
+            unsigned topo = code / 27, rem = code % 27;
+            unsigned s0 = rem % 3, s1 = (rem / 3) % 3, s2 = rem / 9;
+            unsigned p = 0, l, r, sub;
+            switch (topo) {
+                case 0:
+                    l = sg[s1] ? 4u : 1u;
+                    r = sg[s2] ? 14u : 11u;
+                    p = sg[s0] ? (r << 4) + l : (l << 4) + r;
+                    break;
+                case 1:
+                    r = sg[s2] ? 14u : 11u;
+                    sub = sg[s1] ? (r << 2) | 1u : (1u << 4) | r;
+                    p = sg[s0] ? (sub << 2) : sub;
+                    break;
+                case 2:
+                    l = sg[s2] ? 9u : 6u;
+                    sub = sg[s1] ? (3u << 4) | l : (l << 2) | 3u;
+                    p = sg[s0] ? (sub << 2) : sub;
+                    break;
+                case 3:
+                    l = sg[s2] ? 4u : 1u;
+                    sub = sg[s1] ? (2u << 4) | l : (l << 2) | 2u;
+                    p = sg[s0] ? (3u << 6) | sub : (sub << 2) | 3u;
+                    break;
+                default:
+                    l = sg[s2] ? 9u : 6u;
+                    sub = sg[s1] ? (l << 2) : l;
+                    p = sg[s0] ? (3u << 6) | sub : (sub << 2) | 3u;
+                    break;
+            }
+            lut[rs][code] = is_perm(p) ? (uint8_t)p : 27u; /* 27 = P(0,1,2,3) */
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ textures (Texture.hpp) */
+static inline int wrap_index(int i, int n) {
+    int m = i % n;
+    if (m < 0) m += n;
+    return m;
+}
+static inline float channel_at(const scene_t* S, const pt_image* im, int x, int y, int ch) {
+    /* Image::GetChannelAt (Texture.hpp:43-48): reads byte ch-1 of the pixel
+     * whatever the channel count. */
+    int xi = wrap_index(x, im->width), yi = wrap_index(y, im->height);
+    uint64_t idx = im->offset + ((uint64_t)yi * (uint64_t)im->width + (uint64_t)xi) * (uint64_t)im->channels +
+                   (uint64_t)(ch - 1);
+    if (idx >= S->s->n_texel_bytes) return 0.0f;
+    return S->s->texels[idx] / 255.0f;
+}
+static v3 tex_eval(const scene_t* S, int id, const float uv[2]) {
+    const pt_texture* t = &S->s->textures[id];
+    if (t->kind == PT_TEX_SOLID) return vl(t->value); /* colorScale*albedo, precomputed */
+    if (t->kind == PT_TEX_CHECKER) {
+        /* Texture.hpp:203-207 */
+        int ux = (int)floorf(uv[0] * t->inv_scale[0]);
+        int uy = (int)floorf(uv[1] * t->inv_scale[1]);
+        v3 c = ((ux + uy) % 2 == 0) ? tex_eval(S, t->a, uv) : tex_eval(S, t->b, uv);
+        return mul(vl(t->scale), c);
+    }
+    /* ImageTexture::Evaluate (Texture.hpp:143-158) */
+    const pt_image* im = &S->s->images[t->image];
+    float x = uv[0] * im->width - 0.5f;
+    float y = uv[1] * im->height - 0.5f;
+    int xi = (int)floorf(x), yi = (int)floorf(y);
+    float dx = x - xi, dy = y - yi;
+    v3 a = V(channel_at(S, im, xi, yi, 1), channel_at(S, im, xi, yi, 2), channel_at(S, im, xi, yi, 3));
+    v3 b = V(channel_at(S, im, xi + 1, yi, 1), channel_at(S, im, xi + 1, yi, 2), channel_at(S, im, xi + 1, yi, 3));
+    v3 c = V(channel_at(S, im, xi, yi + 1, 1), channel_at(S, im, xi, yi + 1, 2), channel_at(S, im, xi, yi + 1, 3));
+    v3 d = V(channel_at(S, im, xi + 1, yi + 1, 1), channel_at(S, im, xi + 1, yi + 1, 2),
+             channel_at(S, im, xi + 1, yi + 1, 3));
+    v3 r = add(add(add(smul((1 - dx) * (1 - dy), a), smul(dx * (1 - dy), b)), smul((1 - dx) * dy, c)),
+               smul(dx * dy, d));
+    return mul(vl(t->scale), r);
+}
+static float tex_alpha(const scene_t* S, int id, const float uv[2]) {
+    const pt_texture* t = &S->s->textures[id];
+    if (t->kind == PT_TEX_SOLID) return 1.0f;
+    if (t->kind == PT_TEX_CHECKER) {
+        /* Texture.cpp:41-45 */
+        int ux = (int)floorf(uv[0] * t->inv_scale[0]);
+        int uy = (int)floorf(uv[1] * t->inv_scale[1]);
+        return ((ux + uy) % 2 == 0) ? tex_alpha(S, t->a, uv) : tex_alpha(S, t->b, uv);
+    }
+    /* ImageTexture::alpha (Texture.cpp:47-62) */
+    const pt_image* im = &S->s->images[t->image];
+    if (im->channels != 4) return 1.0f;
+    float x = uv[0] * im->width - 0.5f;
+    float y = uv[1] * im->height - 0.5f;
+    int xi = (int)floorf(x), yi = (int)floorf(y);
+    float dx = x - xi, dy = y - yi;
+    float a = channel_at(S, im, xi, yi, 4), b = channel_at(S, im, xi + 1, yi, 4);
+    float c = channel_at(S, im, xi, yi + 1, 4), d = channel_at(S, im, xi + 1, yi + 1, 4);
+    return (1 - dx) * (1 - dy) * a + dx * (1 - dy) * b + (1 - dx) * dy * c + dx * dy * d;
+}
+
+/* Material::Alpha (Material.hpp:336-342, 572-578); base Material: true. */
+static int mat_alpha(const scene_t* S, int mid, const float uv[2], v3 ro, v3 rd, int prim) {
+    if (mid < 0) return 1;
+    const pt_material* m = &S->s->materials[mid];
+    if (m->kind != PT_MAT_DIFFUSE && m->kind != PT_MAT_DIELECTRIC) return 1;
+    float a;
+    if (m->alpha >= 0) a = tex_eval(S, m->alpha, uv).x;
+    else a = tex_alpha(S, m->tex, uv);
+    switch (m->alpha_mode) {
+        case PT_ALPHA_OPAQUE: return 1;
+        case PT_ALPHA_MASK: return a > m->alpha_cutoff;
+        default: return a >= 1.0f ? 1 : (blend_random(ro, rd, prim) < a);
+    }
+}
+static inline int mat_has_alpha(const scene_t* S, int mid) {
+    if (mid < 0) return 0;
+    const pt_material* m = &S->s->materials[mid];
+    if (m->kind != PT_MAT_DIFFUSE && m->kind != PT_MAT_DIELECTRIC) return 0;
+    return m->alpha_mode != PT_ALPHA_OPAQUE;
+}
+
+/* ------------------------------------------------------------------ onb (Onb.hpp) */
+typedef struct { v3 a0, a1, a2; } onb_t;
+static inline onb_t onb_n(v3 n) {
+    onb_t b;
+    b.a2 = n;
+    v3 up = (fabsf(n.x) > 0.9999) ? V(0, 1, 0) : V(1, 0, 0);
+    b.a1 = normalize(cross(b.a2, up));
+    b.a0 = cross(b.a1, b.a2);
+    return b;
+}
+static inline onb_t onb_si(const si_t* si) {
+    onb_t b;
+    b.a2 = si->ns;
+    b.a0 = si->tangent;
+    b.a1 = cross(b.a2, b.a0);
+    return b;
+}
+static inline v3 to_world(const onb_t* b, v3 v) {
+    return add(add(smul(v.x, b->a0), smul(v.y, b->a1)), smul(v.z, b->a2));
+}
+static inline v3 to_local(const onb_t* b, v3 v) { return V(dot(v, b->a0), dot(v, b->a1), dot(v, b->a2)); }
+
+/* sample_normalMap (Material.hpp:344-348, 580-584) */
+static v3 normal_map(const scene_t* S, int mid, const si_t* si) {
+    if (mid < 0) return si->ns;
+    const pt_material* m = &S->s->materials[mid];
+    if ((m->kind != PT_MAT_DIFFUSE && m->kind != PT_MAT_DIELECTRIC) || m->norm < 0) return si->ns;
+    v3 t = tex_eval(S, m->norm, si->uv);
+    v3 nn = normalize(sub(smul(2.0f, t), V(1, 1, 1)));
+    onb_t b = onb_si(si);
+    return to_world(&b, nn);
+}
+
+/* ------------------------------------------------------------------ shapes (Shape.cpp) */
+static void sphere_uv(v3 p, float uv[2]) {
+    /* SphereShape::GetSphereUV (Shape.hpp:35-43) */
+    p = normalize(p);
+    float theta = acosf(clampf(p.y, -1.0f, 1.0f));
+    float phi = atan2f(p.z, p.x);
+    if (phi < 0) phi += 2.0f * PI_F;
+    uv[0] = INV_PI_F * phi * 0.5f;
+    uv[1] = INV_PI_F * theta;
+}
+
+/* glm::intersectRayTriangle (glm/gtx/intersect.inl:29-94) */
+static int tri_glm(v3 o, v3 d, v3 v0, v3 e1, v3 e2, float* bx, float* by, float* t) {
+    v3 p = cross(d, e2);
+    float det = dot(e1, p);
+    v3 perp;
+    if (det > 0.0f) {
+        v3 dist = sub(o, v0);
+        *bx = dot(dist, p);
+        if (*bx < 0.0f || *bx > det) return 0;
+        perp = cross(dist, e1);
+        *by = dot(d, perp);
+        if (*by < 0.0f || *bx + *by > det) return 0;
+    } else if (det < 0.0f) {
+        v3 dist = sub(o, v0);
+        *bx = dot(dist, p);
+        if (*bx > 0.0f || *bx < det) return 0;
+        perp = cross(dist, e1);
+        *by = dot(d, perp);
+        if (*by > 0.0f || *bx + *by < det) return 0;
+    } else {
+        return 0;
+    }
+    float inv = 1.0f / det;
+    *t = dot(e2, perp) * inv;
+    *bx *= inv;
+    *by *= inv;
+    return 1;
+}
+
+typedef struct { v3 v0, v1, v2; uint32_t i0, i1, i2; } tri_t;
+static inline tri_t tri_get(const scene_t* S, uint32_t tri) {
+    tri_t T;
+    T.i0 = S->s->tri_vidx[3 * tri + 0];
+    T.i1 = S->s->tri_vidx[3 * tri + 1];
+    T.i2 = S->s->tri_vidx[3 * tri + 2];
+    T.v0 = vl(S->s->positions + 3 * T.i0);
+    T.v1 = vl(S->s->positions + 3 * T.i1);
+    T.v2 = vl(S->s->positions + 3 * T.i2);
+    return T;
+}
+
+/* TriangleShape::Intersect (Shape.cpp:185-245). Returns hit; fills si. */
+static int tri_intersect(const scene_t* S, uint32_t tri, int mid, const ray_t* r, float max, si_t* si) {
+    tri_t T = tri_get(S, tri);
+    float bx, by, t = INFINITY;
+    int hit = tri_glm(r->o, r->d, T.v0, sub(T.v1, T.v0), sub(T.v2, T.v0), &bx, &by, &t);
+    if (!hit || t > max || t < EPS_SHADOW) return 0;
+    float u = bx, v = by, w = 1.0f - u - v;
+    const float* uvs = S->s->uvs;
+    const float* nr = S->s->normals;
+    si->uv[0] = u * uvs[2 * T.i1] + v * uvs[2 * T.i2] + w * uvs[2 * T.i0];
+    si->uv[1] = u * uvs[2 * T.i1 + 1] + v * uvs[2 * T.i2 + 1] + w * uvs[2 * T.i0 + 1];
+    v3 nn = normalize(add(add(smul(u, vl(nr + 3 * T.i1)), smul(v, vl(nr + 3 * T.i2))), smul(w, vl(nr + 3 * T.i0))));
+    v3 e1 = sub(T.v1, T.v0), e2 = sub(T.v2, T.v0);
+    v3 N = normalize(cross(e1, e2));
+    si->n = N;
+    if (dot(N, nn) < 0) nn = neg(nn);
+    si->t = t;
+    si->ns = nn;
+    si->p = add(at(r, t), muls(smul(EPS_SHADOW, N), dot(r->d, N) > 0.0f ? -1.0f : 1.0f));
+    if (S->s->tri_flags[tri] & 1u) {
+        const float* tg = S->s->tangents;
+        v3 tv = add(add(smul(u, vl(tg + 3 * T.i1)), smul(v, vl(tg + 3 * T.i2))), smul(w, vl(tg + 3 * T.i0)));
+        si->tangent = normalize(sub(tv, smul(dot(si->ns, tv), si->ns)));
+    } else {
+        v3 up = (fabsf(si->ns.x) > 0.9999f) ? V(0, 1, 0) : V(1, 0, 0);
+        si->tangent = normalize(cross(up, si->ns));
+    }
+    si->ns = normal_map(S, mid, si);
+    return 1;
+}
+
+/* TriangleShape::IntersectPred (Shape.cpp:246-268) */
+static int tri_pred(const scene_t* S, uint32_t tri, const ray_t* r, float max) {
+    tri_t T = tri_get(S, tri);
+    v3 edge1 = sub(T.v1, T.v0), edge2 = sub(T.v2, T.v0);
+    v3 h = cross(r->d, edge2);
+    float det = dot(edge1, h);
+    if (det > -FLT_EPS && det < FLT_EPS) return 0;
+    float inv = 1.0f / det;
+    v3 s = sub(r->o, T.v0);
+    float u = dot(s, h) * inv;
+    if (u < 0 || u > 1) return 0;
+    v3 q = cross(s, edge1);
+    float v = dot(r->d, q) * inv;
+    if (v < 0 || u + v > 1) return 0;
+    float t = dot(edge2, q) * inv;
+    return t <= max && t >= EPS_SHADOW;
+}
+
+/* QuadShape::Intersect / IntersectPred (Shape.cpp:320-359) */
+static int quad_hit(const pt_quad* q, const ray_t* r, float max, float* t_out, float* a_out, float* b_out,
+                    v3* nn_out) {
+    v3 normal = vl(q->normal);
+    v3 nn = normal;
+    float DD = q->D;
+    if (dot(r->d, normal) > 0) {
+        nn = neg(normal);
+        DD = -q->D;
+    }
+    float denom = dot(nn, r->d);
+    if (fabsf(denom) < 1e-8f) return 0;
+    float t = (DD - dot(nn, r->o)) / denom;
+    if (t < EPS_SHADOW || t > max) return 0;
+    v3 ph = sub(at(r, t), vl(q->Q));
+    v3 w = vl(q->w);
+    float alpha = dot(w, cross(ph, vl(q->v)));
+    float beta = dot(w, cross(vl(q->u), ph));
+    if (!(alpha >= 0 && alpha <= 1 && beta >= 0 && beta <= 1)) return 0;
+    *t_out = t;
+    *a_out = alpha;
+    *b_out = beta;
+    *nn_out = nn;
+    return 1;
+}
+static int quad_intersect(const pt_quad* q, const ray_t* r, float max, si_t* si) {
+    float t, a, b;
+    v3 nn;
+    if (!quad_hit(q, r, max, &t, &a, &b, &nn)) return 0;
+    si->uv[0] = a;
+    si->uv[1] = b;
+    si->t = t;
+    si->ns = nn;
+    si->n = vl(q->normal);
+    v3 up = (fabsf(si->ns.x) > 0.9999f) ? V(0, 1, 0) : V(1, 0, 0);
+    si->tangent = normalize(cross(up, si->ns));
+    si->p = add(at(r, t), smul(EPS_SHADOW, nn));
+    return 1;
+}
+
+/* SphereShape::Intersect / IntersectPred (Shape.cpp:3-56) */
+static int sphere_root(const pt_sphere* sp, const ray_t* r, float max, float* t_out) {
+    v3 oc = sub(r->o, vl(sp->center));
+    float a = dot(r->d, r->d);
+    float b = dot(oc, r->d);
+    float c = dot(oc, oc) - sp->radius * sp->radius;
+    float disc = b * b - a * c;
+    if (disc > 0) {
+        float temp = (-b - sqrtf(disc)) / a;
+        if (temp < max && temp > EPS_SHADOW) { *t_out = temp; return 1; }
+        temp = (-b + sqrtf(disc)) / a;
+        if (temp < max && temp > EPS_SHADOW) { *t_out = temp; return 1; }
+    }
+    return 0;
+}
+static int sphere_intersect(const pt_sphere* sp, const ray_t* r, float max, si_t* si) {
+    float t;
+    if (!sphere_root(sp, r, max, &t)) return 0;
+    si->t = t;
+    si->ns = normalize(sub(at(r, t), vl(sp->center)));
+    si->n = si->ns;
+    v3 up = (fabsf(si->ns.x) > 0.9999f) ? V(0, 1, 0) : V(1, 0, 0);
+    si->tangent = normalize(cross(up, si->ns));
+    si->p = add(at(r, t), smul(EPS_SHADOW, si->n));
+    sphere_uv(si->n, si->uv);
+    return 1;
+}
+
+/* ------------------------------------------------------------------ traversal (BVH.hpp:1019-1211) */
+typedef struct { uint32_t nodes, tris; } work_t;
+
+static int prim_intersect(const scene_t* S, uint32_t slot, const ray_t* r, float max, si_t* si, work_t* wk);
+static int prim_pred(const scene_t* S, uint32_t slot, const ray_t* r, float max, work_t* wk);
+
+/* BVH4::Intersect: ordered closest hit with entry-distance pruning. */
+static int bvh_intersect(const scene_t* S, const pt_bvh_desc* B, const ray_t* r, float* max, si_t* si, work_t* wk) {
+    const unsigned signs = ((r->d.z < 0) << 2) | ((r->d.y < 0) << 1) | (r->d.x < 0);
+    pt_ref_bvh4_node stack[64];
+    float entry[64];
+    int sp = 0;
+    entry[sp] = 0;
+    stack[sp++] = B->root;
+    int hit = 0;
+    while (sp) {
+        if (entry[--sp] > *max) continue;
+        pt_ref_bvh4_node nd = stack[sp];
+        if (nd.active != 0) {
+            const pt_ref_bvh4_cluster* c = &B->clusters[nd.cluster_idx];
+            wk->nodes++;
+            float te[4];
+            unsigned mask = 0;
+            for (int i = 0; i < 4; i++) {
+                float tx1 = (c->xmin[i] - r->o.x) * r->inv.x, tx2 = (c->xmax[i] - r->o.x) * r->inv.x;
+                float ty1 = (c->ymin[i] - r->o.y) * r->inv.y, ty2 = (c->ymax[i] - r->o.y) * r->inv.y;
+                float tz1 = (c->zmin[i] - r->o.z) * r->inv.z, tz2 = (c->zmax[i] - r->o.z) * r->inv.z;
+                /* _mm_min_ps/_mm_max_ps(a,b): a<b?a:b / a>b?a:b */
+                float tminx = tx1 < tx2 ? tx1 : tx2, tmaxx = tx1 > tx2 ? tx1 : tx2;
+                float tminy = ty1 < ty2 ? ty1 : ty2, tmaxy = ty1 > ty2 ? ty1 : ty2;
+                float tminz = tz1 < tz2 ? tz1 : tz2, tmaxz = tz1 > tz2 ? tz1 : tz2;
+                float tminxy = tminx > tminy ? tminx : tminy;
+                float tEntry = tminxy > tminz ? tminxy : tminz;
+                float tmaxxy = tmaxx < tmaxy ? tmaxx : tmaxy;
+                float tExit = tmaxxy < tmaxz ? tmaxxy : tmaxz;
+                te[i] = tEntry;
+                if (tExit >= EPS_SHADOW && tEntry < *max && tEntry <= tExit) mask |= 1u << i;
+            }
+            unsigned perm = S->lut[signs][nd.perm];
+            /* maskLUT (BVH.hpp:719-738): push far -> near so the nearest pops first */
+            for (int nsh = 0; nsh <= 6; nsh += 2) {
+                unsigned idx = (perm >> nsh) & 3u;
+                if (mask & (1u << idx)) {
+                    if (sp >= 64) return hit;
+                    entry[sp] = te[idx];
+                    stack[sp++] = c->children[idx];
+                }
+            }
+        } else {
+            /* intersectPrimitives (BVH.hpp:107-124) */
+            uint32_t first = B->prim_base + nd.cluster_idx;
+            for (uint32_t i = first; i < first + nd.count; i++) {
+                if (prim_intersect(S, i, r, *max, si, wk)) {
+                    hit = 1;
+                    *max = si->t;
+                }
+            }
+        }
+    }
+    return hit;
+}
+
+static int bvh_pred(const scene_t* S, const pt_bvh_desc* B, const ray_t* r, float max, work_t* wk) {
+    pt_ref_bvh4_node stack[64];
+    int sp = 0;
+    stack[sp++] = B->root;
+    while (sp) {
+        pt_ref_bvh4_node nd = stack[--sp];
+        if (nd.active != 0) {
+            const pt_ref_bvh4_cluster* c = &B->clusters[nd.cluster_idx];
+            wk->nodes++;
+            for (int i = 0; i < 4; i++) {
+                float tx1 = (c->xmin[i] - r->o.x) * r->inv.x, tx2 = (c->xmax[i] - r->o.x) * r->inv.x;
+                float ty1 = (c->ymin[i] - r->o.y) * r->inv.y, ty2 = (c->ymax[i] - r->o.y) * r->inv.y;
+                float tz1 = (c->zmin[i] - r->o.z) * r->inv.z, tz2 = (c->zmax[i] - r->o.z) * r->inv.z;
+                float tminx = tx1 < tx2 ? tx1 : tx2, tmaxx = tx1 > tx2 ? tx1 : tx2;
+                float tminy = ty1 < ty2 ? ty1 : ty2, tmaxy = ty1 > ty2 ? ty1 : ty2;
+                float tminz = tz1 < tz2 ? tz1 : tz2, tmaxz = tz1 > tz2 ? tz1 : tz2;
+                float tminxy = tminx > tminy ? tminx : tminy;
+                float tEntry = tminxy > tminz ? tminxy : tminz;
+                float tmaxxy = tmaxx < tmaxy ? tmaxx : tmaxy;
+                float tExit = tmaxxy < tmaxz ? tmaxxy : tmaxz;
+                if (tExit >= EPS_SHADOW && tEntry < max && tEntry <= tExit) {
+                    if (sp >= 64) return 0;
+                    stack[sp++] = c->children[i];
+                }
+            }
+        } else {
+            uint32_t first = B->prim_base + nd.cluster_idx;
+            for (uint32_t i = first; i < first + nd.count; i++)
+                if (prim_pred(S, i, r, max, wk)) return 1;
+        }
+    }
+    return 0;
+}
+
+/* GeometricPrimitive::Intersect (Primitive.cpp:15-26) / Model::Intersect (Model.hpp:25-27) */
+static int prim_intersect(const scene_t* S, uint32_t slot, const ray_t* r, float max, si_t* si, work_t* wk) {
+    const pt_prim* p = &S->s->prims[slot];
+    if (p->kind == PT_PRIM_BLAS) return bvh_intersect(S, &S->s->bvhs[p->index], r, &max, si, wk);
+    si_t tmp;
+    memset(&tmp, 0, sizeof(tmp));
+    int hit;
+    wk->tris++;
+    if (p->kind == PT_PRIM_TRIANGLE) hit = tri_intersect(S, p->index, p->material, r, max, &tmp);
+    else if (p->kind == PT_PRIM_QUAD) hit = quad_intersect(&S->s->quads[p->index], r, max, &tmp);
+    else hit = sphere_intersect(&S->s->spheres[p->index], r, max, &tmp);
+    if (!hit || (p->material >= 0 && !mat_alpha(S, p->material, tmp.uv, r->o, r->d, (int)slot))) return 0;
+    *si = tmp;
+    si->light = p->light;
+    si->mat = p->material;
+    si->medium = p->medium;
+    si->prim = (int)slot;
+    return 1;
+}
+
+/* GeometricPrimitive::IntersectPred (Primitive.cpp:6-14) */
+static int prim_pred(const scene_t* S, uint32_t slot, const ray_t* r, float max, work_t* wk) {
+    const pt_prim* p = &S->s->prims[slot];
+    if (p->kind == PT_PRIM_BLAS) return bvh_pred(S, &S->s->bvhs[p->index], r, max, wk);
+    wk->tris++;
+    if (mat_has_alpha(S, p->material)) {
+        si_t tmp;
+        memset(&tmp, 0, sizeof(tmp));
+        int hit;
+        if (p->kind == PT_PRIM_TRIANGLE) hit = tri_intersect(S, p->index, p->material, r, max, &tmp);
+        else if (p->kind == PT_PRIM_QUAD) hit = quad_intersect(&S->s->quads[p->index], r, max, &tmp);
+        else hit = sphere_intersect(&S->s->spheres[p->index], r, max, &tmp);
+        return hit && mat_alpha(S, p->material, tmp.uv, r->o, r->d, (int)slot);
+    }
+    if (p->kind == PT_PRIM_TRIANGLE) return tri_pred(S, p->index, r, max);
+    if (p->kind == PT_PRIM_QUAD) {
+        float t, a, b;
+        v3 nn;
+        return quad_hit(&S->s->quads[p->index], r, max, &t, &a, &b, &nn);
+    }
+    float t;
+    return sphere_root(&S->s->spheres[p->index], r, max, &t);
+}
+
+static int scene_intersect(const scene_t* S, const ray_t* r, si_t* si, work_t* wk) {
+    float max = INFINITY;
+    return bvh_intersect(S, &S->s->bvhs[0], r, &max, si, wk);
+}
+static int scene_pred(const scene_t* S, const ray_t* r, float max, work_t* wk) {
+    return bvh_pred(S, &S->s->bvhs[0], r, max, wk);
+}
+
+/* ------------------------------------------------------------------ microfacet (Material.hpp:55-142) */
+typedef struct { float ax, ay; } dist_t;
+static inline dist_t mkdist(float rough) { dist_t d = {rough * rough, rough * rough}; return d; }
+static float lambda_(const dist_t* D, v3 w) {
+    float cos2 = w.z * w.z;
+    if (cos2 == 0) return 0;
+    float sin2 = fmaxf_(0, 1 - cos2);
+    float sinT = sqrtf(sin2);
+    float cosPhi = sinT == 0 ? 1 : clampf(w.x / sinT, -1.0f, 1.0f);
+    float sinPhi = sinT == 0 ? 0 : clampf(w.y / sinT, -1.0f, 1.0f);
+    float alpha2 = (cosPhi * D->ax) * (cosPhi * D->ax) + (sinPhi * D->ay) * (sinPhi * D->ay);
+    return (sqrtf(1.f + alpha2 * sin2 / cos2) - 1.0f) / 2.0f;
+}
+static float D_(const dist_t* D, v3 wh) {
+    float cos2 = wh.z * wh.z;
+    if (cos2 == 0) return 0;
+    float cos4 = cos2 * cos2;
+    float sin2 = fmaxf_(0, 1 - cos2);
+    float sinT = sqrtf(sin2);
+    float cosPhi = sinT == 0 ? 1 : clampf(wh.x / sinT, -1.0f, 1.0f);
+    float sinPhi = sinT == 0 ? 0 : clampf(wh.y / sinT, -1.0f, 1.0f);
+    float e = sin2 / cos2 * ((cosPhi / D->ax) * (cosPhi / D->ax) + (sinPhi / D->ay) * (sinPhi / D->ay));
+    float denom = PI_F * D->ax * D->ay * cos4 * (1 + e) * (1 + e);
+    if (denom <= 0) return INFINITY;
+    return 1 / denom;
+}
+static inline float G1_(const dist_t* D, v3 w) { return 1 / (1 + lambda_(D, w)); }
+static inline float G_(const dist_t* D, v3 wo, v3 wi) { return 1 / (1 + lambda_(D, wo) + lambda_(D, wi)); }
+static inline int smooth_(const dist_t* D) { return fmaxf_(D->ax, D->ay) < 1e-6; }
+static inline float mpdf_(const dist_t* D, v3 wo, v3 wh) { return D_(D, wh) * G1_(D, wo) * fabsf(dot(wo, wh) / wo.z); }
+static v3 vndf_(float ax, float ay, v3 Ve, float U1, float U2) {
+    v3 Vh = normalize(V(ax * Ve.x, ay * Ve.y, Ve.z));
+    float lensq = Vh.x * Vh.x + Vh.y * Vh.y;
+    v3 T1 = lensq > 0 ? muls(V(-Vh.y, Vh.x, 0), 1.0f / sqrtf(lensq)) : V(1, 0, 0);
+    v3 T2 = cross(Vh, T1);
+    float r = sqrtf(U1);
+    float phi = 2.0f * PI_F * U2;
+    float t1 = r * cosf(phi);
+    float t2 = r * sinf(phi);
+    float s = 0.5f * (1.0f + Vh.z);
+    t2 = (1.0f - s) * sqrtf(1.0f - t1 * t1) + s * t2;
+    v3 Nh = add(add(smul(t1, T1), smul(t2, T2)), smul(sqrtf(fmaxf_(0.0f, 1.0f - t1 * t1 - t2 * t2)), Vh));
+    return normalize(V(ax * Nh.x, ay * Nh.y, fmaxf_(0.0f, Nh.z)));
+}
+static v3 sample_wh(const dist_t* D, v3 wo, float u0, float u1) {
+    int flip = wo.z < 0;
+    v3 wh = vndf_(D->ax, D->ay, flip ? neg(wo) : wo, u0, u1);
+    if (flip) wh = neg(wh);
+    return wh;
+}
+static float fresnel_dielectric(float cosi, float eta) {
+    /* Material.hpp:11-28 (T = float) */
+    cosi = clampf(cosi, -1.0f, 1.0f);
+    if (cosi < 0) {
+        eta = 1 / eta;
+        cosi = -cosi;
+    }
+    float sin2i = 1 - cosi * cosi;
+    float sin2t = sin2i / (eta * eta);
+    if (sin2t >= 1) return 1.f;
+    float cost = sqrtf(1 - sin2t);
+    float rpa = (eta * cosi - cost) / (eta * cosi + cost);
+    float rpe = (cosi - eta * cost) / (cosi + eta * cost);
+    return (rpa * rpa + rpe * rpe) / 2;
+}
+static inline v3 schlick(float c, v3 F0) {
+    float p = powf(1.0f - c, 5.0f);
+    return add(F0, muls(sub(V(1, 1, 1), F0), p));
+}
+
+/* ------------------------------------------------------------------ materials */
+typedef struct { v3 f; float pdf; uint32_t flags; v3 o, d; int ok; } bxdf_t;
+#define FL_TRANS 1u
+#define FL_SPEC 2u
+
+static float diffuse_rough(const scene_t* S, const pt_material* m, const si_t* si) {
+    return fmaxf_(tex_eval(S, m->rough, si->uv).y, 0.0001f);
+}
+
+/* MicrofacetDiffuse::scatter (Material.hpp:206-266) */
+static bxdf_t diffuse_scatter(const scene_t* S, const pt_material* m, const ray_t* in, const si_t* si, float u,
+                              float uv0, float uv1) {
+    bxdf_t b;
+    memset(&b, 0, sizeof(b));
+    float rough = diffuse_rough(S, m, si);
+    onb_t tbn = onb_n(dot(in->d, si->ns) > 0 ? neg(si->ns) : si->ns);
+    dist_t D = mkdist(rough);
+    float prob = rough >= 0.7 ? 1.0f : 0.5f;
+    v3 wo = to_local(&tbn, neg(in->d));
+    v3 wi, wh;
+    if (u >= prob) {
+        wh = sample_wh(&D, wo, uv0, uv1);
+        wi = reflect(neg(wo), wh);
+    } else {
+        float z = sqrtf(1.0f - uv1);
+        float phi = 2.0f * PI_F * uv0;
+        float s2 = sqrtf(uv1);
+        float x = cosf(phi) * s2;
+        float y = sinf(phi) * s2;
+        wi = V(x, y, z);
+        wh = normalize(add(wo, wi));
+    }
+    if (wi.z <= 0) return b;
+    float dpdf = prob * wi.z * INV_PI_F;
+    float spdf = (1.0f - prob) * mpdf_(&D, wo, wh) / (4 * fabsf(dot(wo, wh)));
+    float pdf = dpdf + spdf;
+    v3 col = tex_eval(S, m->tex, si->uv);
+    float metal = tex_eval(S, m->metal, si->uv).z;
+    v3 F0 = add(muls(V(0.04f, 0.04f, 0.04f), 1.0f - metal), muls(col, metal)); /* glm::mix */
+    v3 F = schlick(dot(wi, wh), F0);
+    v3 num = muls(F, D_(&D, wh) * G_(&D, wo, wi));
+    float den = fabsf(4.0f * wo.z * wi.z);
+    if (den == 0) return b;
+    v3 spec = divs(num, den);
+    v3 kD = muls(sub(V(1, 1, 1), F), 1.0f - metal);
+    v3 diff = muls(mul(kD, col), INV_PI_F);
+    b.f = add(diff, spec);
+    b.pdf = pdf;
+    b.flags = 0;
+    b.o = si->p;
+    b.d = to_world(&tbn, wi);
+    b.ok = 1;
+    return b;
+}
+static v3 diffuse_f(const scene_t* S, const pt_material* m, const ray_t* in, const si_t* si, v3 dir) {
+    /* calc_attenuation (Material.hpp:299-326) */
+    onb_t tbn = onb_n(dot(in->d, si->ns) > 0 ? neg(si->ns) : si->ns);
+    v3 wo = to_local(&tbn, neg(in->d));
+    v3 wi = to_local(&tbn, dir);
+    v3 wh = normalize(add(wo, wi));
+    float rough = diffuse_rough(S, m, si);
+    float metal = tex_eval(S, m->metal, si->uv).z;
+    dist_t D = mkdist(rough);
+    v3 col = tex_eval(S, m->tex, si->uv);
+    v3 F0 = add(muls(V(0.04f, 0.04f, 0.04f), 1.0f - metal), muls(col, metal));
+    v3 F = schlick(dot(wi, wh), F0);
+    v3 num = muls(F, D_(&D, wh) * G_(&D, wo, wi));
+    float den = fabsf(4.0f * wo.z * wi.z);
+    if (den == 0) return V(0, 0, 0);
+    v3 spec = divs(num, den);
+    v3 kD = muls(sub(V(1, 1, 1), F), 1.0f - metal);
+    v3 diff = muls(mul(kD, col), INV_PI_F);
+    return add(diff, spec);
+}
+static float diffuse_pdf(const scene_t* S, const pt_material* m, const ray_t* in, const si_t* si, v3 dir) {
+    /* MicrofacetDiffuse::PDF (Material.hpp:281-296): no (1-prob) factor (A.7) */
+    float rough = diffuse_rough(S, m, si);
+    dist_t D = mkdist(rough);
+    onb_t tbn = onb_n(dot(in->d, si->ns) > 0 ? neg(si->ns) : si->ns);
+    v3 wo = to_local(&tbn, neg(in->d));
+    v3 wh = to_local(&tbn, normalize(sub(dir, in->d)));
+    float prob = rough >= 0.7 ? 1.0f : 0.5f;
+    float diff = prob * fabsf(dot(si->ns, dir)) * INV_PI_F;
+    float spec = mpdf_(&D, wo, wh) / (4 * fabsf(dot(wo, wh)));
+    return diff + spec;
+}
+
+/* MicrofacetDielectric::scatter (Material.hpp:392-477) */
+static bxdf_t dielectric_scatter(const scene_t* S, const pt_material* m, const ray_t* in, const si_t* si, float u,
+                                 float uv0, float uv1) {
+    bxdf_t b;
+    memset(&b, 0, sizeof(b));
+    float rough = tex_eval(S, m->rough, si->uv).y;
+    dist_t D = mkdist(rough);
+    onb_t tbn = onb_si(si);
+    v3 wo = to_local(&tbn, neg(in->d));
+    float ri = m->ri;
+    float eta = dot(neg(in->d), si->ns) > 0 ? 1 / ri : ri;
+    if (ri == 1 || smooth_(&D)) {
+        v3 N = dot(in->d, si->ns) > 0 ? neg(si->ns) : si->ns;
+        v3 Ng = dot(in->d, si->n) > 0 ? neg(si->n) : si->n;
+        float F = fresnel_dielectric(wo.z, ri);
+        float R = F, T = 1.0f - R;
+        v3 dir;
+        if (u < (R / (R + T))) {
+            dir = to_world(&tbn, V(-wo.x, -wo.y, wo.z));
+            b.o = add(at(in, si->t), smul(EPS_SHADOW, Ng));
+            b.f = divs(muls(tex_eval(S, m->tex, si->uv), R), fabsf(dot(si->ns, dir)));
+            b.pdf = R / (R + T);
+        } else {
+            dir = refract(in->d, N, eta);
+            if (is_zero(dir)) return b;
+            b.o = sub(at(in, si->t), smul(EPS_SHADOW, Ng));
+            b.f = divs(muls(tex_eval(S, m->tex, si->uv), T), fabsf(dot(si->ns, dir)));
+            b.pdf = T / (R + T);
+        }
+        b.d = dir;
+        b.flags = FL_TRANS | FL_SPEC;
+        b.ok = 1;
+        return b;
+    }
+    v3 wh = sample_wh(&D, wo, uv0, uv1);
+    v3 Ng = dot(in->d, si->n) > 0 ? neg(si->n) : si->n;
+    float F = fresnel_dielectric(dot(wo, wh), 1 / eta);
+    float R = F, T = 1 - R;
+    v3 wi;
+    uint32_t fl = FL_TRANS | (rough < 0.001f ? FL_SPEC : 0u);
+    if (u < (R / (R + T))) {
+        wi = reflect(neg(wo), wh);
+        if (wo.z * wi.z < 0) return b;
+        b.o = add(at(in, si->t), smul(EPS_SHADOW, Ng));
+        b.d = to_world(&tbn, wi);
+        b.pdf = mpdf_(&D, wo, wh) / (4 * fabsf(dot(wo, wh))) * R / (R + T);
+        b.f = divs(muls(muls(muls(tex_eval(S, m->tex, si->uv), D_(&D, wh)), G_(&D, wo, wi)), R), fabsf(4 * wi.z * wo.z));
+    } else {
+        wi = refract(neg(wo), wh, eta);
+        if (wo.z * wi.z > 0 || wi.z == 0) return b;
+        b.o = sub(at(in, si->t), smul(EPS_SHADOW, Ng));
+        b.d = to_world(&tbn, wi);
+        float denom = (dot(wi, wh) + dot(wo, wh) * eta) * (dot(wi, wh) + dot(wo, wh) * eta);
+        float dwh = fabsf(dot(wi, wh)) / denom;
+        b.pdf = mpdf_(&D, wo, wh) * dwh * T / (R + T);
+        float ft = T * D_(&D, wh) * G_(&D, wo, wi) * fabsf(dot(wi, wh) * dot(wo, wh) / (denom * wi.z * wo.z));
+        b.f = muls(tex_eval(S, m->tex, si->uv), ft);
+    }
+    b.flags = fl;
+    b.ok = 1;
+    return b;
+}
+static void dielectric_eval(const scene_t* S, const pt_material* m, const ray_t* in, const si_t* si, v3 dir,
+                            v3* f_out, float* pdf_out) {
+    /* MicrofacetDielectric::PDF / calc_attenuation (Material.hpp:484-564) */
+    *f_out = V(0, 0, 0);
+    *pdf_out = 0;
+    float rough = tex_eval(S, m->rough, si->uv).y;
+    dist_t D = mkdist(rough);
+    float ri = m->ri;
+    if (ri == 1 || smooth_(&D)) return;
+    onb_t tbn = onb_si(si);
+    v3 wo = to_local(&tbn, neg(in->d));
+    v3 wi = to_local(&tbn, dir);
+    float co = wo.z, ci = wi.z;
+    int refl = ci * co > 0;
+    float etap = 1;
+    if (!refl) etap = co > 0 ? ri : (1 / ri);
+    v3 wh = add(muls(wi, etap), wo);
+    if (dot(wh, wh) == 0) return;
+    wh = normalize(wh);
+    if (wh.z < 0) wh = neg(wh);
+    if (dot(wh, wi) * ci <= 0.0 || dot(wh, wo) * co <= 0.0) return;
+    float F = fresnel_dielectric(dot(wo, wh), ri);
+    float R = F, T = 1 - R;
+    float pdf = mpdf_(&D, wo, wh);
+    v3 col = tex_eval(S, m->tex, si->uv);
+    if (refl) {
+        *pdf_out = pdf / (4 * fabsf(dot(wo, wh))) * R / (R + T);
+        *f_out = divs(muls(muls(muls(col, D_(&D, wh)), G_(&D, wo, wi)), F), fabsf(4 * ci * co));
+    } else {
+        float den = (dot(wi, wh) + dot(wo, wh) / etap) * (dot(wi, wh) + dot(wo, wh) / etap);
+        float dwh = fabsf(dot(wi, wh)) / den;
+        *pdf_out = pdf * dwh * T / (R + T);
+        float den2 = (dot(wi, wh) + dot(wo, wh) / etap) * (dot(wi, wh) + dot(wo, wh) / etap) * ci * co;
+        float ft = D_(&D, wh) * (1 - F) * G_(&D, wo, wi) * fabsf(dot(wi, wh) * dot(wo, wh) / den2);
+        *f_out = muls(col, ft);
+    }
+}
+
+/* ThinDielectric::scatter (Material.hpp:605-644) */
+static bxdf_t thin_scatter(const scene_t* S, const pt_material* m, const ray_t* in, const si_t* si, float u) {
+    bxdf_t b;
+    memset(&b, 0, sizeof(b));
+    onb_t tbn = onb_si(si);
+    v3 wo = to_local(&tbn, neg(in->d));
+    v3 Ng = dot(in->d, si->n) > 0 ? neg(si->n) : si->n;
+    float F = fresnel_dielectric(wo.z, m->ri);
+    float R = F, T = 1.0f - R;
+    if (R < 1.0f) {
+        R += T * T * R / (1.0f - R * R);
+        T = 1.0f - R;
+    }
+    v3 dir, f;
+    if (u < (R / (R + T))) {
+        dir = to_world(&tbn, V(-wo.x, -wo.y, wo.z));
+        b.o = add(at(in, si->t), smul(EPS_SHADOW, Ng));
+        f = divs(muls(V(1, 1, 1), R), fabsf(dot(si->ns, dir)));
+        b.pdf = R / (R + T);
+    } else {
+        dir = in->d;
+        b.o = sub(at(in, si->t), smul(EPS_SHADOW, Ng));
+        f = divs(muls(V(1, 1, 1), T), fabsf(dot(si->ns, dir)));
+        b.pdf = T / (R + T);
+    }
+    b.f = mul(f, tex_eval(S, m->tex, si->uv));
+    b.d = dir;
+    b.flags = FL_TRANS | FL_SPEC;
+    b.ok = 1;
+    return b;
+}
+
+/* SpecularConductor::scatter (Material.hpp:664-669) */
+static bxdf_t conductor_scatter(const pt_material* m, const ray_t* in, const si_t* si) {
+    bxdf_t b;
+    memset(&b, 0, sizeof(b));
+    v3 d = reflect(in->d, si->ns);
+    float dt = dot(d, si->ns);
+    if (dt <= 0) return b;
+    b.f = divs(schlick(dot(si->ns, neg(in->d)), vl(m->albedo)), dt);
+    b.pdf = 1;
+    b.flags = FL_SPEC;
+    b.o = si->p;
+    b.d = d;
+    b.ok = 1;
+    return b;
+}
+
+static bxdf_t mat_scatter(const scene_t* S, int mid, const ray_t* in, const si_t* si, float u, float uv0, float uv1) {
+    const pt_material* m = &S->s->materials[mid];
+    switch (m->kind) {
+        case PT_MAT_DIFFUSE: return diffuse_scatter(S, m, in, si, u, uv0, uv1);
+        case PT_MAT_DIELECTRIC: return dielectric_scatter(S, m, in, si, u, uv0, uv1);
+        case PT_MAT_THIN: return thin_scatter(S, m, in, si, u);
+        default: return conductor_scatter(m, in, si);
+    }
+}
+static v3 mat_f(const scene_t* S, int mid, const ray_t* in, const si_t* si, v3 dir) {
+    const pt_material* m = &S->s->materials[mid];
+    v3 f;
+    float p;
+    switch (m->kind) {
+        case PT_MAT_DIFFUSE: return diffuse_f(S, m, in, si, dir);
+        case PT_MAT_DIELECTRIC: dielectric_eval(S, m, in, si, dir, &f, &p); return f;
+        case PT_MAT_THIN: return V(0, 0, 0);
+        default: return V(1, 1, 1); /* base Material::calc_attenuation */
+    }
+}
+static float mat_pdf(const scene_t* S, int mid, const ray_t* in, const si_t* si, v3 dir) {
+    const pt_material* m = &S->s->materials[mid];
+    v3 f;
+    float p;
+    switch (m->kind) {
+        case PT_MAT_DIFFUSE: return diffuse_pdf(S, m, in, si, dir);
+        case PT_MAT_DIELECTRIC: dielectric_eval(S, m, in, si, dir, &f, &p); return p;
+        default: return 0;
+    }
+}
+
+/* ------------------------------------------------------------------ lights (Light.cpp) */
+typedef struct { v3 L; si_t si; v3 dir; } lsample_t;
+
+static float shape_area(const scene_t* S, const pt_prim* p) {
+    if (p->kind == PT_PRIM_QUAD) {
+        const pt_quad* q = &S->s->quads[p->index];
+        return length3(cross(vl(q->u), vl(q->v)));
+    }
+    if (p->kind == PT_PRIM_SPHERE) {
+        float r = S->s->spheres[p->index].radius;
+        return 4.0f * PI_F * r * r;
+    }
+    tri_t T = tri_get(S, p->index);
+    return length3(cross(sub(T.v0, T.v2), sub(T.v1, T.v2))) * 0.5f;
+}
+
+static si_t shape_sample(const scene_t* S, const pt_prim* p, float u0, float u1) {
+    si_t si;
+    memset(&si, 0, sizeof(si));
+    if (p->kind == PT_PRIM_QUAD) {
+        const pt_quad* q = &S->s->quads[p->index];
+        si.p = add(add(vl(q->Q), smul(u0, vl(q->u))), smul(u1, vl(q->v)));
+        si.n = vl(q->normal);
+    } else if (p->kind == PT_PRIM_SPHERE) {
+        const pt_sphere* sp = &S->s->spheres[p->index];
+        float z = 1.0f - 2.0f * u0;
+        float r = sqrtf(1.0f - z * z);
+        float phi = 2.0f * PI_F * u1;
+        v3 d = V(r * cosf(phi), r * sinf(phi), z);
+        v3 c = vl(sp->center);
+        si.p = add(c, smul(sp->radius, d));
+        si.n = normalize(sub(si.p, c));
+        sphere_uv(si.p, si.uv);
+    } else {
+        /* TriangleShape::Sample (Shape.cpp:277-297): not folded (A.6) */
+        float w = 1.0f - u0 - u1;
+        tri_t T = tri_get(S, p->index);
+        v3 n = normalize(cross(sub(T.v1, T.v0), sub(T.v2, T.v0)));
+        if (n.x != n.x) n = V(0, 0, 0);
+        si.p = add(add(smul(u0, T.v1), smul(u1, T.v2)), smul(w, T.v0));
+        const float* uvs = S->s->uvs;
+        si.uv[0] = u0 * uvs[2 * T.i1] + u1 * uvs[2 * T.i2] + w * uvs[2 * T.i0];
+        si.uv[1] = u0 * uvs[2 * T.i1 + 1] + u1 * uvs[2 * T.i2 + 1] + w * uvs[2 * T.i0 + 1];
+        si.n = n;
+    }
+    return si;
+}
+static float shape_pdf(const scene_t* S, const pt_prim* p, const si_t* si, const ray_t* r) {
+    v3 to = sub(si->p, r->o);
+    float d2 = dot(to, to);
+    float lc = fabsf(dot(neg(r->d), si->n));
+    float area = shape_area(S, p);
+    if (p->kind == PT_PRIM_QUAD) {
+        if (area == 0) return 0;
+    } else if (p->kind == PT_PRIM_SPHERE) {
+        if (area * lc == 0) return 0;
+    } else {
+        if (area == 0 || lc == 0 || si->n.x != si->n.x) return 0;
+    }
+    return d2 / (lc * area);
+}
+static v3 sky_le(const pt_light* l, v3 d) {
+    float a = 0.5f * (d.y + 1.0f);
+    return smul(l->scale, add(smul(1.0f - a, vl(l->color)), smul(a, vl(l->vec))));
+}
+static v3 inf_le(const pt_light* l, v3 d) { return l->kind == PT_LIGHT_SKY_INF ? sky_le(l, d) : vl(l->color); }
+
+static lsample_t light_sample(const scene_t* S, const pt_light* l, float u0, float u1) {
+    lsample_t ls;
+    memset(&ls, 0, sizeof(ls));
+    if (l->kind == PT_LIGHT_AREA) {
+        ls.si = shape_sample(S, &S->s->prims[l->prim], u0, u1);
+        return ls;
+    }
+    if (l->kind == PT_LIGHT_POINT) {
+        ls.L = vl(l->color);
+        ls.si.p = vl(l->vec);
+        ls.si.n = V(1, 1, 1);
+        ls.si.uv[0] = u0;
+        ls.si.uv[1] = u1;
+        return ls;
+    }
+    float z = 2.0f * u0 - 1.0f;
+    float th = 2.0f * PI_F * u1;
+    float r = sqrtf(1.0f - z * z);
+    float x = r * cosf(th), y = r * sinf(th);
+    v3 d = V(x, y, z);
+    if (l->kind == PT_LIGHT_DISTANT) {
+        ls.L = vl(l->color);
+        ls.si.uv[0] = u0;
+        ls.si.uv[1] = u1;
+        ls.dir = normalize(add(vl(l->vec), muls(d, 0.02f)));
+        return ls;
+    }
+    ls.L = inf_le(l, d);
+    sphere_uv(d, ls.si.uv);
+    ls.dir = d;
+    return ls;
+}
+static inline int light_is_delta(const pt_light* l) { return l->kind == PT_LIGHT_DISTANT || l->kind == PT_LIGHT_POINT; }
+static float light_pdf(const scene_t* S, const pt_light* l, const si_t* si, const ray_t* r) {
+    if (l->kind == PT_LIGHT_AREA) {
+        const pt_prim* p = &S->s->prims[l->prim];
+        if (l->one_sided) return dot(neg(r->d), si->n) > 0 ? shape_pdf(S, p, si, r) : 0;
+        return shape_pdf(S, p, si, r);
+    }
+    if (l->kind == PT_LIGHT_UNIFORM_INF || l->kind == PT_LIGHT_SKY_INF) return 1.0f / (4.0f * PI_F);
+    return 0;
+}
+static v3 light_L(const scene_t* S, const pt_light* l, const si_t* si, const ray_t* r) {
+    if (l->kind == PT_LIGHT_AREA) {
+        if (l->one_sided && dot(r->d, si->n) > 0) return V(0, 0, 0);
+        return tex_eval(S, l->tex, si->uv);
+    }
+    if (l->kind == PT_LIGHT_UNIFORM_INF || l->kind == PT_LIGHT_SKY_INF) return inf_le(l, r->d);
+    return V(0, 0, 0);
+}
+
+/* LightSampler::Sample (LightSampler.cpp:7-11, 34-46) */
+static int ls_sample(const scene_t* S, float u) {
+    uint32_t n = S->s->n_sampler_lights;
+    if (n == 0) return -1;
+    if (S->s->light_sampler == PT_LS_UNIFORM) {
+        int idx = (int)(u * n);
+        if (idx > (int)n - 1) idx = (int)n - 1;
+        return (int)S->s->sampler_lights[idx];
+    }
+    float total = 0;
+    for (uint32_t i = 0; i < n; i++) total += S->s->lights[S->s->sampler_lights[i]].power;
+    float cur = 0, target = u * total;
+    for (uint32_t i = 0; i < n; i++) {
+        cur += S->s->lights[S->s->sampler_lights[i]].power;
+        if (cur >= target) return (int)S->s->sampler_lights[i];
+    }
+    return (int)S->s->sampler_lights[n - 1];
+}
+
+/* ------------------------------------------------------------------ integrators (Integrators.cpp) */
+typedef struct {
+    const scene_t* S;
+    uint32_t max_depth;
+    int simple;
+    oracle_counters* cnt;
+} integ_t;
+
+/* PathIntegrator::SampleLd (Integrators.cpp:260-294) */
+static v3 sample_ld(const integ_t* I, const ray_t* ray, const si_t* si, float u, float uv0, float uv1) {
+    const scene_t* S = I->S;
+    int li = ls_sample(S, u);
+    if (li < 0) return V(0, 0, 0);
+    const pt_light* l = &S->s->lights[li];
+    lsample_t ls = light_sample(S, l, uv0, uv1);
+    v3 ldir;
+    float t;
+    if (is_zero(ls.si.n)) {
+        ldir = ls.dir;
+        t = INFINITY;
+    } else {
+        ldir = sub(ls.si.p, si->p);
+        t = length3(ldir) - EPS_SHADOW;
+    }
+    ray_t sh = mkray(si->p, normalize(ldir));
+    float lpdf = l->pmf;
+    float dt = dot(si->ns, sh.d);
+    if (lpdf <= 0 || dt * dot(ray->d, si->ns) >= 0) return V(0, 0, 0);
+    work_t wk = {0, 0};
+    I->cnt->any++;
+    int occ = scene_pred(S, &sh, t, &wk);
+    I->cnt->nodes_any += wk.nodes;
+    I->cnt->tris_any += wk.tris;
+    if (occ) return V(0, 0, 0);
+    v3 f = muls(mat_f(S, si->mat, ray, si, sh.d), fabsf(dt));
+    if (light_is_delta(l)) return divs(mul(ls.L, f), lpdf);
+    lpdf *= light_pdf(S, l, &ls.si, &sh);
+    if (lpdf <= 0) return V(0, 0, 0);
+    float w2 = lpdf * lpdf;
+    float w1 = mat_pdf(S, si->mat, ray, si, sh.d);
+    w1 = w1 * w1;
+    float wl = w2 / (w1 + w2);
+    return divs(muls(mul(light_L(S, l, &ls.si, &sh), f), wl), lpdf);
+}
+
+static int intersect_counted(const integ_t* I, const ray_t* r, si_t* si) {
+    work_t wk = {0, 0};
+    I->cnt->closest++;
+    int h = scene_intersect(I->S, r, si, &wk);
+    I->cnt->nodes_closest += wk.nodes;
+    I->cnt->tris_closest += wk.tris;
+    return h;
+}
+
+/* PathIntegrator::Li (Integrators.cpp:182-257) */
+static v3 li_path(const integ_t* I, ray_t ray, rng_t* rng) {
+    const scene_t* S = I->S;
+    v3 att = V(1, 1, 1), out = V(0, 0, 0);
+    uint32_t depth = 0, rr = 0;
+    float prev = 1;
+    int spec = 1;
+    while (depth++ < I->max_depth && (att.x + att.y + att.z) > 0.0f) {
+        si_t si;
+        memset(&si, 0, sizeof(si));
+        if (!intersect_counted(I, &ray, &si)) {
+            for (uint32_t k = 0; k < S->s->n_infinite_lights; k++) {
+                const pt_light* l = &S->s->lights[S->s->infinite_lights[k]];
+                if (spec) {
+                    out = add(out, mul(att, inf_le(l, ray.d)));
+                } else if (prev > 0) {
+                    float lp = l->pmf * (1.0f / (4.0f * PI_F));
+                    float w = prev * prev / (prev * prev + lp * lp);
+                    out = add(out, muls(mul(att, inf_le(l, ray.d)), w));
+                }
+            }
+            return out;
+        }
+        float r[8];
+        for (int k = 0; k < 8; k++) r[k] = next1(rng);
+        if (si.light >= 0) {
+            const pt_light* al = &S->s->lights[si.light];
+            v3 L = light_L(S, al, &si, &ray);
+            if (!is_zero(L)) {
+                if (spec) {
+                    out = add(out, mul(att, L));
+                } else if (prev > 0) {
+                    float lp = al->pmf * light_pdf(S, al, &si, &ray);
+                    float w = prev * prev / (prev * prev + lp * lp);
+                    out = add(out, muls(mul(att, L), w));
+                }
+            }
+        }
+        if (si.mat < 0) {
+            spec = 1;
+            ray.o = at(&ray, si.t);
+            continue;
+        }
+        bxdf_t b = mat_scatter(S, si.mat, &ray, &si, r[4], r[0], r[1]);
+        if (!b.ok) return out;
+        ray_t nr = mkray(b.o, b.d);
+        spec = (b.flags & FL_SPEC) != 0;
+        if (!spec) {
+            out = add(out, mul(att, sample_ld(I, &ray, &si, r[5], r[2], r[3])));
+            prev = mat_pdf(S, si.mat, &ray, &si, nr.d);
+        }
+        att = mul(att, divs(muls(b.f, fabsf(dot(si.ns, nr.d))), b.pdf));
+        if (rr++ > 3) {
+            float q = fminf(0.95f, fmaxf(fmaxf(att.x, att.y), att.z));
+            if (r[6] >= q) break;
+            att = divs(att, q);
+        }
+        ray = nr;
+    }
+    return out;
+}
+
+/* SimplePathIntegrator::Li (Integrators.cpp:131-180) */
+static v3 li_simple(const integ_t* I, ray_t ray, rng_t* rng) {
+    const scene_t* S = I->S;
+    v3 att = V(1, 1, 1), out = V(0, 0, 0);
+    uint32_t depth = 0, rr = 0;
+    while (depth++ < I->max_depth && (att.x + att.y + att.z) > 0.0f) {
+        si_t si;
+        memset(&si, 0, sizeof(si));
+        if (!intersect_counted(I, &ray, &si)) {
+            for (uint32_t k = 0; k < S->s->n_infinite_lights; k++) {
+                const pt_light* l = &S->s->lights[S->s->infinite_lights[k]];
+                out = add(out, mul(att, inf_le(l, ray.d)));
+            }
+            return out;
+        }
+        float u0 = next1(rng), u1 = next1(rng);
+        float us = next1(rng);
+        float ur = next1(rng);
+        if (si.light >= 0) {
+            v3 L = light_L(S, &S->s->lights[si.light], &si, &ray);
+            if (!is_zero(L)) out = add(out, mul(att, L));
+        }
+        if (si.mat < 0) {
+            ray.o = at(&ray, si.t);
+            continue;
+        }
+        bxdf_t b = mat_scatter(S, si.mat, &ray, &si, us, u0, u1);
+        if (!b.ok) return out;
+        ray_t nr = mkray(b.o, b.d);
+        att = mul(att, divs(muls(b.f, fabsf(dot(si.ns, nr.d))), b.pdf));
+        if (rr++ > 3) {
+            float q = fminf(0.95f, fmaxf(fmaxf(att.x, att.y), att.z));
+            if (ur >= q) break;
+            att = divs(att, q);
+        }
+        ray = nr;
+    }
+    return out;
+}
+
+/* Camera::GenerateRay (Camera.hpp:21-35) + camera draws (Integrators.cpp:61-64) */
+static ray_t camera_ray(const pt_camera_desc* c, uint32_t x, uint32_t y, rng_t* rng, double* px, double* py) {
+    float a = next1(rng), b = next1(rng);
+    (void)next1(rng); /* time */
+    float l0 = next1(rng), l1 = next1(rng);
+    *px = (double)x + (double)a;
+    *py = (double)y + (double)b;
+    float pxf = (float)*px, pyf = (float)*py;
+    float uc = pxf / (float)c->width;
+    float vc = pyf / (float)c->height;
+    v3 dir = normalize(add(add(neg(vl(c->w)), smul((2.0f * uc - 1.0f) * c->half_width, vl(c->u))),
+                           smul((2.0f * vc - 1.0f) * c->half_height, vl(c->v))));
+    if (c->focus_distance == 0 || c->focus_angle == 0) return mkray(vl(c->origin), dir);
+    float r = sqrtf(l0);
+    float th = 2 * PI_F * l1;
+    float lx = r * cosf(th), ly = r * sinf(th);
+    v3 du = smul(c->defocus_radius, vl(c->u));
+    v3 dv = smul(c->defocus_radius, vl(c->v));
+    dir = muls(dir, c->focus_distance);
+    v3 off = add(smul(lx, du), smul(ly, dv));
+    return mkray(add(vl(c->origin), off), normalize(sub(dir, off)));
+}
+
+static void scene_init(scene_t* S, const pt_scene_desc* s) {
+    S->s = s;
+    build_lut(S->lut);
+}
+
+static v3 li_one(const integ_t* I, const pt_camera_desc* cam, uint32_t seed, uint32_t x, uint32_t y, uint32_t s,
+                 double* px, double* py) {
+    rng_t rng;
+    rng.key = stream_key(seed, y * (uint32_t)cam->width + x, s);
+    rng.dim = 0;
+    ray_t r = camera_ray(cam, x, y, &rng, px, py);
+    I->cnt->paths++;
+    return I->simple ? li_simple(I, r, &rng) : li_path(I, r, &rng);
+}
+
+int oracle_li(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render_desc* rd, uint32_t pb, uint32_t pe,
+              float* out_L, double* out_p, oracle_counters* cnt) {
+    if (!s || !cam || !rd || !out_L) return -1;
+    scene_t S;
+    scene_init(&S, s);
+    oracle_counters local;
+    memset(&local, 0, sizeof(local));
+    integ_t I = {&S, rd->max_depth, rd->integrator == PT_INTEGRATOR_SIMPLE, cnt ? cnt : &local};
+    size_t k = 0;
+    for (uint32_t pix = pb; pix < pe; pix++) {
+        uint32_t x = pix % (uint32_t)cam->width, y = pix / (uint32_t)cam->width;
+        for (uint32_t smp = 0; smp < rd->spp; smp++, k++) {
+            double px, py;
+            v3 L = li_one(&I, cam, rd->seed, x, y, smp, &px, &py);
+            out_L[3 * k] = L.x;
+            out_L[3 * k + 1] = L.y;
+            out_L[3 * k + 2] = L.z;
+            if (out_p) {
+                out_p[2 * k] = px;
+                out_p[2 * k + 1] = py;
+            }
+        }
+    }
+    return 0;
+}
+
+int oracle_trace(const pt_scene_desc* s, const pt_ray* rays, uint32_t n, int any_hit, oracle_hit* out) {
+    scene_t S;
+    scene_init(&S, s);
+    for (uint32_t i = 0; i < n; i++) {
+        ray_t r = mkray(vl(rays[i].o), vl(rays[i].d));
+        oracle_hit* h = &out[i];
+        memset(h, 0, sizeof(*h));
+        h->prim = h->material = h->light = -1;
+        work_t wk = {0, 0};
+        if (any_hit) {
+            h->hit = scene_pred(&S, &r, rays[i].tmax, &wk);
+        } else {
+            si_t si;
+            memset(&si, 0, sizeof(si));
+            si.prim = si.mat = si.light = -1;
+            float max = rays[i].tmax;
+            h->hit = bvh_intersect(&S, &s->bvhs[0], &r, &max, &si, &wk);
+            if (h->hit) {
+                h->t = si.t;
+                memcpy(h->p, &si.p, 12);
+                memcpy(h->n, &si.n, 12);
+                memcpy(h->ns, &si.ns, 12);
+                memcpy(h->tangent, &si.tangent, 12);
+                h->uv[0] = si.uv[0];
+                h->uv[1] = si.uv[1];
+                h->prim = si.prim;
+                h->material = si.mat;
+                h->light = si.light;
+                h->medium = si.medium;
+            }
+        }
+        h->nodes = wk.nodes;
+        h->tris = wk.tris;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ film (Film.hpp:65-82, Filter.hpp) */
+static double mitchell1(double x, double b, double c) {
+    double ax = fabs(x);
+    if (ax <= 1.0) return 1.0 / 6.0 * ((12 - 9 * b - 6 * c) * ax * ax * ax + (-18 + 12 * b + 6 * c) * ax * ax + (6 - 2 * b));
+    if (ax <= 2) return 1.0 / 6.0 * ((-b - 6 * c) * ax * ax * ax + (6 * b + 30 * c) * ax * ax + (-12 * b - 48 * c) * ax + (8 * b + 24 * c));
+    return 0;
+}
+static double gauss1(double x, double sigma) {
+    return 0.56418958354775628695 / (sigma * 1.41421356237309504880) * exp(-(x * x) / (2 * sigma * sigma));
+}
+static double filter_eval(const pt_render_desc* rd, float px, float py) {
+    if (rd->filter == PT_FILTER_BOX) return fabsf(px) <= rd->filter_radius[0] && fabsf(py) <= rd->filter_radius[1];
+    if (rd->filter == PT_FILTER_GAUSSIAN) {
+        double sg = rd->filter_params[0];
+        double X = gauss1(rd->filter_radius[0], sg), Y = gauss1(rd->filter_radius[1], sg);
+        double gx = gauss1(px, sg) - X, gy = gauss1(py, sg) - Y;
+        return (gx > 0 ? gx : 0) * (gy > 0 ? gy : 0);
+    }
+    float ax = 2 * px / rd->filter_radius[0];
+    float ay = 2 * py / rd->filter_radius[1];
+    return mitchell1(ax, rd->filter_params[0], rd->filter_params[1]) *
+           mitchell1(ay, rd->filter_params[0], rd->filter_params[1]);
+}
+static double filter_integral(const pt_render_desc* rd) {
+    float rx = rd->filter_radius[0], ry = rd->filter_radius[1];
+    if (rd->filter == PT_FILTER_BOX) return 4 * rx * ry;
+    if (rd->filter == PT_FILTER_GAUSSIAN) {
+        double sg = rd->filter_params[0];
+        double X = gauss1(rx, sg), Y = gauss1(ry, sg);
+        double s2 = sg * 1.41421356237309504880;
+        double ix = 0.5 * (erf(rx / s2) - erf(-rx / s2));
+        double iy = 0.5 * (erf(ry / s2) - erf(-ry / s2));
+        return (ix - 2 * rx * X) * (iy - 2 * ry * Y);
+    }
+    return rx * ry / 4.0;
+}
+
+int oracle_filter_table(const pt_render_desc* rd, double* out) {
+    int k = 0;
+    for (int j = 0; j <= 32; j++)
+        for (int i = 0; i <= 32; i++) {
+            float px = -2.0f + 4.0f * i / 32.0f, py = -2.0f + 4.0f * j / 32.0f;
+            out[k++] = filter_eval(rd, px, py);
+        }
+    out[k] = filter_integral(rd);
+    return 0;
+}
+
+static void film_add(const pt_render_desc* rd, double inv_int, int W, int H, double* film, double px, double py, v3 L) {
+    int rx = (int)ceilf(rd->filter_radius[0] - 0.5f), ry = (int)ceilf(rd->filter_radius[1] - 0.5f);
+    double fx = px - floor(px), fy = py - floor(py);
+    int ix = (int)floor(px), iy = (int)floor(py);
+    for (int y = -ry; y <= ry; y++)
+        for (int x = -rx; x <= rx; x++) {
+            double sx = (double)x + 0.5 - fx, sy = (double)y + 0.5 - fy;
+            double w = filter_eval(rd, (float)sx, (float)sy) * inv_int;
+            int qx = x + ix, qy = y + iy;
+            if (w <= 0 || qx < 0 || qy < 0 || qx >= W || qy >= H) continue;
+            double* o = film + 4 * ((size_t)qy * W + qx);
+            o[0] += (double)L.x * w;
+            o[1] += (double)L.y * w;
+            o[2] += (double)L.z * w;
+            o[3] += w;
+        }
+}
+
+typedef struct {
+    const pt_scene_desc* s;
+    const pt_camera_desc* cam;
+    const pt_render_desc* rd;
+    double* film;
+    int tiles_x, tiles;
+    volatile int next;
+    pthread_mutex_t mu;
+    oracle_counters total;
+} job_t;
+
+static void* render_worker(void* arg) {
+    job_t* J = (job_t*)arg;
+    scene_t S;
+    scene_init(&S, J->s);
+    oracle_counters c;
+    memset(&c, 0, sizeof(c));
+    integ_t I = {&S, J->rd->max_depth, J->rd->integrator == PT_INTEGRATOR_SIMPLE, &c};
+    int W = J->cam->width, H = J->cam->height;
+    double inv_int = 1.0 / filter_integral(J->rd);
+    int rx = (int)ceilf(J->rd->filter_radius[0] - 0.5f), ry = (int)ceilf(J->rd->filter_radius[1] - 0.5f);
+    uint32_t sc = J->rd->shard_count ? J->rd->shard_count : 1;
+    for (;;) {
+        int tile = __sync_fetch_and_add(&J->next, 1);
+        if (tile >= J->tiles) break;
+        int tx = tile % J->tiles_x, ty = tile / J->tiles_x;
+        int x0 = tx * 32, y0 = ty * 32, x1 = x0 + 32 < W ? x0 + 32 : W, y1 = y0 + 32 < H ? y0 + 32 : H;
+        /* FilmTile over the tile + filter margin (Film.hpp:118-123), merged under a lock */
+        int bx0 = x0 - rx < 0 ? 0 : x0 - rx, by0 = y0 - ry < 0 ? 0 : y0 - ry;
+        int bx1 = x1 + rx > W ? W : x1 + rx, by1 = y1 + ry > H ? H : y1 + ry;
+        int bw = bx1 - bx0, bh = by1 - by0;
+        double* tilebuf = (double*)calloc((size_t)bw * bh * 4, sizeof(double));
+        for (int y = y0; y < y1; y++)
+            for (int x = x0; x < x1; x++)
+                for (uint32_t smp = J->rd->shard_index; smp < J->rd->spp; smp += sc) {
+                    double px, py;
+                    v3 L = li_one(&I, J->cam, J->rd->seed, (uint32_t)x, (uint32_t)y, smp, &px, &py);
+                    film_add(J->rd, inv_int, bw, bh, tilebuf, px - bx0, py - by0, L);
+                }
+        pthread_mutex_lock(&J->mu);
+        for (int y = 0; y < bh; y++)
+            for (int x = 0; x < bw; x++)
+                for (int k = 0; k < 4; k++)
+                    J->film[4 * ((size_t)(y + by0) * W + (x + bx0)) + k] += tilebuf[4 * ((size_t)y * bw + x) + k];
+        pthread_mutex_unlock(&J->mu);
+        free(tilebuf);
+    }
+    pthread_mutex_lock(&J->mu);
+    J->total.closest += c.closest;
+    J->total.any += c.any;
+    J->total.nodes_closest += c.nodes_closest;
+    J->total.tris_closest += c.tris_closest;
+    J->total.nodes_any += c.nodes_any;
+    J->total.tris_any += c.tris_any;
+    J->total.paths += c.paths;
+    pthread_mutex_unlock(&J->mu);
+    return NULL;
+}
+
+int oracle_render(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render_desc* rd, double* film,
+                  int threads, oracle_counters* cnt) {
+    if (!s || !cam || !rd || !film) return -1;
+    if (threads < 1) threads = 1;
+    job_t J;
+    memset(&J, 0, sizeof(J));
+    J.s = s;
+    J.cam = cam;
+    J.rd = rd;
+    J.film = film;
+    J.tiles_x = (cam->width + 31) / 32;
+    J.tiles = J.tiles_x * ((cam->height + 31) / 32);
+    pthread_mutex_init(&J.mu, NULL);
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+    for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, render_worker, &J);
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    free(th);
+    pthread_mutex_destroy(&J.mu);
+    if (cnt) *cnt = J.total;
+    return 0;
+}
+
+/* Note: the film splat above works in tile-local coordinates; the filter
+ * weights only depend on the fractional position, so this equals
+ * FilmTile::Add at the absolute position. */
+
+/* ------------------------------------------------------------------ unit cases */
+int oracle_bsdf(const pt_scene_desc* s, int mid, const float* in, uint32_t n, float* out) {
+    scene_t S;
+    scene_init(&S, s);
+    for (uint32_t i = 0; i < n; i++) {
+        const float* c = in + 27 * (size_t)i;
+        float* o = out + 20 * (size_t)i;
+        memset(o, 0, 20 * sizeof(float));
+        ray_t r = mkray(V(c[0], c[1], c[2]), V(c[3], c[4], c[5]));
+        si_t si;
+        memset(&si, 0, sizeof(si));
+        si.p = V(c[6], c[7], c[8]);
+        si.n = V(c[9], c[10], c[11]);
+        si.ns = V(c[12], c[13], c[14]);
+        si.tangent = V(c[15], c[16], c[17]);
+        si.uv[0] = c[18];
+        si.uv[1] = c[19];
+        si.t = c[20];
+        si.mat = mid;
+        bxdf_t b = mat_scatter(&S, mid, &r, &si, c[21], c[22], c[23]);
+        if (b.ok) {
+            o[0] = 1;
+            o[1] = b.f.x; o[2] = b.f.y; o[3] = b.f.z;
+            o[4] = b.pdf;
+            o[5] = (float)b.flags;
+            o[6] = b.o.x; o[7] = b.o.y; o[8] = b.o.z;
+            o[9] = b.d.x; o[10] = b.d.y; o[11] = b.d.z;
+            ray_t sc = mkray(b.o, b.d);
+            v3 a = mat_f(&S, mid, &r, &si, sc.d);
+            o[12] = a.x; o[13] = a.y; o[14] = a.z;
+            o[15] = mat_pdf(&S, mid, &r, &si, sc.d);
+        }
+        v3 other = V(c[24], c[25], c[26]);
+        v3 a2 = mat_f(&S, mid, &r, &si, other);
+        o[16] = a2.x; o[17] = a2.y; o[18] = a2.z;
+        o[19] = mat_pdf(&S, mid, &r, &si, other);
+    }
+    return 0;
+}
+
+int oracle_lights(const pt_scene_desc* s, const float* in, uint32_t n, float* out) {
+    scene_t S;
+    scene_init(&S, s);
+    size_t k = 0;
+    for (uint32_t li = 0; li < s->n_lights; li++) {
+        const pt_light* l = &s->lights[li];
+        for (uint32_t i = 0; i < n; i++, k++) {
+            const float* c = in + 5 * (size_t)i;
+            float* o = out + 18 * k;
+            memset(o, 0, 18 * sizeof(float));
+            lsample_t ls = light_sample(&S, l, c[0], c[1]);
+            o[0] = ls.L.x; o[1] = ls.L.y; o[2] = ls.L.z;
+            o[3] = ls.si.p.x; o[4] = ls.si.p.y; o[5] = ls.si.p.z;
+            o[6] = ls.si.n.x; o[7] = ls.si.n.y; o[8] = ls.si.n.z;
+            o[9] = ls.si.uv[0]; o[10] = ls.si.uv[1];
+            o[11] = ls.dir.x; o[12] = ls.dir.y; o[13] = ls.dir.z;
+            if (!is_zero(ls.si.n)) {
+                v3 ref = V(c[2], c[3], c[4]);
+                ray_t sh = mkray(ref, normalize(sub(ls.si.p, ref)));
+                o[14] = light_pdf(&S, l, &ls.si, &sh);
+                v3 L = light_L(&S, l, &ls.si, &sh);
+                o[15] = L.x; o[16] = L.y; o[17] = L.z;
+            }
+        }
+    }
+    return 0;
+}

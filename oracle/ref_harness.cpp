@@ -1,0 +1,645 @@
+// TEST INFRASTRUCTURE ONLY — never part of the product path.
+//
+// Golden-vector generator driven by the reference's own public API
+// (marko176/PathTracing, mounted read-only at /root/reference).  It is compiled
+// from the reference sources where they lie, by oracle/Makefile, into
+// oracle/_ref/ref_harness (git-ignored).  It reads a scene recipe written by
+// pathtracing_amd.recipe (tests/golden/gen_golden.py), builds the scene with the
+// reference classes (Mesh -> GeometricPrimitive -> BLAS4 -> TLAS4, no Assimp;
+// SURVEY.md §6), and dumps fixtures that pin our CPU restatement (oracle/) and
+// the HIP path:
+//   bvh   : BVH4 clusters + root + primitive order (BVH.hpp:743-1017)
+//   info  : light list order, kinds, Power(), PMF (LightSampler.cpp:29-64)
+//   trace : closest-hit / any-hit records (BVH.hpp:1019-1211, Shape.cpp)
+//   li    : per-sample Integrator::Li under a deterministic counter-based sampler
+//           (Integrators.cpp:131-294); our own Sampler subclass (Sampler.hpp:9-26)
+//   film  : FilmTile::Add splat of those samples (Film.hpp:65-82)
+//   bsdf  : Material::scatter / calc_attenuation / PDF cases (Material.hpp)
+//   lights: Light::sample / PDF / L cases (Light.cpp)
+//   time  : TileIntegrator::Render timing with a ray-counting TLAS wrapper
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <cstdint>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+#include <map>
+#include <memory>
+#include <atomic>
+#include <thread>
+#include <chrono>
+#include <iostream>
+
+#include "Scene.hpp"
+#include "Mesh.hpp"
+#include "Material.hpp"
+#include "Primitive.hpp"
+#include "Light.hpp"
+#include "LightSampler.hpp"
+#include "Sampler.hpp"
+#include "Filter.hpp"
+#include "Film.hpp"
+#include "Camera.hpp"
+#include "Integrators.hpp"
+#include "Medium.hpp"
+#include "PhaseFunction.hpp"
+#include "Texture.hpp"
+
+// ---------------------------------------------------------------------------
+// Deterministic sample stream (the parity contract):
+//   key  = h(h(seed ^ h(pixel)) + sample)      h = PCG-RXS-M-XS 32-bit hash
+//   draw = (h(key + 0x9E3779B9 * dim) >> 8) * 2^-24, dim = 0,1,2,... per sample
+// ---------------------------------------------------------------------------
+static inline uint32_t pcg_hash(uint32_t v) {
+    uint32_t state = v * 747796405u + 2891336453u;
+    uint32_t word = ((state >> ((state >> 28u) + 4u)) ^ state) * 277803737u;
+    return (word >> 22u) ^ word;
+}
+static inline uint32_t stream_key(uint32_t seed, uint32_t pixel, uint32_t sample) {
+    return pcg_hash(pcg_hash(seed ^ pcg_hash(pixel)) + sample);
+}
+static inline float draw_float(uint32_t key, uint32_t dim) {
+    return (float)(pcg_hash(key + 0x9E3779B9u * dim) >> 8) * (1.0f / 16777216.0f);
+}
+
+class DetSampler : public Sampler {
+public:
+    DetSampler(unsigned spp, uint32_t seed, int width) : spp(spp), seed(seed), width(width) {}
+    unsigned int SamplesPerPixel() const override { return spp; }
+    void StartPixelSample(const glm::ivec2& p, int index) override {
+        key = stream_key(seed, (uint32_t)(p.y * width + p.x), (uint32_t)index);
+        dim = 0;
+    }
+    double get1D() override { return next(); }
+    glm::dvec2 get2D() override {
+        double a = next();
+        double b = next();
+        return {a, b};
+    }
+    glm::dvec2 getPixel2D() override { return get2D(); }
+    std::array<glm::vec2, 4> get2Dx4f() override {
+        std::array<glm::vec2, 4> r;
+        for (int i = 0; i < 4; i++) {
+            float a = next();
+            float b = next();
+            r[i] = {a, b};
+        }
+        return r;
+    }
+    std::shared_ptr<Sampler> Clone() const override { return std::make_shared<DetSampler>(spp, seed, width); }
+    uint32_t dims() const { return dim; }
+
+private:
+    float next() { return draw_float(key, dim++); }
+    unsigned spp;
+    uint32_t seed;
+    int width;
+    uint32_t key = 0;
+    uint32_t dim = 0;
+};
+
+// Expose protected BVH4 arrays (BVH.hpp:1214-1216, 392-394) — API use only.
+template <class T>
+struct Peek : BVH4<T> {
+    using BVH4<T>::BVH4;
+    const std::vector<BVH4_CLUSTER>& Nodes() const { return this->nodes; }
+    BVH4_NODE Root() const { return this->rootNode; }
+    const std::vector<T>& Prims() const { return this->primitives; }
+};
+using PeekTLAS = Peek<std::shared_ptr<Primitive>>;
+using PeekBLAS = Peek<GeometricPrimitive>;
+
+// Ray-counting wrapper used only by the `time` command.
+static std::atomic<uint64_t> g_closest{0}, g_any{0};
+struct CountingPrim : Primitive {
+    std::shared_ptr<Primitive> inner;
+    explicit CountingPrim(std::shared_ptr<Primitive> p) : inner(std::move(p)) {}
+    AABB BoundingBox() const override { return inner->BoundingBox(); }
+    bool IntersectPred(const Ray& r, float max) const override {
+        thread_local uint64_t n = 0;
+        if ((++n & 255) == 0) g_any.fetch_add(256, std::memory_order_relaxed);
+        return inner->IntersectPred(r, max);
+    }
+    bool Intersect(const Ray& r, SurfaceInteraction& si, float max) const override {
+        thread_local uint64_t n = 0;
+        if ((++n & 255) == 0) g_closest.fetch_add(256, std::memory_order_relaxed);
+        return inner->Intersect(r, si, max);
+    }
+    std::vector<std::shared_ptr<Light>> GetLights() const override { return inner->GetLights(); }
+};
+
+// ---------------------------------------------------------------------------
+// Recipe
+// ---------------------------------------------------------------------------
+struct World {
+    std::string dir;
+    std::map<int, std::shared_ptr<Texture>> tex;
+    std::map<int, std::shared_ptr<Material>> mat;
+    std::map<int, std::shared_ptr<Medium>> med;
+    std::map<int, std::shared_ptr<Mesh>> mesh;
+    std::vector<std::shared_ptr<Primitive>> top;          // Add order
+    std::vector<std::shared_ptr<PeekBLAS>> blas;          // per model, in order
+    std::vector<std::shared_ptr<PeekTLAS>> blasPtr;       // pointer twin (prim order)
+    std::vector<std::vector<std::shared_ptr<Primitive>>> blasItems;  // originals, per model
+    std::vector<int> blasTop;                              // top index of each model
+    std::map<const Light*, std::string> lightOwner;       // "top:i" or "tri:model:k"
+    std::map<const Material*, int> matId;
+    std::vector<std::shared_ptr<InfiniteLight>> inf;
+    std::vector<std::shared_ptr<Light>> extra;
+    std::string samplerKind = "uniform";
+    glm::vec3 camFrom{0}, camAt{0, 0, -1};
+    float fov = 1.0f, focusAngle = 0, focusDist = 0;
+    int W = 64, H = 64;
+    std::shared_ptr<Filter> filter = std::make_shared<MitchellFilter>();
+    std::string integ = "path";
+    int maxDepth = 8;
+    uint32_t seed = 1;
+    unsigned spp = 1;
+
+    std::shared_ptr<Scene> scene;
+    std::shared_ptr<PeekTLAS> tlasPeek;                    // same build as the scene TLAS
+    std::shared_ptr<LightSampler> ls;
+    std::shared_ptr<Film> film;
+    std::shared_ptr<Camera> camera;
+};
+
+static std::shared_ptr<Texture> T(World& w, int id) { return id < 0 ? nullptr : w.tex.at(id); }
+
+static void read_recipe(World& w, const std::string& path) {
+    std::ifstream in(path);
+    if (!in) { fprintf(stderr, "cannot open %s\n", path.c_str()); exit(2); }
+    w.dir = path.substr(0, path.find_last_of('/') + 1);
+    std::string line;
+    while (std::getline(in, line)) {
+        std::istringstream s(line);
+        std::string k;
+        if (!(s >> k) || k[0] == '#') continue;
+        if (k == "ptscene") continue;
+        if (k == "texture") {
+            int id; std::string kind; s >> id >> kind;
+            if (kind == "solid") {
+                float r, g, b, sr, sg, sb; s >> r >> g >> b >> sr >> sg >> sb;
+                w.tex[id] = std::make_shared<SolidColor>(glm::vec3(r, g, b), glm::vec3(sr, sg, sb));
+            } else if (kind == "checker") {
+                int a, b; float sx, sy, sr, sg, sb; s >> a >> b >> sx >> sy >> sr >> sg >> sb;
+                w.tex[id] = std::make_shared<CheckerTexture>(w.tex.at(a), w.tex.at(b), glm::vec2(sx, sy), glm::vec3(sr, sg, sb));
+            } else if (kind == "image") {
+                std::string rel; int gamma; float sr, sg, sb; s >> rel >> gamma >> sr >> sg >> sb;
+                w.tex[id] = std::make_shared<ImageTexture>(w.dir + rel, gamma != 0, glm::vec3(sr, sg, sb));
+            }
+        } else if (k == "material") {
+            int id; std::string kind; s >> id >> kind;
+            if (kind == "diffuse") {
+                int tx, nm, ro, me, al, mode; float cut; s >> tx >> nm >> ro >> me >> al >> mode >> cut;
+                auto m = std::make_shared<MicrofacetDiffuse>(T(w, tx), T(w, nm), T(w, ro), T(w, me), T(w, al));
+                if (mode >= 0) m->setAlphaTester(AlphaTester((AlphaMode)mode, cut));
+                w.mat[id] = m;
+            } else if (kind == "dielectric") {
+                float ri; int tx, nm, ro, al, mode; float cut; s >> ri >> tx >> nm >> ro >> al >> mode >> cut;
+                auto m = std::make_shared<MicrofacetDielectric>(ri, T(w, tx), T(w, nm), T(w, ro), T(w, al));
+                if (mode >= 0) m->setAlphaTester(AlphaTester((AlphaMode)mode, cut));
+                w.mat[id] = m;
+            } else if (kind == "thin") {
+                float ri; int tx; s >> ri >> tx;
+                w.mat[id] = std::make_shared<ThinDielectric>(ri, T(w, tx));
+            } else if (kind == "conductor") {
+                float r, g, b; s >> r >> g >> b;
+                w.mat[id] = std::make_shared<SpecularConductor>(glm::vec3(r, g, b));
+            }
+            w.matId[w.mat[id].get()] = id;
+        } else if (k == "medium") {
+            int id; float a0, a1, a2, s0, s1, s2, g, d; s >> id >> a0 >> a1 >> a2 >> s0 >> s1 >> s2 >> g >> d;
+            w.med[id] = std::make_shared<HomogeneusMedium>(glm::vec3(a0, a1, a2), glm::vec3(s0, s1, s2),
+                                                           std::make_shared<HenyeyGreenstein>(g), d);
+        } else if (k == "quad" || k == "sphere") {
+            int pid; s >> pid;
+            std::shared_ptr<Shape> shape;
+            if (k == "quad") {
+                float q[9]; for (float& x : q) s >> x;
+                shape = std::make_shared<QuadShape>(glm::vec3(q[0], q[1], q[2]), glm::vec3(q[3], q[4], q[5]), glm::vec3(q[6], q[7], q[8]));
+            } else {
+                float c[4]; for (float& x : c) s >> x;
+                shape = std::make_shared<SphereShape>(glm::vec3(c[0], c[1], c[2]), c[3]);
+            }
+            int m, em, one, md; s >> m >> em >> one >> md;
+            std::shared_ptr<AreaLight> area;
+            if (em >= 0) area = std::make_shared<AreaLight>(shape, w.tex.at(em), one != 0);
+            auto prim = std::make_shared<GeometricPrimitive>(shape, m < 0 ? nullptr : w.mat.at(m), area,
+                                                             md < 0 ? nullptr : w.med.at(md));
+            if (area) w.lightOwner[area.get()] = "top:" + std::to_string(w.top.size());
+            w.top.push_back(prim);
+        } else if (k == "mesh") {
+            int id, nv, nt, ht, m, em, md; std::string rel;
+            s >> id >> rel >> nv >> nt >> ht >> m >> em >> md;
+            std::ifstream f(w.dir + rel, std::ios::binary);
+            if (!f) { fprintf(stderr, "cannot open mesh %s\n", rel.c_str()); exit(2); }
+            std::vector<uint32_t> idx(3 * (size_t)nt);
+            std::vector<glm::vec3> v(nv), n(nv), tg;
+            std::vector<glm::vec2> uv(nv);
+            f.read((char*)idx.data(), idx.size() * 4);
+            f.read((char*)v.data(), v.size() * 12);
+            f.read((char*)n.data(), n.size() * 12);
+            f.read((char*)uv.data(), uv.size() * 8);
+            if (ht) { tg.resize(nv); f.read((char*)tg.data(), tg.size() * 12); }
+            w.mesh[id] = std::make_shared<Mesh>(idx, v, tg, n, uv, m < 0 ? nullptr : w.mat.at(m),
+                                                em < 0 ? nullptr : w.tex.at(em), md < 0 ? nullptr : w.med.at(md));
+        } else if (k == "model") {
+            // Model::BuildBlas<BLAS4> (Model.hpp:43-60) without Assimp: one
+            // GeometricPrimitive per triangle, an AreaLight per emissive one.
+            int pid, nm; s >> pid >> nm;
+            std::vector<GeometricPrimitive> prims;
+            std::vector<std::shared_ptr<Primitive>> ptrs;
+            int tri = 0;
+            for (int i = 0; i < nm; i++) {
+                int mid; s >> mid;
+                auto& me = w.mesh.at(mid);
+                for (uint32_t j = 0; j < me->GetTriangleCount(); j++, tri++) {
+                    std::shared_ptr<Shape> shape(me->GetControlPtr(), me->GetShape(j));
+                    std::shared_ptr<AreaLight> area = me->GetEmissiveTexture() != nullptr
+                                                          ? std::make_shared<AreaLight>(shape, me->GetEmissiveTexture())
+                                                          : nullptr;
+                    if (area) {
+                        area->PreProcess({});
+                        if (area->Power() <= std::numeric_limits<float>::epsilon()) area = nullptr;
+                    }
+                    if (area) w.lightOwner[area.get()] = "tri:" + std::to_string(w.blas.size()) + ":" + std::to_string(tri);
+                    prims.emplace_back(shape, me->GetMaterial(), area, me->GetMedium());
+                    ptrs.push_back(std::make_shared<GeometricPrimitive>(prims.back()));
+                }
+            }
+            auto b = std::make_shared<PeekBLAS>(prims);
+            w.blas.push_back(b);
+            w.blasPtr.push_back(std::make_shared<PeekTLAS>(ptrs));
+            w.blasItems.push_back(ptrs);
+            w.blasTop.push_back((int)w.top.size());
+            w.top.push_back(b);
+        } else if (k == "infinite") {
+            std::string kind; s >> kind;
+            if (kind == "uniform") {
+                float r, g, b; s >> r >> g >> b;
+                w.inf.push_back(std::make_shared<UniformInfiniteLight>(glm::vec3(r, g, b)));
+            } else if (kind == "sky") {
+                float c[7]; for (float& x : c) s >> x;
+                glm::vec3 c0(c[0], c[1], c[2]), c1(c[3], c[4], c[5]);
+                float sc = c[6];
+                // main.cpp:292-295 gradient, parameterised
+                auto fn = [c0, c1, sc](const Ray& ray) {
+                    float a = 0.5f * (ray.dir.y + 1.0f);
+                    return sc * ((1.0f - a) * c0 + a * c1);
+                };
+                w.inf.push_back(std::make_shared<FunctionInfiniteLight>(fn));
+            }
+            w.lightOwner[w.inf.back().get()] = "inf:" + std::to_string(w.inf.size() - 1);
+        } else if (k == "extralight") {
+            std::string kind; float a, b, c, r, g, bb; s >> kind >> a >> b >> c >> r >> g >> bb;
+            if (kind == "distant") w.extra.push_back(std::make_shared<DistantLight>(glm::vec3(a, b, c), glm::vec3(r, g, bb)));
+            else w.extra.push_back(std::make_shared<PointLight>(glm::vec3(a, b, c), glm::vec3(r, g, bb)));
+            w.lightOwner[w.extra.back().get()] = "extra:" + std::to_string(w.extra.size() - 1);
+        } else if (k == "lightsampler") {
+            s >> w.samplerKind;
+        } else if (k == "camera") {
+            s >> w.camFrom.x >> w.camFrom.y >> w.camFrom.z >> w.camAt.x >> w.camAt.y >> w.camAt.z >> w.fov >> w.W >> w.H >> w.focusAngle >> w.focusDist;
+        } else if (k == "filter") {
+            std::string kind; float rx, ry; s >> kind >> rx >> ry;
+            if (kind == "mitchell") { double b, c; s >> b >> c; w.filter = std::make_shared<MitchellFilter>(glm::vec2(rx, ry), b, c); }
+            else if (kind == "box") w.filter = std::make_shared<BoxFilter>(glm::vec2(rx, ry));
+            else { double sg; s >> sg; w.filter = std::make_shared<GaussianFilter>(glm::vec2(rx, ry), sg); }
+        } else if (k == "integrator") {
+            s >> w.integ >> w.maxDepth;
+        } else if (k == "sampler") {
+            s >> w.seed >> w.spp;
+        }
+    }
+}
+
+static void build_world(World& w, bool counting = false) {
+    w.scene = std::make_shared<Scene>();
+    if (counting) {
+        auto inner = std::make_shared<TLAS4>(w.top);
+        w.scene->Add(std::make_shared<CountingPrim>(inner));
+    } else {
+        for (auto& p : w.top) w.scene->Add(p);
+    }
+    for (auto& l : w.inf) w.scene->infiniteLights.push_back(l);
+    w.scene->BuildTlas<TLAS4>();
+    w.tlasPeek = std::make_shared<PeekTLAS>(w.top);  // identical build (depends on bboxes only)
+    if (w.samplerKind == "power") w.ls = std::make_shared<PowerLightSampler>();
+    else w.ls = std::make_shared<UniformLightSampler>();
+    w.ls->Add(w.scene->GetLights());
+    for (auto& l : w.extra) w.ls->Add(l);
+    w.ls->PreProcess(w.scene->BoundingBox());
+    w.film = std::make_shared<Film>(glm::ivec2{w.W, w.H}, w.filter);
+    if (w.focusAngle != 0 && w.focusDist != 0)
+        w.camera = std::make_shared<Camera>(w.camFrom, w.camAt, w.fov, w.film, w.focusAngle, w.focusDist);
+    else
+        w.camera = std::make_shared<Camera>(w.camFrom, w.camAt, w.fov, w.film);
+}
+
+static std::shared_ptr<Integrator> make_integrator(World& w, std::shared_ptr<Sampler> s) {
+    if (w.integ == "simple") return std::make_shared<SimplePathIntegrator>(w.scene, w.camera, s, w.maxDepth);
+    return std::make_shared<PathIntegrator>(w.scene, w.camera, s, w.ls, w.maxDepth);
+}
+
+template <class V>
+static void wr(const std::string& path, const std::vector<V>& v) {
+    FILE* f = fopen(path.c_str(), "wb");
+    if (!f) { fprintf(stderr, "cannot write %s\n", path.c_str()); exit(2); }
+    if (!v.empty()) fwrite(v.data(), sizeof(V), v.size(), f);
+    fclose(f);
+}
+template <class V>
+static std::vector<V> rd(const std::string& path) {
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) { fprintf(stderr, "cannot read %s\n", path.c_str()); exit(2); }
+    fseek(f, 0, SEEK_END); long n = ftell(f); fseek(f, 0, SEEK_SET);
+    std::vector<V> v(n / sizeof(V));
+    if (!v.empty() && fread(v.data(), sizeof(V), v.size(), f) != v.size()) exit(3);
+    fclose(f);
+    return v;
+}
+
+// --- bvh: clusters raw (128 B), root (8 B), primitive order (top index or tri index)
+template <class P, class Items>
+static void dump_bvh(const std::string& out, const P& peek, const Items& originals, const std::shared_ptr<PeekTLAS>& twin) {
+    wr(out + ".clusters.bin", peek.Nodes());
+    std::vector<BVH4_NODE> root{peek.Root()};
+    wr(out + ".root.bin", root);
+    std::vector<uint32_t> order;
+    for (auto& p : twin->Prims()) {
+        uint32_t k = 0;
+        for (; k < originals.size(); k++) if (originals[k] == p) break;
+        order.push_back(k);
+    }
+    wr(out + ".order.bin", order);
+}
+
+static void cmd_bvh(World& w, const std::string& out) {
+    dump_bvh(out + ".tlas", *w.tlasPeek, w.top, w.tlasPeek);
+    for (size_t i = 0; i < w.blas.size(); i++) {
+        // the pointer twin is built from the same boxes, so its order is the BLAS order
+        auto& twin = w.blasPtr[i];
+        const auto& a = w.blas[i]->Nodes();
+        const auto& b = twin->Nodes();
+        if (a.size() != b.size() || memcmp(a.data(), b.data(), a.size() * sizeof(BVH4_CLUSTER)) != 0) {
+            fprintf(stderr, "twin BVH differs\n"); exit(4);
+        }
+        dump_bvh(out + ".blas" + std::to_string(i), *w.blas[i], w.blasItems[i], twin);
+    }
+}
+
+// --- info: lights in sampler-input order
+static std::string owner(World& w, const Light* l) {
+    auto it = w.lightOwner.find(l);
+    return it == w.lightOwner.end() ? "?" : it->second;
+}
+static void cmd_info(World& w, const std::string& out) {
+    FILE* f = fopen((out + ".lights.txt").c_str(), "w");
+    auto all = w.scene->GetLights();
+    for (auto& l : w.extra) all.push_back(l);
+    for (auto& l : all) {
+        fprintf(f, "%s %d %.9g %.9g\n", owner(w, l.get()).c_str(), (int)l->isDelta(), (double)l->Power(), (double)w.ls->PMF(l));
+    }
+    // Sample(u) on a grid of u
+    for (int i = 0; i <= 64; i++) {
+        float u = i / 64.0f;
+        if (i == 64) u = 0.99999994f;
+        auto l = w.ls->Sample(u);
+        fprintf(f, "sample %.9g %s\n", (double)u, l ? owner(w, l.get()).c_str() : "null");
+    }
+    fclose(f);
+}
+
+// --- trace: rays file f32 [n][7] (o.xyz, d.xyz, tmax) -> closest-hit + any-hit
+static void cmd_trace(World& w, const std::string& out, const std::string& raysPath) {
+    auto raw = rd<float>(raysPath);
+    size_t n = raw.size() / 7;
+    std::vector<float> rec(n * 16, 0.0f);
+    std::vector<int32_t> ids(n * 3, -1);
+    std::vector<uint8_t> anyhit(n, 0);
+    std::map<const Light*, int> lightIdx;
+    {
+        auto all = w.scene->GetLights();
+        for (size_t i = 0; i < all.size(); i++) lightIdx[all[i].get()] = (int)i;
+    }
+    for (size_t i = 0; i < n; i++) {
+        const float* r = &raw[i * 7];
+        Ray ray(glm::vec3(r[0], r[1], r[2]), glm::vec3(r[3], r[4], r[5]));
+        SurfaceInteraction si;
+        bool hit = w.scene->Intersect(ray, si, r[6]);
+        float* o = &rec[i * 16];
+        o[0] = hit ? 1.0f : 0.0f;
+        if (hit) {
+            o[1] = si.t;
+            o[2] = si.p.x; o[3] = si.p.y; o[4] = si.p.z;
+            o[5] = si.n.x; o[6] = si.n.y; o[7] = si.n.z;
+            o[8] = si.ns.x; o[9] = si.ns.y; o[10] = si.ns.z;
+            o[11] = si.uv.x; o[12] = si.uv.y;
+            o[13] = si.tangent.x; o[14] = si.tangent.y; o[15] = si.tangent.z;
+            ids[i * 3 + 0] = si.mat ? w.matId[si.mat.get()] : -1;
+            ids[i * 3 + 1] = si.AreaLight ? lightIdx[si.AreaLight.get()] : -1;
+            ids[i * 3 + 2] = si.medium ? 1 : 0;
+        }
+        anyhit[i] = w.scene->IntersectPred(ray, r[6]) ? 1 : 0;
+    }
+    wr(out + ".hits.bin", rec);
+    wr(out + ".ids.bin", ids);
+    wr(out + ".any.bin", anyhit);
+}
+
+// --- li: per-sample radiance under the deterministic stream
+struct SampleRec { double px, py; float L[3]; uint32_t dims; };
+static std::vector<SampleRec> run_li(World& w, int x0, int y0, int x1, int y1, unsigned spp) {
+    std::vector<SampleRec> out;
+    auto sampler = std::make_shared<DetSampler>(spp, w.seed, w.W);
+    auto integ = make_integrator(w, sampler);
+    for (int y = y0; y < y1; y++)
+        for (int x = x0; x < x1; x++)
+            for (unsigned s = 0; s < spp; s++) {
+                sampler->StartPixelSample({x, y}, (int)s);
+                glm::dvec2 p = glm::dvec2{x, y} + sampler->getPixel2D();
+                float time = (float)sampler->get1D();
+                glm::dvec2 lens = sampler->get2D();
+                Ray ray = w.camera->GenerateRay(p, time, lens);
+                ray.time = 0;  // shutter is uninitialised in the reference
+                glm::vec3 L = integ->Li(ray);
+                out.push_back({p.x, p.y, {L.x, L.y, L.z}, sampler->dims()});
+            }
+    return out;
+}
+static void cmd_li(World& w, const std::string& out, int x0, int y0, int x1, int y1, unsigned spp) {
+    auto recs = run_li(w, x0, y0, x1, y1, spp);
+    wr(out + ".li.bin", recs);
+}
+
+// --- film: FilmTile::Add over the whole film of the same samples (Film.hpp:65-82)
+static void cmd_film(World& w, const std::string& out, unsigned spp) {
+    auto recs = run_li(w, 0, 0, w.W, w.H, spp);
+    Bounds2i all{{0, 0}, {w.W, w.H}};
+    FilmTile tile = w.film->GetFilmTile(all);
+    for (auto& r : recs) tile.Add({r.px, r.py}, glm::dvec3(r.L[0], r.L[1], r.L[2]));
+    std::vector<double> acc((size_t)w.W * w.H * 4);
+    for (int y = 0; y < w.H; y++)
+        for (int x = 0; x < w.W; x++) {
+            const FilmTilePixel& p = tile.At({x, y});
+            double* o = &acc[((size_t)y * w.W + x) * 4];
+            o[0] = p.RGB.x; o[1] = p.RGB.y; o[2] = p.RGB.z; o[3] = p.weight;
+        }
+    wr(out + ".film.bin", acc);
+    // filter weights table on a grid (F6)
+    std::vector<double> fw;
+    for (int j = 0; j <= 32; j++)
+        for (int i = 0; i <= 32; i++) {
+            glm::vec2 p(-2.0f + 4.0f * i / 32.0f, -2.0f + 4.0f * j / 32.0f);
+            fw.push_back(w.filter->Evaluate(p));
+        }
+    fw.push_back(w.filter->Integral());
+    wr(out + ".filter.bin", fw);
+}
+
+// --- bsdf: Material cases (Material.hpp:200-673). Inputs f32 [n][24]:
+// incoming o(3) d(3) | si.p(3) n(3) ns(3) tangent(3) uv(2) t(1) | u(1) uv(2)
+struct BsdfOut { float ok, f[3], pdf, flags, o[3], d[3], att[3], pdfS, att2[3], pdf2; };
+static void cmd_bsdf(World& w, const std::string& out, const std::string& inPath, int matId) {
+    auto raw = rd<float>(inPath);
+    size_t n = raw.size() / 27;
+    auto& m = w.mat.at(matId);
+    std::vector<BsdfOut> res(n);
+    for (size_t i = 0; i < n; i++) {
+        const float* c = &raw[i * 27];
+        Ray in(glm::vec3(c[0], c[1], c[2]), glm::vec3(c[3], c[4], c[5]));
+        SurfaceInteraction si;
+        si.p = {c[6], c[7], c[8]};
+        si.n = {c[9], c[10], c[11]};
+        si.ns = {c[12], c[13], c[14]};
+        si.tangent = {c[15], c[16], c[17]};
+        si.uv = {c[18], c[19]};
+        si.t = c[20];
+        float u = c[21];
+        glm::vec2 uv(c[22], c[23]);
+        glm::vec3 other(c[24], c[25], c[26]);
+        Ray sc;
+        auto b = m->scatter(in, si, sc, u, uv);
+        BsdfOut& o = res[i];
+        memset(&o, 0, sizeof(o));
+        if (b) {
+            o.ok = 1;
+            o.f[0] = b->f.x; o.f[1] = b->f.y; o.f[2] = b->f.z;
+            o.pdf = b->pdf; o.flags = (float)b->flags;
+            o.o[0] = sc.origin.x; o.o[1] = sc.origin.y; o.o[2] = sc.origin.z;
+            o.d[0] = sc.dir.x; o.d[1] = sc.dir.y; o.d[2] = sc.dir.z;
+            glm::vec3 a = m->calc_attenuation(in, si, sc);
+            o.att[0] = a.x; o.att[1] = a.y; o.att[2] = a.z;
+            o.pdfS = m->PDF(in, si, sc);
+        }
+        Ray r2(si.p, other);
+        glm::vec3 a2 = m->calc_attenuation(in, si, r2);
+        o.att2[0] = a2.x; o.att2[1] = a2.y; o.att2[2] = a2.z;
+        o.pdf2 = m->PDF(in, si, r2);
+    }
+    wr(out + ".bsdf" + std::to_string(matId) + ".bin", res);
+}
+
+// --- lights: for each light in sampler-input order and each uv: sample + PDF + L
+struct LightOut { float L[3], p[3], n[3], uv[2], dir[3], pdf, Lsh[3]; };
+static void cmd_lights(World& w, const std::string& out, const std::string& inPath) {
+    auto raw = rd<float>(inPath);  // [n][5]: uv(2), ref point(3)
+    size_t n = raw.size() / 5;
+    auto all = w.scene->GetLights();
+    for (auto& l : w.extra) all.push_back(l);
+    std::vector<LightOut> res;
+    for (auto& l : all) {
+        for (size_t i = 0; i < n; i++) {
+            const float* c = &raw[i * 5];
+            LightSample ls = l->sample({c[0], c[1]}, 0.0f);
+            LightOut o;
+            memset(&o, 0, sizeof(o));
+            o.L[0] = ls.L.x; o.L[1] = ls.L.y; o.L[2] = ls.L.z;
+            o.p[0] = ls.interaction.p.x; o.p[1] = ls.interaction.p.y; o.p[2] = ls.interaction.p.z;
+            o.n[0] = ls.interaction.n.x; o.n[1] = ls.interaction.n.y; o.n[2] = ls.interaction.n.z;
+            o.uv[0] = ls.interaction.uv.x; o.uv[1] = ls.interaction.uv.y;
+            o.dir[0] = ls.dir.x; o.dir[1] = ls.dir.y; o.dir[2] = ls.dir.z;
+            glm::vec3 ref(c[2], c[3], c[4]);
+            if (!ls.isDeltaInteraction()) {
+                Ray sh(ref, glm::normalize(ls.interaction.p - ref));
+                o.pdf = l->PDF(ls.interaction, sh);
+                glm::vec3 L = l->L(ls.interaction, sh);
+                o.Lsh[0] = L.x; o.Lsh[1] = L.y; o.Lsh[2] = L.z;
+            }
+            res.push_back(o);
+        }
+    }
+    wr(out + ".lightsamples.bin", res);
+}
+
+// --- time: Render(threads) with counting, and a fixed-SPP Li tile loop
+static void cmd_time(World& w, int threads, unsigned spp, const std::string& mode) {
+    double secs = 0;
+    if (mode == "render") {
+        auto sampler = std::make_shared<UniformSampler>(spp);
+        auto integ = make_integrator(w, sampler);
+        g_closest = 0; g_any = 0;
+        auto t0 = std::chrono::steady_clock::now();
+        integ->Render(threads);
+        secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    } else {
+        std::atomic<int> next{0};
+        int tiles = ((w.W + 31) / 32) * ((w.H + 31) / 32);
+        g_closest = 0; g_any = 0;
+        auto t0 = std::chrono::steady_clock::now();
+        std::vector<std::thread> ts;
+        for (int t = 0; t < threads; t++)
+            ts.emplace_back([&]() {
+                auto sampler = std::make_shared<DetSampler>(spp, w.seed, w.W);
+                auto integ = make_integrator(w, sampler);
+                int tile;
+                while ((tile = next.fetch_add(1)) < tiles) {
+                    int tx = tile % ((w.W + 31) / 32), ty = tile / ((w.W + 31) / 32);
+                    for (int y = ty * 32; y < std::min(ty * 32 + 32, w.H); y++)
+                        for (int x = tx * 32; x < std::min(tx * 32 + 32, w.W); x++)
+                            for (unsigned s = 0; s < spp; s++) {
+                                sampler->StartPixelSample({x, y}, (int)s);
+                                glm::dvec2 p = glm::dvec2{x, y} + sampler->getPixel2D();
+                                float time = (float)sampler->get1D();
+                                Ray ray = w.camera->GenerateRay(p, time, sampler->get2D());
+                                ray.time = 0;
+                                volatile glm::vec3 L = integ->Li(ray);
+                                (void)L;
+                            }
+                }
+            });
+        for (auto& t : ts) t.join();
+        secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+    double rays = (double)g_closest.load() + (double)g_any.load();
+    printf("{\"mode\":\"%s\",\"threads\":%d,\"spp\":%u,\"seconds\":%.6f,\"closest\":%llu,\"any\":%llu,\"mrays_per_s\":%.4f}\n",
+           mode.c_str(), threads, spp, secs, (unsigned long long)g_closest.load(), (unsigned long long)g_any.load(),
+           rays / secs / 1e6);
+}
+
+int main(int argc, char** argv) {
+    if (argc < 4) {
+        fprintf(stderr, "usage: ref_harness <recipe> <cmd> <out> [args]\n");
+        return 2;
+    }
+    std::cout.setstate(std::ios::failbit);  // silence the reference's progress/log prints
+    World w;
+    read_recipe(w, argv[1]);
+    std::string cmd = argv[2], out = argv[3];
+    build_world(w, cmd == "time");
+    if (cmd == "bvh") cmd_bvh(w, out);
+    else if (cmd == "info") cmd_info(w, out);
+    else if (cmd == "trace") cmd_trace(w, out, argv[4]);
+    else if (cmd == "li") {
+        int x0 = 0, y0 = 0, x1 = w.W, y1 = w.H;
+        unsigned spp = w.spp;
+        if (argc >= 9) { x0 = atoi(argv[4]); y0 = atoi(argv[5]); x1 = atoi(argv[6]); y1 = atoi(argv[7]); spp = atoi(argv[8]); }
+        cmd_li(w, out, x0, y0, x1, y1, spp);
+    } else if (cmd == "film") cmd_film(w, out, w.spp);
+    else if (cmd == "bsdf") cmd_bsdf(w, out, argv[4], atoi(argv[5]));
+    else if (cmd == "lights") cmd_lights(w, out, argv[4]);
+    else if (cmd == "time") cmd_time(w, atoi(argv[4]), (unsigned)atoi(argv[5]), argc > 6 ? argv[6] : "render");
+    else { fprintf(stderr, "unknown cmd %s\n", cmd.c_str()); return 2; }
+    return 0;
+}

@@ -1,0 +1,116 @@
+// Device-side scene layout and shared math for the CDNA4 wavefront tracer.
+// All arithmetic follows the reference's float semantics (see DESIGN.md
+// "Numerics"): correctly rounded division and sqrt (__builtin_sqrtf lowers to
+// the corrected v_sqrt sequence on gfx950), glm operand order.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pt_api.h"
+
+#define PT_EPS 0.00001f  // shadowEpsilon (AABB.hpp:6)
+#define PT_FLT_EPS 1.19209290e-07f
+#define PT_PI 3.14159265358979323846f
+#define PT_INV_PI 0.318309886183790671538f
+
+// ---- device BVH4 node: the reference cluster's boxes (BVH.hpp:45-60) with
+// child references re-encoded for a stack of 32-bit entries, and the octant
+// child order (BVH.hpp:562-738) precomputed per node.  128 bytes, 128-aligned.
+#define REF_EMPTY 0xFFFFFFFFu
+#define REF_LEAF 0x80000000u
+struct alignas(128) DevCluster {
+    float4 xmin, xmax, ymin, ymax, zmin, zmax;  // 4 children per component
+    uint32_t child[4];                          // REF_EMPTY | REF_LEAF|slot | cluster
+    uint32_t order[2];                          // 8 octants x permutation byte
+    uint32_t pad[2];
+};
+static_assert(sizeof(DevCluster) == 128, "cluster layout");
+
+// ---- primitive slot geometry (48 B): what a leaf test reads.
+// a = v0|Q|center + flags, b = e1|u|radius + index, c = e2|v
+#define GF_KIND 3u
+#define GF_LAST 4u        // last primitive of its leaf
+#define GF_ALPHA 8u       // closest hit: run the material alpha test
+#define GF_PRED_GLM 16u   // any hit: material HasAlpha() -> full Intersect + Alpha
+struct alignas(16) DevGeom {
+    float4 a, b, c;
+};
+
+struct DevPrimInfo {
+    int32_t material, light, medium;
+    uint32_t index;  // triangle / quad / sphere id, BLAS root ref
+};
+
+struct DevScene {
+    const DevCluster* nodes;
+    const DevGeom* geom;
+    const DevPrimInfo* info;
+    uint32_t root;
+    uint32_t n_prims;
+    const uint4* tri;          // i0, i1, i2, flags
+    const float* positions;    // 3 per vertex
+    const float* normals;
+    const float* uvs;          // 2 per vertex
+    const float* tangents;
+    const pt_quad* quads;
+    const pt_sphere* spheres;
+    const pt_material* materials;
+    const pt_texture* textures;
+    const pt_image* images;
+    const uint8_t* texels;
+    uint64_t n_texel_bytes;
+    const pt_light* lights;
+    uint32_t n_lights;
+    uint32_t light_sampler;
+    const uint32_t* sampler_lights;
+    const float* sampler_cdf;  // running float sums (PowerLightSampler::Sample order)
+    uint32_t n_sampler_lights;
+    float sampler_total;
+    const uint32_t* infinite_lights;
+    uint32_t n_infinite_lights;
+};
+
+// ------------------------------------------------------------------ float3 helpers
+struct f3 {
+    float x, y, z;
+};
+__device__ __forceinline__ f3 F3(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return F3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return F3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 operator*(f3 a, f3 b) { return F3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ f3 operator*(f3 a, float s) { return F3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ f3 operator*(float s, f3 a) { return F3(s * a.x, s * a.y, s * a.z); }
+__device__ __forceinline__ f3 operator/(f3 a, float s) { return F3(a.x / s, a.y / s, a.z / s); }
+__device__ __forceinline__ f3 operator-(f3 a) { return F3(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+    return F3(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
+}
+__device__ __forceinline__ float csqrt(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ float length(f3 a) { return csqrt(dot(a, a)); }
+__device__ __forceinline__ f3 normalize(f3 a) { return a * (1.0f / csqrt(dot(a, a))); }
+__device__ __forceinline__ bool is_zero(f3 a) { return a.x == 0.0f && a.y == 0.0f && a.z == 0.0f; }
+__device__ __forceinline__ f3 reflect(f3 I, f3 N) { return I - (N * dot(N, I)) * 2.0f; }
+__device__ __forceinline__ f3 refract(f3 I, f3 N, float eta) {
+    float d = dot(N, I);
+    float k = 1.0f - eta * eta * (1.0f - d * d);
+    if (k >= 0.0f) return eta * I - (eta * d + csqrt(k)) * N;
+    return F3(0, 0, 0);
+}
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+__device__ __forceinline__ float smax(float a, float b) { return a < b ? b : a; }  // std::max
+__device__ __forceinline__ f3 xyz(float4 v) { return F3(v.x, v.y, v.z); }
+
+// ------------------------------------------------------------------ sample stream
+__device__ __forceinline__ uint32_t pcg_hash(uint32_t v) {
+    uint32_t state = v * 747796405u + 2891336453u;
+    uint32_t word = ((state >> ((state >> 28u) + 4u)) ^ state) * 277803737u;
+    return (word >> 22u) ^ word;
+}
+__device__ __forceinline__ uint32_t stream_key(uint32_t seed, uint32_t pixel, uint32_t sample) {
+    return pcg_hash(pcg_hash(seed ^ pcg_hash(pixel)) + sample);
+}
+__device__ __forceinline__ float draw(uint32_t key, uint32_t dim) {
+    return (float)(pcg_hash(key + 0x9E3779B9u * dim) >> 8) * (1.0f / 16777216.0f);
+}

@@ -1,0 +1,445 @@
+// Wavefront path tracer kernels for gfx950 (CDNA4).
+//
+// One iteration of the persistent wavefront (host loop in pt_runtime.hip):
+//   k_closest  closest-hit traversal of every active path's ray
+//   k_shade    one body of PathIntegrator::Li / SimplePathIntegrator::Li
+//              (Integrators.cpp:131-294): miss -> infinite lights, emission
+//              with MIS, scatter, NEE light sample -> shadow queue, RR;
+//              continuing paths -> next active queue, finished -> done queue
+//   k_shadow   any-hit of the NEE rays; unoccluded -> contribution added
+//   k_finish   finished paths write their sample radiance, and the slot is
+//              refilled with the next camera sample (Camera::GenerateRay)
+//   k_gather   after a sample chunk: every pixel gathers the Mitchell/box/
+//              Gaussian-weighted samples of its neighbourhood (FilmTile::Add,
+//              Film.hpp:65-82) in float64 — deterministic, no atomics.
+// Queue appends are wave-aggregated: one atomic per wave (__ballot/__popcll).
+#include "pt_kernels.h"
+
+// ------------------------------------------------------------------ wave helpers
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
+    const uint64_t mask = __ballot(pred);
+    if (mask == 0) return 0;
+    const uint32_t lane = __lane_id();
+    const int leader = __ffsll((unsigned long long)mask) - 1;
+    uint32_t base = 0;
+    if ((int)lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
+    base = __shfl(base, leader);
+    return base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+__device__ __forceinline__ void count_add(unsigned long long* dst, uint64_t v) {
+    uint64_t s = wave_sum64(v);
+    if (__lane_id() == 0 && s) atomicAdd(dst, (unsigned long long)s);
+}
+
+// ------------------------------------------------------------------ traversal kernels
+template <bool COUNT>
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(DevScene S, PathSoA P, const uint32_t* __restrict__ q,
+                                                           uint32_t n, unsigned long long* counters) {
+    __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+    __shared__ float s_dist[PT_STACK * PT_TRACE_BLOCK];
+    const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
+    TraceWork wk{0, 0};
+    if (i < n) {
+        const uint32_t p = q[i];
+        const float4 o = P.ray_o[p], d = P.ray_d[p];
+        float t, b1, b2;
+        int prim = trace_closest<COUNT>(S, xyz(o), xyz(d), __int_as_float(0x7f800000), t, b1, b2, s_ref, s_dist, wk);
+        P.hit[p] = make_float4(t, b1, b2, __int_as_float(prim));
+    }
+    if (COUNT) {
+        count_add(&counters[CNT_NODES_CLOSEST], wk.nodes);
+        count_add(&counters[CNT_TRIS_CLOSEST], wk.tris);
+    }
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(DevScene S, PathSoA P, const ShadowRec* __restrict__ sq,
+                                                          const uint32_t* __restrict__ nptr,
+                                                          unsigned long long* counters) {
+    __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+    const uint32_t n = *nptr;
+    const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
+    TraceWork wk{0, 0};
+    if (i < n) {
+        const ShadowRec r = sq[i];
+        const uint32_t p = __float_as_uint(r.d.w);
+        if (!trace_any<COUNT>(S, xyz(r.o), xyz(r.d), r.o.w, s_ref, wk)) {
+            float4 L = P.L[p];
+            L.x += r.c.x;
+            L.y += r.c.y;
+            L.z += r.c.z;
+            P.L[p] = L;
+        }
+    }
+    if (COUNT) {
+        count_add(&counters[CNT_NODES_ANY], wk.nodes);
+        count_add(&counters[CNT_TRIS_ANY], wk.tris);
+    }
+}
+
+// Test hook: trace arbitrary rays (pt_trace).
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(DevScene S, const pt_ray* __restrict__ rays, uint32_t n,
+                                                              int any, pt_hit* __restrict__ out,
+                                                              unsigned long long* counters) {
+    __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+    __shared__ float s_dist[PT_STACK * PT_TRACE_BLOCK];
+    const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
+    TraceWork wk{0, 0};
+    if (i < n) {
+        const pt_ray r = rays[i];
+        f3 o = F3(r.o[0], r.o[1], r.o[2]), d = F3(r.d[0], r.d[1], r.d[2]);
+        pt_hit h;
+        if (any) {
+            h.prim = trace_any<true>(S, o, d, r.tmax, s_ref, wk) ? 1 : 0;
+            h.t = h.b1 = h.b2 = 0;
+        } else {
+            h.prim = trace_closest<true>(S, o, d, r.tmax, h.t, h.b1, h.b2, s_ref, s_dist, wk);
+        }
+        out[i] = h;
+    }
+    count_add(&counters[any ? CNT_NODES_ANY : CNT_NODES_CLOSEST], wk.nodes);
+    count_add(&counters[any ? CNT_TRIS_ANY : CNT_TRIS_CLOSEST], wk.tris);
+}
+
+// ------------------------------------------------------------------ camera / regeneration
+__device__ __forceinline__ void work_pixel(const RenderParams& R, uint32_t pix_i, uint32_t& x, uint32_t& y) {
+    if (R.tiled) {  // 8x8 pixel tiles, tile-major: neighbouring lanes -> neighbouring pixels
+        uint32_t tile = pix_i >> 6, within = pix_i & 63u;
+        uint32_t tx = tile % R.tiles_x, ty = tile / R.tiles_x;
+        x = tx * 8 + (within & 7u);
+        y = ty * 8 + (within >> 3);
+    } else {
+        uint32_t p = R.pixel_begin + pix_i;
+        x = p % (uint32_t)R.cam.width;
+        y = p / (uint32_t)R.cam.width;
+    }
+}
+
+// Camera::GenerateRay (Camera.hpp:21-35) with the camera draws of
+// TileIntegrator::Render (Integrators.cpp:61-64): pixel2D, time, lens2D.
+__device__ __forceinline__ void camera_ray(const pt_camera_desc& c, uint32_t key, uint32_t x, uint32_t y, f3& o, f3& d) {
+    float a = draw(key, 0), b = draw(key, 1);
+    float l0 = draw(key, 3), l1 = draw(key, 4);
+    float pxf = (float)x + a, pyf = (float)y + b;  // == float(double(x) + a): both round the exact sum
+    float uc = pxf / (float)c.width;
+    float vc = pyf / (float)c.height;
+    f3 U = F3(c.u[0], c.u[1], c.u[2]), Vv = F3(c.v[0], c.v[1], c.v[2]), W = F3(c.w[0], c.w[1], c.w[2]);
+    f3 dir = normalize((-W + ((2.0f * uc - 1.0f) * c.half_width) * U) + ((2.0f * vc - 1.0f) * c.half_height) * Vv);
+    f3 org = F3(c.origin[0], c.origin[1], c.origin[2]);
+    if (c.focus_distance == 0 || c.focus_angle == 0) {
+        o = org;
+        d = dir;
+        return;
+    }
+    float r = csqrt(l0);
+    float th = 2 * PT_PI * l1;
+    float lx = r * cosf(th), ly = r * sinf(th);
+    f3 du = c.defocus_radius * U, dv = c.defocus_radius * Vv;
+    dir = dir * c.focus_distance;
+    f3 off = lx * du + ly * dv;
+    o = org + off;
+    d = normalize(dir - off);
+}
+
+// Finished paths store their radiance; free slots take the next sample.
+__global__ __launch_bounds__(256) void k_finish(RenderParams R, PathSoA P, const uint32_t* __restrict__ q,
+                                               const uint32_t* __restrict__ nptr, uint32_t n_direct, int store,
+                                               uint32_t* __restrict__ q_next, uint32_t* __restrict__ cnt,
+                                               unsigned long long* __restrict__ next_sample,
+                                               float* __restrict__ sample_L) {
+    const uint32_t n = nptr ? *nptr : n_direct;
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const bool active = i < n;
+    uint32_t slot = 0;
+    if (active) {
+        slot = q ? q[i] : i;
+        if (store) {
+            const uint4 m = P.meta[slot];
+            const float4 L = P.L[slot];
+            float* o = sample_L + 3ull * (uint64_t)m.w;
+            o[0] = L.x;
+            o[1] = L.y;
+            o[2] = L.z;
+        }
+    }
+    // refill: a sample whose path ends before tracing (maxDepth 0) is stored at once
+    bool enq = false;
+    while (active) {
+        const unsigned long long g = atomicAdd(next_sample, 1ull);
+        if (g >= R.chunk_total) break;
+        const uint32_t s_rel = (uint32_t)(g / R.npix_work), pix_i = (uint32_t)(g % R.npix_work);
+        uint32_t x, y;
+        work_pixel(R, pix_i, x, y);
+        const uint32_t s = R.shard_index + (R.s_lo + s_rel) * R.shard_count;
+        const uint32_t key = stream_key(R.seed, y * (uint32_t)R.cam.width + x, s);
+        if (R.max_depth == 0) {  // Li loop never runs: L = 0
+            float* o = sample_L + 3ull * g;
+            o[0] = o[1] = o[2] = 0.0f;
+            continue;
+        }
+        f3 o, d;
+        camera_ray(R.cam, key, x, y, o, d);
+        P.ray_o[slot] = make_float4(o.x, o.y, o.z, 0.0f);
+        P.ray_d[slot] = make_float4(d.x, d.y, d.z, 0.0f);
+        P.beta[slot] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);  // attenuation, prevPDF = 1
+        P.L[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        // dim 5: camera used 0..4; depth 1 (first loop test passed), spec = true
+        P.meta[slot] = make_uint4(key, 5u, 1u | PF_SPEC, (uint32_t)g);
+        enq = true;
+        break;
+    }
+    const uint32_t at = wave_append(cnt, enq);
+    if (enq) q_next[at] = slot;
+}
+
+// ------------------------------------------------------------------ shading
+template <int INTEGRATOR>
+__global__ __launch_bounds__(256) void k_shade(DevScene S, RenderParams R, PathSoA P, const uint32_t* __restrict__ q,
+                                              uint32_t n, uint32_t* __restrict__ q_next, uint32_t* __restrict__ q_done,
+                                              ShadowRec* __restrict__ sq, uint32_t* __restrict__ cnt) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    bool cont = false, done = false, shadow = false;
+    uint32_t p = 0;
+    ShadowRec srec;
+    if (i < n) {
+        p = q[i];
+        const float4 o4 = P.ray_o[p], d4 = P.ray_d[p], b4 = P.beta[p], L4 = P.L[p];
+        const float4 h = P.hit[p];
+        uint4 m = P.meta[p];
+        f3 ro = xyz(o4), rd = xyz(d4);
+        f3 att = xyz(b4), out = xyz(L4);
+        float prev = b4.w;
+        uint32_t depth = m.z & PF_DEPTH_MASK, rr = (m.z >> PF_RR_SHIFT) & PF_DEPTH_MASK;
+        bool spec = (m.z & PF_SPEC) != 0;
+        const int prim = __float_as_int(h.w);
+        bool alive = true;
+        if (prim < 0) {
+            // miss: infinite lights (Integrators.cpp:140-145, 196-208)
+            for (uint32_t k = 0; k < S.n_infinite_lights; k++) {
+                const pt_light& l = S.lights[S.infinite_lights[k]];
+                if (INTEGRATOR == PT_INTEGRATOR_SIMPLE || spec) {
+                    out = out + att * inf_le(l, rd);
+                } else if (prev > 0) {
+                    float lp = l.pmf * (1.0f / (4.0f * PT_PI));
+                    float w = prev * prev / (prev * prev + lp * lp);
+                    out = out + (att * inf_le(l, rd)) * w;
+                }
+            }
+            alive = false;
+        } else {
+            const uint32_t key = m.x, dim = m.y;
+            float r[8];
+            if (INTEGRATOR == PT_INTEGRATOR_PATH) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) r[k] = draw(key, dim + k);
+                m.y = dim + 8;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; k++) r[k] = draw(key, dim + k);
+                m.y = dim + 4;
+            }
+            const DevGeom g = S.geom[prim];
+            const DevPrimInfo pi = S.info[prim];
+            const uint32_t kind = __float_as_uint(g.a.w) & GF_KIND;
+            SurfInt si;
+            if (kind == PT_PRIM_TRIANGLE) tri_interaction(S, g, pi.index, pi.material, ro, rd, h.x, h.y, h.z, si);
+            else if (kind == PT_PRIM_QUAD) quad_interaction(S.quads[pi.index], ro, rd, h.x, h.y, h.z, si);
+            else sphere_interaction(S.spheres[pi.index], ro, rd, h.x, si);
+            si.mat = pi.material;
+            si.light = pi.light;
+            // emission (Integrators.cpp:151-154, 217-226)
+            if (si.light >= 0) {
+                const pt_light& al = S.lights[si.light];
+                f3 Le = light_L(S, al, si.n, si.u, si.v, rd);
+                if (!is_zero(Le)) {
+                    if (INTEGRATOR == PT_INTEGRATOR_SIMPLE || spec) {
+                        out = out + att * Le;
+                    } else if (prev > 0) {
+                        float lp = al.pmf * light_pdf(S, al, si.p, si.n, ro, rd);
+                        float w = prev * prev / (prev * prev + lp * lp);
+                        out = out + (att * Le) * w;
+                    }
+                }
+            }
+            if (si.mat < 0) {
+                // medium boundary: pass through (Integrators.cpp:156-159, 228-232)
+                if (INTEGRATOR == PT_INTEGRATOR_PATH) spec = true;
+                ro = ro + si.t * rd;
+            } else {
+                const float us = INTEGRATOR == PT_INTEGRATOR_PATH ? r[4] : r[2];
+                const Bxdf b = mat_scatter(S, si.mat, ro, rd, si, us, r[0], r[1]);
+                if (!b.ok) {
+                    alive = false;  // absorbed
+                } else {
+                    if (INTEGRATOR == PT_INTEGRATOR_PATH) {
+                        spec = (b.flags & FL_SPEC) != 0;
+                        if (!spec) {
+                            // PathIntegrator::SampleLd (Integrators.cpp:260-294); occlusion deferred
+                            const int li = ls_sample(S, r[5]);
+                            if (li >= 0) {
+                                const pt_light& l = S.lights[li];
+                                LSample ls = light_sample(S, l, r[2], r[3]);
+                                f3 ldir;
+                                float tmax;
+                                if (is_zero(ls.n)) {
+                                    ldir = ls.dir;
+                                    tmax = __int_as_float(0x7f800000);
+                                } else {
+                                    ldir = ls.p - si.p;
+                                    tmax = length(ldir) - PT_EPS;
+                                }
+                                const f3 sd = normalize(ldir);
+                                float lpdf = l.pmf;
+                                const float dt = dot(si.ns, sd);
+                                if (!(lpdf <= 0 || dt * dot(rd, si.ns) >= 0)) {
+                                    const f3 f = mat_f(S, si.mat, rd, si, sd) * fabsf(dt);
+                                    f3 c;
+                                    bool ok = true;
+                                    if (light_is_delta(l)) {
+                                        c = (ls.L * f) / lpdf;
+                                    } else {
+                                        lpdf *= light_pdf(S, l, ls.p, ls.n, si.p, sd);
+                                        if (lpdf <= 0) {
+                                            ok = false;
+                                        } else {
+                                            float w2 = lpdf * lpdf;
+                                            float w1 = mat_pdf(S, si.mat, rd, si, sd);
+                                            w1 = w1 * w1;
+                                            float wl = w2 / (w1 + w2);
+                                            c = ((light_L(S, l, ls.n, ls.u, ls.v, sd) * f) * wl) / lpdf;
+                                        }
+                                    }
+                                    if (ok) {
+                                        f3 contrib = att * c;
+                                        if (!is_zero(contrib)) {
+                                            shadow = true;
+                                            srec.o = make_float4(si.p.x, si.p.y, si.p.z, tmax);
+                                            srec.d = make_float4(sd.x, sd.y, sd.z, __uint_as_float(p));
+                                            srec.c = make_float4(contrib.x, contrib.y, contrib.z, 0.0f);
+                                        }
+                                    }
+                                }
+                            }
+                            prev = mat_pdf(S, si.mat, rd, si, b.d);
+                        }
+                    }
+                    att = att * ((b.f * fabsf(dot(si.ns, b.d))) / b.pdf);
+                    const float urr = INTEGRATOR == PT_INTEGRATOR_PATH ? r[6] : r[3];
+                    if (rr++ > 3) {
+                        float qq = fminf(0.95f, fmaxf(fmaxf(att.x, att.y), att.z));
+                        if (urr >= qq) alive = false;
+                        else att = att / qq;
+                    }
+                    ro = b.o;
+                    rd = b.d;
+                }
+            }
+        }
+        // loop test `depth++ < maxDepth && sum(att) > 0` (Integrators.cpp:138, 193)
+        if (alive && depth < R.max_depth && (att.x + att.y + att.z) > 0.0f) {
+            depth++;
+            cont = true;
+        } else {
+            done = true;
+        }
+        P.L[p] = make_float4(out.x, out.y, out.z, 0.0f);
+        if (cont) {
+            P.ray_o[p] = make_float4(ro.x, ro.y, ro.z, 0.0f);
+            P.ray_d[p] = make_float4(rd.x, rd.y, rd.z, 0.0f);
+            P.beta[p] = make_float4(att.x, att.y, att.z, prev);
+            m.z = depth | (rr << PF_RR_SHIFT) | (spec ? PF_SPEC : 0u);
+            P.meta[p] = m;
+        }
+    }
+    const uint32_t a = wave_append(&cnt[Q_NEXT], cont);
+    if (cont) q_next[a] = p;
+    const uint32_t b = wave_append(&cnt[Q_DONE], done);
+    if (done) q_done[b] = p;
+    const uint32_t c = wave_append(&cnt[Q_SHADOW], shadow);
+    if (shadow) sq[c] = srec;
+}
+
+// ------------------------------------------------------------------ film gather
+// Filter::Evaluate (Filter.hpp:47-53, 69-75, 93-108) at a float position.
+__device__ __forceinline__ double mitchell1(double x, double b, double c) {
+    double ax = fabs(x);
+    if (ax <= 1.0)
+        return 1.0 / 6.0 * ((12 - 9 * b - 6 * c) * ax * ax * ax + (-18 + 12 * b + 6 * c) * ax * ax + (6 - 2 * b));
+    if (ax <= 2)
+        return 1.0 / 6.0 *
+               ((-b - 6 * c) * ax * ax * ax + (6 * b + 30 * c) * ax * ax + (-12 * b - 48 * c) * ax + (8 * b + 24 * c));
+    return 0;
+}
+__device__ __forceinline__ double gauss1(double x, double sigma) {
+    return 0.56418958354775628695 / (sigma * 1.41421356237309504880) * exp(-(x * x) / (2 * sigma * sigma));
+}
+__device__ __forceinline__ double filter_eval(const RenderParams& R, float px, float py) {
+    if (R.filter == PT_FILTER_BOX) return (fabsf(px) <= R.frad[0] && fabsf(py) <= R.frad[1]) ? 1.0 : 0.0;
+    if (R.filter == PT_FILTER_GAUSSIAN) {
+        double gx = gauss1(px, R.fparam[0]) - R.gauss_x, gy = gauss1(py, R.fparam[0]) - R.gauss_y;
+        return (gx > 0 ? gx : 0) * (gy > 0 ? gy : 0);
+    }
+    float ax = 2 * px / R.frad[0];
+    float ay = 2 * py / R.frad[1];
+    return mitchell1(ax, R.fparam[0], R.fparam[1]) * mitchell1(ay, R.fparam[0], R.fparam[1]);
+}
+
+__global__ __launch_bounds__(256) void k_gather(RenderParams R, const float* __restrict__ sample_L,
+                                               double* __restrict__ film) {
+    const uint32_t tid = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t W = (uint32_t)R.cam.width, H = (uint32_t)R.cam.height;
+    if (tid >= W * H) return;
+    const int x = (int)(tid % W), y = (int)(tid / W);
+    double acc[4] = {0, 0, 0, 0};
+    const uint32_t ns = R.s_hi - R.s_lo;
+    for (int oy = -R.rad_y; oy <= R.rad_y; oy++) {
+        for (int ox = -R.rad_x; ox <= R.rad_x; ox++) {
+            // source pixel whose samples reach (x, y) with offset (ox, oy)
+            const int sx = x - ox, sy = y - oy;
+            if (sx < 0 || sy < 0 || sx >= (int)W || sy >= (int)H) continue;
+            uint32_t pix_i;
+            if (R.tiled) {
+                uint32_t tile = (uint32_t)(sy >> 3) * R.tiles_x + (uint32_t)(sx >> 3);
+                pix_i = tile * 64u + (uint32_t)((sy & 7) * 8 + (sx & 7));
+            } else {
+                pix_i = (uint32_t)(sy * (int)W + sx);
+            }
+            const uint32_t spix = (uint32_t)sy * W + (uint32_t)sx;
+            for (uint32_t k = 0; k < ns; k++) {
+                const uint32_t s = R.shard_index + (R.s_lo + k) * R.shard_count;
+                const uint32_t key = stream_key(R.seed, spix, s);
+                const float a = draw(key, 0), b = draw(key, 1);
+                // FilmTile::Add: pixelSample = fract(p), sample_pos = (o + 0.5) - fract
+                const double fx = (double)a, fy = (double)b;  // fract(x + a) = a, a in [0,1)
+                const double spx = (double)ox + 0.5 - fx, spy = (double)oy + 0.5 - fy;
+                const double w = filter_eval(R, (float)spx, (float)spy) * R.inv_integral;
+                if (w <= 0) continue;
+                const uint64_t g = (uint64_t)k * R.npix_work + pix_i;
+                const float* L = sample_L + 3ull * g;
+                acc[0] += (double)L[0] * w;
+                acc[1] += (double)L[1] * w;
+                acc[2] += (double)L[2] * w;
+                acc[3] += w;
+            }
+        }
+    }
+    double* o = film + 4ull * tid;
+    o[0] += acc[0];
+    o[1] += acc[1];
+    o[2] += acc[2];
+    o[3] += acc[3];
+}
+
+// explicit instantiations used by the runtime
+template __global__ void k_closest<false>(DevScene, PathSoA, const uint32_t*, uint32_t, unsigned long long*);
+template __global__ void k_closest<true>(DevScene, PathSoA, const uint32_t*, uint32_t, unsigned long long*);
+template __global__ void k_shadow<false>(DevScene, PathSoA, const ShadowRec*, const uint32_t*, unsigned long long*);
+template __global__ void k_shadow<true>(DevScene, PathSoA, const ShadowRec*, const uint32_t*, unsigned long long*);
+template __global__ void k_shade<PT_INTEGRATOR_PATH>(DevScene, RenderParams, PathSoA, const uint32_t*, uint32_t,
+                                                     uint32_t*, uint32_t*, ShadowRec*, uint32_t*);
+template __global__ void k_shade<PT_INTEGRATOR_SIMPLE>(DevScene, RenderParams, PathSoA, const uint32_t*, uint32_t,
+                                                       uint32_t*, uint32_t*, ShadowRec*, uint32_t*);

@@ -1,0 +1,739 @@
+// Host runtime of libpt_hip.so: the C ABI of include/pt_api.h.
+//
+// pt_scene_upload converts the host-built scene (reference-form BVH4s,
+// primitives, materials, lights) into the device layout of pt_device.h:
+// one node array for the TLAS and every BLAS, one leaf-ordered primitive slot
+// array, and the light-sampler running sums.  pt_render runs the persistent
+// wavefront (pt_kernels.hip) over sample chunks and gathers the film.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pt_kernels.hip"
+
+struct pt_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // scene
+    std::vector<void*> scene_bufs;
+    uint64_t scene_bytes = 0;
+    DevScene scene{};
+    bool has_scene = false;
+    // wavefront buffers
+    uint32_t cap = 0;
+    PathSoA P{};
+    uint32_t *q_a = nullptr, *q_b = nullptr, *q_done = nullptr, *qcnt = nullptr;
+    ShadowRec* sq = nullptr;
+    unsigned long long* counters = nullptr;
+    uint32_t* host_cnt = nullptr;  // pinned
+    float* sample_L = nullptr;
+    uint64_t sample_cap = 0;  // floats
+    double* film = nullptr;
+    uint64_t film_cap = 0;  // doubles
+    hipEvent_t ev[8] = {};
+};
+
+static pt_status fail(pt_ctx* c, pt_status code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return code;
+}
+#define HIPCHK(c, x)                                                                                  \
+    do {                                                                                              \
+        hipError_t e_ = (x);                                                                          \
+        if (e_ != hipSuccess) return fail(c, PT_ERR_HIP, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), \
+                                          __FILE__, __LINE__);                                        \
+    } while (0)
+
+static thread_local std::string g_err;
+
+extern "C" int pt_version(void) { return PT_API_VERSION; }
+
+extern "C" const char* pt_last_error(const pt_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
+
+extern "C" pt_status pt_create(pt_ctx** out, int device) {
+    if (!out) return PT_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+        g_err = "no HIP device";
+        return PT_ERR_NODEV;
+    }
+    if (device < 0 || device >= n) {
+        g_err = "device index out of range";
+        return PT_ERR_ARG;
+    }
+    pt_ctx* c = new pt_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        g_err = "hip init failed";
+        delete c;
+        return PT_ERR_HIP;
+    }
+    c->stream = c->own_stream;
+    for (auto& e : c->ev) {
+        if (hipEventCreate(&e) != hipSuccess) {
+            g_err = "event create failed";
+            delete c;
+            return PT_ERR_HIP;
+        }
+    }
+    if (hipHostMalloc((void**)&c->host_cnt, 64) != hipSuccess) {
+        g_err = "pinned alloc failed";
+        delete c;
+        return PT_ERR_HIP;
+    }
+    *out = c;
+    return PT_OK;
+}
+
+static void free_scene(pt_ctx* c) {
+    for (void* p : c->scene_bufs) hipFree(p);
+    c->scene_bufs.clear();
+    c->scene_bytes = 0;
+    c->has_scene = false;
+}
+static void free_work(pt_ctx* c) {
+    void* bufs[] = {c->P.ray_o, c->P.ray_d, c->P.beta, c->P.L, c->P.meta, c->P.hit, c->q_a, c->q_b, c->q_done,
+                    c->qcnt, c->sq, c->counters};
+    for (void* p : bufs)
+        if (p) hipFree(p);
+    c->P = PathSoA{};
+    c->q_a = c->q_b = c->q_done = c->qcnt = nullptr;
+    c->sq = nullptr;
+    c->counters = nullptr;
+    c->cap = 0;
+}
+
+extern "C" void pt_destroy(pt_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    free_scene(c);
+    free_work(c);
+    if (c->sample_L) hipFree(c->sample_L);
+    if (c->film) hipFree(c->film);
+    if (c->host_cnt) hipHostFree(c->host_cnt);
+    for (auto& e : c->ev)
+        if (e) hipEventDestroy(e);
+    if (c->own_stream) hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+extern "C" pt_status pt_set_stream(pt_ctx* c, void* s) {
+    if (!c) return PT_ERR_ARG;
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    return PT_OK;
+}
+
+extern "C" uint64_t pt_scene_device_bytes(const pt_ctx* c) { return c ? c->scene_bytes : 0; }
+
+template <class T>
+static pt_status upload(pt_ctx* c, const T* src, size_t n, const T** dst) {
+    *dst = nullptr;
+    size_t bytes = std::max<size_t>(n * sizeof(T), 16);
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return fail(c, PT_ERR_OOM, "hipMalloc(%zu) failed", bytes);
+    c->scene_bufs.push_back(p);
+    c->scene_bytes += bytes;
+    if (n && src) HIPCHK(c, hipMemcpy(p, src, n * sizeof(T), hipMemcpyHostToDevice));
+    else HIPCHK(c, hipMemset(p, 0, bytes));
+    *dst = (const T*)p;
+    return PT_OK;
+}
+
+static bool is_perm(unsigned p) {
+    unsigned seen = 0;
+    for (int s = 0; s < 4; s++) seen |= 1u << ((p >> (2 * s)) & 3);
+    return seen == 0xF;
+}
+
+// Is the material's alpha a constant, and what does the tester return then?
+static bool tex_alpha_const(const pt_scene_desc* s, int id, float& a, int depth = 0) {
+    if (id < 0 || (uint32_t)id >= s->n_textures || depth > 16) return false;
+    const pt_texture& t = s->textures[id];
+    if (t.kind == PT_TEX_SOLID) { a = 1.0f; return true; }
+    if (t.kind == PT_TEX_CHECKER) {
+        float a1, a2;
+        if (tex_alpha_const(s, t.a, a1, depth + 1) && tex_alpha_const(s, t.b, a2, depth + 1) && a1 == a2) {
+            a = a1;
+            return true;
+        }
+        return false;
+    }
+    if (t.image < 0 || (uint32_t)t.image >= s->n_images) return false;
+    if (s->images[t.image].channels != 4) { a = 1.0f; return true; }
+    return false;
+}
+static void material_alpha_flags(const pt_scene_desc* s, int mid, uint32_t& flags) {
+    if (mid < 0) return;
+    const pt_material& m = s->materials[mid];
+    if (m.kind != PT_MAT_DIFFUSE && m.kind != PT_MAT_DIELECTRIC) return;
+    if (m.alpha_mode == PT_ALPHA_OPAQUE) return;
+    flags |= GF_PRED_GLM;  // HasAlpha(): IntersectPred runs Intersect + Alpha
+    float a = 0;
+    bool known;
+    if (m.alpha >= 0) {
+        const pt_texture& t = s->textures[m.alpha];
+        known = t.kind == PT_TEX_SOLID;
+        a = t.value[0];
+    } else {
+        known = tex_alpha_const(s, m.tex, a);
+    }
+    bool always_true = known && (m.alpha_mode == PT_ALPHA_MASK ? (a > m.alpha_cutoff) : (a >= 1.0f));
+    if (!always_true) flags |= GF_ALPHA;
+}
+
+struct Conv {
+    const pt_scene_desc* s;
+    std::vector<DevCluster>& nodes;
+    std::vector<DevGeom>& geom;
+    std::vector<uint32_t>& cbase;
+    uint8_t lut[8][135];
+    std::string err;
+
+    uint32_t convert(const pt_ref_bvh4_node& desc, uint32_t b) {
+        const pt_bvh_desc& B = s->bvhs[b];
+        if (desc.active == 0) {
+            if (desc.count == 0) return REF_EMPTY;
+            uint64_t slot0 = (uint64_t)B.prim_base + desc.cluster_idx;
+            uint64_t last = slot0 + desc.count - 1;
+            if (last >= s->n_prims || desc.cluster_idx + desc.count > B.n_prims) {
+                err = "leaf primitive range out of bounds";
+                return REF_EMPTY;
+            }
+            uint32_t w = __builtin_bit_cast(uint32_t, geom[last].a.w) | GF_LAST;
+            geom[last].a.w = __builtin_bit_cast(float, w);
+            return REF_LEAF | (uint32_t)slot0;
+        }
+        if (desc.cluster_idx >= B.n_clusters) {
+            err = "cluster index out of bounds";
+            return REF_EMPTY;
+        }
+        const uint32_t gi = cbase[b] + desc.cluster_idx;
+        const pt_ref_bvh4_cluster& rc = B.clusters[desc.cluster_idx];
+        DevCluster& dc = nodes[gi];
+        memcpy(&dc.xmin, rc.xmin, 16);
+        memcpy(&dc.xmax, rc.xmax, 16);
+        memcpy(&dc.ymin, rc.ymin, 16);
+        memcpy(&dc.ymax, rc.ymax, 16);
+        memcpy(&dc.zmin, rc.zmin, 16);
+        memcpy(&dc.zmax, rc.zmax, 16);
+        uint32_t perm = desc.perm < 135 ? desc.perm : 0;
+        dc.order[0] = dc.order[1] = 0;
+        for (int o = 0; o < 8; o++) dc.order[o >> 2] |= (uint32_t)lut[o][perm] << (8 * (o & 3));
+        dc.pad[0] = dc.pad[1] = 0;
+        for (int k = 0; k < 4; k++) dc.child[k] = REF_EMPTY;
+        for (int k = 0; k < 4; k++) {
+            pt_ref_bvh4_node ch = rc.children[k];
+            uint32_t r = convert(ch, b);
+            nodes[gi].child[k] = r;  // re-index: the vector is pre-sized, no reallocation
+        }
+        return gi;
+    }
+};
+
+extern "C" pt_status pt_bvh4_order_table(uint8_t* out);
+
+extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
+    if (!c || !s) return PT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    free_scene(c);
+    if (s->n_bvhs == 0 || !s->bvhs || s->n_prims == 0 || !s->prims)
+        return fail(c, PT_ERR_ARG, "scene needs a TLAS and primitives");
+    // ---- validate
+    for (uint32_t i = 0; i < s->n_prims; i++) {
+        const pt_prim& p = s->prims[i];
+        bool ok = true;
+        switch (p.kind) {
+            case PT_PRIM_TRIANGLE: ok = p.index < s->n_triangles; break;
+            case PT_PRIM_QUAD: ok = p.index < s->n_quads; break;
+            case PT_PRIM_SPHERE: ok = p.index < s->n_spheres; break;
+            case PT_PRIM_BLAS: ok = p.index > 0 && p.index < s->n_bvhs; break;
+            default: ok = false;
+        }
+        if (!ok) return fail(c, PT_ERR_ARG, "primitive %u: bad kind/index", i);
+        if (p.material >= (int32_t)s->n_materials) return fail(c, PT_ERR_ARG, "primitive %u: bad material", i);
+        if (p.light >= (int32_t)s->n_lights) return fail(c, PT_ERR_ARG, "primitive %u: bad light", i);
+    }
+    for (uint32_t t = 0; t < s->n_triangles; t++)
+        for (int k = 0; k < 3; k++)
+            if (s->tri_vidx[3 * t + k] >= s->n_vertices) return fail(c, PT_ERR_ARG, "triangle %u: bad vertex", t);
+    for (uint32_t l = 0; l < s->n_lights; l++) {
+        const pt_light& L = s->lights[l];
+        if (L.kind == PT_LIGHT_AREA && (L.prim < 0 || (uint32_t)L.prim >= s->n_prims || L.tex < 0 ||
+                                        (uint32_t)L.tex >= s->n_textures))
+            return fail(c, PT_ERR_ARG, "light %u: bad area light", l);
+    }
+    for (uint32_t m = 0; m < s->n_materials; m++) {
+        const pt_material& M = s->materials[m];
+        int ids[5] = {M.tex, M.norm, M.rough, M.metal, M.alpha};
+        for (int id : ids)
+            if (id >= (int32_t)s->n_textures) return fail(c, PT_ERR_ARG, "material %u: bad texture", m);
+        if ((M.kind == PT_MAT_DIFFUSE || M.kind == PT_MAT_DIELECTRIC || M.kind == PT_MAT_THIN) && M.tex < 0)
+            return fail(c, PT_ERR_ARG, "material %u: missing texture", m);
+        if ((M.kind == PT_MAT_DIFFUSE) && (M.rough < 0 || M.metal < 0))
+            return fail(c, PT_ERR_ARG, "material %u: missing roughness/metallic texture", m);
+        if ((M.kind == PT_MAT_DIELECTRIC) && M.rough < 0) return fail(c, PT_ERR_ARG, "material %u: missing roughness", m);
+    }
+    for (uint32_t i = 0; i < s->n_sampler_lights; i++)
+        if (s->sampler_lights[i] >= s->n_lights) return fail(c, PT_ERR_ARG, "sampler light %u out of range", i);
+    for (uint32_t i = 0; i < s->n_infinite_lights; i++)
+        if (s->infinite_lights[i] >= s->n_lights) return fail(c, PT_ERR_ARG, "infinite light %u out of range", i);
+
+    // ---- geometry slots
+    std::vector<DevGeom> geom(s->n_prims);
+    std::vector<DevPrimInfo> info(s->n_prims);
+    for (uint32_t i = 0; i < s->n_prims; i++) {
+        const pt_prim& p = s->prims[i];
+        uint32_t flags = p.kind;
+        DevGeom g{};
+        if (p.kind == PT_PRIM_TRIANGLE) {
+            const uint32_t* v = s->tri_vidx + 3 * (size_t)p.index;
+            const float* P0 = s->positions + 3 * (size_t)v[0];
+            const float* P1 = s->positions + 3 * (size_t)v[1];
+            const float* P2 = s->positions + 3 * (size_t)v[2];
+            g.a = make_float4(P0[0], P0[1], P0[2], 0);
+            g.b = make_float4(P1[0] - P0[0], P1[1] - P0[1], P1[2] - P0[2], 0);  // edge1 = vert1 - vert0
+            g.c = make_float4(P2[0] - P0[0], P2[1] - P0[1], P2[2] - P0[2], 0);  // edge2 = vert2 - vert0
+        } else if (p.kind == PT_PRIM_QUAD) {
+            const pt_quad& q = s->quads[p.index];
+            g.a = make_float4(q.Q[0], q.Q[1], q.Q[2], 0);
+            g.b = make_float4(q.u[0], q.u[1], q.u[2], 0);
+            g.c = make_float4(q.v[0], q.v[1], q.v[2], 0);
+        } else if (p.kind == PT_PRIM_SPHERE) {
+            const pt_sphere& sp = s->spheres[p.index];
+            g.a = make_float4(sp.center[0], sp.center[1], sp.center[2], 0);
+            g.b = make_float4(sp.radius, 0, 0, 0);
+        }
+        if (p.kind != PT_PRIM_BLAS) material_alpha_flags(s, p.material, flags);
+        g.a.w = __builtin_bit_cast(float, flags);
+        geom[i] = g;
+        info[i] = DevPrimInfo{p.material, p.light, p.medium, p.index};
+    }
+    // ---- nodes: TLAS then every BLAS, converted from the root descriptors
+    std::vector<uint32_t> cbase(s->n_bvhs);
+    uint64_t total = 0;
+    for (uint32_t b = 0; b < s->n_bvhs; b++) {
+        cbase[b] = (uint32_t)total;
+        total += s->bvhs[b].n_clusters;
+        if (s->bvhs[b].n_clusters && !s->bvhs[b].clusters) return fail(c, PT_ERR_ARG, "bvh %u: no clusters", b);
+        if ((uint64_t)s->bvhs[b].prim_base + s->bvhs[b].n_prims > s->n_prims)
+            return fail(c, PT_ERR_ARG, "bvh %u: primitive range out of bounds", b);
+    }
+    if (total >= REF_LEAF) return fail(c, PT_ERR_ARG, "too many clusters");
+    std::vector<DevCluster> nodes(std::max<uint64_t>(total, 1));
+    Conv cv{s, nodes, geom, cbase, {}, {}};
+    pt_bvh4_order_table(&cv.lut[0][0]);
+    std::vector<uint32_t> roots(s->n_bvhs);
+    for (uint32_t b = 0; b < s->n_bvhs; b++) {
+        roots[b] = cv.convert(s->bvhs[b].root, b);
+        if (!cv.err.empty()) return fail(c, PT_ERR_ARG, "bvh %u: %s", b, cv.err.c_str());
+    }
+    for (uint32_t i = 0; i < s->n_prims; i++) {
+        if (s->prims[i].kind == PT_PRIM_BLAS) {
+            geom[i].b.x = __builtin_bit_cast(float, roots[s->prims[i].index]);
+            info[i].index = roots[s->prims[i].index];
+        }
+    }
+    // ---- triangles: vertex indices + flags as uint4
+    std::vector<uint4> tri(s->n_triangles);
+    for (uint32_t t = 0; t < s->n_triangles; t++)
+        tri[t] = make_uint4(s->tri_vidx[3 * t], s->tri_vidx[3 * t + 1], s->tri_vidx[3 * t + 2],
+                            s->tri_flags ? s->tri_flags[t] : 0u);
+    // ---- light sampler running sums (PowerLightSampler::Sample order)
+    std::vector<float> cdf(s->n_sampler_lights);
+    float acc = 0;
+    for (uint32_t i = 0; i < s->n_sampler_lights; i++) {
+        acc += s->lights[s->sampler_lights[i]].power;
+        cdf[i] = acc;
+    }
+    DevScene& S = c->scene;
+    S = DevScene{};
+    pt_status st;
+#define UP(dst, src, n) \
+    if ((st = upload(c, src, n, &dst)) != PT_OK) return st;
+    UP(S.nodes, nodes.data(), nodes.size());
+    UP(S.geom, geom.data(), geom.size());
+    UP(S.info, info.data(), info.size());
+    UP(S.tri, tri.data(), tri.size());
+    UP(S.positions, s->positions, 3 * (size_t)s->n_vertices);
+    UP(S.normals, s->normals, 3 * (size_t)s->n_vertices);
+    UP(S.uvs, s->uvs, 2 * (size_t)s->n_vertices);
+    UP(S.tangents, s->tangents, s->tangents ? 3 * (size_t)s->n_vertices : 0);
+    UP(S.quads, s->quads, s->n_quads);
+    UP(S.spheres, s->spheres, s->n_spheres);
+    UP(S.materials, s->materials, s->n_materials);
+    UP(S.textures, s->textures, s->n_textures);
+    UP(S.images, s->images, s->n_images);
+    UP(S.texels, s->texels, s->n_texel_bytes);
+    UP(S.lights, s->lights, s->n_lights);
+    UP(S.sampler_lights, s->sampler_lights, s->n_sampler_lights);
+    UP(S.sampler_cdf, cdf.data(), cdf.size());
+    UP(S.infinite_lights, s->infinite_lights, s->n_infinite_lights);
+#undef UP
+    S.root = roots[0];
+    S.n_prims = s->n_prims;
+    S.n_texel_bytes = s->n_texel_bytes;
+    S.n_lights = s->n_lights;
+    S.light_sampler = s->light_sampler;
+    S.n_sampler_lights = s->n_sampler_lights;
+    S.sampler_total = acc;
+    S.n_infinite_lights = s->n_infinite_lights;
+    c->has_scene = true;
+    return PT_OK;
+}
+
+static bool is_device_ptr(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+
+template <class T>
+static pt_status ensure(pt_ctx* c, T** p, uint64_t& cap, uint64_t n) {
+    if (cap >= n && *p) return PT_OK;
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    cap = 0;
+    if (hipMalloc((void**)p, std::max<uint64_t>(n, 4) * sizeof(T)) != hipSuccess)
+        return fail(c, PT_ERR_OOM, "hipMalloc(%llu) failed", (unsigned long long)(n * sizeof(T)));
+    cap = n;
+    return PT_OK;
+}
+
+static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
+    if (c->cap >= cap) return PT_OK;
+    free_work(c);
+    size_t n = cap;
+#define AL(p, bytes)                                                                         \
+    if (hipMalloc((void**)&(p), (bytes)) != hipSuccess) {                                    \
+        free_work(c);                                                                        \
+        return fail(c, PT_ERR_OOM, "wavefront allocation of %zu paths failed", (size_t)n); \
+    }
+    AL(c->P.ray_o, n * 16);
+    AL(c->P.ray_d, n * 16);
+    AL(c->P.beta, n * 16);
+    AL(c->P.L, n * 16);
+    AL(c->P.meta, n * 16);
+    AL(c->P.hit, n * 16);
+    AL(c->q_a, n * 4);
+    AL(c->q_b, n * 4);
+    AL(c->q_done, n * 4);
+    AL(c->qcnt, 64);
+    AL(c->sq, n * sizeof(ShadowRec));
+    AL(c->counters, CNT_COUNT * 8);
+#undef AL
+    c->cap = cap;
+    return PT_OK;
+}
+
+static double mitchell_int(float rx, float ry) { return rx * ry / 4.0; }
+static double gauss_h(double x, double sigma) {
+    return 0.56418958354775628695 / (sigma * 1.41421356237309504880) * std::exp(-(x * x) / (2 * sigma * sigma));
+}
+
+// Core loop shared by pt_render / pt_render_samples.  Renders local sample
+// chunks; after each chunk either gathers into `film` (device) or hands the
+// chunk's per-sample radiance to `on_chunk`.
+template <class OnChunk>
+static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_dev,
+                     pt_stats* stats, OnChunk on_chunk) {
+    const uint32_t W = (uint32_t)cam->width, H = (uint32_t)cam->height;
+    RenderParams R{};
+    R.cam = *cam;
+    R.seed = rd->seed;
+    R.max_depth = rd->max_depth;
+    R.shard_count = rd->shard_count ? rd->shard_count : 1;
+    R.shard_index = rd->shard_index;
+    if (R.shard_index >= R.shard_count) return fail(c, PT_ERR_ARG, "shard_index >= shard_count");
+    if (rd->max_depth > PF_DEPTH_MASK - 1) return fail(c, PT_ERR_ARG, "max_depth too large");
+    const bool ranged = !(rd->pixel_begin == 0 && rd->pixel_end == 0);
+    if (ranged) {
+        if (rd->pixel_end <= rd->pixel_begin || rd->pixel_end > W * H) return fail(c, PT_ERR_ARG, "bad pixel range");
+        R.pixel_begin = rd->pixel_begin;
+        R.npix_work = rd->pixel_end - rd->pixel_begin;
+        R.tiled = 0;
+    } else {
+        R.npix_work = W * H;
+        R.tiled = (W % 8 == 0 && H % 8 == 0) ? 1u : 0u;
+        R.tiles_x = W / 8;
+    }
+    R.filter = rd->filter;
+    R.frad[0] = rd->filter_radius[0];
+    R.frad[1] = rd->filter_radius[1];
+    R.fparam[0] = rd->filter_params[0];
+    R.fparam[1] = rd->filter_params[1];
+    R.rad_x = (int)std::ceil(rd->filter_radius[0] - 0.5f);
+    R.rad_y = (int)std::ceil(rd->filter_radius[1] - 0.5f);
+    double integral;
+    if (rd->filter == PT_FILTER_BOX) integral = 4 * rd->filter_radius[0] * rd->filter_radius[1];
+    else if (rd->filter == PT_FILTER_GAUSSIAN) {
+        double sg = rd->filter_params[0];
+        R.gauss_x = gauss_h(rd->filter_radius[0], sg);
+        R.gauss_y = gauss_h(rd->filter_radius[1], sg);
+        double s2 = sg * 1.41421356237309504880;
+        double ix = 0.5 * (std::erf(rd->filter_radius[0] / s2) - std::erf(-rd->filter_radius[0] / s2));
+        double iy = 0.5 * (std::erf(rd->filter_radius[1] / s2) - std::erf(-rd->filter_radius[1] / s2));
+        integral = (ix - 2 * rd->filter_radius[0] * R.gauss_x) * (iy - 2 * rd->filter_radius[1] * R.gauss_y);
+    } else integral = mitchell_int(rd->filter_radius[0], rd->filter_radius[1]);
+    R.inv_integral = 1.0 / integral;
+
+    const uint32_t spp_local = rd->spp > R.shard_index ? (rd->spp - R.shard_index + R.shard_count - 1) / R.shard_count : 0;
+    // sample chunk: keep the per-sample radiance buffer <= ~6 GiB
+    const uint64_t max_floats = 6ull << 28;
+    uint64_t per_s = 3ull * R.npix_work;
+    uint32_t s_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spp_local, max_floats / per_s));
+    pt_status st = ensure(c, &c->sample_L, c->sample_cap, per_s * s_chunk);
+    if (st) return st;
+    uint32_t paths = rd->paths_in_flight ? rd->paths_in_flight : (1u << 21);
+    paths = (uint32_t)std::min<uint64_t>(paths, std::max<uint64_t>(1, (uint64_t)R.npix_work * s_chunk));
+    paths = (paths + 255) & ~255u;
+    if ((st = ensure_work(c, paths)) != PT_OK) return st;
+
+    const bool count = (rd->flags & PT_RENDER_COUNT_NODES) != 0;
+    const bool timing = (rd->flags & PT_RENDER_TIMING) != 0;
+    hipStream_t sm = c->stream;
+    HIPCHK(c, hipMemsetAsync(c->counters, 0, CNT_COUNT * 8, sm));
+    unsigned long long* next_sample = c->counters + CNT_NEXT_SAMPLE;
+    float t_cl = 0, t_sh = 0, t_an = 0;
+
+    for (uint32_t s_lo = 0; s_lo < spp_local; s_lo += s_chunk) {
+        R.s_lo = s_lo;
+        R.s_hi = std::min(spp_local, s_lo + s_chunk);
+        R.chunk_total = (unsigned long long)R.npix_work * (R.s_hi - R.s_lo);
+        HIPCHK(c, hipMemsetAsync(next_sample, 0, 8, sm));
+        HIPCHK(c, hipMemsetAsync(c->qcnt, 0, 64, sm));
+        // initial fill of every slot
+        uint32_t* q_cur = c->q_a;
+        uint32_t* q_nxt = c->q_b;
+        hipLaunchKernelGGL(k_finish, dim3((paths + 255) / 256), dim3(256), 0, sm, R, c->P, (const uint32_t*)nullptr,
+                           (const uint32_t*)nullptr, paths, 0, q_cur, c->qcnt + Q_NEXT, next_sample, c->sample_L);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(c->host_cnt, c->qcnt, 16, hipMemcpyDeviceToHost, sm));
+        HIPCHK(c, hipStreamSynchronize(sm));
+        uint32_t n_active = c->host_cnt[Q_NEXT];
+        while (n_active > 0) {
+            HIPCHK(c, hipMemsetAsync(c->qcnt, 0, 16, sm));
+            const dim3 gt((n_active + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK), gs((n_active + 255) / 256);
+            if (timing) HIPCHK(c, hipEventRecord(c->ev[0], sm));
+            if (count)
+                hipLaunchKernelGGL(k_closest<true>, gt, dim3(PT_TRACE_BLOCK), 0, sm, c->scene, c->P, q_cur, n_active,
+                                   c->counters);
+            else
+                hipLaunchKernelGGL(k_closest<false>, gt, dim3(PT_TRACE_BLOCK), 0, sm, c->scene, c->P, q_cur, n_active,
+                                   c->counters);
+            if (timing) HIPCHK(c, hipEventRecord(c->ev[1], sm));
+            if (rd->integrator == PT_INTEGRATOR_SIMPLE)
+                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_SIMPLE>, gs, dim3(256), 0, sm, c->scene, R, c->P, q_cur,
+                                   n_active, q_nxt, c->q_done, c->sq, c->qcnt);
+            else
+                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_PATH>, gs, dim3(256), 0, sm, c->scene, R, c->P, q_cur,
+                                   n_active, q_nxt, c->q_done, c->sq, c->qcnt);
+            if (timing) HIPCHK(c, hipEventRecord(c->ev[2], sm));
+            if (rd->integrator != PT_INTEGRATOR_SIMPLE) {
+                if (count)
+                    hipLaunchKernelGGL(k_shadow<true>, gt, dim3(PT_TRACE_BLOCK), 0, sm, c->scene, c->P, c->sq,
+                                       c->qcnt + Q_SHADOW, c->counters);
+                else
+                    hipLaunchKernelGGL(k_shadow<false>, gt, dim3(PT_TRACE_BLOCK), 0, sm, c->scene, c->P, c->sq,
+                                       c->qcnt + Q_SHADOW, c->counters);
+            }
+            if (timing) HIPCHK(c, hipEventRecord(c->ev[3], sm));
+            hipLaunchKernelGGL(k_finish, gs, dim3(256), 0, sm, R, c->P, c->q_done, c->qcnt + Q_DONE, 0u, 1, q_nxt,
+                               c->qcnt + Q_NEXT, next_sample, c->sample_L);
+            HIPCHK(c, hipGetLastError());
+            HIPCHK(c, hipMemcpyAsync(c->host_cnt, c->qcnt, 16, hipMemcpyDeviceToHost, sm));
+            HIPCHK(c, hipStreamSynchronize(sm));
+            if (stats) {
+                stats->rays_closest += n_active;
+                stats->rays_any += c->host_cnt[Q_SHADOW];
+                stats->shade_hits += n_active;
+                stats->launches_closest++;
+                if (rd->integrator != PT_INTEGRATOR_SIMPLE) stats->launches_any++;
+            }
+            if (timing) {
+                float a, b, d;
+                HIPCHK(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+                HIPCHK(c, hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+                HIPCHK(c, hipEventElapsedTime(&d, c->ev[2], c->ev[3]));
+                t_cl += a;
+                t_sh += b;
+                t_an += d;
+            }
+            n_active = c->host_cnt[Q_NEXT];
+            std::swap(q_cur, q_nxt);
+        }
+        if (stats) stats->paths += R.chunk_total;
+        if ((st = on_chunk(R)) != PT_OK) return st;
+    }
+    HIPCHK(c, hipStreamSynchronize(sm));
+    if (stats) {
+        unsigned long long h[CNT_COUNT];
+        HIPCHK(c, hipMemcpy(h, c->counters, sizeof(h), hipMemcpyDeviceToHost));
+        stats->nodes_closest += h[CNT_NODES_CLOSEST];
+        stats->tris_closest += h[CNT_TRIS_CLOSEST];
+        stats->nodes_any += h[CNT_NODES_ANY];
+        stats->tris_any += h[CNT_TRIS_ANY];
+        stats->ms_closest += t_cl;
+        stats->ms_shade += t_sh;
+        stats->ms_any += t_an;
+    }
+    (void)film_dev;
+    return PT_OK;
+}
+
+static pt_status check_render_args(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd) {
+    if (!c || !cam || !rd) return PT_ERR_ARG;
+    if (!c->has_scene) return fail(c, PT_ERR_STATE, "no scene uploaded");
+    if (cam->width <= 0 || cam->height <= 0 || (uint64_t)cam->width * cam->height > (1ull << 31))
+        return fail(c, PT_ERR_ARG, "bad film size");
+    if (rd->integrator > PT_INTEGRATOR_SIMPLE || rd->filter > PT_FILTER_GAUSSIAN)
+        return fail(c, PT_ERR_ARG, "bad integrator/filter");
+    if (rd->filter_radius[0] <= 0 || rd->filter_radius[1] <= 0) return fail(c, PT_ERR_ARG, "bad filter radius");
+    return PT_OK;
+}
+
+extern "C" pt_status pt_render(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_accum,
+                               pt_stats* stats) {
+    pt_status st = check_render_args(c, cam, rd);
+    if (st) return st;
+    if (!film_accum) return fail(c, PT_ERR_ARG, "film_accum is null");
+    if (!(rd->pixel_begin == 0 && rd->pixel_end == 0)) return fail(c, PT_ERR_ARG, "pt_render renders whole films");
+    HIPCHK(c, hipSetDevice(c->device));
+    auto t0 = std::chrono::steady_clock::now();
+    const uint64_t nfilm = 4ull * cam->width * cam->height;
+    const bool dev = is_device_ptr(film_accum);
+    double* film = film_accum;
+    if (!dev) {
+        if ((st = ensure(c, &c->film, c->film_cap, nfilm)) != PT_OK) return st;
+        film = c->film;
+        HIPCHK(c, hipMemsetAsync(film, 0, nfilm * 8, c->stream));
+    }
+    pt_stats local{};
+    pt_stats* S = stats ? stats : &local;
+    *S = pt_stats{};
+    st = run(c, cam, rd, film, S, [&](const RenderParams& R) -> pt_status {
+        const uint32_t npx = (uint32_t)cam->width * cam->height;
+        hipLaunchKernelGGL(k_gather, dim3((npx + 255) / 256), dim3(256), 0, c->stream, R, c->sample_L, film);
+        HIPCHK(c, hipGetLastError());
+        return PT_OK;
+    });
+    if (st) return st;
+    if (!dev) {
+        std::vector<double> h(nfilm);
+        HIPCHK(c, hipMemcpyAsync(h.data(), film, nfilm * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        for (uint64_t i = 0; i < nfilm; i++) film_accum[i] += h[i];
+    } else {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    S->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return PT_OK;
+}
+
+extern "C" pt_status pt_render_samples(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, float* out_L,
+                                       pt_stats* stats) {
+    pt_status st = check_render_args(c, cam, rd);
+    if (st) return st;
+    if (!out_L) return fail(c, PT_ERR_ARG, "out_L is null");
+    if (rd->shard_count > 1) return fail(c, PT_ERR_ARG, "pt_render_samples renders unsharded");
+    HIPCHK(c, hipSetDevice(c->device));
+    const bool ranged = !(rd->pixel_begin == 0 && rd->pixel_end == 0);
+    const uint32_t pb = ranged ? rd->pixel_begin : 0;
+    const uint32_t pe = ranged ? rd->pixel_end : (uint32_t)(cam->width * cam->height);
+    pt_render_desc r2 = *rd;
+    r2.pixel_begin = pb;
+    r2.pixel_end = pe;  // always linear pixel order here
+    const uint32_t npix = pe - pb;
+    pt_stats local{};
+    pt_stats* S = stats ? stats : &local;
+    *S = pt_stats{};
+    std::vector<float> h;
+    st = run(c, cam, &r2, nullptr, S, [&](const RenderParams& R) -> pt_status {
+        const uint64_t n = 3ull * R.chunk_total;
+        h.resize(n);
+        HIPCHK(c, hipMemcpyAsync(h.data(), c->sample_L, n * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        const uint32_t ns = R.s_hi - R.s_lo;
+        for (uint32_t k = 0; k < ns; k++)
+            for (uint32_t p = 0; p < npix; p++) {
+                const float* src = &h[3ull * ((uint64_t)k * npix + p)];
+                float* dst = out_L + 3ull * ((uint64_t)p * rd->spp + (R.s_lo + k));
+                dst[0] = src[0];
+                dst[1] = src[1];
+                dst[2] = src[2];
+            }
+        return PT_OK;
+    });
+    return st;
+}
+
+extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any_hit, pt_hit* hits, pt_stats* stats) {
+    if (!c || (n && (!rays || !hits))) return PT_ERR_ARG;
+    if (!c->has_scene) return fail(c, PT_ERR_STATE, "no scene uploaded");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (n == 0) return PT_OK;
+    const bool rdev = is_device_ptr(rays), hdev = is_device_ptr(hits);
+    pt_ray* dr = (pt_ray*)rays;
+    pt_hit* dh = hits;
+    std::vector<void*> tmp;
+    if (!rdev) {
+        HIPCHK(c, hipMalloc((void**)&dr, (size_t)n * sizeof(pt_ray)));
+        tmp.push_back(dr);
+        HIPCHK(c, hipMemcpyAsync(dr, rays, (size_t)n * sizeof(pt_ray), hipMemcpyHostToDevice, c->stream));
+    }
+    if (!hdev) {
+        HIPCHK(c, hipMalloc((void**)&dh, (size_t)n * sizeof(pt_hit)));
+        tmp.push_back(dh);
+    }
+    if (c->cap == 0 && ensure_work(c, 256) != PT_OK) return PT_ERR_OOM;
+    HIPCHK(c, hipMemsetAsync(c->counters, 0, CNT_COUNT * 8, c->stream));
+    auto t0 = std::chrono::steady_clock::now();
+    HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
+    hipLaunchKernelGGL(k_trace_rays, dim3((n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK), dim3(PT_TRACE_BLOCK), 0,
+                       c->stream, c->scene, dr, n, any_hit, dh, c->counters);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
+    if (!hdev) HIPCHK(c, hipMemcpyAsync(hits, dh, (size_t)n * sizeof(pt_hit), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (stats) {
+        *stats = pt_stats{};
+        unsigned long long h[CNT_COUNT];
+        HIPCHK(c, hipMemcpy(h, c->counters, sizeof(h), hipMemcpyDeviceToHost));
+        float ms;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev[4], c->ev[5]));
+        if (any_hit) {
+            stats->rays_any = n;
+            stats->nodes_any = h[CNT_NODES_ANY];
+            stats->tris_any = h[CNT_TRIS_ANY];
+            stats->ms_any = ms;
+        } else {
+            stats->rays_closest = n;
+            stats->nodes_closest = h[CNT_NODES_CLOSEST];
+            stats->tris_closest = h[CNT_TRIS_CLOSEST];
+            stats->ms_closest = ms;
+        }
+        stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    for (void* p : tmp) hipFree(p);
+    return PT_OK;
+}

@@ -1,0 +1,698 @@
+// Device restatement of the reference's surface shading: textures
+// (Texture.hpp/.cpp), materials (Material.hpp), shapes' interaction
+// reconstruction (Shape.cpp), lights and light samplers (Light.cpp,
+// LightSampler.cpp).  Each function cites the reference file:line.
+#pragma once
+#include "pt_device.h"
+
+struct SurfInt {  // SurfaceInteraction (Interaction.hpp:36-51)
+    f3 p, n, ns, tangent;
+    float u, v;  // uv
+    float t;
+    int32_t mat, light;
+};
+
+// ------------------------------------------------------------------ textures
+__device__ __forceinline__ int wrap_index(int i, int n) {
+    int m = i % n;
+    if (m < 0) m += n;
+    return m;
+}
+// Image::GetChannelAt (Texture.hpp:43-48): byte ch-1 of the pixel, any channel count.
+__device__ __forceinline__ float channel_at(const DevScene& S, const pt_image& im, int x, int y, int ch) {
+    int xi = wrap_index(x, im.width), yi = wrap_index(y, im.height);
+    uint64_t idx = im.offset + ((uint64_t)yi * (uint64_t)im.width + (uint64_t)xi) * (uint64_t)im.channels +
+                   (uint64_t)(ch - 1);
+    if (idx >= S.n_texel_bytes) return 0.0f;
+    return S.texels[idx] / 255.0f;
+}
+__device__ __forceinline__ f3 texel3(const DevScene& S, const pt_image& im, int x, int y) {
+    return F3(channel_at(S, im, x, y, 1), channel_at(S, im, x, y, 2), channel_at(S, im, x, y, 3));
+}
+
+// Texture::Evaluate for SolidColor / CheckerTexture / ImageTexture (Texture.hpp:128-207).
+__device__ f3 tex_eval(const DevScene& S, int id, float u, float v) {
+    f3 scale = F3(1, 1, 1);
+    bool scaled = false;
+    for (int guard = 0; guard < 16; guard++) {
+        const pt_texture& t = S.textures[id];
+        if (t.kind == PT_TEX_SOLID) {
+            f3 c = ld3(t.value);
+            return scaled ? scale * c : c;
+        }
+        if (t.kind == PT_TEX_CHECKER) {
+            int ux = (int)floorf(u * t.inv_scale[0]);
+            int uy = (int)floorf(v * t.inv_scale[1]);
+            // colorScale * child (Texture.hpp:205-206); nested scales multiply outward-in
+            scale = scaled ? scale * ld3(t.scale) : ld3(t.scale);
+            scaled = true;
+            id = ((ux + uy) % 2 == 0) ? t.a : t.b;
+            continue;
+        }
+        const pt_image& im = S.images[t.image];
+        float x = u * im.width - 0.5f;
+        float y = v * im.height - 0.5f;
+        int xi = (int)floorf(x), yi = (int)floorf(y);
+        float dx = x - xi, dy = y - yi;
+        f3 a = texel3(S, im, xi, yi), b = texel3(S, im, xi + 1, yi);
+        f3 c = texel3(S, im, xi, yi + 1), d = texel3(S, im, xi + 1, yi + 1);
+        f3 r = ((1 - dx) * (1 - dy)) * a + (dx * (1 - dy)) * b + ((1 - dx) * dy) * c + (dx * dy) * d;
+        r = ld3(t.scale) * r;
+        return scaled ? scale * r : r;
+    }
+    return F3(0, 0, 0);
+}
+
+// Texture::alpha (Texture.hpp:112-114, Texture.cpp:47-62, 41-45)
+__device__ float tex_alpha(const DevScene& S, int id, float u, float v) {
+    for (int guard = 0; guard < 16; guard++) {
+        const pt_texture& t = S.textures[id];
+        if (t.kind == PT_TEX_SOLID) return 1.0f;
+        if (t.kind == PT_TEX_CHECKER) {
+            int ux = (int)floorf(u * t.inv_scale[0]);
+            int uy = (int)floorf(v * t.inv_scale[1]);
+            id = ((ux + uy) % 2 == 0) ? t.a : t.b;
+            continue;
+        }
+        const pt_image& im = S.images[t.image];
+        if (im.channels != 4) return 1.0f;
+        float x = u * im.width - 0.5f;
+        float y = v * im.height - 0.5f;
+        int xi = (int)floorf(x), yi = (int)floorf(y);
+        float dx = x - xi, dy = y - yi;
+        float a = channel_at(S, im, xi, yi, 4), b = channel_at(S, im, xi + 1, yi, 4);
+        float c = channel_at(S, im, xi, yi + 1, 4), d = channel_at(S, im, xi + 1, yi + 1, 4);
+        return (1 - dx) * (1 - dy) * a + dx * (1 - dy) * b + (1 - dx) * dy * c + dx * dy * d;
+    }
+    return 1.0f;
+}
+
+__device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
+// AlphaTester Blend draws random_float() (Material.hpp:189) from an unseeded
+// thread-local generator; parity is waived there: hash of the ray.
+__device__ __forceinline__ float blend_random(f3 o, f3 d, int prim) {
+    uint32_t h = pcg_hash(fbits(o.x) ^ pcg_hash(fbits(d.y) ^ pcg_hash((uint32_t)prim)));
+    return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+
+// Material::Alpha (Material.hpp:336-342, 572-578)
+__device__ bool mat_alpha(const DevScene& S, int mid, float u, float v, f3 ro, f3 rd, int prim) {
+    if (mid < 0) return true;
+    const pt_material& m = S.materials[mid];
+    if (m.kind != PT_MAT_DIFFUSE && m.kind != PT_MAT_DIELECTRIC) return true;
+    float a = m.alpha >= 0 ? tex_eval(S, m.alpha, u, v).x : tex_alpha(S, m.tex, u, v);
+    if (m.alpha_mode == PT_ALPHA_OPAQUE) return true;
+    if (m.alpha_mode == PT_ALPHA_MASK) return a > m.alpha_cutoff;
+    return a >= 1.0f ? true : (blend_random(ro, rd, prim) < a);
+}
+
+// ------------------------------------------------------------------ onb (Onb.hpp:3-30)
+struct Onb {
+    f3 a0, a1, a2;
+};
+__device__ __forceinline__ Onb onb_n(f3 n) {
+    Onb b;
+    b.a2 = n;
+    f3 up = (fabsf(n.x) > 0.9999) ? F3(0, 1, 0) : F3(1, 0, 0);
+    b.a1 = normalize(cross(b.a2, up));
+    b.a0 = cross(b.a1, b.a2);
+    return b;
+}
+__device__ __forceinline__ Onb onb_si(const SurfInt& si) {
+    Onb b;
+    b.a2 = si.ns;
+    b.a0 = si.tangent;
+    b.a1 = cross(b.a2, b.a0);
+    return b;
+}
+__device__ __forceinline__ f3 to_world(const Onb& b, f3 v) { return v.x * b.a0 + v.y * b.a1 + v.z * b.a2; }
+__device__ __forceinline__ f3 to_local(const Onb& b, f3 v) { return F3(dot(v, b.a0), dot(v, b.a1), dot(v, b.a2)); }
+
+// sample_normalMap (Material.hpp:344-348, 580-584)
+__device__ f3 normal_map(const DevScene& S, int mid, const SurfInt& si) {
+    if (mid < 0) return si.ns;
+    const pt_material& m = S.materials[mid];
+    if ((m.kind != PT_MAT_DIFFUSE && m.kind != PT_MAT_DIELECTRIC) || m.norm < 0) return si.ns;
+    f3 t = tex_eval(S, m.norm, si.u, si.v);
+    f3 nn = normalize(2.0f * t - F3(1, 1, 1));
+    return to_world(onb_si(si), nn);
+}
+
+__device__ __forceinline__ void sphere_uv(f3 p, float& u, float& v) {
+    // SphereShape::GetSphereUV (Shape.hpp:35-43)
+    p = normalize(p);
+    float theta = acosf(clampf(p.y, -1.0f, 1.0f));
+    float phi = atan2f(p.z, p.x);
+    if (phi < 0) phi += 2.0f * PT_PI;
+    u = PT_INV_PI * phi * 0.5f;
+    v = PT_INV_PI * theta;
+}
+
+// ------------------------------------------------------------------ interaction reconstruction
+// TriangleShape::Intersect shading part (Shape.cpp:206-242) from the hit's
+// barycentrics; identical to computing it at the candidate (the reference does
+// it per candidate, only the last accepted survives).
+__device__ void tri_interaction(const DevScene& S, const DevGeom& g, uint32_t tri, int mid, f3 o, f3 d, float t,
+                                float bu, float bv, SurfInt& si) {
+    uint4 T = S.tri[tri];
+    float u = bu, v = bv, w = 1.0f - u - v;
+    const float* uvs = S.uvs;
+    si.u = u * uvs[2 * T.y] + v * uvs[2 * T.z] + w * uvs[2 * T.x];
+    si.v = u * uvs[2 * T.y + 1] + v * uvs[2 * T.z + 1] + w * uvs[2 * T.x + 1];
+    const float* nr = S.normals;
+    f3 nn = normalize(u * ld3(nr + 3 * T.y) + v * ld3(nr + 3 * T.z) + w * ld3(nr + 3 * T.x));
+    f3 N = normalize(cross(xyz(g.b), xyz(g.c)));
+    si.n = N;
+    if (dot(N, nn) < 0) nn = -nn;
+    si.t = t;
+    si.ns = nn;
+    si.p = (o + t * d) + (PT_EPS * N) * (dot(d, N) > 0.0f ? -1.0f : 1.0f);
+    if (T.w & 1u) {
+        const float* tg = S.tangents;
+        f3 tv = u * ld3(tg + 3 * T.y) + v * ld3(tg + 3 * T.z) + w * ld3(tg + 3 * T.x);
+        si.tangent = normalize(tv - si.ns * dot(si.ns, tv));
+    } else {
+        f3 up = (fabsf(si.ns.x) > 0.9999f) ? F3(0, 1, 0) : F3(1, 0, 0);
+        si.tangent = normalize(cross(up, si.ns));
+    }
+    si.ns = normal_map(S, mid, si);
+}
+
+// QuadShape::Intersect (Shape.cpp:320-343) interaction part.
+__device__ void quad_interaction(const pt_quad& q, f3 o, f3 d, float t, float a, float b, SurfInt& si) {
+    f3 normal = ld3(q.normal);
+    f3 nn = dot(d, normal) > 0 ? -normal : normal;
+    si.u = a;
+    si.v = b;
+    si.t = t;
+    si.ns = nn;
+    si.n = normal;
+    f3 up = (fabsf(si.ns.x) > 0.9999f) ? F3(0, 1, 0) : F3(1, 0, 0);
+    si.tangent = normalize(cross(up, si.ns));
+    si.p = (o + t * d) + PT_EPS * nn;
+}
+
+// SphereShape::Intersect (Shape.cpp:3-37) interaction part.
+__device__ void sphere_interaction(const pt_sphere& sp, f3 o, f3 d, float t, SurfInt& si) {
+    si.t = t;
+    si.ns = normalize((o + t * d) - ld3(sp.center));
+    si.n = si.ns;
+    f3 up = (fabsf(si.ns.x) > 0.9999f) ? F3(0, 1, 0) : F3(1, 0, 0);
+    si.tangent = normalize(cross(up, si.ns));
+    si.p = (o + t * d) + PT_EPS * si.n;
+    sphere_uv(si.n, si.u, si.v);
+}
+
+// ------------------------------------------------------------------ microfacet (Material.hpp:55-142)
+struct Dist {
+    float ax, ay;
+};
+__device__ __forceinline__ Dist mkdist(float r) { return Dist{r * r, r * r}; }
+__device__ float lambda_(const Dist& D, f3 w) {
+    float cos2 = w.z * w.z;
+    if (cos2 == 0) return 0;
+    float sin2 = smax(0, 1 - cos2);
+    float sinT = csqrt(sin2);
+    float cosPhi = sinT == 0 ? 1 : clampf(w.x / sinT, -1.0f, 1.0f);
+    float sinPhi = sinT == 0 ? 0 : clampf(w.y / sinT, -1.0f, 1.0f);
+    float alpha2 = (cosPhi * D.ax) * (cosPhi * D.ax) + (sinPhi * D.ay) * (sinPhi * D.ay);
+    return (csqrt(1.f + alpha2 * sin2 / cos2) - 1.0f) / 2.0f;
+}
+__device__ float D_(const Dist& D, f3 wh) {
+    float cos2 = wh.z * wh.z;
+    if (cos2 == 0) return 0;
+    float cos4 = cos2 * cos2;
+    float sin2 = smax(0, 1 - cos2);
+    float sinT = csqrt(sin2);
+    float cosPhi = sinT == 0 ? 1 : clampf(wh.x / sinT, -1.0f, 1.0f);
+    float sinPhi = sinT == 0 ? 0 : clampf(wh.y / sinT, -1.0f, 1.0f);
+    float e = sin2 / cos2 * ((cosPhi / D.ax) * (cosPhi / D.ax) + (sinPhi / D.ay) * (sinPhi / D.ay));
+    float denom = PT_PI * D.ax * D.ay * cos4 * (1 + e) * (1 + e);
+    if (denom <= 0) return __int_as_float(0x7f800000);
+    return 1 / denom;
+}
+__device__ __forceinline__ float G1_(const Dist& D, f3 w) { return 1 / (1 + lambda_(D, w)); }
+__device__ __forceinline__ float G_(const Dist& D, f3 wo, f3 wi) { return 1 / (1 + lambda_(D, wo) + lambda_(D, wi)); }
+__device__ __forceinline__ bool smooth_(const Dist& D) { return smax(D.ax, D.ay) < 1e-6; }
+__device__ __forceinline__ float mpdf_(const Dist& D, f3 wo, f3 wh) {
+    return D_(D, wh) * G1_(D, wo) * fabsf(dot(wo, wh) / wo.z);
+}
+__device__ f3 vndf_(float ax, float ay, f3 Ve, float U1, float U2) {
+    f3 Vh = normalize(F3(ax * Ve.x, ay * Ve.y, Ve.z));
+    float lensq = Vh.x * Vh.x + Vh.y * Vh.y;
+    f3 T1 = lensq > 0 ? F3(-Vh.y, Vh.x, 0) * (1.0f / csqrt(lensq)) : F3(1, 0, 0);
+    f3 T2 = cross(Vh, T1);
+    float r = csqrt(U1);
+    float phi = 2.0f * PT_PI * U2;
+    float t1 = r * cosf(phi);
+    float t2 = r * sinf(phi);
+    float s = 0.5f * (1.0f + Vh.z);
+    t2 = (1.0f - s) * csqrt(1.0f - t1 * t1) + s * t2;
+    f3 Nh = t1 * T1 + t2 * T2 + csqrt(smax(0.0f, 1.0f - t1 * t1 - t2 * t2)) * Vh;
+    return normalize(F3(ax * Nh.x, ay * Nh.y, smax(0.0f, Nh.z)));
+}
+__device__ __forceinline__ f3 sample_wh(const Dist& D, f3 wo, float u0, float u1) {
+    bool flip = wo.z < 0;
+    f3 wh = vndf_(D.ax, D.ay, flip ? -wo : wo, u0, u1);
+    return flip ? -wh : wh;
+}
+__device__ float fresnel_dielectric(float cosi, float eta) {  // Material.hpp:11-28
+    cosi = clampf(cosi, -1.0f, 1.0f);
+    if (cosi < 0) {
+        eta = 1 / eta;
+        cosi = -cosi;
+    }
+    float sin2i = 1 - cosi * cosi;
+    float sin2t = sin2i / (eta * eta);
+    if (sin2t >= 1) return 1.f;
+    float cost = csqrt(1 - sin2t);
+    float rpa = (eta * cosi - cost) / (eta * cosi + cost);
+    float rpe = (cosi - eta * cost) / (cosi + eta * cost);
+    return (rpa * rpa + rpe * rpe) / 2;
+}
+__device__ __forceinline__ f3 schlick(float c, f3 F0) {  // Material.hpp:30-32
+    float p = powf(1.0f - c, 5.0f);
+    return F0 + (F3(1, 1, 1) - F0) * p;
+}
+
+// ------------------------------------------------------------------ materials
+#define FL_TRANS 1u
+#define FL_SPEC 2u
+struct Bxdf {
+    f3 f, o, d;
+    float pdf;
+    uint32_t flags;
+    bool ok;
+};
+
+__device__ __forceinline__ float diffuse_rough(const DevScene& S, const pt_material& m, const SurfInt& si) {
+    return smax(tex_eval(S, m.rough, si.u, si.v).y, 0.0001f);
+}
+__device__ __forceinline__ f3 mixv(f3 x, f3 y, float a) { return x * (1.0f - a) + y * a; }
+
+// MicrofacetDiffuse::scatter (Material.hpp:206-266)
+__device__ Bxdf diffuse_scatter(const DevScene& S, const pt_material& m, f3 ind, const SurfInt& si, float u,
+                                float uv0, float uv1) {
+    Bxdf b;
+    b.ok = false;
+    float rough = diffuse_rough(S, m, si);
+    Onb tbn = onb_n(dot(ind, si.ns) > 0 ? -si.ns : si.ns);
+    Dist D = mkdist(rough);
+    float prob = rough >= 0.7 ? 1.0f : 0.5f;
+    f3 wo = to_local(tbn, -ind);
+    f3 wi, wh;
+    if (u >= prob) {
+        wh = sample_wh(D, wo, uv0, uv1);
+        wi = reflect(-wo, wh);
+    } else {
+        float z = csqrt(1.0f - uv1);
+        float phi = 2.0f * PT_PI * uv0;
+        float s2 = csqrt(uv1);
+        wi = F3(cosf(phi) * s2, sinf(phi) * s2, z);
+        wh = normalize(wo + wi);
+    }
+    if (wi.z <= 0) return b;
+    float dpdf = prob * wi.z * PT_INV_PI;
+    float spdf = (1.0f - prob) * mpdf_(D, wo, wh) / (4 * fabsf(dot(wo, wh)));
+    float pdf = dpdf + spdf;
+    f3 col = tex_eval(S, m.tex, si.u, si.v);
+    float metal = tex_eval(S, m.metal, si.u, si.v).z;
+    f3 F0 = mixv(F3(0.04f, 0.04f, 0.04f), col, metal);
+    f3 F = schlick(dot(wi, wh), F0);
+    f3 num = (D_(D, wh) * G_(D, wo, wi)) * F;
+    float den = fabsf(4.0f * wo.z * wi.z);
+    if (den == 0) return b;
+    f3 spec = num / den;
+    f3 kD = (F3(1, 1, 1) - F) * (1.0f - metal);
+    f3 diff = (kD * col) * PT_INV_PI;
+    b.f = diff + spec;
+    b.pdf = pdf;
+    b.flags = 0;
+    b.o = si.p;
+    b.d = to_world(tbn, wi);
+    b.ok = true;
+    return b;
+}
+// MicrofacetDiffuse::calc_attenuation (Material.hpp:299-326)
+__device__ f3 diffuse_f(const DevScene& S, const pt_material& m, f3 ind, const SurfInt& si, f3 dir) {
+    Onb tbn = onb_n(dot(ind, si.ns) > 0 ? -si.ns : si.ns);
+    f3 wo = to_local(tbn, -ind);
+    f3 wi = to_local(tbn, dir);
+    f3 wh = normalize(wo + wi);
+    float rough = diffuse_rough(S, m, si);
+    float metal = tex_eval(S, m.metal, si.u, si.v).z;
+    Dist D = mkdist(rough);
+    f3 col = tex_eval(S, m.tex, si.u, si.v);
+    f3 F0 = mixv(F3(0.04f, 0.04f, 0.04f), col, metal);
+    f3 F = schlick(dot(wi, wh), F0);
+    f3 num = (D_(D, wh) * G_(D, wo, wi)) * F;
+    float den = fabsf(4.0f * wo.z * wi.z);
+    if (den == 0) return F3(0, 0, 0);
+    f3 kD = (F3(1, 1, 1) - F) * (1.0f - metal);
+    return (kD * col) * PT_INV_PI + num / den;
+}
+// MicrofacetDiffuse::PDF (Material.hpp:281-296): no (1-prob) on the specular term (A.7)
+__device__ float diffuse_pdf(const DevScene& S, const pt_material& m, f3 ind, const SurfInt& si, f3 dir) {
+    float rough = diffuse_rough(S, m, si);
+    Dist D = mkdist(rough);
+    Onb tbn = onb_n(dot(ind, si.ns) > 0 ? -si.ns : si.ns);
+    f3 wo = to_local(tbn, -ind);
+    f3 wh = to_local(tbn, normalize(dir - ind));
+    float prob = rough >= 0.7 ? 1.0f : 0.5f;
+    float diff = prob * fabsf(dot(si.ns, dir)) * PT_INV_PI;
+    float spec = mpdf_(D, wo, wh) / (4 * fabsf(dot(wo, wh)));
+    return diff + spec;
+}
+
+// MicrofacetDielectric::scatter (Material.hpp:392-477)
+__device__ Bxdf dielectric_scatter(const DevScene& S, const pt_material& m, f3 ino, f3 ind, const SurfInt& si,
+                                   float u, float uv0, float uv1) {
+    Bxdf b;
+    b.ok = false;
+    float rough = tex_eval(S, m.rough, si.u, si.v).y;
+    Dist D = mkdist(rough);
+    Onb tbn = onb_si(si);
+    f3 wo = to_local(tbn, -ind);
+    float ri = m.ri;
+    float eta = dot(-ind, si.ns) > 0 ? 1 / ri : ri;
+    f3 hitp = ino + si.t * ind;
+    if (ri == 1 || smooth_(D)) {
+        f3 N = dot(ind, si.ns) > 0 ? -si.ns : si.ns;
+        f3 Ng = dot(ind, si.n) > 0 ? -si.n : si.n;
+        float F = fresnel_dielectric(wo.z, ri);
+        float R = F, T = 1.0f - R;
+        f3 dir;
+        if (u < (R / (R + T))) {
+            dir = to_world(tbn, F3(-wo.x, -wo.y, wo.z));
+            b.o = hitp + PT_EPS * Ng;
+            b.f = (tex_eval(S, m.tex, si.u, si.v) * R) / fabsf(dot(si.ns, dir));
+            b.pdf = R / (R + T);
+        } else {
+            dir = refract(ind, N, eta);
+            if (is_zero(dir)) return b;
+            b.o = hitp - PT_EPS * Ng;
+            b.f = (tex_eval(S, m.tex, si.u, si.v) * T) / fabsf(dot(si.ns, dir));
+            b.pdf = T / (R + T);
+        }
+        b.d = dir;
+        b.flags = FL_TRANS | FL_SPEC;
+        b.ok = true;
+        return b;
+    }
+    f3 wh = sample_wh(D, wo, uv0, uv1);
+    f3 Ng = dot(ind, si.n) > 0 ? -si.n : si.n;
+    float F = fresnel_dielectric(dot(wo, wh), 1 / eta);
+    float R = F, T = 1 - R;
+    uint32_t fl = FL_TRANS | (rough < 0.001f ? FL_SPEC : 0u);
+    if (u < (R / (R + T))) {
+        f3 wi = reflect(-wo, wh);
+        if (wo.z * wi.z < 0) return b;
+        b.o = hitp + PT_EPS * Ng;
+        b.d = to_world(tbn, wi);
+        b.pdf = mpdf_(D, wo, wh) / (4 * fabsf(dot(wo, wh))) * R / (R + T);
+        b.f = (((tex_eval(S, m.tex, si.u, si.v) * D_(D, wh)) * G_(D, wo, wi)) * R) / fabsf(4 * wi.z * wo.z);
+    } else {
+        f3 wi = refract(-wo, wh, eta);
+        if (wo.z * wi.z > 0 || wi.z == 0) return b;
+        b.o = hitp - PT_EPS * Ng;
+        b.d = to_world(tbn, wi);
+        float denom = (dot(wi, wh) + dot(wo, wh) * eta) * (dot(wi, wh) + dot(wo, wh) * eta);
+        float dwh = fabsf(dot(wi, wh)) / denom;
+        b.pdf = mpdf_(D, wo, wh) * dwh * T / (R + T);
+        float ft = T * D_(D, wh) * G_(D, wo, wi) * fabsf(dot(wi, wh) * dot(wo, wh) / (denom * wi.z * wo.z));
+        b.f = tex_eval(S, m.tex, si.u, si.v) * ft;
+    }
+    b.flags = fl;
+    b.ok = true;
+    return b;
+}
+// MicrofacetDielectric::PDF / calc_attenuation (Material.hpp:484-564)
+__device__ void dielectric_eval(const DevScene& S, const pt_material& m, f3 ind, const SurfInt& si, f3 dir,
+                                f3& f_out, float& pdf_out) {
+    f_out = F3(0, 0, 0);
+    pdf_out = 0;
+    float rough = tex_eval(S, m.rough, si.u, si.v).y;
+    Dist D = mkdist(rough);
+    float ri = m.ri;
+    if (ri == 1 || smooth_(D)) return;
+    Onb tbn = onb_si(si);
+    f3 wo = to_local(tbn, -ind);
+    f3 wi = to_local(tbn, dir);
+    float co = wo.z, ci = wi.z;
+    bool refl = ci * co > 0;
+    float etap = 1;
+    if (!refl) etap = co > 0 ? ri : (1 / ri);
+    f3 wh = wi * etap + wo;
+    if (dot(wh, wh) == 0) return;
+    wh = normalize(wh);
+    if (wh.z < 0) wh = -wh;
+    if (dot(wh, wi) * ci <= 0.0 || dot(wh, wo) * co <= 0.0) return;
+    float F = fresnel_dielectric(dot(wo, wh), ri);
+    float R = F, T = 1 - R;
+    float pdf = mpdf_(D, wo, wh);
+    f3 col = tex_eval(S, m.tex, si.u, si.v);
+    if (refl) {
+        pdf_out = pdf / (4 * fabsf(dot(wo, wh))) * R / (R + T);
+        f_out = (((col * D_(D, wh)) * G_(D, wo, wi)) * F) / fabsf(4 * ci * co);
+    } else {
+        float den = (dot(wi, wh) + dot(wo, wh) / etap) * (dot(wi, wh) + dot(wo, wh) / etap);
+        float dwh = fabsf(dot(wi, wh)) / den;
+        pdf_out = pdf * dwh * T / (R + T);
+        float den2 = (dot(wi, wh) + dot(wo, wh) / etap) * (dot(wi, wh) + dot(wo, wh) / etap) * ci * co;
+        float ft = D_(D, wh) * (1 - F) * G_(D, wo, wi) * fabsf(dot(wi, wh) * dot(wo, wh) / den2);
+        f_out = col * ft;
+    }
+}
+// ThinDielectric::scatter (Material.hpp:605-644)
+__device__ Bxdf thin_scatter(const DevScene& S, const pt_material& m, f3 ino, f3 ind, const SurfInt& si, float u) {
+    Bxdf b;
+    Onb tbn = onb_si(si);
+    f3 wo = to_local(tbn, -ind);
+    f3 Ng = dot(ind, si.n) > 0 ? -si.n : si.n;
+    float F = fresnel_dielectric(wo.z, m.ri);
+    float R = F, T = 1.0f - R;
+    if (R < 1.0f) {
+        R += T * T * R / (1.0f - R * R);
+        T = 1.0f - R;
+    }
+    f3 hitp = ino + si.t * ind;
+    f3 dir, f;
+    if (u < (R / (R + T))) {
+        dir = to_world(tbn, F3(-wo.x, -wo.y, wo.z));
+        b.o = hitp + PT_EPS * Ng;
+        f = (F3(1, 1, 1) * R) / fabsf(dot(si.ns, dir));
+        b.pdf = R / (R + T);
+    } else {
+        dir = ind;
+        b.o = hitp - PT_EPS * Ng;
+        f = (F3(1, 1, 1) * T) / fabsf(dot(si.ns, dir));
+        b.pdf = T / (R + T);
+    }
+    b.f = f * tex_eval(S, m.tex, si.u, si.v);
+    b.d = dir;
+    b.flags = FL_TRANS | FL_SPEC;
+    b.ok = true;
+    return b;
+}
+// SpecularConductor::scatter (Material.hpp:664-669)
+__device__ Bxdf conductor_scatter(const pt_material& m, f3 ind, const SurfInt& si) {
+    Bxdf b;
+    b.ok = false;
+    f3 d = reflect(ind, si.ns);
+    float dt = dot(d, si.ns);
+    if (dt <= 0) return b;
+    b.f = schlick(dot(si.ns, -ind), ld3(m.albedo)) / dt;
+    b.pdf = 1;
+    b.flags = FL_SPEC;
+    b.o = si.p;
+    b.d = d;
+    b.ok = true;
+    return b;
+}
+
+__device__ Bxdf mat_scatter(const DevScene& S, int mid, f3 ino, f3 ind, const SurfInt& si, float u, float uv0,
+                            float uv1) {
+    const pt_material& m = S.materials[mid];
+    switch (m.kind) {
+        case PT_MAT_DIFFUSE: return diffuse_scatter(S, m, ind, si, u, uv0, uv1);
+        case PT_MAT_DIELECTRIC: return dielectric_scatter(S, m, ino, ind, si, u, uv0, uv1);
+        case PT_MAT_THIN: return thin_scatter(S, m, ino, ind, si, u);
+        default: return conductor_scatter(m, ind, si);
+    }
+}
+__device__ f3 mat_f(const DevScene& S, int mid, f3 ind, const SurfInt& si, f3 dir) {
+    const pt_material& m = S.materials[mid];
+    f3 f;
+    float p;
+    switch (m.kind) {
+        case PT_MAT_DIFFUSE: return diffuse_f(S, m, ind, si, dir);
+        case PT_MAT_DIELECTRIC: dielectric_eval(S, m, ind, si, dir, f, p); return f;
+        case PT_MAT_THIN: return F3(0, 0, 0);
+        default: return F3(1, 1, 1);  // base Material::calc_attenuation
+    }
+}
+__device__ float mat_pdf(const DevScene& S, int mid, f3 ind, const SurfInt& si, f3 dir) {
+    const pt_material& m = S.materials[mid];
+    f3 f;
+    float p;
+    switch (m.kind) {
+        case PT_MAT_DIFFUSE: return diffuse_pdf(S, m, ind, si, dir);
+        case PT_MAT_DIELECTRIC: dielectric_eval(S, m, ind, si, dir, f, p); return p;
+        default: return 0;
+    }
+}
+
+// ------------------------------------------------------------------ lights (Light.cpp)
+struct LSample {
+    f3 L, p, n, dir;
+    float u, v;
+};
+__device__ __forceinline__ uint4 tri_idx(const DevScene& S, uint32_t tri) { return S.tri[tri]; }
+
+__device__ float shape_area(const DevScene& S, uint32_t kind, uint32_t index) {
+    if (kind == PT_PRIM_QUAD) {
+        const pt_quad& q = S.quads[index];
+        return length(cross(ld3(q.u), ld3(q.v)));
+    }
+    if (kind == PT_PRIM_SPHERE) {
+        float r = S.spheres[index].radius;
+        return 4.0f * PT_PI * r * r;
+    }
+    uint4 T = tri_idx(S, index);
+    f3 v0 = ld3(S.positions + 3 * T.x), v1 = ld3(S.positions + 3 * T.y), v2 = ld3(S.positions + 3 * T.z);
+    return length(cross(v0 - v2, v1 - v2)) * 0.5f;
+}
+// Shape::Sample (Shape.cpp:74-81, 277-297; Shape.hpp:139-141)
+__device__ void shape_sample(const DevScene& S, uint32_t kind, uint32_t index, float u0, float u1, LSample& ls) {
+    ls.u = 0;
+    ls.v = 0;
+    if (kind == PT_PRIM_QUAD) {
+        const pt_quad& q = S.quads[index];
+        ls.p = ld3(q.Q) + u0 * ld3(q.u) + u1 * ld3(q.v);
+        ls.n = ld3(q.normal);
+    } else if (kind == PT_PRIM_SPHERE) {
+        const pt_sphere& sp = S.spheres[index];
+        float z = 1.0f - 2.0f * u0;
+        float r = csqrt(1.0f - z * z);
+        float phi = 2.0f * PT_PI * u1;
+        f3 d = F3(r * cosf(phi), r * sinf(phi), z);
+        f3 c = ld3(sp.center);
+        ls.p = c + sp.radius * d;
+        ls.n = normalize(ls.p - c);
+        sphere_uv(ls.p, ls.u, ls.v);
+    } else {
+        float w = 1.0f - u0 - u1;  // not folded
+        uint4 T = tri_idx(S, index);
+        f3 v0 = ld3(S.positions + 3 * T.x), v1 = ld3(S.positions + 3 * T.y), v2 = ld3(S.positions + 3 * T.z);
+        f3 n = normalize(cross(v1 - v0, v2 - v0));
+        if (n.x != n.x) n = F3(0, 0, 0);
+        ls.p = u0 * v1 + u1 * v2 + w * v0;
+        const float* uvs = S.uvs;
+        ls.u = u0 * uvs[2 * T.y] + u1 * uvs[2 * T.z] + w * uvs[2 * T.x];
+        ls.v = u0 * uvs[2 * T.y + 1] + u1 * uvs[2 * T.z + 1] + w * uvs[2 * T.x + 1];
+        ls.n = n;
+    }
+}
+// Shape::PDF(interaction, ray) (Shape.cpp:61-67, 303-315; Shape.hpp:151-158)
+__device__ float shape_pdf(const DevScene& S, uint32_t kind, uint32_t index, f3 p, f3 n, f3 ro, f3 rd) {
+    f3 to = p - ro;
+    float d2 = dot(to, to);
+    float lc = fabsf(dot(-rd, n));
+    float area = shape_area(S, kind, index);
+    if (kind == PT_PRIM_QUAD) {
+        if (area == 0) return 0;
+    } else if (kind == PT_PRIM_SPHERE) {
+        if (area * lc == 0) return 0;
+    } else {
+        if (area == 0 || lc == 0 || n.x != n.x) return 0;
+    }
+    return d2 / (lc * area);
+}
+__device__ __forceinline__ f3 inf_le(const pt_light& l, f3 d) {
+    if (l.kind == PT_LIGHT_SKY_INF) {  // main.cpp:292-295 gradient
+        float a = 0.5f * (d.y + 1.0f);
+        return l.scale * ((1.0f - a) * ld3(l.color) + a * ld3(l.vec));
+    }
+    return ld3(l.color);
+}
+__device__ LSample light_sample(const DevScene& S, const pt_light& l, float u0, float u1) {
+    LSample ls;
+    ls.L = F3(0, 0, 0);
+    ls.p = F3(0, 0, 0);
+    ls.n = F3(0, 0, 0);
+    ls.dir = F3(0, 0, 0);
+    ls.u = ls.v = 0;
+    if (l.kind == PT_LIGHT_AREA) {  // AreaLight::sample (Light.cpp:261-263)
+        const DevPrimInfo& pi = S.info[l.prim];
+        uint32_t kind = __float_as_uint(S.geom[l.prim].a.w) & GF_KIND;
+        shape_sample(S, kind, pi.index, u0, u1, ls);
+        return ls;
+    }
+    if (l.kind == PT_LIGHT_POINT) {  // Light.cpp:236-238
+        ls.L = ld3(l.color);
+        ls.p = ld3(l.vec);
+        ls.n = F3(1, 1, 1);
+        ls.u = u0;
+        ls.v = u1;
+        return ls;
+    }
+    float z = 2.0f * u0 - 1.0f;
+    float th = 2.0f * PT_PI * u1;
+    float r = csqrt(1.0f - z * z);
+    f3 d = F3(r * cosf(th), r * sinf(th), z);
+    if (l.kind == PT_LIGHT_DISTANT) {  // Light.cpp:208-215
+        ls.L = ld3(l.color);
+        ls.u = u0;
+        ls.v = u1;
+        ls.dir = normalize(ld3(l.vec) + d * 0.02f);
+        return ls;
+    }
+    ls.L = inf_le(l, d);  // Light.cpp:35-42, 61-68
+    sphere_uv(d, ls.u, ls.v);
+    ls.dir = d;
+    return ls;
+}
+__device__ __forceinline__ bool light_is_delta(const pt_light& l) {
+    return l.kind == PT_LIGHT_DISTANT || l.kind == PT_LIGHT_POINT;
+}
+// Light::PDF(interaction, ray)
+__device__ float light_pdf(const DevScene& S, const pt_light& l, f3 p, f3 n, f3 ro, f3 rd) {
+    if (l.kind == PT_LIGHT_AREA) {  // Light.cpp:267-272
+        uint32_t kind = __float_as_uint(S.geom[l.prim].a.w) & GF_KIND;
+        uint32_t index = S.info[l.prim].index;
+        if (l.one_sided) return dot(-rd, n) > 0 ? shape_pdf(S, kind, index, p, n, ro, rd) : 0;
+        return shape_pdf(S, kind, index, p, n, ro, rd);
+    }
+    if (l.kind == PT_LIGHT_UNIFORM_INF || l.kind == PT_LIGHT_SKY_INF) return 1.0f / (4.0f * PT_PI);
+    return 0;
+}
+// Light::L(interaction, ray)
+__device__ f3 light_L(const DevScene& S, const pt_light& l, f3 n, float u, float v, f3 rd) {
+    if (l.kind == PT_LIGHT_AREA) {  // Light.cpp:257-260
+        if (l.one_sided && dot(rd, n) > 0) return F3(0, 0, 0);
+        return tex_eval(S, l.tex, u, v);
+    }
+    if (l.kind == PT_LIGHT_UNIFORM_INF || l.kind == PT_LIGHT_SKY_INF) return inf_le(l, rd);
+    return F3(0, 0, 0);
+}
+// LightSampler::Sample (LightSampler.cpp:7-11, 34-46); the power sampler's
+// linear scan becomes a binary search for the first running sum >= u*total
+// over the same float running sums (identical pick for every u).
+__device__ int ls_sample(const DevScene& S, float u) {
+    uint32_t n = S.n_sampler_lights;
+    if (n == 0) return -1;
+    if (S.light_sampler == PT_LS_UNIFORM) {
+        int idx = (int)(u * n);
+        if (idx > (int)n - 1) idx = (int)n - 1;
+        return (int)S.sampler_lights[idx];
+    }
+    float target = u * S.sampler_total;
+    uint32_t lo = 0, hi = n;  // first i with cdf[i] >= target
+    while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (S.sampler_cdf[mid] >= target) hi = mid;
+        else lo = mid + 1;
+    }
+    if (lo >= n) lo = n - 1;
+    return (int)S.sampler_lights[lo];
+}

@@ -1,0 +1,419 @@
+"""Scene -> flat, device-ready arrays (pt_scene_desc of include/pt_api.h).
+
+Primitive slots are laid out in BVH leaf order: slots [0, n_top) are the TLAS
+primitives (Scene::Add order permuted by the TLAS build), followed by every
+Model's BLAS primitives in its own leaf order.  Light order is the reference's:
+Scene::GetLights() walks the TLAS primitives in leaf order, descending into
+each Model's BLAS leaf order (BVH.hpp:69-81, Model.hpp:33-35), then
+Scene::infiniteLights (Scene.cpp:39-43); lights added to the light sampler
+afterwards come last.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from . import native as N
+from .scene import (AlphaMode, AreaLight, CheckerTexture, DistantLight, FunctionInfiniteLight, GeometricPrimitive,
+                    ImageTexture, LightSampler, Material, MicrofacetDielectric, MicrofacetDiffuse, Model, PointLight,
+                    PowerLightSampler, QuadShape, Scene, SolidColor, SpecularConductor, SphereShape, Texture,
+                    ThinDielectric, UniformInfiniteLight, UniformLightSampler)
+
+
+@dataclass
+class FlatScene:
+    positions: np.ndarray
+    normals: np.ndarray
+    uvs: np.ndarray
+    tangents: np.ndarray
+    tri_vidx: np.ndarray
+    tri_flags: np.ndarray
+    quads: np.ndarray
+    spheres: np.ndarray
+    prims: np.ndarray
+    bvh_clusters: List[np.ndarray]
+    bvh_roots: List[np.void]
+    bvh_prim_base: List[int]
+    bvh_n_prims: List[int]
+    materials: np.ndarray
+    textures: np.ndarray
+    images: np.ndarray
+    texels: np.ndarray
+    bbox: np.ndarray
+    tlas_lights: list                 # AreaLights in TLAS GetLights order
+    light_slot: Dict[int, int]        # id(AreaLight) -> prim slot
+    material_ids: Dict[int, int]      # id(Material) -> index
+    top_order: np.ndarray             # TLAS slot -> Scene.Add index
+    blas_orders: List[np.ndarray]     # per model: slot -> model-local triangle
+    model_tri_base: List[int]         # per model: first global triangle id
+    texture_ids: Dict[int, int]
+    # light tables (set by bind_lights)
+    lights: Optional[np.ndarray] = None
+    light_sampler: int = 0
+    sampler_lights: Optional[np.ndarray] = None
+    infinite_lights: Optional[np.ndarray] = None
+    light_objects: list = field(default_factory=list)
+
+    @property
+    def n_prims(self) -> int:
+        return int(self.prims.shape[0])
+
+    def desc(self):
+        """pt_scene_desc referencing these arrays (keep self alive while used)."""
+        d = N.SceneDesc()
+        d.positions = N.ptr(self.positions)
+        d.normals = N.ptr(self.normals)
+        d.uvs = N.ptr(self.uvs)
+        d.tangents = N.ptr(self.tangents)
+        d.n_vertices = self.positions.shape[0] if self.positions.size else 0
+        d.tri_vidx = N.ptr(self.tri_vidx)
+        d.tri_flags = N.ptr(self.tri_flags)
+        d.n_triangles = self.tri_flags.shape[0]
+        d.quads = N.ptr(self.quads)
+        d.n_quads = self.quads.shape[0]
+        d.spheres = N.ptr(self.spheres)
+        d.n_spheres = self.spheres.shape[0]
+        d.prims = N.ptr(self.prims)
+        d.n_prims = self.prims.shape[0]
+        bv = (N.BvhDesc * len(self.bvh_clusters))()
+        for i, (cl, root) in enumerate(zip(self.bvh_clusters, self.bvh_roots)):
+            bv[i].clusters = N.ptr(cl)
+            bv[i].n_clusters = cl.shape[0]
+            bv[i].root = N.RefNode(int(root["count"]), int(root["active"]), int(root["perm"]), 0,
+                                   int(root["cluster_idx"]))
+            bv[i].prim_base = self.bvh_prim_base[i]
+            bv[i].n_prims = self.bvh_n_prims[i]
+        self._bvh_keep = bv
+        d.bvhs = C.cast(bv, C.c_void_p).value
+        d.n_bvhs = len(self.bvh_clusters)
+        d.materials = N.ptr(self.materials)
+        d.n_materials = self.materials.shape[0]
+        d.textures = N.ptr(self.textures)
+        d.n_textures = self.textures.shape[0]
+        d.images = N.ptr(self.images)
+        d.n_images = self.images.shape[0]
+        d.texels = N.ptr(self.texels)
+        d.n_texel_bytes = self.texels.size
+        if self.lights is None:
+            raise RuntimeError("lights not bound: use an Integrator (bind_lights)")
+        d.lights = N.ptr(self.lights)
+        d.n_lights = self.lights.shape[0]
+        d.light_sampler = self.light_sampler
+        d.sampler_lights = N.ptr(self.sampler_lights)
+        d.n_sampler_lights = self.sampler_lights.shape[0]
+        d.infinite_lights = N.ptr(self.infinite_lights)
+        d.n_infinite_lights = self.infinite_lights.shape[0]
+        return d
+
+
+class _Registry:
+    def __init__(self):
+        self.textures: List[np.void] = []
+        self.tex_ids: Dict[int, int] = {}
+        self.images: List[tuple] = []
+        self.texel_chunks: List[np.ndarray] = []
+        self.texel_bytes = 0
+        self.materials: List[np.void] = []
+        self.mat_ids: Dict[int, int] = {}
+
+    def texture(self, t: Optional[Texture]) -> int:
+        if t is None:
+            return -1
+        if id(t) in self.tex_ids:
+            return self.tex_ids[id(t)]
+        rec = np.zeros(1, dtype=N.TEXTURE)[0]
+        rec["scale"] = t.colorScale
+        rec["a"] = -1
+        rec["b"] = -1
+        rec["image"] = -1
+        if isinstance(t, SolidColor):
+            rec["kind"] = N.PT_TEX_SOLID
+            # SolidColor::Evaluate = colorScale * albedo, precomputed in float32
+            rec["value"] = (t.colorScale * t.albedo).astype(np.float32)
+        elif isinstance(t, CheckerTexture):
+            rec["kind"] = N.PT_TEX_CHECKER
+            rec["a"] = self.texture(t.tex1)
+            rec["b"] = self.texture(t.tex2)
+            rec["inv_scale"] = t.invScale
+        elif isinstance(t, ImageTexture):
+            rec["kind"] = N.PT_TEX_IMAGE
+            h, w, c = t.data.shape
+            off = self.texel_bytes
+            data = np.ascontiguousarray(t.data.reshape(-1))
+            self.texel_chunks.append(data)
+            self.texel_bytes += data.size
+            pad = (-self.texel_bytes) % 16
+            if pad:
+                self.texel_chunks.append(np.zeros(pad, dtype=np.uint8))
+                self.texel_bytes += pad
+            rec["image"] = len(self.images)
+            self.images.append((off, w, h, c, 0))
+        else:
+            raise TypeError(f"unsupported texture {type(t).__name__}")
+        self.tex_ids[id(t)] = len(self.textures)
+        self.textures.append(rec)
+        return self.tex_ids[id(t)]
+
+    def material(self, m: Optional[Material]) -> int:
+        if m is None:
+            return -1
+        if id(m) in self.mat_ids:
+            return self.mat_ids[id(m)]
+        rec = np.zeros(1, dtype=N.MATERIAL)[0]
+        rec["kind"] = m.kind
+        for k in ("tex", "norm", "rough", "metal", "alpha"):
+            rec[k] = -1
+        if isinstance(m, (MicrofacetDiffuse, MicrofacetDielectric)):
+            rec["tex"] = self.texture(m.tex)
+            rec["norm"] = self.texture(m.norm)
+            rec["rough"] = self.texture(m.roughnessTexture)
+            if isinstance(m, MicrofacetDiffuse):
+                rec["metal"] = self.texture(m.metallicTexture)
+            else:
+                rec["ri"] = m.ri
+            rec["alpha"] = self.texture(m.alpha)
+            rec["alpha_mode"] = m.alphaTester.mode
+            rec["alpha_cutoff"] = m.alphaTester.cutoff
+        elif isinstance(m, ThinDielectric):
+            rec["ri"] = m.ri
+            rec["tex"] = self.texture(m.tex)
+        elif isinstance(m, SpecularConductor):
+            rec["albedo"] = m.albedo
+        else:
+            raise TypeError(f"unsupported material {type(m).__name__}")
+        self.mat_ids[id(m)] = len(self.materials)
+        self.materials.append(rec)
+        return self.mat_ids[id(m)]
+
+
+def _stack(recs, dtype):
+    if not recs:
+        return np.zeros(0, dtype=dtype)
+    a = np.zeros(len(recs), dtype=dtype)
+    for i, r in enumerate(recs):
+        a[i] = r
+    return a
+
+
+def flatten_scene(scene: Scene) -> FlatScene:
+    reg = _Registry()
+    top = scene.primitives
+    if not top:
+        raise ValueError("empty scene")
+
+    # ---- models: BLAS over their triangles ----
+    models = [p for p in top if isinstance(p, Model)]
+    pos, nrm, uvs, tan, vidx, tflags = [], [], [], [], [], []
+    vbase = 0
+    tri_base = 0
+    model_tri_base = []
+    model_tri_mat = []       # per model: material id per local triangle
+    model_tri_med = []
+    model_blas = []          # (clusters, root, order, bbox)
+    for m in models:
+        model_tri_base.append(tri_base)
+        boxes = []
+        mats, meds = [], []
+        for mesh in m.meshes:
+            nv = mesh.vertices.shape[0]
+            pos.append(mesh.vertices)
+            nrm.append(mesh.normals)
+            uvs.append(mesh.texCoords)
+            tan.append(mesh.tangents if mesh.tangents is not None else np.zeros((nv, 3), np.float32))
+            vidx.append(mesh.indices.reshape(-1, 3).astype(np.uint32) + np.uint32(vbase))
+            nt = mesh.GetTriangleCount()
+            tflags.append(np.full(nt, 1 if mesh.tangents is not None else 0, dtype=np.uint32))
+            boxes.append(mesh.tri_bboxes())
+            mat = m.override_material if m.override_material is not None else mesh.material
+            mats.append(np.full(nt, reg.material(mat), dtype=np.int32))
+            med = m.override_medium if m.override_medium is not None else mesh.medium
+            meds.append(np.full(nt, -1 if med is None else 0, dtype=np.int32))
+            vbase += nv
+            tri_base += nt
+        bx = np.concatenate(boxes) if boxes else np.zeros((0, 6), np.float32)
+        model_blas.append(N.bvh4_build(bx))
+        model_tri_mat.append(np.concatenate(mats) if mats else np.zeros(0, np.int32))
+        model_tri_med.append(np.concatenate(meds) if meds else np.zeros(0, np.int32))
+
+    # ---- TLAS over top-level primitives ----
+    quads, spheres = [], []
+    top_boxes = np.zeros((len(top), 6), dtype=np.float32)
+    mi = 0
+    model_of_top = {}
+    for i, p in enumerate(top):
+        if isinstance(p, Model):
+            top_boxes[i] = model_blas[mi][3]
+            model_of_top[i] = mi
+            mi += 1
+        elif isinstance(p, GeometricPrimitive):
+            top_boxes[i] = p.shape.bbox()
+        else:
+            raise TypeError(f"unsupported primitive {type(p).__name__}")
+    tl_clusters, tl_root, tl_order, tl_bbox = N.bvh4_build(top_boxes)
+
+    n_top = len(top)
+    n_blas_prims = sum(int(b[2].shape[0]) for b in model_blas)
+    prims = np.zeros(n_top + n_blas_prims, dtype=N.PRIM)
+    prims["light"] = -1
+    prims["medium"] = -1
+    light_slot: Dict[int, int] = {}
+    tlas_lights = []
+    # BLAS slot ranges
+    blas_base = []
+    base = n_top
+    for b in model_blas:
+        blas_base.append(base)
+        base += int(b[2].shape[0])
+    # TLAS slots
+    for slot in range(n_top):
+        p = top[int(tl_order[slot])]
+        rec = prims[slot]
+        if isinstance(p, Model):
+            k = model_of_top[int(tl_order[slot])]
+            rec["kind"] = N.PT_PRIM_BLAS
+            rec["index"] = 1 + k
+            rec["material"] = -1
+            # lights of this model in BLAS leaf order
+            order = model_blas[k][2]
+            for j, t in enumerate(order):
+                al = p.tri_lights[int(t)]
+                if al is not None:
+                    light_slot[id(al)] = blas_base[k] + j
+                    tlas_lights.append(al)
+        else:
+            sh = p.shape
+            if isinstance(sh, QuadShape):
+                rec["kind"] = N.PT_PRIM_QUAD
+                rec["index"] = len(quads)
+                q = np.zeros(1, dtype=N.QUAD)[0]
+                q["Q"], q["u"], q["v"], q["normal"], q["D"], q["w"] = sh.Q, sh.u, sh.v, sh.normal, sh.D, sh.w
+                quads.append(q)
+            elif isinstance(sh, SphereShape):
+                rec["kind"] = N.PT_PRIM_SPHERE
+                rec["index"] = len(spheres)
+                s = np.zeros(1, dtype=N.SPHERE)[0]
+                s["center"], s["radius"] = sh.center, sh.radius
+                spheres.append(s)
+            else:
+                raise TypeError(f"unsupported shape {type(sh).__name__}")
+            rec["material"] = reg.material(p.material)
+            rec["medium"] = -1 if p.medium is None else 0
+            if p.areaLight is not None:
+                light_slot[id(p.areaLight)] = slot
+                tlas_lights.append(p.areaLight)
+    # BLAS slots
+    for k, b in enumerate(model_blas):
+        order = b[2]
+        s0 = blas_base[k]
+        n = order.shape[0]
+        prims["kind"][s0:s0 + n] = N.PT_PRIM_TRIANGLE
+        prims["index"][s0:s0 + n] = order + np.uint32(model_tri_base[k])
+        prims["material"][s0:s0 + n] = model_tri_mat[k][order]
+        prims["medium"][s0:s0 + n] = model_tri_med[k][order]
+    for al in tlas_lights:
+        pass
+    # emissive triangle lights: fill prim light ids later in bind_lights
+
+    clusters = [tl_clusters] + [b[0] for b in model_blas]
+    roots = [tl_root] + [b[1] for b in model_blas]
+    pbase = [0] + blas_base
+    npr = [n_top] + [int(b[2].shape[0]) for b in model_blas]
+
+    cat = lambda xs, shape, dt: (np.ascontiguousarray(np.concatenate(xs), dtype=dt) if xs
+                                 else np.zeros(shape, dtype=dt))
+    flat = FlatScene(
+        positions=cat(pos, (0, 3), np.float32), normals=cat(nrm, (0, 3), np.float32),
+        uvs=cat(uvs, (0, 2), np.float32), tangents=cat(tan, (0, 3), np.float32),
+        tri_vidx=cat(vidx, (0, 3), np.uint32), tri_flags=cat(tflags, (0,), np.uint32),
+        quads=_stack(quads, N.QUAD), spheres=_stack(spheres, N.SPHERE), prims=prims,
+        bvh_clusters=clusters, bvh_roots=roots, bvh_prim_base=pbase, bvh_n_prims=npr,
+        materials=_stack(reg.materials, N.MATERIAL), textures=_stack(reg.textures, N.TEXTURE),
+        images=np.array(reg.images, dtype=N.IMAGE) if reg.images else np.zeros(0, dtype=N.IMAGE),
+        texels=(np.ascontiguousarray(np.concatenate(reg.texel_chunks)) if reg.texel_chunks
+                else np.zeros(0, dtype=np.uint8)),
+        bbox=tl_bbox, tlas_lights=tlas_lights, light_slot=light_slot, material_ids=dict(reg.mat_ids),
+        top_order=tl_order, blas_orders=[b[2] for b in model_blas], model_tri_base=model_tri_base,
+        texture_ids=dict(reg.tex_ids))
+    flat._reg = reg
+    return flat
+
+
+def bind_lights(flat: FlatScene, scene: Scene, sampler: Optional[LightSampler]):
+    """Light table = Scene::GetLights() + lights added only to the sampler;
+    power/pmf as the sampler's PreProcess left them (LightSampler.cpp)."""
+    reg = flat._reg
+    lights = list(flat.tlas_lights) + list(scene.infiniteLights)
+    if sampler is not None:
+        seen = {id(l) for l in lights}
+        for l in sampler.all_lights:
+            if id(l) not in seen:
+                lights.append(l)
+                seen.add(id(l))
+    idx = {id(l): i for i, l in enumerate(lights)}
+    table = np.zeros(len(lights), dtype=N.LIGHT)
+    table["prim"] = -1
+    table["tex"] = -1
+    for i, l in enumerate(lights):
+        r = table[i]
+        r["power"] = l.Power()
+        r["pmf"] = sampler.PMF(l) if sampler is not None else 0.0
+        if isinstance(l, AreaLight):
+            r["kind"] = N.PT_LIGHT_AREA
+            r["prim"] = flat.light_slot[id(l)]
+            r["tex"] = reg.texture(l.emissiveTexture)
+            r["one_sided"] = 1 if l.oneSided else 0
+        elif isinstance(l, UniformInfiniteLight):
+            r["kind"] = N.PT_LIGHT_UNIFORM_INF
+            r["color"] = l.color
+        elif isinstance(l, FunctionInfiniteLight):
+            r["kind"] = N.PT_LIGHT_SKY_INF
+            r["color"] = l.c0
+            r["vec"] = l.c1
+            r["scale"] = l.scale
+        elif isinstance(l, DistantLight):
+            r["kind"] = N.PT_LIGHT_DISTANT
+            r["color"] = l.color
+            r["vec"] = l.dir
+        elif isinstance(l, PointLight):
+            r["kind"] = N.PT_LIGHT_POINT
+            r["color"] = l.color
+            r["vec"] = l.p
+        else:
+            raise TypeError(f"unsupported light {type(l).__name__}")
+    # prim -> area light id
+    flat.prims["light"] = -1
+    for i, l in enumerate(lights):
+        if isinstance(l, AreaLight):
+            flat.prims["light"][flat.light_slot[id(l)]] = i
+    # textures may have grown (emissive textures)
+    flat.textures = _stack(reg.textures, N.TEXTURE)
+    flat.images = np.array(reg.images, dtype=N.IMAGE) if reg.images else np.zeros(0, dtype=N.IMAGE)
+    flat.texels = (np.ascontiguousarray(np.concatenate(reg.texel_chunks)) if reg.texel_chunks
+                   else np.zeros(0, dtype=np.uint8))
+    flat.lights = table
+    flat.light_objects = lights
+    flat.light_sampler = sampler.kind if sampler is not None else N.PT_LS_UNIFORM
+    flat.sampler_lights = np.array([idx[id(l)] for l in (sampler.lights if sampler is not None else [])],
+                                   dtype=np.uint32)
+    flat.infinite_lights = np.array([idx[id(l)] for l in scene.infiniteLights], dtype=np.uint32)
+    return flat
+
+
+def camera_desc(cam) -> N.CameraDesc:
+    d = N.CameraDesc()
+    d.origin[:] = [float(x) for x in cam.lookFrom]
+    d.u[:] = [float(x) for x in cam.u]
+    d.v[:] = [float(x) for x in cam.v]
+    d.w[:] = [float(x) for x in cam.w]
+    d.half_width = float(cam.halfWidth)
+    d.half_height = float(cam.halfHeight)
+    d.defocus_radius = float(cam.defocusRadius)
+    d.focus_distance = float(cam.FocusDistance)
+    d.focus_angle = float(cam.FocusAngle)
+    W, H = cam.film.Resolution()
+    d.width = W
+    d.height = H
+    return d

@@ -1,0 +1,195 @@
+"""Integrators backed by the HIP wavefront tracer (libpt_hip.so).
+
+Mirrors the reference's `Integrator` interface (Integrators.hpp:10-67):
+PathIntegrator(scene, camera, sampler, lightSampler, maxDepth) and
+SimplePathIntegrator(scene, camera, sampler, maxDepth); Render() fills the
+camera's Film (sum RGB*w, sum w per pixel, Film.hpp:227-253).
+
+The sample stream is the deterministic counter-based PCG stream of DESIGN.md
+(`PCGSampler`); the reference's `UniformSampler` / `StratifiedSampler` names are
+accepted for their samples-per-pixel count (their RNG is unseeded, so no frame
+of theirs is reproducible anyway: SURVEY.md §0.4).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import native as N
+from .flatten import bind_lights, camera_desc
+from .scene import BoxFilter, Camera, GaussianFilter, LightSampler, MitchellFilter, Scene
+
+
+class Sampler:
+    def __init__(self, samples: int, seed: int = 0x5EED0001):
+        self.samples = int(samples)
+        self.seed = int(seed) & 0xFFFFFFFF
+
+    def SamplesPerPixel(self) -> int:
+        return self.samples
+
+
+class PCGSampler(Sampler):
+    pass
+
+
+class UniformSampler(Sampler):
+    pass
+
+
+class StratifiedSampler(Sampler):
+    def __init__(self, xSamples: int, ySamples: int, seed: int = 0x5EED0001):
+        super().__init__(int(xSamples) * int(ySamples), seed)
+
+
+class Context:
+    """One libpt context (one GPU).  Fails loudly if HIP or the library is missing."""
+
+    def __init__(self, device: int = 0):
+        self._lib = N.lib()
+        self.ptr = C.c_void_p()
+        N.check(self._lib.pt_create(C.byref(self.ptr), int(device)))
+        self.device = device
+        self.scene_key = None
+
+    def close(self):
+        if self.ptr:
+            self._lib.pt_destroy(self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, flat, key=None):
+        d = flat.desc()
+        N.check(self._lib.pt_scene_upload(self.ptr, C.byref(d)), self.ptr)
+        self.scene_key = key
+
+    def set_stream(self, stream_ptr: int | None):
+        N.check(self._lib.pt_set_stream(self.ptr, C.c_void_p(stream_ptr) if stream_ptr else None), self.ptr)
+
+    def render(self, cam: N.CameraDesc, rd: N.RenderDesc, film_ptr: int) -> dict:
+        st = N.Stats()
+        N.check(self._lib.pt_render(self.ptr, C.byref(cam), C.byref(rd), C.c_void_p(film_ptr), C.byref(st)), self.ptr)
+        return st.as_dict()
+
+    def render_samples(self, cam: N.CameraDesc, rd: N.RenderDesc, npix: int) -> tuple[np.ndarray, dict]:
+        out = np.zeros((npix, rd.spp, 3), dtype=np.float32)
+        st = N.Stats()
+        L = self._lib
+        L.pt_render_samples.argtypes = [C.c_void_p, C.POINTER(N.CameraDesc), C.POINTER(N.RenderDesc), C.c_void_p,
+                                        C.POINTER(N.Stats)]
+        L.pt_render_samples.restype = C.c_int32
+        N.check(L.pt_render_samples(self.ptr, C.byref(cam), C.byref(rd), out.ctypes.data, C.byref(st)), self.ptr)
+        return out, st.as_dict()
+
+    def trace(self, rays: np.ndarray, any_hit: bool) -> tuple[np.ndarray, dict]:
+        rays = np.ascontiguousarray(rays, dtype=N.RAY)
+        hits = np.zeros(rays.shape[0], dtype=N.HIT)
+        st = N.Stats()
+        N.check(self._lib.pt_trace(self.ptr, rays.ctypes.data, rays.shape[0], 1 if any_hit else 0, hits.ctypes.data,
+                                   C.byref(st)), self.ptr)
+        return hits, st.as_dict()
+
+
+_contexts: dict[int, Context] = {}
+
+
+def get_context(device: int = 0) -> Context:
+    if device not in _contexts:
+        _contexts[device] = Context(device)
+    return _contexts[device]
+
+
+def render_desc(integrator: int, spp: int, max_depth: int, seed: int, film_filter, shard_index: int = 0,
+                shard_count: int = 1, flags: int = 0, paths_in_flight: int = 0, pixel_begin: int = 0,
+                pixel_end: int = 0) -> N.RenderDesc:
+    rd = N.RenderDesc()
+    rd.integrator = integrator
+    rd.spp = int(spp)
+    rd.max_depth = int(max_depth)
+    rd.seed = int(seed) & 0xFFFFFFFF
+    rd.filter = film_filter.kind
+    rd.filter_radius[0] = float(film_filter.radius[0])
+    rd.filter_radius[1] = float(film_filter.radius[1])
+    p = film_filter.params()
+    rd.filter_params[0] = float(p[0])
+    rd.filter_params[1] = float(p[1])
+    rd.shard_index = int(shard_index)
+    rd.shard_count = int(shard_count)
+    rd.flags = int(flags)
+    rd.paths_in_flight = int(paths_in_flight)
+    rd.pixel_begin = int(pixel_begin)
+    rd.pixel_end = int(pixel_end)
+    return rd
+
+
+class Integrator:
+    kind = N.PT_INTEGRATOR_PATH
+
+    def __init__(self, scene: Scene, camera: Camera, sampler: Sampler, lightSampler: Optional[LightSampler],
+                 maxDepth: int):
+        self.scene = scene
+        self.camera = camera
+        self.sampler = sampler
+        self.lightSampler = lightSampler
+        self.maxDepth = int(maxDepth)
+        if scene.flat is None:
+            scene.BuildTlas()
+        self.flat = bind_lights(scene.flat, scene, lightSampler)
+        self.last_stats: dict = {}
+
+    def context(self, device: int = 0) -> Context:
+        ctx = get_context(device)
+        key = (id(self.flat), id(self.lightSampler))
+        if ctx.scene_key != key:
+            ctx.upload(self.flat, key)
+        return ctx
+
+    def desc(self, **kw) -> tuple[N.CameraDesc, N.RenderDesc]:
+        film = self.camera.GetFilm()
+        rd = render_desc(self.kind, kw.pop("spp", self.sampler.SamplesPerPixel()), self.maxDepth,
+                         kw.pop("seed", self.sampler.seed), film.filter, **kw)
+        return camera_desc(self.camera), rd
+
+    def Render(self, device: int = 0, shard_index: int = 0, shard_count: int = 1, flags: int = 0,
+               film_ptr: int | None = None, paths_in_flight: int = 0) -> dict:
+        """TileIntegrator::Render equivalent: accumulates into camera.GetFilm().accum
+        (or into the float64 device buffer at film_ptr)."""
+        ctx = self.context(device)
+        cam, rd = self.desc(shard_index=shard_index, shard_count=shard_count, flags=flags,
+                            paths_in_flight=paths_in_flight)
+        film = self.camera.GetFilm()
+        ptr = film_ptr if film_ptr is not None else film.accum.ctypes.data
+        self.last_stats = ctx.render(cam, rd, ptr)
+        return self.last_stats
+
+    def RenderSamples(self, pixel_begin: int = 0, pixel_end: int = 0, spp: Optional[int] = None,
+                      device: int = 0) -> np.ndarray:
+        """Per-sample Li for pixels [pixel_begin, pixel_end): (npix, spp, 3) float32."""
+        ctx = self.context(device)
+        W, H = self.camera.GetFilm().Resolution()
+        if pixel_begin == 0 and pixel_end == 0:
+            pixel_end = W * H
+        kw = {} if spp is None else {"spp": spp}
+        cam, rd = self.desc(pixel_begin=pixel_begin, pixel_end=pixel_end, **kw)
+        out, self.last_stats = ctx.render_samples(cam, rd, pixel_end - pixel_begin)
+        return out
+
+
+class PathIntegrator(Integrator):
+    """PathIntegrator (Integrators.hpp:43-54): NEE + MIS (power heuristic) + RR."""
+    kind = N.PT_INTEGRATOR_PATH
+
+
+class SimplePathIntegrator(Integrator):
+    """SimplePathIntegrator (Integrators.hpp:33-41): BSDF sampling + RR."""
+    kind = N.PT_INTEGRATOR_SIMPLE
+
+    def __init__(self, scene: Scene, camera: Camera, sampler: Sampler, maxDepth: int):
+        super().__init__(scene, camera, sampler, None, maxDepth)

@@ -1,0 +1,187 @@
+"""ctypes binding of libpt_hip.so (include/pt_api.h).
+
+The library is built in-tree by __graft_entry__.build() (hipcc, gfx950) into
+pathtracing_amd/_lib/libpt_hip.so.  There is no fallback: if it cannot be
+loaded, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+LIB_DIR = Path(__file__).resolve().parent / "_lib"
+LIB_PATH = LIB_DIR / "libpt_hip.so"
+
+PT_OK = 0
+PT_PRIM_TRIANGLE, PT_PRIM_QUAD, PT_PRIM_SPHERE, PT_PRIM_BLAS = 0, 1, 2, 3
+PT_TEX_SOLID, PT_TEX_IMAGE, PT_TEX_CHECKER = 0, 1, 2
+PT_MAT_DIFFUSE, PT_MAT_DIELECTRIC, PT_MAT_THIN, PT_MAT_CONDUCTOR = 0, 1, 2, 3
+PT_LIGHT_AREA, PT_LIGHT_UNIFORM_INF, PT_LIGHT_SKY_INF, PT_LIGHT_DISTANT, PT_LIGHT_POINT = 0, 1, 2, 3, 4
+PT_LS_UNIFORM, PT_LS_POWER = 0, 1
+PT_INTEGRATOR_PATH, PT_INTEGRATOR_SIMPLE = 0, 1
+PT_FILTER_MITCHELL, PT_FILTER_BOX, PT_FILTER_GAUSSIAN = 0, 1, 2
+PT_RENDER_COUNT_NODES = 0x1
+PT_RENDER_TIMING = 0x2
+
+# ---- numpy mirrors of the array element structs (layouts asserted below) ----
+REF_NODE = np.dtype([("count", "u1"), ("active", "u1"), ("perm", "u1"), ("pad", "u1"), ("cluster_idx", "<u4")])
+REF_CLUSTER = np.dtype([("xmin", "<f4", 4), ("xmax", "<f4", 4), ("ymin", "<f4", 4), ("ymax", "<f4", 4),
+                        ("zmin", "<f4", 4), ("zmax", "<f4", 4), ("children", REF_NODE, 4)])
+PRIM = np.dtype([("kind", "<u4"), ("index", "<u4"), ("material", "<i4"), ("light", "<i4"), ("medium", "<i4")])
+QUAD = np.dtype([("Q", "<f4", 3), ("u", "<f4", 3), ("v", "<f4", 3), ("normal", "<f4", 3), ("D", "<f4"),
+                 ("w", "<f4", 3)])
+SPHERE = np.dtype([("center", "<f4", 3), ("radius", "<f4")])
+TEXTURE = np.dtype([("kind", "<u4"), ("scale", "<f4", 3), ("value", "<f4", 3), ("a", "<i4"), ("b", "<i4"),
+                    ("inv_scale", "<f4", 2), ("image", "<i4")])
+IMAGE = np.dtype([("offset", "<u8"), ("width", "<i4"), ("height", "<i4"), ("channels", "<i4"), ("pad", "<i4")])
+MATERIAL = np.dtype([("kind", "<u4"), ("tex", "<i4"), ("norm", "<i4"), ("rough", "<i4"), ("metal", "<i4"),
+                     ("alpha", "<i4"), ("alpha_mode", "<u4"), ("alpha_cutoff", "<f4"), ("ri", "<f4"),
+                     ("albedo", "<f4", 3)])
+LIGHT = np.dtype([("kind", "<u4"), ("prim", "<i4"), ("tex", "<i4"), ("one_sided", "<u4"), ("power", "<f4"),
+                  ("pmf", "<f4"), ("color", "<f4", 3), ("vec", "<f4", 3), ("scale", "<f4")])
+RAY = np.dtype([("o", "<f4", 3), ("d", "<f4", 3), ("tmax", "<f4")])
+HIT = np.dtype([("t", "<f4"), ("b1", "<f4"), ("b2", "<f4"), ("prim", "<i4")])
+
+assert REF_NODE.itemsize == 8 and REF_CLUSTER.itemsize == 128 and PRIM.itemsize == 20
+assert QUAD.itemsize == 64 and SPHERE.itemsize == 16 and TEXTURE.itemsize == 48 and IMAGE.itemsize == 24
+assert MATERIAL.itemsize == 48 and LIGHT.itemsize == 52 and RAY.itemsize == 28 and HIT.itemsize == 16
+
+
+class RefNode(C.Structure):
+    _fields_ = [("count", C.c_uint8), ("active", C.c_uint8), ("perm", C.c_uint8), ("pad", C.c_uint8),
+                ("cluster_idx", C.c_uint32)]
+
+
+class BvhDesc(C.Structure):
+    _fields_ = [("clusters", C.c_void_p), ("n_clusters", C.c_uint32), ("root", RefNode),
+                ("prim_base", C.c_uint32), ("n_prims", C.c_uint32)]
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [
+        ("positions", C.c_void_p), ("normals", C.c_void_p), ("uvs", C.c_void_p), ("tangents", C.c_void_p),
+        ("n_vertices", C.c_uint32),
+        ("tri_vidx", C.c_void_p), ("tri_flags", C.c_void_p), ("n_triangles", C.c_uint32),
+        ("quads", C.c_void_p), ("n_quads", C.c_uint32),
+        ("spheres", C.c_void_p), ("n_spheres", C.c_uint32),
+        ("prims", C.c_void_p), ("n_prims", C.c_uint32),
+        ("bvhs", C.c_void_p), ("n_bvhs", C.c_uint32),
+        ("materials", C.c_void_p), ("n_materials", C.c_uint32),
+        ("textures", C.c_void_p), ("n_textures", C.c_uint32),
+        ("images", C.c_void_p), ("n_images", C.c_uint32),
+        ("texels", C.c_void_p), ("n_texel_bytes", C.c_uint64),
+        ("lights", C.c_void_p), ("n_lights", C.c_uint32),
+        ("light_sampler", C.c_uint32),
+        ("sampler_lights", C.c_void_p), ("n_sampler_lights", C.c_uint32),
+        ("infinite_lights", C.c_void_p), ("n_infinite_lights", C.c_uint32),
+    ]
+
+
+class CameraDesc(C.Structure):
+    _fields_ = [("origin", C.c_float * 3), ("u", C.c_float * 3), ("v", C.c_float * 3), ("w", C.c_float * 3),
+                ("half_width", C.c_float), ("half_height", C.c_float), ("defocus_radius", C.c_float),
+                ("focus_distance", C.c_float), ("focus_angle", C.c_float), ("width", C.c_int32),
+                ("height", C.c_int32)]
+
+
+class RenderDesc(C.Structure):
+    _fields_ = [("integrator", C.c_uint32), ("spp", C.c_uint32), ("max_depth", C.c_uint32), ("seed", C.c_uint32),
+                ("filter", C.c_uint32), ("filter_radius", C.c_float * 2), ("filter_params", C.c_double * 2),
+                ("shard_index", C.c_uint32), ("shard_count", C.c_uint32), ("flags", C.c_uint32),
+                ("paths_in_flight", C.c_uint32), ("pixel_begin", C.c_uint32), ("pixel_end", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("paths", C.c_uint64), ("rays_closest", C.c_uint64), ("rays_any", C.c_uint64),
+                ("nodes_closest", C.c_uint64), ("tris_closest", C.c_uint64), ("nodes_any", C.c_uint64),
+                ("tris_any", C.c_uint64), ("shade_hits", C.c_uint64), ("ms_total", C.c_double),
+                ("ms_closest", C.c_double), ("ms_any", C.c_double), ("ms_shade", C.c_double),
+                ("launches_closest", C.c_uint64), ("launches_any", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+EXPORTS = [
+    "pt_version", "pt_create", "pt_destroy", "pt_last_error", "pt_set_stream", "pt_scene_upload", "pt_render",
+    "pt_trace", "pt_scene_device_bytes", "pt_bvh4_build", "pt_bvh4_order_table",
+]
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libpt_hip.so (fails loudly: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise NativeError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(str(LIB_PATH))
+    vp = C.c_void_p
+    L.pt_version.restype = C.c_int
+    L.pt_create.argtypes = [C.POINTER(vp), C.c_int]
+    L.pt_create.restype = C.c_int32
+    L.pt_destroy.argtypes = [vp]
+    L.pt_destroy.restype = None
+    L.pt_last_error.argtypes = [vp]
+    L.pt_last_error.restype = C.c_char_p
+    L.pt_set_stream.argtypes = [vp, vp]
+    L.pt_set_stream.restype = C.c_int32
+    L.pt_scene_upload.argtypes = [vp, C.POINTER(SceneDesc)]
+    L.pt_scene_upload.restype = C.c_int32
+    L.pt_render.argtypes = [vp, C.POINTER(CameraDesc), C.POINTER(RenderDesc), vp, C.POINTER(Stats)]
+    L.pt_render.restype = C.c_int32
+    L.pt_trace.argtypes = [vp, vp, C.c_uint32, C.c_int, vp, C.POINTER(Stats)]
+    L.pt_trace.restype = C.c_int32
+    L.pt_scene_device_bytes.argtypes = [vp]
+    L.pt_scene_device_bytes.restype = C.c_uint64
+    L.pt_bvh4_build.argtypes = [vp, C.c_uint32, vp, C.POINTER(C.c_uint32), C.POINTER(RefNode), vp, vp]
+    L.pt_bvh4_build.restype = C.c_int32
+    L.pt_bvh4_order_table.argtypes = [vp]
+    L.pt_bvh4_order_table.restype = C.c_int32
+    _lib = L
+    return L
+
+
+def check(status: int, ctx=None):
+    if status != PT_OK:
+        msg = lib().pt_last_error(ctx)
+        raise NativeError(f"pt status {status}: {msg.decode() if msg else ''}")
+
+
+def ptr(a: np.ndarray | None):
+    if a is None or a.size == 0:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data
+
+
+def bvh4_build(boxes: np.ndarray):
+    """Reference BVH4 build (BVH.hpp:95-105, 290-390, 743-1017) over n boxes
+    {min.xyz, max.xyz} -> (clusters, root, prim_order, bbox)."""
+    boxes = np.ascontiguousarray(boxes, dtype=np.float32).reshape(-1, 6)
+    n = boxes.shape[0]
+    clusters = np.zeros(max(n, 1), dtype=REF_CLUSTER)
+    order = np.zeros(max(n, 1), dtype=np.uint32)
+    nc = C.c_uint32(0)
+    root = RefNode()
+    bbox = np.zeros(6, dtype=np.float32)
+    check(lib().pt_bvh4_build(ptr(boxes), n, clusters.ctypes.data, C.byref(nc), C.byref(root), order.ctypes.data,
+                              bbox.ctypes.data))
+    r = np.zeros(1, dtype=REF_NODE)
+    r[0] = (root.count, root.active, root.perm, root.pad, root.cluster_idx)
+    return clusters[: nc.value].copy(), r[0], order[:n].copy(), bbox
+
+
+def order_table() -> np.ndarray:
+    out = np.zeros(8 * 135, dtype=np.uint8)
+    check(lib().pt_bvh4_order_table(out.ctypes.data))
+    return out.reshape(8, 135)

@@ -1,0 +1,697 @@
+"""Host-side scene API mirroring the reference's classes (marko176/PathTracing).
+
+Names, constructor arguments and defaults follow the reference so scene recipes
+read like its main.cpp / examples/example_1.cpp:
+
+  Textures   SolidColor, ImageTexture, CheckerTexture          (Texture.hpp:122-213)
+  Materials  MicrofacetDiffuse, MicrofacetDielectric,
+             ThinDielectric, SpecularConductor, AlphaTester     (Material.hpp:176-673)
+  Shapes     QuadShape, SphereShape, Mesh (triangles)           (Shape.hpp, Mesh.hpp)
+  Prims      GeometricPrimitive, Model (a BLAS4 over meshes)    (Primitive.hpp:17-31, Model.hpp)
+  Lights     AreaLight, UniformInfiniteLight, FunctionInfiniteLight (sky gradient),
+             DistantLight, PointLight                           (Light.hpp/.cpp)
+  Samplers   UniformLightSampler, PowerLightSampler             (LightSampler.hpp)
+  Scene      Add / BuildTlas / GetLights / BoundingBox / infiniteLights (Scene.hpp)
+  Sensor     Film, MitchellFilter, BoxFilter, GaussianFilter, Camera  (Film.hpp, Filter.hpp, Camera.hpp)
+
+Geometry is held as float32 numpy arrays; every derived quantity the reference
+computes in a constructor (quad normal/D/w, camera basis, light power) is
+computed in float32 in the same operand order.  Rendering goes through the
+native HIP library (pathtracing_amd.integrator); nothing here touches a GPU.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+
+f32 = np.float32
+
+
+def _v3(x) -> np.ndarray:
+    a = np.asarray(x, dtype=np.float32).reshape(-1)
+    if a.size == 1:
+        a = np.repeat(a, 3)
+    if a.size != 3:
+        raise ValueError(f"expected a 3-vector, got {x!r}")
+    return a.astype(np.float32)
+
+
+def _normalize(v: np.ndarray) -> np.ndarray:
+    """glm::normalize = v * (1 / sqrt(dot(v, v))) (glm/detail/func_geometric.inl:88)."""
+    v = v.astype(np.float32)
+    d = _dot(v, v)
+    return (v * (f32(1.0) / f32(np.sqrt(d)))).astype(np.float32)
+
+
+def _cross(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    a = a.astype(np.float32)
+    b = b.astype(np.float32)
+    return np.array([a[1] * b[2] - b[1] * a[2],
+                     a[2] * b[0] - b[2] * a[0],
+                     a[0] * b[1] - b[0] * a[1]], dtype=np.float32)
+
+
+def _dot(a, b) -> np.float32:
+    a = np.asarray(a, dtype=np.float32)
+    b = np.asarray(b, dtype=np.float32)
+    return f32(f32(a[0] * b[0]) + f32(a[1] * b[1])) + f32(a[2] * b[2])
+
+
+def _expand_seq(points) -> np.ndarray:
+    """AABB().Expand(p0).Expand(p1)... with glm::min/max's operand order
+    (AABB.hpp:62-70): keeps the earlier value on ties, so signed zeros match."""
+    pts = [np.asarray(p, dtype=np.float32) for p in points]
+    mn = np.full(pts[0].shape, np.inf, np.float32)
+    mx = np.full(pts[0].shape, -np.inf, np.float32)
+    for p in pts:
+        mn = np.where(p < mn, p, mn)
+        mx = np.where(mx < p, p, mx)
+    return np.concatenate([mn, mx], axis=-1).astype(np.float32)
+
+
+def luminance(c) -> float:
+    """Util.hpp:3-5 (double)."""
+    c = np.asarray(c, dtype=np.float64)
+    return float(c[0] * 0.2126 + c[1] * 0.7152 + c[2] * 0.0722)
+
+
+# --------------------------------------------------------------------------
+# Textures (Texture.hpp:108-213)
+# --------------------------------------------------------------------------
+class Texture:
+    def __init__(self, colorScale=(1, 1, 1)):
+        self.colorScale = _v3(colorScale)
+
+    def Channels(self) -> int:
+        return 3
+
+
+class SolidColor(Texture):
+    def __init__(self, color, colorScale=(1, 1, 1)):
+        super().__init__(colorScale)
+        self.albedo = _v3(color)
+
+
+class ImageTexture(Texture):
+    """u8 image, bilinear, repeat wrap.  `data` is HxWxC uint8 already
+    linearised if the reference would have loaded it with gammaCorrection
+    (Texture.cpp:4-19 re-quantises through sRGBLUT)."""
+
+    def __init__(self, data: np.ndarray, gammaCorrection: bool = False, colorScale=(1, 1, 1), path: str = ""):
+        super().__init__(colorScale)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        if data.ndim == 2:
+            data = data[:, :, None]
+        self.raw = data                      # as stored in a file (for recipes)
+        self.gammaCorrection = bool(gammaCorrection)
+        self.path = path
+        self.data = srgb_linearize_u8(data) if gammaCorrection else data
+
+    def Channels(self) -> int:
+        return int(self.data.shape[2])
+
+
+class CheckerTexture(Texture):
+    def __init__(self, textureA: Texture, textureB: Texture, uvscale, colorScale=(1, 1, 1)):
+        super().__init__(colorScale)
+        self.tex1 = textureA
+        self.tex2 = textureB
+        s = np.asarray(uvscale, dtype=np.float32).reshape(-1)
+        if s.size == 1:
+            s = np.repeat(s, 2)
+        self.uvscale = s.astype(np.float32)
+        self.invScale = (f32(1.0) / self.uvscale).astype(np.float32)
+
+    def Channels(self) -> int:
+        return self.tex1.Channels()
+
+
+def _srgb_lut() -> np.ndarray:
+    """sRGBLUT (Texture.hpp:26-34): lround(sRGB_to_linear(i/255) * 255), in double."""
+    out = np.zeros(256, dtype=np.uint8)
+    for i in range(256):
+        s = i / 255.0
+        lin = s / 12.92 if s <= 0.04045 else ((s + 0.055) / 1.055) ** 2.4
+        lin = min(max(lin, 0.0), 1.0)
+        out[i] = int(math.floor(lin * 255.0 + 0.5))
+    return out
+
+
+SRGB_LUT = _srgb_lut()
+
+
+def srgb_linearize_u8(data: np.ndarray) -> np.ndarray:
+    out = data.copy()
+    c = min(out.shape[2], 3)
+    out[:, :, :c] = SRGB_LUT[out[:, :, :c]]
+    return out
+
+
+# --------------------------------------------------------------------------
+# Materials (Material.hpp:147-673)
+# --------------------------------------------------------------------------
+class AlphaMode:
+    Opaque = 0
+    Blend = 1
+    Mask = 2
+
+
+@dataclass
+class AlphaTester:
+    mode: int = AlphaMode.Blend   # default Blend (Material.hpp:196)
+    cutoff: float = 0.5
+
+
+class Material:
+    kind = -1
+    alpha_tester: Optional[AlphaTester] = None  # None = never set (default Blend)
+
+
+class MicrofacetDiffuse(Material):
+    kind = 0
+
+    def __init__(self, tex, norm: Optional[Texture] = None, roughnessTexture: Optional[Texture] = None,
+                 metallicTexture: Optional[Texture] = None, alpha_mask: Optional[Texture] = None):
+        if not isinstance(tex, Texture):
+            tex = SolidColor(tex)
+        self.tex = tex
+        self.norm = norm
+        self.roughnessTexture = roughnessTexture if roughnessTexture is not None else SolidColor((1, 1, 1))
+        self.metallicTexture = metallicTexture if metallicTexture is not None else SolidColor((0, 0, 0))
+        self.alpha = alpha_mask
+        self.alphaTester = AlphaTester()
+        self.tester_set = False
+
+    def setAlphaTester(self, tester: AlphaTester):
+        """Material.hpp:350-353."""
+        self.alphaTester = AlphaTester(tester.mode, tester.cutoff)
+        self.tester_set = True
+        if self.alpha is None and self.tex.Channels() != 4:
+            self.alphaTester.mode = AlphaMode.Opaque
+
+
+class MicrofacetDielectric(Material):
+    kind = 1
+
+    def __init__(self, refIndex: float, *args):
+        """(ri, albedo) | (ri, roughness, albedo) | (ri, tex, norm, roughTex, alpha) (Material.hpp:366-368)."""
+        self.ri = float(refIndex)
+        self.norm = None
+        self.alpha = None
+        if len(args) == 1 and not isinstance(args[0], Texture):
+            self.tex = SolidColor(args[0])
+            self.roughnessTexture = SolidColor((0, 0, 0))
+        elif len(args) == 2 and not isinstance(args[1], (Texture, type(None))) and np.isscalar(args[0]):
+            self.tex = SolidColor(args[1])
+            self.roughnessTexture = SolidColor((float(args[0]),) * 3)
+        else:
+            self.tex = args[0]
+            self.norm = args[1] if len(args) > 1 else None
+            rt = args[2] if len(args) > 2 else None
+            self.roughnessTexture = rt if rt is not None else SolidColor((0, 0, 0))
+            self.alpha = args[3] if len(args) > 3 else None
+        self.alphaTester = AlphaTester()
+        self.tester_set = False
+
+    def setAlphaTester(self, tester: AlphaTester):
+        self.alphaTester = AlphaTester(tester.mode, tester.cutoff)
+        self.tester_set = True
+        if self.alpha is None and self.tex.Channels() != 4:
+            self.alphaTester.mode = AlphaMode.Opaque
+
+
+class ThinDielectric(Material):
+    kind = 2
+
+    def __init__(self, eta: float, tex: Optional[Texture] = None):
+        self.ri = float(eta)
+        self.tex = tex if tex is not None else SolidColor((1, 1, 1))
+
+
+class SpecularConductor(Material):
+    kind = 3
+
+    def __init__(self, albedo):
+        self.albedo = _v3(albedo)
+
+
+# --------------------------------------------------------------------------
+# Shapes (Shape.hpp)
+# --------------------------------------------------------------------------
+class Shape:
+    pass
+
+
+class QuadShape(Shape):
+    """Shape.hpp:118-171; ctor-derived normal, D, w in float32."""
+
+    def __init__(self, origin, u, v):
+        self.Q = _v3(origin)
+        self.u = _v3(u)
+        self.v = _v3(v)
+        n = _cross(self.u, self.v)
+        self.normal = _normalize(n)
+        self.D = _dot(self.normal, self.Q)
+        self.w = (n / _dot(n, n)).astype(np.float32)
+
+    def bbox(self) -> np.ndarray:
+        qu = (self.Q + self.u).astype(np.float32)
+        quv = (qu + self.v).astype(np.float32)
+        qv = (self.Q + self.v).astype(np.float32)
+        return _expand_seq([self.Q, quv, qu, qv])  # QuadShape ctor (Shape.hpp:120-129)
+
+    def Area(self) -> float:
+        c = _cross(self.u, self.v)
+        return float(f32(np.sqrt(_dot(c, c))))
+
+
+class SphereShape(Shape):
+    def __init__(self, sphereCenter, sphereRadius: float):
+        self.center = _v3(sphereCenter)
+        self.radius = f32(sphereRadius)
+
+    def bbox(self) -> np.ndarray:
+        r = np.full(3, self.radius, dtype=np.float32)
+        return _expand_seq([self.center - r, self.center + r])  # SphereShape ctor (Shape.hpp:22-26)
+
+    def Area(self) -> float:
+        return float(f32(f32(f32(4.0) * f32(math.pi)) * self.radius) * self.radius)
+
+
+class Mesh:
+    """Mesh.hpp:11-93: SoA triangle data + material / emissive texture / medium."""
+
+    def __init__(self, indices, vertices, tangents, normals, texCoords, mat: Optional[Material],
+                 emissiveTex: Optional[Texture] = None, meshMedium=None):
+        self.indices = np.ascontiguousarray(indices, dtype=np.uint32).reshape(-1)
+        self.vertices = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 3)
+        self.normals = np.ascontiguousarray(normals, dtype=np.float32).reshape(-1, 3)
+        self.texCoords = np.ascontiguousarray(texCoords, dtype=np.float32).reshape(-1, 2)
+        t = None if tangents is None or len(tangents) == 0 else np.ascontiguousarray(tangents, dtype=np.float32).reshape(-1, 3)
+        self.tangents = t
+        self.material = mat
+        self.emissiveTexture = emissiveTex
+        self.medium = meshMedium
+        if self.indices.size % 3:
+            raise ValueError("indices must be a multiple of 3")
+        nv = self.vertices.shape[0]
+        if self.normals.shape[0] != nv or self.texCoords.shape[0] != nv or (t is not None and t.shape[0] != nv):
+            raise ValueError("vertex attribute arrays must have equal length")
+        if self.indices.size and int(self.indices.max()) >= nv:
+            raise ValueError("index out of range")
+
+    def GetTriangleCount(self) -> int:
+        return self.indices.size // 3
+
+    def tri_bboxes(self) -> np.ndarray:
+        idx = self.indices.reshape(-1, 3)
+        p = self.vertices[idx]                  # (n,3,3)
+        # AABB(v0).Expand(v1).Expand(v2) (Shape.cpp:270-275)
+        return _expand_seq([p[:, 0], p[:, 1], p[:, 2]])
+
+
+# --------------------------------------------------------------------------
+# Media (only the boundary semantics matter on the hot path)
+# --------------------------------------------------------------------------
+class HomogeneusMedium:
+    def __init__(self, sigma_a, sigma_s, phaseFunction_g: float = 0.0, density: float = 1.0):
+        self.sigma_a = _v3(sigma_a)
+        self.sigma_s = _v3(sigma_s)
+        self.g = float(phaseFunction_g)
+        self.density = float(density)
+
+
+# --------------------------------------------------------------------------
+# Lights (Light.hpp / Light.cpp)
+# --------------------------------------------------------------------------
+class Light:
+    def isDelta(self) -> bool:
+        return False
+
+    def PreProcess(self, bbox):
+        pass
+
+    def Power(self) -> float:
+        return 0.0
+
+
+def _scene_radius(bbox) -> float:
+    """glm::distance(bbox.max, center) in float (Light.cpp:9-12)."""
+    mn = np.asarray(bbox[:3], dtype=np.float32)
+    mx = np.asarray(bbox[3:], dtype=np.float32)
+    c = ((mx + mn) * f32(0.5)).astype(np.float32)
+    d = (mx - c).astype(np.float32)
+    return float(f32(np.sqrt(_dot(d, d))))
+
+
+class AreaLight(Light):
+    def __init__(self, light_shape: Shape, light_color, oneSided: bool = False):
+        self.shape = light_shape
+        self.emissiveTexture = light_color if isinstance(light_color, Texture) else SolidColor(light_color)
+        self.oneSided = bool(oneSided)
+        self.cachedPower = 0.0
+        self.tri = None  # (mesh, local triangle) for mesh lights
+
+    def getShape(self):
+        return self.shape
+
+    def PreProcess(self, bbox):
+        """Light.cpp:277-287 for solid emission: (1|2) * Area * luminance(E)."""
+        tex = self.emissiveTexture
+        if isinstance(tex, SolidColor):
+            e = (tex.colorScale * tex.albedo).astype(np.float32)
+        else:
+            raise NotImplementedError("area light power for non-solid emission is computed by the caller")
+        area = self.shape_area()
+        self.cachedPower = float(f32((1 if self.oneSided else 2) * area * luminance(e)))
+
+    def shape_area(self) -> float:
+        if self.tri is not None:
+            mesh, k = self.tri
+            i0, i1, i2 = (int(x) for x in mesh.indices[3 * k:3 * k + 3])
+            a = mesh.vertices[i0] - mesh.vertices[i2]
+            b = mesh.vertices[i1] - mesh.vertices[i2]
+            c = _cross(a.astype(np.float32), b.astype(np.float32))
+            return float(f32(f32(np.sqrt(_dot(c, c))) * f32(0.5)))
+        return self.shape.Area()
+
+    def Power(self) -> float:
+        return self.cachedPower
+
+
+class InfiniteLight(Light):
+    sceneRadius = 0.0
+
+    def PreProcess(self, bbox):
+        self.sceneRadius = _scene_radius(bbox)
+
+
+class UniformInfiniteLight(InfiniteLight):
+    def __init__(self, light_color):
+        self.color = _v3(light_color)
+
+    def Power(self) -> float:
+        c = self.color
+        return float(f32(f32(f32(c[0] + c[1]) + c[2]) * f32(math.sqrt(self.sceneRadius))))
+
+
+class FunctionInfiniteLight(InfiniteLight):
+    """The sky gradient of main.cpp:292-295, parameterised:
+    Le(dir) = scale * ((1-a) * horizon + a * zenith), a = 0.5 * (dir.y + 1).
+    Power(): the reference estimates it by stratified jittered sampling
+    (Light.cpp:79-107, nondeterministic); we integrate the same luminance
+    deterministically (the PMF only enters MIS weights and light selection)."""
+
+    def __init__(self, horizon=(1, 0.85, 0.55), zenith=(0.45, 0.65, 1), scale: float = 1.5):
+        self.c0 = _v3(horizon)
+        self.c1 = _v3(zenith)
+        self.scale = f32(scale)
+        self.cachedPower = 0.0
+        self.power_override: Optional[float] = None
+
+    def Le(self, d) -> np.ndarray:
+        a = f32(0.5) * (f32(d[1]) + f32(1.0))
+        return (self.scale * ((f32(1.0) - a) * self.c0 + a * self.c1)).astype(np.float32)
+
+    def PreProcess(self, bbox):
+        super().PreProcess(bbox)
+        if self.power_override is not None:
+            self.cachedPower = float(self.power_override)
+            return
+        # uniform-sphere integral of luminance: dir.y = z? Le uses dir.y; under
+        # the sampling of Light.cpp:88-99 y = r sin(theta) is symmetric, so
+        # E[a] = 0.5 and the mean luminance is that of the mean colour.
+        mean = (self.scale * (f32(0.5) * self.c0 + f32(0.5) * self.c1)).astype(np.float64)
+        self.cachedPower = float(f32(luminance(mean) * math.sqrt(self.sceneRadius)))
+
+    def Power(self) -> float:
+        return self.cachedPower
+
+
+class DistantLight(Light):
+    def __init__(self, light_dir, light_color):
+        self.dir = _v3(light_dir)
+        self.color = _v3(light_color)
+        self.sceneRadius = 0.0
+
+    def isDelta(self) -> bool:
+        return True
+
+    def PreProcess(self, bbox):
+        self.sceneRadius = _scene_radius(bbox)
+
+    def Power(self) -> float:
+        c = self.color
+        return float(f32(f32(f32(c[0] + c[1]) + c[2]) * f32(math.sqrt(self.sceneRadius))))
+
+
+class PointLight(Light):
+    def __init__(self, p, light_color):
+        self.p = _v3(p)
+        self.color = _v3(light_color)
+        self.sceneRadius = 0.0
+
+    def isDelta(self) -> bool:
+        return True
+
+    def PreProcess(self, bbox):
+        self.sceneRadius = _scene_radius(bbox)
+
+    def Power(self) -> float:
+        c = self.color
+        return float(f32(f32(f32(c[0] + c[1]) + c[2]) * f32(4.0 * self.sceneRadius)))
+
+
+# --------------------------------------------------------------------------
+# Light samplers (LightSampler.cpp)
+# --------------------------------------------------------------------------
+class LightSampler:
+    kind = 0
+
+    def __init__(self):
+        self.lights: List[Light] = []
+        self.all_lights: List[Light] = []
+
+    def Add(self, light):
+        if isinstance(light, (list, tuple)):
+            for l in light:
+                self.Add(l)
+            return
+        self.lights.append(light)
+        self.all_lights.append(light)
+
+    def PreProcess(self, bbox):
+        valid = []
+        for l in self.lights:
+            l.PreProcess(bbox)
+            if l.Power() < 0.01:
+                continue
+            valid.append(l)
+        self.lights = valid
+
+    def PMF(self, light) -> float:
+        raise NotImplementedError
+
+
+class UniformLightSampler(LightSampler):
+    kind = 0
+
+    def PMF(self, light) -> float:
+        if not self.lights:
+            return 0.0
+        return float(f32(1.0) / f32(len(self.lights)))
+
+
+class PowerLightSampler(LightSampler):
+    kind = 1
+
+    def __init__(self):
+        super().__init__()
+        self.totalPower = 0.0
+
+    def PreProcess(self, bbox):
+        super().PreProcess(bbox)
+        tot = f32(0.0)
+        for l in self.lights:
+            tot = f32(tot + f32(l.Power()))
+        self.totalPower = float(tot)
+
+    def PMF(self, light) -> float:
+        if self.totalPower == 0:
+            return 1.0
+        return float(f32(light.Power()) / f32(self.totalPower))
+
+
+# --------------------------------------------------------------------------
+# Primitives
+# --------------------------------------------------------------------------
+class Primitive:
+    pass
+
+
+class GeometricPrimitive(Primitive):
+    def __init__(self, primitive_shape: Shape, material: Optional[Material], areaLight: Optional[AreaLight] = None,
+                 medium=None):
+        self.shape = primitive_shape
+        self.material = material
+        self.areaLight = areaLight
+        self.medium = medium
+
+
+class Model(Primitive):
+    """A BLAS4 over meshes: Model::BuildBlas<BLAS4> (Model.hpp:43-60) without Assimp.
+    Emissive meshes get one AreaLight per triangle, culled if Power <= FLT_EPSILON."""
+
+    def __init__(self, meshes: Sequence[Mesh], material: Optional[Material] = None, medium=None):
+        self.meshes = list(meshes)
+        self.override_material = material
+        self.override_medium = medium
+        self.tri_lights: List[Optional[AreaLight]] = []
+        for m in self.meshes:
+            for k in range(m.GetTriangleCount()):
+                area = None
+                if m.emissiveTexture is not None:
+                    area = AreaLight(None, m.emissiveTexture)
+                    area.tri = (m, k)
+                    area.PreProcess(None)
+                    if area.Power() <= float(np.finfo(np.float32).eps):
+                        area = None
+                self.tri_lights.append(area)
+
+    def triangle_count(self) -> int:
+        return sum(m.GetTriangleCount() for m in self.meshes)
+
+
+class Scene:
+    """Scene.hpp:5-37."""
+
+    def __init__(self):
+        self.primitives: List[Primitive] = []
+        self.infiniteLights: List[InfiniteLight] = []
+        self.flat = None  # set by BuildTlas
+
+    def Add(self, prim: Primitive):
+        self.primitives.append(prim)
+        self.flat = None
+
+    def BuildTlas(self):
+        """Builds TLAS4 + per-Model BLAS4 with the native builder (reference
+        algorithm) and lays out the flat scene (pathtracing_amd.flatten)."""
+        from .flatten import flatten_scene
+        self.flat = flatten_scene(self)
+        return self.flat
+
+    def GetLights(self) -> List[Light]:
+        if self.flat is None:
+            raise RuntimeError("call BuildTlas() first")
+        return list(self.flat.tlas_lights) + list(self.infiniteLights)
+
+    def BoundingBox(self) -> np.ndarray:
+        if self.flat is None:
+            raise RuntimeError("call BuildTlas() first")
+        return self.flat.bbox.copy()
+
+
+# --------------------------------------------------------------------------
+# Film / filters / camera
+# --------------------------------------------------------------------------
+class Filter:
+    kind = 0
+
+    def __init__(self, radius=(1.5, 1.5)):
+        r = np.asarray(radius, dtype=np.float32).reshape(-1)
+        if r.size == 1:
+            r = np.repeat(r, 2)
+        self.radius = r
+
+
+class MitchellFilter(Filter):
+    kind = 0
+
+    def __init__(self, radius=(1.5, 1.5), b: float = 1.0 / 3.0, c: float = 1.0 / 3.0):
+        super().__init__(radius)
+        self.b = float(b)
+        self.c = float(c)
+
+    def params(self):
+        return (self.b, self.c)
+
+
+class BoxFilter(Filter):
+    kind = 1
+
+    def __init__(self, radius=(0.5, 0.5)):
+        super().__init__(radius)
+
+    def params(self):
+        return (0.0, 0.0)
+
+
+class GaussianFilter(Filter):
+    kind = 2
+
+    def __init__(self, radius=(1.5, 1.5), sigma: float = 0.5):
+        super().__init__(radius)
+        self.sigma = float(np.float32(sigma))  # ctor takes double from a float literal 0.5f
+
+    def params(self):
+        return (self.sigma, 0.0)
+
+
+class Film:
+    """Film.hpp:112-271: accumulation buffer of {sum RGB*w, sum w} in float64."""
+
+    def __init__(self, resolution, filter: Optional[Filter] = None):
+        self.xResolution = int(resolution[0])
+        self.yResolution = int(resolution[1])
+        self.filter = filter if filter is not None else MitchellFilter()
+        self.accum = np.zeros((self.yResolution, self.xResolution, 4), dtype=np.float64)
+
+    def Resolution(self):
+        return (self.xResolution, self.yResolution)
+
+    def Clear(self):
+        self.accum[:] = 0
+
+    def image(self) -> np.ndarray:
+        w = self.accum[..., 3:4]
+        with np.errstate(invalid="ignore", divide="ignore"):
+            return np.where(w != 0, self.accum[..., :3] / w, 0.0)
+
+    def WritePPM(self, path: str):
+        """Film.hpp:154-170 (reinhard_jodie + sRGB, rows bottom-up)."""
+        rgb = self.image()
+        l = rgb @ np.array([0.2126, 0.7152, 0.0722])
+        t = rgb / (1.0 + rgb)
+        tm = (rgb / (1.0 + l[..., None])) * (1 - t) + t * t
+        tm = np.clip(tm, 0.0, 1.0)
+        s = np.where(tm < 0.0031308, 12.92 * tm, 1.055 * np.power(tm, 1.0 / 2.4) - 0.055)
+        out = (255.999 * np.clip(s, 0, 1)).astype(np.uint8)[::-1]
+        with open(path, "wb") as f:
+            f.write(b"P6\n%d %d\n255\n" % (self.xResolution, self.yResolution))
+            f.write(out.tobytes())
+
+
+class Camera:
+    """Camera.hpp:7-35.  The basis is built in float32 like the reference ctor."""
+
+    def __init__(self, lookFrom, lookAt, fov: float, film: Film, FocusAngle: float = 0.0, FocusDistance: float = 0.0):
+        self.lookFrom = _v3(lookFrom)
+        self.lookAt = _v3(lookAt)
+        self.fov = f32(fov)
+        self.film = film
+        self.FocusAngle = f32(FocusAngle)
+        self.FocusDistance = f32(FocusDistance)
+        self.w = _normalize((self.lookFrom - self.lookAt).astype(np.float32))
+        self.u = _normalize(_cross(np.array([0, 1, 0], dtype=np.float32), self.w))
+        self.v = _cross(self.w, self.u)
+        self.defocusRadius = f32(float(self.FocusDistance) * math.tan(float(self.FocusAngle) / 2.0))
+        self.halfWidth = f32(math.tan(float(self.fov) * 0.5))
+        W, H = film.Resolution()
+        self.halfHeight = f32(f32(self.halfWidth * f32(H)) / f32(W))
+
+    def GetFilm(self) -> Film:
+        return self.film

@@ -1,0 +1,59 @@
+"""Parity scenes shared by the golden generator and the tests.
+
+The scenes are built through pathtracing_amd's mirror of the reference API;
+gen_golden.py writes each as a recipe that oracle/ref_harness.cpp rebuilds
+with the reference's own classes.  `load` rebuilds a scene for a test and
+pins the one input the reference computes nondeterministically:
+FunctionInfiniteLight::PreProcess estimates the sky's Power() with jittered
+random samples (Light.cpp:79-107), so the reference's value, recorded in the
+fixture, is used.
+"""
+from __future__ import annotations
+
+from pathlib import Path
+
+import numpy as np
+
+from pathtracing_amd import scenes
+from pathtracing_amd.scene import FunctionInfiniteLight
+
+GOLDEN = Path(__file__).resolve().parent
+
+
+def parity_scenes():
+    return {
+        "example1": lambda: scenes.example_1(W=32, H=32, spp=4),
+        "example1_simple": lambda: scenes.example_1(W=32, H=32, spp=4, integrator="simple", seed=0x5EED0011),
+        "cornell_c2": lambda: scenes.cornell(W=32, H=32, spp=4, config="c2"),
+        "cornell_c3": lambda: scenes.cornell(W=32, H=32, spp=4, config="c3"),
+        "zoo": lambda: scenes.material_zoo(W=32, H=32, spp=4),
+        "zoo_simple": lambda: scenes.material_zoo(W=24, H=24, spp=4, integrator="simple", seed=0x5EED0017),
+        "heightfield": lambda: scenes.heightfield(n=70, W=24, H=24, spp=4),
+    }
+
+
+NAMES = list(parity_scenes().keys())
+
+
+def fixture(name: str):
+    return np.load(GOLDEN / f"{name}.npz", allow_pickle=False)
+
+
+def load(name: str):
+    """(setup, integrator, fixture) with the reference's sky power applied."""
+    fx = fixture(name)
+    setup = parity_scenes()[name]()
+    ls = setup.light_sampler
+    if ls is not None:
+        lights = list(setup.scene.GetLights()) + list(setup.extra_lights)
+        changed = False
+        for l, p in zip(lights, fx["light_power"]):
+            if isinstance(l, FunctionInfiniteLight):
+                l.power_override = float(p)
+                changed = True
+        if changed:
+            fresh = type(ls)()
+            fresh.Add(lights)
+            fresh.PreProcess(setup.scene.BoundingBox())
+            setup.light_sampler = fresh
+    return setup, setup.make_integrator(), fx

@@ -1,0 +1,172 @@
+"""Generate the golden fixtures in tests/golden/*.npz from the reference itself.
+
+TEST INFRASTRUCTURE.  Runs only where /root/reference exists: it builds
+oracle/_ref/ref_harness from the reference sources (oracle/Makefile), writes a
+recipe for each parity scene (pathtracing_amd.recipe), and records what the
+reference computes on it:
+
+  bvh_*      BVH4 clusters / root / primitive order        (F0)
+  lights_*   light order, Power(), PMF; LightSampler::Sample picks (F4)
+  trace_*    closest-hit interactions + any-hit booleans    (F1/F2)
+  li_*       per-sample Integrator::Li under the PCG stream (F7)
+  film       FilmTile splat of those samples + filter table (F6/F8)
+  bsdf_*     Material scatter / calc_attenuation / PDF       (F3)
+  lsample_*  Light::sample / PDF / L                         (F4)
+
+    python tests/golden/gen_golden.py
+"""
+from __future__ import annotations
+
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+
+from pathtracing_amd import scenes  # noqa: E402
+from pathtracing_amd.recipe import write_recipe  # noqa: E402
+from pathtracing_amd.scene import FunctionInfiniteLight  # noqa: E402
+
+HARNESS = ROOT / "oracle" / "_ref" / "ref_harness"
+OUT = ROOT / "tests" / "golden"
+
+
+def harness(*args):
+    subprocess.run([str(HARNESS), *map(str, args)], check=True)
+
+
+def parity_scenes():
+    from fixtures import parity_scenes as ps
+    return {k: f() for k, f in ps().items()}
+
+
+def random_rays(setup, n, rng):
+    bb = setup.scene.BoundingBox().astype(np.float64)
+    lo, hi = bb[:3], bb[3:]
+    span = np.minimum(hi - lo, 20.0)
+    mid = 0.5 * (lo + hi)
+    o = mid + (rng.random((n, 3)) - 0.5) * span
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    # half the rays from the camera toward the scene centre region
+    cam = setup.camera.lookFrom.astype(np.float64)
+    k = n // 2
+    o[:k] = cam
+    tgt = mid + (rng.random((k, 3)) - 0.5) * span * 0.5
+    dd = tgt - cam
+    d[:k] = dd / np.linalg.norm(dd, axis=1, keepdims=True)
+    tmax = np.full(n, np.inf)
+    tmax[::4] = rng.random(len(tmax[::4])) * 3.0  # bounded queries too
+    return np.concatenate([o, d, tmax[:, None]], 1).astype(np.float32)
+
+
+def bsdf_cases(n, rng):
+    def unit(m):
+        v = rng.normal(size=(m, 3))
+        return v / np.linalg.norm(v, axis=1, keepdims=True)
+    ns = unit(n)
+    ng = unit(n) * 0.3 + ns
+    ng /= np.linalg.norm(ng, axis=1, keepdims=True)
+    a = unit(n)
+    tg = a - ns * np.sum(a * ns, 1, keepdims=True)
+    tg /= np.linalg.norm(tg, axis=1, keepdims=True)
+    d = unit(n)
+    o = rng.normal(size=(n, 3))
+    p = o + d * 1.0
+    uv = rng.random((n, 2))
+    u = rng.random((n, 1))
+    uv2 = rng.random((n, 2))
+    other = unit(n)
+    cases = np.concatenate([o, d, p, ng, ns, tg, uv, np.ones((n, 1)), u, uv2, other], 1)
+    return cases.astype(np.float32)
+
+
+def gen(name, setup, rng, tmp: Path):
+    d = tmp / name
+    recipe = write_recipe(d, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
+                          setup.max_depth, setup.light_sampler, setup.extra_lights)
+    out = d / "o"
+    res = {}
+    harness(recipe, "bvh", out)
+    res["tlas_clusters"] = np.fromfile(f"{out}.tlas.clusters.bin", np.uint8)
+    res["tlas_root"] = np.fromfile(f"{out}.tlas.root.bin", np.uint8)
+    res["tlas_order"] = np.fromfile(f"{out}.tlas.order.bin", np.uint32)
+    k = 0
+    while Path(f"{out}.blas{k}.clusters.bin").exists():
+        res[f"blas{k}_clusters"] = np.fromfile(f"{out}.blas{k}.clusters.bin", np.uint8)
+        res[f"blas{k}_root"] = np.fromfile(f"{out}.blas{k}.root.bin", np.uint8)
+        res[f"blas{k}_order"] = np.fromfile(f"{out}.blas{k}.order.bin", np.uint32)
+        k += 1
+    harness(recipe, "info", out)
+    lines = Path(f"{out}.lights.txt").read_text().splitlines()
+    owners, delta, power, pmf, picks_u, picks = [], [], [], [], [], []
+    for ln in lines:
+        f = ln.split()
+        if f[0] == "sample":
+            picks_u.append(float(f[1]))
+            picks.append(f[2])
+        else:
+            owners.append(f[0])
+            delta.append(int(f[1]))
+            power.append(float(f[2]))
+            pmf.append(float(f[3]))
+    res["light_owner"] = np.array(owners)
+    res["light_delta"] = np.array(delta, np.int32)
+    res["light_power"] = np.array(power, np.float64)
+    res["light_pmf"] = np.array(pmf, np.float64)
+    res["pick_u"] = np.array(picks_u, np.float32)
+    res["pick_owner"] = np.array(picks)
+    rays = random_rays(setup, 2048, rng)
+    rays.tofile(d / "rays.bin")
+    harness(recipe, "trace", out, d / "rays.bin")
+    res["rays"] = rays
+    res["hits"] = np.fromfile(f"{out}.hits.bin", np.float32).reshape(-1, 16)
+    res["hit_ids"] = np.fromfile(f"{out}.ids.bin", np.int32).reshape(-1, 3)
+    res["any"] = np.fromfile(f"{out}.any.bin", np.uint8)
+    harness(recipe, "film", out)
+    W, H = setup.camera.film.Resolution()
+    res["film"] = np.fromfile(f"{out}.film.bin", np.float64).reshape(H, W, 4)
+    res["filter_table"] = np.fromfile(f"{out}.filter.bin", np.float64)
+    harness(recipe, "li", out)
+    rec = np.fromfile(f"{out}.li.bin", dtype=np.dtype([("px", "<f8"), ("py", "<f8"), ("L", "<f4", 3),
+                                                      ("dims", "<u4")]))
+    res["li_p"] = np.stack([rec["px"], rec["py"]], 1).reshape(W * H, setup.spp, 2)
+    res["li_L"] = rec["L"].reshape(W * H, setup.spp, 3)
+    res["li_dims"] = rec["dims"].reshape(W * H, setup.spp)
+    # material cases for every material in recipe order
+    nmat = sum(1 for ln in recipe.read_text().splitlines() if ln.startswith("material "))
+    cases = bsdf_cases(256, rng)
+    cases.tofile(d / "bsdf.bin")
+    res["bsdf_cases"] = cases
+    mobj = write_recipe.material_objects
+    res["bsdf_flat_ids"] = np.array([setup.scene.flat.material_ids[mobj[m]] for m in range(nmat)], np.int32)
+    for m in range(nmat):
+        harness(recipe, "bsdf", out, d / "bsdf.bin", m)
+        res[f"bsdf{m}"] = np.fromfile(f"{out}.bsdf{m}.bin", np.float32).reshape(-1, 20)
+    lc = np.concatenate([rng.random((64, 2)), rng.normal(size=(64, 3)) * 0.5], 1).astype(np.float32)
+    lc.tofile(d / "lights.bin")
+    harness(recipe, "lights", out, d / "lights.bin")
+    res["lsample_cases"] = lc
+    res["lsample"] = np.fromfile(f"{out}.lightsamples.bin", np.float32).reshape(-1, 18)
+    np.savez_compressed(OUT / f"{name}.npz", **res)
+    sz = (OUT / f"{name}.npz").stat().st_size
+    print(f"{name}: {sz / 1024:.0f} KiB, {len(owners)} lights, {k} BLAS, "
+          f"nonzero Li {(res['li_L'].sum(-1) > 0).mean():.2f}")
+
+
+def main():
+    if not HARNESS.exists():
+        subprocess.run(["make", "-s", "-j8", "-C", str(ROOT / "oracle"), "ref"], check=True)
+    rng = np.random.default_rng(20261015)
+    with tempfile.TemporaryDirectory() as t:
+        for name, setup in parity_scenes().items():
+            gen(name, setup, rng, Path(t))
+
+
+if __name__ == "__main__":
+    main()

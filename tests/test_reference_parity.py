@@ -1,0 +1,173 @@
+"""CPU tests: the scene host + BVH builder + oracle pinned to the reference.
+
+Golden vectors come from the reference itself (tests/golden/gen_golden.py runs
+oracle/ref_harness.cpp, compiled from /root/reference).  Tolerances (SURVEY.md
+§8c): FP32 unit outputs rel 1e-5 / abs 1e-5 (a few ulp; the reference and the
+oracle contract FMAs in different places); hit agreement >= 99.9 %; per-sample
+Li |dL| <= 1e-4 * max(1, |L|) for >= 99 % of samples (RR / lobe / Fresnel
+branch flips explain the rest); film per-pixel relative L2 <= 1e-3 on >= 99 %.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from fixtures import NAMES, load
+from pathtracing_amd.scene import AreaLight, DistantLight, FunctionInfiniteLight, PointLight, UniformInfiniteLight
+
+
+@pytest.fixture(scope="module", params=NAMES)
+def case(request):
+    setup, integ, fx = load(request.param)
+    return request.param, setup, integ, fx
+
+
+# ---------------------------------------------------------------- BVH builder (F0)
+def _bytes(a, period):
+    """Bytes with BVH4_NODE's padding byte (offset 3 of each 8-byte node,
+    indeterminate in the reference's aggregate init, BVH.hpp:38-43) zeroed."""
+    b = np.frombuffer(a.tobytes(), np.uint8).copy().reshape(-1, period)
+    for off in range(period - (32 if period == 128 else 8), period, 8):
+        b[:, off + 3] = 0
+    return b.tobytes()
+
+
+def test_bvh4_build_is_byte_identical(case):
+    name, setup, integ, fx = case
+    flat = setup.scene.flat
+    assert _bytes(flat.bvh_clusters[0], 128) == _bytes(fx["tlas_clusters"], 128), "TLAS clusters"
+    assert _bytes(flat.bvh_roots[0], 8) == _bytes(fx["tlas_root"], 8), "TLAS root"
+    np.testing.assert_array_equal(flat.top_order, fx["tlas_order"])
+    k = 0
+    while f"blas{k}_clusters" in fx:
+        assert _bytes(flat.bvh_clusters[1 + k], 128) == _bytes(fx[f"blas{k}_clusters"], 128), f"BLAS{k} clusters"
+        assert _bytes(flat.bvh_roots[1 + k], 8) == _bytes(fx[f"blas{k}_root"], 8), f"BLAS{k} root"
+        np.testing.assert_array_equal(flat.blas_orders[k], fx[f"blas{k}_order"])
+        k += 1
+    assert k == len(flat.bvh_clusters) - 1
+
+
+# ---------------------------------------------------------------- lights (F4)
+def _owner(setup, flat, l):
+    if isinstance(l, AreaLight):
+        slot = flat.light_slot[id(l)]
+        if slot < len(flat.top_order):
+            return f"top:{int(flat.top_order[slot])}"
+        for k, base in enumerate(flat.bvh_prim_base[1:]):
+            if base <= slot < base + flat.bvh_n_prims[1 + k]:
+                return f"tri:{k}:{int(flat.blas_orders[k][slot - base])}"
+    if isinstance(l, (UniformInfiniteLight, FunctionInfiniteLight)):
+        return f"inf:{setup.scene.infiniteLights.index(l)}"
+    return f"extra:{setup.extra_lights.index(l)}"
+
+
+def test_light_order_power_pmf(case):
+    name, setup, integ, fx = case
+    flat = integ.flat
+    owners = [_owner(setup, flat, l) for l in flat.light_objects]
+    # without a light sampler, lights added only to the sampler are not bound
+    assert owners == list(fx["light_owner"])[:len(owners)]
+    if integ.lightSampler is None:  # SimplePath binds no sampler (PMF unused)
+        return
+    np.testing.assert_allclose(flat.lights["power"], fx["light_power"], rtol=2e-6)
+    np.testing.assert_allclose(flat.lights["pmf"], fx["light_pmf"], rtol=2e-6)
+
+
+def test_light_sampler_picks(case):
+    """LightSampler::Sample(u) (LightSampler.cpp:7-11, 34-46) on a grid of u."""
+    name, setup, integ, fx = case
+    if integ.lightSampler is None:
+        return
+    flat = integ.flat
+    sl = flat.sampler_lights
+    pw = flat.lights["power"][sl].astype(np.float32)
+    cdf = np.cumsum(pw, dtype=np.float32)  # sequential float running sums
+    for u, want in zip(fx["pick_u"], fx["pick_owner"]):
+        if len(sl) == 0:
+            assert want == "null"
+            continue
+        if flat.light_sampler == 0:
+            i = min(int(np.float32(u) * np.float32(len(sl))), len(sl) - 1)
+        else:
+            target = np.float32(u) * np.float32(cdf[-1])
+            hits = np.nonzero(cdf >= target)[0]
+            i = int(hits[0]) if len(hits) else len(sl) - 1
+        got = _owner(setup, flat, flat.light_objects[int(sl[i])])
+        assert got == want
+
+
+# ---------------------------------------------------------------- traversal (F1/F2)
+def test_oracle_trace_matches_reference(case):
+    name, setup, integ, fx = case
+    flat = integ.flat
+    rays = np.zeros(fx["rays"].shape[0], dtype=[("o", "<f4", 3), ("d", "<f4", 3), ("tmax", "<f4")])
+    rays["o"], rays["d"], rays["tmax"] = fx["rays"][:, :3], fx["rays"][:, 3:6], fx["rays"][:, 6]
+    got = oracle.trace(flat, rays, any_hit=False)
+    ref = fx["hits"]
+    hit_ref = ref[:, 0] > 0
+    agree = (got["hit"] > 0) == hit_ref
+    assert agree.mean() >= 0.999, f"closest-hit agreement {agree.mean():.4f}"
+    both = agree & hit_ref
+    np.testing.assert_allclose(got["t"][both], ref[both, 1], rtol=1e-5, atol=1e-6)
+    for k, sl in (("p", slice(2, 5)), ("n", slice(5, 8)), ("ns", slice(8, 11)), ("uv", slice(11, 13)),
+                  ("tangent", slice(13, 16))):
+        close = np.isclose(got[k][both], ref[both, sl], rtol=1e-4, atol=2e-5).all(1)
+        assert close.mean() >= 0.999, f"{k}: {close.mean():.4f}"
+    mat_map = {v: k for k, v in enumerate(fx["bsdf_flat_ids"])}  # flat id -> recipe id
+    gm = np.array([mat_map.get(int(m), -1) for m in got["material"][both]])
+    assert (gm == fx["hit_ids"][both, 0]).mean() >= 0.999
+    assert ((got["light"][both]) == fx["hit_ids"][both, 1]).mean() >= 0.999
+    anyg = oracle.trace(flat, rays, any_hit=True)
+    agree_any = (anyg["hit"] > 0) == (fx["any"] > 0)
+    assert agree_any.mean() >= 0.999, f"any-hit agreement {agree_any.mean():.4f}"
+
+
+# ---------------------------------------------------------------- materials (F3)
+def test_oracle_bsdf_matches_reference(case):
+    name, setup, integ, fx = case
+    cases = fx["bsdf_cases"]
+    for m, fid in enumerate(fx["bsdf_flat_ids"]):
+        got = oracle.bsdf(integ.flat, int(fid), cases)
+        ref = fx[f"bsdf{m}"]
+        ok = got[:, 0] == ref[:, 0]
+        assert ok.mean() >= 0.99, f"material {m}: scatter validity {ok.mean():.3f}"
+        both = ok & (ref[:, 0] > 0)
+        g, r = got[both], ref[both]
+        close = np.isclose(g[:, 1:], r[:, 1:], rtol=2e-4, atol=2e-5, equal_nan=True).all(1)
+        assert close.mean() >= 0.98, f"material {m}: scatter values {close.mean():.3f}"
+        close2 = np.isclose(got[:, 16:20], ref[:, 16:20], rtol=2e-4, atol=2e-5, equal_nan=True).all(1)
+        assert close2.mean() >= 0.98, f"material {m}: eval values {close2.mean():.3f}"
+
+
+def test_oracle_light_samples_match_reference(case):
+    name, setup, integ, fx = case
+    got = oracle.lights(integ.flat, fx["lsample_cases"])
+    ref = fx["lsample"][:got.shape[0]]  # scene lights first (sampler-only lights absent without a sampler)
+    close = np.isclose(got, ref, rtol=1e-4, atol=1e-5, equal_nan=True).all(1)
+    assert close.mean() >= 0.99, f"{close.mean():.3f}"
+
+
+# ---------------------------------------------------------------- per-sample Li (F7) and film (F6/F8)
+def test_oracle_li_matches_reference(case):
+    name, setup, integ, fx = case
+    L, P, cnt = oracle.li(integ)
+    np.testing.assert_array_equal(P, fx["li_p"])  # camera sample positions are exact
+    ref = fx["li_L"]
+    err = np.abs(L - ref).max(-1)
+    tol = 1e-4 * np.maximum(1.0, np.abs(ref).max(-1))
+    frac = (err <= tol).mean()
+    assert frac >= 0.99, f"{name}: {frac:.4f} of samples within tolerance"
+    # the frame means agree tightly even where single paths flip a branch
+    np.testing.assert_allclose(L.astype(np.float64).mean((0, 1)), ref.astype(np.float64).mean((0, 1)),
+                               rtol=5e-3, atol=1e-6)
+
+
+def test_oracle_film_and_filter_match_reference(case):
+    name, setup, integ, fx = case
+    np.testing.assert_allclose(oracle.filter_table(integ), fx["filter_table"], rtol=1e-12, atol=1e-15)
+    film, _ = oracle.render(integ, threads=2)
+    ref = fx["film"]
+    np.testing.assert_allclose(film[..., 3], ref[..., 3], rtol=1e-12)  # weights: exact up to summation order
+    num = np.linalg.norm(film[..., :3] - ref[..., :3], axis=-1)
+    den = np.maximum(np.linalg.norm(ref[..., :3], axis=-1), 1e-3 * ref[..., 3])
+    frac = (num <= 1e-3 * den + 1e-7).mean()
+    assert frac >= 0.99, f"{name}: film pixels within 1e-3 rel L2: {frac:.4f}"

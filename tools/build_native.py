@@ -1,0 +1,84 @@
+"""Build the in-tree native libraries.
+
+  pathtracing_amd/_lib/libpt_hip.so   product: HIP kernels (gfx950) + C ABI
+                                      + host BVH builder
+  oracle/_build/liboracle.so          test infrastructure: C restatement
+  oracle/_ref/ref_harness             test infrastructure: the reference
+                                      itself (only where /root/reference exists)
+
+hipcc cross-compiles gfx950 code objects without a GPU.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+CSRC = ROOT / "pathtracing_amd" / "csrc"
+LIBDIR = ROOT / "pathtracing_amd" / "_lib"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("PT_OFFLOAD_ARCH", "gfx950")
+
+
+def _run(cmd, cwd=None):
+    print("+", " ".join(str(c) for c in cmd), flush=True)
+    subprocess.run([str(c) for c in cmd], check=True, cwd=cwd)
+
+
+def _stale(out: Path, deps) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def build_product(force: bool = False) -> Path:
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    out = LIBDIR / "libpt_hip.so"
+    deps = list(CSRC.glob("*")) + [ROOT / "include" / "pt_api.h"]
+    if not force and not _stale(out, deps):
+        return out
+    build = ROOT / "build"
+    build.mkdir(exist_ok=True)
+    inc = ["-I", ROOT / "include", "-I", CSRC]
+    # Host BVH builder: GNU dialect keeps GCC's default FP contraction, as the
+    # reference's own -std=gnu++20 build; x86-64-v3 (AVX2+FMA) is portable to
+    # the GPU hosts while contracting like the reference's -march=native build.
+    bvh_o = build / "pt_bvh.o"
+    _run(["g++", "-std=gnu++20", "-O3", "-march=x86-64-v3", "-fPIC", "-c", CSRC / "pt_bvh.cpp", "-o", bvh_o, *inc])
+    rt_o = build / "pt_runtime.o"
+    _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++20", "-munsafe-fp-atomics",
+          "-Wno-unused-result", "-Wno-unused-value", "-c", CSRC / "pt_runtime.hip", "-o", rt_o, *inc])
+    tmp = out.with_suffix(".so.tmp")
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", rt_o, bvh_o, "-o", tmp, "-lpthread"])
+    os.replace(tmp, out)
+    return out
+
+
+def build_oracle() -> Path:
+    _run(["make", "-s", "-C", ROOT / "oracle"])
+    return ROOT / "oracle" / "_build" / "liboracle.so"
+
+
+def build_reference_harness():
+    """The reference itself, compiled from /root/reference (test infrastructure)."""
+    if not Path("/root/reference/Integrators.cpp").exists():
+        return None
+    _run(["make", "-s", "-j8", "-C", ROOT / "oracle", "ref"])
+    return ROOT / "oracle" / "_ref" / "ref_harness"
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    force = "--force" in argv
+    build_product(force)
+    build_oracle()
+    if "--no-ref" not in argv:
+        build_reference_harness()
+
+
+if __name__ == "__main__":
+    main()
