@@ -1,0 +1,141 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and
+the reference's golden vectors.  Tolerances as tests/test_reference_parity.py:
+hit agreement >= 99.9 %, per-sample Li |dL| <= 1e-4 * max(1, |L|) for >= 99 %,
+film per-pixel relative L2 <= 1e-3 on >= 99 % of pixels, weights to 1e-9.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from fixtures import NAMES, load
+from pathtracing_amd import native as N
+from pathtracing_amd import scenes
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", params=NAMES)
+def case(request):
+    setup, integ, fx = load(request.param)
+    return request.param, setup, integ, fx
+
+
+def _rays(fx):
+    rays = np.zeros(fx["rays"].shape[0], dtype=N.RAY)
+    rays["o"], rays["d"], rays["tmax"] = fx["rays"][:, :3], fx["rays"][:, 3:6], fx["rays"][:, 6]
+    return rays
+
+
+def _li_close(got, ref, frac_min=0.99):
+    err = np.abs(got - ref).max(-1)
+    tol = 1e-4 * np.maximum(1.0, np.abs(ref).max(-1))
+    frac = (err <= tol).mean()
+    assert frac >= frac_min, f"{frac:.4f} of samples within tolerance"
+    np.testing.assert_allclose(got.astype(np.float64).mean((0, 1)), ref.astype(np.float64).mean((0, 1)),
+                               rtol=5e-3, atol=1e-6)
+
+
+def _film_close(film, ref, frac_min=0.99):
+    np.testing.assert_allclose(film[..., 3], ref[..., 3], rtol=1e-9, atol=1e-12)
+    num = np.linalg.norm(film[..., :3] - ref[..., :3], axis=-1)
+    den = np.maximum(np.linalg.norm(ref[..., :3], axis=-1), 1e-3 * ref[..., 3])
+    frac = (num <= 1e-3 * den + 1e-7).mean()
+    assert frac >= frac_min, f"film pixels within 1e-3 rel L2: {frac:.4f}"
+
+
+def test_gpu_trace_matches_oracle_and_reference(case):
+    name, setup, integ, fx = case
+    ctx = integ.context()
+    rays = _rays(fx)
+    hits, st = ctx.trace(rays, any_hit=False)
+    ref = oracle.trace(integ.flat, rays, any_hit=False)
+    agree = (hits["prim"] >= 0) == (ref["hit"] > 0)
+    assert agree.mean() >= 0.999
+    both = agree & (ref["hit"] > 0)
+    assert (hits["prim"][both] == ref["prim"][both]).mean() >= 0.999
+    np.testing.assert_allclose(hits["t"][both], ref["t"][both], rtol=1e-5, atol=1e-6)
+    # against the reference's own hits
+    assert ((hits["prim"] >= 0) == (fx["hits"][:, 0] > 0)).mean() >= 0.999
+    anyh, _ = ctx.trace(rays, any_hit=True)
+    assert ((anyh["prim"] > 0) == (fx["any"] > 0)).mean() >= 0.999
+    assert st["rays_closest"] == len(rays) and st["nodes_closest"] > 0
+
+
+def test_gpu_li_matches_oracle_and_reference(case):
+    name, setup, integ, fx = case
+    L = integ.RenderSamples()
+    Lo, _, _ = oracle.li(integ)
+    _li_close(L, Lo)
+    _li_close(L, fx["li_L"])
+
+
+def test_gpu_film_matches_oracle_and_reference(case):
+    name, setup, integ, fx = case
+    film = setup.camera.GetFilm()
+    film.Clear()
+    st = integ.Render()
+    ref, cnt = oracle.render(integ, threads=4)
+    # a sample whose path flips a branch (FMA / ulp) moves its 3x3 filter
+    # footprint: the film bar is the per-sample bar spread over 9 pixels
+    _film_close(film.accum, ref, frac_min=0.98)
+    _film_close(film.accum, fx["film"], frac_min=0.98)
+    assert st["paths"] == cnt["paths"]
+    # the wavefront traces the reference's closest-hit queries (a rare RR /
+    # lobe branch flip may add or drop one)
+    assert abs(st["rays_closest"] - cnt["closest"]) <= 0.002 * cnt["closest"] + 2
+    # NEE rays whose contribution is already zero are not traced; never more
+    assert st["rays_any"] <= cnt["any"]
+
+
+def test_gpu_sharded_films_sum_to_the_frame():
+    setup = scenes.cornell(W=64, H=48, spp=6, config="c3")
+    integ = setup.make_integrator()
+    film = setup.camera.GetFilm()
+    film.Clear()
+    integ.Render()
+    full = film.accum.copy()
+    parts = []
+    for r in range(3):
+        film.Clear()
+        integ.Render(shard_index=r, shard_count=3)
+        parts.append(film.accum.copy())
+    np.testing.assert_allclose(sum(parts), full, rtol=1e-9, atol=1e-12)
+    ref, _ = oracle.render(integ, threads=4)
+    _film_close(full, ref)
+
+
+@pytest.mark.parametrize("W,H,pif", [(37, 23, 0), (64, 64, 256), (8, 8, 64)])
+def test_gpu_odd_sizes_and_tiny_wavefronts(W, H, pif):
+    """Untiled (W, H not multiples of 8) and tiled orders; a wavefront far
+    smaller than the frame forces thousands of refills."""
+    setup = scenes.example_1(W=W, H=H, spp=3)
+    integ = setup.make_integrator()
+    film = setup.camera.GetFilm()
+    film.Clear()
+    integ.Render(paths_in_flight=pif)
+    ref, _ = oracle.render(integ, threads=4)
+    _film_close(film.accum, ref)
+
+
+@pytest.mark.parametrize("depth", [0, 1, 2])
+def test_gpu_shallow_depths(depth):
+    setup = scenes.material_zoo(W=16, H=16, spp=2, max_depth=depth)
+    integ = setup.make_integrator()
+    L = integ.RenderSamples()
+    Lo, _, _ = oracle.li(integ)
+    _li_close(L, Lo)
+    if depth == 0:
+        assert not L.any()
+
+
+def test_gpu_counters_and_timing():
+    setup = scenes.heightfield(n=200, W=64, H=64, spp=2)
+    integ = setup.make_integrator()
+    st = integ.Render(flags=N.PT_RENDER_COUNT_NODES | N.PT_RENDER_TIMING)
+    assert st["nodes_closest"] > st["rays_closest"] > 0
+    assert st["tris_closest"] > 0 and st["ms_closest"] > 0 and st["launches_closest"] > 0
+    _, cnt = oracle.render(integ, threads=4)
+    # node visits per ray of the GPU order vs the reference order (same tree)
+    g = st["nodes_closest"] / st["rays_closest"]
+    o = cnt["nodes_closest"] / cnt["closest"]
+    assert 0.5 * o <= g <= 1.5 * o
