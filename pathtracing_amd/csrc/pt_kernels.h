@@ -2,16 +2,19 @@
 #pragma once
 #include "pt_trace.h"
 
-// path flags (meta.z): depth | rr_depth << 12 | spec
+// path flags (b.w): depth | rr_depth << 12 | spec
 #define PF_DEPTH_MASK 0xFFFu
 #define PF_RR_SHIFT 12
 #define PF_SPEC (1u << 24)
 
-// queue counters
+// queue counters, each on its own 128-byte line (one word saturates at
+// ~88 atomics/us: MI355X_MICROARCH.md "dequeue"); appends are aggregated per
+// block so a launch issues one atomic per block per counter
+#define Q_STRIDE 32
 #define Q_NEXT 0
-#define Q_DONE 1
-#define Q_SHADOW 2
-#define Q_COUNT 4
+#define Q_DONE (1 * Q_STRIDE)
+#define Q_SHADOW (2 * Q_STRIDE)
+#define Q_WORDS (3 * Q_STRIDE)
 
 // 64-bit work counters
 #define CNT_NODES_CLOSEST 0
@@ -20,23 +23,25 @@
 #define CNT_TRIS_ANY 3
 #define CNT_NEXT_SAMPLE 4
 #define CNT_COUNT 8
+#define CNT_SHARDS 64  // work counters are sharded by block to avoid a hot line
 
-// Path state, structure of float4/uint4 arrays indexed by slot (16-B lanes,
-// dwordx4 loads and stores).
+// Compacted path state: the live paths of one bounce occupy entries
+// [0, n) of these arrays, so every kernel reads and writes them coalesced
+// (lane i <-> entry i; appends are contiguous per wave).  64 B per path.
 struct PathSoA {
-    float4* ray_o;  // origin
-    float4* ray_d;  // direction
-    float4* beta;   // attenuation.xyz, prevPDF
-    float4* L;      // radiance so far
-    uint4* meta;    // stream key, next draw dimension, flags, sample id in chunk
-    float4* hit;    // t, b1, b2, prim slot (int bits; -1 = miss)
+    float4* o;    // origin.xyz, stream key (bits)
+    float4* d;    // direction.xyz, flags (bits): depth | rr << 12 | spec
+    float4* beta; // attenuation.xyz, prevPDF
+    float4* L;    // radiance so far .xyz, next draw dimension (bits)
+    uint32_t* sid;// sample id within the chunk
 };
 
 struct ShadowRec {
     float4 o;  // origin, tmax
-    float4 d;  // direction, path slot (bits)
+    float4 d;  // direction, target (bits): entry in next state, or DONE_BIT|entry in done list
     float4 c;  // contribution if unoccluded
 };
+#define SHADOW_DONE_BIT 0x80000000u
 
 struct RenderParams {
     pt_camera_desc cam;
@@ -56,15 +61,15 @@ struct RenderParams {
 };
 
 template <bool COUNT>
-__global__ void k_closest(DevScene S, PathSoA P, const uint32_t* q, uint32_t n, unsigned long long* counters);
+__global__ void k_closest(DevScene S, PathSoA P, uint32_t n, float4* hit, unsigned long long* counters);
 template <bool COUNT>
-__global__ void k_shadow(DevScene S, PathSoA P, const ShadowRec* sq, const uint32_t* nptr,
+__global__ void k_shadow(DevScene S, PathSoA next, float4* done_L, const ShadowRec* sq, const uint32_t* nptr,
                          unsigned long long* counters);
 template <int INTEGRATOR>
-__global__ void k_shade(DevScene S, RenderParams R, PathSoA P, const uint32_t* q, uint32_t n, uint32_t* q_next,
-                        uint32_t* q_done, ShadowRec* sq, uint32_t* cnt);
-__global__ void k_finish(RenderParams R, PathSoA P, const uint32_t* q, const uint32_t* nptr, uint32_t n_direct,
-                         int store, uint32_t* q_next, uint32_t* cnt, unsigned long long* next_sample,
+__global__ void k_shade(DevScene S, RenderParams R, PathSoA cur, uint32_t n, const float4* hit, PathSoA next,
+                        float4* done_L, uint32_t* done_sid, ShadowRec* sq, uint32_t* cnt);
+__global__ void k_finish(RenderParams R, const float4* done_L, const uint32_t* done_sid, const uint32_t* nptr,
+                         uint32_t n_direct, PathSoA next, uint32_t* cnt, unsigned long long* next_sample,
                          float* sample_L);
 __global__ void k_gather(RenderParams R, const float* sample_L, double* film);
 __global__ void k_trace_rays(DevScene S, const pt_ray* rays, uint32_t n, int any, pt_hit* out,

@@ -15,49 +15,73 @@
 // Queue appends are wave-aggregated: one atomic per wave (__ballot/__popcll).
 #include "pt_kernels.h"
 
-// ------------------------------------------------------------------ wave helpers
-__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
-    const uint64_t mask = __ballot(pred);
-    if (mask == 0) return 0;
-    const uint32_t lane = __lane_id();
-    const int leader = __ffsll((unsigned long long)mask) - 1;
-    uint32_t base = 0;
-    if ((int)lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
-    base = __shfl(base, leader);
-    return base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+// ------------------------------------------------------------------ append helpers
+__device__ __forceinline__ uint32_t lanemask_lt_count(uint64_t m) {
+    return (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
 }
+
+// Block-aggregated append to up to three queues: per wave a ballot, per block
+// one prefix over the waves in LDS and one global atomic per queue.  Every
+// thread of the block must call it (it contains barriers).
+template <int NQ, int BLOCK>
+__device__ __forceinline__ void block_append(uint32_t* qcnt, const int (&qoff)[NQ], const bool (&pred)[NQ],
+                                             uint32_t (&slot)[NQ]) {
+    constexpr int NW = BLOCK / 64;
+    __shared__ uint32_t s_cnt[NQ][NW + 1];
+    const uint32_t wave = threadIdx.x >> 6, lane = __lane_id();
+    uint64_t m[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+        m[q] = __ballot(pred[q]);
+        if (lane == 0) s_cnt[q][wave] = (uint32_t)__popcll(m[q]);
+    }
+    __syncthreads();
+    if (threadIdx.x < NQ) {
+        const int q = threadIdx.x;
+        uint32_t tot = 0;
+        for (int w = 0; w < NW; w++) {
+            uint32_t c = s_cnt[q][w];
+            s_cnt[q][w] = tot;
+            tot += c;
+        }
+        s_cnt[q][NW] = tot ? atomicAdd(&qcnt[qoff[q]], tot) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NQ; q++) slot[q] = s_cnt[q][NW] + s_cnt[q][wave] + lanemask_lt_count(m[q]);
+}
+
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     return v;
 }
-__device__ __forceinline__ void count_add(unsigned long long* dst, uint64_t v) {
+__device__ __forceinline__ void count_add(unsigned long long* counters, int which, uint64_t v) {
     uint64_t s = wave_sum64(v);
-    if (__lane_id() == 0 && s) atomicAdd(dst, (unsigned long long)s);
+    if (__lane_id() == 0 && s) atomicAdd(&counters[(blockIdx.x % CNT_SHARDS) * CNT_COUNT + which], (unsigned long long)s);
 }
 
 // ------------------------------------------------------------------ traversal kernels
 template <bool COUNT>
-__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(DevScene S, PathSoA P, const uint32_t* __restrict__ q,
-                                                           uint32_t n, unsigned long long* counters) {
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(DevScene S, PathSoA P, uint32_t n, float4* __restrict__ hit,
+                                                           unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
-    __shared__ float s_dist[PT_STACK * PT_TRACE_BLOCK];
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     TraceWork wk{0, 0};
     if (i < n) {
-        const uint32_t p = q[i];
-        const float4 o = P.ray_o[p], d = P.ray_d[p];
+        const float4 o = P.o[i], d = P.d[i];
         float t, b1, b2;
-        int prim = trace_closest<COUNT>(S, xyz(o), xyz(d), __int_as_float(0x7f800000), t, b1, b2, s_ref, s_dist, wk);
-        P.hit[p] = make_float4(t, b1, b2, __int_as_float(prim));
+        int prim = trace_closest<COUNT>(S, xyz(o), xyz(d), __int_as_float(0x7f800000), t, b1, b2, s_ref, wk);
+        hit[i] = make_float4(t, b1, b2, __int_as_float(prim));
     }
     if (COUNT) {
-        count_add(&counters[CNT_NODES_CLOSEST], wk.nodes);
-        count_add(&counters[CNT_TRIS_CLOSEST], wk.tris);
+        count_add(counters, CNT_NODES_CLOSEST, wk.nodes);
+        count_add(counters, CNT_TRIS_CLOSEST, wk.tris);
     }
 }
 
 template <bool COUNT>
-__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(DevScene S, PathSoA P, const ShadowRec* __restrict__ sq,
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(DevScene S, PathSoA next, float4* __restrict__ done_L,
+                                                          const ShadowRec* __restrict__ sq,
                                                           const uint32_t* __restrict__ nptr,
                                                           unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
@@ -66,18 +90,20 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(DevScene S, PathSoA P
     TraceWork wk{0, 0};
     if (i < n) {
         const ShadowRec r = sq[i];
-        const uint32_t p = __float_as_uint(r.d.w);
         if (!trace_any<COUNT>(S, xyz(r.o), xyz(r.d), r.o.w, s_ref, wk)) {
-            float4 L = P.L[p];
-            L.x += r.c.x;
-            L.y += r.c.y;
-            L.z += r.c.z;
-            P.L[p] = L;
+            // one shadow ray per path per bounce: a plain read-modify-write
+            const uint32_t tgt = __float_as_uint(r.d.w);
+            float4* L = (tgt & SHADOW_DONE_BIT) ? &done_L[tgt & ~SHADOW_DONE_BIT] : &next.L[tgt];
+            float4 v = *L;
+            v.x += r.c.x;
+            v.y += r.c.y;
+            v.z += r.c.z;
+            *L = v;
         }
     }
     if (COUNT) {
-        count_add(&counters[CNT_NODES_ANY], wk.nodes);
-        count_add(&counters[CNT_TRIS_ANY], wk.tris);
+        count_add(counters, CNT_NODES_ANY, wk.nodes);
+        count_add(counters, CNT_TRIS_ANY, wk.tris);
     }
 }
 
@@ -86,7 +112,6 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(DevScene S, const
                                                               int any, pt_hit* __restrict__ out,
                                                               unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
-    __shared__ float s_dist[PT_STACK * PT_TRACE_BLOCK];
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     TraceWork wk{0, 0};
     if (i < n) {
@@ -97,12 +122,12 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(DevScene S, const
             h.prim = trace_any<true>(S, o, d, r.tmax, s_ref, wk) ? 1 : 0;
             h.t = h.b1 = h.b2 = 0;
         } else {
-            h.prim = trace_closest<true>(S, o, d, r.tmax, h.t, h.b1, h.b2, s_ref, s_dist, wk);
+            h.prim = trace_closest<true>(S, o, d, r.tmax, h.t, h.b1, h.b2, s_ref, wk);
         }
         out[i] = h;
     }
-    count_add(&counters[any ? CNT_NODES_ANY : CNT_NODES_CLOSEST], wk.nodes);
-    count_add(&counters[any ? CNT_TRIS_ANY : CNT_TRIS_CLOSEST], wk.tris);
+    count_add(counters, any ? CNT_NODES_ANY : CNT_NODES_CLOSEST, wk.nodes);
+    count_add(counters, any ? CNT_TRIS_ANY : CNT_TRIS_CLOSEST, wk.tris);
 }
 
 // ------------------------------------------------------------------ camera / regeneration
@@ -123,7 +148,6 @@ __device__ __forceinline__ void work_pixel(const RenderParams& R, uint32_t pix_i
 // TileIntegrator::Render (Integrators.cpp:61-64): pixel2D, time, lens2D.
 __device__ __forceinline__ void camera_ray(const pt_camera_desc& c, uint32_t key, uint32_t x, uint32_t y, f3& o, f3& d) {
     float a = draw(key, 0), b = draw(key, 1);
-    float l0 = draw(key, 3), l1 = draw(key, 4);
     float pxf = (float)x + a, pyf = (float)y + b;  // == float(double(x) + a): both round the exact sum
     float uc = pxf / (float)c.width;
     float vc = pyf / (float)c.height;
@@ -135,6 +159,7 @@ __device__ __forceinline__ void camera_ray(const pt_camera_desc& c, uint32_t key
         d = dir;
         return;
     }
+    float l0 = draw(key, 3), l1 = draw(key, 4);
     float r = csqrt(l0);
     float th = 2 * PT_PI * l1;
     float lx = r * cosf(th), ly = r * sinf(th);
@@ -145,76 +170,94 @@ __device__ __forceinline__ void camera_ray(const pt_camera_desc& c, uint32_t key
     d = normalize(dir - off);
 }
 
-// Finished paths store their radiance; free slots take the next sample.
-__global__ __launch_bounds__(256) void k_finish(RenderParams R, PathSoA P, const uint32_t* __restrict__ q,
-                                               const uint32_t* __restrict__ nptr, uint32_t n_direct, int store,
-                                               uint32_t* __restrict__ q_next, uint32_t* __restrict__ cnt,
+// Finished paths store their radiance (per-sample buffer, gathered into the
+// film after the chunk); for each finished path one new camera sample is
+// appended to the next state (consecutive sample ids per block: coherent
+// primary rays).  maxDepth 0 never gets here: the runtime zero-fills.
+__global__ __launch_bounds__(256) void k_finish(RenderParams R, const float4* __restrict__ done_L,
+                                               const uint32_t* __restrict__ done_sid, const uint32_t* __restrict__ nptr,
+                                               uint32_t n_direct, PathSoA next, uint32_t* __restrict__ cnt,
                                                unsigned long long* __restrict__ next_sample,
                                                float* __restrict__ sample_L) {
+    __shared__ uint32_t s_w[5];
+    __shared__ unsigned long long s_base;
     const uint32_t n = nptr ? *nptr : n_direct;
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    const bool active = i < n;
-    uint32_t slot = 0;
-    if (active) {
-        slot = q ? q[i] : i;
-        if (store) {
-            const uint4 m = P.meta[slot];
-            const float4 L = P.L[slot];
-            float* o = sample_L + 3ull * (uint64_t)m.w;
-            o[0] = L.x;
-            o[1] = L.y;
-            o[2] = L.z;
-        }
+    const bool want = i < n;
+    if (want && nptr) {
+        const float4 L = done_L[i];
+        float* o = sample_L + 3ull * (uint64_t)done_sid[i];
+        o[0] = L.x;
+        o[1] = L.y;
+        o[2] = L.z;
     }
-    // refill: a sample whose path ends before tracing (maxDepth 0) is stored at once
-    bool enq = false;
-    while (active) {
-        const unsigned long long g = atomicAdd(next_sample, 1ull);
-        if (g >= R.chunk_total) break;
+    // one returning atomic per block hands out consecutive sample ids
+    const uint64_t m = __ballot(want);
+    const uint32_t wave = threadIdx.x >> 6;
+    if (__lane_id() == 0) s_w[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < 4; w++) {
+            uint32_t c = s_w[w];
+            s_w[w] = tot;
+            tot += c;
+        }
+        s_base = tot ? atomicAdd(next_sample, (unsigned long long)tot) : 0ull;
+    }
+    __syncthreads();
+    const unsigned long long g = s_base + s_w[wave] + lanemask_lt_count(m);
+    const bool enq = want && g < R.chunk_total;
+    f3 o = F3(0, 0, 0), d = F3(0, 0, 0);
+    uint32_t key = 0;
+    if (enq) {
         const uint32_t s_rel = (uint32_t)(g / R.npix_work), pix_i = (uint32_t)(g % R.npix_work);
         uint32_t x, y;
         work_pixel(R, pix_i, x, y);
         const uint32_t s = R.shard_index + (R.s_lo + s_rel) * R.shard_count;
-        const uint32_t key = stream_key(R.seed, y * (uint32_t)R.cam.width + x, s);
-        if (R.max_depth == 0) {  // Li loop never runs: L = 0
-            float* o = sample_L + 3ull * g;
-            o[0] = o[1] = o[2] = 0.0f;
-            continue;
-        }
-        f3 o, d;
+        key = stream_key(R.seed, y * (uint32_t)R.cam.width + x, s);
         camera_ray(R.cam, key, x, y, o, d);
-        P.ray_o[slot] = make_float4(o.x, o.y, o.z, 0.0f);
-        P.ray_d[slot] = make_float4(d.x, d.y, d.z, 0.0f);
-        P.beta[slot] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);  // attenuation, prevPDF = 1
-        P.L[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        // dim 5: camera used 0..4; depth 1 (first loop test passed), spec = true
-        P.meta[slot] = make_uint4(key, 5u, 1u | PF_SPEC, (uint32_t)g);
-        enq = true;
-        break;
     }
-    const uint32_t at = wave_append(cnt, enq);
-    if (enq) q_next[at] = slot;
+    const int qoff[1] = {Q_NEXT};
+    const bool pred[1] = {enq};
+    uint32_t at[1];
+    block_append<1, 256>(cnt, qoff, pred, at);
+    if (enq) {
+        next.o[at[0]] = make_float4(o.x, o.y, o.z, __uint_as_float(key));
+        // depth 1 (first loop test passed), spec = true
+        next.d[at[0]] = make_float4(d.x, d.y, d.z, __uint_as_float(1u | PF_SPEC));
+        next.beta[at[0]] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);  // attenuation, prevPDF = 1
+        next.L[at[0]] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(5u));  // camera used dims 0..4
+        next.sid[at[0]] = (uint32_t)g;
+    }
 }
 
 // ------------------------------------------------------------------ shading
 template <int INTEGRATOR>
-__global__ __launch_bounds__(256) void k_shade(DevScene S, RenderParams R, PathSoA P, const uint32_t* __restrict__ q,
-                                              uint32_t n, uint32_t* __restrict__ q_next, uint32_t* __restrict__ q_done,
+__global__ __launch_bounds__(256) void k_shade(DevScene S, RenderParams R, PathSoA cur, uint32_t n,
+                                              const float4* __restrict__ hit, PathSoA next,
+                                              float4* __restrict__ done_L, uint32_t* __restrict__ done_sid,
                                               ShadowRec* __restrict__ sq, uint32_t* __restrict__ cnt) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     bool cont = false, done = false, shadow = false;
-    uint32_t p = 0;
     ShadowRec srec;
+    f3 ro = F3(0, 0, 0), rd = F3(0, 0, 0), att = F3(0, 0, 0), out = F3(0, 0, 0);
+    float prev = 0;
+    uint32_t key = 0, dim = 0, flags = 0, sid = 0;
     if (i < n) {
-        p = q[i];
-        const float4 o4 = P.ray_o[p], d4 = P.ray_d[p], b4 = P.beta[p], L4 = P.L[p];
-        const float4 h = P.hit[p];
-        uint4 m = P.meta[p];
-        f3 ro = xyz(o4), rd = xyz(d4);
-        f3 att = xyz(b4), out = xyz(L4);
-        float prev = b4.w;
-        uint32_t depth = m.z & PF_DEPTH_MASK, rr = (m.z >> PF_RR_SHIFT) & PF_DEPTH_MASK;
-        bool spec = (m.z & PF_SPEC) != 0;
+        const float4 o4 = cur.o[i], d4 = cur.d[i], b4 = cur.beta[i], L4 = cur.L[i];
+        const float4 h = hit[i];
+        sid = cur.sid[i];
+        ro = xyz(o4);
+        rd = xyz(d4);
+        att = xyz(b4);
+        out = xyz(L4);
+        prev = b4.w;
+        key = __float_as_uint(o4.w);
+        dim = __float_as_uint(L4.w);
+        const uint32_t f0 = __float_as_uint(d4.w);
+        uint32_t depth = f0 & PF_DEPTH_MASK, rr = (f0 >> PF_RR_SHIFT) & PF_DEPTH_MASK;
+        bool spec = (f0 & PF_SPEC) != 0;
         const int prim = __float_as_int(h.w);
         bool alive = true;
         if (prim < 0) {
@@ -231,16 +274,15 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, RenderParams R, PathS
             }
             alive = false;
         } else {
-            const uint32_t key = m.x, dim = m.y;
             float r[8];
             if (INTEGRATOR == PT_INTEGRATOR_PATH) {
 #pragma unroll
                 for (int k = 0; k < 8; k++) r[k] = draw(key, dim + k);
-                m.y = dim + 8;
+                dim += 8;
             } else {
 #pragma unroll
                 for (int k = 0; k < 4; k++) r[k] = draw(key, dim + k);
-                m.y = dim + 4;
+                dim += 4;
             }
             const DevGeom g = S.geom[prim];
             const DevPrimInfo pi = S.info[prim];
@@ -318,7 +360,7 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, RenderParams R, PathS
                                         if (!is_zero(contrib)) {
                                             shadow = true;
                                             srec.o = make_float4(si.p.x, si.p.y, si.p.z, tmax);
-                                            srec.d = make_float4(sd.x, sd.y, sd.z, __uint_as_float(p));
+                                            srec.d = make_float4(sd.x, sd.y, sd.z, 0.0f);
                                             srec.c = make_float4(contrib.x, contrib.y, contrib.z, 0.0f);
                                         }
                                     }
@@ -346,21 +388,28 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, RenderParams R, PathS
         } else {
             done = true;
         }
-        P.L[p] = make_float4(out.x, out.y, out.z, 0.0f);
-        if (cont) {
-            P.ray_o[p] = make_float4(ro.x, ro.y, ro.z, 0.0f);
-            P.ray_d[p] = make_float4(rd.x, rd.y, rd.z, 0.0f);
-            P.beta[p] = make_float4(att.x, att.y, att.z, prev);
-            m.z = depth | (rr << PF_RR_SHIFT) | (spec ? PF_SPEC : 0u);
-            P.meta[p] = m;
-        }
+        flags = depth | (rr << PF_RR_SHIFT) | (spec ? PF_SPEC : 0u);
     }
-    const uint32_t a = wave_append(&cnt[Q_NEXT], cont);
-    if (cont) q_next[a] = p;
-    const uint32_t b = wave_append(&cnt[Q_DONE], done);
-    if (done) q_done[b] = p;
-    const uint32_t c = wave_append(&cnt[Q_SHADOW], shadow);
-    if (shadow) sq[c] = srec;
+    const int qoff[3] = {Q_NEXT, Q_DONE, Q_SHADOW};
+    const bool pred[3] = {cont, done, shadow};
+    uint32_t at[3];
+    block_append<3, 256>(cnt, qoff, pred, at);
+    const uint32_t a = at[0], b = at[1], c = at[2];
+    if (cont) {
+        next.o[a] = make_float4(ro.x, ro.y, ro.z, __uint_as_float(key));
+        next.d[a] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(flags));
+        next.beta[a] = make_float4(att.x, att.y, att.z, prev);
+        next.L[a] = make_float4(out.x, out.y, out.z, __uint_as_float(dim));
+        next.sid[a] = sid;
+    }
+    if (done) {
+        done_L[b] = make_float4(out.x, out.y, out.z, 0.0f);
+        done_sid[b] = sid;
+    }
+    if (shadow) {
+        srec.d.w = __uint_as_float(cont ? a : (SHADOW_DONE_BIT | b));
+        sq[c] = srec;
+    }
 }
 
 // ------------------------------------------------------------------ film gather
@@ -435,11 +484,13 @@ __global__ __launch_bounds__(256) void k_gather(RenderParams R, const float* __r
 }
 
 // explicit instantiations used by the runtime
-template __global__ void k_closest<false>(DevScene, PathSoA, const uint32_t*, uint32_t, unsigned long long*);
-template __global__ void k_closest<true>(DevScene, PathSoA, const uint32_t*, uint32_t, unsigned long long*);
-template __global__ void k_shadow<false>(DevScene, PathSoA, const ShadowRec*, const uint32_t*, unsigned long long*);
-template __global__ void k_shadow<true>(DevScene, PathSoA, const ShadowRec*, const uint32_t*, unsigned long long*);
-template __global__ void k_shade<PT_INTEGRATOR_PATH>(DevScene, RenderParams, PathSoA, const uint32_t*, uint32_t,
-                                                     uint32_t*, uint32_t*, ShadowRec*, uint32_t*);
-template __global__ void k_shade<PT_INTEGRATOR_SIMPLE>(DevScene, RenderParams, PathSoA, const uint32_t*, uint32_t,
-                                                       uint32_t*, uint32_t*, ShadowRec*, uint32_t*);
+template __global__ void k_closest<false>(DevScene, PathSoA, uint32_t, float4*, unsigned long long*);
+template __global__ void k_closest<true>(DevScene, PathSoA, uint32_t, float4*, unsigned long long*);
+template __global__ void k_shadow<false>(DevScene, PathSoA, float4*, const ShadowRec*, const uint32_t*,
+                                         unsigned long long*);
+template __global__ void k_shadow<true>(DevScene, PathSoA, float4*, const ShadowRec*, const uint32_t*,
+                                        unsigned long long*);
+template __global__ void k_shade<PT_INTEGRATOR_PATH>(DevScene, RenderParams, PathSoA, uint32_t, const float4*, PathSoA,
+                                                     float4*, uint32_t*, ShadowRec*, uint32_t*);
+template __global__ void k_shade<PT_INTEGRATOR_SIMPLE>(DevScene, RenderParams, PathSoA, uint32_t, const float4*,
+                                                       PathSoA, float4*, uint32_t*, ShadowRec*, uint32_t*);

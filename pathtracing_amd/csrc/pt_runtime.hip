@@ -27,10 +27,13 @@ struct pt_ctx {
     uint64_t scene_bytes = 0;
     DevScene scene{};
     bool has_scene = false;
-    // wavefront buffers
+    // wavefront buffers: two compacted path states (ping-pong), per-bounce hits,
+    // the finished-path list and the shadow-ray queue
     uint32_t cap = 0;
-    PathSoA P{};
-    uint32_t *q_a = nullptr, *q_b = nullptr, *q_done = nullptr, *qcnt = nullptr;
+    PathSoA PA{}, PB{};
+    float4* hit = nullptr;
+    float4* done_L = nullptr;
+    uint32_t *done_sid = nullptr, *qcnt = nullptr;
     ShadowRec* sq = nullptr;
     unsigned long long* counters = nullptr;
     uint32_t* host_cnt = nullptr;  // pinned
@@ -90,7 +93,7 @@ extern "C" pt_status pt_create(pt_ctx** out, int device) {
             return PT_ERR_HIP;
         }
     }
-    if (hipHostMalloc((void**)&c->host_cnt, 64) != hipSuccess) {
+    if (hipHostMalloc((void**)&c->host_cnt, Q_WORDS * 4) != hipSuccess) {
         g_err = "pinned alloc failed";
         delete c;
         return PT_ERR_HIP;
@@ -106,12 +109,14 @@ static void free_scene(pt_ctx* c) {
     c->has_scene = false;
 }
 static void free_work(pt_ctx* c) {
-    void* bufs[] = {c->P.ray_o, c->P.ray_d, c->P.beta, c->P.L, c->P.meta, c->P.hit, c->q_a, c->q_b, c->q_done,
-                    c->qcnt, c->sq, c->counters};
+    void* bufs[] = {c->PA.o, c->PA.d, c->PA.beta, c->PA.L, c->PA.sid, c->PB.o, c->PB.d, c->PB.beta, c->PB.L,
+                    c->PB.sid, c->hit, c->done_L, c->done_sid, c->qcnt, c->sq, c->counters};
     for (void* p : bufs)
         if (p) hipFree(p);
-    c->P = PathSoA{};
-    c->q_a = c->q_b = c->q_done = c->qcnt = nullptr;
+    c->PA = PathSoA{};
+    c->PB = PathSoA{};
+    c->hit = c->done_L = nullptr;
+    c->done_sid = c->qcnt = nullptr;
     c->sq = nullptr;
     c->counters = nullptr;
     c->cap = 0;
@@ -429,18 +434,19 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
         free_work(c);                                                                        \
         return fail(c, PT_ERR_OOM, "wavefront allocation of %zu paths failed", (size_t)n); \
     }
-    AL(c->P.ray_o, n * 16);
-    AL(c->P.ray_d, n * 16);
-    AL(c->P.beta, n * 16);
-    AL(c->P.L, n * 16);
-    AL(c->P.meta, n * 16);
-    AL(c->P.hit, n * 16);
-    AL(c->q_a, n * 4);
-    AL(c->q_b, n * 4);
-    AL(c->q_done, n * 4);
-    AL(c->qcnt, 64);
+    for (PathSoA* P : {&c->PA, &c->PB}) {
+        AL(P->o, n * 16);
+        AL(P->d, n * 16);
+        AL(P->beta, n * 16);
+        AL(P->L, n * 16);
+        AL(P->sid, n * 4);
+    }
+    AL(c->hit, n * 16);
+    AL(c->done_L, n * 16);
+    AL(c->done_sid, n * 4);
+    AL(c->qcnt, Q_WORDS * 4);
     AL(c->sq, n * sizeof(ShadowRec));
-    AL(c->counters, CNT_COUNT * 8);
+    AL(c->counters, (CNT_SHARDS + 1) * CNT_COUNT * 8);
 #undef AL
     c->cap = cap;
     return PT_OK;
@@ -512,56 +518,63 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     const bool count = (rd->flags & PT_RENDER_COUNT_NODES) != 0;
     const bool timing = (rd->flags & PT_RENDER_TIMING) != 0;
     hipStream_t sm = c->stream;
-    HIPCHK(c, hipMemsetAsync(c->counters, 0, CNT_COUNT * 8, sm));
-    unsigned long long* next_sample = c->counters + CNT_NEXT_SAMPLE;
+    HIPCHK(c, hipMemsetAsync(c->counters, 0, (CNT_SHARDS + 1) * CNT_COUNT * 8, sm));
+    // the sample-id counter sits on its own line after the work-counter shards
+    unsigned long long* next_sample = c->counters + CNT_SHARDS * CNT_COUNT + CNT_NEXT_SAMPLE;
     float t_cl = 0, t_sh = 0, t_an = 0;
 
     for (uint32_t s_lo = 0; s_lo < spp_local; s_lo += s_chunk) {
         R.s_lo = s_lo;
         R.s_hi = std::min(spp_local, s_lo + s_chunk);
         R.chunk_total = (unsigned long long)R.npix_work * (R.s_hi - R.s_lo);
+        if (R.max_depth == 0) {  // the Li loop never runs: every sample is black
+            HIPCHK(c, hipMemsetAsync(c->sample_L, 0, 12ull * R.chunk_total, sm));
+            if (stats) stats->paths += R.chunk_total;
+            if ((st = on_chunk(R)) != PT_OK) return st;
+            continue;
+        }
         HIPCHK(c, hipMemsetAsync(next_sample, 0, 8, sm));
-        HIPCHK(c, hipMemsetAsync(c->qcnt, 0, 64, sm));
-        // initial fill of every slot
-        uint32_t* q_cur = c->q_a;
-        uint32_t* q_nxt = c->q_b;
-        hipLaunchKernelGGL(k_finish, dim3((paths + 255) / 256), dim3(256), 0, sm, R, c->P, (const uint32_t*)nullptr,
-                           (const uint32_t*)nullptr, paths, 0, q_cur, c->qcnt + Q_NEXT, next_sample, c->sample_L);
+        // initial fill: one camera sample per wavefront entry
+        PathSoA cur = c->PA, nxt = c->PB;
+        hipLaunchKernelGGL(k_finish, dim3((paths + 255) / 256), dim3(256), 0, sm, R, (const float4*)nullptr,
+                           (const uint32_t*)nullptr, (const uint32_t*)nullptr, paths, cur, c->qcnt, next_sample,
+                           c->sample_L);
         HIPCHK(c, hipGetLastError());
-        HIPCHK(c, hipMemcpyAsync(c->host_cnt, c->qcnt, 16, hipMemcpyDeviceToHost, sm));
+        HIPCHK(c, hipMemcpyAsync(c->host_cnt, c->qcnt, Q_WORDS * 4, hipMemcpyDeviceToHost, sm));
         HIPCHK(c, hipStreamSynchronize(sm));
         uint32_t n_active = c->host_cnt[Q_NEXT];
         while (n_active > 0) {
-            HIPCHK(c, hipMemsetAsync(c->qcnt, 0, 16, sm));
+            HIPCHK(c, hipMemsetAsync(c->qcnt, 0, Q_WORDS * 4, sm));
             const dim3 gt((n_active + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK), gs((n_active + 255) / 256);
             if (timing) HIPCHK(c, hipEventRecord(c->ev[0], sm));
             if (count)
-                hipLaunchKernelGGL(k_closest<true>, gt, dim3(PT_TRACE_BLOCK), 0, sm, c->scene, c->P, q_cur, n_active,
+                hipLaunchKernelGGL(k_closest<true>, gt, dim3(PT_TRACE_BLOCK), 0, sm, c->scene, cur, n_active, c->hit,
                                    c->counters);
             else
-                hipLaunchKernelGGL(k_closest<false>, gt, dim3(PT_TRACE_BLOCK), 0, sm, c->scene, c->P, q_cur, n_active,
+                hipLaunchKernelGGL(k_closest<false>, gt, dim3(PT_TRACE_BLOCK), 0, sm, c->scene, cur, n_active, c->hit,
                                    c->counters);
             if (timing) HIPCHK(c, hipEventRecord(c->ev[1], sm));
             if (rd->integrator == PT_INTEGRATOR_SIMPLE)
-                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_SIMPLE>, gs, dim3(256), 0, sm, c->scene, R, c->P, q_cur,
-                                   n_active, q_nxt, c->q_done, c->sq, c->qcnt);
+                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_SIMPLE>, gs, dim3(256), 0, sm, c->scene, R, cur, n_active,
+                                   (const float4*)c->hit, nxt, c->done_L, c->done_sid, c->sq, c->qcnt);
             else
-                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_PATH>, gs, dim3(256), 0, sm, c->scene, R, c->P, q_cur,
-                                   n_active, q_nxt, c->q_done, c->sq, c->qcnt);
+                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_PATH>, gs, dim3(256), 0, sm, c->scene, R, cur, n_active,
+                                   (const float4*)c->hit, nxt, c->done_L, c->done_sid, c->sq, c->qcnt);
             if (timing) HIPCHK(c, hipEventRecord(c->ev[2], sm));
             if (rd->integrator != PT_INTEGRATOR_SIMPLE) {
                 if (count)
-                    hipLaunchKernelGGL(k_shadow<true>, gt, dim3(PT_TRACE_BLOCK), 0, sm, c->scene, c->P, c->sq,
-                                       c->qcnt + Q_SHADOW, c->counters);
+                    hipLaunchKernelGGL(k_shadow<true>, gt, dim3(PT_TRACE_BLOCK), 0, sm, c->scene, nxt, c->done_L,
+                                       (const ShadowRec*)c->sq, (const uint32_t*)(c->qcnt + Q_SHADOW), c->counters);
                 else
-                    hipLaunchKernelGGL(k_shadow<false>, gt, dim3(PT_TRACE_BLOCK), 0, sm, c->scene, c->P, c->sq,
-                                       c->qcnt + Q_SHADOW, c->counters);
+                    hipLaunchKernelGGL(k_shadow<false>, gt, dim3(PT_TRACE_BLOCK), 0, sm, c->scene, nxt, c->done_L,
+                                       (const ShadowRec*)c->sq, (const uint32_t*)(c->qcnt + Q_SHADOW), c->counters);
             }
             if (timing) HIPCHK(c, hipEventRecord(c->ev[3], sm));
-            hipLaunchKernelGGL(k_finish, gs, dim3(256), 0, sm, R, c->P, c->q_done, c->qcnt + Q_DONE, 0u, 1, q_nxt,
-                               c->qcnt + Q_NEXT, next_sample, c->sample_L);
+            hipLaunchKernelGGL(k_finish, gs, dim3(256), 0, sm, R, (const float4*)c->done_L,
+                               (const uint32_t*)c->done_sid, (const uint32_t*)(c->qcnt + Q_DONE), 0u, nxt, c->qcnt,
+                               next_sample, c->sample_L);
             HIPCHK(c, hipGetLastError());
-            HIPCHK(c, hipMemcpyAsync(c->host_cnt, c->qcnt, 16, hipMemcpyDeviceToHost, sm));
+            HIPCHK(c, hipMemcpyAsync(c->host_cnt, c->qcnt, Q_WORDS * 4, hipMemcpyDeviceToHost, sm));
             HIPCHK(c, hipStreamSynchronize(sm));
             if (stats) {
                 stats->rays_closest += n_active;
@@ -580,15 +593,17 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                 t_an += d;
             }
             n_active = c->host_cnt[Q_NEXT];
-            std::swap(q_cur, q_nxt);
+            std::swap(cur, nxt);
         }
         if (stats) stats->paths += R.chunk_total;
         if ((st = on_chunk(R)) != PT_OK) return st;
     }
     HIPCHK(c, hipStreamSynchronize(sm));
     if (stats) {
-        unsigned long long h[CNT_COUNT];
-        HIPCHK(c, hipMemcpy(h, c->counters, sizeof(h), hipMemcpyDeviceToHost));
+        unsigned long long hs[CNT_SHARDS * CNT_COUNT], h[CNT_COUNT] = {};
+        HIPCHK(c, hipMemcpy(hs, c->counters, sizeof(hs), hipMemcpyDeviceToHost));
+        for (int k = 0; k < CNT_SHARDS; k++)
+            for (int j = 0; j < CNT_COUNT; j++) h[j] += hs[k * CNT_COUNT + j];
         stats->nodes_closest += h[CNT_NODES_CLOSEST];
         stats->tris_closest += h[CNT_TRIS_CLOSEST];
         stats->nodes_any += h[CNT_NODES_ANY];
@@ -706,7 +721,7 @@ extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any
         tmp.push_back(dh);
     }
     if (c->cap == 0 && ensure_work(c, 256) != PT_OK) return PT_ERR_OOM;
-    HIPCHK(c, hipMemsetAsync(c->counters, 0, CNT_COUNT * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->counters, 0, CNT_SHARDS * CNT_COUNT * 8, c->stream));
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
     hipLaunchKernelGGL(k_trace_rays, dim3((n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK), dim3(PT_TRACE_BLOCK), 0,
@@ -717,8 +732,10 @@ extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (stats) {
         *stats = pt_stats{};
-        unsigned long long h[CNT_COUNT];
-        HIPCHK(c, hipMemcpy(h, c->counters, sizeof(h), hipMemcpyDeviceToHost));
+        unsigned long long hs[CNT_SHARDS * CNT_COUNT], h[CNT_COUNT] = {};
+        HIPCHK(c, hipMemcpy(hs, c->counters, sizeof(hs), hipMemcpyDeviceToHost));
+        for (int k = 0; k < CNT_SHARDS; k++)
+            for (int j = 0; j < CNT_COUNT; j++) h[j] += hs[k * CNT_COUNT + j];
         float ms;
         HIPCHK(c, hipEventElapsedTime(&ms, c->ev[4], c->ev[5]));
         if (any_hit) {

@@ -186,7 +186,7 @@ __device__ __forceinline__ void slab4(const DevCluster* __restrict__ node, f3 o,
 // Closest hit.  Returns prim slot or -1; t, b1, b2 of the accepted hit.
 template <bool COUNT>
 __device__ int trace_closest(const DevScene& S, f3 o, f3 d, float tmax, float& t_out, float& b1_out, float& b2_out,
-                             uint32_t* s_ref, float* s_dist, TraceWork& wk) {
+                             uint32_t* s_ref, TraceWork& wk) {
     const uint32_t lane = threadIdx.x;
     const f3 inv = inv_dir(d);
     const uint32_t oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
@@ -196,17 +196,12 @@ __device__ int trace_closest(const DevScene& S, f3 o, f3 d, float tmax, float& t
     float bb1 = 0, bb2 = 0;
     for (;;) {
         if (ref == REF_EMPTY) {
-            // pop: skip entries farther than the current closest hit
-            bool found = false;
-            while (sp > 0) {
-                --sp;
-                float ed = s_dist[sp * PT_TRACE_BLOCK + lane];
-                if (ed > tmax) continue;
-                ref = s_ref[sp * PT_TRACE_BLOCK + lane];
-                found = true;
-                break;
-            }
-            if (!found) break;
+            // pop.  Entry distances are not kept (4-byte entries double the
+            // occupancy); a node the reference would skip (entry > tmax,
+            // BVH.hpp:1135) is fetched and all its children fail the slab test.
+            if (sp == 0) break;
+            --sp;
+            ref = s_ref[sp * PT_TRACE_BLOCK + lane];
         }
         if (!(ref & REF_LEAF)) {
             const DevCluster* node = S.nodes + ref;
@@ -218,7 +213,6 @@ __device__ int trace_closest(const DevScene& S, f3 o, f3 d, float tmax, float& t
             const uint32_t ow = node->order[oct >> 2];
             const uint32_t perm = (ow >> (8 * (oct & 3))) & 0xFFu;
             uint32_t cand = REF_EMPTY;
-            float cand_d = 0;
 #pragma unroll
             for (int k = 0; k < 4; k++) {  // far -> near: 2-bit fields from the low end
                 const uint32_t idx = (perm >> (2 * k)) & 3u;
@@ -227,11 +221,9 @@ __device__ int trace_closest(const DevScene& S, f3 o, f3 d, float tmax, float& t
                     if (c != REF_EMPTY) {
                         if (cand != REF_EMPTY && sp < PT_STACK) {
                             s_ref[sp * PT_TRACE_BLOCK + lane] = cand;
-                            s_dist[sp * PT_TRACE_BLOCK + lane] = cand_d;
                             ++sp;
                         }
                         cand = c;
-                        cand_d = sel4f(idx, te[0], te[1], te[2], te[3]);
                     }
                 }
             }
@@ -260,7 +252,6 @@ __device__ int trace_closest(const DevScene& S, f3 o, f3 d, float tmax, float& t
                 if (COUNT) wk.tris--;
                 if (sp < PT_STACK) {
                     s_ref[sp * PT_TRACE_BLOCK + lane] = __float_as_uint(g.b.x);
-                    s_dist[sp * PT_TRACE_BLOCK + lane] = 0.0f;
                     ++sp;
                 }
             } else {

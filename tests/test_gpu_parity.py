@@ -83,8 +83,9 @@ def test_gpu_film_matches_oracle_and_reference(case):
     # the wavefront traces the reference's closest-hit queries (a rare RR /
     # lobe branch flip may add or drop one)
     assert abs(st["rays_closest"] - cnt["closest"]) <= 0.002 * cnt["closest"] + 2
-    # NEE rays whose contribution is already zero are not traced; never more
-    assert st["rays_any"] <= cnt["any"]
+    # NEE rays whose contribution is already zero are not traced, so never
+    # more than the reference's (up to the same rare branch flips)
+    assert st["rays_any"] <= cnt["any"] + 0.002 * cnt["any"] + 2
 
 
 def test_gpu_sharded_films_sum_to_the_frame():
