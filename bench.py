@@ -93,6 +93,7 @@ def main():
     import torch
     import torch.distributed as dist
     from pathtracing_amd import native as N
+    from pathtracing_amd.distributed import render_frame
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -109,15 +110,11 @@ def main():
     film = torch.zeros((H, W, 4), dtype=torch.float64, device=f"cuda:{device}")
     ctx = integ.context(device)
     ctx.set_stream(torch.cuda.current_stream(device).cuda_stream)
-    kw = dict(device=device, shard_index=rank, shard_count=world, film_ptr=film.data_ptr(),
-              paths_in_flight=args.paths_in_flight)
 
     def step(flags=0):
-        film.zero_()
-        st = integ.Render(flags=flags, **kw)
-        if world > 1:
-            dist.reduce(film, dst=0)
-        return st
+        # this rank's sample shard into the device film, then the RCCL SUM
+        # reduce of the film onto rank 0 (pathtracing_amd/distributed.py)
+        return render_frame(integ, film, flags=flags, paths_in_flight=args.paths_in_flight)
 
     for _ in range(args.warmup):
         step()

@@ -1,0 +1,82 @@
+"""Multi-GPU frames: one process per GPU, samples interleaved across ranks.
+
+SURVEY.md §8(e): every rank holds a full scene replica and renders the samples
+s ≡ rank (mod world) of every pixel with the same per-sample stream keys, so
+the ranks' films sum to the single-GPU film up to summation order.  The one
+exchange is a SUM reduce of the W×H×4 f64 accumulator {ΣRGB·w, Σw}
+(Film.hpp:227-268) onto the destination rank — RCCL over xGMI with the "nccl"
+backend on ROCm, or gloo for the CPU tests.  It replaces the reference's
+`atomic<double>` film merge (Film.hpp:125-132, 244-249).
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+# stats that are sums over ranks (the rest are per-rank timings)
+_SUMMED = ("paths", "rays_closest", "rays_any", "nodes_closest", "tris_closest", "nodes_any", "tris_any",
+           "shade_hits", "launches_closest", "launches_any")
+
+
+def world() -> tuple[int, int]:
+    """(rank, world_size) of the default process group, (0, 1) without one."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def local_samples(spp: int, rank: int, world_size: int) -> int:
+    """Number of the frame's samples s in [0, spp) with s % world_size == rank."""
+    return (spp - rank + world_size - 1) // world_size if spp > rank else 0
+
+
+def render_frame(integrator, film: torch.Tensor, *, flags: int = 0, paths_in_flight: int = 0, dst: int = 0,
+                 group=None, render_shard: Optional[Callable[[int, int, torch.Tensor], dict]] = None) -> dict:
+    """Render this rank's sample shard of one frame into `film` and reduce it
+    onto rank `dst`.
+
+    film: float64 tensor (H, W, 4) — on this rank's GPU for RCCL; on the CPU
+    for gloo.  It is overwritten (zeroed, then accumulated).
+    render_shard(shard_index, shard_count, film) -> stats overrides the
+    default, which is `integrator.Render` on the tensor's device memory.
+    Returns this rank's stats (use `reduce_stats` for job totals).
+    """
+    rank, n = world() if group is None else (dist.get_rank(group), dist.get_world_size(group))
+    H, W = film.shape[0], film.shape[1]
+    fw, fh = integrator.camera.GetFilm().Resolution()
+    if film.dtype != torch.float64 or tuple(film.shape) != (fh, fw, 4) or not film.is_contiguous():
+        raise ValueError(f"film must be a contiguous float64 ({fh}, {fw}, 4) tensor, got "
+                         f"{tuple(film.shape)} {film.dtype}")
+    film.zero_()
+    if render_shard is None:
+        if film.device.type != "cuda":
+            raise ValueError("the HIP renderer accumulates into device memory: pass a cuda film tensor")
+        st = integrator.Render(device=film.device.index or 0, shard_index=rank, shard_count=n,
+                               film_ptr=film.data_ptr(), flags=flags, paths_in_flight=paths_in_flight)
+    else:
+        st = render_shard(rank, n, film)
+    if n > 1:
+        dist.reduce(film, dst=dst, op=dist.ReduceOp.SUM, group=group)
+    return st
+
+
+def reduce_stats(st: dict, device: torch.device, group=None) -> dict:
+    """Job-wide stats: counts summed over ranks, timings max over ranks."""
+    rank, n = world() if group is None else (dist.get_rank(group), dist.get_world_size(group))
+    out = dict(st)
+    if n == 1:
+        return out
+    keys = [k for k in _SUMMED if k in st]
+    t = torch.tensor([float(st[k]) for k in keys], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    for k, v in zip(keys, t.tolist()):
+        out[k] = int(v)
+    tk = [k for k in st if k.startswith("ms_")]
+    if tk:
+        t = torch.tensor([float(st[k]) for k in tk], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        for k, v in zip(tk, t.tolist()):
+            out[k] = v
+    return out
