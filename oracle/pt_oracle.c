@@ -32,10 +32,25 @@ static inline v3 muls(v3 a, float s) { return V(a.x * s, a.y * s, a.z * s); }
 static inline v3 smul(float s, v3 a) { return V(s * a.x, s * a.y, s * a.z); }
 static inline v3 divs(v3 a, float s) { return V(a.x / s, a.y / s, a.z / s); }
 static inline v3 neg(v3 a) { return V(-a.x, -a.y, -a.z); }
+/* a*b rounded even where -ffp-contract=fast would fuse it into an add */
+static inline float rmul(float a, float b) {
+    float m = a * b;
+    __asm__("" : "+x"(m));
+    return m;
+}
 /* glm::dot: tmp = a*b; tmp.x + tmp.y + tmp.z (func_geometric.inl) */
-static inline float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+/* contracted as the reference's GCC build emits it: x product rounded, then
+ * fma(y) and fma(z) (SphereShape::Intersect disassembly) */
+static inline float dot(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+/* glm::cross as the reference build contracts it (x, y lanes vectorised:
+ * first product rounded, second fused; z scalar: first fused) */
+/* glm::cross in scalar code: first product fused, second rounded
+ * (glm::intersectRayTriangle's cross(dir, e2) in the reference build) */
 static inline v3 cross(v3 a, v3 b) {
-    return V(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
+    return V(fmaf(a.y, b.z, -rmul(b.y, a.z)), fmaf(a.z, b.x, -rmul(b.z, a.x)), fmaf(a.x, b.y, -rmul(b.x, a.y)));
+}
+static inline v3 cross_v(v3 a, v3 b) {
+    return V(fmaf(-b.y, a.z, a.y * b.z), fmaf(-b.z, a.x, a.z * b.x), fmaf(a.x, b.y, -(b.x * a.y)));
 }
 static inline float length3(v3 a) { return sqrtf(dot(a, a)); }
 /* glm::normalize = v * inversesqrt(dot(v,v)), inversesqrt = 1/sqrt */
@@ -47,6 +62,11 @@ static inline v3 refract(v3 I, v3 N, float eta) {
     float k = 1.0f - eta * eta * (1.0f - d * d);
     if (k >= 0.0f) return sub(smul(eta, I), smul(eta * d + sqrtf(k), N));
     return V(0, 0, 0);
+}
+/* u*a + v*b + w*c as glm's vector expressions compile in the reference
+ * build: first product rounded, the others fused in order */
+static inline float lerp3f(float u, float a, float v, float b, float w, float c) {
+    return fmaf(w, c, fmaf(v, b, rmul(u, a)));
 }
 static inline float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 static inline float fmaxf_(float a, float b) { return a < b ? b : a; } /* std::max */
@@ -185,8 +205,12 @@ static v3 tex_eval(const scene_t* S, int id, const float uv[2]) {
     v3 c = V(channel_at(S, im, xi, yi + 1, 1), channel_at(S, im, xi, yi + 1, 2), channel_at(S, im, xi, yi + 1, 3));
     v3 d = V(channel_at(S, im, xi + 1, yi + 1, 1), channel_at(S, im, xi + 1, yi + 1, 2),
              channel_at(S, im, xi + 1, yi + 1, 3));
-    v3 r = add(add(add(smul((1 - dx) * (1 - dy), a), smul(dx * (1 - dy), b)), smul((1 - dx) * dy, c)),
-               smul(dx * dy, d));
+    /* contraction of the reference build: w_a*a rounded, then fma(w_b, b),
+     * fma(w_c, c), fma(w_d, d) in every channel */
+    float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
+    v3 r = V(fmaf(wd, d.x, fmaf(wc, c.x, fmaf(wb, b.x, wa * a.x))),
+             fmaf(wd, d.y, fmaf(wc, c.y, fmaf(wb, b.y, wa * a.y))),
+             fmaf(wd, d.z, fmaf(wc, c.z, fmaf(wb, b.z, wa * a.z))));
     return mul(vl(t->scale), r);
 }
 static float tex_alpha(const scene_t* S, int id, const float uv[2]) {
@@ -207,7 +231,10 @@ static float tex_alpha(const scene_t* S, int id, const float uv[2]) {
     float dx = x - xi, dy = y - yi;
     float a = channel_at(S, im, xi, yi, 4), b = channel_at(S, im, xi + 1, yi, 4);
     float c = channel_at(S, im, xi, yi + 1, 4), d = channel_at(S, im, xi + 1, yi + 1, 4);
-    return (1 - dx) * (1 - dy) * a + dx * (1 - dy) * b + (1 - dx) * dy * c + dx * dy * d;
+    /* contraction of the reference build (ImageTexture::alpha, scalar):
+     * w_b*b rounded, then fma(w_a, a), fma(w_c, c), fma(w_d, d) */
+    float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
+    return fmaf(wd, d, fmaf(wc, c, fmaf(wa, a, wb * b)));
 }
 
 /* Material::Alpha (Material.hpp:336-342, 572-578); base Material: true. */
@@ -245,11 +272,22 @@ static inline onb_t onb_si(const si_t* si) {
     onb_t b;
     b.a2 = si->ns;
     b.a0 = si->tangent;
-    b.a1 = cross(b.a2, b.a0);
+    b.a1 = cross_v(b.a2, b.a0);
     return b;
 }
+/* onb::toWorld (Onb.hpp:18-20) as the reference build compiles it: the
+ * out-of-line copy the scatter functions call is fma(v.z, a2, fma(v.y, a1,
+ * v.x*a0)) in every lane; inlined into sample_normalMap the x, y lanes become
+ * fma(v.z, a2, fma(v.x, a0, v.y*a1)) */
 static inline v3 to_world(const onb_t* b, v3 v) {
-    return add(add(smul(v.x, b->a0), smul(v.y, b->a1)), smul(v.z, b->a2));
+    return V(fmaf(v.z, b->a2.x, fmaf(v.y, b->a1.x, rmul(v.x, b->a0.x))),
+             fmaf(v.z, b->a2.y, fmaf(v.y, b->a1.y, rmul(v.x, b->a0.y))),
+             fmaf(v.z, b->a2.z, fmaf(v.y, b->a1.z, rmul(v.x, b->a0.z))));
+}
+static inline v3 to_world_nm(const onb_t* b, v3 v) {
+    return V(fmaf(v.z, b->a2.x, fmaf(v.x, b->a0.x, v.y * b->a1.x)),
+             fmaf(v.z, b->a2.y, fmaf(v.x, b->a0.y, v.y * b->a1.y)),
+             fmaf(v.z, b->a2.z, fmaf(v.y, b->a1.z, v.x * b->a0.z)));
 }
 static inline v3 to_local(const onb_t* b, v3 v) { return V(dot(v, b->a0), dot(v, b->a1), dot(v, b->a2)); }
 
@@ -261,7 +299,7 @@ static v3 normal_map(const scene_t* S, int mid, const si_t* si) {
     v3 t = tex_eval(S, m->norm, si->uv);
     v3 nn = normalize(sub(smul(2.0f, t), V(1, 1, 1)));
     onb_t b = onb_si(si);
-    return to_world(&b, nn);
+    return to_world_nm(&b, nn);
 }
 
 /* ------------------------------------------------------------------ shapes (Shape.cpp) */
@@ -325,16 +363,23 @@ static int tri_intersect(const scene_t* S, uint32_t tri, int mid, const ray_t* r
     float u = bx, v = by, w = 1.0f - u - v;
     const float* uvs = S->s->uvs;
     const float* nr = S->s->normals;
-    si->uv[0] = u * uvs[2 * T.i1] + v * uvs[2 * T.i2] + w * uvs[2 * T.i0];
-    si->uv[1] = u * uvs[2 * T.i1 + 1] + v * uvs[2 * T.i2 + 1] + w * uvs[2 * T.i0 + 1];
-    v3 nn = normalize(add(add(smul(u, vl(nr + 3 * T.i1)), smul(v, vl(nr + 3 * T.i2))), smul(w, vl(nr + 3 * T.i0))));
+    si->uv[0] = lerp3f(u, uvs[2 * T.i1], v, uvs[2 * T.i2], w, uvs[2 * T.i0]);
+    si->uv[1] = lerp3f(u, uvs[2 * T.i1 + 1], v, uvs[2 * T.i2 + 1], w, uvs[2 * T.i0 + 1]);
+    const float *n1 = nr + 3 * T.i1, *n2 = nr + 3 * T.i2, *n0 = nr + 3 * T.i0;
+    v3 nn = normalize(V(lerp3f(u, n1[0], v, n2[0], w, n0[0]), lerp3f(u, n1[1], v, n2[1], w, n0[1]),
+                        lerp3f(u, n1[2], v, n2[2], w, n0[2])));
     v3 e1 = sub(T.v1, T.v0), e2 = sub(T.v2, T.v0);
-    v3 N = normalize(cross(e1, e2));
+    v3 N = normalize(cross_v(e1, e2));
     si->n = N;
     if (dot(N, nn) < 0) nn = neg(nn);
     si->t = t;
     si->ns = nn;
-    si->p = add(at(r, t), muls(smul(EPS_SHADOW, N), dot(r->d, N) > 0.0f ? -1.0f : 1.0f));
+    /* ray.at(t) + eps*N*sign as the reference build contracts it: x, y lanes
+     * o + round(t*d), z lane fma(t, d, o); then one rounding for +-eps*N */
+    float sg = dot(r->d, N) > 0.0f ? -1.0f : 1.0f;
+    v3 pa = V(r->o.x + rmul(t, r->d.x), r->o.y + rmul(t, r->d.y), fmaf(t, r->d.z, r->o.z));
+    si->p = V(fmaf(rmul(EPS_SHADOW, N.x), sg, pa.x), fmaf(rmul(EPS_SHADOW, N.y), sg, pa.y),
+              fmaf(rmul(EPS_SHADOW, N.z), sg, pa.z));
     if (S->s->tri_flags[tri] & 1u) {
         const float* tg = S->s->tangents;
         v3 tv = add(add(smul(u, vl(tg + 3 * T.i1)), smul(v, vl(tg + 3 * T.i2))), smul(w, vl(tg + 3 * T.i0)));
@@ -410,8 +455,11 @@ static int sphere_root(const pt_sphere* sp, const ray_t* r, float max, float* t_
     v3 oc = sub(r->o, vl(sp->center));
     float a = dot(r->d, r->d);
     float b = dot(oc, r->d);
-    float c = dot(oc, oc) - sp->radius * sp->radius;
-    float disc = b * b - a * c;
+    /* the reference build's contraction (Shape.cpp:6-8 under GCC -O3 FMA):
+     * c = fma(-r, r, oc.oc), disc = fma(b, b, -(a*c)).  The cancellation in
+     * disc makes the root sensitive to it at ~10^2 x radius distances. */
+    float c = fmaf(-sp->radius, sp->radius, dot(oc, oc));
+    float disc = fmaf(b, b, -(a * c));
     if (disc > 0) {
         float temp = (-b - sqrtf(disc)) / a;
         if (temp < max && temp > EPS_SHADOW) { *t_out = temp; return 1; }

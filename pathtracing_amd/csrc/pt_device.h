@@ -83,9 +83,25 @@ __device__ __forceinline__ f3 operator*(f3 a, float s) { return F3(a.x * s, a.y 
 __device__ __forceinline__ f3 operator*(float s, f3 a) { return F3(s * a.x, s * a.y, s * a.z); }
 __device__ __forceinline__ f3 operator/(f3 a, float s) { return F3(a.x / s, a.y / s, a.z / s); }
 __device__ __forceinline__ f3 operator-(f3 a) { return F3(-a.x, -a.y, -a.z); }
-__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// Contraction is spelled out where the reference's GCC build fixes it (its
+// disassembly; DESIGN.md "Numerics"): fma() fuses, rmul() is a product that
+// must stay rounded.  The oracle (oracle/pt_oracle.c) uses the same forms.
+__device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ float rmul(float a, float b) { return __fmul_rn(a, b); }
+// glm::dot: x product rounded, then fma(y), fma(z)
+__device__ __forceinline__ float dot(f3 a, f3 b) { return fma_(a.z, b.z, fma_(a.y, b.y, rmul(a.x, b.x))); }
+// glm::cross in scalar code: first product fused, second rounded
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {
-    return F3(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
+    return F3(fma_(a.y, b.z, -rmul(b.y, a.z)), fma_(a.z, b.x, -rmul(b.z, a.x)), fma_(a.x, b.y, -rmul(b.x, a.y)));
+}
+// glm::cross where the reference build vectorises x, y (first product rounded,
+// second fused) and keeps z scalar (first fused): triangle normals, onb(si)
+__device__ __forceinline__ f3 cross_v(f3 a, f3 b) {
+    return F3(fma_(-b.y, a.z, rmul(a.y, b.z)), fma_(-b.z, a.x, rmul(a.z, b.x)), fma_(a.x, b.y, -rmul(b.x, a.y)));
+}
+// u*a + v*b + w*c of glm vectors: first product rounded, the others fused
+__device__ __forceinline__ float lerp3f(float u, float a, float v, float b, float w, float c) {
+    return fma_(w, c, fma_(v, b, rmul(u, a)));
 }
 __device__ __forceinline__ float csqrt(float x) { return __builtin_sqrtf(x); }
 __device__ __forceinline__ float length(f3 a) { return csqrt(dot(a, a)); }

@@ -56,7 +56,11 @@ __device__ f3 tex_eval(const DevScene& S, int id, float u, float v) {
         float dx = x - xi, dy = y - yi;
         f3 a = texel3(S, im, xi, yi), b = texel3(S, im, xi + 1, yi);
         f3 c = texel3(S, im, xi, yi + 1), d = texel3(S, im, xi + 1, yi + 1);
-        f3 r = ((1 - dx) * (1 - dy)) * a + (dx * (1 - dy)) * b + ((1 - dx) * dy) * c + (dx * dy) * d;
+        // contraction of the reference build: w_a*a rounded, then fma(w_b, b), fma(w_c, c), fma(w_d, d)
+        float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
+        f3 r = F3(fma_(wd, d.x, fma_(wc, c.x, fma_(wb, b.x, rmul(wa, a.x)))),
+                  fma_(wd, d.y, fma_(wc, c.y, fma_(wb, b.y, rmul(wa, a.y)))),
+                  fma_(wd, d.z, fma_(wc, c.z, fma_(wb, b.z, rmul(wa, a.z)))));
         r = ld3(t.scale) * r;
         return scaled ? scale * r : r;
     }
@@ -82,7 +86,9 @@ __device__ float tex_alpha(const DevScene& S, int id, float u, float v) {
         float dx = x - xi, dy = y - yi;
         float a = channel_at(S, im, xi, yi, 4), b = channel_at(S, im, xi + 1, yi, 4);
         float c = channel_at(S, im, xi, yi + 1, 4), d = channel_at(S, im, xi + 1, yi + 1, 4);
-        return (1 - dx) * (1 - dy) * a + dx * (1 - dy) * b + (1 - dx) * dy * c + dx * dy * d;
+        // ImageTexture::alpha as compiled in the reference: w_b*b rounded, then fma(w_a, a), fma(w_c, c), fma(w_d, d)
+        float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
+        return fma_(wd, d, fma_(wc, c, fma_(wa, a, rmul(wb, b))));
     }
     return 1.0f;
 }
@@ -122,10 +128,22 @@ __device__ __forceinline__ Onb onb_si(const SurfInt& si) {
     Onb b;
     b.a2 = si.ns;
     b.a0 = si.tangent;
-    b.a1 = cross(b.a2, b.a0);
+    b.a1 = cross_v(b.a2, b.a0);
     return b;
 }
-__device__ __forceinline__ f3 to_world(const Onb& b, f3 v) { return v.x * b.a0 + v.y * b.a1 + v.z * b.a2; }
+// onb::toWorld as the reference build compiles it: the out-of-line copy the
+// scatter functions call is fma(v.z, a2, fma(v.y, a1, v.x*a0)) in every lane;
+// inlined into sample_normalMap the x, y lanes become fma(v.z, a2, fma(v.x, a0, v.y*a1))
+__device__ __forceinline__ f3 to_world(const Onb& b, f3 v) {
+    return F3(fma_(v.z, b.a2.x, fma_(v.y, b.a1.x, rmul(v.x, b.a0.x))),
+              fma_(v.z, b.a2.y, fma_(v.y, b.a1.y, rmul(v.x, b.a0.y))),
+              fma_(v.z, b.a2.z, fma_(v.y, b.a1.z, rmul(v.x, b.a0.z))));
+}
+__device__ __forceinline__ f3 to_world_nm(const Onb& b, f3 v) {
+    return F3(fma_(v.z, b.a2.x, fma_(v.x, b.a0.x, rmul(v.y, b.a1.x))),
+              fma_(v.z, b.a2.y, fma_(v.x, b.a0.y, rmul(v.y, b.a1.y))),
+              fma_(v.z, b.a2.z, fma_(v.y, b.a1.z, rmul(v.x, b.a0.z))));
+}
 __device__ __forceinline__ f3 to_local(const Onb& b, f3 v) { return F3(dot(v, b.a0), dot(v, b.a1), dot(v, b.a2)); }
 
 // sample_normalMap (Material.hpp:344-348, 580-584)
@@ -135,7 +153,7 @@ __device__ f3 normal_map(const DevScene& S, int mid, const SurfInt& si) {
     if ((m.kind != PT_MAT_DIFFUSE && m.kind != PT_MAT_DIELECTRIC) || m.norm < 0) return si.ns;
     f3 t = tex_eval(S, m.norm, si.u, si.v);
     f3 nn = normalize(2.0f * t - F3(1, 1, 1));
-    return to_world(onb_si(si), nn);
+    return to_world_nm(onb_si(si), nn);
 }
 
 __device__ __forceinline__ void sphere_uv(f3 p, float& u, float& v) {
@@ -157,16 +175,21 @@ __device__ void tri_interaction(const DevScene& S, const DevGeom& g, uint32_t tr
     uint4 T = S.tri[tri];
     float u = bu, v = bv, w = 1.0f - u - v;
     const float* uvs = S.uvs;
-    si.u = u * uvs[2 * T.y] + v * uvs[2 * T.z] + w * uvs[2 * T.x];
-    si.v = u * uvs[2 * T.y + 1] + v * uvs[2 * T.z + 1] + w * uvs[2 * T.x + 1];
-    const float* nr = S.normals;
-    f3 nn = normalize(u * ld3(nr + 3 * T.y) + v * ld3(nr + 3 * T.z) + w * ld3(nr + 3 * T.x));
-    f3 N = normalize(cross(xyz(g.b), xyz(g.c)));
+    si.u = lerp3f(u, uvs[2 * T.y], v, uvs[2 * T.z], w, uvs[2 * T.x]);
+    si.v = lerp3f(u, uvs[2 * T.y + 1], v, uvs[2 * T.z + 1], w, uvs[2 * T.x + 1]);
+    const float *n1 = S.normals + 3 * T.y, *n2 = S.normals + 3 * T.z, *n0 = S.normals + 3 * T.x;
+    f3 nn = normalize(F3(lerp3f(u, n1[0], v, n2[0], w, n0[0]), lerp3f(u, n1[1], v, n2[1], w, n0[1]),
+                         lerp3f(u, n1[2], v, n2[2], w, n0[2])));
+    f3 N = normalize(cross_v(xyz(g.b), xyz(g.c)));
     si.n = N;
     if (dot(N, nn) < 0) nn = -nn;
     si.t = t;
     si.ns = nn;
-    si.p = (o + t * d) + (PT_EPS * N) * (dot(d, N) > 0.0f ? -1.0f : 1.0f);
+    // ray.at(t) + eps*N*sign as the reference build contracts it: x, y lanes
+    // o + round(t*d), z lane fma(t, d, o); then one rounding for +-eps*N
+    float sg = dot(d, N) > 0.0f ? -1.0f : 1.0f;
+    si.p = F3(fma_(rmul(PT_EPS, N.x), sg, o.x + rmul(t, d.x)), fma_(rmul(PT_EPS, N.y), sg, o.y + rmul(t, d.y)),
+              fma_(rmul(PT_EPS, N.z), sg, fma_(t, d.z, o.z)));
     if (T.w & 1u) {
         const float* tg = S.tangents;
         f3 tv = u * ld3(tg + 3 * T.y) + v * ld3(tg + 3 * T.z) + w * ld3(tg + 3 * T.x);

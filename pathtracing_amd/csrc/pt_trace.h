@@ -82,8 +82,10 @@ __device__ __forceinline__ bool sphere_root(const pt_sphere& sp, f3 o, f3 d, flo
     f3 oc = o - ld3(sp.center);
     float a = dot(d, d);
     float b = dot(oc, d);
-    float c = dot(oc, oc) - sp.radius * sp.radius;
-    float disc = b * b - a * c;
+    // contraction of the reference build (DESIGN.md "Numerics"): the
+    // cancellation in disc makes far-away sphere roots sensitive to it
+    float c = fma_(-sp.radius, sp.radius, dot(oc, oc));
+    float disc = fma_(b, b, -rmul(a, c));
     if (disc > 0) {
         float temp = (-b - csqrt(disc)) / a;
         if (temp < tmax && temp > PT_EPS) {

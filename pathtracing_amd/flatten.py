@@ -278,10 +278,12 @@ def flatten_scene(scene: Scene) -> FlatScene:
             rec["material"] = -1
             # lights of this model in BLAS leaf order
             order = model_blas[k][2]
-            for j, t in enumerate(order):
-                al = p.tri_lights[int(t)]
-                if al is not None:
-                    light_slot[id(al)] = blas_base[k] + j
+            if p.tri_lights:
+                emissive = np.zeros(p.triangle_count(), dtype=bool)
+                emissive[np.fromiter(p.tri_lights.keys(), dtype=np.int64)] = True
+                for j in np.nonzero(emissive[order])[0]:
+                    al = p.tri_lights[int(order[j])]
+                    light_slot[id(al)] = blas_base[k] + int(j)
                     tlas_lights.append(al)
         else:
             sh = p.shape

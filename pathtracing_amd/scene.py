@@ -23,7 +23,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass, field
-from typing import Callable, List, Optional, Sequence
+from typing import Callable, List, Optional, Sequence, Dict
 
 import numpy as np
 
@@ -549,17 +549,18 @@ class Model(Primitive):
         self.meshes = list(meshes)
         self.override_material = material
         self.override_medium = medium
-        self.tri_lights: List[Optional[AreaLight]] = []
+        # model-local triangle index -> AreaLight (emissive triangles only)
+        self.tri_lights: Dict[int, AreaLight] = {}
+        base = 0
         for m in self.meshes:
-            for k in range(m.GetTriangleCount()):
-                area = None
-                if m.emissiveTexture is not None:
+            if m.emissiveTexture is not None:
+                for k in range(m.GetTriangleCount()):
                     area = AreaLight(None, m.emissiveTexture)
                     area.tri = (m, k)
                     area.PreProcess(None)
-                    if area.Power() <= float(np.finfo(np.float32).eps):
-                        area = None
-                self.tri_lights.append(area)
+                    if area.Power() > float(np.finfo(np.float32).eps):
+                        self.tri_lights[base + k] = area
+            base += m.GetTriangleCount()
 
     def triangle_count(self) -> int:
         return sum(m.GetTriangleCount() for m in self.meshes)

@@ -282,8 +282,342 @@ def material_zoo(W: int = 48, H: int = 48, spp: int = 4, max_depth: int = 8, see
     return SceneSetup(scene, camera, integrator, PowerLightSampler(), max_depth, seed, spp, extra).finish()
 
 
+# --------------------------------------------------------------------------
+# C4: San-Miguel-class procedural courtyard
+# --------------------------------------------------------------------------
+def _grid_idx(rows: int, cols: int) -> np.ndarray:
+    i = np.arange((rows + 1) * (cols + 1), dtype=np.uint32).reshape(rows + 1, cols + 1)
+    a, b, c, d = i[:-1, :-1], i[:-1, 1:], i[1:, 1:], i[1:, :-1]
+    return np.stack([a, d, c, a, c, b], -1).reshape(-1)
+
+
+def _unit(v):
+    return (v / np.linalg.norm(v, axis=-1, keepdims=True)).astype(np.float32)
+
+
+def _patch(p0, eu, ev, ku: int, kv: int, uv_scale=(1.0, 1.0), disp=None):
+    """ku x kv grid over p0 + s*eu + t*ev (s, t in [0,1]); flat normal
+    cross(eu, ev), tangent eu; optional displacement along the normal."""
+    p0, eu, ev = (np.asarray(x, np.float32) for x in (p0, eu, ev))
+    S, T = np.meshgrid(np.linspace(0, 1, ku + 1, dtype=np.float32), np.linspace(0, 1, kv + 1, dtype=np.float32))
+    n = _unit(np.cross(eu, ev))
+    v = p0 + S[..., None] * eu + T[..., None] * ev
+    if disp is not None:
+        v = v + disp(S, T)[..., None] * n
+    v = v.reshape(-1, 3).astype(np.float32)
+    nr = np.repeat(n[None], v.shape[0], 0)
+    tg = np.repeat(_unit(eu)[None], v.shape[0], 0)
+    uv = np.stack([S * uv_scale[0], T * uv_scale[1]], -1).reshape(-1, 2).astype(np.float32)
+    return _grid_idx(kv, ku), v, tg, nr, uv
+
+
+def _merge_t(parts):
+    """_merge for (idx, v, t, n, uv) parts."""
+    idx, vs, ts, ns, uvs = [], [], [], [], []
+    base = 0
+    for i, v, t, n, uv in parts:
+        idx.append(i + np.uint32(base))
+        vs.append(v)
+        ts.append(t)
+        ns.append(n)
+        uvs.append(uv)
+        base += v.shape[0]
+    cat = lambda x: np.ascontiguousarray(np.concatenate(x), dtype=np.float32)
+    return np.concatenate(idx).astype(np.uint32), cat(vs), cat(ts), cat(ns), cat(uvs)
+
+
+def _sbox(center, size, angle: float, k: int):
+    """Box with every face subdivided k x k, rotated about y."""
+    cx, cy, cz = center
+    sx, sy, sz = (s / 2 for s in size)
+    c, s_ = math.cos(angle), math.sin(angle)
+    R = np.array([[c, 0, -s_], [0, 1, 0], [s_, 0, c]], np.float32)
+    faces = [((-sx, sy, -sz), (2 * sx, 0, 0), (0, 0, 2 * sz)),    # top (+y)
+             ((-sx, -sy, sz), (2 * sx, 0, 0), (0, 2 * sy, 0)),    # +z
+             ((sx, -sy, -sz), (-2 * sx, 0, 0), (0, 2 * sy, 0)),   # -z
+             ((sx, -sy, sz), (0, 0, -2 * sz), (0, 2 * sy, 0)),    # +x
+             ((-sx, -sy, -sz), (0, 0, 2 * sz), (0, 2 * sy, 0)),   # -x
+             ((-sx, -sy, sz), (2 * sx, 0, 0), (0, 0, -2 * sz))]   # bottom (-y)
+    parts = []
+    for p0, eu, ev in faces:
+        p0 = R @ np.array(p0, np.float32) + np.array([cx, cy, cz], np.float32)
+        parts.append(_patch(p0, R @ np.array(eu, np.float32), R @ np.array(ev, np.float32), k, k))
+    return _merge_t(parts)
+
+
+def _cylinder(cx, cz, y0, y1, r, nseg: int, nring: int, uv_scale=(1.0, 1.0), radius_fn=None):
+    th = np.linspace(0, 2 * math.pi, nseg + 1, dtype=np.float32)
+    ys = np.linspace(y0, y1, nring + 1, dtype=np.float32)
+    T, Y = np.meshgrid(th, ys)
+    R = r if radius_fn is None else radius_fn(T, (Y - y0) / (y1 - y0))
+    ct, st = np.cos(T), np.sin(T)
+    v = np.stack([cx + R * ct, Y, cz + R * st], -1).reshape(-1, 3).astype(np.float32)
+    n = np.stack([ct, np.zeros_like(T), st], -1).reshape(-1, 3).astype(np.float32)
+    t = np.stack([-st, np.zeros_like(T), ct], -1).reshape(-1, 3).astype(np.float32)
+    uv = np.stack([T / (2 * math.pi) * uv_scale[0], (Y - y0) / (y1 - y0) * uv_scale[1]], -1)
+    return _grid_idx(nring, nseg), v, t, n, uv.reshape(-1, 2).astype(np.float32)
+
+
+def _uv_sphere(c, r, nlat: int, nlon: int, radius_fn=None):
+    ph = np.linspace(0.02, math.pi - 0.02, nlat + 1, dtype=np.float32)
+    th = np.linspace(0, 2 * math.pi, nlon + 1, dtype=np.float32)
+    TH, PH = np.meshgrid(th, ph)
+    d = np.stack([np.sin(PH) * np.cos(TH), np.cos(PH), np.sin(PH) * np.sin(TH)], -1)
+    R = r if radius_fn is None else radius_fn(TH, PH)
+    v = (np.asarray(c, np.float32) + (R[..., None] if np.ndim(R) else R) * d).reshape(-1, 3).astype(np.float32)
+    n = d.reshape(-1, 3).astype(np.float32)
+    t = _unit(np.stack([-np.sin(TH), np.zeros_like(TH), np.cos(TH)], -1).reshape(-1, 3) + 1e-7)
+    uv = np.stack([TH / (2 * math.pi), PH / math.pi], -1).reshape(-1, 2).astype(np.float32)
+    return _grid_idx(nlat, nlon), v, t, n, uv
+
+
+def _leaf_cards(rng, center, radius: float, n: int, size: float):
+    """n alpha-masked leaf quads scattered in a crown (2 triangles each)."""
+    p = rng.normal(size=(n, 3)).astype(np.float32)
+    p = p / np.linalg.norm(p, axis=1, keepdims=True) * (radius * rng.random((n, 1)) ** 0.33)
+    p = p * np.array([1.0, 0.7, 1.0], np.float32) + np.asarray(center, np.float32)
+    a = _unit(rng.normal(size=(n, 3)).astype(np.float32))
+    b = np.cross(a, _unit(rng.normal(size=(n, 3)).astype(np.float32)))
+    b = _unit(b + 1e-6)
+    a, b = a * size, b * size * 0.6
+    v = np.stack([p - a - b, p + a - b, p + a + b, p - a + b], 1).reshape(-1, 3).astype(np.float32)
+    nr = np.repeat(_unit(np.cross(a, b)), 4, 0)
+    uv = np.tile(np.array([[0, 0], [1, 0], [1, 1], [0, 1]], np.float32), (n, 1))
+    base = (np.arange(n, dtype=np.uint32) * 4)[:, None]
+    idx = (base + np.array([0, 1, 2, 0, 2, 3], np.uint32)).reshape(-1)
+    return idx, v, None, nr, uv
+
+
+def _leaf_image(rng, size: int) -> np.ndarray:
+    rgb = _noise_img(rng, size, size, 3, 0, 255, smooth=max(2, size // 64))
+    g = np.array([40, 110, 35], np.float32) + (rgb.astype(np.float32) - 128) * np.array([0.15, 0.35, 0.12])
+    y, x = np.mgrid[0:size, 0:size].astype(np.float32) / size
+    mask = ((x - 0.5) / 0.47) ** 2 + ((y - 0.5) / 0.3) ** 2 < 1.0
+    a = np.where(mask, 255, 0).astype(np.uint8)
+    return np.concatenate([np.clip(g, 0, 255).astype(np.uint8), a[..., None]], axis=2)
+
+
+def _normal_image(rng, size: int, strength: int = 40) -> np.ndarray:
+    xy = _noise_img(rng, size, size, 2, 128 - strength, 128 + strength, smooth=max(2, size // 128))
+    return np.concatenate([xy, np.full((size, size, 1), 235, np.uint8)], axis=2)
+
+
+def _tinted(rng, size: int, base, spread: float = 40, smooth: int = 8) -> np.ndarray:
+    n = _noise_img(rng, size, size, 1, 0, 255, smooth=smooth).astype(np.float32) - 128
+    out = np.asarray(base, np.float32)[None, None, :] + n * (spread / 128.0)
+    return np.clip(out, 0, 255).astype(np.uint8)
+
+
+def sanmiguel(W: int = 1920, H: int = 1080, spp: int = 1024, max_depth: int = 128, seed: int = 0x5EED0004,
+              detail: float = 1.0, tex_size: int = 1024, integrator: str = "path") -> SceneSetup:
+    """C4: San-Miguel-class procedural courtyard, generator
+    seed 0x5EED0004.  At detail=1: ~10 M triangles in one Model (BLAS4 under a
+    TLAS4 with the lamp globes), 58 u8 textures (tex_size², the ground
+    2·tex_size²), ~20 % of the triangles alpha-masked foliage cards (Mask
+    mode, deterministic), diffuse / textured / normal-mapped / metallic /
+    mirror / rough and smooth glass / thin glass materials, ~3000 emissive
+    lamp triangles, sky gradient x1.5 (main.cpp:292-295) + DistantLight
+    ((-1,6,1), 25*(1,.93,.83)) (main.cpp:304), PowerLightSampler, Mitchell,
+    camera (17.3,1.2,7.2) -> (0,0,0), fov 1.7 (main.cpp:308-315)."""
+    rng = np.random.default_rng(seed)
+    # `detail` scales tessellation and leaf-card counts (triangles ~ detail);
+    # the instance layout (8 trees, 40 bushes, 30 table sets, 12 lamps, ...)
+    # is the same at every detail
+    d = float(detail)
+    g = lambda n: max(2, int(round(n * math.sqrt(d))))   # per-axis tessellation
+    cnt = lambda n: max(1, int(round(n * d)))            # element counts (leaf cards)
+    ts = int(tex_size)
+    Opaque = AlphaTester(AlphaMode.Opaque)
+
+    def diffuse(tex, norm=None, rough=None, metal=None):
+        m = MicrofacetDiffuse(tex, norm, rough, metal)
+        m.setAlphaTester(Opaque)
+        return m
+
+    def img(a, srgb=True):
+        return ImageTexture(a, gammaCorrection=srgb)
+
+    # ---- textures (58) ----
+    ground_alb = img(_tinted(rng, 2 * ts, (150, 135, 115), 60, smooth=4))
+    ground_nrm = img(_normal_image(rng, 2 * ts, 50), False)
+    ground_rgh = img(_noise_img(rng, ts, ts, 3, 150, 255), False)
+    wall_alb = [img(_tinted(rng, ts, c, 35)) for c in ((205, 175, 140), (220, 200, 170), (190, 120, 90),
+                                                        (200, 190, 160))]
+    wall_nrm = [img(_normal_image(rng, ts, 30), False) for _ in range(4)]
+    stone_alb, stone_nrm = img(_tinted(rng, ts, (185, 180, 170), 30)), img(_normal_image(rng, ts, 25), False)
+    bark_alb = [img(_tinted(rng, ts, (90, 65, 45), 40, smooth=3)) for _ in range(2)]
+    bark_nrm = [img(_normal_image(rng, ts, 60), False) for _ in range(2)]
+    leaf_tex = [img(_leaf_image(rng, ts)) for _ in range(6)]
+    bush_alb = [img(_tinted(rng, ts, c, 45, smooth=2)) for c in ((50, 110, 40), (70, 120, 45), (40, 90, 50),
+                                                                 (90, 130, 50), (60, 100, 30), (110, 60, 90))]
+    wood_alb = [img(_tinted(rng, ts, (120 + 12 * i, 80 + 6 * i, 50 + 4 * i), 30, smooth=2)) for i in range(8)]
+    wood_rgh = img(_noise_img(rng, ts, ts, 3, 120, 230), False)
+    frame_alb = [img(_tinted(rng, ts, c, 15)) for c in ((60, 60, 62), (150, 150, 155), (190, 160, 90),
+                                                          (120, 70, 40))]
+    frame_rgh = img(_noise_img(rng, ts, ts, 3, 40, 120), False)
+    fabric_alb = [img(_tinted(rng, ts, c, 25, smooth=1)) for c in ((160, 40, 40), (40, 60, 140), (200, 180, 90),
+                                                                     (60, 120, 90), (180, 180, 180),
+                                                                     (120, 60, 140))]
+    fabric_nrm = img(_normal_image(rng, ts, 20), False)
+    tile_alb = [img(_tinted(rng, ts, c, 30)) for c in ((170, 90, 60), (200, 200, 190), (60, 90, 140),
+                                                        (150, 150, 140))]
+    pot_alb = [img(_tinted(rng, ts, c, 25)) for c in ((180, 95, 60), (160, 85, 55), (140, 120, 100),
+                                                       (90, 110, 130))]
+
+    # ---- materials ----
+    ground_m = diffuse(ground_alb, ground_nrm, ground_rgh)
+    wall_m = [diffuse(a, n) for a, n in zip(wall_alb, wall_nrm)]
+    stone_m = diffuse(stone_alb, stone_nrm)
+    bark_m = [diffuse(a, n) for a, n in zip(bark_alb, bark_nrm)]
+    leaf_m = []
+    for t in leaf_tex:
+        m = MicrofacetDiffuse(t)
+        m.setAlphaTester(AlphaTester(AlphaMode.Mask, 0.5))
+        leaf_m.append(m)
+    bush_m = [diffuse(a) for a in bush_alb]
+    wood_m = [diffuse(a, None, wood_rgh) for a in wood_alb]
+    frame_m = [diffuse(a, None, frame_rgh, SolidColor((1, 1, 1))) for a in frame_alb]
+    fabric_m = [diffuse(a, fabric_nrm) for a in fabric_alb]
+    tile_m = [diffuse(a) for a in tile_alb]
+    pot_m = [diffuse(a) for a in pot_alb]
+    mirror = SpecularConductor((0.9, 0.9, 0.88))
+    # dielectric roughness >= 0.15: below that the GGX lobe is so narrow that
+    # evaluating it is ill-conditioned in fp32 (1-ulp changes of the half
+    # vector move D by >10 %), so no two implementations agree sample-wise;
+    # the water is smooth (the specular branch, Material.hpp:402-435)
+    glass_rough = MicrofacetDielectric(1.5, 0.2, (1, 1, 1))
+    water = MicrofacetDielectric(1.33, (0.85, 0.95, 1.0))
+    pane = ThinDielectric(1.5, SolidColor((0.92, 0.96, 0.95)))
+    bulb_m = diffuse(SolidColor((0.9, 0.9, 0.9)))
+
+    meshes: List[Mesh] = []
+
+    def add(part, mat, emission=None):
+        i, v, t, n, uv = part
+        meshes.append(Mesh(i, v, t, n, uv, mat, emission))
+
+    X0, X1, Z0, Z1, WALL_H = -20.0, 25.0, -15.0, 15.0, 9.0
+    # ground: cobblestone heightfield
+    gx, gz = g(1600), g(1100)
+
+    def cobble(S, T):
+        u, v = S * (X1 - X0), T * (Z1 - Z0)
+        return 0.015 * (np.sin(u * 9.0) * np.sin(v * 9.0)) ** 2 + 0.004 * np.sin(u * 31 + v * 17)
+    add(_patch((X0, 0.0, Z1), (X1 - X0, 0, 0), (0, 0, Z0 - Z1), gx, gz, ((X1 - X0) / 4, (Z1 - Z0) / 4), cobble),
+        ground_m)
+    # tiled path across the courtyard (slightly raised)
+    add(_patch((-18.0, 0.03, 1.2), (40.0, 0, 0), (0, 0, -2.4), g(300), g(20), (20, 1.2)), tile_m[0])
+    # buildings: four stone walls with a displaced ashlar pattern
+    walls = [((X0, 0, Z0), (0, 0, Z1 - Z0), (0, WALL_H, 0)),   # back wall (faces +x)
+             ((X0, 0, Z1), (X1 - X0, 0, 0), (0, WALL_H, 0)),   # +z wall
+             ((X1, 0, Z0), (X0 - X1, 0, 0), (0, WALL_H, 0)),   # -z wall
+             ((X1, 0, Z1), (0, 0, Z0 - Z1), (0, WALL_H, 0))]   # behind the camera
+
+    def ashlar(S, T):
+        return -0.03 * ((np.sin(S * 120) > 0.95) | (np.sin(T * 36) > 0.95)) + 0.006 * np.sin(S * 410) * np.sin(T * 97)
+    for k, (p0, eu, ev) in enumerate(walls):
+        add(_patch(p0, eu, ev, g(400), g(100), (12, 3), ashlar), wall_m[k])
+    # windows: thin glass panes set into the walls, one-sided mirrors as shutters
+    for k in range(40):
+        w = k % 4
+        p0, eu, ev = (np.asarray(x, np.float32) for x in walls[w])
+        s, t = 0.08 + 0.84 * ((k // 4) % 10) / 9.0, 0.45 + 0.3 * ((k // 40) % 2)
+        n = _unit(np.cross(eu, ev))
+        q0 = p0 + s * eu + t * ev + 0.02 * n
+        add(_patch(q0, _unit(eu) * 1.1, _unit(ev) * 1.6, 1, 1), pane)
+    # arcade: columns with a capital and an entablature beam
+    cols = [(-17.0, z) for z in np.linspace(-12, 12, 9)] + [(x, -12.5) for x in np.linspace(-14, 22, 13)]
+    for k, (cx, cz) in enumerate(cols[:22]):
+        fl = lambda T, V: 0.28 * (1 + 0.04 * np.cos(16 * T)) * (1 - 0.12 * V)   # fluted, tapering shaft
+        add(_cylinder(cx, cz, 0.0, 4.0, 0.28, g(64), g(200), (2, 4), fl), stone_m)
+        add(_sbox((cx, 4.1, cz), (0.8, 0.2, 0.8), 0.0, g(10)), stone_m)
+    add(_sbox((-17.0, 4.45, 0.0), (0.9, 0.5, 25.0), 0.0, g(40)), stone_m)
+    add(_sbox((4.0, 4.45, -12.5), (37.0, 0.5, 0.9), 0.0, g(40)), stone_m)
+    # trees: bark trunk + crown of alpha-masked leaf cards
+    trees = [(-10.0, -7.0), (-4.0, 9.0), (6.0, -8.0), (12.0, 10.0), (-13.0, 4.0), (2.0, 3.0), (15.0, -4.0),
+             (-6.0, -2.0)]
+    for k, (cx, cz) in enumerate(trees):
+        h = 3.5 + 1.5 * rng.random()
+        tr = lambda T, V: 0.3 * (1.0 - 0.5 * V) * (1 + 0.08 * np.sin(5 * T + 13 * V))
+        add(_cylinder(cx, cz, 0.0, h, 0.3, g(48), g(96), (2, 3), tr), bark_m[k % 2])
+        add(_leaf_cards(rng, (cx, h + 1.2, cz), 2.4, cnt(120_000), 0.16), leaf_m[k % 6])
+    # bushes in pots along the walls
+    for k in range(40):
+        side = k % 3
+        if side == 0:
+            cx, cz = -18.6, -13.0 + 26.0 * (k / 40.0)
+        elif side == 1:
+            cx, cz = -16.0 + 38.0 * (k / 40.0), 13.6
+        else:
+            cx, cz = -16.0 + 38.0 * (k / 40.0), -13.8
+        r = 0.45 + 0.25 * rng.random()
+        ph = rng.random(3) * 6.0
+        bl = lambda TH, PH, r=r, ph=ph: r * (1 + 0.12 * np.sin(7 * TH + ph[0]) * np.sin(5 * PH + ph[1])
+                                             + 0.05 * np.sin(23 * TH + 17 * PH + ph[2]))
+        add(_uv_sphere((cx, 0.55 + r, cz), r, g(100), g(200), bl), bush_m[k % 6])
+        pot = lambda T, V: 0.42 + 0.12 * V
+        add(_cylinder(cx, cz, 0.0, 0.6, 0.45, g(64), g(32), (3, 1), pot), pot_m[k % 4])
+    # tables with four chairs: wooden tops, metallic frames, fabric seats
+    placed = 0
+    for k in range(200):
+        if placed >= 30:
+            break
+        cx, cz = rng.uniform(-14, 20), rng.uniform(-10, 11)
+        if (cx - 17.3) ** 2 + (cz - 7.2) ** 2 < 9 or min((cx - tx) ** 2 + (cz - tz) ** 2 for tx, tz in trees) < 6:
+            continue
+        placed += 1
+        a = rng.uniform(0, math.pi)
+        kk = g(12)
+        wm, fm, cm = wood_m[placed % 8], frame_m[placed % 4], fabric_m[placed % 6]
+        parts = [_sbox((cx, 0.74, cz), (1.1, 0.05, 1.1), a, kk)]
+        for sx, sz in ((-0.45, -0.45), (0.45, -0.45), (0.45, 0.45), (-0.45, 0.45)):
+            lx, lz = cx + sx * math.cos(a) - sz * math.sin(a), cz + sx * math.sin(a) + sz * math.cos(a)
+            parts.append(_sbox((lx, 0.36, lz), (0.06, 0.72, 0.06), a, kk))
+        add(_merge_t(parts[:1]), wm)
+        add(_merge_t(parts[1:]), fm)
+        for j in range(4):
+            ca = a + j * math.pi / 2
+            ox, oz = cx + 0.95 * math.cos(ca), cz + 0.95 * math.sin(ca)
+            add(_sbox((ox, 0.45, oz), (0.45, 0.06, 0.45), ca, kk), cm)
+            bx, bz = ox + 0.22 * math.cos(ca), oz + 0.22 * math.sin(ca)
+            add(_sbox((bx, 0.75, bz), (0.04, 0.55, 0.45), ca, kk), cm)
+            legs = []
+            for sx, sz in ((-0.2, -0.2), (0.2, -0.2), (0.2, 0.2), (-0.2, 0.2)):
+                lx = ox + sx * math.cos(ca) - sz * math.sin(ca)
+                lz = oz + sx * math.sin(ca) + sz * math.cos(ca)
+                legs.append(_sbox((lx, 0.21, lz), (0.035, 0.42, 0.035), ca, kk))
+            add(_merge_t(legs), fm)
+        # a glass on the table
+        add(_cylinder(cx + 0.2, cz + 0.1, 0.77, 0.9, 0.035, g(32), g(8)), glass_rough)
+    # fountain: stone basin, rough water surface, mirror spout
+    add(_cylinder(3.0, -1.0, 0.0, 0.55, 1.8, g(256), g(32), (8, 1)), stone_m)
+    add(_cylinder(3.0, -1.0, 0.0, 0.55, 1.65, g(256), g(32), (8, 1)), stone_m)
+    add(_patch((1.4, 0.45, 0.6), (3.2, 0, 0), (0, 0, -3.2), g(64), g(64), (1, 1),
+               lambda S, T: 0.01 * np.sin(S * 40) * np.sin(T * 37)), water)
+    add(_cylinder(3.0, -1.0, 0.45, 1.6, 0.12, g(64), g(64)), mirror)
+    # lamp posts: mirror-metal posts, emissive bulbs (triangle area lights)
+    lamps = [(-15.0, -10.0), (-15.0, 10.0), (0.0, -11.0), (0.0, 11.5), (10.0, -11.0), (10.0, 11.5), (20.0, -11.0),
+             (20.0, 11.5), (-8.0, 4.0), (8.0, 4.0), (-8.0, -4.5), (14.0, 0.0)]
+    bulb_light = SolidColor((40.0, 34.0, 24.0))
+    for k, (cx, cz) in enumerate(lamps):
+        add(_cylinder(cx, cz, 0.0, 3.0, 0.06, g(32), g(64)), mirror)
+        add(_uv_sphere((cx, 3.25, cz), 0.1, 8, 16), bulb_m, bulb_light)
+
+    scene = Scene()
+    scene.Add(Model(meshes))
+    # glass lamp globes around the bulbs (analytic spheres, TLAS primitives)
+    for cx, cz in lamps:
+        scene.Add(GeometricPrimitive(SphereShape((cx, 3.25, cz), 0.25), MicrofacetDielectric(1.5, (1, 1, 1))))
+    scene.infiniteLights.append(FunctionInfiniteLight((1, 0.85, 0.55), (0.45, 0.65, 1), 1.5))
+    film = Film((W, H), MitchellFilter())
+    camera = Camera((17.3, 1.2, 7.2), (0, 0, 0), 1.7, film)
+    sun = DistantLight((-1, 6, 1), np.float32(25.0) * np.array([1, 0.93, 0.83], np.float32))
+    return SceneSetup(scene, camera, integrator, PowerLightSampler(), max_depth, seed, spp, [sun]).finish()
+
+
 CONFIGS = {
     "c1": lambda **kw: example_1(**kw),
     "c2": lambda **kw: cornell(config="c2", **kw),
     "c3": lambda **kw: cornell(config="c3", **kw),
+    "c4": lambda **kw: sanmiguel(**kw),
 }

@@ -20,6 +20,7 @@ from __future__ import annotations
 import subprocess
 import sys
 import tempfile
+import zlib
 from pathlib import Path
 
 import numpy as np
@@ -153,20 +154,32 @@ def gen(name, setup, rng, tmp: Path):
     harness(recipe, "lights", out, d / "lights.bin")
     res["lsample_cases"] = lc
     res["lsample"] = np.fromfile(f"{out}.lightsamples.bin", np.float32).reshape(-1, 18)
+    nl = res["lsample"].shape[0] // lc.shape[0]
+    if nl > 256:  # keep the fixture small: a spread of lights (first, evenly spaced, last)
+        sel = np.unique(np.r_[np.arange(64), np.linspace(0, nl - 1, 128).astype(np.int64), np.arange(nl - 8, nl)])
+        res["lsample_lights"] = sel
+        res["lsample"] = res["lsample"].reshape(nl, lc.shape[0], 18)[sel].reshape(-1, 18)
     np.savez_compressed(OUT / f"{name}.npz", **res)
     sz = (OUT / f"{name}.npz").stat().st_size
     print(f"{name}: {sz / 1024:.0f} KiB, {len(owners)} lights, {k} BLAS, "
           f"nonzero Li {(res['li_L'].sum(-1) > 0).mean():.2f}")
 
 
-def main():
+def main(names=None):
+    """All scenes share one rng stream (the committed round-1 fixtures); a
+    scene regenerated alone (`gen_golden.py NAME...`) uses its own stream
+    seeded from its name."""
     if not HARNESS.exists():
         subprocess.run(["make", "-s", "-j8", "-C", str(ROOT / "oracle"), "ref"], check=True)
+    from fixtures import parity_scenes as ps
     rng = np.random.default_rng(20261015)
     with tempfile.TemporaryDirectory() as t:
-        for name, setup in parity_scenes().items():
-            gen(name, setup, rng, Path(t))
+        for name, make in ps().items():
+            if names and name not in names:
+                continue
+            r = np.random.default_rng([20261015, zlib.crc32(name.encode())]) if names else rng
+            gen(name, make(), r, Path(t))
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or None)
