@@ -257,6 +257,21 @@ pt_status pt_render_samples(pt_ctx* ctx, const pt_camera_desc* cam, const pt_ren
                             pt_stats* stats);
 /* Test hook: rays and hits are host or device pointers (detected). */
 pt_status pt_trace(pt_ctx* ctx, const pt_ray* rays, uint32_t n, int any_hit, pt_hit* hits, pt_stats* stats);
+/* Test hook: closest hit + the SurfaceInteraction the renderer reconstructs
+ * (TriangleShape/QuadShape/SphereShape::Intersect incl. sample_normalMap,
+ * Shape.cpp:3-359): out[16*i] = {hit, t, p[3], n[3], ns[3], uv[2], tangent[3]}
+ * (zeros on a miss).  Host pointers. */
+pt_status pt_interact(pt_ctx* ctx, const pt_ray* rays, uint32_t n, float* out);
+/* Test hook: Material::scatter + calc_attenuation + PDF (Material.hpp) of
+ * material `material` on n cases of 27 floats {ray o[3], d[3], p[3], n[3],
+ * ns[3], tangent[3], uv[2], t, u, uv_sample[2], other_dir[3]} ->
+ * 20 floats {ok, f[3], pdf, flags, o[3], d[3], f(d)[3], pdf(d), f(other)[3],
+ * pdf(other)}.  Host pointers. */
+pt_status pt_bsdf_cases(pt_ctx* ctx, int32_t material, const float* cases, uint32_t n, float* out);
+/* Test hook: Light::sample(uv) + PDF + L (Light.cpp) for every light and
+ * n cases of 5 floats {uv[2], reference point[3]} -> n_lights*n records of
+ * 18 floats {L[3], p[3], n[3], uv[2], dir[3], pdf, L(p)[3]}.  Host pointers. */
+pt_status pt_light_cases(pt_ctx* ctx, const float* cases, uint32_t n, float* out);
 /* Device bytes held by the uploaded scene. */
 uint64_t pt_scene_device_bytes(const pt_ctx* ctx);
 

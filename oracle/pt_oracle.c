@@ -12,6 +12,7 @@
 #include <math.h>
 #include <pthread.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
 
 #define EPS_SHADOW 0.00001f /* shadowEpsilon (AABB.hpp:6) */
@@ -48,6 +49,9 @@ static inline float dot(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x *
  * (glm::intersectRayTriangle's cross(dir, e2) in the reference build) */
 static inline v3 cross(v3 a, v3 b) {
     return V(fmaf(a.y, b.z, -rmul(b.y, a.z)), fmaf(a.z, b.x, -rmul(b.z, a.x)), fmaf(a.x, b.y, -rmul(b.x, a.y)));
+}
+static inline v3 cross_r(v3 a, v3 b) { /* every lane: first product rounded, second fused */
+    return V(fmaf(-b.y, a.z, rmul(a.y, b.z)), fmaf(-b.z, a.x, rmul(a.z, b.x)), fmaf(-b.x, a.y, rmul(a.x, b.y)));
 }
 static inline v3 cross_v(v3 a, v3 b) {
     return V(fmaf(-b.y, a.z, a.y * b.z), fmaf(-b.z, a.x, a.z * b.x), fmaf(a.x, b.y, -(b.x * a.y)));
@@ -382,8 +386,11 @@ static int tri_intersect(const scene_t* S, uint32_t tri, int mid, const ray_t* r
               fmaf(rmul(EPS_SHADOW, N.z), sg, pa.z));
     if (S->s->tri_flags[tri] & 1u) {
         const float* tg = S->s->tangents;
-        v3 tv = add(add(smul(u, vl(tg + 3 * T.i1)), smul(v, vl(tg + 3 * T.i2))), smul(w, vl(tg + 3 * T.i0)));
-        si->tangent = normalize(sub(tv, smul(dot(si->ns, tv), si->ns)));
+        const float *t1 = tg + 3 * T.i1, *t2 = tg + 3 * T.i2, *t0 = tg + 3 * T.i0;
+        v3 tv = V(lerp3f(u, t1[0], v, t2[0], w, t0[0]), lerp3f(u, t1[1], v, t2[1], w, t0[1]),
+                  lerp3f(u, t1[2], v, t2[2], w, t0[2]));
+        float k = dot(si->ns, tv); /* tangent - ns*k fused (fixture search) */
+        si->tangent = normalize(V(fmaf(-si->ns.x, k, tv.x), fmaf(-si->ns.y, k, tv.y), fmaf(-si->ns.z, k, tv.z)));
     } else {
         v3 up = (fabsf(si->ns.x) > 0.9999f) ? V(0, 1, 0) : V(1, 0, 0);
         si->tangent = normalize(cross(up, si->ns));
@@ -971,7 +978,7 @@ typedef struct { v3 L; si_t si; v3 dir; } lsample_t;
 static float shape_area(const scene_t* S, const pt_prim* p) {
     if (p->kind == PT_PRIM_QUAD) {
         const pt_quad* q = &S->s->quads[p->index];
-        return length3(cross(vl(q->u), vl(q->v)));
+        return length3(cross_r(vl(q->u), vl(q->v)));  /* QuadShape::Area as compiled (fixture search) */
     }
     if (p->kind == PT_PRIM_SPHERE) {
         float r = S->s->spheres[p->index].radius;
@@ -991,11 +998,11 @@ static si_t shape_sample(const scene_t* S, const pt_prim* p, float u0, float u1)
     } else if (p->kind == PT_PRIM_SPHERE) {
         const pt_sphere* sp = &S->s->spheres[p->index];
         float z = 1.0f - 2.0f * u0;
-        float r = sqrtf(1.0f - z * z);
+        float r = sqrtf(fmaf(-z, z, 1.0f));
         float phi = 2.0f * PI_F * u1;
         v3 d = V(r * cosf(phi), r * sinf(phi), z);
         v3 c = vl(sp->center);
-        si.p = add(c, smul(sp->radius, d));
+        si.p = V(fmaf(sp->radius, d.x, c.x), fmaf(sp->radius, d.y, c.y), fmaf(sp->radius, d.z, c.z));
         si.n = normalize(sub(si.p, c));
         sphere_uv(si.p, si.uv);
     } else {
@@ -1004,17 +1011,20 @@ static si_t shape_sample(const scene_t* S, const pt_prim* p, float u0, float u1)
         tri_t T = tri_get(S, p->index);
         v3 n = normalize(cross(sub(T.v1, T.v0), sub(T.v2, T.v0)));
         if (n.x != n.x) n = V(0, 0, 0);
-        si.p = add(add(smul(u0, T.v1), smul(u1, T.v2)), smul(w, T.v0));
+        si.p = V(lerp3f(u0, T.v1.x, u1, T.v2.x, w, T.v0.x), lerp3f(u0, T.v1.y, u1, T.v2.y, w, T.v0.y),
+                 lerp3f(u0, T.v1.z, u1, T.v2.z, w, T.v0.z));
         const float* uvs = S->s->uvs;
-        si.uv[0] = u0 * uvs[2 * T.i1] + u1 * uvs[2 * T.i2] + w * uvs[2 * T.i0];
-        si.uv[1] = u0 * uvs[2 * T.i1 + 1] + u1 * uvs[2 * T.i2 + 1] + w * uvs[2 * T.i0 + 1];
+        si.uv[0] = lerp3f(u0, uvs[2 * T.i1], u1, uvs[2 * T.i2], w, uvs[2 * T.i0]);
+        si.uv[1] = lerp3f(u0, uvs[2 * T.i1 + 1], u1, uvs[2 * T.i2 + 1], w, uvs[2 * T.i0 + 1]);
         si.n = n;
     }
     return si;
 }
 static float shape_pdf(const scene_t* S, const pt_prim* p, const si_t* si, const ray_t* r) {
     v3 to = sub(si->p, r->o);
-    float d2 = dot(to, to);
+    /* Shape::PDF's dot(to, to) compiles with the x product fused and the y
+     * product rounded (fixture search) */
+    float d2 = fmaf(to.z, to.z, fmaf(to.x, to.x, rmul(to.y, to.y)));
     float lc = fabsf(dot(neg(r->d), si->n));
     float area = shape_area(S, p);
     if (p->kind == PT_PRIM_QUAD) {
@@ -1027,8 +1037,10 @@ static float shape_pdf(const scene_t* S, const pt_prim* p, const si_t* si, const
     return d2 / (lc * area);
 }
 static v3 sky_le(const pt_light* l, v3 d) {
-    float a = 0.5f * (d.y + 1.0f);
-    return smul(l->scale, add(smul(1.0f - a, vl(l->color)), smul(a, vl(l->vec))));
+    /* (1-a)*c0 rounded, a*c1 fused (fixture search) */
+    float a = 0.5f * (d.y + 1.0f), b = 1.0f - a;
+    return smul(l->scale, V(fmaf(a, l->vec[0], rmul(b, l->color[0])), fmaf(a, l->vec[1], rmul(b, l->color[1])),
+                            fmaf(a, l->vec[2], rmul(b, l->color[2]))));
 }
 static v3 inf_le(const pt_light* l, v3 d) { return l->kind == PT_LIGHT_SKY_INF ? sky_le(l, d) : vl(l->color); }
 
@@ -1049,7 +1061,7 @@ static lsample_t light_sample(const scene_t* S, const pt_light* l, float u0, flo
     }
     float z = 2.0f * u0 - 1.0f;
     float th = 2.0f * PI_F * u1;
-    float r = sqrtf(1.0f - z * z);
+    float r = sqrtf(1.0f - rmul(z, z));  /* not fused here (fixture search) */
     float x = r * cosf(th), y = r * sinf(th);
     v3 d = V(x, y, z);
     if (l->kind == PT_LIGHT_DISTANT) {
@@ -1156,8 +1168,22 @@ static int intersect_counted(const integ_t* I, const ray_t* r, si_t* si) {
     return h;
 }
 
+/* debugging aid: ORACLE_DEBUG_KEY=<stream key> prints that path's bounces */
+static uint32_t dbg_key(void) {
+    static int init = 0;
+    static uint32_t k = 0;
+    if (!init) {
+        const char* e = getenv("ORACLE_DEBUG_KEY");
+        k = e ? (uint32_t)strtoul(e, NULL, 0) : 0;
+        init = 1;
+    }
+    return k;
+}
+#define DBG(...) do { if (dbgon) fprintf(stderr, __VA_ARGS__); } while (0)
+
 /* PathIntegrator::Li (Integrators.cpp:182-257) */
 static v3 li_path(const integ_t* I, ray_t ray, rng_t* rng) {
+    const int dbgon = dbg_key() != 0 && rng->key == dbg_key();
     const scene_t* S = I->S;
     v3 att = V(1, 1, 1), out = V(0, 0, 0);
     uint32_t depth = 0, rr = 0;
@@ -1167,6 +1193,7 @@ static v3 li_path(const integ_t* I, ray_t ray, rng_t* rng) {
         si_t si;
         memset(&si, 0, sizeof(si));
         if (!intersect_counted(I, &ray, &si)) {
+            DBG("O d%u miss\n", depth);
             for (uint32_t k = 0; k < S->s->n_infinite_lights; k++) {
                 const pt_light* l = &S->s->lights[S->s->infinite_lights[k]];
                 if (spec) {
@@ -1181,6 +1208,9 @@ static v3 li_path(const integ_t* I, ray_t ray, rng_t* rng) {
         }
         float r[8];
         for (int k = 0; k < 8; k++) r[k] = next1(rng);
+        DBG("O d%u prim %d t %a p %a %a %a ns %a %a %a uv %a %a mat %d light %d out %a %a %a att %a %a %a\n", depth,
+            si.prim, si.t, si.p.x, si.p.y, si.p.z, si.ns.x, si.ns.y, si.ns.z, si.uv[0], si.uv[1], si.mat, si.light,
+            out.x, out.y, out.z, att.x, att.y, att.z);
         if (si.light >= 0) {
             const pt_light* al = &S->s->lights[si.light];
             v3 L = light_L(S, al, &si, &ray);
@@ -1204,9 +1234,12 @@ static v3 li_path(const integ_t* I, ray_t ray, rng_t* rng) {
         ray_t nr = mkray(b.o, b.d);
         spec = (b.flags & FL_SPEC) != 0;
         if (!spec) {
-            out = add(out, mul(att, sample_ld(I, &ray, &si, r[5], r[2], r[3])));
+            v3 ld = sample_ld(I, &ray, &si, r[5], r[2], r[3]);
+            DBG("O  ld %a %a %a (light %d)\n", ld.x, ld.y, ld.z, ls_sample(S, r[5]));
+            out = add(out, mul(att, ld));
             prev = mat_pdf(S, si.mat, &ray, &si, nr.d);
         }
+        DBG("O  scatter d %a %a %a f %a %a %a pdf %a prev %a\n", b.d.x, b.d.y, b.d.z, b.f.x, b.f.y, b.f.z, b.pdf, prev);
         att = mul(att, divs(muls(b.f, fabsf(dot(si.ns, nr.d))), b.pdf));
         if (rr++ > 3) {
             float q = fminf(0.95f, fmaxf(fmaxf(att.x, att.y), att.z));
@@ -1260,16 +1293,18 @@ static v3 li_simple(const integ_t* I, ray_t ray, rng_t* rng) {
 
 /* Camera::GenerateRay (Camera.hpp:21-35) + camera draws (Integrators.cpp:61-64) */
 static ray_t camera_ray(const pt_camera_desc* c, uint32_t x, uint32_t y, rng_t* rng, double* px, double* py) {
-    float a = next1(rng), b = next1(rng);
+    float ja = next1(rng), jb = next1(rng);
     (void)next1(rng); /* time */
     float l0 = next1(rng), l1 = next1(rng);
-    *px = (double)x + (double)a;
-    *py = (double)y + (double)b;
+    *px = (double)x + (double)ja;
+    *py = (double)y + (double)jb;
     float pxf = (float)*px, pyf = (float)*py;
     float uc = pxf / (float)c->width;
     float vc = pyf / (float)c->height;
-    v3 dir = normalize(add(add(neg(vl(c->w)), smul((2.0f * uc - 1.0f) * c->half_width, vl(c->u))),
-                           smul((2.0f * vc - 1.0f) * c->half_height, vl(c->v))));
+    /* fma(b, v, fma(a, u, -w)) as the reference build contracts it (fixture search) */
+    float a = (2.0f * uc - 1.0f) * c->half_width, b = (2.0f * vc - 1.0f) * c->half_height;
+    v3 dir = normalize(V(fmaf(b, c->v[0], fmaf(a, c->u[0], -c->w[0])), fmaf(b, c->v[1], fmaf(a, c->u[1], -c->w[1])),
+                         fmaf(b, c->v[2], fmaf(a, c->u[2], -c->w[2]))));
     if (c->focus_distance == 0 || c->focus_angle == 0) return mkray(vl(c->origin), dir);
     float r = sqrtf(l0);
     float th = 2 * PI_F * l1;

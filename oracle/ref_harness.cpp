@@ -541,6 +541,21 @@ static void cmd_bsdf(World& w, const std::string& out, const std::string& inPath
     wr(out + ".bsdf" + std::to_string(matId) + ".bin", res);
 }
 
+// --- camera: Camera::GenerateRay (Camera.hpp:21-35) for [n][4] {px, py, lens u, v}
+static void cmd_camera(World& w, const std::string& out, const std::string& inPath) {
+    auto raw = rd<float>(inPath);
+    size_t n = raw.size() / 4;
+    std::vector<float> res(n * 6);
+    for (size_t i = 0; i < n; i++) {
+        const float* c = &raw[i * 4];
+        Ray r = w.camera->GenerateRay(glm::vec2(c[0], c[1]), 0.0f, glm::vec2(c[2], c[3]));
+        float* o = &res[i * 6];
+        o[0] = r.origin.x; o[1] = r.origin.y; o[2] = r.origin.z;
+        o[3] = r.dir.x; o[4] = r.dir.y; o[5] = r.dir.z;
+    }
+    wr(out + ".camera.bin", res);
+}
+
 // --- lights: for each light in sampler-input order and each uv: sample + PDF + L
 struct LightOut { float L[3], p[3], n[3], uv[2], dir[3], pdf, Lsh[3]; };
 static void cmd_lights(World& w, const std::string& out, const std::string& inPath) {
@@ -638,6 +653,7 @@ int main(int argc, char** argv) {
         cmd_li(w, out, x0, y0, x1, y1, spp);
     } else if (cmd == "film") cmd_film(w, out, w.spp);
     else if (cmd == "bsdf") cmd_bsdf(w, out, argv[4], atoi(argv[5]));
+    else if (cmd == "camera") cmd_camera(w, out, argv[4]);
     else if (cmd == "lights") cmd_lights(w, out, argv[4]);
     else if (cmd == "time") cmd_time(w, atoi(argv[4]), (unsigned)atoi(argv[5]), argc > 6 ? argv[6] : "render");
     else { fprintf(stderr, "unknown cmd %s\n", cmd.c_str()); return 2; }

@@ -87,12 +87,20 @@ __device__ __forceinline__ f3 operator-(f3 a) { return F3(-a.x, -a.y, -a.z); }
 // disassembly; DESIGN.md "Numerics"): fma() fuses, rmul() is a product that
 // must stay rounded.  The oracle (oracle/pt_oracle.c) uses the same forms.
 __device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
-__device__ __forceinline__ float rmul(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ float rmul(float a, float b) {
+    float m = a * b;
+    __asm__ volatile("" : "+v"(m));  // opaque to contraction: stays a rounded product
+    return m;
+}
 // glm::dot: x product rounded, then fma(y), fma(z)
 __device__ __forceinline__ float dot(f3 a, f3 b) { return fma_(a.z, b.z, fma_(a.y, b.y, rmul(a.x, b.x))); }
 // glm::cross in scalar code: first product fused, second rounded
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {
     return F3(fma_(a.y, b.z, -rmul(b.y, a.z)), fma_(a.z, b.x, -rmul(b.z, a.x)), fma_(a.x, b.y, -rmul(b.x, a.y)));
+}
+// every lane first product rounded, second fused (QuadShape::Area)
+__device__ __forceinline__ f3 cross_r(f3 a, f3 b) {
+    return F3(fma_(-b.y, a.z, rmul(a.y, b.z)), fma_(-b.z, a.x, rmul(a.z, b.x)), fma_(-b.x, a.y, rmul(a.x, b.y)));
 }
 // glm::cross where the reference build vectorises x, y (first product rounded,
 // second fused) and keeps z scalar (first fused): triangle normals, onb(si)
@@ -104,6 +112,16 @@ __device__ __forceinline__ float lerp3f(float u, float a, float v, float b, floa
     return fma_(w, c, fma_(v, b, rmul(u, a)));
 }
 __device__ __forceinline__ float csqrt(float x) { return __builtin_sqrtf(x); }
+// sinf / cosf: the host libm's algorithm, bit-identical (pt_sincosf.h)
+#define PT_SC_FN __device__ __forceinline__ static
+#define PT_SC_FMA __builtin_fma
+#include "pt_sincosf.h"
+__constant__ const double pt_sc_table[2][14] = PT_SC_TABLE;
+__device__ __forceinline__ float cos_cr(float x) { return pt_cosf_t(x, pt_sc_table); }
+__device__ __forceinline__ float sin_cr(float x) { return pt_sinf_t(x, pt_sc_table); }
+// powf: evaluated in double and rounded once (glibc's powf is within 0.82 ulp,
+// so a few results differ from it by one ulp)
+__device__ __forceinline__ float pow_cr(float x, float y) { return (float)pow((double)x, (double)y); }
 __device__ __forceinline__ float length(f3 a) { return csqrt(dot(a, a)); }
 __device__ __forceinline__ f3 normalize(f3 a) { return a * (1.0f / csqrt(dot(a, a))); }
 __device__ __forceinline__ bool is_zero(f3 a) { return a.x == 0.0f && a.y == 0.0f && a.z == 0.0f; }

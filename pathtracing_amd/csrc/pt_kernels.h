@@ -72,5 +72,8 @@ __global__ void k_finish(RenderParams R, const float4* done_L, const uint32_t* d
                          uint32_t n_direct, PathSoA next, uint32_t* cnt, unsigned long long* next_sample,
                          float* sample_L);
 __global__ void k_gather(RenderParams R, const float* sample_L, double* film);
+__global__ void k_interact(DevScene S, const pt_ray* rays, uint32_t n, float* out);
+__global__ void k_bsdf_cases(DevScene S, int mid, const float* in, uint32_t n, float* out);
+__global__ void k_light_cases(DevScene S, const float* in, uint32_t n, float* out);
 __global__ void k_trace_rays(DevScene S, const pt_ray* rays, uint32_t n, int any, pt_hit* out,
                              unsigned long long* counters);

@@ -130,6 +130,96 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(DevScene S, const
     count_add(counters, any ? CNT_TRIS_ANY : CNT_TRIS_CLOSEST, wk.tris);
 }
 
+// Test hook: closest hit + the full SurfaceInteraction the shade kernel
+// reconstructs (pt_interact): {hit, t, p, n, ns, uv, tangent} per ray, the
+// layout of the reference harness's trace records.
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_interact(DevScene S, const pt_ray* __restrict__ rays, uint32_t n,
+                                                            float* __restrict__ out) {
+    __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+    const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
+    TraceWork wk{0, 0};
+    if (i >= n) return;
+    const pt_ray r = rays[i];
+    f3 o = F3(r.o[0], r.o[1], r.o[2]), d = F3(r.d[0], r.d[1], r.d[2]);
+    float t, b1, b2;
+    const int prim = trace_closest<false>(S, o, d, r.tmax, t, b1, b2, s_ref, wk);
+    float* w = out + 16ull * i;
+    for (int k = 0; k < 16; k++) w[k] = 0.0f;
+    if (prim < 0) return;
+    const DevGeom g = S.geom[prim];
+    const DevPrimInfo pi = S.info[prim];
+    const uint32_t kind = __float_as_uint(g.a.w) & GF_KIND;
+    SurfInt si;
+    if (kind == PT_PRIM_TRIANGLE) tri_interaction(S, g, pi.index, pi.material, o, d, t, b1, b2, si);
+    else if (kind == PT_PRIM_QUAD) quad_interaction(S.quads[pi.index], o, d, t, b1, b2, si);
+    else sphere_interaction(S.spheres[pi.index], o, d, t, si);
+    const float rec[16] = {1.0f, si.t, si.p.x, si.p.y, si.p.z, si.n.x, si.n.y, si.n.z, si.ns.x, si.ns.y, si.ns.z,
+                           si.u, si.v, si.tangent.x, si.tangent.y, si.tangent.z};
+    for (int k = 0; k < 16; k++) w[k] = rec[k];
+}
+
+// Test hook: Material::scatter / calc_attenuation / PDF on given
+// interactions (pt_bsdf_cases); case and record layout of oracle_bsdf.
+__global__ void k_bsdf_cases(DevScene S, int mid, const float* __restrict__ in, uint32_t n, float* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* c = in + 27ull * i;
+    float* o = out + 20ull * i;
+    for (int k = 0; k < 20; k++) o[k] = 0.0f;
+    const f3 ro = F3(c[0], c[1], c[2]), rd = F3(c[3], c[4], c[5]);
+    SurfInt si;
+    si.p = F3(c[6], c[7], c[8]);
+    si.n = F3(c[9], c[10], c[11]);
+    si.ns = F3(c[12], c[13], c[14]);
+    si.tangent = F3(c[15], c[16], c[17]);
+    si.u = c[18];
+    si.v = c[19];
+    si.t = c[20];
+    si.mat = mid;
+    si.light = -1;
+    const Bxdf b = mat_scatter(S, mid, ro, rd, si, c[21], c[22], c[23]);
+    if (b.ok) {
+        o[0] = 1.0f;
+        o[1] = b.f.x; o[2] = b.f.y; o[3] = b.f.z;
+        o[4] = b.pdf;
+        o[5] = (float)b.flags;
+        o[6] = b.o.x; o[7] = b.o.y; o[8] = b.o.z;
+        o[9] = b.d.x; o[10] = b.d.y; o[11] = b.d.z;
+        const f3 a = mat_f(S, mid, rd, si, b.d);
+        o[12] = a.x; o[13] = a.y; o[14] = a.z;
+        o[15] = mat_pdf(S, mid, rd, si, b.d);
+    }
+    const f3 other = F3(c[24], c[25], c[26]);
+    const f3 a2 = mat_f(S, mid, rd, si, other);
+    o[16] = a2.x; o[17] = a2.y; o[18] = a2.z;
+    o[19] = mat_pdf(S, mid, rd, si, other);
+}
+
+// Test hook: Light::sample / PDF / L per light x case (pt_light_cases);
+// case {uv[2], ref point[3]}, record layout of oracle_lights.
+__global__ void k_light_cases(DevScene S, const float* __restrict__ in, uint32_t n, float* __restrict__ out) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n * S.n_lights) return;
+    const uint32_t li = k / n, i = k % n;
+    const pt_light& l = S.lights[li];
+    const float* c = in + 5ull * i;
+    float* o = out + 18ull * k;
+    for (int j = 0; j < 18; j++) o[j] = 0.0f;
+    const LSample ls = light_sample(S, l, c[0], c[1]);
+    o[0] = ls.L.x; o[1] = ls.L.y; o[2] = ls.L.z;
+    o[3] = ls.p.x; o[4] = ls.p.y; o[5] = ls.p.z;
+    o[6] = ls.n.x; o[7] = ls.n.y; o[8] = ls.n.z;
+    o[9] = ls.u; o[10] = ls.v;
+    o[11] = ls.dir.x; o[12] = ls.dir.y; o[13] = ls.dir.z;
+    if (!is_zero(ls.n)) {
+        const f3 ref = F3(c[2], c[3], c[4]);
+        const f3 rd = normalize(ls.p - ref);
+        o[14] = light_pdf(S, l, ls.p, ls.n, ref, rd);
+        const f3 L = light_L(S, l, ls.n, ls.u, ls.v, rd);
+        o[15] = L.x; o[16] = L.y; o[17] = L.z;
+    }
+}
+
 // ------------------------------------------------------------------ camera / regeneration
 __device__ __forceinline__ void work_pixel(const RenderParams& R, uint32_t pix_i, uint32_t& x, uint32_t& y) {
     if (R.tiled) {  // 8x8 pixel tiles, tile-major: neighbouring lanes -> neighbouring pixels
@@ -152,7 +242,10 @@ __device__ __forceinline__ void camera_ray(const pt_camera_desc& c, uint32_t key
     float uc = pxf / (float)c.width;
     float vc = pyf / (float)c.height;
     f3 U = F3(c.u[0], c.u[1], c.u[2]), Vv = F3(c.v[0], c.v[1], c.v[2]), W = F3(c.w[0], c.w[1], c.w[2]);
-    f3 dir = normalize((-W + ((2.0f * uc - 1.0f) * c.half_width) * U) + ((2.0f * vc - 1.0f) * c.half_height) * Vv);
+    // fma(b, v, fma(a, u, -w)) as the reference build contracts it (fixture search)
+    const float ca = (2.0f * uc - 1.0f) * c.half_width, cb = (2.0f * vc - 1.0f) * c.half_height;
+    f3 dir = normalize(F3(fma_(cb, Vv.x, fma_(ca, U.x, -W.x)), fma_(cb, Vv.y, fma_(ca, U.y, -W.y)),
+                          fma_(cb, Vv.z, fma_(ca, U.z, -W.z))));
     f3 org = F3(c.origin[0], c.origin[1], c.origin[2]);
     if (c.focus_distance == 0 || c.focus_angle == 0) {
         o = org;
@@ -162,7 +255,7 @@ __device__ __forceinline__ void camera_ray(const pt_camera_desc& c, uint32_t key
     float l0 = draw(key, 3), l1 = draw(key, 4);
     float r = csqrt(l0);
     float th = 2 * PT_PI * l1;
-    float lx = r * cosf(th), ly = r * sinf(th);
+    float lx = r * cos_cr(th), ly = r * sin_cr(th);
     f3 du = c.defocus_radius * U, dv = c.defocus_radius * Vv;
     dir = dir * c.focus_distance;
     f3 off = lx * du + ly * dv;
@@ -293,6 +386,12 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, RenderParams R, PathS
             else sphere_interaction(S.spheres[pi.index], ro, rd, h.x, si);
             si.mat = pi.material;
             si.light = pi.light;
+#ifdef PT_DEBUG_KEY
+            if (key == PT_DEBUG_KEY)
+                printf("G d%u prim %d t %a p %a %a %a ns %a %a %a uv %a %a mat %d light %d out %a %a %a att %a %a %a\n",
+                       depth, prim, si.t, si.p.x, si.p.y, si.p.z, si.ns.x, si.ns.y, si.ns.z, si.u, si.v, si.mat,
+                       si.light, out.x, out.y, out.z, att.x, att.y, att.z);
+#endif
             // emission (Integrators.cpp:151-154, 217-226)
             if (si.light >= 0) {
                 const pt_light& al = S.lights[si.light];
@@ -367,8 +466,18 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, RenderParams R, PathS
                                 }
                             }
                             prev = mat_pdf(S, si.mat, rd, si, b.d);
+#ifdef PT_DEBUG_KEY
+                            if (key == PT_DEBUG_KEY)
+                                printf("G  nee c %a %a %a (light %d) shadow %d\n", srec.c.x, srec.c.y, srec.c.z, li,
+                                       (int)shadow);
+#endif
                         }
                     }
+#ifdef PT_DEBUG_KEY
+                    if (key == PT_DEBUG_KEY)
+                        printf("G  scatter d %a %a %a f %a %a %a pdf %a prev %a\n", b.d.x, b.d.y, b.d.z, b.f.x, b.f.y,
+                               b.f.z, b.pdf, prev);
+#endif
                     att = att * ((b.f * fabsf(dot(si.ns, b.d))) / b.pdf);
                     const float urr = INTEGRATOR == PT_INTEGRATOR_PATH ? r[6] : r[3];
                     if (rr++ > 3) {

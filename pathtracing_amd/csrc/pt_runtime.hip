@@ -27,6 +27,7 @@ struct pt_ctx {
     uint64_t scene_bytes = 0;
     DevScene scene{};
     bool has_scene = false;
+    uint32_t n_materials = 0;
     // wavefront buffers: two compacted path states (ping-pong), per-bounce hits,
     // the finished-path list and the shadow-ray queue
     uint32_t cap = 0;
@@ -399,6 +400,7 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
     S.sampler_total = acc;
     S.n_infinite_lights = s->n_infinite_lights;
     c->has_scene = true;
+    c->n_materials = s->n_materials;
     return PT_OK;
 }
 
@@ -753,4 +755,68 @@ extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any
     }
     for (void* p : tmp) hipFree(p);
     return PT_OK;
+}
+
+// Copies n*in_stride floats/records to the device, runs `launch`, copies
+// n*out_stride floats back (test hooks; host pointers).
+template <class L>
+static pt_status run_hook(pt_ctx* c, const void* in, size_t in_bytes, float* out, size_t out_bytes, L launch) {
+    void* din = nullptr;
+    float* dout = nullptr;
+    if (hipMalloc(&din, in_bytes ? in_bytes : 1) != hipSuccess) return fail(c, PT_ERR_OOM, "hook input");
+    if (hipMalloc((void**)&dout, out_bytes ? out_bytes : 4) != hipSuccess) {
+        hipFree(din);
+        return fail(c, PT_ERR_OOM, "hook output");
+    }
+    pt_status st = PT_OK;
+    if (hipMemcpyAsync(din, in, in_bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) st = PT_ERR_HIP;
+    if (st == PT_OK) {
+        launch(din, dout);
+        if (hipGetLastError() != hipSuccess) st = PT_ERR_HIP;
+    }
+    if (st == PT_OK && hipMemcpyAsync(out, dout, out_bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        st = PT_ERR_HIP;
+    if (st == PT_OK && hipStreamSynchronize(c->stream) != hipSuccess) st = PT_ERR_HIP;
+    hipFree(din);
+    hipFree(dout);
+    return st == PT_OK ? PT_OK : fail(c, st, "hook kernel failed");
+}
+
+extern "C" pt_status pt_interact(pt_ctx* c, const pt_ray* rays, uint32_t n, float* out) {
+    if (!c || (n && (!rays || !out))) return PT_ERR_ARG;
+    if (!c->has_scene) return fail(c, PT_ERR_STATE, "no scene uploaded");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (n == 0) return PT_OK;
+    return run_hook(c, rays, (size_t)n * sizeof(pt_ray), out, (size_t)n * 16 * sizeof(float),
+                    [&](void* din, float* dout) {
+                        hipLaunchKernelGGL(k_interact, dim3((n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK),
+                                           dim3(PT_TRACE_BLOCK), 0, c->stream, c->scene, (const pt_ray*)din, n, dout);
+                    });
+}
+
+extern "C" pt_status pt_bsdf_cases(pt_ctx* c, int32_t material, const float* cases, uint32_t n, float* out) {
+    if (!c || (n && (!cases || !out))) return PT_ERR_ARG;
+    if (!c->has_scene) return fail(c, PT_ERR_STATE, "no scene uploaded");
+    if (material < 0 || (uint32_t)material >= c->n_materials) return fail(c, PT_ERR_ARG, "bad material id");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (n == 0) return PT_OK;
+    return run_hook(c, cases, (size_t)n * 27 * sizeof(float), out, (size_t)n * 20 * sizeof(float),
+                    [&](void* din, float* dout) {
+                        hipLaunchKernelGGL(k_bsdf_cases, dim3((n + 127) / 128), dim3(128), 0, c->stream, c->scene,
+                                           (int)material, (const float*)din, n, dout);
+                    });
+}
+
+extern "C" pt_status pt_light_cases(pt_ctx* c, const float* cases, uint32_t n, float* out) {
+    if (!c || (n && (!cases || !out))) return PT_ERR_ARG;
+    if (!c->has_scene) return fail(c, PT_ERR_STATE, "no scene uploaded");
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t total = (uint64_t)n * c->scene.n_lights;
+    if (total == 0) return PT_OK;
+    if (total > 0xFFFFFFFFull) return fail(c, PT_ERR_ARG, "too many light cases");
+    return run_hook(c, cases, (size_t)n * 5 * sizeof(float), out, (size_t)total * 18 * sizeof(float),
+                    [&](void* din, float* dout) {
+                        hipLaunchKernelGGL(k_light_cases, dim3((uint32_t)((total + 127) / 128)), dim3(128), 0,
+                                           c->stream, c->scene, (const float*)din, n, dout);
+                    });
 }

@@ -192,8 +192,11 @@ __device__ void tri_interaction(const DevScene& S, const DevGeom& g, uint32_t tr
               fma_(rmul(PT_EPS, N.z), sg, fma_(t, d.z, o.z)));
     if (T.w & 1u) {
         const float* tg = S.tangents;
-        f3 tv = u * ld3(tg + 3 * T.y) + v * ld3(tg + 3 * T.z) + w * ld3(tg + 3 * T.x);
-        si.tangent = normalize(tv - si.ns * dot(si.ns, tv));
+        const float *t1 = tg + 3 * T.y, *t2 = tg + 3 * T.z, *t0 = tg + 3 * T.x;
+        f3 tv = F3(lerp3f(u, t1[0], v, t2[0], w, t0[0]), lerp3f(u, t1[1], v, t2[1], w, t0[1]),
+                   lerp3f(u, t1[2], v, t2[2], w, t0[2]));
+        float k = dot(si.ns, tv);  // tangent - ns*k fused (fixture search)
+        si.tangent = normalize(F3(fma_(-si.ns.x, k, tv.x), fma_(-si.ns.y, k, tv.y), fma_(-si.ns.z, k, tv.z)));
     } else {
         f3 up = (fabsf(si.ns.x) > 0.9999f) ? F3(0, 1, 0) : F3(1, 0, 0);
         si.tangent = normalize(cross(up, si.ns));
@@ -212,17 +215,19 @@ __device__ void quad_interaction(const pt_quad& q, f3 o, f3 d, float t, float a,
     si.n = normal;
     f3 up = (fabsf(si.ns.x) > 0.9999f) ? F3(0, 1, 0) : F3(1, 0, 0);
     si.tangent = normalize(cross(up, si.ns));
-    si.p = (o + t * d) + PT_EPS * nn;
+    const f3 at = F3(fma_(t, d.x, o.x), fma_(t, d.y, o.y), fma_(t, d.z, o.z));  // ray.at: fused (fixture search)
+    si.p = at + PT_EPS * nn;
 }
 
 // SphereShape::Intersect (Shape.cpp:3-37) interaction part.
 __device__ void sphere_interaction(const pt_sphere& sp, f3 o, f3 d, float t, SurfInt& si) {
     si.t = t;
-    si.ns = normalize((o + t * d) - ld3(sp.center));
+    const f3 at = F3(fma_(t, d.x, o.x), fma_(t, d.y, o.y), fma_(t, d.z, o.z));  // ray.at: fused (fixture search)
+    si.ns = normalize(at - ld3(sp.center));
     si.n = si.ns;
     f3 up = (fabsf(si.ns.x) > 0.9999f) ? F3(0, 1, 0) : F3(1, 0, 0);
     si.tangent = normalize(cross(up, si.ns));
-    si.p = (o + t * d) + PT_EPS * si.n;
+    si.p = at + PT_EPS * si.n;
     sphere_uv(si.n, si.u, si.v);
 }
 
@@ -267,8 +272,8 @@ __device__ f3 vndf_(float ax, float ay, f3 Ve, float U1, float U2) {
     f3 T2 = cross(Vh, T1);
     float r = csqrt(U1);
     float phi = 2.0f * PT_PI * U2;
-    float t1 = r * cosf(phi);
-    float t2 = r * sinf(phi);
+    float t1 = r * cos_cr(phi);
+    float t2 = r * sin_cr(phi);
     float s = 0.5f * (1.0f + Vh.z);
     t2 = (1.0f - s) * csqrt(1.0f - t1 * t1) + s * t2;
     f3 Nh = t1 * T1 + t2 * T2 + csqrt(smax(0.0f, 1.0f - t1 * t1 - t2 * t2)) * Vh;
@@ -294,7 +299,7 @@ __device__ float fresnel_dielectric(float cosi, float eta) {  // Material.hpp:11
     return (rpa * rpa + rpe * rpe) / 2;
 }
 __device__ __forceinline__ f3 schlick(float c, f3 F0) {  // Material.hpp:30-32
-    float p = powf(1.0f - c, 5.0f);
+    float p = pow_cr(1.0f - c, 5.0f);
     return F0 + (F3(1, 1, 1) - F0) * p;
 }
 
@@ -331,7 +336,7 @@ __device__ Bxdf diffuse_scatter(const DevScene& S, const pt_material& m, f3 ind,
         float z = csqrt(1.0f - uv1);
         float phi = 2.0f * PT_PI * uv0;
         float s2 = csqrt(uv1);
-        wi = F3(cosf(phi) * s2, sinf(phi) * s2, z);
+        wi = F3(cos_cr(phi) * s2, sin_cr(phi) * s2, z);
         wh = normalize(wo + wi);
     }
     if (wi.z <= 0) return b;
@@ -575,7 +580,7 @@ __device__ __forceinline__ uint4 tri_idx(const DevScene& S, uint32_t tri) { retu
 __device__ float shape_area(const DevScene& S, uint32_t kind, uint32_t index) {
     if (kind == PT_PRIM_QUAD) {
         const pt_quad& q = S.quads[index];
-        return length(cross(ld3(q.u), ld3(q.v)));
+        return length(cross_r(ld3(q.u), ld3(q.v)));  // QuadShape::Area as compiled (fixture search)
     }
     if (kind == PT_PRIM_SPHERE) {
         float r = S.spheres[index].radius;
@@ -596,11 +601,11 @@ __device__ void shape_sample(const DevScene& S, uint32_t kind, uint32_t index, f
     } else if (kind == PT_PRIM_SPHERE) {
         const pt_sphere& sp = S.spheres[index];
         float z = 1.0f - 2.0f * u0;
-        float r = csqrt(1.0f - z * z);
+        float r = csqrt(fma_(-z, z, 1.0f));
         float phi = 2.0f * PT_PI * u1;
-        f3 d = F3(r * cosf(phi), r * sinf(phi), z);
+        f3 d = F3(r * cos_cr(phi), r * sin_cr(phi), z);
         f3 c = ld3(sp.center);
-        ls.p = c + sp.radius * d;
+        ls.p = F3(fma_(sp.radius, d.x, c.x), fma_(sp.radius, d.y, c.y), fma_(sp.radius, d.z, c.z));
         ls.n = normalize(ls.p - c);
         sphere_uv(ls.p, ls.u, ls.v);
     } else {
@@ -609,17 +614,19 @@ __device__ void shape_sample(const DevScene& S, uint32_t kind, uint32_t index, f
         f3 v0 = ld3(S.positions + 3 * T.x), v1 = ld3(S.positions + 3 * T.y), v2 = ld3(S.positions + 3 * T.z);
         f3 n = normalize(cross(v1 - v0, v2 - v0));
         if (n.x != n.x) n = F3(0, 0, 0);
-        ls.p = u0 * v1 + u1 * v2 + w * v0;
+        ls.p = F3(lerp3f(u0, v1.x, u1, v2.x, w, v0.x), lerp3f(u0, v1.y, u1, v2.y, w, v0.y),
+                  lerp3f(u0, v1.z, u1, v2.z, w, v0.z));
         const float* uvs = S.uvs;
-        ls.u = u0 * uvs[2 * T.y] + u1 * uvs[2 * T.z] + w * uvs[2 * T.x];
-        ls.v = u0 * uvs[2 * T.y + 1] + u1 * uvs[2 * T.z + 1] + w * uvs[2 * T.x + 1];
+        ls.u = lerp3f(u0, uvs[2 * T.y], u1, uvs[2 * T.z], w, uvs[2 * T.x]);
+        ls.v = lerp3f(u0, uvs[2 * T.y + 1], u1, uvs[2 * T.z + 1], w, uvs[2 * T.x + 1]);
         ls.n = n;
     }
 }
 // Shape::PDF(interaction, ray) (Shape.cpp:61-67, 303-315; Shape.hpp:151-158)
 __device__ float shape_pdf(const DevScene& S, uint32_t kind, uint32_t index, f3 p, f3 n, f3 ro, f3 rd) {
     f3 to = p - ro;
-    float d2 = dot(to, to);
+    // Shape::PDF's dot(to, to): x product fused, y rounded (fixture search)
+    float d2 = fma_(to.z, to.z, fma_(to.x, to.x, rmul(to.y, to.y)));
     float lc = fabsf(dot(-rd, n));
     float area = shape_area(S, kind, index);
     if (kind == PT_PRIM_QUAD) {
@@ -633,8 +640,10 @@ __device__ float shape_pdf(const DevScene& S, uint32_t kind, uint32_t index, f3 
 }
 __device__ __forceinline__ f3 inf_le(const pt_light& l, f3 d) {
     if (l.kind == PT_LIGHT_SKY_INF) {  // main.cpp:292-295 gradient
-        float a = 0.5f * (d.y + 1.0f);
-        return l.scale * ((1.0f - a) * ld3(l.color) + a * ld3(l.vec));
+        // (1-a)*c0 rounded, a*c1 fused (fixture search)
+        float a = 0.5f * (d.y + 1.0f), b = 1.0f - a;
+        return l.scale * F3(fma_(a, l.vec[0], rmul(b, l.color[0])), fma_(a, l.vec[1], rmul(b, l.color[1])),
+                            fma_(a, l.vec[2], rmul(b, l.color[2])));
     }
     return ld3(l.color);
 }
@@ -661,8 +670,8 @@ __device__ LSample light_sample(const DevScene& S, const pt_light& l, float u0, 
     }
     float z = 2.0f * u0 - 1.0f;
     float th = 2.0f * PT_PI * u1;
-    float r = csqrt(1.0f - z * z);
-    f3 d = F3(r * cosf(th), r * sinf(th), z);
+    float r = csqrt(1.0f - rmul(z, z));  // not fused here (fixture search)
+    f3 d = F3(r * cos_cr(th), r * sin_cr(th), z);
     if (l.kind == PT_LIGHT_DISTANT) {  // Light.cpp:208-215
         ls.L = ld3(l.color);
         ls.u = u0;

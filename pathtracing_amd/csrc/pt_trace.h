@@ -111,8 +111,9 @@ __device__ __noinline__ bool tri_alpha(const DevScene& S, uint32_t slot, float b
     const DevPrimInfo pi = S.info[slot];
     uint4 T = S.tri[pi.index];
     float u = bu, v = bv, w = 1.0f - u - v;
-    float tu = u * S.uvs[2 * T.y] + v * S.uvs[2 * T.z] + w * S.uvs[2 * T.x];
-    float tv = u * S.uvs[2 * T.y + 1] + v * S.uvs[2 * T.z + 1] + w * S.uvs[2 * T.x + 1];
+    // the uv TriangleShape::Intersect computes (same contraction as tri_interaction)
+    float tu = lerp3f(u, S.uvs[2 * T.y], v, S.uvs[2 * T.z], w, S.uvs[2 * T.x]);
+    float tv = lerp3f(u, S.uvs[2 * T.y + 1], v, S.uvs[2 * T.z + 1], w, S.uvs[2 * T.x + 1]);
     return mat_alpha(S, pi.material, tu, tv, o, d, (int)slot);
 }
 

@@ -97,6 +97,30 @@ class Context:
         return hits, st.as_dict()
 
 
+    def interact(self, rays: np.ndarray) -> np.ndarray:
+        """Closest hit + reconstructed SurfaceInteraction per ray: (n, 16)
+        {hit, t, p, n, ns, uv, tangent} (test hook)."""
+        rays = np.ascontiguousarray(rays, dtype=N.RAY)
+        out = np.zeros((rays.shape[0], 16), np.float32)
+        N.check(self._lib.pt_interact(self.ptr, rays.ctypes.data, rays.shape[0], out.ctypes.data), self.ptr)
+        return out
+
+    def bsdf_cases(self, material: int, cases: np.ndarray) -> np.ndarray:
+        """Material scatter / f / pdf on (n, 27) cases -> (n, 20) (test hook)."""
+        cases = np.ascontiguousarray(cases, np.float32)
+        out = np.zeros((cases.shape[0], 20), np.float32)
+        N.check(self._lib.pt_bsdf_cases(self.ptr, int(material), cases.ctypes.data, cases.shape[0],
+                                        out.ctypes.data), self.ptr)
+        return out
+
+    def light_cases(self, cases: np.ndarray, n_lights: int) -> np.ndarray:
+        """Light sample / PDF / L for every light x case: (n_lights*n, 18) (test hook)."""
+        cases = np.ascontiguousarray(cases, np.float32)
+        out = np.zeros((n_lights * cases.shape[0], 18), np.float32)
+        N.check(self._lib.pt_light_cases(self.ptr, cases.ctypes.data, cases.shape[0], out.ctypes.data), self.ptr)
+        return out
+
+
 _contexts: dict[int, Context] = {}
 
 

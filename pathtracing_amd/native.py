@@ -13,7 +13,7 @@ from pathlib import Path
 import numpy as np
 
 LIB_DIR = Path(__file__).resolve().parent / "_lib"
-LIB_PATH = LIB_DIR / "libpt_hip.so"
+LIB_PATH = Path(os.environ["PT_HIP_LIB"]) if os.environ.get("PT_HIP_LIB") else LIB_DIR / "libpt_hip.so"  # override: debugging builds
 
 PT_OK = 0
 PT_PRIM_TRIANGLE, PT_PRIM_QUAD, PT_PRIM_SPHERE, PT_PRIM_BLAS = 0, 1, 2, 3
@@ -141,6 +141,12 @@ def lib():
     L.pt_render.restype = C.c_int32
     L.pt_trace.argtypes = [vp, vp, C.c_uint32, C.c_int, vp, C.POINTER(Stats)]
     L.pt_trace.restype = C.c_int32
+    L.pt_interact.argtypes = [vp, vp, C.c_uint32, vp]
+    L.pt_interact.restype = C.c_int32
+    L.pt_bsdf_cases.argtypes = [vp, C.c_int32, vp, C.c_uint32, vp]
+    L.pt_bsdf_cases.restype = C.c_int32
+    L.pt_light_cases.argtypes = [vp, vp, C.c_uint32, vp]
+    L.pt_light_cases.restype = C.c_int32
     L.pt_scene_device_bytes.argtypes = [vp]
     L.pt_scene_device_bytes.restype = C.c_uint64
     L.pt_bvh4_build.argtypes = [vp, C.c_uint32, vp, C.POINTER(C.c_uint32), C.POINTER(RefNode), vp, vp]

@@ -39,6 +39,32 @@ def _v3(x) -> np.ndarray:
     return a.astype(np.float32)
 
 
+def _fma32(a, b, c) -> np.float32:
+    """fmaf(a, b, c): the exact a*b + c rounded once to float32."""
+    from fractions import Fraction
+    exact = Fraction(float(a)) * Fraction(float(b)) + Fraction(float(c))
+    r = np.float32(float(exact))
+    best = r
+    for cand in (np.nextafter(r, np.float32(-np.inf)), np.nextafter(r, np.float32(np.inf))):
+        dc, db = abs(Fraction(float(cand)) - exact), abs(Fraction(float(best)) - exact)
+        if dc < db or (dc == db and (int(cand.view(np.uint32)) & 1) == 0):
+            best = cand
+    return np.float32(best)
+
+
+def _dot_c(a, b) -> np.float32:
+    """glm::dot as the reference build contracts it: x product rounded, then
+    fma(y), fma(z) (DESIGN.md "Numerics")."""
+    a = np.asarray(a, dtype=np.float32)
+    b = np.asarray(b, dtype=np.float32)
+    return _fma32(a[2], b[2], _fma32(a[1], b[1], f32(a[0] * b[0])))
+
+
+def _normalize_c(v) -> np.ndarray:
+    v = np.asarray(v, dtype=np.float32)
+    return (v * (f32(1.0) / f32(np.sqrt(_dot_c(v, v))))).astype(np.float32)
+
+
 def _normalize(v: np.ndarray) -> np.ndarray:
     """glm::normalize = v * (1 / sqrt(dot(v, v))) (glm/detail/func_geometric.inl:88)."""
     v = v.astype(np.float32)
@@ -686,9 +712,13 @@ class Camera:
         self.film = film
         self.FocusAngle = f32(FocusAngle)
         self.FocusDistance = f32(FocusDistance)
-        self.w = _normalize((self.lookFrom - self.lookAt).astype(np.float32))
-        self.u = _normalize(_cross(np.array([0, 1, 0], dtype=np.float32), self.w))
-        self.v = _cross(self.w, self.u)
+        # the ctor's arithmetic as the reference build contracts it (fixture
+        # search against Camera::GenerateRay): dot-pattern normalize, and
+        # v.y = fma(w.z, u.x, -(u.z*w.x)); the other products are by 0 or 1
+        w = _normalize_c((self.lookFrom - self.lookAt).astype(np.float32))
+        u = _normalize_c(np.array([w[2], 0.0, -w[0]], dtype=np.float32))  # cross((0,1,0), w)
+        v = np.array([f32(w[1] * u[2]), _fma32(w[2], u[0], -f32(u[2] * w[0])), -f32(u[0] * w[1])], np.float32)
+        self.w, self.u, self.v = w, u, v
         self.defocusRadius = f32(float(self.FocusDistance) * math.tan(float(self.FocusAngle) / 2.0))
         self.halfWidth = f32(math.tan(float(self.fov) * 0.5))
         W, H = film.Resolution()
