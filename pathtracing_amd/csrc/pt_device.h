@@ -70,6 +70,12 @@ struct DevScene {
     uint32_t n_infinite_lights;
 };
 
+// The uploaded scene of the current context, in constant memory: every
+// device function reads it directly (no per-lane copy of the struct, and the
+// array pointers come from scalar loads).  The runtime re-sends it before a
+// launch whenever another context last used the device (pt_runtime.hip).
+__constant__ DevScene S;
+
 // ------------------------------------------------------------------ float3 helpers
 struct f3 {
     float x, y, z;

@@ -61,19 +61,19 @@ struct RenderParams {
 };
 
 template <bool COUNT>
-__global__ void k_closest(DevScene S, PathSoA P, uint32_t n, float4* hit, unsigned long long* counters);
+__global__ void k_closest(PathSoA P, uint32_t n, float4* hit, unsigned long long* counters);
 template <bool COUNT>
-__global__ void k_shadow(DevScene S, PathSoA next, float4* done_L, const ShadowRec* sq, const uint32_t* nptr,
+__global__ void k_shadow(PathSoA next, float4* done_L, const ShadowRec* sq, const uint32_t* nptr,
                          unsigned long long* counters);
 template <int INTEGRATOR>
-__global__ void k_shade(DevScene S, RenderParams R, PathSoA cur, uint32_t n, const float4* hit, PathSoA next,
+__global__ void k_shade(RenderParams R, PathSoA cur, uint32_t n, const float4* hit, PathSoA next,
                         float4* done_L, uint32_t* done_sid, ShadowRec* sq, uint32_t* cnt);
 __global__ void k_finish(RenderParams R, const float4* done_L, const uint32_t* done_sid, const uint32_t* nptr,
                          uint32_t n_direct, PathSoA next, uint32_t* cnt, unsigned long long* next_sample,
                          float* sample_L);
 __global__ void k_gather(RenderParams R, const float* sample_L, double* film);
-__global__ void k_interact(DevScene S, const pt_ray* rays, uint32_t n, float* out);
-__global__ void k_bsdf_cases(DevScene S, int mid, const float* in, uint32_t n, float* out);
-__global__ void k_light_cases(DevScene S, const float* in, uint32_t n, float* out);
-__global__ void k_trace_rays(DevScene S, const pt_ray* rays, uint32_t n, int any, pt_hit* out,
+__global__ void k_interact(const pt_ray* rays, uint32_t n, float* out);
+__global__ void k_bsdf_cases(int mid, const float* in, uint32_t n, float* out);
+__global__ void k_light_cases(const float* in, uint32_t n, float* out);
+__global__ void k_trace_rays(const pt_ray* rays, uint32_t n, int any, pt_hit* out,
                              unsigned long long* counters);

@@ -62,7 +62,7 @@ __device__ __forceinline__ void count_add(unsigned long long* counters, int whic
 
 // ------------------------------------------------------------------ traversal kernels
 template <bool COUNT>
-__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(DevScene S, PathSoA P, uint32_t n, float4* __restrict__ hit,
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(PathSoA P, uint32_t n, float4* __restrict__ hit,
                                                            unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
@@ -70,7 +70,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(DevScene S, PathSoA 
     if (i < n) {
         const float4 o = P.o[i], d = P.d[i];
         float t, b1, b2;
-        int prim = trace_closest<COUNT>(S, xyz(o), xyz(d), __int_as_float(0x7f800000), t, b1, b2, s_ref, wk);
+        int prim = trace_closest<COUNT>(xyz(o), xyz(d), __int_as_float(0x7f800000), t, b1, b2, s_ref, wk);
         hit[i] = make_float4(t, b1, b2, __int_as_float(prim));
     }
     if (COUNT) {
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(DevScene S, PathSoA 
 }
 
 template <bool COUNT>
-__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(DevScene S, PathSoA next, float4* __restrict__ done_L,
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(PathSoA next, float4* __restrict__ done_L,
                                                           const ShadowRec* __restrict__ sq,
                                                           const uint32_t* __restrict__ nptr,
                                                           unsigned long long* counters) {
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(DevScene S, PathSoA n
     TraceWork wk{0, 0};
     if (i < n) {
         const ShadowRec r = sq[i];
-        if (!trace_any<COUNT>(S, xyz(r.o), xyz(r.d), r.o.w, s_ref, wk)) {
+        if (!trace_any<COUNT>(xyz(r.o), xyz(r.d), r.o.w, s_ref, wk)) {
             // one shadow ray per path per bounce: a plain read-modify-write
             const uint32_t tgt = __float_as_uint(r.d.w);
             float4* L = (tgt & SHADOW_DONE_BIT) ? &done_L[tgt & ~SHADOW_DONE_BIT] : &next.L[tgt];
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(DevScene S, PathSoA n
 }
 
 // Test hook: trace arbitrary rays (pt_trace).
-__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(DevScene S, const pt_ray* __restrict__ rays, uint32_t n,
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(const pt_ray* __restrict__ rays, uint32_t n,
                                                               int any, pt_hit* __restrict__ out,
                                                               unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
@@ -119,10 +119,10 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(DevScene S, const
         f3 o = F3(r.o[0], r.o[1], r.o[2]), d = F3(r.d[0], r.d[1], r.d[2]);
         pt_hit h;
         if (any) {
-            h.prim = trace_any<true>(S, o, d, r.tmax, s_ref, wk) ? 1 : 0;
+            h.prim = trace_any<true>(o, d, r.tmax, s_ref, wk) ? 1 : 0;
             h.t = h.b1 = h.b2 = 0;
         } else {
-            h.prim = trace_closest<true>(S, o, d, r.tmax, h.t, h.b1, h.b2, s_ref, wk);
+            h.prim = trace_closest<true>(o, d, r.tmax, h.t, h.b1, h.b2, s_ref, wk);
         }
         out[i] = h;
     }
@@ -133,7 +133,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(DevScene S, const
 // Test hook: closest hit + the full SurfaceInteraction the shade kernel
 // reconstructs (pt_interact): {hit, t, p, n, ns, uv, tangent} per ray, the
 // layout of the reference harness's trace records.
-__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_interact(DevScene S, const pt_ray* __restrict__ rays, uint32_t n,
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_interact(const pt_ray* __restrict__ rays, uint32_t n,
                                                             float* __restrict__ out) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_interact(DevScene S, const p
     const pt_ray r = rays[i];
     f3 o = F3(r.o[0], r.o[1], r.o[2]), d = F3(r.d[0], r.d[1], r.d[2]);
     float t, b1, b2;
-    const int prim = trace_closest<false>(S, o, d, r.tmax, t, b1, b2, s_ref, wk);
+    const int prim = trace_closest<false>(o, d, r.tmax, t, b1, b2, s_ref, wk);
     float* w = out + 16ull * i;
     for (int k = 0; k < 16; k++) w[k] = 0.0f;
     if (prim < 0) return;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_interact(DevScene S, const p
     const DevPrimInfo pi = S.info[prim];
     const uint32_t kind = __float_as_uint(g.a.w) & GF_KIND;
     SurfInt si;
-    if (kind == PT_PRIM_TRIANGLE) tri_interaction(S, g, pi.index, pi.material, o, d, t, b1, b2, si);
+    if (kind == PT_PRIM_TRIANGLE) tri_interaction(g, pi.index, pi.material, o, d, t, b1, b2, si);
     else if (kind == PT_PRIM_QUAD) quad_interaction(S.quads[pi.index], o, d, t, b1, b2, si);
     else sphere_interaction(S.spheres[pi.index], o, d, t, si);
     const float rec[16] = {1.0f, si.t, si.p.x, si.p.y, si.p.z, si.n.x, si.n.y, si.n.z, si.ns.x, si.ns.y, si.ns.z,
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_interact(DevScene S, const p
 
 // Test hook: Material::scatter / calc_attenuation / PDF on given
 // interactions (pt_bsdf_cases); case and record layout of oracle_bsdf.
-__global__ void k_bsdf_cases(DevScene S, int mid, const float* __restrict__ in, uint32_t n, float* __restrict__ out) {
+__global__ void k_bsdf_cases(int mid, const float* __restrict__ in, uint32_t n, float* __restrict__ out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float* c = in + 27ull * i;
@@ -177,7 +177,7 @@ __global__ void k_bsdf_cases(DevScene S, int mid, const float* __restrict__ in, 
     si.t = c[20];
     si.mat = mid;
     si.light = -1;
-    const Bxdf b = mat_scatter(S, mid, ro, rd, si, c[21], c[22], c[23]);
+    const Bxdf b = mat_scatter(mid, ro, rd, si, c[21], c[22], c[23]);
     if (b.ok) {
         o[0] = 1.0f;
         o[1] = b.f.x; o[2] = b.f.y; o[3] = b.f.z;
@@ -185,19 +185,19 @@ __global__ void k_bsdf_cases(DevScene S, int mid, const float* __restrict__ in, 
         o[5] = (float)b.flags;
         o[6] = b.o.x; o[7] = b.o.y; o[8] = b.o.z;
         o[9] = b.d.x; o[10] = b.d.y; o[11] = b.d.z;
-        const f3 a = mat_f(S, mid, rd, si, b.d);
+        const f3 a = mat_f(mid, rd, si, b.d);
         o[12] = a.x; o[13] = a.y; o[14] = a.z;
-        o[15] = mat_pdf(S, mid, rd, si, b.d);
+        o[15] = mat_pdf(mid, rd, si, b.d);
     }
     const f3 other = F3(c[24], c[25], c[26]);
-    const f3 a2 = mat_f(S, mid, rd, si, other);
+    const f3 a2 = mat_f(mid, rd, si, other);
     o[16] = a2.x; o[17] = a2.y; o[18] = a2.z;
-    o[19] = mat_pdf(S, mid, rd, si, other);
+    o[19] = mat_pdf(mid, rd, si, other);
 }
 
 // Test hook: Light::sample / PDF / L per light x case (pt_light_cases);
 // case {uv[2], ref point[3]}, record layout of oracle_lights.
-__global__ void k_light_cases(DevScene S, const float* __restrict__ in, uint32_t n, float* __restrict__ out) {
+__global__ void k_light_cases(const float* __restrict__ in, uint32_t n, float* __restrict__ out) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n * S.n_lights) return;
     const uint32_t li = k / n, i = k % n;
@@ -205,7 +205,7 @@ __global__ void k_light_cases(DevScene S, const float* __restrict__ in, uint32_t
     const float* c = in + 5ull * i;
     float* o = out + 18ull * k;
     for (int j = 0; j < 18; j++) o[j] = 0.0f;
-    const LSample ls = light_sample(S, l, c[0], c[1]);
+    const LSample ls = light_sample(l, c[0], c[1]);
     o[0] = ls.L.x; o[1] = ls.L.y; o[2] = ls.L.z;
     o[3] = ls.p.x; o[4] = ls.p.y; o[5] = ls.p.z;
     o[6] = ls.n.x; o[7] = ls.n.y; o[8] = ls.n.z;
@@ -214,8 +214,8 @@ __global__ void k_light_cases(DevScene S, const float* __restrict__ in, uint32_t
     if (!is_zero(ls.n)) {
         const f3 ref = F3(c[2], c[3], c[4]);
         const f3 rd = normalize(ls.p - ref);
-        o[14] = light_pdf(S, l, ls.p, ls.n, ref, rd);
-        const f3 L = light_L(S, l, ls.n, ls.u, ls.v, rd);
+        o[14] = light_pdf(l, ls.p, ls.n, ref, rd);
+        const f3 L = light_L(l, ls.n, ls.u, ls.v, rd);
         o[15] = L.x; o[16] = L.y; o[17] = L.z;
     }
 }
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256) void k_finish(RenderParams R, const float4* __
 
 // ------------------------------------------------------------------ shading
 template <int INTEGRATOR>
-__global__ __launch_bounds__(256) void k_shade(DevScene S, RenderParams R, PathSoA cur, uint32_t n,
+__global__ __launch_bounds__(256) void k_shade(RenderParams R, PathSoA cur, uint32_t n,
                                               const float4* __restrict__ hit, PathSoA next,
                                               float4* __restrict__ done_L, uint32_t* __restrict__ done_sid,
                                               ShadowRec* __restrict__ sq, uint32_t* __restrict__ cnt) {
@@ -381,7 +381,7 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, RenderParams R, PathS
             const DevPrimInfo pi = S.info[prim];
             const uint32_t kind = __float_as_uint(g.a.w) & GF_KIND;
             SurfInt si;
-            if (kind == PT_PRIM_TRIANGLE) tri_interaction(S, g, pi.index, pi.material, ro, rd, h.x, h.y, h.z, si);
+            if (kind == PT_PRIM_TRIANGLE) tri_interaction(g, pi.index, pi.material, ro, rd, h.x, h.y, h.z, si);
             else if (kind == PT_PRIM_QUAD) quad_interaction(S.quads[pi.index], ro, rd, h.x, h.y, h.z, si);
             else sphere_interaction(S.spheres[pi.index], ro, rd, h.x, si);
             si.mat = pi.material;
@@ -395,12 +395,12 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, RenderParams R, PathS
             // emission (Integrators.cpp:151-154, 217-226)
             if (si.light >= 0) {
                 const pt_light& al = S.lights[si.light];
-                f3 Le = light_L(S, al, si.n, si.u, si.v, rd);
+                f3 Le = light_L(al, si.n, si.u, si.v, rd);
                 if (!is_zero(Le)) {
                     if (INTEGRATOR == PT_INTEGRATOR_SIMPLE || spec) {
                         out = out + att * Le;
                     } else if (prev > 0) {
-                        float lp = al.pmf * light_pdf(S, al, si.p, si.n, ro, rd);
+                        float lp = al.pmf * light_pdf(al, si.p, si.n, ro, rd);
                         float w = prev * prev / (prev * prev + lp * lp);
                         out = out + (att * Le) * w;
                     }
@@ -412,7 +412,7 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, RenderParams R, PathS
                 ro = ro + si.t * rd;
             } else {
                 const float us = INTEGRATOR == PT_INTEGRATOR_PATH ? r[4] : r[2];
-                const Bxdf b = mat_scatter(S, si.mat, ro, rd, si, us, r[0], r[1]);
+                const Bxdf b = mat_scatter(si.mat, ro, rd, si, us, r[0], r[1]);
                 if (!b.ok) {
                     alive = false;  // absorbed
                 } else {
@@ -420,10 +420,10 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, RenderParams R, PathS
                         spec = (b.flags & FL_SPEC) != 0;
                         if (!spec) {
                             // PathIntegrator::SampleLd (Integrators.cpp:260-294); occlusion deferred
-                            const int li = ls_sample(S, r[5]);
+                            const int li = ls_sample(r[5]);
                             if (li >= 0) {
                                 const pt_light& l = S.lights[li];
-                                LSample ls = light_sample(S, l, r[2], r[3]);
+                                LSample ls = light_sample(l, r[2], r[3]);
                                 f3 ldir;
                                 float tmax;
                                 if (is_zero(ls.n)) {
@@ -437,21 +437,21 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, RenderParams R, PathS
                                 float lpdf = l.pmf;
                                 const float dt = dot(si.ns, sd);
                                 if (!(lpdf <= 0 || dt * dot(rd, si.ns) >= 0)) {
-                                    const f3 f = mat_f(S, si.mat, rd, si, sd) * fabsf(dt);
+                                    const f3 f = mat_f(si.mat, rd, si, sd) * fabsf(dt);
                                     f3 c;
                                     bool ok = true;
                                     if (light_is_delta(l)) {
                                         c = (ls.L * f) / lpdf;
                                     } else {
-                                        lpdf *= light_pdf(S, l, ls.p, ls.n, si.p, sd);
+                                        lpdf *= light_pdf(l, ls.p, ls.n, si.p, sd);
                                         if (lpdf <= 0) {
                                             ok = false;
                                         } else {
                                             float w2 = lpdf * lpdf;
-                                            float w1 = mat_pdf(S, si.mat, rd, si, sd);
+                                            float w1 = mat_pdf(si.mat, rd, si, sd);
                                             w1 = w1 * w1;
                                             float wl = w2 / (w1 + w2);
-                                            c = ((light_L(S, l, ls.n, ls.u, ls.v, sd) * f) * wl) / lpdf;
+                                            c = ((light_L(l, ls.n, ls.u, ls.v, sd) * f) * wl) / lpdf;
                                         }
                                     }
                                     if (ok) {
@@ -465,7 +465,7 @@ __global__ __launch_bounds__(256) void k_shade(DevScene S, RenderParams R, PathS
                                     }
                                 }
                             }
-                            prev = mat_pdf(S, si.mat, rd, si, b.d);
+                            prev = mat_pdf(si.mat, rd, si, b.d);
 #ifdef PT_DEBUG_KEY
                             if (key == PT_DEBUG_KEY)
                                 printf("G  nee c %a %a %a (light %d) shadow %d\n", srec.c.x, srec.c.y, srec.c.z, li,
@@ -593,13 +593,13 @@ __global__ __launch_bounds__(256) void k_gather(RenderParams R, const float* __r
 }
 
 // explicit instantiations used by the runtime
-template __global__ void k_closest<false>(DevScene, PathSoA, uint32_t, float4*, unsigned long long*);
-template __global__ void k_closest<true>(DevScene, PathSoA, uint32_t, float4*, unsigned long long*);
-template __global__ void k_shadow<false>(DevScene, PathSoA, float4*, const ShadowRec*, const uint32_t*,
+template __global__ void k_closest<false>(PathSoA, uint32_t, float4*, unsigned long long*);
+template __global__ void k_closest<true>(PathSoA, uint32_t, float4*, unsigned long long*);
+template __global__ void k_shadow<false>(PathSoA, float4*, const ShadowRec*, const uint32_t*,
                                          unsigned long long*);
-template __global__ void k_shadow<true>(DevScene, PathSoA, float4*, const ShadowRec*, const uint32_t*,
+template __global__ void k_shadow<true>(PathSoA, float4*, const ShadowRec*, const uint32_t*,
                                         unsigned long long*);
-template __global__ void k_shade<PT_INTEGRATOR_PATH>(DevScene, RenderParams, PathSoA, uint32_t, const float4*, PathSoA,
+template __global__ void k_shade<PT_INTEGRATOR_PATH>(RenderParams, PathSoA, uint32_t, const float4*, PathSoA,
                                                      float4*, uint32_t*, ShadowRec*, uint32_t*);
-template __global__ void k_shade<PT_INTEGRATOR_SIMPLE>(DevScene, RenderParams, PathSoA, uint32_t, const float4*,
+template __global__ void k_shade<PT_INTEGRATOR_SIMPLE>(RenderParams, PathSoA, uint32_t, const float4*,
                                                        PathSoA, float4*, uint32_t*, ShadowRec*, uint32_t*);

@@ -367,38 +367,38 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
         acc += s->lights[s->sampler_lights[i]].power;
         cdf[i] = acc;
     }
-    DevScene& S = c->scene;
-    S = DevScene{};
+    DevScene& DS = c->scene;
+    DS = DevScene{};
     pt_status st;
 #define UP(dst, src, n) \
     if ((st = upload(c, src, n, &dst)) != PT_OK) return st;
-    UP(S.nodes, nodes.data(), nodes.size());
-    UP(S.geom, geom.data(), geom.size());
-    UP(S.info, info.data(), info.size());
-    UP(S.tri, tri.data(), tri.size());
-    UP(S.positions, s->positions, 3 * (size_t)s->n_vertices);
-    UP(S.normals, s->normals, 3 * (size_t)s->n_vertices);
-    UP(S.uvs, s->uvs, 2 * (size_t)s->n_vertices);
-    UP(S.tangents, s->tangents, s->tangents ? 3 * (size_t)s->n_vertices : 0);
-    UP(S.quads, s->quads, s->n_quads);
-    UP(S.spheres, s->spheres, s->n_spheres);
-    UP(S.materials, s->materials, s->n_materials);
-    UP(S.textures, s->textures, s->n_textures);
-    UP(S.images, s->images, s->n_images);
-    UP(S.texels, s->texels, s->n_texel_bytes);
-    UP(S.lights, s->lights, s->n_lights);
-    UP(S.sampler_lights, s->sampler_lights, s->n_sampler_lights);
-    UP(S.sampler_cdf, cdf.data(), cdf.size());
-    UP(S.infinite_lights, s->infinite_lights, s->n_infinite_lights);
+    UP(DS.nodes, nodes.data(), nodes.size());
+    UP(DS.geom, geom.data(), geom.size());
+    UP(DS.info, info.data(), info.size());
+    UP(DS.tri, tri.data(), tri.size());
+    UP(DS.positions, s->positions, 3 * (size_t)s->n_vertices);
+    UP(DS.normals, s->normals, 3 * (size_t)s->n_vertices);
+    UP(DS.uvs, s->uvs, 2 * (size_t)s->n_vertices);
+    UP(DS.tangents, s->tangents, s->tangents ? 3 * (size_t)s->n_vertices : 0);
+    UP(DS.quads, s->quads, s->n_quads);
+    UP(DS.spheres, s->spheres, s->n_spheres);
+    UP(DS.materials, s->materials, s->n_materials);
+    UP(DS.textures, s->textures, s->n_textures);
+    UP(DS.images, s->images, s->n_images);
+    UP(DS.texels, s->texels, s->n_texel_bytes);
+    UP(DS.lights, s->lights, s->n_lights);
+    UP(DS.sampler_lights, s->sampler_lights, s->n_sampler_lights);
+    UP(DS.sampler_cdf, cdf.data(), cdf.size());
+    UP(DS.infinite_lights, s->infinite_lights, s->n_infinite_lights);
 #undef UP
-    S.root = roots[0];
-    S.n_prims = s->n_prims;
-    S.n_texel_bytes = s->n_texel_bytes;
-    S.n_lights = s->n_lights;
-    S.light_sampler = s->light_sampler;
-    S.n_sampler_lights = s->n_sampler_lights;
-    S.sampler_total = acc;
-    S.n_infinite_lights = s->n_infinite_lights;
+    DS.root = roots[0];
+    DS.n_prims = s->n_prims;
+    DS.n_texel_bytes = s->n_texel_bytes;
+    DS.n_lights = s->n_lights;
+    DS.light_sampler = s->light_sampler;
+    DS.n_sampler_lights = s->n_sampler_lights;
+    DS.sampler_total = acc;
+    DS.n_infinite_lights = s->n_infinite_lights;
     c->has_scene = true;
     c->n_materials = s->n_materials;
     return PT_OK;
@@ -462,9 +462,17 @@ static double gauss_h(double x, double sigma) {
 // Core loop shared by pt_render / pt_render_samples.  Renders local sample
 // chunks; after each chunk either gathers into `film` (device) or hands the
 // chunk's per-sample radiance to `on_chunk`.
+// Makes this context's scene the one the kernels read (constant-memory `S`),
+// ordered on the context's stream.  Called by every entry point that launches.
+static pt_status bind_scene(pt_ctx* c) {
+    HIPCHK(c, hipMemcpyToSymbolAsync(HIP_SYMBOL(S), &c->scene, sizeof(DevScene), 0, hipMemcpyHostToDevice, c->stream));
+    return PT_OK;
+}
+
 template <class OnChunk>
 static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_dev,
                      pt_stats* stats, OnChunk on_chunk) {
+    if (pt_status bs = bind_scene(c)) return bs;
     const uint32_t W = (uint32_t)cam->width, H = (uint32_t)cam->height;
     RenderParams R{};
     R.cam = *cam;
@@ -550,25 +558,25 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             const dim3 gt((n_active + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK), gs((n_active + 255) / 256);
             if (timing) HIPCHK(c, hipEventRecord(c->ev[0], sm));
             if (count)
-                hipLaunchKernelGGL(k_closest<true>, gt, dim3(PT_TRACE_BLOCK), 0, sm, c->scene, cur, n_active, c->hit,
+                hipLaunchKernelGGL(k_closest<true>, gt, dim3(PT_TRACE_BLOCK), 0, sm, cur, n_active, c->hit,
                                    c->counters);
             else
-                hipLaunchKernelGGL(k_closest<false>, gt, dim3(PT_TRACE_BLOCK), 0, sm, c->scene, cur, n_active, c->hit,
+                hipLaunchKernelGGL(k_closest<false>, gt, dim3(PT_TRACE_BLOCK), 0, sm, cur, n_active, c->hit,
                                    c->counters);
             if (timing) HIPCHK(c, hipEventRecord(c->ev[1], sm));
             if (rd->integrator == PT_INTEGRATOR_SIMPLE)
-                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_SIMPLE>, gs, dim3(256), 0, sm, c->scene, R, cur, n_active,
+                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_SIMPLE>, gs, dim3(256), 0, sm, R, cur, n_active,
                                    (const float4*)c->hit, nxt, c->done_L, c->done_sid, c->sq, c->qcnt);
             else
-                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_PATH>, gs, dim3(256), 0, sm, c->scene, R, cur, n_active,
+                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_PATH>, gs, dim3(256), 0, sm, R, cur, n_active,
                                    (const float4*)c->hit, nxt, c->done_L, c->done_sid, c->sq, c->qcnt);
             if (timing) HIPCHK(c, hipEventRecord(c->ev[2], sm));
             if (rd->integrator != PT_INTEGRATOR_SIMPLE) {
                 if (count)
-                    hipLaunchKernelGGL(k_shadow<true>, gt, dim3(PT_TRACE_BLOCK), 0, sm, c->scene, nxt, c->done_L,
+                    hipLaunchKernelGGL(k_shadow<true>, gt, dim3(PT_TRACE_BLOCK), 0, sm, nxt, c->done_L,
                                        (const ShadowRec*)c->sq, (const uint32_t*)(c->qcnt + Q_SHADOW), c->counters);
                 else
-                    hipLaunchKernelGGL(k_shadow<false>, gt, dim3(PT_TRACE_BLOCK), 0, sm, c->scene, nxt, c->done_L,
+                    hipLaunchKernelGGL(k_shadow<false>, gt, dim3(PT_TRACE_BLOCK), 0, sm, nxt, c->done_L,
                                        (const ShadowRec*)c->sq, (const uint32_t*)(c->qcnt + Q_SHADOW), c->counters);
             }
             if (timing) HIPCHK(c, hipEventRecord(c->ev[3], sm));
@@ -723,11 +731,12 @@ extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any
         tmp.push_back(dh);
     }
     if (c->cap == 0 && ensure_work(c, 256) != PT_OK) return PT_ERR_OOM;
+    if (pt_status bs = bind_scene(c)) return bs;
     HIPCHK(c, hipMemsetAsync(c->counters, 0, CNT_SHARDS * CNT_COUNT * 8, c->stream));
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
     hipLaunchKernelGGL(k_trace_rays, dim3((n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK), dim3(PT_TRACE_BLOCK), 0,
-                       c->stream, c->scene, dr, n, any_hit, dh, c->counters);
+                       c->stream, dr, n, any_hit, dh, c->counters);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
     if (!hdev) HIPCHK(c, hipMemcpyAsync(hits, dh, (size_t)n * sizeof(pt_hit), hipMemcpyDeviceToHost, c->stream));
@@ -768,8 +777,9 @@ static pt_status run_hook(pt_ctx* c, const void* in, size_t in_bytes, float* out
         hipFree(din);
         return fail(c, PT_ERR_OOM, "hook output");
     }
-    pt_status st = PT_OK;
-    if (hipMemcpyAsync(din, in, in_bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) st = PT_ERR_HIP;
+    pt_status st = bind_scene(c);
+    if (st == PT_OK && hipMemcpyAsync(din, in, in_bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        st = PT_ERR_HIP;
     if (st == PT_OK) {
         launch(din, dout);
         if (hipGetLastError() != hipSuccess) st = PT_ERR_HIP;
@@ -790,7 +800,7 @@ extern "C" pt_status pt_interact(pt_ctx* c, const pt_ray* rays, uint32_t n, floa
     return run_hook(c, rays, (size_t)n * sizeof(pt_ray), out, (size_t)n * 16 * sizeof(float),
                     [&](void* din, float* dout) {
                         hipLaunchKernelGGL(k_interact, dim3((n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK),
-                                           dim3(PT_TRACE_BLOCK), 0, c->stream, c->scene, (const pt_ray*)din, n, dout);
+                                           dim3(PT_TRACE_BLOCK), 0, c->stream, (const pt_ray*)din, n, dout);
                     });
 }
 
@@ -802,7 +812,7 @@ extern "C" pt_status pt_bsdf_cases(pt_ctx* c, int32_t material, const float* cas
     if (n == 0) return PT_OK;
     return run_hook(c, cases, (size_t)n * 27 * sizeof(float), out, (size_t)n * 20 * sizeof(float),
                     [&](void* din, float* dout) {
-                        hipLaunchKernelGGL(k_bsdf_cases, dim3((n + 127) / 128), dim3(128), 0, c->stream, c->scene,
+                        hipLaunchKernelGGL(k_bsdf_cases, dim3((n + 127) / 128), dim3(128), 0, c->stream,
                                            (int)material, (const float*)din, n, dout);
                     });
 }
@@ -817,6 +827,6 @@ extern "C" pt_status pt_light_cases(pt_ctx* c, const float* cases, uint32_t n, f
     return run_hook(c, cases, (size_t)n * 5 * sizeof(float), out, (size_t)total * 18 * sizeof(float),
                     [&](void* din, float* dout) {
                         hipLaunchKernelGGL(k_light_cases, dim3((uint32_t)((total + 127) / 128)), dim3(128), 0,
-                                           c->stream, c->scene, (const float*)din, n, dout);
+                                           c->stream, (const float*)din, n, dout);
                     });
 }

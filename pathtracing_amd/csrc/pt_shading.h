@@ -19,19 +19,19 @@ __device__ __forceinline__ int wrap_index(int i, int n) {
     return m;
 }
 // Image::GetChannelAt (Texture.hpp:43-48): byte ch-1 of the pixel, any channel count.
-__device__ __forceinline__ float channel_at(const DevScene& S, const pt_image& im, int x, int y, int ch) {
+__device__ __forceinline__ float channel_at(const pt_image& im, int x, int y, int ch) {
     int xi = wrap_index(x, im.width), yi = wrap_index(y, im.height);
     uint64_t idx = im.offset + ((uint64_t)yi * (uint64_t)im.width + (uint64_t)xi) * (uint64_t)im.channels +
                    (uint64_t)(ch - 1);
     if (idx >= S.n_texel_bytes) return 0.0f;
     return S.texels[idx] / 255.0f;
 }
-__device__ __forceinline__ f3 texel3(const DevScene& S, const pt_image& im, int x, int y) {
-    return F3(channel_at(S, im, x, y, 1), channel_at(S, im, x, y, 2), channel_at(S, im, x, y, 3));
+__device__ __forceinline__ f3 texel3(const pt_image& im, int x, int y) {
+    return F3(channel_at(im, x, y, 1), channel_at(im, x, y, 2), channel_at(im, x, y, 3));
 }
 
 // Texture::Evaluate for SolidColor / CheckerTexture / ImageTexture (Texture.hpp:128-207).
-__device__ f3 tex_eval(const DevScene& S, int id, float u, float v) {
+__device__ f3 tex_eval(int id, float u, float v) {
     f3 scale = F3(1, 1, 1);
     bool scaled = false;
     for (int guard = 0; guard < 16; guard++) {
@@ -54,8 +54,8 @@ __device__ f3 tex_eval(const DevScene& S, int id, float u, float v) {
         float y = v * im.height - 0.5f;
         int xi = (int)floorf(x), yi = (int)floorf(y);
         float dx = x - xi, dy = y - yi;
-        f3 a = texel3(S, im, xi, yi), b = texel3(S, im, xi + 1, yi);
-        f3 c = texel3(S, im, xi, yi + 1), d = texel3(S, im, xi + 1, yi + 1);
+        f3 a = texel3(im, xi, yi), b = texel3(im, xi + 1, yi);
+        f3 c = texel3(im, xi, yi + 1), d = texel3(im, xi + 1, yi + 1);
         // contraction of the reference build: w_a*a rounded, then fma(w_b, b), fma(w_c, c), fma(w_d, d)
         float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
         f3 r = F3(fma_(wd, d.x, fma_(wc, c.x, fma_(wb, b.x, rmul(wa, a.x)))),
@@ -68,7 +68,7 @@ __device__ f3 tex_eval(const DevScene& S, int id, float u, float v) {
 }
 
 // Texture::alpha (Texture.hpp:112-114, Texture.cpp:47-62, 41-45)
-__device__ float tex_alpha(const DevScene& S, int id, float u, float v) {
+__device__ float tex_alpha(int id, float u, float v) {
     for (int guard = 0; guard < 16; guard++) {
         const pt_texture& t = S.textures[id];
         if (t.kind == PT_TEX_SOLID) return 1.0f;
@@ -84,8 +84,8 @@ __device__ float tex_alpha(const DevScene& S, int id, float u, float v) {
         float y = v * im.height - 0.5f;
         int xi = (int)floorf(x), yi = (int)floorf(y);
         float dx = x - xi, dy = y - yi;
-        float a = channel_at(S, im, xi, yi, 4), b = channel_at(S, im, xi + 1, yi, 4);
-        float c = channel_at(S, im, xi, yi + 1, 4), d = channel_at(S, im, xi + 1, yi + 1, 4);
+        float a = channel_at(im, xi, yi, 4), b = channel_at(im, xi + 1, yi, 4);
+        float c = channel_at(im, xi, yi + 1, 4), d = channel_at(im, xi + 1, yi + 1, 4);
         // ImageTexture::alpha as compiled in the reference: w_b*b rounded, then fma(w_a, a), fma(w_c, c), fma(w_d, d)
         float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
         return fma_(wd, d, fma_(wc, c, fma_(wa, a, rmul(wb, b))));
@@ -102,11 +102,11 @@ __device__ __forceinline__ float blend_random(f3 o, f3 d, int prim) {
 }
 
 // Material::Alpha (Material.hpp:336-342, 572-578)
-__device__ bool mat_alpha(const DevScene& S, int mid, float u, float v, f3 ro, f3 rd, int prim) {
+__device__ bool mat_alpha(int mid, float u, float v, f3 ro, f3 rd, int prim) {
     if (mid < 0) return true;
     const pt_material& m = S.materials[mid];
     if (m.kind != PT_MAT_DIFFUSE && m.kind != PT_MAT_DIELECTRIC) return true;
-    float a = m.alpha >= 0 ? tex_eval(S, m.alpha, u, v).x : tex_alpha(S, m.tex, u, v);
+    float a = m.alpha >= 0 ? tex_eval(m.alpha, u, v).x : tex_alpha(m.tex, u, v);
     if (m.alpha_mode == PT_ALPHA_OPAQUE) return true;
     if (m.alpha_mode == PT_ALPHA_MASK) return a > m.alpha_cutoff;
     return a >= 1.0f ? true : (blend_random(ro, rd, prim) < a);
@@ -147,11 +147,11 @@ __device__ __forceinline__ f3 to_world_nm(const Onb& b, f3 v) {
 __device__ __forceinline__ f3 to_local(const Onb& b, f3 v) { return F3(dot(v, b.a0), dot(v, b.a1), dot(v, b.a2)); }
 
 // sample_normalMap (Material.hpp:344-348, 580-584)
-__device__ f3 normal_map(const DevScene& S, int mid, const SurfInt& si) {
+__device__ f3 normal_map(int mid, const SurfInt& si) {
     if (mid < 0) return si.ns;
     const pt_material& m = S.materials[mid];
     if ((m.kind != PT_MAT_DIFFUSE && m.kind != PT_MAT_DIELECTRIC) || m.norm < 0) return si.ns;
-    f3 t = tex_eval(S, m.norm, si.u, si.v);
+    f3 t = tex_eval(m.norm, si.u, si.v);
     f3 nn = normalize(2.0f * t - F3(1, 1, 1));
     return to_world_nm(onb_si(si), nn);
 }
@@ -170,7 +170,7 @@ __device__ __forceinline__ void sphere_uv(f3 p, float& u, float& v) {
 // TriangleShape::Intersect shading part (Shape.cpp:206-242) from the hit's
 // barycentrics; identical to computing it at the candidate (the reference does
 // it per candidate, only the last accepted survives).
-__device__ void tri_interaction(const DevScene& S, const DevGeom& g, uint32_t tri, int mid, f3 o, f3 d, float t,
+__device__ void tri_interaction(const DevGeom& g, uint32_t tri, int mid, f3 o, f3 d, float t,
                                 float bu, float bv, SurfInt& si) {
     uint4 T = S.tri[tri];
     float u = bu, v = bv, w = 1.0f - u - v;
@@ -201,7 +201,7 @@ __device__ void tri_interaction(const DevScene& S, const DevGeom& g, uint32_t tr
         f3 up = (fabsf(si.ns.x) > 0.9999f) ? F3(0, 1, 0) : F3(1, 0, 0);
         si.tangent = normalize(cross(up, si.ns));
     }
-    si.ns = normal_map(S, mid, si);
+    si.ns = normal_map(mid, si);
 }
 
 // QuadShape::Intersect (Shape.cpp:320-343) interaction part.
@@ -313,17 +313,17 @@ struct Bxdf {
     bool ok;
 };
 
-__device__ __forceinline__ float diffuse_rough(const DevScene& S, const pt_material& m, const SurfInt& si) {
-    return smax(tex_eval(S, m.rough, si.u, si.v).y, 0.0001f);
+__device__ __forceinline__ float diffuse_rough(const pt_material& m, const SurfInt& si) {
+    return smax(tex_eval(m.rough, si.u, si.v).y, 0.0001f);
 }
 __device__ __forceinline__ f3 mixv(f3 x, f3 y, float a) { return x * (1.0f - a) + y * a; }
 
 // MicrofacetDiffuse::scatter (Material.hpp:206-266)
-__device__ Bxdf diffuse_scatter(const DevScene& S, const pt_material& m, f3 ind, const SurfInt& si, float u,
+__device__ Bxdf diffuse_scatter(const pt_material& m, f3 ind, const SurfInt& si, float u,
                                 float uv0, float uv1) {
     Bxdf b;
     b.ok = false;
-    float rough = diffuse_rough(S, m, si);
+    float rough = diffuse_rough(m, si);
     Onb tbn = onb_n(dot(ind, si.ns) > 0 ? -si.ns : si.ns);
     Dist D = mkdist(rough);
     float prob = rough >= 0.7 ? 1.0f : 0.5f;
@@ -343,8 +343,8 @@ __device__ Bxdf diffuse_scatter(const DevScene& S, const pt_material& m, f3 ind,
     float dpdf = prob * wi.z * PT_INV_PI;
     float spdf = (1.0f - prob) * mpdf_(D, wo, wh) / (4 * fabsf(dot(wo, wh)));
     float pdf = dpdf + spdf;
-    f3 col = tex_eval(S, m.tex, si.u, si.v);
-    float metal = tex_eval(S, m.metal, si.u, si.v).z;
+    f3 col = tex_eval(m.tex, si.u, si.v);
+    float metal = tex_eval(m.metal, si.u, si.v).z;
     f3 F0 = mixv(F3(0.04f, 0.04f, 0.04f), col, metal);
     f3 F = schlick(dot(wi, wh), F0);
     f3 num = (D_(D, wh) * G_(D, wo, wi)) * F;
@@ -362,15 +362,15 @@ __device__ Bxdf diffuse_scatter(const DevScene& S, const pt_material& m, f3 ind,
     return b;
 }
 // MicrofacetDiffuse::calc_attenuation (Material.hpp:299-326)
-__device__ f3 diffuse_f(const DevScene& S, const pt_material& m, f3 ind, const SurfInt& si, f3 dir) {
+__device__ f3 diffuse_f(const pt_material& m, f3 ind, const SurfInt& si, f3 dir) {
     Onb tbn = onb_n(dot(ind, si.ns) > 0 ? -si.ns : si.ns);
     f3 wo = to_local(tbn, -ind);
     f3 wi = to_local(tbn, dir);
     f3 wh = normalize(wo + wi);
-    float rough = diffuse_rough(S, m, si);
-    float metal = tex_eval(S, m.metal, si.u, si.v).z;
+    float rough = diffuse_rough(m, si);
+    float metal = tex_eval(m.metal, si.u, si.v).z;
     Dist D = mkdist(rough);
-    f3 col = tex_eval(S, m.tex, si.u, si.v);
+    f3 col = tex_eval(m.tex, si.u, si.v);
     f3 F0 = mixv(F3(0.04f, 0.04f, 0.04f), col, metal);
     f3 F = schlick(dot(wi, wh), F0);
     f3 num = (D_(D, wh) * G_(D, wo, wi)) * F;
@@ -380,8 +380,8 @@ __device__ f3 diffuse_f(const DevScene& S, const pt_material& m, f3 ind, const S
     return (kD * col) * PT_INV_PI + num / den;
 }
 // MicrofacetDiffuse::PDF (Material.hpp:281-296): no (1-prob) on the specular term (A.7)
-__device__ float diffuse_pdf(const DevScene& S, const pt_material& m, f3 ind, const SurfInt& si, f3 dir) {
-    float rough = diffuse_rough(S, m, si);
+__device__ float diffuse_pdf(const pt_material& m, f3 ind, const SurfInt& si, f3 dir) {
+    float rough = diffuse_rough(m, si);
     Dist D = mkdist(rough);
     Onb tbn = onb_n(dot(ind, si.ns) > 0 ? -si.ns : si.ns);
     f3 wo = to_local(tbn, -ind);
@@ -393,11 +393,11 @@ __device__ float diffuse_pdf(const DevScene& S, const pt_material& m, f3 ind, co
 }
 
 // MicrofacetDielectric::scatter (Material.hpp:392-477)
-__device__ Bxdf dielectric_scatter(const DevScene& S, const pt_material& m, f3 ino, f3 ind, const SurfInt& si,
+__device__ Bxdf dielectric_scatter(const pt_material& m, f3 ino, f3 ind, const SurfInt& si,
                                    float u, float uv0, float uv1) {
     Bxdf b;
     b.ok = false;
-    float rough = tex_eval(S, m.rough, si.u, si.v).y;
+    float rough = tex_eval(m.rough, si.u, si.v).y;
     Dist D = mkdist(rough);
     Onb tbn = onb_si(si);
     f3 wo = to_local(tbn, -ind);
@@ -413,13 +413,13 @@ __device__ Bxdf dielectric_scatter(const DevScene& S, const pt_material& m, f3 i
         if (u < (R / (R + T))) {
             dir = to_world(tbn, F3(-wo.x, -wo.y, wo.z));
             b.o = hitp + PT_EPS * Ng;
-            b.f = (tex_eval(S, m.tex, si.u, si.v) * R) / fabsf(dot(si.ns, dir));
+            b.f = (tex_eval(m.tex, si.u, si.v) * R) / fabsf(dot(si.ns, dir));
             b.pdf = R / (R + T);
         } else {
             dir = refract(ind, N, eta);
             if (is_zero(dir)) return b;
             b.o = hitp - PT_EPS * Ng;
-            b.f = (tex_eval(S, m.tex, si.u, si.v) * T) / fabsf(dot(si.ns, dir));
+            b.f = (tex_eval(m.tex, si.u, si.v) * T) / fabsf(dot(si.ns, dir));
             b.pdf = T / (R + T);
         }
         b.d = dir;
@@ -438,7 +438,7 @@ __device__ Bxdf dielectric_scatter(const DevScene& S, const pt_material& m, f3 i
         b.o = hitp + PT_EPS * Ng;
         b.d = to_world(tbn, wi);
         b.pdf = mpdf_(D, wo, wh) / (4 * fabsf(dot(wo, wh))) * R / (R + T);
-        b.f = (((tex_eval(S, m.tex, si.u, si.v) * D_(D, wh)) * G_(D, wo, wi)) * R) / fabsf(4 * wi.z * wo.z);
+        b.f = (((tex_eval(m.tex, si.u, si.v) * D_(D, wh)) * G_(D, wo, wi)) * R) / fabsf(4 * wi.z * wo.z);
     } else {
         f3 wi = refract(-wo, wh, eta);
         if (wo.z * wi.z > 0 || wi.z == 0) return b;
@@ -448,18 +448,18 @@ __device__ Bxdf dielectric_scatter(const DevScene& S, const pt_material& m, f3 i
         float dwh = fabsf(dot(wi, wh)) / denom;
         b.pdf = mpdf_(D, wo, wh) * dwh * T / (R + T);
         float ft = T * D_(D, wh) * G_(D, wo, wi) * fabsf(dot(wi, wh) * dot(wo, wh) / (denom * wi.z * wo.z));
-        b.f = tex_eval(S, m.tex, si.u, si.v) * ft;
+        b.f = tex_eval(m.tex, si.u, si.v) * ft;
     }
     b.flags = fl;
     b.ok = true;
     return b;
 }
 // MicrofacetDielectric::PDF / calc_attenuation (Material.hpp:484-564)
-__device__ void dielectric_eval(const DevScene& S, const pt_material& m, f3 ind, const SurfInt& si, f3 dir,
+__device__ void dielectric_eval(const pt_material& m, f3 ind, const SurfInt& si, f3 dir,
                                 f3& f_out, float& pdf_out) {
     f_out = F3(0, 0, 0);
     pdf_out = 0;
-    float rough = tex_eval(S, m.rough, si.u, si.v).y;
+    float rough = tex_eval(m.rough, si.u, si.v).y;
     Dist D = mkdist(rough);
     float ri = m.ri;
     if (ri == 1 || smooth_(D)) return;
@@ -478,7 +478,7 @@ __device__ void dielectric_eval(const DevScene& S, const pt_material& m, f3 ind,
     float F = fresnel_dielectric(dot(wo, wh), ri);
     float R = F, T = 1 - R;
     float pdf = mpdf_(D, wo, wh);
-    f3 col = tex_eval(S, m.tex, si.u, si.v);
+    f3 col = tex_eval(m.tex, si.u, si.v);
     if (refl) {
         pdf_out = pdf / (4 * fabsf(dot(wo, wh))) * R / (R + T);
         f_out = (((col * D_(D, wh)) * G_(D, wo, wi)) * F) / fabsf(4 * ci * co);
@@ -492,7 +492,7 @@ __device__ void dielectric_eval(const DevScene& S, const pt_material& m, f3 ind,
     }
 }
 // ThinDielectric::scatter (Material.hpp:605-644)
-__device__ Bxdf thin_scatter(const DevScene& S, const pt_material& m, f3 ino, f3 ind, const SurfInt& si, float u) {
+__device__ Bxdf thin_scatter(const pt_material& m, f3 ino, f3 ind, const SurfInt& si, float u) {
     Bxdf b;
     Onb tbn = onb_si(si);
     f3 wo = to_local(tbn, -ind);
@@ -516,7 +516,7 @@ __device__ Bxdf thin_scatter(const DevScene& S, const pt_material& m, f3 ino, f3
         f = (F3(1, 1, 1) * T) / fabsf(dot(si.ns, dir));
         b.pdf = T / (R + T);
     }
-    b.f = f * tex_eval(S, m.tex, si.u, si.v);
+    b.f = f * tex_eval(m.tex, si.u, si.v);
     b.d = dir;
     b.flags = FL_TRANS | FL_SPEC;
     b.ok = true;
@@ -538,34 +538,34 @@ __device__ Bxdf conductor_scatter(const pt_material& m, f3 ind, const SurfInt& s
     return b;
 }
 
-__device__ Bxdf mat_scatter(const DevScene& S, int mid, f3 ino, f3 ind, const SurfInt& si, float u, float uv0,
+__device__ Bxdf mat_scatter(int mid, f3 ino, f3 ind, const SurfInt& si, float u, float uv0,
                             float uv1) {
     const pt_material& m = S.materials[mid];
     switch (m.kind) {
-        case PT_MAT_DIFFUSE: return diffuse_scatter(S, m, ind, si, u, uv0, uv1);
-        case PT_MAT_DIELECTRIC: return dielectric_scatter(S, m, ino, ind, si, u, uv0, uv1);
-        case PT_MAT_THIN: return thin_scatter(S, m, ino, ind, si, u);
+        case PT_MAT_DIFFUSE: return diffuse_scatter(m, ind, si, u, uv0, uv1);
+        case PT_MAT_DIELECTRIC: return dielectric_scatter(m, ino, ind, si, u, uv0, uv1);
+        case PT_MAT_THIN: return thin_scatter(m, ino, ind, si, u);
         default: return conductor_scatter(m, ind, si);
     }
 }
-__device__ f3 mat_f(const DevScene& S, int mid, f3 ind, const SurfInt& si, f3 dir) {
+__device__ f3 mat_f(int mid, f3 ind, const SurfInt& si, f3 dir) {
     const pt_material& m = S.materials[mid];
     f3 f;
     float p;
     switch (m.kind) {
-        case PT_MAT_DIFFUSE: return diffuse_f(S, m, ind, si, dir);
-        case PT_MAT_DIELECTRIC: dielectric_eval(S, m, ind, si, dir, f, p); return f;
+        case PT_MAT_DIFFUSE: return diffuse_f(m, ind, si, dir);
+        case PT_MAT_DIELECTRIC: dielectric_eval(m, ind, si, dir, f, p); return f;
         case PT_MAT_THIN: return F3(0, 0, 0);
         default: return F3(1, 1, 1);  // base Material::calc_attenuation
     }
 }
-__device__ float mat_pdf(const DevScene& S, int mid, f3 ind, const SurfInt& si, f3 dir) {
+__device__ float mat_pdf(int mid, f3 ind, const SurfInt& si, f3 dir) {
     const pt_material& m = S.materials[mid];
     f3 f;
     float p;
     switch (m.kind) {
-        case PT_MAT_DIFFUSE: return diffuse_pdf(S, m, ind, si, dir);
-        case PT_MAT_DIELECTRIC: dielectric_eval(S, m, ind, si, dir, f, p); return p;
+        case PT_MAT_DIFFUSE: return diffuse_pdf(m, ind, si, dir);
+        case PT_MAT_DIELECTRIC: dielectric_eval(m, ind, si, dir, f, p); return p;
         default: return 0;
     }
 }
@@ -575,9 +575,9 @@ struct LSample {
     f3 L, p, n, dir;
     float u, v;
 };
-__device__ __forceinline__ uint4 tri_idx(const DevScene& S, uint32_t tri) { return S.tri[tri]; }
+__device__ __forceinline__ uint4 tri_idx(uint32_t tri) { return S.tri[tri]; }
 
-__device__ float shape_area(const DevScene& S, uint32_t kind, uint32_t index) {
+__device__ float shape_area(uint32_t kind, uint32_t index) {
     if (kind == PT_PRIM_QUAD) {
         const pt_quad& q = S.quads[index];
         return length(cross_r(ld3(q.u), ld3(q.v)));  // QuadShape::Area as compiled (fixture search)
@@ -586,12 +586,12 @@ __device__ float shape_area(const DevScene& S, uint32_t kind, uint32_t index) {
         float r = S.spheres[index].radius;
         return 4.0f * PT_PI * r * r;
     }
-    uint4 T = tri_idx(S, index);
+    uint4 T = tri_idx(index);
     f3 v0 = ld3(S.positions + 3 * T.x), v1 = ld3(S.positions + 3 * T.y), v2 = ld3(S.positions + 3 * T.z);
     return length(cross(v0 - v2, v1 - v2)) * 0.5f;
 }
 // Shape::Sample (Shape.cpp:74-81, 277-297; Shape.hpp:139-141)
-__device__ void shape_sample(const DevScene& S, uint32_t kind, uint32_t index, float u0, float u1, LSample& ls) {
+__device__ void shape_sample(uint32_t kind, uint32_t index, float u0, float u1, LSample& ls) {
     ls.u = 0;
     ls.v = 0;
     if (kind == PT_PRIM_QUAD) {
@@ -610,7 +610,7 @@ __device__ void shape_sample(const DevScene& S, uint32_t kind, uint32_t index, f
         sphere_uv(ls.p, ls.u, ls.v);
     } else {
         float w = 1.0f - u0 - u1;  // not folded
-        uint4 T = tri_idx(S, index);
+        uint4 T = tri_idx(index);
         f3 v0 = ld3(S.positions + 3 * T.x), v1 = ld3(S.positions + 3 * T.y), v2 = ld3(S.positions + 3 * T.z);
         f3 n = normalize(cross(v1 - v0, v2 - v0));
         if (n.x != n.x) n = F3(0, 0, 0);
@@ -623,12 +623,12 @@ __device__ void shape_sample(const DevScene& S, uint32_t kind, uint32_t index, f
     }
 }
 // Shape::PDF(interaction, ray) (Shape.cpp:61-67, 303-315; Shape.hpp:151-158)
-__device__ float shape_pdf(const DevScene& S, uint32_t kind, uint32_t index, f3 p, f3 n, f3 ro, f3 rd) {
+__device__ float shape_pdf(uint32_t kind, uint32_t index, f3 p, f3 n, f3 ro, f3 rd) {
     f3 to = p - ro;
     // Shape::PDF's dot(to, to): x product fused, y rounded (fixture search)
     float d2 = fma_(to.z, to.z, fma_(to.x, to.x, rmul(to.y, to.y)));
     float lc = fabsf(dot(-rd, n));
-    float area = shape_area(S, kind, index);
+    float area = shape_area(kind, index);
     if (kind == PT_PRIM_QUAD) {
         if (area == 0) return 0;
     } else if (kind == PT_PRIM_SPHERE) {
@@ -647,7 +647,7 @@ __device__ __forceinline__ f3 inf_le(const pt_light& l, f3 d) {
     }
     return ld3(l.color);
 }
-__device__ LSample light_sample(const DevScene& S, const pt_light& l, float u0, float u1) {
+__device__ LSample light_sample(const pt_light& l, float u0, float u1) {
     LSample ls;
     ls.L = F3(0, 0, 0);
     ls.p = F3(0, 0, 0);
@@ -657,7 +657,7 @@ __device__ LSample light_sample(const DevScene& S, const pt_light& l, float u0, 
     if (l.kind == PT_LIGHT_AREA) {  // AreaLight::sample (Light.cpp:261-263)
         const DevPrimInfo& pi = S.info[l.prim];
         uint32_t kind = __float_as_uint(S.geom[l.prim].a.w) & GF_KIND;
-        shape_sample(S, kind, pi.index, u0, u1, ls);
+        shape_sample(kind, pi.index, u0, u1, ls);
         return ls;
     }
     if (l.kind == PT_LIGHT_POINT) {  // Light.cpp:236-238
@@ -688,21 +688,21 @@ __device__ __forceinline__ bool light_is_delta(const pt_light& l) {
     return l.kind == PT_LIGHT_DISTANT || l.kind == PT_LIGHT_POINT;
 }
 // Light::PDF(interaction, ray)
-__device__ float light_pdf(const DevScene& S, const pt_light& l, f3 p, f3 n, f3 ro, f3 rd) {
+__device__ float light_pdf(const pt_light& l, f3 p, f3 n, f3 ro, f3 rd) {
     if (l.kind == PT_LIGHT_AREA) {  // Light.cpp:267-272
         uint32_t kind = __float_as_uint(S.geom[l.prim].a.w) & GF_KIND;
         uint32_t index = S.info[l.prim].index;
-        if (l.one_sided) return dot(-rd, n) > 0 ? shape_pdf(S, kind, index, p, n, ro, rd) : 0;
-        return shape_pdf(S, kind, index, p, n, ro, rd);
+        if (l.one_sided) return dot(-rd, n) > 0 ? shape_pdf(kind, index, p, n, ro, rd) : 0;
+        return shape_pdf(kind, index, p, n, ro, rd);
     }
     if (l.kind == PT_LIGHT_UNIFORM_INF || l.kind == PT_LIGHT_SKY_INF) return 1.0f / (4.0f * PT_PI);
     return 0;
 }
 // Light::L(interaction, ray)
-__device__ f3 light_L(const DevScene& S, const pt_light& l, f3 n, float u, float v, f3 rd) {
+__device__ f3 light_L(const pt_light& l, f3 n, float u, float v, f3 rd) {
     if (l.kind == PT_LIGHT_AREA) {  // Light.cpp:257-260
         if (l.one_sided && dot(rd, n) > 0) return F3(0, 0, 0);
-        return tex_eval(S, l.tex, u, v);
+        return tex_eval(l.tex, u, v);
     }
     if (l.kind == PT_LIGHT_UNIFORM_INF || l.kind == PT_LIGHT_SKY_INF) return inf_le(l, rd);
     return F3(0, 0, 0);
@@ -710,7 +710,7 @@ __device__ f3 light_L(const DevScene& S, const pt_light& l, f3 n, float u, float
 // LightSampler::Sample (LightSampler.cpp:7-11, 34-46); the power sampler's
 // linear scan becomes a binary search for the first running sum >= u*total
 // over the same float running sums (identical pick for every u).
-__device__ int ls_sample(const DevScene& S, float u) {
+__device__ int ls_sample(float u) {
     uint32_t n = S.n_sampler_lights;
     if (n == 0) return -1;
     if (S.light_sampler == PT_LS_UNIFORM) {

@@ -107,18 +107,18 @@ __device__ __forceinline__ f3 inv_dir(f3 d) {  // Ray ctor (Ray.hpp:32-35)
 }
 
 // Candidate uv for the alpha test on an alpha-tested triangle (rare path).
-__device__ __noinline__ bool tri_alpha(const DevScene& S, uint32_t slot, float bu, float bv, f3 o, f3 d) {
+__device__ __noinline__ bool tri_alpha(uint32_t slot, float bu, float bv, f3 o, f3 d) {
     const DevPrimInfo pi = S.info[slot];
     uint4 T = S.tri[pi.index];
     float u = bu, v = bv, w = 1.0f - u - v;
     // the uv TriangleShape::Intersect computes (same contraction as tri_interaction)
     float tu = lerp3f(u, S.uvs[2 * T.y], v, S.uvs[2 * T.z], w, S.uvs[2 * T.x]);
     float tv = lerp3f(u, S.uvs[2 * T.y + 1], v, S.uvs[2 * T.z + 1], w, S.uvs[2 * T.x + 1]);
-    return mat_alpha(S, pi.material, tu, tv, o, d, (int)slot);
+    return mat_alpha(pi.material, tu, tv, o, d, (int)slot);
 }
 
 // Rare primitive kinds (quad / sphere), closest hit.  Returns accepted hit.
-__device__ __noinline__ bool other_closest(const DevScene& S, uint32_t slot, uint32_t w0, f3 o, f3 d, float tmax,
+__device__ __noinline__ bool other_closest(uint32_t slot, uint32_t w0, f3 o, f3 d, float tmax,
                                            float& t, float& b1, float& b2) {
     const DevPrimInfo pi = S.info[slot];
     float a = 0, b = 0;
@@ -134,12 +134,12 @@ __device__ __noinline__ bool other_closest(const DevScene& S, uint32_t slot, uin
         }
     }
     if (!hit) return false;
-    if ((w0 & GF_ALPHA) && !mat_alpha(S, pi.material, a, b, o, d, (int)slot)) return false;
+    if ((w0 & GF_ALPHA) && !mat_alpha(pi.material, a, b, o, d, (int)slot)) return false;
     b1 = a;
     b2 = b;
     return true;
 }
-__device__ __noinline__ bool other_pred(const DevScene& S, uint32_t slot, uint32_t w0, f3 o, f3 d, float tmax) {
+__device__ __noinline__ bool other_pred(uint32_t slot, uint32_t w0, f3 o, f3 d, float tmax) {
     const DevPrimInfo pi = S.info[slot];
     float t, a = 0, b = 0;
     bool hit;
@@ -154,7 +154,7 @@ __device__ __noinline__ bool other_pred(const DevScene& S, uint32_t slot, uint32
         }
     }
     if (!hit) return false;
-    if ((w0 & GF_PRED_GLM) && (w0 & GF_ALPHA)) return mat_alpha(S, pi.material, a, b, o, d, (int)slot);
+    if ((w0 & GF_PRED_GLM) && (w0 & GF_ALPHA)) return mat_alpha(pi.material, a, b, o, d, (int)slot);
     return true;
 }
 
@@ -188,7 +188,7 @@ __device__ __forceinline__ void slab4(const DevCluster* __restrict__ node, f3 o,
 
 // Closest hit.  Returns prim slot or -1; t, b1, b2 of the accepted hit.
 template <bool COUNT>
-__device__ int trace_closest(const DevScene& S, f3 o, f3 d, float tmax, float& t_out, float& b1_out, float& b2_out,
+__device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out, float& b2_out,
                              uint32_t* s_ref, TraceWork& wk) {
     const uint32_t lane = threadIdx.x;
     const f3 inv = inv_dir(d);
@@ -244,7 +244,7 @@ __device__ int trace_closest(const DevScene& S, f3 o, f3 d, float tmax, float& t
             if (kind == PT_PRIM_TRIANGLE) {
                 float bx, by, t;
                 if (tri_glm(o, d, xyz(g.a), xyz(g.b), xyz(g.c), bx, by, t) && !(t > tmax || t < PT_EPS)) {
-                    if (!(w0 & GF_ALPHA) || tri_alpha(S, slot, bx, by, o, d)) {
+                    if (!(w0 & GF_ALPHA) || tri_alpha(slot, bx, by, o, d)) {
                         tmax = t;
                         best = (int)slot;
                         bb1 = bx;
@@ -259,7 +259,7 @@ __device__ int trace_closest(const DevScene& S, f3 o, f3 d, float tmax, float& t
                 }
             } else {
                 float t, a, b;
-                if (other_closest(S, slot, w0, o, d, tmax, t, a, b)) {
+                if (other_closest(slot, w0, o, d, tmax, t, a, b)) {
                     tmax = t;
                     best = (int)slot;
                     bb1 = a;
@@ -279,7 +279,7 @@ __device__ int trace_closest(const DevScene& S, f3 o, f3 d, float tmax, float& t
 // Any hit (Scene::IntersectPred).  Children pushed in slot order like the
 // reference (BVH.hpp:1099-1102); the last one is visited next without a push.
 template <bool COUNT>
-__device__ bool trace_any(const DevScene& S, f3 o, f3 d, float tmax, uint32_t* s_ref, TraceWork& wk) {
+__device__ bool trace_any(f3 o, f3 d, float tmax, uint32_t* s_ref, TraceWork& wk) {
     const uint32_t lane = threadIdx.x;
     const f3 inv = inv_dir(d);
     int sp = 0;
@@ -326,7 +326,7 @@ __device__ bool trace_any(const DevScene& S, f3 o, f3 d, float tmax, uint32_t* s
                     // material HasAlpha(): full Intersect + Alpha (Primitive.cpp:7-10)
                     float bx, by, t;
                     if (tri_glm(o, d, xyz(g.a), xyz(g.b), xyz(g.c), bx, by, t) && !(t > tmax || t < PT_EPS)) {
-                        if (!(w0 & GF_ALPHA) || tri_alpha(S, slot, bx, by, o, d)) return true;
+                        if (!(w0 & GF_ALPHA) || tri_alpha(slot, bx, by, o, d)) return true;
                     }
                 } else if (tri_pred(o, d, xyz(g.a), xyz(g.b), xyz(g.c), tmax)) {
                     return true;
@@ -337,7 +337,7 @@ __device__ bool trace_any(const DevScene& S, f3 o, f3 d, float tmax, uint32_t* s
                     s_ref[sp * PT_TRACE_BLOCK + lane] = __float_as_uint(g.b.x);
                     ++sp;
                 }
-            } else if (other_pred(S, slot, w0, o, d, tmax)) {
+            } else if (other_pred(slot, w0, o, d, tmax)) {
                 return true;
             }
             if (w0 & GF_LAST) break;
