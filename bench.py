@@ -86,6 +86,8 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--paths-in-flight", type=int, default=0)
+    ap.add_argument("--traversal", choices=("auto", "pool", "simple"), default="auto",
+                    help="BVH traversal kernel (auto: by BVH size)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -111,10 +113,12 @@ def main():
     ctx = integ.context(device)
     ctx.set_stream(torch.cuda.current_stream(device).cuda_stream)
 
+    tflag = {"auto": 0, "pool": N.PT_RENDER_TRAVERSAL_POOL, "simple": N.PT_RENDER_TRAVERSAL_SIMPLE}[args.traversal]
+
     def step(flags=0):
         # this rank's sample shard into the device film, then the RCCL SUM
         # reduce of the film onto rank 0 (pathtracing_amd/distributed.py)
-        return render_frame(integ, film, flags=flags, paths_in_flight=args.paths_in_flight)
+        return render_frame(integ, film, flags=flags | tflag, paths_in_flight=args.paths_in_flight)
 
     for _ in range(args.warmup):
         step()

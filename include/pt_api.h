@@ -197,6 +197,8 @@ enum { PT_INTEGRATOR_PATH = 0, PT_INTEGRATOR_SIMPLE = 1 };
 enum { PT_FILTER_MITCHELL = 0, PT_FILTER_BOX = 1, PT_FILTER_GAUSSIAN = 2 };
 #define PT_RENDER_COUNT_NODES 0x1u  /* instrumented traversal: node/tri counts */
 #define PT_RENDER_TIMING 0x2u       /* per-kernel HIP-event timing into stats   */
+#define PT_RENDER_TRAVERSAL_POOL 0x4u   /* force the persistent refilling traversal */
+#define PT_RENDER_TRAVERSAL_SIMPLE 0x8u /* force one ray per lane (default: by BVH size) */
 
 typedef struct pt_render_desc {
     uint32_t integrator;       /* PT_INTEGRATOR_*                               */

@@ -61,9 +61,84 @@ __device__ __forceinline__ void count_add(unsigned long long* counters, int whic
 }
 
 // ------------------------------------------------------------------ traversal kernels
+// Persistent, refilling traversal (pt_pool.h): grid = resident blocks, rays
+// claimed from the pool counters (zeroed with the queue counters).
+struct ClosestSrc {
+    PathSoA P;
+    float4* hit;
+    __device__ __forceinline__ bool load(uint32_t i, f3& o, f3& d, float& tmax) {
+        o = xyz(P.o[i]);
+        d = xyz(P.d[i]);
+        tmax = __int_as_float(0x7f800000);
+        return true;
+    }
+    __device__ __forceinline__ void closest(uint32_t i, float t, float b1, float b2, int prim) {
+        hit[i] = make_float4(t, b1, b2, __int_as_float(prim));
+    }
+    __device__ __forceinline__ void any(uint32_t, bool) {}
+};
+
+template <bool COUNT>
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest_pool(PathSoA P, uint32_t n, float4* __restrict__ hit,
+                                                                uint32_t* __restrict__ pool,
+                                                                unsigned long long* counters) {
+    __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+    TraceWork wk{0, 0};
+    ClosestSrc src{P, hit};
+    trace_pool<false, COUNT>(n, pool, src, s_ref, wk);
+    if (COUNT) {
+        count_add(counters, CNT_NODES_CLOSEST, wk.nodes);
+        count_add(counters, CNT_TRIS_CLOSEST, wk.tris);
+    }
+}
+
+struct ShadowSrc {
+    const ShadowRec* sq;
+    PathSoA next;
+    float4* done_L;
+    __device__ __forceinline__ bool load(uint32_t i, f3& o, f3& d, float& tmax) {
+        const float4 ro = sq[i].o, rd = sq[i].d;
+        o = xyz(ro);
+        d = xyz(rd);
+        tmax = ro.w;
+        return true;
+    }
+    __device__ __forceinline__ void closest(uint32_t, float, float, float, int) {}
+    __device__ __forceinline__ void any(uint32_t i, bool hit) {
+        if (hit) return;
+        // unoccluded: add the contribution; one shadow ray per path per bounce,
+        // so a plain read-modify-write
+        const uint32_t tgt = __float_as_uint(sq[i].d.w);
+        const float4 c = sq[i].c;
+        float4* L = (tgt & SHADOW_DONE_BIT) ? &done_L[tgt & ~SHADOW_DONE_BIT] : &next.L[tgt];
+        float4 v = *L;
+        v.x += c.x;
+        v.y += c.y;
+        v.z += c.z;
+        *L = v;
+    }
+};
+
+template <bool COUNT>
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow_pool(PathSoA next, float4* __restrict__ done_L,
+                                                               const ShadowRec* __restrict__ sq,
+                                                               const uint32_t* __restrict__ nptr,
+                                                               uint32_t* __restrict__ pool, unsigned long long* counters) {
+    __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+    TraceWork wk{0, 0};
+    ShadowSrc src{sq, next, done_L};
+    trace_pool<true, COUNT>(*nptr, pool, src, s_ref, wk);
+    if (COUNT) {
+        count_add(counters, CNT_NODES_ANY, wk.nodes);
+        count_add(counters, CNT_TRIS_ANY, wk.tris);
+    }
+}
+
+// One ray per lane (grid covers all rays): lower overhead where traversal
+// lengths are uniform (small scenes); the runtime picks per scene.
 template <bool COUNT>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(PathSoA P, uint32_t n, float4* __restrict__ hit,
-                                                           unsigned long long* counters) {
+                                                           uint32_t* __restrict__, unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     TraceWork wk{0, 0};
@@ -82,24 +157,16 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(PathSoA P, uint32_t 
 template <bool COUNT>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(PathSoA next, float4* __restrict__ done_L,
                                                           const ShadowRec* __restrict__ sq,
-                                                          const uint32_t* __restrict__ nptr,
+                                                          const uint32_t* __restrict__ nptr, uint32_t* __restrict__,
                                                           unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
     const uint32_t n = *nptr;
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     TraceWork wk{0, 0};
     if (i < n) {
+        ShadowSrc src{sq, next, done_L};
         const ShadowRec r = sq[i];
-        if (!trace_any<COUNT>(xyz(r.o), xyz(r.d), r.o.w, s_ref, wk)) {
-            // one shadow ray per path per bounce: a plain read-modify-write
-            const uint32_t tgt = __float_as_uint(r.d.w);
-            float4* L = (tgt & SHADOW_DONE_BIT) ? &done_L[tgt & ~SHADOW_DONE_BIT] : &next.L[tgt];
-            float4 v = *L;
-            v.x += r.c.x;
-            v.y += r.c.y;
-            v.z += r.c.z;
-            *L = v;
-        }
+        src.any(i, trace_any<COUNT>(xyz(r.o), xyz(r.d), r.o.w, s_ref, wk));
     }
     if (COUNT) {
         count_add(counters, CNT_NODES_ANY, wk.nodes);
@@ -107,25 +174,31 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(PathSoA next, float4*
     }
 }
 
-// Test hook: trace arbitrary rays (pt_trace).
-__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(const pt_ray* __restrict__ rays, uint32_t n,
-                                                              int any, pt_hit* __restrict__ out,
+// Test hook: trace arbitrary rays (pt_trace), through the product traversal.
+struct RaysSrc {
+    const pt_ray* rays;
+    pt_hit* out;
+    __device__ __forceinline__ bool load(uint32_t i, f3& o, f3& d, float& tmax) {
+        const pt_ray r = rays[i];
+        o = F3(r.o[0], r.o[1], r.o[2]);
+        d = F3(r.d[0], r.d[1], r.d[2]);
+        tmax = r.tmax;
+        return true;
+    }
+    __device__ __forceinline__ void closest(uint32_t i, float t, float b1, float b2, int prim) {
+        out[i] = pt_hit{t, b1, b2, prim};
+    }
+    __device__ __forceinline__ void any(uint32_t i, bool hit) { out[i] = pt_hit{0, 0, 0, hit ? 1 : 0}; }
+};
+
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(const pt_ray* __restrict__ rays, uint32_t n, int any,
+                                                              pt_hit* __restrict__ out, uint32_t* __restrict__ pool,
                                                               unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
-    const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     TraceWork wk{0, 0};
-    if (i < n) {
-        const pt_ray r = rays[i];
-        f3 o = F3(r.o[0], r.o[1], r.o[2]), d = F3(r.d[0], r.d[1], r.d[2]);
-        pt_hit h;
-        if (any) {
-            h.prim = trace_any<true>(o, d, r.tmax, s_ref, wk) ? 1 : 0;
-            h.t = h.b1 = h.b2 = 0;
-        } else {
-            h.prim = trace_closest<true>(o, d, r.tmax, h.t, h.b1, h.b2, s_ref, wk);
-        }
-        out[i] = h;
-    }
+    RaysSrc src{rays, out};
+    if (any) trace_pool<true, true>(n, pool, src, s_ref, wk);
+    else trace_pool<false, true>(n, pool, src, s_ref, wk);
     count_add(counters, any ? CNT_NODES_ANY : CNT_NODES_CLOSEST, wk.nodes);
     count_add(counters, any ? CNT_TRIS_ANY : CNT_TRIS_CLOSEST, wk.tris);
 }
@@ -593,12 +666,18 @@ __global__ __launch_bounds__(256) void k_gather(RenderParams R, const float* __r
 }
 
 // explicit instantiations used by the runtime
-template __global__ void k_closest<false>(PathSoA, uint32_t, float4*, unsigned long long*);
-template __global__ void k_closest<true>(PathSoA, uint32_t, float4*, unsigned long long*);
-template __global__ void k_shadow<false>(PathSoA, float4*, const ShadowRec*, const uint32_t*,
+template __global__ void k_closest<false>(PathSoA, uint32_t, float4*, uint32_t*, unsigned long long*);
+template __global__ void k_closest<true>(PathSoA, uint32_t, float4*, uint32_t*, unsigned long long*);
+template __global__ void k_closest_pool<false>(PathSoA, uint32_t, float4*, uint32_t*, unsigned long long*);
+template __global__ void k_closest_pool<true>(PathSoA, uint32_t, float4*, uint32_t*, unsigned long long*);
+template __global__ void k_shadow<false>(PathSoA, float4*, const ShadowRec*, const uint32_t*, uint32_t*,
                                          unsigned long long*);
-template __global__ void k_shadow<true>(PathSoA, float4*, const ShadowRec*, const uint32_t*,
+template __global__ void k_shadow<true>(PathSoA, float4*, const ShadowRec*, const uint32_t*, uint32_t*,
                                         unsigned long long*);
+template __global__ void k_shadow_pool<false>(PathSoA, float4*, const ShadowRec*, const uint32_t*, uint32_t*,
+                                              unsigned long long*);
+template __global__ void k_shadow_pool<true>(PathSoA, float4*, const ShadowRec*, const uint32_t*, uint32_t*,
+                                             unsigned long long*);
 template __global__ void k_shade<PT_INTEGRATOR_PATH>(RenderParams, PathSoA, uint32_t, const float4*, PathSoA,
                                                      float4*, uint32_t*, ShadowRec*, uint32_t*);
 template __global__ void k_shade<PT_INTEGRATOR_SIMPLE>(RenderParams, PathSoA, uint32_t, const float4*,

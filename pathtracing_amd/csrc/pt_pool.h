@@ -1,0 +1,202 @@
+// Persistent BVH4 traversal with per-lane ray refill.
+//
+// Incoherent secondary rays make per-lane traversal lengths vary by an order
+// of magnitude, so a wave that traces exactly its 64 rays runs as long as its
+// longest one.  Here a resident wave keeps pulling rays: whenever at least
+// PT_REFILL of its lanes are idle, it claims that many rays with one atomic
+// on a pool counter and the idle lanes start them, so lanes stay busy until
+// the pool drains.  The ray range is split into
+// PT_POOL_CHUNKS chunks with one counter each (own 128-byte line); a block starts on chunk
+// blockIdx % 8 (its XCD under round-robin dispatch) and moves to the next
+// non-empty chunk when its own runs dry, so no single counter line takes every
+// claim (MI355X_MICROARCH.md "dequeue": one word saturates near 88 claims/us).
+//
+// Each step advances a lane by one pop, one interior cluster or one leaf, with
+// the exact semantics of trace_closest / trace_any (pt_trace.h): same octant
+// child order, same leaf tests, so results are identical to the one-ray-per-
+// lane kernels; only the assignment of rays to lanes changes.
+#pragma once
+#include "pt_trace.h"
+
+#define PT_POOL_CHUNKS 8
+#define PT_POOL_STRIDE 32  // uint32 words between chunk counters (128 B)
+#define PT_POOL_WORDS (PT_POOL_CHUNKS * PT_POOL_STRIDE)
+#ifndef PT_REFILL
+#define PT_REFILL 8
+#endif
+
+// Src interface:
+//   bool load(uint32_t ri, f3& o, f3& d, float& tmax)   (false: skip this ray)
+//   void closest(uint32_t ri, float t, float b1, float b2, int prim)
+//   void any(uint32_t ri, bool hit)
+template <bool ANY, bool COUNT, class Src>
+__device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, uint32_t* s_ref, TraceWork& wk) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t wl = __lane_id();
+    const uint32_t cs = (n + PT_POOL_CHUNKS - 1) / PT_POOL_CHUNKS;
+    const uint32_t home = blockIdx.x % PT_POOL_CHUNKS;
+    uint32_t dead = 0;  // wave-uniform: chunks found empty
+
+    int ri = -1;
+    f3 o = F3(0, 0, 0), d = F3(0, 0, 0), inv = F3(0, 0, 0);
+    uint32_t oct = 0, ref = REF_EMPTY;
+    float tmax = 0, bb1 = 0, bb2 = 0;
+    int sp = 0, best = -1;
+
+    const uint32_t all_dead = (1u << PT_POOL_CHUNKS) - 1u;
+    for (;;) {
+        const uint64_t idle = __ballot(ri < 0);
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+        if (nidle >= PT_REFILL || idle == __ballot(true)) {
+            // claim exactly as many rays as lanes are idle (one atomic) from the
+            // home chunk or the next non-empty one; no reserve is held, so no
+            // wave sits on unstarted rays while others run dry
+            uint32_t base = 0, got = 0;
+            if (dead != all_dead) {
+                if (wl == 0) {
+                    for (uint32_t k = 0; k < PT_POOL_CHUNKS; k++) {
+                        const uint32_t c = (home + k) % PT_POOL_CHUNKS;
+                        if ((dead >> c) & 1u) continue;
+                        const uint32_t lo = c * cs, hi = min(n, lo + cs);
+                        const uint32_t old = lo < hi ? atomicAdd(&pool[c * PT_POOL_STRIDE], nidle) : hi;
+                        if (lo + old < hi) {
+                            base = lo + old;
+                            got = min(nidle, hi - base);
+                            break;
+                        }
+                        dead |= 1u << c;
+                    }
+                }
+                base = __builtin_amdgcn_readfirstlane(base);
+                got = __builtin_amdgcn_readfirstlane(got);
+                dead = __builtin_amdgcn_readfirstlane(dead);
+                if (ri < 0) {
+                    const uint32_t k = (uint32_t)__popcll(idle & ((1ull << wl) - 1ull));
+                    if (k < got) {
+                        ri = (int)(base + k);
+                        if (src.load((uint32_t)ri, o, d, tmax)) {
+                            inv = inv_dir(d);
+                            oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
+                            ref = S.root;
+                            sp = 0;
+                            best = -1;
+                            bb1 = bb2 = 0;
+                        } else {
+                            ri = -1;
+                        }
+                    }
+                }
+            }
+            if (got == 0 && dead == all_dead && __ballot(ri >= 0) == 0) break;
+        }
+        if (ri < 0) continue;
+
+        // ---- one step of this lane's traversal
+        if (ref == REF_EMPTY) {
+            if (sp == 0) {  // finished: no hit (any) / closest result
+                if (ANY) src.any((uint32_t)ri, false);
+                else src.closest((uint32_t)ri, tmax, bb1, bb2, best);
+                ri = -1;
+                continue;
+            }
+            --sp;
+            ref = s_ref[sp * PT_TRACE_BLOCK + lane];
+        }
+        if (!(ref & REF_LEAF)) {
+            const DevCluster* node = S.nodes + ref;
+            if (COUNT) wk.nodes++;
+            uint32_t mask;
+            float te[4];
+            slab4<COUNT>(node, o, inv, tmax, mask, te);
+            const uint4 ch = *reinterpret_cast<const uint4*>(&node->child[0]);
+            uint32_t cand = REF_EMPTY;
+            if (ANY) {
+                // slot order, last visited next (BVH.hpp:1099-1102)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    if ((mask >> i) & 1u) {
+                        const uint32_t c = sel4u((uint32_t)i, ch);
+                        if (c != REF_EMPTY) {
+                            if (cand != REF_EMPTY && sp < PT_STACK) {
+                                s_ref[sp * PT_TRACE_BLOCK + lane] = cand;
+                                ++sp;
+                            }
+                            cand = c;
+                        }
+                    }
+                }
+            } else {
+                // octant order far -> near (BVH4::LUT, BVH.hpp:1195-1204)
+                const uint32_t ow = node->order[oct >> 2];
+                const uint32_t perm = (ow >> (8 * (oct & 3))) & 0xFFu;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t idx = (perm >> (2 * k)) & 3u;
+                    if ((mask >> idx) & 1u) {
+                        const uint32_t c = sel4u(idx, ch);
+                        if (c != REF_EMPTY) {
+                            if (cand != REF_EMPTY && sp < PT_STACK) {
+                                s_ref[sp * PT_TRACE_BLOCK + lane] = cand;
+                                ++sp;
+                            }
+                            cand = c;
+                        }
+                    }
+                }
+            }
+            ref = cand;
+            continue;
+        }
+        // leaf: primitives from slot until the one flagged LAST
+        uint32_t slot = ref & ~REF_LEAF;
+        ref = REF_EMPTY;
+        bool anyhit = false;
+        for (;;) {
+            const DevGeom g = S.geom[slot];
+            const uint32_t w0 = __float_as_uint(g.a.w);
+            const uint32_t kind = w0 & GF_KIND;
+            if (COUNT) wk.tris++;
+            if (kind == PT_PRIM_TRIANGLE) {
+                if (ANY && !(w0 & GF_PRED_GLM)) {
+                    if (tri_pred(o, d, xyz(g.a), xyz(g.b), xyz(g.c), tmax)) anyhit = true;
+                } else {
+                    float bx, by, t;
+                    if (tri_glm(o, d, xyz(g.a), xyz(g.b), xyz(g.c), bx, by, t) && !(t > tmax || t < PT_EPS)) {
+                        if (!(w0 & GF_ALPHA) || tri_alpha(slot, bx, by, o, d)) {
+                            if (ANY) {
+                                anyhit = true;
+                            } else {
+                                tmax = t;
+                                best = (int)slot;
+                                bb1 = bx;
+                                bb2 = by;
+                            }
+                        }
+                    }
+                }
+            } else if (kind == PT_PRIM_BLAS) {
+                if (COUNT) wk.tris--;
+                if (sp < PT_STACK) {
+                    s_ref[sp * PT_TRACE_BLOCK + lane] = __float_as_uint(g.b.x);
+                    ++sp;
+                }
+            } else if (ANY) {
+                if (other_pred(slot, w0, o, d, tmax)) anyhit = true;
+            } else {
+                float t, a, b;
+                if (other_closest(slot, w0, o, d, tmax, t, a, b)) {
+                    tmax = t;
+                    best = (int)slot;
+                    bb1 = a;
+                    bb2 = b;
+                }
+            }
+            if (anyhit || (w0 & GF_LAST)) break;
+            ++slot;
+        }
+        if (ANY && anyhit) {  // early exit (BVH.hpp:1104-1105)
+            src.any((uint32_t)ri, true);
+            ri = -1;
+        }
+    }
+}

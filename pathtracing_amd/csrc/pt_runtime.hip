@@ -28,6 +28,8 @@ struct pt_ctx {
     DevScene scene{};
     bool has_scene = false;
     uint32_t n_materials = 0;
+    uint32_t trace_blocks = 0;  // resident traversal blocks on this device (persistent grid)
+    uint64_t n_clusters = 0;    // BVH clusters of the uploaded scene (traversal choice)
     // wavefront buffers: two compacted path states (ping-pong), per-bounce hits,
     // the finished-path list and the shadow-ray queue
     uint32_t cap = 0;
@@ -93,6 +95,17 @@ extern "C" pt_status pt_create(pt_ctx** out, int device) {
             delete c;
             return PT_ERR_HIP;
         }
+    }
+    {
+        int cus = 0, per_cu = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_closest<false>),
+                                                         PT_TRACE_BLOCK, 0) != hipSuccess) {
+            g_err = "occupancy query failed";
+            delete c;
+            return PT_ERR_HIP;
+        }
+        c->trace_blocks = (uint32_t)std::max(1, cus * std::max(1, per_cu));
     }
     if (hipHostMalloc((void**)&c->host_cnt, Q_WORDS * 4) != hipSuccess) {
         g_err = "pinned alloc failed";
@@ -401,6 +414,7 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
     DS.n_infinite_lights = s->n_infinite_lights;
     c->has_scene = true;
     c->n_materials = s->n_materials;
+    c->n_clusters = nodes.size();
     return PT_OK;
 }
 
@@ -446,7 +460,7 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
     AL(c->hit, n * 16);
     AL(c->done_L, n * 16);
     AL(c->done_sid, n * 4);
-    AL(c->qcnt, Q_WORDS * 4);
+    AL(c->qcnt, (Q_WORDS + 3 * PT_POOL_WORDS) * 4);  // queue counters, then the traversal pools
     AL(c->sq, n * sizeof(ShadowRec));
     AL(c->counters, (CNT_SHARDS + 1) * CNT_COUNT * 8);
 #undef AL
@@ -464,6 +478,8 @@ static double gauss_h(double x, double sigma) {
 // chunk's per-sample radiance to `on_chunk`.
 // Makes this context's scene the one the kernels read (constant-memory `S`),
 // ordered on the context's stream.  Called by every entry point that launches.
+#define PT_POOL_MIN_CLUSTERS (1u << 20)  // measured: C4 (2.6M clusters) gains 31%; 0.5M-cluster heightfield and C2/C3 lose
+
 static pt_status bind_scene(pt_ctx* c) {
     HIPCHK(c, hipMemcpyToSymbolAsync(HIP_SYMBOL(S), &c->scene, sizeof(DevScene), 0, hipMemcpyHostToDevice, c->stream));
     return PT_OK;
@@ -526,6 +542,11 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     if ((st = ensure_work(c, paths)) != PT_OK) return st;
 
     const bool count = (rd->flags & PT_RENDER_COUNT_NODES) != 0;
+    // traversal variant: pool (persistent, refilling) for deep trees where ray
+    // lengths diverge, one ray per lane for small ones; flags override
+    const bool use_pool = (rd->flags & PT_RENDER_TRAVERSAL_POOL)     ? true
+                          : (rd->flags & PT_RENDER_TRAVERSAL_SIMPLE) ? false
+                                                                     : c->n_clusters >= PT_POOL_MIN_CLUSTERS;
     const bool timing = (rd->flags & PT_RENDER_TIMING) != 0;
     hipStream_t sm = c->stream;
     HIPCHK(c, hipMemsetAsync(c->counters, 0, (CNT_SHARDS + 1) * CNT_COUNT * 8, sm));
@@ -554,15 +575,20 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         HIPCHK(c, hipStreamSynchronize(sm));
         uint32_t n_active = c->host_cnt[Q_NEXT];
         while (n_active > 0) {
-            HIPCHK(c, hipMemsetAsync(c->qcnt, 0, Q_WORDS * 4, sm));
-            const dim3 gt((n_active + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK), gs((n_active + 255) / 256);
+            HIPCHK(c, hipMemsetAsync(c->qcnt, 0, (Q_WORDS + 2 * PT_POOL_WORDS) * 4, sm));
+            // pool traversal: at most the resident blocks, rays claimed from the
+            // pools; simple traversal: one ray per lane
+            const uint32_t nb = (n_active + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK;
+            const dim3 gt(use_pool ? std::max(1u, std::min(nb, c->trace_blocks)) : nb), gs((n_active + 255) / 256);
+            uint32_t* pool_closest = c->qcnt + Q_WORDS;
+            uint32_t* pool_shadow = c->qcnt + Q_WORDS + PT_POOL_WORDS;
             if (timing) HIPCHK(c, hipEventRecord(c->ev[0], sm));
-            if (count)
-                hipLaunchKernelGGL(k_closest<true>, gt, dim3(PT_TRACE_BLOCK), 0, sm, cur, n_active, c->hit,
+            {
+                auto kc = use_pool ? (count ? k_closest_pool<true> : k_closest_pool<false>)
+                                   : (count ? k_closest<true> : k_closest<false>);
+                hipLaunchKernelGGL(kc, gt, dim3(PT_TRACE_BLOCK), 0, sm, cur, n_active, c->hit, pool_closest,
                                    c->counters);
-            else
-                hipLaunchKernelGGL(k_closest<false>, gt, dim3(PT_TRACE_BLOCK), 0, sm, cur, n_active, c->hit,
-                                   c->counters);
+            }
             if (timing) HIPCHK(c, hipEventRecord(c->ev[1], sm));
             if (rd->integrator == PT_INTEGRATOR_SIMPLE)
                 hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_SIMPLE>, gs, dim3(256), 0, sm, R, cur, n_active,
@@ -572,12 +598,10 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                                    (const float4*)c->hit, nxt, c->done_L, c->done_sid, c->sq, c->qcnt);
             if (timing) HIPCHK(c, hipEventRecord(c->ev[2], sm));
             if (rd->integrator != PT_INTEGRATOR_SIMPLE) {
-                if (count)
-                    hipLaunchKernelGGL(k_shadow<true>, gt, dim3(PT_TRACE_BLOCK), 0, sm, nxt, c->done_L,
-                                       (const ShadowRec*)c->sq, (const uint32_t*)(c->qcnt + Q_SHADOW), c->counters);
-                else
-                    hipLaunchKernelGGL(k_shadow<false>, gt, dim3(PT_TRACE_BLOCK), 0, sm, nxt, c->done_L,
-                                       (const ShadowRec*)c->sq, (const uint32_t*)(c->qcnt + Q_SHADOW), c->counters);
+                auto ks = use_pool ? (count ? k_shadow_pool<true> : k_shadow_pool<false>)
+                                   : (count ? k_shadow<true> : k_shadow<false>);
+                hipLaunchKernelGGL(ks, gt, dim3(PT_TRACE_BLOCK), 0, sm, nxt, c->done_L, (const ShadowRec*)c->sq,
+                                   (const uint32_t*)(c->qcnt + Q_SHADOW), pool_shadow, c->counters);
             }
             if (timing) HIPCHK(c, hipEventRecord(c->ev[3], sm));
             hipLaunchKernelGGL(k_finish, gs, dim3(256), 0, sm, R, (const float4*)c->done_L,
@@ -735,8 +759,11 @@ extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any
     HIPCHK(c, hipMemsetAsync(c->counters, 0, CNT_SHARDS * CNT_COUNT * 8, c->stream));
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
-    hipLaunchKernelGGL(k_trace_rays, dim3((n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK), dim3(PT_TRACE_BLOCK), 0,
-                       c->stream, dr, n, any_hit, dh, c->counters);
+    uint32_t* pool = c->qcnt + Q_WORDS + 2 * PT_POOL_WORDS;
+    HIPCHK(c, hipMemsetAsync(pool, 0, PT_POOL_WORDS * 4, c->stream));
+    hipLaunchKernelGGL(k_trace_rays,
+                       dim3(std::max(1u, std::min((n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK, c->trace_blocks))),
+                       dim3(PT_TRACE_BLOCK), 0, c->stream, dr, n, any_hit, dh, pool, c->counters);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
     if (!hdev) HIPCHK(c, hipMemcpyAsync(hits, dh, (size_t)n * sizeof(pt_hit), hipMemcpyDeviceToHost, c->stream));

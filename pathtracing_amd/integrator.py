@@ -194,14 +194,14 @@ class Integrator:
         return self.last_stats
 
     def RenderSamples(self, pixel_begin: int = 0, pixel_end: int = 0, spp: Optional[int] = None,
-                      device: int = 0) -> np.ndarray:
+                      device: int = 0, flags: int = 0) -> np.ndarray:
         """Per-sample Li for pixels [pixel_begin, pixel_end): (npix, spp, 3) float32."""
         ctx = self.context(device)
         W, H = self.camera.GetFilm().Resolution()
         if pixel_begin == 0 and pixel_end == 0:
             pixel_end = W * H
         kw = {} if spp is None else {"spp": spp}
-        cam, rd = self.desc(pixel_begin=pixel_begin, pixel_end=pixel_end, **kw)
+        cam, rd = self.desc(pixel_begin=pixel_begin, pixel_end=pixel_end, flags=flags, **kw)
         out, self.last_stats = ctx.render_samples(cam, rd, pixel_end - pixel_begin)
         return out
 

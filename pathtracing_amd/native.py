@@ -25,6 +25,8 @@ PT_INTEGRATOR_PATH, PT_INTEGRATOR_SIMPLE = 0, 1
 PT_FILTER_MITCHELL, PT_FILTER_BOX, PT_FILTER_GAUSSIAN = 0, 1, 2
 PT_RENDER_COUNT_NODES = 0x1
 PT_RENDER_TIMING = 0x2
+PT_RENDER_TRAVERSAL_POOL = 0x4
+PT_RENDER_TRAVERSAL_SIMPLE = 0x8
 
 # ---- numpy mirrors of the array element structs (layouts asserted below) ----
 REF_NODE = np.dtype([("count", "u1"), ("active", "u1"), ("perm", "u1"), ("pad", "u1"), ("cluster_idx", "<u4")])

@@ -251,3 +251,13 @@ def test_gpu_light_samples_match_oracle_and_reference(case):
         r = r[:g.shape[0]]
     close = np.isclose(g.reshape(-1, 18), r.reshape(-1, 18), rtol=1e-4, atol=1e-5, equal_nan=True).all(1)
     assert close.mean() >= 0.99
+
+
+@pytest.mark.parametrize("name", ["cornell_c3", "zoo", "sanmiguel"])
+def test_gpu_pool_and_simple_traversal_agree_bit_for_bit(name):
+    """The persistent refilling traversal (pt_pool.h) and the one-ray-per-lane
+    one visit the same nodes in the same order per ray: identical radiance."""
+    setup, integ, fx = load(name)
+    a = integ.RenderSamples(flags=N.PT_RENDER_TRAVERSAL_POOL)
+    b = integ.RenderSamples(flags=N.PT_RENDER_TRAVERSAL_SIMPLE)
+    np.testing.assert_array_equal(a, b)
