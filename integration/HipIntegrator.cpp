@@ -1,0 +1,646 @@
+// HipPathIntegrator / HipSimplePathIntegrator: see HipIntegrator.hpp.
+//
+// Scene export.  The reference keeps most of the state the device needs in
+// private or protected members (BVH4::nodes BVH.hpp:1214-1216, the
+// primitive / material / texture / light fields).  Rather than editing the
+// reference, the exporter reads them through member pointers formed by
+// explicit template instantiation (which the language exempts from access
+// checking); a maintainer merging this into the tree would replace the
+// PT_MEMBER lines with `friend class pt::SceneExport;` declarations.
+#include "HipIntegrator.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <stdexcept>
+#include <thread>
+#include <unordered_map>
+
+#include "BVH.hpp"
+#include "Camera.hpp"
+#include "Film.hpp"
+#include "Filter.hpp"
+#include "Light.hpp"
+#include "LightSampler.hpp"
+#include "Material.hpp"
+#include "Mesh.hpp"
+#include "Primitive.hpp"
+#include "Scene.hpp"
+#include "Shape.hpp"
+#include "Texture.hpp"
+#ifdef PT_WITH_MODEL
+#include "Model.hpp"
+#endif
+#include "pt_api.h"
+
+namespace {
+
+template <class Tag, typename Tag::type M>
+struct Member {
+    friend typename Tag::type get(Tag) { return M; }
+};
+#define PT_MEMBER(NAME, CLASS, TYPE, FIELD)      \
+    struct NAME {                                \
+        using type = TYPE CLASS::*;              \
+        friend type get(NAME);                   \
+    };                                           \
+    template struct Member<NAME, &CLASS::FIELD>
+#define PT_GET(OBJ, NAME) ((OBJ).*get(NAME{}))
+
+using PrimPtr = std::shared_ptr<Primitive>;
+using TexPtr = std::shared_ptr<Texture>;
+using TLASBase = BVHBase<PrimPtr>;
+using BLASBase = BVHBase<GeometricPrimitive>;
+
+PT_MEMBER(SceneBvh, Scene, std::shared_ptr<TLASBase>, scene_bvh);
+PT_MEMBER(TlasNodes, TLAS4, std::vector<BVH4_CLUSTER>, nodes);
+PT_MEMBER(TlasRoot, TLAS4, BVH4_NODE, rootNode);
+PT_MEMBER(TlasPrims, TLASBase, std::vector<PrimPtr>, primitives);
+PT_MEMBER(BlasNodes, BLAS4, std::vector<BVH4_CLUSTER>, nodes);
+PT_MEMBER(BlasRoot, BLAS4, BVH4_NODE, rootNode);
+PT_MEMBER(BlasPrims, BLASBase, std::vector<GeometricPrimitive>, primitives);
+PT_MEMBER(GpShape, GeometricPrimitive, std::shared_ptr<Shape>, shape);
+PT_MEMBER(GpMaterial, GeometricPrimitive, std::shared_ptr<Material>, material);
+PT_MEMBER(GpArea, GeometricPrimitive, std::shared_ptr<AreaLight>, areaLight);
+PT_MEMBER(GpMedium, GeometricPrimitive, std::shared_ptr<Medium>, medium);
+PT_MEMBER(SphCenter, SphereShape, glm::vec3, center);
+PT_MEMBER(SphRadius, SphereShape, float, radius);
+PT_MEMBER(QuadQ, QuadShape, glm::vec3, Q);
+PT_MEMBER(QuadU, QuadShape, glm::vec3, u);
+PT_MEMBER(QuadV, QuadShape, glm::vec3, v);
+PT_MEMBER(QuadN, QuadShape, glm::vec3, normal);
+PT_MEMBER(QuadD, QuadShape, float, D);
+PT_MEMBER(QuadW, QuadShape, glm::vec3, w);
+PT_MEMBER(DifTex, MicrofacetDiffuse, TexPtr, tex);
+PT_MEMBER(DifNorm, MicrofacetDiffuse, TexPtr, norm);
+PT_MEMBER(DifRough, MicrofacetDiffuse, TexPtr, roughnessTexture);
+PT_MEMBER(DifMetal, MicrofacetDiffuse, TexPtr, metallicTexture);
+PT_MEMBER(DifAlpha, MicrofacetDiffuse, TexPtr, alpha);
+PT_MEMBER(DifTester, MicrofacetDiffuse, AlphaTester, alphaTester);
+PT_MEMBER(DieRi, MicrofacetDielectric, float, ri);
+PT_MEMBER(DieTex, MicrofacetDielectric, TexPtr, tex);
+PT_MEMBER(DieNorm, MicrofacetDielectric, TexPtr, norm);
+PT_MEMBER(DieRough, MicrofacetDielectric, TexPtr, roughnessTexture);
+PT_MEMBER(DieAlpha, MicrofacetDielectric, TexPtr, alpha);
+PT_MEMBER(DieTester, MicrofacetDielectric, AlphaTester, alphaTester);
+PT_MEMBER(ThinRi, ThinDielectric, float, ri);
+PT_MEMBER(ThinAlbedo, ThinDielectric, TexPtr, albedo);
+PT_MEMBER(CondAlbedo, SpecularConductor, glm::vec3, albedo);
+PT_MEMBER(TexScale, Texture, glm::vec3, colorScale);
+PT_MEMBER(SolidAlbedo, SolidColor, glm::vec3, albedo);
+PT_MEMBER(ImgTexImage, ImageTexture, Image, image);
+PT_MEMBER(ImgData, Image, unsigned char*, data);
+PT_MEMBER(ImgW, Image, int, width);
+PT_MEMBER(ImgH, Image, int, height);
+PT_MEMBER(ImgC, Image, int, channels);
+PT_MEMBER(ChkA, CheckerTexture, TexPtr, tex1);
+PT_MEMBER(ChkB, CheckerTexture, TexPtr, tex2);
+PT_MEMBER(ChkInv, CheckerTexture, glm::vec2, invScale);
+PT_MEMBER(AreaShape, AreaLight, std::shared_ptr<Shape>, shape);
+PT_MEMBER(AreaTex, AreaLight, TexPtr, emissiveTexture);
+PT_MEMBER(AreaOneSided, AreaLight, bool, oneSided);
+PT_MEMBER(UniColor, UniformInfiniteLight, glm::vec3, color);
+PT_MEMBER(FunFn, FunctionInfiniteLight, std::function<glm::vec3(const Ray&)>, lightFunction);
+PT_MEMBER(DistDir, DistantLight, glm::vec3, dir);
+PT_MEMBER(DistColor, DistantLight, glm::vec3, color);
+PT_MEMBER(PointP, PointLight, glm::vec3, p);
+PT_MEMBER(PointColor, PointLight, glm::vec3, color);
+PT_MEMBER(UlsLights, UniformLightSampler, std::vector<std::shared_ptr<Light>>, lights);
+PT_MEMBER(PlsLights, PowerLightSampler, std::vector<std::shared_ptr<Light>>, lights);
+PT_MEMBER(CamFrom, Camera, glm::vec3, lookFrom);
+PT_MEMBER(CamU, Camera, glm::vec3, u);
+PT_MEMBER(CamV, Camera, glm::vec3, v);
+PT_MEMBER(CamW, Camera, glm::vec3, w);
+PT_MEMBER(CamHW, Camera, float, halfWidth);
+PT_MEMBER(CamHH, Camera, float, halfHeight);
+PT_MEMBER(CamDefocus, Camera, float, defocusRadius);
+PT_MEMBER(CamFocusDist, Camera, float, FocusDistance);
+PT_MEMBER(CamFocusAngle, Camera, float, FocusAngle);
+PT_MEMBER(FilmFilter, Film, std::shared_ptr<Filter>, filter);
+PT_MEMBER(MitB, MitchellFilter, double, b);
+PT_MEMBER(MitC, MitchellFilter, double, c);
+PT_MEMBER(GaussSigma, GaussianFilter, double, sigma);
+#ifdef PT_WITH_MODEL
+PT_MEMBER(ModelBvh, Model, std::shared_ptr<BLASBase>, model_bvh);
+#endif
+
+void check(pt_status st, const char* what, pt_ctx* c = nullptr) {
+    if (st != PT_OK) throw std::runtime_error(std::string(what) + ": " + pt_last_error(c));
+}
+
+void put3(float* d, const glm::vec3& v) {
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+}
+
+// ---------------------------------------------------------------------------
+// Flattened scene (owns every array a pt_scene_desc points at)
+struct Flat {
+    std::vector<float> positions, normals, uvs, tangents;
+    std::vector<uint32_t> tri_vidx, tri_flags;
+    std::vector<pt_quad> quads;
+    std::vector<pt_sphere> spheres;
+    std::vector<pt_prim> prims;
+    std::vector<pt_bvh_desc> bvhs;
+    std::vector<pt_material> materials;
+    std::vector<pt_texture> textures;
+    std::vector<pt_image> images;
+    std::vector<uint8_t> texels;
+    std::vector<pt_light> lights;
+    std::vector<uint32_t> sampler_lights, infinite_lights;
+    uint32_t light_sampler = PT_LS_UNIFORM;
+
+    std::unordered_map<const Mesh*, uint32_t> mesh_vbase, mesh_tbase;
+    std::unordered_map<const Texture*, int32_t> tex_ids;
+    std::unordered_map<const Material*, int32_t> mat_ids;
+    std::unordered_map<const Light*, int32_t> light_slot;  // AreaLight -> prim slot
+
+    int32_t texture(const TexPtr& t) {
+        if (!t) return -1;
+        auto it = tex_ids.find(t.get());
+        if (it != tex_ids.end()) return it->second;
+        pt_texture r{};
+        r.a = r.b = r.image = -1;
+        put3(r.scale, PT_GET(*t, TexScale));
+        if (auto* s = dynamic_cast<const SolidColor*>(t.get())) {
+            r.kind = PT_TEX_SOLID;
+            glm::vec3 v = PT_GET(*t, TexScale) * PT_GET(*s, SolidAlbedo);  // SolidColor::Evaluate
+            put3(r.value, v);
+        } else if (auto* c = dynamic_cast<const CheckerTexture*>(t.get())) {
+            r.kind = PT_TEX_CHECKER;
+            r.a = texture(PT_GET(*c, ChkA));
+            r.b = texture(PT_GET(*c, ChkB));
+            glm::vec2 inv = PT_GET(*c, ChkInv);
+            r.inv_scale[0] = inv.x;
+            r.inv_scale[1] = inv.y;
+        } else if (auto* im = dynamic_cast<const ImageTexture*>(t.get())) {
+            const Image& img = PT_GET(*im, ImgTexImage);
+            pt_image pi{};
+            pi.offset = texels.size();
+            pi.width = PT_GET(img, ImgW);
+            pi.height = PT_GET(img, ImgH);
+            pi.channels = PT_GET(img, ImgC);
+            const unsigned char* px = PT_GET(img, ImgData);
+            texels.insert(texels.end(), px, px + (size_t)pi.width * pi.height * pi.channels);
+            texels.resize((texels.size() + 15) & ~size_t(15));
+            r.kind = PT_TEX_IMAGE;
+            r.image = (int32_t)images.size();
+            images.push_back(pi);
+        } else {
+            throw std::runtime_error("HipPathIntegrator: unsupported texture type");
+        }
+        int32_t id = (int32_t)textures.size();
+        textures.push_back(r);
+        tex_ids[t.get()] = id;
+        return id;
+    }
+
+    int32_t material(const std::shared_ptr<Material>& m) {
+        if (!m) return -1;
+        auto it = mat_ids.find(m.get());
+        if (it != mat_ids.end()) return it->second;
+        pt_material r{};
+        r.tex = r.norm = r.rough = r.metal = r.alpha = -1;
+        if (auto* d = dynamic_cast<const MicrofacetDiffuse*>(m.get())) {
+            r.kind = PT_MAT_DIFFUSE;
+            r.tex = texture(PT_GET(*d, DifTex));
+            r.norm = texture(PT_GET(*d, DifNorm));
+            r.rough = texture(PT_GET(*d, DifRough));
+            r.metal = texture(PT_GET(*d, DifMetal));
+            r.alpha = texture(PT_GET(*d, DifAlpha));
+            const AlphaTester& at = PT_GET(*d, DifTester);
+            r.alpha_mode = (uint32_t)at.mode;
+            r.alpha_cutoff = at.cutoff;
+        } else if (auto* e = dynamic_cast<const MicrofacetDielectric*>(m.get())) {
+            r.kind = PT_MAT_DIELECTRIC;
+            r.ri = PT_GET(*e, DieRi);
+            r.tex = texture(PT_GET(*e, DieTex));
+            r.norm = texture(PT_GET(*e, DieNorm));
+            r.rough = texture(PT_GET(*e, DieRough));
+            r.alpha = texture(PT_GET(*e, DieAlpha));
+            const AlphaTester& at = PT_GET(*e, DieTester);
+            r.alpha_mode = (uint32_t)at.mode;
+            r.alpha_cutoff = at.cutoff;
+        } else if (auto* t = dynamic_cast<const ThinDielectric*>(m.get())) {
+            r.kind = PT_MAT_THIN;
+            r.ri = PT_GET(*t, ThinRi);
+            r.tex = texture(PT_GET(*t, ThinAlbedo));
+        } else if (auto* c = dynamic_cast<const SpecularConductor*>(m.get())) {
+            r.kind = PT_MAT_CONDUCTOR;
+            put3(r.albedo, PT_GET(*c, CondAlbedo));
+        } else {
+            throw std::runtime_error("HipPathIntegrator: unsupported material type");
+        }
+        int32_t id = (int32_t)materials.size();
+        materials.push_back(r);
+        mat_ids[m.get()] = id;
+        return id;
+    }
+
+    uint32_t triangle(const TriangleShape& ts) {
+        const Mesh* mesh = TriangleShape::getMeshAt(ts.getMeshIndex());
+        auto it = mesh_tbase.find(mesh);
+        if (it == mesh_tbase.end()) {  // first triangle of this mesh: append the mesh
+            const uint32_t vb = (uint32_t)(positions.size() / 3), tb = (uint32_t)tri_flags.size();
+            auto v = mesh->GetVertices();
+            auto n = mesh->GetNormals();
+            auto uv = mesh->GetTexCoords();
+            auto tg = mesh->GetTangents();
+            auto idx = mesh->GetIndices();
+            for (size_t i = 0; i < v.size(); i++) {
+                positions.insert(positions.end(), {v[i].x, v[i].y, v[i].z});
+                normals.insert(normals.end(), {n[i].x, n[i].y, n[i].z});
+                uvs.insert(uvs.end(), {uv[i].x, uv[i].y});
+                if (tg.empty()) tangents.insert(tangents.end(), {0.0f, 0.0f, 0.0f});
+                else tangents.insert(tangents.end(), {tg[i].x, tg[i].y, tg[i].z});
+            }
+            for (uint32_t i : idx) tri_vidx.push_back(vb + i);
+            tri_flags.insert(tri_flags.end(), idx.size() / 3, tg.empty() ? 0u : 1u);
+            it = mesh_tbase.emplace(mesh, tb).first;
+        }
+        return it->second + ts.getTriIndex();
+    }
+
+    // One GeometricPrimitive into slot `slot`.
+    void geometric(const GeometricPrimitive& gp, uint32_t slot) {
+        pt_prim& p = prims[slot];
+        const auto& shape = PT_GET(gp, GpShape);
+        if (auto* t = dynamic_cast<const TriangleShape*>(shape.get())) {
+            p.kind = PT_PRIM_TRIANGLE;
+            p.index = triangle(*t);
+        } else if (auto* q = dynamic_cast<const QuadShape*>(shape.get())) {
+            pt_quad r{};
+            put3(r.Q, PT_GET(*q, QuadQ));
+            put3(r.u, PT_GET(*q, QuadU));
+            put3(r.v, PT_GET(*q, QuadV));
+            put3(r.normal, PT_GET(*q, QuadN));
+            r.D = PT_GET(*q, QuadD);
+            put3(r.w, PT_GET(*q, QuadW));
+            p.kind = PT_PRIM_QUAD;
+            p.index = (uint32_t)quads.size();
+            quads.push_back(r);
+        } else if (auto* s = dynamic_cast<const SphereShape*>(shape.get())) {
+            pt_sphere r{};
+            put3(r.center, PT_GET(*s, SphCenter));
+            r.radius = PT_GET(*s, SphRadius);
+            p.kind = PT_PRIM_SPHERE;
+            p.index = (uint32_t)spheres.size();
+            spheres.push_back(r);
+        } else {
+            throw std::runtime_error("HipPathIntegrator: unsupported shape type");
+        }
+        p.material = material(PT_GET(gp, GpMaterial));
+        p.medium = PT_GET(gp, GpMedium) ? 0 : -1;
+        p.light = -1;
+        if (const auto& al = PT_GET(gp, GpArea)) light_slot[al.get()] = (int32_t)slot;
+    }
+
+    void build(const Scene& scene, const std::shared_ptr<LightSampler>& ls) {
+        const auto& tb = PT_GET(scene, SceneBvh);
+        auto* tlas = dynamic_cast<TLAS4*>(tb.get());
+        if (!tlas) throw std::runtime_error("HipPathIntegrator: the scene must be built with BuildTlas<TLAS4>()");
+        const auto& top = PT_GET(*static_cast<TLASBase*>(tlas), TlasPrims);
+        const auto& tnodes = PT_GET(*tlas, TlasNodes);
+        static_assert(sizeof(BVH4_CLUSTER) == sizeof(pt_ref_bvh4_cluster), "cluster layout");
+        const uint32_t n_top = (uint32_t)top.size();
+        // BLAS list in TLAS slot order
+        std::vector<const BLAS4*> blas;
+        std::vector<uint32_t> blas_of_slot(n_top, UINT32_MAX);
+        for (uint32_t i = 0; i < n_top; i++) {
+            const Primitive* p = top[i].get();
+            const BLAS4* b = dynamic_cast<const BLAS4*>(p);
+#ifdef PT_WITH_MODEL
+            if (!b)
+                if (auto* m = dynamic_cast<const Model*>(p)) b = dynamic_cast<const BLAS4*>(PT_GET(*m, ModelBvh).get());
+#endif
+            if (b) {
+                blas_of_slot[i] = (uint32_t)blas.size();
+                blas.push_back(b);
+            } else if (!dynamic_cast<const GeometricPrimitive*>(p)) {
+                throw std::runtime_error("HipPathIntegrator: unsupported TLAS primitive (instancing is not supported)");
+            }
+        }
+        uint32_t total = n_top;
+        std::vector<uint32_t> base(blas.size());
+        for (size_t k = 0; k < blas.size(); k++) {
+            base[k] = total;
+            total += (uint32_t)PT_GET(*static_cast<const BLASBase*>(blas[k]), BlasPrims).size();
+        }
+        prims.assign(total, pt_prim{});
+        pt_bvh_desc t{};
+        t.clusters = reinterpret_cast<const pt_ref_bvh4_cluster*>(tnodes.data());
+        t.n_clusters = (uint32_t)tnodes.size();
+        std::memcpy(&t.root, &PT_GET(*tlas, TlasRoot), sizeof(t.root));
+        t.prim_base = 0;
+        t.n_prims = n_top;
+        bvhs.push_back(t);
+        for (uint32_t i = 0; i < n_top; i++) {
+            if (blas_of_slot[i] != UINT32_MAX) {
+                prims[i] = pt_prim{PT_PRIM_BLAS, 1 + blas_of_slot[i], -1, -1, -1};
+            } else {
+                geometric(*static_cast<const GeometricPrimitive*>(top[i].get()), i);
+            }
+        }
+        for (size_t k = 0; k < blas.size(); k++) {
+            const auto& bp = PT_GET(*static_cast<const BLASBase*>(blas[k]), BlasPrims);
+            for (size_t j = 0; j < bp.size(); j++) geometric(bp[j], base[k] + (uint32_t)j);
+            const auto& bn = PT_GET(*blas[k], BlasNodes);
+            pt_bvh_desc d{};
+            d.clusters = reinterpret_cast<const pt_ref_bvh4_cluster*>(bn.data());
+            d.n_clusters = (uint32_t)bn.size();
+            std::memcpy(&d.root, &PT_GET(*blas[k], BlasRoot), sizeof(d.root));
+            d.prim_base = base[k];
+            d.n_prims = (uint32_t)bp.size();
+            bvhs.push_back(d);
+        }
+        // lights: Scene::GetLights() order, then lights only the sampler holds
+        std::vector<std::shared_ptr<Light>> all = scene.GetLights();
+        const std::vector<std::shared_ptr<Light>>* sl = nullptr;
+        if (ls) {
+            if (auto* u = dynamic_cast<UniformLightSampler*>(ls.get())) {
+                sl = &PT_GET(*u, UlsLights);
+                light_sampler = PT_LS_UNIFORM;
+            } else if (auto* pw = dynamic_cast<PowerLightSampler*>(ls.get())) {
+                sl = &PT_GET(*pw, PlsLights);
+                light_sampler = PT_LS_POWER;
+            } else {
+                throw std::runtime_error("HipPathIntegrator: unsupported LightSampler");
+            }
+            for (const auto& l : *sl)
+                if (std::find(all.begin(), all.end(), l) == all.end()) all.push_back(l);
+        }
+        std::unordered_map<const Light*, uint32_t> lid;
+        for (const auto& l : all) {
+            pt_light r{};
+            r.prim = r.tex = -1;
+            r.power = l->Power();
+            r.pmf = ls ? ls->PMF(l) : 0.0f;
+            if (auto* a = dynamic_cast<const AreaLight*>(l.get())) {
+                auto it = light_slot.find(a);
+                if (it == light_slot.end()) throw std::runtime_error("HipPathIntegrator: area light without a primitive");
+                r.kind = PT_LIGHT_AREA;
+                r.prim = it->second;
+                r.tex = texture(PT_GET(*a, AreaTex));
+                r.one_sided = PT_GET(*a, AreaOneSided) ? 1u : 0u;
+                prims[it->second].light = (int32_t)lights.size();
+            } else if (auto* u = dynamic_cast<const UniformInfiniteLight*>(l.get())) {
+                r.kind = PT_LIGHT_UNIFORM_INF;
+                put3(r.color, PT_GET(*u, UniColor));
+            } else if (auto* f = dynamic_cast<const FunctionInfiniteLight*>(l.get())) {
+                const auto* g = PT_GET(*f, FunFn).target<pt::SkyGradient>();
+                if (!g) throw std::runtime_error("HipPathIntegrator: FunctionInfiniteLight needs a pt::SkyGradient");
+                r.kind = PT_LIGHT_SKY_INF;
+                put3(r.color, g->horizon);
+                put3(r.vec, g->zenith);
+                r.scale = g->scale;
+            } else if (auto* d = dynamic_cast<const DistantLight*>(l.get())) {
+                r.kind = PT_LIGHT_DISTANT;
+                put3(r.color, PT_GET(*d, DistColor));
+                put3(r.vec, PT_GET(*d, DistDir));
+            } else if (auto* p = dynamic_cast<const PointLight*>(l.get())) {
+                r.kind = PT_LIGHT_POINT;
+                put3(r.color, PT_GET(*p, PointColor));
+                put3(r.vec, PT_GET(*p, PointP));
+            } else {
+                throw std::runtime_error("HipPathIntegrator: unsupported light type");
+            }
+            lid[l.get()] = (uint32_t)lights.size();
+            lights.push_back(r);
+        }
+        if (sl)
+            for (const auto& l : *sl) sampler_lights.push_back(lid.at(l.get()));
+        for (const auto& l : scene.infiniteLights) infinite_lights.push_back(lid.at(l.get()));
+    }
+
+    pt_scene_desc desc() const {
+        pt_scene_desc d{};
+        d.positions = positions.data();
+        d.normals = normals.data();
+        d.uvs = uvs.data();
+        d.tangents = tangents.data();
+        d.n_vertices = (uint32_t)(positions.size() / 3);
+        d.tri_vidx = tri_vidx.data();
+        d.tri_flags = tri_flags.data();
+        d.n_triangles = (uint32_t)tri_flags.size();
+        d.quads = quads.data();
+        d.n_quads = (uint32_t)quads.size();
+        d.spheres = spheres.data();
+        d.n_spheres = (uint32_t)spheres.size();
+        d.prims = prims.data();
+        d.n_prims = (uint32_t)prims.size();
+        d.bvhs = bvhs.data();
+        d.n_bvhs = (uint32_t)bvhs.size();
+        d.materials = materials.data();
+        d.n_materials = (uint32_t)materials.size();
+        d.textures = textures.data();
+        d.n_textures = (uint32_t)textures.size();
+        d.images = images.data();
+        d.n_images = (uint32_t)images.size();
+        d.texels = texels.data();
+        d.n_texel_bytes = texels.size();
+        d.lights = lights.data();
+        d.n_lights = (uint32_t)lights.size();
+        d.light_sampler = light_sampler;
+        d.sampler_lights = sampler_lights.data();
+        d.n_sampler_lights = (uint32_t)sampler_lights.size();
+        d.infinite_lights = infinite_lights.data();
+        d.n_infinite_lights = (uint32_t)infinite_lights.size();
+        return d;
+    }
+};
+
+pt_camera_desc camera_desc(const Camera& cam) {
+    pt_camera_desc c{};
+    put3(c.origin, PT_GET(cam, CamFrom));
+    put3(c.u, PT_GET(cam, CamU));
+    put3(c.v, PT_GET(cam, CamV));
+    put3(c.w, PT_GET(cam, CamW));
+    c.half_width = PT_GET(cam, CamHW);
+    c.half_height = PT_GET(cam, CamHH);
+    c.defocus_radius = PT_GET(cam, CamDefocus);
+    c.focus_distance = PT_GET(cam, CamFocusDist);
+    c.focus_angle = PT_GET(cam, CamFocusAngle);
+    glm::ivec2 res = cam.GetFilm()->Resolution();
+    c.width = res.x;
+    c.height = res.y;
+    return c;
+}
+
+void filter_desc(const Film& film, pt_render_desc& rd) {
+    const auto& f = PT_GET(film, FilmFilter);
+    glm::vec2 r = f->Radius();
+    rd.filter_radius[0] = r.x;
+    rd.filter_radius[1] = r.y;
+    if (auto* m = dynamic_cast<const MitchellFilter*>(f.get())) {
+        rd.filter = PT_FILTER_MITCHELL;
+        rd.filter_params[0] = PT_GET(*m, MitB);
+        rd.filter_params[1] = PT_GET(*m, MitC);
+    } else if (dynamic_cast<const BoxFilter*>(f.get())) {
+        rd.filter = PT_FILTER_BOX;
+    } else if (auto* g = dynamic_cast<const GaussianFilter*>(f.get())) {
+        rd.filter = PT_FILTER_GAUSSIAN;
+        rd.filter_params[0] = PT_GET(*g, GaussSigma);
+    } else {
+        throw std::runtime_error("HipPathIntegrator: unsupported film filter");
+    }
+}
+
+}  // namespace
+
+namespace pt {
+
+// ---------------------------------------------------------------------------
+static inline uint32_t pcg_hash(uint32_t v) {
+    uint32_t state = v * 747796405u + 2891336453u;
+    uint32_t word = ((state >> ((state >> 28u) + 4u)) ^ state) * 277803737u;
+    return (word >> 22u) ^ word;
+}
+void PCGSampler::StartPixelSample(const glm::ivec2& p, int index) {
+    key_ = pcg_hash(pcg_hash(seed_ ^ pcg_hash((uint32_t)(p.y * width_ + p.x))) + (uint32_t)index);
+    dim_ = 0;
+}
+float PCGSampler::next() { return (float)(pcg_hash(key_ + 0x9E3779B9u * dim_++) >> 8) * (1.0f / 16777216.0f); }
+glm::dvec2 PCGSampler::get2D() {
+    double a = next();
+    double b = next();
+    return {a, b};
+}
+std::array<glm::vec2, 4> PCGSampler::get2Dx4f() {
+    std::array<glm::vec2, 4> r;
+    for (auto& v : r) {
+        float a = next();
+        float b = next();
+        v = {a, b};
+    }
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+class HipBackend {
+public:
+    Flat flat;
+    std::vector<pt_ctx*> ctx;
+    RenderStats stats;
+    std::vector<double> last;  // the merged accumulation of the last frame
+
+    ~HipBackend() {
+        for (pt_ctx* c : ctx) pt_destroy(c);
+    }
+
+    void ensure(const Scene& scene, const std::shared_ptr<LightSampler>& ls, unsigned n) {
+        if (ctx.empty()) flat.build(scene, ls);
+        int devices = 0;
+        if (hipcount(&devices) != 0 || devices <= 0) throw std::runtime_error("HipPathIntegrator: no HIP device");
+        const unsigned want = std::max(1u, std::min<unsigned>(n, (unsigned)devices));
+        const pt_scene_desc d = flat.desc();
+        while (ctx.size() < want) {
+            pt_ctx* c = nullptr;
+            check(pt_create(&c, (int)ctx.size()), "pt_create");
+            ctx.push_back(c);
+            check(pt_scene_upload(c, &d), "pt_scene_upload", c);
+        }
+    }
+
+    // Renders shards 0..n-1 (one host thread per GPU) and merges into film.
+    void render(const Camera& cam, uint32_t integrator, uint32_t spp, uint32_t depth, uint32_t seed, unsigned n) {
+        const pt_camera_desc cd = camera_desc(cam);
+        const auto film = cam.GetFilm();
+        const glm::ivec2 res = film->Resolution();
+        const size_t npx = (size_t)res.x * res.y;
+        pt_render_desc rd{};
+        rd.integrator = integrator;
+        rd.spp = spp;
+        rd.max_depth = depth;
+        rd.seed = seed;
+        filter_desc(*film, rd);
+        rd.shard_count = n;
+        std::vector<std::vector<double>> acc(n, std::vector<double>(4 * npx, 0.0));
+        std::vector<pt_stats> st(n);
+        std::vector<std::string> err(n);
+        auto t0 = std::chrono::steady_clock::now();
+        std::vector<std::thread> th;
+        for (unsigned g = 0; g < n; g++) {
+            th.emplace_back([&, g] {
+                pt_render_desc r = rd;
+                r.shard_index = g;
+                if (pt_render(ctx[g], &cd, &r, acc[g].data(), &st[g]) != PT_OK) err[g] = pt_last_error(ctx[g]);
+            });
+        }
+        for (auto& t : th) t.join();
+        for (unsigned g = 0; g < n; g++)
+            if (!err[g].empty()) throw std::runtime_error("pt_render: " + err[g]);
+        // {sum RGB*w, sum w} per pixel into the Film (Film.hpp:118-132)
+        last.assign(4 * npx, 0.0);
+        for (unsigned g = 0; g < n; g++)
+            for (size_t i = 0; i < 4 * npx; i++) last[i] += acc[g][i];
+        FilmTile tile = film->GetFilmTile(Bounds2i{{0, 0}, res});
+        for (int y = 0; y < res.y; y++)
+            for (int x = 0; x < res.x; x++) {
+                FilmTilePixel& px = tile.At({x, y});
+                const size_t i = 4 * ((size_t)y * res.x + x);
+                px.RGB = glm::dvec3(last[i], last[i + 1], last[i + 2]);
+                px.weight = last[i + 3];
+            }
+        film->Merge(tile);
+        stats = RenderStats{};
+        for (const auto& s : st) {
+            stats.paths += s.paths;
+            stats.rays_closest += s.rays_closest;
+            stats.rays_any += s.rays_any;
+        }
+        stats.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+
+private:
+    static int hipcount(int* n);
+};
+
+}  // namespace pt
+
+#include <hip/hip_runtime_api.h>
+int pt::HipBackend::hipcount(int* n) { return hipGetDeviceCount(n) == hipSuccess ? 0 : -1; }
+
+namespace pt {
+
+static uint32_t seed_of(const std::shared_ptr<Sampler>& s) {
+    if (auto* p = dynamic_cast<const PCGSampler*>(s.get())) return p->Seed();
+    return 0x5EED0001u;
+}
+
+HipPathIntegrator::HipPathIntegrator(const std::shared_ptr<Scene>& scene, const std::shared_ptr<Camera>& camera,
+                                     const std::shared_ptr<Sampler>& sampler,
+                                     const std::shared_ptr<LightSampler>& lightSampler, uint32_t maxDepth)
+    : PathIntegrator(scene, camera, sampler, lightSampler, maxDepth), ls_(lightSampler), depth_(maxDepth) {}
+HipPathIntegrator::~HipPathIntegrator() = default;
+
+void HipPathIntegrator::Render(unsigned int n) const {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!be_) be_ = std::make_unique<HipBackend>();
+    be_->ensure(*scene, ls_, n);
+    be_->render(*camera, PT_INTEGRATOR_PATH, sampler->SamplesPerPixel(), depth_, seed_of(sampler),
+                (unsigned)be_->ctx.size());
+}
+RenderStats HipPathIntegrator::LastStats() const { return be_ ? be_->stats : RenderStats{}; }
+static const std::vector<double> kEmpty;
+const std::vector<double>& HipPathIntegrator::LastAccumulation() const { return be_ ? be_->last : kEmpty; }
+
+HipSimplePathIntegrator::HipSimplePathIntegrator(const std::shared_ptr<Scene>& scene,
+                                                 const std::shared_ptr<Camera>& camera,
+                                                 const std::shared_ptr<Sampler>& sampler, uint32_t maxDepth)
+    : SimplePathIntegrator(scene, camera, sampler, maxDepth), depth_(maxDepth) {}
+HipSimplePathIntegrator::~HipSimplePathIntegrator() = default;
+
+void HipSimplePathIntegrator::Render(unsigned int n) const {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!be_) be_ = std::make_unique<HipBackend>();
+    be_->ensure(*scene, nullptr, n);
+    be_->render(*camera, PT_INTEGRATOR_SIMPLE, sampler->SamplesPerPixel(), depth_, seed_of(sampler),
+                (unsigned)be_->ctx.size());
+}
+RenderStats HipSimplePathIntegrator::LastStats() const { return be_ ? be_->stats : RenderStats{}; }
+const std::vector<double>& HipSimplePathIntegrator::LastAccumulation() const { return be_ ? be_->last : kEmpty; }
+
+}  // namespace pt

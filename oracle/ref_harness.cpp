@@ -46,6 +46,9 @@
 #include "Medium.hpp"
 #include "PhaseFunction.hpp"
 #include "Texture.hpp"
+#ifdef PT_WITH_HIP
+#include "HipIntegrator.hpp"  // integration/: the drop-in GPU integrators
+#endif
 
 // ---------------------------------------------------------------------------
 // Deterministic sample stream (the parity contract):
@@ -285,11 +288,16 @@ static void read_recipe(World& w, const std::string& path) {
                 glm::vec3 c0(c[0], c[1], c[2]), c1(c[3], c[4], c[5]);
                 float sc = c[6];
                 // main.cpp:292-295 gradient, parameterised
+#ifdef PT_WITH_HIP
+                // the GPU integrator recognises the gradient by its functor type
+                w.inf.push_back(std::make_shared<FunctionInfiniteLight>(pt::SkyGradient{c0, c1, sc}));
+#else
                 auto fn = [c0, c1, sc](const Ray& ray) {
                     float a = 0.5f * (ray.dir.y + 1.0f);
                     return sc * ((1.0f - a) * c0 + a * c1);
                 };
                 w.inf.push_back(std::make_shared<FunctionInfiniteLight>(fn));
+#endif
             }
             w.lightOwner[w.inf.back().get()] = "inf:" + std::to_string(w.inf.size() - 1);
         } else if (k == "extralight") {
@@ -633,6 +641,27 @@ static void cmd_time(World& w, int threads, unsigned spp, const std::string& mod
            rays / secs / 1e6);
 }
 
+#ifdef PT_WITH_HIP
+// --- hip: the drop-in pt::HipPathIntegrator / HipSimplePathIntegrator on the
+// reference-built scene (integration/HipIntegrator.hpp), Render(gpus) into the
+// reference Film; dumps the merged accumulation like `film`.
+static void cmd_hip(World& w, const std::string& out, unsigned gpus) {
+    auto sampler = std::make_shared<pt::PCGSampler>(w.spp, w.seed, w.W);
+    std::vector<double> acc;
+    if (w.integ == "simple") {
+        pt::HipSimplePathIntegrator integ(w.scene, w.camera, sampler, w.maxDepth);
+        integ.Render(gpus);
+        acc = integ.LastAccumulation();
+    } else {
+        pt::HipPathIntegrator integ(w.scene, w.camera, sampler, w.ls, w.maxDepth);
+        integ.Render(gpus);
+        acc = integ.LastAccumulation();
+    }
+    wr(out + ".hipfilm.bin", acc);
+    cmd_film(w, out, w.spp);  // the reference's own Li on the same objects (same sky power)
+}
+#endif
+
 int main(int argc, char** argv) {
     if (argc < 4) {
         fprintf(stderr, "usage: ref_harness <recipe> <cmd> <out> [args]\n");
@@ -656,6 +685,9 @@ int main(int argc, char** argv) {
     else if (cmd == "camera") cmd_camera(w, out, argv[4]);
     else if (cmd == "lights") cmd_lights(w, out, argv[4]);
     else if (cmd == "time") cmd_time(w, atoi(argv[4]), (unsigned)atoi(argv[5]), argc > 6 ? argv[6] : "render");
+#ifdef PT_WITH_HIP
+    else if (cmd == "hip") cmd_hip(w, out, argc > 4 ? (unsigned)atoi(argv[4]) : 1u);
+#endif
     else { fprintf(stderr, "unknown cmd %s\n", cmd.c_str()); return 2; }
     return 0;
 }

@@ -68,6 +68,9 @@ def build_reference_harness():
     if not Path("/root/reference/Integrators.cpp").exists():
         return None
     _run(["make", "-s", "-j8", "-C", ROOT / "oracle", "ref"])
+    # the same harness driving the C++ drop-in integrator (integration/) on
+    # libpt_hip.so, for the GPU tests of the drop-in (tests/test_gpu_integration.py)
+    _run(["make", "-s", "-j8", "-C", ROOT / "oracle", "hip"])
     return ROOT / "oracle" / "_ref" / "ref_harness"
 
 
