@@ -78,6 +78,30 @@ def cpu_baseline(setup, target_s: float = 15.0):
                       f"{threads} threads)"}
 
 
+def pmc_traffic(config: str, spp: int, world: int):
+    """HBM bytes per k_closest launch from the committed rocprofv3 counter
+    summary of this workload (tools/profile_pmc.sh + tools/pmc_summary.py,
+    profiles/*_<config>_pmc.json): FETCH_SIZE doubled (gfx950 reports half
+    of 16-byte-per-lane reads, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, both
+    in KB per dispatch.  None when no profile of this configuration exists."""
+    import glob
+    cands = sorted(glob.glob(str(ROOT / "profiles" / f"*_{config}_pmc.json")))
+    for path in reversed(cands):
+        try:
+            prof = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        meta = prof.get("_meta", {})
+        if meta.get("spp") != spp or meta.get("n_gpus", 1) != world:
+            continue
+        k = prof.get(meta.get("kernel", "k_closest<false>"), {})
+        if "FETCH_SIZE_per_dispatch" not in k:
+            continue
+        b = (2.0 * k["FETCH_SIZE_per_dispatch"] + k.get("WRITE_SIZE_per_dispatch", 0.0)) * 1024.0
+        return round(b), Path(path).name
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -122,8 +146,12 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    # traversal work per closest-hit ray on this rank's samples (untimed pass)
+    # traversal work per closest-hit ray (untimed, instrumented pass over the
+    # first spp/16 samples of every pixel: same scene, same sample stream)
+    count_spp = max(1, setup.spp // 16)
+    integ.sampler.samples = count_spp
     cst = step(N.PT_RENDER_COUNT_NODES)
+    integ.sampler.samples = setup.spp
     nodes_per_ray = cst["nodes_closest"] / max(1, cst["rays_closest"])
     tris_per_ray = cst["tris_closest"] / max(1, cst["rays_closest"])
     bytes_per_ray = 128.0 * nodes_per_ray + 48.0 * tris_per_ray
@@ -155,6 +183,7 @@ def main():
         avg_ms = totals["ms_closest"] / max(1, totals["launches_closest"])
         launch_bytes = bytes_per_ray * totals["rays_closest"] / max(1, totals["launches_closest"])
         achieved = launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        traffic, traffic_src = pmc_traffic(args.config, setup.spp, world)
         out = {
             "metric": "Mrays/s",
             "value": round(total_rays / elapsed_max / 1e6, 3),
@@ -172,7 +201,7 @@ def main():
                        "spp": setup.spp, "max_depth": setup.max_depth, "integrator": setup.integrator,
                        "rays_per_step": int(total_rays / args.steps), "parallelism": f"sample-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "k_closest (BVH4 closest-hit traversal)",
                          "bytes_per_ray": round(bytes_per_ray, 1), "nodes_per_ray": round(nodes_per_ray, 2),
                          "tris_per_ray": round(tris_per_ray, 2), "avg_launch_ms": round(avg_ms, 4),

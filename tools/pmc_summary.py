@@ -2,7 +2,10 @@
 and per-dispatch averages of each PMC counter (FETCH_SIZE/WRITE_SIZE in KB as
 rocprofv3 reports them).  Writes JSON + prints a table.
 
-    python tools/pmc_summary.py <profile dir> <out.json>
+    python tools/pmc_summary.py <profile dir> <out.json> [config spp kernel]
+
+With the optional workload fields the JSON carries a "_meta" record that
+bench.py uses to attach the counter traffic to its roofline line.
 """
 import csv
 import glob
@@ -15,7 +18,7 @@ def short(name):
     return name.split("(")[0].replace("void ", "")
 
 
-def main(d, out):
+def main(d, out, meta=None):
     res = defaultdict(lambda: {"calls": 0, "dur_ns": 0.0, "counters": defaultdict(float), "dispatches": defaultdict(set)})
     for f in glob.glob(f"{d}/trace/**/*kernel_trace.csv", recursive=True):
         for r in csv.DictReader(open(f)):
@@ -36,10 +39,16 @@ def main(d, out):
         for c, tot in v["counters"].items():
             row[c + "_per_dispatch"] = tot / max(1, len(v["dispatches"][c]))
         table[k] = row
+    if meta:
+        table["_meta"] = meta
     json.dump(table, open(out, "w"), indent=1, sort_keys=True)
-    for k, row in sorted(table.items(), key=lambda kv: -kv[1]["calls"] * kv[1]["avg_us"]):
+    for k, row in sorted(((k, r) for k, r in table.items() if k != "_meta"),
+                         key=lambda kv: -kv[1]["calls"] * kv[1]["avg_us"]):
         print(k, {a: round(b, 1) for a, b in row.items()})
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    meta = None
+    if len(sys.argv) > 5:
+        meta = {"config": sys.argv[3], "spp": int(sys.argv[4]), "kernel": sys.argv[5], "n_gpus": 1}
+    main(sys.argv[1], sys.argv[2], meta)
