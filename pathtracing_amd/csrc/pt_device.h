@@ -47,6 +47,7 @@ struct DevScene {
     const DevPrimInfo* info;
     uint32_t root;
     uint32_t n_prims;
+    uint32_t n_nodes;
     const uint4* tri;          // i0, i1, i2, flags
     const float* positions;    // 3 per vertex
     const float* normals;

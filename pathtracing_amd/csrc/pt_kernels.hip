@@ -135,19 +135,30 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow_pool(PathSoA next, fl
 }
 
 // One ray per lane (grid covers all rays): lower overhead where traversal
-// lengths are uniform (small scenes); the runtime picks per scene.
+// lengths are uniform (small scenes); the runtime picks per scene.  The
+// whole-leaf inner loop of trace_closest / trace_any measures faster here than
+// the one-primitive-per-step loop of pt_pool.h (C2: 171 vs 191 us per launch),
+// PT_SIMPLE_STEP=1 selects the latter.
+#ifndef PT_SIMPLE_STEP
+#define PT_SIMPLE_STEP 0
+#endif
 template <bool COUNT>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(PathSoA P, uint32_t n, float4* __restrict__ hit,
                                                            uint32_t* __restrict__, unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
-    const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     TraceWork wk{0, 0};
+#if PT_SIMPLE_STEP
+    ClosestSrc src{P, hit};
+    trace_pool<false, COUNT, ClosestSrc, false>(n, nullptr, src, s_ref, wk);
+#else
+    const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     if (i < n) {
         const float4 o = P.o[i], d = P.d[i];
         float t, b1, b2;
         int prim = trace_closest<COUNT>(xyz(o), xyz(d), __int_as_float(0x7f800000), t, b1, b2, s_ref, wk);
         hit[i] = make_float4(t, b1, b2, __int_as_float(prim));
     }
+#endif
     if (COUNT) {
         count_add(counters, CNT_NODES_CLOSEST, wk.nodes);
         count_add(counters, CNT_TRIS_CLOSEST, wk.tris);
@@ -161,13 +172,17 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(PathSoA next, float4*
                                                           unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
     const uint32_t n = *nptr;
-    const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     TraceWork wk{0, 0};
+    ShadowSrc src{sq, next, done_L};
+#if PT_SIMPLE_STEP
+    if (blockIdx.x * PT_TRACE_BLOCK < n) trace_pool<true, COUNT, ShadowSrc, false>(n, nullptr, src, s_ref, wk);
+#else
+    const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     if (i < n) {
-        ShadowSrc src{sq, next, done_L};
         const ShadowRec r = sq[i];
         src.any(i, trace_any<COUNT>(xyz(r.o), xyz(r.d), r.o.w, s_ref, wk));
     }
+#endif
     if (COUNT) {
         count_add(counters, CNT_NODES_ANY, wk.nodes);
         count_add(counters, CNT_TRIS_ANY, wk.tris);
@@ -424,7 +439,14 @@ __global__ __launch_bounds__(256) void k_shade(RenderParams R, PathSoA cur, uint
         const uint32_t f0 = __float_as_uint(d4.w);
         uint32_t depth = f0 & PF_DEPTH_MASK, rr = (f0 >> PF_RR_SHIFT) & PF_DEPTH_MASK;
         bool spec = (f0 & PF_SPEC) != 0;
-        const int prim = __float_as_int(h.w);
+        int prim = __float_as_int(h.w);
+#if PT_POOL_CHECK
+        if (__float_as_uint(h.x) == 0xFFFFFFFFu) atomicAdd(&pt_diag[2], 1u);  // debugging builds only
+        if (prim >= (int)S.n_prims) {
+            atomicAdd(&pt_diag[1], 1u);
+            prim = -1;
+        }
+#endif
         bool alive = true;
         if (prim < 0) {
             // miss: infinite lights (Integrators.cpp:140-145, 196-208)

@@ -21,6 +21,18 @@
 #define PT_POOL_CHUNKS 8
 #define PT_POOL_STRIDE 32  // uint32 words between chunk counters (128 B)
 #define PT_POOL_WORDS (PT_POOL_CHUNKS * PT_POOL_STRIDE)
+#ifndef PT_POOL_STEP
+#define PT_POOL_STEP 1
+#endif
+#ifndef PT_POOL_CHECK
+#define PT_POOL_CHECK 0
+#endif
+#if PT_POOL_CHECK
+// debugging builds: [0] bad refs (popped instead), [1] shade prim out of range,
+// [2] shade saw an unwritten hit, [3] dropped stack pushes; the runtime prints
+// them after every render
+__device__ unsigned int pt_diag[4];
+#endif
 #ifndef PT_REFILL
 #define PT_REFILL 8
 #endif
@@ -29,7 +41,9 @@
 //   bool load(uint32_t ri, f3& o, f3& d, float& tmax)   (false: skip this ray)
 //   void closest(uint32_t ri, float t, float b1, float b2, int prim)
 //   void any(uint32_t ri, bool hit)
-template <bool ANY, bool COUNT, class Src>
+// POOL = false: no refill, lane i of the grid traces ray i (small scenes,
+// where traversal lengths are uniform and the claims would only cost).
+template <bool ANY, bool COUNT, class Src, bool POOL = true>
 __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, uint32_t* s_ref, TraceWork& wk) {
     const uint32_t lane = threadIdx.x;
     const uint32_t wl = __lane_id();
@@ -44,10 +58,23 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
     int sp = 0, best = -1;
 
     const uint32_t all_dead = (1u << PT_POOL_CHUNKS) - 1u;
+    if (!POOL) {
+        const uint32_t gi = blockIdx.x * PT_TRACE_BLOCK + lane;
+        if (gi < n && src.load(gi, o, d, tmax)) {
+            ri = (int)gi;
+            inv = inv_dir(d);
+            oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
+            ref = S.root;
+        }
+    }
     for (;;) {
+        if (!POOL) {
+            if (__ballot(ri >= 0) == 0) break;
+            if (ri < 0) continue;
+        }
         const uint64_t idle = __ballot(ri < 0);
         const uint32_t nidle = (uint32_t)__popcll(idle);
-        if (nidle >= PT_REFILL || idle == __ballot(true)) {
+        if (POOL && (nidle >= PT_REFILL || idle == __ballot(true))) {
             // claim exactly as many rays as lanes are idle (one atomic) from the
             // home chunk or the next non-empty one; no reserve is held, so no
             // wave sits on unstarted rays while others run dry
@@ -91,6 +118,143 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         }
         if (ri < 0) continue;
 
+#if PT_POOL_STEP == 1
+        // ---- one step of this lane's traversal: one cluster or ONE leaf
+        // primitive.  Node lanes and primitive lanes issue their loads in the
+        // same pass (one memory round trip per step for the whole wave);
+        // a leaf is walked one primitive per step (ref = REF_LEAF | next slot).
+        if (ref == REF_EMPTY) {
+            if (sp == 0) {  // finished: no hit (any) / closest result
+                if (ANY) src.any((uint32_t)ri, false);
+                else src.closest((uint32_t)ri, tmax, bb1, bb2, best);
+                ri = -1;
+                continue;
+            }
+            --sp;
+            ref = s_ref[sp * PT_TRACE_BLOCK + lane];
+        }
+        const bool node_step = !(ref & REF_LEAF);
+        const uint32_t idx = ref & ~REF_LEAF;
+#if PT_POOL_CHECK
+        if (node_step ? idx >= S.n_nodes : idx >= S.n_prims) {  // debugging builds only
+            atomicAdd(&pt_diag[0], 1u);
+            ref = REF_EMPTY;
+            continue;
+        }
+#endif
+        // all eight loads issue before any use: a primitive lane reads its
+        // 48-byte slot and repeats its first 16 bytes for the node-only words
+        // (same line, no extra traffic), and the cluster test below runs
+        // unconditionally (its result masked off on primitive lanes) so the
+        // compiler cannot sink the node loads behind the primitive branch
+        const float4* __restrict__ q = node_step ? reinterpret_cast<const float4*>(S.nodes + idx)
+                                                 : reinterpret_cast<const float4*>(S.geom + idx);
+        const uint32_t nk = node_step ? 1u : 0u;
+        const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+        const float4 q3 = q[3 * nk], q4 = q[4 * nk], q5 = q[5 * nk], q6 = q[6 * nk], q7 = q[7 * nk];
+        {
+            uint32_t mask;
+            float te[4];
+            slab4q(q0, q1, q2, q3, q4, q5, o, inv, tmax, mask, te);
+            if (!node_step) mask = 0;
+            const uint4 ch = make_uint4(__float_as_uint(q6.x), __float_as_uint(q6.y), __float_as_uint(q6.z),
+                                        __float_as_uint(q6.w));
+            uint32_t cand = REF_EMPTY;
+            if (ANY) {
+                // slot order, last visited next (BVH.hpp:1099-1102)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    if ((mask >> i) & 1u) {
+                        const uint32_t c = sel4u((uint32_t)i, ch);
+                        if (c != REF_EMPTY) {
+                            if (cand != REF_EMPTY && sp < PT_STACK) {
+                                s_ref[sp * PT_TRACE_BLOCK + lane] = cand;
+                                ++sp;
+                            }
+#if PT_POOL_CHECK
+                            else if (cand != REF_EMPTY) atomicAdd(&pt_diag[3], 1u);
+#endif
+                            cand = c;
+                        }
+                    }
+                }
+            } else {
+                // octant order far -> near (BVH4::LUT, BVH.hpp:1195-1204)
+                const uint32_t ow = __float_as_uint((oct >> 2) ? q7.y : q7.x);
+                const uint32_t perm = (ow >> (8 * (oct & 3))) & 0xFFu;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t ci = (perm >> (2 * k)) & 3u;
+                    if ((mask >> ci) & 1u) {
+                        const uint32_t c = sel4u(ci, ch);
+                        if (c != REF_EMPTY) {
+                            if (cand != REF_EMPTY && sp < PT_STACK) {
+                                s_ref[sp * PT_TRACE_BLOCK + lane] = cand;
+                                ++sp;
+                            }
+#if PT_POOL_CHECK
+                            else if (cand != REF_EMPTY) atomicAdd(&pt_diag[3], 1u);
+#endif
+                            cand = c;
+                        }
+                    }
+                }
+            }
+            if (node_step) {
+                if (COUNT) wk.nodes++;
+                ref = cand;
+                continue;
+            }
+        }
+        // one leaf primitive at slot idx
+        {
+            const uint32_t slot = idx;
+            const uint32_t w0 = __float_as_uint(q0.w);
+            const uint32_t kind = w0 & GF_KIND;
+            bool anyhit = false;
+            if (COUNT) wk.tris++;
+            if (kind == PT_PRIM_TRIANGLE) {
+                if (ANY && !(w0 & GF_PRED_GLM)) {
+                    if (tri_pred(o, d, xyz(q0), xyz(q1), xyz(q2), tmax)) anyhit = true;
+                } else {
+                    float bx, by, t;
+                    if (tri_glm(o, d, xyz(q0), xyz(q1), xyz(q2), bx, by, t) && !(t > tmax || t < PT_EPS)) {
+                        if (!(w0 & GF_ALPHA) || tri_alpha(slot, bx, by, o, d)) {
+                            if (ANY) {
+                                anyhit = true;
+                            } else {
+                                tmax = t;
+                                best = (int)slot;
+                                bb1 = bx;
+                                bb2 = by;
+                            }
+                        }
+                    }
+                }
+            } else if (kind == PT_PRIM_BLAS) {
+                if (COUNT) wk.tris--;
+                if (sp < PT_STACK) {
+                    s_ref[sp * PT_TRACE_BLOCK + lane] = __float_as_uint(q1.x);
+                    ++sp;
+                }
+            } else if (ANY) {
+                if (other_pred(slot, w0, o, d, tmax)) anyhit = true;
+            } else {
+                float t, a, b;
+                if (other_closest(slot, w0, o, d, tmax, t, a, b)) {
+                    tmax = t;
+                    best = (int)slot;
+                    bb1 = a;
+                    bb2 = b;
+                }
+            }
+            ref = (w0 & GF_LAST) ? REF_EMPTY : (REF_LEAF | (slot + 1));
+            if (ANY && anyhit) {  // early exit (BVH.hpp:1104-1105)
+                src.any((uint32_t)ri, true);
+                ri = -1;
+            }
+        }
+#else
         // ---- one step of this lane's traversal
         if (ref == REF_EMPTY) {
             if (sp == 0) {  // finished: no hit (any) / closest result
@@ -121,6 +285,9 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                                 s_ref[sp * PT_TRACE_BLOCK + lane] = cand;
                                 ++sp;
                             }
+#if PT_POOL_CHECK
+                            else if (cand != REF_EMPTY) atomicAdd(&pt_diag[3], 1u);
+#endif
                             cand = c;
                         }
                     }
@@ -139,6 +306,9 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                                 s_ref[sp * PT_TRACE_BLOCK + lane] = cand;
                                 ++sp;
                             }
+#if PT_POOL_CHECK
+                            else if (cand != REF_EMPTY) atomicAdd(&pt_diag[3], 1u);
+#endif
                             cand = c;
                         }
                     }
@@ -198,5 +368,6 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             src.any((uint32_t)ri, true);
             ri = -1;
         }
+#endif
     }
 }

@@ -406,6 +406,7 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
 #undef UP
     DS.root = roots[0];
     DS.n_prims = s->n_prims;
+    DS.n_nodes = (uint32_t)nodes.size();
     DS.n_texel_bytes = s->n_texel_bytes;
     DS.n_lights = s->n_lights;
     DS.light_sampler = s->light_sampler;
@@ -464,6 +465,10 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
     AL(c->sq, n * sizeof(ShadowRec));
     AL(c->counters, (CNT_SHARDS + 1) * CNT_COUNT * 8);
 #undef AL
+    if (hipMemset(c->qcnt, 0, (Q_WORDS + 3 * PT_POOL_WORDS) * 4) != hipSuccess) {
+        free_work(c);
+        return fail(c, PT_ERR_HIP, "hipMemset of the queue counters failed");
+    }
     c->cap = cap;
     return PT_OK;
 }
@@ -565,6 +570,9 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             continue;
         }
         HIPCHK(c, hipMemsetAsync(next_sample, 0, 8, sm));
+        // the fill appends to Q_NEXT: start the queue counters from zero (a
+        // fresh allocation holds whatever the memory held before)
+        HIPCHK(c, hipMemsetAsync(c->qcnt, 0, (Q_WORDS + 2 * PT_POOL_WORDS) * 4, sm));
         // initial fill: one camera sample per wavefront entry
         PathSoA cur = c->PA, nxt = c->PB;
         hipLaunchKernelGGL(k_finish, dim3((paths + 255) / 256), dim3(256), 0, sm, R, (const float4*)nullptr,
@@ -582,6 +590,9 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             const dim3 gt(use_pool ? std::max(1u, std::min(nb, c->trace_blocks)) : nb), gs((n_active + 255) / 256);
             uint32_t* pool_closest = c->qcnt + Q_WORDS;
             uint32_t* pool_shadow = c->qcnt + Q_WORDS + PT_POOL_WORDS;
+#if PT_POOL_CHECK
+            HIPCHK(c, hipMemsetAsync(c->hit, 0xFF, (size_t)n_active * sizeof(float4), sm));
+#endif
             if (timing) HIPCHK(c, hipEventRecord(c->ev[0], sm));
             {
                 auto kc = use_pool ? (count ? k_closest_pool<true> : k_closest_pool<false>)
@@ -626,6 +637,18 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                 t_sh += b;
                 t_an += d;
             }
+#if PT_POOL_CHECK
+            {
+                unsigned int dg[4];
+                HIPCHK(c, hipMemcpyFromSymbol(dg, HIP_SYMBOL(pt_diag), sizeof(dg)));
+                if (dg[0] | dg[1] | dg[2] | dg[3]) {
+                    fprintf(stderr, "pt_diag: n_active %u use_pool %d bad_ref %u bad_prim %u unwritten_hit %u dropped_push %u\n",
+                            n_active, (int)use_pool, dg[0], dg[1], dg[2], dg[3]);
+                    const unsigned int z[4] = {0, 0, 0, 0};
+                    HIPCHK(c, hipMemcpyToSymbol(HIP_SYMBOL(pt_diag), z, sizeof(z)));
+                }
+            }
+#endif
             n_active = c->host_cnt[Q_NEXT];
             std::swap(cur, nxt);
         }

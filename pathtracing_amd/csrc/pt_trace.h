@@ -165,11 +165,10 @@ __device__ __forceinline__ float sel4f(uint32_t i, float a, float b, float c, fl
     return i == 0 ? a : (i == 1 ? b : (i == 2 ? c : d));
 }
 
-template <bool COUNT>
-__device__ __forceinline__ void slab4(const DevCluster* __restrict__ node, f3 o, f3 inv, float tmax, uint32_t& mask,
-                                      float te[4]) {
-    const float4* c4 = reinterpret_cast<const float4*>(node);
-    float4 xmn = c4[0], xmx = c4[1], ymn = c4[2], ymx = c4[3], zmn = c4[4], zmx = c4[5];
+// 4-wide slab test (BVH.hpp:1049-1092 / 1140-1183) on a cluster's boxes
+// xmin..zmax (one float4 per component, the 4 children in its lanes)
+__device__ __forceinline__ void slab4q(float4 xmn, float4 xmx, float4 ymn, float4 ymx, float4 zmn, float4 zmx, f3 o,
+                                       f3 inv, float tmax, uint32_t& mask, float te[4]) {
     float xa[4] = {xmn.x, xmn.y, xmn.z, xmn.w}, xb[4] = {xmx.x, xmx.y, xmx.z, xmx.w};
     float ya[4] = {ymn.x, ymn.y, ymn.z, ymn.w}, yb[4] = {ymx.x, ymx.y, ymx.z, ymx.w};
     float za[4] = {zmn.x, zmn.y, zmn.z, zmn.w}, zb[4] = {zmx.x, zmx.y, zmx.z, zmx.w};
@@ -184,6 +183,13 @@ __device__ __forceinline__ void slab4(const DevCluster* __restrict__ node, f3 o,
         te[i] = tEntry;
         if (tExit >= PT_EPS && tEntry < tmax && tEntry <= tExit) mask |= 1u << i;
     }
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void slab4(const DevCluster* __restrict__ node, f3 o, f3 inv, float tmax, uint32_t& mask,
+                                      float te[4]) {
+    const float4* c4 = reinterpret_cast<const float4*>(node);
+    slab4q(c4[0], c4[1], c4[2], c4[3], c4[4], c4[5], o, inv, tmax, mask, te);
 }
 
 // Closest hit.  Returns prim slot or -1; t, b1, b2 of the accepted hit.

@@ -35,14 +35,17 @@ def _stale(out: Path, deps) -> bool:
     return any(Path(d).stat().st_mtime > t for d in deps)
 
 
-def build_product(force: bool = False) -> Path:
-    LIBDIR.mkdir(parents=True, exist_ok=True)
-    out = LIBDIR / "libpt_hip.so"
+def build_product(force: bool = False, variant: str = "", defines=()) -> Path:
+    """The product library; `variant` + `defines` (-D flags) build an A/B
+    copy under pathtracing_amd/_lib/variants/ for tuning runs (PT_HIP_LIB)."""
+    libdir = LIBDIR / "variants" if variant else LIBDIR
+    libdir.mkdir(parents=True, exist_ok=True)
+    out = libdir / (f"libpt_hip_{variant}.so" if variant else "libpt_hip.so")
     deps = list(CSRC.glob("*")) + [ROOT / "include" / "pt_api.h"]
     if not force and not _stale(out, deps):
         return out
-    build = ROOT / "build"
-    build.mkdir(exist_ok=True)
+    build = ROOT / "build" / variant if variant else ROOT / "build"
+    build.mkdir(parents=True, exist_ok=True)
     inc = ["-I", ROOT / "include", "-I", CSRC]
     # Host BVH builder: GNU dialect keeps GCC's default FP contraction, as the
     # reference's own -std=gnu++20 build; x86-64-v3 (AVX2+FMA) is portable to
@@ -51,7 +54,8 @@ def build_product(force: bool = False) -> Path:
     _run(["g++", "-std=gnu++20", "-O3", "-march=x86-64-v3", "-fPIC", "-c", CSRC / "pt_bvh.cpp", "-o", bvh_o, *inc])
     rt_o = build / "pt_runtime.o"
     _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++20", "-munsafe-fp-atomics",
-          "-Wno-unused-result", "-Wno-unused-value", "-c", CSRC / "pt_runtime.hip", "-o", rt_o, *inc])
+          "-Wno-unused-result", "-Wno-unused-value", *[f"-D{d}" for d in defines],
+          "-c", CSRC / "pt_runtime.hip", "-o", rt_o, *inc])
     tmp = out.with_suffix(".so.tmp")
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", rt_o, bvh_o, "-o", tmp, "-lpthread"])
     os.replace(tmp, out)
@@ -77,6 +81,12 @@ def build_reference_harness():
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     force = "--force" in argv
+    variants = [a.split("=", 1)[1] for a in argv if a.startswith("--variant=")]
+    if variants:  # --variant=name:DEF1,DEF2=3 ...  (tuning builds only)
+        for v in variants:
+            name, _, defs = v.partition(":")
+            build_product(True, name, [d for d in defs.split(",") if d])
+        return
     build_product(force)
     build_oracle()
     if "--no-ref" not in argv:
