@@ -61,15 +61,17 @@ struct RenderParams {
 };
 
 template <bool COUNT>
-__global__ void k_closest(PathSoA P, uint32_t n, float4* hit, uint32_t* pool, unsigned long long* counters);
+__global__ void k_closest(PathSoA P, uint32_t n, float4* hit, uint32_t* pool, uint32_t* ovf,
+                          unsigned long long* counters);
 template <bool COUNT>
-__global__ void k_closest_pool(PathSoA P, uint32_t n, float4* hit, uint32_t* pool, unsigned long long* counters);
+__global__ void k_closest_pool(PathSoA P, uint32_t n, float4* hit, uint32_t* pool, uint32_t* ovf,
+                               unsigned long long* counters);
 template <bool COUNT>
 __global__ void k_shadow(PathSoA next, float4* done_L, const ShadowRec* sq, const uint32_t* nptr, uint32_t* pool,
-                         unsigned long long* counters);
+                         uint32_t* ovf, unsigned long long* counters);
 template <bool COUNT>
 __global__ void k_shadow_pool(PathSoA next, float4* done_L, const ShadowRec* sq, const uint32_t* nptr, uint32_t* pool,
-                              unsigned long long* counters);
+                              uint32_t* ovf, unsigned long long* counters);
 template <int INTEGRATOR>
 __global__ void k_shade(RenderParams R, PathSoA cur, uint32_t n, const float4* hit, PathSoA next,
                         float4* done_L, uint32_t* done_sid, ShadowRec* sq, uint32_t* cnt);
@@ -80,5 +82,5 @@ __global__ void k_gather(RenderParams R, const float* sample_L, double* film);
 __global__ void k_interact(const pt_ray* rays, uint32_t n, float* out);
 __global__ void k_bsdf_cases(int mid, const float* in, uint32_t n, float* out);
 __global__ void k_light_cases(const float* in, uint32_t n, float* out);
-__global__ void k_trace_rays(const pt_ray* rays, uint32_t n, int any, pt_hit* out, uint32_t* pool,
+__global__ void k_trace_rays(const pt_ray* rays, uint32_t n, int any, pt_hit* out, uint32_t* pool, uint32_t* ovf,
                              unsigned long long* counters);

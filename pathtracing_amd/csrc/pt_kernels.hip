@@ -80,12 +80,12 @@ struct ClosestSrc {
 
 template <bool COUNT>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest_pool(PathSoA P, uint32_t n, float4* __restrict__ hit,
-                                                                uint32_t* __restrict__ pool,
+                                                                uint32_t* __restrict__ pool, uint32_t* __restrict__ ovf,
                                                                 unsigned long long* counters) {
-    __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+    __shared__ uint32_t s_ref[PT_POOL_LDS * PT_TRACE_BLOCK];
     TraceWork wk{0, 0};
     ClosestSrc src{P, hit};
-    trace_pool<false, COUNT>(n, pool, src, s_ref, wk);
+    trace_pool<false, COUNT>(n, pool, src, s_ref, ovf, wk);
     if (COUNT) {
         count_add(counters, CNT_NODES_CLOSEST, wk.nodes);
         count_add(counters, CNT_TRIS_CLOSEST, wk.tris);
@@ -123,11 +123,12 @@ template <bool COUNT>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow_pool(PathSoA next, float4* __restrict__ done_L,
                                                                const ShadowRec* __restrict__ sq,
                                                                const uint32_t* __restrict__ nptr,
-                                                               uint32_t* __restrict__ pool, unsigned long long* counters) {
-    __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+                                                               uint32_t* __restrict__ pool, uint32_t* __restrict__ ovf,
+                                                               unsigned long long* counters) {
+    __shared__ uint32_t s_ref[PT_POOL_LDS * PT_TRACE_BLOCK];
     TraceWork wk{0, 0};
     ShadowSrc src{sq, next, done_L};
-    trace_pool<true, COUNT>(*nptr, pool, src, s_ref, wk);
+    trace_pool<true, COUNT>(*nptr, pool, src, s_ref, ovf, wk);
     if (COUNT) {
         count_add(counters, CNT_NODES_ANY, wk.nodes);
         count_add(counters, CNT_TRIS_ANY, wk.tris);
@@ -144,12 +145,13 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow_pool(PathSoA next, fl
 #endif
 template <bool COUNT>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(PathSoA P, uint32_t n, float4* __restrict__ hit,
-                                                           uint32_t* __restrict__, unsigned long long* counters) {
+                                                           uint32_t* __restrict__, uint32_t* __restrict__,
+                                                           unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
     TraceWork wk{0, 0};
 #if PT_SIMPLE_STEP
     ClosestSrc src{P, hit};
-    trace_pool<false, COUNT, ClosestSrc, false>(n, nullptr, src, s_ref, wk);
+    trace_pool<false, COUNT, ClosestSrc, false>(n, nullptr, src, s_ref, nullptr, wk);
 #else
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     if (i < n) {
@@ -169,13 +171,13 @@ template <bool COUNT>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(PathSoA next, float4* __restrict__ done_L,
                                                           const ShadowRec* __restrict__ sq,
                                                           const uint32_t* __restrict__ nptr, uint32_t* __restrict__,
-                                                          unsigned long long* counters) {
+                                                          uint32_t* __restrict__, unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
     const uint32_t n = *nptr;
     TraceWork wk{0, 0};
     ShadowSrc src{sq, next, done_L};
 #if PT_SIMPLE_STEP
-    if (blockIdx.x * PT_TRACE_BLOCK < n) trace_pool<true, COUNT, ShadowSrc, false>(n, nullptr, src, s_ref, wk);
+    if (blockIdx.x * PT_TRACE_BLOCK < n) trace_pool<true, COUNT, ShadowSrc, false>(n, nullptr, src, s_ref, nullptr, wk);
 #else
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     if (i < n) {
@@ -208,12 +210,12 @@ struct RaysSrc {
 
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(const pt_ray* __restrict__ rays, uint32_t n, int any,
                                                               pt_hit* __restrict__ out, uint32_t* __restrict__ pool,
-                                                              unsigned long long* counters) {
-    __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+                                                              uint32_t* __restrict__ ovf, unsigned long long* counters) {
+    __shared__ uint32_t s_ref[PT_POOL_LDS * PT_TRACE_BLOCK];
     TraceWork wk{0, 0};
     RaysSrc src{rays, out};
-    if (any) trace_pool<true, true>(n, pool, src, s_ref, wk);
-    else trace_pool<false, true>(n, pool, src, s_ref, wk);
+    if (any) trace_pool<true, true>(n, pool, src, s_ref, ovf, wk);
+    else trace_pool<false, true>(n, pool, src, s_ref, ovf, wk);
     count_add(counters, any ? CNT_NODES_ANY : CNT_NODES_CLOSEST, wk.nodes);
     count_add(counters, any ? CNT_TRIS_ANY : CNT_TRIS_CLOSEST, wk.tris);
 }
@@ -688,18 +690,16 @@ __global__ __launch_bounds__(256) void k_gather(RenderParams R, const float* __r
 }
 
 // explicit instantiations used by the runtime
-template __global__ void k_closest<false>(PathSoA, uint32_t, float4*, uint32_t*, unsigned long long*);
-template __global__ void k_closest<true>(PathSoA, uint32_t, float4*, uint32_t*, unsigned long long*);
-template __global__ void k_closest_pool<false>(PathSoA, uint32_t, float4*, uint32_t*, unsigned long long*);
-template __global__ void k_closest_pool<true>(PathSoA, uint32_t, float4*, uint32_t*, unsigned long long*);
-template __global__ void k_shadow<false>(PathSoA, float4*, const ShadowRec*, const uint32_t*, uint32_t*,
-                                         unsigned long long*);
-template __global__ void k_shadow<true>(PathSoA, float4*, const ShadowRec*, const uint32_t*, uint32_t*,
-                                        unsigned long long*);
-template __global__ void k_shadow_pool<false>(PathSoA, float4*, const ShadowRec*, const uint32_t*, uint32_t*,
-                                              unsigned long long*);
-template __global__ void k_shadow_pool<true>(PathSoA, float4*, const ShadowRec*, const uint32_t*, uint32_t*,
-                                             unsigned long long*);
+#define PT_INST_TRACE(B)                                                                                            \
+    template __global__ void k_closest<B>(PathSoA, uint32_t, float4*, uint32_t*, uint32_t*, unsigned long long*);    \
+    template __global__ void k_closest_pool<B>(PathSoA, uint32_t, float4*, uint32_t*, uint32_t*,                     \
+                                               unsigned long long*);                                                 \
+    template __global__ void k_shadow<B>(PathSoA, float4*, const ShadowRec*, const uint32_t*, uint32_t*, uint32_t*,  \
+                                         unsigned long long*);                                                       \
+    template __global__ void k_shadow_pool<B>(PathSoA, float4*, const ShadowRec*, const uint32_t*, uint32_t*,        \
+                                              uint32_t*, unsigned long long*);
+PT_INST_TRACE(false)
+PT_INST_TRACE(true)
 template __global__ void k_shade<PT_INTEGRATOR_PATH>(RenderParams, PathSoA, uint32_t, const float4*, PathSoA,
                                                      float4*, uint32_t*, ShadowRec*, uint32_t*);
 template __global__ void k_shade<PT_INTEGRATOR_SIMPLE>(RenderParams, PathSoA, uint32_t, const float4*,

@@ -21,8 +21,12 @@
 #define PT_POOL_CHUNKS 8
 #define PT_POOL_STRIDE 32  // uint32 words between chunk counters (128 B)
 #define PT_POOL_WORDS (PT_POOL_CHUNKS * PT_POOL_STRIDE)
-#ifndef PT_POOL_STEP
-#define PT_POOL_STEP 1
+// Stack entries the pool kernels keep in LDS; entries [PT_POOL_LDS, PT_STACK)
+// live in a global overflow array ([entry][grid lane], written and read back by
+// the same lane only).  Deep stacks are rare, and a 20-entry LDS stack (10 KB
+// per block) lets 32 waves per CU fit instead of 20 with all 32 in LDS.
+#ifndef PT_POOL_LDS
+#define PT_POOL_LDS 20
 #endif
 #ifndef PT_POOL_CHECK
 #define PT_POOL_CHECK 0
@@ -37,6 +41,39 @@ __device__ unsigned int pt_diag[4];
 #define PT_REFILL 8
 #endif
 
+// 4-wide slab test (BVH.hpp:1049-1092 / 1140-1183), children in pairs on the
+// packed-FP32 ALU (v_pk_add_f32 / v_pk_mul_f32: two lanes per instruction,
+// each lane the same rounded (bound - o) * inv as the scalar form)
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void slab4p(float4 xmn, float4 xmx, float4 ymn, float4 ymx, float4 zmn, float4 zmx, f3 o,
+                                       f3 inv, float tmax, uint32_t& mask) {
+    const v2f ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+    const v2f ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
+    v2f t[2][6];
+    t[0][0] = (v2f{xmn.x, xmn.y} - ox) * ix;
+    t[1][0] = (v2f{xmn.z, xmn.w} - ox) * ix;
+    t[0][1] = (v2f{xmx.x, xmx.y} - ox) * ix;
+    t[1][1] = (v2f{xmx.z, xmx.w} - ox) * ix;
+    t[0][2] = (v2f{ymn.x, ymn.y} - oy) * iy;
+    t[1][2] = (v2f{ymn.z, ymn.w} - oy) * iy;
+    t[0][3] = (v2f{ymx.x, ymx.y} - oy) * iy;
+    t[1][3] = (v2f{ymx.z, ymx.w} - oy) * iy;
+    t[0][4] = (v2f{zmn.x, zmn.y} - oz) * iz;
+    t[1][4] = (v2f{zmn.z, zmn.w} - oz) * iz;
+    t[0][5] = (v2f{zmx.x, zmx.y} - oz) * iz;
+    t[1][5] = (v2f{zmx.z, zmx.w} - oz) * iz;
+    mask = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int h = i >> 1, l = i & 1;
+        const float tx1 = t[h][0][l], tx2 = t[h][1][l], ty1 = t[h][2][l], ty2 = t[h][3][l];
+        const float tz1 = t[h][4][l], tz2 = t[h][5][l];
+        const float tEntry = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+        const float tExit = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+        if (tExit >= PT_EPS && tEntry < tmax && tEntry <= tExit) mask |= 1u << i;
+    }
+}
+
 // Src interface:
 //   bool load(uint32_t ri, f3& o, f3& d, float& tmax)   (false: skip this ray)
 //   void closest(uint32_t ri, float t, float b1, float b2, int prim)
@@ -44,8 +81,13 @@ __device__ unsigned int pt_diag[4];
 // POOL = false: no refill, lane i of the grid traces ray i (small scenes,
 // where traversal lengths are uniform and the claims would only cost).
 template <bool ANY, bool COUNT, class Src, bool POOL = true>
-__device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, uint32_t* s_ref, TraceWork& wk) {
+__device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, uint32_t* s_ref,
+                           uint32_t* __restrict__ ovf, TraceWork& wk) {
     const uint32_t lane = threadIdx.x;
+    // LDS part of the stack; the rest in ovf (pool kernels only: their grid is
+    // bounded by the resident blocks, which sizes ovf)
+    constexpr int LN = POOL ? PT_POOL_LDS : PT_STACK;
+    const uint32_t gl = blockIdx.x * PT_TRACE_BLOCK + lane, G = gridDim.x * PT_TRACE_BLOCK;
     const uint32_t wl = __lane_id();
     const uint32_t cs = (n + PT_POOL_CHUNKS - 1) / PT_POOL_CHUNKS;
     const uint32_t home = blockIdx.x % PT_POOL_CHUNKS;
@@ -58,6 +100,19 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
     int sp = 0, best = -1;
 
     const uint32_t all_dead = (1u << PT_POOL_CHUNKS) - 1u;
+    // pushes beyond PT_STACK are dropped, like the one-ray-per-lane kernels
+    auto push = [&](uint32_t v) {
+        if (sp < PT_STACK) {
+            if (LN >= PT_STACK || sp < LN) s_ref[sp * PT_TRACE_BLOCK + lane] = v;
+            else ovf[(size_t)(sp - LN) * G + gl] = v;
+            ++sp;
+        }
+    };
+    auto pop = [&]() -> uint32_t {
+        --sp;
+        if (LN >= PT_STACK || sp < LN) return s_ref[sp * PT_TRACE_BLOCK + lane];
+        return ovf[(size_t)(sp - LN) * G + gl];
+    };
     if (!POOL) {
         const uint32_t gi = blockIdx.x * PT_TRACE_BLOCK + lane;
         if (gi < n && src.load(gi, o, d, tmax)) {
@@ -118,7 +173,6 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         }
         if (ri < 0) continue;
 
-#if PT_POOL_STEP == 1
         // ---- one step of this lane's traversal: one cluster or ONE leaf
         // primitive.  Node lanes and primitive lanes issue their loads in the
         // same pass (one memory round trip per step for the whole wave);
@@ -130,8 +184,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 ri = -1;
                 continue;
             }
-            --sp;
-            ref = s_ref[sp * PT_TRACE_BLOCK + lane];
+            ref = pop();
         }
         const bool node_step = !(ref & REF_LEAF);
         const uint32_t idx = ref & ~REF_LEAF;
@@ -154,51 +207,31 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         const float4 q3 = q[3 * nk], q4 = q[4 * nk], q5 = q[5 * nk], q6 = q[6 * nk], q7 = q[7 * nk];
         {
             uint32_t mask;
-            float te[4];
-            slab4q(q0, q1, q2, q3, q4, q5, o, inv, tmax, mask, te);
-            if (!node_step) mask = 0;
-            const uint4 ch = make_uint4(__float_as_uint(q6.x), __float_as_uint(q6.y), __float_as_uint(q6.z),
-                                        __float_as_uint(q6.w));
-            uint32_t cand = REF_EMPTY;
-            if (ANY) {
-                // slot order, last visited next (BVH.hpp:1099-1102)
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    if ((mask >> i) & 1u) {
-                        const uint32_t c = sel4u((uint32_t)i, ch);
-                        if (c != REF_EMPTY) {
-                            if (cand != REF_EMPTY && sp < PT_STACK) {
-                                s_ref[sp * PT_TRACE_BLOCK + lane] = cand;
-                                ++sp;
-                            }
-#if PT_POOL_CHECK
-                            else if (cand != REF_EMPTY) atomicAdd(&pt_diag[3], 1u);
-#endif
-                            cand = c;
-                        }
-                    }
-                }
-            } else {
-                // octant order far -> near (BVH4::LUT, BVH.hpp:1195-1204)
+            slab4p(q0, q1, q2, q3, q4, q5, o, inv, tmax, mask);
+            const uint32_t c0 = __float_as_uint(q6.x), c1 = __float_as_uint(q6.y), c2 = __float_as_uint(q6.z),
+                           c3 = __float_as_uint(q6.w);
+            // children that pass the slab test and exist; none on primitive lanes
+            const uint32_t vm = node_step ? mask & ((uint32_t)(c0 != REF_EMPTY) | (uint32_t)(c1 != REF_EMPTY) << 1 |
+                                                    (uint32_t)(c2 != REF_EMPTY) << 2 | (uint32_t)(c3 != REF_EMPTY) << 3)
+                                          : 0u;
+            // visit order: slot order for any hit (BVH.hpp:1099-1102), octant
+            // order far -> near for closest hit (BVH4::LUT, BVH.hpp:1195-1204);
+            // every valid child but the last is pushed, the last is visited next.
+            // Selects only: the one conditional is the stack store itself.
+            uint32_t perm = 0xE4u;  // identity 0,1,2,3
+            if (!ANY) {
                 const uint32_t ow = __float_as_uint((oct >> 2) ? q7.y : q7.x);
-                const uint32_t perm = (ow >> (8 * (oct & 3))) & 0xFFu;
+                perm = (ow >> (8 * (oct & 3))) & 0xFFu;
+            }
+            uint32_t cand = REF_EMPTY;
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t ci = (perm >> (2 * k)) & 3u;
-                    if ((mask >> ci) & 1u) {
-                        const uint32_t c = sel4u(ci, ch);
-                        if (c != REF_EMPTY) {
-                            if (cand != REF_EMPTY && sp < PT_STACK) {
-                                s_ref[sp * PT_TRACE_BLOCK + lane] = cand;
-                                ++sp;
-                            }
-#if PT_POOL_CHECK
-                            else if (cand != REF_EMPTY) atomicAdd(&pt_diag[3], 1u);
-#endif
-                            cand = c;
-                        }
-                    }
-                }
+            for (int k = 0; k < 4; k++) {
+                const uint32_t ci = (perm >> (2 * k)) & 3u;
+                const uint32_t lo = (ci & 1u) ? c1 : c0, hi = (ci & 1u) ? c3 : c2;
+                const uint32_t c = (ci & 2u) ? hi : lo;
+                const bool v = (vm >> ci) & 1u;
+                if (v && cand != REF_EMPTY) push(cand);
+                cand = v ? c : cand;
             }
             if (node_step) {
                 if (COUNT) wk.nodes++;
@@ -233,10 +266,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 }
             } else if (kind == PT_PRIM_BLAS) {
                 if (COUNT) wk.tris--;
-                if (sp < PT_STACK) {
-                    s_ref[sp * PT_TRACE_BLOCK + lane] = __float_as_uint(q1.x);
-                    ++sp;
-                }
+                push(__float_as_uint(q1.x));
             } else if (ANY) {
                 if (other_pred(slot, w0, o, d, tmax)) anyhit = true;
             } else {
@@ -254,120 +284,5 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 ri = -1;
             }
         }
-#else
-        // ---- one step of this lane's traversal
-        if (ref == REF_EMPTY) {
-            if (sp == 0) {  // finished: no hit (any) / closest result
-                if (ANY) src.any((uint32_t)ri, false);
-                else src.closest((uint32_t)ri, tmax, bb1, bb2, best);
-                ri = -1;
-                continue;
-            }
-            --sp;
-            ref = s_ref[sp * PT_TRACE_BLOCK + lane];
-        }
-        if (!(ref & REF_LEAF)) {
-            const DevCluster* node = S.nodes + ref;
-            if (COUNT) wk.nodes++;
-            uint32_t mask;
-            float te[4];
-            slab4<COUNT>(node, o, inv, tmax, mask, te);
-            const uint4 ch = *reinterpret_cast<const uint4*>(&node->child[0]);
-            uint32_t cand = REF_EMPTY;
-            if (ANY) {
-                // slot order, last visited next (BVH.hpp:1099-1102)
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    if ((mask >> i) & 1u) {
-                        const uint32_t c = sel4u((uint32_t)i, ch);
-                        if (c != REF_EMPTY) {
-                            if (cand != REF_EMPTY && sp < PT_STACK) {
-                                s_ref[sp * PT_TRACE_BLOCK + lane] = cand;
-                                ++sp;
-                            }
-#if PT_POOL_CHECK
-                            else if (cand != REF_EMPTY) atomicAdd(&pt_diag[3], 1u);
-#endif
-                            cand = c;
-                        }
-                    }
-                }
-            } else {
-                // octant order far -> near (BVH4::LUT, BVH.hpp:1195-1204)
-                const uint32_t ow = node->order[oct >> 2];
-                const uint32_t perm = (ow >> (8 * (oct & 3))) & 0xFFu;
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint32_t idx = (perm >> (2 * k)) & 3u;
-                    if ((mask >> idx) & 1u) {
-                        const uint32_t c = sel4u(idx, ch);
-                        if (c != REF_EMPTY) {
-                            if (cand != REF_EMPTY && sp < PT_STACK) {
-                                s_ref[sp * PT_TRACE_BLOCK + lane] = cand;
-                                ++sp;
-                            }
-#if PT_POOL_CHECK
-                            else if (cand != REF_EMPTY) atomicAdd(&pt_diag[3], 1u);
-#endif
-                            cand = c;
-                        }
-                    }
-                }
-            }
-            ref = cand;
-            continue;
-        }
-        // leaf: primitives from slot until the one flagged LAST
-        uint32_t slot = ref & ~REF_LEAF;
-        ref = REF_EMPTY;
-        bool anyhit = false;
-        for (;;) {
-            const DevGeom g = S.geom[slot];
-            const uint32_t w0 = __float_as_uint(g.a.w);
-            const uint32_t kind = w0 & GF_KIND;
-            if (COUNT) wk.tris++;
-            if (kind == PT_PRIM_TRIANGLE) {
-                if (ANY && !(w0 & GF_PRED_GLM)) {
-                    if (tri_pred(o, d, xyz(g.a), xyz(g.b), xyz(g.c), tmax)) anyhit = true;
-                } else {
-                    float bx, by, t;
-                    if (tri_glm(o, d, xyz(g.a), xyz(g.b), xyz(g.c), bx, by, t) && !(t > tmax || t < PT_EPS)) {
-                        if (!(w0 & GF_ALPHA) || tri_alpha(slot, bx, by, o, d)) {
-                            if (ANY) {
-                                anyhit = true;
-                            } else {
-                                tmax = t;
-                                best = (int)slot;
-                                bb1 = bx;
-                                bb2 = by;
-                            }
-                        }
-                    }
-                }
-            } else if (kind == PT_PRIM_BLAS) {
-                if (COUNT) wk.tris--;
-                if (sp < PT_STACK) {
-                    s_ref[sp * PT_TRACE_BLOCK + lane] = __float_as_uint(g.b.x);
-                    ++sp;
-                }
-            } else if (ANY) {
-                if (other_pred(slot, w0, o, d, tmax)) anyhit = true;
-            } else {
-                float t, a, b;
-                if (other_closest(slot, w0, o, d, tmax, t, a, b)) {
-                    tmax = t;
-                    best = (int)slot;
-                    bb1 = a;
-                    bb2 = b;
-                }
-            }
-            if (anyhit || (w0 & GF_LAST)) break;
-            ++slot;
-        }
-        if (ANY && anyhit) {  // early exit (BVH.hpp:1104-1105)
-            src.any((uint32_t)ri, true);
-            ri = -1;
-        }
-#endif
     }
 }

@@ -37,6 +37,7 @@ struct pt_ctx {
     float4* hit = nullptr;
     float4* done_L = nullptr;
     uint32_t *done_sid = nullptr, *qcnt = nullptr;
+    uint32_t* ovf = nullptr;  // pool traversal stack entries beyond PT_POOL_LDS
     ShadowRec* sq = nullptr;
     unsigned long long* counters = nullptr;
     uint32_t* host_cnt = nullptr;  // pinned
@@ -97,15 +98,19 @@ extern "C" pt_status pt_create(pt_ctx** out, int device) {
         }
     }
     {
-        int cus = 0, per_cu = 0;
+        // the persistent (pool) traversal grid: the blocks of the pool kernels
+        // that are resident together (the fewer of closest / any hit)
+        int cus = 0, per_cu = 0, per_cu_any = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_closest<false>),
-                                                         PT_TRACE_BLOCK, 0) != hipSuccess) {
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_closest_pool<false>),
+                                                         PT_TRACE_BLOCK, 0) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &per_cu_any, reinterpret_cast<const void*>(&k_shadow_pool<false>), PT_TRACE_BLOCK, 0) != hipSuccess) {
             g_err = "occupancy query failed";
             delete c;
             return PT_ERR_HIP;
         }
-        c->trace_blocks = (uint32_t)std::max(1, cus * std::max(1, per_cu));
+        c->trace_blocks = (uint32_t)std::max(1, cus * std::max(1, std::min(per_cu, per_cu_any)));
     }
     if (hipHostMalloc((void**)&c->host_cnt, Q_WORDS * 4) != hipSuccess) {
         g_err = "pinned alloc failed";
@@ -124,7 +129,7 @@ static void free_scene(pt_ctx* c) {
 }
 static void free_work(pt_ctx* c) {
     void* bufs[] = {c->PA.o, c->PA.d, c->PA.beta, c->PA.L, c->PA.sid, c->PB.o, c->PB.d, c->PB.beta, c->PB.L,
-                    c->PB.sid, c->hit, c->done_L, c->done_sid, c->qcnt, c->sq, c->counters};
+                    c->PB.sid, c->hit, c->done_L, c->done_sid, c->qcnt, c->sq, c->counters, c->ovf};
     for (void* p : bufs)
         if (p) hipFree(p);
     c->PA = PathSoA{};
@@ -133,6 +138,7 @@ static void free_work(pt_ctx* c) {
     c->done_sid = c->qcnt = nullptr;
     c->sq = nullptr;
     c->counters = nullptr;
+    c->ovf = nullptr;
     c->cap = 0;
 }
 
@@ -464,6 +470,7 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
     AL(c->qcnt, (Q_WORDS + 3 * PT_POOL_WORDS) * 4);  // queue counters, then the traversal pools
     AL(c->sq, n * sizeof(ShadowRec));
     AL(c->counters, (CNT_SHARDS + 1) * CNT_COUNT * 8);
+    if (PT_STACK > PT_POOL_LDS) AL(c->ovf, (size_t)c->trace_blocks * PT_TRACE_BLOCK * (PT_STACK - PT_POOL_LDS) * 4);
 #undef AL
     if (hipMemset(c->qcnt, 0, (Q_WORDS + 3 * PT_POOL_WORDS) * 4) != hipSuccess) {
         free_work(c);
@@ -483,6 +490,12 @@ static double gauss_h(double x, double sigma) {
 // chunk's per-sample radiance to `on_chunk`.
 // Makes this context's scene the one the kernels read (constant-memory `S`),
 // ordered on the context's stream.  Called by every entry point that launches.
+#ifndef PT_PATHS_POOL
+#define PT_PATHS_POOL (1u << 24)
+#endif
+#ifndef PT_PATHS_SIMPLE
+#define PT_PATHS_SIMPLE (1u << 21)
+#endif
 #define PT_POOL_MIN_CLUSTERS (1u << 20)  // measured: C4 (2.6M clusters) gains 31%; 0.5M-cluster heightfield and C2/C3 lose
 
 static pt_status bind_scene(pt_ctx* c) {
@@ -541,7 +554,11 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     uint32_t s_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spp_local, max_floats / per_s));
     pt_status st = ensure(c, &c->sample_L, c->sample_cap, per_s * s_chunk);
     if (st) return st;
-    uint32_t paths = rd->paths_in_flight ? rd->paths_in_flight : (1u << 21);
+    // wavefront size: large scenes (pool traversal) take 16 M paths in flight,
+    // so each traversal launch's tail (the last, longest rays) is amortised
+    // over more rays (C4 at 256 spp: 2 M -> 8 M paths +22 %, 8 M -> 16 M +5 %)
+    const bool big_scene = c->n_clusters >= PT_POOL_MIN_CLUSTERS;
+    uint32_t paths = rd->paths_in_flight ? rd->paths_in_flight : (big_scene ? PT_PATHS_POOL : PT_PATHS_SIMPLE);
     paths = (uint32_t)std::min<uint64_t>(paths, std::max<uint64_t>(1, (uint64_t)R.npix_work * s_chunk));
     paths = (paths + 255) & ~255u;
     if ((st = ensure_work(c, paths)) != PT_OK) return st;
@@ -597,7 +614,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             {
                 auto kc = use_pool ? (count ? k_closest_pool<true> : k_closest_pool<false>)
                                    : (count ? k_closest<true> : k_closest<false>);
-                hipLaunchKernelGGL(kc, gt, dim3(PT_TRACE_BLOCK), 0, sm, cur, n_active, c->hit, pool_closest,
+                hipLaunchKernelGGL(kc, gt, dim3(PT_TRACE_BLOCK), 0, sm, cur, n_active, c->hit, pool_closest, c->ovf,
                                    c->counters);
             }
             if (timing) HIPCHK(c, hipEventRecord(c->ev[1], sm));
@@ -612,7 +629,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                 auto ks = use_pool ? (count ? k_shadow_pool<true> : k_shadow_pool<false>)
                                    : (count ? k_shadow<true> : k_shadow<false>);
                 hipLaunchKernelGGL(ks, gt, dim3(PT_TRACE_BLOCK), 0, sm, nxt, c->done_L, (const ShadowRec*)c->sq,
-                                   (const uint32_t*)(c->qcnt + Q_SHADOW), pool_shadow, c->counters);
+                                   (const uint32_t*)(c->qcnt + Q_SHADOW), pool_shadow, c->ovf, c->counters);
             }
             if (timing) HIPCHK(c, hipEventRecord(c->ev[3], sm));
             hipLaunchKernelGGL(k_finish, gs, dim3(256), 0, sm, R, (const float4*)c->done_L,
@@ -786,7 +803,7 @@ extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any
     HIPCHK(c, hipMemsetAsync(pool, 0, PT_POOL_WORDS * 4, c->stream));
     hipLaunchKernelGGL(k_trace_rays,
                        dim3(std::max(1u, std::min((n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK, c->trace_blocks))),
-                       dim3(PT_TRACE_BLOCK), 0, c->stream, dr, n, any_hit, dh, pool, c->counters);
+                       dim3(PT_TRACE_BLOCK), 0, c->stream, dr, n, any_hit, dh, pool, c->ovf, c->counters);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
     if (!hdev) HIPCHK(c, hipMemcpyAsync(hits, dh, (size_t)n * sizeof(pt_hit), hipMemcpyDeviceToHost, c->stream));
