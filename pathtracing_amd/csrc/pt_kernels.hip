@@ -61,6 +61,17 @@ __device__ __forceinline__ void count_add(unsigned long long* counters, int whic
 }
 
 // ------------------------------------------------------------------ traversal kernels
+// Register budget of the pool kernels: PT_POOL_WPE waves per SIMD.  7 (72
+// VGPRs, no hot-path spills) measured +4.5 % on C4 over the unconstrained 76;
+// 8 (64 VGPRs) spills inside the step loop and loses 30 %.
+#ifndef PT_POOL_WPE
+#define PT_POOL_WPE 7
+#endif
+#if PT_POOL_WPE
+#define PT_POOL_WAVES __attribute__((amdgpu_waves_per_eu(PT_POOL_WPE, PT_POOL_WPE)))
+#else
+#define PT_POOL_WAVES
+#endif
 // Persistent, refilling traversal (pt_pool.h): grid = resident blocks, rays
 // claimed from the pool counters (zeroed with the queue counters).
 struct ClosestSrc {
@@ -79,7 +90,7 @@ struct ClosestSrc {
 };
 
 template <bool COUNT>
-__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest_pool(PathSoA P, uint32_t n, float4* __restrict__ hit,
+__global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_closest_pool(PathSoA P, uint32_t n, float4* __restrict__ hit,
                                                                 uint32_t* __restrict__ pool, uint32_t* __restrict__ ovf,
                                                                 unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_POOL_LDS * PT_TRACE_BLOCK];
@@ -120,7 +131,7 @@ struct ShadowSrc {
 };
 
 template <bool COUNT>
-__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow_pool(PathSoA next, float4* __restrict__ done_L,
+__global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_shadow_pool(PathSoA next, float4* __restrict__ done_L,
                                                                const ShadowRec* __restrict__ sq,
                                                                const uint32_t* __restrict__ nptr,
                                                                uint32_t* __restrict__ pool, uint32_t* __restrict__ ovf,

@@ -136,6 +136,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             uint32_t base = 0, got = 0;
             if (dead != all_dead) {
                 if (wl == 0) {
+                    #pragma unroll 1
                     for (uint32_t k = 0; k < PT_POOL_CHUNKS; k++) {
                         const uint32_t c = (home + k) % PT_POOL_CHUNKS;
                         if ((dead >> c) & 1u) continue;
