@@ -11,10 +11,19 @@
 // ~88 atomics/us: MI355X_MICROARCH.md "dequeue"); appends are aggregated per
 // block so a launch issues one atomic per block per counter
 #define Q_STRIDE 32
-#define Q_NEXT 0
-#define Q_DONE (1 * Q_STRIDE)
-#define Q_SHADOW (2 * Q_STRIDE)
+#define Q_NEXT 0                 // continuing paths, appended from the front
+#define Q_SHADOW (1 * Q_STRIDE)  // shadow rays
+#define Q_NEW (2 * Q_STRIDE)     // new camera paths, appended from the back
 #define Q_WORDS (3 * Q_STRIDE)
+// one counter set: the queue counts an iteration produces, then the pools its
+// two traversals claim rays from.  The runtime rotates three sets: iteration i
+// reads its input count from set i % 3 (written by iteration i - 1), appends
+// into set (i + 1) % 3 and zeroes set (i + 2) % 3 for iteration i + 1.
+#define SET_WORDS (Q_WORDS + 2 * PT_POOL_WORDS)
+// host snapshot slot (pinned, written by the iteration prologue)
+#define SNAP_PATHS 0        // paths entering the iteration
+#define SNAP_SHADOW_PREV 1  // shadow rays of the previous iteration
+#define SNAP_WORDS 16
 
 // 64-bit work counters
 #define CNT_NODES_CLOSEST 0
@@ -28,13 +37,21 @@
 // Compacted path state: the live paths of one bounce occupy entries
 // [0, n) of these arrays, so every kernel reads and writes them coalesced
 // (lane i <-> entry i; appends are contiguous per wave).  64 B per path.
+// Continuing paths fill entries [0, c) from the front and new camera paths
+// [cap - r, cap) from the back, so camera rays stay in coherent waves of their
+// own; path i of an iteration (i < c + r) lives at path_slot(i).
 struct PathSoA {
     float4* o;    // origin.xyz, stream key (bits)
     float4* d;    // direction.xyz, flags (bits): depth | rr << 12 | spec
     float4* beta; // attenuation.xyz, prevPDF
     float4* L;    // radiance so far .xyz, next draw dimension (bits)
     uint32_t* sid;// sample id within the chunk
+    uint32_t cap; // entries
 };
+__device__ __forceinline__ uint32_t path_count(const uint32_t* set) { return set[Q_NEXT] + set[Q_NEW]; }
+__device__ __forceinline__ uint32_t path_slot(uint32_t i, uint32_t c, uint32_t cap) {
+    return i < c ? i : cap - 1u - (i - c);
+}
 
 struct ShadowRec {
     float4 o;  // origin, tmax
@@ -61,23 +78,21 @@ struct RenderParams {
 };
 
 template <bool COUNT>
-__global__ void k_closest(PathSoA P, uint32_t n, float4* hit, uint32_t* pool, uint32_t* ovf,
-                          unsigned long long* counters);
+__global__ void k_closest(PathSoA P, const uint32_t* in, float4* hit, uint32_t* pool, uint32_t* ovf, uint32_t* spare,
+                          uint32_t* snap, unsigned long long* counters);
 template <bool COUNT>
-__global__ void k_closest_pool(PathSoA P, uint32_t n, float4* hit, uint32_t* pool, uint32_t* ovf,
-                               unsigned long long* counters);
+__global__ void k_closest_pool(PathSoA P, const uint32_t* in, float4* hit, uint32_t* pool, uint32_t* ovf,
+                               uint32_t* spare, uint32_t* snap, unsigned long long* counters);
 template <bool COUNT>
-__global__ void k_shadow(PathSoA next, float4* done_L, const ShadowRec* sq, const uint32_t* nptr, uint32_t* pool,
+__global__ void k_shadow(PathSoA next, float* sample_L, const ShadowRec* sq, const uint32_t* nptr, uint32_t* pool,
                          uint32_t* ovf, unsigned long long* counters);
 template <bool COUNT>
-__global__ void k_shadow_pool(PathSoA next, float4* done_L, const ShadowRec* sq, const uint32_t* nptr, uint32_t* pool,
-                              uint32_t* ovf, unsigned long long* counters);
+__global__ void k_shadow_pool(PathSoA next, float* sample_L, const ShadowRec* sq, const uint32_t* nptr,
+                              uint32_t* pool, uint32_t* ovf, unsigned long long* counters);
 template <int INTEGRATOR>
-__global__ void k_shade(RenderParams R, PathSoA cur, uint32_t n, const float4* hit, PathSoA next,
-                        float4* done_L, uint32_t* done_sid, ShadowRec* sq, uint32_t* cnt);
-__global__ void k_finish(RenderParams R, const float4* done_L, const uint32_t* done_sid, const uint32_t* nptr,
-                         uint32_t n_direct, PathSoA next, uint32_t* cnt, unsigned long long* next_sample,
-                         float* sample_L);
+__global__ void k_shade(RenderParams R, PathSoA cur, const uint32_t* nptr, const float4* hit, PathSoA next,
+                        float* sample_L, unsigned long long* next_sample, ShadowRec* sq, uint32_t* cnt);
+__global__ void k_fill(RenderParams R, uint32_t n, PathSoA next, uint32_t* cnt, unsigned long long* next_sample);
 __global__ void k_gather(RenderParams R, const float* sample_L, double* film);
 __global__ void k_interact(const pt_ray* rays, uint32_t n, float* out);
 __global__ void k_bsdf_cases(int mid, const float* in, uint32_t n, float* out);

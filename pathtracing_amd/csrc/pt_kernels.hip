@@ -1,18 +1,22 @@
 // Wavefront path tracer kernels for gfx950 (CDNA4).
 //
 // One iteration of the persistent wavefront (host loop in pt_runtime.hip):
-//   k_closest  closest-hit traversal of every active path's ray
+//   k_closest  closest-hit traversal of every active path's ray (its block 0
+//              also zeroes the next counter set and publishes the input count
+//              to the host's pinned snapshot)
 //   k_shade    one body of PathIntegrator::Li / SimplePathIntegrator::Li
 //              (Integrators.cpp:131-294): miss -> infinite lights, emission
 //              with MIS, scatter, NEE light sample -> shadow queue, RR;
-//              continuing paths -> next active queue, finished -> done queue
-//   k_shadow   any-hit of the NEE rays; unoccluded -> contribution added
-//   k_finish   finished paths write their sample radiance, and the slot is
-//              refilled with the next camera sample (Camera::GenerateRay)
+//              continuing paths -> next state; finished paths store their
+//              sample's radiance and their entry takes the next camera sample
+//              (Camera::GenerateRay)
+//   k_shadow   any-hit of the NEE rays; unoccluded -> contribution added to
+//              the path (or to the finished sample's radiance)
+//   k_fill     the initial camera samples of a chunk
 //   k_gather   after a sample chunk: every pixel gathers the Mitchell/box/
 //              Gaussian-weighted samples of its neighbourhood (FilmTile::Add,
-//              Film.hpp:65-82) in float64 — deterministic, no atomics.
-// Queue appends are wave-aggregated: one atomic per wave (__ballot/__popcll).
+//              Film.hpp:65-82) in float64 -- deterministic, no atomics.
+// Queue appends are block-aggregated: one atomic per block (__ballot/__popcll).
 #include "pt_kernels.h"
 
 // ------------------------------------------------------------------ append helpers
@@ -60,6 +64,20 @@ __device__ __forceinline__ void count_add(unsigned long long* counters, int whic
     if (__lane_id() == 0 && s) atomicAdd(&counters[(blockIdx.x % CNT_SHARDS) * CNT_COUNT + which], (unsigned long long)s);
 }
 
+// Wavefront iteration prologue, run by block 0 of the iteration's first kernel
+// (the closest-hit traversal): zero the spare counter set (the next
+// iteration's output) and publish this iteration's input counts to the host's
+// pinned snapshot slot, so the host learns them without a copy or a sync.
+__device__ __forceinline__ void iteration_prologue(const uint32_t* __restrict__ in, uint32_t* __restrict__ spare,
+                                                   uint32_t* __restrict__ snap) {
+    if (blockIdx.x != 0 || !spare) return;
+    for (uint32_t k = threadIdx.x; k < SET_WORDS; k += blockDim.x) spare[k] = 0;
+    if (threadIdx.x == 0) {
+        snap[SNAP_PATHS] = path_count(in);
+        snap[SNAP_SHADOW_PREV] = in[Q_SHADOW];
+    }
+}
+
 // ------------------------------------------------------------------ traversal kernels
 // Register budget of the pool kernels: PT_POOL_WPE waves per SIMD.  7 (72
 // VGPRs, no hot-path spills) measured +4.5 % on C4 over the unconstrained 76;
@@ -77,9 +95,11 @@ __device__ __forceinline__ void count_add(unsigned long long* counters, int whic
 struct ClosestSrc {
     PathSoA P;
     float4* hit;
+    uint32_t front;  // continuing paths at the front of P
     __device__ __forceinline__ bool load(uint32_t i, f3& o, f3& d, float& tmax) {
-        o = xyz(P.o[i]);
-        d = xyz(P.d[i]);
+        const uint32_t e = path_slot(i, front, P.cap);
+        o = xyz(P.o[e]);
+        d = xyz(P.d[e]);
         tmax = __int_as_float(0x7f800000);
         return true;
     }
@@ -90,12 +110,17 @@ struct ClosestSrc {
 };
 
 template <bool COUNT>
-__global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_closest_pool(PathSoA P, uint32_t n, float4* __restrict__ hit,
-                                                                uint32_t* __restrict__ pool, uint32_t* __restrict__ ovf,
+__global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_closest_pool(PathSoA P, const uint32_t* __restrict__ nptr,
+                                                                float4* __restrict__ hit, uint32_t* __restrict__ pool,
+                                                                uint32_t* __restrict__ ovf, uint32_t* __restrict__ spare,
+                                                                uint32_t* __restrict__ snap,
                                                                 unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_POOL_LDS * PT_TRACE_BLOCK];
+    iteration_prologue(nptr, spare, snap);
+    const uint32_t n = path_count(nptr);
+    if (n == 0) return;
     TraceWork wk{0, 0};
-    ClosestSrc src{P, hit};
+    ClosestSrc src{P, hit, nptr[Q_NEXT]};
     trace_pool<false, COUNT>(n, pool, src, s_ref, ovf, wk);
     if (COUNT) {
         count_add(counters, CNT_NODES_CLOSEST, wk.nodes);
@@ -106,7 +131,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_closest_pool(P
 struct ShadowSrc {
     const ShadowRec* sq;
     PathSoA next;
-    float4* done_L;
+    float* sample_L;
     __device__ __forceinline__ bool load(uint32_t i, f3& o, f3& d, float& tmax) {
         const float4 ro = sq[i].o, rd = sq[i].d;
         o = xyz(ro);
@@ -121,7 +146,14 @@ struct ShadowSrc {
         // so a plain read-modify-write
         const uint32_t tgt = __float_as_uint(sq[i].d.w);
         const float4 c = sq[i].c;
-        float4* L = (tgt & SHADOW_DONE_BIT) ? &done_L[tgt & ~SHADOW_DONE_BIT] : &next.L[tgt];
+        if (tgt & SHADOW_DONE_BIT) {  // the path ended this bounce: its sample's radiance
+            float* L = sample_L + 3ull * (tgt & ~SHADOW_DONE_BIT);
+            L[0] += c.x;
+            L[1] += c.y;
+            L[2] += c.z;
+            return;
+        }
+        float4* L = &next.L[tgt];
         float4 v = *L;
         v.x += c.x;
         v.y += c.y;
@@ -131,15 +163,17 @@ struct ShadowSrc {
 };
 
 template <bool COUNT>
-__global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_shadow_pool(PathSoA next, float4* __restrict__ done_L,
+__global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_shadow_pool(PathSoA next, float* __restrict__ sample_L,
                                                                const ShadowRec* __restrict__ sq,
                                                                const uint32_t* __restrict__ nptr,
                                                                uint32_t* __restrict__ pool, uint32_t* __restrict__ ovf,
                                                                unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_POOL_LDS * PT_TRACE_BLOCK];
     TraceWork wk{0, 0};
-    ShadowSrc src{sq, next, done_L};
-    trace_pool<true, COUNT>(*nptr, pool, src, s_ref, ovf, wk);
+    ShadowSrc src{sq, next, sample_L};
+    const uint32_t n = *nptr;
+    if (n == 0) return;
+    trace_pool<true, COUNT>(n, pool, src, s_ref, ovf, wk);
     if (COUNT) {
         count_add(counters, CNT_NODES_ANY, wk.nodes);
         count_add(counters, CNT_TRIS_ANY, wk.tris);
@@ -155,18 +189,23 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_shadow_pool(Pa
 #define PT_SIMPLE_STEP 0
 #endif
 template <bool COUNT>
-__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(PathSoA P, uint32_t n, float4* __restrict__ hit,
-                                                           uint32_t* __restrict__, uint32_t* __restrict__,
-                                                           unsigned long long* counters) {
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(PathSoA P, const uint32_t* __restrict__ nptr,
+                                                           float4* __restrict__ hit, uint32_t* __restrict__,
+                                                           uint32_t* __restrict__, uint32_t* __restrict__ spare,
+                                                           uint32_t* __restrict__ snap, unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+    iteration_prologue(nptr, spare, snap);
+    const uint32_t n = path_count(nptr);  // the grid covers the wavefront's capacity
+    if (blockIdx.x * PT_TRACE_BLOCK >= n) return;
     TraceWork wk{0, 0};
 #if PT_SIMPLE_STEP
-    ClosestSrc src{P, hit};
+    ClosestSrc src{P, hit, nptr[Q_NEXT]};
     trace_pool<false, COUNT, ClosestSrc, false>(n, nullptr, src, s_ref, nullptr, wk);
 #else
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     if (i < n) {
-        const float4 o = P.o[i], d = P.d[i];
+        const uint32_t e = path_slot(i, nptr[Q_NEXT], P.cap);
+        const float4 o = P.o[e], d = P.d[e];
         float t, b1, b2;
         int prim = trace_closest<COUNT>(xyz(o), xyz(d), __int_as_float(0x7f800000), t, b1, b2, s_ref, wk);
         hit[i] = make_float4(t, b1, b2, __int_as_float(prim));
@@ -179,14 +218,15 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(PathSoA P, uint32_t 
 }
 
 template <bool COUNT>
-__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(PathSoA next, float4* __restrict__ done_L,
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(PathSoA next, float* __restrict__ sample_L,
                                                           const ShadowRec* __restrict__ sq,
                                                           const uint32_t* __restrict__ nptr, uint32_t* __restrict__,
                                                           uint32_t* __restrict__, unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
     const uint32_t n = *nptr;
+    if (blockIdx.x * PT_TRACE_BLOCK >= n) return;
     TraceWork wk{0, 0};
-    ShadowSrc src{sq, next, done_L};
+    ShadowSrc src{sq, next, sample_L};
 #if PT_SIMPLE_STEP
     if (blockIdx.x * PT_TRACE_BLOCK < n) trace_pool<true, COUNT, ShadowSrc, false>(n, nullptr, src, s_ref, nullptr, wk);
 #else
@@ -364,35 +404,26 @@ __device__ __forceinline__ void camera_ray(const pt_camera_desc& c, uint32_t key
     d = normalize(dir - off);
 }
 
-// Finished paths store their radiance (per-sample buffer, gathered into the
-// film after the chunk); for each finished path one new camera sample is
-// appended to the next state (consecutive sample ids per block: coherent
-// primary rays).  maxDepth 0 never gets here: the runtime zero-fills.
-__global__ __launch_bounds__(256) void k_finish(RenderParams R, const float4* __restrict__ done_L,
-                                               const uint32_t* __restrict__ done_sid, const uint32_t* __restrict__ nptr,
-                                               uint32_t n_direct, PathSoA next, uint32_t* __restrict__ cnt,
-                                               unsigned long long* __restrict__ next_sample,
-                                               float* __restrict__ sample_L) {
+// One new camera sample per `want` lane: a block-aggregated claim of
+// consecutive sample ids (one returning atomic per block: coherent primary
+// rays), then Camera::GenerateRay for the claimed ids below the chunk's end.
+// Every thread of the block calls it (barriers).
+struct NewSample {
+    bool enq;
+    uint32_t sid, key;
+    f3 o, d;
+};
+__device__ __forceinline__ NewSample claim_camera_sample(const RenderParams& R, bool want,
+                                                         unsigned long long* __restrict__ next_sample) {
     __shared__ uint32_t s_w[5];
     __shared__ unsigned long long s_base;
-    const uint32_t n = nptr ? *nptr : n_direct;
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    const bool want = i < n;
-    if (want && nptr) {
-        const float4 L = done_L[i];
-        float* o = sample_L + 3ull * (uint64_t)done_sid[i];
-        o[0] = L.x;
-        o[1] = L.y;
-        o[2] = L.z;
-    }
-    // one returning atomic per block hands out consecutive sample ids
     const uint64_t m = __ballot(want);
     const uint32_t wave = threadIdx.x >> 6;
     if (__lane_id() == 0) s_w[wave] = (uint32_t)__popcll(m);
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t tot = 0;
-        for (int w = 0; w < 4; w++) {
+        for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
             uint32_t c = s_w[w];
             s_w[w] = tot;
             tot += c;
@@ -401,37 +432,50 @@ __global__ __launch_bounds__(256) void k_finish(RenderParams R, const float4* __
     }
     __syncthreads();
     const unsigned long long g = s_base + s_w[wave] + lanemask_lt_count(m);
-    const bool enq = want && g < R.chunk_total;
-    f3 o = F3(0, 0, 0), d = F3(0, 0, 0);
-    uint32_t key = 0;
-    if (enq) {
+    NewSample ns{want && g < R.chunk_total, (uint32_t)g, 0u, F3(0, 0, 0), F3(0, 0, 0)};
+    if (ns.enq) {
         const uint32_t s_rel = (uint32_t)(g / R.npix_work), pix_i = (uint32_t)(g % R.npix_work);
         uint32_t x, y;
         work_pixel(R, pix_i, x, y);
         const uint32_t s = R.shard_index + (R.s_lo + s_rel) * R.shard_count;
-        key = stream_key(R.seed, y * (uint32_t)R.cam.width + x, s);
-        camera_ray(R.cam, key, x, y, o, d);
+        ns.key = stream_key(R.seed, y * (uint32_t)R.cam.width + x, s);
+        camera_ray(R.cam, ns.key, x, y, ns.o, ns.d);
     }
+    return ns;
+}
+__device__ __forceinline__ void store_camera_path(PathSoA& next, uint32_t at, const NewSample& ns) {
+    next.o[at] = make_float4(ns.o.x, ns.o.y, ns.o.z, __uint_as_float(ns.key));
+    // depth 1 (first loop test passed), spec = true
+    next.d[at] = make_float4(ns.d.x, ns.d.y, ns.d.z, __uint_as_float(1u | PF_SPEC));
+    next.beta[at] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);  // attenuation, prevPDF = 1
+    next.L[at] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(5u));  // camera used dims 0..4
+    next.sid[at] = ns.sid;
+}
+
+// Initial fill of a chunk's wavefront: one camera sample per entry.  Later
+// refills happen in k_shade, where paths finish.  maxDepth 0 never gets here:
+// the runtime zero-fills.
+__global__ __launch_bounds__(256) void k_fill(RenderParams R, uint32_t n, PathSoA next, uint32_t* __restrict__ cnt,
+                                             unsigned long long* __restrict__ next_sample) {
+    if (blockIdx.x * 256 >= n) return;
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const NewSample ns = claim_camera_sample(R, i < n, next_sample);
     const int qoff[1] = {Q_NEXT};
-    const bool pred[1] = {enq};
+    const bool pred[1] = {ns.enq};
     uint32_t at[1];
     block_append<1, 256>(cnt, qoff, pred, at);
-    if (enq) {
-        next.o[at[0]] = make_float4(o.x, o.y, o.z, __uint_as_float(key));
-        // depth 1 (first loop test passed), spec = true
-        next.d[at[0]] = make_float4(d.x, d.y, d.z, __uint_as_float(1u | PF_SPEC));
-        next.beta[at[0]] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);  // attenuation, prevPDF = 1
-        next.L[at[0]] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(5u));  // camera used dims 0..4
-        next.sid[at[0]] = (uint32_t)g;
-    }
+    if (ns.enq) store_camera_path(next, at[0], ns);
 }
 
 // ------------------------------------------------------------------ shading
 template <int INTEGRATOR>
-__global__ __launch_bounds__(256) void k_shade(RenderParams R, PathSoA cur, uint32_t n,
+__global__ __launch_bounds__(256) void k_shade(RenderParams R, PathSoA cur, const uint32_t* __restrict__ nptr,
                                               const float4* __restrict__ hit, PathSoA next,
-                                              float4* __restrict__ done_L, uint32_t* __restrict__ done_sid,
+                                              float* __restrict__ sample_L,
+                                              unsigned long long* __restrict__ next_sample,
                                               ShadowRec* __restrict__ sq, uint32_t* __restrict__ cnt) {
+    const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
+    if (blockIdx.x * 256 >= n) return;  // block-uniform: the grid covers the capacity
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     bool cont = false, done = false, shadow = false;
     ShadowRec srec;
@@ -439,9 +483,10 @@ __global__ __launch_bounds__(256) void k_shade(RenderParams R, PathSoA cur, uint
     float prev = 0;
     uint32_t key = 0, dim = 0, flags = 0, sid = 0;
     if (i < n) {
-        const float4 o4 = cur.o[i], d4 = cur.d[i], b4 = cur.beta[i], L4 = cur.L[i];
+        const uint32_t e = path_slot(i, front, cur.cap);
+        const float4 o4 = cur.o[e], d4 = cur.d[e], b4 = cur.beta[e], L4 = cur.L[e];
         const float4 h = hit[i];
-        sid = cur.sid[i];
+        sid = cur.sid[e];
         ro = xyz(o4);
         rd = xyz(d4);
         att = xyz(b4);
@@ -607,24 +652,31 @@ __global__ __launch_bounds__(256) void k_shade(RenderParams R, PathSoA cur, uint
         }
         flags = depth | (rr << PF_RR_SHIFT) | (spec ? PF_SPEC : 0u);
     }
-    const int qoff[3] = {Q_NEXT, Q_DONE, Q_SHADOW};
-    const bool pred[3] = {cont, done, shadow};
+    // a finished path stores its sample's radiance (the pending NEE ray, if
+    // any, adds to it later) and its entry takes the next camera sample
+    if (done) {
+        float* o = sample_L + 3ull * sid;
+        o[0] = out.x;
+        o[1] = out.y;
+        o[2] = out.z;
+    }
+    const NewSample ns = claim_camera_sample(R, done, next_sample);
+    const int qoff[3] = {Q_NEXT, Q_SHADOW, Q_NEW};
+    const bool pred[3] = {cont, shadow, ns.enq};
     uint32_t at[3];
     block_append<3, 256>(cnt, qoff, pred, at);
-    const uint32_t a = at[0], b = at[1], c = at[2];
+    const uint32_t a = cont ? at[0] : next.cap - 1u - at[2], c = at[1];
     if (cont) {
         next.o[a] = make_float4(ro.x, ro.y, ro.z, __uint_as_float(key));
         next.d[a] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(flags));
         next.beta[a] = make_float4(att.x, att.y, att.z, prev);
         next.L[a] = make_float4(out.x, out.y, out.z, __uint_as_float(dim));
         next.sid[a] = sid;
-    }
-    if (done) {
-        done_L[b] = make_float4(out.x, out.y, out.z, 0.0f);
-        done_sid[b] = sid;
+    } else if (ns.enq) {
+        store_camera_path(next, a, ns);
     }
     if (shadow) {
-        srec.d.w = __uint_as_float(cont ? a : (SHADOW_DONE_BIT | b));
+        srec.d.w = __uint_as_float(cont ? a : (SHADOW_DONE_BIT | sid));
         sq[c] = srec;
     }
 }
@@ -702,16 +754,17 @@ __global__ __launch_bounds__(256) void k_gather(RenderParams R, const float* __r
 
 // explicit instantiations used by the runtime
 #define PT_INST_TRACE(B)                                                                                            \
-    template __global__ void k_closest<B>(PathSoA, uint32_t, float4*, uint32_t*, uint32_t*, unsigned long long*);    \
-    template __global__ void k_closest_pool<B>(PathSoA, uint32_t, float4*, uint32_t*, uint32_t*,                     \
-                                               unsigned long long*);                                                 \
-    template __global__ void k_shadow<B>(PathSoA, float4*, const ShadowRec*, const uint32_t*, uint32_t*, uint32_t*,  \
+    template __global__ void k_closest<B>(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*, uint32_t*,        \
+                                          uint32_t*, unsigned long long*);                                           \
+    template __global__ void k_closest_pool<B>(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*, uint32_t*,   \
+                                               uint32_t*, unsigned long long*);                                      \
+    template __global__ void k_shadow<B>(PathSoA, float*, const ShadowRec*, const uint32_t*, uint32_t*, uint32_t*,   \
                                          unsigned long long*);                                                       \
-    template __global__ void k_shadow_pool<B>(PathSoA, float4*, const ShadowRec*, const uint32_t*, uint32_t*,        \
+    template __global__ void k_shadow_pool<B>(PathSoA, float*, const ShadowRec*, const uint32_t*, uint32_t*,         \
                                               uint32_t*, unsigned long long*);
 PT_INST_TRACE(false)
 PT_INST_TRACE(true)
-template __global__ void k_shade<PT_INTEGRATOR_PATH>(RenderParams, PathSoA, uint32_t, const float4*, PathSoA,
-                                                     float4*, uint32_t*, ShadowRec*, uint32_t*);
-template __global__ void k_shade<PT_INTEGRATOR_SIMPLE>(RenderParams, PathSoA, uint32_t, const float4*,
-                                                       PathSoA, float4*, uint32_t*, ShadowRec*, uint32_t*);
+template __global__ void k_shade<PT_INTEGRATOR_PATH>(RenderParams, PathSoA, const uint32_t*, const float4*, PathSoA,
+                                                     float*, unsigned long long*, ShadowRec*, uint32_t*);
+template __global__ void k_shade<PT_INTEGRATOR_SIMPLE>(RenderParams, PathSoA, const uint32_t*, const float4*,
+                                                       PathSoA, float*, unsigned long long*, ShadowRec*, uint32_t*);

@@ -17,6 +17,12 @@
 
 #include "pt_kernels.hip"
 
+// The host keeps up to PT_LAG wavefront iterations queued ahead of the one
+// whose counts it reads (no per-bounce round trip; iterations past the end of
+// a chunk find zero paths and return at once)
+#define PT_LAG 4
+#define PT_RING (PT_LAG + 1)
+
 struct pt_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
@@ -35,17 +41,18 @@ struct pt_ctx {
     uint32_t cap = 0;
     PathSoA PA{}, PB{};
     float4* hit = nullptr;
-    float4* done_L = nullptr;
-    uint32_t *done_sid = nullptr, *qcnt = nullptr;
+    uint32_t* qcnt = nullptr;
     uint32_t* ovf = nullptr;  // pool traversal stack entries beyond PT_POOL_LDS
     ShadowRec* sq = nullptr;
     unsigned long long* counters = nullptr;
-    uint32_t* host_cnt = nullptr;  // pinned
+    uint32_t* host_cnt = nullptr;  // pinned, PT_RING counter snapshots (SNAP_WORDS each)
+    uint32_t* host_cnt_dev = nullptr;  // the same memory as the kernels address it
     float* sample_L = nullptr;
     uint64_t sample_cap = 0;  // floats
     double* film = nullptr;
     uint64_t film_cap = 0;  // doubles
     hipEvent_t ev[8] = {};
+    hipEvent_t rev[PT_RING][5] = {};  // per in-flight iteration: kernel boundaries [0..2], end [4] ([3] unused)
 };
 
 static pt_status fail(pt_ctx* c, pt_status code, const char* fmt, ...) {
@@ -90,7 +97,14 @@ extern "C" pt_status pt_create(pt_ctx** out, int device) {
         return PT_ERR_HIP;
     }
     c->stream = c->own_stream;
-    for (auto& e : c->ev) {
+    for (hipEvent_t* e = &c->ev[0]; e != &c->ev[0] + 8; ++e)
+        if (hipEventCreate(e) != hipSuccess) {
+            g_err = "event create failed";
+            delete c;
+            return PT_ERR_HIP;
+        }
+    for (auto& r : c->rev)
+        for (auto& e : r) {
         if (hipEventCreate(&e) != hipSuccess) {
             g_err = "event create failed";
             delete c;
@@ -112,7 +126,9 @@ extern "C" pt_status pt_create(pt_ctx** out, int device) {
         }
         c->trace_blocks = (uint32_t)std::max(1, cus * std::max(1, std::min(per_cu, per_cu_any)));
     }
-    if (hipHostMalloc((void**)&c->host_cnt, Q_WORDS * 4) != hipSuccess) {
+    if (hipHostMalloc((void**)&c->host_cnt, PT_RING * SNAP_WORDS * 4, hipHostMallocCoherent | hipHostMallocMapped) !=
+            hipSuccess ||
+        hipHostGetDevicePointer((void**)&c->host_cnt_dev, c->host_cnt, 0) != hipSuccess) {
         g_err = "pinned alloc failed";
         delete c;
         return PT_ERR_HIP;
@@ -129,13 +145,13 @@ static void free_scene(pt_ctx* c) {
 }
 static void free_work(pt_ctx* c) {
     void* bufs[] = {c->PA.o, c->PA.d, c->PA.beta, c->PA.L, c->PA.sid, c->PB.o, c->PB.d, c->PB.beta, c->PB.L,
-                    c->PB.sid, c->hit, c->done_L, c->done_sid, c->qcnt, c->sq, c->counters, c->ovf};
+                    c->PB.sid, c->hit, c->qcnt, c->sq, c->counters, c->ovf};
     for (void* p : bufs)
         if (p) hipFree(p);
     c->PA = PathSoA{};
     c->PB = PathSoA{};
-    c->hit = c->done_L = nullptr;
-    c->done_sid = c->qcnt = nullptr;
+    c->hit = nullptr;
+    c->qcnt = nullptr;
     c->sq = nullptr;
     c->counters = nullptr;
     c->ovf = nullptr;
@@ -153,6 +169,9 @@ extern "C" void pt_destroy(pt_ctx* c) {
     if (c->host_cnt) hipHostFree(c->host_cnt);
     for (auto& e : c->ev)
         if (e) hipEventDestroy(e);
+    for (auto& r : c->rev)
+        for (auto& e : r)
+            if (e) hipEventDestroy(e);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -458,6 +477,7 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
         return fail(c, PT_ERR_OOM, "wavefront allocation of %zu paths failed", (size_t)n); \
     }
     for (PathSoA* P : {&c->PA, &c->PB}) {
+        P->cap = (uint32_t)n;
         AL(P->o, n * 16);
         AL(P->d, n * 16);
         AL(P->beta, n * 16);
@@ -465,14 +485,12 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
         AL(P->sid, n * 4);
     }
     AL(c->hit, n * 16);
-    AL(c->done_L, n * 16);
-    AL(c->done_sid, n * 4);
-    AL(c->qcnt, (Q_WORDS + 3 * PT_POOL_WORDS) * 4);  // queue counters, then the traversal pools
+    AL(c->qcnt, (3 * SET_WORDS + PT_POOL_WORDS) * 4);  // three counter sets, then pt_trace's pool
     AL(c->sq, n * sizeof(ShadowRec));
     AL(c->counters, (CNT_SHARDS + 1) * CNT_COUNT * 8);
     if (PT_STACK > PT_POOL_LDS) AL(c->ovf, (size_t)c->trace_blocks * PT_TRACE_BLOCK * (PT_STACK - PT_POOL_LDS) * 4);
 #undef AL
-    if (hipMemset(c->qcnt, 0, (Q_WORDS + 3 * PT_POOL_WORDS) * 4) != hipSuccess) {
+    if (hipMemset(c->qcnt, 0, (3 * SET_WORDS + PT_POOL_WORDS) * 4) != hipSuccess) {
         free_work(c);
         return fail(c, PT_ERR_HIP, "hipMemset of the queue counters failed");
     }
@@ -587,88 +605,106 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             continue;
         }
         HIPCHK(c, hipMemsetAsync(next_sample, 0, 8, sm));
-        // the fill appends to Q_NEXT: start the queue counters from zero (a
-        // fresh allocation holds whatever the memory held before)
-        HIPCHK(c, hipMemsetAsync(c->qcnt, 0, (Q_WORDS + 2 * PT_POOL_WORDS) * 4, sm));
+        // Counter sets rotate (pt_kernels.h SET_WORDS): iteration i reads its
+        // path count from set[i % 3] (written by iteration i - 1, or the
+        // initial fill), appends into set[(i + 1) % 3] and zeroes
+        // set[(i + 2) % 3].  Every kernel reads its count from device memory,
+        // so the host never waits for a bounce: it keeps PT_LAG iterations
+        // queued ahead of the one whose counts it reads (the pinned snapshot
+        // the iteration's first kernel writes, behind an event).
+        uint32_t* set[3] = {c->qcnt, c->qcnt + SET_WORDS, c->qcnt + 2 * SET_WORDS};
+        HIPCHK(c, hipMemsetAsync(c->qcnt, 0, 3 * SET_WORDS * 4, sm));
         // initial fill: one camera sample per wavefront entry
         PathSoA cur = c->PA, nxt = c->PB;
-        hipLaunchKernelGGL(k_finish, dim3((paths + 255) / 256), dim3(256), 0, sm, R, (const float4*)nullptr,
-                           (const uint32_t*)nullptr, (const uint32_t*)nullptr, paths, cur, c->qcnt, next_sample,
-                           c->sample_L);
+        hipLaunchKernelGGL(k_fill, dim3((paths + 255) / 256), dim3(256), 0, sm, R, paths, cur, set[0], next_sample);
         HIPCHK(c, hipGetLastError());
-        HIPCHK(c, hipMemcpyAsync(c->host_cnt, c->qcnt, Q_WORDS * 4, hipMemcpyDeviceToHost, sm));
-        HIPCHK(c, hipStreamSynchronize(sm));
-        uint32_t n_active = c->host_cnt[Q_NEXT];
-        while (n_active > 0) {
-            HIPCHK(c, hipMemsetAsync(c->qcnt, 0, (Q_WORDS + 2 * PT_POOL_WORDS) * 4, sm));
-            // pool traversal: at most the resident blocks, rays claimed from the
-            // pools; simple traversal: one ray per lane
-            const uint32_t nb = (n_active + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK;
-            const dim3 gt(use_pool ? std::max(1u, std::min(nb, c->trace_blocks)) : nb), gs((n_active + 255) / 256);
-            uint32_t* pool_closest = c->qcnt + Q_WORDS;
-            uint32_t* pool_shadow = c->qcnt + Q_WORDS + PT_POOL_WORDS;
-#if PT_POOL_CHECK
-            HIPCHK(c, hipMemsetAsync(c->hit, 0xFF, (size_t)n_active * sizeof(float4), sm));
-#endif
-            if (timing) HIPCHK(c, hipEventRecord(c->ev[0], sm));
-            {
-                auto kc = use_pool ? (count ? k_closest_pool<true> : k_closest_pool<false>)
-                                   : (count ? k_closest<true> : k_closest<false>);
-                hipLaunchKernelGGL(kc, gt, dim3(PT_TRACE_BLOCK), 0, sm, cur, n_active, c->hit, pool_closest, c->ovf,
-                                   c->counters);
-            }
-            if (timing) HIPCHK(c, hipEventRecord(c->ev[1], sm));
-            if (rd->integrator == PT_INTEGRATOR_SIMPLE)
-                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_SIMPLE>, gs, dim3(256), 0, sm, R, cur, n_active,
-                                   (const float4*)c->hit, nxt, c->done_L, c->done_sid, c->sq, c->qcnt);
-            else
-                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_PATH>, gs, dim3(256), 0, sm, R, cur, n_active,
-                                   (const float4*)c->hit, nxt, c->done_L, c->done_sid, c->sq, c->qcnt);
-            if (timing) HIPCHK(c, hipEventRecord(c->ev[2], sm));
-            if (rd->integrator != PT_INTEGRATOR_SIMPLE) {
-                auto ks = use_pool ? (count ? k_shadow_pool<true> : k_shadow_pool<false>)
-                                   : (count ? k_shadow<true> : k_shadow<false>);
-                hipLaunchKernelGGL(ks, gt, dim3(PT_TRACE_BLOCK), 0, sm, nxt, c->done_L, (const ShadowRec*)c->sq,
-                                   (const uint32_t*)(c->qcnt + Q_SHADOW), pool_shadow, c->ovf, c->counters);
-            }
-            if (timing) HIPCHK(c, hipEventRecord(c->ev[3], sm));
-            hipLaunchKernelGGL(k_finish, gs, dim3(256), 0, sm, R, (const float4*)c->done_L,
-                               (const uint32_t*)c->done_sid, (const uint32_t*)(c->qcnt + Q_DONE), 0u, nxt, c->qcnt,
-                               next_sample, c->sample_L);
-            HIPCHK(c, hipGetLastError());
-            HIPCHK(c, hipMemcpyAsync(c->host_cnt, c->qcnt, Q_WORDS * 4, hipMemcpyDeviceToHost, sm));
-            HIPCHK(c, hipStreamSynchronize(sm));
+        const dim3 gt(use_pool ? c->trace_blocks : (paths + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK);
+        const dim3 gs((paths + 255) / 256);
+        uint32_t issued = 0, read = 0;
+        bool drained = false;
+        // reads iteration `read`'s snapshot (after its event): stats, timing, end test
+        auto consume = [&]() -> pt_status {
+            const uint32_t slot = read % PT_RING;
+            HIPCHK(c, hipEventSynchronize(c->rev[slot][4]));
+            const volatile uint32_t* hc = c->host_cnt + slot * SNAP_WORDS;
+            const uint32_t n_in = hc[SNAP_PATHS];
             if (stats) {
-                stats->rays_closest += n_active;
-                stats->rays_any += c->host_cnt[Q_SHADOW];
-                stats->shade_hits += n_active;
-                stats->launches_closest++;
-                if (rd->integrator != PT_INTEGRATOR_SIMPLE) stats->launches_any++;
+                stats->rays_any += hc[SNAP_SHADOW_PREV];
+                if (n_in) {
+                    stats->rays_closest += n_in;
+                    stats->shade_hits += n_in;
+                    stats->launches_closest++;
+                    if (rd->integrator != PT_INTEGRATOR_SIMPLE) stats->launches_any++;
+                }
             }
-            if (timing) {
+            if (timing && n_in) {
                 float a, b, d;
-                HIPCHK(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
-                HIPCHK(c, hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
-                HIPCHK(c, hipEventElapsedTime(&d, c->ev[2], c->ev[3]));
+                HIPCHK(c, hipEventElapsedTime(&a, c->rev[slot][0], c->rev[slot][1]));
+                HIPCHK(c, hipEventElapsedTime(&b, c->rev[slot][1], c->rev[slot][2]));
+                HIPCHK(c, hipEventElapsedTime(&d, c->rev[slot][2], c->rev[slot][4]));
                 t_cl += a;
                 t_sh += b;
                 t_an += d;
             }
-#if PT_POOL_CHECK
-            {
-                unsigned int dg[4];
-                HIPCHK(c, hipMemcpyFromSymbol(dg, HIP_SYMBOL(pt_diag), sizeof(dg)));
-                if (dg[0] | dg[1] | dg[2] | dg[3]) {
-                    fprintf(stderr, "pt_diag: n_active %u use_pool %d bad_ref %u bad_prim %u unwritten_hit %u dropped_push %u\n",
-                            n_active, (int)use_pool, dg[0], dg[1], dg[2], dg[3]);
-                    const unsigned int z[4] = {0, 0, 0, 0};
-                    HIPCHK(c, hipMemcpyToSymbol(HIP_SYMBOL(pt_diag), z, sizeof(z)));
-                }
+            if (n_in == 0) drained = true;  // and every later iteration finds none
+            ++read;
+            return PT_OK;
+        };
+        while (!drained) {
+            if (issued - read >= PT_LAG) {
+                if ((st = consume()) != PT_OK) return st;
+                continue;
             }
-#endif
-            n_active = c->host_cnt[Q_NEXT];
+            const uint32_t i = issued;
+            uint32_t* in = set[i % 3];
+            uint32_t* out = set[(i + 1) % 3];
+            uint32_t* spare = set[(i + 2) % 3];
+            hipEvent_t* ev = c->rev[i % PT_RING];
+            if (timing) HIPCHK(c, hipEventRecord(ev[0], sm));
+            {
+                auto kc = use_pool ? (count ? k_closest_pool<true> : k_closest_pool<false>)
+                                   : (count ? k_closest<true> : k_closest<false>);
+                hipLaunchKernelGGL(kc, gt, dim3(PT_TRACE_BLOCK), 0, sm, cur, (const uint32_t*)in, c->hit,
+                                   out + Q_WORDS, c->ovf, spare, c->host_cnt_dev + (i % PT_RING) * SNAP_WORDS,
+                                   c->counters);
+            }
+            if (timing) HIPCHK(c, hipEventRecord(ev[1], sm));
+            if (rd->integrator == PT_INTEGRATOR_SIMPLE)
+                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_SIMPLE>, gs, dim3(256), 0, sm, R, cur,
+                                   (const uint32_t*)(in + Q_NEXT), (const float4*)c->hit, nxt, c->sample_L,
+                                   next_sample, c->sq, out);
+            else
+                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_PATH>, gs, dim3(256), 0, sm, R, cur,
+                                   (const uint32_t*)(in + Q_NEXT), (const float4*)c->hit, nxt, c->sample_L,
+                                   next_sample, c->sq, out);
+            if (timing) HIPCHK(c, hipEventRecord(ev[2], sm));
+            if (rd->integrator != PT_INTEGRATOR_SIMPLE) {
+                auto ks = use_pool ? (count ? k_shadow_pool<true> : k_shadow_pool<false>)
+                                   : (count ? k_shadow<true> : k_shadow<false>);
+                hipLaunchKernelGGL(ks, gt, dim3(PT_TRACE_BLOCK), 0, sm, nxt, c->sample_L, (const ShadowRec*)c->sq,
+                                   (const uint32_t*)(out + Q_SHADOW), out + Q_WORDS + PT_POOL_WORDS, c->ovf,
+                                   c->counters);
+            }
+            HIPCHK(c, hipGetLastError());
+            HIPCHK(c, hipEventRecord(ev[4], sm));
             std::swap(cur, nxt);
+            ++issued;
         }
+        // iterations queued past the end find zero paths; let them drain
+        while (read < issued)
+            if ((st = consume()) != PT_OK) return st;
+#if PT_POOL_CHECK
+        {
+            unsigned int dg[4];
+            HIPCHK(c, hipMemcpyFromSymbol(dg, HIP_SYMBOL(pt_diag), sizeof(dg)));
+            if (dg[0] | dg[1] | dg[2] | dg[3]) {
+                fprintf(stderr, "pt_diag: use_pool %d bad_ref %u bad_prim %u unwritten_hit %u dropped_push %u\n",
+                        (int)use_pool, dg[0], dg[1], dg[2], dg[3]);
+                const unsigned int z[4] = {0, 0, 0, 0};
+                HIPCHK(c, hipMemcpyToSymbol(HIP_SYMBOL(pt_diag), z, sizeof(z)));
+            }
+        }
+#endif
         if (stats) stats->paths += R.chunk_total;
         if ((st = on_chunk(R)) != PT_OK) return st;
     }
@@ -799,7 +835,7 @@ extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any
     HIPCHK(c, hipMemsetAsync(c->counters, 0, CNT_SHARDS * CNT_COUNT * 8, c->stream));
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
-    uint32_t* pool = c->qcnt + Q_WORDS + 2 * PT_POOL_WORDS;
+    uint32_t* pool = c->qcnt + 3 * SET_WORDS;
     HIPCHK(c, hipMemsetAsync(pool, 0, PT_POOL_WORDS * 4, c->stream));
     hipLaunchKernelGGL(k_trace_rays,
                        dim3(std::max(1u, std::min((n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK, c->trace_blocks))),
