@@ -188,19 +188,24 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_shadow_pool(Pa
 #ifndef PT_SIMPLE_STEP
 #define PT_SIMPLE_STEP 0
 #endif
+#if PT_SIMPLE_STEP
+#define PT_SIMPLE_LDS PT_POOL_LDS  // split stack, as the pool kernels
+#else
+#define PT_SIMPLE_LDS PT_STACK
+#endif
 template <bool COUNT>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(PathSoA P, const uint32_t* __restrict__ nptr,
                                                            float4* __restrict__ hit, uint32_t* __restrict__,
-                                                           uint32_t* __restrict__, uint32_t* __restrict__ spare,
+                                                           uint32_t* __restrict__ ovf, uint32_t* __restrict__ spare,
                                                            uint32_t* __restrict__ snap, unsigned long long* counters) {
-    __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+    __shared__ uint32_t s_ref[PT_SIMPLE_LDS * PT_TRACE_BLOCK];
     iteration_prologue(nptr, spare, snap);
     const uint32_t n = path_count(nptr);  // the grid covers the wavefront's capacity
     if (blockIdx.x * PT_TRACE_BLOCK >= n) return;
     TraceWork wk{0, 0};
 #if PT_SIMPLE_STEP
     ClosestSrc src{P, hit, nptr[Q_NEXT]};
-    trace_pool<false, COUNT, ClosestSrc, false>(n, nullptr, src, s_ref, nullptr, wk);
+    trace_pool<false, COUNT, ClosestSrc, false>(n, nullptr, src, s_ref, ovf, wk);
 #else
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     if (i < n) {
@@ -221,14 +226,14 @@ template <bool COUNT>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(PathSoA next, float* __restrict__ sample_L,
                                                           const ShadowRec* __restrict__ sq,
                                                           const uint32_t* __restrict__ nptr, uint32_t* __restrict__,
-                                                          uint32_t* __restrict__, unsigned long long* counters) {
-    __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+                                                          uint32_t* __restrict__ ovf, unsigned long long* counters) {
+    __shared__ uint32_t s_ref[PT_SIMPLE_LDS * PT_TRACE_BLOCK];
     const uint32_t n = *nptr;
     if (blockIdx.x * PT_TRACE_BLOCK >= n) return;
     TraceWork wk{0, 0};
     ShadowSrc src{sq, next, sample_L};
 #if PT_SIMPLE_STEP
-    if (blockIdx.x * PT_TRACE_BLOCK < n) trace_pool<true, COUNT, ShadowSrc, false>(n, nullptr, src, s_ref, nullptr, wk);
+    if (blockIdx.x * PT_TRACE_BLOCK < n) trace_pool<true, COUNT, ShadowSrc, false>(n, nullptr, src, s_ref, ovf, wk);
 #else
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     if (i < n) {

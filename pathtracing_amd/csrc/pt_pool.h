@@ -41,39 +41,6 @@ __device__ unsigned int pt_diag[4];
 #define PT_REFILL 8
 #endif
 
-// 4-wide slab test (BVH.hpp:1049-1092 / 1140-1183), children in pairs on the
-// packed-FP32 ALU (v_pk_add_f32 / v_pk_mul_f32: two lanes per instruction,
-// each lane the same rounded (bound - o) * inv as the scalar form)
-typedef float v2f __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void slab4p(float4 xmn, float4 xmx, float4 ymn, float4 ymx, float4 zmn, float4 zmx, f3 o,
-                                       f3 inv, float tmax, uint32_t& mask) {
-    const v2f ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
-    const v2f ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
-    v2f t[2][6];
-    t[0][0] = (v2f{xmn.x, xmn.y} - ox) * ix;
-    t[1][0] = (v2f{xmn.z, xmn.w} - ox) * ix;
-    t[0][1] = (v2f{xmx.x, xmx.y} - ox) * ix;
-    t[1][1] = (v2f{xmx.z, xmx.w} - ox) * ix;
-    t[0][2] = (v2f{ymn.x, ymn.y} - oy) * iy;
-    t[1][2] = (v2f{ymn.z, ymn.w} - oy) * iy;
-    t[0][3] = (v2f{ymx.x, ymx.y} - oy) * iy;
-    t[1][3] = (v2f{ymx.z, ymx.w} - oy) * iy;
-    t[0][4] = (v2f{zmn.x, zmn.y} - oz) * iz;
-    t[1][4] = (v2f{zmn.z, zmn.w} - oz) * iz;
-    t[0][5] = (v2f{zmx.x, zmx.y} - oz) * iz;
-    t[1][5] = (v2f{zmx.z, zmx.w} - oz) * iz;
-    mask = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int h = i >> 1, l = i & 1;
-        const float tx1 = t[h][0][l], tx2 = t[h][1][l], ty1 = t[h][2][l], ty2 = t[h][3][l];
-        const float tz1 = t[h][4][l], tz2 = t[h][5][l];
-        const float tEntry = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
-        const float tExit = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
-        if (tExit >= PT_EPS && tEntry < tmax && tEntry <= tExit) mask |= 1u << i;
-    }
-}
-
 // Src interface:
 //   bool load(uint32_t ri, f3& o, f3& d, float& tmax)   (false: skip this ray)
 //   void closest(uint32_t ri, float t, float b1, float b2, int prim)
@@ -84,9 +51,9 @@ template <bool ANY, bool COUNT, class Src, bool POOL = true>
 __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, uint32_t* s_ref,
                            uint32_t* __restrict__ ovf, TraceWork& wk) {
     const uint32_t lane = threadIdx.x;
-    // LDS part of the stack; the rest in ovf (pool kernels only: their grid is
-    // bounded by the resident blocks, which sizes ovf)
-    constexpr int LN = POOL ? PT_POOL_LDS : PT_STACK;
+    // LDS part of the stack; the rest in ovf ([entry][grid lane]; the runtime
+    // sizes it for the larger of the pool grid and the one-ray-per-lane grid)
+    constexpr int LN = PT_POOL_LDS;
     const uint32_t gl = blockIdx.x * PT_TRACE_BLOCK + lane, G = gridDim.x * PT_TRACE_BLOCK;
     const uint32_t wl = __lane_id();
     const uint32_t cs = (n + PT_POOL_CHUNKS - 1) / PT_POOL_CHUNKS;
@@ -209,31 +176,17 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         {
             uint32_t mask;
             slab4p(q0, q1, q2, q3, q4, q5, o, inv, tmax, mask);
-            const uint32_t c0 = __float_as_uint(q6.x), c1 = __float_as_uint(q6.y), c2 = __float_as_uint(q6.z),
-                           c3 = __float_as_uint(q6.w);
-            // children that pass the slab test and exist; none on primitive lanes
-            const uint32_t vm = node_step ? mask & ((uint32_t)(c0 != REF_EMPTY) | (uint32_t)(c1 != REF_EMPTY) << 1 |
-                                                    (uint32_t)(c2 != REF_EMPTY) << 2 | (uint32_t)(c3 != REF_EMPTY) << 3)
-                                          : 0u;
+            if (!node_step) mask = 0;  // no children on primitive lanes
             // visit order: slot order for any hit (BVH.hpp:1099-1102), octant
-            // order far -> near for closest hit (BVH4::LUT, BVH.hpp:1195-1204);
-            // every valid child but the last is pushed, the last is visited next.
-            // Selects only: the one conditional is the stack store itself.
-            uint32_t perm = 0xE4u;  // identity 0,1,2,3
+            // order far -> near for closest hit (BVH4::LUT, BVH.hpp:1195-1204)
+            uint32_t perm = 0xE4u;
             if (!ANY) {
                 const uint32_t ow = __float_as_uint((oct >> 2) ? q7.y : q7.x);
                 perm = (ow >> (8 * (oct & 3))) & 0xFFu;
             }
-            uint32_t cand = REF_EMPTY;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t ci = (perm >> (2 * k)) & 3u;
-                const uint32_t lo = (ci & 1u) ? c1 : c0, hi = (ci & 1u) ? c3 : c2;
-                const uint32_t c = (ci & 2u) ? hi : lo;
-                const bool v = (vm >> ci) & 1u;
-                if (v && cand != REF_EMPTY) push(cand);
-                cand = v ? c : cand;
-            }
+            const uint32_t cand = order_children(mask, make_uint4(__float_as_uint(q6.x), __float_as_uint(q6.y),
+                                                                  __float_as_uint(q6.z), __float_as_uint(q6.w)),
+                                                 perm, push);
             if (node_step) {
                 if (COUNT) wk.nodes++;
                 ref = cand;

@@ -158,38 +158,59 @@ __device__ __noinline__ bool other_pred(uint32_t slot, uint32_t w0, f3 o, f3 d, 
     return true;
 }
 
-__device__ __forceinline__ uint32_t sel4u(uint32_t i, uint4 v) {
-    return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
-}
-__device__ __forceinline__ float sel4f(uint32_t i, float a, float b, float c, float d) {
-    return i == 0 ? a : (i == 1 ? b : (i == 2 ? c : d));
-}
-
-// 4-wide slab test (BVH.hpp:1049-1092 / 1140-1183) on a cluster's boxes
-// xmin..zmax (one float4 per component, the 4 children in its lanes)
-__device__ __forceinline__ void slab4q(float4 xmn, float4 xmx, float4 ymn, float4 ymx, float4 zmn, float4 zmx, f3 o,
-                                       f3 inv, float tmax, uint32_t& mask, float te[4]) {
-    float xa[4] = {xmn.x, xmn.y, xmn.z, xmn.w}, xb[4] = {xmx.x, xmx.y, xmx.z, xmx.w};
-    float ya[4] = {ymn.x, ymn.y, ymn.z, ymn.w}, yb[4] = {ymx.x, ymx.y, ymx.z, ymx.w};
-    float za[4] = {zmn.x, zmn.y, zmn.z, zmn.w}, zb[4] = {zmx.x, zmx.y, zmx.z, zmx.w};
+// 4-wide slab test (BVH.hpp:1049-1092 / 1140-1183), children in pairs on the
+// packed-FP32 ALU (v_pk_add_f32 / v_pk_mul_f32: two lanes per instruction,
+// each lane the same rounded (bound - o) * inv as the scalar form)
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void slab4p(float4 xmn, float4 xmx, float4 ymn, float4 ymx, float4 zmn, float4 zmx, f3 o,
+                                       f3 inv, float tmax, uint32_t& mask) {
+    const v2f ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+    const v2f ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
+    v2f t[2][6];
+    t[0][0] = (v2f{xmn.x, xmn.y} - ox) * ix;
+    t[1][0] = (v2f{xmn.z, xmn.w} - ox) * ix;
+    t[0][1] = (v2f{xmx.x, xmx.y} - ox) * ix;
+    t[1][1] = (v2f{xmx.z, xmx.w} - ox) * ix;
+    t[0][2] = (v2f{ymn.x, ymn.y} - oy) * iy;
+    t[1][2] = (v2f{ymn.z, ymn.w} - oy) * iy;
+    t[0][3] = (v2f{ymx.x, ymx.y} - oy) * iy;
+    t[1][3] = (v2f{ymx.z, ymx.w} - oy) * iy;
+    t[0][4] = (v2f{zmn.x, zmn.y} - oz) * iz;
+    t[1][4] = (v2f{zmn.z, zmn.w} - oz) * iz;
+    t[0][5] = (v2f{zmx.x, zmx.y} - oz) * iz;
+    t[1][5] = (v2f{zmx.z, zmx.w} - oz) * iz;
     mask = 0;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        float tx1 = (xa[i] - o.x) * inv.x, tx2 = (xb[i] - o.x) * inv.x;
-        float ty1 = (ya[i] - o.y) * inv.y, ty2 = (yb[i] - o.y) * inv.y;
-        float tz1 = (za[i] - o.z) * inv.z, tz2 = (zb[i] - o.z) * inv.z;
-        float tEntry = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
-        float tExit = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
-        te[i] = tEntry;
+        const int h = i >> 1, l = i & 1;
+        const float tx1 = t[h][0][l], tx2 = t[h][1][l], ty1 = t[h][2][l], ty2 = t[h][3][l];
+        const float tz1 = t[h][4][l], tz2 = t[h][5][l];
+        const float tEntry = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+        const float tExit = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
         if (tExit >= PT_EPS && tEntry < tmax && tEntry <= tExit) mask |= 1u << i;
     }
 }
 
-template <bool COUNT>
-__device__ __forceinline__ void slab4(const DevCluster* __restrict__ node, f3 o, f3 inv, float tmax, uint32_t& mask,
-                                      float te[4]) {
-    const float4* c4 = reinterpret_cast<const float4*>(node);
-    slab4q(c4[0], c4[1], c4[2], c4[3], c4[4], c4[5], o, inv, tmax, mask, te);
+// Children of a cluster in visit order: every valid child (passes the slab
+// test, exists) but the last is pushed, the last becomes the next ref.  perm
+// holds the visit order as 2-bit slot indices from the low end (0xE4 = slot
+// order, any hit; the octant byte of BVH4::LUT, closest hit).  Selects only:
+// the one conditional is the stack store, done by `push`.
+template <class Push>
+__device__ __forceinline__ uint32_t order_children(uint32_t mask, uint4 ch, uint32_t perm, Push&& push) {
+    const uint32_t vm = mask & ((uint32_t)(ch.x != REF_EMPTY) | (uint32_t)(ch.y != REF_EMPTY) << 1 |
+                                (uint32_t)(ch.z != REF_EMPTY) << 2 | (uint32_t)(ch.w != REF_EMPTY) << 3);
+    uint32_t cand = REF_EMPTY;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t ci = (perm >> (2 * k)) & 3u;
+        const uint32_t lo = (ci & 1u) ? ch.y : ch.x, hi = (ci & 1u) ? ch.w : ch.z;
+        const uint32_t c = (ci & 2u) ? hi : lo;
+        const bool v = (vm >> ci) & 1u;
+        if (v && cand != REF_EMPTY) push(cand);
+        cand = v ? c : cand;
+    }
+    return cand;
 }
 
 // Closest hit.  Returns prim slot or -1; t, b1, b2 of the accepted hit.
@@ -213,30 +234,22 @@ __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out
             ref = s_ref[sp * PT_TRACE_BLOCK + lane];
         }
         if (!(ref & REF_LEAF)) {
-            const DevCluster* node = S.nodes + ref;
+            const float4* __restrict__ q = reinterpret_cast<const float4*>(S.nodes + ref);
             if (COUNT) wk.nodes++;
+            const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4], q5 = q[5], q6 = q[6];
+            const uint2 q7 = *reinterpret_cast<const uint2*>(q + 7);
             uint32_t mask;
-            float te[4];
-            slab4<COUNT>(node, o, inv, tmax, mask, te);
-            const uint4 ch = *reinterpret_cast<const uint4*>(&node->child[0]);
-            const uint32_t ow = node->order[oct >> 2];
-            const uint32_t perm = (ow >> (8 * (oct & 3))) & 0xFFu;
-            uint32_t cand = REF_EMPTY;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {  // far -> near: 2-bit fields from the low end
-                const uint32_t idx = (perm >> (2 * k)) & 3u;
-                if ((mask >> idx) & 1u) {
-                    const uint32_t c = sel4u(idx, ch);
-                    if (c != REF_EMPTY) {
-                        if (cand != REF_EMPTY && sp < PT_STACK) {
-                            s_ref[sp * PT_TRACE_BLOCK + lane] = cand;
-                            ++sp;
-                        }
-                        cand = c;
-                    }
-                }
-            }
-            ref = cand;
+            slab4p(q0, q1, q2, q3, q4, q5, o, inv, tmax, mask);
+            const uint32_t ow = (oct >> 2) ? q7.y : q7.x;
+            const uint32_t perm = (ow >> (8 * (oct & 3))) & 0xFFu;  // far -> near (BVH.hpp:1195-1204)
+            ref = order_children(mask, make_uint4(__float_as_uint(q6.x), __float_as_uint(q6.y),
+                                                  __float_as_uint(q6.z), __float_as_uint(q6.w)),
+                                 perm, [&](uint32_t v) {
+                                     if (sp < PT_STACK) {
+                                         s_ref[sp * PT_TRACE_BLOCK + lane] = v;
+                                         ++sp;
+                                     }
+                                 });
             continue;
         }
         // leaf: primitives from slot until the one flagged LAST
@@ -297,27 +310,20 @@ __device__ bool trace_any(f3 o, f3 d, float tmax, uint32_t* s_ref, TraceWork& wk
             ref = s_ref[sp * PT_TRACE_BLOCK + lane];
         }
         if (!(ref & REF_LEAF)) {
-            const DevCluster* node = S.nodes + ref;
+            const float4* __restrict__ q = reinterpret_cast<const float4*>(S.nodes + ref);
             if (COUNT) wk.nodes++;
+            const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3], q4 = q[4], q5 = q[5], q6 = q[6];
             uint32_t mask;
-            float te[4];
-            slab4<COUNT>(node, o, inv, tmax, mask, te);
-            const uint4 ch = *reinterpret_cast<const uint4*>(&node->child[0]);
-            uint32_t cand = REF_EMPTY;
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                if ((mask >> i) & 1u) {
-                    const uint32_t c = sel4u((uint32_t)i, ch);
-                    if (c != REF_EMPTY) {
-                        if (cand != REF_EMPTY && sp < PT_STACK) {
-                            s_ref[sp * PT_TRACE_BLOCK + lane] = cand;
-                            ++sp;
-                        }
-                        cand = c;
-                    }
-                }
-            }
-            ref = cand;
+            slab4p(q0, q1, q2, q3, q4, q5, o, inv, tmax, mask);
+            // slot order, the last visited next (BVH.hpp:1099-1102)
+            ref = order_children(mask, make_uint4(__float_as_uint(q6.x), __float_as_uint(q6.y),
+                                                  __float_as_uint(q6.z), __float_as_uint(q6.w)),
+                                 0xE4u, [&](uint32_t v) {
+                                     if (sp < PT_STACK) {
+                                         s_ref[sp * PT_TRACE_BLOCK + lane] = v;
+                                         ++sp;
+                                     }
+                                 });
             continue;
         }
         uint32_t slot = ref & ~REF_LEAF;
