@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PT_API_VERSION 1
+#define PT_API_VERSION 2
 
 typedef int32_t pt_status;
 #define PT_OK 0
@@ -79,7 +79,9 @@ typedef struct pt_prim {
                           BLAS: index into pt_scene_desc.bvhs                    */
     int32_t material;  /* -1 = none: medium boundary, rays pass through         */
     int32_t light;     /* area light id or -1                                    */
-    int32_t medium;    /* medium id or -1 (carried, unused by Path/SimplePath)   */
+    int32_t medium;    /* inside medium of the boundary (MediumInterface), or -1:
+                          GeometricInteraction::getMedium (Interaction.hpp:26-29),
+                          used by VolPath only                                     */
 } pt_prim;
 
 typedef struct pt_bvh_desc {
@@ -146,6 +148,16 @@ typedef struct pt_light {
 
 enum { PT_LS_UNIFORM = 0, PT_LS_POWER = 1 };
 
+/* HomogeneusMedium (Medium.hpp:14-61) after its ctor (density applied:
+ * sigma_a = d*sa, sigma_s = d*ss, sigma_t = d*(sa+ss), Le = Le*LeDensity) with
+ * its HenyeyGreenstein phase function (PhaseFunction.hpp:17-27, g clamped to
+ * [-0.99, 0.99]). */
+typedef struct pt_medium {
+    float sigma_a[3], sigma_s[3], sigma_t[3];
+    float Le[3];
+    float g;
+} pt_medium;
+
 typedef struct pt_scene_desc {
     /* triangle meshes, global arrays */
     const float* positions;      /* 3 * n_vertices */
@@ -182,6 +194,10 @@ typedef struct pt_scene_desc {
     uint32_t n_sampler_lights;
     const uint32_t* infinite_lights; /* Scene::infiniteLights, in order         */
     uint32_t n_infinite_lights;
+    /* participating media (VolPath): pt_prim.medium and the ids below index it */
+    const pt_medium* media;
+    uint32_t n_media;
+    int32_t scene_medium;            /* Scene::GetMedium() (Scene.hpp:26), or -1 */
 } pt_scene_desc;
 
 /* Camera (Camera.hpp:7-35) after its ctor. */
@@ -191,9 +207,11 @@ typedef struct pt_camera_desc {
     float half_width, half_height;
     float defocus_radius, focus_distance, focus_angle;
     int32_t width, height;
+    int32_t medium;      /* Camera::GetMedium() (Camera.hpp:41-47), or -1   */
 } pt_camera_desc;
 
-enum { PT_INTEGRATOR_PATH = 0, PT_INTEGRATOR_SIMPLE = 1 };
+/* PathIntegrator / SimplePathIntegrator / VolPathIntegrator (Integrators.hpp:33-67) */
+enum { PT_INTEGRATOR_PATH = 0, PT_INTEGRATOR_SIMPLE = 1, PT_INTEGRATOR_VOLPATH = 2 };
 enum { PT_FILTER_MITCHELL = 0, PT_FILTER_BOX = 1, PT_FILTER_GAUSSIAN = 2 };
 #define PT_RENDER_COUNT_NODES 0x1u  /* instrumented traversal: node/tri counts */
 #define PT_RENDER_TIMING 0x2u       /* per-kernel HIP-event timing into stats   */

@@ -293,7 +293,7 @@ struct Flat {
             throw std::runtime_error("HipPathIntegrator: unsupported shape type");
         }
         p.material = material(PT_GET(gp, GpMaterial));
-        p.medium = PT_GET(gp, GpMedium) ? 0 : -1;
+        p.medium = -1;  // media: HipVolPathIntegrator (flattened below) only
         p.light = -1;
         if (const auto& al = PT_GET(gp, GpArea)) light_slot[al.get()] = (int32_t)slot;
     }
@@ -448,6 +448,7 @@ struct Flat {
         d.n_sampler_lights = (uint32_t)sampler_lights.size();
         d.infinite_lights = infinite_lights.data();
         d.n_infinite_lights = (uint32_t)infinite_lights.size();
+        d.scene_medium = -1;
         return d;
     }
 };
@@ -466,6 +467,7 @@ pt_camera_desc camera_desc(const Camera& cam) {
     glm::ivec2 res = cam.GetFilm()->Resolution();
     c.width = res.x;
     c.height = res.y;
+    c.medium = -1;
     return c;
 }
 

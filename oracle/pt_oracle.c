@@ -1120,6 +1120,7 @@ typedef struct {
     uint32_t max_depth;
     int simple;
     oracle_counters* cnt;
+    uint32_t kind; /* PT_INTEGRATOR_* */
 } integ_t;
 
 /* PathIntegrator::SampleLd (Integrators.cpp:260-294) */
@@ -1291,6 +1292,211 @@ static v3 li_simple(const integ_t* I, ray_t ray, rng_t* rng) {
     return out;
 }
 
+/* ------------------------------------------------------------------ media (Medium.hpp, PhaseFunction.*) */
+/* phaseHG (PhaseFunction.hpp:4-8) */
+static float phase_hg(float cosT, float g) {
+    float denom = 1 + g * g + 2 * g * cosT;
+    return 0.25f * (1.0f / PI_F) * (1.0f - g * g) / (denom * sqrtf(denom));
+}
+/* HenyeyGreenstein::Sample (PhaseFunction.cpp:8-25): direction, returns pdf */
+static v3 phase_sample(float g, v3 in, float u0, float u1) {
+    float cosT;
+    if (fabsf(g) < 1e-3f) {
+        cosT = 1 - 2 * u0;
+    } else {
+        float sqr = (1 - g * g) / (1 - g + 2 * g * u0);
+        cosT = (1 + g * g - sqr * sqr) / (2 * g);
+    }
+    float sinT = sqrtf(fmaxf_(0.0f, 1 - cosT * cosT));
+    float phi = 2 * PI_F * u1;
+    float x = sinT * cosf(phi), y = sinT * sinf(phi), z = cosT;
+    onb_t b = onb_n(in);
+    return normalize(to_world(&b, V(x, y, z)));
+}
+/* HomogeneusMedium::Tr (Medium.hpp:21-24) */
+static v3 medium_tr(const pt_medium* m, float t) {
+    float tt = t < 3.402823466e38f ? t : 3.402823466e38f;
+    return V(expf(-m->sigma_t[0] * tt), expf(-m->sigma_t[1] * tt), expf(-m->sigma_t[2] * tt));
+}
+/* HomogeneusMedium::Sample (Medium.hpp:26-45) with its two draws from the
+ * stream (channel, then distance); *scat receives the scatter point. */
+static v3 medium_sample(const pt_medium* m, const ray_t* r, float t, float u0, float u1, int* sampled, v3* scat) {
+    int ch = (int)(0.0f + 3.0f * u0);
+    float sd = (float)(-log(1.0 - (double)u1) / (double)m->sigma_t[ch]);
+    if (!(sd < t)) sd = t; /* std::min<float>(sd, t) */
+    *sampled = sd < t;
+    if (*sampled) *scat = V(fmaf(sd, r->d.x, r->o.x), fmaf(sd, r->d.y, r->o.y), fmaf(sd, r->d.z, r->o.z));
+    v3 tr = medium_tr(m, sd);
+    v3 den = *sampled ? mul(vl(m->sigma_t), tr) : tr;
+    float pdf = 0;
+    pdf += den.x;
+    pdf += den.y;
+    pdf += den.z;
+    pdf = (float)((double)pdf / 3.0);
+    return *sampled ? divs(mul(tr, vl(m->sigma_s)), pdf) : divs(tr, pdf);
+}
+/* GeometricInteraction::getMedium (Interaction.hpp:26-29) */
+static inline int get_medium(const si_t* si, v3 dir) { return dot(dir, si->n) < 0 ? si->medium : -1; }
+
+/* Scene::IntersectTr (Scene.cpp:8-29): returns 1 if a surface with a material
+ * blocks the segment; *Tr = transmittance through the media crossed. */
+static int intersect_tr(const integ_t* I, ray_t ray, int med, float max, v3* Tr) {
+    const scene_t* S = I->S;
+    *Tr = V(1, 1, 1);
+    while (max > 0) {
+        si_t si;
+        memset(&si, 0, sizeof(si));
+        work_t wk = {0, 0};
+        I->cnt->any++;
+        float m = max;
+        int hit = bvh_intersect(S, &S->s->bvhs[0], &ray, &m, &si, &wk);
+        I->cnt->nodes_any += wk.nodes;
+        I->cnt->tris_any += wk.tris;
+        if (!hit) {
+            if (med >= 0) *Tr = mul(*Tr, medium_tr(&S->s->media[med], max));
+            return 0;
+        }
+        if (med >= 0) *Tr = mul(*Tr, medium_tr(&S->s->media[med], si.t));
+        if (si.mat >= 0) return 1;
+        ray = mkray(at(&ray, si.t), ray.d);
+        med = get_medium(&si, ray.d);
+        max -= si.t;
+    }
+    return 0;
+}
+
+/* VolPathIntegrator::SampleLd (Integrators.cpp:416-479); phase_g >= -1 marks a
+ * medium interaction (p = si->p, f = phase pdf) */
+static v3 sample_ld_vol(const integ_t* I, const ray_t* ray, int ray_med, const si_t* si, int medium_it, float g,
+                        float u, float uv0, float uv1) {
+    const scene_t* S = I->S;
+    int li = ls_sample(S, u);
+    if (li < 0) return V(0, 0, 0);
+    const pt_light* l = &S->s->lights[li];
+    lsample_t ls = light_sample(S, l, uv0, uv1);
+    v3 ldir;
+    float t;
+    if (is_zero(ls.si.n)) {
+        ldir = ls.dir;
+        t = INFINITY;
+    } else {
+        ldir = sub(ls.si.p, si->p);
+        t = length3(ldir) - EPS_SHADOW;
+        t -= EPS_SHADOW;
+    }
+    ray_t sh = mkray(si->p, normalize(ldir));
+    float lpdf = l->pmf;
+    if (lpdf <= 0) return V(0, 0, 0);
+    v3 f;
+    float spdf;
+    if (medium_it) {
+        spdf = phase_hg(dot(ray->d, sh.d), g);
+        f = V(spdf, spdf, spdf);
+    } else {
+        float dt = dot(si->ns, sh.d);
+        if (dt * dot(ray->d, si->ns) >= 0) return V(0, 0, 0);
+        spdf = mat_pdf(S, si->mat, ray, si, sh.d);
+        f = muls(mat_f(S, si->mat, ray, si, sh.d), fabsf(dt));
+    }
+    v3 Tr;
+    if (is_zero(f) || intersect_tr(I, sh, ray_med, t, &Tr)) return V(0, 0, 0);
+    if (light_is_delta(l)) return divs(mul(mul(Tr, ls.L), f), lpdf);
+    lpdf *= light_pdf(S, l, &ls.si, &sh);
+    if (lpdf <= 0) return V(0, 0, 0);
+    float w2 = lpdf * lpdf;
+    float w1 = spdf;
+    w1 = w1 * w1;
+    float wl = w2 / (w1 + w2);
+    return divs(muls(mul(mul(Tr, light_L(S, l, &ls.si, &sh)), f), wl), lpdf);
+}
+
+/* VolPathIntegrator::Li (Integrators.cpp:296-413) */
+static v3 li_volpath(const integ_t* I, ray_t ray, int med, rng_t* rng) {
+    const scene_t* S = I->S;
+    v3 att = V(1, 1, 1), out = V(0, 0, 0);
+    uint32_t depth = 0, rr = 0;
+    float prev = 1;
+    int spec = 1;
+    while (depth++ < I->max_depth && (att.x + att.y + att.z) > 0.0f) {
+        si_t si;
+        memset(&si, 0, sizeof(si));
+        if (!intersect_counted(I, &ray, &si)) {
+            for (uint32_t k = 0; k < S->s->n_infinite_lights; k++) {
+                const pt_light* l = &S->s->lights[S->s->infinite_lights[k]];
+                if (spec) {
+                    out = add(out, mul(att, inf_le(l, ray.d)));
+                } else if (prev > 0) {
+                    float lp = l->pmf * (1.0f / (4.0f * PI_F));
+                    float w = prev * prev / (prev * prev + lp * lp);
+                    out = add(out, muls(mul(att, inf_le(l, ray.d)), w));
+                }
+            }
+            return out;
+        }
+        if (med < 0) med = S->s->scene_medium;
+        int mvalid = 0;
+        v3 mp = V(0, 0, 0);
+        if (med >= 0) {
+            float u0 = next1(rng), u1 = next1(rng);
+            att = mul(att, medium_sample(&S->s->media[med], &ray, si.t, u0, u1, &mvalid, &mp));
+        }
+        float r[9];
+        for (int k = 0; k < 9; k++) r[k] = next1(rng);
+        if (mvalid) {
+            const pt_medium* M = &S->s->media[med];
+            si_t mi;
+            memset(&mi, 0, sizeof(mi));
+            mi.p = mp;
+            out = add(out, mul(att, sample_ld_vol(I, &ray, med, &mi, 1, M->g, r[5], r[2], r[3])));
+            out = add(out, mul(att, vl(M->Le)));
+            v3 sc = phase_sample(M->g, ray.d, r[6], r[7]);
+            int nm = get_medium(&si, sc);
+            ray = mkray(mp, sc);
+            med = nm;
+            spec = 0;
+        } else {
+            if (si.light >= 0) {
+                const pt_light* al = &S->s->lights[si.light];
+                v3 L = light_L(S, al, &si, &ray);
+                if (!is_zero(L)) {
+                    if (spec) {
+                        out = add(out, mul(att, L));
+                    } else if (prev > 0) {
+                        float lp = al->pmf * light_pdf(S, al, &si, &ray);
+                        float w = prev * prev / (prev * prev + lp * lp);
+                        out = add(out, muls(mul(att, L), w));
+                    }
+                }
+            }
+            spec = 0;
+            if (si.mat < 0) {
+                ray.o = at(&ray, si.t);
+                med = get_medium(&si, ray.d);
+                continue;
+            }
+            bxdf_t b = mat_scatter(S, si.mat, &ray, &si, r[4], r[0], r[1]);
+            if (!b.ok) return out;
+            ray_t nr = mkray(b.o, b.d);
+            int nm = get_medium(&si, nr.d);
+            if (!(b.flags & FL_TRANS) && dot(ray.d, si.ns) <= 0) nm = med;
+            spec = (b.flags & FL_SPEC) != 0;
+            if (!spec) {
+                out = add(out, mul(att, sample_ld_vol(I, &ray, med, &si, 0, 0.0f, r[5], r[2], r[3])));
+                prev = mat_pdf(S, si.mat, &ray, &si, nr.d);
+            }
+            att = mul(att, divs(muls(b.f, fabsf(dot(si.ns, nr.d))), b.pdf));
+            ray = nr;
+            med = nm;
+        }
+        if (rr++ > 3) {
+            float q = fminf(0.95f, fmaxf(fmaxf(att.x, att.y), att.z));
+            if (r[8] >= q) break;
+            att = divs(att, q);
+        }
+    }
+    return out;
+}
+
 /* Camera::GenerateRay (Camera.hpp:21-35) + camera draws (Integrators.cpp:61-64) */
 static ray_t camera_ray(const pt_camera_desc* c, uint32_t x, uint32_t y, rng_t* rng, double* px, double* py) {
     float ja = next1(rng), jb = next1(rng);
@@ -1328,6 +1534,7 @@ static v3 li_one(const integ_t* I, const pt_camera_desc* cam, uint32_t seed, uin
     rng.dim = 0;
     ray_t r = camera_ray(cam, x, y, &rng, px, py);
     I->cnt->paths++;
+    if (I->kind == PT_INTEGRATOR_VOLPATH) return li_volpath(I, r, cam->medium, &rng);
     return I->simple ? li_simple(I, r, &rng) : li_path(I, r, &rng);
 }
 
@@ -1338,7 +1545,7 @@ int oracle_li(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render
     scene_init(&S, s);
     oracle_counters local;
     memset(&local, 0, sizeof(local));
-    integ_t I = {&S, rd->max_depth, rd->integrator == PT_INTEGRATOR_SIMPLE, cnt ? cnt : &local};
+    integ_t I = {&S, rd->max_depth, rd->integrator == PT_INTEGRATOR_SIMPLE, cnt ? cnt : &local, rd->integrator};
     size_t k = 0;
     for (uint32_t pix = pb; pix < pe; pix++) {
         uint32_t x = pix % (uint32_t)cam->width, y = pix / (uint32_t)cam->width;
@@ -1477,7 +1684,7 @@ static void* render_worker(void* arg) {
     scene_init(&S, J->s);
     oracle_counters c;
     memset(&c, 0, sizeof(c));
-    integ_t I = {&S, J->rd->max_depth, J->rd->integrator == PT_INTEGRATOR_SIMPLE, &c};
+    integ_t I = {&S, J->rd->max_depth, J->rd->integrator == PT_INTEGRATOR_SIMPLE, &c, J->rd->integrator};
     int W = J->cam->width, H = J->cam->height;
     double inv_int = 1.0 / filter_integral(J->rd);
     int rx = (int)ceilf(J->rd->filter_radius[0] - 0.5f), ry = (int)ceilf(J->rd->filter_radius[1] - 0.5f);

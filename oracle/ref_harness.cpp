@@ -103,6 +103,51 @@ private:
     uint32_t dim = 0;
 };
 
+// The sampler of the sample being traced (run_li is single-threaded).
+static DetSampler* g_stream = nullptr;
+
+// HomogeneusMedium (Medium.hpp:14-61) with its two hidden random_float() draws
+// (Medium.hpp:28-30) taken from the deterministic stream instead of the
+// unseeded thread-local PCG, so that VolPathIntegrator::Li is reproducible
+// (DESIGN.md §4): channel draw, then scatter-distance draw,
+// before the bounce's get2Dx4f()/get1D().  Tr, Le and the rest of Sample are
+// the reference's arithmetic; the scatter point is o + t*d with the products
+// fused (std::fma), the contract the oracle and the GPU path share.
+class StreamMedium : public Medium {
+public:
+    StreamMedium(const glm::vec3& sa, const glm::vec3& ss, std::shared_ptr<PhaseFunction> pf, float density,
+                 const glm::vec3& Le, float LeDensity)
+        : sigma_a(density * sa), sigma_s(density * ss), sigma_t(density * (sa + ss)), emission(Le * LeDensity),
+          phase(std::move(pf)) {}
+    glm::vec3 Tr(const Ray&, float t) const override {
+        return glm::exp(-sigma_t * std::min(t, std::numeric_limits<float>::max()));
+    }
+    glm::vec3 Sample(const Ray& ray, float t, MediumInteraction& interaction) const override {
+        const float u0 = g_stream ? (float)g_stream->get1D() : random_float();
+        const float u1 = g_stream ? (float)g_stream->get1D() : random_float();
+        int channel = (int)(0.0f + (3.0f - 0.0f) * u0);
+        float scatterDist = std::min<float>(-std::log(1.0 - u1) / sigma_t[channel], t);
+        bool sampledMedium = scatterDist < t;
+        if (sampledMedium) {
+            glm::vec3 p(std::fma(scatterDist, ray.dir.x, ray.origin.x), std::fma(scatterDist, ray.dir.y, ray.origin.y),
+                        std::fma(scatterDist, ray.dir.z, ray.origin.z));
+            interaction = MediumInteraction(p, {0, 0, 0}, ray.medium, phase);
+        }
+        glm::vec3 tr = Tr(ray, scatterDist);
+        glm::vec3 density = sampledMedium ? (sigma_t * tr) : tr;
+        float pdf = 0;
+        for (int i = 0; i < 3; i++) pdf += density[i];
+        pdf /= 3.0;
+        return sampledMedium ? (tr * sigma_s / pdf) : (tr / pdf);
+    }
+    bool IsEmmisive() const override { return Le() != glm::vec3(0, 0, 0); }
+    glm::vec3 Le() const override { return emission; }
+
+private:
+    glm::vec3 sigma_a, sigma_s, sigma_t, emission;
+    std::shared_ptr<PhaseFunction> phase;
+};
+
 // Expose protected BVH4 arrays (BVH.hpp:1214-1216, 392-394) — API use only.
 template <class T>
 struct Peek : BVH4<T> {
@@ -152,6 +197,7 @@ struct World {
     std::vector<std::shared_ptr<InfiniteLight>> inf;
     std::vector<std::shared_ptr<Light>> extra;
     std::string samplerKind = "uniform";
+    std::shared_ptr<Medium> sceneMedium, cameraMedium;
     glm::vec3 camFrom{0}, camAt{0, 0, -1};
     float fov = 1.0f, focusAngle = 0, focusDist = 0;
     int W = 64, H = 64;
@@ -213,9 +259,12 @@ static void read_recipe(World& w, const std::string& path) {
             }
             w.matId[w.mat[id].get()] = id;
         } else if (k == "medium") {
-            int id; float a0, a1, a2, s0, s1, s2, g, d; s >> id >> a0 >> a1 >> a2 >> s0 >> s1 >> s2 >> g >> d;
-            w.med[id] = std::make_shared<HomogeneusMedium>(glm::vec3(a0, a1, a2), glm::vec3(s0, s1, s2),
-                                                           std::make_shared<HenyeyGreenstein>(g), d);
+            int id; float a0, a1, a2, s0, s1, s2, g, d, l0 = 0, l1 = 0, l2 = 0, ld = 1;
+            s >> id >> a0 >> a1 >> a2 >> s0 >> s1 >> s2 >> g >> d;
+            if (!(s >> l0 >> l1 >> l2 >> ld)) { l0 = l1 = l2 = 0; ld = 1; }
+            w.med[id] = std::make_shared<StreamMedium>(glm::vec3(a0, a1, a2), glm::vec3(s0, s1, s2),
+                                                       std::make_shared<HenyeyGreenstein>(g), d,
+                                                       glm::vec3(l0, l1, l2), ld);
         } else if (k == "quad" || k == "sphere") {
             int pid; s >> pid;
             std::shared_ptr<Shape> shape;
@@ -305,6 +354,10 @@ static void read_recipe(World& w, const std::string& path) {
             if (kind == "distant") w.extra.push_back(std::make_shared<DistantLight>(glm::vec3(a, b, c), glm::vec3(r, g, bb)));
             else w.extra.push_back(std::make_shared<PointLight>(glm::vec3(a, b, c), glm::vec3(r, g, bb)));
             w.lightOwner[w.extra.back().get()] = "extra:" + std::to_string(w.extra.size() - 1);
+        } else if (k == "scenemedium") {
+            int id; s >> id; w.sceneMedium = w.med.at(id);
+        } else if (k == "cameramedium") {
+            int id; s >> id; w.cameraMedium = w.med.at(id);
         } else if (k == "lightsampler") {
             s >> w.samplerKind;
         } else if (k == "camera") {
@@ -324,6 +377,7 @@ static void read_recipe(World& w, const std::string& path) {
 
 static void build_world(World& w, bool counting = false) {
     w.scene = std::make_shared<Scene>();
+    if (w.sceneMedium) w.scene->SetMedium(w.sceneMedium);
     if (counting) {
         auto inner = std::make_shared<TLAS4>(w.top);
         w.scene->Add(std::make_shared<CountingPrim>(inner));
@@ -343,10 +397,12 @@ static void build_world(World& w, bool counting = false) {
         w.camera = std::make_shared<Camera>(w.camFrom, w.camAt, w.fov, w.film, w.focusAngle, w.focusDist);
     else
         w.camera = std::make_shared<Camera>(w.camFrom, w.camAt, w.fov, w.film);
+    if (w.cameraMedium) w.camera->SetMedium(w.cameraMedium);
 }
 
 static std::shared_ptr<Integrator> make_integrator(World& w, std::shared_ptr<Sampler> s) {
     if (w.integ == "simple") return std::make_shared<SimplePathIntegrator>(w.scene, w.camera, s, w.maxDepth);
+    if (w.integ == "volpath") return std::make_shared<VolPathIntegrator>(w.scene, w.camera, s, w.ls, w.maxDepth);
     return std::make_shared<PathIntegrator>(w.scene, w.camera, s, w.ls, w.maxDepth);
 }
 
@@ -461,6 +517,7 @@ struct SampleRec { double px, py; float L[3]; uint32_t dims; };
 static std::vector<SampleRec> run_li(World& w, int x0, int y0, int x1, int y1, unsigned spp) {
     std::vector<SampleRec> out;
     auto sampler = std::make_shared<DetSampler>(spp, w.seed, w.W);
+    g_stream = sampler.get();
     auto integ = make_integrator(w, sampler);
     for (int y = y0; y < y1; y++)
         for (int x = x0; x < x1; x++)

@@ -69,6 +69,9 @@ struct DevScene {
     float sampler_total;
     const uint32_t* infinite_lights;
     uint32_t n_infinite_lights;
+    const pt_medium* media;
+    uint32_t n_media;
+    int32_t scene_medium;
 };
 
 // The uploaded scene of the current context, in constant memory: every

@@ -1,6 +1,7 @@
 // Shared declarations between the wavefront kernels and the host runtime.
 #pragma once
 #include "pt_pool.h"
+#include "pt_medium.h"
 
 // path flags (b.w): depth | rr_depth << 12 | spec
 #define PF_DEPTH_MASK 0xFFFu
@@ -31,6 +32,7 @@
 #define CNT_NODES_ANY 2
 #define CNT_TRIS_ANY 3
 #define CNT_NEXT_SAMPLE 4
+#define CNT_EXTRA_ANY 5  // VolPath: shadow-ray continuations past medium boundaries
 #define CNT_COUNT 8
 #define CNT_SHARDS 64  // work counters are sharded by block to avoid a hot line
 
@@ -92,6 +94,11 @@ __global__ void k_shadow_pool(PathSoA next, float* sample_L, const ShadowRec* sq
 template <int INTEGRATOR>
 __global__ void k_shade(RenderParams R, PathSoA cur, const uint32_t* nptr, const float4* hit, PathSoA next,
                         float* sample_L, unsigned long long* next_sample, ShadowRec* sq, uint32_t* cnt);
+__global__ void k_shade_vol(RenderParams R, PathSoA cur, const uint32_t* nptr, const float4* hit, PathSoA next,
+                            float* sample_L, unsigned long long* next_sample, ShadowRec* sq, uint32_t* cnt);
+template <bool COUNT>
+__global__ void k_shadow_tr(PathSoA next, float* sample_L, const ShadowRec* sq, const uint32_t* nptr,
+                            unsigned long long* counters);
 __global__ void k_fill(RenderParams R, uint32_t n, PathSoA next, uint32_t* cnt, unsigned long long* next_sample);
 __global__ void k_gather(RenderParams R, const float* sample_L, double* film);
 __global__ void k_interact(const pt_ray* rays, uint32_t n, float* out);

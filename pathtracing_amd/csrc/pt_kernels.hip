@@ -448,10 +448,10 @@ __device__ __forceinline__ NewSample claim_camera_sample(const RenderParams& R, 
     }
     return ns;
 }
-__device__ __forceinline__ void store_camera_path(PathSoA& next, uint32_t at, const NewSample& ns) {
+__device__ __forceinline__ void store_camera_path(PathSoA& next, uint32_t at, const NewSample& ns, int cam_medium) {
     next.o[at] = make_float4(ns.o.x, ns.o.y, ns.o.z, __uint_as_float(ns.key));
-    // depth 1 (first loop test passed), spec = true
-    next.d[at] = make_float4(ns.d.x, ns.d.y, ns.d.z, __uint_as_float(1u | PF_SPEC));
+    // depth 1 (first loop test passed), spec = true, the camera's medium (Camera.hpp:27, 34)
+    next.d[at] = make_float4(ns.d.x, ns.d.y, ns.d.z, __uint_as_float(1u | PF_SPEC | medium_bits(cam_medium)));
     next.beta[at] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);  // attenuation, prevPDF = 1
     next.L[at] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(5u));  // camera used dims 0..4
     next.sid[at] = ns.sid;
@@ -469,7 +469,7 @@ __global__ __launch_bounds__(256) void k_fill(RenderParams R, uint32_t n, PathSo
     const bool pred[1] = {ns.enq};
     uint32_t at[1];
     block_append<1, 256>(cnt, qoff, pred, at);
-    if (ns.enq) store_camera_path(next, at[0], ns);
+    if (ns.enq) store_camera_path(next, at[0], ns, R.cam.medium);
 }
 
 // ------------------------------------------------------------------ shading
@@ -678,12 +678,320 @@ __global__ __launch_bounds__(256) void k_shade(RenderParams R, PathSoA cur, cons
         next.L[a] = make_float4(out.x, out.y, out.z, __uint_as_float(dim));
         next.sid[a] = sid;
     } else if (ns.enq) {
-        store_camera_path(next, a, ns);
+        store_camera_path(next, a, ns, R.cam.medium);
     }
     if (shadow) {
         srec.d.w = __uint_as_float(cont ? a : (SHADOW_DONE_BIT | sid));
         sq[c] = srec;
     }
+}
+
+// ------------------------------------------------------------------ VolPathIntegrator
+// SurfaceInteraction of a closest hit (prim slot, t and barycentrics / quad
+// coordinates from the traversal)
+__device__ __forceinline__ void hit_interaction(int prim, f3 ro, f3 rd, float t, float b1, float b2, SurfInt& si,
+                                                int& medium) {
+    const DevGeom g = S.geom[prim];
+    const DevPrimInfo pi = S.info[prim];
+    const uint32_t kind = __float_as_uint(g.a.w) & GF_KIND;
+    if (kind == PT_PRIM_TRIANGLE) tri_interaction(g, pi.index, pi.material, ro, rd, t, b1, b2, si);
+    else if (kind == PT_PRIM_QUAD) quad_interaction(S.quads[pi.index], ro, rd, t, b1, b2, si);
+    else sphere_interaction(S.spheres[pi.index], ro, rd, t, si);
+    si.mat = pi.material;
+    si.light = pi.light;
+    medium = pi.medium;
+}
+// GeometricInteraction::getMedium (Interaction.hpp:26-29)
+__device__ __forceinline__ int get_medium(const SurfInt& si, int medium, f3 dir) {
+    return dot(dir, si.n) < 0 ? medium : -1;
+}
+
+// One body of VolPathIntegrator::Li (Integrators.cpp:296-413).  Draw order per
+// bounce: the medium's (channel, distance) when the ray is in a medium, then
+// get2Dx4f() + get1D().  NEE (VolPathIntegrator::SampleLd, 416-479) becomes a
+// shadow record whose transmittance k_shadow_tr accumulates (Scene::IntersectTr).
+__global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, const uint32_t* __restrict__ nptr,
+                                                  const float4* __restrict__ hit, PathSoA next,
+                                                  float* __restrict__ sample_L,
+                                                  unsigned long long* __restrict__ next_sample,
+                                                  ShadowRec* __restrict__ sq, uint32_t* __restrict__ cnt) {
+    const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
+    if (blockIdx.x * 256 >= n) return;  // block-uniform: the grid covers the capacity
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    bool cont = false, done = false, shadow = false;
+    ShadowRec srec;
+    f3 ro = F3(0, 0, 0), rd = F3(0, 0, 0), att = F3(0, 0, 0), out = F3(0, 0, 0);
+    float prev = 0;
+    uint32_t key = 0, dim = 0, flags = 0, sid = 0;
+    if (i < n) {
+        const uint32_t e = path_slot(i, front, cur.cap);
+        const float4 o4 = cur.o[e], d4 = cur.d[e], b4 = cur.beta[e], L4 = cur.L[e];
+        const float4 h = hit[i];
+        sid = cur.sid[e];
+        ro = xyz(o4);
+        rd = xyz(d4);
+        att = xyz(b4);
+        out = xyz(L4);
+        prev = b4.w;
+        key = __float_as_uint(o4.w);
+        dim = __float_as_uint(L4.w);
+        const uint32_t f0 = __float_as_uint(d4.w);
+        uint32_t depth = f0 & PF_DEPTH_MASK, rr = (f0 >> PF_RR_SHIFT) & PF_DEPTH_MASK;
+        bool spec = (f0 & PF_SPEC) != 0;
+        int med = flags_medium(f0);
+        const int prim = __float_as_int(h.w);
+        bool alive = true, do_rr = true;
+        if (prim < 0) {
+            // miss: infinite lights, no medium attenuation (Integrators.cpp:308-329)
+            for (uint32_t k = 0; k < S.n_infinite_lights; k++) {
+                const pt_light& l = S.lights[S.infinite_lights[k]];
+                if (spec) {
+                    out = out + att * inf_le(l, rd);
+                } else if (prev > 0) {
+                    float lp = l.pmf * (1.0f / (4.0f * PT_PI));
+                    float w = prev * prev / (prev * prev + lp * lp);
+                    out = out + (att * inf_le(l, rd)) * w;
+                }
+            }
+            alive = false;
+        } else {
+            SurfInt si;
+            int smed;
+            hit_interaction(prim, ro, rd, h.x, h.y, h.z, si, smed);
+            if (med < 0) med = S.scene_medium;
+            bool mvalid = false;
+            f3 mp = F3(0, 0, 0);
+            if (med >= 0) {
+                const float u0 = draw(key, dim), u1 = draw(key, dim + 1);
+                dim += 2;
+                att = att * medium_sample(S.media[med], ro, rd, si.t, u0, u1, mvalid, mp);
+            }
+            float r[9];
+#pragma unroll
+            for (int k = 0; k < 9; k++) r[k] = draw(key, dim + k);
+            dim += 9;
+            // NEE (SampleLd): from the medium point with the phase function, or
+            // from the surface with the BSDF; shadow ray in the current medium
+            bool nee = false, nee_medium = false;
+            if (mvalid) {
+                const pt_medium& M = S.media[med];
+                nee = true;
+                nee_medium = true;
+                out = out + att * ld3(M.Le);  // output += att * Le (Integrators.cpp:357)
+                si.p = mp;
+            } else {
+                if (si.light >= 0) {
+                    const pt_light& al = S.lights[si.light];
+                    f3 Le = light_L(al, si.n, si.u, si.v, rd);
+                    if (!is_zero(Le)) {
+                        if (spec) {
+                            out = out + att * Le;
+                        } else if (prev > 0) {
+                            float lp = al.pmf * light_pdf(al, si.p, si.n, ro, rd);
+                            float w = prev * prev / (prev * prev + lp * lp);
+                            out = out + (att * Le) * w;
+                        }
+                    }
+                }
+            }
+            Bxdf b;
+            b.ok = false;
+            if (!mvalid && si.mat >= 0) {
+                b = mat_scatter(si.mat, ro, rd, si, r[4], r[0], r[1]);
+                if (b.ok && !(b.flags & FL_SPEC)) nee = true;
+            }
+            if (nee) {
+                const int li = ls_sample(r[5]);
+                if (li >= 0 && S.lights[li].pmf > 0) {
+                    const pt_light& l = S.lights[li];
+                    LSample ls = light_sample(l, r[2], r[3]);
+                    f3 ldir;
+                    float tmax;
+                    if (is_zero(ls.n)) {
+                        ldir = ls.dir;
+                        tmax = __int_as_float(0x7f800000);
+                    } else {
+                        ldir = ls.p - si.p;
+                        tmax = length(ldir) - PT_EPS;
+                        tmax -= PT_EPS;
+                    }
+                    const f3 sd = normalize(ldir);
+                    float lpdf = l.pmf;
+                    f3 f;
+                    float spdf;
+                    bool ok = true;
+                    if (nee_medium) {
+                        spdf = phase_hg(dot(rd, sd), S.media[med].g);
+                        f = F3(spdf, spdf, spdf);
+                    } else {
+                        const float dt = dot(si.ns, sd);
+                        ok = !(dt * dot(rd, si.ns) >= 0);
+                        spdf = ok ? mat_pdf(si.mat, rd, si, sd) : 0.0f;
+                        f = ok ? mat_f(si.mat, rd, si, sd) * fabsf(dt) : F3(0, 0, 0);
+                    }
+                    f3 c;
+                    if (ok && !is_zero(f)) {
+                        if (light_is_delta(l)) {
+                            c = (ls.L * f) / lpdf;
+                        } else {
+                            lpdf *= light_pdf(l, ls.p, ls.n, si.p, sd);
+                            if (lpdf <= 0) {
+                                ok = false;
+                            } else {
+                                float w2 = lpdf * lpdf;
+                                float w1 = spdf * spdf;
+                                float wl = w2 / (w1 + w2);
+                                c = ((light_L(l, ls.n, ls.u, ls.v, sd) * f) * wl) / lpdf;
+                            }
+                        }
+                        if (ok) {
+                            const f3 contrib = att * c;  // the shadow kernel multiplies Tr in
+                            if (!is_zero(contrib)) {
+                                shadow = true;
+                                srec.o = make_float4(si.p.x, si.p.y, si.p.z, tmax);
+                                srec.d = make_float4(sd.x, sd.y, sd.z, 0.0f);
+                                srec.c = make_float4(contrib.x, contrib.y, contrib.z, __int_as_float(med));
+                            }
+                        }
+                    }
+                }
+            }
+            if (mvalid) {
+                // phase scattering (Integrators.cpp:358-361)
+                const f3 sc = phase_sample(S.media[med].g, rd, r[6], r[7]);
+                const int nm = get_medium(si, smed, sc);
+                ro = mp;
+                rd = sc;
+                med = nm;
+                spec = false;
+            } else {
+                spec = false;
+                if (si.mat < 0) {
+                    // medium boundary: pass through, no RR (Integrators.cpp:378-382)
+                    ro = ro + si.t * rd;
+                    med = get_medium(si, smed, rd);
+                    do_rr = false;
+                } else if (!b.ok) {
+                    alive = false;  // absorbed
+                } else {
+                    int nm = get_medium(si, smed, b.d);
+                    if (!(b.flags & FL_TRANS) && dot(rd, si.ns) <= 0) nm = med;
+                    spec = (b.flags & FL_SPEC) != 0;
+                    if (!spec) prev = mat_pdf(si.mat, rd, si, b.d);
+                    att = att * ((b.f * fabsf(dot(si.ns, b.d))) / b.pdf);
+                    ro = b.o;
+                    rd = b.d;
+                    med = nm;
+                }
+            }
+            if (alive && do_rr && rr++ > 3) {
+                float qq = fminf(0.95f, fmaxf(fmaxf(att.x, att.y), att.z));
+                if (r[8] >= qq) alive = false;
+                else att = att / qq;
+            }
+        }
+        if (alive && depth < R.max_depth && (att.x + att.y + att.z) > 0.0f) {
+            depth++;
+            cont = true;
+        } else {
+            done = true;
+        }
+        flags = depth | (rr << PF_RR_SHIFT) | (spec ? PF_SPEC : 0u) | medium_bits(med);
+    }
+    if (done) {
+        float* o = sample_L + 3ull * sid;
+        o[0] = out.x;
+        o[1] = out.y;
+        o[2] = out.z;
+    }
+    const NewSample ns = claim_camera_sample(R, done, next_sample);
+    const int qoff[3] = {Q_NEXT, Q_SHADOW, Q_NEW};
+    const bool pred[3] = {cont, shadow, ns.enq};
+    uint32_t at[3];
+    block_append<3, 256>(cnt, qoff, pred, at);
+    const uint32_t a = cont ? at[0] : next.cap - 1u - at[2], c = at[1];
+    if (cont) {
+        next.o[a] = make_float4(ro.x, ro.y, ro.z, __uint_as_float(key));
+        next.d[a] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(flags));
+        next.beta[a] = make_float4(att.x, att.y, att.z, prev);
+        next.L[a] = make_float4(out.x, out.y, out.z, __uint_as_float(dim));
+        next.sid[a] = sid;
+    } else if (ns.enq) {
+        store_camera_path(next, a, ns, R.cam.medium);
+    }
+    if (shadow) {
+        srec.d.w = __uint_as_float(cont ? a : (SHADOW_DONE_BIT | sid));
+        sq[c] = srec;
+    }
+}
+
+// NEE shadow rays of VolPath: Scene::IntersectTr (Scene.cpp:8-29) — closest
+// hits along the segment, passing medium boundaries (no material) and
+// multiplying the transmittance of the media crossed; a surface with a
+// material occludes.  One ray per lane (media scenes are small).
+template <bool COUNT>
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow_tr(PathSoA next, float* __restrict__ sample_L,
+                                                             const ShadowRec* __restrict__ sq,
+                                                             const uint32_t* __restrict__ nptr,
+                                                             unsigned long long* counters) {
+    __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+    const uint32_t n = *nptr;
+    if (blockIdx.x * PT_TRACE_BLOCK >= n) return;
+    const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
+    TraceWork wk{0, 0};
+    uint32_t extra = 0;
+    if (i < n) {
+        const ShadowRec r = sq[i];
+        f3 o = xyz(r.o), d = xyz(r.d);
+        float max = r.o.w;
+        int med = __float_as_int(r.c.w);
+        f3 Tr = F3(1, 1, 1);
+        bool occluded = false;
+        bool first = true;
+        while (max > 0) {
+            if (!first) extra++;
+            first = false;
+            float t, b1, b2;
+            const int prim = trace_closest<COUNT>(o, d, max, t, b1, b2, s_ref, wk);
+            if (prim < 0) {
+                if (med >= 0) Tr = Tr * medium_tr(S.media[med], max);
+                break;
+            }
+            if (med >= 0) Tr = Tr * medium_tr(S.media[med], t);
+            if (S.info[prim].material >= 0) {
+                occluded = true;
+                break;
+            }
+            SurfInt si;
+            int smed;
+            hit_interaction(prim, o, d, t, b1, b2, si, smed);
+            o = o + t * d;
+            med = get_medium(si, smed, d);
+            max -= t;
+        }
+        if (!occluded) {
+            const f3 c = Tr * xyz(r.c);
+            const uint32_t tgt = __float_as_uint(r.d.w);
+            if (tgt & SHADOW_DONE_BIT) {
+                float* L = sample_L + 3ull * (tgt & ~SHADOW_DONE_BIT);
+                L[0] += c.x;
+                L[1] += c.y;
+                L[2] += c.z;
+            } else {
+                float4* L = &next.L[tgt];
+                float4 v = *L;
+                v.x += c.x;
+                v.y += c.y;
+                v.z += c.z;
+                *L = v;
+            }
+        }
+    }
+    if (COUNT) {
+        count_add(counters, CNT_NODES_ANY, wk.nodes);
+        count_add(counters, CNT_TRIS_ANY, wk.tris);
+    }
+    count_add(counters, CNT_EXTRA_ANY, extra);
 }
 
 // ------------------------------------------------------------------ film gather
@@ -769,6 +1077,8 @@ __global__ __launch_bounds__(256) void k_gather(RenderParams R, const float* __r
                                               uint32_t*, unsigned long long*);
 PT_INST_TRACE(false)
 PT_INST_TRACE(true)
+template __global__ void k_shadow_tr<false>(PathSoA, float*, const ShadowRec*, const uint32_t*, unsigned long long*);
+template __global__ void k_shadow_tr<true>(PathSoA, float*, const ShadowRec*, const uint32_t*, unsigned long long*);
 template __global__ void k_shade<PT_INTEGRATOR_PATH>(RenderParams, PathSoA, const uint32_t*, const float4*, PathSoA,
                                                      float*, unsigned long long*, ShadowRec*, uint32_t*);
 template __global__ void k_shade<PT_INTEGRATOR_SIMPLE>(RenderParams, PathSoA, const uint32_t*, const float4*,

@@ -34,6 +34,7 @@ struct pt_ctx {
     DevScene scene{};
     bool has_scene = false;
     uint32_t n_materials = 0;
+    uint32_t n_media = 0;
     uint32_t trace_blocks = 0;  // resident traversal blocks on this device (persistent grid)
     uint64_t n_clusters = 0;    // BVH clusters of the uploaded scene (traversal choice)
     // wavefront buffers: two compacted path states (ping-pong), per-bounce hits,
@@ -311,6 +312,7 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
         }
         if (!ok) return fail(c, PT_ERR_ARG, "primitive %u: bad kind/index", i);
         if (p.material >= (int32_t)s->n_materials) return fail(c, PT_ERR_ARG, "primitive %u: bad material", i);
+        if (p.medium < -1 || p.medium >= (int32_t)s->n_media) return fail(c, PT_ERR_ARG, "primitive %u: bad medium", i);
         if (p.light >= (int32_t)s->n_lights) return fail(c, PT_ERR_ARG, "primitive %u: bad light", i);
     }
     for (uint32_t t = 0; t < s->n_triangles; t++)
@@ -335,6 +337,9 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
     }
     for (uint32_t i = 0; i < s->n_sampler_lights; i++)
         if (s->sampler_lights[i] >= s->n_lights) return fail(c, PT_ERR_ARG, "sampler light %u out of range", i);
+    if (s->n_media && !s->media) return fail(c, PT_ERR_ARG, "media array missing");
+    if (s->n_media > PT_MAX_MEDIA) return fail(c, PT_ERR_ARG, "more than %d media", PT_MAX_MEDIA);
+    if (s->scene_medium < -1 || s->scene_medium >= (int32_t)s->n_media) return fail(c, PT_ERR_ARG, "bad scene medium");
     for (uint32_t i = 0; i < s->n_infinite_lights; i++)
         if (s->infinite_lights[i] >= s->n_lights) return fail(c, PT_ERR_ARG, "infinite light %u out of range", i);
 
@@ -428,6 +433,7 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
     UP(DS.sampler_lights, s->sampler_lights, s->n_sampler_lights);
     UP(DS.sampler_cdf, cdf.data(), cdf.size());
     UP(DS.infinite_lights, s->infinite_lights, s->n_infinite_lights);
+    UP(DS.media, s->media, s->n_media);
 #undef UP
     DS.root = roots[0];
     DS.n_prims = s->n_prims;
@@ -438,7 +444,10 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
     DS.n_sampler_lights = s->n_sampler_lights;
     DS.sampler_total = acc;
     DS.n_infinite_lights = s->n_infinite_lights;
+    DS.n_media = s->n_media;
+    DS.scene_medium = s->scene_medium;
     c->has_scene = true;
+    c->n_media = s->n_media;
     c->n_materials = s->n_materials;
     c->n_clusters = nodes.size();
     return PT_OK;
@@ -675,12 +684,21 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                 hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_SIMPLE>, gs, dim3(256), 0, sm, R, cur,
                                    (const uint32_t*)(in + Q_NEXT), (const float4*)c->hit, nxt, c->sample_L,
                                    next_sample, c->sq, out);
+            else if (rd->integrator == PT_INTEGRATOR_VOLPATH)
+                hipLaunchKernelGGL(k_shade_vol, gs, dim3(256), 0, sm, R, cur, (const uint32_t*)(in + Q_NEXT),
+                                   (const float4*)c->hit, nxt, c->sample_L, next_sample, c->sq, out);
             else
                 hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_PATH>, gs, dim3(256), 0, sm, R, cur,
                                    (const uint32_t*)(in + Q_NEXT), (const float4*)c->hit, nxt, c->sample_L,
                                    next_sample, c->sq, out);
             if (timing) HIPCHK(c, hipEventRecord(ev[2], sm));
-            if (rd->integrator != PT_INTEGRATOR_SIMPLE) {
+            if (rd->integrator == PT_INTEGRATOR_VOLPATH) {
+                // transmittance along the shadow rays: one ray per lane, the grid covers the capacity
+                hipLaunchKernelGGL(count ? k_shadow_tr<true> : k_shadow_tr<false>,
+                                   dim3((paths + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK), dim3(PT_TRACE_BLOCK), 0, sm,
+                                   nxt, c->sample_L, (const ShadowRec*)c->sq, (const uint32_t*)(out + Q_SHADOW),
+                                   c->counters);
+            } else if (rd->integrator != PT_INTEGRATOR_SIMPLE) {
                 auto ks = use_pool ? (count ? k_shadow_pool<true> : k_shadow_pool<false>)
                                    : (count ? k_shadow<true> : k_shadow<false>);
                 hipLaunchKernelGGL(ks, gt, dim3(PT_TRACE_BLOCK), 0, sm, nxt, c->sample_L, (const ShadowRec*)c->sq,
@@ -719,6 +737,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         stats->nodes_closest += h[CNT_NODES_CLOSEST];
         stats->tris_closest += h[CNT_TRIS_CLOSEST];
         stats->nodes_any += h[CNT_NODES_ANY];
+        stats->rays_any += h[CNT_EXTRA_ANY];
         stats->tris_any += h[CNT_TRIS_ANY];
         stats->ms_closest += t_cl;
         stats->ms_shade += t_sh;
@@ -733,8 +752,9 @@ static pt_status check_render_args(pt_ctx* c, const pt_camera_desc* cam, const p
     if (!c->has_scene) return fail(c, PT_ERR_STATE, "no scene uploaded");
     if (cam->width <= 0 || cam->height <= 0 || (uint64_t)cam->width * cam->height > (1ull << 31))
         return fail(c, PT_ERR_ARG, "bad film size");
-    if (rd->integrator > PT_INTEGRATOR_SIMPLE || rd->filter > PT_FILTER_GAUSSIAN)
+    if (rd->integrator > PT_INTEGRATOR_VOLPATH || rd->filter > PT_FILTER_GAUSSIAN)
         return fail(c, PT_ERR_ARG, "bad integrator/filter");
+    if (cam->medium < -1 || cam->medium >= (int32_t)c->n_media) return fail(c, PT_ERR_ARG, "bad camera medium");
     if (rd->filter_radius[0] <= 0 || rd->filter_radius[1] <= 0) return fail(c, PT_ERR_ARG, "bad filter radius");
     return PT_OK;
 }

@@ -56,6 +56,23 @@ class FlatScene:
     sampler_lights: Optional[np.ndarray] = None
     infinite_lights: Optional[np.ndarray] = None
     light_objects: list = field(default_factory=list)
+    # participating media: id(HomogeneusMedium) -> index into `media`
+    media: Optional[np.ndarray] = None
+    medium_ids: Dict[int, int] = field(default_factory=dict)
+    scene_medium: int = -1
+
+    def medium_id(self, md) -> int:
+        """Index of medium `md` (registered on first use), -1 for None."""
+        if md is None:
+            return -1
+        if id(md) not in self.medium_ids:
+            rec = np.zeros(1, dtype=N.MEDIUM)
+            rec["sigma_a"], rec["sigma_s"], rec["sigma_t"] = md.sigma_a, md.sigma_s, md.sigma_t
+            rec["Le"], rec["g"] = md.Le(), md.g
+            self.medium_ids[id(md)] = len(self.medium_ids)
+            self.media = rec if self.media is None else np.concatenate([self.media, rec])
+            self._medium_keep = getattr(self, "_medium_keep", []) + [md]
+        return self.medium_ids[id(md)]
 
     @property
     def n_prims(self) -> int:
@@ -106,6 +123,9 @@ class FlatScene:
         d.n_sampler_lights = self.sampler_lights.shape[0]
         d.infinite_lights = N.ptr(self.infinite_lights)
         d.n_infinite_lights = self.infinite_lights.shape[0]
+        d.media = N.ptr(self.media)
+        d.n_media = 0 if self.media is None else self.media.shape[0]
+        d.scene_medium = self.scene_medium
         return d
 
 
@@ -216,7 +236,7 @@ def flatten_scene(scene: Scene) -> FlatScene:
     for m in models:
         model_tri_base.append(tri_base)
         boxes = []
-        mats, meds = [], []
+        mats, meds, med_objs = [], [], []
         for mesh in m.meshes:
             nv = mesh.vertices.shape[0]
             pos.append(mesh.vertices)
@@ -230,13 +250,14 @@ def flatten_scene(scene: Scene) -> FlatScene:
             mat = m.override_material if m.override_material is not None else mesh.material
             mats.append(np.full(nt, reg.material(mat), dtype=np.int32))
             med = m.override_medium if m.override_medium is not None else mesh.medium
-            meds.append(np.full(nt, -1 if med is None else 0, dtype=np.int32))
+            meds.append(np.full(nt, -1, dtype=np.int32))
+            med_objs.append((len(meds) - 1, med))
             vbase += nv
             tri_base += nt
         bx = np.concatenate(boxes) if boxes else np.zeros((0, 6), np.float32)
         model_blas.append(N.bvh4_build(bx))
         model_tri_mat.append(np.concatenate(mats) if mats else np.zeros(0, np.int32))
-        model_tri_med.append(np.concatenate(meds) if meds else np.zeros(0, np.int32))
+        model_tri_med.append((meds, med_objs))
 
     # ---- TLAS over top-level primitives ----
     quads, spheres = [], []
@@ -261,6 +282,7 @@ def flatten_scene(scene: Scene) -> FlatScene:
     prims["medium"] = -1
     light_slot: Dict[int, int] = {}
     tlas_lights = []
+    top_media = []  # (slot, medium object) of top-level primitives
     # BLAS slot ranges
     blas_base = []
     base = n_top
@@ -302,7 +324,7 @@ def flatten_scene(scene: Scene) -> FlatScene:
             else:
                 raise TypeError(f"unsupported shape {type(sh).__name__}")
             rec["material"] = reg.material(p.material)
-            rec["medium"] = -1 if p.medium is None else 0
+            top_media.append((slot, p.medium))
             if p.areaLight is not None:
                 light_slot[id(p.areaLight)] = slot
                 tlas_lights.append(p.areaLight)
@@ -314,7 +336,7 @@ def flatten_scene(scene: Scene) -> FlatScene:
         prims["kind"][s0:s0 + n] = N.PT_PRIM_TRIANGLE
         prims["index"][s0:s0 + n] = order + np.uint32(model_tri_base[k])
         prims["material"][s0:s0 + n] = model_tri_mat[k][order]
-        prims["medium"][s0:s0 + n] = model_tri_med[k][order]
+        model_tri_med[k] = (order, s0, n, model_tri_med[k])
     for al in tlas_lights:
         pass
     # emissive triangle lights: fill prim light ids later in bind_lights
@@ -340,6 +362,15 @@ def flatten_scene(scene: Scene) -> FlatScene:
         top_order=tl_order, blas_orders=[b[2] for b in model_blas], model_tri_base=model_tri_base,
         texture_ids=dict(reg.tex_ids))
     flat._reg = reg
+    # media: the scene's first, then primitives in slot order, then meshes
+    flat.scene_medium = flat.medium_id(scene.GetMedium())
+    for slot, md in top_media:
+        prims["medium"][slot] = flat.medium_id(md)
+    for order, s0, n, (meds, med_objs) in model_tri_med:
+        for j, md in med_objs:
+            meds[j][:] = flat.medium_id(md)
+        tri_med = np.concatenate(meds) if meds else np.zeros(0, np.int32)
+        prims["medium"][s0:s0 + n] = tri_med[order]
     return flat
 
 
@@ -404,8 +435,12 @@ def bind_lights(flat: FlatScene, scene: Scene, sampler: Optional[LightSampler]):
     return flat
 
 
-def camera_desc(cam) -> N.CameraDesc:
+def camera_desc(cam, flat: Optional[FlatScene] = None) -> N.CameraDesc:
     d = N.CameraDesc()
+    md = cam.GetMedium() if hasattr(cam, "GetMedium") else None
+    if md is not None and (flat is None or id(md) not in flat.medium_ids):
+        raise ValueError("camera medium not registered with the flat scene (use an Integrator)")
+    d.medium = -1 if md is None else flat.medium_ids[id(md)]
     d.origin[:] = [float(x) for x in cam.lookFrom]
     d.u[:] = [float(x) for x in cam.u]
     d.v[:] = [float(x) for x in cam.v]

@@ -166,11 +166,12 @@ class Integrator:
         if scene.flat is None:
             scene.BuildTlas()
         self.flat = bind_lights(scene.flat, scene, lightSampler)
+        self.flat.medium_id(camera.GetMedium())  # registered before upload
         self.last_stats: dict = {}
 
     def context(self, device: int = 0) -> Context:
         ctx = get_context(device)
-        key = (id(self.flat), id(self.lightSampler))
+        key = (id(self.flat), id(self.lightSampler), len(self.flat.medium_ids))
         if ctx.scene_key != key:
             ctx.upload(self.flat, key)
         return ctx
@@ -179,7 +180,7 @@ class Integrator:
         film = self.camera.GetFilm()
         rd = render_desc(self.kind, kw.pop("spp", self.sampler.SamplesPerPixel()), self.maxDepth,
                          kw.pop("seed", self.sampler.seed), film.filter, **kw)
-        return camera_desc(self.camera), rd
+        return camera_desc(self.camera, self.flat), rd
 
     def Render(self, device: int = 0, shard_index: int = 0, shard_count: int = 1, flags: int = 0,
                film_ptr: int | None = None, paths_in_flight: int = 0) -> dict:
@@ -209,6 +210,16 @@ class Integrator:
 class PathIntegrator(Integrator):
     """PathIntegrator (Integrators.hpp:43-54): NEE + MIS (power heuristic) + RR."""
     kind = N.PT_INTEGRATOR_PATH
+
+
+class VolPathIntegrator(Integrator):
+    """VolPathIntegrator (Integrators.hpp:56-67, Integrators.cpp:296-479):
+    PathIntegrator plus homogeneous media (Medium.hpp), Henyey-Greenstein
+    phase sampling, NEE from medium points and transmittance along shadow rays
+    (Scene::IntersectTr, Scene.cpp:8-29).  The medium's two hidden
+    random_float() draws (Medium.hpp:28-30) come from the sample stream, right
+    before the bounce's nine draws."""
+    kind = N.PT_INTEGRATOR_VOLPATH
 
 
 class SimplePathIntegrator(Integrator):

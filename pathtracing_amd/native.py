@@ -21,7 +21,7 @@ PT_TEX_SOLID, PT_TEX_IMAGE, PT_TEX_CHECKER = 0, 1, 2
 PT_MAT_DIFFUSE, PT_MAT_DIELECTRIC, PT_MAT_THIN, PT_MAT_CONDUCTOR = 0, 1, 2, 3
 PT_LIGHT_AREA, PT_LIGHT_UNIFORM_INF, PT_LIGHT_SKY_INF, PT_LIGHT_DISTANT, PT_LIGHT_POINT = 0, 1, 2, 3, 4
 PT_LS_UNIFORM, PT_LS_POWER = 0, 1
-PT_INTEGRATOR_PATH, PT_INTEGRATOR_SIMPLE = 0, 1
+PT_INTEGRATOR_PATH, PT_INTEGRATOR_SIMPLE, PT_INTEGRATOR_VOLPATH = 0, 1, 2
 PT_FILTER_MITCHELL, PT_FILTER_BOX, PT_FILTER_GAUSSIAN = 0, 1, 2
 PT_RENDER_COUNT_NODES = 0x1
 PT_RENDER_TIMING = 0x2
@@ -44,6 +44,8 @@ MATERIAL = np.dtype([("kind", "<u4"), ("tex", "<i4"), ("norm", "<i4"), ("rough",
                      ("albedo", "<f4", 3)])
 LIGHT = np.dtype([("kind", "<u4"), ("prim", "<i4"), ("tex", "<i4"), ("one_sided", "<u4"), ("power", "<f4"),
                   ("pmf", "<f4"), ("color", "<f4", 3), ("vec", "<f4", 3), ("scale", "<f4")])
+MEDIUM = np.dtype([("sigma_a", "<f4", 3), ("sigma_s", "<f4", 3), ("sigma_t", "<f4", 3), ("Le", "<f4", 3),
+                   ("g", "<f4")])
 RAY = np.dtype([("o", "<f4", 3), ("d", "<f4", 3), ("tmax", "<f4")])
 HIT = np.dtype([("t", "<f4"), ("b1", "<f4"), ("b2", "<f4"), ("prim", "<i4")])
 
@@ -79,6 +81,7 @@ class SceneDesc(C.Structure):
         ("light_sampler", C.c_uint32),
         ("sampler_lights", C.c_void_p), ("n_sampler_lights", C.c_uint32),
         ("infinite_lights", C.c_void_p), ("n_infinite_lights", C.c_uint32),
+        ("media", C.c_void_p), ("n_media", C.c_uint32), ("scene_medium", C.c_int32),
     ]
 
 
@@ -86,7 +89,7 @@ class CameraDesc(C.Structure):
     _fields_ = [("origin", C.c_float * 3), ("u", C.c_float * 3), ("v", C.c_float * 3), ("w", C.c_float * 3),
                 ("half_width", C.c_float), ("half_height", C.c_float), ("defocus_radius", C.c_float),
                 ("focus_distance", C.c_float), ("focus_angle", C.c_float), ("width", C.c_int32),
-                ("height", C.c_int32)]
+                ("height", C.c_int32), ("medium", C.c_int32)]
 
 
 class RenderDesc(C.Structure):

@@ -96,8 +96,9 @@ def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: 
         if id(md) not in med_ids:
             i = len(med_ids)
             med_ids[id(md)] = i
-            lines.append(f"medium {i} {' '.join(_f(x) for x in md.sigma_a)} {' '.join(_f(x) for x in md.sigma_s)} "
-                         f"{_f(md.g)} {_f(md.density)}")
+            lines.append(f"medium {i} {' '.join(_f(x) for x in md.sigma_a_in)} "
+                         f"{' '.join(_f(x) for x in md.sigma_s_in)} {_f(md.phaseFunction.G)} {_f(md.density)} "
+                         f"{' '.join(_f(x) for x in md.Le_in)} {_f(md.LeDensity)}")
         return med_ids[id(md)]
 
     def mesh(me) -> int:
@@ -154,6 +155,10 @@ def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: 
         else:
             raise TypeError(type(l))
     lines.append(f"lightsampler {'power' if isinstance(light_sampler, PowerLightSampler) else 'uniform'}")
+    if scene.GetMedium() is not None:
+        lines.append(f"scenemedium {med(scene.GetMedium())}")
+    if camera.GetMedium() is not None:
+        lines.append(f"cameramedium {med(camera.GetMedium())}")
     W, H = camera.film.Resolution()
     lines.append(f"camera {' '.join(_f(x) for x in [*camera.lookFrom, *camera.lookAt])} {_f(camera.fov)} {W} {H} "
                  f"{_f(camera.FocusAngle)} {_f(camera.FocusDistance)}")

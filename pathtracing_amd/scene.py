@@ -340,14 +340,46 @@ class Mesh:
 
 
 # --------------------------------------------------------------------------
-# Media (only the boundary semantics matter on the hot path)
+# Media (Medium.hpp, PhaseFunction.hpp): VolPathIntegrator's participating media
 # --------------------------------------------------------------------------
+class HenyeyGreenstein:
+    """PhaseFunction.hpp:17-27: g clamped to [-0.99, 0.99] by the ctor."""
+
+    def __init__(self, G: float):
+        self.G = float(np.float32(G))
+        self.g = float(np.clip(np.float32(G), np.float32(-0.99), np.float32(0.99)))
+
+
 class HomogeneusMedium:
-    def __init__(self, sigma_a, sigma_s, phaseFunction_g: float = 0.0, density: float = 1.0):
-        self.sigma_a = _v3(sigma_a)
-        self.sigma_s = _v3(sigma_s)
-        self.g = float(phaseFunction_g)
-        self.density = float(density)
+    """HomogeneusMedium (Medium.hpp:14-61).  The ctor's products are kept in
+    float32 as glm computes them: sigma_a = d*sa, sigma_s = d*ss,
+    sigma_t = d*(sa + ss), Le = Le*LeDensity.  `phaseFunction` is a
+    HenyeyGreenstein or its g (the reference takes a shared_ptr<PhaseFunction>)."""
+
+    def __init__(self, sigma_a, sigma_s, phaseFunction=0.0, density: float = 1.0, Le=(0.0, 0.0, 0.0),
+                 LeDensity: float = 1.0):
+        self.sigma_a_in = _v3(sigma_a)
+        self.sigma_s_in = _v3(sigma_s)
+        self.phaseFunction = (phaseFunction if isinstance(phaseFunction, HenyeyGreenstein)
+                              else HenyeyGreenstein(float(phaseFunction)))
+        self.density = float(np.float32(density))
+        self.Le_in = _v3(Le)
+        self.LeDensity = float(np.float32(LeDensity))
+        d = np.float32(density)
+        self.sigma_a = (d * self.sigma_a_in).astype(np.float32)
+        self.sigma_s = (d * self.sigma_s_in).astype(np.float32)
+        self.sigma_t = (d * (self.sigma_a_in + self.sigma_s_in).astype(np.float32)).astype(np.float32)
+        self.emission = (self.Le_in * np.float32(LeDensity)).astype(np.float32)
+
+    @property
+    def g(self) -> float:
+        return self.phaseFunction.g
+
+    def Le(self) -> np.ndarray:
+        return self.emission
+
+    def IsEmmisive(self) -> bool:
+        return bool(np.any(self.emission != 0))
 
 
 # --------------------------------------------------------------------------
@@ -595,10 +627,18 @@ class Model(Primitive):
 class Scene:
     """Scene.hpp:5-37."""
 
-    def __init__(self):
+    def __init__(self, medium: Optional[HomogeneusMedium] = None):
         self.primitives: List[Primitive] = []
         self.infiniteLights: List[InfiniteLight] = []
+        self.sceneMedium = medium
         self.flat = None  # set by BuildTlas
+
+    def GetMedium(self) -> Optional[HomogeneusMedium]:
+        return self.sceneMedium
+
+    def SetMedium(self, medium: Optional[HomogeneusMedium]):
+        self.sceneMedium = medium
+        self.flat = None
 
     def Add(self, prim: Primitive):
         self.primitives.append(prim)
@@ -705,7 +745,9 @@ class Film:
 class Camera:
     """Camera.hpp:7-35.  The basis is built in float32 like the reference ctor."""
 
-    def __init__(self, lookFrom, lookAt, fov: float, film: Film, FocusAngle: float = 0.0, FocusDistance: float = 0.0):
+    def __init__(self, lookFrom, lookAt, fov: float, film: Film, FocusAngle: float = 0.0, FocusDistance: float = 0.0,
+                 medium: Optional[HomogeneusMedium] = None):
+        self.cameraMedium = medium
         self.lookFrom = _v3(lookFrom)
         self.lookAt = _v3(lookAt)
         self.fov = f32(fov)
@@ -726,3 +768,9 @@ class Camera:
 
     def GetFilm(self) -> Film:
         return self.film
+
+    def GetMedium(self) -> Optional[HomogeneusMedium]:
+        return self.cameraMedium
+
+    def SetMedium(self, medium: Optional[HomogeneusMedium]):
+        self.cameraMedium = medium

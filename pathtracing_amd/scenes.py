@@ -21,7 +21,8 @@ from typing import List, Optional
 import numpy as np
 
 from .scene import (AlphaMode, AlphaTester, AreaLight, Camera, CheckerTexture, DistantLight, Film,
-                    FunctionInfiniteLight, GeometricPrimitive, HomogeneusMedium, ImageTexture, Mesh,
+                    FunctionInfiniteLight, GeometricPrimitive, HenyeyGreenstein, HomogeneusMedium, ImageTexture,
+                    Mesh,
                     MicrofacetDielectric, MicrofacetDiffuse, MitchellFilter, Model, PointLight, PowerLightSampler,
                     QuadShape, Scene, SolidColor, SpecularConductor, SphereShape, ThinDielectric,
                     UniformInfiniteLight, UniformLightSampler)
@@ -31,7 +32,7 @@ from .scene import (AlphaMode, AlphaTester, AreaLight, Camera, CheckerTexture, D
 class SceneSetup:
     scene: Scene
     camera: Camera
-    integrator: str            # "path" | "simple"
+    integrator: str            # "path" | "simple" | "volpath"
     light_sampler: object
     max_depth: int
     seed: int
@@ -49,10 +50,12 @@ class SceneSetup:
         return self
 
     def make_integrator(self):
-        from .integrator import PathIntegrator, PCGSampler, SimplePathIntegrator
+        from .integrator import PathIntegrator, PCGSampler, SimplePathIntegrator, VolPathIntegrator
         sampler = PCGSampler(self.spp, self.seed)
         if self.integrator == "simple":
             return SimplePathIntegrator(self.scene, self.camera, sampler, self.max_depth)
+        if self.integrator == "volpath":
+            return VolPathIntegrator(self.scene, self.camera, sampler, self.light_sampler, self.max_depth)
         return PathIntegrator(self.scene, self.camera, sampler, self.light_sampler, self.max_depth)
 
 
@@ -129,17 +132,22 @@ def _box(center, size, angle):
 
 
 def cornell(W: int = 1024, H: int = 1024, spp: int = 256, config: str = "c2", max_depth: int = 8,
-            seed: Optional[int] = None) -> SceneSetup:
+            seed: Optional[int] = None, fog: bool = False) -> SceneSetup:
     """C2/C3 Cornell box: 5 walls + 2 boxes as one triangle Model (34 tris) and
     a quad area light under the ceiling.  C2: MicrofacetDiffuse(albedo)
     (roughness 1, metallic 0), SimplePathIntegrator.  C3: + rough glass sphere
     MicrofacetDielectric(1.5, 0.15), mirror SpecularConductor tall box,
     metallic MicrofacetDiffuse(metallic 1, rough 0.3) short box,
     PathIntegrator with UniformLightSampler.  maxDepth 8."""
-    c3 = config == "c3"
+    c3 = config == "c3" or fog
     if seed is None:
-        seed = 0x5EED0003 if c3 else 0x5EED0002
-    scene = Scene()
+        seed = 0x5EED0005 if fog else (0x5EED0003 if c3 else 0x5EED0002)
+    # fog: the C3 box filled with a thin forward-scattering medium (scene and
+    # camera medium, main.cpp:150-153, 264-266), an emissive medium inside the
+    # glass sphere (main.cpp:208) and a medium-only sphere boundary, lit also
+    # by a point light: VolPathIntegrator
+    fog_md = HomogeneusMedium((0.05, 0.05, 0.08), (0.6, 0.6, 0.5), HenyeyGreenstein(0.6), 0.35) if fog else None
+    scene = Scene(fog_md)
     white = MicrofacetDiffuse((0.73, 0.73, 0.73))
     red = MicrofacetDiffuse((0.65, 0.05, 0.05))
     green = MicrofacetDiffuse((0.12, 0.45, 0.15))
@@ -165,13 +173,23 @@ def cornell(W: int = 1024, H: int = 1024, spp: int = 256, config: str = "c2", ma
     scene.Add(Model(meshes))
     light = AreaLight(QuadShape((-0.25, 0.999, -0.25), (0.5, 0, 0), (0, 0, 0.5)), (17.0, 12.0, 4.0), False)
     scene.Add(GeometricPrimitive(light.getShape(), MicrofacetDiffuse((0.78, 0.78, 0.78)), light))
+    extra = []
     if c3:
+        inner = (HomogeneusMedium((0.2, 0.4, 0.6), (1.5, 1.0, 0.5), HenyeyGreenstein(-0.3), 2.0, (0.4, 0.6, 1.0), 1.5)
+                 if fog else None)
         scene.Add(GeometricPrimitive(SphereShape((0.35, 0.05, 0.35), 0.3),
-                                     MicrofacetDielectric(1.5, 0.15, (1, 1, 1))))
+                                     MicrofacetDielectric(1.5, 0.15, (1, 1, 1)), None, inner))
+    if fog:
+        # medium-only boundary: a sphere (a mesh without material would crash
+        # the reference's TriangleShape::Intersect, Shape.cpp:237-241)
+        dense = HomogeneusMedium((0.9, 0.3, 0.1), (2.0, 3.0, 4.0), 0.0, 1.0)
+        scene.Add(GeometricPrimitive(SphereShape((-0.55, 0.45, 0.45), 0.22), None, None, dense))
+        extra.append(PointLight((0.5, 0.6, 0.6), (0.8, 0.8, 1.2)))
     film = Film((W, H), MitchellFilter())
-    camera = Camera((0, 0, 3.7), (0, 0, 0), 0.75, film)
-    return SceneSetup(scene, camera, "path" if c3 else "simple", UniformLightSampler() if c3 else None, max_depth,
-                      seed, spp).finish()
+    camera = Camera((0, 0, 3.7), (0, 0, 0), 0.75, film, medium=fog_md)
+    kind = "volpath" if fog else ("path" if c3 else "simple")
+    ls = PowerLightSampler() if fog else (UniformLightSampler() if c3 else None)
+    return SceneSetup(scene, camera, kind, ls, max_depth, seed, spp, extra).finish()
 
 
 # --------------------------------------------------------------------------

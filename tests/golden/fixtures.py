@@ -29,6 +29,10 @@ def parity_scenes():
         "zoo": lambda: scenes.material_zoo(W=32, H=32, spp=4),
         "zoo_simple": lambda: scenes.material_zoo(W=24, H=24, spp=4, integrator="simple", seed=0x5EED0017),
         "heightfield": lambda: scenes.heightfield(n=70, W=24, H=24, spp=4),
+        # VolPathIntegrator: C1's medium sphere; the fog box (scene + camera
+        # medium, emissive medium in glass, medium-only mesh, point light)
+        "example1_volpath": lambda: scenes.example_1(W=32, H=32, spp=4, integrator="volpath", seed=0x5EED0021),
+        "fog": lambda: scenes.cornell(W=32, H=32, spp=4, fog=True),
         # C4 recipe at 0.3 % detail: every C4 feature (foliage masks, 58 textures,
         # ~2700 lights under the PowerLightSampler, sky + sun, depth 128)
         "sanmiguel": lambda: scenes.sanmiguel(W=32, H=18, spp=4, detail=0.003, tex_size=32),
