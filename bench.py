@@ -40,6 +40,11 @@ def build_setup(config: str, spp: int | None = None):
         return scenes.cornell(W=1024, H=1024, spp=spp or 256, config="c3")
     if config == "c4":
         return scenes.sanmiguel(W=1920, H=1080, spp=spp or 1024)
+    if config == "c1v":  # examples/example_1.cpp's VolPathIntegrator frame, at C2's size
+        return scenes.example_1(W=1024, H=1024, spp=spp or 256, integrator="volpath", max_depth=8,
+                                seed=0x5EED0021)
+    if config == "fog":  # C3 box in fog, VolPathIntegrator
+        return scenes.cornell(W=1024, H=1024, spp=spp or 256, fog=True)
     if config.startswith("hf"):  # heightfield probe, e.g. hf1000 = 2M triangles
         return scenes.heightfield(n=int(config[2:]), W=1024, H=1024, spp=spp or 16)
     raise ValueError(config)
@@ -50,6 +55,9 @@ WORKLOADS = {
     "c2": "C2 Cornell box (34 tris + quad light) 1024x1024 256spp depth 8 SimplePathIntegrator, Lambertian",
     "c3": "C3 Cornell box + GGX dielectric/conductor 1024x1024 256spp depth 8 PathIntegrator NEE+MIS+RR",
     "c4": "C4 San-Miguel-class procedural ~10M tris 1920x1080 1024spp depth 128 PathIntegrator",
+    "c1v": "C1 examples/example_1 scene (HG medium sphere) 1024x1024 256spp depth 8 VolPathIntegrator",
+    "fog": "C3 Cornell box in a homogeneous fog (scene+camera medium, emissive medium, point light) "
+           "1024x1024 256spp depth 8 VolPathIntegrator",
 }
 
 

@@ -25,7 +25,9 @@
 #include "Light.hpp"
 #include "LightSampler.hpp"
 #include "Material.hpp"
+#include "Medium.hpp"
 #include "Mesh.hpp"
+#include "PhaseFunction.hpp"
 #include "Primitive.hpp"
 #include "Scene.hpp"
 #include "Shape.hpp"
@@ -65,6 +67,12 @@ PT_MEMBER(GpShape, GeometricPrimitive, std::shared_ptr<Shape>, shape);
 PT_MEMBER(GpMaterial, GeometricPrimitive, std::shared_ptr<Material>, material);
 PT_MEMBER(GpArea, GeometricPrimitive, std::shared_ptr<AreaLight>, areaLight);
 PT_MEMBER(GpMedium, GeometricPrimitive, std::shared_ptr<Medium>, medium);
+PT_MEMBER(MedSigmaA, HomogeneusMedium, glm::vec3, sigma_a);
+PT_MEMBER(MedSigmaS, HomogeneusMedium, glm::vec3, sigma_s);
+PT_MEMBER(MedSigmaT, HomogeneusMedium, glm::vec3, sigma_t);
+PT_MEMBER(MedLe, HomogeneusMedium, glm::vec3, emmision);
+PT_MEMBER(MedPhase, HomogeneusMedium, std::shared_ptr<PhaseFunction>, phaseFunction);
+PT_MEMBER(HgG, HenyeyGreenstein, float, g);
 PT_MEMBER(SphCenter, SphereShape, glm::vec3, center);
 PT_MEMBER(SphRadius, SphereShape, float, radius);
 PT_MEMBER(QuadQ, QuadShape, glm::vec3, Q);
@@ -152,6 +160,30 @@ struct Flat {
     std::vector<pt_light> lights;
     std::vector<uint32_t> sampler_lights, infinite_lights;
     uint32_t light_sampler = PT_LS_UNIFORM;
+    std::vector<pt_medium> media;
+    int32_t scene_medium = -1;
+    std::unordered_map<const Medium*, int32_t> med_ids;
+
+    // HomogeneusMedium + HenyeyGreenstein (Medium.hpp:14-61, PhaseFunction.hpp:17-27)
+    int32_t medium(const std::shared_ptr<Medium>& m) {
+        if (!m) return -1;
+        auto it = med_ids.find(m.get());
+        if (it != med_ids.end()) return it->second;
+        auto* h = dynamic_cast<const HomogeneusMedium*>(m.get());
+        if (!h) throw std::runtime_error("HipVolPathIntegrator: unsupported medium type");
+        auto* hg = dynamic_cast<const HenyeyGreenstein*>(PT_GET(*h, MedPhase).get());
+        if (!hg) throw std::runtime_error("HipVolPathIntegrator: unsupported phase function");
+        pt_medium r{};
+        put3(r.sigma_a, PT_GET(*h, MedSigmaA));
+        put3(r.sigma_s, PT_GET(*h, MedSigmaS));
+        put3(r.sigma_t, PT_GET(*h, MedSigmaT));
+        put3(r.Le, PT_GET(*h, MedLe));
+        r.g = PT_GET(*hg, HgG);
+        const int32_t id = (int32_t)media.size();
+        media.push_back(r);
+        med_ids[m.get()] = id;
+        return id;
+    }
 
     std::unordered_map<const Mesh*, uint32_t> mesh_vbase, mesh_tbase;
     std::unordered_map<const Texture*, int32_t> tex_ids;
@@ -293,7 +325,7 @@ struct Flat {
             throw std::runtime_error("HipPathIntegrator: unsupported shape type");
         }
         p.material = material(PT_GET(gp, GpMaterial));
-        p.medium = -1;  // media: HipVolPathIntegrator (flattened below) only
+        p.medium = medium(PT_GET(gp, GpMedium));
         p.light = -1;
         if (const auto& al = PT_GET(gp, GpArea)) light_slot[al.get()] = (int32_t)slot;
     }
@@ -306,6 +338,7 @@ struct Flat {
         const auto& tnodes = PT_GET(*tlas, TlasNodes);
         static_assert(sizeof(BVH4_CLUSTER) == sizeof(pt_ref_bvh4_cluster), "cluster layout");
         const uint32_t n_top = (uint32_t)top.size();
+        scene_medium = medium(scene.GetMedium());
         // BLAS list in TLAS slot order
         std::vector<const BLAS4*> blas;
         std::vector<uint32_t> blas_of_slot(n_top, UINT32_MAX);
@@ -448,12 +481,14 @@ struct Flat {
         d.n_sampler_lights = (uint32_t)sampler_lights.size();
         d.infinite_lights = infinite_lights.data();
         d.n_infinite_lights = (uint32_t)infinite_lights.size();
-        d.scene_medium = -1;
+        d.media = media.data();
+        d.n_media = (uint32_t)media.size();
+        d.scene_medium = scene_medium;
         return d;
     }
 };
 
-pt_camera_desc camera_desc(const Camera& cam) {
+pt_camera_desc camera_desc(const Camera& cam, const Flat& flat) {
     pt_camera_desc c{};
     put3(c.origin, PT_GET(cam, CamFrom));
     put3(c.u, PT_GET(cam, CamU));
@@ -467,7 +502,10 @@ pt_camera_desc camera_desc(const Camera& cam) {
     glm::ivec2 res = cam.GetFilm()->Resolution();
     c.width = res.x;
     c.height = res.y;
-    c.medium = -1;
+    const auto m = cam.GetMedium();
+    if (m && !flat.med_ids.count(m.get()))
+        throw std::runtime_error("HipVolPathIntegrator: the camera's medium must be one the scene uses");
+    c.medium = m ? flat.med_ids.at(m.get()) : -1;
     return c;
 }
 
@@ -532,8 +570,12 @@ public:
         for (pt_ctx* c : ctx) pt_destroy(c);
     }
 
-    void ensure(const Scene& scene, const std::shared_ptr<LightSampler>& ls, unsigned n) {
-        if (ctx.empty()) flat.build(scene, ls);
+    void ensure(const Scene& scene, const std::shared_ptr<LightSampler>& ls, unsigned n,
+                const std::shared_ptr<Medium>& camera_medium = nullptr) {
+        if (ctx.empty()) {
+            flat.build(scene, ls);
+            flat.medium(camera_medium);
+        }
         int devices = 0;
         if (hipcount(&devices) != 0 || devices <= 0) throw std::runtime_error("HipPathIntegrator: no HIP device");
         const unsigned want = std::max(1u, std::min<unsigned>(n, (unsigned)devices));
@@ -548,7 +590,7 @@ public:
 
     // Renders shards 0..n-1 (one host thread per GPU) and merges into film.
     void render(const Camera& cam, uint32_t integrator, uint32_t spp, uint32_t depth, uint32_t seed, unsigned n) {
-        const pt_camera_desc cd = camera_desc(cam);
+        const pt_camera_desc cd = camera_desc(cam, flat);
         const auto film = cam.GetFilm();
         const glm::ivec2 res = film->Resolution();
         const size_t npx = (size_t)res.x * res.y;
@@ -643,6 +685,22 @@ void HipSimplePathIntegrator::Render(unsigned int n) const {
                 (unsigned)be_->ctx.size());
 }
 RenderStats HipSimplePathIntegrator::LastStats() const { return be_ ? be_->stats : RenderStats{}; }
+
+HipVolPathIntegrator::HipVolPathIntegrator(const std::shared_ptr<Scene>& scene, const std::shared_ptr<Camera>& camera,
+                                           const std::shared_ptr<Sampler>& sampler,
+                                           const std::shared_ptr<LightSampler>& lightSampler, uint32_t maxDepth)
+    : VolPathIntegrator(scene, camera, sampler, lightSampler, maxDepth), ls_(lightSampler), depth_(maxDepth) {}
+HipVolPathIntegrator::~HipVolPathIntegrator() = default;
+
+void HipVolPathIntegrator::Render(unsigned int n) const {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!be_) be_ = std::make_unique<HipBackend>();
+    be_->ensure(*scene, ls_, n, camera->GetMedium());
+    be_->render(*camera, PT_INTEGRATOR_VOLPATH, sampler->SamplesPerPixel(), depth_, seed_of(sampler),
+                (unsigned)be_->ctx.size());
+}
+RenderStats HipVolPathIntegrator::LastStats() const { return be_ ? be_->stats : RenderStats{}; }
+const std::vector<double>& HipVolPathIntegrator::LastAccumulation() const { return be_ ? be_->last : kEmpty; }
 const std::vector<double>& HipSimplePathIntegrator::LastAccumulation() const { return be_ ? be_->last : kEmpty; }
 
 }  // namespace pt

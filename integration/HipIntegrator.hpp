@@ -105,4 +105,25 @@ private:
     mutable std::mutex mu_;
 };
 
+// VolPathIntegrator (Integrators.hpp:56-67) on the GPU: HomogeneusMedium with a
+// HenyeyGreenstein phase function (scene, camera and primitive media).  The
+// medium's two hidden random_float() draws (Medium.hpp:28-30) come from the
+// PCG stream on the GPU.
+class HipVolPathIntegrator : public VolPathIntegrator {
+public:
+    HipVolPathIntegrator(const std::shared_ptr<Scene>& scene, const std::shared_ptr<Camera>& camera,
+                         const std::shared_ptr<Sampler>& sampler, const std::shared_ptr<LightSampler>& lightSampler,
+                         uint32_t maxDepth);
+    ~HipVolPathIntegrator() override;
+    void Render(unsigned int n = 1) const override;
+    RenderStats LastStats() const;
+    const std::vector<double>& LastAccumulation() const;
+
+private:
+    std::shared_ptr<LightSampler> ls_;
+    uint32_t depth_;
+    mutable std::unique_ptr<HipBackend> be_;
+    mutable std::mutex mu_;
+};
+
 }  // namespace pt

@@ -113,15 +113,12 @@ static DetSampler* g_stream = nullptr;
 // before the bounce's get2Dx4f()/get1D().  Tr, Le and the rest of Sample are
 // the reference's arithmetic; the scatter point is o + t*d with the products
 // fused (std::fma), the contract the oracle and the GPU path share.
-class StreamMedium : public Medium {
+class StreamMedium : public HomogeneusMedium {
 public:
     StreamMedium(const glm::vec3& sa, const glm::vec3& ss, std::shared_ptr<PhaseFunction> pf, float density,
                  const glm::vec3& Le, float LeDensity)
-        : sigma_a(density * sa), sigma_s(density * ss), sigma_t(density * (sa + ss)), emission(Le * LeDensity),
-          phase(std::move(pf)) {}
-    glm::vec3 Tr(const Ray&, float t) const override {
-        return glm::exp(-sigma_t * std::min(t, std::numeric_limits<float>::max()));
-    }
+        : HomogeneusMedium(sa, ss, pf, density, Le, LeDensity), sigma_s(density * ss),
+          sigma_t(density * (sa + ss)), phase(std::move(pf)) {}
     glm::vec3 Sample(const Ray& ray, float t, MediumInteraction& interaction) const override {
         const float u0 = g_stream ? (float)g_stream->get1D() : random_float();
         const float u1 = g_stream ? (float)g_stream->get1D() : random_float();
@@ -140,11 +137,9 @@ public:
         pdf /= 3.0;
         return sampledMedium ? (tr * sigma_s / pdf) : (tr / pdf);
     }
-    bool IsEmmisive() const override { return Le() != glm::vec3(0, 0, 0); }
-    glm::vec3 Le() const override { return emission; }
 
 private:
-    glm::vec3 sigma_a, sigma_s, sigma_t, emission;
+    glm::vec3 sigma_s, sigma_t;  // as the base's private members
     std::shared_ptr<PhaseFunction> phase;
 };
 
@@ -699,7 +694,8 @@ static void cmd_time(World& w, int threads, unsigned spp, const std::string& mod
 }
 
 #ifdef PT_WITH_HIP
-// --- hip: the drop-in pt::HipPathIntegrator / HipSimplePathIntegrator on the
+// --- hip: the drop-in pt::HipPathIntegrator / HipSimplePathIntegrator /
+// HipVolPathIntegrator on the
 // reference-built scene (integration/HipIntegrator.hpp), Render(gpus) into the
 // reference Film; dumps the merged accumulation like `film`.
 static void cmd_hip(World& w, const std::string& out, unsigned gpus) {
@@ -707,6 +703,10 @@ static void cmd_hip(World& w, const std::string& out, unsigned gpus) {
     std::vector<double> acc;
     if (w.integ == "simple") {
         pt::HipSimplePathIntegrator integ(w.scene, w.camera, sampler, w.maxDepth);
+        integ.Render(gpus);
+        acc = integ.LastAccumulation();
+    } else if (w.integ == "volpath") {
+        pt::HipVolPathIntegrator integ(w.scene, w.camera, sampler, w.ls, w.maxDepth);
         integ.Render(gpus);
         acc = integ.LastAccumulation();
     } else {
