@@ -292,6 +292,16 @@ pt_status pt_bsdf_cases(pt_ctx* ctx, int32_t material, const float* cases, uint3
  * n cases of 5 floats {uv[2], reference point[3]} -> n_lights*n records of
  * 18 floats {L[3], p[3], n[3], uv[2], dir[3], pdf, L(p)[3]}.  Host pointers. */
 pt_status pt_light_cases(pt_ctx* ctx, const float* cases, uint32_t n, float* out);
+/* Film resolve (Film::WritePNG / WritePPM, Film.hpp:154-217): per pixel
+ * color = sum RGB*w / sum w, the tone mapper (through the writers'
+ * std::function<vec3(vec3)>, i.e. in float around a double body),
+ * linear_to_sRGB (Texture.hpp:13-17) and 255.999*clamp(., 0, 1) truncated to
+ * u8.  rgb_out: width*height*3 bytes, row y = film row y (the PNG writer's
+ * buffer; the files are written bottom row first).  film_accum / rgb_out are
+ * host or device pointers (detected).  Needs a context, not a scene. */
+enum { PT_TONEMAP_REINHARD_JODIE = 0, PT_TONEMAP_ACES = 1 };
+pt_status pt_film_resolve(pt_ctx* ctx, const double* film_accum, int32_t width, int32_t height, uint32_t tonemap,
+                          uint8_t* rgb_out);
 /* Device bytes held by the uploaded scene. */
 uint64_t pt_scene_device_bytes(const pt_ctx* ctx);
 

@@ -43,8 +43,9 @@ def lib():
         L.oracle_bsdf.argtypes = [vp, C.c_int, vp, C.c_uint32, vp]
         L.oracle_lights.argtypes = [vp, vp, C.c_uint32, vp]
         L.oracle_filter_table.argtypes = [vp, vp]
+        L.oracle_resolve.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp]
         for f in ("oracle_trace", "oracle_li", "oracle_render", "oracle_bsdf", "oracle_lights",
-                  "oracle_filter_table"):
+                  "oracle_filter_table", "oracle_resolve"):
             getattr(L, f).restype = C.c_int
         _lib = L
     return _lib
@@ -103,6 +104,15 @@ def lights(flat, cases: np.ndarray) -> np.ndarray:
     cases = np.ascontiguousarray(cases, np.float32)
     out = np.zeros((flat.lights.shape[0] * cases.shape[0], 18), np.float32)
     assert lib().oracle_lights(_desc(flat), cases.ctypes.data, cases.shape[0], out.ctypes.data) == 0
+    return out
+
+
+def resolve(film: np.ndarray, tonemap: int = 0) -> np.ndarray:
+    """Film::WritePNG's u8 image (H, W, 3) of an accumulation (H, W, 4)."""
+    film = np.ascontiguousarray(film, np.float64)
+    H, W = film.shape[:2]
+    out = np.zeros((H, W, 3), np.uint8)
+    assert lib().oracle_resolve(film.ctypes.data, W, H, int(tonemap), out.ctypes.data) == 0
     return out
 
 

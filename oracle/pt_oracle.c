@@ -1753,6 +1753,42 @@ int oracle_render(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_re
  * FilmTile::Add at the absolute position. */
 
 /* ------------------------------------------------------------------ unit cases */
+/* Film::WritePNG's pixel body (Film.hpp:183-196): reinhard_jodie / ACESFilm
+ * (Film.hpp:34-47) through std::function<vec3(vec3)> (float in and out),
+ * linear_to_sRGB (Texture.hpp:13-17), 255.999 * clamp truncated to u8. */
+static double glm_clamp01(double x) {
+    double m = x < 0.0 ? 0.0 : x;
+    return 1.0 < m ? 1.0 : m;
+}
+static double linear_to_srgb(double v) {
+    v = glm_clamp01(v);
+    return v < 0.0031308 ? 12.92 * v : 1.055 * pow(v, 1.0 / 2.4) - 0.055;
+}
+int oracle_resolve(const double* film, int W, int H, int tonemap, uint8_t* out) {
+    for (size_t i = 0; i < (size_t)W * H; i++) {
+        const double* a = film + 4 * i;
+        double c[3], m[3];
+        for (int k = 0; k < 3; k++) c[k] = (double)(float)(a[k] / a[3]);
+        if (tonemap == 1) {
+            const double A = 2.51f, B = 0.03f, C = 2.43f, D = 0.59f, E = 0.14f;
+            for (int k = 0; k < 3; k++) m[k] = glm_clamp01((c[k] * (A * c[k] + B)) / (c[k] * (C * c[k] + D) + E));
+        } else {
+            double l = c[0] * 0.2126 + c[1] * 0.7152 + c[2] * 0.0722;
+            for (int k = 0; k < 3; k++) {
+                double t = c[k] / (1.0 + c[k]);
+                m[k] = (c[k] / (1.0 + l)) * (1.0 - t) + t * t;
+            }
+        }
+        for (int k = 0; k < 3; k++) {
+            double s = linear_to_srgb((double)(float)m[k]);
+            double lo = (s < 1.0) ? s : 1.0;  /* std::min(1.0, s) */
+            double v = (0.0 < lo) ? lo : 0.0; /* std::max(0.0, .) */
+            out[3 * i + k] = (uint8_t)(255.999 * v);
+        }
+    }
+    return 0;
+}
+
 int oracle_bsdf(const pt_scene_desc* s, int mid, const float* in, uint32_t n, float* out) {
     scene_t S;
     scene_init(&S, s);

@@ -50,6 +50,9 @@ int oracle_bsdf(const pt_scene_desc* s, int material, const float* in, uint32_t 
 /* Light cases, layout as ref_harness cmd_lights (5 floats in, 18 out per light per case). */
 int oracle_lights(const pt_scene_desc* s, const float* in, uint32_t n, float* out);
 
+/* Film::WritePNG tone map + sRGB + u8 of a W*H*4 accumulation (0 = reinhard_jodie, 1 = ACES). */
+int oracle_resolve(const double* film, int W, int H, int tonemap, uint8_t* out);
+
 /* Filter weight table (33x33 grid on [-2,2]^2 + integral), as ref_harness cmd_film. */
 int oracle_filter_table(const pt_render_desc* rd, double* out);
 

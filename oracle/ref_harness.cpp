@@ -693,6 +693,32 @@ static void cmd_time(World& w, int threads, unsigned spp, const std::string& mod
            rays / secs / 1e6);
 }
 
+// --- tonemap: Film::WritePNG's pixel loop (Film.hpp:183-196) over an
+// accumulation buffer {sum RGB*w, sum w} (W*H*4 doubles): the reference's own
+// reinhard_jodie / ACESFilm and linear_to_sRGB, through the writer's
+// std::function<glm::vec3(glm::vec3)>; u8 RGB rows in film order.
+static void cmd_tonemap(const std::string& out, const std::string& inPath, int W, int H) {
+    auto acc = rd<double>(inPath);
+    const std::function<glm::vec3(glm::vec3)> mappers[2] = {reinhard_jodie, ACESFilm};
+    for (int m = 0; m < 2; m++) {
+        const auto& toneMapper = mappers[m];
+        std::vector<uint8_t> img((size_t)W * H * 3);
+        for (int i = 0; i < H; i++)
+            for (int j = 0; j < W; j++) {
+                const double* px = &acc[((size_t)i * W + j) * 4];
+                glm::dvec3 color = glm::dvec3{px[0], px[1], px[2]} / px[3];
+                color = toneMapper(color);
+                double r = linear_to_sRGB(color.r);
+                double g = linear_to_sRGB(color.g);
+                double b = linear_to_sRGB(color.b);
+                img[((size_t)i * W + j) * 3 + 0] = 255.999 * std::max(0.0, std::min(1.0, r));
+                img[((size_t)i * W + j) * 3 + 1] = 255.999 * std::max(0.0, std::min(1.0, g));
+                img[((size_t)i * W + j) * 3 + 2] = 255.999 * std::max(0.0, std::min(1.0, b));
+            }
+        wr(out + (m == 0 ? ".ldr_jodie.bin" : ".ldr_aces.bin"), img);
+    }
+}
+
 #ifdef PT_WITH_HIP
 // --- hip: the drop-in pt::HipPathIntegrator / HipSimplePathIntegrator /
 // HipVolPathIntegrator on the
@@ -723,6 +749,11 @@ int main(int argc, char** argv) {
     if (argc < 4) {
         fprintf(stderr, "usage: ref_harness <recipe> <cmd> <out> [args]\n");
         return 2;
+    }
+    if (std::string(argv[1]) == "tonemap") {  // ref_harness tonemap <out> <film.bin> <W> <H>
+        if (argc < 6) return 2;
+        cmd_tonemap(argv[2], argv[3], atoi(argv[4]), atoi(argv[5]));
+        return 0;
     }
     std::cout.setstate(std::ios::failbit);  // silence the reference's progress/log prints
     World w;

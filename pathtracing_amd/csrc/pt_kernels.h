@@ -100,6 +100,7 @@ template <bool COUNT>
 __global__ void k_shadow_tr(PathSoA next, float* sample_L, const ShadowRec* sq, const uint32_t* nptr,
                             unsigned long long* counters);
 __global__ void k_fill(RenderParams R, uint32_t n, PathSoA next, uint32_t* cnt, unsigned long long* next_sample);
+__global__ void k_resolve(const double* film, uint32_t npx, uint32_t tonemap, uint8_t* rgb);
 __global__ void k_gather(RenderParams R, const float* sample_L, double* film);
 __global__ void k_interact(const pt_ray* rays, uint32_t n, float* out);
 __global__ void k_bsdf_cases(int mid, const float* in, uint32_t n, float* out);

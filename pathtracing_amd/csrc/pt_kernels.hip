@@ -1065,6 +1065,45 @@ __global__ __launch_bounds__(256) void k_gather(RenderParams R, const float* __r
     o[3] += acc[3];
 }
 
+// ------------------------------------------------------------------ film resolve
+// Film::WritePNG's per-pixel body (Film.hpp:183-196) with reinhard_jodie /
+// ACESFilm (Film.hpp:34-47) and linear_to_sRGB (Texture.hpp:13-17).  The
+// writers take the tone mapper as std::function<glm::vec3(glm::vec3)>, so the
+// color is rounded to float on the way in and on the way out.
+__device__ __forceinline__ double dmin_(double a, double b) { return b < a ? b : a; }  // std::min
+__device__ __forceinline__ double dmax_(double a, double b) { return a < b ? b : a; }  // std::max
+__device__ __forceinline__ double glm_clamp01(double x) {  // glm::clamp = min(max(x, 0), 1), NaN-propagating
+    const double m = x < 0.0 ? 0.0 : x;                     // glm::max(x, 0): (x < 0) ? 0 : x
+    return 1.0 < m ? 1.0 : m;                               // glm::min(m, 1): (1 < m) ? 1 : m
+}
+__device__ __forceinline__ double linear_to_srgb(double v) {
+    v = glm_clamp01(v);
+    return v < 0.0031308 ? 12.92 * v : 1.055 * pow(v, 1.0 / 2.4) - 0.055;
+}
+__global__ __launch_bounds__(256) void k_resolve(const double* __restrict__ film, uint32_t npx, uint32_t tonemap,
+                                                uint8_t* __restrict__ rgb) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= npx) return;
+    const double4 a = reinterpret_cast<const double4*>(film)[i];
+    // dvec3 / weight, then the std::function<vec3(vec3)> boundary
+    double c[3] = {(double)(float)(a.x / a.w), (double)(float)(a.y / a.w), (double)(float)(a.z / a.w)};
+    double m[3];
+    if (tonemap == PT_TONEMAP_ACES) {
+        const double A = 2.51f, B = 0.03f, C = 2.43f, D = 0.59f, E = 0.14f;
+        for (int k = 0; k < 3; k++) m[k] = glm_clamp01((c[k] * (A * c[k] + B)) / (c[k] * (C * c[k] + D) + E));
+    } else {
+        const double l = c[0] * 0.2126 + c[1] * 0.7152 + c[2] * 0.0722;  // luminance (Util.hpp:4-6)
+        for (int k = 0; k < 3; k++) {
+            const double t = c[k] / (1.0 + c[k]);
+            m[k] = (c[k] / (1.0 + l)) * (1.0 - t) + t * t;  // glm::mix(color/(1+l), t, t)
+        }
+    }
+    for (int k = 0; k < 3; k++) {
+        const double s = linear_to_srgb((double)(float)m[k]);
+        rgb[3ull * i + k] = (uint8_t)(255.999 * dmax_(0.0, dmin_(1.0, s)));
+    }
+}
+
 // explicit instantiations used by the runtime
 #define PT_INST_TRACE(B)                                                                                            \
     template __global__ void k_closest<B>(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*, uint32_t*,        \

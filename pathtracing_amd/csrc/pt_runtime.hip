@@ -834,6 +834,49 @@ extern "C" pt_status pt_render_samples(pt_ctx* c, const pt_camera_desc* cam, con
     return st;
 }
 
+extern "C" pt_status pt_film_resolve(pt_ctx* c, const double* film, int32_t width, int32_t height, uint32_t tonemap,
+                                     uint8_t* rgb) {
+    if (!c || !film || !rgb || width <= 0 || height <= 0 || (uint64_t)width * height > (1ull << 31) ||
+        tonemap > PT_TONEMAP_ACES)
+        return PT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint32_t npx = (uint32_t)width * (uint32_t)height;
+    const bool fdev = is_device_ptr(film), odev = is_device_ptr(rgb);
+    const double* df = film;
+    uint8_t* dout = rgb;
+    std::vector<void*> tmp;
+    auto cleanup = [&]() {
+        hipStreamSynchronize(c->stream);
+        for (void* p : tmp) hipFree(p);
+    };
+    if (!fdev) {
+        void* p = nullptr;
+        if (hipMalloc(&p, 32ull * npx) != hipSuccess) return fail(c, PT_ERR_OOM, "film resolve: device film");
+        tmp.push_back(p);
+        df = (const double*)p;
+        if (hipMemcpyAsync(p, film, 32ull * npx, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+            cleanup();
+            return fail(c, PT_ERR_HIP, "film resolve: upload");
+        }
+    }
+    if (!odev) {
+        void* p = nullptr;
+        if (hipMalloc(&p, 3ull * npx) != hipSuccess) {
+            cleanup();
+            return fail(c, PT_ERR_OOM, "film resolve: device image");
+        }
+        tmp.push_back(p);
+        dout = (uint8_t*)p;
+    }
+    hipLaunchKernelGGL(k_resolve, dim3((npx + 255) / 256), dim3(256), 0, c->stream, df, npx, tonemap, dout);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && !odev) e = hipMemcpyAsync(rgb, dout, 3ull * npx, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    cleanup();
+    if (e != hipSuccess) return fail(c, PT_ERR_HIP, "film resolve: %s", hipGetErrorString(e));
+    return PT_OK;
+}
+
 extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any_hit, pt_hit* hits, pt_stats* stats) {
     if (!c || (n && (!rays || !hits))) return PT_ERR_ARG;
     if (!c->has_scene) return fail(c, PT_ERR_STATE, "no scene uploaded");

@@ -23,6 +23,7 @@ PT_LIGHT_AREA, PT_LIGHT_UNIFORM_INF, PT_LIGHT_SKY_INF, PT_LIGHT_DISTANT, PT_LIGH
 PT_LS_UNIFORM, PT_LS_POWER = 0, 1
 PT_INTEGRATOR_PATH, PT_INTEGRATOR_SIMPLE, PT_INTEGRATOR_VOLPATH = 0, 1, 2
 PT_FILTER_MITCHELL, PT_FILTER_BOX, PT_FILTER_GAUSSIAN = 0, 1, 2
+PT_TONEMAP_REINHARD_JODIE, PT_TONEMAP_ACES = 0, 1
 PT_RENDER_COUNT_NODES = 0x1
 PT_RENDER_TIMING = 0x2
 PT_RENDER_TRAVERSAL_POOL = 0x4
@@ -112,7 +113,7 @@ class Stats(C.Structure):
 
 EXPORTS = [
     "pt_version", "pt_create", "pt_destroy", "pt_last_error", "pt_set_stream", "pt_scene_upload", "pt_render",
-    "pt_trace", "pt_scene_device_bytes", "pt_bvh4_build", "pt_bvh4_order_table",
+    "pt_trace", "pt_scene_device_bytes", "pt_bvh4_build", "pt_bvh4_order_table", "pt_film_resolve",
 ]
 
 _lib = None
@@ -146,6 +147,8 @@ def lib():
     L.pt_render.restype = C.c_int32
     L.pt_trace.argtypes = [vp, vp, C.c_uint32, C.c_int, vp, C.POINTER(Stats)]
     L.pt_trace.restype = C.c_int32
+    L.pt_film_resolve.argtypes = [vp, vp, C.c_int32, C.c_int32, C.c_uint32, vp]
+    L.pt_film_resolve.restype = C.c_int32
     L.pt_interact.argtypes = [vp, vp, C.c_uint32, vp]
     L.pt_interact.restype = C.c_int32
     L.pt_bsdf_cases.argtypes = [vp, C.c_int32, vp, C.c_uint32, vp]

@@ -728,18 +728,50 @@ class Film:
         with np.errstate(invalid="ignore", divide="ignore"):
             return np.where(w != 0, self.accum[..., :3] / w, 0.0)
 
-    def WritePPM(self, path: str):
-        """Film.hpp:154-170 (reinhard_jodie + sRGB, rows bottom-up)."""
-        rgb = self.image()
-        l = rgb @ np.array([0.2126, 0.7152, 0.0722])
-        t = rgb / (1.0 + rgb)
-        tm = (rgb / (1.0 + l[..., None])) * (1 - t) + t * t
-        tm = np.clip(tm, 0.0, 1.0)
-        s = np.where(tm < 0.0031308, 12.92 * tm, 1.055 * np.power(tm, 1.0 / 2.4) - 0.055)
-        out = (255.999 * np.clip(s, 0, 1)).astype(np.uint8)[::-1]
+    def Resolve(self, toneMapper: str = "reinhard_jodie", device: int = 0, accum=None) -> np.ndarray:
+        """The writers' 8-bit image (Film.hpp:154-217): tone map + linear_to_sRGB
+        + 255.999*clamp, on the GPU (pt_film_resolve).  Rows in film order
+        (y = 0 first); `accum` (a host array or a cuda float64 tensor) defaults
+        to this film's accumulator."""
+        import ctypes as C
+        from . import native as N
+        from .integrator import get_context
+        tm = {"reinhard_jodie": N.PT_TONEMAP_REINHARD_JODIE, "aces": N.PT_TONEMAP_ACES}[toneMapper]
+        src = self.accum if accum is None else accum
+        H, W = self.yResolution, self.xResolution
+        out = np.zeros((H, W, 3), np.uint8)
+        if hasattr(src, "data_ptr"):  # torch tensor (device film)
+            ptr = src.data_ptr()
+        else:
+            src = np.ascontiguousarray(src, np.float64)
+            ptr = src.ctypes.data
+        ctx = get_context(device)
+        N.check(N.lib().pt_film_resolve(ctx.ptr, C.c_void_p(ptr), W, H, tm, out.ctypes.data), ctx.ptr)
+        return out
+
+    def WritePPM(self, path: str, toneMapper: str = "reinhard_jodie"):
+        """Film::WritePPM (Film.hpp:154-170): binary P6, bottom row first."""
+        out = self.Resolve(toneMapper)[::-1]
         with open(path, "wb") as f:
             f.write(b"P6\n%d %d\n255\n" % (self.xResolution, self.yResolution))
-            f.write(out.tobytes())
+            f.write(np.ascontiguousarray(out).tobytes())
+
+    def WritePNG(self, path: str, toneMapper: str = "reinhard_jodie"):
+        """Film::WritePNG (Film.hpp:172-196): 8-bit RGB, flipped vertically on
+        write like stbi_flip_vertically_on_write(true).  Encoded with zlib
+        (the pixels, not the encoder's byte stream, are the contract)."""
+        import struct
+        import zlib
+        img = np.ascontiguousarray(self.Resolve(toneMapper)[::-1])
+        raw = b"".join(b"\x00" + img[y].tobytes() for y in range(img.shape[0]))
+
+        def chunk(t, d):
+            return struct.pack(">I", len(d)) + t + d + struct.pack(">I", zlib.crc32(t + d) & 0xFFFFFFFF)
+        with open(path, "wb") as f:
+            f.write(b"\x89PNG\r\n\x1a\n")
+            f.write(chunk(b"IHDR", struct.pack(">IIBBBBB", self.xResolution, self.yResolution, 8, 2, 0, 0, 0)))
+            f.write(chunk(b"IDAT", zlib.compress(raw, 6)))
+            f.write(chunk(b"IEND", b""))
 
 
 class Camera:

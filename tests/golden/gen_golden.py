@@ -165,6 +165,41 @@ def gen(name, setup, rng, tmp: Path):
           f"nonzero Li {(res['li_L'].sum(-1) > 0).mean():.2f}")
 
 
+def resolve_films(rng):
+    """Film accumulations the resolve fixture covers: the parity scenes'
+    reference films plus a synthetic HDR film with the edge cases (zero
+    weight, tiny / huge / negative radiance, the sRGB knee)."""
+    films = {}
+    for name in ("example1", "cornell_c3", "fog", "sanmiguel"):
+        films[name] = np.load(OUT / f"{name}.npz", allow_pickle=False)["film"]
+    H, W = 40, 48
+    rgb = np.exp(rng.uniform(np.log(1e-5), np.log(1e4), (H, W, 3)))
+    w = rng.uniform(0.5, 30.0, (H, W, 1))
+    syn = np.concatenate([rgb * w, w], -1)
+    syn[0, :4] = 0.0                                   # zero weight: 0/0
+    syn[1, :3, :3] = -syn[1, :3, :3]                   # negative radiance
+    syn[2, :3, :3] = syn[2, :3, 3:4] * 0.0031308       # at the sRGB knee
+    syn[3, :3, :3] = syn[3, :3, 3:4] * 1e30            # overflow in float
+    films["synthetic"] = syn
+    return films
+
+
+def gen_resolve(rng, tmp: Path):
+    """Film::WritePNG's tone map + sRGB + u8 (Film.hpp:183-196) by the
+    reference's own functions, for pt_film_resolve."""
+    res = {}
+    for name, film in resolve_films(rng).items():
+        H, W = film.shape[:2]
+        p = tmp / f"{name}.film.bin"
+        np.ascontiguousarray(film, np.float64).tofile(p)
+        harness("tonemap", tmp / name, p, W, H)
+        res[f"{name}_film"] = film
+        res[f"{name}_jodie"] = np.fromfile(f"{tmp / name}.ldr_jodie.bin", np.uint8).reshape(H, W, 3)
+        res[f"{name}_aces"] = np.fromfile(f"{tmp / name}.ldr_aces.bin", np.uint8).reshape(H, W, 3)
+    np.savez_compressed(OUT / "film_resolve.npz", **res)
+    print(f"film_resolve: {(OUT / 'film_resolve.npz').stat().st_size / 1024:.0f} KiB")
+
+
 def main(names=None):
     """All scenes share one rng stream (the committed round-1 fixtures); a
     scene regenerated alone (`gen_golden.py NAME...`) uses its own stream
@@ -179,6 +214,8 @@ def main(names=None):
                 continue
             r = np.random.default_rng([20261015, zlib.crc32(name.encode())]) if names else rng
             gen(name, make(), r, Path(t))
+        if not names or "film_resolve" in names:
+            gen_resolve(np.random.default_rng([20261016, 7]), Path(t))
 
 
 if __name__ == "__main__":

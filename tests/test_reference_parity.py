@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import oracle
-from fixtures import NAMES, load
+from fixtures import GOLDEN as GOLDEN_DIR, NAMES, load
 from pathtracing_amd.scene import AreaLight, DistantLight, FunctionInfiniteLight, PointLight, UniformInfiniteLight
 
 
@@ -179,3 +179,17 @@ def test_oracle_film_and_filter_match_reference(case):
     den = np.maximum(np.linalg.norm(ref[..., :3], axis=-1), 1e-3 * ref[..., 3])
     frac = (num <= 1e-3 * den + 1e-7).mean()
     assert frac >= 0.99, f"{name}: film pixels within 1e-3 rel L2: {frac:.4f}"
+
+
+# ---------------------------------------------------------------- film resolve (Film::WritePNG, Film.hpp:154-217)
+RESOLVE_FILMS = ("example1", "cornell_c3", "fog", "sanmiguel", "synthetic")
+
+
+@pytest.mark.parametrize("film", RESOLVE_FILMS)
+@pytest.mark.parametrize("tonemap,key", [(0, "jodie"), (1, "aces")])
+def test_oracle_resolve_matches_reference(film, tonemap, key):
+    """reinhard_jodie / ACESFilm + linear_to_sRGB + u8, bit for bit against the
+    reference's own functions (tests/golden/film_resolve.npz: parity films and
+    a synthetic film with zero weights, negative, knee and overflowing values)."""
+    fx = np.load(GOLDEN_DIR / "film_resolve.npz", allow_pickle=False)
+    np.testing.assert_array_equal(oracle.resolve(fx[f"{film}_film"], tonemap), fx[f"{film}_{key}"])
