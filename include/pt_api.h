@@ -61,6 +61,10 @@ typedef struct pt_ref_bvh4_cluster {
 pt_status pt_bvh4_build(const float* boxes, uint32_t n, pt_ref_bvh4_cluster* clusters, uint32_t* n_clusters,
                         pt_ref_bvh4_node* root, uint32_t* prim_order, float* bbox);
 
+/* glm::inverse(mat4) as the reference build computes TransformedPrimitive's
+ * invTransform (Primitive.hpp:37), host-side; column-major m[c*4+r]. */
+pt_status pt_mat4_inverse(const float* m, float* out);
+
 /* The octant traversal order byte for (ray-sign octant, perm) exactly as
  * BVH4::LUT / PermToIndexLUT (BVH.hpp:10-24, 562-718): 2-bit child slots,
  * most significant = nearest.  out: 8*135 bytes. */
@@ -69,20 +73,34 @@ pt_status pt_bvh4_order_table(uint8_t* out);
 /* ------------------------------------------------------------------------ */
 /* Flat scene                                                                */
 /* ------------------------------------------------------------------------ */
-enum { PT_PRIM_TRIANGLE = 0, PT_PRIM_QUAD = 1, PT_PRIM_SPHERE = 2, PT_PRIM_BLAS = 3 };
+enum { PT_PRIM_TRIANGLE = 0, PT_PRIM_QUAD = 1, PT_PRIM_SPHERE = 2, PT_PRIM_BLAS = 3, PT_PRIM_INSTANCE = 4 };
 
 /* One GeometricPrimitive (Primitive.hpp:17-31) or a nested BLAS (a Model,
  * Model.hpp:25-31), indexed by its global leaf-order slot. */
 typedef struct pt_prim {
     uint32_t kind;     /* PT_PRIM_*                                              */
     uint32_t index;    /* TRIANGLE: triangle id; QUAD: quad id; SPHERE: sphere id;
-                          BLAS: index into pt_scene_desc.bvhs                    */
+                          BLAS: index into pt_scene_desc.bvhs;
+                          INSTANCE: index into pt_scene_desc.instances (TLAS only) */
     int32_t material;  /* -1 = none: medium boundary, rays pass through         */
     int32_t light;     /* area light id or -1                                    */
     int32_t medium;    /* inside medium of the boundary (MediumInterface), or -1:
                           GeometricInteraction::getMedium (Interaction.hpp:26-29),
                           used by VolPath only                                     */
 } pt_prim;
+
+/* TransformedPrimitive / AnimatedPrimitive (Primitive.hpp:34-66): a BLAS
+ * (bvhs[bvh], a Model or a one-primitive BVH) under a glm::mat4 transform,
+ * column-major m[col][row], and its glm::inverse.  A hit inside the instance
+ * is reported as the virtual slot virt_base + (BLAS slot - prim_base); virtual
+ * slots start at n_prims and the instances' ranges are ascending.  One level:
+ * no instance inside an instance, no area light inside an instance. */
+typedef struct pt_instance {
+    float transform[16];
+    float inv[16];
+    uint32_t bvh;
+    uint32_t virt_base;
+} pt_instance;
 
 typedef struct pt_bvh_desc {
     const pt_ref_bvh4_cluster* clusters;
@@ -198,6 +216,9 @@ typedef struct pt_scene_desc {
     const pt_medium* media;
     uint32_t n_media;
     int32_t scene_medium;            /* Scene::GetMedium() (Scene.hpp:26), or -1 */
+    /* instances (TLAS slots of kind PT_PRIM_INSTANCE index it) */
+    const pt_instance* instances;
+    uint32_t n_instances;
 } pt_scene_desc;
 
 /* Camera (Camera.hpp:7-35) after its ctor. */

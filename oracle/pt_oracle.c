@@ -584,10 +584,88 @@ static int bvh_pred(const scene_t* S, const pt_bvh_desc* B, const ray_t* r, floa
     return 0;
 }
 
+/* ---- TransformedPrimitive (Primitive.cpp:42-72): glm mat4 (column-major
+ * m[c*4+r]) times vec4: (m0*x + m1*y) + (m2*z + m3*w), each product rounded
+ * (glm/detail/type_mat4x4.inl:561-572; the TLAS fixture confirms the form) */
+/* the reference build's contraction (fixture search on the instance traces):
+ * a0 = fma(m0, x, m1*y), a1 = fma(m2, z, m3*w), then a0 + a1 */
+static inline float m4_a0(float m0, float x, float m1, float y) { return fmaf(m0, x, rmul(m1, y)); }
+static inline float m4_a1(float m2, float z, float m3, float w) { return fmaf(m2, z, rmul(m3, w)); }
+static v3 m4_point(const float* m, v3 p) {
+    float o[3];
+    for (int r = 0; r < 3; r++) o[r] = m4_a0(m[r], p.x, m[4 + r], p.y) + m4_a1(m[8 + r], p.z, m[12 + r], 1.0f);
+    return V(o[0], o[1], o[2]);
+}
+static v3 m4_dir(const float* m, v3 v) {
+    float o[3];
+    for (int r = 0; r < 3; r++) o[r] = m4_a0(m[r], v.x, m[4 + r], v.y) + m4_a1(m[8 + r], v.z, m[12 + r], 0.0f);
+    return V(o[0], o[1], o[2]);
+}
+/* transpose(inverse(mat3(transform))) (glm compute_inverse<3,3>), NM[c*3+r] */
+static void normal_matrix(const float* T, float* NM) {
+#define M(c, r) T[(c) * 4 + (r)]
+#define DF(a, b, c, d) fmaf(a, b, -rmul(c, d)) /* the reference build's contraction */
+    const float D0 = DF(M(1, 1), M(2, 2), M(2, 1), M(1, 2)), D1 = DF(M(0, 1), M(2, 2), M(2, 1), M(0, 2));
+    const float D2 = DF(M(0, 1), M(1, 2), M(1, 1), M(0, 2));
+    /* as GCC contracts glm's determinant: fma(m20, D2, fma(m00, D0, -(m10*D1))) */
+    float od = 1.0f / fmaf(M(2, 0), D2, fmaf(M(0, 0), D0, -rmul(M(1, 0), D1)));
+    float inv[3][3];
+    inv[0][0] = +DF(M(1, 1), M(2, 2), M(2, 1), M(1, 2)) * od;
+    inv[1][0] = -DF(M(1, 0), M(2, 2), M(2, 0), M(1, 2)) * od;
+    inv[2][0] = +DF(M(1, 0), M(2, 1), M(2, 0), M(1, 1)) * od;
+    inv[0][1] = -DF(M(0, 1), M(2, 2), M(2, 1), M(0, 2)) * od;
+    inv[1][1] = +DF(M(0, 0), M(2, 2), M(2, 0), M(0, 2)) * od;
+    inv[2][1] = -DF(M(0, 0), M(2, 1), M(2, 0), M(0, 1)) * od;
+    inv[0][2] = +DF(M(0, 1), M(1, 2), M(1, 1), M(0, 2)) * od;
+    inv[1][2] = -DF(M(0, 0), M(1, 2), M(1, 0), M(0, 2)) * od;
+    inv[2][2] = +DF(M(0, 0), M(1, 1), M(1, 0), M(0, 1)) * od;
+#undef M
+#undef DF
+    for (int c = 0; c < 3; c++)
+        for (int r = 0; r < 3; r++) NM[c * 3 + r] = inv[r][c];
+}
+static inline float m3_row(float a, float x, float b, float y, float c, float z) {
+    return fmaf(c, z, fmaf(a, x, rmul(b, y))); /* as the reference build contracts it */
+}
+static v3 m3_mul(const float* M, v3 v) { /* glm mat3 * vec3 (type_mat3x3.inl:468-474) */
+    return V(m3_row(M[0], v.x, M[3], v.y, M[6], v.z), m3_row(M[1], v.x, M[4], v.y, M[7], v.z),
+             m3_row(M[2], v.x, M[5], v.y, M[8], v.z));
+}
+/* glm::normalize(vec4 with w = 0): v * (1 / sqrt((x*x + y*y) + (z*z + w*w))) */
+static v3 normalize4(v3 v) {
+    const float d = fmaf(v.y, v.y, rmul(v.x, v.x)) + rmul(v.z, v.z); /* fixture search */
+    return muls(v, 1.0f / sqrtf(d));
+}
+static ray_t instance_ray(const pt_instance* I, const ray_t* r, float* len) {
+    v3 dir = m4_dir(I->inv, r->d);
+    *len = length3(dir);
+    return mkray(m4_point(I->inv, r->o), divs(dir, *len));
+}
+
 /* GeometricPrimitive::Intersect (Primitive.cpp:15-26) / Model::Intersect (Model.hpp:25-27) */
 static int prim_intersect(const scene_t* S, uint32_t slot, const ray_t* r, float max, si_t* si, work_t* wk) {
     const pt_prim* p = &S->s->prims[slot];
     if (p->kind == PT_PRIM_BLAS) return bvh_intersect(S, &S->s->bvhs[p->index], r, &max, si, wk);
+    if (p->kind == PT_PRIM_INSTANCE) {
+        const pt_instance* I = &S->s->instances[p->index];
+        const pt_bvh_desc* B = &S->s->bvhs[I->bvh];
+        float len;
+        ray_t tr = instance_ray(I, r, &len);
+        float m = max * len;
+        si_t tmp;
+        memset(&tmp, 0, sizeof(tmp));
+        if (!bvh_intersect(S, B, &tr, &m, &tmp, wk)) return 0;
+        float NM[9];
+        normal_matrix(I->transform, NM);
+        *si = tmp;
+        si->p = m4_point(I->transform, tmp.p);
+        si->n = normalize(m3_mul(NM, tmp.n));
+        si->ns = normalize(m3_mul(NM, tmp.ns));
+        si->t = tmp.t / len;
+        si->tangent = normalize4(m4_dir(I->transform, tmp.tangent));
+        si->prim = (int)(I->virt_base + ((uint32_t)tmp.prim - B->prim_base));
+        return 1;
+    }
     si_t tmp;
     memset(&tmp, 0, sizeof(tmp));
     int hit;
@@ -608,6 +686,12 @@ static int prim_intersect(const scene_t* S, uint32_t slot, const ray_t* r, float
 static int prim_pred(const scene_t* S, uint32_t slot, const ray_t* r, float max, work_t* wk) {
     const pt_prim* p = &S->s->prims[slot];
     if (p->kind == PT_PRIM_BLAS) return bvh_pred(S, &S->s->bvhs[p->index], r, max, wk);
+    if (p->kind == PT_PRIM_INSTANCE) { /* TransformedPrimitive::IntersectPred (Primitive.cpp:42-47) */
+        const pt_instance* I = &S->s->instances[p->index];
+        float len;
+        ray_t tr = instance_ray(I, r, &len);
+        return bvh_pred(S, &S->s->bvhs[I->bvh], &tr, max * len, wk);
+    }
     wk->tris++;
     if (mat_has_alpha(S, p->material)) {
         si_t tmp;

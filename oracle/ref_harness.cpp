@@ -211,6 +211,13 @@ struct World {
 
 static std::shared_ptr<Texture> T(World& w, int id) { return id < 0 ? nullptr : w.tex.at(id); }
 
+static glm::mat4 read_mat4(std::istringstream& s) {  // 16 floats, glm column-major
+    glm::mat4 m;
+    for (int c = 0; c < 4; c++)
+        for (int r = 0; r < 4; r++) s >> m[c][r];
+    return m;
+}
+
 static void read_recipe(World& w, const std::string& path) {
     std::ifstream in(path);
     if (!in) { fprintf(stderr, "cannot open %s\n", path.c_str()); exit(2); }
@@ -292,9 +299,28 @@ static void read_recipe(World& w, const std::string& path) {
             if (ht) { tg.resize(nv); f.read((char*)tg.data(), tg.size() * 12); }
             w.mesh[id] = std::make_shared<Mesh>(idx, v, tg, n, uv, m < 0 ? nullptr : w.mat.at(m),
                                                 em < 0 ? nullptr : w.tex.at(em), md < 0 ? nullptr : w.med.at(md));
-        } else if (k == "model") {
+        } else if (k == "instance" || k == "animinstance") {
+            // TransformedPrimitive / AnimatedPrimitive over a defined BLAS
+            int pid, bid; s >> pid >> bid;
+            std::shared_ptr<Primitive> inner = w.blas.at(bid);
+            if (k == "instance") w.top.push_back(std::make_shared<TransformedPrimitive>(inner, read_mat4(s)));
+            else {
+                float dx, dy, dz, t0, t1; s >> dx >> dy >> dz >> t0 >> t1;
+                w.top.push_back(std::make_shared<AnimatedPrimitive>(inner, glm::vec3(dx, dy, dz), glm::vec2(t0, t1)));
+            }
+        } else if (k == "wrapprim") {
+            w.top.back() = std::make_shared<TransformedPrimitive>(w.top.back(), read_mat4(s));
+        } else if (k == "wrapanim") {
+            float dx, dy, dz, t0, t1; s >> dx >> dy >> dz >> t0 >> t1;
+            w.top.back() = std::make_shared<AnimatedPrimitive>(w.top.back(), glm::vec3(dx, dy, dz), glm::vec2(t0, t1));
+        } else if (k == "topblas") {
+            int pid, bid; s >> pid >> bid;
+            w.top.push_back(w.blas.at(bid));
+        } else if (k == "model" || k == "blasdef") {
             // Model::BuildBlas<BLAS4> (Model.hpp:43-60) without Assimp: one
             // GeometricPrimitive per triangle, an AreaLight per emissive one.
+            // blasdef: the BLAS of a model that is only instanced (not in the TLAS).
+            const bool top = k == "model";
             int pid, nm; s >> pid >> nm;
             std::vector<GeometricPrimitive> prims;
             std::vector<std::shared_ptr<Primitive>> ptrs;
@@ -320,8 +346,8 @@ static void read_recipe(World& w, const std::string& path) {
             w.blas.push_back(b);
             w.blasPtr.push_back(std::make_shared<PeekTLAS>(ptrs));
             w.blasItems.push_back(ptrs);
-            w.blasTop.push_back((int)w.top.size());
-            w.top.push_back(b);
+            w.blasTop.push_back(top ? (int)w.top.size() : -1);
+            if (top) w.top.push_back(b);
         } else if (k == "infinite") {
             std::string kind; s >> kind;
             if (kind == "uniform") {

@@ -379,3 +379,65 @@ extern "C" pt_status pt_bvh4_build(const float* boxes, uint32_t n, pt_ref_bvh4_c
     }
     return PT_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Instance matrices (host).  glm::inverse(mat4) (glm/detail/func_matrix.inl,
+// compute_inverse<4,4>) with glm's expression structure, compiled like the
+// reference (GNU dialect, FMA contraction) so that TransformedPrimitive's
+// invTransform (Primitive.hpp:37) comes out the same.  m, out: column-major
+// m[c*4+r].
+namespace {
+struct V4 {
+    float v[4];
+};
+inline V4 operator*(const V4& a, const V4& b) { return {{a.v[0] * b.v[0], a.v[1] * b.v[1], a.v[2] * b.v[2], a.v[3] * b.v[3]}}; }
+inline V4 operator-(const V4& a, const V4& b) { return {{a.v[0] - b.v[0], a.v[1] - b.v[1], a.v[2] - b.v[2], a.v[3] - b.v[3]}}; }
+inline V4 operator+(const V4& a, const V4& b) { return {{a.v[0] + b.v[0], a.v[1] + b.v[1], a.v[2] + b.v[2], a.v[3] + b.v[3]}}; }
+inline V4 operator*(const V4& a, float s) { return {{a.v[0] * s, a.v[1] * s, a.v[2] * s, a.v[3] * s}}; }
+}  // namespace
+
+extern "C" pt_status pt_mat4_inverse(const float* mm, float* out) {
+    if (!mm || !out) return PT_ERR_ARG;
+    float m[4][4];
+    for (int c = 0; c < 4; c++)
+        for (int r = 0; r < 4; r++) m[c][r] = mm[c * 4 + r];
+    const float Coef00 = m[2][2] * m[3][3] - m[3][2] * m[2][3];
+    const float Coef02 = m[1][2] * m[3][3] - m[3][2] * m[1][3];
+    const float Coef03 = m[1][2] * m[2][3] - m[2][2] * m[1][3];
+    const float Coef04 = m[2][1] * m[3][3] - m[3][1] * m[2][3];
+    const float Coef06 = m[1][1] * m[3][3] - m[3][1] * m[1][3];
+    const float Coef07 = m[1][1] * m[2][3] - m[2][1] * m[1][3];
+    const float Coef08 = m[2][1] * m[3][2] - m[3][1] * m[2][2];
+    const float Coef10 = m[1][1] * m[3][2] - m[3][1] * m[1][2];
+    const float Coef11 = m[1][1] * m[2][2] - m[2][1] * m[1][2];
+    const float Coef12 = m[2][0] * m[3][3] - m[3][0] * m[2][3];
+    const float Coef14 = m[1][0] * m[3][3] - m[3][0] * m[1][3];
+    const float Coef15 = m[1][0] * m[2][3] - m[2][0] * m[1][3];
+    const float Coef16 = m[2][0] * m[3][2] - m[3][0] * m[2][2];
+    const float Coef18 = m[1][0] * m[3][2] - m[3][0] * m[1][2];
+    const float Coef19 = m[1][0] * m[2][2] - m[2][0] * m[1][2];
+    const float Coef20 = m[2][0] * m[3][1] - m[3][0] * m[2][1];
+    const float Coef22 = m[1][0] * m[3][1] - m[3][0] * m[1][1];
+    const float Coef23 = m[1][0] * m[2][1] - m[2][0] * m[1][1];
+    const V4 Fac0{{Coef00, Coef00, Coef02, Coef03}}, Fac1{{Coef04, Coef04, Coef06, Coef07}};
+    const V4 Fac2{{Coef08, Coef08, Coef10, Coef11}}, Fac3{{Coef12, Coef12, Coef14, Coef15}};
+    const V4 Fac4{{Coef16, Coef16, Coef18, Coef19}}, Fac5{{Coef20, Coef20, Coef22, Coef23}};
+    const V4 Vec0{{m[1][0], m[0][0], m[0][0], m[0][0]}}, Vec1{{m[1][1], m[0][1], m[0][1], m[0][1]}};
+    const V4 Vec2{{m[1][2], m[0][2], m[0][2], m[0][2]}}, Vec3{{m[1][3], m[0][3], m[0][3], m[0][3]}};
+    const V4 Inv0 = Vec1 * Fac0 - Vec2 * Fac1 + Vec3 * Fac2;
+    const V4 Inv1 = Vec0 * Fac0 - Vec2 * Fac3 + Vec3 * Fac4;
+    const V4 Inv2 = Vec0 * Fac1 - Vec1 * Fac3 + Vec3 * Fac5;
+    const V4 Inv3 = Vec0 * Fac2 - Vec1 * Fac4 + Vec2 * Fac5;
+    const V4 SignA{{+1, -1, +1, -1}}, SignB{{-1, +1, -1, +1}};
+    const V4 I[4] = {Inv0 * SignA, Inv1 * SignB, Inv2 * SignA, Inv3 * SignB};
+    const V4 Row0{{I[0].v[0], I[1].v[0], I[2].v[0], I[3].v[0]}};
+    const V4 M0{{m[0][0], m[0][1], m[0][2], m[0][3]}};
+    const V4 Dot0 = M0 * Row0;
+    const float Dot1 = (Dot0.v[0] + Dot0.v[1]) + (Dot0.v[2] + Dot0.v[3]);
+    const float OneOverDeterminant = 1.0f / Dot1;
+    for (int c = 0; c < 4; c++) {
+        const V4 r = I[c] * OneOverDeterminant;
+        for (int k = 0; k < 4; k++) out[c * 4 + k] = r.v[k];
+    }
+    return PT_OK;
+}

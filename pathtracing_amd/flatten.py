@@ -19,6 +19,7 @@ import numpy as np
 from . import native as N
 from .scene import (AlphaMode, AreaLight, CheckerTexture, DistantLight, FunctionInfiniteLight, GeometricPrimitive,
                     ImageTexture, LightSampler, Material, MicrofacetDielectric, MicrofacetDiffuse, Model, PointLight,
+                    TransformedPrimitive, AnimatedPrimitive, mat4_identity, mat4_translate, _expand_seq,
                     PowerLightSampler, QuadShape, Scene, SolidColor, SpecularConductor, SphereShape, Texture,
                     ThinDielectric, UniformInfiniteLight, UniformLightSampler)
 
@@ -56,6 +57,7 @@ class FlatScene:
     sampler_lights: Optional[np.ndarray] = None
     infinite_lights: Optional[np.ndarray] = None
     light_objects: list = field(default_factory=list)
+    instances: Optional[np.ndarray] = None   # pt_instance records
     # participating media: id(HomogeneusMedium) -> index into `media`
     media: Optional[np.ndarray] = None
     medium_ids: Dict[int, int] = field(default_factory=dict)
@@ -123,6 +125,8 @@ class FlatScene:
         d.n_sampler_lights = self.sampler_lights.shape[0]
         d.infinite_lights = N.ptr(self.infinite_lights)
         d.n_infinite_lights = self.infinite_lights.shape[0]
+        d.instances = N.ptr(self.instances)
+        d.n_instances = 0 if self.instances is None else self.instances.shape[0]
         d.media = N.ptr(self.media)
         d.n_media = 0 if self.media is None else self.media.shape[0]
         d.scene_medium = self.scene_medium
@@ -218,14 +222,57 @@ def _stack(recs, dtype):
     return a
 
 
+def _fma32(a, b, c):
+    return (np.asarray(a, np.float64) * np.asarray(b, np.float64) + np.asarray(c, np.float64)).astype(np.float32)
+
+
+def mat4_mul_point(m: np.ndarray, p) -> np.ndarray:
+    """glm mat4 * vec4(p, 1) (glm/detail/type_mat4x4.inl:561-572) as the
+    reference build contracts it: fma(m0, x, m1*y) + fma(m2, z, m3*1)."""
+    f = np.float32
+    x, y, z = (f(v) for v in p)
+    a0 = _fma32(m[0], x, (m[1] * y).astype(f))
+    a1 = _fma32(m[2], z, m[3])
+    return (a0 + a1).astype(f)[:3]
+
+
+def instance_bbox(inner: np.ndarray, m: np.ndarray) -> np.ndarray:
+    """TransformedPrimitive::BoundingBox (Primitive.cpp:32-40): the 8 corners
+    (AABB::Corner, AABB.hpp:133-137) transformed and expanded in order."""
+    lo, hi = inner[:3], inner[3:]
+    pts = []
+    for i in range(8):
+        c = (lo[0] if not (i & 1) else hi[0], hi[1] if (i & 2) else lo[1], hi[2] if (i & 4) else lo[2])
+        pts.append(mat4_mul_point(m, c))
+    from .scene import _expand_seq
+    return _expand_seq(pts)
+
+
 def flatten_scene(scene: Scene) -> FlatScene:
     reg = _Registry()
     top = scene.primitives
     if not top:
         raise ValueError("empty scene")
 
-    # ---- models: BLAS over their triangles ----
-    models = [p for p in top if isinstance(p, Model)]
+    # ---- models: BLAS over their triangles (top-level and instanced, once each) ----
+    models, model_index = [], {}
+    for p in top:
+        m = p.primitive if isinstance(p, TransformedPrimitive) else p
+        if isinstance(m, Model) and id(m) not in model_index:
+            model_index[id(m)] = len(models)
+            models.append(m)
+        if isinstance(p, TransformedPrimitive):
+            if isinstance(m, Model) and m.tri_lights:
+                raise ValueError("emissive meshes inside an instance are not supported")
+            if isinstance(m, GeometricPrimitive) and m.areaLight is not None:
+                raise ValueError("area lights inside an instance are not supported")
+    # instanced GeometricPrimitives: a one-primitive BLAS each
+    gp_inst, gp_index = [], {}
+    for p in top:
+        if isinstance(p, TransformedPrimitive) and isinstance(p.primitive, GeometricPrimitive):
+            if id(p.primitive) not in gp_index:
+                gp_index[id(p.primitive)] = len(gp_inst)
+                gp_inst.append(p.primitive)
     pos, nrm, uvs, tan, vidx, tflags = [], [], [], [], [], []
     vbase = 0
     tri_base = 0
@@ -259,24 +306,34 @@ def flatten_scene(scene: Scene) -> FlatScene:
         model_tri_mat.append(np.concatenate(mats) if mats else np.zeros(0, np.int32))
         model_tri_med.append((meds, med_objs))
 
+    gp_blas = [N.bvh4_build(g.shape.bbox()[None]) for g in gp_inst]
+
     # ---- TLAS over top-level primitives ----
     quads, spheres = [], []
     top_boxes = np.zeros((len(top), 6), dtype=np.float32)
-    mi = 0
     model_of_top = {}
     for i, p in enumerate(top):
         if isinstance(p, Model):
-            top_boxes[i] = model_blas[mi][3]
-            model_of_top[i] = mi
-            mi += 1
+            top_boxes[i] = model_blas[model_index[id(p)]][3]
+            model_of_top[i] = model_index[id(p)]
         elif isinstance(p, GeometricPrimitive):
             top_boxes[i] = p.shape.bbox()
+        elif isinstance(p, TransformedPrimitive):
+            m = p.primitive
+            inner = model_blas[model_index[id(m)]][3] if isinstance(m, Model) else m.shape.bbox()
+            if isinstance(p, AnimatedPrimitive):
+                # AnimatedPrimitive::BoundingBox (Primitive.cpp:76-80): the box at
+                # rest expanded by the box translated by the whole direction
+                moved = instance_bbox(inner, mat4_translate(mat4_identity(), p.direction))
+                top_boxes[i] = _expand_seq([inner[:3], inner[3:], moved[:3], moved[3:]])
+            else:
+                top_boxes[i] = instance_bbox(inner, p.transform)
         else:
             raise TypeError(f"unsupported primitive {type(p).__name__}")
     tl_clusters, tl_root, tl_order, tl_bbox = N.bvh4_build(top_boxes)
 
     n_top = len(top)
-    n_blas_prims = sum(int(b[2].shape[0]) for b in model_blas)
+    n_blas_prims = sum(int(b[2].shape[0]) for b in model_blas) + len(gp_blas)
     prims = np.zeros(n_top + n_blas_prims, dtype=N.PRIM)
     prims["light"] = -1
     prims["medium"] = -1
@@ -286,13 +343,29 @@ def flatten_scene(scene: Scene) -> FlatScene:
     # BLAS slot ranges
     blas_base = []
     base = n_top
-    for b in model_blas:
+    for b in model_blas + gp_blas:
         blas_base.append(base)
         base += int(b[2].shape[0])
+    instances = []  # pt_instance records, TLAS slot order
+    virt_base = n_top + n_blas_prims
     # TLAS slots
     for slot in range(n_top):
         p = top[int(tl_order[slot])]
         rec = prims[slot]
+        if isinstance(p, TransformedPrimitive):
+            m = p.primitive
+            b = 1 + (model_index[id(m)] if isinstance(m, Model) else len(model_blas) + gp_index[id(m)])
+            ins = np.zeros(1, dtype=N.INSTANCE)[0]
+            ins["transform"] = p.transform.reshape(16)
+            ins["inv"] = p.invTransform.reshape(16)
+            ins["bvh"] = b
+            ins["virt_base"] = virt_base
+            virt_base += int((model_blas + gp_blas)[b - 1][2].shape[0])
+            rec["kind"] = N.PT_PRIM_INSTANCE
+            rec["index"] = len(instances)
+            rec["material"] = -1
+            instances.append(ins)
+            continue
         if isinstance(p, Model):
             k = model_of_top[int(tl_order[slot])]
             rec["kind"] = N.PT_PRIM_BLAS
@@ -337,14 +410,31 @@ def flatten_scene(scene: Scene) -> FlatScene:
         prims["index"][s0:s0 + n] = order + np.uint32(model_tri_base[k])
         prims["material"][s0:s0 + n] = model_tri_mat[k][order]
         model_tri_med[k] = (order, s0, n, model_tri_med[k])
-    for al in tlas_lights:
-        pass
+    # one-primitive BLASes of instanced GeometricPrimitives
+    for j, g in enumerate(gp_inst):
+        s0 = blas_base[len(model_blas) + j]
+        rec = prims[s0]
+        sh = g.shape
+        if isinstance(sh, QuadShape):
+            rec["kind"] = N.PT_PRIM_QUAD
+            rec["index"] = len(quads)
+            q = np.zeros(1, dtype=N.QUAD)[0]
+            q["Q"], q["u"], q["v"], q["normal"], q["D"], q["w"] = sh.Q, sh.u, sh.v, sh.normal, sh.D, sh.w
+            quads.append(q)
+        else:
+            rec["kind"] = N.PT_PRIM_SPHERE
+            rec["index"] = len(spheres)
+            s = np.zeros(1, dtype=N.SPHERE)[0]
+            s["center"], s["radius"] = sh.center, sh.radius
+            spheres.append(s)
+        rec["material"] = reg.material(g.material)
+        top_media.append((s0, g.medium))
     # emissive triangle lights: fill prim light ids later in bind_lights
 
-    clusters = [tl_clusters] + [b[0] for b in model_blas]
-    roots = [tl_root] + [b[1] for b in model_blas]
+    clusters = [tl_clusters] + [b[0] for b in model_blas + gp_blas]
+    roots = [tl_root] + [b[1] for b in model_blas + gp_blas]
     pbase = [0] + blas_base
-    npr = [n_top] + [int(b[2].shape[0]) for b in model_blas]
+    npr = [n_top] + [int(b[2].shape[0]) for b in model_blas + gp_blas]
 
     cat = lambda xs, shape, dt: (np.ascontiguousarray(np.concatenate(xs), dtype=dt) if xs
                                  else np.zeros(shape, dtype=dt))
@@ -362,6 +452,7 @@ def flatten_scene(scene: Scene) -> FlatScene:
         top_order=tl_order, blas_orders=[b[2] for b in model_blas], model_tri_base=model_tri_base,
         texture_ids=dict(reg.tex_ids))
     flat._reg = reg
+    flat.instances = _stack(instances, N.INSTANCE)
     # media: the scene's first, then primitives in slot order, then meshes
     flat.scene_medium = flat.medium_id(scene.GetMedium())
     for slot, md in top_media:

@@ -16,7 +16,7 @@ LIB_DIR = Path(__file__).resolve().parent / "_lib"
 LIB_PATH = Path(os.environ["PT_HIP_LIB"]) if os.environ.get("PT_HIP_LIB") else LIB_DIR / "libpt_hip.so"  # override: debugging builds
 
 PT_OK = 0
-PT_PRIM_TRIANGLE, PT_PRIM_QUAD, PT_PRIM_SPHERE, PT_PRIM_BLAS = 0, 1, 2, 3
+PT_PRIM_TRIANGLE, PT_PRIM_QUAD, PT_PRIM_SPHERE, PT_PRIM_BLAS, PT_PRIM_INSTANCE = 0, 1, 2, 3, 4
 PT_TEX_SOLID, PT_TEX_IMAGE, PT_TEX_CHECKER = 0, 1, 2
 PT_MAT_DIFFUSE, PT_MAT_DIELECTRIC, PT_MAT_THIN, PT_MAT_CONDUCTOR = 0, 1, 2, 3
 PT_LIGHT_AREA, PT_LIGHT_UNIFORM_INF, PT_LIGHT_SKY_INF, PT_LIGHT_DISTANT, PT_LIGHT_POINT = 0, 1, 2, 3, 4
@@ -45,6 +45,7 @@ MATERIAL = np.dtype([("kind", "<u4"), ("tex", "<i4"), ("norm", "<i4"), ("rough",
                      ("albedo", "<f4", 3)])
 LIGHT = np.dtype([("kind", "<u4"), ("prim", "<i4"), ("tex", "<i4"), ("one_sided", "<u4"), ("power", "<f4"),
                   ("pmf", "<f4"), ("color", "<f4", 3), ("vec", "<f4", 3), ("scale", "<f4")])
+INSTANCE = np.dtype([("transform", "<f4", 16), ("inv", "<f4", 16), ("bvh", "<u4"), ("virt_base", "<u4")])
 MEDIUM = np.dtype([("sigma_a", "<f4", 3), ("sigma_s", "<f4", 3), ("sigma_t", "<f4", 3), ("Le", "<f4", 3),
                    ("g", "<f4")])
 RAY = np.dtype([("o", "<f4", 3), ("d", "<f4", 3), ("tmax", "<f4")])
@@ -83,6 +84,7 @@ class SceneDesc(C.Structure):
         ("sampler_lights", C.c_void_p), ("n_sampler_lights", C.c_uint32),
         ("infinite_lights", C.c_void_p), ("n_infinite_lights", C.c_uint32),
         ("media", C.c_void_p), ("n_media", C.c_uint32), ("scene_medium", C.c_int32),
+        ("instances", C.c_void_p), ("n_instances", C.c_uint32),
     ]
 
 
@@ -114,6 +116,7 @@ class Stats(C.Structure):
 EXPORTS = [
     "pt_version", "pt_create", "pt_destroy", "pt_last_error", "pt_set_stream", "pt_scene_upload", "pt_render",
     "pt_trace", "pt_scene_device_bytes", "pt_bvh4_build", "pt_bvh4_order_table", "pt_film_resolve",
+    "pt_mat4_inverse",
 ]
 
 _lib = None
@@ -147,6 +150,8 @@ def lib():
     L.pt_render.restype = C.c_int32
     L.pt_trace.argtypes = [vp, vp, C.c_uint32, C.c_int, vp, C.POINTER(Stats)]
     L.pt_trace.restype = C.c_int32
+    L.pt_mat4_inverse.argtypes = [vp, vp]
+    L.pt_mat4_inverse.restype = C.c_int32
     L.pt_film_resolve.argtypes = [vp, vp, C.c_int32, C.c_int32, C.c_uint32, vp]
     L.pt_film_resolve.restype = C.c_int32
     L.pt_interact.argtypes = [vp, vp, C.c_uint32, vp]
@@ -163,6 +168,14 @@ def lib():
     L.pt_bvh4_order_table.restype = C.c_int32
     _lib = L
     return L
+
+
+def mat4_inverse(m: np.ndarray) -> np.ndarray:
+    """glm::inverse of a column-major float32 mat4 (host routine of libpt_hip)."""
+    m = np.ascontiguousarray(m, np.float32).reshape(4, 4)
+    out = np.zeros((4, 4), np.float32)
+    check(lib().pt_mat4_inverse(m.ctypes.data, out.ctypes.data))
+    return out
 
 
 def check(status: int, ctx=None):

@@ -10,7 +10,8 @@ from typing import Dict, List, Optional
 
 import numpy as np
 
-from .scene import (AreaLight, CheckerTexture, DistantLight, FunctionInfiniteLight, GeometricPrimitive, ImageTexture,
+from .scene import (AnimatedPrimitive, AreaLight, CheckerTexture, DistantLight, FunctionInfiniteLight,
+                    GeometricPrimitive, ImageTexture, TransformedPrimitive,
                     MicrofacetDielectric, MicrofacetDiffuse, Model, PointLight, PowerLightSampler, QuadShape,
                     SolidColor, SpecularConductor, SphereShape, ThinDielectric, UniformInfiniteLight)
 
@@ -119,11 +120,35 @@ def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: 
                      f"{1 if me.tangents is not None else 0} {m} {em} {md}")
         return i
 
+    blas_ids: Dict[int, int] = {}  # id(Model) -> BLAS index (model / blasdef line order)
+
+    def model_ids(p):
+        if p.override_material is not None or p.override_medium is not None:
+            raise ValueError("recipes do not carry Model material overrides")
+        return [mesh(me) for me in p.meshes]
+
     for k, p in enumerate(scene.primitives):
+        wrap = None
+        if isinstance(p, TransformedPrimitive):
+            m16 = " ".join(_f(x) for x in p.transform.reshape(16))
+            anim = (f"{' '.join(_f(x) for x in p.direction)} {_f(p.timeBounds[0])} {_f(p.timeBounds[1])}"
+                    if isinstance(p, AnimatedPrimitive) else None)
+            if isinstance(p.primitive, Model):
+                if id(p.primitive) not in blas_ids:
+                    ids = model_ids(p.primitive)
+                    blas_ids[id(p.primitive)] = len(blas_ids)
+                    lines.append(f"blasdef {blas_ids[id(p.primitive)]} {len(ids)} {' '.join(map(str, ids))}")
+                b = blas_ids[id(p.primitive)]
+                lines.append(f"animinstance {k} {b} {anim}" if anim else f"instance {k} {b} {m16}")
+                continue
+            wrap = f"wrapanim {anim}" if anim else f"wrapprim {m16}"
+            p = p.primitive
         if isinstance(p, Model):
-            if p.override_material is not None or p.override_medium is not None:
-                raise ValueError("recipes do not carry Model material overrides")
-            ids = [mesh(me) for me in p.meshes]
+            if id(p) in blas_ids:
+                lines.append(f"topblas {k} {blas_ids[id(p)]}")
+                continue
+            ids = model_ids(p)
+            blas_ids[id(p)] = len(blas_ids)
             lines.append(f"model {k} {len(ids)} {' '.join(map(str, ids))}")
         else:
             sh = p.shape
@@ -140,6 +165,8 @@ def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: 
                 lines.append(f"sphere {k} {g} {m} {em} {one} {md}")
             else:
                 raise TypeError(type(sh))
+            if wrap:
+                lines.append(wrap)
     for l in scene.infiniteLights:
         if isinstance(l, UniformInfiniteLight):
             lines.append(f"infinite uniform {' '.join(_f(x) for x in l.color)}")

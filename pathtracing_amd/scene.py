@@ -599,6 +599,121 @@ class GeometricPrimitive(Primitive):
         self.medium = medium
 
 
+# glm::mat4 helpers.  Matrices are float32 arrays m[col][row] (glm's layout);
+# the products are glm's, rounded per operation.
+def mat4_identity() -> np.ndarray:
+    return np.eye(4, dtype=np.float32)
+
+
+def mat4_translate(m, v) -> np.ndarray:
+    """glm::translate (glm/ext/matrix_transform.inl): m[3] = m0*v0 + m1*v1 + m2*v2 + m3."""
+    m = np.asarray(m, np.float32)
+    v = _v3(v)
+    r = m.copy()
+    r[3] = ((m[0] * v[0] + m[1] * v[1]).astype(np.float32) + (m[2] * v[2]).astype(np.float32)).astype(np.float32)
+    r[3] = (r[3] + m[3]).astype(np.float32)
+    return r
+
+
+def mat4_scale(m, v) -> np.ndarray:
+    m = np.asarray(m, np.float32)
+    v = _v3(v)
+    r = m.copy()
+    for i in range(3):
+        r[i] = (m[i] * v[i]).astype(np.float32)
+    return r
+
+
+def mat4_rotate(m, angle: float, axis) -> np.ndarray:
+    """glm::rotate(m, angle, axis) (glm/ext/matrix_transform.inl)."""
+    m = np.asarray(m, np.float32)
+    a = np.float32(angle)
+    c, s = np.float32(math.cos(a)), np.float32(math.sin(a))
+    ax = _v3(axis)
+    ax = (ax / np.float32(np.sqrt(np.float32(_dot(ax, ax))))).astype(np.float32)
+    t = ((np.float32(1) - c) * ax).astype(np.float32)
+    R = np.zeros((3, 3), np.float32)
+    R[0, 0] = c + t[0] * ax[0]
+    R[0, 1] = t[0] * ax[1] + s * ax[2]
+    R[0, 2] = t[0] * ax[2] - s * ax[1]
+    R[1, 0] = t[1] * ax[0] - s * ax[2]
+    R[1, 1] = c + t[1] * ax[1]
+    R[1, 2] = t[1] * ax[2] + s * ax[0]
+    R[2, 0] = t[2] * ax[0] + s * ax[1]
+    R[2, 1] = t[2] * ax[1] - s * ax[0]
+    R[2, 2] = c + t[2] * ax[2]
+    r = m.copy()
+    for i in range(3):
+        r[i] = ((m[0] * R[i, 0] + m[1] * R[i, 1]).astype(np.float32) + (m[2] * R[i, 2]).astype(np.float32))
+    return r.astype(np.float32)
+
+
+def mat4_inverse(m) -> np.ndarray:
+    """glm::inverse(mat4) (glm/detail/func_matrix.inl compute_inverse<4,4>),
+    float32 per operation."""
+    m = np.asarray(m, np.float32)
+    f = np.float32
+    def d(a, b, c, e):
+        return f(f(a * b) - f(c * e))
+    C00 = d(m[2][2], m[3][3], m[3][2], m[2][3]); C02 = d(m[1][2], m[3][3], m[3][2], m[1][3])
+    C03 = d(m[1][2], m[2][3], m[2][2], m[1][3]); C04 = d(m[2][1], m[3][3], m[3][1], m[2][3])
+    C06 = d(m[1][1], m[3][3], m[3][1], m[1][3]); C07 = d(m[1][1], m[2][3], m[2][1], m[1][3])
+    C08 = d(m[2][1], m[3][2], m[3][1], m[2][2]); C10 = d(m[1][1], m[3][2], m[3][1], m[1][2])
+    C11 = d(m[1][1], m[2][2], m[2][1], m[1][2]); C12 = d(m[2][0], m[3][3], m[3][0], m[2][3])
+    C14 = d(m[1][0], m[3][3], m[3][0], m[1][3]); C15 = d(m[1][0], m[2][3], m[2][0], m[1][3])
+    C16 = d(m[2][0], m[3][2], m[3][0], m[2][2]); C18 = d(m[1][0], m[3][2], m[3][0], m[1][2])
+    C19 = d(m[1][0], m[2][2], m[2][0], m[1][2]); C20 = d(m[2][0], m[3][1], m[3][0], m[2][1])
+    C22 = d(m[1][0], m[3][1], m[3][0], m[1][1]); C23 = d(m[1][0], m[2][1], m[2][0], m[1][1])
+    F = [np.array(x, np.float32) for x in ([C00, C00, C02, C03], [C04, C04, C06, C07], [C08, C08, C10, C11],
+                                          [C12, C12, C14, C15], [C16, C16, C18, C19], [C20, C20, C22, C23])]
+    V = [np.array([m[1][k], m[0][k], m[0][k], m[0][k]], np.float32) for k in range(4)]
+    def comb(a, fa, b, fb, c, fc):
+        return (((a * fa).astype(f) - (b * fb).astype(f)).astype(f) + (c * fc).astype(f)).astype(f)
+    I0 = comb(V[1], F[0], V[2], F[1], V[3], F[2])
+    I1 = comb(V[0], F[0], V[2], F[3], V[3], F[4])
+    I2 = comb(V[0], F[1], V[1], F[3], V[3], F[5])
+    I3 = comb(V[0], F[2], V[1], F[4], V[2], F[5])
+    SA = np.array([1, -1, 1, -1], np.float32)
+    SB = -SA
+    inv = np.stack([I0 * SA, I1 * SB, I2 * SA, I3 * SB]).astype(np.float32)
+    row0 = np.array([inv[0][0], inv[1][0], inv[2][0], inv[3][0]], np.float32)
+    dot0 = (m[0] * row0).astype(np.float32)
+    det = f(f(dot0[0] + dot0[1]) + f(dot0[2] + dot0[3]))
+    return (inv * f(f(1) / det)).astype(np.float32)
+
+
+class TransformedPrimitive(Primitive):
+    """TransformedPrimitive (Primitive.hpp:34-48, Primitive.cpp:32-72): an
+    instance of a Model (BLAS) or of a GeometricPrimitive under an affine
+    glm::mat4 (float32 [col][row]).  Rays are taken to object space with the
+    inverse, the hit back with the transform and its normal matrix."""
+
+    def __init__(self, primitive: Primitive, transform):
+        if not isinstance(primitive, (Model, GeometricPrimitive)):
+            raise TypeError("instances of a Model or a GeometricPrimitive only (no nested instances)")
+        self.primitive = primitive
+        self.transform = np.ascontiguousarray(transform, np.float32).reshape(4, 4)
+        # glm::inverse as the reference build contracts it: the native host
+        # routine (pt_mat4_inverse, compiled like the reference); mat4_inverse
+        # is its per-operation-rounded twin
+        from . import native as N
+        self.invTransform = N.mat4_inverse(self.transform)
+
+
+class AnimatedPrimitive(TransformedPrimitive):
+    """AnimatedPrimitive (Primitive.hpp:52-66, Primitive.cpp:76-96): a
+    translation by direction * t, t = clamp(time - t0, t0, t1) / (t1 - t0).
+    Camera rays carry time 0 (the reference's shutter is uninitialised, SURVEY
+    A.14), so the instance is the translation at time 0."""
+
+    def __init__(self, primitive: Primitive, direction, timeBounds):
+        self.direction = _v3(direction)
+        self.timeBounds = np.asarray(timeBounds, np.float32).reshape(2)
+        t0, t1 = self.timeBounds
+        t = f32(f32(np.clip(f32(f32(0.0) - t0), t0, t1)) / f32(t1 - t0))
+        super().__init__(primitive, mat4_translate(mat4_identity(), (self.direction * t).astype(np.float32)))
+
+
 class Model(Primitive):
     """A BLAS4 over meshes: Model::BuildBlas<BLAS4> (Model.hpp:43-60) without Assimp.
     Emissive meshes get one AreaLight per triangle, culled if Power <= FLT_EPSILON."""

@@ -639,3 +639,69 @@ CONFIGS = {
     "c3": lambda **kw: cornell(config="c3", **kw),
     "c4": lambda **kw: sanmiguel(**kw),
 }
+
+
+# --------------------------------------------------------------------------
+def _uv_sphere(nu: int, nv: int, tangents: bool = True):
+    """A smooth-shaded sphere mesh (unit radius) with uvs and tangents."""
+    th = np.linspace(0, np.pi, nv + 1)
+    ph = np.linspace(0, 2 * np.pi, nu + 1)
+    T, P = np.meshgrid(th, ph, indexing="ij")
+    n = np.stack([np.sin(T) * np.cos(P), np.cos(T), np.sin(T) * np.sin(P)], -1).reshape(-1, 3)
+    v = (n * np.array([1.0, 0.8, 1.0])).astype(np.float32)  # squashed: the normal matrix matters
+    uv = np.stack([P / (2 * np.pi), T / np.pi], -1).reshape(-1, 2).astype(np.float32)
+    i = np.arange((nv + 1) * (nu + 1)).reshape(nv + 1, nu + 1)
+    a, b, c, d = i[:-1, :-1], i[:-1, 1:], i[1:, 1:], i[1:, :-1]
+    idx = np.stack([a, b, c, a, c, d], -1).reshape(-1).astype(np.uint32)
+    nrm = (n / np.linalg.norm(n, axis=1, keepdims=True)).astype(np.float32)
+    t = None
+    if tangents:
+        t = np.stack([-np.sin(P), np.zeros_like(P), np.cos(P)], -1).reshape(-1, 3).astype(np.float32)
+    return idx, v, t, nrm, uv
+
+
+def instances(W: int = 1024, H: int = 1024, spp: int = 256, max_depth: int = 8,
+              seed: int = 0x5EED0006) -> SceneSetup:
+    """Instancing (§8f): the C2 room (a top-level Model) with one glossy model
+    (a squashed smooth sphere mesh with tangents and a normal-mapped checker)
+    instanced three times under rotate / scale / translate
+    (TransformedPrimitive), a glass sphere and a metal quad as instanced
+    GeometricPrimitives, and an AnimatedPrimitive sphere (main.cpp:186-190);
+    PathIntegrator, PowerLightSampler."""
+    from .scene import (AnimatedPrimitive, TransformedPrimitive, mat4_identity, mat4_rotate, mat4_scale,
+                        mat4_translate)
+    scene = Scene()
+    white = MicrofacetDiffuse((0.73, 0.73, 0.73))
+    red = MicrofacetDiffuse((0.65, 0.05, 0.05))
+    green = MicrofacetDiffuse((0.12, 0.45, 0.15))
+    walls = [
+        (_quad_tris((-1, -1, 1), (1, -1, 1), (1, -1, -1), (-1, -1, -1)), white),
+        (_quad_tris((-1, 1, -1), (1, 1, -1), (1, 1, 1), (-1, 1, 1)), white),
+        (_quad_tris((-1, -1, -1), (1, -1, -1), (1, 1, -1), (-1, 1, -1)), white),
+        (_quad_tris((-1, -1, 1), (-1, -1, -1), (-1, 1, -1), (-1, 1, 1)), red),
+        (_quad_tris((1, -1, -1), (1, -1, 1), (1, 1, 1), (1, 1, -1)), green),
+    ]
+    scene.Add(Model([Mesh(i, v, None, n, uv, m) for (i, v, n, uv), m in walls]))
+    light = AreaLight(QuadShape((-0.25, 0.999, -0.25), (0.5, 0, 0), (0, 0, 0.5)), (17.0, 12.0, 4.0), False)
+    scene.Add(GeometricPrimitive(light.getShape(), MicrofacetDiffuse((0.78, 0.78, 0.78)), light))
+    idx, v, t, n, uv = _uv_sphere(24, 12)
+    glossy = MicrofacetDiffuse(CheckerTexture(SolidColor((0.9, 0.6, 0.2)), SolidColor((0.2, 0.3, 0.8)), (0.125, 0.25)),
+                               None, SolidColor((0.35, 0.35, 0.35)), SolidColor((0.0, 0.0, 0.0)))
+    rock = Model([Mesh(idx, v, t, n, uv, glossy)])
+    placements = [((-0.5, -0.72, -0.3), 0.6, (0, 1, 0), (0.28, 0.28, 0.28)),
+                  ((0.45, -0.6, 0.2), -0.9, (1, 1, 0), (0.25, 0.4, 0.25)),
+                  ((0.0, 0.1, -0.5), 1.7, (0, 0, 1), (0.35, 0.2, 0.2))]
+    for pos, ang, ax, sc in placements:
+        m = mat4_scale(mat4_rotate(mat4_translate(mat4_identity(), pos), ang, ax), sc)
+        scene.Add(TransformedPrimitive(rock, m))
+    glass = GeometricPrimitive(SphereShape((0, 0, 0), 1.0), MicrofacetDielectric(1.5, 0.05, (1, 1, 1)))
+    scene.Add(TransformedPrimitive(glass, mat4_scale(mat4_translate(mat4_identity(), (-0.45, -0.1, 0.45)),
+                                                      (0.22, 0.22, 0.22))))
+    plate = GeometricPrimitive(QuadShape((-0.5, 0, -0.5), (1, 0, 0), (0, 0, 1)), SpecularConductor((0.9, 0.85, 0.8)))
+    scene.Add(TransformedPrimitive(plate, mat4_rotate(mat4_scale(mat4_translate(mat4_identity(), (0.55, 0.3, -0.6)),
+                                                                  (0.5, 1, 0.5)), 1.1, (1, 0, 0.3))))
+    ball = GeometricPrimitive(SphereShape((0.3, -0.85, 0.55), 0.15), MicrofacetDiffuse((0.1, 0.2, 0.5)))
+    scene.Add(AnimatedPrimitive(ball, (0, 0.2, 0), (0.25, 1.0)))
+    film = Film((W, H), MitchellFilter())
+    camera = Camera((0, 0, 3.7), (0, 0, 0), 0.75, film)
+    return SceneSetup(scene, camera, "path", PowerLightSampler(), max_depth, seed, spp).finish()

@@ -33,6 +33,9 @@ def parity_scenes():
         # medium, emissive medium in glass, medium-only mesh, point light)
         "example1_volpath": lambda: scenes.example_1(W=32, H=32, spp=4, integrator="volpath", seed=0x5EED0021),
         "fog": lambda: scenes.cornell(W=32, H=32, spp=4, fog=True),
+        # instancing: one model three times, instanced glass sphere / metal
+        # quad, an AnimatedPrimitive (TransformedPrimitive, Primitive.cpp:32-96)
+        "instances": lambda: scenes.instances(W=32, H=32, spp=4),
         # C4 recipe at 0.3 % detail: every C4 feature (foliage masks, 58 textures,
         # ~2700 lights under the PowerLightSampler, sky + sun, depth 128)
         "sanmiguel": lambda: scenes.sanmiguel(W=32, H=18, spp=4, detail=0.003, tex_size=32),

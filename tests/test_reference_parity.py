@@ -43,7 +43,11 @@ def test_bvh4_build_is_byte_identical(case):
         assert _bytes(flat.bvh_roots[1 + k], 8) == _bytes(fx[f"blas{k}_root"], 8), f"BLAS{k} root"
         np.testing.assert_array_equal(flat.blas_orders[k], fx[f"blas{k}_order"])
         k += 1
-    assert k == len(flat.bvh_clusters) - 1
+    # the rest: the one-primitive BVHs of instanced GeometricPrimitives (the
+    # reference instances the primitive itself, no BVH)
+    assert all(n == 1 for n in flat.bvh_n_prims[1 + k:])
+    assert k + sum(1 for ins in (flat.instances if flat.instances is not None else [])
+                   if int(ins["bvh"]) > k) >= len(flat.bvh_clusters) - 1
 
 
 # ---------------------------------------------------------------- lights (F4)
