@@ -642,7 +642,7 @@ CONFIGS = {
 
 
 # --------------------------------------------------------------------------
-def _uv_sphere(nu: int, nv: int, tangents: bool = True):
+def _smooth_sphere(nu: int, nv: int, tangents: bool = True):
     """A smooth-shaded sphere mesh (unit radius) with uvs and tangents."""
     th = np.linspace(0, np.pi, nv + 1)
     ph = np.linspace(0, 2 * np.pi, nu + 1)
@@ -684,7 +684,7 @@ def instances(W: int = 1024, H: int = 1024, spp: int = 256, max_depth: int = 8,
     scene.Add(Model([Mesh(i, v, None, n, uv, m) for (i, v, n, uv), m in walls]))
     light = AreaLight(QuadShape((-0.25, 0.999, -0.25), (0.5, 0, 0), (0, 0, 0.5)), (17.0, 12.0, 4.0), False)
     scene.Add(GeometricPrimitive(light.getShape(), MicrofacetDiffuse((0.78, 0.78, 0.78)), light))
-    idx, v, t, n, uv = _uv_sphere(24, 12)
+    idx, v, t, n, uv = _smooth_sphere(24, 12)
     glossy = MicrofacetDiffuse(CheckerTexture(SolidColor((0.9, 0.6, 0.2)), SolidColor((0.2, 0.3, 0.8)), (0.125, 0.25)),
                                None, SolidColor((0.35, 0.35, 0.35)), SolidColor((0.0, 0.0, 0.0)))
     rock = Model([Mesh(idx, v, t, n, uv, glossy)])
