@@ -36,6 +36,28 @@ struct alignas(16) DevGeom {
     float4 a, b, c;
 };
 
+// Instances (TransformedPrimitive, Primitive.cpp:32-72).  A TLAS leaf slot of
+// an instance is encoded like a BLAS hop whose pushed ref is
+// REF_INST_ENTER | slot; popping it takes the lane's ray to object space
+// (state saved in a per-lane scratch row) and pushes REF_INST_EXIT, which
+// restores the world ray when the instance's BLAS is done.  Node refs stay
+// below REF_LEAF and leaf slots below 2^30, so refs >= REF_SPECIAL are free.
+#define REF_SPECIAL 0xC0000000u
+#define REF_INST_ENTER 0xC0000000u
+#define REF_INST_EXIT 0xFFFFFFFEu
+#define REF_SLOT_MASK 0x3FFFFFFFu
+#define OCT_MASK 7u
+#define OCT_INST 8u   // the lane's ray is in an instance's object space
+#define OCT_HIT 16u   // ... and accepted a hit there
+#define SCR_WORDS 9   // scratch row: world o, d, tmax, length, instance
+struct DevInstance {
+    float T[16], inv[16];  // glm column-major transform and inverse
+    uint32_t root;         // BLAS root ref
+    uint32_t prim_base;    // first slot of the BLAS
+    uint32_t n_prims;
+    uint32_t virt_base;    // virtual slot of the BLAS's first primitive
+};
+
 struct DevPrimInfo {
     int32_t material, light, medium;
     uint32_t index;  // triangle / quad / sphere id, BLAS root ref
@@ -72,6 +94,10 @@ struct DevScene {
     const pt_medium* media;
     uint32_t n_media;
     int32_t scene_medium;
+    const DevInstance* instances;
+    uint32_t n_instances;
+    uint32_t* scratch;       // SCR_WORDS x scratch_lanes (instance traversal state)
+    uint32_t scratch_lanes;
 };
 
 // The uploaded scene of the current context, in constant memory: every

@@ -79,16 +79,16 @@ struct RenderParams {
     double gauss_x, gauss_y;
 };
 
-template <bool COUNT>
+template <bool COUNT, bool INST>
 __global__ void k_closest(PathSoA P, const uint32_t* in, float4* hit, uint32_t* pool, uint32_t* ovf, uint32_t* spare,
                           uint32_t* snap, unsigned long long* counters);
-template <bool COUNT>
+template <bool COUNT, bool INST>
 __global__ void k_closest_pool(PathSoA P, const uint32_t* in, float4* hit, uint32_t* pool, uint32_t* ovf,
                                uint32_t* spare, uint32_t* snap, unsigned long long* counters);
-template <bool COUNT>
+template <bool COUNT, bool INST>
 __global__ void k_shadow(PathSoA next, float* sample_L, const ShadowRec* sq, const uint32_t* nptr, uint32_t* pool,
                          uint32_t* ovf, unsigned long long* counters);
-template <bool COUNT>
+template <bool COUNT, bool INST>
 __global__ void k_shadow_pool(PathSoA next, float* sample_L, const ShadowRec* sq, const uint32_t* nptr,
                               uint32_t* pool, uint32_t* ovf, unsigned long long* counters);
 template <int INTEGRATOR>

@@ -78,6 +78,59 @@ __device__ __forceinline__ void iteration_prologue(const uint32_t* __restrict__ 
     }
 }
 
+// SurfaceInteraction of a closest hit (Shape.cpp:58-244 via
+// GeometricPrimitive::Intersect, Primitive.cpp:15-26): prim slot (or virtual
+// slot of an instance), t and barycentrics / quad coordinates from the
+// traversal.  Instance hits (TransformedPrimitive::Intersect,
+// Primitive.cpp:48-64): the object-space ray is rebuilt, the primitive test
+// re-run for t (the traversal kept the world t) and the object-space
+// interaction carried back with the transform and its normal matrix.
+__device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, float b1, float b2, SurfInt& si,
+                                         int& medium) {
+    float len = 1.0f;
+    const DevInstance* I = nullptr;
+    if ((uint32_t)prim >= S.n_prims) {
+        for (uint32_t k = 0; k < S.n_instances; k++) {
+            const DevInstance& c = S.instances[k];
+            if ((uint32_t)prim >= c.virt_base && (uint32_t)prim < c.virt_base + c.n_prims) I = &c;
+        }
+        prim = (int)(I->prim_base + ((uint32_t)prim - I->virt_base));
+        const f3 dir = m4_dir(I->inv, rd);
+        len = length(dir);
+        ro = m4_point(I->inv, ro);
+        rd = dir / len;
+    }
+    const DevGeom g = S.geom[prim];
+    const DevPrimInfo pi = S.info[prim];
+    const uint32_t kind = __float_as_uint(g.a.w) & GF_KIND;
+    if (I) {  // the object-space t of the accepted hit
+        if (kind == PT_PRIM_TRIANGLE) {
+            float bx, by;
+            tri_glm(ro, rd, xyz(g.a), xyz(g.b), xyz(g.c), bx, by, t);
+        } else if (kind == PT_PRIM_QUAD) {
+            float a, b;
+            quad_hit(S.quads[pi.index], ro, rd, __int_as_float(0x7f800000), t, a, b);
+        } else {
+            sphere_root(S.spheres[pi.index], ro, rd, __int_as_float(0x7f800000), t);
+        }
+    }
+    if (kind == PT_PRIM_TRIANGLE) tri_interaction(g, pi.index, pi.material, ro, rd, t, b1, b2, si);
+    else if (kind == PT_PRIM_QUAD) quad_interaction(S.quads[pi.index], ro, rd, t, b1, b2, si);
+    else sphere_interaction(S.spheres[pi.index], ro, rd, t, si);
+    si.mat = pi.material;
+    si.light = pi.light;
+    medium = pi.medium;
+    if (I) {
+        float NM[9];
+        normal_matrix(I->T, NM);
+        si.p = m4_point(I->T, si.p);
+        si.n = normalize(m3_mul(NM, si.n));
+        si.ns = normalize(m3_mul(NM, si.ns));
+        si.t = si.t / len;
+        si.tangent = normalize4(m4_dir(I->T, si.tangent));
+    }
+}
+
 // ------------------------------------------------------------------ traversal kernels
 // Register budget of the pool kernels: PT_POOL_WPE waves per SIMD.  7 (72
 // VGPRs, no hot-path spills) measured +4.5 % on C4 over the unconstrained 76;
@@ -109,7 +162,7 @@ struct ClosestSrc {
     __device__ __forceinline__ void any(uint32_t, bool) {}
 };
 
-template <bool COUNT>
+template <bool COUNT, bool INST>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_closest_pool(PathSoA P, const uint32_t* __restrict__ nptr,
                                                                 float4* __restrict__ hit, uint32_t* __restrict__ pool,
                                                                 uint32_t* __restrict__ ovf, uint32_t* __restrict__ spare,
@@ -121,7 +174,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_closest_pool(P
     if (n == 0) return;
     TraceWork wk{0, 0};
     ClosestSrc src{P, hit, nptr[Q_NEXT]};
-    trace_pool<false, COUNT>(n, pool, src, s_ref, ovf, wk);
+    trace_pool<false, COUNT, ClosestSrc, true, INST>(n, pool, src, s_ref, ovf, wk);
     if (COUNT) {
         count_add(counters, CNT_NODES_CLOSEST, wk.nodes);
         count_add(counters, CNT_TRIS_CLOSEST, wk.tris);
@@ -162,7 +215,7 @@ struct ShadowSrc {
     }
 };
 
-template <bool COUNT>
+template <bool COUNT, bool INST>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_shadow_pool(PathSoA next, float* __restrict__ sample_L,
                                                                const ShadowRec* __restrict__ sq,
                                                                const uint32_t* __restrict__ nptr,
@@ -173,7 +226,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_shadow_pool(Pa
     ShadowSrc src{sq, next, sample_L};
     const uint32_t n = *nptr;
     if (n == 0) return;
-    trace_pool<true, COUNT>(n, pool, src, s_ref, ovf, wk);
+    trace_pool<true, COUNT, ShadowSrc, true, INST>(n, pool, src, s_ref, ovf, wk);
     if (COUNT) {
         count_add(counters, CNT_NODES_ANY, wk.nodes);
         count_add(counters, CNT_TRIS_ANY, wk.tris);
@@ -193,7 +246,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_shadow_pool(Pa
 #else
 #define PT_SIMPLE_LDS PT_STACK
 #endif
-template <bool COUNT>
+template <bool COUNT, bool INST>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(PathSoA P, const uint32_t* __restrict__ nptr,
                                                            float4* __restrict__ hit, uint32_t* __restrict__,
                                                            uint32_t* __restrict__ ovf, uint32_t* __restrict__ spare,
@@ -205,14 +258,14 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(PathSoA P, const uin
     TraceWork wk{0, 0};
 #if PT_SIMPLE_STEP
     ClosestSrc src{P, hit, nptr[Q_NEXT]};
-    trace_pool<false, COUNT, ClosestSrc, false>(n, nullptr, src, s_ref, ovf, wk);
+    trace_pool<false, COUNT, ClosestSrc, false, INST>(n, nullptr, src, s_ref, ovf, wk);
 #else
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     if (i < n) {
         const uint32_t e = path_slot(i, nptr[Q_NEXT], P.cap);
         const float4 o = P.o[e], d = P.d[e];
         float t, b1, b2;
-        int prim = trace_closest<COUNT>(xyz(o), xyz(d), __int_as_float(0x7f800000), t, b1, b2, s_ref, wk);
+        int prim = trace_closest<COUNT, INST>(xyz(o), xyz(d), __int_as_float(0x7f800000), t, b1, b2, s_ref, wk);
         hit[i] = make_float4(t, b1, b2, __int_as_float(prim));
     }
 #endif
@@ -222,7 +275,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(PathSoA P, const uin
     }
 }
 
-template <bool COUNT>
+template <bool COUNT, bool INST>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(PathSoA next, float* __restrict__ sample_L,
                                                           const ShadowRec* __restrict__ sq,
                                                           const uint32_t* __restrict__ nptr, uint32_t* __restrict__,
@@ -233,12 +286,12 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(PathSoA next, float* 
     TraceWork wk{0, 0};
     ShadowSrc src{sq, next, sample_L};
 #if PT_SIMPLE_STEP
-    if (blockIdx.x * PT_TRACE_BLOCK < n) trace_pool<true, COUNT, ShadowSrc, false>(n, nullptr, src, s_ref, ovf, wk);
+    if (blockIdx.x * PT_TRACE_BLOCK < n) trace_pool<true, COUNT, ShadowSrc, false, INST>(n, nullptr, src, s_ref, ovf, wk);
 #else
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     if (i < n) {
         const ShadowRec r = sq[i];
-        src.any(i, trace_any<COUNT>(xyz(r.o), xyz(r.d), r.o.w, s_ref, wk));
+        src.any(i, trace_any<COUNT, INST>(xyz(r.o), xyz(r.d), r.o.w, s_ref, wk));
     }
 #endif
     if (COUNT) {
@@ -292,13 +345,9 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_interact(const pt_ray* __res
     float* w = out + 16ull * i;
     for (int k = 0; k < 16; k++) w[k] = 0.0f;
     if (prim < 0) return;
-    const DevGeom g = S.geom[prim];
-    const DevPrimInfo pi = S.info[prim];
-    const uint32_t kind = __float_as_uint(g.a.w) & GF_KIND;
     SurfInt si;
-    if (kind == PT_PRIM_TRIANGLE) tri_interaction(g, pi.index, pi.material, o, d, t, b1, b2, si);
-    else if (kind == PT_PRIM_QUAD) quad_interaction(S.quads[pi.index], o, d, t, b1, b2, si);
-    else sphere_interaction(S.spheres[pi.index], o, d, t, si);
+    int medium;
+    hit_surface(prim, o, d, t, b1, b2, si, medium);
     const float rec[16] = {1.0f, si.t, si.p.x, si.p.y, si.p.z, si.n.x, si.n.y, si.n.z, si.ns.x, si.ns.y, si.ns.z,
                            si.u, si.v, si.tangent.x, si.tangent.y, si.tangent.z};
     for (int k = 0; k < 16; k++) w[k] = rec[k];
@@ -535,15 +584,9 @@ __global__ __launch_bounds__(256) void k_shade(RenderParams R, PathSoA cur, cons
                 for (int k = 0; k < 4; k++) r[k] = draw(key, dim + k);
                 dim += 4;
             }
-            const DevGeom g = S.geom[prim];
-            const DevPrimInfo pi = S.info[prim];
-            const uint32_t kind = __float_as_uint(g.a.w) & GF_KIND;
             SurfInt si;
-            if (kind == PT_PRIM_TRIANGLE) tri_interaction(g, pi.index, pi.material, ro, rd, h.x, h.y, h.z, si);
-            else if (kind == PT_PRIM_QUAD) quad_interaction(S.quads[pi.index], ro, rd, h.x, h.y, h.z, si);
-            else sphere_interaction(S.spheres[pi.index], ro, rd, h.x, si);
-            si.mat = pi.material;
-            si.light = pi.light;
+            int smed;
+            hit_surface(prim, ro, rd, h.x, h.y, h.z, si, smed);
 #ifdef PT_DEBUG_KEY
             if (key == PT_DEBUG_KEY)
                 printf("G d%u prim %d t %a p %a %a %a ns %a %a %a uv %a %a mat %d light %d out %a %a %a att %a %a %a\n",
@@ -687,20 +730,6 @@ __global__ __launch_bounds__(256) void k_shade(RenderParams R, PathSoA cur, cons
 }
 
 // ------------------------------------------------------------------ VolPathIntegrator
-// SurfaceInteraction of a closest hit (prim slot, t and barycentrics / quad
-// coordinates from the traversal)
-__device__ __forceinline__ void hit_interaction(int prim, f3 ro, f3 rd, float t, float b1, float b2, SurfInt& si,
-                                                int& medium) {
-    const DevGeom g = S.geom[prim];
-    const DevPrimInfo pi = S.info[prim];
-    const uint32_t kind = __float_as_uint(g.a.w) & GF_KIND;
-    if (kind == PT_PRIM_TRIANGLE) tri_interaction(g, pi.index, pi.material, ro, rd, t, b1, b2, si);
-    else if (kind == PT_PRIM_QUAD) quad_interaction(S.quads[pi.index], ro, rd, t, b1, b2, si);
-    else sphere_interaction(S.spheres[pi.index], ro, rd, t, si);
-    si.mat = pi.material;
-    si.light = pi.light;
-    medium = pi.medium;
-}
 // GeometricInteraction::getMedium (Interaction.hpp:26-29)
 __device__ __forceinline__ int get_medium(const SurfInt& si, int medium, f3 dir) {
     return dot(dir, si.n) < 0 ? medium : -1;
@@ -757,7 +786,7 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
         } else {
             SurfInt si;
             int smed;
-            hit_interaction(prim, ro, rd, h.x, h.y, h.z, si, smed);
+            hit_surface(prim, ro, rd, h.x, h.y, h.z, si, smed);
             if (med < 0) med = S.scene_medium;
             bool mvalid = false;
             f3 mp = F3(0, 0, 0);
@@ -964,7 +993,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow_tr(PathSoA next, floa
             }
             SurfInt si;
             int smed;
-            hit_interaction(prim, o, d, t, b1, b2, si, smed);
+            hit_surface(prim, o, d, t, b1, b2, si, smed);
             o = o + t * d;
             med = get_medium(si, smed, d);
             max -= t;
@@ -1105,17 +1134,21 @@ __global__ __launch_bounds__(256) void k_resolve(const double* __restrict__ film
 }
 
 // explicit instantiations used by the runtime
-#define PT_INST_TRACE(B)                                                                                            \
-    template __global__ void k_closest<B>(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*, uint32_t*,        \
-                                          uint32_t*, unsigned long long*);                                           \
-    template __global__ void k_closest_pool<B>(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*, uint32_t*,   \
-                                               uint32_t*, unsigned long long*);                                      \
-    template __global__ void k_shadow<B>(PathSoA, float*, const ShadowRec*, const uint32_t*, uint32_t*, uint32_t*,   \
-                                         unsigned long long*);                                                       \
-    template __global__ void k_shadow_pool<B>(PathSoA, float*, const ShadowRec*, const uint32_t*, uint32_t*,         \
-                                              uint32_t*, unsigned long long*);
-PT_INST_TRACE(false)
-PT_INST_TRACE(true)
+// INST: the instance enter/exit step is compiled in only for scenes that have
+// instances (it costs the pool kernels registers: see DESIGN.md).
+#define PT_INST_TRACE(B, I)                                                                                         \
+    template __global__ void k_closest<B, I>(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*, uint32_t*,     \
+                                             uint32_t*, unsigned long long*);                                        \
+    template __global__ void k_closest_pool<B, I>(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*,           \
+                                                  uint32_t*, uint32_t*, unsigned long long*);                        \
+    template __global__ void k_shadow<B, I>(PathSoA, float*, const ShadowRec*, const uint32_t*, uint32_t*,           \
+                                            uint32_t*, unsigned long long*);                                         \
+    template __global__ void k_shadow_pool<B, I>(PathSoA, float*, const ShadowRec*, const uint32_t*, uint32_t*,      \
+                                                 uint32_t*, unsigned long long*);
+PT_INST_TRACE(false, false)
+PT_INST_TRACE(true, false)
+PT_INST_TRACE(false, true)
+PT_INST_TRACE(true, true)
 template __global__ void k_shadow_tr<false>(PathSoA, float*, const ShadowRec*, const uint32_t*, unsigned long long*);
 template __global__ void k_shadow_tr<true>(PathSoA, float*, const ShadowRec*, const uint32_t*, unsigned long long*);
 template __global__ void k_shade<PT_INTEGRATOR_PATH>(RenderParams, PathSoA, const uint32_t*, const float4*, PathSoA,

@@ -47,7 +47,7 @@ __device__ unsigned int pt_diag[4];
 //   void any(uint32_t ri, bool hit)
 // POOL = false: no refill, lane i of the grid traces ray i (small scenes,
 // where traversal lengths are uniform and the claims would only cost).
-template <bool ANY, bool COUNT, class Src, bool POOL = true>
+template <bool ANY, bool COUNT, class Src, bool POOL = true, bool INST = true>
 __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, uint32_t* s_ref,
                            uint32_t* __restrict__ ovf, TraceWork& wk) {
     const uint32_t lane = threadIdx.x;
@@ -154,6 +154,10 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             }
             ref = pop();
         }
+        if (INST && ref >= REF_SPECIAL) {  // instance enter / exit (pt_trace.h instance_step)
+            PT_INSTANCE_STEP(ANY);
+            continue;
+        }
         const bool node_step = !(ref & REF_LEAF);
         const uint32_t idx = ref & ~REF_LEAF;
 #if PT_POOL_CHECK
@@ -181,7 +185,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             // order far -> near for closest hit (BVH4::LUT, BVH.hpp:1195-1204)
             uint32_t perm = 0xE4u;
             if (!ANY) {
-                const uint32_t ow = __float_as_uint((oct >> 2) ? q7.y : q7.x);
+                const uint32_t ow = __float_as_uint(((oct >> 2) & 1u) ? q7.y : q7.x);
                 perm = (ow >> (8 * (oct & 3))) & 0xFFu;
             }
             const uint32_t cand = order_children(mask, make_uint4(__float_as_uint(q6.x), __float_as_uint(q6.y),
@@ -214,6 +218,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                                 best = (int)slot;
                                 bb1 = bx;
                                 bb2 = by;
+                                oct |= (oct & OCT_INST) << 1;  // OCT_HIT inside an instance
                             }
                         }
                     }
@@ -230,6 +235,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                     best = (int)slot;
                     bb1 = a;
                     bb2 = b;
+                    oct |= (oct & OCT_INST) << 1;
                 }
             }
             ref = (w0 & GF_LAST) ? REF_EMPTY : (REF_LEAF | (slot + 1));

@@ -44,6 +44,8 @@ struct pt_ctx {
     float4* hit = nullptr;
     uint32_t* qcnt = nullptr;
     uint32_t* ovf = nullptr;  // pool traversal stack entries beyond PT_POOL_LDS
+    uint32_t* scratch = nullptr;  // instance traversal state, SCR_WORDS x scratch_lanes
+    uint64_t scratch_lanes = 0;
     ShadowRec* sq = nullptr;
     unsigned long long* counters = nullptr;
     uint32_t* host_cnt = nullptr;  // pinned, PT_RING counter snapshots (SNAP_WORDS each)
@@ -115,17 +117,24 @@ extern "C" pt_status pt_create(pt_ctx** out, int device) {
     {
         // the persistent (pool) traversal grid: the blocks of the pool kernels
         // that are resident together (the fewer of closest / any hit)
-        int cus = 0, per_cu = 0, per_cu_any = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_closest_pool<false>),
-                                                         PT_TRACE_BLOCK, 0) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &per_cu_any, reinterpret_cast<const void*>(&k_shadow_pool<false>), PT_TRACE_BLOCK, 0) != hipSuccess) {
+        // (instanced variants included)
+        int cus = 0, per_cu = 1 << 30;
+        const void* pool_kernels[4] = {reinterpret_cast<const void*>(&k_closest_pool<false, false>),
+                                       reinterpret_cast<const void*>(&k_shadow_pool<false, false>),
+                                       reinterpret_cast<const void*>(&k_closest_pool<false, true>),
+                                       reinterpret_cast<const void*>(&k_shadow_pool<false, true>)};
+        bool ok = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess;
+        for (int k = 0; ok && k < 4; k++) {
+            int b = 0;
+            ok = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, pool_kernels[k], PT_TRACE_BLOCK, 0) == hipSuccess;
+            per_cu = std::min(per_cu, b);
+        }
+        if (!ok) {
             g_err = "occupancy query failed";
             delete c;
             return PT_ERR_HIP;
         }
-        c->trace_blocks = (uint32_t)std::max(1, cus * std::max(1, std::min(per_cu, per_cu_any)));
+        c->trace_blocks = (uint32_t)std::max(1, cus * std::max(1, per_cu));
     }
     if (hipHostMalloc((void**)&c->host_cnt, PT_RING * SNAP_WORDS * 4, hipHostMallocCoherent | hipHostMallocMapped) !=
             hipSuccess ||
@@ -165,6 +174,7 @@ extern "C" void pt_destroy(pt_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     free_scene(c);
     free_work(c);
+    if (c->scratch) hipFree(c->scratch);
     if (c->sample_L) hipFree(c->sample_L);
     if (c->film) hipFree(c->film);
     if (c->host_cnt) hipHostFree(c->host_cnt);
@@ -308,6 +318,7 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
             case PT_PRIM_QUAD: ok = p.index < s->n_quads; break;
             case PT_PRIM_SPHERE: ok = p.index < s->n_spheres; break;
             case PT_PRIM_BLAS: ok = p.index > 0 && p.index < s->n_bvhs; break;
+            case PT_PRIM_INSTANCE: ok = p.index < s->n_instances && s->instances; break;
             default: ok = false;
         }
         if (!ok) return fail(c, PT_ERR_ARG, "primitive %u: bad kind/index", i);
@@ -339,6 +350,23 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
         if (s->sampler_lights[i] >= s->n_lights) return fail(c, PT_ERR_ARG, "sampler light %u out of range", i);
     if (s->n_media && !s->media) return fail(c, PT_ERR_ARG, "media array missing");
     if (s->n_media > PT_MAX_MEDIA) return fail(c, PT_ERR_ARG, "more than %d media", PT_MAX_MEDIA);
+    if (s->n_prims > REF_SLOT_MASK) return fail(c, PT_ERR_ARG, "too many primitives");
+    {  // instances: one level, BLAS targets without instances / nested BLAS / area lights,
+       // ascending virtual ranges past the real slots
+        uint64_t next = s->n_prims;
+        for (uint32_t k = 0; k < s->n_instances; k++) {
+            const pt_instance& I = s->instances[k];
+            if (I.bvh == 0 || I.bvh >= s->n_bvhs) return fail(c, PT_ERR_ARG, "instance %u: bad bvh", k);
+            const pt_bvh_desc& B = s->bvhs[I.bvh];
+            if ((uint64_t)B.prim_base + B.n_prims > s->n_prims) return fail(c, PT_ERR_ARG, "instance %u: bad bvh", k);
+            for (uint32_t j = B.prim_base; j < B.prim_base + B.n_prims; j++)
+                if (s->prims[j].kind == PT_PRIM_BLAS || s->prims[j].kind == PT_PRIM_INSTANCE || s->prims[j].light >= 0)
+                    return fail(c, PT_ERR_ARG, "instance %u: nested instance or area light inside", k);
+            if (I.virt_base < next || (uint64_t)I.virt_base + B.n_prims > REF_SLOT_MASK)
+                return fail(c, PT_ERR_ARG, "instance %u: bad virtual slot range", k);
+            next = (uint64_t)I.virt_base + B.n_prims;
+        }
+    }
     if (s->scene_medium < -1 || s->scene_medium >= (int32_t)s->n_media) return fail(c, PT_ERR_ARG, "bad scene medium");
     for (uint32_t i = 0; i < s->n_infinite_lights; i++)
         if (s->infinite_lights[i] >= s->n_lights) return fail(c, PT_ERR_ARG, "infinite light %u out of range", i);
@@ -368,7 +396,8 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
             g.a = make_float4(sp.center[0], sp.center[1], sp.center[2], 0);
             g.b = make_float4(sp.radius, 0, 0, 0);
         }
-        if (p.kind != PT_PRIM_BLAS) material_alpha_flags(s, p.material, flags);
+        if (p.kind == PT_PRIM_INSTANCE) flags = PT_PRIM_BLAS;  // device: a hop that pushes REF_INST_ENTER | slot
+        if (p.kind != PT_PRIM_BLAS && p.kind != PT_PRIM_INSTANCE) material_alpha_flags(s, p.material, flags);
         g.a.w = __builtin_bit_cast(float, flags);
         geom[i] = g;
         info[i] = DevPrimInfo{p.material, p.light, p.medium, p.index};
@@ -396,7 +425,21 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
         if (s->prims[i].kind == PT_PRIM_BLAS) {
             geom[i].b.x = __builtin_bit_cast(float, roots[s->prims[i].index]);
             info[i].index = roots[s->prims[i].index];
+        } else if (s->prims[i].kind == PT_PRIM_INSTANCE) {
+            geom[i].b.x = __builtin_bit_cast(float, REF_INST_ENTER | i);
+            geom[i].b.y = __builtin_bit_cast(float, s->prims[i].index);
         }
+    }
+    std::vector<DevInstance> inst(s->n_instances);
+    for (uint32_t k = 0; k < s->n_instances; k++) {
+        const pt_instance& I = s->instances[k];
+        DevInstance& D = inst[k];
+        std::memcpy(D.T, I.transform, sizeof(D.T));
+        std::memcpy(D.inv, I.inv, sizeof(D.inv));
+        D.root = roots[I.bvh];
+        D.prim_base = s->bvhs[I.bvh].prim_base;
+        D.n_prims = s->bvhs[I.bvh].n_prims;
+        D.virt_base = I.virt_base;
     }
     // ---- triangles: vertex indices + flags as uint4
     std::vector<uint4> tri(s->n_triangles);
@@ -434,6 +477,7 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
     UP(DS.sampler_cdf, cdf.data(), cdf.size());
     UP(DS.infinite_lights, s->infinite_lights, s->n_infinite_lights);
     UP(DS.media, s->media, s->n_media);
+    UP(DS.instances, inst.data(), inst.size());
 #undef UP
     DS.root = roots[0];
     DS.n_prims = s->n_prims;
@@ -446,6 +490,9 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
     DS.n_infinite_lights = s->n_infinite_lights;
     DS.n_media = s->n_media;
     DS.scene_medium = s->scene_medium;
+    DS.n_instances = s->n_instances;
+    DS.scratch = nullptr;
+    DS.scratch_lanes = 0;
     c->has_scene = true;
     c->n_media = s->n_media;
     c->n_materials = s->n_materials;
@@ -527,7 +574,30 @@ static double gauss_h(double x, double sigma) {
 #endif
 #define PT_POOL_MIN_CLUSTERS (1u << 20)  // measured: C4 (2.6M clusters) gains 31%; 0.5M-cluster heightfield and C2/C3 lose
 
-static pt_status bind_scene(pt_ctx* c) {
+// Per-lane scratch rows for instance traversal (scenes with instances only):
+// enough for the largest grid a traversal kernel launches with (the pool grid,
+// the one-ray-per-lane grid of the wavefront, or a test hook's `lanes`).
+static pt_status ensure_scratch(pt_ctx* c, uint64_t lanes) {
+    if (c->scene.n_instances == 0) return PT_OK;
+    lanes = std::max<uint64_t>({lanes, (uint64_t)c->trace_blocks * PT_TRACE_BLOCK,
+                                (uint64_t)(c->cap + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK * PT_TRACE_BLOCK});
+    if (lanes <= c->scratch_lanes) return PT_OK;
+    if (c->scratch) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        hipFree(c->scratch);
+        c->scratch = nullptr;
+        c->scratch_lanes = 0;
+    }
+    if (hipMalloc((void**)&c->scratch, lanes * SCR_WORDS * 4) != hipSuccess)
+        return fail(c, PT_ERR_OOM, "instance scratch of %llu lanes", (unsigned long long)lanes);
+    c->scratch_lanes = lanes;
+    return PT_OK;
+}
+
+static pt_status bind_scene(pt_ctx* c, uint64_t lanes = 0) {
+    if (pt_status st = ensure_scratch(c, lanes)) return st;
+    c->scene.scratch = c->scratch;
+    c->scene.scratch_lanes = (uint32_t)c->scratch_lanes;
     HIPCHK(c, hipMemcpyToSymbolAsync(HIP_SYMBOL(S), &c->scene, sizeof(DevScene), 0, hipMemcpyHostToDevice, c->stream));
     return PT_OK;
 }
@@ -591,6 +661,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     paths = (uint32_t)std::min<uint64_t>(paths, std::max<uint64_t>(1, (uint64_t)R.npix_work * s_chunk));
     paths = (paths + 255) & ~255u;
     if ((st = ensure_work(c, paths)) != PT_OK) return st;
+    if ((st = bind_scene(c)) != PT_OK) return st;  // instance scratch sized for this wavefront
 
     const bool count = (rd->flags & PT_RENDER_COUNT_NODES) != 0;
     // traversal variant: pool (persistent, refilling) for deep trees where ray
@@ -598,6 +669,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     const bool use_pool = (rd->flags & PT_RENDER_TRAVERSAL_POOL)     ? true
                           : (rd->flags & PT_RENDER_TRAVERSAL_SIMPLE) ? false
                                                                      : c->n_clusters >= PT_POOL_MIN_CLUSTERS;
+    const bool inst = c->scene.n_instances > 0;  // kernels with the instance step compiled in
     const bool timing = (rd->flags & PT_RENDER_TIMING) != 0;
     hipStream_t sm = c->stream;
     HIPCHK(c, hipMemsetAsync(c->counters, 0, (CNT_SHARDS + 1) * CNT_COUNT * 8, sm));
@@ -673,8 +745,10 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             hipEvent_t* ev = c->rev[i % PT_RING];
             if (timing) HIPCHK(c, hipEventRecord(ev[0], sm));
             {
-                auto kc = use_pool ? (count ? k_closest_pool<true> : k_closest_pool<false>)
-                                   : (count ? k_closest<true> : k_closest<false>);
+                auto kc = inst ? (use_pool ? (count ? k_closest_pool<true, true> : k_closest_pool<false, true>)
+                                           : (count ? k_closest<true, true> : k_closest<false, true>))
+                               : (use_pool ? (count ? k_closest_pool<true, false> : k_closest_pool<false, false>)
+                                           : (count ? k_closest<true, false> : k_closest<false, false>));
                 hipLaunchKernelGGL(kc, gt, dim3(PT_TRACE_BLOCK), 0, sm, cur, (const uint32_t*)in, c->hit,
                                    out + Q_WORDS, c->ovf, spare, c->host_cnt_dev + (i % PT_RING) * SNAP_WORDS,
                                    c->counters);
@@ -699,8 +773,10 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                                    nxt, c->sample_L, (const ShadowRec*)c->sq, (const uint32_t*)(out + Q_SHADOW),
                                    c->counters);
             } else if (rd->integrator != PT_INTEGRATOR_SIMPLE) {
-                auto ks = use_pool ? (count ? k_shadow_pool<true> : k_shadow_pool<false>)
-                                   : (count ? k_shadow<true> : k_shadow<false>);
+                auto ks = inst ? (use_pool ? (count ? k_shadow_pool<true, true> : k_shadow_pool<false, true>)
+                                           : (count ? k_shadow<true, true> : k_shadow<false, true>))
+                               : (use_pool ? (count ? k_shadow_pool<true, false> : k_shadow_pool<false, false>)
+                                           : (count ? k_shadow<true, false> : k_shadow<false, false>));
                 hipLaunchKernelGGL(ks, gt, dim3(PT_TRACE_BLOCK), 0, sm, nxt, c->sample_L, (const ShadowRec*)c->sq,
                                    (const uint32_t*)(out + Q_SHADOW), out + Q_WORDS + PT_POOL_WORDS, c->ovf,
                                    c->counters);
@@ -965,6 +1041,8 @@ extern "C" pt_status pt_interact(pt_ctx* c, const pt_ray* rays, uint32_t n, floa
     if (!c->has_scene) return fail(c, PT_ERR_STATE, "no scene uploaded");
     HIPCHK(c, hipSetDevice(c->device));
     if (n == 0) return PT_OK;
+    if (pt_status st = ensure_scratch(c, (uint64_t)(n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK * PT_TRACE_BLOCK))
+        return st;
     return run_hook(c, rays, (size_t)n * sizeof(pt_ray), out, (size_t)n * 16 * sizeof(float),
                     [&](void* din, float* dout) {
                         hipLaunchKernelGGL(k_interact, dim3((n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK),

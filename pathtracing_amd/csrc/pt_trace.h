@@ -213,17 +213,133 @@ __device__ __forceinline__ uint32_t order_children(uint32_t mask, uint4 ch, uint
     return cand;
 }
 
+// ---- instances (TransformedPrimitive::Intersect / IntersectPred,
+// Primitive.cpp:42-72): glm mat4 * vec4 as the reference build contracts it
+// (fixture search): fma(m0, x, m1*y) + fma(m2, z, m3*w)
+__device__ __forceinline__ f3 m4_point(const float* m, f3 p) {
+    return F3(fma_(m[0], p.x, rmul(m[4], p.y)) + fma_(m[8], p.z, m[12]),
+              fma_(m[1], p.x, rmul(m[5], p.y)) + fma_(m[9], p.z, m[13]),
+              fma_(m[2], p.x, rmul(m[6], p.y)) + fma_(m[10], p.z, m[14]));
+}
+__device__ __forceinline__ f3 m4_dir(const float* m, f3 v) {
+    return F3(fma_(m[0], v.x, rmul(m[4], v.y)) + fma_(m[8], v.z, rmul(m[12], 0.0f)),
+              fma_(m[1], v.x, rmul(m[5], v.y)) + fma_(m[9], v.z, rmul(m[13], 0.0f)),
+              fma_(m[2], v.x, rmul(m[6], v.y)) + fma_(m[10], v.z, rmul(m[14], 0.0f)));
+}
+// transpose(inverse(mat3(T))) (glm compute_inverse<3,3>) with the reference
+// build's contraction (fixture search), NM[c*3+r]
+__device__ __forceinline__ float df_(float a, float b, float c, float d) { return fma_(a, b, -rmul(c, d)); }
+__device__ void normal_matrix(const float* T, float* NM) {
+#define M(c, r) T[(c) * 4 + (r)]
+    const float D0 = df_(M(1, 1), M(2, 2), M(2, 1), M(1, 2)), D1 = df_(M(0, 1), M(2, 2), M(2, 1), M(0, 2));
+    const float D2 = df_(M(0, 1), M(1, 2), M(1, 1), M(0, 2));
+    const float od = 1.0f / fma_(M(2, 0), D2, fma_(M(0, 0), D0, -rmul(M(1, 0), D1)));
+    // NM[c*3 + r] = Inverse[r][c]
+    NM[0] = D0 * od;
+    NM[1] = -df_(M(1, 0), M(2, 2), M(2, 0), M(1, 2)) * od;
+    NM[2] = df_(M(1, 0), M(2, 1), M(2, 0), M(1, 1)) * od;
+    NM[3] = -D1 * od;
+    NM[4] = df_(M(0, 0), M(2, 2), M(2, 0), M(0, 2)) * od;
+    NM[5] = -df_(M(0, 0), M(2, 1), M(2, 0), M(0, 1)) * od;
+    NM[6] = D2 * od;
+    NM[7] = -df_(M(0, 0), M(1, 2), M(1, 0), M(0, 2)) * od;
+    NM[8] = df_(M(0, 0), M(1, 1), M(1, 0), M(0, 1)) * od;
+#undef M
+}
+// glm mat3 * vec3: fma(m2, z, fma(m0, x, m1*y)) per row (fixture search)
+__device__ __forceinline__ f3 m3_mul(const float* M, f3 v) {
+    return F3(fma_(M[6], v.z, fma_(M[0], v.x, rmul(M[3], v.y))), fma_(M[7], v.z, fma_(M[1], v.x, rmul(M[4], v.y))),
+              fma_(M[8], v.z, fma_(M[2], v.x, rmul(M[5], v.y))));
+}
+// glm::normalize of a vec4 with w = 0: dot = fma(y, y, x*x) + z*z (fixture search)
+__device__ __forceinline__ f3 normalize4(f3 v) {
+    const float d = fma_(v.y, v.y, rmul(v.x, v.x)) + rmul(v.z, v.z);
+    return v * (1.0f / csqrt(d));
+}
+
+__device__ __forceinline__ uint32_t octant(f3 d) { return ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0); }
+
+// Pops of REF_INST_ENTER / REF_INST_EXIT.  Enter: save the world ray, take it
+// to object space (dir = inv*d, length, origin = inv*o, d = dir/length,
+// max*length); the caller pushes the exit marker and continues at the BLAS
+// root.  Exit: restore; a hit accepted inside becomes t/length and its
+// virtual slot.  Out of line and by value, so the traversal loop's registers
+// are untouched by this rare path.
+struct InstState {
+    f3 o, d, inv;
+    float tmax;
+    uint32_t oct;
+    int best;
+    uint32_t ref;
+};
+template <bool ANY>
+__device__ __noinline__ InstState instance_step(InstState s) {
+    const uint32_t L = S.scratch_lanes;
+    uint32_t* sc = S.scratch + blockIdx.x * blockDim.x + threadIdx.x;
+    if (s.ref == REF_INST_EXIT) {
+        const uint32_t inst = sc[8 * L];
+        if (!ANY && (s.oct & OCT_HIT)) {
+            const DevInstance& I = S.instances[inst];
+            s.tmax = s.tmax / __uint_as_float(sc[7 * L]);
+            s.best = (int)(I.virt_base + ((uint32_t)s.best - I.prim_base));
+        } else {
+            s.tmax = __uint_as_float(sc[6 * L]);
+        }
+        s.o = F3(__uint_as_float(sc[0]), __uint_as_float(sc[L]), __uint_as_float(sc[2 * L]));
+        s.d = F3(__uint_as_float(sc[3 * L]), __uint_as_float(sc[4 * L]), __uint_as_float(sc[5 * L]));
+        s.inv = inv_dir(s.d);
+        s.oct = octant(s.d);
+        s.ref = REF_EMPTY;
+        return s;
+    }
+    const uint32_t slot = s.ref & REF_SLOT_MASK;
+    const uint32_t inst = __float_as_uint(S.geom[slot].b.y);
+    const DevInstance& I = S.instances[inst];
+    const float w[7] = {s.o.x, s.o.y, s.o.z, s.d.x, s.d.y, s.d.z, s.tmax};
+    for (int k = 0; k < 7; k++) sc[k * L] = __float_as_uint(w[k]);
+    const f3 dir = m4_dir(I.inv, s.d);
+    const float len = length(dir);
+    sc[7 * L] = __float_as_uint(len);
+    sc[8 * L] = inst;
+    s.o = m4_point(I.inv, s.o);
+    s.d = dir / len;
+    s.inv = inv_dir(s.d);
+    s.oct = octant(s.d) | OCT_INST;
+    s.tmax = s.tmax * len;
+    s.ref = I.root;
+    return s;
+}
+#define PT_INSTANCE_STEP(ANY_)                                                          \
+    do {                                                                                \
+        const bool enter_ = ref != REF_INST_EXIT;                                       \
+        const InstState st_ = instance_step<ANY_>(InstState{o, d, inv, tmax, oct, best, ref}); \
+        o = st_.o;                                                                      \
+        d = st_.d;                                                                      \
+        inv = st_.inv;                                                                  \
+        tmax = st_.tmax;                                                                \
+        oct = st_.oct;                                                                  \
+        best = st_.best;                                                                \
+        if (enter_) push(REF_INST_EXIT);                                                \
+        ref = st_.ref;                                                                  \
+    } while (0)
+
 // Closest hit.  Returns prim slot or -1; t, b1, b2 of the accepted hit.
-template <bool COUNT>
+template <bool COUNT, bool INST = true>
 __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out, float& b2_out,
                              uint32_t* s_ref, TraceWork& wk) {
     const uint32_t lane = threadIdx.x;
-    const f3 inv = inv_dir(d);
-    const uint32_t oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
+    f3 inv = inv_dir(d);
+    uint32_t oct = octant(d);
     int sp = 0;
     uint32_t ref = S.root;
     int best = -1;
     float bb1 = 0, bb2 = 0;
+    auto push = [&](uint32_t v) {
+        if (sp < PT_STACK) {
+            s_ref[sp * PT_TRACE_BLOCK + lane] = v;
+            ++sp;
+        }
+    };
     for (;;) {
         if (ref == REF_EMPTY) {
             // pop.  Entry distances are not kept (4-byte entries double the
@@ -233,6 +349,10 @@ __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out
             --sp;
             ref = s_ref[sp * PT_TRACE_BLOCK + lane];
         }
+        if (INST && ref >= REF_SPECIAL) {
+            PT_INSTANCE_STEP(false);
+            continue;
+        }
         if (!(ref & REF_LEAF)) {
             const float4* __restrict__ q = reinterpret_cast<const float4*>(S.nodes + ref);
             if (COUNT) wk.nodes++;
@@ -240,16 +360,11 @@ __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out
             const uint2 q7 = *reinterpret_cast<const uint2*>(q + 7);
             uint32_t mask;
             slab4p(q0, q1, q2, q3, q4, q5, o, inv, tmax, mask);
-            const uint32_t ow = (oct >> 2) ? q7.y : q7.x;
+            const uint32_t ow = ((oct >> 2) & 1u) ? q7.y : q7.x;
             const uint32_t perm = (ow >> (8 * (oct & 3))) & 0xFFu;  // far -> near (BVH.hpp:1195-1204)
             ref = order_children(mask, make_uint4(__float_as_uint(q6.x), __float_as_uint(q6.y),
                                                   __float_as_uint(q6.z), __float_as_uint(q6.w)),
-                                 perm, [&](uint32_t v) {
-                                     if (sp < PT_STACK) {
-                                         s_ref[sp * PT_TRACE_BLOCK + lane] = v;
-                                         ++sp;
-                                     }
-                                 });
+                                 perm, push);
             continue;
         }
         // leaf: primitives from slot until the one flagged LAST
@@ -268,14 +383,12 @@ __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out
                         best = (int)slot;
                         bb1 = bx;
                         bb2 = by;
+                        oct |= (oct & OCT_INST) << 1;  // OCT_HIT inside an instance
                     }
                 }
-            } else if (kind == PT_PRIM_BLAS) {
+            } else if (kind == PT_PRIM_BLAS) {  // a Model's BLAS root, or REF_INST_ENTER | slot
                 if (COUNT) wk.tris--;
-                if (sp < PT_STACK) {
-                    s_ref[sp * PT_TRACE_BLOCK + lane] = __float_as_uint(g.b.x);
-                    ++sp;
-                }
+                push(__float_as_uint(g.b.x));
             } else {
                 float t, a, b;
                 if (other_closest(slot, w0, o, d, tmax, t, a, b)) {
@@ -283,6 +396,7 @@ __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out
                     best = (int)slot;
                     bb1 = a;
                     bb2 = b;
+                    oct |= (oct & OCT_INST) << 1;
                 }
             }
             if (w0 & GF_LAST) break;
@@ -297,17 +411,29 @@ __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out
 
 // Any hit (Scene::IntersectPred).  Children pushed in slot order like the
 // reference (BVH.hpp:1099-1102); the last one is visited next without a push.
-template <bool COUNT>
+template <bool COUNT, bool INST = true>
 __device__ bool trace_any(f3 o, f3 d, float tmax, uint32_t* s_ref, TraceWork& wk) {
     const uint32_t lane = threadIdx.x;
-    const f3 inv = inv_dir(d);
+    f3 inv = inv_dir(d);
+    uint32_t oct = 0;
+    int best = -1;
     int sp = 0;
     uint32_t ref = S.root;
+    auto push = [&](uint32_t v) {
+        if (sp < PT_STACK) {
+            s_ref[sp * PT_TRACE_BLOCK + lane] = v;
+            ++sp;
+        }
+    };
     for (;;) {
         if (ref == REF_EMPTY) {
             if (sp == 0) return false;
             --sp;
             ref = s_ref[sp * PT_TRACE_BLOCK + lane];
+        }
+        if (INST && ref >= REF_SPECIAL) {
+            PT_INSTANCE_STEP(true);
+            continue;
         }
         if (!(ref & REF_LEAF)) {
             const float4* __restrict__ q = reinterpret_cast<const float4*>(S.nodes + ref);
@@ -318,12 +444,7 @@ __device__ bool trace_any(f3 o, f3 d, float tmax, uint32_t* s_ref, TraceWork& wk
             // slot order, the last visited next (BVH.hpp:1099-1102)
             ref = order_children(mask, make_uint4(__float_as_uint(q6.x), __float_as_uint(q6.y),
                                                   __float_as_uint(q6.z), __float_as_uint(q6.w)),
-                                 0xE4u, [&](uint32_t v) {
-                                     if (sp < PT_STACK) {
-                                         s_ref[sp * PT_TRACE_BLOCK + lane] = v;
-                                         ++sp;
-                                     }
-                                 });
+                                 0xE4u, push);
             continue;
         }
         uint32_t slot = ref & ~REF_LEAF;
@@ -343,12 +464,9 @@ __device__ bool trace_any(f3 o, f3 d, float tmax, uint32_t* s_ref, TraceWork& wk
                 } else if (tri_pred(o, d, xyz(g.a), xyz(g.b), xyz(g.c), tmax)) {
                     return true;
                 }
-            } else if (kind == PT_PRIM_BLAS) {
+            } else if (kind == PT_PRIM_BLAS) {  // a Model's BLAS root, or REF_INST_ENTER | slot
                 if (COUNT) wk.tris--;
-                if (sp < PT_STACK) {
-                    s_ref[sp * PT_TRACE_BLOCK + lane] = __float_as_uint(g.b.x);
-                    ++sp;
-                }
+                push(__float_as_uint(g.b.x));
             } else if (other_pred(slot, w0, o, d, tmax)) {
                 return true;
             }
