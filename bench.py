@@ -45,6 +45,8 @@ def build_setup(config: str, spp: int | None = None):
                                 seed=0x5EED0021)
     if config == "fog":  # C3 box in fog, VolPathIntegrator
         return scenes.cornell(W=1024, H=1024, spp=spp or 256, fog=True)
+    if config == "inst":  # instancing: C2 room + instanced meshes / shapes (TransformedPrimitive)
+        return scenes.instances(W=1024, H=1024, spp=spp or 256)
     if config.startswith("hf"):  # heightfield probe, e.g. hf1000 = 2M triangles
         return scenes.heightfield(n=int(config[2:]), W=1024, H=1024, spp=spp or 16)
     raise ValueError(config)
@@ -58,6 +60,8 @@ WORKLOADS = {
     "c1v": "C1 examples/example_1 scene (HG medium sphere) 1024x1024 256spp depth 8 VolPathIntegrator",
     "fog": "C3 Cornell box in a homogeneous fog (scene+camera medium, emissive medium, point light) "
            "1024x1024 256spp depth 8 VolPathIntegrator",
+    "inst": "C2 room + 3 instanced glossy meshes, instanced glass sphere / metal quad, animated sphere "
+            "(TransformedPrimitive / AnimatedPrimitive) 1024x1024 256spp depth 8 PathIntegrator",
 }
 
 

@@ -133,6 +133,12 @@ PT_MEMBER(GaussSigma, GaussianFilter, double, sigma);
 #ifdef PT_WITH_MODEL
 PT_MEMBER(ModelBvh, Model, std::shared_ptr<BLASBase>, model_bvh);
 #endif
+PT_MEMBER(TpPrim, TransformedPrimitive, std::shared_ptr<Primitive>, primitive);
+PT_MEMBER(TpXf, TransformedPrimitive, glm::mat4, transform);
+PT_MEMBER(TpInv, TransformedPrimitive, glm::mat4, invTransform);
+PT_MEMBER(ApPrim, AnimatedPrimitive, std::shared_ptr<Primitive>, primitive);
+PT_MEMBER(ApDir, AnimatedPrimitive, glm::vec3, dir);
+PT_MEMBER(ApTb, AnimatedPrimitive, glm::vec2, timeBounds);
 
 void check(pt_status st, const char* what, pt_ctx* c = nullptr) {
     if (st != PT_OK) throw std::runtime_error(std::string(what) + ": " + pt_last_error(c));
@@ -163,6 +169,9 @@ struct Flat {
     std::vector<pt_medium> media;
     int32_t scene_medium = -1;
     std::unordered_map<const Medium*, int32_t> med_ids;
+    std::vector<pt_instance> instances;
+    // one-primitive BLASes of instanced GeometricPrimitives (own node storage)
+    std::vector<std::vector<pt_ref_bvh4_cluster>> own_clusters;
 
     // HomogeneusMedium + HenyeyGreenstein (Medium.hpp:14-61, PhaseFunction.hpp:17-27)
     int32_t medium(const std::shared_ptr<Medium>& m) {
@@ -339,28 +348,72 @@ struct Flat {
         static_assert(sizeof(BVH4_CLUSTER) == sizeof(pt_ref_bvh4_cluster), "cluster layout");
         const uint32_t n_top = (uint32_t)top.size();
         scene_medium = medium(scene.GetMedium());
-        // BLAS list in TLAS slot order
-        std::vector<const BLAS4*> blas;
-        std::vector<uint32_t> blas_of_slot(n_top, UINT32_MAX);
-        for (uint32_t i = 0; i < n_top; i++) {
-            const Primitive* p = top[i].get();
+        // BLAS list: the Models of the TLAS slots and the instanced primitives
+        // (TransformedPrimitive / AnimatedPrimitive), once each, in slot
+        // order; an instanced GeometricPrimitive gets a one-primitive BLAS
+        struct Blas {
+            const BLAS4* b = nullptr;                // a Model's BLAS4
+            const GeometricPrimitive* gp = nullptr;  // or one GeometricPrimitive
+        };
+        std::vector<Blas> blas;
+        std::unordered_map<const void*, uint32_t> blas_index;
+        auto blas_of = [&](const Primitive* p) -> uint32_t {
             const BLAS4* b = dynamic_cast<const BLAS4*>(p);
 #ifdef PT_WITH_MODEL
             if (!b)
                 if (auto* m = dynamic_cast<const Model*>(p)) b = dynamic_cast<const BLAS4*>(PT_GET(*m, ModelBvh).get());
 #endif
-            if (b) {
-                blas_of_slot[i] = (uint32_t)blas.size();
-                blas.push_back(b);
-            } else if (!dynamic_cast<const GeometricPrimitive*>(p)) {
-                throw std::runtime_error("HipPathIntegrator: unsupported TLAS primitive (instancing is not supported)");
+            const GeometricPrimitive* gp = b ? nullptr : dynamic_cast<const GeometricPrimitive*>(p);
+            if (!b && !gp) return UINT32_MAX;
+            const void* key = b ? (const void*)b : (const void*)gp;
+            auto it = blas_index.find(key);
+            if (it != blas_index.end()) return it->second;
+            blas.push_back(Blas{b, gp});
+            return blas_index[key] = (uint32_t)blas.size() - 1;
+        };
+        struct Inst {
+            uint32_t blas;
+            glm::mat4 xf, inv;
+        };
+        std::vector<Inst> inst;
+        std::vector<uint32_t> blas_of_slot(n_top, UINT32_MAX), inst_of_slot(n_top, UINT32_MAX);
+        for (uint32_t i = 0; i < n_top; i++) {
+            const Primitive* p = top[i].get();
+            if (dynamic_cast<const GeometricPrimitive*>(p)) continue;
+            const Primitive* inner = nullptr;
+            glm::mat4 xf, inv;
+            if (auto* tp = dynamic_cast<const TransformedPrimitive*>(p)) {
+                inner = PT_GET(*tp, TpPrim).get();
+                xf = PT_GET(*tp, TpXf);
+                inv = PT_GET(*tp, TpInv);
+            } else if (auto* ap = dynamic_cast<const AnimatedPrimitive*>(p)) {
+                // AnimatedPrimitive::Intersect (Primitive.cpp:86-89) at the
+                // rays' time 0 (the shutter is not sampled)
+                inner = PT_GET(*ap, ApPrim).get();
+                const glm::vec2 tb = PT_GET(*ap, ApTb);
+                const float t = glm::clamp(0.0f - tb.x, tb.x, tb.y) / (tb.y - tb.x);
+                xf = glm::translate(glm::mat4(1), PT_GET(*ap, ApDir) * t);
+                inv = glm::inverse(xf);
+            } else {
+                blas_of_slot[i] = blas_of(p);
+                if (blas_of_slot[i] == UINT32_MAX) throw std::runtime_error("HipPathIntegrator: unsupported TLAS primitive");
+                continue;
             }
+            if (!inner->GetLights().empty())
+                throw std::runtime_error("HipPathIntegrator: lights inside an instance are not supported");
+            const uint32_t b = blas_of(inner);
+            if (b == UINT32_MAX) throw std::runtime_error("HipPathIntegrator: unsupported instanced primitive");
+            inst_of_slot[i] = (uint32_t)inst.size();
+            inst.push_back(Inst{b, xf, inv});
         }
+        auto blas_count = [&](const Blas& b) -> uint32_t {
+            return b.gp ? 1u : (uint32_t)PT_GET(*static_cast<const BLASBase*>(b.b), BlasPrims).size();
+        };
         uint32_t total = n_top;
         std::vector<uint32_t> base(blas.size());
         for (size_t k = 0; k < blas.size(); k++) {
             base[k] = total;
-            total += (uint32_t)PT_GET(*static_cast<const BLASBase*>(blas[k]), BlasPrims).size();
+            total += blas_count(blas[k]);
         }
         prims.assign(total, pt_prim{});
         pt_bvh_desc t{};
@@ -370,23 +423,48 @@ struct Flat {
         t.prim_base = 0;
         t.n_prims = n_top;
         bvhs.push_back(t);
+        uint32_t virt = total;  // virtual slots of the instances' primitives, ascending
         for (uint32_t i = 0; i < n_top; i++) {
-            if (blas_of_slot[i] != UINT32_MAX) {
+            if (inst_of_slot[i] != UINT32_MAX) {
+                const Inst& in = inst[inst_of_slot[i]];
+                pt_instance r{};
+                std::memcpy(r.transform, &in.xf[0][0], sizeof(r.transform));
+                std::memcpy(r.inv, &in.inv[0][0], sizeof(r.inv));
+                r.bvh = 1 + in.blas;
+                r.virt_base = virt;
+                virt += blas_count(blas[in.blas]);
+                prims[i] = pt_prim{PT_PRIM_INSTANCE, (uint32_t)instances.size(), -1, -1, -1};
+                instances.push_back(r);
+            } else if (blas_of_slot[i] != UINT32_MAX) {
                 prims[i] = pt_prim{PT_PRIM_BLAS, 1 + blas_of_slot[i], -1, -1, -1};
             } else {
                 geometric(*static_cast<const GeometricPrimitive*>(top[i].get()), i);
             }
         }
+        own_clusters.reserve(blas.size());
         for (size_t k = 0; k < blas.size(); k++) {
-            const auto& bp = PT_GET(*static_cast<const BLASBase*>(blas[k]), BlasPrims);
-            for (size_t j = 0; j < bp.size(); j++) geometric(bp[j], base[k] + (uint32_t)j);
-            const auto& bn = PT_GET(*blas[k], BlasNodes);
             pt_bvh_desc d{};
-            d.clusters = reinterpret_cast<const pt_ref_bvh4_cluster*>(bn.data());
-            d.n_clusters = (uint32_t)bn.size();
-            std::memcpy(&d.root, &PT_GET(*blas[k], BlasRoot), sizeof(d.root));
+            if (blas[k].gp) {
+                geometric(*blas[k].gp, base[k]);
+                const AABB bb = PT_GET(*blas[k].gp, GpShape)->BoundingBox();
+                const float box[6] = {bb.min.x, bb.min.y, bb.min.z, bb.max.x, bb.max.y, bb.max.z};
+                own_clusters.emplace_back(1);
+                uint32_t nc = 0, order = 0;
+                float bbox[6];
+                check(pt_bvh4_build(box, 1, own_clusters.back().data(), &nc, &d.root, &order, bbox), "pt_bvh4_build");
+                d.clusters = own_clusters.back().data();
+                d.n_clusters = nc;
+                d.n_prims = 1;
+            } else {
+                const auto& bp = PT_GET(*static_cast<const BLASBase*>(blas[k].b), BlasPrims);
+                for (size_t j = 0; j < bp.size(); j++) geometric(bp[j], base[k] + (uint32_t)j);
+                const auto& bn = PT_GET(*blas[k].b, BlasNodes);
+                d.clusters = reinterpret_cast<const pt_ref_bvh4_cluster*>(bn.data());
+                d.n_clusters = (uint32_t)bn.size();
+                std::memcpy(&d.root, &PT_GET(*blas[k].b, BlasRoot), sizeof(d.root));
+                d.n_prims = (uint32_t)bp.size();
+            }
             d.prim_base = base[k];
-            d.n_prims = (uint32_t)bp.size();
             bvhs.push_back(d);
         }
         // lights: Scene::GetLights() order, then lights only the sampler holds
@@ -484,6 +562,8 @@ struct Flat {
         d.media = media.data();
         d.n_media = (uint32_t)media.size();
         d.scene_medium = scene_medium;
+        d.instances = instances.data();
+        d.n_instances = (uint32_t)instances.size();
         return d;
     }
 };

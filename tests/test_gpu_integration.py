@@ -26,7 +26,7 @@ HARNESS = ROOT / "oracle" / "_ref" / "hip_harness"
 
 @pytest.mark.skipif(not HARNESS.exists(), reason="hip_harness not built (needs /root/reference at build time)")
 @pytest.mark.parametrize("name", ["example1", "cornell_c2", "cornell_c3", "zoo", "heightfield", "sanmiguel",
-                                  "example1_volpath", "fog"])
+                                  "example1_volpath", "fog", "instances"])
 def test_drop_in_integrator_matches_reference_film(name, tmp_path):
     setup = parity_scenes()[name]()
     recipe = write_recipe(tmp_path, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
