@@ -241,13 +241,23 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_shadow_pool(Pa
 #ifndef PT_SIMPLE_STEP
 #define PT_SIMPLE_STEP 0
 #endif
+// PT_SIMPLE_LN: stack entries the one-ray-per-lane kernels keep in LDS (the
+// rest in the global overflow array); PT_SIMPLE_WPE: their waves-per-SIMD budget.
+#ifndef PT_SIMPLE_LN
+#define PT_SIMPLE_LN PT_STACK
+#endif
 #if PT_SIMPLE_STEP
 #define PT_SIMPLE_LDS PT_POOL_LDS  // split stack, as the pool kernels
 #else
-#define PT_SIMPLE_LDS PT_STACK
+#define PT_SIMPLE_LDS PT_SIMPLE_LN
+#endif
+#ifdef PT_SIMPLE_WPE
+#define PT_SIMPLE_WAVES __attribute__((amdgpu_waves_per_eu(PT_SIMPLE_WPE, PT_SIMPLE_WPE)))
+#else
+#define PT_SIMPLE_WAVES
 #endif
 template <bool COUNT, bool INST>
-__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(PathSoA P, const uint32_t* __restrict__ nptr,
+__global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SIMPLE_WAVES void k_closest(PathSoA P, const uint32_t* __restrict__ nptr,
                                                            float4* __restrict__ hit, uint32_t* __restrict__,
                                                            uint32_t* __restrict__ ovf, uint32_t* __restrict__ spare,
                                                            uint32_t* __restrict__ snap, unsigned long long* counters) {
@@ -265,7 +275,8 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(PathSoA P, const uin
         const uint32_t e = path_slot(i, nptr[Q_NEXT], P.cap);
         const float4 o = P.o[e], d = P.d[e];
         float t, b1, b2;
-        int prim = trace_closest<COUNT, INST>(xyz(o), xyz(d), __int_as_float(0x7f800000), t, b1, b2, s_ref, wk);
+        int prim = trace_closest<COUNT, INST, PT_SIMPLE_LN>(xyz(o), xyz(d), __int_as_float(0x7f800000), t, b1, b2,
+                                                            s_ref, wk, ovf);
         hit[i] = make_float4(t, b1, b2, __int_as_float(prim));
     }
 #endif
@@ -276,7 +287,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest(PathSoA P, const uin
 }
 
 template <bool COUNT, bool INST>
-__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(PathSoA next, float* __restrict__ sample_L,
+__global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SIMPLE_WAVES void k_shadow(PathSoA next, float* __restrict__ sample_L,
                                                           const ShadowRec* __restrict__ sq,
                                                           const uint32_t* __restrict__ nptr, uint32_t* __restrict__,
                                                           uint32_t* __restrict__ ovf, unsigned long long* counters) {
@@ -291,7 +302,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow(PathSoA next, float* 
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     if (i < n) {
         const ShadowRec r = sq[i];
-        src.any(i, trace_any<COUNT, INST>(xyz(r.o), xyz(r.d), r.o.w, s_ref, wk));
+        src.any(i, trace_any<COUNT, INST, PT_SIMPLE_LN>(xyz(r.o), xyz(r.d), r.o.w, s_ref, wk, ovf));
     }
 #endif
     if (COUNT) {
@@ -523,7 +534,12 @@ __global__ __launch_bounds__(256) void k_fill(RenderParams R, uint32_t n, PathSo
 
 // ------------------------------------------------------------------ shading
 template <int INTEGRATOR>
-__global__ __launch_bounds__(256) void k_shade(RenderParams R, PathSoA cur, const uint32_t* __restrict__ nptr,
+#ifdef PT_SHADE_WPE  // tuning: a waves-per-SIMD budget for k_shade
+#define PT_SHADE_WAVES __attribute__((amdgpu_waves_per_eu(PT_SHADE_WPE, PT_SHADE_WPE)))
+#else
+#define PT_SHADE_WAVES
+#endif
+__global__ __launch_bounds__(256) PT_SHADE_WAVES void k_shade(RenderParams R, PathSoA cur, const uint32_t* __restrict__ nptr,
                                               const float4* __restrict__ hit, PathSoA next,
                                               float* __restrict__ sample_L,
                                               unsigned long long* __restrict__ next_sample,

@@ -544,9 +544,12 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
     AL(c->qcnt, (3 * SET_WORDS + PT_POOL_WORDS) * 4);  // three counter sets, then pt_trace's pool
     AL(c->sq, n * sizeof(ShadowRec));
     AL(c->counters, (CNT_SHARDS + 1) * CNT_COUNT * 8);
-    if (PT_STACK > PT_POOL_LDS)  // lanes of the larger traversal grid: pool (resident) or one ray per lane
+    // lanes of the larger traversal grid (pool: resident; one ray per lane: the
+    // capacity) x the stack entries beyond the smaller LDS part
+    constexpr int ovf_entries = PT_STACK - std::min(PT_POOL_LDS, PT_SIMPLE_LN);
+    if (ovf_entries > 0)
         AL(c->ovf, std::max<size_t>((size_t)c->trace_blocks * PT_TRACE_BLOCK, (n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK * PT_TRACE_BLOCK) *
-                       (PT_STACK - PT_POOL_LDS) * 4);
+                       ovf_entries * 4);
 #undef AL
     if (hipMemset(c->qcnt, 0, (3 * SET_WORDS + PT_POOL_WORDS) * 4) != hipSuccess) {
         free_work(c);

@@ -273,7 +273,7 @@ struct InstState {
     uint32_t ref;
 };
 template <bool ANY>
-__device__ __noinline__ InstState instance_step(InstState s) {
+__device__ __forceinline__ InstState instance_step_inl(InstState s) {
     const uint32_t L = S.scratch_lanes;
     uint32_t* sc = S.scratch + blockIdx.x * blockDim.x + threadIdx.x;
     if (s.ref == REF_INST_EXIT) {
@@ -309,10 +309,16 @@ __device__ __noinline__ InstState instance_step(InstState s) {
     s.ref = I.root;
     return s;
 }
-#define PT_INSTANCE_STEP(ANY_)                                                          \
+// The pool kernels (7 waves per SIMD, 72 VGPRs) call it out of line; the
+// one-ray-per-lane kernels (5 waves) inline it (+4 % on the instanced scene).
+template <bool ANY>
+__device__ __noinline__ InstState instance_step(InstState s) {
+    return instance_step_inl<ANY>(s);
+}
+#define PT_INSTANCE_STEP_FN(ANY_, FN_)                                                          \
     do {                                                                                \
         const bool enter_ = ref != REF_INST_EXIT;                                       \
-        const InstState st_ = instance_step<ANY_>(InstState{o, d, inv, tmax, oct, best, ref}); \
+        const InstState st_ = FN_<ANY_>(InstState{o, d, inv, tmax, oct, best, ref});          \
         o = st_.o;                                                                      \
         d = st_.d;                                                                      \
         inv = st_.inv;                                                                  \
@@ -322,11 +328,15 @@ __device__ __noinline__ InstState instance_step(InstState s) {
         if (enter_) push(REF_INST_EXIT);                                                \
         ref = st_.ref;                                                                  \
     } while (0)
+#define PT_INSTANCE_STEP(ANY_) PT_INSTANCE_STEP_FN(ANY_, instance_step)
+#define PT_INSTANCE_STEP_INL(ANY_) PT_INSTANCE_STEP_FN(ANY_, instance_step_inl)
 
 // Closest hit.  Returns prim slot or -1; t, b1, b2 of the accepted hit.
-template <bool COUNT, bool INST = true>
+// LN: stack entries kept in LDS; entries [LN, PT_STACK) go to ovf
+// ([entry][grid lane], sized by the runtime for the one-ray-per-lane grid).
+template <bool COUNT, bool INST = true, int LN = PT_STACK>
 __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out, float& b2_out,
-                             uint32_t* s_ref, TraceWork& wk) {
+                             uint32_t* s_ref, TraceWork& wk, uint32_t* __restrict__ ovf = nullptr) {
     const uint32_t lane = threadIdx.x;
     f3 inv = inv_dir(d);
     uint32_t oct = octant(d);
@@ -334,9 +344,11 @@ __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out
     uint32_t ref = S.root;
     int best = -1;
     float bb1 = 0, bb2 = 0;
+    const uint32_t gl = blockIdx.x * PT_TRACE_BLOCK + lane, G = gridDim.x * PT_TRACE_BLOCK;
     auto push = [&](uint32_t v) {
         if (sp < PT_STACK) {
-            s_ref[sp * PT_TRACE_BLOCK + lane] = v;
+            if (LN >= PT_STACK || sp < LN) s_ref[sp * PT_TRACE_BLOCK + lane] = v;
+            else ovf[(size_t)(sp - LN) * G + gl] = v;
             ++sp;
         }
     };
@@ -347,10 +359,10 @@ __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out
             // BVH.hpp:1135) is fetched and all its children fail the slab test.
             if (sp == 0) break;
             --sp;
-            ref = s_ref[sp * PT_TRACE_BLOCK + lane];
+            ref = (LN >= PT_STACK || sp < LN) ? s_ref[sp * PT_TRACE_BLOCK + lane] : ovf[(size_t)(sp - LN) * G + gl];
         }
         if (INST && ref >= REF_SPECIAL) {
-            PT_INSTANCE_STEP(false);
+            PT_INSTANCE_STEP_INL(false);
             continue;
         }
         if (!(ref & REF_LEAF)) {
@@ -411,17 +423,20 @@ __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out
 
 // Any hit (Scene::IntersectPred).  Children pushed in slot order like the
 // reference (BVH.hpp:1099-1102); the last one is visited next without a push.
-template <bool COUNT, bool INST = true>
-__device__ bool trace_any(f3 o, f3 d, float tmax, uint32_t* s_ref, TraceWork& wk) {
+template <bool COUNT, bool INST = true, int LN = PT_STACK>
+__device__ bool trace_any(f3 o, f3 d, float tmax, uint32_t* s_ref, TraceWork& wk,
+                          uint32_t* __restrict__ ovf = nullptr) {
     const uint32_t lane = threadIdx.x;
     f3 inv = inv_dir(d);
     uint32_t oct = 0;
     int best = -1;
     int sp = 0;
     uint32_t ref = S.root;
+    const uint32_t gl = blockIdx.x * PT_TRACE_BLOCK + lane, G = gridDim.x * PT_TRACE_BLOCK;
     auto push = [&](uint32_t v) {
         if (sp < PT_STACK) {
-            s_ref[sp * PT_TRACE_BLOCK + lane] = v;
+            if (LN >= PT_STACK || sp < LN) s_ref[sp * PT_TRACE_BLOCK + lane] = v;
+            else ovf[(size_t)(sp - LN) * G + gl] = v;
             ++sp;
         }
     };
@@ -429,10 +444,10 @@ __device__ bool trace_any(f3 o, f3 d, float tmax, uint32_t* s_ref, TraceWork& wk
         if (ref == REF_EMPTY) {
             if (sp == 0) return false;
             --sp;
-            ref = s_ref[sp * PT_TRACE_BLOCK + lane];
+            ref = (LN >= PT_STACK || sp < LN) ? s_ref[sp * PT_TRACE_BLOCK + lane] : ovf[(size_t)(sp - LN) * G + gl];
         }
         if (INST && ref >= REF_SPECIAL) {
-            PT_INSTANCE_STEP(true);
+            PT_INSTANCE_STEP_INL(true);
             continue;
         }
         if (!(ref & REF_LEAF)) {
