@@ -326,6 +326,25 @@ pt_status pt_film_resolve(pt_ctx* ctx, const double* film_accum, int32_t width, 
 /* Device bytes held by the uploaded scene. */
 uint64_t pt_scene_device_bytes(const pt_ctx* ctx);
 
+/* Device BVH build on the context's GPU: the same
+ * BVHBase::BuildBaseThreaded binned SAH (BVH.hpp:290-390) as pt_bvh4_build,
+ * level-synchronous on the device (binning, SAH decision, std::partition's
+ * exact permutation), small subtrees one per lane, then the BVH4 collapse
+ * (BVH.hpp:788-1017) level by level.  Same arguments and byte-identical outputs
+ * as pt_bvh4_build; boxes are host memory.  stats may be NULL. */
+typedef struct pt_bvh_build_stats {
+    double ms_total;     /* host wall time of the call                     */
+    double ms_device;    /* upload + device build + download (HIP events) */
+    double ms_collapse;  /* BVH4 collapse + cluster download (HIP events)  */
+    uint32_t levels;     /* level-synchronous passes                       */
+    uint32_t small_tasks;/* subtrees finished one per lane                 */
+    uint32_t nodes;      /* binary nodes                                   */
+    uint32_t pad;
+} pt_bvh_build_stats;
+pt_status pt_bvh4_build_device(pt_ctx* ctx, const float* boxes, uint32_t n, pt_ref_bvh4_cluster* clusters,
+                               uint32_t* n_clusters, pt_ref_bvh4_node* root, uint32_t* prim_order, float* bbox,
+                               pt_bvh_build_stats* stats);
+
 #ifdef __cplusplus
 }
 #endif

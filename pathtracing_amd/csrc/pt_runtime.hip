@@ -1079,3 +1079,6 @@ extern "C" pt_status pt_light_cases(pt_ctx* c, const float* cases, uint32_t n, f
                                            c->stream, (const float*)din, n, dout);
                     });
 }
+
+// Device BVH build (pt_bvh4_build_device)
+#include "pt_bvh_gpu.hip"

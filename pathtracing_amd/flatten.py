@@ -213,6 +213,17 @@ class _Registry:
         return self.mat_ids[id(m)]
 
 
+# Where model BLASes and the TLAS are built: the host builder (default) or the
+# device build (pt_bvh4_build_device, byte-identical output) on that GPU.
+BVH_DEVICE: Optional[int] = None
+
+
+def bvh_build(boxes: np.ndarray):
+    if BVH_DEVICE is None:
+        return N.bvh4_build(boxes)
+    return N.bvh4_build_device(boxes, device=BVH_DEVICE)
+
+
 def _stack(recs, dtype):
     if not recs:
         return np.zeros(0, dtype=dtype)
@@ -302,7 +313,7 @@ def flatten_scene(scene: Scene) -> FlatScene:
             vbase += nv
             tri_base += nt
         bx = np.concatenate(boxes) if boxes else np.zeros((0, 6), np.float32)
-        model_blas.append(N.bvh4_build(bx))
+        model_blas.append(bvh_build(bx))
         model_tri_mat.append(np.concatenate(mats) if mats else np.zeros(0, np.int32))
         model_tri_med.append((meds, med_objs))
 
@@ -330,7 +341,7 @@ def flatten_scene(scene: Scene) -> FlatScene:
                 top_boxes[i] = instance_bbox(inner, p.transform)
         else:
             raise TypeError(f"unsupported primitive {type(p).__name__}")
-    tl_clusters, tl_root, tl_order, tl_bbox = N.bvh4_build(top_boxes)
+    tl_clusters, tl_root, tl_order, tl_bbox = bvh_build(top_boxes)
 
     n_top = len(top)
     n_blas_prims = sum(int(b[2].shape[0]) for b in model_blas) + len(gp_blas)

@@ -113,10 +113,18 @@ class Stats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class BvhBuildStats(C.Structure):
+    _fields_ = [("ms_total", C.c_double), ("ms_device", C.c_double), ("ms_collapse", C.c_double),
+                ("levels", C.c_uint32), ("small_tasks", C.c_uint32), ("nodes", C.c_uint32), ("pad", C.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+
+
 EXPORTS = [
     "pt_version", "pt_create", "pt_destroy", "pt_last_error", "pt_set_stream", "pt_scene_upload", "pt_render",
     "pt_trace", "pt_scene_device_bytes", "pt_bvh4_build", "pt_bvh4_order_table", "pt_film_resolve",
-    "pt_mat4_inverse",
+    "pt_mat4_inverse", "pt_bvh4_build_device",
 ]
 
 _lib = None
@@ -164,6 +172,9 @@ def lib():
     L.pt_scene_device_bytes.restype = C.c_uint64
     L.pt_bvh4_build.argtypes = [vp, C.c_uint32, vp, C.POINTER(C.c_uint32), C.POINTER(RefNode), vp, vp]
     L.pt_bvh4_build.restype = C.c_int32
+    L.pt_bvh4_build_device.argtypes = [vp, vp, C.c_uint32, vp, C.POINTER(C.c_uint32), C.POINTER(RefNode), vp, vp,
+                                       C.POINTER(BvhBuildStats)]
+    L.pt_bvh4_build_device.restype = C.c_int32
     L.pt_bvh4_order_table.argtypes = [vp]
     L.pt_bvh4_order_table.restype = C.c_int32
     _lib = L
@@ -203,6 +214,32 @@ def bvh4_build(boxes: np.ndarray):
     bbox = np.zeros(6, dtype=np.float32)
     check(lib().pt_bvh4_build(ptr(boxes), n, clusters.ctypes.data, C.byref(nc), C.byref(root), order.ctypes.data,
                               bbox.ctypes.data))
+    r = np.zeros(1, dtype=REF_NODE)
+    r[0] = (root.count, root.active, root.perm, root.pad, root.cluster_idx)
+    return clusters[: nc.value].copy(), r[0], order[:n].copy(), bbox
+
+
+def bvh4_build_device(boxes: np.ndarray, device: int = 0, stats: dict | None = None):
+    """pt_bvh4_build_device: the same build as bvh4_build (byte-identical
+    outputs) run on the GPU.  `stats`, if given, receives the timings."""
+    boxes = np.ascontiguousarray(boxes, dtype=np.float32).reshape(-1, 6)
+    n = boxes.shape[0]
+    clusters = np.zeros(max(n, 1), dtype=REF_CLUSTER)
+    order = np.zeros(max(n, 1), dtype=np.uint32)
+    nc = C.c_uint32(0)
+    root = RefNode()
+    bbox = np.zeros(6, dtype=np.float32)
+    st = BvhBuildStats()
+    L = lib()
+    ctx = C.c_void_p()
+    check(L.pt_create(C.byref(ctx), device))
+    try:
+        check(L.pt_bvh4_build_device(ctx, ptr(boxes), n, clusters.ctypes.data, C.byref(nc), C.byref(root),
+                                     order.ctypes.data, bbox.ctypes.data, C.byref(st)), ctx)
+    finally:
+        L.pt_destroy(ctx)
+    if stats is not None:
+        stats.update(st.as_dict())
     r = np.zeros(1, dtype=REF_NODE)
     r[0] = (root.count, root.active, root.perm, root.pad, root.cluster_idx)
     return clusters[: nc.value].copy(), r[0], order[:n].copy(), bbox
