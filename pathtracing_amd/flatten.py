@@ -11,6 +11,7 @@ afterwards come last.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -215,7 +216,8 @@ class _Registry:
 
 # Where model BLASes and the TLAS are built: the host builder (default) or the
 # device build (pt_bvh4_build_device, byte-identical output) on that GPU.
-BVH_DEVICE: Optional[int] = None
+BVH_DEVICE: Optional[int] = (int(os.environ["PT_BVH_DEVICE"]) if os.environ.get("PT_BVH_DEVICE", "") != ""
+                              else None)
 
 
 def bvh_build(boxes: np.ndarray):
