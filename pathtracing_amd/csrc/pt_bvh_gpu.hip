@@ -148,26 +148,79 @@ __device__ void wave_count(Acc* acc, uint32_t key, bool active, uint32_t v) {
     }
 }
 
+// Item passes cover kSpan = kBlock * kIPT consecutive items per workgroup
+// (round r touches items b0 + r*kBlock + tid, coalesced).  When a workgroup
+// lies inside one node, accumulators stay in registers across the rounds and
+// are reduced once per workgroup: a few global atomics per 4096 items instead
+// of per wave (the top levels otherwise serialise on a dozen addresses).
+constexpr int kIPT = 16;
+constexpr uint32_t kSpan = kBlock * kIPT;
+
+__device__ __forceinline__ void acc_ident(uint32_t a[12]) {
+#pragma unroll
+    for (int j = 0; j < 12; j++) a[j] = key_is_min(j) ? 0xFFFFFFFFu : 0u;
+}
+__device__ __forceinline__ void acc_merge(uint32_t a[12], const uint32_t v[12]) {
+#pragma unroll
+    for (int j = 0; j < 12; j++) a[j] = key_is_min(j) ? min(a[j], v[j]) : max(a[j], v[j]);
+}
+// wave reduction of a[12] into the workgroup's LDS accumulator s[12]
+__device__ __forceinline__ void wave_to_lds(uint32_t* s, const uint32_t a[12]) {
+#pragma unroll
+    for (int j = 0; j < 12; j++) {
+        const bool mn = key_is_min(j);
+        uint32_t x = a[j];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const uint32_t y = __shfl_xor(x, off);
+            x = mn ? min(x, y) : max(x, y);
+        }
+        if (__lane_id() == 0) {
+            if (mn)
+                atomicMin(&s[j], x);
+            else
+                atomicMax(&s[j], x);
+        }
+    }
+}
+__device__ __forceinline__ void lds_to_global(Acc* acc, uint32_t key, const uint32_t* s, int j) {
+    const bool mn = key_is_min(j);
+    if (s[j] == (mn ? 0xFFFFFFFFu : 0u)) return;
+    if (mn)
+        atomicMin(&acc[key].k[j], s[j]);
+    else
+        atomicMax(&acc[key].k[j], s[j]);
+}
+
 // PrimitiveInfo (BVH.hpp:84-93): box + centroid 0.5*(max+min); the root task
 // accumulates every box.
-__global__ void k_init(const float* __restrict__ boxes, uint32_t n, Item* __restrict__ items,
-                       uint32_t* __restrict__ seg, Acc* acc) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t v[12] = {};
-    const bool act = i < n;
-    if (act) {
+__global__ __launch_bounds__(kBlock) void k_init(const float* __restrict__ boxes, uint32_t n,
+                                                 Item* __restrict__ items, uint32_t* __restrict__ seg, Acc* acc) {
+    __shared__ uint32_t s_acc[12];
+    if (threadIdx.x < 12) s_acc[threadIdx.x] = key_is_min(threadIdx.x) ? 0xFFFFFFFFu : 0u;
+    __syncthreads();
+    uint32_t a[12];
+    acc_ident(a);
+    const uint32_t b0 = blockIdx.x * kSpan;
+    for (int r = 0; r < kIPT; r++) {
+        const uint32_t i = b0 + r * kBlock + threadIdx.x;
+        if (i >= n) break;
         Item it;
-        for (int a = 0; a < 3; a++) {
-            it.mn[a] = boxes[6ull * i + a];
-            it.mx[a] = boxes[6ull * i + 3 + a];
-            it.c[a] = 0.5f * (it.mx[a] + it.mn[a]);
+        for (int q = 0; q < 3; q++) {
+            it.mn[q] = boxes[6ull * i + q];
+            it.mx[q] = boxes[6ull * i + 3 + q];
+            it.c[q] = 0.5f * (it.mx[q] + it.mn[q]);
         }
         it.idx = i;
         items[i] = it;
         seg[i] = 0;
+        uint32_t v[12];
         item_keys(it, v);
+        acc_merge(a, v);
     }
-    wave_acc(acc, 0, act, v);
+    wave_to_lds(s_acc, a);
+    __syncthreads();
+    if (threadIdx.x < 12) lds_to_global(acc, 0, s_acc, threadIdx.x);
 }
 
 // Per task: node box, default leaf record, bin layout (BVH.hpp:300-330).
@@ -207,9 +260,8 @@ __global__ __launch_bounds__(kBlock) void k_bin(const Item* __restrict__ items, 
                                                 uint32_t n, const Dec* __restrict__ dec, uint32_t* bcnt,
                                                 uint32_t* bmin, uint32_t* bmax) {
     __shared__ uint32_t s_cnt[96], s_min[288], s_max[288];
-    const uint32_t b0 = blockIdx.x * kBlock;
-    const uint32_t i = b0 + threadIdx.x;
-    const uint32_t last = min(n, b0 + kBlock) - 1;
+    const uint32_t b0 = blockIdx.x * kSpan;
+    const uint32_t last = min(n, b0 + kSpan) - 1;
     const uint32_t t0 = seg[b0], tl = seg[last];
     const bool uniform = t0 != kInv && t0 == tl;
     if (uniform) {
@@ -220,8 +272,10 @@ __global__ __launch_bounds__(kBlock) void k_bin(const Item* __restrict__ items, 
         }
         __syncthreads();
     }
-    const uint32_t t = i < n ? seg[i] : kInv;
-    if (t != kInv) {
+    for (int r = 0; r < kIPT; r++) {
+        const uint32_t i = b0 + r * kBlock + threadIdx.x;
+        const uint32_t t = i < n ? seg[i] : kInv;
+        if (t == kInv) continue;
         const Dec d = dec[t];
         const Item it = items[i];
         uint32_t v[6];
@@ -433,19 +487,55 @@ __global__ void k_swap(const uint32_t* __restrict__ seg, uint32_t n, const Task*
 }
 
 // Items follow their node into the child task; child bounds accumulate.
-__global__ void k_advance(const Item* __restrict__ items, uint32_t* __restrict__ seg, uint32_t n,
-                          const Dec* __restrict__ dec, Acc* next_acc) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t t = i < n ? seg[i] : kInv;
-    uint32_t child = kInv;
-    uint32_t v[12] = {};
-    if (t != kInv) {
-        const Dec d = dec[t];
-        if (d.split) child = i < d.mid ? d.lt : d.rt;
-        seg[i] = child;
-        if (child != kInv) item_keys(items[i], v);
+__global__ __launch_bounds__(kBlock) void k_advance(const Item* __restrict__ items, uint32_t* __restrict__ seg,
+                                                    uint32_t n, const Dec* __restrict__ dec, Acc* next_acc) {
+    __shared__ uint32_t s_acc[2][12];
+    const uint32_t b0 = blockIdx.x * kSpan;
+    const uint32_t last = min(n, b0 + kSpan) - 1;
+    const uint32_t t0 = seg[b0], tl = seg[last];
+    if (t0 != kInv && t0 == tl) {  // one parent: two children at most, kept in registers
+        const Dec d = dec[t0];
+        if (threadIdx.x < 24) s_acc[threadIdx.x / 12][threadIdx.x % 12] = key_is_min(threadIdx.x % 12) ? 0xFFFFFFFFu : 0u;
+        __syncthreads();
+        uint32_t a0[12], a1[12];
+        acc_ident(a0);
+        acc_ident(a1);
+        for (int r = 0; r < kIPT; r++) {
+            const uint32_t i = b0 + r * kBlock + threadIdx.x;
+            if (i > last) break;
+            const uint32_t child = d.split ? (i < d.mid ? d.lt : d.rt) : kInv;
+            seg[i] = child;
+            if (child == kInv) continue;
+            uint32_t v[12];
+            item_keys(items[i], v);
+            if (i < d.mid)
+                acc_merge(a0, v);
+            else
+                acc_merge(a1, v);
+        }
+        wave_to_lds(s_acc[0], a0);
+        wave_to_lds(s_acc[1], a1);
+        __syncthreads();
+        if (threadIdx.x < 24) {
+            const int side = threadIdx.x / 12;
+            const uint32_t key = side ? d.rt : d.lt;
+            if (d.split && key != kInv) lds_to_global(next_acc, key, s_acc[side], threadIdx.x % 12);
+        }
+        return;
     }
-    wave_acc(next_acc, child, child != kInv, v);
+    for (int r = 0; r < kIPT; r++) {
+        const uint32_t i = b0 + r * kBlock + threadIdx.x;
+        const uint32_t t = i < n ? seg[i] : kInv;
+        uint32_t child = kInv;
+        uint32_t v[12] = {};
+        if (t != kInv) {
+            const Dec d = dec[t];
+            if (d.split) child = i < d.mid ? d.lt : d.rt;
+            seg[i] = child;
+            if (child != kInv) item_keys(items[i], v);
+        }
+        wave_acc(next_acc, child, child != kInv, v);
+    }
 }
 
 // A subtree of at most kSmall primitives, sequentially in one lane: build2 of
@@ -792,7 +882,7 @@ extern "C" pt_status pt_bvh4_build_device(pt_ctx* c, const float* boxes, uint32_
         }
         BVHCHK(hipMemcpyAsync(ctr, &c0, sizeof(Ctr), hipMemcpyHostToDevice, sm));
     }
-    hipLaunchKernelGGL(k_init, dim3(blocks(n)), dim3(kBlock), 0, sm, d_boxes, n, items, seg, acc[0]);
+    hipLaunchKernelGGL(k_init, dim3(blocks(n, kSpan)), dim3(kBlock), 0, sm, d_boxes, n, items, seg, acc[0]);
     uint32_t T = n > kSmall ? 1 : 0;
     int cur = 0;
     Ctr h{};
@@ -809,7 +899,7 @@ extern "C" pt_status pt_bvh4_build_device(pt_ctx* c, const float* boxes, uint32_
         BVHCHK(hipMemsetAsync(bmin, 0xFF, 4ull * 288 * T, sm));
         BVHCHK(hipMemsetAsync(bmax, 0x00, 4ull * 288 * T, sm));
         hipLaunchKernelGGL(k_prep, dim3(blocks(T, 64)), dim3(64), 0, sm, T, tk, ac, dec, nodes);
-        hipLaunchKernelGGL(k_bin, dim3(blocks(n)), dim3(kBlock), 0, sm, items, seg, n, dec, bcnt, bmin, bmax);
+        hipLaunchKernelGGL(k_bin, dim3(blocks(n, kSpan)), dim3(kBlock), 0, sm, items, seg, n, dec, bcnt, bmin, bmax);
         hipLaunchKernelGGL(k_sah, dim3(blocks(T, 64)), dim3(64), 0, sm, T, tk, ac, dec, bcnt, bmin, bmax);
         hipLaunchKernelGGL(k_flag, dim3(blocks(n)), dim3(kBlock), 0, sm, items, seg, n, dec, pred, ac);
         hipLaunchKernelGGL(k_mid, dim3(blocks(T, 64)), dim3(64), 0, sm, T, tk, ac, dec, nodes, ctr, tasks[cur ^ 1],
@@ -819,7 +909,7 @@ extern "C" pt_status pt_bvh4_build_device(pt_ctx* c, const float* boxes, uint32_
                                        rocprim::plus<unsigned long long>(), sm));
         hipLaunchKernelGGL(k_rank, dim3(blocks(n)), dim3(kBlock), 0, sm, seg, n, tk, dec, vals, ex, pos);
         hipLaunchKernelGGL(k_swap, dim3(blocks(n)), dim3(kBlock), 0, sm, seg, n, tk, vals, ex, pos, items);
-        hipLaunchKernelGGL(k_advance, dim3(blocks(n)), dim3(kBlock), 0, sm, items, seg, n, dec, acc[cur ^ 1]);
+        hipLaunchKernelGGL(k_advance, dim3(blocks(n, kSpan)), dim3(kBlock), 0, sm, items, seg, n, dec, acc[cur ^ 1]);
         BVHCHK(hipGetLastError());
         BVHCHK(hipMemcpyAsync(&h, ctr, sizeof(Ctr), hipMemcpyDeviceToHost, sm));
         BVHCHK(hipStreamSynchronize(sm));
