@@ -33,7 +33,7 @@
 namespace bvhg {
 
 constexpr uint32_t kLeaf = 2;    // BVH.hpp:95 leafSize
-constexpr uint32_t kSmall = 128; // subtrees up to this many primitives finish in one lane
+constexpr uint32_t kSmall = 48;  // subtrees up to this many primitives finish in one lane (tuned on C4)
 constexpr uint32_t kInv = 0xFFFFFFFFu;
 constexpr int kBlock = 256;
 static_assert(kSmall < 1024, "one-lane subtrees use at most 16 bins");
@@ -256,24 +256,44 @@ __global__ void k_prep(uint32_t T, const Task* __restrict__ tasks, const Acc* __
 
 // Bin counts and bin boxes per (task, axis, bin) (BVH.hpp:320-327).
 // bcnt [T][3][32]; bmin / bmax [T][3][32][3] ordered keys.
+// Uniformity is decided per 256-item chunk: a chunk inside one node bins
+// into the workgroup's LDS histogram (flushed when the node changes); a chunk
+// that straddles nodes bins straight into the global histograms.
 __global__ __launch_bounds__(kBlock) void k_bin(const Item* __restrict__ items, const uint32_t* __restrict__ seg,
                                                 uint32_t n, const Dec* __restrict__ dec, uint32_t* bcnt,
                                                 uint32_t* bmin, uint32_t* bmax) {
     __shared__ uint32_t s_cnt[96], s_min[288], s_max[288];
     const uint32_t b0 = blockIdx.x * kSpan;
-    const uint32_t last = min(n, b0 + kSpan) - 1;
-    const uint32_t t0 = seg[b0], tl = seg[last];
-    const bool uniform = t0 != kInv && t0 == tl;
-    if (uniform) {
-        for (int j = threadIdx.x; j < 288; j += kBlock) {
-            s_min[j] = 0xFFFFFFFFu;
-            s_max[j] = 0;
-            if (j < 96) s_cnt[j] = 0;
+    uint32_t cur = kInv;  // node of the LDS histogram (workgroup-uniform)
+    auto flush = [&]() {
+        __syncthreads();
+        for (int j = threadIdx.x; j < 96; j += kBlock) {
+            if (!s_cnt[j]) continue;
+            const uint64_t g = (uint64_t)cur * 96 + j;
+            atomicAdd(&bcnt[g], s_cnt[j]);
+            for (int a = 0; a < 3; a++) {
+                atomicMin(&bmin[g * 3 + a], s_min[j * 3 + a]);
+                atomicMax(&bmax[g * 3 + a], s_max[j * 3 + a]);
+            }
         }
         __syncthreads();
-    }
+    };
     for (int r = 0; r < kIPT; r++) {
-        const uint32_t i = b0 + r * kBlock + threadIdx.x;
+        const uint32_t c0 = b0 + r * kBlock;
+        if (c0 >= n) break;
+        const uint32_t ta = seg[c0], tb = seg[min(n, c0 + kBlock) - 1];
+        const bool uniform = ta != kInv && ta == tb;
+        if (uniform && ta != cur) {
+            if (cur != kInv) flush();
+            for (int j = threadIdx.x; j < 288; j += kBlock) {
+                s_min[j] = 0xFFFFFFFFu;
+                s_max[j] = 0;
+                if (j < 96) s_cnt[j] = 0;
+            }
+            __syncthreads();
+            cur = ta;
+        }
+        const uint32_t i = c0 + threadIdx.x;
         const uint32_t t = i < n ? seg[i] : kInv;
         if (t == kInv) continue;
         const Dec d = dec[t];
@@ -303,18 +323,7 @@ __global__ __launch_bounds__(kBlock) void k_bin(const Item* __restrict__ items, 
             }
         }
     }
-    if (uniform) {
-        __syncthreads();
-        for (int j = threadIdx.x; j < 96; j += kBlock) {
-            if (!s_cnt[j]) continue;
-            const uint64_t g = (uint64_t)t0 * 96 + j;
-            atomicAdd(&bcnt[g], s_cnt[j]);
-            for (int a = 0; a < 3; a++) {
-                atomicMin(&bmin[g * 3 + a], s_min[j * 3 + a]);
-                atomicMax(&bmax[g * 3 + a], s_max[j * 3 + a]);
-            }
-        }
-    }
+    if (cur != kInv) flush();
 }
 
 // The SAH sweep of one node (BVH.hpp:329-360), one lane per task.
