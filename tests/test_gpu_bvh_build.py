@@ -34,7 +34,7 @@ def _tri_boxes(rng, n, spread=10.0, size=0.05):
     return np.concatenate([t.min(1), t.max(1)], 1).astype(np.float32)
 
 
-@pytest.mark.parametrize("n", [1, 2, 3, 5, 64, 127, 128, 129, 130, 1000, 4097])
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 47, 48, 49, 50, 64, 127, 128, 129, 1000, 4097, 4098])
 def test_device_build_small_sizes(n):
     _same(_tri_boxes(np.random.default_rng(n), n))
 
