@@ -1110,6 +1110,92 @@ __global__ __launch_bounds__(256) void k_gather(RenderParams R, const float* __r
     o[3] += acc[3];
 }
 
+// The same gather for a whole frame, 16x16 pixels per workgroup: every filter
+// above is separable (w = f(px) * f(py) * 1/integral, the product formed as in
+// filter_eval), so per sample index the workgroup draws each source pixel's
+// jitter once, evaluates its 2*RAD+1 x- and y-weights once into LDS, and every
+// target pixel combines them for its (2*RAD+1)^2 neighbours -- instead of
+// re-hashing and re-evaluating the filter per (source, target).  Weights are
+// bit-identical to k_gather's; the f64 sums run sample-major instead of
+// neighbour-major.
+__device__ __forceinline__ double filter_1d(const RenderParams& R, float p, int axis) {
+    if (R.filter == PT_FILTER_BOX) return fabsf(p) <= R.frad[axis] ? 1.0 : 0.0;
+    if (R.filter == PT_FILTER_GAUSSIAN) {
+        const double g = gauss1(p, R.fparam[0]) - (axis ? R.gauss_y : R.gauss_x);
+        return g > 0 ? g : 0;
+    }
+    return mitchell1(2 * p / R.frad[axis], R.fparam[0], R.fparam[1]);
+}
+
+template <int RAD>
+__global__ __launch_bounds__(256) void k_gather_tile(RenderParams R, const float* __restrict__ sample_L,
+                                                     double* __restrict__ film) {
+    constexpr int T = 16, SW = T + 2 * RAD, NS = SW * SW, NW = 2 * RAD + 1;
+    __shared__ float s_L[NS][3];
+    __shared__ double s_wx[NS][NW], s_wy[NS][NW];
+    const int W = R.cam.width, H = R.cam.height;
+    const int tx0 = blockIdx.x * T, ty0 = blockIdx.y * T;
+    const int lx = threadIdx.x % T, ly = threadIdx.x / T;
+    const int x = tx0 + lx, y = ty0 + ly;
+    const bool inside = x < W && y < H;
+    const int rx = R.rad_x, ry = R.rad_y;
+    const uint32_t ns = R.s_hi - R.s_lo;
+    double acc[4] = {0, 0, 0, 0};
+    for (uint32_t k = 0; k < ns; k++) {
+        for (int q = threadIdx.x; q < NS; q += 256) {
+            const int sx = tx0 - RAD + q % SW, sy = ty0 - RAD + q / SW;
+            float L0 = 0, L1 = 0, L2 = 0;
+            double wx[NW], wy[NW];
+#pragma unroll
+            for (int o = 0; o < NW; o++) wx[o] = wy[o] = 0;
+            if (sx >= 0 && sy >= 0 && sx < W && sy < H) {
+                uint32_t pix_i;
+                if (R.tiled) {
+                    const uint32_t tile = (uint32_t)(sy >> 3) * R.tiles_x + (uint32_t)(sx >> 3);
+                    pix_i = tile * 64u + (uint32_t)((sy & 7) * 8 + (sx & 7));
+                } else {
+                    pix_i = (uint32_t)(sy * W + sx);
+                }
+                const uint32_t spix = (uint32_t)sy * (uint32_t)W + (uint32_t)sx;
+                const uint32_t s = R.shard_index + (R.s_lo + k) * R.shard_count;
+                const uint32_t key = stream_key(R.seed, spix, s);
+                const double fx = (double)draw(key, 0), fy = (double)draw(key, 1);
+#pragma unroll
+                for (int o = -RAD; o <= RAD; o++) {
+                    if (o >= -rx && o <= rx) wx[o + RAD] = filter_1d(R, (float)((double)o + 0.5 - fx), 0);
+                    if (o >= -ry && o <= ry) wy[o + RAD] = filter_1d(R, (float)((double)o + 0.5 - fy), 1);
+                }
+                const float* L = sample_L + 3ull * ((uint64_t)k * R.npix_work + pix_i);
+                L0 = L[0], L1 = L[1], L2 = L[2];
+            }
+            s_L[q][0] = L0, s_L[q][1] = L1, s_L[q][2] = L2;
+#pragma unroll
+            for (int o = 0; o < NW; o++) s_wx[q][o] = wx[o], s_wy[q][o] = wy[o];
+        }
+        __syncthreads();
+        if (inside) {
+            for (int oy = -ry; oy <= ry; oy++) {
+                for (int ox = -rx; ox <= rx; ox++) {
+                    const int q = (ly - oy + RAD) * SW + (lx - ox + RAD);  // source (x - ox, y - oy)
+                    const double w = (s_wx[q][ox + RAD] * s_wy[q][oy + RAD]) * R.inv_integral;
+                    if (w <= 0) continue;
+                    acc[0] += (double)s_L[q][0] * w;
+                    acc[1] += (double)s_L[q][1] * w;
+                    acc[2] += (double)s_L[q][2] * w;
+                    acc[3] += w;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (!inside) return;
+    double* o = film + 4ull * ((uint64_t)y * W + x);
+    o[0] += acc[0];
+    o[1] += acc[1];
+    o[2] += acc[2];
+    o[3] += acc[3];
+}
+
 // ------------------------------------------------------------------ film resolve
 // Film::WritePNG's per-pixel body (Film.hpp:183-196) with reinhard_jodie /
 // ACESFilm (Film.hpp:34-47) and linear_to_sRGB (Texture.hpp:13-17).  The

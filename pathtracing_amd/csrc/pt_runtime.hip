@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -859,7 +860,14 @@ extern "C" pt_status pt_render(pt_ctx* c, const pt_camera_desc* cam, const pt_re
     *S = pt_stats{};
     st = run(c, cam, rd, film, S, [&](const RenderParams& R) -> pt_status {
         const uint32_t npx = (uint32_t)cam->width * cam->height;
-        hipLaunchKernelGGL(k_gather, dim3((npx + 255) / 256), dim3(256), 0, c->stream, R, c->sample_L, film);
+        const int rad = std::max(R.rad_x, R.rad_y);
+        const dim3 tiles((cam->width + 15) / 16, (cam->height + 15) / 16);
+        if (R.npix_work == npx && rad <= 1 && !getenv("PT_GATHER_PIXEL"))
+            hipLaunchKernelGGL(k_gather_tile<1>, tiles, dim3(256), 0, c->stream, R, c->sample_L, film);
+        else if (R.npix_work == npx && rad == 2 && !getenv("PT_GATHER_PIXEL"))
+            hipLaunchKernelGGL(k_gather_tile<2>, tiles, dim3(256), 0, c->stream, R, c->sample_L, film);
+        else
+            hipLaunchKernelGGL(k_gather, dim3((npx + 255) / 256), dim3(256), 0, c->stream, R, c->sample_L, film);
         HIPCHK(c, hipGetLastError());
         return PT_OK;
     });
