@@ -256,44 +256,47 @@ __global__ void k_prep(uint32_t T, const Task* __restrict__ tasks, const Acc* __
 
 // Bin counts and bin boxes per (task, axis, bin) (BVH.hpp:320-327).
 // bcnt [T][3][32]; bmin / bmax [T][3][32][3] ordered keys.
-// Uniformity is decided per 256-item chunk: a chunk inside one node bins
-// into the workgroup's LDS histogram (flushed when the node changes); a chunk
-// that straddles nodes bins straight into the global histograms.
+// Each wave bins a contiguous 1024-item range, 64 items per round.  A round
+// inside one node bins into the wave's own LDS histogram (flushed to the
+// global one when the node changes); a round that straddles nodes bins
+// straight into the global histograms.
 __global__ __launch_bounds__(kBlock) void k_bin(const Item* __restrict__ items, const uint32_t* __restrict__ seg,
                                                 uint32_t n, const Dec* __restrict__ dec, uint32_t* bcnt,
                                                 uint32_t* bmin, uint32_t* bmax) {
-    __shared__ uint32_t s_cnt[96], s_min[288], s_max[288];
-    const uint32_t b0 = blockIdx.x * kSpan;
-    uint32_t cur = kInv;  // node of the LDS histogram (workgroup-uniform)
+    constexpr int NWV = kBlock / 64;
+    __shared__ uint32_t s_cnt[NWV][96], s_min[NWV][288], s_max[NWV][288];
+    const int wv = threadIdx.x >> 6, lane = __lane_id();
+    uint32_t* hc = s_cnt[wv];
+    uint32_t* hmn = s_min[wv];
+    uint32_t* hmx = s_max[wv];
+    const uint32_t w0 = blockIdx.x * kSpan + (uint32_t)wv * (kSpan / NWV);
+    uint32_t cur = kInv;  // node of this wave's LDS histogram (wave-uniform)
     auto flush = [&]() {
-        __syncthreads();
-        for (int j = threadIdx.x; j < 96; j += kBlock) {
-            if (!s_cnt[j]) continue;
+        for (int j = lane; j < 96; j += 64) {
+            if (!hc[j]) continue;
             const uint64_t g = (uint64_t)cur * 96 + j;
-            atomicAdd(&bcnt[g], s_cnt[j]);
+            atomicAdd(&bcnt[g], hc[j]);
             for (int a = 0; a < 3; a++) {
-                atomicMin(&bmin[g * 3 + a], s_min[j * 3 + a]);
-                atomicMax(&bmax[g * 3 + a], s_max[j * 3 + a]);
+                atomicMin(&bmin[g * 3 + a], hmn[j * 3 + a]);
+                atomicMax(&bmax[g * 3 + a], hmx[j * 3 + a]);
             }
         }
-        __syncthreads();
     };
-    for (int r = 0; r < kIPT; r++) {
-        const uint32_t c0 = b0 + r * kBlock;
+    for (int r = 0; r < (int)(kSpan / NWV / 64); r++) {
+        const uint32_t c0 = w0 + r * 64;
         if (c0 >= n) break;
-        const uint32_t ta = seg[c0], tb = seg[min(n, c0 + kBlock) - 1];
+        const uint32_t ta = seg[c0], tb = seg[min(n, c0 + 64) - 1];
         const bool uniform = ta != kInv && ta == tb;
         if (uniform && ta != cur) {
             if (cur != kInv) flush();
-            for (int j = threadIdx.x; j < 288; j += kBlock) {
-                s_min[j] = 0xFFFFFFFFu;
-                s_max[j] = 0;
-                if (j < 96) s_cnt[j] = 0;
+            for (int j = lane; j < 288; j += 64) {
+                hmn[j] = 0xFFFFFFFFu;
+                hmx[j] = 0;
+                if (j < 96) hc[j] = 0;
             }
-            __syncthreads();
             cur = ta;
         }
-        const uint32_t i = c0 + threadIdx.x;
+        const uint32_t i = c0 + lane;
         const uint32_t t = i < n ? seg[i] : kInv;
         if (t == kInv) continue;
         const Dec d = dec[t];
@@ -308,10 +311,10 @@ __global__ __launch_bounds__(kBlock) void k_bin(const Item* __restrict__ items, 
             const int b = min((int)d.nbins - 1, (int)((it.c[ax] - d.lo[ax]) * d.scale[ax]));
             const uint32_t slot = ax * 32 + b;
             if (uniform) {
-                atomicAdd(&s_cnt[slot], 1u);
+                atomicAdd(&hc[slot], 1u);
                 for (int a = 0; a < 3; a++) {
-                    atomicMin(&s_min[slot * 3 + a], v[a]);
-                    atomicMax(&s_max[slot * 3 + a], v[3 + a]);
+                    atomicMin(&hmn[slot * 3 + a], v[a]);
+                    atomicMax(&hmx[slot * 3 + a], v[3 + a]);
                 }
             } else {
                 const uint64_t g = (uint64_t)t * 96 + slot;
