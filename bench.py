@@ -5,21 +5,29 @@ A step is one frame at fixed SPP (adaptive sampling off): every camera sample
 of the frame traced to termination, NEE shadow rays included, and the film
 gathered (+ the RCCL reduce onto rank 0 for N > 1).  One ray = one BVH query
 (Scene::Intersect or Scene::IntersectPred), counted as the reference does
-(SURVEY.md §8d).  Default workload = configs[1] (C2: Cornell box, 1024x1024,
-256 SPP, SimplePath, maxDepth 8).  Inputs (scene, BVH) are resident in HBM
+(SURVEY.md §8d).  Default workload = C4 (configs[3]: San-Miguel-class
+procedural scene, ~10 M triangles, 1920x1080, 1024 SPP, PathIntegrator,
+maxDepth 128) — BASELINE.json publishes no number, so the headline is the
+largest single-GPU configuration.  Inputs (scene, BVH) are resident in HBM
 before the timed region.
 
-  python bench.py [--gpus N --steps K --warmup W --config c2|c3|c1|c4]
+  python bench.py [--gpus N --steps K --warmup W --config c4|c2|c3|c1|...]
 
-For N > 1 the driver launches one rank per GPU (torch.distributed, RCCL);
-samples are interleaved across ranks (s % N == rank), the per-rank films are
-summed onto rank 0 with dist.reduce; value = all ranks' rays / max-rank time.
+--gpus N without a torch.distributed environment starts N ranks itself
+(torch.distributed.run, one process per GPU) before anything touches the GPU;
+under the driver's own launcher (WORLD_SIZE set) it checks WORLD_SIZE == N.
+Samples are interleaved across ranks (s % N == rank), the per-rank films are
+summed onto rank 0 with dist.reduce (RCCL); value = all ranks' rays / max-rank
+time.  Total work per frame is fixed as N grows ("scaling": "strong").
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -28,6 +36,9 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+# configurations whose BVH + primitive slots exceed the 256 MiB Infinity Cache:
+# their traversal bytes stream from HBM.  The small scenes live in L2/MALL.
+HBM_CONFIGS = ("c4",)
 
 
 def build_setup(config: str, spp: int | None = None):
@@ -65,13 +76,37 @@ WORKLOADS = {
 }
 
 
+def src_sha() -> str:
+    """Hash of the sources libpt_hip.so is built from (csrc/ + the C ABI
+    header): ties a committed counter profile to the binary being benched
+    (.git does not travel to the GPU box)."""
+    h = hashlib.sha256()
+    files = sorted((ROOT / "pathtracing_amd" / "csrc").glob("*")) + [ROOT / "include" / "pt_api.h"]
+    for p in files:
+        if p.is_file():
+            h.update(p.name.encode())
+            h.update(p.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def _json(path: Path):
+    try:
+        return json.loads(path.read_text())
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(setup, target_s: float = 15.0):
     """The oracle (CPU restatement, 'port') on the host cores, on a bounded
     sample of the same workload: full frame at a reduced SPP sized from a
-    pilot run to take about target_s seconds."""
+    pilot run to take about target_s seconds.  The port/reference speed ratio
+    measured in the build container (tools/cpu_ratio.py, where the reference
+    itself compiles; it cannot travel to the GPU box) rides along."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    nproc = os.cpu_count() or 1
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    threads = max(1, min(16, affinity))
     integ = setup.make_integrator()
     W, H = setup.camera.GetFilm().Resolution()
     t0 = time.perf_counter()
@@ -85,33 +120,72 @@ def cpu_baseline(setup, target_s: float = 15.0):
     else:
         dt = pilot
     rays = cnt["closest"] + cnt["any"]
-    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/pt_oracle.c, same scene {W}x{H} at {spp} spp ({rays} rays in {dt:.1f} s, "
-                      f"{threads} threads)"}
+    out = {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+           "nproc": nproc, "affinity": affinity,
+           "sample": f"oracle/pt_oracle.c, same scene {W}x{H} at {spp} spp ({rays} rays in {dt:.1f} s, "
+                     f"{threads} threads; the box's cpu budget is 16 threads)"}
+    ratio = _json(ROOT / "profiles" / "r02_cpu_ratio.json")
+    if ratio:
+        out["port_vs_reference"] = ratio.get("summary")
+    return out
 
 
-def pmc_traffic(config: str, spp: int, world: int):
-    """HBM bytes per k_closest launch from the committed rocprofv3 counter
-    summary of this workload (tools/profile_pmc.sh + tools/pmc_summary.py,
-    profiles/*_<config>_pmc.json): FETCH_SIZE doubled (gfx950 reports half
-    of 16-byte-per-lane reads, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, both
-    in KB per dispatch.  None when no profile of this configuration exists."""
+def pmc_traffic(config: str, spp: int, world: int, kernel: str, sha: str):
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 counter
+    summary of this workload AND this build (profiles/r02_<config>_pmc.json,
+    written by tools/profile_r02.sh; `_meta.src_sha` must equal the sources
+    being benched).  FETCH_SIZE is scaled by the factor calibrated on this
+    kernel's own access pattern (profiles/r02_fetch_calib.json: one 128-B
+    node per lane as 8 x 16-B loads, known byte count), WRITE_SIZE is exact
+    for 16-B stores (MI355X_MICROARCH.md "HBM").  Returns (bytes|None, info)."""
     import glob
-    cands = sorted(glob.glob(str(ROOT / "profiles" / f"*_{config}_pmc.json")))
-    for path in reversed(cands):
-        try:
-            prof = json.load(open(path))
-        except (OSError, ValueError):
+    calib = _json(ROOT / "profiles" / "r02_fetch_calib.json") or {}
+    factor = calib.get("factor_node_gather")
+    info = {"fetch_factor": factor, "fetch_factor_source": "r02_fetch_calib.json" if factor else None}
+    for path in sorted(glob.glob(str(ROOT / "profiles" / f"r*_{config}_pmc.json")), reverse=True):
+        prof = _json(Path(path))
+        if not prof:
             continue
         meta = prof.get("_meta", {})
         if meta.get("spp") != spp or meta.get("n_gpus", 1) != world:
             continue
-        k = prof.get(meta.get("kernel", "k_closest<false>"), {})
+        k = prof.get(kernel, {})
         if "FETCH_SIZE_per_dispatch" not in k:
             continue
-        b = (2.0 * k["FETCH_SIZE_per_dispatch"] + k.get("WRITE_SIZE_per_dispatch", 0.0)) * 1024.0
-        return round(b), Path(path).name
-    return None, None
+        info["traffic_source"] = Path(path).name
+        info["traffic_src_sha"] = meta.get("src_sha")
+        if meta.get("src_sha") != sha:
+            info["traffic_note"] = "newest counter profile is of another build; traffic not reported"
+            return None, info
+        if factor is None:
+            info["traffic_note"] = "no FETCH_SIZE calibration for this access pattern"
+            return None, info
+        b = (factor * k["FETCH_SIZE_per_dispatch"] + k.get("WRITE_SIZE_per_dispatch", 0.0)) * 1024.0
+        info["traffic_raw_fetch_kb"] = round(k["FETCH_SIZE_per_dispatch"], 1)
+        return round(b), info
+    info["traffic_note"] = "no counter profile of this workload"
+    return None, info
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """Start n ranks of this script (one per GPU) as children; nothing in this
+    process has touched the GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(Path(__file__).resolve()),
+           *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def log(msg: str):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
 def main():
@@ -119,14 +193,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c2")
+    ap.add_argument("--config", default="c4")
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--paths-in-flight", type=int, default=0)
     ap.add_argument("--traversal", choices=("auto", "pool", "simple"), default="auto",
                     help="BVH traversal kernel (auto: by BVH size)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-count", action="store_true", help="skip the instrumented node-count pass")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
@@ -136,18 +214,25 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == args.gpus
     device = local if world > 1 else 0
     torch.cuda.set_device(device)
 
+    t_setup = time.perf_counter()
     setup = build_setup(args.config, args.spp)
     integ = setup.make_integrator()
     W, H = setup.camera.GetFilm().Resolution()
     film = torch.zeros((H, W, 4), dtype=torch.float64, device=f"cuda:{device}")
-    ctx = integ.context(device)
-    ctx.set_stream(torch.cuda.current_stream(device).cuda_stream)
+    integ.context(device)  # scene upload
+    torch.cuda.synchronize(device)
+    setup_s = time.perf_counter() - t_setup
+    if rank == 0:
+        log(f"{args.config}: scene + BVH + upload {setup_s:.1f} s, {world} rank(s)")
 
     tflag = {"auto": 0, "pool": N.PT_RENDER_TRAVERSAL_POOL, "simple": N.PT_RENDER_TRAVERSAL_SIMPLE}[args.traversal]
 
@@ -156,27 +241,37 @@ def main():
         # reduce of the film onto rank 0 (pathtracing_amd/distributed.py)
         return render_frame(integ, film, flags=flags | tflag, paths_in_flight=args.paths_in_flight)
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
+        t0 = time.perf_counter()
         step()
-    # traversal work per closest-hit ray (untimed, instrumented pass over the
-    # first spp/16 samples of every pixel: same scene, same sample stream)
-    count_spp = max(1, setup.spp // 16)
-    integ.sampler.samples = count_spp
-    cst = step(N.PT_RENDER_COUNT_NODES)
-    integ.sampler.samples = setup.spp
-    nodes_per_ray = cst["nodes_closest"] / max(1, cst["rays_closest"])
-    tris_per_ray = cst["tris_closest"] / max(1, cst["rays_closest"])
-    bytes_per_ray = 128.0 * nodes_per_ray + 48.0 * tris_per_ray
+        if rank == 0:
+            log(f"warmup {i + 1}/{args.warmup}: {time.perf_counter() - t0:.2f} s")
+    # traversal work per ray (untimed, instrumented pass over the first spp/16
+    # samples of every pixel: same scene, same sample stream)
+    bytes_closest = bytes_any = None
+    cst = {}
+    if not args.no_count:
+        count_spp = max(1, setup.spp // 16)
+        integ.sampler.samples = count_spp
+        cst = step(N.PT_RENDER_COUNT_NODES)
+        integ.sampler.samples = setup.spp
+        bytes_closest = (128.0 * cst["nodes_closest"] + 48.0 * cst["tris_closest"]) / max(1, cst["rays_closest"])
+        if cst["rays_any"]:
+            bytes_any = (128.0 * cst["nodes_any"] + 48.0 * cst["tris_any"]) / cst["rays_any"]
 
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    totals = {"rays_closest": 0, "rays_any": 0, "ms_closest": 0.0, "launches_closest": 0, "paths": 0}
-    for _ in range(args.steps):
+    totals = {"rays_closest": 0, "rays_any": 0, "ms_closest": 0.0, "ms_any": 0.0, "ms_shade": 0.0,
+              "launches_closest": 0, "launches_any": 0, "paths": 0}
+    for i in range(args.steps):
+        ts = time.perf_counter()
         st = step(N.PT_RENDER_TIMING)
         for k in totals:
             totals[k] += st[k]
+        if rank == 0:
+            log(f"step {i + 1}/{args.steps}: {time.perf_counter() - ts:.2f} s")
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
@@ -192,10 +287,41 @@ def main():
     total_rays = float(rays.item())
 
     if rank == 0:
-        avg_ms = totals["ms_closest"] / max(1, totals["launches_closest"])
-        launch_bytes = bytes_per_ray * totals["rays_closest"] / max(1, totals["launches_closest"])
-        achieved = launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        traffic, traffic_src = pmc_traffic(args.config, setup.spp, world)
+        pool = args.traversal == "pool" or (args.traversal == "auto" and args.config in HBM_CONFIGS)
+        kname = "k_closest_pool<false, false>" if pool else "k_closest<false, false>"
+        sname = "k_shadow_pool<false, false>" if pool else "k_shadow<false, false>"
+        sha = src_sha()
+
+        def kernel_roof(name, bpr, ms, launches, nrays):
+            avg_ms = ms / max(1, launches)
+            if bpr is None or avg_ms <= 0:
+                return None
+            launch_bytes = bpr * nrays / max(1, launches)
+            achieved = launch_bytes / (avg_ms * 1e-3) / 1e9
+            return {"kernel": name, "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "bytes_per_ray": round(bpr, 1), "bytes_per_launch": round(launch_bytes),
+                    "avg_launch_ms": round(avg_ms, 4), "launches": launches}
+
+        rc = kernel_roof(kname, bytes_closest, totals["ms_closest"], totals["launches_closest"],
+                         totals["rays_closest"])
+        ra = kernel_roof(sname, bytes_any, totals["ms_any"], totals["launches_any"], totals["rays_any"])
+        traffic, tinfo = pmc_traffic(args.config, setup.spp, world, kname, sha)
+        roof = {"bound": "hbm" if args.config in HBM_CONFIGS else "l2/latency",
+                "achieved": rc["achieved"] if rc else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": rc["frac"] if rc else None, "traffic": traffic,
+                "traffic_frac": (round(traffic / (rc["avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                 if traffic and rc else None),
+                "src_sha": sha, **tinfo}
+        if rc:
+            roof.update({"kernel": kname, "bytes_per_ray": rc["bytes_per_ray"],
+                         "nodes_per_ray": round(cst["nodes_closest"] / max(1, cst["rays_closest"]), 2),
+                         "tris_per_ray": round(cst["tris_closest"] / max(1, cst["rays_closest"]), 2),
+                         "avg_launch_ms": rc["avg_launch_ms"], "launches": rc["launches"],
+                         "bytes_per_launch": rc["bytes_per_launch"]})
+        if ra:
+            ra["nodes_per_ray"] = round(cst["nodes_any"] / max(1, cst["rays_any"]), 2)
+            ra["tris_per_ray"] = round(cst["tris_any"] / max(1, cst["rays_any"]), 2)
+            roof["shadow"] = ra
         out = {
             "metric": "Mrays/s",
             "value": round(total_rays / elapsed_max / 1e6, 3),
@@ -211,13 +337,10 @@ def main():
             "data": "synthetic",
             "config": {"workload": WORKLOADS.get(args.config, args.config), "width": W, "height": H,
                        "spp": setup.spp, "max_depth": setup.max_depth, "integrator": setup.integrator,
-                       "rays_per_step": int(total_rays / args.steps), "parallelism": f"sample-shard x{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "k_closest (BVH4 closest-hit traversal)",
-                         "bytes_per_ray": round(bytes_per_ray, 1), "nodes_per_ray": round(nodes_per_ray, 2),
-                         "tris_per_ray": round(tris_per_ray, 2), "avg_launch_ms": round(avg_ms, 4),
-                         "launches": totals["launches_closest"]},
+                       "rays_per_step": int(total_rays / args.steps), "parallelism": f"sample-shard x{world}",
+                       "world_size": dist.get_world_size() if world > 1 else 1,
+                       "setup_s": round(setup_s, 1)},
+            "roofline": roof,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(build_setup(args.config, args.spp), args.cpu_seconds)

@@ -49,13 +49,19 @@ def render_frame(integrator, film: torch.Tensor, *, flags: int = 0, paths_in_fli
     if film.dtype != torch.float64 or tuple(film.shape) != (fh, fw, 4) or not film.is_contiguous():
         raise ValueError(f"film must be a contiguous float64 ({fh}, {fw}, 4) tensor, got "
                          f"{tuple(film.shape)} {film.dtype}")
-    film.zero_()
     if render_shard is None:
         if film.device.type != "cuda":
             raise ValueError("the HIP renderer accumulates into device memory: pass a cuda film tensor")
-        st = integrator.Render(device=film.device.index or 0, shard_index=rank, shard_count=n,
+        dev = film.device.index or 0
+        # the library's launches go on torch's current stream of the film's
+        # device, so they are ordered after zero_() and after any earlier
+        # collective that wrote into the same tensor
+        integrator.context(dev).set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        film.zero_()
+        st = integrator.Render(device=dev, shard_index=rank, shard_count=n,
                                film_ptr=film.data_ptr(), flags=flags, paths_in_flight=paths_in_flight)
     else:
+        film.zero_()
         st = render_shard(rank, n, film)
     if n > 1:
         dist.reduce(film, dst=dst, op=dist.ReduceOp.SUM, group=group)

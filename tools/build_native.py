@@ -62,6 +62,15 @@ def build_product(force: bool = False, variant: str = "", defines=()) -> Path:
     return out
 
 
+def build_tools() -> None:
+    """Measurement helpers run on the GPU box (tools/_bin/, git-ignored)."""
+    src = ROOT / "tools" / "fetch_calib.hip"
+    out = ROOT / "tools" / "_bin" / "fetch_calib"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    if _stale(out, [src]):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", src, "-o", out])
+
+
 def build_oracle() -> Path:
     _run(["make", "-s", "-C", ROOT / "oracle"])
     return ROOT / "oracle" / "_build" / "liboracle.so"
@@ -88,6 +97,7 @@ def main(argv=None):
             build_product(True, name, [d for d in defs.split(",") if d])
         return
     build_product(force)
+    build_tools()
     build_oracle()
     if "--no-ref" not in argv:
         build_reference_harness()

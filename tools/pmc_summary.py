@@ -2,7 +2,7 @@
 and per-dispatch averages of each PMC counter (FETCH_SIZE/WRITE_SIZE in KB as
 rocprofv3 reports them).  Writes JSON + prints a table.
 
-    python tools/pmc_summary.py <profile dir> <out.json> [config spp kernel]
+    python tools/pmc_summary.py <profile dir> <out.json> [config spp kernel [src_sha]]
 
 With the optional workload fields the JSON carries a "_meta" record that
 bench.py uses to attach the counter traffic to its roofline line.
@@ -51,4 +51,6 @@ if __name__ == "__main__":
     meta = None
     if len(sys.argv) > 5:
         meta = {"config": sys.argv[3], "spp": int(sys.argv[4]), "kernel": sys.argv[5], "n_gpus": 1}
+        if len(sys.argv) > 6:
+            meta["src_sha"] = sys.argv[6]
     main(sys.argv[1], sys.argv[2], meta)
