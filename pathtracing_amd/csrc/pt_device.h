@@ -39,8 +39,8 @@ struct alignas(16) DevGeom {
 // Instances (TransformedPrimitive, Primitive.cpp:32-72).  A TLAS leaf slot of
 // an instance is encoded like a BLAS hop whose pushed ref is
 // REF_INST_ENTER | slot; popping it takes the lane's ray to object space
-// (state saved in a per-lane scratch row) and pushes REF_INST_EXIT, which
-// restores the world ray when the instance's BLAS is done.  Node refs stay
+// (state saved in a per-lane scratch row) and records the stack depth; the
+// world ray is restored (REF_INST_EXIT step) when the instance's BLAS is done.  Node refs stay
 // below REF_LEAF and leaf slots below 2^30, so refs >= REF_SPECIAL are free.
 #define REF_SPECIAL 0xC0000000u
 #define REF_INST_ENTER 0xC0000000u
@@ -49,6 +49,7 @@ struct alignas(16) DevGeom {
 #define OCT_MASK 7u
 #define OCT_INST 8u   // the lane's ray is in an instance's object space
 #define OCT_HIT 16u   // ... and accepted a hit there
+#define OCT_SP_SHIFT 8  // ... entered at this stack depth (bits 8-13)
 #define SCR_WORDS 9   // scratch row: world o, d, tmax, length, instance
 struct DevInstance {
     float T[16], inv[16];  // glm column-major transform and inverse

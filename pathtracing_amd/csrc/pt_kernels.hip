@@ -143,6 +143,16 @@ __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, flo
 #else
 #define PT_POOL_WAVES
 #endif
+// the any-hit pool kernel's own budget (it needs fewer registers: no octant
+// order, no hit record)
+#ifndef PT_SHADOW_WPE
+#define PT_SHADOW_WPE PT_POOL_WPE
+#endif
+#if PT_SHADOW_WPE
+#define PT_SHADOW_WAVES __attribute__((amdgpu_waves_per_eu(PT_SHADOW_WPE, PT_SHADOW_WPE)))
+#else
+#define PT_SHADOW_WAVES
+#endif
 // Persistent, refilling traversal (pt_pool.h): grid = resident blocks, rays
 // claimed from the pool counters (zeroed with the queue counters).
 struct ClosestSrc {
@@ -168,13 +178,14 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_closest_pool(P
                                                                 uint32_t* __restrict__ ovf, uint32_t* __restrict__ spare,
                                                                 uint32_t* __restrict__ snap,
                                                                 unsigned long long* counters) {
-    __shared__ uint32_t s_ref[PT_POOL_LDS * PT_TRACE_BLOCK];
+    __shared__ uint32_t s_ref[PT_POOL_LDS_C * PT_TRACE_BLOCK];
+    __shared__ uint16_t s_ent[PT_ENTRY ? PT_POOL_LDS_C * PT_TRACE_BLOCK : 1];
     iteration_prologue(nptr, spare, snap);
     const uint32_t n = path_count(nptr);
     if (n == 0) return;
     TraceWork wk{0, 0};
     ClosestSrc src{P, hit, nptr[Q_NEXT]};
-    trace_pool<false, COUNT, ClosestSrc, true, INST>(n, pool, src, s_ref, ovf, wk);
+    trace_pool<false, COUNT, ClosestSrc, true, INST>(n, pool, src, s_ref, s_ent, ovf, wk);
     if (COUNT) {
         count_add(counters, CNT_NODES_CLOSEST, wk.nodes);
         count_add(counters, CNT_TRIS_CLOSEST, wk.tris);
@@ -216,7 +227,7 @@ struct ShadowSrc {
 };
 
 template <bool COUNT, bool INST>
-__global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_shadow_pool(PathSoA next, float* __restrict__ sample_L,
+__global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SHADOW_WAVES void k_shadow_pool(PathSoA next, float* __restrict__ sample_L,
                                                                const ShadowRec* __restrict__ sq,
                                                                const uint32_t* __restrict__ nptr,
                                                                uint32_t* __restrict__ pool, uint32_t* __restrict__ ovf,
@@ -226,7 +237,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_shadow_pool(Pa
     ShadowSrc src{sq, next, sample_L};
     const uint32_t n = *nptr;
     if (n == 0) return;
-    trace_pool<true, COUNT, ShadowSrc, true, INST>(n, pool, src, s_ref, ovf, wk);
+    trace_pool<true, COUNT, ShadowSrc, true, INST>(n, pool, src, s_ref, nullptr, ovf, wk);
     if (COUNT) {
         count_add(counters, CNT_NODES_ANY, wk.nodes);
         count_add(counters, CNT_TRIS_ANY, wk.tris);
@@ -267,8 +278,9 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SIMPLE_WAVES void k_closest(Path
     if (blockIdx.x * PT_TRACE_BLOCK >= n) return;
     TraceWork wk{0, 0};
 #if PT_SIMPLE_STEP
+    __shared__ uint16_t s_ent[PT_SIMPLE_LDS * PT_TRACE_BLOCK];
     ClosestSrc src{P, hit, nptr[Q_NEXT]};
-    trace_pool<false, COUNT, ClosestSrc, false, INST>(n, nullptr, src, s_ref, ovf, wk);
+    trace_pool<false, COUNT, ClosestSrc, false, INST, PT_SIMPLE_LDS>(n, nullptr, src, s_ref, s_ent, ovf, wk);
 #else
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     if (i < n) {
@@ -297,7 +309,8 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SIMPLE_WAVES void k_shadow(PathS
     TraceWork wk{0, 0};
     ShadowSrc src{sq, next, sample_L};
 #if PT_SIMPLE_STEP
-    if (blockIdx.x * PT_TRACE_BLOCK < n) trace_pool<true, COUNT, ShadowSrc, false, INST>(n, nullptr, src, s_ref, ovf, wk);
+    if (blockIdx.x * PT_TRACE_BLOCK < n)
+        trace_pool<true, COUNT, ShadowSrc, false, INST, PT_SIMPLE_LDS>(n, nullptr, src, s_ref, nullptr, ovf, wk);
 #else
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     if (i < n) {
@@ -332,10 +345,11 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(const pt_ray* __r
                                                               pt_hit* __restrict__ out, uint32_t* __restrict__ pool,
                                                               uint32_t* __restrict__ ovf, unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_POOL_LDS * PT_TRACE_BLOCK];
+    __shared__ uint16_t s_ent[PT_POOL_LDS_C * PT_TRACE_BLOCK];
     TraceWork wk{0, 0};
     RaysSrc src{rays, out};
-    if (any) trace_pool<true, true>(n, pool, src, s_ref, ovf, wk);
-    else trace_pool<false, true>(n, pool, src, s_ref, ovf, wk);
+    if (any) trace_pool<true, true>(n, pool, src, s_ref, nullptr, ovf, wk);
+    else trace_pool<false, true>(n, pool, src, s_ref, s_ent, ovf, wk);
     count_add(counters, any ? CNT_NODES_ANY : CNT_NODES_CLOSEST, wk.nodes);
     count_add(counters, any ? CNT_TRIS_ANY : CNT_TRIS_CLOSEST, wk.tris);
 }

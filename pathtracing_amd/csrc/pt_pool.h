@@ -41,20 +41,49 @@ __device__ unsigned int pt_diag[4];
 #define PT_REFILL 8
 #endif
 
+// Closest-hit pool kernels keep each stack entry's entry distance (BVH4::
+// Intersect's entryDist[], BVH.hpp:1128-1135) and drop a popped node or leaf
+// whose entry exceeds the current max without fetching it.  In LDS the
+// distance is the float's upper 16 bits (truncated toward zero, so never
+// above the true entry: a node is dropped only when the reference drops it);
+// entries past the LDS part keep the full float in the overflow array.
+// PT_POOL_LDS_C: stack entries in LDS for those kernels (4 + 2 B each, so
+// 14 entries per lane keep 14 blocks = 28 waves per CU within 160 KiB).
+// Off by default: on C4 it drops only 5 % of the node fetches (32.9 -> 31.3
+// per ray) and the shorter LDS stack and extra registers (spills at 72
+// VGPRs) cost more: 844 -> 676 Mrays/s (gpurun_out/r2b, profiles/r02_ab_c4.txt).
+#ifndef PT_ENTRY
+#define PT_ENTRY 0
+#endif
+#ifndef PT_POOL_LDS_C
+#define PT_POOL_LDS_C (PT_ENTRY ? 14 : PT_POOL_LDS)
+#endif
+// Leaf steps test up to two primitives of the leaf (consecutive 48-B slots,
+// one 96-B read), so a two-triangle leaf costs one memory round trip.
+// Off by default: at 72 VGPRs the second test spills inside the step loop,
+// 844 -> 711 Mrays/s on C4 (same A/B).
+#ifndef PT_LEAF2
+#define PT_LEAF2 0
+#endif
+// overflow words per stack entry per lane (ref + entry distance)
+#define PT_OVF_WORDS 2
+
 // Src interface:
 //   bool load(uint32_t ri, f3& o, f3& d, float& tmax)   (false: skip this ray)
 //   void closest(uint32_t ri, float t, float b1, float b2, int prim)
 //   void any(uint32_t ri, bool hit)
 // POOL = false: no refill, lane i of the grid traces ray i (small scenes,
 // where traversal lengths are uniform and the claims would only cost).
-template <bool ANY, bool COUNT, class Src, bool POOL = true, bool INST = true>
-__device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, uint32_t* s_ref,
+// LN: stack entries in LDS (s_ref, and s_ent for closest hit with PT_ENTRY);
+// the rest in ovf ([entry][grid lane] refs, then as many entry distances).
+template <bool ANY, bool COUNT, class Src, bool POOL = true, bool INST = true,
+          int LN = (ANY ? PT_POOL_LDS : PT_POOL_LDS_C)>
+__device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, uint32_t* s_ref, uint16_t* s_ent,
                            uint32_t* __restrict__ ovf, TraceWork& wk) {
+    constexpr bool ENT = PT_ENTRY && !ANY;
     const uint32_t lane = threadIdx.x;
-    // LDS part of the stack; the rest in ovf ([entry][grid lane]; the runtime
-    // sizes it for the larger of the pool grid and the one-ray-per-lane grid)
-    constexpr int LN = PT_POOL_LDS;
     const uint32_t gl = blockIdx.x * PT_TRACE_BLOCK + lane, G = gridDim.x * PT_TRACE_BLOCK;
+    uint32_t* __restrict__ ovf_e = ovf + (size_t)(PT_STACK - LN) * G;
     const uint32_t wl = __lane_id();
     const uint32_t cs = (n + PT_POOL_CHUNKS - 1) / PT_POOL_CHUNKS;
     const uint32_t home = blockIdx.x % PT_POOL_CHUNKS;
@@ -67,26 +96,46 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
     int sp = 0, best = -1;
 
     const uint32_t all_dead = (1u << PT_POOL_CHUNKS) - 1u;
-    // pushes beyond PT_STACK are dropped, like the one-ray-per-lane kernels
-    auto push = [&](uint32_t v) {
+    // pushes beyond PT_STACK are dropped, like the one-ray-per-lane kernels;
+    // e < 0: never dropped at pop (BLAS roots: a fresh traversal, entry 0)
+    auto push = [&](uint32_t v, float e = -1.0f) {
         if (sp < PT_STACK) {
-            if (LN >= PT_STACK || sp < LN) s_ref[sp * PT_TRACE_BLOCK + lane] = v;
-            else ovf[(size_t)(sp - LN) * G + gl] = v;
+            if (LN >= PT_STACK || sp < LN) {
+                s_ref[sp * PT_TRACE_BLOCK + lane] = v;
+                if (ENT) s_ent[sp * PT_TRACE_BLOCK + lane] = (uint16_t)(__float_as_uint(e) >> 16);
+            } else {
+                ovf[(size_t)(sp - LN) * G + gl] = v;
+                if (ENT) ovf_e[(size_t)(sp - LN) * G + gl] = __float_as_uint(e);
+            }
             ++sp;
         }
     };
-    auto pop = [&]() -> uint32_t {
+    // pop; false: the popped entry lies beyond the current max (ENT only)
+    auto pop = [&](uint32_t& r) -> bool {
         --sp;
-        if (LN >= PT_STACK || sp < LN) return s_ref[sp * PT_TRACE_BLOCK + lane];
-        return ovf[(size_t)(sp - LN) * G + gl];
+        float e = -1.0f;
+        if (LN >= PT_STACK || sp < LN) {
+            r = s_ref[sp * PT_TRACE_BLOCK + lane];
+            if (ENT) e = __uint_as_float((uint32_t)s_ent[sp * PT_TRACE_BLOCK + lane] << 16);
+        } else {
+            r = ovf[(size_t)(sp - LN) * G + gl];
+            if (ENT) e = __uint_as_float(ovf_e[(size_t)(sp - LN) * G + gl]);
+        }
+        return !(ENT && e > tmax);
+    };
+    auto start = [&]() {
+        inv = inv_dir(d);
+        oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
+        ref = S.root;
+        sp = 0;
+        best = -1;
+        bb1 = bb2 = 0;
     };
     if (!POOL) {
         const uint32_t gi = blockIdx.x * PT_TRACE_BLOCK + lane;
         if (gi < n && src.load(gi, o, d, tmax)) {
             ri = (int)gi;
-            inv = inv_dir(d);
-            oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
-            ref = S.root;
+            start();
         }
     }
     for (;;) {
@@ -124,16 +173,8 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                     const uint32_t k = (uint32_t)__popcll(idle & ((1ull << wl) - 1ull));
                     if (k < got) {
                         ri = (int)(base + k);
-                        if (src.load((uint32_t)ri, o, d, tmax)) {
-                            inv = inv_dir(d);
-                            oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
-                            ref = S.root;
-                            sp = 0;
-                            best = -1;
-                            bb1 = bb2 = 0;
-                        } else {
-                            ri = -1;
-                        }
+                        if (src.load((uint32_t)ri, o, d, tmax)) start();
+                        else ri = -1;
                     }
                 }
             }
@@ -141,18 +182,33 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         }
         if (ri < 0) continue;
 
-        // ---- one step of this lane's traversal: one cluster or ONE leaf
-        // primitive.  Node lanes and primitive lanes issue their loads in the
-        // same pass (one memory round trip per step for the whole wave);
-        // a leaf is walked one primitive per step (ref = REF_LEAF | next slot).
+        // ---- one step of this lane's traversal: one cluster or one leaf step
+        // (one or two primitives).  Node lanes and primitive lanes issue their
+        // loads in the same pass (one memory round trip per step for the whole
+        // wave); a leaf continues at ref = REF_LEAF | next slot.
         if (ref == REF_EMPTY) {
-            if (sp == 0) {  // finished: no hit (any) / closest result
+            bool finished = false;
+            for (;;) {
+                if (INST && PT_INSTANCE_DONE()) {  // back at the depth the instance was entered at
+                    ref = REF_INST_EXIT;
+                    break;
+                }
+                if (sp == 0) {
+                    finished = true;
+                    break;
+                }
+                uint32_t r;
+                if (pop(r)) {
+                    ref = r;
+                    break;
+                }
+            }
+            if (finished) {  // no hit (any) / closest result
                 if (ANY) src.any((uint32_t)ri, false);
                 else src.closest((uint32_t)ri, tmax, bb1, bb2, best);
                 ri = -1;
                 continue;
             }
-            ref = pop();
         }
         if (INST && ref >= REF_SPECIAL) {  // instance enter / exit (pt_trace.h instance_step)
             PT_INSTANCE_STEP(ANY);
@@ -168,18 +224,22 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         }
 #endif
         // all eight loads issue before any use: a primitive lane reads its
-        // 48-byte slot and repeats its first 16 bytes for the node-only words
-        // (same line, no extra traffic), and the cluster test below runs
+        // 48-byte slot and the next one (PT_LEAF2; the slot array has a pad
+        // slot at its end) and repeats its first 16 bytes for the node-only
+        // words (same line, no extra traffic), and the cluster test below runs
         // unconditionally (its result masked off on primitive lanes) so the
         // compiler cannot sink the node loads behind the primitive branch
         const float4* __restrict__ q = node_step ? reinterpret_cast<const float4*>(S.nodes + idx)
                                                  : reinterpret_cast<const float4*>(S.geom + idx);
         const uint32_t nk = node_step ? 1u : 0u;
+        constexpr uint32_t pk = PT_LEAF2 ? 1u : 0u;
+        const uint32_t k3 = 3u * (nk | pk);
         const float4 q0 = q[0], q1 = q[1], q2 = q[2];
-        const float4 q3 = q[3 * nk], q4 = q[4 * nk], q5 = q[5 * nk], q6 = q[6 * nk], q7 = q[7 * nk];
+        const float4 q3 = q[k3], q4 = q[k3 ? 4u : 0u], q5 = q[k3 ? 5u : 0u], q6 = q[6 * nk], q7 = q[7 * nk];
         {
             uint32_t mask;
-            slab4p(q0, q1, q2, q3, q4, q5, o, inv, tmax, mask);
+            float te[4];
+            slab4pe(q0, q1, q2, q3, q4, q5, o, inv, tmax, mask, te);
             if (!node_step) mask = 0;  // no children on primitive lanes
             // visit order: slot order for any hit (BVH.hpp:1099-1102), octant
             // order far -> near for closest hit (BVH4::LUT, BVH.hpp:1195-1204)
@@ -188,34 +248,38 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 const uint32_t ow = __float_as_uint(((oct >> 2) & 1u) ? q7.y : q7.x);
                 perm = (ow >> (8 * (oct & 3))) & 0xFFu;
             }
-            const uint32_t cand = order_children(mask, make_uint4(__float_as_uint(q6.x), __float_as_uint(q6.y),
-                                                                  __float_as_uint(q6.z), __float_as_uint(q6.w)),
-                                                 perm, push);
+            const uint4 ch = make_uint4(__float_as_uint(q6.x), __float_as_uint(q6.y), __float_as_uint(q6.z),
+                                        __float_as_uint(q6.w));
+            uint32_t cand;
+            if (ENT) cand = order_children_e(mask, ch, perm, te, push);
+            else cand = order_children(mask, ch, perm, [&](uint32_t v) { push(v); });
             if (node_step) {
                 if (COUNT) wk.nodes++;
                 ref = cand;
                 continue;
             }
         }
-        // one leaf primitive at slot idx
+        // leaf primitives at slot idx (and idx + 1)
         {
             const uint32_t slot = idx;
             const uint32_t w0 = __float_as_uint(q0.w);
             const uint32_t kind = w0 & GF_KIND;
             bool anyhit = false;
-            if (COUNT) wk.tris++;
-            if (kind == PT_PRIM_TRIANGLE) {
-                if (ANY && !(w0 & GF_PRED_GLM)) {
-                    if (tri_pred(o, d, xyz(q0), xyz(q1), xyz(q2), tmax)) anyhit = true;
+            // one triangle of the leaf: Intersect (glm) or IntersectPred
+            // semantics + the material alpha test (Primitive.cpp:6-26)
+            auto tri = [&](uint32_t sl, uint32_t w, float4 a, float4 b, float4 c) {
+                if (COUNT) wk.tris++;
+                if (ANY && !(w & GF_PRED_GLM)) {
+                    if (tri_pred(o, d, xyz(a), xyz(b), xyz(c), tmax)) anyhit = true;
                 } else {
                     float bx, by, t;
-                    if (tri_glm(o, d, xyz(q0), xyz(q1), xyz(q2), bx, by, t) && !(t > tmax || t < PT_EPS)) {
-                        if (!(w0 & GF_ALPHA) || tri_alpha(slot, bx, by, o, d)) {
+                    if (tri_glm(o, d, xyz(a), xyz(b), xyz(c), bx, by, t) && !(t > tmax || t < PT_EPS)) {
+                        if (!(w & GF_ALPHA) || tri_alpha(sl, bx, by, o, d)) {
                             if (ANY) {
                                 anyhit = true;
                             } else {
                                 tmax = t;
-                                best = (int)slot;
+                                best = (int)sl;
                                 bb1 = bx;
                                 bb2 = by;
                                 oct |= (oct & OCT_INST) << 1;  // OCT_HIT inside an instance
@@ -223,22 +287,33 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                         }
                     }
                 }
+            };
+            uint32_t next = (w0 & GF_LAST) ? REF_EMPTY : (REF_LEAF | (slot + 1));
+            if (kind == PT_PRIM_TRIANGLE) {
+                tri(slot, w0, q0, q1, q2);
+                const uint32_t w1 = __float_as_uint(q3.w);
+                if (PT_LEAF2 && next != REF_EMPTY && (w1 & GF_KIND) == PT_PRIM_TRIANGLE && !(ANY && anyhit)) {
+                    tri(slot + 1, w1, q3, q4, q5);
+                    next = (w1 & GF_LAST) ? REF_EMPTY : (REF_LEAF | (slot + 2));
+                }
             } else if (kind == PT_PRIM_BLAS) {
-                if (COUNT) wk.tris--;
                 push(__float_as_uint(q1.x));
-            } else if (ANY) {
-                if (other_pred(slot, w0, o, d, tmax)) anyhit = true;
             } else {
-                float t, a, b;
-                if (other_closest(slot, w0, o, d, tmax, t, a, b)) {
-                    tmax = t;
-                    best = (int)slot;
-                    bb1 = a;
-                    bb2 = b;
-                    oct |= (oct & OCT_INST) << 1;
+                if (COUNT) wk.tris++;
+                if (ANY) {
+                    if (other_pred(slot, w0, o, d, tmax)) anyhit = true;
+                } else {
+                    float t, a, b;
+                    if (other_closest(slot, w0, o, d, tmax, t, a, b)) {
+                        tmax = t;
+                        best = (int)slot;
+                        bb1 = a;
+                        bb2 = b;
+                        oct |= (oct & OCT_INST) << 1;
+                    }
                 }
             }
-            ref = (w0 & GF_LAST) ? REF_EMPTY : (REF_LEAF | (slot + 1));
+            ref = next;
             if (ANY && anyhit) {  // early exit (BVH.hpp:1104-1105)
                 src.any((uint32_t)ri, true);
                 ri = -1;

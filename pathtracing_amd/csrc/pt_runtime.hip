@@ -36,7 +36,8 @@ struct pt_ctx {
     bool has_scene = false;
     uint32_t n_materials = 0;
     uint32_t n_media = 0;
-    uint32_t trace_blocks = 0;  // resident traversal blocks on this device (persistent grid)
+    uint32_t trace_blocks = 0;  // resident traversal blocks on this device (persistent grid), max of the two
+    uint32_t blocks_closest = 0, blocks_any = 0;  // per pool kernel
     uint64_t n_clusters = 0;    // BVH clusters of the uploaded scene (traversal choice)
     // wavefront buffers: two compacted path states (ping-pong), per-bounce hits,
     // the finished-path list and the shadow-ray queue
@@ -119,7 +120,7 @@ extern "C" pt_status pt_create(pt_ctx** out, int device) {
         // the persistent (pool) traversal grid: the blocks of the pool kernels
         // that are resident together (the fewer of closest / any hit)
         // (instanced variants included)
-        int cus = 0, per_cu = 1 << 30;
+        int cus = 0, per_cu[2] = {1 << 30, 1 << 30};
         const void* pool_kernels[4] = {reinterpret_cast<const void*>(&k_closest_pool<false, false>),
                                        reinterpret_cast<const void*>(&k_shadow_pool<false, false>),
                                        reinterpret_cast<const void*>(&k_closest_pool<false, true>),
@@ -128,14 +129,16 @@ extern "C" pt_status pt_create(pt_ctx** out, int device) {
         for (int k = 0; ok && k < 4; k++) {
             int b = 0;
             ok = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, pool_kernels[k], PT_TRACE_BLOCK, 0) == hipSuccess;
-            per_cu = std::min(per_cu, b);
+            per_cu[k & 1] = std::min(per_cu[k & 1], b);
         }
         if (!ok) {
             g_err = "occupancy query failed";
             delete c;
             return PT_ERR_HIP;
         }
-        c->trace_blocks = (uint32_t)std::max(1, cus * std::max(1, per_cu));
+        c->blocks_closest = (uint32_t)std::max(1, cus * std::max(1, per_cu[0]));
+        c->blocks_any = (uint32_t)std::max(1, cus * std::max(1, per_cu[1]));
+        c->trace_blocks = std::max(c->blocks_closest, c->blocks_any);
     }
     if (hipHostMalloc((void**)&c->host_cnt, PT_RING * SNAP_WORDS * 4, hipHostMallocCoherent | hipHostMallocMapped) !=
             hipSuccess ||
@@ -373,7 +376,8 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
         if (s->infinite_lights[i] >= s->n_lights) return fail(c, PT_ERR_ARG, "infinite light %u out of range", i);
 
     // ---- geometry slots
-    std::vector<DevGeom> geom(s->n_prims);
+    // one zero pad slot past the end: pool leaf steps read slot + 1 unconditionally
+    std::vector<DevGeom> geom(s->n_prims + 1);
     std::vector<DevPrimInfo> info(s->n_prims);
     for (uint32_t i = 0; i < s->n_prims; i++) {
         const pt_prim& p = s->prims[i];
@@ -547,10 +551,11 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
     AL(c->counters, (CNT_SHARDS + 1) * CNT_COUNT * 8);
     // lanes of the larger traversal grid (pool: resident; one ray per lane: the
     // capacity) x the stack entries beyond the smaller LDS part
-    constexpr int ovf_entries = PT_STACK - std::min(PT_POOL_LDS, PT_SIMPLE_LN);
+    // (refs, then as many entry distances: PT_OVF_WORDS words per entry)
+    constexpr int ovf_entries = PT_STACK - std::min({PT_POOL_LDS, PT_POOL_LDS_C, PT_SIMPLE_LN});
     if (ovf_entries > 0)
         AL(c->ovf, std::max<size_t>((size_t)c->trace_blocks * PT_TRACE_BLOCK, (n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK * PT_TRACE_BLOCK) *
-                       ovf_entries * 4);
+                       ovf_entries * PT_OVF_WORDS * 4);
 #undef AL
     if (hipMemset(c->qcnt, 0, (3 * SET_WORDS + PT_POOL_WORDS) * 4) != hipSuccess) {
         free_work(c);
@@ -570,6 +575,9 @@ static double gauss_h(double x, double sigma) {
 // chunk's per-sample radiance to `on_chunk`.
 // Makes this context's scene the one the kernels read (constant-memory `S`),
 // ordered on the context's stream.  Called by every entry point that launches.
+#ifndef PT_SAMPLE_GIB
+#define PT_SAMPLE_GIB 6
+#endif
 #ifndef PT_PATHS_POOL
 #define PT_PATHS_POOL (1u << 24)
 #endif
@@ -651,8 +659,8 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     R.inv_integral = 1.0 / integral;
 
     const uint32_t spp_local = rd->spp > R.shard_index ? (rd->spp - R.shard_index + R.shard_count - 1) / R.shard_count : 0;
-    // sample chunk: keep the per-sample radiance buffer <= ~6 GiB
-    const uint64_t max_floats = 6ull << 28;
+    // sample chunk: keep the per-sample radiance buffer <= PT_SAMPLE_GIB
+    const uint64_t max_floats = (uint64_t)PT_SAMPLE_GIB << 28;
     uint64_t per_s = 3ull * R.npix_work;
     uint32_t s_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spp_local, max_floats / per_s));
     pt_status st = ensure(c, &c->sample_L, c->sample_cap, per_s * s_chunk);
@@ -705,7 +713,8 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         PathSoA cur = c->PA, nxt = c->PB;
         hipLaunchKernelGGL(k_fill, dim3((paths + 255) / 256), dim3(256), 0, sm, R, paths, cur, set[0], next_sample);
         HIPCHK(c, hipGetLastError());
-        const dim3 gt(use_pool ? c->trace_blocks : (paths + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK);
+        const dim3 gt(use_pool ? c->blocks_closest : (paths + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK);
+        const dim3 ga(use_pool ? c->blocks_any : (paths + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK);
         const dim3 gs((paths + 255) / 256);
         uint32_t issued = 0, read = 0;
         bool drained = false;
@@ -781,7 +790,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                                            : (count ? k_shadow<true, true> : k_shadow<false, true>))
                                : (use_pool ? (count ? k_shadow_pool<true, false> : k_shadow_pool<false, false>)
                                            : (count ? k_shadow<true, false> : k_shadow<false, false>));
-                hipLaunchKernelGGL(ks, gt, dim3(PT_TRACE_BLOCK), 0, sm, nxt, c->sample_L, (const ShadowRec*)c->sq,
+                hipLaunchKernelGGL(ks, ga, dim3(PT_TRACE_BLOCK), 0, sm, nxt, c->sample_L, (const ShadowRec*)c->sq,
                                    (const uint32_t*)(out + Q_SHADOW), out + Q_WORDS + PT_POOL_WORDS, c->ovf,
                                    c->counters);
             }

@@ -162,8 +162,8 @@ __device__ __noinline__ bool other_pred(uint32_t slot, uint32_t w0, f3 o, f3 d, 
 // packed-FP32 ALU (v_pk_add_f32 / v_pk_mul_f32: two lanes per instruction,
 // each lane the same rounded (bound - o) * inv as the scalar form)
 typedef float v2f __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void slab4p(float4 xmn, float4 xmx, float4 ymn, float4 ymx, float4 zmn, float4 zmx, f3 o,
-                                       f3 inv, float tmax, uint32_t& mask) {
+__device__ __forceinline__ void slab4pe(float4 xmn, float4 xmx, float4 ymn, float4 ymx, float4 zmn, float4 zmx, f3 o,
+                                        f3 inv, float tmax, uint32_t& mask, float (&te)[4]) {
     const v2f ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
     const v2f ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
     v2f t[2][6];
@@ -188,7 +188,13 @@ __device__ __forceinline__ void slab4p(float4 xmn, float4 xmx, float4 ymn, float
         const float tEntry = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
         const float tExit = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
         if (tExit >= PT_EPS && tEntry < tmax && tEntry <= tExit) mask |= 1u << i;
+        te[i] = tEntry;
     }
+}
+__device__ __forceinline__ void slab4p(float4 xmn, float4 xmx, float4 ymn, float4 ymx, float4 zmn, float4 zmx, f3 o,
+                                       f3 inv, float tmax, uint32_t& mask) {
+    float te[4];
+    slab4pe(xmn, xmx, ymn, ymx, zmn, zmx, o, inv, tmax, mask, te);
 }
 
 // Children of a cluster in visit order: every valid child (passes the slab
@@ -209,6 +215,31 @@ __device__ __forceinline__ uint32_t order_children(uint32_t mask, uint4 ch, uint
         const bool v = (vm >> ci) & 1u;
         if (v && cand != REF_EMPTY) push(cand);
         cand = v ? c : cand;
+    }
+    return cand;
+}
+
+// The same with each pushed child's entry distance (BVH4::Intersect keeps
+// entryDist[] beside the stack and skips a popped node whose entry exceeds
+// the current max, BVH.hpp:1134-1135, 1200-1203): push(ref, tEntry).
+template <class Push>
+__device__ __forceinline__ uint32_t order_children_e(uint32_t mask, uint4 ch, uint32_t perm, const float (&te)[4],
+                                                     Push&& push) {
+    const uint32_t vm = mask & ((uint32_t)(ch.x != REF_EMPTY) | (uint32_t)(ch.y != REF_EMPTY) << 1 |
+                                (uint32_t)(ch.z != REF_EMPTY) << 2 | (uint32_t)(ch.w != REF_EMPTY) << 3);
+    uint32_t cand = REF_EMPTY;
+    float ce = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t ci = (perm >> (2 * k)) & 3u;
+        const uint32_t lo = (ci & 1u) ? ch.y : ch.x, hi = (ci & 1u) ? ch.w : ch.z;
+        const uint32_t c = (ci & 2u) ? hi : lo;
+        const float elo = (ci & 1u) ? te[1] : te[0], ehi = (ci & 1u) ? te[3] : te[2];
+        const float e = (ci & 2u) ? ehi : elo;
+        const bool v = (vm >> ci) & 1u;
+        if (v && cand != REF_EMPTY) push(cand, ce);
+        cand = v ? c : cand;
+        ce = v ? e : ce;
     }
     return cand;
 }
@@ -259,11 +290,11 @@ __device__ __forceinline__ f3 normalize4(f3 v) {
 
 __device__ __forceinline__ uint32_t octant(f3 d) { return ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0); }
 
-// Pops of REF_INST_ENTER / REF_INST_EXIT.  Enter: save the world ray, take it
-// to object space (dir = inv*d, length, origin = inv*o, d = dir/length,
-// max*length); the caller pushes the exit marker and continues at the BLAS
-// root.  Exit: restore; a hit accepted inside becomes t/length and its
-// virtual slot.  Out of line and by value, so the traversal loop's registers
+// Pops of REF_INST_ENTER, and the instance exit (ref = REF_INST_EXIT, not a
+// stack entry).  Enter: save the world ray, take it to object space (dir =
+// inv*d, length, origin = inv*o, d = dir/length, max*length); the caller
+// records its stack depth and continues at the BLAS root.  Exit: restore; a
+// hit accepted inside becomes t/length and its virtual slot.  Out of line and by value, so the traversal loop's registers
 // are untouched by this rare path.
 struct InstState {
     f3 o, d, inv;
@@ -315,6 +346,10 @@ template <bool ANY>
 __device__ __noinline__ InstState instance_step(InstState s) {
     return instance_step_inl<ANY>(s);
 }
+// Entering records the stack depth in oct (OCT_SP_SHIFT); the instance is
+// left when the traversal is back at that depth with nothing to visit
+// (PT_INSTANCE_LEAVE), so no marker takes a stack entry that a full stack
+// could drop.
 #define PT_INSTANCE_STEP_FN(ANY_, FN_)                                                          \
     do {                                                                                \
         const bool enter_ = ref != REF_INST_EXIT;                                       \
@@ -323,11 +358,12 @@ __device__ __noinline__ InstState instance_step(InstState s) {
         d = st_.d;                                                                      \
         inv = st_.inv;                                                                  \
         tmax = st_.tmax;                                                                \
-        oct = st_.oct;                                                                  \
+        oct = st_.oct | (enter_ ? (uint32_t)sp << OCT_SP_SHIFT : 0u);                   \
         best = st_.best;                                                                \
-        if (enter_) push(REF_INST_EXIT);                                                \
         ref = st_.ref;                                                                  \
     } while (0)
+// true when the lane's ray is inside an instance whose BLAS is exhausted
+#define PT_INSTANCE_DONE() ((oct & OCT_INST) && (uint32_t)sp == (oct >> OCT_SP_SHIFT))
 #define PT_INSTANCE_STEP(ANY_) PT_INSTANCE_STEP_FN(ANY_, instance_step)
 #define PT_INSTANCE_STEP_INL(ANY_) PT_INSTANCE_STEP_FN(ANY_, instance_step_inl)
 
@@ -354,6 +390,11 @@ __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out
     };
     for (;;) {
         if (ref == REF_EMPTY) {
+            if (INST && PT_INSTANCE_DONE()) {  // leave the instance
+                ref = REF_INST_EXIT;
+                PT_INSTANCE_STEP_INL(false);
+                continue;
+            }
             // pop.  Entry distances are not kept (4-byte entries double the
             // occupancy); a node the reference would skip (entry > tmax,
             // BVH.hpp:1135) is fetched and all its children fail the slab test.
@@ -442,6 +483,11 @@ __device__ bool trace_any(f3 o, f3 d, float tmax, uint32_t* s_ref, TraceWork& wk
     };
     for (;;) {
         if (ref == REF_EMPTY) {
+            if (INST && PT_INSTANCE_DONE()) {  // leave the instance
+                ref = REF_INST_EXIT;
+                PT_INSTANCE_STEP_INL(true);
+                continue;
+            }
             if (sp == 0) return false;
             --sp;
             ref = (LN >= PT_STACK || sp < LN) ? s_ref[sp * PT_TRACE_BLOCK + lane] : ovf[(size_t)(sp - LN) * G + gl];

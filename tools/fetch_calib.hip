@@ -61,6 +61,28 @@ __global__ void k_node_gather(const float4* __restrict__ t, unsigned long long n
     if (s == -1.0f) sink[0] = s;
 }
 
+// the random-line gather ceiling: each lane gathers G independent 128-B lines
+// (8G loads in flight per lane) -- what a traversal step could at best move
+template <int G>
+__global__ void k_node_gather_n(const float4* __restrict__ t, unsigned long long n, unsigned long long mask,
+                                unsigned mul, float* sink) {
+    unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float4 v[G][8];
+#pragma unroll
+    for (int g = 0; g < G; g++) {
+        const float4* q = t + scatter(i * G + g, mask, mul) * 8;
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[g][k] = q[k];
+    }
+    float s = 0;
+#pragma unroll
+    for (int g = 0; g < G; g++)
+#pragma unroll
+        for (int k = 0; k < 8; k++) s += v[g][k].x;
+    if (s == -1.0f) sink[0] = s;
+}
+
 __global__ void k_slot_gather(const float4* __restrict__ t, unsigned long long n, unsigned long long mask,
                               unsigned mul, float* sink) {
     unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
@@ -107,6 +129,20 @@ int main(int argc, char** argv) {
         CHK(hipEventSynchronize(e1));
         CHK(hipEventElapsedTime(&ms, e0, e1));
         printf("{\"kernel\":\"k_slot_gather\",\"bytes\":%llu,\"ms\":%.4f}\n", n * 48, ms);
+        CHK(hipEventRecord(e0));
+        hipLaunchKernelGGL(k_node_gather_n<4>, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, 0, t, n / 4, mask,
+                           muls[rep], sink);
+        CHK(hipEventRecord(e1));
+        CHK(hipEventSynchronize(e1));
+        CHK(hipEventElapsedTime(&ms, e0, e1));
+        printf("{\"kernel\":\"k_node_gather_n<4>\",\"bytes\":%llu,\"ms\":%.4f}\n", n / 4 * 4 * 128, ms);
+        CHK(hipEventRecord(e0));
+        hipLaunchKernelGGL(k_node_gather_n<2>, dim3((unsigned)((n / 2 + 255) / 256)), dim3(256), 0, 0, t, n / 2, mask,
+                           muls[rep], sink);
+        CHK(hipEventRecord(e1));
+        CHK(hipEventSynchronize(e1));
+        CHK(hipEventElapsedTime(&ms, e0, e1));
+        printf("{\"kernel\":\"k_node_gather_n<2>\",\"bytes\":%llu,\"ms\":%.4f}\n", n / 2 * 2 * 128, ms);
     }
     CHK(hipDeviceSynchronize());
     CHK(hipFree(t));

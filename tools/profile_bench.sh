@@ -26,5 +26,22 @@ timeout -s KILL 400 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv
 sha=$(cd "$root" && python3 -c "import bench; print(bench.src_sha())")
 python3 "$root/tools/pmc_summary.py" "$out" "$out/summary.json" "$cfg" "$spp" "$kern" "$sha" > "$out/summary.txt"
 cp "$out"/trace/run_kernel_stats.csv "$out/kernel_stats.csv"
+# compact per-dispatch timeline of the wavefront kernels (order, kernel, us)
+python3 - "$out" <<'PY'
+import csv, glob, sys
+d = sys.argv[1]
+rows = []
+for f in glob.glob(f"{d}/trace/**/*kernel_trace.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        if k.startswith("k_"):
+            rows.append((int(r["Start_Timestamp"]), k, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+rows.sort()
+with open(f"{d}/dispatches.csv", "w") as o:
+    o.write("start_us,kernel,us\n")
+    t0 = rows[0][0] if rows else 0
+    for s, k, us in rows:
+        o.write(f"{(s - t0) / 1e3:.1f},{k},{us:.1f}\n")
+PY
 rm -rf "$out/trace" "$out/fetch" "$out/write" "$out/sq" "$out/tcc"
 echo done
