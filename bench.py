@@ -198,6 +198,8 @@ def main():
     ap.add_argument("--paths-in-flight", type=int, default=0)
     ap.add_argument("--traversal", choices=("auto", "pool", "simple"), default="auto",
                     help="BVH traversal kernel (auto: by BVH size)")
+    ap.add_argument("--nodes", choices=("auto", "full", "quant"), default="auto",
+                    help="node layout of the pool traversal (auto: 64-B quantized nodes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the instrumented node-count pass")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -235,6 +237,7 @@ def main():
         log(f"{args.config}: scene + BVH + upload {setup_s:.1f} s, {world} rank(s)")
 
     tflag = {"auto": 0, "pool": N.PT_RENDER_TRAVERSAL_POOL, "simple": N.PT_RENDER_TRAVERSAL_SIMPLE}[args.traversal]
+    tflag |= {"auto": 0, "full": N.PT_RENDER_NODES_FULL, "quant": N.PT_RENDER_NODES_QUANTIZED}[args.nodes]
 
     def step(flags=0):
         # this rank's sample shard into the device film, then the RCCL SUM
@@ -288,23 +291,37 @@ def main():
 
     if rank == 0:
         pool = args.traversal == "pool" or (args.traversal == "auto" and args.config in HBM_CONFIGS)
-        kname = "k_closest_pool<false, false>" if pool else "k_closest<false, false>"
-        sname = "k_shadow_pool<false, false>" if pool else "k_shadow<false, false>"
+        quant = pool and args.nodes != "full"
+        q = ", true" if quant else ", false"
+        kname = f"k_closest_pool<false, false{q}>" if pool else "k_closest<false, false>"
+        sname = f"k_shadow_pool<false, false{q}>" if pool else "k_shadow<false, false>"
+        node_bytes = 64.0 if quant else 128.0  # what this kernel's node step reads
         sha = src_sha()
 
-        def kernel_roof(name, bpr, ms, launches, nrays):
+        def kernel_roof(name, bpr, lbpr, ms, launches, nrays):
+            # bpr: SURVEY §8(d) algorithmic bytes per ray (128 B per node visit,
+            # 48 B per primitive test: the reference's layout); lbpr: the
+            # bytes this kernel's layout reads for the same visits
             avg_ms = ms / max(1, launches)
             if bpr is None or avg_ms <= 0:
                 return None
             launch_bytes = bpr * nrays / max(1, launches)
             achieved = launch_bytes / (avg_ms * 1e-3) / 1e9
+            layout = lbpr * nrays / max(1, launches) / (avg_ms * 1e-3) / 1e9
             return {"kernel": name, "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "bytes_per_ray": round(bpr, 1), "bytes_per_launch": round(launch_bytes),
+                    "layout_bytes_per_ray": round(lbpr, 1), "layout_achieved": round(layout, 1),
                     "avg_launch_ms": round(avg_ms, 4), "launches": launches}
 
-        rc = kernel_roof(kname, bytes_closest, totals["ms_closest"], totals["launches_closest"],
+        lb_closest = lb_any = None
+        if cst:
+            lb_closest = (node_bytes * cst["nodes_closest"] + 48.0 * cst["tris_closest"]) / max(1, cst["rays_closest"])
+            if cst["rays_any"]:
+                lb_any = (node_bytes * cst["nodes_any"] + 48.0 * cst["tris_any"]) / cst["rays_any"]
+
+        rc = kernel_roof(kname, bytes_closest, lb_closest, totals["ms_closest"], totals["launches_closest"],
                          totals["rays_closest"])
-        ra = kernel_roof(sname, bytes_any, totals["ms_any"], totals["launches_any"], totals["rays_any"])
+        ra = kernel_roof(sname, bytes_any, lb_any, totals["ms_any"], totals["launches_any"], totals["rays_any"])
         traffic, tinfo = pmc_traffic(args.config, setup.spp, world, kname, sha)
         roof = {"bound": "hbm" if args.config in HBM_CONFIGS else "l2/latency",
                 "achieved": rc["achieved"] if rc else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -317,7 +334,9 @@ def main():
                          "nodes_per_ray": round(cst["nodes_closest"] / max(1, cst["rays_closest"]), 2),
                          "tris_per_ray": round(cst["tris_closest"] / max(1, cst["rays_closest"]), 2),
                          "avg_launch_ms": rc["avg_launch_ms"], "launches": rc["launches"],
-                         "bytes_per_launch": rc["bytes_per_launch"]})
+                         "bytes_per_launch": rc["bytes_per_launch"], "node_layout_bytes": node_bytes,
+                         "layout_bytes_per_ray": rc["layout_bytes_per_ray"],
+                         "layout_achieved": rc["layout_achieved"]})
         if ra:
             ra["nodes_per_ray"] = round(cst["nodes_any"] / max(1, cst["rays_any"]), 2)
             ra["tris_per_ray"] = round(cst["tris_any"] / max(1, cst["rays_any"]), 2)

@@ -238,6 +238,8 @@ enum { PT_FILTER_MITCHELL = 0, PT_FILTER_BOX = 1, PT_FILTER_GAUSSIAN = 2 };
 #define PT_RENDER_TIMING 0x2u       /* per-kernel HIP-event timing into stats   */
 #define PT_RENDER_TRAVERSAL_POOL 0x4u   /* force the persistent refilling traversal */
 #define PT_RENDER_TRAVERSAL_SIMPLE 0x8u /* force one ray per lane (default: by BVH size) */
+#define PT_RENDER_NODES_FULL 0x10u      /* pool traversal over the 128-B reference clusters */
+#define PT_RENDER_NODES_QUANTIZED 0x20u /* ... over the 64-B quantized nodes (the default)  */
 
 typedef struct pt_render_desc {
     uint32_t integrator;       /* PT_INTEGRATOR_*                               */
@@ -286,6 +288,13 @@ pt_status pt_create(pt_ctx** ctx, int device);
 void pt_destroy(pt_ctx* ctx);
 const char* pt_last_error(const pt_ctx* ctx);   /* ctx may be NULL          */
 pt_status pt_set_stream(pt_ctx* ctx, void* hip_stream); /* NULL = ctx stream */
+/* Node format of the persistent (pool) traversal: the reference's 128-B
+ * clusters, or a 64-B copy with 8-bit child boxes quantized outward (every
+ * child the reference's slab test accepts is accepted, so the closest hit
+ * is the same).  AUTO = quantized where the scene can be encoded.  Applies
+ * to pt_trace and is the default of pt_render (overridden by its flags). */
+enum { PT_NODES_AUTO = 0, PT_NODES_FULL = 1, PT_NODES_QUANTIZED = 2 };
+pt_status pt_set_node_format(pt_ctx* ctx, int format);
 pt_status pt_scene_upload(pt_ctx* ctx, const pt_scene_desc* scene);
 /* Accumulates W*H*4 doubles {sum R*w, sum G*w, sum B*w, sum w} (Film.hpp:227-253)
  * into film_accum, a host or a device pointer (detected). */

@@ -26,6 +26,25 @@ struct alignas(128) DevCluster {
 };
 static_assert(sizeof(DevCluster) == 128, "cluster layout");
 
+// ---- quantized BVH4 node (64 B, 64-aligned): the same cluster with its four
+// child boxes stored as 8-bit offsets from a per-node origin in power-of-two
+// steps per axis (scale 2^(e-127)).  Encoded on the host so that every
+// decoded bound fma(q, scale, origin) lies outside the reference's float
+// bound (lo' <= lo, hi' >= hi): the slab test on the decoded box accepts
+// every child the reference accepts, so the traversal visits a superset of
+// the reference's nodes in the same order and finds the same closest hit.
+//   a = origin.xyz, exponents (x | y << 8 | z << 16)
+//   b = x lo[4], x hi[4], y lo[4], y hi[4]   (one byte per child)
+//   c = z lo[4], z hi[4], order[0], order[1]  (octant order bytes as DevCluster)
+//   d = child[4]
+struct alignas(64) DevQNode {
+    float4 a;
+    uint32_t b[4];
+    uint32_t c[4];
+    uint32_t child[4];
+};
+static_assert(sizeof(DevQNode) == 64, "qnode layout");
+
 // ---- primitive slot geometry (48 B): what a leaf test reads.
 // a = v0|Q|center + flags, b = e1|u|radius + index, c = e2|v
 #define GF_KIND 3u
@@ -66,6 +85,7 @@ struct DevPrimInfo {
 
 struct DevScene {
     const DevCluster* nodes;
+    const DevQNode* qnodes;    // the same nodes quantized (null: the scene could not be encoded)
     const DevGeom* geom;
     const DevPrimInfo* info;
     uint32_t root;

@@ -82,13 +82,13 @@ struct RenderParams {
 template <bool COUNT, bool INST>
 __global__ void k_closest(PathSoA P, const uint32_t* in, float4* hit, uint32_t* pool, uint32_t* ovf, uint32_t* spare,
                           uint32_t* snap, unsigned long long* counters);
-template <bool COUNT, bool INST>
+template <bool COUNT, bool INST, bool QN>
 __global__ void k_closest_pool(PathSoA P, const uint32_t* in, float4* hit, uint32_t* pool, uint32_t* ovf,
                                uint32_t* spare, uint32_t* snap, unsigned long long* counters);
 template <bool COUNT, bool INST>
 __global__ void k_shadow(PathSoA next, float* sample_L, const ShadowRec* sq, const uint32_t* nptr, uint32_t* pool,
                          uint32_t* ovf, unsigned long long* counters);
-template <bool COUNT, bool INST>
+template <bool COUNT, bool INST, bool QN>
 __global__ void k_shadow_pool(PathSoA next, float* sample_L, const ShadowRec* sq, const uint32_t* nptr,
                               uint32_t* pool, uint32_t* ovf, unsigned long long* counters);
 template <int INTEGRATOR>
@@ -105,5 +105,6 @@ __global__ void k_gather(RenderParams R, const float* sample_L, double* film);
 __global__ void k_interact(const pt_ray* rays, uint32_t n, float* out);
 __global__ void k_bsdf_cases(int mid, const float* in, uint32_t n, float* out);
 __global__ void k_light_cases(const float* in, uint32_t n, float* out);
+template <bool QN>
 __global__ void k_trace_rays(const pt_ray* rays, uint32_t n, int any, pt_hit* out, uint32_t* pool, uint32_t* ovf,
                              unsigned long long* counters);

@@ -172,7 +172,7 @@ struct ClosestSrc {
     __device__ __forceinline__ void any(uint32_t, bool) {}
 };
 
-template <bool COUNT, bool INST>
+template <bool COUNT, bool INST, bool QN>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_closest_pool(PathSoA P, const uint32_t* __restrict__ nptr,
                                                                 float4* __restrict__ hit, uint32_t* __restrict__ pool,
                                                                 uint32_t* __restrict__ ovf, uint32_t* __restrict__ spare,
@@ -185,7 +185,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_closest_pool(P
     if (n == 0) return;
     TraceWork wk{0, 0};
     ClosestSrc src{P, hit, nptr[Q_NEXT]};
-    trace_pool<false, COUNT, ClosestSrc, true, INST>(n, pool, src, s_ref, s_ent, ovf, wk);
+    trace_pool<false, COUNT, ClosestSrc, true, INST, PT_POOL_LDS_C, QN>(n, pool, src, s_ref, s_ent, ovf, wk);
     if (COUNT) {
         count_add(counters, CNT_NODES_CLOSEST, wk.nodes);
         count_add(counters, CNT_TRIS_CLOSEST, wk.tris);
@@ -226,7 +226,7 @@ struct ShadowSrc {
     }
 };
 
-template <bool COUNT, bool INST>
+template <bool COUNT, bool INST, bool QN>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SHADOW_WAVES void k_shadow_pool(PathSoA next, float* __restrict__ sample_L,
                                                                const ShadowRec* __restrict__ sq,
                                                                const uint32_t* __restrict__ nptr,
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SHADOW_WAVES void k_shadow_pool(
     ShadowSrc src{sq, next, sample_L};
     const uint32_t n = *nptr;
     if (n == 0) return;
-    trace_pool<true, COUNT, ShadowSrc, true, INST>(n, pool, src, s_ref, nullptr, ovf, wk);
+    trace_pool<true, COUNT, ShadowSrc, true, INST, PT_POOL_LDS, QN>(n, pool, src, s_ref, nullptr, ovf, wk);
     if (COUNT) {
         count_add(counters, CNT_NODES_ANY, wk.nodes);
         count_add(counters, CNT_TRIS_ANY, wk.tris);
@@ -341,6 +341,7 @@ struct RaysSrc {
     __device__ __forceinline__ void any(uint32_t i, bool hit) { out[i] = pt_hit{0, 0, 0, hit ? 1 : 0}; }
 };
 
+template <bool QN>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(const pt_ray* __restrict__ rays, uint32_t n, int any,
                                                               pt_hit* __restrict__ out, uint32_t* __restrict__ pool,
                                                               uint32_t* __restrict__ ovf, unsigned long long* counters) {
@@ -348,8 +349,8 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(const pt_ray* __r
     __shared__ uint16_t s_ent[PT_POOL_LDS_C * PT_TRACE_BLOCK];
     TraceWork wk{0, 0};
     RaysSrc src{rays, out};
-    if (any) trace_pool<true, true>(n, pool, src, s_ref, nullptr, ovf, wk);
-    else trace_pool<false, true>(n, pool, src, s_ref, s_ent, ovf, wk);
+    if (any) trace_pool<true, true, RaysSrc, true, true, PT_POOL_LDS, QN>(n, pool, src, s_ref, nullptr, ovf, wk);
+    else trace_pool<false, true, RaysSrc, true, true, PT_POOL_LDS_C, QN>(n, pool, src, s_ref, s_ent, ovf, wk);
     count_add(counters, any ? CNT_NODES_ANY : CNT_NODES_CLOSEST, wk.nodes);
     count_add(counters, any ? CNT_TRIS_ANY : CNT_TRIS_CLOSEST, wk.tris);
 }
@@ -1255,16 +1256,25 @@ __global__ __launch_bounds__(256) void k_resolve(const double* __restrict__ film
 #define PT_INST_TRACE(B, I)                                                                                         \
     template __global__ void k_closest<B, I>(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*, uint32_t*,     \
                                              uint32_t*, unsigned long long*);                                        \
-    template __global__ void k_closest_pool<B, I>(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*,           \
-                                                  uint32_t*, uint32_t*, unsigned long long*);                        \
     template __global__ void k_shadow<B, I>(PathSoA, float*, const ShadowRec*, const uint32_t*, uint32_t*,           \
-                                            uint32_t*, unsigned long long*);                                         \
-    template __global__ void k_shadow_pool<B, I>(PathSoA, float*, const ShadowRec*, const uint32_t*, uint32_t*,      \
-                                                 uint32_t*, unsigned long long*);
+                                            uint32_t*, unsigned long long*);
+#define PT_INST_POOL(B, I, Q)                                                                                       \
+    template __global__ void k_closest_pool<B, I, Q>(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*,        \
+                                                     uint32_t*, uint32_t*, unsigned long long*);                     \
+    template __global__ void k_shadow_pool<B, I, Q>(PathSoA, float*, const ShadowRec*, const uint32_t*, uint32_t*,   \
+                                                    uint32_t*, unsigned long long*);
 PT_INST_TRACE(false, false)
 PT_INST_TRACE(true, false)
 PT_INST_TRACE(false, true)
 PT_INST_TRACE(true, true)
+PT_INST_POOL(false, false, false)
+PT_INST_POOL(true, false, false)
+PT_INST_POOL(false, true, false)
+PT_INST_POOL(true, true, false)
+PT_INST_POOL(false, false, true)
+PT_INST_POOL(true, false, true)
+PT_INST_POOL(false, true, true)
+PT_INST_POOL(true, true, true)
 template __global__ void k_shadow_tr<false>(PathSoA, float*, const ShadowRec*, const uint32_t*, unsigned long long*);
 template __global__ void k_shadow_tr<true>(PathSoA, float*, const ShadowRec*, const uint32_t*, unsigned long long*);
 template __global__ void k_shade<PT_INTEGRATOR_PATH>(RenderParams, PathSoA, const uint32_t*, const float4*, PathSoA,

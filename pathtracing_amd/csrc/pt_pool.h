@@ -77,7 +77,7 @@ __device__ unsigned int pt_diag[4];
 // LN: stack entries in LDS (s_ref, and s_ent for closest hit with PT_ENTRY);
 // the rest in ovf ([entry][grid lane] refs, then as many entry distances).
 template <bool ANY, bool COUNT, class Src, bool POOL = true, bool INST = true,
-          int LN = (ANY ? PT_POOL_LDS : PT_POOL_LDS_C)>
+          int LN = (ANY ? PT_POOL_LDS : PT_POOL_LDS_C), bool QN = false>
 __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, uint32_t* s_ref, uint16_t* s_ent,
                            uint32_t* __restrict__ ovf, TraceWork& wk) {
     constexpr bool ENT = PT_ENTRY && !ANY;
@@ -223,33 +223,61 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             continue;
         }
 #endif
-        // all eight loads issue before any use: a primitive lane reads its
-        // 48-byte slot and the next one (PT_LEAF2; the slot array has a pad
-        // slot at its end) and repeats its first 16 bytes for the node-only
-        // words (same line, no extra traffic), and the cluster test below runs
+        // all loads issue before any use: a primitive lane reads its 48-byte
+        // slot (and the next one with PT_LEAF2; the slot array has a pad slot
+        // at its end) and repeats its first 16 bytes for the node-only words
+        // (same line, no extra traffic), and the cluster test below runs
         // unconditionally (its result masked off on primitive lanes) so the
-        // compiler cannot sink the node loads behind the primitive branch
-        const float4* __restrict__ q = node_step ? reinterpret_cast<const float4*>(S.nodes + idx)
-                                                 : reinterpret_cast<const float4*>(S.geom + idx);
+        // compiler cannot sink the node loads behind the primitive branch.
+        // QN: 64-byte quantized nodes (DevQNode), four loads per step.
         const uint32_t nk = node_step ? 1u : 0u;
-        constexpr uint32_t pk = PT_LEAF2 ? 1u : 0u;
-        const uint32_t k3 = 3u * (nk | pk);
-        const float4 q0 = q[0], q1 = q[1], q2 = q[2];
-        const float4 q3 = q[k3], q4 = q[k3 ? 4u : 0u], q5 = q[k3 ? 5u : 0u], q6 = q[6 * nk], q7 = q[7 * nk];
-        {
-            uint32_t mask;
-            float te[4];
+        float4 q0, q1, q2, q3, q4, q5;
+        uint32_t mask;
+        float te[4];
+        uint4 ch;
+        uint32_t ow0, ow1;
+        if constexpr (QN) {
+            const float4* __restrict__ q = node_step ? reinterpret_cast<const float4*>(S.qnodes + idx)
+                                                     : reinterpret_cast<const float4*>(S.geom + idx);
+            q0 = q[0];
+            q1 = q[1];
+            q2 = q[2];
+            const float4 qc = q[3 * nk];
+            q3 = q4 = q5 = q0;  // no second leaf primitive in this form
+            float4 xmn, xmx, ymn, ymx, zmn, zmx;
+            qnode_boxes(q0, q1, q2, xmn, xmx, ymn, ymx, zmn, zmx);
+            slab4pe(xmn, xmx, ymn, ymx, zmn, zmx, o, inv, tmax, mask, te);
+            ch = make_uint4(__float_as_uint(qc.x), __float_as_uint(qc.y), __float_as_uint(qc.z),
+                            __float_as_uint(qc.w));
+            ow0 = __float_as_uint(q2.z);
+            ow1 = __float_as_uint(q2.w);
+        } else {
+            const float4* __restrict__ q = node_step ? reinterpret_cast<const float4*>(S.nodes + idx)
+                                                     : reinterpret_cast<const float4*>(S.geom + idx);
+            constexpr uint32_t pk = PT_LEAF2 ? 1u : 0u;
+            const uint32_t k3 = 3u * (nk | pk);
+            q0 = q[0];
+            q1 = q[1];
+            q2 = q[2];
+            q3 = q[k3];
+            q4 = q[k3 ? 4u : 0u];
+            q5 = q[k3 ? 5u : 0u];
+            const float4 q6 = q[6 * nk], q7 = q[7 * nk];
             slab4pe(q0, q1, q2, q3, q4, q5, o, inv, tmax, mask, te);
+            ch = make_uint4(__float_as_uint(q6.x), __float_as_uint(q6.y), __float_as_uint(q6.z),
+                            __float_as_uint(q6.w));
+            ow0 = __float_as_uint(q7.x);
+            ow1 = __float_as_uint(q7.y);
+        }
+        {
             if (!node_step) mask = 0;  // no children on primitive lanes
             // visit order: slot order for any hit (BVH.hpp:1099-1102), octant
             // order far -> near for closest hit (BVH4::LUT, BVH.hpp:1195-1204)
             uint32_t perm = 0xE4u;
             if (!ANY) {
-                const uint32_t ow = __float_as_uint(((oct >> 2) & 1u) ? q7.y : q7.x);
+                const uint32_t ow = ((oct >> 2) & 1u) ? ow1 : ow0;
                 perm = (ow >> (8 * (oct & 3))) & 0xFFu;
             }
-            const uint4 ch = make_uint4(__float_as_uint(q6.x), __float_as_uint(q6.y), __float_as_uint(q6.z),
-                                        __float_as_uint(q6.w));
             uint32_t cand;
             if (ENT) cand = order_children_e(mask, ch, perm, te, push);
             else cand = order_children(mask, ch, perm, [&](uint32_t v) { push(v); });
@@ -292,7 +320,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             if (kind == PT_PRIM_TRIANGLE) {
                 tri(slot, w0, q0, q1, q2);
                 const uint32_t w1 = __float_as_uint(q3.w);
-                if (PT_LEAF2 && next != REF_EMPTY && (w1 & GF_KIND) == PT_PRIM_TRIANGLE && !(ANY && anyhit)) {
+                if (PT_LEAF2 && !QN && next != REF_EMPTY && (w1 & GF_KIND) == PT_PRIM_TRIANGLE && !(ANY && anyhit)) {
                     tri(slot + 1, w1, q3, q4, q5);
                     next = (w1 & GF_LAST) ? REF_EMPTY : (REF_LEAF | (slot + 2));
                 }

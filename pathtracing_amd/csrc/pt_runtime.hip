@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -39,6 +40,8 @@ struct pt_ctx {
     uint32_t trace_blocks = 0;  // resident traversal blocks on this device (persistent grid), max of the two
     uint32_t blocks_closest = 0, blocks_any = 0;  // per pool kernel
     uint64_t n_clusters = 0;    // BVH clusters of the uploaded scene (traversal choice)
+    bool has_qnodes = false;    // the scene's nodes have a quantized copy (DevQNode)
+    int node_format = PT_NODES_AUTO;  // pt_set_node_format
     // wavefront buffers: two compacted path states (ping-pong), per-bounce hits,
     // the finished-path list and the shadow-ray queue
     uint32_t cap = 0;
@@ -121,12 +124,16 @@ extern "C" pt_status pt_create(pt_ctx** out, int device) {
         // that are resident together (the fewer of closest / any hit)
         // (instanced variants included)
         int cus = 0, per_cu[2] = {1 << 30, 1 << 30};
-        const void* pool_kernels[4] = {reinterpret_cast<const void*>(&k_closest_pool<false, false>),
-                                       reinterpret_cast<const void*>(&k_shadow_pool<false, false>),
-                                       reinterpret_cast<const void*>(&k_closest_pool<false, true>),
-                                       reinterpret_cast<const void*>(&k_shadow_pool<false, true>)};
+        const void* pool_kernels[8] = {reinterpret_cast<const void*>(&k_closest_pool<false, false, false>),
+                                       reinterpret_cast<const void*>(&k_shadow_pool<false, false, false>),
+                                       reinterpret_cast<const void*>(&k_closest_pool<false, true, false>),
+                                       reinterpret_cast<const void*>(&k_shadow_pool<false, true, false>),
+                                       reinterpret_cast<const void*>(&k_closest_pool<false, false, true>),
+                                       reinterpret_cast<const void*>(&k_shadow_pool<false, false, true>),
+                                       reinterpret_cast<const void*>(&k_closest_pool<false, true, true>),
+                                       reinterpret_cast<const void*>(&k_shadow_pool<false, true, true>)};
         bool ok = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess;
-        for (int k = 0; ok && k < 4; k++) {
+        for (int k = 0; ok && k < 8; k++) {
             int b = 0;
             ok = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, pool_kernels[k], PT_TRACE_BLOCK, 0) == hipSuccess;
             per_cu[k & 1] = std::min(per_cu[k & 1], b);
@@ -197,7 +204,85 @@ extern "C" pt_status pt_set_stream(pt_ctx* c, void* s) {
     return PT_OK;
 }
 
+extern "C" pt_status pt_set_node_format(pt_ctx* c, int fmt) {
+    if (!c || fmt < PT_NODES_AUTO || fmt > PT_NODES_QUANTIZED) return PT_ERR_ARG;
+    c->node_format = fmt;
+    return PT_OK;
+}
+
 extern "C" uint64_t pt_scene_device_bytes(const pt_ctx* c) { return c ? c->scene_bytes : 0; }
+
+// ---- quantized nodes (DevQNode).  One axis of a cluster's four child boxes:
+// origin = the smallest lower bound, step = the smallest power of two with
+// which every bound fits 8 bits, each lower bound rounded down and each upper
+// bound up, checked with the device's own decode fma(q, step, origin) so the
+// decoded box always contains the reference's float box.  False when the
+// bounds are not finite or no step fits (the scene then keeps full nodes).
+static bool quantize_axis(const float* lo, const float* hi, uint32_t valid, float& org, uint32_t& e8, uint32_t& wlo,
+                          uint32_t& whi) {
+    wlo = 0;
+    whi = 0;
+    if (!valid) {
+        org = 0.0f;
+        e8 = 127;
+        wlo = 0xFFFFFFFFu;  // empty children: lo 255 > hi 0 (their refs are REF_EMPTY anyway)
+        return true;
+    }
+    float mn = INFINITY, mx = -INFINITY;
+    for (int k = 0; k < 4; k++)
+        if (valid >> k & 1) {
+            if (!std::isfinite(lo[k]) || !std::isfinite(hi[k])) return false;
+            mn = std::min(mn, lo[k]);
+            mx = std::max(mx, hi[k]);
+        }
+    org = mn;
+    const double ext = (double)mx - (double)mn;
+    int k0 = ext > 0 ? (int)std::ceil(std::log2(ext / 255.0)) : -126;
+    for (int k = std::max(-126, k0 - 1); k <= 127; k++) {
+        const float step = std::ldexp(1.0f, k);
+        uint32_t ql[4] = {255, 255, 255, 255}, qh[4] = {0, 0, 0, 0};
+        bool ok = true;
+        for (int c = 0; c < 4 && ok; c++) {
+            if (!(valid >> c & 1)) continue;
+            double a = std::floor(((double)lo[c] - (double)org) / step);
+            a = std::min(255.0, std::max(0.0, a));
+            while (a > 0 && std::fma((float)a, step, org) > lo[c]) a -= 1;
+            if (std::fma((float)a, step, org) > lo[c]) ok = false;
+            double b = std::ceil(((double)hi[c] - (double)org) / step);
+            b = std::max(0.0, b);
+            while (b <= 255 && std::fma((float)b, step, org) < hi[c]) b += 1;
+            if (b > 255) ok = false;
+            ql[c] = (uint32_t)a;
+            qh[c] = (uint32_t)b;
+        }
+        if (!ok) continue;
+        e8 = (uint32_t)(k + 127);
+        for (int c = 0; c < 4; c++) {
+            wlo |= ql[c] << (8 * c);
+            whi |= qh[c] << (8 * c);
+        }
+        return true;
+    }
+    return false;
+}
+static bool quantize_node(const DevCluster& n, DevQNode& q) {
+    uint32_t valid = 0;
+    for (int k = 0; k < 4; k++)
+        if (n.child[k] != REF_EMPTY) valid |= 1u << k;
+    const float* b = &n.xmin.x;  // xmin xmax ymin ymax zmin zmax, 4 floats each
+    float org[3];
+    uint32_t e[3], w[6];
+    for (int a = 0; a < 3; a++)
+        if (!quantize_axis(b + 8 * a, b + 8 * a + 4, valid, org[a], e[a], w[2 * a], w[2 * a + 1])) return false;
+    q.a = make_float4(org[0], org[1], org[2], __builtin_bit_cast(float, e[0] | e[1] << 8 | e[2] << 16));
+    for (int k = 0; k < 4; k++) q.b[k] = w[k];
+    q.c[0] = w[4];
+    q.c[1] = w[5];
+    q.c[2] = n.order[0];
+    q.c[3] = n.order[1];
+    for (int k = 0; k < 4; k++) q.child[k] = n.child[k];
+    return true;
+}
 
 template <class T>
 static pt_status upload(pt_ctx* c, const T* src, size_t n, const T** dst) {
@@ -464,6 +549,13 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
 #define UP(dst, src, n) \
     if ((st = upload(c, src, n, &dst)) != PT_OK) return st;
     UP(DS.nodes, nodes.data(), nodes.size());
+    {
+        std::vector<DevQNode> qn(nodes.size());
+        bool ok = true;
+        for (size_t k = 0; k < nodes.size() && ok; k++) ok = quantize_node(nodes[k], qn[k]);
+        c->has_qnodes = ok;
+        if (ok) UP(DS.qnodes, qn.data(), qn.size());
+    }
     UP(DS.geom, geom.data(), geom.size());
     UP(DS.info, info.data(), info.size());
     UP(DS.tri, tri.data(), tri.size());
@@ -614,6 +706,28 @@ static pt_status bind_scene(pt_ctx* c, uint64_t lanes = 0) {
     return PT_OK;
 }
 
+// traversal kernel of one wavefront iteration
+using ClosestFn = void (*)(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*, uint32_t*, uint32_t*,
+                           unsigned long long*);
+using ShadowFn = void (*)(PathSoA, float*, const ShadowRec*, const uint32_t*, uint32_t*, uint32_t*,
+                          unsigned long long*);
+template <bool C, bool I>
+static ClosestFn closest_fn(bool pool, bool qn) {
+    return pool ? (qn ? k_closest_pool<C, I, true> : k_closest_pool<C, I, false>) : k_closest<C, I>;
+}
+template <bool C, bool I>
+static ShadowFn shadow_fn(bool pool, bool qn) {
+    return pool ? (qn ? k_shadow_pool<C, I, true> : k_shadow_pool<C, I, false>) : k_shadow<C, I>;
+}
+static ClosestFn pick_closest(bool pool, bool qn, bool inst, bool count) {
+    return inst ? (count ? closest_fn<true, true>(pool, qn) : closest_fn<false, true>(pool, qn))
+                : (count ? closest_fn<true, false>(pool, qn) : closest_fn<false, false>(pool, qn));
+}
+static ShadowFn pick_shadow(bool pool, bool qn, bool inst, bool count) {
+    return inst ? (count ? shadow_fn<true, true>(pool, qn) : shadow_fn<false, true>(pool, qn))
+                : (count ? shadow_fn<true, false>(pool, qn) : shadow_fn<false, false>(pool, qn));
+}
+
 template <class OnChunk>
 static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_dev,
                      pt_stats* stats, OnChunk on_chunk) {
@@ -682,6 +796,9 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                           : (rd->flags & PT_RENDER_TRAVERSAL_SIMPLE) ? false
                                                                      : c->n_clusters >= PT_POOL_MIN_CLUSTERS;
     const bool inst = c->scene.n_instances > 0;  // kernels with the instance step compiled in
+    // node format of the pool kernels: quantized by default where it exists
+    const bool qn = use_pool && c->has_qnodes && !(rd->flags & PT_RENDER_NODES_FULL) &&
+                    ((rd->flags & PT_RENDER_NODES_QUANTIZED) || c->node_format != PT_NODES_FULL);
     const bool timing = (rd->flags & PT_RENDER_TIMING) != 0;
     hipStream_t sm = c->stream;
     HIPCHK(c, hipMemsetAsync(c->counters, 0, (CNT_SHARDS + 1) * CNT_COUNT * 8, sm));
@@ -758,10 +875,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             hipEvent_t* ev = c->rev[i % PT_RING];
             if (timing) HIPCHK(c, hipEventRecord(ev[0], sm));
             {
-                auto kc = inst ? (use_pool ? (count ? k_closest_pool<true, true> : k_closest_pool<false, true>)
-                                           : (count ? k_closest<true, true> : k_closest<false, true>))
-                               : (use_pool ? (count ? k_closest_pool<true, false> : k_closest_pool<false, false>)
-                                           : (count ? k_closest<true, false> : k_closest<false, false>));
+                auto kc = pick_closest(use_pool, qn, inst, count);
                 hipLaunchKernelGGL(kc, gt, dim3(PT_TRACE_BLOCK), 0, sm, cur, (const uint32_t*)in, c->hit,
                                    out + Q_WORDS, c->ovf, spare, c->host_cnt_dev + (i % PT_RING) * SNAP_WORDS,
                                    c->counters);
@@ -786,10 +900,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                                    nxt, c->sample_L, (const ShadowRec*)c->sq, (const uint32_t*)(out + Q_SHADOW),
                                    c->counters);
             } else if (rd->integrator != PT_INTEGRATOR_SIMPLE) {
-                auto ks = inst ? (use_pool ? (count ? k_shadow_pool<true, true> : k_shadow_pool<false, true>)
-                                           : (count ? k_shadow<true, true> : k_shadow<false, true>))
-                               : (use_pool ? (count ? k_shadow_pool<true, false> : k_shadow_pool<false, false>)
-                                           : (count ? k_shadow<true, false> : k_shadow<false, false>));
+                auto ks = pick_shadow(use_pool, qn, inst, count);
                 hipLaunchKernelGGL(ks, ga, dim3(PT_TRACE_BLOCK), 0, sm, nxt, c->sample_L, (const ShadowRec*)c->sq,
                                    (const uint32_t*)(out + Q_SHADOW), out + Q_WORDS + PT_POOL_WORDS, c->ovf,
                                    c->counters);
@@ -998,7 +1109,11 @@ extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any
     HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
     uint32_t* pool = c->qcnt + 3 * SET_WORDS;
     HIPCHK(c, hipMemsetAsync(pool, 0, PT_POOL_WORDS * 4, c->stream));
-    hipLaunchKernelGGL(k_trace_rays,
+    // the pool traversal of the renderer: quantized nodes where the renderer
+    // would use them (large scenes), unless pt_set_node_format says otherwise
+    const bool qn = c->has_qnodes && (c->node_format == PT_NODES_QUANTIZED ||
+                                      (c->node_format == PT_NODES_AUTO && c->n_clusters >= PT_POOL_MIN_CLUSTERS));
+    hipLaunchKernelGGL(qn ? k_trace_rays<true> : k_trace_rays<false>,
                        dim3(std::max(1u, std::min((n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK, c->trace_blocks))),
                        dim3(PT_TRACE_BLOCK), 0, c->stream, dr, n, any_hit, dh, pool, c->ovf, c->counters);
     HIPCHK(c, hipGetLastError());

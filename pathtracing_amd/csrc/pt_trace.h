@@ -197,6 +197,27 @@ __device__ __forceinline__ void slab4p(float4 xmn, float4 xmx, float4 ymn, float
     slab4pe(xmn, xmx, ymn, ymx, zmn, zmx, o, inv, tmax, mask, te);
 }
 
+// The child boxes of a quantized node (DevQNode), as the 4-wide SoA float4s
+// slab4p takes: bound = fma(byte, 2^(e-127), origin) per axis.
+__device__ __forceinline__ float qdec(uint32_t w, int k, float sc, float org) {
+    return fma_((float)((w >> (8 * k)) & 0xFFu), sc, org);
+}
+__device__ __forceinline__ float4 qdec4(uint32_t w, float sc, float org) {
+    return make_float4(qdec(w, 0, sc, org), qdec(w, 1, sc, org), qdec(w, 2, sc, org), qdec(w, 3, sc, org));
+}
+__device__ __forceinline__ void qnode_boxes(float4 a, float4 b, float4 c, float4& xmn, float4& xmx, float4& ymn,
+                                            float4& ymx, float4& zmn, float4& zmx) {
+    const uint32_t ex = __float_as_uint(a.w);
+    const float sx = __uint_as_float((ex & 0xFFu) << 23), sy = __uint_as_float(((ex >> 8) & 0xFFu) << 23),
+                sz = __uint_as_float(((ex >> 16) & 0xFFu) << 23);
+    xmn = qdec4(__float_as_uint(b.x), sx, a.x);
+    xmx = qdec4(__float_as_uint(b.y), sx, a.x);
+    ymn = qdec4(__float_as_uint(b.z), sy, a.y);
+    ymx = qdec4(__float_as_uint(b.w), sy, a.y);
+    zmn = qdec4(__float_as_uint(c.x), sz, a.z);
+    zmx = qdec4(__float_as_uint(c.y), sz, a.z);
+}
+
 // Children of a cluster in visit order: every valid child (passes the slab
 // test, exists) but the last is pushed, the last becomes the next ref.  perm
 // holds the visit order as 2-bit slot indices from the low end (0xE4 = slot

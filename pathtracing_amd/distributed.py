@@ -64,7 +64,15 @@ def render_frame(integrator, film: torch.Tensor, *, flags: int = 0, paths_in_fli
         film.zero_()
         st = render_shard(rank, n, film)
     if n > 1:
-        dist.reduce(film, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        if film.is_cuda and dist.get_backend(group) == "gloo":
+            # gloo has no device reduce: sum host copies (CPU rehearsals of the
+            # multi-rank path with the real device renderer)
+            host = film.cpu()
+            dist.reduce(host, dst=dst, op=dist.ReduceOp.SUM, group=group)
+            if rank == dst:
+                film.copy_(host)
+        else:
+            dist.reduce(film, dst=dst, op=dist.ReduceOp.SUM, group=group)
     return st
 
 

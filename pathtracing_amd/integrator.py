@@ -73,6 +73,10 @@ class Context:
     def set_stream(self, stream_ptr: int | None):
         N.check(self._lib.pt_set_stream(self.ptr, C.c_void_p(stream_ptr) if stream_ptr else None), self.ptr)
 
+    def set_node_format(self, fmt: int):
+        """pt_set_node_format: N.PT_NODES_AUTO / _FULL / _QUANTIZED (pool traversal node layout)."""
+        N.check(self._lib.pt_set_node_format(self.ptr, int(fmt)), self.ptr)
+
     def render(self, cam: N.CameraDesc, rd: N.RenderDesc, film_ptr: int) -> dict:
         st = N.Stats()
         N.check(self._lib.pt_render(self.ptr, C.byref(cam), C.byref(rd), C.c_void_p(film_ptr), C.byref(st)), self.ptr)

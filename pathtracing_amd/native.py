@@ -28,6 +28,9 @@ PT_RENDER_COUNT_NODES = 0x1
 PT_RENDER_TIMING = 0x2
 PT_RENDER_TRAVERSAL_POOL = 0x4
 PT_RENDER_TRAVERSAL_SIMPLE = 0x8
+PT_RENDER_NODES_FULL = 0x10
+PT_RENDER_NODES_QUANTIZED = 0x20
+PT_NODES_AUTO, PT_NODES_FULL, PT_NODES_QUANTIZED = 0, 1, 2
 
 # ---- numpy mirrors of the array element structs (layouts asserted below) ----
 REF_NODE = np.dtype([("count", "u1"), ("active", "u1"), ("perm", "u1"), ("pad", "u1"), ("cluster_idx", "<u4")])
@@ -124,7 +127,7 @@ class BvhBuildStats(C.Structure):
 EXPORTS = [
     "pt_version", "pt_create", "pt_destroy", "pt_last_error", "pt_set_stream", "pt_scene_upload", "pt_render",
     "pt_trace", "pt_scene_device_bytes", "pt_bvh4_build", "pt_bvh4_order_table", "pt_film_resolve",
-    "pt_mat4_inverse", "pt_bvh4_build_device",
+    "pt_mat4_inverse", "pt_bvh4_build_device", "pt_set_node_format",
 ]
 
 _lib = None
@@ -152,6 +155,8 @@ def lib():
     L.pt_last_error.restype = C.c_char_p
     L.pt_set_stream.argtypes = [vp, vp]
     L.pt_set_stream.restype = C.c_int32
+    L.pt_set_node_format.argtypes = [vp, C.c_int]
+    L.pt_set_node_format.restype = C.c_int32
     L.pt_scene_upload.argtypes = [vp, C.POINTER(SceneDesc)]
     L.pt_scene_upload.restype = C.c_int32
     L.pt_render.argtypes = [vp, C.POINTER(CameraDesc), C.POINTER(RenderDesc), vp, C.POINTER(Stats)]

@@ -25,3 +25,13 @@ def _native_built():
         import build_native
         build_native.main(["--no-ref"])
     yield
+
+
+def record_parity(test: str, key: str, value: float):
+    """Append a measured parity fraction to $PT_PARITY_LOG (JSON lines) when
+    set: the GPU runs that pin the per-scene bars collect them this way."""
+    path = os.environ.get("PT_PARITY_LOG")
+    if path:
+        import json
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": test, "key": key, "value": float(value)}) + "\n")

@@ -14,6 +14,7 @@ from pathlib import Path
 import numpy as np
 import pytest
 
+from conftest import record_parity
 from fixtures import parity_scenes
 from pathtracing_amd.recipe import write_recipe
 from pathtracing_amd.scene import FunctionInfiniteLight
@@ -22,6 +23,8 @@ pytestmark = pytest.mark.gpu
 
 ROOT = Path(__file__).resolve().parents[1]
 HARNESS = ROOT / "oracle" / "_ref" / "hip_harness"
+# measured bars (round 2); default 0.999
+DROPIN_FILM_MIN = {"sanmiguel": 0.99}
 
 
 @pytest.mark.skipif(not HARNESS.exists(), reason="hip_harness not built (needs /root/reference at build time)")
@@ -40,7 +43,8 @@ def test_drop_in_integrator_matches_reference_film(name, tmp_path):
     num = np.linalg.norm(gpu[..., :3] - ref[..., :3], axis=-1)
     den = np.maximum(np.linalg.norm(ref[..., :3], axis=-1), 1e-3 * ref[..., 3])
     frac = (num <= 1e-3 * den + 1e-7).mean()
-    assert frac >= 0.98, f"{name}: {frac:.4f} of pixels within 1e-3 rel L2"
+    record_parity(f"dropin_film_ref/{name}", "film", frac)
+    assert frac >= DROPIN_FILM_MIN.get(name, 0.999), f"{name}: {frac:.4f} of pixels within 1e-3 rel L2"
     # and the drop-in renders what the Python-side API renders for the same
     # scene (skipped with a sky: the reference estimates its power randomly)
     if any(isinstance(l, FunctionInfiniteLight) for l in setup.scene.infiniteLights):
@@ -49,4 +53,6 @@ def test_drop_in_integrator_matches_reference_film(name, tmp_path):
     film = setup.camera.GetFilm()
     film.Clear()
     integ.Render()
-    assert np.isclose(film.accum, gpu, rtol=1e-3, atol=1e-6).mean() >= 0.98
+    same = np.isclose(film.accum, gpu, rtol=1e-3, atol=1e-6).mean()
+    record_parity(f"dropin_vs_python/{name}", "film", same)
+    assert same >= 0.999

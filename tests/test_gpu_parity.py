@@ -1,17 +1,30 @@
 """GPU parity tests: the HIP path (through the C ABI) against the oracle and
-the reference's golden vectors.  Tolerances as tests/test_reference_parity.py:
-hit agreement >= 99.9 %, per-sample Li |dL| <= 1e-4 * max(1, |L|) for >= 99 %,
-film per-pixel relative L2 <= 1e-3 on >= 99 % of pixels, weights to 1e-9.
+the reference's golden vectors.
+
+Bars, pinned per scene to what was measured
+(tools/parity_report.py, gpurun_out/r2d/parity.json, round 2):
+  - closest-hit / any-hit agreement >= 99.99 % (measured 100 % on every
+    scene, both node layouts of the pool traversal);
+  - per-sample Li |dL| <= 1e-4 * max(1, |L|) for >= 99.9 % of samples
+    (measured 100 %, sanmiguel 2302 / 2304);
+  - film per-pixel relative L2 <= 1e-3 on every pixel (measured 100 %;
+    sanmiguel vs the reference 575 / 576: one sample's branch flip moves its
+    3x3 splat).
 """
 import numpy as np
 import pytest
 
 import oracle
+from conftest import record_parity
 from fixtures import NAMES, load
 from pathtracing_amd import native as N
 from pathtracing_amd import scenes
 
 pytestmark = pytest.mark.gpu
+
+HIT_MIN = 0.9999
+LI_MIN = {"sanmiguel": 0.999}           # default 1.0 (measured)
+FILM_MIN = {"sanmiguel": 0.998}         # default 1.0 (measured)
 
 
 @pytest.fixture(scope="module", params=NAMES)
@@ -26,47 +39,59 @@ def _rays(fx):
     return rays
 
 
-def _li_close(got, ref, frac_min=0.99):
+def _li_close(got, ref, frac_min=0.999, tag=None):
     err = np.abs(got - ref).max(-1)
     tol = 1e-4 * np.maximum(1.0, np.abs(ref).max(-1))
     frac = (err <= tol).mean()
-    assert frac >= frac_min, f"{frac:.4f} of samples within tolerance"
+    if tag:
+        record_parity(tag, "li", frac)
+    assert frac >= frac_min, f"{frac:.5f} of samples within tolerance (bar {frac_min})"
     np.testing.assert_allclose(got.astype(np.float64).mean((0, 1)), ref.astype(np.float64).mean((0, 1)),
                                rtol=5e-3, atol=1e-6)
 
 
-def _film_close(film, ref, frac_min=0.99):
+def _film_close(film, ref, frac_min=0.999, tag=None):
     np.testing.assert_allclose(film[..., 3], ref[..., 3], rtol=1e-9, atol=1e-12)
     num = np.linalg.norm(film[..., :3] - ref[..., :3], axis=-1)
     den = np.maximum(np.linalg.norm(ref[..., :3], axis=-1), 1e-3 * ref[..., 3])
     frac = (num <= 1e-3 * den + 1e-7).mean()
-    assert frac >= frac_min, f"film pixels within 1e-3 rel L2: {frac:.4f}"
+    if tag:
+        record_parity(tag, "film", frac)
+    assert frac >= frac_min, f"film pixels within 1e-3 rel L2: {frac:.5f} (bar {frac_min})"
 
 
-def test_gpu_trace_matches_oracle_and_reference(case):
+@pytest.mark.parametrize("nodes", [N.PT_NODES_FULL, N.PT_NODES_QUANTIZED])
+def test_gpu_trace_matches_oracle_and_reference(case, nodes):
+    """pt_trace runs the pool traversal, over the reference's 128-B clusters
+    or over the 64-B quantized nodes."""
     name, setup, integ, fx = case
     ctx = integ.context()
-    rays = _rays(fx)
-    hits, st = ctx.trace(rays, any_hit=False)
-    ref = oracle.trace(integ.flat, rays, any_hit=False)
-    agree = (hits["prim"] >= 0) == (ref["hit"] > 0)
-    assert agree.mean() >= 0.999
-    both = agree & (ref["hit"] > 0)
-    assert (hits["prim"][both] == ref["prim"][both]).mean() >= 0.999
-    np.testing.assert_allclose(hits["t"][both], ref["t"][both], rtol=1e-5, atol=1e-6)
-    # against the reference's own hits
-    assert ((hits["prim"] >= 0) == (fx["hits"][:, 0] > 0)).mean() >= 0.999
-    anyh, _ = ctx.trace(rays, any_hit=True)
-    assert ((anyh["prim"] > 0) == (fx["any"] > 0)).mean() >= 0.999
-    assert st["rays_closest"] == len(rays) and st["nodes_closest"] > 0
+    ctx.set_node_format(nodes)
+    try:
+        rays = _rays(fx)
+        hits, st = ctx.trace(rays, any_hit=False)
+        ref = oracle.trace(integ.flat, rays, any_hit=False)
+        agree = (hits["prim"] >= 0) == (ref["hit"] > 0)
+        assert agree.mean() >= HIT_MIN
+        both = agree & (ref["hit"] > 0)
+        assert (hits["prim"][both] == ref["prim"][both]).mean() >= HIT_MIN
+        np.testing.assert_allclose(hits["t"][both], ref["t"][both], rtol=1e-5, atol=1e-6)
+        # against the reference's own hits
+        assert ((hits["prim"] >= 0) == (fx["hits"][:, 0] > 0)).mean() >= HIT_MIN
+        anyh, _ = ctx.trace(rays, any_hit=True)
+        assert ((anyh["prim"] > 0) == (fx["any"] > 0)).mean() >= HIT_MIN
+        assert st["rays_closest"] == len(rays) and st["nodes_closest"] > 0
+    finally:
+        ctx.set_node_format(N.PT_NODES_AUTO)
 
 
 def test_gpu_li_matches_oracle_and_reference(case):
     name, setup, integ, fx = case
     L = integ.RenderSamples()
     Lo, _, _ = oracle.li(integ)
-    _li_close(L, Lo)
-    _li_close(L, fx["li_L"])
+    bar = LI_MIN.get(name, 1.0)
+    _li_close(L, Lo, bar, f"li_oracle/{name}")
+    _li_close(L, fx["li_L"], bar, f"li_ref/{name}")
 
 
 def test_gpu_film_matches_oracle_and_reference(case):
@@ -76,9 +101,10 @@ def test_gpu_film_matches_oracle_and_reference(case):
     st = integ.Render()
     ref, cnt = oracle.render(integ, threads=4)
     # a sample whose path flips a branch (FMA / ulp) moves its 3x3 filter
-    # footprint: the film bar is the per-sample bar spread over 9 pixels
-    _film_close(film.accum, ref, frac_min=0.98)
-    _film_close(film.accum, fx["film"], frac_min=0.98)
+    # footprint: the bar is pinned per scene to the measured fraction
+    bar = FILM_MIN.get(name, 1.0)
+    _film_close(film.accum, ref, bar, f"film_oracle/{name}")
+    _film_close(film.accum, fx["film"], bar, f"film_ref/{name}")
     assert st["paths"] == cnt["paths"]
     # the wavefront traces the reference's closest-hit queries (a rare RR /
     # lobe branch flip may add or drop one)
@@ -102,7 +128,7 @@ def test_gpu_sharded_films_sum_to_the_frame():
         parts.append(film.accum.copy())
     np.testing.assert_allclose(sum(parts), full, rtol=1e-9, atol=1e-12)
     ref, _ = oracle.render(integ, threads=4)
-    _film_close(full, ref)
+    _film_close(full, ref, 0.999, "film_oracle/sharded_c3")
 
 
 @pytest.mark.parametrize("W,H,pif", [(37, 23, 0), (64, 64, 256), (8, 8, 64)])
@@ -115,7 +141,7 @@ def test_gpu_odd_sizes_and_tiny_wavefronts(W, H, pif):
     film.Clear()
     integ.Render(paths_in_flight=pif)
     ref, _ = oracle.render(integ, threads=4)
-    _film_close(film.accum, ref)
+    _film_close(film.accum, ref, 0.999, f"film_oracle/odd_{W}x{H}_{pif}")
 
 
 @pytest.mark.parametrize("depth", [0, 1, 2])
@@ -124,7 +150,7 @@ def test_gpu_shallow_depths(depth):
     integ = setup.make_integrator()
     L = integ.RenderSamples()
     Lo, _, _ = oracle.li(integ)
-    _li_close(L, Lo)
+    _li_close(L, Lo, 0.999, f"li_oracle/zoo_depth{depth}")
     if depth == 0:
         assert not L.any()
 
@@ -149,7 +175,7 @@ def test_gpu_sanmiguel_small_matches_oracle():
     integ = setup.make_integrator()
     L = integ.RenderSamples()
     Lo, _, _ = oracle.li(integ)
-    _li_close(L, Lo)
+    _li_close(L, Lo, 0.995, "li_oracle/sanmiguel_2pct")
 
 
 @pytest.fixture(scope="module")
@@ -160,13 +186,20 @@ def c4_full():
 
 def test_gpu_sanmiguel_full_size_per_sample_parity(c4_full):
     """The full ~10 M-triangle C4 scene: per-sample Li of a pixel band against
-    the oracle over the same BVH."""
+    the oracle over the same BVH, through the default big-scene path (pool
+    traversal over quantized nodes), and the same band over the reference's
+    full clusters bit for bit.  Measured 99.19 % of 3,072 samples within the
+    per-sample bar: depth-128 paths through ~10 M triangles cross many RR /
+    lobe / alpha thresholds, and an ulp of FMA difference at any of them
+    changes the rest of the path (identical for both node layouts)."""
     setup, integ = c4_full
     assert integ.flat.tri_flags.shape[0] > 9_000_000
     b, e = 192 * 40, 192 * 48
     L = integ.RenderSamples(pixel_begin=b, pixel_end=e)
     Lo, _, _ = oracle.li(integ, pixel_begin=b, pixel_end=e)
-    _li_close(L, Lo)
+    _li_close(L, Lo, 0.99, "li_oracle/c4_band")
+    Lf = integ.RenderSamples(pixel_begin=b, pixel_end=e, flags=N.PT_RENDER_NODES_FULL)
+    np.testing.assert_array_equal(L, Lf)
 
 
 def test_gpu_sanmiguel_full_size_shards_sum(c4_full):
@@ -274,12 +307,15 @@ def test_gpu_light_samples_match_oracle_and_reference(case):
     assert close.mean() >= 0.99
 
 
-@pytest.mark.parametrize("name", ["cornell_c3", "zoo", "sanmiguel"])
-def test_gpu_pool_and_simple_traversal_agree_bit_for_bit(name):
+@pytest.mark.parametrize("name", ["cornell_c3", "zoo", "sanmiguel", "instances"])
+@pytest.mark.parametrize("nodes", [N.PT_RENDER_NODES_FULL, N.PT_RENDER_NODES_QUANTIZED])
+def test_gpu_pool_and_simple_traversal_agree_bit_for_bit(name, nodes):
     """The persistent refilling traversal (pt_pool.h) and the one-ray-per-lane
-    one visit the same nodes in the same order per ray: identical radiance."""
+    one visit the same nodes in the same order per ray: identical radiance.
+    Over the quantized nodes the pool traversal visits a superset of nodes
+    (outward-rounded boxes) in the same order, with the same result here."""
     setup, integ, fx = load(name)
-    a = integ.RenderSamples(flags=N.PT_RENDER_TRAVERSAL_POOL)
+    a = integ.RenderSamples(flags=N.PT_RENDER_TRAVERSAL_POOL | nodes)
     b = integ.RenderSamples(flags=N.PT_RENDER_TRAVERSAL_SIMPLE)
     np.testing.assert_array_equal(a, b)
 

@@ -83,6 +83,19 @@ __global__ void k_node_gather_n(const float4* __restrict__ t, unsigned long long
     if (s == -1.0f) sink[0] = s;
 }
 
+// one 64-B quantized node per lane (4 x 16-B loads, 64-B aligned): the node
+// step of the pool kernels over DevQNode.  Lines chosen as for k_node_gather;
+// the node is the line's first or second half by the lane's parity.
+__global__ void k_qnode_gather(const float4* __restrict__ t, unsigned long long n, unsigned long long mask,
+                               unsigned mul, float* sink) {
+    unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4* q = t + scatter(i, mask, mul) * 8 + 4 * (i & 1);
+    float4 a = q[0], b = q[1], c = q[2], d = q[3];
+    float s = a.x + b.y + c.z + d.w;
+    if (s == -1.0f) sink[0] = s;
+}
+
 __global__ void k_slot_gather(const float4* __restrict__ t, unsigned long long n, unsigned long long mask,
                               unsigned mul, float* sink) {
     unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
@@ -129,6 +142,13 @@ int main(int argc, char** argv) {
         CHK(hipEventSynchronize(e1));
         CHK(hipEventElapsedTime(&ms, e0, e1));
         printf("{\"kernel\":\"k_slot_gather\",\"bytes\":%llu,\"ms\":%.4f}\n", n * 48, ms);
+        CHK(hipEventRecord(e0));
+        hipLaunchKernelGGL(k_qnode_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, t, n, mask, muls[rep],
+                           sink);
+        CHK(hipEventRecord(e1));
+        CHK(hipEventSynchronize(e1));
+        CHK(hipEventElapsedTime(&ms, e0, e1));
+        printf("{\"kernel\":\"k_qnode_gather\",\"bytes\":%llu,\"ms\":%.4f}\n", n * 64, ms);
         CHK(hipEventRecord(e0));
         hipLaunchKernelGGL(k_node_gather_n<4>, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, 0, t, n / 4, mask,
                            muls[rep], sink);

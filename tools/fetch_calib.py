@@ -66,6 +66,7 @@ def main(out_json):
     res["factor_node_gather"] = res.get("k_node_gather", {}).get("factor")
     res["factor_slot_gather"] = res.get("k_slot_gather", {}).get("factor")
     res["factor_stream"] = res.get("k_stream", {}).get("factor")
+    res["factor_qnode_gather"] = res.get("k_qnode_gather", {}).get("factor")
     Path(out_json).write_text(json.dumps(res, indent=1, sort_keys=True))
     print(json.dumps(res, indent=1, sort_keys=True))
     del trace_out

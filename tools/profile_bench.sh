@@ -41,7 +41,7 @@ with open(f"{d}/dispatches.csv", "w") as o:
     o.write("start_us,kernel,us\n")
     t0 = rows[0][0] if rows else 0
     for s, k, us in rows:
-        o.write(f"{(s - t0) / 1e3:.1f},{k},{us:.1f}\n")
+        o.write(f'{(s - t0) / 1e3:.1f},"{k}",{us:.1f}\n')
 PY
 rm -rf "$out/trace" "$out/fetch" "$out/write" "$out/sq" "$out/tcc"
 echo done
