@@ -96,7 +96,7 @@ def _json(path: Path):
         return None
 
 
-def cpu_baseline(setup, target_s: float = 15.0):
+def cpu_baseline(setup, config: str, target_s: float = 15.0):
     """The oracle (CPU restatement, 'port') on the host cores, on a bounded
     sample of the same workload: full frame at a reduced SPP sized from a
     pilot run to take about target_s seconds.  The port/reference speed ratio
@@ -127,6 +127,14 @@ def cpu_baseline(setup, target_s: float = 15.0):
     ratio = _json(ROOT / "profiles" / "r02_cpu_ratio.json")
     if ratio:
         out["port_vs_reference"] = ratio.get("summary")
+        # the reference's own speed on this host, estimated from the port
+        # through the ratio measured on the closest scene class
+        key = {"c4": "c4_recipe_2pct_160x90_16spp_depth128", "c1": "c1_example1_path_256x256_16spp"}.get(
+            config, "c1_example1_path_256x256_16spp")
+        r = ratio.get(key, {}).get("port_over_reference")
+        if r:
+            out["reference_estimate"] = {"value": round(out["value"] / r, 3), "port_over_reference": r,
+                                         "scene_class": key}
     return out
 
 
@@ -362,7 +370,7 @@ def main():
             "roofline": roof,
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(build_setup(args.config, args.spp), args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(build_setup(args.config, args.spp), args.config, args.cpu_seconds)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -1,0 +1,88 @@
+"""Speed of the CPU restatement (oracle/pt_oracle.c, the `port` bench.py
+times on the GPU box) against the reference itself (oracle/_ref/ref_harness,
+built from /root/reference; it cannot travel to the GPU box), on the same
+scenes, sample stream and thread count, in this container (BASELINE.md §3,
+SURVEY.md §8(d) "CPU baseline timing").  TEST INFRASTRUCTURE.
+
+    python tools/cpu_ratio.py profiles/r02_cpu_ratio.json
+
+Both sides run a fixed-SPP tile loop over Li with the counter-based sample
+stream (ref_harness `time ... li`; oracle.render); Mrays/s counts every
+Scene::Intersect + Scene::IntersectPred.  Median of 3 runs each.  The
+reference's own TileIntegrator::Render (adaptive rounds, UniformSampler) is
+timed beside them for scale.
+"""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "oracle"))
+
+HARNESS = ROOT / "oracle" / "_ref" / "ref_harness"
+
+
+def scenes_():
+    from pathtracing_amd import scenes
+    return {
+        "c1_example1_path_256x256_16spp": lambda: scenes.example_1(W=256, H=256, spp=16),
+        "heightfield_1M_tris_256x256_16spp": lambda: scenes.heightfield(n=700, W=256, H=256, spp=16),
+        "c4_recipe_2pct_160x90_16spp_depth128": lambda: scenes.sanmiguel(W=160, H=90, spp=16, detail=0.02,
+                                                                       tex_size=64),
+    }
+
+
+def _rec(stdout):
+    # Render's progress line ends in '\r' without a newline: take the record from its brace
+    return next(json.loads(l[l.index("{"):]) for l in stdout.replace("\r", "\n").splitlines()
+                if "{" in l)["mrays_per_s"]
+
+
+def median(xs):
+    return sorted(xs)[len(xs) // 2]
+
+
+def main(out):
+    import oracle
+    from pathtracing_amd.recipe import write_recipe
+    threads = os.cpu_count() or 8
+    res = {"_meta": {"threads": threads, "host": "build container", "runs": 3,
+                     "cpu": next((l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
+                                  if l.startswith("model name")), "?")}}
+    for name, mk in scenes_().items():
+        setup = mk()
+        integ = setup.make_integrator()
+        with tempfile.TemporaryDirectory() as tmp:
+            recipe = write_recipe(Path(tmp), setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
+                                  setup.max_depth, setup.light_sampler, setup.extra_lights)
+            ref, ren = [], []
+            for _ in range(3):
+                r = subprocess.run([str(HARNESS), str(recipe), "time", str(Path(tmp) / "o"), str(threads),
+                                    str(setup.spp), "li"], capture_output=True, text=True, check=True)
+                ref.append(_rec(r.stdout))
+                r = subprocess.run([str(HARNESS), str(recipe), "time", str(Path(tmp) / "o"), str(threads),
+                                    str(setup.spp), "render"], capture_output=True, text=True, check=True)
+                ren.append(_rec(r.stdout))
+        port = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            _, cnt = oracle.render(integ, threads=threads)
+            dt = time.perf_counter() - t0
+            port.append((cnt["closest"] + cnt["any"]) / dt / 1e6)
+        res[name] = {"reference_li_loop_mrays": round(median(ref), 3), "port_mrays": round(median(port), 3),
+                     "port_over_reference": round(median(port) / median(ref), 3),
+                     "reference_render_mrays": round(median(ren), 3)}
+        print(name, res[name], flush=True)
+    ratios = [v["port_over_reference"] for k, v in res.items() if not k.startswith("_")]
+    res["summary"] = {"port_over_reference_min": min(ratios), "port_over_reference_max": max(ratios),
+                      "threads": threads, "source": "profiles/r02_cpu_ratio.json (tools/cpu_ratio.py)"}
+    Path(out).write_text(json.dumps(res, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
