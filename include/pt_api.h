@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PT_API_VERSION 2
+#define PT_API_VERSION 3
 
 typedef int32_t pt_status;
 #define PT_OK 0
@@ -240,6 +240,7 @@ enum { PT_FILTER_MITCHELL = 0, PT_FILTER_BOX = 1, PT_FILTER_GAUSSIAN = 2 };
 #define PT_RENDER_TRAVERSAL_SIMPLE 0x8u /* force one ray per lane (default: by BVH size) */
 #define PT_RENDER_NODES_FULL 0x10u      /* pool traversal over the 128-B reference clusters */
 #define PT_RENDER_NODES_QUANTIZED 0x20u /* ... over the 64-B quantized nodes (the default)  */
+#define PT_RENDER_ADAPTIVE 0x40u        /* pt_render: TileIntegrator::Render's adaptive rounds */
 
 typedef struct pt_render_desc {
     uint32_t integrator;       /* PT_INTEGRATOR_*                               */
@@ -300,6 +301,18 @@ pt_status pt_scene_upload(pt_ctx* ctx, const pt_scene_desc* scene);
  * into film_accum, a host or a device pointer (detected). */
 pt_status pt_render(pt_ctx* ctx, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_accum,
                     pt_stats* stats);
+/* TileIntegrator::Render's adaptive sampling (Integrators.cpp:55-86,
+ * Util.hpp:8-43): each pixel renders rounds of spp samples (round r = stream
+ * samples r*spp .. r*spp+spp-1) until the relative variance of all three
+ * luminance-weighted channels is <= 1.5 or it has 128*spp samples; every
+ * sample is splatted into film_accum as in pt_render.  sample_counts (NULL,
+ * or W*H u32, host or device) receives each pixel's sample count (0 for
+ * pixels outside this call's work).  pixel_begin/end select the work pixels;
+ * shard_count > 1 splits the frame by 32x32 tiles (tile % shard_count ==
+ * shard_index; Integrators.cpp:33), so each pixel's rounds run on one shard.
+ * pt_render with PT_RENDER_ADAPTIVE is this call with sample_counts NULL. */
+pt_status pt_render_adaptive(pt_ctx* ctx, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_accum,
+                             uint32_t* sample_counts, pt_stats* stats);
 /* Per-sample radiance of pixels [pixel_begin, pixel_end) (0,0 = all), samples
  * [0, spp): out_L[((pix - pixel_begin) * spp + s) * 3] (host pointer).  The
  * unfiltered Integrator::Li values behind pt_render; for parity tests. */

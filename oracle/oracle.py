@@ -40,6 +40,7 @@ def lib():
         L.oracle_trace.argtypes = [vp, vp, C.c_uint32, C.c_int, vp]
         L.oracle_li.argtypes = [vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp, C.POINTER(Counters)]
         L.oracle_render.argtypes = [vp, vp, vp, vp, C.c_int, C.POINTER(Counters)]
+        L.oracle_render_adaptive.argtypes = [vp, vp, vp, vp, vp, C.c_int, C.POINTER(Counters)]
         L.oracle_bsdf.argtypes = [vp, C.c_int, vp, C.c_uint32, vp]
         L.oracle_lights.argtypes = [vp, vp, C.c_uint32, vp]
         L.oracle_filter_table.argtypes = [vp, vp]
@@ -91,6 +92,19 @@ def render(integrator, threads: int = 1, shard_index: int = 0, shard_count: int 
     assert lib().oracle_render(_desc(integrator.flat), C.byref(cam), C.byref(rd), film.ctypes.data, int(threads),
                                C.byref(cnt)) == 0
     return film, cnt.as_dict()
+
+
+def render_adaptive(integrator, threads: int = 1, shard_index: int = 0, shard_count: int = 1):
+    """(film, per-pixel sample counts (H, W), counters) of TileIntegrator::
+    Render's adaptive loop."""
+    cam, rd = integrator.desc(shard_index=shard_index, shard_count=shard_count)
+    W, H = integrator.camera.GetFilm().Resolution()
+    film = np.zeros((H, W, 4), np.float64)
+    counts = np.zeros((H, W), np.uint32)
+    cnt = Counters()
+    assert lib().oracle_render_adaptive(_desc(integrator.flat), C.byref(cam), C.byref(rd), film.ctypes.data,
+                                        counts.ctypes.data, int(threads), C.byref(cnt)) == 0
+    return film, counts, cnt.as_dict()
 
 
 def bsdf(flat, material: int, cases: np.ndarray) -> np.ndarray:

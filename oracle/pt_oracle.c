@@ -1756,11 +1756,51 @@ typedef struct {
     const pt_camera_desc* cam;
     const pt_render_desc* rd;
     double* film;
+    uint32_t* counts; /* adaptive: per-pixel sample counts, else NULL */
     int tiles_x, tiles;
     volatile int next;
     pthread_mutex_t mu;
     oracle_counters total;
 } job_t;
+
+/* TileIntegrator::Render's adaptive rounds for one pixel (Integrators.cpp:
+ * 55-86; VarianceEstimator, Util.hpp:8-43): rounds of spp samples, round r
+ * drawing stream samples r*spp .. r*spp+spp-1, until all three relative
+ * variances of color * dvec3(0.2126f, 0.7152f, 0.0722f) are <= 1.5, at most
+ * 128*spp samples.  Welford with the reference build's contraction: the
+ * luminance product fused into both differences and into S's update.
+ * Returns the pixel's sample count. */
+static double rel_variance(double mean, double S, uint64_t n) {
+    if (mean == 0) return 0;
+    double var = n > 1 ? S / (double)(n - 1) : 0.0;
+    return 1.96 * sqrt(var / (double)n) / mean;
+}
+static uint32_t adaptive_pixel(const integ_t* I, const job_t* J, double inv_int, int bx0, int by0, int bw, int bh,
+                               double* tilebuf, int x, int y) {
+    const double wl[3] = {(double)0.2126f, (double)0.7152f, (double)0.0722f};
+    const uint32_t spp = J->rd->spp;
+    double mean[3] = {0, 0, 0}, S[3] = {0, 0, 0};
+    uint64_t n = 0;
+    for (uint32_t round = 0; n < 128ull * spp; round++) {
+        for (uint32_t k = 0; k < spp; k++) {
+            double px, py;
+            v3 L = li_one(I, J->cam, J->rd->seed, (uint32_t)x, (uint32_t)y, round * spp + k, &px, &py);
+            film_add(J->rd, inv_int, bw, bh, tilebuf, px - bx0, py - by0, L);
+            const double v[3] = {(double)L.x, (double)L.y, (double)L.z};
+            const double dn = (double)(++n);
+            for (int c = 0; c < 3; c++) {
+                const double delta = fma(v[c], wl[c], -mean[c]);
+                mean[c] = delta / dn + mean[c];
+                const double delta2 = fma(v[c], wl[c], -mean[c]);
+                S[c] = fma(delta, delta2, S[c]);
+            }
+        }
+        if (rel_variance(mean[0], S[0], n) <= 1.5 && rel_variance(mean[1], S[1], n) <= 1.5 &&
+            rel_variance(mean[2], S[2], n) <= 1.5)
+            break;
+    }
+    return (uint32_t)n;
+}
 
 static void* render_worker(void* arg) {
     job_t* J = (job_t*)arg;
@@ -1783,13 +1823,22 @@ static void* render_worker(void* arg) {
         int bx1 = x1 + rx > W ? W : x1 + rx, by1 = y1 + ry > H ? H : y1 + ry;
         int bw = bx1 - bx0, bh = by1 - by0;
         double* tilebuf = (double*)calloc((size_t)bw * bh * 4, sizeof(double));
+        if (J->counts && (uint32_t)tile % sc != J->rd->shard_index) { /* adaptive shards own whole tiles */
+            free(tilebuf);
+            continue;
+        }
         for (int y = y0; y < y1; y++)
-            for (int x = x0; x < x1; x++)
+            for (int x = x0; x < x1; x++) {
+                if (J->counts) {
+                    J->counts[(size_t)y * W + x] = adaptive_pixel(&I, J, inv_int, bx0, by0, bw, bh, tilebuf, x, y);
+                    continue;
+                }
                 for (uint32_t smp = J->rd->shard_index; smp < J->rd->spp; smp += sc) {
                     double px, py;
                     v3 L = li_one(&I, J->cam, J->rd->seed, (uint32_t)x, (uint32_t)y, smp, &px, &py);
                     film_add(J->rd, inv_int, bw, bh, tilebuf, px - bx0, py - by0, L);
                 }
+            }
         pthread_mutex_lock(&J->mu);
         for (int y = 0; y < bh; y++)
             for (int x = 0; x < bw; x++)
@@ -1810,8 +1859,20 @@ static void* render_worker(void* arg) {
     return NULL;
 }
 
+static int render_job(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render_desc* rd, double* film,
+                      uint32_t* counts, int threads, oracle_counters* cnt);
 int oracle_render(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render_desc* rd, double* film,
                   int threads, oracle_counters* cnt) {
+    return render_job(s, cam, rd, film, NULL, threads, cnt);
+}
+int oracle_render_adaptive(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render_desc* rd,
+                           double* film, uint32_t* counts, int threads, oracle_counters* cnt) {
+    if (!counts) return -1;
+    memset(counts, 0, sizeof(uint32_t) * (size_t)cam->width * cam->height);
+    return render_job(s, cam, rd, film, counts, threads, cnt);
+}
+static int render_job(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render_desc* rd, double* film,
+                      uint32_t* counts, int threads, oracle_counters* cnt) {
     if (!s || !cam || !rd || !film) return -1;
     if (threads < 1) threads = 1;
     job_t J;
@@ -1820,6 +1881,7 @@ int oracle_render(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_re
     J.cam = cam;
     J.rd = rd;
     J.film = film;
+    J.counts = counts;
     J.tiles_x = (cam->width + 31) / 32;
     J.tiles = J.tiles_x * ((cam->height + 31) / 32);
     pthread_mutex_init(&J.mu, NULL);

@@ -43,6 +43,10 @@ int oracle_li(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render
  * 32x32 tiles, samples s with s % shard_count == shard_index. */
 int oracle_render(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_accum,
                   int threads, oracle_counters* cnt);
+/* TileIntegrator::Render's adaptive sampling (Integrators.cpp:55-86): the
+ * film plus each pixel's sample count (W*H u32).  Shards own 32x32 tiles. */
+int oracle_render_adaptive(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render_desc* rd,
+                           double* film_accum, uint32_t* counts, int threads, oracle_counters* cnt);
 
 /* Material cases, layout as oracle/ref_harness.cpp cmd_bsdf (27 floats in, 20 out). */
 int oracle_bsdf(const pt_scene_desc* s, int material, const float* in, uint32_t n, float* out);

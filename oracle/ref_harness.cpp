@@ -67,13 +67,33 @@ static inline float draw_float(uint32_t key, uint32_t dim) {
     return (float)(pcg_hash(key + 0x9E3779B9u * dim) >> 8) * (1.0f / 16777216.0f);
 }
 
-class DetSampler : public Sampler {
+// TileIntegrator::Render's adaptive loop calls StartPixelSample(p, 0..spp-1)
+// once per round for the same pixel (Integrators.cpp:59-62): in `rounds`
+// mode the sampler numbers them r*spp + index, the stream samples the device
+// draws for round r (its index restart stands for the reference samplers'
+// fresh random state each round).
+class DetSampler;
+static thread_local DetSampler* g_stream = nullptr;  // the sampler of the sample being traced on this thread
+class DetSampler : public Sampler, public std::enable_shared_from_this<DetSampler> {
 public:
-    DetSampler(unsigned spp, uint32_t seed, int width) : spp(spp), seed(seed), width(width) {}
+    DetSampler(unsigned spp, uint32_t seed, int width, bool rounds = false)
+        : spp(spp), seed(seed), width(width), rounds(rounds) {}
     unsigned int SamplesPerPixel() const override { return spp; }
     void StartPixelSample(const glm::ivec2& p, int index) override {
-        key = stream_key(seed, (uint32_t)(p.y * width + p.x), (uint32_t)index);
+        pix = (uint32_t)(p.y * width + p.x);
+        smp = (uint32_t)index;
+        if (rounds) {
+            if (p != cur) {
+                cur = p;
+                round = 0;
+            } else if (index == 0) {
+                round++;
+            }
+            smp = round * spp + (uint32_t)index;
+        }
+        key = stream_key(seed, pix, smp);
         dim = 0;
+        g_stream = this;
     }
     double get1D() override { return next(); }
     glm::dvec2 get2D() override {
@@ -91,20 +111,30 @@ public:
         }
         return r;
     }
-    std::shared_ptr<Sampler> Clone() const override { return std::make_shared<DetSampler>(spp, seed, width); }
+    // Render clones the sampler for the camera draws, but Li draws from the
+    // integrator's own `sampler` (Integrators.cpp:38 vs 147, 210): in rounds
+    // mode (single-threaded Render) the clone is this object, so a sample's
+    // path draws continue its camera draws as on the device
+    std::shared_ptr<Sampler> Clone() const override {
+        if (rounds) return std::const_pointer_cast<DetSampler>(shared_from_this());
+        return std::make_shared<DetSampler>(spp, seed, width, rounds);
+    }
     uint32_t dims() const { return dim; }
+    uint32_t pixel() const { return pix; }
+    uint32_t sample() const { return smp; }
 
 private:
     float next() { return draw_float(key, dim++); }
     unsigned spp;
     uint32_t seed;
     int width;
+    bool rounds;
+    glm::ivec2 cur{-1, -1};
+    uint32_t round = 0, pix = 0, smp = 0;
     uint32_t key = 0;
     uint32_t dim = 0;
 };
 
-// The sampler of the sample being traced (run_li is single-threaded).
-static DetSampler* g_stream = nullptr;
 
 // HomogeneusMedium (Medium.hpp:14-61) with its two hidden random_float() draws
 // (Medium.hpp:28-30) taken from the deterministic stream instead of the
@@ -719,6 +749,55 @@ static void cmd_time(World& w, int threads, unsigned spp, const std::string& mod
            rays / secs / 1e6);
 }
 
+// --- adaptive: the reference's own TileIntegrator::Render (Integrators.cpp:23-129)
+// with its adaptive rounds, driven by DetSampler in rounds mode on one
+// thread.  Li is wrapped to record every sample Render traces (pixel, stream
+// sample, radiance); the film is rebuilt from the records with FilmTile::Add
+// (Film.private keeps the reference's own accumulation out of reach) and the
+// per-pixel sample counts are the records per pixel.
+struct AdaptRec { uint32_t pixel, sample; float L[3]; };
+static std::vector<AdaptRec> g_adapt;
+template <class Base>
+struct Recording : Base {
+    using Base::Base;
+    glm::vec3 Li(Ray ray) const override {
+        ray.time = 0;  // shutter is uninitialised in the reference
+        glm::vec3 L = Base::Li(ray);
+        g_adapt.push_back({g_stream->pixel(), g_stream->sample(), {L.x, L.y, L.z}});
+        return L;
+    }
+};
+static void cmd_adaptive(World& w, const std::string& out) {
+    auto sampler = std::make_shared<DetSampler>(w.spp, w.seed, w.W, true);
+    std::shared_ptr<Integrator> integ;
+    if (w.integ == "simple") integ = std::make_shared<Recording<SimplePathIntegrator>>(w.scene, w.camera, sampler, w.maxDepth);
+    else if (w.integ == "volpath")
+        integ = std::make_shared<Recording<VolPathIntegrator>>(w.scene, w.camera, sampler, w.ls, w.maxDepth);
+    else integ = std::make_shared<Recording<PathIntegrator>>(w.scene, w.camera, sampler, w.ls, w.maxDepth);
+    g_adapt.clear();
+    integ->Render(1);
+    std::vector<uint32_t> counts((size_t)w.W * w.H, 0);
+    Bounds2i all{{0, 0}, {w.W, w.H}};
+    FilmTile tile = w.film->GetFilmTile(all);
+    for (const auto& r : g_adapt) {
+        counts[r.pixel]++;
+        const uint32_t key = stream_key(w.seed, r.pixel, r.sample);
+        const glm::dvec2 jit{(double)draw_float(key, 0), (double)draw_float(key, 1)};
+        const glm::dvec2 p = glm::dvec2{(double)(r.pixel % w.W), (double)(r.pixel / w.W)} + jit;
+        tile.Add(p, glm::dvec3(r.L[0], r.L[1], r.L[2]));
+    }
+    std::vector<double> acc((size_t)w.W * w.H * 4);
+    for (int y = 0; y < w.H; y++)
+        for (int x = 0; x < w.W; x++) {
+            const FilmTilePixel& p = tile.At({x, y});
+            double* o = &acc[((size_t)y * w.W + x) * 4];
+            o[0] = p.RGB.x; o[1] = p.RGB.y; o[2] = p.RGB.z; o[3] = p.weight;
+        }
+    wr(out + ".adaptive_film.bin", acc);
+    wr(out + ".adaptive_counts.bin", counts);
+    wr(out + ".adaptive_recs.bin", g_adapt);
+}
+
 // --- tonemap: Film::WritePNG's pixel loop (Film.hpp:183-196) over an
 // accumulation buffer {sum RGB*w, sum w} (W*H*4 doubles): the reference's own
 // reinhard_jodie / ACESFilm and linear_to_sRGB, through the writer's
@@ -795,6 +874,7 @@ int main(int argc, char** argv) {
         if (argc >= 9) { x0 = atoi(argv[4]); y0 = atoi(argv[5]); x1 = atoi(argv[6]); y1 = atoi(argv[7]); spp = atoi(argv[8]); }
         cmd_li(w, out, x0, y0, x1, y1, spp);
     } else if (cmd == "film") cmd_film(w, out, w.spp);
+    else if (cmd == "adaptive") cmd_adaptive(w, out);
     else if (cmd == "bsdf") cmd_bsdf(w, out, argv[4], atoi(argv[5]));
     else if (cmd == "camera") cmd_camera(w, out, argv[4]);
     else if (cmd == "lights") cmd_lights(w, out, argv[4]);

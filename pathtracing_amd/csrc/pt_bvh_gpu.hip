@@ -271,7 +271,17 @@ __global__ __launch_bounds__(kBlock) void k_bin(const Item* __restrict__ items, 
     uint32_t* hmx = s_max[wv];
     const uint32_t w0 = blockIdx.x * kSpan + (uint32_t)wv * (kSpan / NWV);
     uint32_t cur = kInv;  // node of this wave's LDS histogram (wave-uniform)
+    // the histogram is private to the wave, but its lanes hand entries to
+    // each other between phases (init -> atomics -> flush): an LDS fence at
+    // wave scope + a wave barrier orders them under the memory model, not
+    // just by gfx9's in-order LDS issue
+    auto wave_sync = []() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
     auto flush = [&]() {
+        wave_sync();
         for (int j = lane; j < 96; j += 64) {
             if (!hc[j]) continue;
             const uint64_t g = (uint64_t)cur * 96 + j;
@@ -281,6 +291,7 @@ __global__ __launch_bounds__(kBlock) void k_bin(const Item* __restrict__ items, 
                 atomicMax(&bmax[g * 3 + a], hmx[j * 3 + a]);
             }
         }
+        wave_sync();
     };
     for (int r = 0; r < (int)(kSpan / NWV / 64); r++) {
         const uint32_t c0 = w0 + r * 64;
@@ -294,6 +305,7 @@ __global__ __launch_bounds__(kBlock) void k_bin(const Item* __restrict__ items, 
                 hmx[j] = 0;
                 if (j < 96) hc[j] = 0;
             }
+            wave_sync();
             cur = ta;
         }
         const uint32_t i = c0 + lane;

@@ -70,6 +70,7 @@ struct RenderParams {
     uint32_t npix_work;             // pixels per sample index
     uint32_t tiled, tiles_x;
     uint32_t pixel_begin;
+    const uint32_t* pix_list;       // adaptive rounds: work pixel i = pix_list[i] (linear id), else null
     unsigned long long chunk_total; // npix_work * (s_hi - s_lo)
     uint32_t filter;
     int rad_x, rad_y;
@@ -102,6 +103,21 @@ __global__ void k_shadow_tr(PathSoA next, float* sample_L, const ShadowRec* sq, 
 __global__ void k_fill(RenderParams R, uint32_t n, PathSoA next, uint32_t* cnt, unsigned long long* next_sample);
 __global__ void k_resolve(const double* film, uint32_t npx, uint32_t tonemap, uint8_t* rgb);
 __global__ void k_gather(RenderParams R, const float* sample_L, double* film);
+
+// Adaptive sampling (TileIntegrator::Render's per-pixel rounds,
+// Integrators.cpp:59-86): three VarianceEstimators per pixel (Util.hpp:8-43)
+struct AdaptEst {
+    double mean[3], S[3];
+};
+#define PT_ADAPT_MAX_ROUNDS 128   // while (Samples() < 128 * samplesPerPixel)
+#define PT_ADAPT_REL_VAR 1.5      // minRelativeVariance
+__global__ void k_adapt_init(RenderParams R, uint32_t shard_index, uint32_t shard_count, uint32_t* list,
+                             uint32_t* cnt, AdaptEst* est, uint32_t* counts);
+__global__ void k_adapt_map(const uint32_t* list, const uint32_t* n, int32_t* map);
+__global__ void k_adapt_accum(RenderParams R, const float* sample_L, AdaptEst* est, uint32_t* counts);
+__global__ void k_adapt_gather(RenderParams R, const int32_t* map, const float* sample_L, double* film);
+__global__ void k_adapt_decide(const uint32_t* list, const uint32_t* n, const AdaptEst* est, const uint32_t* counts,
+                               uint32_t max_samples, int32_t* map, uint32_t* out_list, uint32_t* out_cnt);
 __global__ void k_interact(const pt_ray* rays, uint32_t n, float* out);
 __global__ void k_bsdf_cases(int mid, const float* in, uint32_t n, float* out);
 __global__ void k_light_cases(const float* in, uint32_t n, float* out);

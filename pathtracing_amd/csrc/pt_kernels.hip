@@ -443,7 +443,11 @@ __global__ void k_light_cases(const float* __restrict__ in, uint32_t n, float* _
 
 // ------------------------------------------------------------------ camera / regeneration
 __device__ __forceinline__ void work_pixel(const RenderParams& R, uint32_t pix_i, uint32_t& x, uint32_t& y) {
-    if (R.tiled) {  // 8x8 pixel tiles, tile-major: neighbouring lanes -> neighbouring pixels
+    if (R.pix_list) {  // adaptive round: the still-active pixels
+        const uint32_t p = R.pix_list[pix_i];
+        x = p % (uint32_t)R.cam.width;
+        y = p / (uint32_t)R.cam.width;
+    } else if (R.tiled) {  // 8x8 pixel tiles, tile-major: neighbouring lanes -> neighbouring pixels
         uint32_t tile = pix_i >> 6, within = pix_i & 63u;
         uint32_t tx = tile % R.tiles_x, ty = tile / R.tiles_x;
         x = tx * 8 + (within & 7u);
@@ -1248,6 +1252,162 @@ __global__ __launch_bounds__(256) void k_resolve(const double* __restrict__ film
         const double s = linear_to_srgb((double)(float)m[k]);
         rgb[3ull * i + k] = (uint8_t)(255.999 * dmax_(0.0, dmin_(1.0, s)));
     }
+}
+
+// ------------------------------------------------------------------ adaptive sampling
+// TileIntegrator::Render (Integrators.cpp:55-86): each pixel takes rounds of
+// samplesPerPixel samples; after a round its three luminance-weighted
+// VarianceEstimators (Util.hpp:8-43) stop it when every RelativeVariance is
+// <= 1.5, else it goes on while it has fewer than 128 * spp samples.  Round r
+// of a pixel draws stream samples r*spp .. r*spp + spp - 1 (the reference's
+// samplers restart the sample index each round with fresh random state).
+// The device runs one round for all still-active pixels at once: the active
+// list is the wavefront's pixel set (RenderParams::pix_list), sample g of a
+// round chunk is (pix_list[g % n], s_lo + g / n) as in the fixed-SPP chunks.
+
+// The frame's work pixels (tile-major 8x8 order when the frame tiles, as the
+// fixed-SPP path) restricted to this shard's 32x32 tiles (Integrators.cpp:33):
+// a pixel's rounds stay on one rank.  Zeroes their estimators and counts.
+__global__ __launch_bounds__(256) void k_adapt_init(RenderParams R, uint32_t shard_index, uint32_t shard_count,
+                                                   uint32_t* __restrict__ list, uint32_t* __restrict__ cnt,
+                                                   AdaptEst* __restrict__ est, uint32_t* __restrict__ counts) {
+    if (blockIdx.x * 256 >= R.npix_work) return;
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    bool take = false;
+    uint32_t p = 0;
+    if (i < R.npix_work) {
+        uint32_t x, y;
+        work_pixel(R, i, x, y);
+        p = y * (uint32_t)R.cam.width + x;
+        const uint32_t tiles_x32 = ((uint32_t)R.cam.width + 31u) / 32u;
+        take = ((y >> 5) * tiles_x32 + (x >> 5)) % shard_count == shard_index;
+        if (take) {
+            est[p] = AdaptEst{{0, 0, 0}, {0, 0, 0}};
+            counts[p] = 0;
+        }
+    }
+    const int qoff[1] = {0};
+    const bool pred[1] = {take};
+    uint32_t at[1];
+    block_append<1, 256>(cnt, qoff, pred, at);
+    if (take) list[at[0]] = p;
+}
+
+// pixel -> its entry in this round's active list (-1 elsewhere)
+__global__ __launch_bounds__(256) void k_adapt_map(const uint32_t* __restrict__ list, const uint32_t* __restrict__ n,
+                                                  int32_t* __restrict__ map) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < *n) map[list[i]] = (int32_t)i;
+}
+
+// VarianceEstimator::Add of the chunk's samples, per pixel in sample order, on
+// color * dvec3(0.2126f, 0.7152f, 0.0722f).  GCC's contraction of the
+// reference build (TileIntegrator::Render disassembly): the luminance product
+// is fused into both differences and S's update,
+//   delta = fma(c, w, -mean); mean = delta / n + mean;
+//   delta2 = fma(c, w, -mean); S = fma(delta, delta2, S).
+__global__ __launch_bounds__(256) void k_adapt_accum(RenderParams R, const float* __restrict__ sample_L,
+                                                    AdaptEst* __restrict__ est, uint32_t* __restrict__ counts) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= R.npix_work) return;
+    const uint32_t p = R.pix_list[i];
+    const double wl[3] = {(double)0.2126f, (double)0.7152f, (double)0.0722f};
+    AdaptEst e = est[p];
+    uint32_t n = counts[p];
+    const uint32_t ns = R.s_hi - R.s_lo;
+    for (uint32_t k = 0; k < ns; k++) {
+        const float* L = sample_L + 3ull * ((uint64_t)k * R.npix_work + i);
+        const double dn = (double)(++n);
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const double v = (double)L[c];
+            const double delta = fma(v, wl[c], -e.mean[c]);
+            e.mean[c] = delta / dn + e.mean[c];
+            const double delta2 = fma(v, wl[c], -e.mean[c]);
+            e.S[c] = fma(delta, delta2, e.S[c]);
+        }
+    }
+    est[p] = e;
+    counts[p] = n;
+}
+
+// FilmTile::Add of a round chunk's samples: every pixel of the frame gathers
+// the samples of its active neighbours (k_gather with the source pixel's
+// entry looked up in `map`), in a fixed order -- deterministic, no atomics.
+__global__ __launch_bounds__(256) void k_adapt_gather(RenderParams R, const int32_t* __restrict__ map,
+                                                     const float* __restrict__ sample_L, double* __restrict__ film) {
+    const uint32_t tid = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t W = (uint32_t)R.cam.width, H = (uint32_t)R.cam.height;
+    if (tid >= W * H) return;
+    const int x = (int)(tid % W), y = (int)(tid / W);
+    double acc[4] = {0, 0, 0, 0};
+    bool any = false;
+    const uint32_t ns = R.s_hi - R.s_lo;
+    for (int oy = -R.rad_y; oy <= R.rad_y; oy++) {
+        for (int ox = -R.rad_x; ox <= R.rad_x; ox++) {
+            const int sx = x - ox, sy = y - oy;
+            if (sx < 0 || sy < 0 || sx >= (int)W || sy >= (int)H) continue;
+            const uint32_t spix = (uint32_t)sy * W + (uint32_t)sx;
+            const int32_t j = map[spix];
+            if (j < 0) continue;
+            any = true;
+            for (uint32_t k = 0; k < ns; k++) {
+                const uint32_t key = stream_key(R.seed, spix, R.s_lo + k);
+                const double fx = (double)draw(key, 0), fy = (double)draw(key, 1);
+                const double spx = (double)ox + 0.5 - fx, spy = (double)oy + 0.5 - fy;
+                const double w = filter_eval(R, (float)spx, (float)spy) * R.inv_integral;
+                if (w <= 0) continue;
+                const float* L = sample_L + 3ull * ((uint64_t)k * R.npix_work + (uint32_t)j);
+                acc[0] += (double)L[0] * w;
+                acc[1] += (double)L[1] * w;
+                acc[2] += (double)L[2] * w;
+                acc[3] += w;
+            }
+        }
+    }
+    if (!any) return;
+    double* o = film + 4ull * tid;
+    o[0] += acc[0];
+    o[1] += acc[1];
+    o[2] += acc[2];
+    o[3] += acc[3];
+}
+
+// VarianceEstimator::RelativeVariance (Util.hpp:36-38)
+__device__ __forceinline__ double rel_variance(double mean, double S, uint32_t n) {
+    if (mean == 0) return 0;
+    const double var = n > 1 ? S / (double)(n - 1) : 0.0;
+    return 1.96 * sqrt(var / (double)n) / mean;
+}
+
+// End of a round: a pixel goes on unless all three relative variances are
+// <= 1.5, and only while it has fewer than 128 * spp samples (the loop test).
+// Clears its map entry; survivors are appended to the next round's list.
+__global__ __launch_bounds__(256) void k_adapt_decide(const uint32_t* __restrict__ list, const uint32_t* __restrict__ n,
+                                                     const AdaptEst* __restrict__ est,
+                                                     const uint32_t* __restrict__ counts, uint32_t max_samples,
+                                                     int32_t* __restrict__ map, uint32_t* __restrict__ out_list,
+                                                     uint32_t* __restrict__ out_cnt) {
+    const uint32_t nn = *n;
+    if (blockIdx.x * 256 >= nn) return;
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    bool go = false;
+    uint32_t p = 0;
+    if (i < nn) {
+        p = list[i];
+        map[p] = -1;
+        const AdaptEst e = est[p];
+        const uint32_t c = counts[p];
+        bool done = true;
+#pragma unroll
+        for (int k = 0; k < 3; k++) done = done && rel_variance(e.mean[k], e.S[k], c) <= PT_ADAPT_REL_VAR;
+        go = !done && c < max_samples;
+    }
+    const int qoff[1] = {0};
+    const bool pred[1] = {go};
+    uint32_t at[1];
+    block_append<1, 256>(out_cnt, qoff, pred, at);
+    if (go) out_list[at[0]] = p;
 }
 
 // explicit instantiations used by the runtime

@@ -59,6 +59,14 @@ struct pt_ctx {
     uint64_t sample_cap = 0;  // floats
     double* film = nullptr;
     uint64_t film_cap = 0;  // doubles
+    // adaptive sampling: per-pixel estimators / sample counts / active-list
+    // entry, the two active lists and their counters
+    AdaptEst* a_est = nullptr;
+    uint32_t* a_counts = nullptr;
+    int32_t* a_map = nullptr;
+    uint32_t* a_list = nullptr;
+    uint32_t* a_cnt = nullptr;
+    uint64_t a_est_cap = 0, a_counts_cap = 0, a_map_cap = 0, a_list_cap = 0, a_cnt_cap = 0;
     hipEvent_t ev[8] = {};
     hipEvent_t rev[PT_RING][5] = {};  // per in-flight iteration: kernel boundaries [0..2], end [4] ([3] unused)
 };
@@ -188,6 +196,8 @@ extern "C" void pt_destroy(pt_ctx* c) {
     if (c->scratch) hipFree(c->scratch);
     if (c->sample_L) hipFree(c->sample_L);
     if (c->film) hipFree(c->film);
+    for (void* p : {(void*)c->a_est, (void*)c->a_counts, (void*)c->a_map, (void*)c->a_list, (void*)c->a_cnt})
+        if (p) hipFree(p);
     if (c->host_cnt) hipHostFree(c->host_cnt);
     for (auto& e : c->ev)
         if (e) hipEventDestroy(e);
@@ -728,9 +738,11 @@ static ShadowFn pick_shadow(bool pool, bool qn, bool inst, bool count) {
                 : (count ? shadow_fn<true, false>(pool, qn) : shadow_fn<false, false>(pool, qn));
 }
 
-template <class OnChunk>
-static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_dev,
-                     pt_stats* stats, OnChunk on_chunk) {
+// `drive(R, spp_local, s_chunk, trace)` decides which sample chunks are traced:
+// trace(R) runs the wavefront over R's work pixels x samples [s_lo, s_hi) and
+// leaves their radiance in c->sample_L (sample-major, R.npix_work per index).
+template <class Drive>
+static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, pt_stats* stats, Drive drive) {
     if (pt_status bs = bind_scene(c)) return bs;
     const uint32_t W = (uint32_t)cam->width, H = (uint32_t)cam->height;
     RenderParams R{};
@@ -740,6 +752,10 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     R.shard_count = rd->shard_count ? rd->shard_count : 1;
     R.shard_index = rd->shard_index;
     if (R.shard_index >= R.shard_count) return fail(c, PT_ERR_ARG, "shard_index >= shard_count");
+    if (rd->flags & PT_RENDER_ADAPTIVE) {  // adaptive: shards own whole pixels (32x32 tiles), not samples
+        R.shard_index = 0;
+        R.shard_count = 1;
+    }
     if (rd->max_depth > PF_DEPTH_MASK - 1) return fail(c, PT_ERR_ARG, "max_depth too large");
     const bool ranged = !(rd->pixel_begin == 0 && rd->pixel_end == 0);
     if (ranged) {
@@ -806,15 +822,13 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     unsigned long long* next_sample = c->counters + CNT_SHARDS * CNT_COUNT + CNT_NEXT_SAMPLE;
     float t_cl = 0, t_sh = 0, t_an = 0;
 
-    for (uint32_t s_lo = 0; s_lo < spp_local; s_lo += s_chunk) {
-        R.s_lo = s_lo;
-        R.s_hi = std::min(spp_local, s_lo + s_chunk);
+    auto trace = [&](RenderParams& R) -> pt_status {
+        pt_status st;
         R.chunk_total = (unsigned long long)R.npix_work * (R.s_hi - R.s_lo);
         if (R.max_depth == 0) {  // the Li loop never runs: every sample is black
             HIPCHK(c, hipMemsetAsync(c->sample_L, 0, 12ull * R.chunk_total, sm));
             if (stats) stats->paths += R.chunk_total;
-            if ((st = on_chunk(R)) != PT_OK) return st;
-            continue;
+            return PT_OK;
         }
         HIPCHK(c, hipMemsetAsync(next_sample, 0, 8, sm));
         // Counter sets rotate (pt_kernels.h SET_WORDS): iteration i reads its
@@ -926,8 +940,9 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         }
 #endif
         if (stats) stats->paths += R.chunk_total;
-        if ((st = on_chunk(R)) != PT_OK) return st;
-    }
+        return PT_OK;
+    };
+    if ((st = drive(R, spp_local, s_chunk, trace)) != PT_OK) return st;
     HIPCHK(c, hipStreamSynchronize(sm));
     if (stats) {
         unsigned long long hs[CNT_SHARDS * CNT_COUNT], h[CNT_COUNT] = {};
@@ -943,8 +958,21 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         stats->ms_shade += t_sh;
         stats->ms_any += t_an;
     }
-    (void)film_dev;
     return PT_OK;
+}
+
+// The fixed-SPP driver: consecutive sample chunks, each handed to on_chunk.
+template <class OnChunk>
+static auto fixed_chunks(OnChunk on_chunk) {
+    return [on_chunk](RenderParams& R, uint32_t spp_local, uint32_t s_chunk, auto& trace) -> pt_status {
+        for (uint32_t s_lo = 0; s_lo < spp_local; s_lo += s_chunk) {
+            R.s_lo = s_lo;
+            R.s_hi = std::min(spp_local, s_lo + s_chunk);
+            if (pt_status st = trace(R)) return st;
+            if (pt_status st = on_chunk(R)) return st;
+        }
+        return PT_OK;
+    };
 }
 
 static pt_status check_render_args(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd) {
@@ -959,39 +987,22 @@ static pt_status check_render_args(pt_ctx* c, const pt_camera_desc* cam, const p
     return PT_OK;
 }
 
-extern "C" pt_status pt_render(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_accum,
-                               pt_stats* stats) {
-    pt_status st = check_render_args(c, cam, rd);
-    if (st) return st;
-    if (!film_accum) return fail(c, PT_ERR_ARG, "film_accum is null");
-    if (!(rd->pixel_begin == 0 && rd->pixel_end == 0)) return fail(c, PT_ERR_ARG, "pt_render renders whole films");
-    HIPCHK(c, hipSetDevice(c->device));
+// Film accumulation on the device: `film_accum` itself when it is device
+// memory, else a zeroed scratch film whose sum is added to the host array.
+template <class Body>
+static pt_status with_film(pt_ctx* c, const pt_camera_desc* cam, double* film_accum, pt_stats* S, Body body) {
     auto t0 = std::chrono::steady_clock::now();
     const uint64_t nfilm = 4ull * cam->width * cam->height;
     const bool dev = is_device_ptr(film_accum);
     double* film = film_accum;
+    pt_status st;
     if (!dev) {
         if ((st = ensure(c, &c->film, c->film_cap, nfilm)) != PT_OK) return st;
         film = c->film;
         HIPCHK(c, hipMemsetAsync(film, 0, nfilm * 8, c->stream));
     }
-    pt_stats local{};
-    pt_stats* S = stats ? stats : &local;
     *S = pt_stats{};
-    st = run(c, cam, rd, film, S, [&](const RenderParams& R) -> pt_status {
-        const uint32_t npx = (uint32_t)cam->width * cam->height;
-        const int rad = std::max(R.rad_x, R.rad_y);
-        const dim3 tiles((cam->width + 15) / 16, (cam->height + 15) / 16);
-        if (R.npix_work == npx && rad <= 1 && !getenv("PT_GATHER_PIXEL"))
-            hipLaunchKernelGGL(k_gather_tile<1>, tiles, dim3(256), 0, c->stream, R, c->sample_L, film);
-        else if (R.npix_work == npx && rad == 2 && !getenv("PT_GATHER_PIXEL"))
-            hipLaunchKernelGGL(k_gather_tile<2>, tiles, dim3(256), 0, c->stream, R, c->sample_L, film);
-        else
-            hipLaunchKernelGGL(k_gather, dim3((npx + 255) / 256), dim3(256), 0, c->stream, R, c->sample_L, film);
-        HIPCHK(c, hipGetLastError());
-        return PT_OK;
-    });
-    if (st) return st;
+    if ((st = body(film)) != PT_OK) return st;
     if (!dev) {
         std::vector<double> h(nfilm);
         HIPCHK(c, hipMemcpyAsync(h.data(), film, nfilm * 8, hipMemcpyDeviceToHost, c->stream));
@@ -1001,6 +1012,108 @@ extern "C" pt_status pt_render(pt_ctx* c, const pt_camera_desc* cam, const pt_re
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
     S->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return PT_OK;
+}
+
+extern "C" pt_status pt_render(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_accum,
+                               pt_stats* stats) {
+    pt_status st = check_render_args(c, cam, rd);
+    if (st) return st;
+    if (rd->flags & PT_RENDER_ADAPTIVE) return pt_render_adaptive(c, cam, rd, film_accum, nullptr, stats);
+    if (!film_accum) return fail(c, PT_ERR_ARG, "film_accum is null");
+    if (!(rd->pixel_begin == 0 && rd->pixel_end == 0)) return fail(c, PT_ERR_ARG, "pt_render renders whole films");
+    HIPCHK(c, hipSetDevice(c->device));
+    pt_stats local{};
+    pt_stats* S = stats ? stats : &local;
+    return with_film(c, cam, film_accum, S, [&](double* film) {
+        return run(c, cam, rd, S, fixed_chunks([&](const RenderParams& R) -> pt_status {
+            const uint32_t npx = (uint32_t)cam->width * cam->height;
+            const int rad = std::max(R.rad_x, R.rad_y);
+            const dim3 tiles((cam->width + 15) / 16, (cam->height + 15) / 16);
+            if (R.npix_work == npx && rad <= 1 && !getenv("PT_GATHER_PIXEL"))
+                hipLaunchKernelGGL(k_gather_tile<1>, tiles, dim3(256), 0, c->stream, R, c->sample_L, film);
+            else if (R.npix_work == npx && rad == 2 && !getenv("PT_GATHER_PIXEL"))
+                hipLaunchKernelGGL(k_gather_tile<2>, tiles, dim3(256), 0, c->stream, R, c->sample_L, film);
+            else
+                hipLaunchKernelGGL(k_gather, dim3((npx + 255) / 256), dim3(256), 0, c->stream, R, c->sample_L, film);
+            HIPCHK(c, hipGetLastError());
+            return PT_OK;
+        }));
+    });
+}
+
+// TileIntegrator::Render's adaptive loop (Integrators.cpp:55-86), round by
+// round over the still-active pixels (pt_kernels.hip "adaptive sampling").
+// The host reads one count per round (the next round's active pixels).
+extern "C" pt_status pt_render_adaptive(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd,
+                                        double* film_accum, uint32_t* sample_counts, pt_stats* stats) {
+    pt_status st = check_render_args(c, cam, rd);
+    if (st) return st;
+    if (!film_accum) return fail(c, PT_ERR_ARG, "film_accum is null");
+    if (rd->spp == 0) return fail(c, PT_ERR_ARG, "adaptive sampling needs spp >= 1");
+    if (rd->spp > (1u << 24) / PT_ADAPT_MAX_ROUNDS) return fail(c, PT_ERR_ARG, "spp too large for 128 rounds");
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint32_t npx = (uint32_t)cam->width * cam->height;
+    if ((st = ensure(c, &c->a_est, c->a_est_cap, npx)) != PT_OK) return st;
+    if ((st = ensure(c, &c->a_counts, c->a_counts_cap, npx)) != PT_OK) return st;
+    if ((st = ensure(c, &c->a_map, c->a_map_cap, npx)) != PT_OK) return st;
+    if ((st = ensure(c, &c->a_list, c->a_list_cap, 2ull * npx)) != PT_OK) return st;
+    if ((st = ensure(c, &c->a_cnt, c->a_cnt_cap, 2 * Q_STRIDE)) != PT_OK) return st;
+    const uint32_t shard_count = rd->shard_count ? rd->shard_count : 1, shard_index = rd->shard_index;
+    pt_render_desc r2 = *rd;
+    r2.flags |= PT_RENDER_ADAPTIVE;
+    pt_stats local{};
+    pt_stats* S = stats ? stats : &local;
+    hipStream_t sm = c->stream;
+    st = with_film(c, cam, film_accum, S, [&](double* film) {
+        HIPCHK(c, hipMemsetAsync(c->a_map, 0xFF, 4ull * npx, sm));
+        HIPCHK(c, hipMemsetAsync(c->a_counts, 0, 4ull * npx, sm));
+        return run(c, cam, &r2, S, [&](RenderParams& R, uint32_t spp, uint32_t s_chunk, auto& trace) -> pt_status {
+            uint32_t* list[2] = {c->a_list, c->a_list + npx};
+            uint32_t* cnt[2] = {c->a_cnt, c->a_cnt + Q_STRIDE};
+            HIPCHK(c, hipMemsetAsync(c->a_cnt, 0, 8ull * Q_STRIDE, sm));
+            const uint32_t nwork = R.npix_work;
+            hipLaunchKernelGGL(k_adapt_init, dim3((nwork + 255) / 256), dim3(256), 0, sm, R, shard_index, shard_count,
+                               list[0], cnt[0], c->a_est, c->a_counts);
+            HIPCHK(c, hipGetLastError());
+            uint32_t n = 0;
+            HIPCHK(c, hipMemcpyAsync(&n, cnt[0], 4, hipMemcpyDeviceToHost, sm));
+            HIPCHK(c, hipStreamSynchronize(sm));
+            R.tiled = 0;
+            for (uint32_t round = 0; n > 0 && round < PT_ADAPT_MAX_ROUNDS; round++) {
+                const uint32_t a = round & 1u;
+                hipLaunchKernelGGL(k_adapt_map, dim3((n + 255) / 256), dim3(256), 0, sm, (const uint32_t*)list[a],
+                                   (const uint32_t*)cnt[a], c->a_map);
+                R.pix_list = list[a];
+                R.npix_work = n;
+                for (uint32_t s0 = 0; s0 < spp; s0 += s_chunk) {
+                    R.s_lo = round * spp + s0;
+                    R.s_hi = R.s_lo + std::min(s_chunk, spp - s0);
+                    if (pt_status e = trace(R)) return e;
+                    hipLaunchKernelGGL(k_adapt_accum, dim3((n + 255) / 256), dim3(256), 0, sm, R, (const float*)c->sample_L,
+                                       c->a_est, c->a_counts);
+                    hipLaunchKernelGGL(k_adapt_gather, dim3((npx + 255) / 256), dim3(256), 0, sm, R,
+                                       (const int32_t*)c->a_map, (const float*)c->sample_L, film);
+                    HIPCHK(c, hipGetLastError());
+                }
+                HIPCHK(c, hipMemsetAsync(cnt[a ^ 1u], 0, 4, sm));
+                hipLaunchKernelGGL(k_adapt_decide, dim3((n + 255) / 256), dim3(256), 0, sm, (const uint32_t*)list[a],
+                                   (const uint32_t*)cnt[a], (const AdaptEst*)c->a_est, (const uint32_t*)c->a_counts,
+                                   PT_ADAPT_MAX_ROUNDS * spp, c->a_map, list[a ^ 1u], cnt[a ^ 1u]);
+                HIPCHK(c, hipGetLastError());
+                HIPCHK(c, hipMemcpyAsync(&n, cnt[a ^ 1u], 4, hipMemcpyDeviceToHost, sm));
+                HIPCHK(c, hipStreamSynchronize(sm));
+            }
+            R.pix_list = nullptr;
+            return PT_OK;
+        });
+    });
+    if (st) return st;
+    if (sample_counts) {
+        const hipMemcpyKind k = is_device_ptr(sample_counts) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        HIPCHK(c, hipMemcpyAsync(sample_counts, c->a_counts, 4ull * npx, k, sm));
+        HIPCHK(c, hipStreamSynchronize(sm));
+    }
     return PT_OK;
 }
 
@@ -1022,7 +1135,8 @@ extern "C" pt_status pt_render_samples(pt_ctx* c, const pt_camera_desc* cam, con
     pt_stats* S = stats ? stats : &local;
     *S = pt_stats{};
     std::vector<float> h;
-    st = run(c, cam, &r2, nullptr, S, [&](const RenderParams& R) -> pt_status {
+    r2.flags &= ~PT_RENDER_ADAPTIVE;
+    return run(c, cam, &r2, S, fixed_chunks([&](const RenderParams& R) -> pt_status {
         const uint64_t n = 3ull * R.chunk_total;
         h.resize(n);
         HIPCHK(c, hipMemcpyAsync(h.data(), c->sample_L, n * 4, hipMemcpyDeviceToHost, c->stream));
@@ -1037,8 +1151,7 @@ extern "C" pt_status pt_render_samples(pt_ctx* c, const pt_camera_desc* cam, con
                 dst[2] = src[2];
             }
         return PT_OK;
-    });
-    return st;
+    }));
 }
 
 extern "C" pt_status pt_film_resolve(pt_ctx* c, const double* film, int32_t width, int32_t height, uint32_t tonemap,

@@ -82,6 +82,14 @@ class Context:
         N.check(self._lib.pt_render(self.ptr, C.byref(cam), C.byref(rd), C.c_void_p(film_ptr), C.byref(st)), self.ptr)
         return st.as_dict()
 
+    def render_adaptive(self, cam: N.CameraDesc, rd: N.RenderDesc, film_ptr: int) -> tuple[dict, np.ndarray]:
+        """pt_render_adaptive: (stats, per-pixel sample counts (H, W) u32)."""
+        st = N.Stats()
+        counts = np.zeros((cam.height, cam.width), np.uint32)
+        N.check(self._lib.pt_render_adaptive(self.ptr, C.byref(cam), C.byref(rd), C.c_void_p(film_ptr),
+                                             counts.ctypes.data, C.byref(st)), self.ptr)
+        return st.as_dict(), counts
+
     def render_samples(self, cam: N.CameraDesc, rd: N.RenderDesc, npix: int) -> tuple[np.ndarray, dict]:
         out = np.zeros((npix, rd.spp, 3), dtype=np.float32)
         st = N.Stats()
@@ -187,15 +195,25 @@ class Integrator:
         return camera_desc(self.camera, self.flat), rd
 
     def Render(self, device: int = 0, shard_index: int = 0, shard_count: int = 1, flags: int = 0,
-               film_ptr: int | None = None, paths_in_flight: int = 0) -> dict:
+               film_ptr: int | None = None, paths_in_flight: int = 0, adaptive: bool = False) -> dict:
         """TileIntegrator::Render equivalent: accumulates into camera.GetFilm().accum
-        (or into the float64 device buffer at film_ptr)."""
+        (or into the float64 device buffer at film_ptr).
+
+        adaptive=False renders exactly spp samples per pixel (the benchmark's
+        fixed-SPP frame); adaptive=True runs the reference's own loop
+        (Integrators.cpp:55-86): rounds of spp samples per pixel until the
+        luminance-weighted relative variance of every channel is <= 1.5, at
+        most 128*spp samples; the per-pixel sample counts land in
+        `last_sample_counts` (H, W).  Shards then own 32x32 tiles, not samples."""
         ctx = self.context(device)
         cam, rd = self.desc(shard_index=shard_index, shard_count=shard_count, flags=flags,
                             paths_in_flight=paths_in_flight)
         film = self.camera.GetFilm()
         ptr = film_ptr if film_ptr is not None else film.accum.ctypes.data
-        self.last_stats = ctx.render(cam, rd, ptr)
+        if adaptive:
+            self.last_stats, self.last_sample_counts = ctx.render_adaptive(cam, rd, ptr)
+        else:
+            self.last_stats = ctx.render(cam, rd, ptr)
         return self.last_stats
 
     def RenderSamples(self, pixel_begin: int = 0, pixel_end: int = 0, spp: Optional[int] = None,

@@ -30,6 +30,7 @@ PT_RENDER_TRAVERSAL_POOL = 0x4
 PT_RENDER_TRAVERSAL_SIMPLE = 0x8
 PT_RENDER_NODES_FULL = 0x10
 PT_RENDER_NODES_QUANTIZED = 0x20
+PT_RENDER_ADAPTIVE = 0x40
 PT_NODES_AUTO, PT_NODES_FULL, PT_NODES_QUANTIZED = 0, 1, 2
 
 # ---- numpy mirrors of the array element structs (layouts asserted below) ----
@@ -127,7 +128,7 @@ class BvhBuildStats(C.Structure):
 EXPORTS = [
     "pt_version", "pt_create", "pt_destroy", "pt_last_error", "pt_set_stream", "pt_scene_upload", "pt_render",
     "pt_trace", "pt_scene_device_bytes", "pt_bvh4_build", "pt_bvh4_order_table", "pt_film_resolve",
-    "pt_mat4_inverse", "pt_bvh4_build_device", "pt_set_node_format",
+    "pt_mat4_inverse", "pt_bvh4_build_device", "pt_set_node_format", "pt_render_adaptive", "pt_render_samples",
 ]
 
 _lib = None
@@ -161,6 +162,8 @@ def lib():
     L.pt_scene_upload.restype = C.c_int32
     L.pt_render.argtypes = [vp, C.POINTER(CameraDesc), C.POINTER(RenderDesc), vp, C.POINTER(Stats)]
     L.pt_render.restype = C.c_int32
+    L.pt_render_adaptive.argtypes = [vp, C.POINTER(CameraDesc), C.POINTER(RenderDesc), vp, vp, C.POINTER(Stats)]
+    L.pt_render_adaptive.restype = C.c_int32
     L.pt_trace.argtypes = [vp, vp, C.c_uint32, C.c_int, vp, C.POINTER(Stats)]
     L.pt_trace.restype = C.c_int32
     L.pt_mat4_inverse.argtypes = [vp, vp]

@@ -61,8 +61,10 @@ class SceneSetup:
 
 # --------------------------------------------------------------------------
 def example_1(W: int = 256, H: int = 256, spp: int = 16, integrator: str = "path", max_depth: int = 8,
-              seed: int = 0x5EED0001, medium: bool = True) -> SceneSetup:
-    """C1: examples/example_1.cpp:17-104 (UniformLightSampler, Mitchell 1.5)."""
+              seed: int = 0x5EED0001, medium: bool = True, filt=None, lens=None) -> SceneSetup:
+    """C1: examples/example_1.cpp:17-104 (UniformLightSampler, Mitchell 1.5).
+    `filt` replaces the film's filter, `lens` = (FocusAngle, FocusDistance)
+    turns on the thin lens (Camera.hpp:27-33)."""
     scene = Scene()
     white = SolidColor((0.9, 0.9, 0.9))
     green = SolidColor((0.2, 0.3, 0.1))
@@ -81,8 +83,8 @@ def example_1(W: int = 256, H: int = 256, spp: int = 16, integrator: str = "path
         med = HomogeneusMedium((0.01, 0.9, 0.9), (1.0, 0.1, 0.1), 0.8, 5.0)
         scene.Add(GeometricPrimitive(medium_sphere, None, None, med))
     scene.infiniteLights.append(UniformInfiniteLight((0.45, 0.65, 1)))
-    film = Film((W, H), MitchellFilter())
-    camera = Camera((0.3, 0.4, 1), (0, 0, 0), 1.7, film)
+    film = Film((W, H), filt or MitchellFilter())
+    camera = Camera((0.3, 0.4, 1), (0, 0, 0), 1.7, film, *(lens or (0.0, 0.0)))
     return SceneSetup(scene, camera, integrator, UniformLightSampler(), max_depth, seed, spp).finish()
 
 
@@ -132,7 +134,7 @@ def _box(center, size, angle):
 
 
 def cornell(W: int = 1024, H: int = 1024, spp: int = 256, config: str = "c2", max_depth: int = 8,
-            seed: Optional[int] = None, fog: bool = False) -> SceneSetup:
+            seed: Optional[int] = None, fog: bool = False, filt=None, lens=None) -> SceneSetup:
     """C2/C3 Cornell box: 5 walls + 2 boxes as one triangle Model (34 tris) and
     a quad area light under the ceiling.  C2: MicrofacetDiffuse(albedo)
     (roughness 1, metallic 0), SimplePathIntegrator.  C3: + rough glass sphere
@@ -185,8 +187,8 @@ def cornell(W: int = 1024, H: int = 1024, spp: int = 256, config: str = "c2", ma
         dense = HomogeneusMedium((0.9, 0.3, 0.1), (2.0, 3.0, 4.0), 0.0, 1.0)
         scene.Add(GeometricPrimitive(SphereShape((-0.55, 0.45, 0.45), 0.22), None, None, dense))
         extra.append(PointLight((0.5, 0.6, 0.6), (0.8, 0.8, 1.2)))
-    film = Film((W, H), MitchellFilter())
-    camera = Camera((0, 0, 3.7), (0, 0, 0), 0.75, film, medium=fog_md)
+    film = Film((W, H), filt or MitchellFilter())
+    camera = Camera((0, 0, 3.7), (0, 0, 0), 0.75, film, *(lens or (0.0, 0.0)), medium=fog_md)
     kind = "volpath" if fog else ("path" if c3 else "simple")
     ls = PowerLightSampler() if fog else (UniformLightSampler() if c3 else None)
     return SceneSetup(scene, camera, kind, ls, max_depth, seed, spp, extra).finish()

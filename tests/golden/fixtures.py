@@ -15,7 +15,7 @@ from pathlib import Path
 import numpy as np
 
 from pathtracing_amd import scenes
-from pathtracing_amd.scene import FunctionInfiniteLight
+from pathtracing_amd.scene import BoxFilter, FunctionInfiniteLight, GaussianFilter, MitchellFilter
 
 GOLDEN = Path(__file__).resolve().parent
 
@@ -39,6 +39,14 @@ def parity_scenes():
         # C4 recipe at 0.3 % detail: every C4 feature (foliage masks, 58 textures,
         # ~2700 lights under the PowerLightSampler, sky + sun, depth 128)
         "sanmiguel": lambda: scenes.sanmiguel(W=32, H=18, spp=4, detail=0.003, tex_size=32),
+        # thin-lens camera (Camera.hpp:27-33) with the other two filters
+        # (Filter.hpp:47-75) and Mitchell at radius 2 (the two-pixel gather)
+        "lens_box": lambda: scenes.cornell(W=32, H=32, spp=4, config="c3", seed=0x5EED0031,
+                                           filt=BoxFilter((0.5, 0.5)), lens=(0.12, 3.2)),
+        "lens_gauss": lambda: scenes.example_1(W=32, H=24, spp=4, seed=0x5EED0032,
+                                               filt=GaussianFilter((1.5, 1.5), 0.5), lens=(0.3, 1.2)),
+        "mitchell2": lambda: scenes.cornell(W=32, H=32, spp=4, config="c3", seed=0x5EED0033,
+                                            filt=MitchellFilter((2.0, 2.0))),
     }
 
 

@@ -12,6 +12,8 @@ reference computes on it:
   film       FilmTile splat of those samples + filter table (F6/F8)
   bsdf_*     Material scatter / calc_attenuation / PDF       (F3)
   lsample_*  Light::sample / PDF / L                         (F4)
+  adaptive.npz  TileIntegrator::Render's own adaptive loop (Integrators.cpp:
+             55-86) on the PCG stream: per-pixel sample counts + film
 
     python tests/golden/gen_golden.py
 """
@@ -200,6 +202,30 @@ def gen_resolve(rng, tmp: Path):
     print(f"film_resolve: {(OUT / 'film_resolve.npz').stat().st_size / 1024:.0f} KiB")
 
 
+ADAPTIVE_SCENES = ("cornell_c3", "example1", "example1_simple", "zoo", "fog", "lens_box", "instances", "mitchell2")
+
+
+def gen_adaptive(tmp: Path):
+    """The reference's TileIntegrator::Render, adaptive rounds included, run
+    by ref_harness `adaptive` (one thread, DetSampler numbering round r's
+    samples r*spp + index) on the parity scenes without a randomly
+    pre-processed sky (their Power() would differ between harness runs)."""
+    from fixtures import load
+    res = {}
+    for name in ADAPTIVE_SCENES:
+        setup, _, _ = load(name)
+        d = tmp / f"adaptive_{name}"
+        recipe = write_recipe(d, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
+                              setup.max_depth, setup.light_sampler, setup.extra_lights)
+        out = d / "o"
+        subprocess.run([str(HARNESS), str(recipe), "adaptive", str(out)], check=True, stdout=subprocess.DEVNULL)
+        W, H = setup.camera.film.Resolution()
+        res[f"{name}_counts"] = np.fromfile(f"{out}.adaptive_counts.bin", np.uint32).reshape(H, W)
+        res[f"{name}_film"] = np.fromfile(f"{out}.adaptive_film.bin", np.float64).reshape(H, W, 4)
+    np.savez_compressed(OUT / "adaptive.npz", **res)
+    print(f"adaptive: {(OUT / 'adaptive.npz').stat().st_size / 1024:.0f} KiB, {len(ADAPTIVE_SCENES)} scenes")
+
+
 def main(names=None):
     """All scenes share one rng stream (the committed round-1 fixtures); a
     scene regenerated alone (`gen_golden.py NAME...`) uses its own stream
@@ -216,6 +242,8 @@ def main(names=None):
             gen(name, make(), r, Path(t))
         if not names or "film_resolve" in names:
             gen_resolve(np.random.default_rng([20261016, 7]), Path(t))
+        if not names or "adaptive" in names:
+            gen_adaptive(Path(t))
 
 
 if __name__ == "__main__":
