@@ -645,6 +645,7 @@ public:
     std::vector<pt_ctx*> ctx;
     RenderStats stats;
     std::vector<double> last;  // the merged accumulation of the last frame
+    std::vector<uint32_t> counts;  // samples per pixel of the last frame
 
     ~HipBackend() {
         for (pt_ctx* c : ctx) pt_destroy(c);
@@ -668,8 +669,10 @@ public:
         }
     }
 
-    // Renders shards 0..n-1 (one host thread per GPU) and merges into film.
-    void render(const Camera& cam, uint32_t integrator, uint32_t spp, uint32_t depth, uint32_t seed, unsigned n) {
+    // Renders shards 0..n-1 (one host thread per GPU) and merges into film:
+    // interleaved sample shards at fixed SPP, 32x32-tile shards when adaptive.
+    void render(const Camera& cam, uint32_t integrator, uint32_t spp, uint32_t depth, uint32_t seed, unsigned n,
+                bool adaptive) {
         const pt_camera_desc cd = camera_desc(cam, flat);
         const auto film = cam.GetFilm();
         const glm::ivec2 res = film->Resolution();
@@ -682,6 +685,7 @@ public:
         filter_desc(*film, rd);
         rd.shard_count = n;
         std::vector<std::vector<double>> acc(n, std::vector<double>(4 * npx, 0.0));
+        std::vector<std::vector<uint32_t>> cnt(n, std::vector<uint32_t>(npx, 0));
         std::vector<pt_stats> st(n);
         std::vector<std::string> err(n);
         auto t0 = std::chrono::steady_clock::now();
@@ -690,7 +694,9 @@ public:
             th.emplace_back([&, g] {
                 pt_render_desc r = rd;
                 r.shard_index = g;
-                if (pt_render(ctx[g], &cd, &r, acc[g].data(), &st[g]) != PT_OK) err[g] = pt_last_error(ctx[g]);
+                const pt_status e = adaptive ? pt_render_adaptive(ctx[g], &cd, &r, acc[g].data(), cnt[g].data(), &st[g])
+                                             : pt_render(ctx[g], &cd, &r, acc[g].data(), &st[g]);
+                if (e != PT_OK) err[g] = pt_last_error(ctx[g]);
             });
         }
         for (auto& t : th) t.join();
@@ -700,6 +706,10 @@ public:
         last.assign(4 * npx, 0.0);
         for (unsigned g = 0; g < n; g++)
             for (size_t i = 0; i < 4 * npx; i++) last[i] += acc[g][i];
+        counts.assign(npx, adaptive ? 0u : spp);
+        if (adaptive)
+            for (unsigned g = 0; g < n; g++)
+                for (size_t i = 0; i < npx; i++) counts[i] += cnt[g][i];
         FilmTile tile = film->GetFilmTile(Bounds2i{{0, 0}, res});
         for (int y = 0; y < res.y; y++)
             for (int x = 0; x < res.x; x++) {
@@ -745,7 +755,7 @@ void HipPathIntegrator::Render(unsigned int n) const {
     if (!be_) be_ = std::make_unique<HipBackend>();
     be_->ensure(*scene, ls_, n);
     be_->render(*camera, PT_INTEGRATOR_PATH, sampler->SamplesPerPixel(), depth_, seed_of(sampler),
-                (unsigned)be_->ctx.size());
+                (unsigned)be_->ctx.size(), adaptive_);
 }
 RenderStats HipPathIntegrator::LastStats() const { return be_ ? be_->stats : RenderStats{}; }
 static const std::vector<double> kEmpty;
@@ -762,7 +772,7 @@ void HipSimplePathIntegrator::Render(unsigned int n) const {
     if (!be_) be_ = std::make_unique<HipBackend>();
     be_->ensure(*scene, nullptr, n);
     be_->render(*camera, PT_INTEGRATOR_SIMPLE, sampler->SamplesPerPixel(), depth_, seed_of(sampler),
-                (unsigned)be_->ctx.size());
+                (unsigned)be_->ctx.size(), adaptive_);
 }
 RenderStats HipSimplePathIntegrator::LastStats() const { return be_ ? be_->stats : RenderStats{}; }
 
@@ -777,10 +787,14 @@ void HipVolPathIntegrator::Render(unsigned int n) const {
     if (!be_) be_ = std::make_unique<HipBackend>();
     be_->ensure(*scene, ls_, n, camera->GetMedium());
     be_->render(*camera, PT_INTEGRATOR_VOLPATH, sampler->SamplesPerPixel(), depth_, seed_of(sampler),
-                (unsigned)be_->ctx.size());
+                (unsigned)be_->ctx.size(), adaptive_);
 }
 RenderStats HipVolPathIntegrator::LastStats() const { return be_ ? be_->stats : RenderStats{}; }
 const std::vector<double>& HipVolPathIntegrator::LastAccumulation() const { return be_ ? be_->last : kEmpty; }
 const std::vector<double>& HipSimplePathIntegrator::LastAccumulation() const { return be_ ? be_->last : kEmpty; }
+static const std::vector<uint32_t> kNoCounts;
+const std::vector<uint32_t>& HipPathIntegrator::LastSampleCounts() const { return be_ ? be_->counts : kNoCounts; }
+const std::vector<uint32_t>& HipSimplePathIntegrator::LastSampleCounts() const { return be_ ? be_->counts : kNoCounts; }
+const std::vector<uint32_t>& HipVolPathIntegrator::LastSampleCounts() const { return be_ ? be_->counts : kNoCounts; }
 
 }  // namespace pt

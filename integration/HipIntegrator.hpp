@@ -11,6 +11,13 @@
 // camera's Film through FilmTile / Film::Merge (Film.hpp:118-132).  Li(Ray)
 // is inherited unchanged: the CPU integrator stays available for tests.
 //
+// Render(n) is adaptive like the reference's TileIntegrator::Render
+// (Integrators.cpp:55-86: per-pixel rounds of spp samples until the
+// luminance-weighted relative variance is <= 1.5, at most 128*spp) -- on the
+// GPUs, with the devices splitting the frame by 32x32 tiles.
+// SetAdaptive(false) renders exactly spp samples per pixel (interleaved
+// sample shards), the fixed-SPP frame of the benchmark.
+//
 // The sample stream is the counter-based PCG stream of DESIGN.md; use
 // pt::PCGSampler to choose its seed (any other Sampler supplies only its
 // SamplesPerPixel(); the reference's own samplers are unseeded).
@@ -82,10 +89,15 @@ public:
     RenderStats LastStats() const;
     // W*H*4 {sum R*w, sum G*w, sum B*w, sum w} the last Render merged into the Film
     const std::vector<double>& LastAccumulation() const;
+    // adaptive sampling on (default, as the reference's Render) or fixed SPP
+    void SetAdaptive(bool on) { adaptive_ = on; }
+    // W*H samples per pixel of the last Render
+    const std::vector<uint32_t>& LastSampleCounts() const;
 
 private:
     std::shared_ptr<LightSampler> ls_;
     uint32_t depth_;
+    bool adaptive_ = true;
     mutable std::unique_ptr<HipBackend> be_;
     mutable std::mutex mu_;
 };
@@ -98,9 +110,14 @@ public:
     void Render(unsigned int n = 1) const override;
     RenderStats LastStats() const;
     const std::vector<double>& LastAccumulation() const;
+    // adaptive sampling on (default, as the reference's Render) or fixed SPP
+    void SetAdaptive(bool on) { adaptive_ = on; }
+    // W*H samples per pixel of the last Render
+    const std::vector<uint32_t>& LastSampleCounts() const;
 
 private:
     uint32_t depth_;
+    bool adaptive_ = true;
     mutable std::unique_ptr<HipBackend> be_;
     mutable std::mutex mu_;
 };
@@ -118,10 +135,15 @@ public:
     void Render(unsigned int n = 1) const override;
     RenderStats LastStats() const;
     const std::vector<double>& LastAccumulation() const;
+    // adaptive sampling on (default, as the reference's Render) or fixed SPP
+    void SetAdaptive(bool on) { adaptive_ = on; }
+    // W*H samples per pixel of the last Render
+    const std::vector<uint32_t>& LastSampleCounts() const;
 
 private:
     std::shared_ptr<LightSampler> ls_;
     uint32_t depth_;
+    bool adaptive_ = true;
     mutable std::unique_ptr<HipBackend> be_;
     mutable std::mutex mu_;
 };

@@ -829,24 +829,32 @@ static void cmd_tonemap(const std::string& out, const std::string& inPath, int W
 // HipVolPathIntegrator on the
 // reference-built scene (integration/HipIntegrator.hpp), Render(gpus) into the
 // reference Film; dumps the merged accumulation like `film`.
-static void cmd_hip(World& w, const std::string& out, unsigned gpus) {
+static void cmd_hip(World& w, const std::string& out, unsigned gpus, bool adaptive) {
     auto sampler = std::make_shared<pt::PCGSampler>(w.spp, w.seed, w.W);
     std::vector<double> acc;
+    std::vector<uint32_t> counts;
+    auto go = [&](auto& integ) {
+        integ.SetAdaptive(adaptive);
+        integ.Render(gpus);
+        acc = integ.LastAccumulation();
+        counts = integ.LastSampleCounts();
+    };
     if (w.integ == "simple") {
         pt::HipSimplePathIntegrator integ(w.scene, w.camera, sampler, w.maxDepth);
-        integ.Render(gpus);
-        acc = integ.LastAccumulation();
+        go(integ);
     } else if (w.integ == "volpath") {
         pt::HipVolPathIntegrator integ(w.scene, w.camera, sampler, w.ls, w.maxDepth);
-        integ.Render(gpus);
-        acc = integ.LastAccumulation();
+        go(integ);
     } else {
         pt::HipPathIntegrator integ(w.scene, w.camera, sampler, w.ls, w.maxDepth);
-        integ.Render(gpus);
-        acc = integ.LastAccumulation();
+        go(integ);
     }
     wr(out + ".hipfilm.bin", acc);
-    cmd_film(w, out, w.spp);  // the reference's own Li on the same objects (same sky power)
+    wr(out + ".hipcounts.bin", counts);
+    // the reference's own frame on the same objects (same sky power): its
+    // fixed-SPP Li splat, or its own adaptive Render
+    if (adaptive) cmd_adaptive(w, out);
+    else cmd_film(w, out, w.spp);
 }
 #endif
 
@@ -880,7 +888,7 @@ int main(int argc, char** argv) {
     else if (cmd == "lights") cmd_lights(w, out, argv[4]);
     else if (cmd == "time") cmd_time(w, atoi(argv[4]), (unsigned)atoi(argv[5]), argc > 6 ? argv[6] : "render");
 #ifdef PT_WITH_HIP
-    else if (cmd == "hip") cmd_hip(w, out, argc > 4 ? (unsigned)atoi(argv[4]) : 1u);
+    else if (cmd == "hip") cmd_hip(w, out, argc > 4 ? (unsigned)atoi(argv[4]) : 1u, argc > 5 && std::string(argv[5]) == "adaptive");
 #endif
     else { fprintf(stderr, "unknown cmd %s\n", cmd.c_str()); return 2; }
     return 0;

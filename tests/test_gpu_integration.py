@@ -56,3 +56,30 @@ def test_drop_in_integrator_matches_reference_film(name, tmp_path):
     same = np.isclose(film.accum, gpu, rtol=1e-3, atol=1e-6).mean()
     record_parity(f"dropin_vs_python/{name}", "film", same)
     assert same >= 0.999
+
+
+@pytest.mark.skipif(not HARNESS.exists(), reason="hip_harness not built (needs /root/reference at build time)")
+@pytest.mark.parametrize("name", ["example1", "cornell_c3", "zoo", "fog", "instances", "sanmiguel", "lens_box"])
+def test_drop_in_adaptive_render_matches_reference_render(name, tmp_path):
+    """The drop-in's default Render (adaptive, like TileIntegrator::Render)
+    against the reference's own adaptive Render of the same objects in the
+    same process (so a randomly pre-processed sky has one power): identical
+    per-pixel sample counts, film within the film tolerance."""
+    setup = parity_scenes()[name]()
+    recipe = write_recipe(tmp_path, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
+                          setup.max_depth, setup.light_sampler, setup.extra_lights)
+    out = tmp_path / "o"
+    subprocess.run([str(HARNESS), str(recipe), "hip", str(out), "1", "adaptive"], check=True, timeout=300)
+    W, H = setup.camera.film.Resolution()
+    counts = np.fromfile(f"{out}.hipcounts.bin", np.uint32).reshape(H, W)
+    ref_counts = np.fromfile(f"{out}.adaptive_counts.bin", np.uint32).reshape(H, W)
+    same = (counts == ref_counts).mean()
+    record_parity(f"dropin_adaptive_counts/{name}", "counts", same)
+    assert same >= DROPIN_FILM_MIN.get(name, 1.0), f"{name}: {same:.4f} of pixels with the reference's sample count"
+    gpu = np.fromfile(f"{out}.hipfilm.bin", np.float64).reshape(H, W, 4)
+    ref = np.fromfile(f"{out}.adaptive_film.bin", np.float64).reshape(H, W, 4)
+    num = np.linalg.norm(gpu[..., :3] - ref[..., :3], axis=-1)
+    den = np.maximum(np.linalg.norm(ref[..., :3], axis=-1), 1e-3 * ref[..., 3])
+    frac = (num <= 1e-3 * den + 1e-7).mean()
+    record_parity(f"dropin_adaptive_film/{name}", "film", frac)
+    assert frac >= DROPIN_FILM_MIN.get(name, 0.999), f"{name}: {frac:.4f} of pixels within 1e-3 rel L2"
