@@ -96,8 +96,14 @@ static inline uint32_t fbits(float f) {
     memcpy(&u, &f, 4);
     return u;
 }
-static inline float blend_random(v3 o, v3 d, int prim) {
-    uint32_t h = pcg_hash(fbits(o.x) ^ pcg_hash(fbits(d.y) ^ pcg_hash((uint32_t)prim)));
+static inline float blend_random(v3 o, v3 d, int prim) { /* the device's draw (pt_shading.h) */
+    uint32_t h = pcg_hash((uint32_t)prim);
+    h = pcg_hash(h ^ fbits(o.x));
+    h = pcg_hash(h ^ fbits(o.y));
+    h = pcg_hash(h ^ fbits(o.z));
+    h = pcg_hash(h ^ fbits(d.x));
+    h = pcg_hash(h ^ fbits(d.y));
+    h = pcg_hash(h ^ fbits(d.z));
     return (float)(h >> 8) * (1.0f / 16777216.0f);
 }
 

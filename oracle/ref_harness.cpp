@@ -798,6 +798,71 @@ static void cmd_adaptive(World& w, const std::string& out) {
     wr(out + ".adaptive_recs.bin", g_adapt);
 }
 
+// --- stats: the reference's own TileIntegrator::Render with its own
+// StratifiedSampler (main.cpp's sampler) or UniformSampler and unseeded RNGs,
+// multi-threaded, adaptive rounds and all: per pixel the number of samples
+// Render traced and their mean / unbiased variance per channel (F8, for the
+// statistical comparison; nothing here is deterministic).  A forwarding
+// sampler records which pixel each thread is on; Li is wrapped to accumulate.
+static thread_local int t_pixel = -1;
+class TrackSampler : public Sampler {
+public:
+    TrackSampler(std::shared_ptr<Sampler> in, int width) : in(std::move(in)), width(width) {}
+    unsigned int SamplesPerPixel() const override { return in->SamplesPerPixel(); }
+    void StartPixelSample(const glm::ivec2& p, int index) override {
+        t_pixel = p.y * width + p.x;
+        in->StartPixelSample(p, index);
+    }
+    double get1D() override { return in->get1D(); }
+    glm::dvec2 get2D() override { return in->get2D(); }
+    glm::dvec2 getPixel2D() override { return in->getPixel2D(); }
+    std::array<glm::vec2, 4> get2Dx4f() override { return in->get2Dx4f(); }
+    std::shared_ptr<Sampler> Clone() const override { return std::make_shared<TrackSampler>(in->Clone(), width); }
+
+private:
+    std::shared_ptr<Sampler> in;
+    int width;
+};
+struct PixStat { double n = 0, sum[3] = {0, 0, 0}, sq[3] = {0, 0, 0}; };
+static std::vector<PixStat> g_stat;
+template <class Base>
+struct StatRec : Base {
+    using Base::Base;
+    glm::vec3 Li(Ray ray) const override {
+        ray.time = 0;
+        glm::vec3 L = Base::Li(ray);
+        PixStat& s = g_stat[t_pixel];  // a pixel is rendered by one thread
+        s.n += 1;
+        for (int c = 0; c < 3; c++) {
+            s.sum[c] += L[c];
+            s.sq[c] += (double)L[c] * L[c];
+        }
+        return L;
+    }
+};
+static void cmd_stats(World& w, const std::string& out, int threads) {
+    const unsigned r = (unsigned)std::lround(std::sqrt((double)w.spp));
+    std::shared_ptr<Sampler> inner;
+    if (r * r == w.spp) inner = std::make_shared<StratifiedSampler>(r, r);
+    else inner = std::make_shared<UniformSampler>(w.spp);
+    auto sampler = std::make_shared<TrackSampler>(inner, w.W);
+    std::shared_ptr<Integrator> integ;
+    if (w.integ == "simple") integ = std::make_shared<StatRec<SimplePathIntegrator>>(w.scene, w.camera, sampler, w.maxDepth);
+    else if (w.integ == "volpath")
+        integ = std::make_shared<StatRec<VolPathIntegrator>>(w.scene, w.camera, sampler, w.ls, w.maxDepth);
+    else integ = std::make_shared<StatRec<PathIntegrator>>(w.scene, w.camera, sampler, w.ls, w.maxDepth);
+    g_stat.assign((size_t)w.W * w.H, PixStat{});
+    integ->Render(threads);
+    std::vector<double> res;
+    for (const auto& s : g_stat) {
+        res.push_back(s.n);
+        for (int c = 0; c < 3; c++) res.push_back(s.n > 0 ? s.sum[c] / s.n : 0.0);
+        for (int c = 0; c < 3; c++)
+            res.push_back(s.n > 1 ? (s.sq[c] - s.sum[c] * s.sum[c] / s.n) / (s.n - 1) : 0.0);
+    }
+    wr(out + ".stats.bin", res);
+}
+
 // --- tonemap: Film::WritePNG's pixel loop (Film.hpp:183-196) over an
 // accumulation buffer {sum RGB*w, sum w} (W*H*4 doubles): the reference's own
 // reinhard_jodie / ACESFilm and linear_to_sRGB, through the writer's
@@ -883,6 +948,7 @@ int main(int argc, char** argv) {
         cmd_li(w, out, x0, y0, x1, y1, spp);
     } else if (cmd == "film") cmd_film(w, out, w.spp);
     else if (cmd == "adaptive") cmd_adaptive(w, out);
+    else if (cmd == "stats") cmd_stats(w, out, argc > 4 ? atoi(argv[4]) : 8);
     else if (cmd == "bsdf") cmd_bsdf(w, out, argv[4], atoi(argv[5]));
     else if (cmd == "camera") cmd_camera(w, out, argv[4]);
     else if (cmd == "lights") cmd_lights(w, out, argv[4]);

@@ -95,9 +95,19 @@ __device__ float tex_alpha(int id, float u, float v) {
 
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
 // AlphaTester Blend draws random_float() (Material.hpp:189) from an unseeded
-// thread-local generator; parity is waived there: hash of the ray.
+// thread-local generator; no frame of the reference reproduces it, so the
+// draw is a hash of the whole ray (its origin and direction come from the
+// sample's stream, so every ray and bounce of every sample gets its own
+// value) and the primitive; the accept rate is checked statistically against
+// the reference's own Render (tests: blend_box).
 __device__ __forceinline__ float blend_random(f3 o, f3 d, int prim) {
-    uint32_t h = pcg_hash(fbits(o.x) ^ pcg_hash(fbits(d.y) ^ pcg_hash((uint32_t)prim)));
+    uint32_t h = pcg_hash((uint32_t)prim);
+    h = pcg_hash(h ^ fbits(o.x));
+    h = pcg_hash(h ^ fbits(o.y));
+    h = pcg_hash(h ^ fbits(o.z));
+    h = pcg_hash(h ^ fbits(d.x));
+    h = pcg_hash(h ^ fbits(d.y));
+    h = pcg_hash(h ^ fbits(d.z));
     return (float)(h >> 8) * (1.0f / 16777216.0f);
 }
 

@@ -194,6 +194,22 @@ def cornell(W: int = 1024, H: int = 1024, spp: int = 256, config: str = "c2", ma
     return SceneSetup(scene, camera, kind, ls, max_depth, seed, spp, extra).finish()
 
 
+def blend_box(W: int = 64, H: int = 64, spp: int = 16, max_depth: int = 8, alpha: float = 0.35,
+              seed: int = 0x5EED0041) -> SceneSetup:
+    """C3 Cornell box behind a see-through panel: a two-triangle mesh with a
+    constant alpha texture under AlphaTester Blend (Material.hpp:181-198), so
+    every ray crossing it passes with probability 1 - alpha (the reference's
+    hidden random_float() < a, Material.hpp:189)."""
+    setup = cornell(W=W, H=H, spp=spp, config="c3", max_depth=max_depth, seed=seed)
+    scene = setup.scene
+    panel = _quad_tris((-0.55, -0.6, 1.2), (0.55, -0.6, 1.2), (0.55, 0.5, 1.2), (-0.55, 0.5, 1.2))
+    mat = MicrofacetDiffuse(SolidColor((0.1, 0.6, 0.2)), None, None, None, SolidColor((alpha, alpha, alpha)))
+    mat.setAlphaTester(AlphaTester(AlphaMode.Blend))
+    idx, v, n, uv = panel
+    scene.Add(Model([Mesh(idx, v, None, n, uv, mat)]))
+    return SceneSetup(scene, setup.camera, setup.integrator, UniformLightSampler(), max_depth, seed, spp).finish()
+
+
 # --------------------------------------------------------------------------
 def _grid_mesh(nx: int, nz: int, size: float, y_fn, rng, tangents: bool, uv_scale: float = 1.0):
     xs = np.linspace(-size, size, nx + 1, dtype=np.float32)

@@ -75,3 +75,25 @@ def load(name: str):
             fresh.PreProcess(setup.scene.BoundingBox())
             setup.light_sampler = fresh
     return setup, setup.make_integrator(), fx
+
+
+# ---------------------------------------------------------------- F8: statistical parity
+def stats_scenes():
+    """Scenes of tests/golden/stats.npz: the reference's own Render with its
+    StratifiedSampler(32, 32) and unseeded RNGs (gen_golden.gen_stats)."""
+    from gen_golden import STATS_SCENES
+    return STATS_SCENES
+
+
+def z_test(L: np.ndarray, ref: np.ndarray) -> np.ndarray:
+    """Per pixel and channel: does our per-pixel sample mean agree with the
+    reference's within 4 standard errors, |mu1 - mu2| <= 4 sqrt(s1^2/n1 +
+    s2^2/n2)?  L: (H, W, n, 3) samples; ref: (H, W, 7)
+    {n, mean[3], var[3]}.  Zero-variance pixels (sky) compare their means to
+    1e-5 relative."""
+    L = L.astype(np.float64)
+    n = L.shape[2]
+    mg, vg = L.mean(2), L.var(2, ddof=1)
+    nr, mr, vr = ref[..., 0:1], ref[..., 1:4], np.maximum(ref[..., 4:7], 0.0)
+    se = np.sqrt(vg / n + vr / nr)
+    return np.abs(mg - mr) <= np.maximum(4.0 * se, 1e-5 * np.abs(mr))

@@ -14,6 +14,8 @@ reference computes on it:
   lsample_*  Light::sample / PDF / L                         (F4)
   adaptive.npz  TileIntegrator::Render's own adaptive loop (Integrators.cpp:
              55-86) on the PCG stream: per-pixel sample counts + film
+  stats.npz  the same Render with its own StratifiedSampler and unseeded RNGs:
+             per-pixel sample count, mean and variance (F8)
 
     python tests/golden/gen_golden.py
 """
@@ -226,6 +228,31 @@ def gen_adaptive(tmp: Path):
     print(f"adaptive: {(OUT / 'adaptive.npz').stat().st_size / 1024:.0f} KiB, {len(ADAPTIVE_SCENES)} scenes")
 
 
+STATS_SCENES = {
+    "example1": lambda: scenes.example_1(W=48, H=48, spp=1024, seed=0x5EED0051),
+    "cornell_c3": lambda: scenes.cornell(W=48, H=48, spp=1024, config="c3", seed=0x5EED0052),
+    "blend_box": lambda: scenes.blend_box(W=48, H=48, spp=1024, seed=0x5EED0053),
+}
+
+
+def gen_stats(tmp: Path):
+    """F8: the reference's own TileIntegrator::Render with main.cpp's
+    StratifiedSampler(32, 32) and its unseeded random numbers (8 threads,
+    adaptive rounds): per pixel the samples traced, their mean and variance."""
+    res = {}
+    for name, make in STATS_SCENES.items():
+        setup = make()
+        d = tmp / f"stats_{name}"
+        recipe = write_recipe(d, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
+                              setup.max_depth, setup.light_sampler, setup.extra_lights)
+        out = d / "o"
+        subprocess.run([str(HARNESS), str(recipe), "stats", str(out), "8"], check=True, stdout=subprocess.DEVNULL)
+        W, H = setup.camera.film.Resolution()
+        res[name] = np.fromfile(f"{out}.stats.bin", np.float64).reshape(H, W, 7)
+    np.savez_compressed(OUT / "stats.npz", **res)
+    print(f"stats: {(OUT / 'stats.npz').stat().st_size / 1024:.0f} KiB, {len(res)} scenes")
+
+
 def main(names=None):
     """All scenes share one rng stream (the committed round-1 fixtures); a
     scene regenerated alone (`gen_golden.py NAME...`) uses its own stream
@@ -244,6 +271,8 @@ def main(names=None):
             gen_resolve(np.random.default_rng([20261016, 7]), Path(t))
         if not names or "adaptive" in names:
             gen_adaptive(Path(t))
+        if not names or "stats" in names:
+            gen_stats(Path(t))
 
 
 if __name__ == "__main__":
