@@ -162,6 +162,9 @@ typedef struct pt_light {
     float color[3];      /* UNIFORM/DISTANT/POINT colour; SKY: horizon c0   */
     float vec[3];        /* DISTANT dir; POINT position; SKY: zenith c1     */
     float scale;         /* SKY scale                                       */
+    int32_t instance;    /* AREA: -1, or the instance whose transform moves
+                          * the shape (TransformedLight / AnimatedLight,
+                          * Light.cpp:300-364; prim is then the BLAS slot)  */
 } pt_light;
 
 enum { PT_LS_UNIFORM = 0, PT_LS_POWER = 1 };

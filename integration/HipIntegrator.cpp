@@ -133,6 +133,11 @@ PT_MEMBER(GaussSigma, GaussianFilter, double, sigma);
 #ifdef PT_WITH_MODEL
 PT_MEMBER(ModelBvh, Model, std::shared_ptr<BLASBase>, model_bvh);
 #endif
+PT_MEMBER(TlLight, TransformedLight, std::shared_ptr<Light>, light);
+PT_MEMBER(TlXf, TransformedLight, glm::mat4, transform);
+PT_MEMBER(AlLight, AnimatedLight, std::shared_ptr<Light>, light);
+PT_MEMBER(AlDir, AnimatedLight, glm::vec3, dir);
+PT_MEMBER(AlTb, AnimatedLight, glm::vec2, timeBounds);
 PT_MEMBER(TpPrim, TransformedPrimitive, std::shared_ptr<Primitive>, primitive);
 PT_MEMBER(TpXf, TransformedPrimitive, glm::mat4, transform);
 PT_MEMBER(TpInv, TransformedPrimitive, glm::mat4, invTransform);
@@ -377,6 +382,9 @@ struct Flat {
         };
         std::vector<Inst> inst;
         std::vector<uint32_t> blas_of_slot(n_top, UINT32_MAX), inst_of_slot(n_top, UINT32_MAX);
+        auto mat_key = [](const glm::mat4& m) { return std::string((const char*)&m[0][0], sizeof(glm::mat4)); };
+        std::map<std::pair<const Light*, std::string>, int32_t> inst_light;  // (inner light, matrix) -> instance
+        std::vector<std::shared_ptr<Light>> inner_lights;
         for (uint32_t i = 0; i < n_top; i++) {
             const Primitive* p = top[i].get();
             if (dynamic_cast<const GeometricPrimitive*>(p)) continue;
@@ -399,8 +407,13 @@ struct Flat {
                 if (blas_of_slot[i] == UINT32_MAX) throw std::runtime_error("HipPathIntegrator: unsupported TLAS primitive");
                 continue;
             }
-            if (!inner->GetLights().empty())
-                throw std::runtime_error("HipPathIntegrator: lights inside an instance are not supported");
+            // emitters inside the instance: TransformedPrimitive / AnimatedPrimitive
+            // ::GetLights wrap its inner AreaLights with this very matrix
+            // (Primitive.cpp:66-73, 91-96; Light.cpp:338-364)
+            for (const auto& l : inner->GetLights()) {
+                inst_light[{l.get(), mat_key(xf)}] = (int32_t)inst.size();
+                inner_lights.push_back(l);
+            }
             const uint32_t b = blas_of(inner);
             if (b == UINT32_MAX) throw std::runtime_error("HipPathIntegrator: unsupported instanced primitive");
             inst_of_slot[i] = (uint32_t)inst.size();
@@ -484,12 +497,39 @@ struct Flat {
                 if (std::find(all.begin(), all.end(), l) == all.end()) all.push_back(l);
         }
         std::unordered_map<const Light*, uint32_t> lid;
+        auto area = [&](pt_light& r, const Light* inner, int32_t instance) {
+            auto* a = dynamic_cast<const AreaLight*>(inner);
+            if (!a) throw std::runtime_error("HipPathIntegrator: only area lights inside an instance");
+            auto it = light_slot.find(a);
+            if (it == light_slot.end()) throw std::runtime_error("HipPathIntegrator: area light without a primitive");
+            r.kind = PT_LIGHT_AREA;
+            r.prim = it->second;
+            r.tex = texture(PT_GET(*a, AreaTex));
+            r.one_sided = PT_GET(*a, AreaOneSided) ? 1u : 0u;
+            r.instance = instance;
+            return it->second;
+        };
+        auto wrapped = [&](const Light* inner, const glm::mat4& xf) {
+            auto it = inst_light.find({inner, mat_key(xf)});
+            if (it == inst_light.end()) throw std::runtime_error("HipPathIntegrator: light of an unknown instance");
+            return it->second;
+        };
         for (const auto& l : all) {
             pt_light r{};
             r.prim = r.tex = -1;
+            r.instance = -1;
             r.power = l->Power();
             r.pmf = ls ? ls->PMF(l) : 0.0f;
-            if (auto* a = dynamic_cast<const AreaLight*>(l.get())) {
+            if (auto* t = dynamic_cast<const TransformedLight*>(l.get())) {
+                const Light* inner = PT_GET(*t, TlLight).get();
+                area(r, inner, wrapped(inner, PT_GET(*t, TlXf)));
+            } else if (auto* an = dynamic_cast<const AnimatedLight*>(l.get())) {
+                // AnimatedLight at the rays' time 0: the AnimatedPrimitive's matrix
+                const Light* inner = PT_GET(*an, AlLight).get();
+                const glm::vec2 tb = PT_GET(*an, AlTb);
+                const float tt = glm::clamp(0.0f - tb.x, tb.x, tb.y) / (tb.y - tb.x);
+                area(r, inner, wrapped(inner, glm::translate(glm::mat4(1), PT_GET(*an, AlDir) * tt)));
+            } else if (auto* a = dynamic_cast<const AreaLight*>(l.get())) {
                 auto it = light_slot.find(a);
                 if (it == light_slot.end()) throw std::runtime_error("HipPathIntegrator: area light without a primitive");
                 r.kind = PT_LIGHT_AREA;
@@ -518,6 +558,17 @@ struct Flat {
             } else {
                 throw std::runtime_error("HipPathIntegrator: unsupported light type");
             }
+            lid[l.get()] = (uint32_t)lights.size();
+            lights.push_back(r);
+        }
+        // the inner AreaLight of an emitter inside an instance: what a path
+        // that hits it sees (interaction.AreaLight, Primitive.cpp:58)
+        for (const auto& l : inner_lights) {
+            if (lid.count(l.get())) continue;
+            pt_light r{};
+            r.power = l->Power();
+            r.pmf = ls ? ls->PMF(l) : 0.0f;
+            prims[area(r, l.get(), -1)].light = (int32_t)lights.size();
             lid[l.get()] = (uint32_t)lights.size();
             lights.push_back(r);
         }

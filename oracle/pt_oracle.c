@@ -1134,11 +1134,23 @@ static v3 sky_le(const pt_light* l, v3 d) {
 }
 static v3 inf_le(const pt_light* l, v3 d) { return l->kind == PT_LIGHT_SKY_INF ? sky_le(l, d) : vl(l->color); }
 
+/* TransformedLight / AnimatedLight (Light.cpp:300-364): the inner
+ * AreaLight's shape in the instance's object space */
+static const pt_instance* light_instance(const scene_t* S, const pt_light* l) {
+    return (l->kind == PT_LIGHT_AREA && l->instance >= 0) ? &S->s->instances[l->instance] : NULL;
+}
 static lsample_t light_sample(const scene_t* S, const pt_light* l, float u0, float u1) {
     lsample_t ls;
     memset(&ls, 0, sizeof(ls));
     if (l->kind == PT_LIGHT_AREA) {
         ls.si = shape_sample(S, &S->s->prims[l->prim], u0, u1);
+        const pt_instance* I = light_instance(S, l);
+        if (I) { /* TransformedLight::sample: p by the transform, n by the normal matrix */
+            float NM[9];
+            normal_matrix(I->transform, NM);
+            ls.si.p = m4_point(I->transform, ls.si.p);
+            ls.si.n = m3_mul(NM, ls.si.n);
+        }
         return ls;
     }
     if (l->kind == PT_LIGHT_POINT) {
@@ -1170,6 +1182,17 @@ static inline int light_is_delta(const pt_light* l) { return l->kind == PT_LIGHT
 static float light_pdf(const scene_t* S, const pt_light* l, const si_t* si, const ray_t* r) {
     if (l->kind == PT_LIGHT_AREA) {
         const pt_prim* p = &S->s->prims[l->prim];
+        const pt_instance* I = light_instance(S, l);
+        if (I) { /* TransformedLight::PDF: point, normal and ray to object space */
+            si_t lo = *si;
+            lo.p = m4_point(I->inv, si->p);
+            lo.n = normalize(m4_dir(I->inv, si->n));
+            ray_t lr = *r;
+            lr.o = m4_point(I->inv, r->o);
+            lr.d = normalize(m4_dir(I->inv, r->d));
+            if (l->one_sided) return dot(neg(lr.d), lo.n) > 0 ? shape_pdf(S, p, &lo, &lr) : 0;
+            return shape_pdf(S, p, &lo, &lr);
+        }
         if (l->one_sided) return dot(neg(r->d), si->n) > 0 ? shape_pdf(S, p, si, r) : 0;
         return shape_pdf(S, p, si, r);
     }
@@ -1178,6 +1201,15 @@ static float light_pdf(const scene_t* S, const pt_light* l, const si_t* si, cons
 }
 static v3 light_L(const scene_t* S, const pt_light* l, const si_t* si, const ray_t* r) {
     if (l->kind == PT_LIGHT_AREA) {
+        const pt_instance* I = light_instance(S, l);
+        if (I) { /* TransformedLight::L: a fresh interaction, n by the normal matrix, uv (0, 0) */
+            float NM[9];
+            normal_matrix(I->transform, NM);
+            const v3 n = m3_mul(NM, si->n);
+            const float uv0[2] = {0, 0};
+            if (l->one_sided && dot(r->d, n) > 0) return V(0, 0, 0);
+            return tex_eval(S, l->tex, uv0);
+        }
         if (l->one_sided && dot(r->d, si->n) > 0) return V(0, 0, 0);
         return tex_eval(S, l->tex, si->uv);
     }

@@ -505,9 +505,27 @@ static void cmd_bvh(World& w, const std::string& out) {
 }
 
 // --- info: lights in sampler-input order
+// TransformedLight / AnimatedLight (Light.hpp) keep their inner light
+// private; GetLights() makes fresh wrappers on every call, so a wrapper is
+// named by what it wraps ("xf:" / "anim:" + the inner light's owner)
+template <class Tag, typename Tag::type M>
+struct Member {
+    friend typename Tag::type get(Tag) { return M; }
+};
+#define REF_MEMBER(NAME, CLASS, TYPE, FIELD) \
+    struct NAME {                            \
+        using type = TYPE CLASS::*;          \
+        friend type get(NAME);               \
+    };                                       \
+    template struct Member<NAME, &CLASS::FIELD>
+REF_MEMBER(TlInner, TransformedLight, std::shared_ptr<Light>, light);
+REF_MEMBER(AlInner, AnimatedLight, std::shared_ptr<Light>, light);
 static std::string owner(World& w, const Light* l) {
     auto it = w.lightOwner.find(l);
-    return it == w.lightOwner.end() ? "?" : it->second;
+    if (it != w.lightOwner.end()) return it->second;
+    if (auto* t = dynamic_cast<const TransformedLight*>(l)) return "xf:" + owner(w, ((*t).*get(TlInner{})).get());
+    if (auto* a = dynamic_cast<const AnimatedLight*>(l)) return "anim:" + owner(w, ((*a).*get(AlInner{})).get());
+    return "?";
 }
 static void cmd_info(World& w, const std::string& out) {
     FILE* f = fopen((out + ".lights.txt").c_str(), "w");
@@ -553,7 +571,10 @@ static void cmd_trace(World& w, const std::string& out, const std::string& raysP
             o[11] = si.uv.x; o[12] = si.uv.y;
             o[13] = si.tangent.x; o[14] = si.tangent.y; o[15] = si.tangent.z;
             ids[i * 3 + 0] = si.mat ? w.matId[si.mat.get()] : -1;
-            ids[i * 3 + 1] = si.AreaLight ? lightIdx[si.AreaLight.get()] : -1;
+            // -2: an emitter whose light is not in Scene::GetLights() (the
+            // inner AreaLight of an instance, Primitive.cpp:58)
+            ids[i * 3 + 1] = !si.AreaLight ? -1
+                             : (lightIdx.count(si.AreaLight.get()) ? lightIdx[si.AreaLight.get()] : -2);
             ids[i * 3 + 2] = si.medium ? 1 : 0;
         }
         anyhit[i] = w.scene->IntersectPred(ray, r[6]) ? 1 : 0;

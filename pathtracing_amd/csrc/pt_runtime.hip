@@ -431,7 +431,8 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
     for (uint32_t l = 0; l < s->n_lights; l++) {
         const pt_light& L = s->lights[l];
         if (L.kind == PT_LIGHT_AREA && (L.prim < 0 || (uint32_t)L.prim >= s->n_prims || L.tex < 0 ||
-                                        (uint32_t)L.tex >= s->n_textures))
+                                        (uint32_t)L.tex >= s->n_textures || L.instance < -1 ||
+                                        (L.instance >= 0 && (uint32_t)L.instance >= s->n_instances)))
             return fail(c, PT_ERR_ARG, "light %u: bad area light", l);
     }
     for (uint32_t m = 0; m < s->n_materials; m++) {
@@ -450,7 +451,7 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
     if (s->n_media && !s->media) return fail(c, PT_ERR_ARG, "media array missing");
     if (s->n_media > PT_MAX_MEDIA) return fail(c, PT_ERR_ARG, "more than %d media", PT_MAX_MEDIA);
     if (s->n_prims > REF_SLOT_MASK) return fail(c, PT_ERR_ARG, "too many primitives");
-    {  // instances: one level, BLAS targets without instances / nested BLAS / area lights,
+    {  // instances: one level, BLAS targets without instances / nested BLAS,
        // ascending virtual ranges past the real slots
         uint64_t next = s->n_prims;
         for (uint32_t k = 0; k < s->n_instances; k++) {
@@ -459,8 +460,8 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
             const pt_bvh_desc& B = s->bvhs[I.bvh];
             if ((uint64_t)B.prim_base + B.n_prims > s->n_prims) return fail(c, PT_ERR_ARG, "instance %u: bad bvh", k);
             for (uint32_t j = B.prim_base; j < B.prim_base + B.n_prims; j++)
-                if (s->prims[j].kind == PT_PRIM_BLAS || s->prims[j].kind == PT_PRIM_INSTANCE || s->prims[j].light >= 0)
-                    return fail(c, PT_ERR_ARG, "instance %u: nested instance or area light inside", k);
+                if (s->prims[j].kind == PT_PRIM_BLAS || s->prims[j].kind == PT_PRIM_INSTANCE)
+                    return fail(c, PT_ERR_ARG, "instance %u: nested instance", k);
             if (I.virt_base < next || (uint64_t)I.virt_base + B.n_prims > REF_SLOT_MASK)
                 return fail(c, PT_ERR_ARG, "instance %u: bad virtual slot range", k);
             next = (uint64_t)I.virt_base + B.n_prims;

@@ -581,6 +581,50 @@ __device__ float mat_pdf(int mid, f3 ind, const SurfInt& si, f3 dir) {
 }
 
 // ------------------------------------------------------------------ lights (Light.cpp)
+// ---- instance transforms (TransformedPrimitive::Intersect / IntersectPred,
+// Primitive.cpp:42-72; TransformedLight, Light.cpp:300-336): glm mat4 * vec4 as the reference build contracts it
+// (fixture search): fma(m0, x, m1*y) + fma(m2, z, m3*w)
+__device__ __forceinline__ f3 m4_point(const float* m, f3 p) {
+    return F3(fma_(m[0], p.x, rmul(m[4], p.y)) + fma_(m[8], p.z, m[12]),
+              fma_(m[1], p.x, rmul(m[5], p.y)) + fma_(m[9], p.z, m[13]),
+              fma_(m[2], p.x, rmul(m[6], p.y)) + fma_(m[10], p.z, m[14]));
+}
+__device__ __forceinline__ f3 m4_dir(const float* m, f3 v) {
+    return F3(fma_(m[0], v.x, rmul(m[4], v.y)) + fma_(m[8], v.z, rmul(m[12], 0.0f)),
+              fma_(m[1], v.x, rmul(m[5], v.y)) + fma_(m[9], v.z, rmul(m[13], 0.0f)),
+              fma_(m[2], v.x, rmul(m[6], v.y)) + fma_(m[10], v.z, rmul(m[14], 0.0f)));
+}
+// transpose(inverse(mat3(T))) (glm compute_inverse<3,3>) with the reference
+// build's contraction (fixture search), NM[c*3+r]
+__device__ __forceinline__ float df_(float a, float b, float c, float d) { return fma_(a, b, -rmul(c, d)); }
+__device__ void normal_matrix(const float* T, float* NM) {
+#define M(c, r) T[(c) * 4 + (r)]
+    const float D0 = df_(M(1, 1), M(2, 2), M(2, 1), M(1, 2)), D1 = df_(M(0, 1), M(2, 2), M(2, 1), M(0, 2));
+    const float D2 = df_(M(0, 1), M(1, 2), M(1, 1), M(0, 2));
+    const float od = 1.0f / fma_(M(2, 0), D2, fma_(M(0, 0), D0, -rmul(M(1, 0), D1)));
+    // NM[c*3 + r] = Inverse[r][c]
+    NM[0] = D0 * od;
+    NM[1] = -df_(M(1, 0), M(2, 2), M(2, 0), M(1, 2)) * od;
+    NM[2] = df_(M(1, 0), M(2, 1), M(2, 0), M(1, 1)) * od;
+    NM[3] = -D1 * od;
+    NM[4] = df_(M(0, 0), M(2, 2), M(2, 0), M(0, 2)) * od;
+    NM[5] = -df_(M(0, 0), M(2, 1), M(2, 0), M(0, 1)) * od;
+    NM[6] = D2 * od;
+    NM[7] = -df_(M(0, 0), M(1, 2), M(1, 0), M(0, 2)) * od;
+    NM[8] = df_(M(0, 0), M(1, 1), M(1, 0), M(0, 1)) * od;
+#undef M
+}
+// glm mat3 * vec3: fma(m2, z, fma(m0, x, m1*y)) per row (fixture search)
+__device__ __forceinline__ f3 m3_mul(const float* M, f3 v) {
+    return F3(fma_(M[6], v.z, fma_(M[0], v.x, rmul(M[3], v.y))), fma_(M[7], v.z, fma_(M[1], v.x, rmul(M[4], v.y))),
+              fma_(M[8], v.z, fma_(M[2], v.x, rmul(M[5], v.y))));
+}
+// glm::normalize of a vec4 with w = 0: dot = fma(y, y, x*x) + z*z (fixture search)
+__device__ __forceinline__ f3 normalize4(f3 v) {
+    const float d = fma_(v.y, v.y, rmul(v.x, v.x)) + rmul(v.z, v.z);
+    return v * (1.0f / csqrt(d));
+}
+
 struct LSample {
     f3 L, p, n, dir;
     float u, v;
@@ -657,6 +701,29 @@ __device__ __forceinline__ f3 inf_le(const pt_light& l, f3 d) {
     }
     return ld3(l.color);
 }
+// TransformedLight / AnimatedLight (Light.cpp:300-364): an emitter inside an
+// instance; its AreaLight's shape stays in object space (l.prim is the BLAS
+// slot).  Out of line: the rare path keeps k_shade's registers.
+__device__ __noinline__ void tlight_to_world(int inst, f3& p, f3& n) {  // TransformedLight::sample
+    const DevInstance& I = S.instances[inst];
+    float NM[9];
+    normal_matrix(I.T, NM);
+    p = m4_point(I.T, p);
+    n = m3_mul(NM, n);
+}
+__device__ __noinline__ void tlight_to_object(int inst, f3& p, f3& n, f3& ro, f3& rd) {  // TransformedLight::PDF
+    const DevInstance& I = S.instances[inst];
+    p = m4_point(I.inv, p);
+    n = normalize(m4_dir(I.inv, n));
+    ro = m4_point(I.inv, ro);
+    rd = normalize(m4_dir(I.inv, rd));
+}
+__device__ __noinline__ f3 tlight_normal(int inst, f3 n) {  // TransformedLight::L's temp.n
+    float NM[9];
+    normal_matrix(S.instances[inst].T, NM);
+    return m3_mul(NM, n);
+}
+
 __device__ LSample light_sample(const pt_light& l, float u0, float u1) {
     LSample ls;
     ls.L = F3(0, 0, 0);
@@ -668,6 +735,7 @@ __device__ LSample light_sample(const pt_light& l, float u0, float u1) {
         const DevPrimInfo& pi = S.info[l.prim];
         uint32_t kind = __float_as_uint(S.geom[l.prim].a.w) & GF_KIND;
         shape_sample(kind, pi.index, u0, u1, ls);
+        if (l.instance >= 0) tlight_to_world(l.instance, ls.p, ls.n);
         return ls;
     }
     if (l.kind == PT_LIGHT_POINT) {  // Light.cpp:236-238
@@ -702,6 +770,7 @@ __device__ float light_pdf(const pt_light& l, f3 p, f3 n, f3 ro, f3 rd) {
     if (l.kind == PT_LIGHT_AREA) {  // Light.cpp:267-272
         uint32_t kind = __float_as_uint(S.geom[l.prim].a.w) & GF_KIND;
         uint32_t index = S.info[l.prim].index;
+        if (l.instance >= 0) tlight_to_object(l.instance, p, n, ro, rd);
         if (l.one_sided) return dot(-rd, n) > 0 ? shape_pdf(kind, index, p, n, ro, rd) : 0;
         return shape_pdf(kind, index, p, n, ro, rd);
     }
@@ -711,6 +780,10 @@ __device__ float light_pdf(const pt_light& l, f3 p, f3 n, f3 ro, f3 rd) {
 // Light::L(interaction, ray)
 __device__ f3 light_L(const pt_light& l, f3 n, float u, float v, f3 rd) {
     if (l.kind == PT_LIGHT_AREA) {  // Light.cpp:257-260
+        if (l.instance >= 0) {  // TransformedLight::L: fresh interaction, uv (0, 0)
+            n = tlight_normal(l.instance, n);
+            u = v = 0;
+        }
         if (l.one_sided && dot(rd, n) > 0) return F3(0, 0, 0);
         return tex_eval(l.tex, u, v);
     }

@@ -265,49 +265,8 @@ __device__ __forceinline__ uint32_t order_children_e(uint32_t mask, uint4 ch, ui
     return cand;
 }
 
-// ---- instances (TransformedPrimitive::Intersect / IntersectPred,
-// Primitive.cpp:42-72): glm mat4 * vec4 as the reference build contracts it
-// (fixture search): fma(m0, x, m1*y) + fma(m2, z, m3*w)
-__device__ __forceinline__ f3 m4_point(const float* m, f3 p) {
-    return F3(fma_(m[0], p.x, rmul(m[4], p.y)) + fma_(m[8], p.z, m[12]),
-              fma_(m[1], p.x, rmul(m[5], p.y)) + fma_(m[9], p.z, m[13]),
-              fma_(m[2], p.x, rmul(m[6], p.y)) + fma_(m[10], p.z, m[14]));
-}
-__device__ __forceinline__ f3 m4_dir(const float* m, f3 v) {
-    return F3(fma_(m[0], v.x, rmul(m[4], v.y)) + fma_(m[8], v.z, rmul(m[12], 0.0f)),
-              fma_(m[1], v.x, rmul(m[5], v.y)) + fma_(m[9], v.z, rmul(m[13], 0.0f)),
-              fma_(m[2], v.x, rmul(m[6], v.y)) + fma_(m[10], v.z, rmul(m[14], 0.0f)));
-}
-// transpose(inverse(mat3(T))) (glm compute_inverse<3,3>) with the reference
-// build's contraction (fixture search), NM[c*3+r]
-__device__ __forceinline__ float df_(float a, float b, float c, float d) { return fma_(a, b, -rmul(c, d)); }
-__device__ void normal_matrix(const float* T, float* NM) {
-#define M(c, r) T[(c) * 4 + (r)]
-    const float D0 = df_(M(1, 1), M(2, 2), M(2, 1), M(1, 2)), D1 = df_(M(0, 1), M(2, 2), M(2, 1), M(0, 2));
-    const float D2 = df_(M(0, 1), M(1, 2), M(1, 1), M(0, 2));
-    const float od = 1.0f / fma_(M(2, 0), D2, fma_(M(0, 0), D0, -rmul(M(1, 0), D1)));
-    // NM[c*3 + r] = Inverse[r][c]
-    NM[0] = D0 * od;
-    NM[1] = -df_(M(1, 0), M(2, 2), M(2, 0), M(1, 2)) * od;
-    NM[2] = df_(M(1, 0), M(2, 1), M(2, 0), M(1, 1)) * od;
-    NM[3] = -D1 * od;
-    NM[4] = df_(M(0, 0), M(2, 2), M(2, 0), M(0, 2)) * od;
-    NM[5] = -df_(M(0, 0), M(2, 1), M(2, 0), M(0, 1)) * od;
-    NM[6] = D2 * od;
-    NM[7] = -df_(M(0, 0), M(1, 2), M(1, 0), M(0, 2)) * od;
-    NM[8] = df_(M(0, 0), M(1, 1), M(1, 0), M(0, 1)) * od;
-#undef M
-}
-// glm mat3 * vec3: fma(m2, z, fma(m0, x, m1*y)) per row (fixture search)
-__device__ __forceinline__ f3 m3_mul(const float* M, f3 v) {
-    return F3(fma_(M[6], v.z, fma_(M[0], v.x, rmul(M[3], v.y))), fma_(M[7], v.z, fma_(M[1], v.x, rmul(M[4], v.y))),
-              fma_(M[8], v.z, fma_(M[2], v.x, rmul(M[5], v.y))));
-}
-// glm::normalize of a vec4 with w = 0: dot = fma(y, y, x*x) + z*z (fixture search)
-__device__ __forceinline__ f3 normalize4(f3 v) {
-    const float d = fma_(v.y, v.y, rmul(v.x, v.x)) + rmul(v.z, v.z);
-    return v * (1.0f / csqrt(d));
-}
+// ---- instances: the glm matrix helpers (m4_point, m4_dir, normal_matrix,
+// m3_mul, normalize4) live in pt_shading.h (TransformedLight uses them too)
 
 __device__ __forceinline__ uint32_t octant(f3 d) { return ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0); }
 

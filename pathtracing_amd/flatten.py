@@ -22,7 +22,7 @@ from .scene import (AlphaMode, AreaLight, CheckerTexture, DistantLight, Function
                     ImageTexture, LightSampler, Material, MicrofacetDielectric, MicrofacetDiffuse, Model, PointLight,
                     TransformedPrimitive, AnimatedPrimitive, mat4_identity, mat4_translate, _expand_seq,
                     PowerLightSampler, QuadShape, Scene, SolidColor, SpecularConductor, SphereShape, Texture,
-                    ThinDielectric, UniformInfiniteLight, UniformLightSampler)
+                    ThinDielectric, TransformedLight, UniformInfiniteLight, UniformLightSampler)
 
 
 @dataclass
@@ -274,11 +274,6 @@ def flatten_scene(scene: Scene) -> FlatScene:
         if isinstance(m, Model) and id(m) not in model_index:
             model_index[id(m)] = len(models)
             models.append(m)
-        if isinstance(p, TransformedPrimitive):
-            if isinstance(m, Model) and m.tri_lights:
-                raise ValueError("emissive meshes inside an instance are not supported")
-            if isinstance(m, GeometricPrimitive) and m.areaLight is not None:
-                raise ValueError("area lights inside an instance are not supported")
     # instanced GeometricPrimitives: a one-primitive BLAS each
     gp_inst, gp_index = [], {}
     for p in top:
@@ -351,6 +346,8 @@ def flatten_scene(scene: Scene) -> FlatScene:
     prims["light"] = -1
     prims["medium"] = -1
     light_slot: Dict[int, int] = {}
+    light_instance: Dict[int, int] = {}  # id(TransformedLight) -> instance index
+    inner_area_lights = []               # AreaLights inside instances (hit identity)
     tlas_lights = []
     top_media = []  # (slot, medium object) of top-level primitives
     # BLAS slot ranges
@@ -377,6 +374,25 @@ def flatten_scene(scene: Scene) -> FlatScene:
             rec["kind"] = N.PT_PRIM_INSTANCE
             rec["index"] = len(instances)
             rec["material"] = -1
+            # TransformedPrimitive::GetLights: the inner primitive's lights
+            # (a Model's in BLAS leaf order) wrapped (Primitive.cpp:66-73)
+            inner_lights = []
+            if isinstance(m, Model) and m.tri_lights:
+                kb = model_index[id(m)]
+                order = model_blas[kb][2]
+                emissive = np.zeros(m.triangle_count(), dtype=bool)
+                emissive[np.fromiter(m.tri_lights.keys(), dtype=np.int64)] = True
+                inner_lights = [(m.tri_lights[int(order[j])], blas_base[kb] + int(j))
+                                for j in np.nonzero(emissive[order])[0]]
+            elif isinstance(m, GeometricPrimitive) and m.areaLight is not None:
+                inner_lights = [(m.areaLight, blas_base[len(model_blas) + gp_index[id(m)]])]
+            for al, bslot in inner_lights:
+                tl = TransformedLight(al, p)
+                light_slot[id(tl)] = bslot
+                light_instance[id(tl)] = len(instances)
+                light_slot[id(al)] = bslot
+                inner_area_lights.append(al)
+                tlas_lights.append(tl)
             instances.append(ins)
             continue
         if isinstance(p, Model):
@@ -466,6 +482,8 @@ def flatten_scene(scene: Scene) -> FlatScene:
         texture_ids=dict(reg.tex_ids))
     flat._reg = reg
     flat.instances = _stack(instances, N.INSTANCE)
+    flat.light_instance = light_instance
+    flat.inner_area_lights = inner_area_lights
     # media: the scene's first, then primitives in slot order, then meshes
     flat.scene_medium = flat.medium_id(scene.GetMedium())
     for slot, md in top_media:
@@ -483,21 +501,34 @@ def bind_lights(flat: FlatScene, scene: Scene, sampler: Optional[LightSampler]):
     power/pmf as the sampler's PreProcess left them (LightSampler.cpp)."""
     reg = flat._reg
     lights = list(flat.tlas_lights) + list(scene.infiniteLights)
+    seen = {id(l) for l in lights}
     if sampler is not None:
-        seen = {id(l) for l in lights}
         for l in sampler.all_lights:
             if id(l) not in seen:
                 lights.append(l)
                 seen.add(id(l))
+    # the inner AreaLight of an emitter inside an instance: what a path that
+    # hits it sees (interaction.AreaLight, Primitive.cpp:58), not in the sampler
+    for l in getattr(flat, "inner_area_lights", []):
+        if id(l) not in seen:
+            lights.append(l)
+            seen.add(id(l))
     idx = {id(l): i for i, l in enumerate(lights)}
     table = np.zeros(len(lights), dtype=N.LIGHT)
     table["prim"] = -1
     table["tex"] = -1
+    table["instance"] = -1
     for i, l in enumerate(lights):
         r = table[i]
         r["power"] = l.Power()
         r["pmf"] = sampler.PMF(l) if sampler is not None else 0.0
-        if isinstance(l, AreaLight):
+        if isinstance(l, TransformedLight):
+            r["kind"] = N.PT_LIGHT_AREA
+            r["prim"] = flat.light_slot[id(l)]
+            r["tex"] = reg.texture(l.light.emissiveTexture)
+            r["one_sided"] = 1 if l.light.oneSided else 0
+            r["instance"] = flat.light_instance[id(l)]
+        elif isinstance(l, AreaLight):
             r["kind"] = N.PT_LIGHT_AREA
             r["prim"] = flat.light_slot[id(l)]
             r["tex"] = reg.texture(l.emissiveTexture)

@@ -523,6 +523,37 @@ class PointLight(Light):
         return float(f32(f32(f32(c[0] + c[1]) + c[2]) * f32(4.0 * self.sceneRadius)))
 
 
+class TransformedLight(Light):
+    """TransformedLight / AnimatedLight (Light.cpp:300-364): what
+    TransformedPrimitive::GetLights / AnimatedPrimitive::GetLights
+    (Primitive.cpp:66-73, 91-96) hand the light sampler for an emitter inside
+    an instance.  The inner AreaLight keeps its object-space shape; sample()
+    moves the point by the instance transform and the normal by its normal
+    matrix, PDF() takes point, normal and ray back to object space, L() sees
+    a fresh interaction (normal matrix applied, uv = (0, 0)).  Power() is the
+    inner power times det(transform) (TransformedLight) or the inner power
+    (AnimatedLight).  A path that hits the emitter sees the inner AreaLight
+    itself (Primitive.cpp:58)."""
+
+    def __init__(self, light: "AreaLight", instance: "TransformedPrimitive"):
+        self.light = light
+        self.instance = instance
+        self.animated = isinstance(instance, AnimatedPrimitive)
+
+    def isDelta(self) -> bool:
+        return self.light.isDelta()
+
+    def PreProcess(self, bbox):
+        self.light.PreProcess(bbox)
+
+    def Power(self) -> float:
+        if self.animated:
+            return self.light.Power()
+        # glm::determinant(mat4) in float; evaluated in double and rounded
+        # (a last-bit difference only moves the PMF by an ulp)
+        return float(f32(f32(self.light.Power()) * f32(np.linalg.det(self.instance.transform.astype(np.float64)))))
+
+
 # --------------------------------------------------------------------------
 # Light samplers (LightSampler.cpp)
 # --------------------------------------------------------------------------

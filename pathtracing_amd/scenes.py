@@ -194,6 +194,49 @@ def cornell(W: int = 1024, H: int = 1024, spp: int = 256, config: str = "c2", ma
     return SceneSetup(scene, camera, kind, ls, max_depth, seed, spp, extra).finish()
 
 
+def lit_instances(W: int = 1024, H: int = 1024, spp: int = 256, max_depth: int = 8,
+                  seed: int = 0x5EED0061) -> SceneSetup:
+    """Emitters inside instances (§8f f2): an emissive lamp Model (a box mesh,
+    one AreaLight per triangle) at the top level and instanced twice under
+    rotate / non-uniform scale / translate (TransformedLight: Power x det),
+    an instanced one-sided quad light and an AnimatedPrimitive emissive sphere
+    (AnimatedLight), in the C2 room under its ceiling light;
+    PathIntegrator, PowerLightSampler (Light.cpp:300-364, Primitive.cpp:66-96)."""
+    from .scene import (AnimatedPrimitive, TransformedPrimitive, mat4_identity, mat4_rotate, mat4_scale,
+                        mat4_translate)
+    scene = Scene()
+    white = MicrofacetDiffuse((0.73, 0.73, 0.73))
+    red = MicrofacetDiffuse((0.65, 0.05, 0.05))
+    green = MicrofacetDiffuse((0.12, 0.45, 0.15))
+    walls = [
+        (_quad_tris((-1, -1, 1), (1, -1, 1), (1, -1, -1), (-1, -1, -1)), white),
+        (_quad_tris((-1, 1, -1), (1, 1, -1), (1, 1, 1), (-1, 1, 1)), white),
+        (_quad_tris((-1, -1, -1), (1, -1, -1), (1, 1, -1), (-1, 1, -1)), white),
+        (_quad_tris((-1, -1, 1), (-1, -1, -1), (-1, 1, -1), (-1, 1, 1)), red),
+        (_quad_tris((1, -1, -1), (1, -1, 1), (1, 1, 1), (1, 1, -1)), green),
+    ]
+    scene.Add(Model([Mesh(i, v, None, n, uv, m) for (i, v, n, uv), m in walls]))
+    light = AreaLight(QuadShape((-0.25, 0.999, -0.25), (0.5, 0, 0), (0, 0, 0.5)), (6.0, 5.0, 4.0), False)
+    scene.Add(GeometricPrimitive(light.getShape(), MicrofacetDiffuse((0.78, 0.78, 0.78)), light))
+    bi, bv, bn, buv = _box((0, 0, 0), (0.16, 0.1, 0.16), 0.2)
+    lamp = Model([Mesh(bi, bv, None, bn, buv, MicrofacetDiffuse((0.8, 0.8, 0.8)), SolidColor((3.0, 2.2, 1.2)))])
+    scene.Add(lamp)  # top level: its AreaLights directly
+    for pos, ang, ax, sc in [((-0.55, -0.7, -0.2), 0.7, (0, 1, 0), (1.5, 0.8, 1.2)),
+                             ((0.5, 0.45, -0.45), -1.1, (1, 0, 1), (0.9, 1.6, 0.9))]:
+        m = mat4_scale(mat4_rotate(mat4_translate(mat4_identity(), pos), ang, ax), sc)
+        scene.Add(TransformedPrimitive(lamp, m))
+    ql = AreaLight(QuadShape((-0.5, 0, -0.5), (1, 0, 0), (0, 0, 1)), (2.0, 3.0, 4.0), True)
+    panel = GeometricPrimitive(ql.getShape(), MicrofacetDiffuse((0.5, 0.5, 0.5)), ql)
+    scene.Add(TransformedPrimitive(panel, mat4_rotate(mat4_scale(mat4_translate(mat4_identity(), (0.6, -0.3, 0.3)),
+                                                                  (0.3, 1, 0.2)), 2.0, (1, 0, 0.2))))
+    sl = AreaLight(SphereShape((-0.3, -0.8, 0.5), 0.1), (5.0, 1.5, 1.0), False)
+    scene.Add(AnimatedPrimitive(GeometricPrimitive(sl.getShape(), MicrofacetDiffuse((0.9, 0.9, 0.9)), sl),
+                                (0.3, 0.2, 0), (0.25, 1.0)))
+    film = Film((W, H), MitchellFilter())
+    camera = Camera((0, 0, 3.7), (0, 0, 0), 0.75, film)
+    return SceneSetup(scene, camera, "path", PowerLightSampler(), max_depth, seed, spp).finish()
+
+
 def blend_box(W: int = 64, H: int = 64, spp: int = 16, max_depth: int = 8, alpha: float = 0.35,
               seed: int = 0x5EED0041) -> SceneSetup:
     """C3 Cornell box behind a see-through panel: a two-triangle mesh with a

@@ -47,6 +47,9 @@ def parity_scenes():
                                                filt=GaussianFilter((1.5, 1.5), 0.5), lens=(0.3, 1.2)),
         "mitchell2": lambda: scenes.cornell(W=32, H=32, spp=4, config="c3", seed=0x5EED0033,
                                             filt=MitchellFilter((2.0, 2.0))),
+        # emitters inside instances: TransformedLight / AnimatedLight
+        # (Light.cpp:300-364) for an emissive Model, a quad and a sphere light
+        "lit_instances": lambda: scenes.lit_instances(W=32, H=32, spp=4),
     }
 
 

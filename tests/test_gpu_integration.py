@@ -29,7 +29,7 @@ DROPIN_FILM_MIN = {"sanmiguel": 0.99}
 
 @pytest.mark.skipif(not HARNESS.exists(), reason="hip_harness not built (needs /root/reference at build time)")
 @pytest.mark.parametrize("name", ["example1", "cornell_c2", "cornell_c3", "zoo", "heightfield", "sanmiguel",
-                                  "example1_volpath", "fog", "instances"])
+                                  "example1_volpath", "fog", "instances", "lit_instances"])
 def test_drop_in_integrator_matches_reference_film(name, tmp_path):
     setup = parity_scenes()[name]()
     recipe = write_recipe(tmp_path, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
@@ -59,7 +59,8 @@ def test_drop_in_integrator_matches_reference_film(name, tmp_path):
 
 
 @pytest.mark.skipif(not HARNESS.exists(), reason="hip_harness not built (needs /root/reference at build time)")
-@pytest.mark.parametrize("name", ["example1", "cornell_c3", "zoo", "fog", "instances", "sanmiguel", "lens_box"])
+@pytest.mark.parametrize("name", ["example1", "cornell_c3", "zoo", "fog", "instances", "sanmiguel", "lens_box",
+                                  "lit_instances"])
 def test_drop_in_adaptive_render_matches_reference_render(name, tmp_path):
     """The drop-in's default Render (adaptive, like TileIntegrator::Render)
     against the reference's own adaptive Render of the same objects in the

@@ -320,6 +320,7 @@ def test_gpu_light_samples_match_oracle_and_reference(case):
         keep = sel < g.shape[0]
         g, r = g[sel[keep]], r[keep]
     else:
+        g = g[:r.shape[0]]  # inner lights of instances (hit identity only) are not Light::sample'd
         r = r[:g.shape[0]]
     close = np.isclose(g.reshape(-1, 18), r.reshape(-1, 18), rtol=1e-4, atol=1e-5, equal_nan=True).all(1)
     assert close.mean() >= 0.99
