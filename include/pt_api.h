@@ -130,10 +130,13 @@ typedef struct pt_texture {
     int32_t image;       /* IMAGE: image id                                */
 } pt_texture;
 
+enum { PT_IMAGE_U8 = 0, PT_IMAGE_F32 = 1 };
 typedef struct pt_image {
     uint64_t offset;     /* byte offset into pt_scene_desc.texels          */
     int32_t width, height, channels;
-    int32_t pad;
+    int32_t format;      /* PT_IMAGE_U8 (Image: byte / 255) or PT_IMAGE_F32
+                          * (FloatImage, Texture.hpp:70-103: float texels,
+                          * offset 4-byte aligned)                          */
 } pt_image;
 
 enum { PT_MAT_DIFFUSE = 0, PT_MAT_DIELECTRIC = 1, PT_MAT_THIN = 2, PT_MAT_CONDUCTOR = 3 };
@@ -149,7 +152,11 @@ typedef struct pt_material {
     float albedo[3];     /* CONDUCTOR                                       */
 } pt_material;
 
-enum { PT_LIGHT_AREA = 0, PT_LIGHT_UNIFORM_INF = 1, PT_LIGHT_SKY_INF = 2, PT_LIGHT_DISTANT = 3, PT_LIGHT_POINT = 4 };
+enum { PT_LIGHT_AREA = 0, PT_LIGHT_UNIFORM_INF = 1, PT_LIGHT_SKY_INF = 2, PT_LIGHT_DISTANT = 3, PT_LIGHT_POINT = 4,
+       PT_LIGHT_TEX_INF = 5 };
+/* TextureInfiniteLight's cell grid (Light.hpp:120-122): xSamples x ySamples */
+#define PT_TEXINF_X 1920
+#define PT_TEXINF_Y 1080
 /* AreaLight / UniformInfiniteLight / FunctionInfiniteLight (sky gradient of
  * main.cpp:292-295, parameterised) / DistantLight / PointLight (Light.cpp). */
 typedef struct pt_light {
@@ -166,6 +173,9 @@ typedef struct pt_light {
                           * the shape (TransformedLight / AnimatedLight,
                           * Light.cpp:300-364; prim is then the BLAS slot)  */
 } pt_light;
+/* TEX_INF (TextureInfiniteLight, Light.cpp:110-200): tex = its texture,
+ * scale = LeScale, prim = offset of its PT_TEXINF_X*PT_TEXINF_Y running sums
+ * (accWeights, float, std::partial_sum order) in pt_scene_desc.light_dist. */
 
 enum { PT_LS_UNIFORM = 0, PT_LS_POWER = 1 };
 
@@ -215,6 +225,8 @@ typedef struct pt_scene_desc {
     uint32_t n_sampler_lights;
     const uint32_t* infinite_lights; /* Scene::infiniteLights, in order         */
     uint32_t n_infinite_lights;
+    const float* light_dist;         /* TEX_INF lights' cell running sums       */
+    uint64_t n_light_dist;
     /* participating media (VolPath): pt_prim.medium and the ids below index it */
     const pt_medium* media;
     uint32_t n_media;
@@ -348,6 +360,15 @@ pt_status pt_light_cases(pt_ctx* ctx, const float* cases, uint32_t n, float* out
 enum { PT_TONEMAP_REINHARD_JODIE = 0, PT_TONEMAP_ACES = 1 };
 pt_status pt_film_resolve(pt_ctx* ctx, const double* film_accum, int32_t width, int32_t height, uint32_t tonemap,
                           uint8_t* rgb_out);
+/* TextureInfiniteLight::PreProcess's cell weights (Light.cpp:150-196) for a
+ * FloatImageTexture environment (float texels, w x h x channels, row 0
+ * first, colorScale), LeScale le_scale: per cell k of the 1920 x 1080 grid
+ * (the reference's indexing: x = k % 1080, y = k / 1080) the mean luminance
+ * of Le over 8 x 8 jittered strata, jitter from a fixed counter-based hash
+ * (the reference's StratifiedSampler jitter is unseeded).  Host code, up to
+ * `threads` threads; weights: PT_TEXINF_X*PT_TEXINF_Y floats. */
+pt_status pt_texinf_weights(const float* texels, int32_t width, int32_t height, int32_t channels,
+                            const float color_scale[3], float le_scale, float* weights, int32_t threads);
 /* Device bytes held by the uploaded scene. */
 uint64_t pt_scene_device_bytes(const pt_ctx* ctx);
 

@@ -41,6 +41,8 @@ def lib():
         L.oracle_li.argtypes = [vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp, C.POINTER(Counters)]
         L.oracle_render.argtypes = [vp, vp, vp, vp, C.c_int, C.POINTER(Counters)]
         L.oracle_render_adaptive.argtypes = [vp, vp, vp, vp, vp, C.c_int, C.POINTER(Counters)]
+        L.oracle_inf_le.argtypes = [vp, C.c_int, vp, C.c_uint32, vp]
+        L.oracle_texinf_weights.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp, C.c_float, vp, C.c_uint32, vp]
         L.oracle_bsdf.argtypes = [vp, C.c_int, vp, C.c_uint32, vp]
         L.oracle_lights.argtypes = [vp, vp, C.c_uint32, vp]
         L.oracle_filter_table.argtypes = [vp, vp]
@@ -105,6 +107,25 @@ def render_adaptive(integrator, threads: int = 1, shard_index: int = 0, shard_co
     assert lib().oracle_render_adaptive(_desc(integrator.flat), C.byref(cam), C.byref(rd), film.ctypes.data,
                                         counts.ctypes.data, int(threads), C.byref(cnt)) == 0
     return film, counts, cnt.as_dict()
+
+
+def inf_le(flat, light: int, dirs: np.ndarray) -> np.ndarray:
+    """(n, 4) {Le rgb, PDF({}, dir)} of infinite light `light` for directions."""
+    dirs = np.ascontiguousarray(dirs, np.float32)
+    out = np.zeros((dirs.shape[0], 4), np.float32)
+    assert lib().oracle_inf_le(_desc(flat), int(light), dirs.ctypes.data, dirs.shape[0], out.ctypes.data) == 0
+    return out
+
+
+def texinf_weights(texels: np.ndarray, color_scale, scale: float, cells: np.ndarray) -> np.ndarray:
+    t = np.ascontiguousarray(texels, np.float32)
+    h, w, c = t.shape
+    cs = np.ascontiguousarray(color_scale, np.float32)
+    cells = np.ascontiguousarray(cells, np.uint32)
+    out = np.zeros(cells.shape[0], np.float32)
+    assert lib().oracle_texinf_weights(t.ctypes.data, w, h, c, cs.ctypes.data, float(scale), cells.ctypes.data,
+                                       cells.shape[0], out.ctypes.data) == 0
+    return out
 
 
 def bsdf(flat, material: int, cases: np.ndarray) -> np.ndarray:

@@ -191,6 +191,13 @@ static inline float channel_at(const scene_t* S, const pt_image* im, int x, int 
     int xi = wrap_index(x, im->width), yi = wrap_index(y, im->height);
     uint64_t idx = im->offset + ((uint64_t)yi * (uint64_t)im->width + (uint64_t)xi) * (uint64_t)im->channels +
                    (uint64_t)(ch - 1);
+    if (im->format == PT_IMAGE_F32) { /* FloatImage::GetChannelAt (Texture.hpp:78-83) */
+        uint64_t fi = im->offset + 4ull * (idx - im->offset);
+        if (fi + 4 > S->s->n_texel_bytes) return 0.0f;
+        float f;
+        memcpy(&f, S->s->texels + fi, 4);
+        return f;
+    }
     if (idx >= S->s->n_texel_bytes) return 0.0f;
     return S->s->texels[idx] / 255.0f;
 }
@@ -1132,16 +1139,61 @@ static v3 sky_le(const pt_light* l, v3 d) {
     return smul(l->scale, V(fmaf(a, l->vec[0], rmul(b, l->color[0])), fmaf(a, l->vec[1], rmul(b, l->color[1])),
                             fmaf(a, l->vec[2], rmul(b, l->color[2]))));
 }
-static v3 inf_le(const pt_light* l, v3 d) { return l->kind == PT_LIGHT_SKY_INF ? sky_le(l, d) : vl(l->color); }
+/* TextureInfiniteLight (Light.cpp:110-150): Le = LeScale * tex(GetSphereUV(dir)) */
+static v3 texinf_le(const scene_t* S, const pt_light* l, v3 d) {
+    float uv[2];
+    sphere_uv(d, uv);
+    return smul(l->scale, tex_eval(S, l->tex, uv));
+}
+static v3 inf_le_s(const scene_t* S, const pt_light* l, v3 d) {
+    if (l->kind == PT_LIGHT_TEX_INF) return texinf_le(S, l, d);
+    return l->kind == PT_LIGHT_SKY_INF ? sky_le(l, d) : vl(l->color);
+}
+#define inf_le(l, d) inf_le_s(S, l, d)
+static float texinf_pdf(const scene_t* S, const pt_light* l, v3 rd) {
+    v3 le = texinf_le(S, l, rd);
+    double lum = fma((double)le.z, 0.0722, fma((double)le.y, 0.7152, (double)le.x * 0.2126));
+    double tot = (double)S->s->light_dist[(size_t)l->prim + (size_t)PT_TEXINF_X * PT_TEXINF_Y - 1];
+    const float cell_omega = 4.0f * PI_F / (float)(PT_TEXINF_X * PT_TEXINF_Y);
+    return (float)((lum / tot) * (double)(1.0f / cell_omega));
+}
+/* Light::PDF({}, ray) of an infinite light */
+static float inf_pdf(const scene_t* S, const pt_light* l, v3 rd) {
+    return l->kind == PT_LIGHT_TEX_INF ? texinf_pdf(S, l, rd) : 1.0f / (4.0f * PI_F);
+}
+/* the hidden random_float() of TextureInfiniteLight::sample (Light.cpp:120),
+ * drawn outside the stream's numbered dimensions (pt_shading.h texinf_uc) */
+static float texinf_uc(const rng_t* r) {
+    return (float)(pcg_hash((r->key ^ 0xC3115EEDu) + 0x9E3779B9u * r->dim) >> 8) * (1.0f / 16777216.0f);
+}
 
 /* TransformedLight / AnimatedLight (Light.cpp:300-364): the inner
  * AreaLight's shape in the instance's object space */
 static const pt_instance* light_instance(const scene_t* S, const pt_light* l) {
     return (l->kind == PT_LIGHT_AREA && l->instance >= 0) ? &S->s->instances[l->instance] : NULL;
 }
-static lsample_t light_sample(const scene_t* S, const pt_light* l, float u0, float u1) {
+static lsample_t light_sample(const scene_t* S, const pt_light* l, float u0, float u1, float uc) {
     lsample_t ls;
     memset(&ls, 0, sizeof(ls));
+    if (l->kind == PT_LIGHT_TEX_INF) { /* TextureInfiniteLight::sample (Light.cpp:118-144) */
+        const float* acc = S->s->light_dist + l->prim;
+        const uint32_t N = (uint32_t)PT_TEXINF_X * PT_TEXINF_Y;
+        double weight = (double)uc * (double)acc[N - 1];
+        uint32_t i = 0, hi = N; /* std::upper_bound: first running sum > weight */
+        while (i < hi) {
+            uint32_t mid = (i + hi) >> 1;
+            if ((double)acc[mid] > weight) hi = mid;
+            else i = mid + 1;
+        }
+        int cx = (int)(i % PT_TEXINF_Y), cy = (int)(i / PT_TEXINF_Y);
+        float cu = ((float)cx + u0) / (float)PT_TEXINF_X, cv = ((float)cy + u1) / (float)PT_TEXINF_Y;
+        float z = 2.0f * cu - 1.0f;
+        float th = 2.0f * PI_F * cv;
+        float r = sqrtf(1.0f - rmul(z, z));
+        ls.dir = V(r * cosf(th), r * sinf(th), z);
+        sphere_uv(ls.dir, ls.si.uv);
+        return ls;
+    }
     if (l->kind == PT_LIGHT_AREA) {
         ls.si = shape_sample(S, &S->s->prims[l->prim], u0, u1);
         const pt_instance* I = light_instance(S, l);
@@ -1197,6 +1249,7 @@ static float light_pdf(const scene_t* S, const pt_light* l, const si_t* si, cons
         return shape_pdf(S, p, si, r);
     }
     if (l->kind == PT_LIGHT_UNIFORM_INF || l->kind == PT_LIGHT_SKY_INF) return 1.0f / (4.0f * PI_F);
+    if (l->kind == PT_LIGHT_TEX_INF) return texinf_pdf(S, l, r->d);
     return 0;
 }
 static v3 light_L(const scene_t* S, const pt_light* l, const si_t* si, const ray_t* r) {
@@ -1213,7 +1266,8 @@ static v3 light_L(const scene_t* S, const pt_light* l, const si_t* si, const ray
         if (l->one_sided && dot(r->d, si->n) > 0) return V(0, 0, 0);
         return tex_eval(S, l->tex, si->uv);
     }
-    if (l->kind == PT_LIGHT_UNIFORM_INF || l->kind == PT_LIGHT_SKY_INF) return inf_le(l, r->d);
+    if (l->kind == PT_LIGHT_UNIFORM_INF || l->kind == PT_LIGHT_SKY_INF || l->kind == PT_LIGHT_TEX_INF)
+        return inf_le(l, r->d);
     return V(0, 0, 0);
 }
 
@@ -1246,12 +1300,12 @@ typedef struct {
 } integ_t;
 
 /* PathIntegrator::SampleLd (Integrators.cpp:260-294) */
-static v3 sample_ld(const integ_t* I, const ray_t* ray, const si_t* si, float u, float uv0, float uv1) {
+static v3 sample_ld(const integ_t* I, const ray_t* ray, const si_t* si, float u, float uv0, float uv1, float uc) {
     const scene_t* S = I->S;
     int li = ls_sample(S, u);
     if (li < 0) return V(0, 0, 0);
     const pt_light* l = &S->s->lights[li];
-    lsample_t ls = light_sample(S, l, uv0, uv1);
+    lsample_t ls = light_sample(S, l, uv0, uv1, uc);
     v3 ldir;
     float t;
     if (is_zero(ls.si.n)) {
@@ -1322,7 +1376,7 @@ static v3 li_path(const integ_t* I, ray_t ray, rng_t* rng) {
                 if (spec) {
                     out = add(out, mul(att, inf_le(l, ray.d)));
                 } else if (prev > 0) {
-                    float lp = l->pmf * (1.0f / (4.0f * PI_F));
+                    float lp = l->pmf * inf_pdf(S, l, ray.d);
                     float w = prev * prev / (prev * prev + lp * lp);
                     out = add(out, muls(mul(att, inf_le(l, ray.d)), w));
                 }
@@ -1357,7 +1411,7 @@ static v3 li_path(const integ_t* I, ray_t ray, rng_t* rng) {
         ray_t nr = mkray(b.o, b.d);
         spec = (b.flags & FL_SPEC) != 0;
         if (!spec) {
-            v3 ld = sample_ld(I, &ray, &si, r[5], r[2], r[3]);
+            v3 ld = sample_ld(I, &ray, &si, r[5], r[2], r[3], texinf_uc(rng));
             DBG("O  ld %a %a %a (light %d)\n", ld.x, ld.y, ld.z, ls_sample(S, r[5]));
             out = add(out, mul(att, ld));
             prev = mat_pdf(S, si.mat, &ray, &si, nr.d);
@@ -1490,12 +1544,12 @@ static int intersect_tr(const integ_t* I, ray_t ray, int med, float max, v3* Tr)
 /* VolPathIntegrator::SampleLd (Integrators.cpp:416-479); phase_g >= -1 marks a
  * medium interaction (p = si->p, f = phase pdf) */
 static v3 sample_ld_vol(const integ_t* I, const ray_t* ray, int ray_med, const si_t* si, int medium_it, float g,
-                        float u, float uv0, float uv1) {
+                        float u, float uv0, float uv1, float uc) {
     const scene_t* S = I->S;
     int li = ls_sample(S, u);
     if (li < 0) return V(0, 0, 0);
     const pt_light* l = &S->s->lights[li];
-    lsample_t ls = light_sample(S, l, uv0, uv1);
+    lsample_t ls = light_sample(S, l, uv0, uv1, uc);
     v3 ldir;
     float t;
     if (is_zero(ls.si.n)) {
@@ -1548,7 +1602,7 @@ static v3 li_volpath(const integ_t* I, ray_t ray, int med, rng_t* rng) {
                 if (spec) {
                     out = add(out, mul(att, inf_le(l, ray.d)));
                 } else if (prev > 0) {
-                    float lp = l->pmf * (1.0f / (4.0f * PI_F));
+                    float lp = l->pmf * inf_pdf(S, l, ray.d);
                     float w = prev * prev / (prev * prev + lp * lp);
                     out = add(out, muls(mul(att, inf_le(l, ray.d)), w));
                 }
@@ -1569,7 +1623,7 @@ static v3 li_volpath(const integ_t* I, ray_t ray, int med, rng_t* rng) {
             si_t mi;
             memset(&mi, 0, sizeof(mi));
             mi.p = mp;
-            out = add(out, mul(att, sample_ld_vol(I, &ray, med, &mi, 1, M->g, r[5], r[2], r[3])));
+            out = add(out, mul(att, sample_ld_vol(I, &ray, med, &mi, 1, M->g, r[5], r[2], r[3], texinf_uc(rng))));
             out = add(out, mul(att, vl(M->Le)));
             v3 sc = phase_sample(M->g, ray.d, r[6], r[7]);
             int nm = get_medium(&si, sc);
@@ -1603,7 +1657,7 @@ static v3 li_volpath(const integ_t* I, ray_t ray, int med, rng_t* rng) {
             if (!(b.flags & FL_TRANS) && dot(ray.d, si.ns) <= 0) nm = med;
             spec = (b.flags & FL_SPEC) != 0;
             if (!spec) {
-                out = add(out, mul(att, sample_ld_vol(I, &ray, med, &si, 0, 0.0f, r[5], r[2], r[3])));
+                out = add(out, mul(att, sample_ld_vol(I, &ray, med, &si, 0, 0.0f, r[5], r[2], r[3], texinf_uc(rng))));
                 prev = mat_pdf(S, si.mat, &ray, &si, nr.d);
             }
             att = mul(att, divs(muls(b.f, fabsf(dot(si.ns, nr.d))), b.pdf));
@@ -2022,7 +2076,12 @@ int oracle_lights(const pt_scene_desc* s, const float* in, uint32_t n, float* ou
             const float* c = in + 5 * (size_t)i;
             float* o = out + 18 * k;
             memset(o, 0, 18 * sizeof(float));
-            lsample_t ls = light_sample(&S, l, c[0], c[1]);
+            /* a TextureInfiniteLight's hidden cell draw: a hash of the case (k_light_cases) */
+            uint32_t h0, h1;
+            memcpy(&h0, &c[0], 4);
+            memcpy(&h1, &c[1], 4);
+            const float uc = (float)(pcg_hash(pcg_hash(h0 ^ pcg_hash(h1))) >> 8) * (1.0f / 16777216.0f);
+            lsample_t ls = light_sample(&S, l, c[0], c[1], uc);
             o[0] = ls.L.x; o[1] = ls.L.y; o[2] = ls.L.z;
             o[3] = ls.si.p.x; o[4] = ls.si.p.y; o[5] = ls.si.p.z;
             o[6] = ls.si.n.x; o[7] = ls.si.n.y; o[8] = ls.si.n.z;
@@ -2036,6 +2095,70 @@ int oracle_lights(const pt_scene_desc* s, const float* in, uint32_t n, float* ou
                 o[15] = L.x; o[16] = L.y; o[17] = L.z;
             }
         }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ TextureInfiniteLight checks */
+/* Le(dir) and PDF({}, dir) of light `li` for n directions -> out[4n] */
+int oracle_inf_le(const pt_scene_desc* s, int li, const float* dirs, uint32_t n, float* out) {
+    scene_t Sc;
+    scene_init(&Sc, s);
+    const scene_t* S = &Sc;
+    const pt_light* l = &s->lights[li];
+    for (uint32_t i = 0; i < n; i++) {
+        v3 d = V(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2]);
+        v3 le = inf_le(l, d);
+        out[4 * i] = le.x;
+        out[4 * i + 1] = le.y;
+        out[4 * i + 2] = le.z;
+        out[4 * i + 3] = inf_pdf(S, l, d);
+    }
+    return 0;
+}
+
+/* TextureInfiniteLight::PreProcess's weight of cells k (Light.cpp:163-186),
+ * restated independently of pt_envmap.cpp: a FloatImageTexture sky, the
+ * jitter of the fixed hash (seed 0x7E1F5EED) */
+static float envtex(const float* tx, int w, int h, int c, int x, int y, int ch) {
+    int xi = x % w, yi = y % h;
+    if (xi < 0) xi += w;
+    if (yi < 0) yi += h;
+    return tx[((size_t)yi * w + xi) * c + ch];
+}
+int oracle_texinf_weights(const float* tx, int w, int h, int c, const float cs[3], float scale, const uint32_t* cells,
+                          uint32_t n, float* out) {
+    for (uint32_t i = 0; i < n; i++) {
+        uint32_t k = cells[i];
+        int x = (int)(k % PT_TEXINF_Y), y = (int)(k / PT_TEXINF_Y);
+        uint32_t key = pcg_hash(pcg_hash(0x7E1F5EEDu ^ pcg_hash(k)) + 0u);
+        double temp = 0;
+        for (int sp = 0; sp < 64; sp++) {
+            int sx = sp % 8, sy = sp / 8;
+            double jx = (double)((float)(pcg_hash(key + 0x9E3779B9u * (uint32_t)(2 * sp)) >> 8) * (1.0f / 16777216.0f));
+            double jy = (double)((float)(pcg_hash(key + 0x9E3779B9u * (uint32_t)(2 * sp + 1)) >> 8) * (1.0f / 16777216.0f));
+            float UVx = (float)((sx + jx) / 8.0), UVy = (float)((sy + jy) / 8.0);
+            float u = ((float)x + UVx) / (float)PT_TEXINF_X, v = ((float)y + UVy) / (float)PT_TEXINF_Y;
+            float z = 2.0f * u - 1.0f;
+            float th = 2.0f * PI_F * v;
+            float r = sqrtf(1.0f - rmul(z, z));
+            v3 d = V(r * cosf(th), r * sinf(th), z);
+            float uv[2];
+            sphere_uv(d, uv);
+            float fx = uv[0] * w - 0.5f, fy = uv[1] * h - 0.5f;
+            int xi = (int)floorf(fx), yi = (int)floorf(fy);
+            float dx = fx - xi, dy = fy - yi;
+            float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
+            float L[3];
+            for (int ch = 0; ch < 3; ch++) {
+                float rr = fmaf(wd, envtex(tx, w, h, c, xi + 1, yi + 1, ch),
+                                fmaf(wc, envtex(tx, w, h, c, xi, yi + 1, ch),
+                                     fmaf(wb, envtex(tx, w, h, c, xi + 1, yi, ch), rmul(wa, envtex(tx, w, h, c, xi, yi, ch)))));
+                L[ch] = scale * rmul(cs[ch], rr);
+            }
+            temp += fma((double)L[2], 0.0722, fma((double)L[1], 0.7152, (double)L[0] * 0.2126));
+        }
+        out[i] = (float)(temp / 64);
     }
     return 0;
 }

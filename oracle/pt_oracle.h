@@ -45,6 +45,11 @@ int oracle_render(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_re
                   int threads, oracle_counters* cnt);
 /* TileIntegrator::Render's adaptive sampling (Integrators.cpp:55-86): the
  * film plus each pixel's sample count (W*H u32).  Shards own 32x32 tiles. */
+/* TextureInfiniteLight: Le / PDF of light li for directions (out[4n]); the
+ * cell weights of pt_texinf_weights for a list of cells */
+int oracle_inf_le(const pt_scene_desc* s, int li, const float* dirs, uint32_t n, float* out);
+int oracle_texinf_weights(const float* tx, int w, int h, int c, const float cs[3], float scale, const uint32_t* cells,
+                          uint32_t n, float* out);
 int oracle_render_adaptive(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render_desc* rd,
                            double* film_accum, uint32_t* counts, int threads, oracle_counters* cnt);
 

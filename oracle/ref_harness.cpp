@@ -266,6 +266,9 @@ static void read_recipe(World& w, const std::string& path) {
             } else if (kind == "checker") {
                 int a, b; float sx, sy, sr, sg, sb; s >> a >> b >> sx >> sy >> sr >> sg >> sb;
                 w.tex[id] = std::make_shared<CheckerTexture>(w.tex.at(a), w.tex.at(b), glm::vec2(sx, sy), glm::vec3(sr, sg, sb));
+            } else if (kind == "floatimage") {
+                std::string rel; float sr, sg, sb; s >> rel >> sr >> sg >> sb;
+                w.tex[id] = std::make_shared<FloatImageTexture>(w.dir + rel, glm::vec3(sr, sg, sb));
             } else if (kind == "image") {
                 std::string rel; int gamma; float sr, sg, sb; s >> rel >> gamma >> sr >> sg >> sb;
                 w.tex[id] = std::make_shared<ImageTexture>(w.dir + rel, gamma != 0, glm::vec3(sr, sg, sb));
@@ -383,6 +386,9 @@ static void read_recipe(World& w, const std::string& path) {
             if (kind == "uniform") {
                 float r, g, b; s >> r >> g >> b;
                 w.inf.push_back(std::make_shared<UniformInfiniteLight>(glm::vec3(r, g, b)));
+            } else if (kind == "texture") {
+                int id; float sc; s >> id >> sc;
+                w.inf.push_back(std::make_shared<TextureInfiniteLight>(w.tex.at(id), sc));
             } else if (kind == "sky") {
                 float c[7]; for (float& x : c) s >> x;
                 glm::vec3 c0(c[0], c[1], c[2]), c1(c[3], c[4], c[5]);
@@ -884,6 +890,23 @@ static void cmd_stats(World& w, const std::string& out, int threads) {
     wr(out + ".stats.bin", res);
 }
 
+// --- envle: an infinite light's Le(dir) and PDF(dir) for [n][3] directions
+// (deterministic given the light's PreProcess), with Power() appended
+static void cmd_envle(World& w, const std::string& out, const std::string& inPath) {
+    auto raw = rd<float>(inPath);
+    size_t n = raw.size() / 3;
+    const auto& l = w.inf.at(0);
+    std::vector<float> res;
+    for (size_t i = 0; i < n; i++) {
+        Ray r(glm::vec3(0), glm::vec3(raw[3 * i], raw[3 * i + 1], raw[3 * i + 2]));
+        glm::vec3 le = l->Le(r);
+        res.push_back(le.x); res.push_back(le.y); res.push_back(le.z);
+        res.push_back(l->PDF(GeometricInteraction{}, r));
+    }
+    res.push_back(l->Power());
+    wr(out + ".envle.bin", res);
+}
+
 // --- tonemap: Film::WritePNG's pixel loop (Film.hpp:183-196) over an
 // accumulation buffer {sum RGB*w, sum w} (W*H*4 doubles): the reference's own
 // reinhard_jodie / ACESFilm and linear_to_sRGB, through the writer's
@@ -969,6 +992,7 @@ int main(int argc, char** argv) {
         cmd_li(w, out, x0, y0, x1, y1, spp);
     } else if (cmd == "film") cmd_film(w, out, w.spp);
     else if (cmd == "adaptive") cmd_adaptive(w, out);
+    else if (cmd == "envle") cmd_envle(w, out, argv[4]);
     else if (cmd == "stats") cmd_stats(w, out, argc > 4 ? atoi(argv[4]) : 8);
     else if (cmd == "bsdf") cmd_bsdf(w, out, argv[4], atoi(argv[5]));
     else if (cmd == "camera") cmd_camera(w, out, argv[4]);

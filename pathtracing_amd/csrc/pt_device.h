@@ -112,6 +112,7 @@ struct DevScene {
     float sampler_total;
     const uint32_t* infinite_lights;
     uint32_t n_infinite_lights;
+    const float* light_dist;  // TEX_INF cell running sums
     const pt_medium* media;
     uint32_t n_media;
     int32_t scene_medium;

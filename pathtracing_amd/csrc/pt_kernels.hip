@@ -426,7 +426,9 @@ __global__ void k_light_cases(const float* __restrict__ in, uint32_t n, float* _
     const float* c = in + 5ull * i;
     float* o = out + 18ull * k;
     for (int j = 0; j < 18; j++) o[j] = 0.0f;
-    const LSample ls = light_sample(l, c[0], c[1]);
+    // a TextureInfiniteLight's hidden cell draw: a hash of the case
+    const float uc = draw(pcg_hash(__float_as_uint(c[0]) ^ pcg_hash(__float_as_uint(c[1]))), 0);
+    const LSample ls = light_sample(l, c[0], c[1], uc);
     o[0] = ls.L.x; o[1] = ls.L.y; o[2] = ls.L.z;
     o[3] = ls.p.x; o[4] = ls.p.y; o[5] = ls.p.z;
     o[6] = ls.n.x; o[7] = ls.n.y; o[8] = ls.n.z;
@@ -602,7 +604,7 @@ __global__ __launch_bounds__(256) PT_SHADE_WAVES void k_shade(RenderParams R, Pa
                 if (INTEGRATOR == PT_INTEGRATOR_SIMPLE || spec) {
                     out = out + att * inf_le(l, rd);
                 } else if (prev > 0) {
-                    float lp = l.pmf * (1.0f / (4.0f * PT_PI));
+                    float lp = l.pmf * inf_pdf(l, rd);
                     float w = prev * prev / (prev * prev + lp * lp);
                     out = out + (att * inf_le(l, rd)) * w;
                 }
@@ -659,7 +661,7 @@ __global__ __launch_bounds__(256) PT_SHADE_WAVES void k_shade(RenderParams R, Pa
                             const int li = ls_sample(r[5]);
                             if (li >= 0) {
                                 const pt_light& l = S.lights[li];
-                                LSample ls = light_sample(l, r[2], r[3]);
+                                LSample ls = light_sample(l, r[2], r[3], texinf_uc(key, dim));
                                 f3 ldir;
                                 float tmax;
                                 if (is_zero(ls.n)) {
@@ -812,7 +814,7 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                 if (spec) {
                     out = out + att * inf_le(l, rd);
                 } else if (prev > 0) {
-                    float lp = l.pmf * (1.0f / (4.0f * PT_PI));
+                    float lp = l.pmf * inf_pdf(l, rd);
                     float w = prev * prev / (prev * prev + lp * lp);
                     out = out + (att * inf_le(l, rd)) * w;
                 }
@@ -868,7 +870,7 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                 const int li = ls_sample(r[5]);
                 if (li >= 0 && S.lights[li].pmf > 0) {
                     const pt_light& l = S.lights[li];
-                    LSample ls = light_sample(l, r[2], r[3]);
+                    LSample ls = light_sample(l, r[2], r[3], texinf_uc(key, dim));
                     f3 ldir;
                     float tmax;
                     if (is_zero(ls.n)) {

@@ -430,6 +430,10 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
             if (s->tri_vidx[3 * t + k] >= s->n_vertices) return fail(c, PT_ERR_ARG, "triangle %u: bad vertex", t);
     for (uint32_t l = 0; l < s->n_lights; l++) {
         const pt_light& L = s->lights[l];
+        if (L.kind == PT_LIGHT_TEX_INF &&
+            (L.prim < 0 || (uint64_t)L.prim + (uint64_t)PT_TEXINF_X * PT_TEXINF_Y > s->n_light_dist || !s->light_dist ||
+             L.tex < 0 || (uint32_t)L.tex >= s->n_textures))
+            return fail(c, PT_ERR_ARG, "light %u: bad texture infinite light", l);
         if (L.kind == PT_LIGHT_AREA && (L.prim < 0 || (uint32_t)L.prim >= s->n_prims || L.tex < 0 ||
                                         (uint32_t)L.tex >= s->n_textures || L.instance < -1 ||
                                         (L.instance >= 0 && (uint32_t)L.instance >= s->n_instances)))
@@ -584,6 +588,7 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
     UP(DS.sampler_lights, s->sampler_lights, s->n_sampler_lights);
     UP(DS.sampler_cdf, cdf.data(), cdf.size());
     UP(DS.infinite_lights, s->infinite_lights, s->n_infinite_lights);
+    UP(DS.light_dist, s->light_dist, s->n_light_dist);
     UP(DS.media, s->media, s->n_media);
     UP(DS.instances, inst.data(), inst.size());
 #undef UP

@@ -23,6 +23,11 @@ __device__ __forceinline__ float channel_at(const pt_image& im, int x, int y, in
     int xi = wrap_index(x, im.width), yi = wrap_index(y, im.height);
     uint64_t idx = im.offset + ((uint64_t)yi * (uint64_t)im.width + (uint64_t)xi) * (uint64_t)im.channels +
                    (uint64_t)(ch - 1);
+    if (im.format == PT_IMAGE_F32) {  // FloatImage::GetChannelAt (Texture.hpp:78-83): floats, no /255
+        const uint64_t fi = im.offset + 4ull * (idx - im.offset);
+        if (fi + 4 > S.n_texel_bytes) return 0.0f;
+        return *reinterpret_cast<const float*>(S.texels + fi);
+    }
     if (idx >= S.n_texel_bytes) return 0.0f;
     return S.texels[idx] / 255.0f;
 }
@@ -692,7 +697,14 @@ __device__ float shape_pdf(uint32_t kind, uint32_t index, f3 p, f3 n, f3 ro, f3 
     }
     return d2 / (lc * area);
 }
+// TextureInfiniteLight::Le (Light.cpp:110-112): LeScale * tex(GetSphereUV(dir))
+__device__ __noinline__ f3 texinf_le(const pt_light& l, f3 d) {
+    float u, v;
+    sphere_uv(d, u, v);
+    return l.scale * tex_eval(l.tex, u, v);
+}
 __device__ __forceinline__ f3 inf_le(const pt_light& l, f3 d) {
+    if (l.kind == PT_LIGHT_TEX_INF) return texinf_le(l, d);
     if (l.kind == PT_LIGHT_SKY_INF) {  // main.cpp:292-295 gradient
         // (1-a)*c0 rounded, a*c1 fused (fixture search)
         float a = 0.5f * (d.y + 1.0f), b = 1.0f - a;
@@ -724,7 +736,48 @@ __device__ __noinline__ f3 tlight_normal(int inst, f3 n) {  // TransformedLight:
     return m3_mul(NM, n);
 }
 
-__device__ LSample light_sample(const pt_light& l, float u0, float u1) {
+// TextureInfiniteLight::sample (Light.cpp:118-144): the cell whose running
+// sum first exceeds uc * totalWeight (std::upper_bound over the float sums,
+// compared in double), then the point (u0, u1) of that cell mapped to the
+// sphere.  uc is the reference's hidden random_float() (Light.cpp:120),
+// drawn from the sample stream by the caller.
+__device__ __noinline__ void texinf_sample(const pt_light& l, float uc, float u0, float u1, LSample& ls) {
+    const float* acc = S.light_dist + l.prim;
+    constexpr uint32_t N = (uint32_t)PT_TEXINF_X * PT_TEXINF_Y;
+    const double weight = (double)uc * (double)acc[N - 1];
+    uint32_t lo = 0, hi = N;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((double)acc[mid] > weight) hi = mid;
+        else lo = mid + 1;
+    }
+    const int cx = (int)(lo % PT_TEXINF_Y), cy = (int)(lo / PT_TEXINF_Y);
+    const float cu = ((float)cx + u0) / (float)PT_TEXINF_X, cv = ((float)cy + u1) / (float)PT_TEXINF_Y;
+    const float z = 2.0f * cu - 1.0f;
+    const float th = 2.0f * PT_PI * cv;
+    const float r = csqrt(1.0f - rmul(z, z));
+    ls.dir = F3(r * cos_cr(th), r * sin_cr(th), z);
+    sphere_uv(ls.dir, ls.u, ls.v);
+}
+// TextureInfiniteLight::PDF (Light.cpp:146-150): luminance(Le) / totalWeight
+// / cellOmega, luminance in double (Util.hpp:4-6)
+__device__ __noinline__ float texinf_pdf(const pt_light& l, f3 rd) {
+    const f3 le = texinf_le(l, rd);
+    const double lum = fma((double)le.z, 0.0722, fma((double)le.y, 0.7152, (double)le.x * 0.2126));
+    const double tot = (double)S.light_dist[l.prim + (uint32_t)PT_TEXINF_X * PT_TEXINF_Y - 1u];
+    constexpr float cell_omega = 4.0f * PT_PI / (float)(PT_TEXINF_X * PT_TEXINF_Y);
+    return (float)((lum / tot) * (double)(1.0f / cell_omega));
+}
+// TextureInfiniteLight::sample's hidden random_float() (Light.cpp:120) as a
+// draw of the sample's stream outside its numbered dimensions: keyed by the
+// stream key and the bounce's next dimension, so every bounce gets its own
+__device__ __forceinline__ float texinf_uc(uint32_t key, uint32_t dim) { return draw(key ^ 0xC3115EEDu, dim); }
+// Light::PDF({}, ray) of an infinite light (the escape MIS weight)
+__device__ __forceinline__ float inf_pdf(const pt_light& l, f3 rd) {
+    return l.kind == PT_LIGHT_TEX_INF ? texinf_pdf(l, rd) : 1.0f / (4.0f * PT_PI);
+}
+
+__device__ LSample light_sample(const pt_light& l, float u0, float u1, float uc = 0.0f) {
     LSample ls;
     ls.L = F3(0, 0, 0);
     ls.p = F3(0, 0, 0);
@@ -744,6 +797,10 @@ __device__ LSample light_sample(const pt_light& l, float u0, float u1) {
         ls.n = F3(1, 1, 1);
         ls.u = u0;
         ls.v = u1;
+        return ls;
+    }
+    if (l.kind == PT_LIGHT_TEX_INF) {
+        texinf_sample(l, uc, u0, u1, ls);
         return ls;
     }
     float z = 2.0f * u0 - 1.0f;
@@ -775,6 +832,7 @@ __device__ float light_pdf(const pt_light& l, f3 p, f3 n, f3 ro, f3 rd) {
         return shape_pdf(kind, index, p, n, ro, rd);
     }
     if (l.kind == PT_LIGHT_UNIFORM_INF || l.kind == PT_LIGHT_SKY_INF) return 1.0f / (4.0f * PT_PI);
+    if (l.kind == PT_LIGHT_TEX_INF) return texinf_pdf(l, rd);
     return 0;
 }
 // Light::L(interaction, ray)
@@ -787,7 +845,7 @@ __device__ f3 light_L(const pt_light& l, f3 n, float u, float v, f3 rd) {
         if (l.one_sided && dot(rd, n) > 0) return F3(0, 0, 0);
         return tex_eval(l.tex, u, v);
     }
-    if (l.kind == PT_LIGHT_UNIFORM_INF || l.kind == PT_LIGHT_SKY_INF) return inf_le(l, rd);
+    if (l.kind == PT_LIGHT_UNIFORM_INF || l.kind == PT_LIGHT_SKY_INF || l.kind == PT_LIGHT_TEX_INF) return inf_le(l, rd);
     return F3(0, 0, 0);
 }
 // LightSampler::Sample (LightSampler.cpp:7-11, 34-46); the power sampler's

@@ -22,7 +22,8 @@ from .scene import (AlphaMode, AreaLight, CheckerTexture, DistantLight, Function
                     ImageTexture, LightSampler, Material, MicrofacetDielectric, MicrofacetDiffuse, Model, PointLight,
                     TransformedPrimitive, AnimatedPrimitive, mat4_identity, mat4_translate, _expand_seq,
                     PowerLightSampler, QuadShape, Scene, SolidColor, SpecularConductor, SphereShape, Texture,
-                    ThinDielectric, TransformedLight, UniformInfiniteLight, UniformLightSampler)
+                    ThinDielectric, TransformedLight, UniformInfiniteLight, UniformLightSampler,
+                    FloatImageTexture, TextureInfiniteLight)
 
 
 @dataclass
@@ -58,6 +59,7 @@ class FlatScene:
     sampler_lights: Optional[np.ndarray] = None
     infinite_lights: Optional[np.ndarray] = None
     light_objects: list = field(default_factory=list)
+    light_dist: np.ndarray = field(default_factory=lambda: np.zeros(0, np.float32))
     instances: Optional[np.ndarray] = None   # pt_instance records
     # participating media: id(HomogeneusMedium) -> index into `media`
     media: Optional[np.ndarray] = None
@@ -126,6 +128,8 @@ class FlatScene:
         d.n_sampler_lights = self.sampler_lights.shape[0]
         d.infinite_lights = N.ptr(self.infinite_lights)
         d.n_infinite_lights = self.infinite_lights.shape[0]
+        d.light_dist = N.ptr(self.light_dist) if self.light_dist.size else None
+        d.n_light_dist = self.light_dist.shape[0]
         d.instances = N.ptr(self.instances)
         d.n_instances = 0 if self.instances is None else self.instances.shape[0]
         d.media = N.ptr(self.media)
@@ -176,6 +180,20 @@ class _Registry:
                 self.texel_bytes += pad
             rec["image"] = len(self.images)
             self.images.append((off, w, h, c, 0))
+        elif isinstance(t, FloatImageTexture):
+            # FloatImage texels (Texture.hpp:70-103): float32 bytes, 4-aligned
+            rec["kind"] = N.PT_TEX_IMAGE
+            h, w, c = t.data.shape
+            off = self.texel_bytes
+            data = np.ascontiguousarray(t.data.reshape(-1), np.float32).view(np.uint8)
+            self.texel_chunks.append(data)
+            self.texel_bytes += data.size
+            pad = (-self.texel_bytes) % 16
+            if pad:
+                self.texel_chunks.append(np.zeros(pad, dtype=np.uint8))
+                self.texel_bytes += pad
+            rec["image"] = len(self.images)
+            self.images.append((off, w, h, c, N.PT_IMAGE_F32))
         else:
             raise TypeError(f"unsupported texture {type(t).__name__}")
         self.tex_ids[id(t)] = len(self.textures)
@@ -518,6 +536,7 @@ def bind_lights(flat: FlatScene, scene: Scene, sampler: Optional[LightSampler]):
     table["prim"] = -1
     table["tex"] = -1
     table["instance"] = -1
+    dists = []  # TEX_INF running sums, concatenated
     for i, l in enumerate(lights):
         r = table[i]
         r["power"] = l.Power()
@@ -541,6 +560,14 @@ def bind_lights(flat: FlatScene, scene: Scene, sampler: Optional[LightSampler]):
             r["color"] = l.c0
             r["vec"] = l.c1
             r["scale"] = l.scale
+        elif isinstance(l, TextureInfiniteLight):
+            if l.accWeights is None:  # no light sampler ran PreProcess (SimplePath): Le only
+                l.PreProcess(flat.bbox)
+            r["kind"] = N.PT_LIGHT_TEX_INF
+            r["tex"] = reg.texture(l.tex)
+            r["scale"] = l.LeScale
+            r["prim"] = sum(a.shape[0] for a in dists)
+            dists.append(l.accWeights)
         elif isinstance(l, DistantLight):
             r["kind"] = N.PT_LIGHT_DISTANT
             r["color"] = l.color
@@ -562,6 +589,7 @@ def bind_lights(flat: FlatScene, scene: Scene, sampler: Optional[LightSampler]):
     flat.texels = (np.ascontiguousarray(np.concatenate(reg.texel_chunks)) if reg.texel_chunks
                    else np.zeros(0, dtype=np.uint8))
     flat.lights = table
+    flat.light_dist = np.ascontiguousarray(np.concatenate(dists) if dists else np.zeros(0, np.float32), np.float32)
     flat.light_objects = lights
     flat.light_sampler = sampler.kind if sampler is not None else N.PT_LS_UNIFORM
     flat.sampler_lights = np.array([idx[id(l)] for l in (sampler.lights if sampler is not None else [])],

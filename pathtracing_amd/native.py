@@ -19,7 +19,9 @@ PT_OK = 0
 PT_PRIM_TRIANGLE, PT_PRIM_QUAD, PT_PRIM_SPHERE, PT_PRIM_BLAS, PT_PRIM_INSTANCE = 0, 1, 2, 3, 4
 PT_TEX_SOLID, PT_TEX_IMAGE, PT_TEX_CHECKER = 0, 1, 2
 PT_MAT_DIFFUSE, PT_MAT_DIELECTRIC, PT_MAT_THIN, PT_MAT_CONDUCTOR = 0, 1, 2, 3
-PT_LIGHT_AREA, PT_LIGHT_UNIFORM_INF, PT_LIGHT_SKY_INF, PT_LIGHT_DISTANT, PT_LIGHT_POINT = 0, 1, 2, 3, 4
+PT_LIGHT_AREA, PT_LIGHT_UNIFORM_INF, PT_LIGHT_SKY_INF, PT_LIGHT_DISTANT, PT_LIGHT_POINT, PT_LIGHT_TEX_INF = 0, 1, 2, 3, 4, 5
+PT_IMAGE_U8, PT_IMAGE_F32 = 0, 1
+PT_TEXINF_X, PT_TEXINF_Y = 1920, 1080
 PT_LS_UNIFORM, PT_LS_POWER = 0, 1
 PT_INTEGRATOR_PATH, PT_INTEGRATOR_SIMPLE, PT_INTEGRATOR_VOLPATH = 0, 1, 2
 PT_FILTER_MITCHELL, PT_FILTER_BOX, PT_FILTER_GAUSSIAN = 0, 1, 2
@@ -43,7 +45,7 @@ QUAD = np.dtype([("Q", "<f4", 3), ("u", "<f4", 3), ("v", "<f4", 3), ("normal", "
 SPHERE = np.dtype([("center", "<f4", 3), ("radius", "<f4")])
 TEXTURE = np.dtype([("kind", "<u4"), ("scale", "<f4", 3), ("value", "<f4", 3), ("a", "<i4"), ("b", "<i4"),
                     ("inv_scale", "<f4", 2), ("image", "<i4")])
-IMAGE = np.dtype([("offset", "<u8"), ("width", "<i4"), ("height", "<i4"), ("channels", "<i4"), ("pad", "<i4")])
+IMAGE = np.dtype([("offset", "<u8"), ("width", "<i4"), ("height", "<i4"), ("channels", "<i4"), ("format", "<i4")])
 MATERIAL = np.dtype([("kind", "<u4"), ("tex", "<i4"), ("norm", "<i4"), ("rough", "<i4"), ("metal", "<i4"),
                      ("alpha", "<i4"), ("alpha_mode", "<u4"), ("alpha_cutoff", "<f4"), ("ri", "<f4"),
                      ("albedo", "<f4", 3)])
@@ -87,6 +89,7 @@ class SceneDesc(C.Structure):
         ("light_sampler", C.c_uint32),
         ("sampler_lights", C.c_void_p), ("n_sampler_lights", C.c_uint32),
         ("infinite_lights", C.c_void_p), ("n_infinite_lights", C.c_uint32),
+        ("light_dist", C.c_void_p), ("n_light_dist", C.c_uint64),
         ("media", C.c_void_p), ("n_media", C.c_uint32), ("scene_medium", C.c_int32),
         ("instances", C.c_void_p), ("n_instances", C.c_uint32),
     ]
@@ -129,6 +132,7 @@ EXPORTS = [
     "pt_version", "pt_create", "pt_destroy", "pt_last_error", "pt_set_stream", "pt_scene_upload", "pt_render",
     "pt_trace", "pt_scene_device_bytes", "pt_bvh4_build", "pt_bvh4_order_table", "pt_film_resolve",
     "pt_mat4_inverse", "pt_bvh4_build_device", "pt_set_node_format", "pt_render_adaptive", "pt_render_samples",
+    "pt_texinf_weights",
 ]
 
 _lib = None
@@ -183,10 +187,24 @@ def lib():
     L.pt_bvh4_build_device.argtypes = [vp, vp, C.c_uint32, vp, C.POINTER(C.c_uint32), C.POINTER(RefNode), vp, vp,
                                        C.POINTER(BvhBuildStats)]
     L.pt_bvh4_build_device.restype = C.c_int32
+    L.pt_texinf_weights.argtypes = [vp, C.c_int32, C.c_int32, C.c_int32, vp, C.c_float, vp, C.c_int32]
+    L.pt_texinf_weights.restype = C.c_int32
     L.pt_bvh4_order_table.argtypes = [vp]
     L.pt_bvh4_order_table.restype = C.c_int32
     _lib = L
     return L
+
+
+def texinf_weights(texels: np.ndarray, color_scale, le_scale: float, threads: int = 0) -> np.ndarray:
+    """TextureInfiniteLight::PreProcess's 1920 x 1080 cell weights (host
+    routine of libpt_hip, pt_texinf_weights); texels HxWxC float32."""
+    t = np.ascontiguousarray(texels, np.float32)
+    h, w, c = t.shape
+    cs = np.ascontiguousarray(color_scale, np.float32).reshape(3)
+    out = np.zeros(PT_TEXINF_X * PT_TEXINF_Y, np.float32)
+    n = threads or min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1))
+    check(lib().pt_texinf_weights(t.ctypes.data, w, h, c, cs.ctypes.data, float(le_scale), out.ctypes.data, int(n)))
+    return out
 
 
 def mat4_inverse(m: np.ndarray) -> np.ndarray:

@@ -13,7 +13,8 @@ import numpy as np
 from .scene import (AnimatedPrimitive, AreaLight, CheckerTexture, DistantLight, FunctionInfiniteLight,
                     GeometricPrimitive, ImageTexture, TransformedPrimitive,
                     MicrofacetDielectric, MicrofacetDiffuse, Model, PointLight, PowerLightSampler, QuadShape,
-                    SolidColor, SpecularConductor, SphereShape, ThinDielectric, UniformInfiniteLight)
+                    SolidColor, SpecularConductor, SphereShape, ThinDielectric, UniformInfiniteLight,
+                    FloatImageTexture, TextureInfiniteLight)
 
 
 def _f(x) -> str:
@@ -29,6 +30,15 @@ def write_png(path: Path, data: np.ndarray):
     if data.ndim == 3 and data.shape[2] == 2:
         mode = "LA"
     Image.fromarray(data, mode=mode).save(path)
+
+
+def write_hdr(path: Path, rgbe: np.ndarray):
+    """Radiance RGBE, flat (not run-length) scanlines, rows top first: what
+    stbi_loadf decodes back to FloatImageTexture.data exactly."""
+    h, w = rgbe.shape[:2]
+    with open(path, "wb") as f:
+        f.write(b"#?RADIANCE\nFORMAT=32-bit_rle_rgbe\n\n" + f"-Y {h} +X {w}\n".encode())
+        f.write(np.ascontiguousarray(rgbe, np.uint8).tobytes())
 
 
 def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: str, max_depth: int,
@@ -55,6 +65,10 @@ def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: 
             lines.append(f"texture {i} solid {' '.join(_f(x) for x in t.albedo)} {s}")
         elif isinstance(t, CheckerTexture):
             lines.append(f"texture {i} checker {a} {b} {_f(t.uvscale[0])} {_f(t.uvscale[1])} {s}")
+        elif isinstance(t, FloatImageTexture):
+            name = f"tex{i}.hdr"
+            write_hdr(out_dir / name, t.rgbe)
+            lines.append(f"texture {i} floatimage {name} {s}")
         elif isinstance(t, ImageTexture):
             name = f"tex{i}.png"
             write_png(out_dir / name, t.raw)
@@ -172,6 +186,8 @@ def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: 
             lines.append(f"infinite uniform {' '.join(_f(x) for x in l.color)}")
         elif isinstance(l, FunctionInfiniteLight):
             lines.append(f"infinite sky {' '.join(_f(x) for x in [*l.c0, *l.c1, l.scale])}")
+        elif isinstance(l, TextureInfiniteLight):
+            lines.append(f"infinite texture {tex(l.tex)} {_f(l.LeScale)}")
         else:
             raise TypeError(type(l))
     for l in extra_lights or []:

@@ -140,6 +140,24 @@ class ImageTexture(Texture):
         return int(self.data.shape[2])
 
 
+class FloatImageTexture(Texture):
+    """FloatImageTexture (Texture.hpp:167-194): float texels (an HDR image as
+    stbi_loadf returns it, HxWxC, row 0 first), bilinear, repeat wrap, no
+    sRGB step.  `data` is the decoded float array; `path` names the file a
+    recipe writes it to (tests: Radiance .hdr, whose decode is exact)."""
+
+    def __init__(self, data: np.ndarray, colorScale=(1, 1, 1), path: str = ""):
+        super().__init__(colorScale)
+        data = np.ascontiguousarray(data, dtype=np.float32)
+        if data.ndim == 2:
+            data = data[:, :, None]
+        self.data = data
+        self.path = path
+
+    def Channels(self) -> int:
+        return int(self.data.shape[2])
+
+
 class CheckerTexture(Texture):
     def __init__(self, textureA: Texture, textureB: Texture, uvscale, colorScale=(1, 1, 1)):
         super().__init__(colorScale)
@@ -484,6 +502,41 @@ class FunctionInfiniteLight(InfiniteLight):
         # E[a] = 0.5 and the mean luminance is that of the mean colour.
         mean = (self.scale * (f32(0.5) * self.c0 + f32(0.5) * self.c1)).astype(np.float64)
         self.cachedPower = float(f32(luminance(mean) * math.sqrt(self.sceneRadius)))
+
+    def Power(self) -> float:
+        return self.cachedPower
+
+
+class TextureInfiniteLight(InfiniteLight):
+    """TextureInfiniteLight (Light.hpp:94-123, Light.cpp:110-200): an
+    environment map, Le(dir) = LeScale * tex(GetSphereUV(dir)), sampled by a
+    1920 x 1080 grid of cells weighted by their mean luminance.  PreProcess
+    runs the native host restatement of the reference's cell estimate
+    (pt_texinf_weights: its unseeded jitter becomes a fixed hash) and keeps
+    the float running sums (std::partial_sum) for the device."""
+    NX, NY = 1920, 1080
+
+    def __init__(self, tex: "FloatImageTexture", LeScale: float = 1.0):
+        if not isinstance(tex, FloatImageTexture):
+            raise TypeError("TextureInfiniteLight takes a FloatImageTexture (main.cpp:115-116, 222-224)")
+        self.tex = tex
+        self.LeScale = f32(LeScale)
+        self.cachedPower = 0.0
+        self.accWeights: Optional[np.ndarray] = None
+        self.weights_override: Optional[np.ndarray] = None
+
+    def PreProcess(self, bbox):
+        super().PreProcess(bbox)
+        from . import native as N
+        if self.weights_override is not None:
+            w = np.ascontiguousarray(self.weights_override, np.float32)
+        else:
+            w = N.texinf_weights(self.tex.data, self.tex.colorScale, float(self.LeScale))
+        # std::partial_sum in float (sequential), totalWeight = back()
+        self.accWeights = np.cumsum(w, dtype=np.float32)
+        total = float(self.accWeights[-1])
+        # totalWeight / samples * sqrt(sceneRadius) (Light.cpp:195)
+        self.cachedPower = float(f32(total / (self.NX * self.NY) * float(f32(math.sqrt(self.sceneRadius)))))
 
     def Power(self) -> float:
         return self.cachedPower

@@ -21,6 +21,7 @@ from typing import List, Optional
 import numpy as np
 
 from .scene import (AlphaMode, AlphaTester, AreaLight, Camera, CheckerTexture, DistantLight, Film,
+                    FloatImageTexture, TextureInfiniteLight,
                     FunctionInfiniteLight, GeometricPrimitive, HenyeyGreenstein, HomogeneusMedium, ImageTexture,
                     Mesh,
                     MicrofacetDielectric, MicrofacetDiffuse, MitchellFilter, Model, PointLight, PowerLightSampler,
@@ -235,6 +236,46 @@ def lit_instances(W: int = 1024, H: int = 1024, spp: int = 256, max_depth: int =
     film = Film((W, H), MitchellFilter())
     camera = Camera((0, 0, 3.7), (0, 0, 0), 0.75, film)
     return SceneSetup(scene, camera, "path", PowerLightSampler(), max_depth, seed, spp).finish()
+
+
+def env_texels(rng, w: int = 64, h: int = 32) -> np.ndarray:
+    """A procedural HDR sky (sky gradient + a bright sun blob + noise) whose
+    float values are exact Radiance RGBE decodes (m * 2^(e - 136)), so the
+    .hdr file a recipe writes decodes (stbi_loadf) to the very same floats."""
+    y = (np.arange(h, dtype=np.float64) + 0.5) / h
+    x = (np.arange(w, dtype=np.float64) + 0.5) / w
+    X, Y = np.meshgrid(x, y)
+    base = np.stack([0.4 + 0.6 * Y, 0.55 + 0.4 * Y, 0.9 + 0.2 * (1 - Y)], -1)
+    sun = 40.0 * np.exp(-(((X - 0.3) / 0.05) ** 2 + ((Y - 0.35) / 0.08) ** 2))[..., None] * np.array([1.0, 0.9, 0.7])
+    v = base * (0.8 + 0.4 * rng.random((h, w, 1))) + sun
+    e = np.ceil(np.log2(np.maximum(v.max(-1), 1e-30))).astype(np.int64)  # shared exponent: max < 2^e
+    m = np.clip(np.floor(v / np.exp2(e - 8)[..., None]), 0, 255).astype(np.int64)
+    rgbe = np.concatenate([m, (e + 128)[..., None]], -1).astype(np.uint8)
+    rgbe[0, 0, 0] = max(3, int(rgbe[0, 0, 0]))  # a flat (not run-length) file: first byte != 2
+    return rgbe
+
+
+def rgbe_decode(rgbe: np.ndarray) -> np.ndarray:
+    """stbi__hdr_convert: m * ldexp(1, e - 136) in float, 0 for e = 0."""
+    f = np.ldexp(np.float32(1.0), rgbe[..., 3].astype(np.int32) - 136).astype(np.float32)
+    out = (rgbe[..., :3].astype(np.float32) * f[..., None]).astype(np.float32)
+    out[rgbe[..., 3] == 0] = 0.0
+    return out
+
+
+def envmap(W: int = 256, H: int = 256, spp: int = 16, max_depth: int = 8, seed: int = 0x5EED0071,
+           le_scale: float = 1.5, integrator: str = "path") -> SceneSetup:
+    """C1's floor and spheres under a TextureInfiniteLight (Light.cpp:110-200)
+    over a FloatImageTexture HDR sky (main.cpp:115-116, 222-224 use one),
+    PowerLightSampler (main.cpp's) with the red quad light."""
+    rng = np.random.default_rng(71)
+    rgbe = env_texels(rng)
+    sky = FloatImageTexture(rgbe_decode(rgbe))
+    sky.rgbe = rgbe
+    s = example_1(W=W, H=H, spp=spp, integrator=integrator, max_depth=max_depth, seed=seed, medium=False)
+    scene = s.scene
+    scene.infiniteLights = [TextureInfiniteLight(sky, le_scale)]
+    return SceneSetup(scene, s.camera, integrator, PowerLightSampler(), max_depth, seed, spp).finish()
 
 
 def blend_box(W: int = 64, H: int = 64, spp: int = 16, max_depth: int = 8, alpha: float = 0.35,

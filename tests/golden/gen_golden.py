@@ -228,10 +228,32 @@ def gen_adaptive(tmp: Path):
     print(f"adaptive: {(OUT / 'adaptive.npz').stat().st_size / 1024:.0f} KiB, {len(ADAPTIVE_SCENES)} scenes")
 
 
+def gen_envmap(tmp: Path):
+    """TextureInfiniteLight (Light.cpp:110-200) through the reference: Le(dir)
+    and PDF(dir) for a spread of directions and Power(), ref_harness `envle`
+    (its PreProcess is randomly jittered: PDF and Power vary by the estimate's
+    noise; Le is exact)."""
+    setup = scenes.envmap(W=32, H=32, spp=4)
+    d = tmp / "envmap"
+    recipe = write_recipe(d, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
+                          setup.max_depth, setup.light_sampler, setup.extra_lights)
+    rng = np.random.default_rng(20261016)
+    dirs = rng.normal(size=(1024, 3))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    dirs = dirs.astype(np.float32)
+    dirs.tofile(d / "dirs.bin")
+    out = d / "o"
+    harness(recipe, "envle", out, d / "dirs.bin")
+    raw = np.fromfile(f"{out}.envle.bin", np.float32)
+    np.savez_compressed(OUT / "envmap.npz", dirs=dirs, le_pdf=raw[:-1].reshape(-1, 4), power=raw[-1:])
+    print(f"envmap: {(OUT / 'envmap.npz').stat().st_size / 1024:.0f} KiB")
+
+
 STATS_SCENES = {
     "example1": lambda: scenes.example_1(W=48, H=48, spp=1024, seed=0x5EED0051),
     "cornell_c3": lambda: scenes.cornell(W=48, H=48, spp=1024, config="c3", seed=0x5EED0052),
     "blend_box": lambda: scenes.blend_box(W=48, H=48, spp=1024, seed=0x5EED0053),
+    "envmap": lambda: scenes.envmap(W=48, H=48, spp=1024, seed=0x5EED0054),
 }
 
 
@@ -273,6 +295,8 @@ def main(names=None):
             gen_adaptive(Path(t))
         if not names or "stats" in names:
             gen_stats(Path(t))
+        if not names or "envmap" in names:
+            gen_envmap(Path(t))
 
 
 if __name__ == "__main__":

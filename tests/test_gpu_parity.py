@@ -451,7 +451,7 @@ def test_gpu_adaptive_one_sample_rounds():
 
 
 # ---------------------------------------------------------------- F8: vs the reference's own random Render
-@pytest.mark.parametrize("name", ["example1", "cornell_c3", "blend_box"])
+@pytest.mark.parametrize("name", ["example1", "cornell_c3", "blend_box", "envmap"])
 def test_gpu_matches_reference_render_statistically(name):
     """pt_render_samples at 1024 spp against the reference's own Render with
     its StratifiedSampler(32, 32) and unseeded RNGs (tests/golden/stats.npz):
@@ -488,3 +488,21 @@ def test_gpu_blend_alpha_accept_rate():
     np.testing.assert_array_equal(hits["prim"], ref["prim"])
     rate = on_panel.mean()
     assert abs(rate - 0.35) <= 4 * np.sqrt(0.35 * 0.65 / n), f"accept rate {rate:.4f}"
+
+
+# ---------------------------------------------------------------- TextureInfiniteLight (f4)
+@pytest.mark.parametrize("integrator", ["path", "simple"])
+def test_gpu_envmap_matches_oracle(integrator):
+    """A FloatImageTexture environment (TextureInfiniteLight): the device's
+    Le / cell pick / PDF (NEE and the escape MIS weight) against the oracle
+    per sample and per film pixel, on the same cell running sums."""
+    setup = scenes.envmap(W=32, H=32, spp=8, integrator=integrator)
+    integ = setup.make_integrator()
+    L = integ.RenderSamples()
+    Lo, _, _ = oracle.li(integ)
+    _li_close(L, Lo, 1.0, f"li_oracle/envmap_{integrator}")
+    film = setup.camera.GetFilm()
+    film.Clear()
+    integ.Render()
+    ref, _ = oracle.render(integ, threads=4)
+    _film_close(film.accum, ref, 1.0, f"film_oracle/envmap_{integrator}")

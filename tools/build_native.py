@@ -52,12 +52,17 @@ def build_product(force: bool = False, variant: str = "", defines=()) -> Path:
     # the GPU hosts while contracting like the reference's -march=native build.
     bvh_o = build / "pt_bvh.o"
     _run(["g++", "-std=gnu++20", "-O3", "-march=x86-64-v3", "-fPIC", "-c", CSRC / "pt_bvh.cpp", "-o", bvh_o, *inc])
+    # TextureInfiniteLight pre-process (host): no contraction, every fused
+    # multiply-add of the reference build is spelled out
+    env_o = build / "pt_envmap.o"
+    _run(["g++", "-std=gnu++20", "-O3", "-march=x86-64-v3", "-ffp-contract=off", "-fPIC", "-c",
+          CSRC / "pt_envmap.cpp", "-o", env_o, *inc])
     rt_o = build / "pt_runtime.o"
     _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++20", "-munsafe-fp-atomics",
           "-Wno-unused-result", "-Wno-unused-value", *[f"-D{d}" for d in defines],
           "-c", CSRC / "pt_runtime.hip", "-o", rt_o, *inc])
     tmp = out.with_suffix(".so.tmp")
-    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", rt_o, bvh_o, "-o", tmp, "-lpthread"])
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", rt_o, bvh_o, env_o, "-o", tmp, "-lpthread"])
     os.replace(tmp, out)
     return out
 
