@@ -103,6 +103,14 @@ PT_MEMBER(ImgData, Image, unsigned char*, data);
 PT_MEMBER(ImgW, Image, int, width);
 PT_MEMBER(ImgH, Image, int, height);
 PT_MEMBER(ImgC, Image, int, channels);
+PT_MEMBER(FImgTexImage, FloatImageTexture, FloatImage, image);
+PT_MEMBER(FImgData, FloatImage, float*, data);
+PT_MEMBER(FImgW, FloatImage, int, width);
+PT_MEMBER(FImgH, FloatImage, int, height);
+PT_MEMBER(FImgC, FloatImage, int, channels);
+PT_MEMBER(TexInfTex, TextureInfiniteLight, TexPtr, tex);
+PT_MEMBER(TexInfScale, TextureInfiniteLight, float, LeScale);
+PT_MEMBER(TexInfAcc, TextureInfiniteLight, std::vector<float>, accWeights);
 PT_MEMBER(ChkA, CheckerTexture, TexPtr, tex1);
 PT_MEMBER(ChkB, CheckerTexture, TexPtr, tex2);
 PT_MEMBER(ChkInv, CheckerTexture, glm::vec2, invScale);
@@ -170,6 +178,7 @@ struct Flat {
     std::vector<uint8_t> texels;
     std::vector<pt_light> lights;
     std::vector<uint32_t> sampler_lights, infinite_lights;
+    std::vector<float> light_dist;  // TextureInfiniteLight running sums
     uint32_t light_sampler = PT_LS_UNIFORM;
     std::vector<pt_medium> media;
     int32_t scene_medium = -1;
@@ -231,6 +240,21 @@ struct Flat {
             pi.channels = PT_GET(img, ImgC);
             const unsigned char* px = PT_GET(img, ImgData);
             texels.insert(texels.end(), px, px + (size_t)pi.width * pi.height * pi.channels);
+            texels.resize((texels.size() + 15) & ~size_t(15));
+            r.kind = PT_TEX_IMAGE;
+            r.image = (int32_t)images.size();
+            images.push_back(pi);
+        } else if (auto* fm = dynamic_cast<const FloatImageTexture*>(t.get())) {
+            // FloatImage texels (Texture.hpp:70-103): float bytes, 4-aligned
+            const FloatImage& img = PT_GET(*fm, FImgTexImage);
+            pt_image pi{};
+            pi.offset = texels.size();
+            pi.width = PT_GET(img, FImgW);
+            pi.height = PT_GET(img, FImgH);
+            pi.channels = PT_GET(img, FImgC);
+            pi.format = PT_IMAGE_F32;
+            const auto* px = reinterpret_cast<const uint8_t*>(PT_GET(img, FImgData));
+            texels.insert(texels.end(), px, px + 4 * (size_t)pi.width * pi.height * pi.channels);
             texels.resize((texels.size() + 15) & ~size_t(15));
             r.kind = PT_TEX_IMAGE;
             r.image = (int32_t)images.size();
@@ -547,6 +571,16 @@ struct Flat {
                 put3(r.color, g->horizon);
                 put3(r.vec, g->zenith);
                 r.scale = g->scale;
+            } else if (auto* ti = dynamic_cast<const TextureInfiniteLight*>(l.get())) {
+                // the reference's own PreProcess result: its cell running sums
+                const auto& acc = PT_GET(*ti, TexInfAcc);
+                if (acc.size() != (size_t)PT_TEXINF_X * PT_TEXINF_Y)
+                    throw std::runtime_error("HipPathIntegrator: TextureInfiniteLight before PreProcess");
+                r.kind = PT_LIGHT_TEX_INF;
+                r.tex = texture(PT_GET(*ti, TexInfTex));
+                r.scale = PT_GET(*ti, TexInfScale);
+                r.prim = (int32_t)light_dist.size();
+                light_dist.insert(light_dist.end(), acc.begin(), acc.end());
             } else if (auto* d = dynamic_cast<const DistantLight*>(l.get())) {
                 r.kind = PT_LIGHT_DISTANT;
                 put3(r.color, PT_GET(*d, DistColor));
@@ -610,6 +644,8 @@ struct Flat {
         d.n_sampler_lights = (uint32_t)sampler_lights.size();
         d.infinite_lights = infinite_lights.data();
         d.n_infinite_lights = (uint32_t)infinite_lights.size();
+        d.light_dist = light_dist.data();
+        d.n_light_dist = light_dist.size();
         d.media = media.data();
         d.n_media = (uint32_t)media.size();
         d.scene_medium = scene_medium;
