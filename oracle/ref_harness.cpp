@@ -614,6 +614,12 @@ static std::vector<SampleRec> run_li(World& w, int x0, int y0, int x1, int y1, u
 static void cmd_li(World& w, const std::string& out, int x0, int y0, int x1, int y1, unsigned spp) {
     auto recs = run_li(w, x0, y0, x1, y1, spp);
     wr(out + ".li.bin", recs);
+    // this run's light powers (a sky's Power() is a random estimate per run)
+    std::vector<double> pw;
+    auto all = w.scene->GetLights();
+    for (auto& l : w.extra) all.push_back(l);
+    for (auto& l : all) pw.push_back(l->Power());
+    wr(out + ".lipower.bin", pw);
 }
 
 // --- film: FilmTile::Add over the whole film of the same samples (Film.hpp:65-82)

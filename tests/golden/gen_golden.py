@@ -228,6 +228,25 @@ def gen_adaptive(tmp: Path):
     print(f"adaptive: {(OUT / 'adaptive.npz').stat().st_size / 1024:.0f} KiB, {len(ADAPTIVE_SCENES)} scenes")
 
 
+def gen_c4_band(tmp: Path):
+    """The full-size C4 scene (~10 M triangles, sanmiguel at detail 1) at
+    192 x 108: the reference's own per-sample Li (ref_harness li, PCG stream)
+    for the pixel rows 40..47 at 2 spp, with that run's light powers (the
+    sky's is a random estimate per run).  Only the samples are kept."""
+    setup = scenes.sanmiguel(W=192, H=108, spp=2)
+    d = tmp / "c4band"
+    recipe = write_recipe(d, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
+                          setup.max_depth, setup.light_sampler, setup.extra_lights)
+    out = d / "o"
+    harness(recipe, "li", out, 0, 40, 192, 48, 2)
+    rec = np.fromfile(f"{out}.li.bin", dtype=np.dtype([("px", "<f8"), ("py", "<f8"), ("L", "<f4", 3),
+                                                      ("dims", "<u4")]))
+    np.savez_compressed(OUT / "c4_band.npz", li_L=rec["L"].reshape(192 * 8, 2, 3),
+                        li_p=np.stack([rec["px"], rec["py"]], 1).reshape(192 * 8, 2, 2),
+                        light_power=np.fromfile(f"{out}.lipower.bin", np.float64))
+    print(f"c4_band: {(OUT / 'c4_band.npz').stat().st_size / 1024:.0f} KiB")
+
+
 def gen_envmap(tmp: Path):
     """TextureInfiniteLight (Light.cpp:110-200) through the reference: Le(dir)
     and PDF(dir) for a spread of directions and Power(), ref_harness `envle`
@@ -297,6 +316,8 @@ def main(names=None):
             gen_stats(Path(t))
         if not names or "envmap" in names:
             gen_envmap(Path(t))
+        if not names or "c4_band" in names:
+            gen_c4_band(Path(t))
 
 
 if __name__ == "__main__":
