@@ -208,6 +208,8 @@ def main():
                     help="BVH traversal kernel (auto: by BVH size)")
     ap.add_argument("--nodes", choices=("auto", "full", "quant"), default="auto",
                     help="node layout of the pool traversal (auto: 64-B quantized nodes)")
+    ap.add_argument("--sort-material", action="store_true",
+                    help="shade each bounce binned by hit material (PT_RENDER_SORT_MATERIAL)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the instrumented node-count pass")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -246,6 +248,8 @@ def main():
 
     tflag = {"auto": 0, "pool": N.PT_RENDER_TRAVERSAL_POOL, "simple": N.PT_RENDER_TRAVERSAL_SIMPLE}[args.traversal]
     tflag |= {"auto": 0, "full": N.PT_RENDER_NODES_FULL, "quant": N.PT_RENDER_NODES_QUANTIZED}[args.nodes]
+    if args.sort_material:
+        tflag |= N.PT_RENDER_SORT_MATERIAL
 
     def step(flags=0):
         # this rank's sample shard into the device film, then the RCCL SUM

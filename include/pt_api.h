@@ -256,6 +256,7 @@ enum { PT_FILTER_MITCHELL = 0, PT_FILTER_BOX = 1, PT_FILTER_GAUSSIAN = 2 };
 #define PT_RENDER_NODES_FULL 0x10u      /* pool traversal over the 128-B reference clusters */
 #define PT_RENDER_NODES_QUANTIZED 0x20u /* ... over the 64-B quantized nodes (the default)  */
 #define PT_RENDER_ADAPTIVE 0x40u        /* pt_render: TileIntegrator::Render's adaptive rounds */
+#define PT_RENDER_SORT_MATERIAL 0x80u   /* shade each bounce's paths binned by hit material */
 
 typedef struct pt_render_desc {
     uint32_t integrator;       /* PT_INTEGRATOR_*                               */

@@ -71,6 +71,7 @@ struct RenderParams {
     uint32_t tiled, tiles_x;
     uint32_t pixel_begin;
     const uint32_t* pix_list;       // adaptive rounds: work pixel i = pix_list[i] (linear id), else null
+    const uint32_t* order;          // material sort: k_shade thread t shades path order[t], else t
     unsigned long long chunk_total; // npix_work * (s_hi - s_lo)
     uint32_t filter;
     int rad_x, rad_y;
@@ -111,6 +112,13 @@ struct AdaptEst {
 };
 #define PT_ADAPT_MAX_ROUNDS 128   // while (Samples() < 128 * samplesPerPixel)
 #define PT_ADAPT_REL_VAR 1.5      // minRelativeVariance
+// Material / hit-state binning of a bounce's paths before shading
+// (PT_RENDER_SORT_MATERIAL): bin 0 = miss, 1 + material % 254 for a hit,
+// 255 for hits inside instances; counting sort into `order`.
+#define PT_SORT_BINS 256
+__global__ void k_sort_count(const uint32_t* nptr, const float4* hit, uint32_t* counts);
+__global__ void k_sort_scan(uint32_t* counts);
+__global__ void k_sort_scatter(const uint32_t* nptr, const float4* hit, uint32_t* offsets, uint32_t* order);
 __global__ void k_adapt_init(RenderParams R, uint32_t shard_index, uint32_t shard_count, uint32_t* list,
                              uint32_t* cnt, AdaptEst* est, uint32_t* counts);
 __global__ void k_adapt_map(const uint32_t* list, const uint32_t* n, int32_t* map);

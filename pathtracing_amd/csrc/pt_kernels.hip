@@ -567,7 +567,8 @@ __global__ __launch_bounds__(256) PT_SHADE_WAVES void k_shade(RenderParams R, Pa
                                               ShadowRec* __restrict__ sq, uint32_t* __restrict__ cnt) {
     const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
     if (blockIdx.x * 256 >= n) return;  // block-uniform: the grid covers the capacity
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t i = (R.order && t < n) ? R.order[t] : t;  // material-sorted order, or the path order
     bool cont = false, done = false, shadow = false;
     ShadowRec srec;
     f3 ro = F3(0, 0, 0), rd = F3(0, 0, 0), att = F3(0, 0, 0), out = F3(0, 0, 0);
@@ -783,7 +784,8 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                                                   ShadowRec* __restrict__ sq, uint32_t* __restrict__ cnt) {
     const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
     if (blockIdx.x * 256 >= n) return;  // block-uniform: the grid covers the capacity
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t i = (R.order && t < n) ? R.order[t] : t;  // material-sorted order, or the path order
     bool cont = false, done = false, shadow = false;
     ShadowRec srec;
     f3 ro = F3(0, 0, 0), rd = F3(0, 0, 0), att = F3(0, 0, 0), out = F3(0, 0, 0);
@@ -1254,6 +1256,68 @@ __global__ __launch_bounds__(256) void k_resolve(const double* __restrict__ film
         const double s = linear_to_srgb((double)(float)m[k]);
         rgb[3ull * i + k] = (uint8_t)(255.999 * dmax_(0.0, dmin_(1.0, s)));
     }
+}
+
+// ------------------------------------------------------------------ material sort
+// north_star "sort of active rays by material and hit state": the paths of a
+// bounce are binned by what they hit (miss / the hit primitive's material)
+// and k_shade walks them bin by bin, so a wave shades one material (one
+// branch of the material code, one texture) at a time.  A counting sort:
+// per-block LDS histograms folded into 256 global counters, one exclusive
+// scan, then a scatter that reserves each block's range of every bin with one
+// atomic.  Per-path results do not depend on the order (each path and sample
+// is computed on its own), only the schedule does.
+__device__ __forceinline__ uint32_t sort_bin(const float4* __restrict__ hit, uint32_t i) {
+    const int prim = __float_as_int(hit[i].w);
+    if (prim < 0) return 0u;
+    if ((uint32_t)prim >= S.n_prims) return PT_SORT_BINS - 1u;  // a virtual slot inside an instance
+    const int mat = S.info[prim].material;
+    return mat < 0 ? 0u : 1u + (uint32_t)mat % (PT_SORT_BINS - 2u);
+}
+__global__ __launch_bounds__(256) void k_sort_count(const uint32_t* __restrict__ nptr, const float4* __restrict__ hit,
+                                                   uint32_t* __restrict__ counts) {
+    __shared__ uint32_t h[PT_SORT_BINS];
+    const uint32_t n = path_count(nptr);
+    if (blockIdx.x * 256 >= n) return;
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t < n) atomicAdd(&h[sort_bin(hit, t)], 1u);
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
+}
+__global__ __launch_bounds__(256) void k_sort_scan(uint32_t* __restrict__ counts) {  // one block
+    __shared__ uint32_t v[PT_SORT_BINS];
+    v[threadIdx.x] = counts[threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int b = 0; b < PT_SORT_BINS; b++) {
+            const uint32_t c = v[b];
+            v[b] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    counts[threadIdx.x] = v[threadIdx.x];
+}
+__global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict__ nptr, const float4* __restrict__ hit,
+                                                     uint32_t* __restrict__ offsets, uint32_t* __restrict__ order) {
+    __shared__ uint32_t h[PT_SORT_BINS], base[PT_SORT_BINS];
+    const uint32_t n = path_count(nptr);
+    if (blockIdx.x * 256 >= n) return;
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    uint32_t bin = 0, rank = 0;
+    if (t < n) {
+        bin = sort_bin(hit, t);
+        rank = atomicAdd(&h[bin], 1u);
+    }
+    __syncthreads();
+    if (h[threadIdx.x]) base[threadIdx.x] = atomicAdd(&offsets[threadIdx.x], h[threadIdx.x]);
+    __syncthreads();
+    if (t < n) order[base[bin] + rank] = t;
 }
 
 // ------------------------------------------------------------------ adaptive sampling

@@ -67,6 +67,10 @@ struct pt_ctx {
     uint32_t* a_list = nullptr;
     uint32_t* a_cnt = nullptr;
     uint64_t a_est_cap = 0, a_counts_cap = 0, a_map_cap = 0, a_list_cap = 0, a_cnt_cap = 0;
+    // material sort (PT_RENDER_SORT_MATERIAL): shading order + bin counters
+    uint32_t* sort_order = nullptr;
+    uint32_t* sort_counts = nullptr;
+    uint64_t sort_order_cap = 0, sort_counts_cap = 0;
     hipEvent_t ev[8] = {};
     hipEvent_t rev[PT_RING][5] = {};  // per in-flight iteration: kernel boundaries [0..2], end [4] ([3] unused)
 };
@@ -196,7 +200,8 @@ extern "C" void pt_destroy(pt_ctx* c) {
     if (c->scratch) hipFree(c->scratch);
     if (c->sample_L) hipFree(c->sample_L);
     if (c->film) hipFree(c->film);
-    for (void* p : {(void*)c->a_est, (void*)c->a_counts, (void*)c->a_map, (void*)c->a_list, (void*)c->a_cnt})
+    for (void* p : {(void*)c->a_est, (void*)c->a_counts, (void*)c->a_map, (void*)c->a_list, (void*)c->a_cnt,
+                    (void*)c->sort_order, (void*)c->sort_counts})
         if (p) hipFree(p);
     if (c->host_cnt) hipHostFree(c->host_cnt);
     for (auto& e : c->ev)
@@ -822,6 +827,11 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     const bool qn = use_pool && c->has_qnodes && !(rd->flags & PT_RENDER_NODES_FULL) &&
                     ((rd->flags & PT_RENDER_NODES_QUANTIZED) || c->node_format != PT_NODES_FULL);
     const bool timing = (rd->flags & PT_RENDER_TIMING) != 0;
+    const bool sort = (rd->flags & PT_RENDER_SORT_MATERIAL) != 0;
+    if (sort) {
+        if ((st = ensure(c, &c->sort_order, c->sort_order_cap, paths)) != PT_OK) return st;
+        if ((st = ensure(c, &c->sort_counts, c->sort_counts_cap, PT_SORT_BINS)) != PT_OK) return st;
+    }
     hipStream_t sm = c->stream;
     HIPCHK(c, hipMemsetAsync(c->counters, 0, (CNT_SHARDS + 1) * CNT_COUNT * 8, sm));
     // the sample-id counter sits on its own line after the work-counter shards
@@ -901,6 +911,15 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                                    c->counters);
             }
             if (timing) HIPCHK(c, hipEventRecord(ev[1], sm));
+            if (sort) {  // bin this bounce's paths by hit material (k_sort_*), shade in that order
+                HIPCHK(c, hipMemsetAsync(c->sort_counts, 0, PT_SORT_BINS * 4, sm));
+                hipLaunchKernelGGL(k_sort_count, gs, dim3(256), 0, sm, (const uint32_t*)in, (const float4*)c->hit,
+                                   c->sort_counts);
+                hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(PT_SORT_BINS), 0, sm, c->sort_counts);
+                hipLaunchKernelGGL(k_sort_scatter, gs, dim3(256), 0, sm, (const uint32_t*)in, (const float4*)c->hit,
+                                   c->sort_counts, c->sort_order);
+                R.order = c->sort_order;
+            }
             if (rd->integrator == PT_INTEGRATOR_SIMPLE)
                 hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_SIMPLE>, gs, dim3(256), 0, sm, R, cur,
                                    (const uint32_t*)(in + Q_NEXT), (const float4*)c->hit, nxt, c->sample_L,

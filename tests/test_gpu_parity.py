@@ -365,6 +365,16 @@ def test_gpu_pool_and_simple_traversal_agree_bit_for_bit(name, nodes):
     np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("name", ["zoo", "sanmiguel", "lit_instances", "fog"])
+def test_gpu_material_sorted_shading_is_identical(name):
+    """PT_RENDER_SORT_MATERIAL only changes which lane shades which path: the
+    per-sample radiance is bit-identical to the unsorted wavefront."""
+    setup, integ, fx = load(name)
+    a = integ.RenderSamples(flags=N.PT_RENDER_SORT_MATERIAL)
+    b = integ.RenderSamples()
+    np.testing.assert_array_equal(a, b)
+
+
 # ---------------------------------------------------------------- film resolve (pt_film_resolve)
 @pytest.mark.parametrize("film", ["example1", "cornell_c3", "fog", "sanmiguel", "synthetic"])
 @pytest.mark.parametrize("tonemap,key", [("reinhard_jodie", "jodie"), ("aces", "aces")])
