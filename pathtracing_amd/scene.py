@@ -435,14 +435,58 @@ class AreaLight(Light):
         return self.shape
 
     def PreProcess(self, bbox):
-        """Light.cpp:277-287 for solid emission: (1|2) * Area * luminance(E)."""
+        """AreaLight::PreProcess (Light.cpp:277-287): (1|2) * Area *
+        luminance(mean emission over 16 x 16 samples of the shape).  A solid
+        emission is that colour exactly; a textured one is averaged at
+        stratified points with a fixed jitter hash (the reference's sampler
+        there is a fresh, never-started StratifiedSampler with unseeded
+        jitter: its estimate is random, this one deterministic)."""
         tex = self.emissiveTexture
         if isinstance(tex, SolidColor):
             e = (tex.colorScale * tex.albedo).astype(np.float32)
         else:
-            raise NotImplementedError("area light power for non-solid emission is computed by the caller")
+            e = self._mean_emission(tex)
         area = self.shape_area()
         self.cachedPower = float(f32((1 if self.oneSided else 2) * area * luminance(e)))
+
+    def _mean_emission(self, tex) -> np.ndarray:
+        # the reference's fresh StratifiedSampler(16, 16): never started, so
+        # call k draws stratum PermutationElement(0, 256, Hash(0u, 0u, 2k))
+        # (Sampler.hpp:98-110, Util.hpp:44-175) -- a fixed set of strata,
+        # with repeats -- plus unseeded jitter, here a fixed hash
+        k = np.arange(256)
+        strata = np.array([_permutation_element(0, 256, _ref_hash_u32x2_u64(0, 0, 2 * i) & 0xFFFFFFFF)
+                           for i in range(256)])
+        h = (k * 2654435761 + 0x5EED) & 0xFFFFFFFF
+        jx = ((h * 747796405 + 2891336453) & 0xFFFFFF) / 16777216.0
+        jy = ((h * 277803737 + 1442695041) & 0xFFFFFF) / 16777216.0
+        u0 = ((strata % 16) + jx) / 16.0
+        u1 = ((strata // 16) + jy) / 16.0
+        u, v = self._sample_uv(u0.astype(np.float32), u1.astype(np.float32))
+        return _tex_eval_np(tex, u, v).mean(0)
+
+    def _sample_uv(self, u0, u1):
+        """uv of Shape::Sample(u) (Shape.cpp:74-81, 277-297; Shape.hpp:139-141)."""
+        if self.tri is not None:
+            mesh, t = self.tri
+            i0, i1, i2 = (int(x) for x in mesh.indices[3 * t:3 * t + 3])
+            uv = mesh.texCoords
+            w = 1.0 - u0 - u1  # not folded (SURVEY A.6)
+            uu = u0 * uv[i1, 0] + u1 * uv[i2, 0] + w * uv[i0, 0]
+            vv = u0 * uv[i1, 1] + u1 * uv[i2, 1] + w * uv[i0, 1]
+            return uu, vv
+        if isinstance(self.shape, SphereShape):
+            z = 1.0 - 2.0 * u0
+            r = np.sqrt(np.maximum(0.0, 1.0 - z * z))
+            phi = 2.0 * np.pi * u1
+            d = np.stack([r * np.cos(phi), r * np.sin(phi), z], 1)
+            p = self.shape.center + self.shape.radius * d  # GetSphereUV of the point itself (Shape.cpp:80)
+            d = p / np.linalg.norm(p, axis=1, keepdims=True)
+            theta = np.arccos(np.clip(d[:, 1], -1, 1))
+            ph = np.arctan2(d[:, 2], d[:, 0])
+            ph = np.where(ph < 0, ph + 2 * np.pi, ph)
+            return ph / (2 * np.pi), theta / np.pi
+        return np.zeros_like(u0), np.zeros_like(u0)  # QuadShape::Sample leaves uv at 0
 
     def shape_area(self) -> float:
         if self.tri is not None:
@@ -456,6 +500,72 @@ class AreaLight(Light):
 
     def Power(self) -> float:
         return self.cachedPower
+
+
+_M64 = 0xFFFFFFFFFFFFFFFF
+
+
+def _ref_hash_u32x2_u64(a: int, b: int, c: int) -> int:
+    """Hash(unsigned, unsigned, uint64_t) (Util.hpp:162-170): MurmurHash64A
+    over the 16 packed bytes, seed 0."""
+    m, r = 0xC6A4A7935BD1E995, 47
+    h = (0 ^ (16 * m)) & _M64
+    for k in (a | (b << 32), c):
+        k = (k * m) & _M64
+        k ^= k >> r
+        k = (k * m) & _M64
+        h ^= k
+        h = (h * m) & _M64
+    h ^= h >> r
+    h = (h * m) & _M64
+    h ^= h >> r
+    return h
+
+
+def _permutation_element(i: int, l: int, p: int) -> int:
+    """PermutationElement (Util.hpp:44-72), uint32 arithmetic."""
+    M = 0xFFFFFFFF
+    w = l - 1
+    for sh in (1, 2, 4, 8, 16):
+        w |= w >> sh
+    while True:
+        i ^= p; i = (i * 0xE170893D) & M; i ^= p >> 16; i ^= (i & w) >> 4; i ^= p >> 8
+        i = (i * 0x0929EB3F) & M; i ^= p >> 23; i ^= (i & w) >> 1; i = (i * (1 | p >> 27)) & M
+        i = (i * 0x6935FA69) & M; i ^= (i & w) >> 11; i = (i * 0x74DCB303) & M; i ^= (i & w) >> 2
+        i = (i * 0x9E501CC3) & M; i ^= (i & w) >> 2; i = (i * 0xC860A3DF) & M; i &= w; i ^= i >> 5
+        if i < l:
+            break
+    return (i + p) % l
+
+
+def _tex_eval_np(tex, u, v) -> np.ndarray:
+    """Texture::Evaluate at arrays of uv (host estimate for PreProcess):
+    SolidColor, CheckerTexture, ImageTexture (u8 / 255), FloatImageTexture,
+    bilinear with repeat wrap (Texture.hpp:128-207)."""
+    u = np.asarray(u, np.float64)
+    v = np.asarray(v, np.float64)
+    cs = np.asarray(tex.colorScale, np.float64)
+    if isinstance(tex, SolidColor):
+        return np.broadcast_to(cs * tex.albedo, (u.shape[0], 3)).astype(np.float64)
+    if isinstance(tex, CheckerTexture):
+        ux = np.floor(u * tex.invScale[0]).astype(np.int64)
+        uy = np.floor(v * tex.invScale[1]).astype(np.int64)
+        a, b = _tex_eval_np(tex.tex1, u, v), _tex_eval_np(tex.tex2, u, v)
+        return cs * np.where(((ux + uy) % 2 == 0)[:, None], a, b)
+    data = tex.data.astype(np.float64)
+    if isinstance(tex, ImageTexture):
+        data = data / 255.0
+    h, w = data.shape[:2]
+    x, y = u * w - 0.5, v * h - 0.5
+    xi, yi = np.floor(x).astype(np.int64), np.floor(y).astype(np.int64)
+    dx, dy = (x - xi)[:, None], (y - yi)[:, None]
+
+    def tx(a, b):
+        px = data[np.mod(b, h), np.mod(a, w)]
+        return px[:, :3] if px.shape[1] >= 3 else np.repeat(px[:, :1], 3, 1)
+    r = ((1 - dx) * (1 - dy) * tx(xi, yi) + dx * (1 - dy) * tx(xi + 1, yi) + (1 - dx) * dy * tx(xi, yi + 1) +
+         dx * dy * tx(xi + 1, yi + 1))
+    return cs * r
 
 
 class InfiniteLight(Light):

@@ -278,6 +278,26 @@ def envmap(W: int = 256, H: int = 256, spp: int = 16, max_depth: int = 8, seed: 
     return SceneSetup(scene, s.camera, integrator, PowerLightSampler(), max_depth, seed, spp).finish()
 
 
+def textured_emitters(W: int = 32, H: int = 32, spp: int = 4, seed: int = 0x5EED0081) -> SceneSetup:
+    """Area lights with textured emission (AreaLight::PreProcess averages the
+    emissive texture over its shape, Light.cpp:277-287): an image-textured
+    quad, a checker-emission sphere and an image-textured emissive mesh in the
+    C2 room; PowerLightSampler."""
+    rng = np.random.default_rng(81)
+    s = cornell(W=W, H=H, spp=spp, config="c2", seed=seed)
+    scene = s.scene
+    img = _noise_img(rng, 16, 16, 3, lo=40, hi=255, smooth=2)
+    ql = AreaLight(QuadShape((-0.6, -0.9, -0.6), (0.3, 0, 0), (0, 0.2, 0.1)), ImageTexture(img, True, (6, 5, 4)), True)
+    scene.Add(GeometricPrimitive(ql.getShape(), MicrofacetDiffuse((0.5, 0.5, 0.5)), ql))
+    sl = AreaLight(SphereShape((0.5, -0.2, 0.4), 0.12),
+                   CheckerTexture(SolidColor((4, 4, 3)), SolidColor((0.5, 0.5, 2)), (0.1, 0.2)), False)
+    scene.Add(GeometricPrimitive(sl.getShape(), MicrofacetDiffuse((0.9, 0.9, 0.9)), sl))
+    bi, bv, bn, buv = _box((-0.3, 0.5, -0.4), (0.2, 0.2, 0.2), 0.4)
+    scene.Add(Model([Mesh(bi, bv, None, bn, buv, MicrofacetDiffuse((0.8, 0.8, 0.8)),
+                          ImageTexture(_noise_img(rng, 8, 8, 3, lo=100, hi=255, smooth=1), False, (3, 3, 3)))]))
+    return SceneSetup(scene, s.camera, "path", PowerLightSampler(), 8, seed, spp).finish()
+
+
 def blend_box(W: int = 64, H: int = 64, spp: int = 16, max_depth: int = 8, alpha: float = 0.35,
               seed: int = 0x5EED0041) -> SceneSetup:
     """C3 Cornell box behind a see-through panel: a two-triangle mesh with a

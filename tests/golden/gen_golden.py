@@ -247,6 +247,23 @@ def gen_c4_band(tmp: Path):
     print(f"c4_band: {(OUT / 'c4_band.npz').stat().st_size / 1024:.0f} KiB")
 
 
+def gen_emission_power(tmp: Path):
+    """AreaLight::PreProcess's Power() with textured emission (Light.cpp:
+    277-287), by the reference (ref_harness info, 5 runs: its jittered
+    estimate is random), for scenes.textured_emitters."""
+    setup = scenes.textured_emitters()
+    d = tmp / "emission"
+    recipe = write_recipe(d, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
+                          setup.max_depth, setup.light_sampler, setup.extra_lights)
+    runs = []
+    for r in range(5):
+        harness(recipe, "info", d / f"o{r}")
+        runs.append([float(ln.split()[2]) for ln in Path(f"{d}/o{r}.lights.txt").read_text().splitlines()
+                     if not ln.startswith("sample")])
+    np.savez_compressed(OUT / "emission_power.npz", power=np.array(runs, np.float64))
+    print(f"emission_power: {len(runs[0])} lights x 5 runs")
+
+
 def gen_envmap(tmp: Path):
     """TextureInfiniteLight (Light.cpp:110-200) through the reference: Le(dir)
     and PDF(dir) for a spread of directions and Power(), ref_harness `envle`
@@ -318,6 +335,8 @@ def main(names=None):
             gen_envmap(Path(t))
         if not names or "c4_band" in names:
             gen_c4_band(Path(t))
+        if not names or "emission_power" in names:
+            gen_emission_power(Path(t))
 
 
 if __name__ == "__main__":
