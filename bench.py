@@ -210,6 +210,10 @@ def main():
                     help="node layout of the pool traversal (auto: 64-B quantized nodes)")
     ap.add_argument("--sort-material", action="store_true",
                     help="shade each bounce binned by hit material (PT_RENDER_SORT_MATERIAL)")
+    ap.add_argument("--sort-spatial", action="store_true",
+                    help="shade each bounce binned by the hit point's cell (PT_RENDER_SORT_SPATIAL; "
+                         "the library's default for large scenes)")
+    ap.add_argument("--no-sort", action="store_true", help="no hit sort before shading (PT_RENDER_NO_SORT)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the instrumented node-count pass")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -250,6 +254,10 @@ def main():
     tflag |= {"auto": 0, "full": N.PT_RENDER_NODES_FULL, "quant": N.PT_RENDER_NODES_QUANTIZED}[args.nodes]
     if args.sort_material:
         tflag |= N.PT_RENDER_SORT_MATERIAL
+    if args.sort_spatial:
+        tflag |= N.PT_RENDER_SORT_SPATIAL
+    if args.no_sort:
+        tflag |= N.PT_RENDER_NO_SORT
 
     def step(flags=0):
         # this rank's sample shard into the device film, then the RCCL SUM

@@ -257,6 +257,9 @@ enum { PT_FILTER_MITCHELL = 0, PT_FILTER_BOX = 1, PT_FILTER_GAUSSIAN = 2 };
 #define PT_RENDER_NODES_QUANTIZED 0x20u /* ... over the 64-B quantized nodes (the default)  */
 #define PT_RENDER_ADAPTIVE 0x40u        /* pt_render: TileIntegrator::Render's adaptive rounds */
 #define PT_RENDER_SORT_MATERIAL 0x80u   /* shade each bounce's paths binned by hit material */
+#define PT_RENDER_SORT_SPATIAL 0x100u   /* ... binned by the hit point's cell (16^3 Morton grid);
+                                         * the default for large scenes (pool traversal) */
+#define PT_RENDER_NO_SORT 0x200u        /* no hit sort (shade in path order) */
 
 typedef struct pt_render_desc {
     uint32_t integrator;       /* PT_INTEGRATOR_*                               */

@@ -112,13 +112,19 @@ struct AdaptEst {
 };
 #define PT_ADAPT_MAX_ROUNDS 128   // while (Samples() < 128 * samplesPerPixel)
 #define PT_ADAPT_REL_VAR 1.5      // minRelativeVariance
-// Material / hit-state binning of a bounce's paths before shading
-// (PT_RENDER_SORT_MATERIAL): bin 0 = miss, 1 + material % 254 for a hit,
-// 255 for hits inside instances; counting sort into `order`.
-#define PT_SORT_BINS 256
-__global__ void k_sort_count(const uint32_t* nptr, const float4* hit, uint32_t* counts);
+// Hit-state binning of a bounce's paths before shading
+// (PT_RENDER_SORT_MATERIAL / PT_RENDER_SORT_SPATIAL): counting sort into
+// RenderParams::order.  Material: bin 0 = miss, 1 + material % 254, 255 for
+// hits inside instances.  Spatial: the hit point's 16^3 Morton cell.
+enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1 };
+#define PT_SORT_BINS_MATERIAL 256
+#define PT_SORT_BINS_SPATIAL 4096
+template <int KEY, int NB>
+__global__ void k_sort_count(PathSoA cur, const uint32_t* nptr, const float4* hit, uint32_t* counts);
+template <int NB>
 __global__ void k_sort_scan(uint32_t* counts);
-__global__ void k_sort_scatter(const uint32_t* nptr, const float4* hit, uint32_t* offsets, uint32_t* order);
+template <int KEY, int NB>
+__global__ void k_sort_scatter(PathSoA cur, const uint32_t* nptr, const float4* hit, uint32_t* offsets, uint32_t* order);
 __global__ void k_adapt_init(RenderParams R, uint32_t shard_index, uint32_t shard_count, uint32_t* list,
                              uint32_t* cnt, AdaptEst* est, uint32_t* counts);
 __global__ void k_adapt_map(const uint32_t* list, const uint32_t* n, int32_t* map);

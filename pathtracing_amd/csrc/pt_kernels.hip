@@ -1258,67 +1258,115 @@ __global__ __launch_bounds__(256) void k_resolve(const double* __restrict__ film
     }
 }
 
-// ------------------------------------------------------------------ material sort
+// ------------------------------------------------------------------ hit sort
 // north_star "sort of active rays by material and hit state": the paths of a
-// bounce are binned by what they hit (miss / the hit primitive's material)
-// and k_shade walks them bin by bin, so a wave shades one material (one
-// branch of the material code, one texture) at a time.  A counting sort:
-// per-block LDS histograms folded into 256 global counters, one exclusive
-// scan, then a scatter that reserves each block's range of every bin with one
-// atomic.  Per-path results do not depend on the order (each path and sample
-// is computed on its own), only the schedule does.
-__device__ __forceinline__ uint32_t sort_bin(const float4* __restrict__ hit, uint32_t i) {
-    const int prim = __float_as_int(hit[i].w);
+// bounce are binned by what they hit and k_shade walks them bin by bin.
+// KEY = PT_SORT_MATERIAL: miss / the hit primitive's material (one branch of
+// the material code, one texture per wave); KEY = PT_SORT_SPATIAL: miss /
+// the hit point's cell in a 16x16x16 Morton grid over the scene box (the
+// shading gathers of nearby triangles, and the next bounce's and the shadow
+// rays' origins -- appended in shading order -- stay together).  A counting
+// sort: per-block LDS histograms folded into global counters, one scan, then
+// a scatter that reserves each block's range of every bin with one atomic.
+// Per-path results do not depend on the order, only the schedule does.
+template <int KEY>
+__device__ __forceinline__ uint32_t sort_bin(const PathSoA& cur, uint32_t front, const float4* __restrict__ hit,
+                                             uint32_t i) {
+    const float4 h = hit[i];
+    const int prim = __float_as_int(h.w);
     if (prim < 0) return 0u;
-    if ((uint32_t)prim >= S.n_prims) return PT_SORT_BINS - 1u;  // a virtual slot inside an instance
-    const int mat = S.info[prim].material;
-    return mat < 0 ? 0u : 1u + (uint32_t)mat % (PT_SORT_BINS - 2u);
+    if (KEY == PT_SORT_MATERIAL) {
+        if ((uint32_t)prim >= S.n_prims) return PT_SORT_BINS_MATERIAL - 1u;  // a virtual slot inside an instance
+        const int mat = S.info[prim].material;
+        return mat < 0 ? 0u : 1u + (uint32_t)mat % (PT_SORT_BINS_MATERIAL - 2u);
+    }
+    const uint32_t e = path_slot(i, front, cur.cap);
+    const f3 o = xyz(cur.o[e]), d = xyz(cur.d[e]);
+    const float t = h.x;
+    uint32_t code = 0;
+    const float p[3] = {fmaf(t, d.x, o.x), fmaf(t, d.y, o.y), fmaf(t, d.z, o.z)};
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const float q = (p[a] - S.bb_lo[a]) * S.bb_scale[a];  // [0, 16)
+        const uint32_t c = (uint32_t)fminf(fmaxf(q, 0.0f), 15.0f);
+#pragma unroll
+        for (int b = 0; b < 4; b++) code |= ((c >> b) & 1u) << (3 * b + a);
+    }
+    return code;
 }
-__global__ __launch_bounds__(256) void k_sort_count(const uint32_t* __restrict__ nptr, const float4* __restrict__ hit,
-                                                   uint32_t* __restrict__ counts) {
-    __shared__ uint32_t h[PT_SORT_BINS];
-    const uint32_t n = path_count(nptr);
+template <int KEY, int NB>
+__global__ __launch_bounds__(256) void k_sort_count(PathSoA cur, const uint32_t* __restrict__ nptr,
+                                                   const float4* __restrict__ hit, uint32_t* __restrict__ counts) {
+    __shared__ uint32_t h[NB];
+    const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
     if (blockIdx.x * 256 >= n) return;
-    h[threadIdx.x] = 0;
+    for (int b = threadIdx.x; b < NB; b += 256) h[b] = 0;
     __syncthreads();
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-    if (t < n) atomicAdd(&h[sort_bin(hit, t)], 1u);
+    if (t < n) atomicAdd(&h[sort_bin<KEY>(cur, front, hit, t)], 1u);
     __syncthreads();
-    if (h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
+    for (int b = threadIdx.x; b < NB; b += 256)
+        if (h[b]) atomicAdd(&counts[b], h[b]);
 }
+template <int NB>
 __global__ __launch_bounds__(256) void k_sort_scan(uint32_t* __restrict__ counts) {  // one block
-    __shared__ uint32_t v[PT_SORT_BINS];
-    v[threadIdx.x] = counts[threadIdx.x];
+    constexpr int PER = NB / 256;
+    __shared__ uint32_t part[256];
+    uint32_t v[PER], acc = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        v[k] = counts[threadIdx.x * PER + k];
+        acc += v[k];
+    }
+    part[threadIdx.x] = acc;
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (int b = 0; b < PT_SORT_BINS; b++) {
-            const uint32_t c = v[b];
-            v[b] = acc;
-            acc += c;
+        uint32_t run = 0;
+        for (int b = 0; b < 256; b++) {
+            const uint32_t c = part[b];
+            part[b] = run;
+            run += c;
         }
     }
     __syncthreads();
-    counts[threadIdx.x] = v[threadIdx.x];
+    uint32_t run = part[threadIdx.x];
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        counts[threadIdx.x * PER + k] = run;
+        run += v[k];
+    }
 }
-__global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict__ nptr, const float4* __restrict__ hit,
-                                                     uint32_t* __restrict__ offsets, uint32_t* __restrict__ order) {
-    __shared__ uint32_t h[PT_SORT_BINS], base[PT_SORT_BINS];
-    const uint32_t n = path_count(nptr);
+template <int KEY, int NB>
+__global__ __launch_bounds__(256) void k_sort_scatter(PathSoA cur, const uint32_t* __restrict__ nptr,
+                                                     const float4* __restrict__ hit, uint32_t* __restrict__ offsets,
+                                                     uint32_t* __restrict__ order) {
+    __shared__ uint32_t h[NB], base[NB];
+    const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
     if (blockIdx.x * 256 >= n) return;
-    h[threadIdx.x] = 0;
+    for (int b = threadIdx.x; b < NB; b += 256) h[b] = 0;
     __syncthreads();
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
     uint32_t bin = 0, rank = 0;
     if (t < n) {
-        bin = sort_bin(hit, t);
+        bin = sort_bin<KEY>(cur, front, hit, t);
         rank = atomicAdd(&h[bin], 1u);
     }
     __syncthreads();
-    if (h[threadIdx.x]) base[threadIdx.x] = atomicAdd(&offsets[threadIdx.x], h[threadIdx.x]);
+    for (int b = threadIdx.x; b < NB; b += 256)
+        if (h[b]) base[b] = atomicAdd(&offsets[b], h[b]);
     __syncthreads();
     if (t < n) order[base[bin] + rank] = t;
 }
+template __global__ void k_sort_count<PT_SORT_MATERIAL, PT_SORT_BINS_MATERIAL>(PathSoA, const uint32_t*, const float4*,
+                                                                             uint32_t*);
+template __global__ void k_sort_count<PT_SORT_SPATIAL, PT_SORT_BINS_SPATIAL>(PathSoA, const uint32_t*, const float4*,
+                                                                           uint32_t*);
+template __global__ void k_sort_scan<PT_SORT_BINS_MATERIAL>(uint32_t*);
+template __global__ void k_sort_scan<PT_SORT_BINS_SPATIAL>(uint32_t*);
+template __global__ void k_sort_scatter<PT_SORT_MATERIAL, PT_SORT_BINS_MATERIAL>(PathSoA, const uint32_t*,
+                                                                               const float4*, uint32_t*, uint32_t*);
+template __global__ void k_sort_scatter<PT_SORT_SPATIAL, PT_SORT_BINS_SPATIAL>(PathSoA, const uint32_t*, const float4*,
+                                                                             uint32_t*, uint32_t*);
 
 // ------------------------------------------------------------------ adaptive sampling
 // TileIntegrator::Render (Integrators.cpp:55-86): each pixel takes rounds of

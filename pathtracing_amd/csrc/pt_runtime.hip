@@ -599,6 +599,30 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
 #undef UP
     DS.root = roots[0];
     DS.n_prims = s->n_prims;
+    {  // scene box from the TLAS root cluster's child boxes (spatial hit sort)
+        float lo[3] = {0, 0, 0}, hi[3] = {1, 1, 1};
+        const pt_bvh_desc& T = s->bvhs[0];
+        if (T.root.count == 0 && T.n_clusters > 0 && T.root.cluster_idx < T.n_clusters) {
+            const pt_ref_bvh4_cluster& cl = T.clusters[T.root.cluster_idx];
+            const float* mn[3] = {cl.xmin, cl.ymin, cl.zmin};
+            const float* mx[3] = {cl.xmax, cl.ymax, cl.zmax};
+            bool any = false;
+            for (int k = 0; k < 4; k++) {
+                bool ok = true;
+                for (int a = 0; a < 3; a++) ok = ok && std::isfinite(mn[a][k]) && std::isfinite(mx[a][k]) && mn[a][k] <= mx[a][k];
+                if (!ok) continue;
+                for (int a = 0; a < 3; a++) {
+                    lo[a] = any ? std::min(lo[a], mn[a][k]) : mn[a][k];
+                    hi[a] = any ? std::max(hi[a], mx[a][k]) : mx[a][k];
+                }
+                any = true;
+            }
+        }
+        for (int a = 0; a < 3; a++) {
+            DS.bb_lo[a] = lo[a];
+            DS.bb_scale[a] = hi[a] > lo[a] ? 16.0f / (hi[a] - lo[a]) : 0.0f;
+        }
+    }
     DS.n_nodes = (uint32_t)nodes.size();
     DS.n_texel_bytes = s->n_texel_bytes;
     DS.n_lights = s->n_lights;
@@ -827,10 +851,15 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     const bool qn = use_pool && c->has_qnodes && !(rd->flags & PT_RENDER_NODES_FULL) &&
                     ((rd->flags & PT_RENDER_NODES_QUANTIZED) || c->node_format != PT_NODES_FULL);
     const bool timing = (rd->flags & PT_RENDER_TIMING) != 0;
-    const bool sort = (rd->flags & PT_RENDER_SORT_MATERIAL) != 0;
-    if (sort) {
+    // hit sort before shading: spatial by default for large scenes (C4 at 256
+    // spp: 897 -> 949 Mrays/s, profiles/r02_ab_sort.txt), off for small ones
+    // (the three passes cost ~0.1 ms a bounce, more than a small scene gains)
+    const bool sort_mat = (rd->flags & PT_RENDER_SORT_MATERIAL) != 0;
+    const bool sort_sp = !sort_mat && !(rd->flags & PT_RENDER_NO_SORT) &&
+                         ((rd->flags & PT_RENDER_SORT_SPATIAL) || big_scene);
+    if (sort_mat || sort_sp) {
         if ((st = ensure(c, &c->sort_order, c->sort_order_cap, paths)) != PT_OK) return st;
-        if ((st = ensure(c, &c->sort_counts, c->sort_counts_cap, PT_SORT_BINS)) != PT_OK) return st;
+        if ((st = ensure(c, &c->sort_counts, c->sort_counts_cap, PT_SORT_BINS_SPATIAL)) != PT_OK) return st;
     }
     hipStream_t sm = c->stream;
     HIPCHK(c, hipMemsetAsync(c->counters, 0, (CNT_SHARDS + 1) * CNT_COUNT * 8, sm));
@@ -911,13 +940,23 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                                    c->counters);
             }
             if (timing) HIPCHK(c, hipEventRecord(ev[1], sm));
-            if (sort) {  // bin this bounce's paths by hit material (k_sort_*), shade in that order
-                HIPCHK(c, hipMemsetAsync(c->sort_counts, 0, PT_SORT_BINS * 4, sm));
-                hipLaunchKernelGGL(k_sort_count, gs, dim3(256), 0, sm, (const uint32_t*)in, (const float4*)c->hit,
-                                   c->sort_counts);
-                hipLaunchKernelGGL(k_sort_scan, dim3(1), dim3(PT_SORT_BINS), 0, sm, c->sort_counts);
-                hipLaunchKernelGGL(k_sort_scatter, gs, dim3(256), 0, sm, (const uint32_t*)in, (const float4*)c->hit,
-                                   c->sort_counts, c->sort_order);
+            if (sort_mat) {  // bin this bounce's paths by hit material (k_sort_*), shade in that order
+                constexpr int NB = PT_SORT_BINS_MATERIAL;
+                HIPCHK(c, hipMemsetAsync(c->sort_counts, 0, NB * 4, sm));
+                hipLaunchKernelGGL((k_sort_count<PT_SORT_MATERIAL, NB>), gs, dim3(256), 0, sm, cur, (const uint32_t*)in,
+                                   (const float4*)c->hit, c->sort_counts);
+                hipLaunchKernelGGL((k_sort_scan<NB>), dim3(1), dim3(256), 0, sm, c->sort_counts);
+                hipLaunchKernelGGL((k_sort_scatter<PT_SORT_MATERIAL, NB>), gs, dim3(256), 0, sm, cur,
+                                   (const uint32_t*)in, (const float4*)c->hit, c->sort_counts, c->sort_order);
+                R.order = c->sort_order;
+            } else if (sort_sp) {  // ... by the hit point's Morton cell
+                constexpr int NB = PT_SORT_BINS_SPATIAL;
+                HIPCHK(c, hipMemsetAsync(c->sort_counts, 0, NB * 4, sm));
+                hipLaunchKernelGGL((k_sort_count<PT_SORT_SPATIAL, NB>), gs, dim3(256), 0, sm, cur, (const uint32_t*)in,
+                                   (const float4*)c->hit, c->sort_counts);
+                hipLaunchKernelGGL((k_sort_scan<NB>), dim3(1), dim3(256), 0, sm, c->sort_counts);
+                hipLaunchKernelGGL((k_sort_scatter<PT_SORT_SPATIAL, NB>), gs, dim3(256), 0, sm, cur,
+                                   (const uint32_t*)in, (const float4*)c->hit, c->sort_counts, c->sort_order);
                 R.order = c->sort_order;
             }
             if (rd->integrator == PT_INTEGRATOR_SIMPLE)

@@ -366,12 +366,13 @@ def test_gpu_pool_and_simple_traversal_agree_bit_for_bit(name, nodes):
 
 
 @pytest.mark.parametrize("name", ["zoo", "sanmiguel", "lit_instances", "fog"])
-def test_gpu_material_sorted_shading_is_identical(name):
-    """PT_RENDER_SORT_MATERIAL only changes which lane shades which path: the
-    per-sample radiance is bit-identical to the unsorted wavefront."""
+@pytest.mark.parametrize("flag", [N.PT_RENDER_SORT_MATERIAL, N.PT_RENDER_SORT_SPATIAL])
+def test_gpu_hit_sorted_shading_is_identical(name, flag):
+    """PT_RENDER_SORT_MATERIAL / _SPATIAL only change which lane shades which
+    path: the per-sample radiance is bit-identical to the unsorted wavefront."""
     setup, integ, fx = load(name)
-    a = integ.RenderSamples(flags=N.PT_RENDER_SORT_MATERIAL)
-    b = integ.RenderSamples()
+    a = integ.RenderSamples(flags=flag)
+    b = integ.RenderSamples(flags=N.PT_RENDER_NO_SORT)
     np.testing.assert_array_equal(a, b)
 
 
