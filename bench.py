@@ -214,6 +214,8 @@ def main():
                     help="shade each bounce binned by the hit point's cell (PT_RENDER_SORT_SPATIAL; "
                          "the library's default for large scenes)")
     ap.add_argument("--no-sort", action="store_true", help="no hit sort before shading (PT_RENDER_NO_SORT)")
+    ap.add_argument("--sort-rays", action="store_true",
+                    help="trace closest-hit rays in origin-cell + octant order (PT_RENDER_SORT_RAYS)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the instrumented node-count pass")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -258,6 +260,8 @@ def main():
         tflag |= N.PT_RENDER_SORT_SPATIAL
     if args.no_sort:
         tflag |= N.PT_RENDER_NO_SORT
+    if args.sort_rays:
+        tflag |= N.PT_RENDER_SORT_RAYS
 
     def step(flags=0):
         # this rank's sample shard into the device film, then the RCCL SUM

@@ -260,6 +260,7 @@ enum { PT_FILTER_MITCHELL = 0, PT_FILTER_BOX = 1, PT_FILTER_GAUSSIAN = 2 };
 #define PT_RENDER_SORT_SPATIAL 0x100u   /* ... binned by the hit point's cell (16^3 Morton grid);
                                          * the default for large scenes (pool traversal) */
 #define PT_RENDER_NO_SORT 0x200u        /* no hit sort (shade in path order) */
+#define PT_RENDER_SORT_RAYS 0x400u      /* trace closest-hit rays in origin-cell + octant order */
 
 typedef struct pt_render_desc {
     uint32_t integrator;       /* PT_INTEGRATOR_*                               */

@@ -116,7 +116,7 @@ struct AdaptEst {
 // (PT_RENDER_SORT_MATERIAL / PT_RENDER_SORT_SPATIAL): counting sort into
 // RenderParams::order.  Material: bin 0 = miss, 1 + material % 254, 255 for
 // hits inside instances.  Spatial: the hit point's 16^3 Morton cell.
-enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1 };
+enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1, PT_SORT_RAYS = 2 };
 #define PT_SORT_BINS_MATERIAL 256
 #define PT_SORT_BINS_SPATIAL 4096
 template <int KEY, int NB>

@@ -159,15 +159,17 @@ struct ClosestSrc {
     PathSoA P;
     float4* hit;
     uint32_t front;  // continuing paths at the front of P
+    // S.ray_order (PT_RENDER_SORT_RAYS): claim i traces path ray_order[i]
     __device__ __forceinline__ bool load(uint32_t i, f3& o, f3& d, float& tmax) {
-        const uint32_t e = path_slot(i, front, P.cap);
+        const uint32_t j = S.ray_order ? S.ray_order[i] : i;
+        const uint32_t e = path_slot(j, front, P.cap);
         o = xyz(P.o[e]);
         d = xyz(P.d[e]);
         tmax = __int_as_float(0x7f800000);
         return true;
     }
     __device__ __forceinline__ void closest(uint32_t i, float t, float b1, float b2, int prim) {
-        hit[i] = make_float4(t, b1, b2, __int_as_float(prim));
+        hit[S.ray_order ? S.ray_order[i] : i] = make_float4(t, b1, b2, __int_as_float(prim));
     }
     __device__ __forceinline__ void any(uint32_t, bool) {}
 };
@@ -1272,6 +1274,20 @@ __global__ __launch_bounds__(256) void k_resolve(const double* __restrict__ film
 template <int KEY>
 __device__ __forceinline__ uint32_t sort_bin(const PathSoA& cur, uint32_t front, const float4* __restrict__ hit,
                                              uint32_t i) {
+    if (KEY == PT_SORT_RAYS) {  // the ray's origin cell (8^3 Morton) and direction octant
+        const uint32_t e = path_slot(i, front, cur.cap);
+        const f3 o = xyz(cur.o[e]), d = xyz(cur.d[e]);
+        const float p[3] = {o.x, o.y, o.z};
+        uint32_t code = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            const float q = (p[a] - S.bb_lo[a]) * S.bb_scale[a] * 0.5f;  // [0, 8)
+            const uint32_t c = (uint32_t)fminf(fmaxf(q, 0.0f), 7.0f);
+#pragma unroll
+            for (int b = 0; b < 3; b++) code |= ((c >> b) & 1u) << (3 + 3 * b + a);
+        }
+        return code;
+    }
     const float4 h = hit[i];
     const int prim = __float_as_int(h.w);
     if (prim < 0) return 0u;
@@ -1361,6 +1377,10 @@ template __global__ void k_sort_count<PT_SORT_MATERIAL, PT_SORT_BINS_MATERIAL>(P
                                                                              uint32_t*);
 template __global__ void k_sort_count<PT_SORT_SPATIAL, PT_SORT_BINS_SPATIAL>(PathSoA, const uint32_t*, const float4*,
                                                                            uint32_t*);
+template __global__ void k_sort_count<PT_SORT_RAYS, PT_SORT_BINS_SPATIAL>(PathSoA, const uint32_t*, const float4*,
+                                                                        uint32_t*);
+template __global__ void k_sort_scatter<PT_SORT_RAYS, PT_SORT_BINS_SPATIAL>(PathSoA, const uint32_t*, const float4*,
+                                                                          uint32_t*, uint32_t*);
 template __global__ void k_sort_scan<PT_SORT_BINS_MATERIAL>(uint32_t*);
 template __global__ void k_sort_scan<PT_SORT_BINS_SPATIAL>(uint32_t*);
 template __global__ void k_sort_scatter<PT_SORT_MATERIAL, PT_SORT_BINS_MATERIAL>(PathSoA, const uint32_t*,

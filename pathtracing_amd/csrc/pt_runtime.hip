@@ -71,6 +71,9 @@ struct pt_ctx {
     uint32_t* sort_order = nullptr;
     uint32_t* sort_counts = nullptr;
     uint64_t sort_order_cap = 0, sort_counts_cap = 0;
+    uint32_t* ray_order = nullptr;  // PT_RENDER_SORT_RAYS: closest-hit claim order
+    uint32_t* ray_counts = nullptr;
+    uint64_t ray_order_cap = 0, ray_counts_cap = 0;
     hipEvent_t ev[8] = {};
     hipEvent_t rev[PT_RING][5] = {};  // per in-flight iteration: kernel boundaries [0..2], end [4] ([3] unused)
 };
@@ -201,7 +204,7 @@ extern "C" void pt_destroy(pt_ctx* c) {
     if (c->sample_L) hipFree(c->sample_L);
     if (c->film) hipFree(c->film);
     for (void* p : {(void*)c->a_est, (void*)c->a_counts, (void*)c->a_map, (void*)c->a_list, (void*)c->a_cnt,
-                    (void*)c->sort_order, (void*)c->sort_counts})
+                    (void*)c->sort_order, (void*)c->sort_counts, (void*)c->ray_order, (void*)c->ray_counts})
         if (p) hipFree(p);
     if (c->host_cnt) hipHostFree(c->host_cnt);
     for (auto& e : c->ev)
@@ -854,6 +857,17 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     // hit sort before shading: spatial by default for large scenes (C4 at 256
     // spp: 897 -> 949 Mrays/s, profiles/r02_ab_sort.txt), off for small ones
     // (the three passes cost ~0.1 ms a bounce, more than a small scene gains)
+    const bool sort_rays = (rd->flags & PT_RENDER_SORT_RAYS) != 0;
+    if (sort_rays) {
+        if ((st = ensure(c, &c->ray_order, c->ray_order_cap, paths)) != PT_OK) return st;
+        if ((st = ensure(c, &c->ray_counts, c->ray_counts_cap, PT_SORT_BINS_SPATIAL)) != PT_OK) return st;
+    }
+    c->scene.ray_order = sort_rays ? c->ray_order : nullptr;
+    struct ResetOrder {  // other entry points bind the scene without a claim order
+        pt_ctx* c;
+        ~ResetOrder() { c->scene.ray_order = nullptr; }
+    } reset_order{c};
+    if ((st = bind_scene(c)) != PT_OK) return st;
     const bool sort_mat = (rd->flags & PT_RENDER_SORT_MATERIAL) != 0;
     const bool sort_sp = !sort_mat && !(rd->flags & PT_RENDER_NO_SORT) &&
                          ((rd->flags & PT_RENDER_SORT_SPATIAL) || big_scene);
@@ -933,6 +947,15 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             uint32_t* spare = set[(i + 2) % 3];
             hipEvent_t* ev = c->rev[i % PT_RING];
             if (timing) HIPCHK(c, hipEventRecord(ev[0], sm));
+            if (sort_rays) {  // claim order of this bounce's closest-hit rays: origin cell + octant
+                constexpr int NB = PT_SORT_BINS_SPATIAL;
+                HIPCHK(c, hipMemsetAsync(c->ray_counts, 0, NB * 4, sm));
+                hipLaunchKernelGGL((k_sort_count<PT_SORT_RAYS, NB>), gs, dim3(256), 0, sm, cur, (const uint32_t*)in,
+                                   (const float4*)c->hit, c->ray_counts);
+                hipLaunchKernelGGL((k_sort_scan<NB>), dim3(1), dim3(256), 0, sm, c->ray_counts);
+                hipLaunchKernelGGL((k_sort_scatter<PT_SORT_RAYS, NB>), gs, dim3(256), 0, sm, cur, (const uint32_t*)in,
+                                   (const float4*)c->hit, c->ray_counts, c->ray_order);
+            }
             {
                 auto kc = pick_closest(use_pool, qn, inst, count);
                 hipLaunchKernelGGL(kc, gt, dim3(PT_TRACE_BLOCK), 0, sm, cur, (const uint32_t*)in, c->hit,

@@ -366,7 +366,8 @@ def test_gpu_pool_and_simple_traversal_agree_bit_for_bit(name, nodes):
 
 
 @pytest.mark.parametrize("name", ["zoo", "sanmiguel", "lit_instances", "fog"])
-@pytest.mark.parametrize("flag", [N.PT_RENDER_SORT_MATERIAL, N.PT_RENDER_SORT_SPATIAL])
+@pytest.mark.parametrize("flag", [N.PT_RENDER_SORT_MATERIAL, N.PT_RENDER_SORT_SPATIAL,
+                                  N.PT_RENDER_SORT_RAYS | N.PT_RENDER_TRAVERSAL_POOL])
 def test_gpu_hit_sorted_shading_is_identical(name, flag):
     """PT_RENDER_SORT_MATERIAL / _SPATIAL only change which lane shades which
     path: the per-sample radiance is bit-identical to the unsorted wavefront."""
