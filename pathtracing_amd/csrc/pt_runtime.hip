@@ -715,11 +715,16 @@ static double gauss_h(double x, double sigma) {
 // chunk's per-sample radiance to `on_chunk`.
 // Makes this context's scene the one the kernels read (constant-memory `S`),
 // ordered on the context's stream.  Called by every entry point that launches.
+// Large scenes keep 128 M paths in flight and a whole 1024-spp 1080p frame in
+// one sample chunk (≈ 52 GB of HBM): each traversal launch's tail is
+// amortised over more rays and the spatial hit sort finds more rays per cell
+// (C4: 16 M / 6 GiB 931 -> 64 M / 32 GiB 1015 -> 128 M / 32 GiB 1027 Mrays/s,
+// profiles/r02_ab_c4.txt)
 #ifndef PT_SAMPLE_GIB
-#define PT_SAMPLE_GIB 6
+#define PT_SAMPLE_GIB 32
 #endif
 #ifndef PT_PATHS_POOL
-#define PT_PATHS_POOL (1u << 24)
+#define PT_PATHS_POOL (1u << 27)
 #endif
 #ifndef PT_PATHS_SIMPLE
 #define PT_PATHS_SIMPLE (1u << 21)
@@ -833,9 +838,10 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     uint32_t s_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spp_local, max_floats / per_s));
     pt_status st = ensure(c, &c->sample_L, c->sample_cap, per_s * s_chunk);
     if (st) return st;
-    // wavefront size: large scenes (pool traversal) take 16 M paths in flight,
+    // wavefront size: large scenes (pool traversal) take 128 M paths in flight,
     // so each traversal launch's tail (the last, longest rays) is amortised
-    // over more rays (C4 at 256 spp: 2 M -> 8 M paths +22 %, 8 M -> 16 M +5 %)
+    // over more rays (C4 at 256 spp: 2 M -> 8 M paths +22 %, 8 M -> 16 M +5 %;
+    // with the spatial hit sort at 1024 spp 16 M -> 128 M +10 %)
     const bool big_scene = c->n_clusters >= PT_POOL_MIN_CLUSTERS;
     uint32_t paths = rd->paths_in_flight ? rd->paths_in_flight : (big_scene ? PT_PATHS_POOL : PT_PATHS_SIMPLE);
     paths = (uint32_t)std::min<uint64_t>(paths, std::max<uint64_t>(1, (uint64_t)R.npix_work * s_chunk));
