@@ -78,6 +78,18 @@ struct DevInstance {
     uint32_t virt_base;    // virtual slot of the BLAS's first primitive
 };
 
+// ---- per-triangle shading record (128 B, one cache line): the three
+// vertices' normals and uvs and the flags in the first 64 B, the tangents in
+// the second (read only for meshes that carry them).  The same values as the
+// indexed mesh arrays, gathered once at upload: the shading of a hit reads one
+// line instead of the index and up to nine scattered vertex attributes.
+//   a = n0.xyz n1.x, b = n1.yz n2.xy, c = n2.z uv0 uv1.u, d = uv1.v uv2 flags
+//   e = t0.xyz t1.x, f = t1.yz t2.xy, g = t2.z
+struct alignas(128) DevTriShade {
+    float4 a, b, c, d, e, f, g, pad;
+};
+static_assert(sizeof(DevTriShade) == 128, "shading record layout");
+
 struct DevPrimInfo {
     int32_t material, light, medium;
     uint32_t index;  // triangle / quad / sphere id, BLAS root ref
@@ -98,6 +110,7 @@ struct DevScene {
     const float* normals;
     const float* uvs;          // 2 per vertex
     const float* tangents;
+    const DevTriShade* tshade;  // per-triangle shading records (vertex order x, y, z of tri)
     const pt_quad* quads;
     const pt_sphere* spheres;
     const pt_material* materials;

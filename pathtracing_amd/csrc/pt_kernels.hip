@@ -1236,6 +1236,38 @@ __device__ __forceinline__ double linear_to_srgb(double v) {
     v = glm_clamp01(v);
     return v < 0.0031308 ? 12.92 * v : 1.055 * pow(v, 1.0 / 2.4) - 0.055;
 }
+// Per-triangle shading records (DevTriShade) from the indexed mesh arrays,
+// once per scene upload.
+__global__ __launch_bounds__(256) void k_tri_shade(const uint4* __restrict__ tri, const float* __restrict__ normals,
+                                                   const float* __restrict__ uvs,
+                                                   const float* __restrict__ tangents, uint32_t n,
+                                                   DevTriShade* __restrict__ out) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const uint4 T = tri[t];
+    const float* n0 = normals + 3 * (size_t)T.x;
+    const float* n1 = normals + 3 * (size_t)T.y;
+    const float* n2 = normals + 3 * (size_t)T.z;
+    const float* u0 = uvs + 2 * (size_t)T.x;
+    const float* u1 = uvs + 2 * (size_t)T.y;
+    const float* u2 = uvs + 2 * (size_t)T.z;
+    DevTriShade r;
+    r.a = make_float4(n0[0], n0[1], n0[2], n1[0]);
+    r.b = make_float4(n1[1], n1[2], n2[0], n2[1]);
+    r.c = make_float4(n2[2], u0[0], u0[1], u1[0]);
+    r.d = make_float4(u1[1], u2[0], u2[1], __uint_as_float(T.w));
+    r.e = r.f = r.g = r.pad = make_float4(0, 0, 0, 0);
+    if ((T.w & 1u) && tangents) {
+        const float* t0 = tangents + 3 * (size_t)T.x;
+        const float* t1 = tangents + 3 * (size_t)T.y;
+        const float* t2 = tangents + 3 * (size_t)T.z;
+        r.e = make_float4(t0[0], t0[1], t0[2], t1[0]);
+        r.f = make_float4(t1[1], t1[2], t2[0], t2[1]);
+        r.g = make_float4(t2[2], 0, 0, 0);
+    }
+    out[t] = r;
+}
+
 __global__ __launch_bounds__(256) void k_resolve(const double* __restrict__ film, uint32_t npx, uint32_t tonemap,
                                                 uint8_t* __restrict__ rgb) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;

@@ -586,6 +586,14 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
     UP(DS.normals, s->normals, 3 * (size_t)s->n_vertices);
     UP(DS.uvs, s->uvs, 2 * (size_t)s->n_vertices);
     UP(DS.tangents, s->tangents, s->tangents ? 3 * (size_t)s->n_vertices : 0);
+    UP(DS.tshade, (const DevTriShade*)nullptr, s->n_triangles);
+    if (s->n_triangles) {
+        hipLaunchKernelGGL(k_tri_shade, dim3((s->n_triangles + 255) / 256), dim3(256), 0, c->stream, DS.tri,
+                           DS.normals, DS.uvs, s->tangents ? DS.tangents : nullptr, s->n_triangles,
+                           const_cast<DevTriShade*>(DS.tshade));
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
     UP(DS.quads, s->quads, s->n_quads);
     UP(DS.spheres, s->spheres, s->n_spheres);
     UP(DS.materials, s->materials, s->n_materials);

@@ -187,14 +187,16 @@ __device__ __forceinline__ void sphere_uv(f3 p, float& u, float& v) {
 // it per candidate, only the last accepted survives).
 __device__ void tri_interaction(const DevGeom& g, uint32_t tri, int mid, f3 o, f3 d, float t,
                                 float bu, float bv, SurfInt& si) {
-    uint4 T = S.tri[tri];
+    // one shading record (DevTriShade) instead of S.tri + the indexed
+    // normals / uvs / tangents: the same values, the same arithmetic
+    const DevTriShade* R = S.tshade + tri;
+    const float4 ra = R->a, rb = R->b, rc = R->c, rd = R->d;
     float u = bu, v = bv, w = 1.0f - u - v;
-    const float* uvs = S.uvs;
-    si.u = lerp3f(u, uvs[2 * T.y], v, uvs[2 * T.z], w, uvs[2 * T.x]);
-    si.v = lerp3f(u, uvs[2 * T.y + 1], v, uvs[2 * T.z + 1], w, uvs[2 * T.x + 1]);
-    const float *n1 = S.normals + 3 * T.y, *n2 = S.normals + 3 * T.z, *n0 = S.normals + 3 * T.x;
-    f3 nn = normalize(F3(lerp3f(u, n1[0], v, n2[0], w, n0[0]), lerp3f(u, n1[1], v, n2[1], w, n0[1]),
-                         lerp3f(u, n1[2], v, n2[2], w, n0[2])));
+    si.u = lerp3f(u, rc.w, v, rd.y, w, rc.y);
+    si.v = lerp3f(u, rd.x, v, rd.z, w, rc.z);
+    // n0 = (a.x a.y a.z), n1 = (a.w b.x b.y), n2 = (b.z b.w c.x)
+    f3 nn = normalize(F3(lerp3f(u, ra.w, v, rb.z, w, ra.x), lerp3f(u, rb.x, v, rb.w, w, ra.y),
+                         lerp3f(u, rb.y, v, rc.x, w, ra.z)));
     f3 N = normalize(cross_v(xyz(g.b), xyz(g.c)));
     si.n = N;
     if (dot(N, nn) < 0) nn = -nn;
@@ -205,11 +207,11 @@ __device__ void tri_interaction(const DevGeom& g, uint32_t tri, int mid, f3 o, f
     float sg = dot(d, N) > 0.0f ? -1.0f : 1.0f;
     si.p = F3(fma_(rmul(PT_EPS, N.x), sg, o.x + rmul(t, d.x)), fma_(rmul(PT_EPS, N.y), sg, o.y + rmul(t, d.y)),
               fma_(rmul(PT_EPS, N.z), sg, fma_(t, d.z, o.z)));
-    if (T.w & 1u) {
-        const float* tg = S.tangents;
-        const float *t1 = tg + 3 * T.y, *t2 = tg + 3 * T.z, *t0 = tg + 3 * T.x;
-        f3 tv = F3(lerp3f(u, t1[0], v, t2[0], w, t0[0]), lerp3f(u, t1[1], v, t2[1], w, t0[1]),
-                   lerp3f(u, t1[2], v, t2[2], w, t0[2]));
+    if (__float_as_uint(rd.w) & 1u) {
+        const float4 re = R->e, rf = R->f, rg = R->g;
+        // t0 = (e.x e.y e.z), t1 = (e.w f.x f.y), t2 = (f.z f.w g.x)
+        f3 tv = F3(lerp3f(u, re.w, v, rf.z, w, re.x), lerp3f(u, rf.x, v, rf.w, w, re.y),
+                   lerp3f(u, rf.y, v, rg.x, w, re.z));
         float k = dot(si.ns, tv);  // tangent - ns*k fused (fixture search)
         si.tangent = normalize(F3(fma_(-si.ns.x, k, tv.x), fma_(-si.ns.y, k, tv.y), fma_(-si.ns.z, k, tv.z)));
     } else {

@@ -109,11 +109,12 @@ __device__ __forceinline__ f3 inv_dir(f3 d) {  // Ray ctor (Ray.hpp:32-35)
 // Candidate uv for the alpha test on an alpha-tested triangle (rare path).
 __device__ __noinline__ bool tri_alpha(uint32_t slot, float bu, float bv, f3 o, f3 d) {
     const DevPrimInfo pi = S.info[slot];
-    uint4 T = S.tri[pi.index];
+    const DevTriShade* R = S.tshade + pi.index;
+    const float4 rc = R->c, rd = R->d;
     float u = bu, v = bv, w = 1.0f - u - v;
     // the uv TriangleShape::Intersect computes (same contraction as tri_interaction)
-    float tu = lerp3f(u, S.uvs[2 * T.y], v, S.uvs[2 * T.z], w, S.uvs[2 * T.x]);
-    float tv = lerp3f(u, S.uvs[2 * T.y + 1], v, S.uvs[2 * T.z + 1], w, S.uvs[2 * T.x + 1]);
+    float tu = lerp3f(u, rc.w, v, rd.y, w, rc.y);
+    float tv = lerp3f(u, rd.x, v, rd.z, w, rc.z);
     return mat_alpha(pi.material, tu, tv, o, d, (int)slot);
 }
 

@@ -153,6 +153,14 @@ def lib():
         return _lib
     if not LIB_PATH.exists():
         raise NativeError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    # One HIP runtime per process: torch bundles its own libamdhip64.so.7.
+    # Loaded first, the library binds to it by soname; loaded before torch, it
+    # would pull in /opt/rocm's copy and torch's later GPU init fails ("No HIP
+    # GPUs are available").  torch stays plumbing (device tensors, streams).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(str(LIB_PATH))
     vp = C.c_void_p
     L.pt_version.restype = C.c_int
