@@ -555,7 +555,10 @@ __device__ Bxdf conductor_scatter(const pt_material& m, f3 ind, const SurfInt& s
     return b;
 }
 
-__device__ Bxdf mat_scatter(int mid, f3 ino, f3 ind, const SurfInt& si, float u, float uv0,
+// The material and light entry points are inlined into k_shade: taken out of
+// line, their `const SurfInt&` argument kept the interaction in scratch memory
+// on every path (k_shade<PATH>: 160 -> 16 B of scratch per lane).
+__device__ __forceinline__ Bxdf mat_scatter(int mid, f3 ino, f3 ind, const SurfInt& si, float u, float uv0,
                             float uv1) {
     const pt_material& m = S.materials[mid];
     switch (m.kind) {
@@ -565,7 +568,7 @@ __device__ Bxdf mat_scatter(int mid, f3 ino, f3 ind, const SurfInt& si, float u,
         default: return conductor_scatter(m, ind, si);
     }
 }
-__device__ f3 mat_f(int mid, f3 ind, const SurfInt& si, f3 dir) {
+__device__ __forceinline__ f3 mat_f(int mid, f3 ind, const SurfInt& si, f3 dir) {
     const pt_material& m = S.materials[mid];
     f3 f;
     float p;
@@ -576,7 +579,7 @@ __device__ f3 mat_f(int mid, f3 ind, const SurfInt& si, f3 dir) {
         default: return F3(1, 1, 1);  // base Material::calc_attenuation
     }
 }
-__device__ float mat_pdf(int mid, f3 ind, const SurfInt& si, f3 dir) {
+__device__ __forceinline__ float mat_pdf(int mid, f3 ind, const SurfInt& si, f3 dir) {
     const pt_material& m = S.materials[mid];
     f3 f;
     float p;
@@ -717,20 +720,24 @@ __device__ __forceinline__ f3 inf_le(const pt_light& l, f3 d) {
 }
 // TransformedLight / AnimatedLight (Light.cpp:300-364): an emitter inside an
 // instance; its AreaLight's shape stays in object space (l.prim is the BLAS
-// slot).  Out of line: the rare path keeps k_shade's registers.
-__device__ __noinline__ void tlight_to_world(int inst, f3& p, f3& n) {  // TransformedLight::sample
+// slot).  Out of line: the rare path keeps k_shade's registers.  Values in and
+// out (returned in registers): a reference argument would keep the caller's
+// variables in scratch memory on every path.
+struct PN {
+    f3 p, n;
+};
+__device__ __noinline__ PN tlight_to_world(int inst, f3 p, f3 n) {  // TransformedLight::sample
     const DevInstance& I = S.instances[inst];
     float NM[9];
     normal_matrix(I.T, NM);
-    p = m4_point(I.T, p);
-    n = m3_mul(NM, n);
+    return PN{m4_point(I.T, p), m3_mul(NM, n)};
 }
-__device__ __noinline__ void tlight_to_object(int inst, f3& p, f3& n, f3& ro, f3& rd) {  // TransformedLight::PDF
+struct TLObj {
+    f3 p, n, ro, rd;
+};
+__device__ __noinline__ TLObj tlight_to_object(int inst, f3 p, f3 n, f3 ro, f3 rd) {  // TransformedLight::PDF
     const DevInstance& I = S.instances[inst];
-    p = m4_point(I.inv, p);
-    n = normalize(m4_dir(I.inv, n));
-    ro = m4_point(I.inv, ro);
-    rd = normalize(m4_dir(I.inv, rd));
+    return TLObj{m4_point(I.inv, p), normalize(m4_dir(I.inv, n)), m4_point(I.inv, ro), normalize(m4_dir(I.inv, rd))};
 }
 __device__ __noinline__ f3 tlight_normal(int inst, f3 n) {  // TransformedLight::L's temp.n
     float NM[9];
@@ -743,7 +750,11 @@ __device__ __noinline__ f3 tlight_normal(int inst, f3 n) {  // TransformedLight:
 // compared in double), then the point (u0, u1) of that cell mapped to the
 // sphere.  uc is the reference's hidden random_float() (Light.cpp:120),
 // drawn from the sample stream by the caller.
-__device__ __noinline__ void texinf_sample(const pt_light& l, float uc, float u0, float u1, LSample& ls) {
+struct DirUV {
+    f3 dir;
+    float u, v;
+};
+__device__ __noinline__ DirUV texinf_sample(const pt_light& l, float uc, float u0, float u1) {
     const float* acc = S.light_dist + l.prim;
     constexpr uint32_t N = (uint32_t)PT_TEXINF_X * PT_TEXINF_Y;
     const double weight = (double)uc * (double)acc[N - 1];
@@ -758,8 +769,10 @@ __device__ __noinline__ void texinf_sample(const pt_light& l, float uc, float u0
     const float z = 2.0f * cu - 1.0f;
     const float th = 2.0f * PT_PI * cv;
     const float r = csqrt(1.0f - rmul(z, z));
-    ls.dir = F3(r * cos_cr(th), r * sin_cr(th), z);
-    sphere_uv(ls.dir, ls.u, ls.v);
+    DirUV o;
+    o.dir = F3(r * cos_cr(th), r * sin_cr(th), z);
+    sphere_uv(o.dir, o.u, o.v);
+    return o;
 }
 // TextureInfiniteLight::PDF (Light.cpp:146-150): luminance(Le) / totalWeight
 // / cellOmega, luminance in double (Util.hpp:4-6)
@@ -779,7 +792,7 @@ __device__ __forceinline__ float inf_pdf(const pt_light& l, f3 rd) {
     return l.kind == PT_LIGHT_TEX_INF ? texinf_pdf(l, rd) : 1.0f / (4.0f * PT_PI);
 }
 
-__device__ LSample light_sample(const pt_light& l, float u0, float u1, float uc = 0.0f) {
+__device__ __forceinline__ LSample light_sample(const pt_light& l, float u0, float u1, float uc = 0.0f) {
     LSample ls;
     ls.L = F3(0, 0, 0);
     ls.p = F3(0, 0, 0);
@@ -790,7 +803,11 @@ __device__ LSample light_sample(const pt_light& l, float u0, float u1, float uc 
         const DevPrimInfo& pi = S.info[l.prim];
         uint32_t kind = __float_as_uint(S.geom[l.prim].a.w) & GF_KIND;
         shape_sample(kind, pi.index, u0, u1, ls);
-        if (l.instance >= 0) tlight_to_world(l.instance, ls.p, ls.n);
+        if (l.instance >= 0) {
+            const PN w = tlight_to_world(l.instance, ls.p, ls.n);
+            ls.p = w.p;
+            ls.n = w.n;
+        }
         return ls;
     }
     if (l.kind == PT_LIGHT_POINT) {  // Light.cpp:236-238
@@ -802,7 +819,10 @@ __device__ LSample light_sample(const pt_light& l, float u0, float u1, float uc 
         return ls;
     }
     if (l.kind == PT_LIGHT_TEX_INF) {
-        texinf_sample(l, uc, u0, u1, ls);
+        const DirUV o = texinf_sample(l, uc, u0, u1);
+        ls.dir = o.dir;
+        ls.u = o.u;
+        ls.v = o.v;
         return ls;
     }
     float z = 2.0f * u0 - 1.0f;
@@ -825,11 +845,17 @@ __device__ __forceinline__ bool light_is_delta(const pt_light& l) {
     return l.kind == PT_LIGHT_DISTANT || l.kind == PT_LIGHT_POINT;
 }
 // Light::PDF(interaction, ray)
-__device__ float light_pdf(const pt_light& l, f3 p, f3 n, f3 ro, f3 rd) {
+__device__ __forceinline__ float light_pdf(const pt_light& l, f3 p, f3 n, f3 ro, f3 rd) {
     if (l.kind == PT_LIGHT_AREA) {  // Light.cpp:267-272
         uint32_t kind = __float_as_uint(S.geom[l.prim].a.w) & GF_KIND;
         uint32_t index = S.info[l.prim].index;
-        if (l.instance >= 0) tlight_to_object(l.instance, p, n, ro, rd);
+        if (l.instance >= 0) {
+            const TLObj o = tlight_to_object(l.instance, p, n, ro, rd);
+            p = o.p;
+            n = o.n;
+            ro = o.ro;
+            rd = o.rd;
+        }
         if (l.one_sided) return dot(-rd, n) > 0 ? shape_pdf(kind, index, p, n, ro, rd) : 0;
         return shape_pdf(kind, index, p, n, ro, rd);
     }
@@ -838,7 +864,7 @@ __device__ float light_pdf(const pt_light& l, f3 p, f3 n, f3 ro, f3 rd) {
     return 0;
 }
 // Light::L(interaction, ray)
-__device__ f3 light_L(const pt_light& l, f3 n, float u, float v, f3 rd) {
+__device__ __forceinline__ f3 light_L(const pt_light& l, f3 n, float u, float v, f3 rd) {
     if (l.kind == PT_LIGHT_AREA) {  // Light.cpp:257-260
         if (l.instance >= 0) {  // TransformedLight::L: fresh interaction, uv (0, 0)
             n = tlight_normal(l.instance, n);
