@@ -121,6 +121,9 @@ struct AdaptEst {
 enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1, PT_SORT_RAYS = 2 };
 #define PT_SORT_BINS_MATERIAL 256
 #define PT_SORT_BINS_SPATIAL 4096
+#ifndef PT_SORT_PER
+#define PT_SORT_PER 16u  // paths per thread of k_sort_count / k_sort_scatter
+#endif
 template <int KEY, int NB>
 __global__ void k_sort_count(PathSoA cur, const uint32_t* nptr, const float4* hit, uint32_t* counts);
 template <int NB>

@@ -1342,16 +1342,23 @@ __device__ __forceinline__ uint32_t sort_bin(const PathSoA& cur, uint32_t front,
     }
     return code;
 }
+// Each block bins PT_SORT_PER paths per thread (PT_SORT_PER x 256
+// consecutive paths), so clearing and folding the block's 4096-bin LDS
+// histogram is paid once per 4096 paths rather than once per 256.
 template <int KEY, int NB>
 __global__ __launch_bounds__(256) void k_sort_count(PathSoA cur, const uint32_t* __restrict__ nptr,
                                                    const float4* __restrict__ hit, uint32_t* __restrict__ counts) {
     __shared__ uint32_t h[NB];
     const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
-    if (blockIdx.x * 256 >= n) return;
+    const uint32_t t0 = blockIdx.x * (256u * PT_SORT_PER);
+    if (t0 >= n) return;
     for (int b = threadIdx.x; b < NB; b += 256) h[b] = 0;
     __syncthreads();
-    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-    if (t < n) atomicAdd(&h[sort_bin<KEY>(cur, front, hit, t)], 1u);
+#pragma unroll 4
+    for (uint32_t k = 0; k < PT_SORT_PER; k++) {
+        const uint32_t t = t0 + k * 256u + threadIdx.x;
+        if (t < n) atomicAdd(&h[sort_bin<KEY>(cur, front, hit, t)], 1u);
+    }
     __syncthreads();
     for (int b = threadIdx.x; b < NB; b += 256)
         if (h[b]) atomicAdd(&counts[b], h[b]);
@@ -1384,26 +1391,35 @@ __global__ __launch_bounds__(256) void k_sort_scan(uint32_t* __restrict__ counts
         run += v[k];
     }
 }
+// The block's paths keep their bins in registers between the two passes; a
+// path's position inside its bin's block range comes from an LDS atomic, so
+// the order within a bin is arbitrary (results do not depend on it).
 template <int KEY, int NB>
 __global__ __launch_bounds__(256) void k_sort_scatter(PathSoA cur, const uint32_t* __restrict__ nptr,
                                                      const float4* __restrict__ hit, uint32_t* __restrict__ offsets,
                                                      uint32_t* __restrict__ order) {
-    __shared__ uint32_t h[NB], base[NB];
+    __shared__ uint32_t h[NB];
     const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
-    if (blockIdx.x * 256 >= n) return;
+    const uint32_t t0 = blockIdx.x * (256u * PT_SORT_PER);
+    if (t0 >= n) return;
     for (int b = threadIdx.x; b < NB; b += 256) h[b] = 0;
     __syncthreads();
-    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-    uint32_t bin = 0, rank = 0;
-    if (t < n) {
-        bin = sort_bin<KEY>(cur, front, hit, t);
-        rank = atomicAdd(&h[bin], 1u);
+    uint32_t bin[PT_SORT_PER];
+#pragma unroll
+    for (uint32_t k = 0; k < PT_SORT_PER; k++) {
+        const uint32_t t = t0 + k * 256u + threadIdx.x;
+        bin[k] = t < n ? sort_bin<KEY>(cur, front, hit, t) : 0u;
+        if (t < n) atomicAdd(&h[bin[k]], 1u);
     }
     __syncthreads();
     for (int b = threadIdx.x; b < NB; b += 256)
-        if (h[b]) base[b] = atomicAdd(&offsets[b], h[b]);
+        if (h[b]) h[b] = atomicAdd(&offsets[b], h[b]);  // the block's range of bin b
     __syncthreads();
-    if (t < n) order[base[bin] + rank] = t;
+#pragma unroll
+    for (uint32_t k = 0; k < PT_SORT_PER; k++) {
+        const uint32_t t = t0 + k * 256u + threadIdx.x;
+        if (t < n) order[atomicAdd(&h[bin[k]], 1u)] = t;
+    }
 }
 template __global__ void k_sort_count<PT_SORT_MATERIAL, PT_SORT_BINS_MATERIAL>(PathSoA, const uint32_t*, const float4*,
                                                                              uint32_t*);

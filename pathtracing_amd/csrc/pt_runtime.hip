@@ -920,6 +920,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         const dim3 gt(use_pool ? c->blocks_closest : (paths + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK);
         const dim3 ga(use_pool ? c->blocks_any : (paths + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK);
         const dim3 gs((paths + 255) / 256);
+        const dim3 gsort((paths + 256 * PT_SORT_PER - 1) / (256 * PT_SORT_PER));  // k_sort_count / k_sort_scatter
         uint32_t issued = 0, read = 0;
         bool drained = false;
         // reads iteration `read`'s snapshot (after its event): stats, timing, end test
@@ -964,10 +965,10 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             if (sort_rays) {  // claim order of this bounce's closest-hit rays: origin cell + octant
                 constexpr int NB = PT_SORT_BINS_SPATIAL;
                 HIPCHK(c, hipMemsetAsync(c->ray_counts, 0, NB * 4, sm));
-                hipLaunchKernelGGL((k_sort_count<PT_SORT_RAYS, NB>), gs, dim3(256), 0, sm, cur, (const uint32_t*)in,
+                hipLaunchKernelGGL((k_sort_count<PT_SORT_RAYS, NB>), gsort, dim3(256), 0, sm, cur, (const uint32_t*)in,
                                    (const float4*)c->hit, c->ray_counts);
                 hipLaunchKernelGGL((k_sort_scan<NB>), dim3(1), dim3(256), 0, sm, c->ray_counts);
-                hipLaunchKernelGGL((k_sort_scatter<PT_SORT_RAYS, NB>), gs, dim3(256), 0, sm, cur, (const uint32_t*)in,
+                hipLaunchKernelGGL((k_sort_scatter<PT_SORT_RAYS, NB>), gsort, dim3(256), 0, sm, cur, (const uint32_t*)in,
                                    (const float4*)c->hit, c->ray_counts, c->ray_order);
             }
             {
@@ -980,19 +981,19 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             if (sort_mat) {  // bin this bounce's paths by hit material (k_sort_*), shade in that order
                 constexpr int NB = PT_SORT_BINS_MATERIAL;
                 HIPCHK(c, hipMemsetAsync(c->sort_counts, 0, NB * 4, sm));
-                hipLaunchKernelGGL((k_sort_count<PT_SORT_MATERIAL, NB>), gs, dim3(256), 0, sm, cur, (const uint32_t*)in,
+                hipLaunchKernelGGL((k_sort_count<PT_SORT_MATERIAL, NB>), gsort, dim3(256), 0, sm, cur, (const uint32_t*)in,
                                    (const float4*)c->hit, c->sort_counts);
                 hipLaunchKernelGGL((k_sort_scan<NB>), dim3(1), dim3(256), 0, sm, c->sort_counts);
-                hipLaunchKernelGGL((k_sort_scatter<PT_SORT_MATERIAL, NB>), gs, dim3(256), 0, sm, cur,
+                hipLaunchKernelGGL((k_sort_scatter<PT_SORT_MATERIAL, NB>), gsort, dim3(256), 0, sm, cur,
                                    (const uint32_t*)in, (const float4*)c->hit, c->sort_counts, c->sort_order);
                 R.order = c->sort_order;
             } else if (sort_sp) {  // ... by the hit point's Morton cell
                 constexpr int NB = PT_SORT_BINS_SPATIAL;
                 HIPCHK(c, hipMemsetAsync(c->sort_counts, 0, NB * 4, sm));
-                hipLaunchKernelGGL((k_sort_count<PT_SORT_SPATIAL, NB>), gs, dim3(256), 0, sm, cur, (const uint32_t*)in,
+                hipLaunchKernelGGL((k_sort_count<PT_SORT_SPATIAL, NB>), gsort, dim3(256), 0, sm, cur, (const uint32_t*)in,
                                    (const float4*)c->hit, c->sort_counts);
                 hipLaunchKernelGGL((k_sort_scan<NB>), dim3(1), dim3(256), 0, sm, c->sort_counts);
-                hipLaunchKernelGGL((k_sort_scatter<PT_SORT_SPATIAL, NB>), gs, dim3(256), 0, sm, cur,
+                hipLaunchKernelGGL((k_sort_scatter<PT_SORT_SPATIAL, NB>), gsort, dim3(256), 0, sm, cur,
                                    (const uint32_t*)in, (const float4*)c->hit, c->sort_counts, c->sort_order);
                 R.order = c->sort_order;
             }
