@@ -143,10 +143,11 @@ __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, flo
 #else
 #define PT_POOL_WAVES
 #endif
-// the any-hit pool kernel's own budget (it needs fewer registers: no octant
-// order, no hit record)
+// the any-hit pool kernel's own budget (it needs fewer registers: no hit
+// record): 8 waves per SIMD, C4 k_shadow_pool 10.72 -> 10.34 ms per launch
+// over 7 (6: 11.50; profiles/r02_ab_shade.txt)
 #ifndef PT_SHADOW_WPE
-#define PT_SHADOW_WPE PT_POOL_WPE
+#define PT_SHADOW_WPE 8
 #endif
 #if PT_SHADOW_WPE
 #define PT_SHADOW_WAVES __attribute__((amdgpu_waves_per_eu(PT_SHADOW_WPE, PT_SHADOW_WPE)))

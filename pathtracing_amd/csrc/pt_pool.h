@@ -65,6 +65,15 @@ __device__ unsigned int pt_diag[4];
 #ifndef PT_LEAF2
 #define PT_LEAF2 0
 #endif
+// Any-hit visit order: 0 = slot order (BVH4::IntersectPred, BVH.hpp:1099-1102),
+// 1 = the closest-hit octant order.  The occlusion result does not depend on
+// the order (every primitive's test, alpha included, is a function of the ray
+// and the primitive); only the node visit count does.  Octant order finds an
+// occluder sooner: C4 k_shadow_pool 10.72 -> 9.44 ms per launch
+// (profiles/r02_ab_shade.txt).
+#ifndef PT_ANY_OCT
+#define PT_ANY_OCT 1
+#endif
 // overflow words per stack entry per lane (ref + entry distance)
 #define PT_OVF_WORDS 2
 
@@ -274,7 +283,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             // visit order: slot order for any hit (BVH.hpp:1099-1102), octant
             // order far -> near for closest hit (BVH4::LUT, BVH.hpp:1195-1204)
             uint32_t perm = 0xE4u;
-            if (!ANY) {
+            if (!ANY || PT_ANY_OCT) {
                 const uint32_t ow = ((oct >> 2) & 1u) ? ow1 : ow0;
                 perm = (ow >> (8 * (oct & 3))) & 0xFFu;
             }
