@@ -37,8 +37,12 @@
 // them after every render
 __device__ unsigned int pt_diag[4];
 #endif
+// Idle lanes that trigger a refill: fewer claims (one atomic and one
+// divergent ray start per refill) against lanes left idle meanwhile.  C4:
+// 4 -> 1081, 8 -> 1198, 16 -> 1235, 24 -> 1224, 32 -> 1188 Mrays/s
+// (profiles/r02_ab_shade.txt).
 #ifndef PT_REFILL
-#define PT_REFILL 8
+#define PT_REFILL 16
 #endif
 
 // Closest-hit pool kernels keep each stack entry's entry distance (BVH4::
