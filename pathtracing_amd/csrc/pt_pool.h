@@ -78,6 +78,11 @@ __device__ unsigned int pt_diag[4];
 #ifndef PT_ANY_OCT
 #define PT_ANY_OCT 1
 #endif
+// Quantized-node slab test with the bounds pre-ordered by the ray's
+// direction signs (qslab4pe, bit-identical to slab4pe)
+#ifndef PT_QSLAB_ORDERED
+#define PT_QSLAB_ORDERED 1
+#endif
 // overflow words per stack entry per lane (ref + entry distance)
 #define PT_OVF_WORDS 2
 
@@ -257,9 +262,13 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             q2 = q[2];
             const float4 qc = q[3 * nk];
             q3 = q4 = q5 = q0;  // no second leaf primitive in this form
+#if PT_QSLAB_ORDERED
+            qslab4pe(q0, q1, q2, o, inv, tmax, mask, te);
+#else
             float4 xmn, xmx, ymn, ymx, zmn, zmx;
             qnode_boxes(q0, q1, q2, xmn, xmx, ymn, ymx, zmn, zmx);
             slab4pe(xmn, xmx, ymn, ymx, zmn, zmx, o, inv, tmax, mask, te);
+#endif
             ch = make_uint4(__float_as_uint(qc.x), __float_as_uint(qc.y), __float_as_uint(qc.z),
                             __float_as_uint(qc.w));
             ow0 = __float_as_uint(q2.z);

@@ -219,6 +219,49 @@ __device__ __forceinline__ void qnode_boxes(float4 a, float4 b, float4 c, float4
     zmx = qdec4(__float_as_uint(c.y), sz, a.z);
 }
 
+// The same test on a quantized node with each axis's bounds pre-ordered by
+// the sign of inv (near bound first): then min(t1, t2) is the near plane's t
+// and max(t1, t2) the far plane's exactly (rounding is monotone, lo' <= hi'),
+// so tEntry / tExit are one max3 / min3 per child instead of six min/max, and
+// the result is bit-identical to slab4pe.  The bound words are swapped before
+// decoding (one select per axis and side instead of one per child).
+__device__ __forceinline__ void qslab4pe(float4 a, float4 b, float4 c, f3 o, f3 inv, float tmax, uint32_t& mask,
+                                         float (&te)[4]) {
+    const uint32_t ex = __float_as_uint(a.w);
+    const float sx = __uint_as_float((ex & 0xFFu) << 23), sy = __uint_as_float(((ex >> 8) & 0xFFu) << 23),
+                sz = __uint_as_float(((ex >> 16) & 0xFFu) << 23);
+    const bool nx = inv.x < 0.0f, ny = inv.y < 0.0f, nz = inv.z < 0.0f;
+    const uint32_t xl = __float_as_uint(b.x), xh = __float_as_uint(b.y), yl = __float_as_uint(b.z),
+                   yh = __float_as_uint(b.w), zl = __float_as_uint(c.x), zh = __float_as_uint(c.y);
+    const float4 xn = qdec4(nx ? xh : xl, sx, a.x), xf = qdec4(nx ? xl : xh, sx, a.x);
+    const float4 yn = qdec4(ny ? yh : yl, sy, a.y), yf = qdec4(ny ? yl : yh, sy, a.y);
+    const float4 zn = qdec4(nz ? zh : zl, sz, a.z), zf = qdec4(nz ? zl : zh, sz, a.z);
+    const v2f ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+    const v2f ix = {inv.x, inv.x}, iy = {inv.y, inv.y}, iz = {inv.z, inv.z};
+    v2f t[2][6];
+    t[0][0] = (v2f{xn.x, xn.y} - ox) * ix;
+    t[1][0] = (v2f{xn.z, xn.w} - ox) * ix;
+    t[0][1] = (v2f{xf.x, xf.y} - ox) * ix;
+    t[1][1] = (v2f{xf.z, xf.w} - ox) * ix;
+    t[0][2] = (v2f{yn.x, yn.y} - oy) * iy;
+    t[1][2] = (v2f{yn.z, yn.w} - oy) * iy;
+    t[0][3] = (v2f{yf.x, yf.y} - oy) * iy;
+    t[1][3] = (v2f{yf.z, yf.w} - oy) * iy;
+    t[0][4] = (v2f{zn.x, zn.y} - oz) * iz;
+    t[1][4] = (v2f{zn.z, zn.w} - oz) * iz;
+    t[0][5] = (v2f{zf.x, zf.y} - oz) * iz;
+    t[1][5] = (v2f{zf.z, zf.w} - oz) * iz;
+    mask = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int h = i >> 1, l = i & 1;
+        const float tEntry = fmaxf(fmaxf(t[h][0][l], t[h][2][l]), t[h][4][l]);
+        const float tExit = fminf(fminf(t[h][1][l], t[h][3][l]), t[h][5][l]);
+        if (tExit >= PT_EPS && tEntry < tmax && tEntry <= tExit) mask |= 1u << i;
+        te[i] = tEntry;
+    }
+}
+
 // Children of a cluster in visit order: every valid child (passes the slab
 // test, exists) but the last is pushed, the last becomes the next ref.  perm
 // holds the visit order as 2-bit slot indices from the low end (0xE4 = slot
