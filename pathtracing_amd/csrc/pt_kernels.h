@@ -120,7 +120,10 @@ struct AdaptEst {
 // hits inside instances.  Spatial: the hit point's 16^3 Morton cell.
 enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1, PT_SORT_RAYS = 2 };
 #define PT_SORT_BINS_MATERIAL 256
-#define PT_SORT_BINS_SPATIAL 4096
+#ifndef PT_SORT_CELL_BITS
+#define PT_SORT_CELL_BITS 4  // spatial sort: 2^bits cells per axis of the scene box
+#endif
+#define PT_SORT_BINS_SPATIAL (1 << (3 * PT_SORT_CELL_BITS))
 #ifndef PT_SORT_PER
 #define PT_SORT_PER 16u  // paths per thread of k_sort_count / k_sort_scatter
 #endif

@@ -1314,10 +1314,10 @@ __device__ __forceinline__ uint32_t sort_bin(const PathSoA& cur, uint32_t front,
         uint32_t code = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
 #pragma unroll
         for (int a = 0; a < 3; a++) {
-            const float q = (p[a] - S.bb_lo[a]) * S.bb_scale[a] * 0.5f;  // [0, 8)
-            const uint32_t c = (uint32_t)fminf(fmaxf(q, 0.0f), 7.0f);
+            const float q = (p[a] - S.bb_lo[a]) * S.bb_scale[a] * 0.5f;  // [0, 2^(bits-1))
+            const uint32_t c = (uint32_t)fminf(fmaxf(q, 0.0f), (float)((1 << (PT_SORT_CELL_BITS - 1)) - 1));
 #pragma unroll
-            for (int b = 0; b < 3; b++) code |= ((c >> b) & 1u) << (3 + 3 * b + a);
+            for (int b = 0; b < PT_SORT_CELL_BITS - 1; b++) code |= ((c >> b) & 1u) << (3 + 3 * b + a);
         }
         return code;
     }
@@ -1336,10 +1336,10 @@ __device__ __forceinline__ uint32_t sort_bin(const PathSoA& cur, uint32_t front,
     const float p[3] = {fmaf(t, d.x, o.x), fmaf(t, d.y, o.y), fmaf(t, d.z, o.z)};
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-        const float q = (p[a] - S.bb_lo[a]) * S.bb_scale[a];  // [0, 16)
-        const uint32_t c = (uint32_t)fminf(fmaxf(q, 0.0f), 15.0f);
+        const float q = (p[a] - S.bb_lo[a]) * S.bb_scale[a];  // [0, 2^bits)
+        const uint32_t c = (uint32_t)fminf(fmaxf(q, 0.0f), (float)((1 << PT_SORT_CELL_BITS) - 1));
 #pragma unroll
-        for (int b = 0; b < 4; b++) code |= ((c >> b) & 1u) << (3 * b + a);
+        for (int b = 0; b < PT_SORT_CELL_BITS; b++) code |= ((c >> b) & 1u) << (3 * b + a);
     }
     return code;
 }

@@ -631,7 +631,7 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
         }
         for (int a = 0; a < 3; a++) {
             DS.bb_lo[a] = lo[a];
-            DS.bb_scale[a] = hi[a] > lo[a] ? 16.0f / (hi[a] - lo[a]) : 0.0f;
+            DS.bb_scale[a] = hi[a] > lo[a] ? (float)(1 << PT_SORT_CELL_BITS) / (hi[a] - lo[a]) : 0.0f;
         }
     }
     DS.n_nodes = (uint32_t)nodes.size();
