@@ -303,9 +303,9 @@ static bool quantize_node(const DevCluster& n, DevQNode& q) {
 }
 
 template <class T>
-static pt_status upload(pt_ctx* c, const T* src, size_t n, const T** dst) {
+static pt_status upload(pt_ctx* c, const T* src, size_t n, const T** dst, size_t pad = 0) {
     *dst = nullptr;
-    size_t bytes = std::max<size_t>(n * sizeof(T), 16);
+    size_t bytes = std::max<size_t>(n * sizeof(T) + pad, 16);
     void* p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) return fail(c, PT_ERR_OOM, "hipMalloc(%zu) failed", bytes);
     c->scene_bufs.push_back(p);
@@ -599,7 +599,8 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
     UP(DS.materials, s->materials, s->n_materials);
     UP(DS.textures, s->textures, s->n_textures);
     UP(DS.images, s->images, s->n_images);
-    UP(DS.texels, s->texels, s->n_texel_bytes);
+    // texels: 16 bytes of padding for the word loads of texel_pair_u8
+    if ((st = upload(c, s->texels, s->n_texel_bytes, &DS.texels, 16)) != PT_OK) return st;
     UP(DS.lights, s->lights, s->n_lights);
     UP(DS.sampler_lights, s->sampler_lights, s->n_sampler_lights);
     UP(DS.sampler_cdf, cdf.data(), cdf.size());

@@ -35,8 +35,35 @@ __device__ __forceinline__ f3 texel3(const pt_image& im, int x, int y) {
     return F3(channel_at(im, x, y, 1), channel_at(im, x, y, 2), channel_at(im, x, y, 3));
 }
 
+// The two texels (x, y), (x + 1, y) of a bilinear row of a u8 RGB / RGBA image
+// with three aligned word loads instead of six byte loads: the 2C bytes from
+// the first texel's byte on, realigned with v_alignbyte.  Same values as
+// texel3 (byte / 255); false (caller falls back to texel3) when x + 1 wraps,
+// for other formats, or near the end of the texel buffer (the upload pads it
+// by 16 bytes, so the word loads stay inside the allocation).
+__device__ __forceinline__ bool texel_pair_u8(const pt_image& im, int x, int y, f3& a, f3& b) {
+    const int C = im.channels;
+    if (im.format != PT_IMAGE_U8 || (C != 3 && C != 4)) return false;
+    const int xi = wrap_index(x, im.width), yi = wrap_index(y, im.height);
+    if (xi + 1 >= im.width) return false;
+    const uint64_t idx = im.offset + ((uint64_t)yi * (uint64_t)im.width + (uint64_t)xi) * (uint64_t)C;
+    if (idx + 2u * (uint64_t)C > S.n_texel_bytes) return false;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(S.texels + (idx & ~3ull));
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+    const uint32_t sh = (uint32_t)(idx & 3u);
+    const uint32_t q0 = __builtin_amdgcn_alignbyte(w1, w0, sh), q1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    const uint32_t qb = C == 4 ? q1 : __builtin_amdgcn_alignbyte(q1, q0, 3u);  // second texel's bytes
+    auto ch = [](uint32_t q, int k) { return (float)((q >> (8 * k)) & 0xFFu) / 255.0f; };
+    a = F3(ch(q0, 0), ch(q0, 1), ch(q0, 2));
+    b = F3(ch(qb, 0), ch(qb, 1), ch(qb, 2));
+    return true;
+}
+
 // Texture::Evaluate for SolidColor / CheckerTexture / ImageTexture (Texture.hpp:128-207).
-__device__ f3 tex_eval(int id, float u, float v) {
+// PAIR: texel_pair_u8 row loads (shading); the alpha test inside the traversal
+// kernels keeps the byte loads (its callee registers count toward theirs).
+template <bool PAIR>
+__device__ f3 tex_eval_t(int id, float u, float v) {
     f3 scale = F3(1, 1, 1);
     bool scaled = false;
     for (int guard = 0; guard < 16; guard++) {
@@ -59,8 +86,15 @@ __device__ f3 tex_eval(int id, float u, float v) {
         float y = v * im.height - 0.5f;
         int xi = (int)floorf(x), yi = (int)floorf(y);
         float dx = x - xi, dy = y - yi;
-        f3 a = texel3(im, xi, yi), b = texel3(im, xi + 1, yi);
-        f3 c = texel3(im, xi, yi + 1), d = texel3(im, xi + 1, yi + 1);
+        f3 a, b, c, d;
+        if (!PAIR || !texel_pair_u8(im, xi, yi, a, b)) {
+            a = texel3(im, xi, yi);
+            b = texel3(im, xi + 1, yi);
+        }
+        if (!PAIR || !texel_pair_u8(im, xi, yi + 1, c, d)) {
+            c = texel3(im, xi, yi + 1);
+            d = texel3(im, xi + 1, yi + 1);
+        }
         // contraction of the reference build: w_a*a rounded, then fma(w_b, b), fma(w_c, c), fma(w_d, d)
         float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
         f3 r = F3(fma_(wd, d.x, fma_(wc, c.x, fma_(wb, b.x, rmul(wa, a.x)))),
@@ -71,6 +105,8 @@ __device__ f3 tex_eval(int id, float u, float v) {
     }
     return F3(0, 0, 0);
 }
+
+__device__ __forceinline__ f3 tex_eval(int id, float u, float v) { return tex_eval_t<true>(id, u, v); }
 
 // Texture::alpha (Texture.hpp:112-114, Texture.cpp:47-62, 41-45)
 __device__ float tex_alpha(int id, float u, float v) {
@@ -121,7 +157,7 @@ __device__ bool mat_alpha(int mid, float u, float v, f3 ro, f3 rd, int prim) {
     if (mid < 0) return true;
     const pt_material& m = S.materials[mid];
     if (m.kind != PT_MAT_DIFFUSE && m.kind != PT_MAT_DIELECTRIC) return true;
-    float a = m.alpha >= 0 ? tex_eval(m.alpha, u, v).x : tex_alpha(m.tex, u, v);
+    float a = m.alpha >= 0 ? tex_eval_t<false>(m.alpha, u, v).x : tex_alpha(m.tex, u, v);
     if (m.alpha_mode == PT_ALPHA_OPAQUE) return true;
     if (m.alpha_mode == PT_ALPHA_MASK) return a > m.alpha_cutoff;
     return a >= 1.0f ? true : (blend_random(ro, rd, prim) < a);
