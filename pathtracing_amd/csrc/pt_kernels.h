@@ -24,6 +24,7 @@
 // host snapshot slot (pinned, written by the iteration prologue)
 #define SNAP_PATHS 0        // paths entering the iteration
 #define SNAP_SHADOW_PREV 1  // shadow rays of the previous iteration
+#define SNAP_NEW 2          // camera paths the previous iteration started
 #define SNAP_WORDS 16
 
 // 64-bit work counters

@@ -75,6 +75,7 @@ __device__ __forceinline__ void iteration_prologue(const uint32_t* __restrict__ 
     if (threadIdx.x == 0) {
         snap[SNAP_PATHS] = path_count(in);
         snap[SNAP_SHADOW_PREV] = in[Q_SHADOW];
+        snap[SNAP_NEW] = in[Q_NEW];
     }
 }
 

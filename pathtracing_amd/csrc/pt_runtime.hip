@@ -918,18 +918,23 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         PathSoA cur = c->PA, nxt = c->PB;
         hipLaunchKernelGGL(k_fill, dim3((paths + 255) / 256), dim3(256), 0, sm, R, paths, cur, set[0], next_sample);
         HIPCHK(c, hipGetLastError());
-        const dim3 gt(use_pool ? c->blocks_closest : (paths + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK);
-        const dim3 ga(use_pool ? c->blocks_any : (paths + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK);
-        const dim3 gs((paths + 255) / 256);
-        const dim3 gsort((paths + 256 * PT_SORT_PER - 1) / (256 * PT_SORT_PER));  // k_sort_count / k_sort_scatter
         uint32_t issued = 0, read = 0;
         bool drained = false;
+        // Tail grids: once every camera sample of the chunk has been started
+        // (read from the snapshots: the fill, then each iteration's new paths),
+        // path counts can only fall, so the count entering the last iteration
+        // read bounds every later one and the grids shrink to it (the kernels
+        // still read their exact counts from device memory).
+        uint64_t started = 0;
+        uint32_t bound = paths;
         // reads iteration `read`'s snapshot (after its event): stats, timing, end test
         auto consume = [&]() -> pt_status {
             const uint32_t slot = read % PT_RING;
             HIPCHK(c, hipEventSynchronize(c->rev[slot][4]));
             const volatile uint32_t* hc = c->host_cnt + slot * SNAP_WORDS;
             const uint32_t n_in = hc[SNAP_PATHS];
+            started += read == 0 ? n_in : hc[SNAP_NEW];
+            if (started >= R.chunk_total) bound = std::min(bound, n_in);
             if (stats) {
                 stats->rays_any += hc[SNAP_SHADOW_PREV];
                 if (n_in) {
@@ -958,6 +963,13 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                 continue;
             }
             const uint32_t i = issued;
+            const uint32_t nb = std::max(bound, 1u);
+            const dim3 gt(use_pool ? std::min(c->blocks_closest, (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK)
+                                   : (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK);
+            const dim3 ga(use_pool ? std::min(c->blocks_any, (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK)
+                                   : (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK);
+            const dim3 gs((nb + 255) / 256);
+            const dim3 gsort((nb + 256 * PT_SORT_PER - 1) / (256 * PT_SORT_PER));  // k_sort_count / k_sort_scatter
             uint32_t* in = set[i % 3];
             uint32_t* out = set[(i + 1) % 3];
             uint32_t* spare = set[(i + 2) % 3];
@@ -1013,7 +1025,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             if (rd->integrator == PT_INTEGRATOR_VOLPATH) {
                 // transmittance along the shadow rays: one ray per lane, the grid covers the capacity
                 hipLaunchKernelGGL(count ? k_shadow_tr<true> : k_shadow_tr<false>,
-                                   dim3((paths + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK), dim3(PT_TRACE_BLOCK), 0, sm,
+                                   dim3((nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK), dim3(PT_TRACE_BLOCK), 0, sm,
                                    nxt, c->sample_L, (const ShadowRec*)c->sq, (const uint32_t*)(out + Q_SHADOW),
                                    c->counters);
             } else if (rd->integrator != PT_INTEGRATOR_SIMPLE) {
