@@ -95,6 +95,12 @@ struct DevPrimInfo {
     uint32_t index;  // triangle / quad / sphere id, BLAS root ref
 };
 
+// Guide table of the power light sampler: entry b = the first light whose
+// running sum reaches fl(b / PT_LS_GUIDE * total) (PT_LS_GUIDE: the count of
+// n lights when none does).  A draw u in bucket floor(u * PT_LS_GUIDE) has its
+// pick between entries b and b + 1, so the search covers a few lights.
+#define PT_LS_GUIDE 4096u
+
 struct DevScene {
     float bb_lo[3], bb_scale[3];  // scene box: lo and 16 / extent per axis (spatial hit sort)
     const uint32_t* ray_order;    // closest-hit claim order (PT_RENDER_SORT_RAYS), else null
@@ -123,6 +129,7 @@ struct DevScene {
     uint32_t light_sampler;
     const uint32_t* sampler_lights;
     const float* sampler_cdf;  // running float sums (PowerLightSampler::Sample order)
+    const uint32_t* sampler_guide;  // PT_LS_GUIDE + 1 search starts over sampler_cdf (ls_sample)
     uint32_t n_sampler_lights;
     float sampler_total;
     const uint32_t* infinite_lights;

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <vector>
 
@@ -604,6 +605,18 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
     UP(DS.lights, s->lights, s->n_lights);
     UP(DS.sampler_lights, s->sampler_lights, s->n_sampler_lights);
     UP(DS.sampler_cdf, cdf.data(), cdf.size());
+    {  // guide table (pt_device.h PT_LS_GUIDE): bucket b starts at the first
+       // running sum >= fl(b / K * total), computed in float like ls_sample
+        std::vector<uint32_t> guide(PT_LS_GUIDE + 1);
+        uint32_t i = 0;
+        for (uint32_t b = 0; b <= PT_LS_GUIDE; b++) {
+            const float lo = b == PT_LS_GUIDE ? std::numeric_limits<float>::infinity()
+                                              : ((float)b / (float)PT_LS_GUIDE) * acc;
+            while (i < cdf.size() && !(cdf[i] >= lo)) i++;
+            guide[b] = b == PT_LS_GUIDE ? (uint32_t)cdf.size() : i;
+        }
+        UP(DS.sampler_guide, guide.data(), guide.size());
+    }
     UP(DS.infinite_lights, s->infinite_lights, s->n_infinite_lights);
     UP(DS.light_dist, s->light_dist, s->n_light_dist);
     UP(DS.media, s->media, s->n_media);

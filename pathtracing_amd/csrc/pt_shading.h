@@ -924,7 +924,11 @@ __device__ int ls_sample(float u) {
         return (int)S.sampler_lights[idx];
     }
     float target = u * S.sampler_total;
-    uint32_t lo = 0, hi = n;  // first i with cdf[i] >= target
+    // first i with cdf[i] >= target; the guide table narrows [0, n) to
+    // [guide[b], guide[b + 1]): target >= fl(b / K * total) because u >= b / K
+    // and rounding is monotone, and target <= fl((b + 1) / K * total)
+    const uint32_t b = min((uint32_t)(u * (float)PT_LS_GUIDE), PT_LS_GUIDE - 1u);
+    uint32_t lo = S.sampler_guide[b], hi = S.sampler_guide[b + 1];
     while (lo < hi) {
         uint32_t mid = (lo + hi) >> 1;
         if (S.sampler_cdf[mid] >= target) hi = mid;
