@@ -355,6 +355,11 @@ pt_status pt_bsdf_cases(pt_ctx* ctx, int32_t material, const float* cases, uint3
  * n cases of 5 floats {uv[2], reference point[3]} -> n_lights*n records of
  * 18 floats {L[3], p[3], n[3], uv[2], dir[3], pdf, L(p)[3]}.  Host pointers. */
 pt_status pt_light_cases(pt_ctx* ctx, const float* cases, uint32_t n, float* out);
+/* Test hook: LightSampler::Sample(u) (LightSampler.cpp:7-11, 34-46; replaces
+ * the reference's in-Li call at Integrators.cpp:262) for n draws u ->
+ * the picked light's index into pt_scene_desc.lights, -1 when the sampler
+ * is empty.  Host pointers. */
+pt_status pt_light_picks(pt_ctx* ctx, const float* u, uint32_t n, int32_t* out);
 /* Film resolve (Film::WritePNG / WritePPM, Film.hpp:154-217): per pixel
  * color = sum RGB*w / sum w, the tone mapper (through the writers'
  * std::function<vec3(vec3)>, i.e. in float around a double body),

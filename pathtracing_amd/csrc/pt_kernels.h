@@ -144,6 +144,7 @@ __global__ void k_adapt_decide(const uint32_t* list, const uint32_t* n, const Ad
 __global__ void k_interact(const pt_ray* rays, uint32_t n, float* out);
 __global__ void k_bsdf_cases(int mid, const float* in, uint32_t n, float* out);
 __global__ void k_light_cases(const float* in, uint32_t n, float* out);
+__global__ void k_light_picks(const float* u, uint32_t n, int32_t* out);
 template <bool QN>
 __global__ void k_trace_rays(const pt_ray* rays, uint32_t n, int any, pt_hit* out, uint32_t* pool, uint32_t* ovf,
                              unsigned long long* counters);

@@ -420,6 +420,13 @@ __global__ void k_bsdf_cases(int mid, const float* __restrict__ in, uint32_t n, 
     o[19] = mat_pdf(mid, rd, si, other);
 }
 
+// Test hook: LightSampler::Sample(u) picks (pt_light_picks): the light index
+// ls_sample returns (-1: no light), one per u.
+__global__ void k_light_picks(const float* __restrict__ u, uint32_t n, int32_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = ls_sample(u[i]);
+}
+
 // Test hook: Light::sample / PDF / L per light x case (pt_light_cases);
 // case {uv[2], ref point[3]}, record layout of oracle_lights.
 __global__ void k_light_cases(const float* __restrict__ in, uint32_t n, float* __restrict__ out) {

@@ -1453,5 +1453,17 @@ extern "C" pt_status pt_light_cases(pt_ctx* c, const float* cases, uint32_t n, f
                     });
 }
 
+extern "C" pt_status pt_light_picks(pt_ctx* c, const float* u, uint32_t n, int32_t* out) {
+    if (!c || (n && (!u || !out))) return PT_ERR_ARG;
+    if (!c->has_scene) return fail(c, PT_ERR_STATE, "no scene uploaded");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (n == 0) return PT_OK;
+    return run_hook(c, u, (size_t)n * sizeof(float), reinterpret_cast<float*>(out), (size_t)n * sizeof(int32_t),
+                    [&](void* din, float* dout) {
+                        hipLaunchKernelGGL(k_light_picks, dim3((n + 255) / 256), dim3(256), 0, c->stream,
+                                           (const float*)din, n, reinterpret_cast<int32_t*>(dout));
+                    });
+}
+
 // Device BVH build (pt_bvh4_build_device)
 #include "pt_bvh_gpu.hip"

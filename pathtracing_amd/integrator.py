@@ -125,6 +125,13 @@ class Context:
                                         out.ctypes.data), self.ptr)
         return out
 
+    def light_picks(self, u: np.ndarray) -> np.ndarray:
+        """LightSampler::Sample(u) on the device: picked light index per u (test hook)."""
+        u = np.ascontiguousarray(u, np.float32)
+        out = np.zeros(u.shape[0], np.int32)
+        N.check(self._lib.pt_light_picks(self.ptr, u.ctypes.data, u.shape[0], out.ctypes.data), self.ptr)
+        return out
+
     def light_cases(self, cases: np.ndarray, n_lights: int) -> np.ndarray:
         """Light sample / PDF / L for every light x case: (n_lights*n, 18) (test hook)."""
         cases = np.ascontiguousarray(cases, np.float32)

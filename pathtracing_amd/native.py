@@ -192,6 +192,8 @@ def lib():
     L.pt_bsdf_cases.restype = C.c_int32
     L.pt_light_cases.argtypes = [vp, vp, C.c_uint32, vp]
     L.pt_light_cases.restype = C.c_int32
+    L.pt_light_picks.argtypes = [vp, vp, C.c_uint32, vp]
+    L.pt_light_picks.restype = C.c_int32
     L.pt_scene_device_bytes.argtypes = [vp]
     L.pt_scene_device_bytes.restype = C.c_uint64
     L.pt_bvh4_build.argtypes = [vp, C.c_uint32, vp, C.POINTER(C.c_uint32), C.POINTER(RefNode), vp, vp]

@@ -328,6 +328,40 @@ def test_gpu_bsdf_matches_oracle_and_reference(case):
         assert close.mean() >= 0.98, f"material {m}: {close.mean():.3f} close to the reference"
 
 
+def test_gpu_light_sampler_picks_match_the_running_sum_scan(case):
+    """LightSampler::Sample(u) on the device (pt_light_picks: guide table +
+    search over the float running sums) against the reference's scan
+    restated in numpy (UniformLightSampler: min(u*n, n-1); PowerLightSampler:
+    first running sum >= u*total, LightSampler.cpp:7-11, 34-46), on random
+    draws, both sides of every guide-bucket edge and the draws whose u*total
+    lands on a running sum: identical picks."""
+    name, setup, integ, fx = case
+    flat = integ.flat
+    sl = np.asarray(flat.sampler_lights, np.int64)
+    rng = np.random.default_rng(7)
+    one = np.float32(1.0)
+    u = [rng.integers(0, 1 << 24, 100_000) * np.float32(2.0 ** -24)]
+    edges = np.arange(4096, dtype=np.float32) / np.float32(4096)
+    u += [edges, np.nextafter(edges, np.float32(0)), np.nextafter(edges, one)]
+    n = len(sl)
+    if n:
+        pw = flat.lights["power"][sl].astype(np.float32)
+        cdf = np.cumsum(pw, dtype=np.float32)
+        uc = (cdf / cdf[-1]).astype(np.float32)
+        u += [uc, np.nextafter(uc, np.float32(0)), np.nextafter(uc, one)]
+    u = np.clip(np.concatenate(u).astype(np.float32), 0, np.float32(1 - 2.0 ** -24))
+    got = integ.context().light_picks(u)
+    if n == 0:
+        assert (got == -1).all()
+        return
+    if flat.light_sampler == 0:
+        i = np.minimum((u * np.float32(n)).astype(np.int64), n - 1)
+    else:
+        target = (u * cdf[-1]).astype(np.float32)
+        i = np.minimum(np.searchsorted(cdf, target, side="left"), n - 1)
+    np.testing.assert_array_equal(got, sl[i])
+
+
 def test_gpu_light_samples_match_oracle_and_reference(case):
     """Light::sample / PDF / L on the fixture cases, device vs oracle (bit for
     bit) and vs the reference (unit-fixture tolerance)."""
