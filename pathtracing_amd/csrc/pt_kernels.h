@@ -125,6 +125,9 @@ enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1, PT_SORT_RAYS = 2 };
 #define PT_SORT_CELL_BITS 4  // spatial sort: 2^bits cells per axis of the scene box
 #endif
 #define PT_SORT_BINS_SPATIAL (1 << (3 * PT_SORT_CELL_BITS))
+#ifndef PT_SHADE_BLOCK
+#define PT_SHADE_BLOCK 256  // k_shade threads per block (its appends aggregate per block)
+#endif
 #ifndef PT_SORT_PER
 #define PT_SORT_PER 16u  // paths per thread of k_sort_count / k_sort_scatter
 #endif

@@ -571,14 +571,14 @@ template <int INTEGRATOR>
 #else
 #define PT_SHADE_WAVES
 #endif
-__global__ __launch_bounds__(256) PT_SHADE_WAVES void k_shade(RenderParams R, PathSoA cur, const uint32_t* __restrict__ nptr,
+__global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderParams R, PathSoA cur, const uint32_t* __restrict__ nptr,
                                               const float4* __restrict__ hit, PathSoA next,
                                               float* __restrict__ sample_L,
                                               unsigned long long* __restrict__ next_sample,
                                               ShadowRec* __restrict__ sq, uint32_t* __restrict__ cnt) {
     const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
-    if (blockIdx.x * 256 >= n) return;  // block-uniform: the grid covers the capacity
-    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (blockIdx.x * PT_SHADE_BLOCK >= n) return;  // block-uniform: the grid covers the capacity
+    const uint32_t t = blockIdx.x * PT_SHADE_BLOCK + threadIdx.x;
     const uint32_t i = (R.order && t < n) ? R.order[t] : t;  // material-sorted order, or the path order
     bool cont = false, done = false, shadow = false;
     ShadowRec srec;
@@ -761,7 +761,7 @@ __global__ __launch_bounds__(256) PT_SHADE_WAVES void k_shade(RenderParams R, Pa
     const int qoff[3] = {Q_NEXT, Q_SHADOW, Q_NEW};
     const bool pred[3] = {cont, shadow, ns.enq};
     uint32_t at[3];
-    block_append<3, 256>(cnt, qoff, pred, at);
+    block_append<3, PT_SHADE_BLOCK>(cnt, qoff, pred, at);
     const uint32_t a = cont ? at[0] : next.cap - 1u - at[2], c = at[1];
     if (cont) {
         next.o[a] = make_float4(ro.x, ro.y, ro.z, __uint_as_float(key));

@@ -981,7 +981,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                                    : (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK);
             const dim3 ga(use_pool ? std::min(c->blocks_any, (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK)
                                    : (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK);
-            const dim3 gs((nb + 255) / 256);
+            const dim3 gs((nb + 255) / 256), gsh((nb + PT_SHADE_BLOCK - 1) / PT_SHADE_BLOCK);
             const dim3 gsort((nb + 256 * PT_SORT_PER - 1) / (256 * PT_SORT_PER));  // k_sort_count / k_sort_scatter
             uint32_t* in = set[i % 3];
             uint32_t* out = set[(i + 1) % 3];
@@ -1024,14 +1024,14 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                 R.order = c->sort_order;
             }
             if (rd->integrator == PT_INTEGRATOR_SIMPLE)
-                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_SIMPLE>, gs, dim3(256), 0, sm, R, cur,
+                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_SIMPLE>, gsh, dim3(PT_SHADE_BLOCK), 0, sm, R, cur,
                                    (const uint32_t*)(in + Q_NEXT), (const float4*)c->hit, nxt, c->sample_L,
                                    next_sample, c->sq, out);
             else if (rd->integrator == PT_INTEGRATOR_VOLPATH)
                 hipLaunchKernelGGL(k_shade_vol, gs, dim3(256), 0, sm, R, cur, (const uint32_t*)(in + Q_NEXT),
                                    (const float4*)c->hit, nxt, c->sample_L, next_sample, c->sq, out);
             else
-                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_PATH>, gs, dim3(256), 0, sm, R, cur,
+                hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_PATH>, gsh, dim3(PT_SHADE_BLOCK), 0, sm, R, cur,
                                    (const uint32_t*)(in + Q_NEXT), (const float4*)c->hit, nxt, c->sample_L,
                                    next_sample, c->sq, out);
             if (timing) HIPCHK(c, hipEventRecord(ev[2], sm));
