@@ -126,7 +126,10 @@ enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1, PT_SORT_RAYS = 2 };
 #endif
 #define PT_SORT_BINS_SPATIAL (1 << (3 * PT_SORT_CELL_BITS))
 #ifndef PT_SHADE_BLOCK
-#define PT_SHADE_BLOCK 256  // k_shade threads per block (its appends aggregate per block)
+// k_shade threads per block (its appends aggregate per block): C4 64 / 128 /
+// 256 / 512 / 1024 -> 1206 / 1236 / 1270 / 1205 / 1278 Mrays/s
+// (profiles/r02_ab_shade.txt)
+#define PT_SHADE_BLOCK 1024
 #endif
 #ifndef PT_SORT_PER
 #define PT_SORT_PER 16u  // paths per thread of k_sort_count / k_sort_scatter

@@ -512,7 +512,7 @@ struct NewSample {
 };
 __device__ __forceinline__ NewSample claim_camera_sample(const RenderParams& R, bool want,
                                                          unsigned long long* __restrict__ next_sample) {
-    __shared__ uint32_t s_w[5];
+    __shared__ uint32_t s_w[17];  // up to 1024 threads per block
     __shared__ unsigned long long s_base;
     const uint64_t m = __ballot(want);
     const uint32_t wave = threadIdx.x >> 6;
