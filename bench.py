@@ -17,8 +17,9 @@ before the timed region.
 (torch.distributed.run, one process per GPU) before anything touches the GPU;
 under the driver's own launcher (WORLD_SIZE set) it checks WORLD_SIZE == N.
 Samples are interleaved across ranks (s % N == rank), the per-rank films are
-summed onto rank 0 with dist.reduce (RCCL); value = all ranks' rays / max-rank
-time.  Total work per frame is fixed as N grows ("scaling": "strong").
+summed onto rank 0 by the library's own RCCL communicator (pt_film_reduce;
+torch.distributed's reduce if RCCL refuses it); value = all ranks' rays /
+max-rank time.  Total work per frame is fixed as N grows ("scaling": "strong").
 """
 from __future__ import annotations
 
@@ -249,6 +250,11 @@ def main():
     integ.context(device)  # scene upload
     torch.cuda.synchronize(device)
     setup_s = time.perf_counter() - t_setup
+    film_reduce = None
+    if world > 1:  # the film reduce through the library's own RCCL communicator
+        from pathtracing_amd.distributed import init_film_comm
+        film_reduce = ("pt_film_reduce (library RCCL communicator)" if init_film_comm(integ, device)
+                       else "torch.distributed.reduce (RCCL)")
     if rank == 0:
         log(f"{args.config}: scene + BVH + upload {setup_s:.1f} s, {world} rank(s)")
 
@@ -382,6 +388,7 @@ def main():
                        "spp": setup.spp, "max_depth": setup.max_depth, "integrator": setup.integrator,
                        "rays_per_step": int(total_rays / args.steps), "parallelism": f"sample-shard x{world}",
                        "world_size": dist.get_world_size() if world > 1 else 1,
+                       "film_reduce": film_reduce,
                        "setup_s": round(setup_s, 1)},
             "roofline": roof,
         }

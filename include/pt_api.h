@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PT_API_VERSION 3
+#define PT_API_VERSION 4
 
 typedef int32_t pt_status;
 #define PT_OK 0
@@ -34,6 +34,7 @@ typedef int32_t pt_status;
 #define PT_ERR_OOM (-3)     /* device allocation failed                     */
 #define PT_ERR_STATE (-4)   /* call order (e.g. render before upload)       */
 #define PT_ERR_NODEV (-5)   /* no HIP device                                */
+#define PT_ERR_COMM (-6)    /* RCCL communicator error                      */
 
 /* ------------------------------------------------------------------------ */
 /* Reference-form BVH4 (BVH.hpp:38-60), byte-identical to BVH4_NODE /        */
@@ -290,6 +291,10 @@ typedef struct pt_stats {
     double ms_shade;           /* TIMING: summed shade kernel time              */
     uint64_t launches_closest;
     uint64_t launches_any;
+    uint64_t stack_overflows;  /* traversal stack pushes beyond the stack's
+                                  capacity (dropped; the test suite asserts 0) */
+    uint32_t n_devices;        /* devices that rendered                         */
+    uint32_t pad;
 } pt_stats;
 
 /* Rays for the pt_trace test hook (Scene::Intersect / IntersectPred). */
@@ -305,7 +310,28 @@ typedef struct pt_hit {
 typedef struct pt_ctx pt_ctx;
 
 int pt_version(void);
-pt_status pt_create(pt_ctx** ctx, int device);
+/* A context over n_devices GPUs (device_ids: n_devices HIP device indices,
+ * NULL = 0 .. n_devices-1).  It owns per device the scene replica, wavefront
+ * buffers and streams, and for n_devices > 1 one RCCL communicator per device
+ * (ncclCommInitAll).  pt_render / pt_render_adaptive then shard the frame over
+ * the devices (one host thread per device: interleaved samples at fixed SPP,
+ * 32x32 tiles when adaptive) and reduce the per-device films with
+ * ncclReduce(ncclSum) onto the first device before the result reaches
+ * film_accum -- the reference's Film::Merge of atomic<double> adds
+ * (Film.hpp:125-132, 244-253) called from TileIntegrator::Render
+ * (Integrators.cpp:112).  Test hooks run on the first device. */
+pt_status pt_create(pt_ctx** ctx, int n_devices, const int* device_ids);
+int pt_device_count(const pt_ctx* ctx);
+/* Multi-process form of the film reduce (one process per GPU, e.g. under
+ * torch.distributed): rank 0 draws an id (PT_COMM_ID_BYTES bytes), the host
+ * broadcasts it, every rank joins with its rank; pt_film_reduce then sums
+ * n doubles of device memory film (on the context's first device) over the
+ * ranks onto `root` (ncclReduce, in place, on the context's stream; blocks).
+ * A 1-rank communicator is valid (the reduce is then the identity). */
+#define PT_COMM_ID_BYTES 128
+pt_status pt_comm_unique_id(uint8_t* id_out);
+pt_status pt_comm_init_rank(pt_ctx* ctx, int n_ranks, int rank, const uint8_t* id);
+pt_status pt_film_reduce(pt_ctx* ctx, double* film, uint64_t n, int root);
 void pt_destroy(pt_ctx* ctx);
 const char* pt_last_error(const pt_ctx* ctx);   /* ctx may be NULL          */
 pt_status pt_set_stream(pt_ctx* ctx, void* hip_stream); /* NULL = ctx stream */

@@ -729,37 +729,39 @@ std::array<glm::vec2, 4> PCGSampler::get2Dx4f() {
 class HipBackend {
 public:
     Flat flat;
-    std::vector<pt_ctx*> ctx;
+    pt_ctx* ctx = nullptr;  // one context over the frame's GPUs (pt_create(ctx, n, ids))
     RenderStats stats;
-    std::vector<double> last;  // the merged accumulation of the last frame
+    std::vector<double> last;  // the reduced accumulation of the last frame
     std::vector<uint32_t> counts;  // samples per pixel of the last frame
 
-    ~HipBackend() {
-        for (pt_ctx* c : ctx) pt_destroy(c);
-    }
+    ~HipBackend() { pt_destroy(ctx); }
 
+    // The scene is flattened once; the context (and its RCCL communicators)
+    // is rebuilt when the requested GPU count changes.
     void ensure(const Scene& scene, const std::shared_ptr<LightSampler>& ls, unsigned n,
                 const std::shared_ptr<Medium>& camera_medium = nullptr) {
-        if (ctx.empty()) {
+        if (!flat_built) {
             flat.build(scene, ls);
             flat.medium(camera_medium);
+            flat_built = true;
         }
         int devices = 0;
         if (hipcount(&devices) != 0 || devices <= 0) throw std::runtime_error("HipPathIntegrator: no HIP device");
-        const unsigned want = std::max(1u, std::min<unsigned>(n, (unsigned)devices));
+        const int want = (int)std::max(1u, std::min<unsigned>(n, (unsigned)devices));
+        if (ctx && pt_device_count(ctx) == want) return;
+        pt_destroy(ctx);
+        ctx = nullptr;
+        check(pt_create(&ctx, want, nullptr), "pt_create");
         const pt_scene_desc d = flat.desc();
-        while (ctx.size() < want) {
-            pt_ctx* c = nullptr;
-            check(pt_create(&c, (int)ctx.size()), "pt_create");
-            ctx.push_back(c);
-            check(pt_scene_upload(c, &d), "pt_scene_upload", c);
-        }
+        check(pt_scene_upload(ctx, &d), "pt_scene_upload", ctx);
     }
 
-    // Renders shards 0..n-1 (one host thread per GPU) and merges into film:
-    // interleaved sample shards at fixed SPP, 32x32-tile shards when adaptive.
-    void render(const Camera& cam, uint32_t integrator, uint32_t spp, uint32_t depth, uint32_t seed, unsigned n,
-                bool adaptive) {
+    // One pt_render over the context's GPUs: the library shards the frame
+    // (interleaved samples at fixed SPP, 32x32 tiles when adaptive), renders
+    // one host thread per GPU and reduces the per-GPU films with ncclReduce
+    // onto the first GPU; the result is merged into the Film once
+    // (Film::Merge, Film.hpp:125-132).
+    void render(const Camera& cam, uint32_t integrator, uint32_t spp, uint32_t depth, uint32_t seed, bool adaptive) {
         const pt_camera_desc cd = camera_desc(cam, flat);
         const auto film = cam.GetFilm();
         const glm::ivec2 res = film->Resolution();
@@ -770,33 +772,18 @@ public:
         rd.max_depth = depth;
         rd.seed = seed;
         filter_desc(*film, rd);
-        rd.shard_count = n;
-        std::vector<std::vector<double>> acc(n, std::vector<double>(4 * npx, 0.0));
-        std::vector<std::vector<uint32_t>> cnt(n, std::vector<uint32_t>(npx, 0));
-        std::vector<pt_stats> st(n);
-        std::vector<std::string> err(n);
-        auto t0 = std::chrono::steady_clock::now();
-        std::vector<std::thread> th;
-        for (unsigned g = 0; g < n; g++) {
-            th.emplace_back([&, g] {
-                pt_render_desc r = rd;
-                r.shard_index = g;
-                const pt_status e = adaptive ? pt_render_adaptive(ctx[g], &cd, &r, acc[g].data(), cnt[g].data(), &st[g])
-                                             : pt_render(ctx[g], &cd, &r, acc[g].data(), &st[g]);
-                if (e != PT_OK) err[g] = pt_last_error(ctx[g]);
-            });
-        }
-        for (auto& t : th) t.join();
-        for (unsigned g = 0; g < n; g++)
-            if (!err[g].empty()) throw std::runtime_error("pt_render: " + err[g]);
-        // {sum RGB*w, sum w} per pixel into the Film (Film.hpp:118-132)
+        rd.shard_count = 1;
         last.assign(4 * npx, 0.0);
-        for (unsigned g = 0; g < n; g++)
-            for (size_t i = 0; i < 4 * npx; i++) last[i] += acc[g][i];
-        counts.assign(npx, adaptive ? 0u : spp);
-        if (adaptive)
-            for (unsigned g = 0; g < n; g++)
-                for (size_t i = 0; i < npx; i++) counts[i] += cnt[g][i];
+        pt_stats st{};
+        auto t0 = std::chrono::steady_clock::now();
+        if (adaptive) {
+            counts.assign(npx, 0u);
+            check(pt_render_adaptive(ctx, &cd, &rd, last.data(), counts.data(), &st), "pt_render_adaptive", ctx);
+        } else {
+            counts.assign(npx, spp);
+            check(pt_render(ctx, &cd, &rd, last.data(), &st), "pt_render", ctx);
+        }
+        // {sum RGB*w, sum w} per pixel into the Film (Film.hpp:118-132)
         FilmTile tile = film->GetFilmTile(Bounds2i{{0, 0}, res});
         for (int y = 0; y < res.y; y++)
             for (int x = 0; x < res.x; x++) {
@@ -807,15 +794,15 @@ public:
             }
         film->Merge(tile);
         stats = RenderStats{};
-        for (const auto& s : st) {
-            stats.paths += s.paths;
-            stats.rays_closest += s.rays_closest;
-            stats.rays_any += s.rays_any;
-        }
+        stats.paths = st.paths;
+        stats.rays_closest = st.rays_closest;
+        stats.rays_any = st.rays_any;
+        stats.devices = st.n_devices;
         stats.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
 
 private:
+    bool flat_built = false;
     static int hipcount(int* n);
 };
 
@@ -842,7 +829,7 @@ void HipPathIntegrator::Render(unsigned int n) const {
     if (!be_) be_ = std::make_unique<HipBackend>();
     be_->ensure(*scene, ls_, n);
     be_->render(*camera, PT_INTEGRATOR_PATH, sampler->SamplesPerPixel(), depth_, seed_of(sampler),
-                (unsigned)be_->ctx.size(), adaptive_);
+                adaptive_);
 }
 RenderStats HipPathIntegrator::LastStats() const { return be_ ? be_->stats : RenderStats{}; }
 static const std::vector<double> kEmpty;
@@ -859,7 +846,7 @@ void HipSimplePathIntegrator::Render(unsigned int n) const {
     if (!be_) be_ = std::make_unique<HipBackend>();
     be_->ensure(*scene, nullptr, n);
     be_->render(*camera, PT_INTEGRATOR_SIMPLE, sampler->SamplesPerPixel(), depth_, seed_of(sampler),
-                (unsigned)be_->ctx.size(), adaptive_);
+                adaptive_);
 }
 RenderStats HipSimplePathIntegrator::LastStats() const { return be_ ? be_->stats : RenderStats{}; }
 
@@ -874,7 +861,7 @@ void HipVolPathIntegrator::Render(unsigned int n) const {
     if (!be_) be_ = std::make_unique<HipBackend>();
     be_->ensure(*scene, ls_, n, camera->GetMedium());
     be_->render(*camera, PT_INTEGRATOR_VOLPATH, sampler->SamplesPerPixel(), depth_, seed_of(sampler),
-                (unsigned)be_->ctx.size(), adaptive_);
+                adaptive_);
 }
 RenderStats HipVolPathIntegrator::LastStats() const { return be_ ? be_->stats : RenderStats{}; }
 const std::vector<double>& HipVolPathIntegrator::LastAccumulation() const { return be_ ? be_->last : kEmpty; }

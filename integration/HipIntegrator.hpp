@@ -72,10 +72,11 @@ private:
 
 struct RenderStats {
     uint64_t paths = 0, rays_closest = 0, rays_any = 0;
+    uint32_t devices = 0;  // GPUs that rendered (films reduced over RCCL)
     double ms = 0;
 };
 
-class HipBackend;  // flattened scene + one pt_ctx per GPU
+class HipBackend;  // flattened scene + one multi-GPU pt_ctx
 
 class HipPathIntegrator : public PathIntegrator {
 public:

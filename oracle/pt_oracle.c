@@ -1178,11 +1178,12 @@ static lsample_t light_sample(const scene_t* S, const pt_light* l, float u0, flo
     if (l->kind == PT_LIGHT_TEX_INF) { /* TextureInfiniteLight::sample (Light.cpp:118-144) */
         const float* acc = S->s->light_dist + l->prim;
         const uint32_t N = (uint32_t)PT_TEXINF_X * PT_TEXINF_Y;
-        double weight = (double)uc * (double)acc[N - 1];
+        /* float weight = random_float() * totalWeight (double product, rounded) */
+        float weight = (float)((double)uc * (double)acc[N - 1]);
         uint32_t i = 0, hi = N; /* std::upper_bound: first running sum > weight */
         while (i < hi) {
             uint32_t mid = (i + hi) >> 1;
-            if ((double)acc[mid] > weight) hi = mid;
+            if (acc[mid] > weight) hi = mid;
             else i = mid + 1;
         }
         int cx = (int)(i % PT_TEXINF_Y), cy = (int)(i / PT_TEXINF_Y);

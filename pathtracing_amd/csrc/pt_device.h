@@ -142,6 +142,7 @@ struct DevScene {
     uint32_t n_instances;
     uint32_t* scratch;       // SCR_WORDS x scratch_lanes (instance traversal state)
     uint32_t scratch_lanes;
+    uint32_t* stack_drops;   // traversal pushes past the stack capacity (counted, rare)
 };
 
 // The uploaded scene of the current context, in constant memory: every

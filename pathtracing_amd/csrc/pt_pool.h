@@ -21,7 +21,7 @@
 #define PT_POOL_CHUNKS 8
 #define PT_POOL_STRIDE 32  // uint32 words between chunk counters (128 B)
 #define PT_POOL_WORDS (PT_POOL_CHUNKS * PT_POOL_STRIDE)
-// Stack entries the pool kernels keep in LDS; entries [PT_POOL_LDS, PT_STACK)
+// Stack entries the pool kernels keep in LDS; entries [PT_POOL_LDS, PT_POOL_STACK)
 // live in a global overflow array ([entry][grid lane], written and read back by
 // the same lane only).  Deep stacks are rare, and a 20-entry LDS stack (10 KB
 // per block) lets 32 waves per CU fit instead of 20 with all 32 in LDS.
@@ -85,6 +85,14 @@ __device__ unsigned int pt_diag[4];
 #endif
 // overflow words per stack entry per lane (ref + entry distance)
 #define PT_OVF_WORDS 2
+// Stack capacity of the pool kernels.  The reference's stack[32] is undefined
+// behaviour past 32 entries (BVH.hpp:1128); here the entries past the LDS part
+// live in HBM, so a deeper stack costs only that array.  A push past the
+// capacity is dropped and counted (DevScene::stack_drops -> pt_stats::
+// stack_overflows; the full-size C4 test asserts none).
+#ifndef PT_POOL_STACK
+#define PT_POOL_STACK 48
+#endif
 
 // Src interface:
 //   bool load(uint32_t ri, f3& o, f3& d, float& tmax)   (false: skip this ray)
@@ -101,7 +109,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
     constexpr bool ENT = PT_ENTRY && !ANY;
     const uint32_t lane = threadIdx.x;
     const uint32_t gl = blockIdx.x * PT_TRACE_BLOCK + lane, G = gridDim.x * PT_TRACE_BLOCK;
-    uint32_t* __restrict__ ovf_e = ovf + (size_t)(PT_STACK - LN) * G;
+    uint32_t* __restrict__ ovf_e = ovf + (size_t)(PT_POOL_STACK - LN) * G;
     const uint32_t wl = __lane_id();
     const uint32_t cs = (n + PT_POOL_CHUNKS - 1) / PT_POOL_CHUNKS;
     const uint32_t home = blockIdx.x % PT_POOL_CHUNKS;
@@ -114,11 +122,11 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
     int sp = 0, best = -1;
 
     const uint32_t all_dead = (1u << PT_POOL_CHUNKS) - 1u;
-    // pushes beyond PT_STACK are dropped, like the one-ray-per-lane kernels;
+    // pushes beyond PT_POOL_STACK are dropped and counted;
     // e < 0: never dropped at pop (BLAS roots: a fresh traversal, entry 0)
     auto push = [&](uint32_t v, float e = -1.0f) {
-        if (sp < PT_STACK) {
-            if (LN >= PT_STACK || sp < LN) {
+        if (sp < PT_POOL_STACK) {
+            if (LN >= PT_POOL_STACK || sp < LN) {
                 s_ref[sp * PT_TRACE_BLOCK + lane] = v;
                 if (ENT) s_ent[sp * PT_TRACE_BLOCK + lane] = (uint16_t)(__float_as_uint(e) >> 16);
             } else {
@@ -126,13 +134,15 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 if (ENT) ovf_e[(size_t)(sp - LN) * G + gl] = __float_as_uint(e);
             }
             ++sp;
+        } else {
+            atomicAdd(S.stack_drops, 1u);
         }
     };
     // pop; false: the popped entry lies beyond the current max (ENT only)
     auto pop = [&](uint32_t& r) -> bool {
         --sp;
         float e = -1.0f;
-        if (LN >= PT_STACK || sp < LN) {
+        if (LN >= PT_POOL_STACK || sp < LN) {
             r = s_ref[sp * PT_TRACE_BLOCK + lane];
             if (ENT) e = __uint_as_float((uint32_t)s_ent[sp * PT_TRACE_BLOCK + lane] << 16);
         } else {

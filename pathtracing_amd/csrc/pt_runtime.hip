@@ -6,6 +6,7 @@
 // array, and the light-sampler running sums.  pt_render runs the persistent
 // wavefront (pt_kernels.hip) over sample chunks and gathers the film.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -16,6 +17,7 @@
 #include <cstring>
 #include <limits>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pt_kernels.hip"
@@ -77,6 +79,13 @@ struct pt_ctx {
     uint64_t ray_order_cap = 0, ray_counts_cap = 0;
     hipEvent_t ev[8] = {};
     hipEvent_t rev[PT_RING][5] = {};  // per in-flight iteration: kernel boundaries [0..2], end [4] ([3] unused)
+    uint32_t* stack_drops = nullptr;  // device word: traversal pushes beyond the stack (DevScene::stack_drops)
+    // multi-device context (pt_create with n_devices > 1): the other devices'
+    // contexts (owned) and, per device, an RCCL communicator for the film reduce
+    std::vector<pt_ctx*> peers;
+    bool multi = false;  // renders through render_multi (n_devices > 1, or forced for tests)
+    ncclComm_t comm = nullptr;
+    int comm_ranks = 0, comm_rank = 0;
 };
 
 static pt_status fail(pt_ctx* c, pt_status code, const char* fmt, ...) {
@@ -101,8 +110,10 @@ extern "C" int pt_version(void) { return PT_API_VERSION; }
 
 extern "C" const char* pt_last_error(const pt_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
 
-extern "C" pt_status pt_create(pt_ctx** out, int device) {
-    if (!out) return PT_ERR_ARG;
+extern "C" void pt_destroy(pt_ctx* c);
+
+// One device's context (the whole context for n_devices = 1).
+static pt_status create_dev(pt_ctx** out, int device) {
     *out = nullptr;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
@@ -167,10 +178,116 @@ extern "C" pt_status pt_create(pt_ctx** out, int device) {
             hipSuccess ||
         hipHostGetDevicePointer((void**)&c->host_cnt_dev, c->host_cnt, 0) != hipSuccess) {
         g_err = "pinned alloc failed";
-        delete c;
+        pt_destroy(c);
         return PT_ERR_HIP;
     }
+    if (hipMalloc((void**)&c->stack_drops, 128) != hipSuccess || hipMemset(c->stack_drops, 0, 128) != hipSuccess) {
+        g_err = "device alloc failed";
+        pt_destroy(c);
+        return PT_ERR_OOM;
+    }
+    c->scene.stack_drops = c->stack_drops;
     *out = c;
+    return PT_OK;
+}
+
+extern "C" pt_status pt_create(pt_ctx** out, int n_devices, const int* device_ids) {
+    if (!out) return PT_ERR_ARG;
+    *out = nullptr;
+    if (n_devices < 1 || n_devices > 64) {
+        g_err = "n_devices out of range";
+        return PT_ERR_ARG;
+    }
+    std::vector<int> ids(n_devices);
+    for (int i = 0; i < n_devices; i++) {
+        ids[i] = device_ids ? device_ids[i] : i;
+        for (int j = 0; j < i; j++)
+            if (ids[j] == ids[i]) {
+                g_err = "a device is listed twice";
+                return PT_ERR_ARG;
+            }
+    }
+    pt_ctx* c = nullptr;
+    pt_status st = create_dev(&c, ids[0]);
+    if (st) return st;
+    for (int i = 1; i < n_devices; i++) {
+        pt_ctx* p = nullptr;
+        if ((st = create_dev(&p, ids[i])) != PT_OK) {
+            pt_destroy(c);
+            return st;
+        }
+        c->peers.push_back(p);
+    }
+    // PT_MULTI_DEVICE_PATH=1 (tests on a one-GPU box): a one-device context
+    // still gets its communicator and renders through render_multi
+    c->multi = n_devices > 1 || (getenv("PT_MULTI_DEVICE_PATH") && atoi(getenv("PT_MULTI_DEVICE_PATH")) != 0);
+    if (c->multi) {  // one communicator per device, ranks in device_ids order
+        std::vector<ncclComm_t> comms(n_devices);
+        const ncclResult_t r = ncclCommInitAll(comms.data(), n_devices, ids.data());
+        if (r != ncclSuccess) {
+            g_err = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
+            pt_destroy(c);
+            return PT_ERR_COMM;
+        }
+        for (int i = 0; i < n_devices; i++) {
+            pt_ctx* d = i ? c->peers[i - 1] : c;
+            d->comm = comms[i];
+            d->comm_ranks = n_devices;
+            d->comm_rank = i;
+        }
+    }
+    *out = c;
+    return PT_OK;
+}
+
+extern "C" int pt_device_count(const pt_ctx* c) { return c ? 1 + (int)c->peers.size() : 0; }
+
+extern "C" pt_status pt_comm_unique_id(uint8_t* id_out) {
+    static_assert(sizeof(ncclUniqueId) == PT_COMM_ID_BYTES, "RCCL unique id size");
+    if (!id_out) return PT_ERR_ARG;
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) {
+        g_err = std::string("ncclGetUniqueId: ") + ncclGetErrorString(r);
+        return PT_ERR_COMM;
+    }
+    memcpy(id_out, &id, sizeof(id));
+    return PT_OK;
+}
+
+extern "C" pt_status pt_comm_init_rank(pt_ctx* c, int n_ranks, int rank, const uint8_t* id) {
+    if (!c || !id || n_ranks < 1 || rank < 0 || rank >= n_ranks) return PT_ERR_ARG;
+    if (c->multi) return fail(c, PT_ERR_STATE, "a multi-device context has its communicators");
+    if (c->comm) return fail(c, PT_ERR_STATE, "communicator already initialised");
+    HIPCHK(c, hipSetDevice(c->device));
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof(uid));
+    const ncclResult_t r = ncclCommInitRank(&c->comm, n_ranks, uid, rank);
+    if (r != ncclSuccess) {
+        c->comm = nullptr;
+        return fail(c, PT_ERR_COMM, "ncclCommInitRank(%d of %d): %s", rank, n_ranks, ncclGetErrorString(r));
+    }
+    c->comm_ranks = n_ranks;
+    c->comm_rank = rank;
+    return PT_OK;
+}
+
+// In-place SUM reduce of n doubles onto `root` over the context's communicator,
+// on its stream (replaces Film::Merge's atomic<double> adds, Film.hpp:125-132).
+static pt_status film_reduce_async(pt_ctx* c, double* film, uint64_t n, int root) {
+    const ncclResult_t r = ncclReduce(film, film, n, ncclDouble, ncclSum, root, c->comm, c->stream);
+    if (r != ncclSuccess) return fail(c, PT_ERR_COMM, "ncclReduce: %s", ncclGetErrorString(r));
+    return PT_OK;
+}
+
+extern "C" pt_status pt_film_reduce(pt_ctx* c, double* film, uint64_t n, int root) {
+    if (!c || !film) return PT_ERR_ARG;
+    if (!c->comm) return fail(c, PT_ERR_STATE, "no communicator (pt_comm_init_rank)");
+    if (c->multi) return fail(c, PT_ERR_STATE, "multi-device contexts reduce inside pt_render");
+    if (root < 0 || root >= c->comm_ranks) return fail(c, PT_ERR_ARG, "root out of range");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (pt_status st = film_reduce_async(c, film, n, root)) return st;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return PT_OK;
 }
 
@@ -197,6 +314,9 @@ static void free_work(pt_ctx* c) {
 
 extern "C" void pt_destroy(pt_ctx* c) {
     if (!c) return;
+    for (pt_ctx* p : c->peers) pt_destroy(p);
+    c->peers.clear();
+    if (c->comm) ncclCommDestroy(c->comm);
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     free_scene(c);
@@ -208,6 +328,7 @@ extern "C" void pt_destroy(pt_ctx* c) {
                     (void*)c->sort_order, (void*)c->sort_counts, (void*)c->ray_order, (void*)c->ray_counts})
         if (p) hipFree(p);
     if (c->host_cnt) hipHostFree(c->host_cnt);
+    if (c->stack_drops) hipFree(c->stack_drops);
     for (auto& e : c->ev)
         if (e) hipEventDestroy(e);
     for (auto& r : c->rev)
@@ -226,6 +347,7 @@ extern "C" pt_status pt_set_stream(pt_ctx* c, void* s) {
 extern "C" pt_status pt_set_node_format(pt_ctx* c, int fmt) {
     if (!c || fmt < PT_NODES_AUTO || fmt > PT_NODES_QUANTIZED) return PT_ERR_ARG;
     c->node_format = fmt;
+    for (pt_ctx* p : c->peers) p->node_format = fmt;
     return PT_OK;
 }
 
@@ -410,7 +532,16 @@ struct Conv {
 
 extern "C" pt_status pt_bvh4_order_table(uint8_t* out);
 
+static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s);
 extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
+    if (!c) return PT_ERR_ARG;
+    // every device holds a full replica (C4 ~1 GB of 288 GB)
+    if (pt_status st = upload_dev(c, s)) return st;
+    for (pt_ctx* p : c->peers)
+        if (pt_status st = upload_dev(p, s)) return fail(c, st, "device %d: %s", p->device, p->err.c_str());
+    return PT_OK;
+}
+static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     if (!c || !s) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -660,6 +791,7 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
     DS.n_instances = s->n_instances;
     DS.scratch = nullptr;
     DS.scratch_lanes = 0;
+    DS.stack_drops = c->stack_drops;
     c->has_scene = true;
     c->n_media = s->n_media;
     c->n_materials = s->n_materials;
@@ -711,13 +843,18 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
     AL(c->qcnt, (3 * SET_WORDS + PT_POOL_WORDS) * 4);  // three counter sets, then pt_trace's pool
     AL(c->sq, n * sizeof(ShadowRec));
     AL(c->counters, (CNT_SHARDS + 1) * CNT_COUNT * 8);
-    // lanes of the larger traversal grid (pool: resident; one ray per lane: the
-    // capacity) x the stack entries beyond the smaller LDS part
+    // stack entries past the LDS part: the pool kernels' resident grid x
+    // (PT_POOL_STACK - their smaller LDS part); the one-ray-per-lane kernels
+    // keep their whole stack in LDS unless a tuning build splits it, and then
+    // the array covers their grid (the capacity) too
     // (refs, then as many entry distances: PT_OVF_WORDS words per entry)
-    constexpr int ovf_entries = PT_STACK - std::min({PT_POOL_LDS, PT_POOL_LDS_C, PT_SIMPLE_LN});
-    if (ovf_entries > 0)
-        AL(c->ovf, std::max<size_t>((size_t)c->trace_blocks * PT_TRACE_BLOCK, (n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK * PT_TRACE_BLOCK) *
-                       ovf_entries * PT_OVF_WORDS * 4);
+    {
+        constexpr bool simple_ovf = PT_SIMPLE_STEP || PT_SIMPLE_LN < PT_STACK;
+        constexpr int ovf_entries = PT_POOL_STACK - std::min({PT_POOL_LDS, PT_POOL_LDS_C, PT_SIMPLE_LDS});
+        size_t lanes = (size_t)c->trace_blocks * PT_TRACE_BLOCK;
+        if (simple_ovf) lanes = std::max<size_t>(lanes, (n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK * PT_TRACE_BLOCK);
+        AL(c->ovf, lanes * ovf_entries * PT_OVF_WORDS * 4);
+    }
 #undef AL
     if (hipMemset(c->qcnt, 0, (3 * SET_WORDS + PT_POOL_WORDS) * 4) != hipSuccess) {
         free_work(c);
@@ -858,7 +995,17 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     const uint64_t max_floats = (uint64_t)PT_SAMPLE_GIB << 28;
     uint64_t per_s = 3ull * R.npix_work;
     uint32_t s_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spp_local, max_floats / per_s));
-    pt_status st = ensure(c, &c->sample_L, c->sample_cap, per_s * s_chunk);
+    // a chunk's sample ids stay below SHADOW_DONE_BIT: a finished path's
+    // pending shadow record carries SHADOW_DONE_BIT | sid (pt_kernels.hip)
+    if ((uint64_t)R.npix_work >= SHADOW_DONE_BIT) return fail(c, PT_ERR_ARG, "film too large for 31-bit sample ids");
+    s_chunk = (uint32_t)std::min<uint64_t>(s_chunk, (SHADOW_DONE_BIT - 1ull) / R.npix_work);
+    pt_status st;
+    // a device with less free HBM (or a second context on it) gets smaller
+    // chunks instead of PT_ERR_OOM
+    while ((st = ensure(c, &c->sample_L, c->sample_cap, per_s * s_chunk)) == PT_ERR_OOM && s_chunk > 1) {
+        (void)hipGetLastError();
+        s_chunk = (s_chunk + 1) / 2;
+    }
     if (st) return st;
     // wavefront size: large scenes (pool traversal) take 128 M paths in flight,
     // so each traversal launch's tail (the last, longest rays) is amortised
@@ -868,7 +1015,12 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     uint32_t paths = rd->paths_in_flight ? rd->paths_in_flight : (big_scene ? PT_PATHS_POOL : PT_PATHS_SIMPLE);
     paths = (uint32_t)std::min<uint64_t>(paths, std::max<uint64_t>(1, (uint64_t)R.npix_work * s_chunk));
     paths = (paths + 255) & ~255u;
-    if ((st = ensure_work(c, paths)) != PT_OK) return st;
+    // ... and a smaller wavefront
+    while ((st = ensure_work(c, paths)) == PT_ERR_OOM && paths > (1u << 20)) {
+        (void)hipGetLastError();
+        paths = ((paths >> 1) + 255) & ~255u;
+    }
+    if (st) return st;
     if ((st = bind_scene(c)) != PT_OK) return st;  // instance scratch sized for this wavefront
 
     const bool count = (rd->flags & PT_RENDER_COUNT_NODES) != 0;
@@ -905,6 +1057,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     }
     hipStream_t sm = c->stream;
     HIPCHK(c, hipMemsetAsync(c->counters, 0, (CNT_SHARDS + 1) * CNT_COUNT * 8, sm));
+    HIPCHK(c, hipMemsetAsync(c->stack_drops, 0, 4, sm));
     // the sample-id counter sits on its own line after the work-counter shards
     unsigned long long* next_sample = c->counters + CNT_SHARDS * CNT_COUNT + CNT_NEXT_SAMPLE;
     float t_cl = 0, t_sh = 0, t_an = 0;
@@ -929,7 +1082,10 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         HIPCHK(c, hipMemsetAsync(c->qcnt, 0, 3 * SET_WORDS * 4, sm));
         // initial fill: one camera sample per wavefront entry
         PathSoA cur = c->PA, nxt = c->PB;
-        hipLaunchKernelGGL(k_fill, dim3((paths + 255) / 256), dim3(256), 0, sm, R, paths, cur, set[0], next_sample);
+        // never more paths in flight than the chunk has samples (late adaptive
+        // rounds hold a few active pixels): fill and grids sized to that
+        const uint32_t pfill = (uint32_t)std::min<uint64_t>(paths, (R.chunk_total + 255) & ~255ull);
+        hipLaunchKernelGGL(k_fill, dim3((pfill + 255) / 256), dim3(256), 0, sm, R, pfill, cur, set[0], next_sample);
         HIPCHK(c, hipGetLastError());
         uint32_t issued = 0, read = 0;
         bool drained = false;
@@ -939,7 +1095,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         // read bounds every later one and the grids shrink to it (the kernels
         // still read their exact counts from device memory).
         uint64_t started = 0;
-        uint32_t bound = paths;
+        uint32_t bound = pfill;
         // reads iteration `read`'s snapshot (after its event): stats, timing, end test
         auto consume = [&]() -> pt_status {
             const uint32_t slot = read % PT_RING;
@@ -1085,6 +1241,10 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         stats->ms_closest += t_cl;
         stats->ms_shade += t_sh;
         stats->ms_any += t_an;
+        uint32_t drops = 0;
+        HIPCHK(c, hipMemcpy(&drops, c->stack_drops, 4, hipMemcpyDeviceToHost));
+        stats->stack_overflows += drops;
+        stats->n_devices = 1;
     }
     return PT_OK;
 }
@@ -1143,11 +1303,27 @@ static pt_status with_film(pt_ctx* c, const pt_camera_desc* cam, double* film_ac
     return PT_OK;
 }
 
+static pt_status render_adaptive_dev(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd,
+                                     double* film_accum, uint32_t* sample_counts, pt_stats* stats);
+static pt_status render_multi(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_accum,
+                              uint32_t* sample_counts, pt_stats* stats, bool adaptive);
+static pt_status render_dev(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_accum,
+                            pt_stats* stats);
+
 extern "C" pt_status pt_render(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_accum,
                                pt_stats* stats) {
     pt_status st = check_render_args(c, cam, rd);
     if (st) return st;
     if (rd->flags & PT_RENDER_ADAPTIVE) return pt_render_adaptive(c, cam, rd, film_accum, nullptr, stats);
+    if (!film_accum) return fail(c, PT_ERR_ARG, "film_accum is null");
+    if (c->multi) return render_multi(c, cam, rd, film_accum, nullptr, stats, false);
+    return render_dev(c, cam, rd, film_accum, stats);
+}
+
+// One device's fixed-SPP frame (shard rd->shard_index of rd->shard_count).
+static pt_status render_dev(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_accum,
+                            pt_stats* stats) {
+    pt_status st;
     if (!film_accum) return fail(c, PT_ERR_ARG, "film_accum is null");
     if (!(rd->pixel_begin == 0 && rd->pixel_end == 0)) return fail(c, PT_ERR_ARG, "pt_render renders whole films");
     HIPCHK(c, hipSetDevice(c->device));
@@ -1180,6 +1356,115 @@ extern "C" pt_status pt_render_adaptive(pt_ctx* c, const pt_camera_desc* cam, co
     if (!film_accum) return fail(c, PT_ERR_ARG, "film_accum is null");
     if (rd->spp == 0) return fail(c, PT_ERR_ARG, "adaptive sampling needs spp >= 1");
     if (rd->spp > (1u << 24) / PT_ADAPT_MAX_ROUNDS) return fail(c, PT_ERR_ARG, "spp too large for 128 rounds");
+    if (c->multi) return render_multi(c, cam, rd, film_accum, sample_counts, stats, true);
+    return render_adaptive_dev(c, cam, rd, film_accum, sample_counts, stats);
+}
+
+// Multi-device frame: device g renders shard rd->shard_index + rd->shard_count*g
+// of rd->shard_count*n (interleaved samples; 32x32 tiles when adaptive) into
+// its own device film, on one host thread per device; then one grouped
+// ncclReduce(ncclSum) per device sums the films (and the adaptive sample
+// counts) onto the first device, whose result reaches film_accum.  This is
+// the reference's Film::Merge (Film.hpp:125-132, 244-253) after
+// TileIntegrator::Render's tiles (Integrators.cpp:112), over xGMI.
+static pt_status render_multi(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_accum,
+                              uint32_t* sample_counts, pt_stats* stats, bool adaptive) {
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<pt_ctx*> dv{c};
+    dv.insert(dv.end(), c->peers.begin(), c->peers.end());
+    const uint32_t n = (uint32_t)dv.size();
+    const uint64_t npx = (uint64_t)cam->width * cam->height, nf = 4 * npx;
+    for (pt_ctx* d : dv)
+        if (!d->comm) return fail(c, PT_ERR_STATE, "multi-device context without communicators");
+    const bool dev_film = is_device_ptr(film_accum);
+    std::vector<double*> films(n);
+    for (uint32_t g = 0; g < n; g++) {
+        pt_ctx* d = dv[g];
+        HIPCHK(c, hipSetDevice(d->device));
+        if (g == 0 && dev_film) {
+            films[g] = film_accum;  // accumulates in place; the reduce adds the others
+            continue;
+        }
+        if (pt_status st = ensure(d, &d->film, d->film_cap, nf)) return fail(c, st, "device %d: %s", d->device, d->err.c_str());
+        HIPCHK(c, hipMemsetAsync(d->film, 0, nf * 8, d->stream));
+        films[g] = d->film;
+    }
+    std::vector<pt_stats> st(n);
+    std::vector<pt_status> res(n, PT_OK);
+    {
+        std::vector<std::thread> th;
+        for (uint32_t g = 0; g < n; g++)
+            th.emplace_back([&, g] {
+                pt_ctx* d = dv[g];
+                if (hipSetDevice(d->device) != hipSuccess) {
+                    res[g] = fail(d, PT_ERR_HIP, "hipSetDevice(%d)", d->device);
+                    return;
+                }
+                pt_render_desc r = *rd;
+                const uint32_t sc = rd->shard_count ? rd->shard_count : 1;
+                r.shard_index = rd->shard_index + sc * g;
+                r.shard_count = sc * n;
+                r.flags &= ~PT_RENDER_ADAPTIVE;
+                res[g] = adaptive ? render_adaptive_dev(d, cam, &r, films[g], nullptr, &st[g])
+                                  : render_dev(d, cam, &r, films[g], &st[g]);
+            });
+        for (auto& t : th) t.join();
+    }
+    for (uint32_t g = 0; g < n; g++)
+        if (res[g] != PT_OK) return fail(c, res[g], "device %d: %s", dv[g]->device, dv[g]->err.c_str());
+    // the film (and count) reduce onto the first device, one grouped call
+    ncclResult_t r = ncclGroupStart();
+    for (uint32_t g = 0; g < n && r == ncclSuccess; g++) {
+        r = ncclReduce(films[g], films[g], nf, ncclDouble, ncclSum, 0, dv[g]->comm, dv[g]->stream);
+        if (r == ncclSuccess && adaptive)
+            r = ncclReduce(dv[g]->a_counts, dv[g]->a_counts, npx, ncclUint32, ncclSum, 0, dv[g]->comm, dv[g]->stream);
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+        return fail(c, PT_ERR_COMM, "film reduce: %s", ncclGetErrorString(r != ncclSuccess ? r : r2));
+    for (uint32_t g = 0; g < n; g++) {
+        HIPCHK(c, hipSetDevice(dv[g]->device));
+        HIPCHK(c, hipStreamSynchronize(dv[g]->stream));
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!dev_film) {
+        std::vector<double> h(nf);
+        HIPCHK(c, hipMemcpy(h.data(), films[0], nf * 8, hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < nf; i++) film_accum[i] += h[i];
+    }
+    if (adaptive && sample_counts) {
+        const hipMemcpyKind k = is_device_ptr(sample_counts) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+        HIPCHK(c, hipMemcpy(sample_counts, c->a_counts, 4 * npx, k));
+    }
+    if (stats) {
+        pt_stats S{};
+        for (const pt_stats& x : st) {
+            S.paths += x.paths;
+            S.rays_closest += x.rays_closest;
+            S.rays_any += x.rays_any;
+            S.nodes_closest += x.nodes_closest;
+            S.tris_closest += x.tris_closest;
+            S.nodes_any += x.nodes_any;
+            S.tris_any += x.tris_any;
+            S.shade_hits += x.shade_hits;
+            S.launches_closest += x.launches_closest;
+            S.launches_any += x.launches_any;
+            S.stack_overflows += x.stack_overflows;
+            S.ms_closest = std::max(S.ms_closest, x.ms_closest);
+            S.ms_any = std::max(S.ms_any, x.ms_any);
+            S.ms_shade = std::max(S.ms_shade, x.ms_shade);
+        }
+        S.n_devices = n;
+        S.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        *stats = S;
+    }
+    return PT_OK;
+}
+
+// One device's adaptive frame (pt_render_adaptive on a one-device context).
+static pt_status render_adaptive_dev(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd,
+                                     double* film_accum, uint32_t* sample_counts, pt_stats* stats) {
+    pt_status st;
     HIPCHK(c, hipSetDevice(c->device));
     const uint32_t npx = (uint32_t)cam->width * cam->height;
     if ((st = ensure(c, &c->a_est, c->a_est_cap, npx)) != PT_OK) return st;
@@ -1346,6 +1631,7 @@ extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any
     if (c->cap == 0 && ensure_work(c, 256) != PT_OK) return PT_ERR_OOM;
     if (pt_status bs = bind_scene(c)) return bs;
     HIPCHK(c, hipMemsetAsync(c->counters, 0, CNT_SHARDS * CNT_COUNT * 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->stack_drops, 0, 4, c->stream));
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
     uint32_t* pool = c->qcnt + 3 * SET_WORDS;
@@ -1380,6 +1666,10 @@ extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any
             stats->tris_closest = h[CNT_TRIS_CLOSEST];
             stats->ms_closest = ms;
         }
+        uint32_t drops = 0;
+        HIPCHK(c, hipMemcpy(&drops, c->stack_drops, 4, hipMemcpyDeviceToHost));
+        stats->stack_overflows = drops;
+        stats->n_devices = 1;
         stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     for (void* p : tmp) hipFree(p);

@@ -782,8 +782,8 @@ __device__ __noinline__ f3 tlight_normal(int inst, f3 n) {  // TransformedLight:
 }
 
 // TextureInfiniteLight::sample (Light.cpp:118-144): the cell whose running
-// sum first exceeds uc * totalWeight (std::upper_bound over the float sums,
-// compared in double), then the point (u0, u1) of that cell mapped to the
+// sum first exceeds fl(uc * totalWeight) (std::upper_bound over the float
+// sums), then the point (u0, u1) of that cell mapped to the
 // sphere.  uc is the reference's hidden random_float() (Light.cpp:120),
 // drawn from the sample stream by the caller.
 struct DirUV {
@@ -793,11 +793,13 @@ struct DirUV {
 __device__ __noinline__ DirUV texinf_sample(const pt_light& l, float uc, float u0, float u1) {
     const float* acc = S.light_dist + l.prim;
     constexpr uint32_t N = (uint32_t)PT_TEXINF_X * PT_TEXINF_Y;
-    const double weight = (double)uc * (double)acc[N - 1];
+    // float weight = random_float() * totalWeight: the double product rounded
+    // to float, then std::upper_bound compares float with float
+    const float weight = (float)((double)uc * (double)acc[N - 1]);
     uint32_t lo = 0, hi = N;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
-        if ((double)acc[mid] > weight) hi = mid;
+        if (acc[mid] > weight) hi = mid;
         else lo = mid + 1;
     }
     const int cx = (int)(lo % PT_TEXINF_Y), cy = (int)(lo / PT_TEXINF_Y);

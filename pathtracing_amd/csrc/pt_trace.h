@@ -410,6 +410,8 @@ __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out
             if (LN >= PT_STACK || sp < LN) s_ref[sp * PT_TRACE_BLOCK + lane] = v;
             else ovf[(size_t)(sp - LN) * G + gl] = v;
             ++sp;
+        } else {
+            atomicAdd(S.stack_drops, 1u);  // counted: pt_stats::stack_overflows
         }
     };
     for (;;) {
@@ -503,6 +505,8 @@ __device__ bool trace_any(f3 o, f3 d, float tmax, uint32_t* s_ref, TraceWork& wk
             if (LN >= PT_STACK || sp < LN) s_ref[sp * PT_TRACE_BLOCK + lane] = v;
             else ovf[(size_t)(sp - LN) * G + gl] = v;
             ++sp;
+        } else {
+            atomicAdd(S.stack_drops, 1u);  // counted: pt_stats::stack_overflows
         }
     };
     for (;;) {

@@ -4,9 +4,13 @@ SURVEY.md §8(e): every rank holds a full scene replica and renders the samples
 s ≡ rank (mod world) of every pixel with the same per-sample stream keys, so
 the ranks' films sum to the single-GPU film up to summation order.  The one
 exchange is a SUM reduce of the W×H×4 f64 accumulator {ΣRGB·w, Σw}
-(Film.hpp:227-268) onto the destination rank — RCCL over xGMI with the "nccl"
-backend on ROCm, or gloo for the CPU tests.  It replaces the reference's
-`atomic<double>` film merge (Film.hpp:125-132, 244-249).
+(Film.hpp:227-268) onto the destination rank over xGMI: the library's own
+RCCL communicator (`init_film_comm` -> pt_comm_init_rank, pt_film_reduce)
+when it has one, else torch.distributed's reduce (RCCL with the "nccl"
+backend, gloo for the CPU tests).  It replaces the reference's
+`atomic<double>` film merge (Film.hpp:125-132, 244-249).  (One process
+driving several GPUs uses a multi-device context instead: pt_create(ctx, n,
+ids) reduces inside pt_render.)
 """
 from __future__ import annotations
 
@@ -32,6 +36,36 @@ def local_samples(spp: int, rank: int, world_size: int) -> int:
     return (spp - rank + world_size - 1) // world_size if spp > rank else 0
 
 
+def init_film_comm(integrator, device: int, group=None) -> bool:
+    """Give this rank's library context an RCCL communicator over the group's
+    ranks (rank 0 draws the id, the group broadcasts it).  Returns False, with
+    the reason logged, if RCCL refuses; render_frame then reduces through
+    torch.distributed instead."""
+    from .integrator import Context
+    rank, n = world() if group is None else (dist.get_rank(group), dist.get_world_size(group))
+    ctx = integrator.context(device)
+    if ctx.comm_ranks == n:
+        return True
+    obj = [Context.comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    ok = True
+    try:
+        ctx.comm_init_rank(n, rank, obj[0])
+    except RuntimeError as e:  # N.NativeError
+        import sys
+        print(f"[distributed] rank {rank}: library RCCL communicator unavailable ({e}); "
+              "reducing through torch.distributed", file=sys.stderr, flush=True)
+        ok = False
+    # every rank must agree on the reduce path
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
+                        device=f"cuda:{device}" if dist.get_backend(group) == "nccl" else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    if not int(flag.item()):
+        ctx.comm_ranks = 0  # (a communicator some ranks built stays unused)
+        return False
+    return True
+
+
 def render_frame(integrator, film: torch.Tensor, *, flags: int = 0, paths_in_flight: int = 0, dst: int = 0,
                  group=None, render_shard: Optional[Callable[[int, int, torch.Tensor], dict]] = None) -> dict:
     """Render this rank's sample shard of one frame into `film` and reduce it
@@ -55,16 +89,29 @@ def render_frame(integrator, film: torch.Tensor, *, flags: int = 0, paths_in_fli
         dev = film.device.index or 0
         # the library's launches go on torch's current stream of the film's
         # device, so they are ordered after zero_() and after any earlier
-        # collective that wrote into the same tensor
-        integrator.context(dev).set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        # collective that wrote into the same tensor.  On torch's null stream
+        # (handle 0) the library keeps its own non-blocking stream, which does
+        # not wait for the null stream: synchronise it first.
+        torch_stream = torch.cuda.current_stream(dev)
+        ctx = integrator.context(dev)
+        ctx.set_stream(torch_stream.cuda_stream)
         film.zero_()
-        st = integrator.Render(device=dev, shard_index=rank, shard_count=n,
-                               film_ptr=film.data_ptr(), flags=flags, paths_in_flight=paths_in_flight)
+        if torch_stream.cuda_stream == 0:
+            torch_stream.synchronize()
+        try:
+            st = integrator.Render(device=dev, shard_index=rank, shard_count=n,
+                                   film_ptr=film.data_ptr(), flags=flags, paths_in_flight=paths_in_flight)
+        finally:
+            ctx.set_stream(None)  # the cached context goes back to its own stream
     else:
         film.zero_()
         st = render_shard(rank, n, film)
     if n > 1:
-        if film.is_cuda and dist.get_backend(group) == "gloo":
+        ctx = integrator.context(film.device.index or 0) if render_shard is None else None
+        if ctx is not None and ctx.comm_ranks == n:
+            # the library's RCCL communicator: in-place ncclReduce on its stream
+            ctx.film_reduce(film.data_ptr(), film.numel(), dst)
+        elif film.is_cuda and dist.get_backend(group) == "gloo":
             # gloo has no device reduce: sum host copies (CPU rehearsals of the
             # multi-rank path with the real device renderer)
             host = film.cpu()

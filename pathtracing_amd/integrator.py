@@ -45,14 +45,37 @@ class StratifiedSampler(Sampler):
 
 
 class Context:
-    """One libpt context (one GPU).  Fails loudly if HIP or the library is missing."""
+    """One libpt context: one GPU, or several (`devices`) with the library's
+    own RCCL film reduce (pt_create(ctx, n_devices, device_ids)).  Fails
+    loudly if HIP or the library is missing."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, devices: Optional[list[int]] = None):
         self._lib = N.lib()
         self.ptr = C.c_void_p()
-        N.check(self._lib.pt_create(C.byref(self.ptr), int(device)))
-        self.device = device
+        ids = [int(device)] if devices is None else [int(d) for d in devices]
+        arr = (C.c_int * len(ids))(*ids)
+        N.check(self._lib.pt_create(C.byref(self.ptr), len(ids), arr))
+        self.device = ids[0]
+        self.devices = ids
         self.scene_key = None
+        self.comm_ranks = 0
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """pt_comm_unique_id: the RCCL id rank 0 broadcasts (PT_COMM_ID_BYTES)."""
+        buf = (C.c_uint8 * N.PT_COMM_ID_BYTES)()
+        N.check(N.lib().pt_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init_rank(self, n_ranks: int, rank: int, uid: bytes):
+        """pt_comm_init_rank: join the film-reduce communicator (one process per GPU)."""
+        buf = (C.c_uint8 * N.PT_COMM_ID_BYTES).from_buffer_copy(uid)
+        N.check(self._lib.pt_comm_init_rank(self.ptr, int(n_ranks), int(rank), buf), self.ptr)
+        self.comm_ranks = int(n_ranks)
+
+    def film_reduce(self, film_ptr: int, n_doubles: int, root: int = 0):
+        """pt_film_reduce: in-place ncclReduce(SUM) of a device film onto `root`."""
+        N.check(self._lib.pt_film_reduce(self.ptr, C.c_void_p(film_ptr), int(n_doubles), int(root)), self.ptr)
 
     def close(self):
         if self.ptr:

@@ -118,10 +118,11 @@ class Stats(C.Structure):
                 ("nodes_closest", C.c_uint64), ("tris_closest", C.c_uint64), ("nodes_any", C.c_uint64),
                 ("tris_any", C.c_uint64), ("shade_hits", C.c_uint64), ("ms_total", C.c_double),
                 ("ms_closest", C.c_double), ("ms_any", C.c_double), ("ms_shade", C.c_double),
-                ("launches_closest", C.c_uint64), ("launches_any", C.c_uint64)]
+                ("launches_closest", C.c_uint64), ("launches_any", C.c_uint64),
+                ("stack_overflows", C.c_uint64), ("n_devices", C.c_uint32), ("pad", C.c_uint32)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
 
 
 class BvhBuildStats(C.Structure):
@@ -136,8 +137,9 @@ EXPORTS = [
     "pt_version", "pt_create", "pt_destroy", "pt_last_error", "pt_set_stream", "pt_scene_upload", "pt_render",
     "pt_trace", "pt_scene_device_bytes", "pt_bvh4_build", "pt_bvh4_order_table", "pt_film_resolve",
     "pt_mat4_inverse", "pt_bvh4_build_device", "pt_set_node_format", "pt_render_adaptive", "pt_render_samples",
-    "pt_texinf_weights",
+    "pt_texinf_weights", "pt_device_count", "pt_comm_unique_id", "pt_comm_init_rank", "pt_film_reduce",
 ]
+PT_COMM_ID_BYTES = 128
 
 _lib = None
 
@@ -164,8 +166,16 @@ def lib():
     L = C.CDLL(str(LIB_PATH))
     vp = C.c_void_p
     L.pt_version.restype = C.c_int
-    L.pt_create.argtypes = [C.POINTER(vp), C.c_int]
+    L.pt_create.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(C.c_int)]
     L.pt_create.restype = C.c_int32
+    L.pt_device_count.argtypes = [vp]
+    L.pt_device_count.restype = C.c_int
+    L.pt_comm_unique_id.argtypes = [vp]
+    L.pt_comm_unique_id.restype = C.c_int32
+    L.pt_comm_init_rank.argtypes = [vp, C.c_int, C.c_int, vp]
+    L.pt_comm_init_rank.restype = C.c_int32
+    L.pt_film_reduce.argtypes = [vp, vp, C.c_uint64, C.c_int]
+    L.pt_film_reduce.restype = C.c_int32
     L.pt_destroy.argtypes = [vp]
     L.pt_destroy.restype = None
     L.pt_last_error.argtypes = [vp]
@@ -272,7 +282,8 @@ def bvh4_build_device(boxes: np.ndarray, device: int = 0, stats: dict | None = N
     st = BvhBuildStats()
     L = lib()
     ctx = C.c_void_p()
-    check(L.pt_create(C.byref(ctx), device))
+    dev = (C.c_int * 1)(int(device))
+    check(L.pt_create(C.byref(ctx), 1, dev))
     try:
         check(L.pt_bvh4_build_device(ctx, ptr(boxes), n, clusters.ctypes.data, C.byref(nc), C.byref(root),
                                      order.ctypes.data, bbox.ctypes.data, C.byref(st)), ctx)

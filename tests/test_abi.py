@@ -29,12 +29,21 @@ def test_library_exports_every_declared_symbol():
 
 def test_version_and_error_paths_without_device():
     lib = N.lib()
-    assert lib.pt_version() == 3
+    assert lib.pt_version() == 4
     # argument validation never aborts
     assert lib.pt_scene_upload(None, None) == -1
     assert lib.pt_render(None, None, None, None, None) == -1
     assert lib.pt_trace(None, None, 0, 0, None, None) == -1
-    assert lib.pt_create(None, 0) == -1
+    assert lib.pt_create(None, 1, None) == -1
+    ctx = C.c_void_p()
+    assert lib.pt_create(C.byref(ctx), 0, None) == -1  # n_devices out of range
+    dup = (C.c_int * 2)(0, 0)
+    assert lib.pt_create(C.byref(ctx), 2, dup) == -1  # a device listed twice
+    assert not ctx.value
+    assert lib.pt_device_count(None) == 0
+    assert lib.pt_film_reduce(None, None, 0, 0) == -1
+    assert lib.pt_comm_init_rank(None, 1, 0, None) == -1
+    assert lib.pt_comm_unique_id(None) == -1
     lib.pt_destroy(None)
     assert isinstance(lib.pt_last_error(None), (bytes, type(None)))
 

@@ -74,3 +74,62 @@ def test_two_gpu_ranks_sum_to_the_one_process_frame():
     torch.cuda.synchronize()
     np.testing.assert_allclose(film, one.cpu().numpy(), rtol=1e-9, atol=1e-12)
     assert tot["paths"] == st["paths"] == W * H * setup.spp
+
+
+# ---------------------------------------------------------------- the library's own RCCL film reduce
+def test_library_rccl_film_reduce_one_rank():
+    """pt_comm_unique_id + pt_comm_init_rank + pt_film_reduce on a one-rank
+    communicator: the in-place ncclReduce(SUM) runs on the library's stream
+    and leaves the film unchanged (the sum over one rank)."""
+    from pathtracing_amd.integrator import Context
+    ctx = Context(0)
+    try:
+        ctx.comm_init_rank(1, 0, Context.comm_unique_id())
+        rng = np.random.default_rng(1)
+        host = rng.uniform(-1, 1, (48, 64, 4))
+        film = torch.from_numpy(host).to("cuda:0")
+        torch.cuda.synchronize()
+        ctx.film_reduce(film.data_ptr(), film.numel(), 0)
+        np.testing.assert_array_equal(film.cpu().numpy(), host)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_multi_device_context_path_on_one_gpu(monkeypatch, adaptive):
+    """pt_render through render_multi (the n-GPU path of pt_create(ctx, n,
+    ids): per-device host threads, device films, the grouped ncclReduce of the
+    films and adaptive counts onto the first device, the copy into a host
+    film) forced on a one-device context: bit-identical to the one-device
+    render, host and device films, fixed SPP and adaptive."""
+    from pathtracing_amd.integrator import Context
+    setup = _setup()
+    integ = setup.make_integrator()
+    W, H = setup.camera.GetFilm().Resolution()
+    cam, rd = integ.desc()
+    ref = np.zeros((H, W, 4))
+    base = integ.context(0)
+    if adaptive:
+        st0, c0 = base.render_adaptive(cam, rd, ref.ctypes.data)
+    else:
+        st0 = base.render(cam, rd, ref.ctypes.data)
+    monkeypatch.setenv("PT_MULTI_DEVICE_PATH", "1")
+    ctx = Context(devices=[0])
+    try:
+        ctx.upload(integ.flat)
+        got = np.zeros((H, W, 4))
+        dev = torch.zeros((H, W, 4), dtype=torch.float64, device="cuda:0")
+        torch.cuda.synchronize()
+        if adaptive:
+            st1, c1 = ctx.render_adaptive(cam, rd, got.ctypes.data)
+            st2, c2 = ctx.render_adaptive(cam, rd, dev.data_ptr())
+            np.testing.assert_array_equal(c1, c0)
+            np.testing.assert_array_equal(c2, c0)
+        else:
+            st1 = ctx.render(cam, rd, got.ctypes.data)
+            st2 = ctx.render(cam, rd, dev.data_ptr())
+        np.testing.assert_array_equal(got, ref)
+        np.testing.assert_array_equal(dev.cpu().numpy(), ref)
+        assert st1["n_devices"] == 1 and st1["paths"] == st0["paths"] and st1["stack_overflows"] == 0
+    finally:
+        ctx.close()

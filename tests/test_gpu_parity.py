@@ -253,6 +253,9 @@ def test_gpu_sanmiguel_full_size_shards_sum(c4_full):
     st = integ.Render(flags=N.PT_RENDER_COUNT_NODES)
     full = film.accum.copy()
     assert st["paths"] == 192 * 108 * 2 and st["rays_any"] > 0
+    # no traversal stack push was dropped (pt_stats::stack_overflows: the
+    # pool kernels' 48-entry stack, LDS + HBM)
+    assert st["stack_overflows"] == 0
     parts = []
     for r in range(2):
         film.Clear()

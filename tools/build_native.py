@@ -62,7 +62,7 @@ def build_product(force: bool = False, variant: str = "", defines=()) -> Path:
           "-Wno-unused-result", "-Wno-unused-value", *[f"-D{d}" for d in defines],
           "-c", CSRC / "pt_runtime.hip", "-o", rt_o, *inc])
     tmp = out.with_suffix(".so.tmp")
-    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", rt_o, bvh_o, env_o, "-o", tmp, "-lpthread"])
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", rt_o, bvh_o, env_o, "-o", tmp, "-lrccl", "-lpthread"])
     os.replace(tmp, out)
     return out
 
