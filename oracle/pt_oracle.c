@@ -799,7 +799,11 @@ static float fresnel_dielectric(float cosi, float eta) {
     return (rpa * rpa + rpe * rpe) / 2;
 }
 static inline v3 schlick(float c, v3 F0) {
+#ifdef ORACLE_POW_CR
+    float p = (float)pow((double)(1.0f - c), 5.0);
+#else
     float p = powf(1.0f - c, 5.0f);
+#endif
     return add(F0, muls(sub(V(1, 1, 1), F0), p));
 }
 

@@ -20,6 +20,8 @@ ROOT = Path(__file__).resolve().parents[1]
 CSRC = ROOT / "pathtracing_amd" / "csrc"
 LIBDIR = ROOT / "pathtracing_amd" / "_lib"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# device float semantics: hipcc's default contraction (fast) for now; see DESIGN.md §4
+FP_FLAGS: list[str] = []
 ARCH = os.environ.get("PT_OFFLOAD_ARCH", "gfx950")
 
 
@@ -58,8 +60,10 @@ def build_product(force: bool = False, variant: str = "", defines=()) -> Path:
     _run(["g++", "-std=gnu++20", "-O3", "-march=x86-64-v3", "-ffp-contract=off", "-fPIC", "-c",
           CSRC / "pt_envmap.cpp", "-o", env_o, *inc])
     rt_o = build / "pt_runtime.o"
+    extra = [d for d in defines if d.startswith("-")]  # raw compiler flags of a tuning variant
+    defs = [f"-D{d}" for d in defines if not d.startswith("-")]
     _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++20", "-munsafe-fp-atomics",
-          "-Wno-unused-result", "-Wno-unused-value", *[f"-D{d}" for d in defines],
+          "-Wno-unused-result", "-Wno-unused-value", *FP_FLAGS, *extra, *defs,
           "-c", CSRC / "pt_runtime.hip", "-o", rt_o, *inc])
     tmp = out.with_suffix(".so.tmp")
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", rt_o, bvh_o, env_o, "-o", tmp, "-lrccl", "-lpthread"])
