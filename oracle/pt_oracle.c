@@ -43,6 +43,10 @@ static inline float rmul(float a, float b) {
 /* contracted as the reference's GCC build emits it: x product rounded, then
  * fma(y) and fma(z) (SphereShape::Intersect disassembly) */
 static inline float dot(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+/* other orders the build emits for glm::dot (tools/refgimple.py): y product
+ * rounded then fma(x), fma(z); and the unfused sum (x + y) + z */
+static inline float dot_yxz(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.x, b.x, a.y * b.y)); }
+static inline float dot_p(v3 a, v3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 /* glm::cross as the reference build contracts it (x, y lanes vectorised:
  * first product rounded, second fused; z scalar: first fused) */
 /* glm::cross in scalar code: first product fused, second rounded
@@ -73,6 +77,9 @@ static inline float lerp3f(float u, float a, float v, float b, float w, float c)
     return fmaf(w, c, fmaf(v, b, rmul(u, a)));
 }
 static inline float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+/* a*b + c per lane, fused (glm's `c += a * b` as the reference build contracts it) */
+static inline v3 fma3(v3 a, v3 b, v3 c) { return V(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y), fmaf(a.z, b.z, c.z)); }
+static inline v3 fma3s(float s, v3 b, v3 c) { return V(fmaf(s, b.x, c.x), fmaf(s, b.y, c.y), fmaf(s, b.z, c.z)); }
 static inline float fmaxf_(float a, float b) { return a < b ? b : a; } /* std::max */
 
 /* ------------------------------------------------------------------ RNG */
@@ -307,6 +314,21 @@ static inline v3 to_world_nm(const onb_t* b, v3 v) {
              fmaf(v.z, b->a2.z, fmaf(v.y, b->a1.z, v.x * b->a0.z)));
 }
 static inline v3 to_local(const onb_t* b, v3 v) { return V(dot(v, b->a0), dot(v, b->a1), dot(v, b->a2)); }
+/* the out-of-line onb::toLocal (the dielectric's calls): x, y lanes in y, x, z order */
+static inline v3 to_local_ool(const onb_t* b, v3 v) { return V(dot_yxz(v, b->a0), dot_yxz(v, b->a1), dot(v, b->a2)); }
+/* ray.at(t) fused in every lane */
+static inline v3 at_f(const ray_t* r, float t) {
+    return V(fmaf(t, r->d.x, r->o.x), fmaf(t, r->d.y, r->o.y), fmaf(t, r->d.z, r->o.z));
+}
+/* glm::refract with the build's contractions, given d = dot(N, I) */
+static inline v3 refract_f(v3 I, v3 N, float eta, float d) {
+    float k = fmaf(-(eta * eta), fmaf(-d, d, 1.0f), 1.0f);
+    if (k >= 0.0f) {
+        float c = fmaf(eta, d, sqrtf(k));
+        return V(fmaf(-c, N.x, eta * I.x), fmaf(-c, N.y, eta * I.y), fmaf(-c, N.z, eta * I.z));
+    }
+    return V(0, 0, 0);
+}
 
 /* sample_normalMap (Material.hpp:344-348, 580-584) */
 static v3 normal_map(const scene_t* S, int mid, const si_t* si) {
@@ -320,9 +342,10 @@ static v3 normal_map(const scene_t* S, int mid, const si_t* si) {
 }
 
 /* ------------------------------------------------------------------ shapes (Shape.cpp) */
-static void sphere_uv(v3 p, float uv[2]) {
-    /* SphereShape::GetSphereUV (Shape.hpp:35-43) */
-    p = normalize(p);
+static void sphere_uv_n(v3 p, float uv[2]);
+static void sphere_uv(v3 p, float uv[2]) { sphere_uv_n(normalize(p), uv); }
+static void sphere_uv_n(v3 p, float uv[2]) {
+    /* SphereShape::GetSphereUV (Shape.hpp:35-43) after its normalisation */
     float theta = acosf(clampf(p.y, -1.0f, 1.0f));
     float phi = atan2f(p.z, p.x);
     if (phi < 0) phi += 2.0f * PI_F;
@@ -431,23 +454,27 @@ static int tri_pred(const scene_t* S, uint32_t tri, const ray_t* r, float max) {
 }
 
 /* QuadShape::Intersect / IntersectPred (Shape.cpp:320-359) */
-static int quad_hit(const pt_quad* q, const ray_t* r, float max, float* t_out, float* a_out, float* b_out,
-                    v3* nn_out) {
+/* as built: Intersect tests and divides by dot(d, nn) fused, IntersectPred
+ * by the unfused dot; alpha = dot(w, cross(ph, v)), beta = dot(w, cross(u, ph))
+ * with the second cross rounded-first and its dot in y, x, z order */
+static int quad_hit_(const pt_quad* q, const ray_t* r, float max, float* t_out, float* a_out, float* b_out,
+                     v3* nn_out, int pred) {
     v3 normal = vl(q->normal);
     v3 nn = normal;
     float DD = q->D;
-    if (dot(r->d, normal) > 0) {
+    float dn = pred ? dot_p(normal, r->d) : dot(r->d, normal);
+    if (dn > 0) {
         nn = neg(normal);
         DD = -q->D;
     }
-    float denom = dot(nn, r->d);
+    float denom = pred ? (dn > 0 ? -dn : dn) : dot(r->d, nn);
     if (fabsf(denom) < 1e-8f) return 0;
     float t = (DD - dot(nn, r->o)) / denom;
     if (t < EPS_SHADOW || t > max) return 0;
-    v3 ph = sub(at(r, t), vl(q->Q));
+    v3 ph = sub(at_f(r, t), vl(q->Q));
     v3 w = vl(q->w);
     float alpha = dot(w, cross(ph, vl(q->v)));
-    float beta = dot(w, cross(vl(q->u), ph));
+    float beta = dot_yxz(cross_r(vl(q->u), ph), w);
     if (!(alpha >= 0 && alpha <= 1 && beta >= 0 && beta <= 1)) return 0;
     *t_out = t;
     *a_out = alpha;
@@ -455,10 +482,14 @@ static int quad_hit(const pt_quad* q, const ray_t* r, float max, float* t_out, f
     *nn_out = nn;
     return 1;
 }
+static int quad_hit(const pt_quad* q, const ray_t* r, float max, float* t_out, float* a_out, float* b_out,
+                    v3* nn_out) {
+    return quad_hit_(q, r, max, t_out, a_out, b_out, nn_out, 1);
+}
 static int quad_intersect(const pt_quad* q, const ray_t* r, float max, si_t* si) {
     float t, a, b;
     v3 nn;
-    if (!quad_hit(q, r, max, &t, &a, &b, &nn)) return 0;
+    if (!quad_hit_(q, r, max, &t, &a, &b, &nn, 0)) return 0;
     si->uv[0] = a;
     si->uv[1] = b;
     si->t = t;
@@ -466,7 +497,8 @@ static int quad_intersect(const pt_quad* q, const ray_t* r, float max, si_t* si)
     si->n = vl(q->normal);
     v3 up = (fabsf(si->ns.x) > 0.9999f) ? V(0, 1, 0) : V(1, 0, 0);
     si->tangent = normalize(cross(up, si->ns));
-    si->p = add(at(r, t), smul(EPS_SHADOW, nn));
+    v3 pa = at_f(r, t);
+    si->p = V(pa.x + EPS_SHADOW * nn.x, pa.y + EPS_SHADOW * nn.y, fmaf(nn.z, EPS_SHADOW, pa.z));
     return 1;
 }
 
@@ -492,11 +524,12 @@ static int sphere_intersect(const pt_sphere* sp, const ray_t* r, float max, si_t
     float t;
     if (!sphere_root(sp, r, max, &t)) return 0;
     si->t = t;
-    si->ns = normalize(sub(at(r, t), vl(sp->center)));
+    v3 pa = at_f(r, t);
+    si->ns = normalize(sub(pa, vl(sp->center)));
     si->n = si->ns;
     v3 up = (fabsf(si->ns.x) > 0.9999f) ? V(0, 1, 0) : V(1, 0, 0);
     si->tangent = normalize(cross(up, si->ns));
-    si->p = add(at(r, t), smul(EPS_SHADOW, si->n));
+    si->p = V(fmaf(si->n.x, EPS_SHADOW, pa.x), fmaf(si->n.y, EPS_SHADOW, pa.y), fmaf(si->n.z, EPS_SHADOW, pa.z));
     sphere_uv(si->n, si->uv);
     return 1;
 }
@@ -743,7 +776,9 @@ static float lambda_(const dist_t* D, v3 w) {
     float sinT = sqrtf(sin2);
     float cosPhi = sinT == 0 ? 1 : clampf(w.x / sinT, -1.0f, 1.0f);
     float sinPhi = sinT == 0 ? 0 : clampf(w.y / sinT, -1.0f, 1.0f);
-    float alpha2 = (cosPhi * D->ax) * (cosPhi * D->ax) + (sinPhi * D->ay) * (sinPhi * D->ay);
+    /* Material.hpp:66 as built: fma(cosPhi*ax, cosPhi*ax, (sinPhi*ay)^2) */
+    float ca = cosPhi * D->ax, sa = sinPhi * D->ay;
+    float alpha2 = fmaf(ca, ca, sa * sa);
     return (sqrtf(1.f + alpha2 * sin2 / cos2) - 1.0f) / 2.0f;
 }
 static float D_(const dist_t* D, v3 wh) {
@@ -754,32 +789,47 @@ static float D_(const dist_t* D, v3 wh) {
     float sinT = sqrtf(sin2);
     float cosPhi = sinT == 0 ? 1 : clampf(wh.x / sinT, -1.0f, 1.0f);
     float sinPhi = sinT == 0 ? 0 : clampf(wh.y / sinT, -1.0f, 1.0f);
-    float e = sin2 / cos2 * ((cosPhi / D->ax) * (cosPhi / D->ax) + (sinPhi / D->ay) * (sinPhi / D->ay));
-    float denom = PI_F * D->ax * D->ay * cos4 * (1 + e) * (1 + e);
+    /* Material.hpp:78-79 as built: the sum of squares fused, and 1 + e fused
+     * into one fma(sin2/cos2, sum, 1) (e itself is never rounded) */
+    float cx = cosPhi / D->ax, sy = sinPhi / D->ay;
+    float e1 = fmaf(sin2 / cos2, fmaf(cx, cx, sy * sy), 1.0f);
+    float denom = PI_F * D->ax * D->ay * cos4 * e1 * e1;
     if (denom <= 0) return INFINITY;
     return 1 / denom;
 }
 static inline float G1_(const dist_t* D, v3 w) { return 1 / (1 + lambda_(D, w)); }
 static inline float G_(const dist_t* D, v3 wo, v3 wi) { return 1 / (1 + lambda_(D, wo) + lambda_(D, wi)); }
 static inline int smooth_(const dist_t* D) { return fmaxf_(D->ax, D->ay) < 1e-6; }
-static inline float mpdf_(const dist_t* D, v3 wo, v3 wh) { return D_(D, wh) * G1_(D, wo) * fabsf(dot(wo, wh) / wo.z); }
-static v3 vndf_(float ax, float ay, v3 Ve, float U1, float U2) {
+/* MicrofacetDistribution::PDF with the caller's dot(wo, wh) (its order differs by call site) */
+static inline float mpdf_(const dist_t* D, v3 wo, v3 wh, float dwh) { return D_(D, wh) * G1_(D, wo) * fabsf(dwh / wo.z); }
+/* sampleGGXVNDF (Material.hpp:119-139) with the contractions of the
+ * reference build (MicrofacetDiffuse::scatter's inlined copy) */
+static v3 vndf_(float ax, float ay, v3 Ve, float U1, float U2, int ne_inline) {
     v3 Vh = normalize(V(ax * Ve.x, ay * Ve.y, Ve.z));
-    float lensq = Vh.x * Vh.x + Vh.y * Vh.y;
+    float lensq = fmaf(Vh.x, Vh.x, Vh.y * Vh.y);
     v3 T1 = lensq > 0 ? muls(V(-Vh.y, Vh.x, 0), 1.0f / sqrtf(lensq)) : V(1, 0, 0);
-    v3 T2 = cross(Vh, T1);
+    v3 T2 = cross_v(Vh, T1);
     float r = sqrtf(U1);
     float phi = 2.0f * PI_F * U2;
     float t1 = r * cosf(phi);
     float t2 = r * sinf(phi);
     float s = 0.5f * (1.0f + Vh.z);
-    t2 = (1.0f - s) * sqrtf(1.0f - t1 * t1) + s * t2;
-    v3 Nh = add(add(smul(t1, T1), smul(t2, T2)), smul(sqrtf(fmaxf_(0.0f, 1.0f - t1 * t1 - t2 * t2)), Vh));
-    return normalize(V(ax * Nh.x, ay * Nh.y, fmaxf_(0.0f, Nh.z)));
+    float q1 = fmaf(-t1, t1, 1.0f); /* 1 - t1*t1 */
+    t2 = fmaf(1.0f - s, sqrtf(q1), s * t2);
+    float q = fmaf(-t2, t2, q1);
+    float sq = sqrtf(fmaxf_(0.0f, q));
+    /* x, y lanes: t2*T2 rounded, t1*T1 fused; z lane: t1*T1 rounded, t2*T2 fused */
+    v3 Nh = V(fmaf(sq, Vh.x, fmaf(t1, T1.x, t2 * T2.x)), fmaf(sq, Vh.y, fmaf(t1, T1.y, t2 * T2.y)),
+              fmaf(sq, Vh.z, fmaf(t2, T2.z, t1 * T1.z)));
+    v3 ne = V(ax * Nh.x, ay * Nh.y, fmaxf_(0.0f, Nh.z));
+    if (!ne_inline) return normalize(ne);
+    /* MicrofacetDielectric::scatter's inlined copy: z^2 added unfused */
+    float zz = Nh.z > 0 ? ne.z * ne.z : 0.0f;
+    return muls(ne, 1.0f / sqrtf(fmaf(ne.y, ne.y, ne.x * ne.x) + zz));
 }
-static v3 sample_wh(const dist_t* D, v3 wo, float u0, float u1) {
+static v3 sample_wh(const dist_t* D, v3 wo, float u0, float u1, int ne_inline) {
     int flip = wo.z < 0;
-    v3 wh = vndf_(D->ax, D->ay, flip ? neg(wo) : wo, u0, u1);
+    v3 wh = vndf_(D->ax, D->ay, flip ? neg(wo) : wo, u0, u1, ne_inline);
     if (flip) wh = neg(wh);
     return wh;
 }
@@ -790,13 +840,14 @@ static float fresnel_dielectric(float cosi, float eta) {
         eta = 1 / eta;
         cosi = -cosi;
     }
-    float sin2i = 1 - cosi * cosi;
+    /* as built: 1 - cos^2, eta*cos -+ cost, cos -+ eta*cost and the sum of squares fused */
+    float sin2i = fmaf(-cosi, cosi, 1.0f);
     float sin2t = sin2i / (eta * eta);
     if (sin2t >= 1) return 1.f;
     float cost = sqrtf(1 - sin2t);
-    float rpa = (eta * cosi - cost) / (eta * cosi + cost);
-    float rpe = (cosi - eta * cost) / (cosi + eta * cost);
-    return (rpa * rpa + rpe * rpe) / 2;
+    float rpa = fmaf(cosi, eta, -cost) / fmaf(cosi, eta, cost);
+    float rpe = fmaf(-eta, cost, cosi) / fmaf(eta, cost, cosi);
+    return fmaf(rpa, rpa, rpe * rpe) * 0.5f;
 }
 static inline v3 schlick(float c, v3 F0) {
 #ifdef ORACLE_POW_CR
@@ -804,7 +855,8 @@ static inline v3 schlick(float c, v3 F0) {
 #else
     float p = powf(1.0f - c, 5.0f);
 #endif
-    return add(F0, muls(sub(V(1, 1, 1), F0), p));
+    /* F0 + (1 - F0) * p, fused */
+    return V(fmaf(p, 1.0f - F0.x, F0.x), fmaf(p, 1.0f - F0.y, F0.y), fmaf(p, 1.0f - F0.z, F0.z));
 }
 
 /* ------------------------------------------------------------------ materials */
@@ -812,6 +864,15 @@ typedef struct { v3 f; float pdf; uint32_t flags; v3 o, d; int ok; } bxdf_t;
 #define FL_TRANS 1u
 #define FL_SPEC 2u
 
+/* onb TBN(dot(d, ns) > 0 ? -ns : ns) and wo = TBN.toLocal(-d) as MicrofacetDiffuse's
+ * three entry points are built: the sign test is the unfused dot, and wo.z reuses it
+ * (+-dot(d, ns)) instead of dot(-d, n) */
+static inline v3 diffuse_frame(v3 d, v3 ns, onb_t* tbn) {
+    float pd = dot_p(d, ns);
+    *tbn = onb_n(pd > 0 ? neg(ns) : ns);
+    v3 md = neg(d);
+    return V(dot(md, tbn->a0), dot(md, tbn->a1), pd > 0 ? pd : -pd);
+}
 static float diffuse_rough(const scene_t* S, const pt_material* m, const si_t* si) {
     return fmaxf_(tex_eval(S, m->rough, si->uv).y, 0.0001f);
 }
@@ -822,13 +883,13 @@ static bxdf_t diffuse_scatter(const scene_t* S, const pt_material* m, const ray_
     bxdf_t b;
     memset(&b, 0, sizeof(b));
     float rough = diffuse_rough(S, m, si);
-    onb_t tbn = onb_n(dot(in->d, si->ns) > 0 ? neg(si->ns) : si->ns);
-    dist_t D = mkdist(rough);
     float prob = rough >= 0.7 ? 1.0f : 0.5f;
-    v3 wo = to_local(&tbn, neg(in->d));
+    dist_t D = mkdist(rough);
+    onb_t tbn;
+    v3 wo = diffuse_frame(in->d, si->ns, &tbn);
     v3 wi, wh;
     if (u >= prob) {
-        wh = sample_wh(&D, wo, uv0, uv1);
+        wh = sample_wh(&D, wo, uv0, uv1, 0);
         wi = reflect(neg(wo), wh);
     } else {
         float z = sqrtf(1.0f - uv1);
@@ -840,20 +901,22 @@ static bxdf_t diffuse_scatter(const scene_t* S, const pt_material* m, const ray_
         wh = normalize(add(wo, wi));
     }
     if (wi.z <= 0) return b;
-    float dpdf = prob * wi.z * INV_PI_F;
-    float spdf = (1.0f - prob) * mpdf_(&D, wo, wh) / (4 * fabsf(dot(wo, wh)));
-    float pdf = dpdf + spdf;
+    /* as built: dot(wo, wh) in y, x, z order; prob*wi.z*inv_pi + spdf fused */
+    float spdf = (1.0f - prob) * mpdf_(&D, wo, wh, dot_yxz(wo, wh)) / (4 * fabsf(dot_yxz(wo, wh)));
+    float pdf = fmaf(prob * wi.z, INV_PI_F, spdf);
     v3 col = tex_eval(S, m->tex, si->uv);
     float metal = tex_eval(S, m->metal, si->uv).z;
-    v3 F0 = add(muls(V(0.04f, 0.04f, 0.04f), 1.0f - metal), muls(col, metal)); /* glm::mix */
-    v3 F = schlick(dot(wi, wh), F0);
+    /* glm::mix(0.04, col, metal) as built here: col*metal rounded, the other fused */
+    float om = 1.0f - metal;
+    v3 F0 = V(fmaf(om, 0.04f, col.x * metal), fmaf(om, 0.04f, col.y * metal), fmaf(om, 0.04f, col.z * metal));
+    v3 F = schlick(dot_yxz(wi, wh), F0);
     v3 num = muls(F, D_(&D, wh) * G_(&D, wo, wi));
     float den = fabsf(4.0f * wo.z * wi.z);
     if (den == 0) return b;
     v3 spec = divs(num, den);
-    v3 kD = muls(sub(V(1, 1, 1), F), 1.0f - metal);
-    v3 diff = muls(mul(kD, col), INV_PI_F);
-    b.f = add(diff, spec);
+    v3 kD = muls(sub(V(1, 1, 1), F), om);
+    v3 kc = mul(kD, col);
+    b.f = V(fmaf(kc.x, INV_PI_F, spec.x), fmaf(kc.y, INV_PI_F, spec.y), fmaf(kc.z, INV_PI_F, spec.z));
     b.pdf = pdf;
     b.flags = 0;
     b.o = si->p;
@@ -863,38 +926,39 @@ static bxdf_t diffuse_scatter(const scene_t* S, const pt_material* m, const ray_
 }
 static v3 diffuse_f(const scene_t* S, const pt_material* m, const ray_t* in, const si_t* si, v3 dir) {
     /* calc_attenuation (Material.hpp:299-326) */
-    onb_t tbn = onb_n(dot(in->d, si->ns) > 0 ? neg(si->ns) : si->ns);
-    v3 wo = to_local(&tbn, neg(in->d));
+    onb_t tbn;
+    v3 wo = diffuse_frame(in->d, si->ns, &tbn);
     v3 wi = to_local(&tbn, dir);
     v3 wh = normalize(add(wo, wi));
     float rough = diffuse_rough(S, m, si);
     float metal = tex_eval(S, m->metal, si->uv).z;
     dist_t D = mkdist(rough);
     v3 col = tex_eval(S, m->tex, si->uv);
-    v3 F0 = add(muls(V(0.04f, 0.04f, 0.04f), 1.0f - metal), muls(col, metal));
-    v3 F = schlick(dot(wi, wh), F0);
+    /* glm::mix as built here: (1-metal)*0.04 rounded, col*metal fused */
+    float om = 1.0f - metal, c4 = om * 0.04f;
+    v3 F0 = V(fmaf(col.x, metal, c4), fmaf(col.y, metal, c4), fmaf(col.z, metal, c4));
+    v3 F = schlick(dot_yxz(wi, wh), F0);
     v3 num = muls(F, D_(&D, wh) * G_(&D, wo, wi));
     float den = fabsf(4.0f * wo.z * wi.z);
     if (den == 0) return V(0, 0, 0);
     v3 spec = divs(num, den);
-    v3 kD = muls(sub(V(1, 1, 1), F), 1.0f - metal);
-    v3 diff = muls(mul(kD, col), INV_PI_F);
-    return add(diff, spec);
+    v3 kc = mul(muls(sub(V(1, 1, 1), F), om), col);
+    return V(fmaf(kc.x, INV_PI_F, spec.x), fmaf(kc.y, INV_PI_F, spec.y), fmaf(kc.z, INV_PI_F, spec.z));
 }
 static float diffuse_pdf(const scene_t* S, const pt_material* m, const ray_t* in, const si_t* si, v3 dir) {
     /* MicrofacetDiffuse::PDF (Material.hpp:281-296): no (1-prob) factor (A.7) */
     float rough = diffuse_rough(S, m, si);
     dist_t D = mkdist(rough);
-    onb_t tbn = onb_n(dot(in->d, si->ns) > 0 ? neg(si->ns) : si->ns);
-    v3 wo = to_local(&tbn, neg(in->d));
+    onb_t tbn;
+    v3 wo = diffuse_frame(in->d, si->ns, &tbn);
     v3 wh = to_local(&tbn, normalize(sub(dir, in->d)));
     float prob = rough >= 0.7 ? 1.0f : 0.5f;
     float diff = prob * fabsf(dot(si->ns, dir)) * INV_PI_F;
-    float spec = mpdf_(&D, wo, wh) / (4 * fabsf(dot(wo, wh)));
+    float spec = mpdf_(&D, wo, wh, dot(wo, wh)) / (4 * fabsf(dot(wo, wh)));
     return diff + spec;
 }
 
-/* MicrofacetDielectric::scatter (Material.hpp:392-477) */
+/* MicrofacetDielectric::scatter (Material.hpp:392-477), contractions as built */
 static bxdf_t dielectric_scatter(const scene_t* S, const pt_material* m, const ray_t* in, const si_t* si, float u,
                                  float uv0, float uv1) {
     bxdf_t b;
@@ -902,24 +966,27 @@ static bxdf_t dielectric_scatter(const scene_t* S, const pt_material* m, const r
     float rough = tex_eval(S, m->rough, si->uv).y;
     dist_t D = mkdist(rough);
     onb_t tbn = onb_si(si);
-    v3 wo = to_local(&tbn, neg(in->d));
+    v3 md = neg(in->d);
+    v3 wo = to_local_ool(&tbn, md);
     float ri = m->ri;
-    float eta = dot(neg(in->d), si->ns) > 0 ? 1 / ri : ri;
+    float eta = dot_p(md, si->ns) > 0 ? 1 / ri : ri;
+    v3 eps_n;
     if (ri == 1 || smooth_(&D)) {
-        v3 N = dot(in->d, si->ns) > 0 ? neg(si->ns) : si->ns;
+        v3 N = dot_p(in->d, si->ns) > 0 ? neg(si->ns) : si->ns;
         v3 Ng = dot(in->d, si->n) > 0 ? neg(si->n) : si->n;
         float F = fresnel_dielectric(wo.z, ri);
         float R = F, T = 1.0f - R;
-        v3 dir;
+        v3 dir, p = at_f(in, si->t);
+        eps_n = V(EPS_SHADOW * Ng.x, EPS_SHADOW * Ng.y, 0);
         if (u < (R / (R + T))) {
             dir = to_world(&tbn, V(-wo.x, -wo.y, wo.z));
-            b.o = add(at(in, si->t), smul(EPS_SHADOW, Ng));
+            b.o = V(p.x + eps_n.x, p.y + eps_n.y, fmaf(Ng.z, EPS_SHADOW, p.z));
             b.f = divs(muls(tex_eval(S, m->tex, si->uv), R), fabsf(dot(si->ns, dir)));
             b.pdf = R / (R + T);
         } else {
-            dir = refract(in->d, N, eta);
+            dir = refract_f(in->d, N, eta, dot(in->d, N));
             if (is_zero(dir)) return b;
-            b.o = sub(at(in, si->t), smul(EPS_SHADOW, Ng));
+            b.o = V(p.x - eps_n.x, p.y - eps_n.y, fmaf(-Ng.z, EPS_SHADOW, p.z));
             b.f = divs(muls(tex_eval(S, m->tex, si->uv), T), fabsf(dot(si->ns, dir)));
             b.pdf = T / (R + T);
         }
@@ -928,69 +995,100 @@ static bxdf_t dielectric_scatter(const scene_t* S, const pt_material* m, const r
         b.ok = 1;
         return b;
     }
-    v3 wh = sample_wh(&D, wo, uv0, uv1);
+    v3 wh = sample_wh(&D, wo, uv0, uv1, 1);
     v3 Ng = dot(in->d, si->n) > 0 ? neg(si->n) : si->n;
-    float F = fresnel_dielectric(dot(wo, wh), 1 / eta);
+    float dow = dot_p(wo, wh); /* dot(wo, wh), unfused, shared by every use below */
+    float F = fresnel_dielectric(dow, 1 / eta);
     float R = F, T = 1 - R;
-    v3 wi;
+    v3 wi, p = at_f(in, si->t);
+    eps_n = V(EPS_SHADOW * Ng.x, EPS_SHADOW * Ng.y, 0);
     uint32_t fl = FL_TRANS | (rough < 0.001f ? FL_SPEC : 0u);
     if (u < (R / (R + T))) {
-        wi = reflect(neg(wo), wh);
+        float d = -dow;
+        wi = sub(neg(wo), muls(muls(wh, d), 2.0f));
         if (wo.z * wi.z < 0) return b;
-        b.o = add(at(in, si->t), smul(EPS_SHADOW, Ng));
+        b.o = V(p.x + eps_n.x, p.y + eps_n.y, fmaf(Ng.z, EPS_SHADOW, p.z));
         b.d = to_world(&tbn, wi);
-        b.pdf = mpdf_(&D, wo, wh) / (4 * fabsf(dot(wo, wh))) * R / (R + T);
+        b.pdf = mpdf_(&D, wo, wh, dot(wo, wh)) / (fabsf(dow) * 4) * R / (R + T);
         b.f = divs(muls(muls(muls(tex_eval(S, m->tex, si->uv), D_(&D, wh)), G_(&D, wo, wi)), R), fabsf(4 * wi.z * wo.z));
     } else {
-        wi = refract(neg(wo), wh, eta);
+        wi = refract_f(neg(wo), wh, eta, -dow);
         if (wo.z * wi.z > 0 || wi.z == 0) return b;
-        b.o = sub(at(in, si->t), smul(EPS_SHADOW, Ng));
+        b.o = V(p.x - eps_n.x, p.y - eps_n.y, fmaf(-Ng.z, EPS_SHADOW, p.z));
         b.d = to_world(&tbn, wi);
-        float denom = (dot(wi, wh) + dot(wo, wh) * eta) * (dot(wi, wh) + dot(wo, wh) * eta);
-        float dwh = fabsf(dot(wi, wh)) / denom;
-        b.pdf = mpdf_(&D, wo, wh) * dwh * T / (R + T);
-        float ft = T * D_(&D, wh) * G_(&D, wo, wi) * fabsf(dot(wi, wh) * dot(wo, wh) / (denom * wi.z * wo.z));
+        float diw = dot(wi, wh);
+        float dn = fmaf(eta, dow, diw);
+        float denom = dn * dn;
+        float dwh = fabsf(diw) / denom;
+        b.pdf = mpdf_(&D, wo, wh, dot(wo, wh)) * dwh * T / (R + T);
+        float ft = T * D_(&D, wh) * G_(&D, wo, wi) * fabsf(diw * dow / (denom * wi.z * wo.z));
         b.f = muls(tex_eval(S, m->tex, si->uv), ft);
     }
     b.flags = fl;
     b.ok = 1;
     return b;
 }
+/* MicrofacetDielectric::PDF / calc_attenuation (Material.hpp:484-564); each
+ * builds its own half vector: wi*etap + wo unfused in PDF, x and y lanes fused
+ * in calc_attenuation (and normalised out of line there) */
+static int dielectric_frame(const scene_t* S, const pt_material* m, const ray_t* in, const si_t* si, v3 dir,
+                            int for_f, dist_t* D, v3* wo, v3* wi, v3* wh, float* etap, int* refl) {
+    float rough = tex_eval(S, m->rough, si->uv).y;
+    *D = mkdist(rough);
+    float ri = m->ri;
+    if (ri == 1 || smooth_(D)) return 0;
+    onb_t tbn = onb_si(si);
+    *wo = to_local_ool(&tbn, neg(in->d));
+    *wi = to_local_ool(&tbn, dir);
+    float co = wo->z, ci = wi->z;
+    *refl = ci * co > 0;
+    *etap = 1;
+    if (!*refl) *etap = co > 0 ? ri : (1 / ri);
+    v3 h;
+    if (for_f && !*refl)
+        h = V(fmaf(wi->x, *etap, wo->x), fmaf(wi->y, *etap, wo->y), co + ci * *etap);
+    else
+        h = add(muls(*wi, *etap), *wo);
+    if (dot(h, h) == 0) return 0;
+    h = normalize(h);
+    if (h.z < 0) h = neg(h);
+    *wh = h;
+    if (dot(h, *wi) * ci <= 0.0 || dot(h, *wo) * co <= 0.0) return 0;
+    return 1;
+}
 static void dielectric_eval(const scene_t* S, const pt_material* m, const ray_t* in, const si_t* si, v3 dir,
                             v3* f_out, float* pdf_out) {
-    /* MicrofacetDielectric::PDF / calc_attenuation (Material.hpp:484-564) */
     *f_out = V(0, 0, 0);
     *pdf_out = 0;
-    float rough = tex_eval(S, m->rough, si->uv).y;
-    dist_t D = mkdist(rough);
-    float ri = m->ri;
-    if (ri == 1 || smooth_(&D)) return;
-    onb_t tbn = onb_si(si);
-    v3 wo = to_local(&tbn, neg(in->d));
-    v3 wi = to_local(&tbn, dir);
-    float co = wo.z, ci = wi.z;
-    int refl = ci * co > 0;
-    float etap = 1;
-    if (!refl) etap = co > 0 ? ri : (1 / ri);
-    v3 wh = add(muls(wi, etap), wo);
-    if (dot(wh, wh) == 0) return;
-    wh = normalize(wh);
-    if (wh.z < 0) wh = neg(wh);
-    if (dot(wh, wi) * ci <= 0.0 || dot(wh, wo) * co <= 0.0) return;
-    float F = fresnel_dielectric(dot(wo, wh), ri);
-    float R = F, T = 1 - R;
-    float pdf = mpdf_(&D, wo, wh);
-    v3 col = tex_eval(S, m->tex, si->uv);
-    if (refl) {
-        *pdf_out = pdf / (4 * fabsf(dot(wo, wh))) * R / (R + T);
-        *f_out = divs(muls(muls(muls(col, D_(&D, wh)), G_(&D, wo, wi)), F), fabsf(4 * ci * co));
-    } else {
-        float den = (dot(wi, wh) + dot(wo, wh) / etap) * (dot(wi, wh) + dot(wo, wh) / etap);
-        float dwh = fabsf(dot(wi, wh)) / den;
-        *pdf_out = pdf * dwh * T / (R + T);
-        float den2 = (dot(wi, wh) + dot(wo, wh) / etap) * (dot(wi, wh) + dot(wo, wh) / etap) * ci * co;
-        float ft = D_(&D, wh) * (1 - F) * G_(&D, wo, wi) * fabsf(dot(wi, wh) * dot(wo, wh) / den2);
-        *f_out = muls(col, ft);
+    dist_t D;
+    v3 wo, wi, wh;
+    float etap;
+    int refl;
+    if (dielectric_frame(S, m, in, si, dir, 0, &D, &wo, &wi, &wh, &etap, &refl)) {
+        float dow = dot(wh, wo), diw = dot(wh, wi);
+        float F = fresnel_dielectric(dow, m->ri);
+        float R = F, T = 1 - R;
+        float pdf = mpdf_(&D, wo, wh, dow);
+        if (refl) {
+            *pdf_out = pdf / (fabsf(dow) * 4) * R / (R + T);
+        } else {
+            float dn = dow / etap + diw;
+            float dwh = fabsf(diw) / (dn * dn);
+            *pdf_out = dwh * pdf * T / (R + T);
+        }
+    }
+    if (dielectric_frame(S, m, in, si, dir, 1, &D, &wo, &wi, &wh, &etap, &refl)) {
+        float dow = dot(wh, wo), diw = dot(wh, wi);
+        float F = fresnel_dielectric(dow, m->ri);
+        v3 col = tex_eval(S, m->tex, si->uv);
+        if (refl) {
+            *f_out = divs(muls(muls(muls(col, D_(&D, wh)), G_(&D, wo, wi)), F), fabsf(4 * wi.z * wo.z));
+        } else {
+            float dn = dow / etap + diw;
+            float den2 = dn * dn * wi.z * wo.z;
+            float ft = (1 - F) * D_(&D, wh) * G_(&D, wo, wi) * fabsf(diw * dow / den2);
+            *f_out = muls(col, ft);
+        }
     }
 }
 
@@ -998,24 +1096,30 @@ static void dielectric_eval(const scene_t* S, const pt_material* m, const ray_t*
 static bxdf_t thin_scatter(const scene_t* S, const pt_material* m, const ray_t* in, const si_t* si, float u) {
     bxdf_t b;
     memset(&b, 0, sizeof(b));
-    onb_t tbn = onb_si(si);
-    v3 wo = to_local(&tbn, neg(in->d));
+    /* as built: onb(si)'s cross with the first product rounded in every lane,
+     * wo.x and wo.y in y, x, z order */
+    onb_t tbn;
+    tbn.a2 = si->ns;
+    tbn.a0 = si->tangent;
+    tbn.a1 = cross_r(tbn.a2, tbn.a0);
+    v3 md = neg(in->d);
+    v3 wo = V(dot_yxz(md, tbn.a0), dot_yxz(md, tbn.a1), dot(md, tbn.a2));
     v3 Ng = dot(in->d, si->n) > 0 ? neg(si->n) : si->n;
     float F = fresnel_dielectric(wo.z, m->ri);
     float R = F, T = 1.0f - R;
     if (R < 1.0f) {
-        R += T * T * R / (1.0f - R * R);
+        R += T * T * R / fmaf(-R, R, 1.0f);
         T = 1.0f - R;
     }
     v3 dir, f;
     if (u < (R / (R + T))) {
         dir = to_world(&tbn, V(-wo.x, -wo.y, wo.z));
-        b.o = add(at(in, si->t), smul(EPS_SHADOW, Ng));
+        b.o = add(smul(EPS_SHADOW, Ng), at_f(in, si->t));
         f = divs(muls(V(1, 1, 1), R), fabsf(dot(si->ns, dir)));
         b.pdf = R / (R + T);
     } else {
         dir = in->d;
-        b.o = sub(at(in, si->t), smul(EPS_SHADOW, Ng));
+        b.o = sub(at_f(in, si->t), smul(EPS_SHADOW, Ng));
         f = divs(muls(V(1, 1, 1), T), fabsf(dot(si->ns, dir)));
         b.pdf = T / (R + T);
     }
@@ -1079,7 +1183,7 @@ typedef struct { v3 L; si_t si; v3 dir; } lsample_t;
 static float shape_area(const scene_t* S, const pt_prim* p) {
     if (p->kind == PT_PRIM_QUAD) {
         const pt_quad* q = &S->s->quads[p->index];
-        return length3(cross_r(vl(q->u), vl(q->v)));  /* QuadShape::Area as compiled (fixture search) */
+        return length3(cross(vl(q->u), vl(q->v)));
     }
     if (p->kind == PT_PRIM_SPHERE) {
         float r = S->s->spheres[p->index].radius;
@@ -1094,7 +1198,9 @@ static si_t shape_sample(const scene_t* S, const pt_prim* p, float u0, float u1)
     memset(&si, 0, sizeof(si));
     if (p->kind == PT_PRIM_QUAD) {
         const pt_quad* q = &S->s->quads[p->index];
-        si.p = add(add(vl(q->Q), smul(u0, vl(q->u))), smul(u1, vl(q->v)));
+        v3 Q = vl(q->Q), qu = vl(q->u), qv = vl(q->v); /* Q + u0*u + u1*v, both fused */
+        si.p = V(fmaf(qv.x, u1, fmaf(qu.x, u0, Q.x)), fmaf(qv.y, u1, fmaf(qu.y, u0, Q.y)),
+                 fmaf(qv.z, u1, fmaf(qu.z, u0, Q.z)));
         si.n = vl(q->normal);
     } else if (p->kind == PT_PRIM_SPHERE) {
         const pt_sphere* sp = &S->s->spheres[p->index];
@@ -1121,12 +1227,13 @@ static si_t shape_sample(const scene_t* S, const pt_prim* p, float u0, float u1)
     }
     return si;
 }
-static float shape_pdf(const scene_t* S, const pt_prim* p, const si_t* si, const ray_t* r) {
+/* Shape::PDF(interaction, ray) as built: dot(to, to) in y, x, z order; the
+ * quad's (inlined into AreaLight::PDF) light cosine also in y, x, z order,
+ * except behind the one-sided test, whose dot(-d, n) it reuses */
+static float shape_pdf(const scene_t* S, const pt_prim* p, const si_t* si, const ray_t* r, int one_sided) {
     v3 to = sub(si->p, r->o);
-    /* Shape::PDF's dot(to, to) compiles with the x product fused and the y
-     * product rounded (fixture search) */
-    float d2 = fmaf(to.z, to.z, fmaf(to.x, to.x, rmul(to.y, to.y)));
-    float lc = fabsf(dot(neg(r->d), si->n));
+    float d2 = dot_yxz(to, to);
+    float lc = fabsf(p->kind == PT_PRIM_QUAD && !one_sided ? dot_yxz(neg(r->d), si->n) : dot(neg(r->d), si->n));
     float area = shape_area(S, p);
     if (p->kind == PT_PRIM_QUAD) {
         if (area == 0) return 0;
@@ -1218,20 +1325,28 @@ static lsample_t light_sample(const scene_t* S, const pt_light* l, float u0, flo
         ls.si.uv[1] = u1;
         return ls;
     }
+    /* Distant / Uniform / Function light sample (Light.cpp:36-41, 62-67, 209-214):
+     * 1 - z*z fused except in FunctionInfiniteLight::sample, which also adds
+     * z*z unfused in its GetSphereUV normalisation */
+    const int sky = l->kind == PT_LIGHT_SKY_INF;
     float z = 2.0f * u0 - 1.0f;
     float th = 2.0f * PI_F * u1;
-    float r = sqrtf(1.0f - rmul(z, z));  /* not fused here (fixture search) */
-    float x = r * cosf(th), y = r * sinf(th);
+    float r = sky ? sqrtf(1.0f - z * z) : sqrtf(fmaf(-z, z, 1.0f));
+    float x = cosf(th) * r, y = sinf(th) * r;
     v3 d = V(x, y, z);
     if (l->kind == PT_LIGHT_DISTANT) {
         ls.L = vl(l->color);
         ls.si.uv[0] = u0;
         ls.si.uv[1] = u1;
-        ls.dir = normalize(add(vl(l->vec), muls(d, 0.02f)));
+        v3 vv = vl(l->vec);
+        ls.dir = normalize(V(fmaf(d.x, 0.02f, vv.x), fmaf(d.y, 0.02f, vv.y), fmaf(d.z, 0.02f, vv.z)));
         return ls;
     }
     ls.L = inf_le(l, d);
-    sphere_uv(d, ls.si.uv);
+    if (sky)
+        sphere_uv_n(muls(d, 1.0f / sqrtf(fmaf(y, y, x * x) + z * z)), ls.si.uv);
+    else
+        sphere_uv(d, ls.si.uv);
     ls.dir = d;
     return ls;
 }
@@ -1247,11 +1362,11 @@ static float light_pdf(const scene_t* S, const pt_light* l, const si_t* si, cons
             ray_t lr = *r;
             lr.o = m4_point(I->inv, r->o);
             lr.d = normalize(m4_dir(I->inv, r->d));
-            if (l->one_sided) return dot(neg(lr.d), lo.n) > 0 ? shape_pdf(S, p, &lo, &lr) : 0;
-            return shape_pdf(S, p, &lo, &lr);
+            if (l->one_sided) return dot(neg(lr.d), lo.n) > 0 ? shape_pdf(S, p, &lo, &lr, 1) : 0;
+            return shape_pdf(S, p, &lo, &lr, 0);
         }
-        if (l->one_sided) return dot(neg(r->d), si->n) > 0 ? shape_pdf(S, p, si, r) : 0;
-        return shape_pdf(S, p, si, r);
+        if (l->one_sided) return dot(neg(r->d), si->n) > 0 ? shape_pdf(S, p, si, r, 1) : 0;
+        return shape_pdf(S, p, si, r, 0);
     }
     if (l->kind == PT_LIGHT_UNIFORM_INF || l->kind == PT_LIGHT_SKY_INF) return 1.0f / (4.0f * PI_F);
     if (l->kind == PT_LIGHT_TEX_INF) return texinf_pdf(S, l, r->d);
@@ -1322,7 +1437,7 @@ static v3 sample_ld(const integ_t* I, const ray_t* ray, const si_t* si, float u,
     }
     ray_t sh = mkray(si->p, normalize(ldir));
     float lpdf = l->pmf;
-    float dt = dot(si->ns, sh.d);
+    float dt = dot_yxz(si->ns, sh.d); /* as built: y, x, z order */
     if (lpdf <= 0 || dt * dot(ray->d, si->ns) >= 0) return V(0, 0, 0);
     work_t wk = {0, 0};
     I->cnt->any++;
@@ -1336,8 +1451,7 @@ static v3 sample_ld(const integ_t* I, const ray_t* ray, const si_t* si, float u,
     if (lpdf <= 0) return V(0, 0, 0);
     float w2 = lpdf * lpdf;
     float w1 = mat_pdf(S, si->mat, ray, si, sh.d);
-    w1 = w1 * w1;
-    float wl = w2 / (w1 + w2);
+    float wl = w2 / fmaf(w1, w1, w2); /* w1*w1 + w2 fused */
     return divs(muls(mul(light_L(S, l, &ls.si, &sh), f), wl), lpdf);
 }
 
@@ -1378,12 +1492,15 @@ static v3 li_path(const integ_t* I, ray_t ray, rng_t* rng) {
             DBG("O d%u miss\n", depth);
             for (uint32_t k = 0; k < S->s->n_infinite_lights; k++) {
                 const pt_light* l = &S->s->lights[S->s->infinite_lights[k]];
+                /* as built: out += att*Le fused; the MIS weight's lp*lp + p*p
+                 * and out += (att*Le)*w fused */
                 if (spec) {
-                    out = add(out, mul(att, inf_le(l, ray.d)));
+                    out = fma3(inf_le(l, ray.d), att, out);
                 } else if (prev > 0) {
                     float lp = l->pmf * inf_pdf(S, l, ray.d);
-                    float w = prev * prev / (prev * prev + lp * lp);
-                    out = add(out, muls(mul(att, inf_le(l, ray.d)), w));
+                    float p2 = prev * prev;
+                    float w = p2 / fmaf(lp, lp, p2);
+                    out = fma3s(w, mul(inf_le(l, ray.d), att), out);
                 }
             }
             return out;
@@ -1398,17 +1515,18 @@ static v3 li_path(const integ_t* I, ray_t ray, rng_t* rng) {
             v3 L = light_L(S, al, &si, &ray);
             if (!is_zero(L)) {
                 if (spec) {
-                    out = add(out, mul(att, L));
+                    out = fma3(L, att, out);
                 } else if (prev > 0) {
                     float lp = al->pmf * light_pdf(S, al, &si, &ray);
-                    float w = prev * prev / (prev * prev + lp * lp);
-                    out = add(out, muls(mul(att, L), w));
+                    float p2 = prev * prev;
+                    float w = p2 / fmaf(lp, lp, p2);
+                    out = fma3s(w, mul(L, att), out);
                 }
             }
         }
         if (si.mat < 0) {
             spec = 1;
-            ray.o = at(&ray, si.t);
+            ray.o = at_f(&ray, si.t);
             continue;
         }
         bxdf_t b = mat_scatter(S, si.mat, &ray, &si, r[4], r[0], r[1]);
@@ -1418,7 +1536,7 @@ static v3 li_path(const integ_t* I, ray_t ray, rng_t* rng) {
         if (!spec) {
             v3 ld = sample_ld(I, &ray, &si, r[5], r[2], r[3], texinf_uc(rng));
             DBG("O  ld %a %a %a (light %d)\n", ld.x, ld.y, ld.z, ls_sample(S, r[5]));
-            out = add(out, mul(att, ld));
+            out = fma3(ld, att, out);
             prev = mat_pdf(S, si.mat, &ray, &si, nr.d);
         }
         DBG("O  scatter d %a %a %a f %a %a %a pdf %a prev %a\n", b.d.x, b.d.y, b.d.z, b.f.x, b.f.y, b.f.z, b.pdf, prev);
@@ -1444,7 +1562,7 @@ static v3 li_simple(const integ_t* I, ray_t ray, rng_t* rng) {
         if (!intersect_counted(I, &ray, &si)) {
             for (uint32_t k = 0; k < S->s->n_infinite_lights; k++) {
                 const pt_light* l = &S->s->lights[S->s->infinite_lights[k]];
-                out = add(out, mul(att, inf_le(l, ray.d)));
+                out = fma3(inf_le(l, ray.d), att, out);
             }
             return out;
         }
@@ -1453,10 +1571,10 @@ static v3 li_simple(const integ_t* I, ray_t ray, rng_t* rng) {
         float ur = next1(rng);
         if (si.light >= 0) {
             v3 L = light_L(S, &S->s->lights[si.light], &si, &ray);
-            if (!is_zero(L)) out = add(out, mul(att, L));
+            if (!is_zero(L)) out = fma3(L, att, out);
         }
         if (si.mat < 0) {
-            ray.o = at(&ray, si.t);
+            ray.o = at_f(&ray, si.t);
             continue;
         }
         bxdf_t b = mat_scatter(S, si.mat, &ray, &si, us, u0, u1);
@@ -1476,23 +1594,34 @@ static v3 li_simple(const integ_t* I, ray_t ray, rng_t* rng) {
 /* ------------------------------------------------------------------ media (Medium.hpp, PhaseFunction.*) */
 /* phaseHG (PhaseFunction.hpp:4-8) */
 static float phase_hg(float cosT, float g) {
-    float denom = 1 + g * g + 2 * g * cosT;
-    return 0.25f * (1.0f / PI_F) * (1.0f - g * g) / (denom * sqrtf(denom));
+    /* phaseHG (PhaseFunction.hpp:5-8) as built: 1 + g*g, + 2g*cos and 1 - g*g fused */
+    float denom = fmaf(cosT, 2.0f * g, fmaf(g, g, 1.0f));
+    return fmaf(-g, g, 1.0f) * (0.25f * (1.0f / PI_F)) / (denom * sqrtf(denom));
 }
 /* HenyeyGreenstein::Sample (PhaseFunction.cpp:8-25): direction, returns pdf */
 static v3 phase_sample(float g, v3 in, float u0, float u1) {
     float cosT;
-    if (fabsf(g) < 1e-3f) {
+    if (fabs(g) < 1e-3) {
         cosT = 1 - 2 * u0;
     } else {
-        float sqr = (1 - g * g) / (1 - g + 2 * g * u0);
-        cosT = (1 + g * g - sqr * sqr) / (2 * g);
+        float sqr = fmaf(-g, g, 1.0f) / fmaf(2.0f * g, u0, 1 - g);
+        cosT = fmaf(-sqr, sqr, fmaf(g, g, 1.0f)) / (2 * g);
     }
-    float sinT = sqrtf(fmaxf_(0.0f, 1 - cosT * cosT));
+    float q = fmaf(-cosT, cosT, 1.0f);
+    float sinT = q > 0 ? sqrtf(q) : 0.0f;
     float phi = 2 * PI_F * u1;
-    float x = sinT * cosf(phi), y = sinT * sinf(phi), z = cosT;
-    onb_t b = onb_n(in);
-    return normalize(to_world(&b, V(x, y, z)));
+    float x = cosf(phi) * sinT, y = sinf(phi) * sinT, z = cosT;
+    /* onb(in).toWorld as built here: a0 = cross(a1, a2) with the x, y lanes
+     * rounded-first; x, y lanes (x*a0 fused onto y*a1) + z*a2 unfused, z lane
+     * the usual chain */
+    onb_t b;
+    b.a2 = in;
+    v3 up = (fabsf(in.x) > 0.9999) ? V(0, 1, 0) : V(1, 0, 0);
+    b.a1 = normalize(cross(b.a2, up));
+    b.a0 = cross_v(b.a1, b.a2);
+    v3 w = V(fmaf(b.a0.x, x, y * b.a1.x) + z * b.a2.x, fmaf(b.a0.y, x, y * b.a1.y) + z * b.a2.y,
+             fmaf(z, b.a2.z, fmaf(y, b.a1.z, x * b.a0.z)));
+    return normalize(w);
 }
 /* HomogeneusMedium::Tr (Medium.hpp:21-24) */
 static v3 medium_tr(const pt_medium* m, float t) {
@@ -1508,11 +1637,11 @@ static v3 medium_sample(const pt_medium* m, const ray_t* r, float t, float u0, f
     *sampled = sd < t;
     if (*sampled) *scat = V(fmaf(sd, r->d.x, r->o.x), fmaf(sd, r->d.y, r->o.y), fmaf(sd, r->d.z, r->o.z));
     v3 tr = medium_tr(m, sd);
-    v3 den = *sampled ? mul(vl(m->sigma_t), tr) : tr;
-    float pdf = 0;
-    pdf += den.x;
-    pdf += den.y;
-    pdf += den.z;
+    float pdf;
+    if (*sampled) /* the sum of sigma_t*tr with the products fused */
+        pdf = fmaf(m->sigma_t[2], tr.z, fmaf(m->sigma_t[1], tr.y, tr.x * m->sigma_t[0]));
+    else
+        pdf = ((0.0f + tr.x) + tr.y) + tr.z;
     pdf = (float)((double)pdf / 3.0);
     return *sampled ? divs(mul(tr, vl(m->sigma_s)), pdf) : divs(tr, pdf);
 }
@@ -1539,7 +1668,7 @@ static int intersect_tr(const integ_t* I, ray_t ray, int med, float max, v3* Tr)
         }
         if (med >= 0) *Tr = mul(*Tr, medium_tr(&S->s->media[med], si.t));
         if (si.mat >= 0) return 1;
-        ray = mkray(at(&ray, si.t), ray.d);
+        ray = mkray(at_f(&ray, si.t), ray.d);
         med = get_medium(&si, ray.d);
         max -= si.t;
     }
@@ -1585,9 +1714,7 @@ static v3 sample_ld_vol(const integ_t* I, const ray_t* ray, int ray_med, const s
     lpdf *= light_pdf(S, l, &ls.si, &sh);
     if (lpdf <= 0) return V(0, 0, 0);
     float w2 = lpdf * lpdf;
-    float w1 = spdf;
-    w1 = w1 * w1;
-    float wl = w2 / (w1 + w2);
+    float wl = w2 / fmaf(spdf, spdf, w2);
     return divs(muls(mul(mul(Tr, light_L(S, l, &ls.si, &sh)), f), wl), lpdf);
 }
 
@@ -1605,11 +1732,12 @@ static v3 li_volpath(const integ_t* I, ray_t ray, int med, rng_t* rng) {
             for (uint32_t k = 0; k < S->s->n_infinite_lights; k++) {
                 const pt_light* l = &S->s->lights[S->s->infinite_lights[k]];
                 if (spec) {
-                    out = add(out, mul(att, inf_le(l, ray.d)));
+                    out = fma3(inf_le(l, ray.d), att, out);
                 } else if (prev > 0) {
                     float lp = l->pmf * inf_pdf(S, l, ray.d);
-                    float w = prev * prev / (prev * prev + lp * lp);
-                    out = add(out, muls(mul(att, inf_le(l, ray.d)), w));
+                    float p2 = prev * prev;
+                    float w = p2 / fmaf(lp, lp, p2);
+                    out = fma3s(w, mul(inf_le(l, ray.d), att), out);
                 }
             }
             return out;
@@ -1628,8 +1756,8 @@ static v3 li_volpath(const integ_t* I, ray_t ray, int med, rng_t* rng) {
             si_t mi;
             memset(&mi, 0, sizeof(mi));
             mi.p = mp;
-            out = add(out, mul(att, sample_ld_vol(I, &ray, med, &mi, 1, M->g, r[5], r[2], r[3], texinf_uc(rng))));
-            out = add(out, mul(att, vl(M->Le)));
+            out = fma3(att, sample_ld_vol(I, &ray, med, &mi, 1, M->g, r[5], r[2], r[3], texinf_uc(rng)), out);
+            out = fma3(att, vl(M->Le), out);
             v3 sc = phase_sample(M->g, ray.d, r[6], r[7]);
             int nm = get_medium(&si, sc);
             ray = mkray(mp, sc);
@@ -1641,17 +1769,18 @@ static v3 li_volpath(const integ_t* I, ray_t ray, int med, rng_t* rng) {
                 v3 L = light_L(S, al, &si, &ray);
                 if (!is_zero(L)) {
                     if (spec) {
-                        out = add(out, mul(att, L));
+                        out = fma3(att, L, out);
                     } else if (prev > 0) {
                         float lp = al->pmf * light_pdf(S, al, &si, &ray);
-                        float w = prev * prev / (prev * prev + lp * lp);
-                        out = add(out, muls(mul(att, L), w));
+                        float p2 = prev * prev;
+                        float w = p2 / fmaf(lp, lp, p2);
+                        out = fma3s(w, mul(att, L), out);
                     }
                 }
             }
             spec = 0;
             if (si.mat < 0) {
-                ray.o = at(&ray, si.t);
+                ray.o = at_f(&ray, si.t);
                 med = get_medium(&si, ray.d);
                 continue;
             }
@@ -1662,7 +1791,7 @@ static v3 li_volpath(const integ_t* I, ray_t ray, int med, rng_t* rng) {
             if (!(b.flags & FL_TRANS) && dot(ray.d, si.ns) <= 0) nm = med;
             spec = (b.flags & FL_SPEC) != 0;
             if (!spec) {
-                out = add(out, mul(att, sample_ld_vol(I, &ray, med, &si, 0, 0.0f, r[5], r[2], r[3], texinf_uc(rng))));
+                out = fma3(att, sample_ld_vol(I, &ray, med, &si, 0, 0.0f, r[5], r[2], r[3], texinf_uc(rng)), out);
                 prev = mat_pdf(S, si.mat, &ray, &si, nr.d);
             }
             att = mul(att, divs(muls(b.f, fabsf(dot(si.ns, nr.d))), b.pdf));
@@ -1699,8 +1828,9 @@ static ray_t camera_ray(const pt_camera_desc* c, uint32_t x, uint32_t y, rng_t* 
     v3 du = smul(c->defocus_radius, vl(c->u));
     v3 dv = smul(c->defocus_radius, vl(c->v));
     dir = muls(dir, c->focus_distance);
-    v3 off = add(smul(lx, du), smul(ly, dv));
-    return mkray(add(vl(c->origin), off), normalize(sub(dir, off)));
+    /* offset = pLens.x*du + pLens.y*dv with the second product fused (as built) */
+    v3 off = V(fmaf(dv.x, ly, du.x * lx), fmaf(dv.y, ly, du.y * lx), fmaf(dv.z, ly, du.z * lx));
+    return mkray(add(off, vl(c->origin)), normalize(sub(dir, off)));
 }
 
 static void scene_init(scene_t* S, const pt_scene_desc* s) {

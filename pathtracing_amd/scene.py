@@ -80,6 +80,15 @@ def _cross(a: np.ndarray, b: np.ndarray) -> np.ndarray:
                      a[0] * b[1] - b[0] * a[1]], dtype=np.float32)
 
 
+def _cross_c(a, b) -> np.ndarray:
+    """glm::cross as the reference build contracts it in Shape::Area: each
+    lane's first product fused, the second rounded."""
+    a = np.asarray(a, dtype=np.float32)
+    b = np.asarray(b, dtype=np.float32)
+    return np.array([_fma32(a[1], b[2], -f32(b[1] * a[2])), _fma32(a[2], b[0], -f32(b[2] * a[0])),
+                     _fma32(a[0], b[1], -f32(b[0] * a[1]))], dtype=np.float32)
+
+
 def _dot(a, b) -> np.float32:
     a = np.asarray(a, dtype=np.float32)
     b = np.asarray(b, dtype=np.float32)
@@ -98,10 +107,17 @@ def _expand_seq(points) -> np.ndarray:
     return np.concatenate([mn, mx], axis=-1).astype(np.float32)
 
 
+def _fma64(a, b, c) -> float:
+    """fma(a, b, c) in double: the exact a*b + c rounded once."""
+    from fractions import Fraction
+    return float(Fraction(float(a)) * Fraction(float(b)) + Fraction(float(c)))
+
+
 def luminance(c) -> float:
-    """Util.hpp:3-5 (double)."""
+    """Util.hpp:3-5 (double), as the reference build contracts it: the x
+    product rounded, then fma(y), fma(z) (AreaLight::PreProcess's GIMPLE)."""
     c = np.asarray(c, dtype=np.float64)
-    return float(c[0] * 0.2126 + c[1] * 0.7152 + c[2] * 0.0722)
+    return _fma64(c[2], 0.0722, _fma64(c[1], 0.7152, c[0] * 0.2126))
 
 
 # --------------------------------------------------------------------------
@@ -308,8 +324,8 @@ class QuadShape(Shape):
         return _expand_seq([self.Q, quv, qu, qv])  # QuadShape ctor (Shape.hpp:120-129)
 
     def Area(self) -> float:
-        c = _cross(self.u, self.v)
-        return float(f32(np.sqrt(_dot(c, c))))
+        c = _cross_c(self.u, self.v)  # QuadShape::Area (Shape.hpp:143-145) as built
+        return float(f32(np.sqrt(_dot_c(c, c))))
 
 
 class SphereShape(Shape):
@@ -494,8 +510,8 @@ class AreaLight(Light):
             i0, i1, i2 = (int(x) for x in mesh.indices[3 * k:3 * k + 3])
             a = mesh.vertices[i0] - mesh.vertices[i2]
             b = mesh.vertices[i1] - mesh.vertices[i2]
-            c = _cross(a.astype(np.float32), b.astype(np.float32))
-            return float(f32(f32(np.sqrt(_dot(c, c))) * f32(0.5)))
+            c = _cross_c(a, b)  # TriangleShape::Area (Shape.cpp:298-301) as built
+            return float(f32(f32(np.sqrt(_dot_c(c, c))) * f32(0.5)))
         return self.shape.Area()
 
     def Power(self) -> float:
