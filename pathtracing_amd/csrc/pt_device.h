@@ -164,9 +164,13 @@ __device__ __forceinline__ f3 operator*(f3 a, float s) { return F3(a.x * s, a.y 
 __device__ __forceinline__ f3 operator*(float s, f3 a) { return F3(s * a.x, s * a.y, s * a.z); }
 __device__ __forceinline__ f3 operator/(f3 a, float s) { return F3(a.x / s, a.y / s, a.z / s); }
 __device__ __forceinline__ f3 operator-(f3 a) { return F3(-a.x, -a.y, -a.z); }
-// Contraction is spelled out where the reference's GCC build fixes it (its
-// disassembly; DESIGN.md "Numerics"): fma() fuses, rmul() is a product that
-// must stay rounded.  The oracle (oracle/pt_oracle.c) uses the same forms.
+// Float semantics: the device is compiled with -ffp-contract=off and every
+// fused multiply-add the reference's GCC build emits is spelled out with fma_
+// at the same site (read from the reference's optimized GIMPLE,
+// tools/refgimple.py; DESIGN.md "Numerics"); everything else rounds each
+// operation.  The oracle (oracle/pt_oracle.c, also contract-off) writes the
+// same expressions, so device and oracle agree bit for bit, and both with the
+// reference.  rmul() marks a product that must stay rounded.
 __device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 __device__ __forceinline__ float rmul(float a, float b) {
     float m = a * b;
@@ -175,6 +179,10 @@ __device__ __forceinline__ float rmul(float a, float b) {
 }
 // glm::dot: x product rounded, then fma(y), fma(z)
 __device__ __forceinline__ float dot(f3 a, f3 b) { return fma_(a.z, b.z, fma_(a.y, b.y, rmul(a.x, b.x))); }
+// the other orders the build emits: y product rounded, then fma(x), fma(z);
+// and the unfused (x + y) + z
+__device__ __forceinline__ float dot_yxz(f3 a, f3 b) { return fma_(a.z, b.z, fma_(a.x, b.x, rmul(a.y, b.y))); }
+__device__ __forceinline__ float dot_p(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 // glm::cross in scalar code: first product fused, second rounded
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {
     return F3(fma_(a.y, b.z, -rmul(b.y, a.z)), fma_(a.z, b.x, -rmul(b.z, a.x)), fma_(a.x, b.y, -rmul(b.x, a.y)));
@@ -192,6 +200,11 @@ __device__ __forceinline__ f3 cross_v(f3 a, f3 b) {
 __device__ __forceinline__ float lerp3f(float u, float a, float v, float b, float w, float c) {
     return fma_(w, c, fma_(v, b, rmul(u, a)));
 }
+// a*b + c per lane, fused (glm's `c += a * b` as the reference build contracts it)
+__device__ __forceinline__ f3 fma3(f3 a, f3 b, f3 c) { return F3(fma_(a.x, b.x, c.x), fma_(a.y, b.y, c.y), fma_(a.z, b.z, c.z)); }
+__device__ __forceinline__ f3 fma3s(float s, f3 b, f3 c) { return F3(fma_(s, b.x, c.x), fma_(s, b.y, c.y), fma_(s, b.z, c.z)); }
+// ray.at(t) fused in every lane
+__device__ __forceinline__ f3 at_f(f3 o, f3 d, float t) { return F3(fma_(t, d.x, o.x), fma_(t, d.y, o.y), fma_(t, d.z, o.z)); }
 __device__ __forceinline__ float csqrt(float x) { return __builtin_sqrtf(x); }
 // sinf / cosf: the host libm's algorithm, bit-identical (pt_sincosf.h)
 #define PT_SC_FN __device__ __forceinline__ static
@@ -200,17 +213,23 @@ __device__ __forceinline__ float csqrt(float x) { return __builtin_sqrtf(x); }
 __constant__ const double pt_sc_table[2][14] = PT_SC_TABLE;
 __device__ __forceinline__ float cos_cr(float x) { return pt_cosf_t(x, pt_sc_table); }
 __device__ __forceinline__ float sin_cr(float x) { return pt_sinf_t(x, pt_sc_table); }
-// powf: evaluated in double and rounded once (glibc's powf is within 0.82 ulp,
-// so a few results differ from it by one ulp)
-__device__ __forceinline__ float pow_cr(float x, float y) { return (float)pow((double)x, (double)y); }
+// expf / powf / acosf / atan2f: the host libm's algorithms, bit-identical (pt_libmf.h)
+#include "pt_libmf.h"
+__constant__ const uint64_t pt_expf_table[32] = PT_EXPF_TABLE;
+__constant__ const double pt_powf_log2_table[32] = PT_POWF_LOG2_TABLE;
+__device__ __forceinline__ float pow_cr(float x, float y) { return pt_powf_t(x, y, pt_powf_log2_table, pt_expf_table); }
+__device__ __forceinline__ float exp_cr(float x) { return pt_expf_t(x, pt_expf_table); }
 __device__ __forceinline__ float length(f3 a) { return csqrt(dot(a, a)); }
 __device__ __forceinline__ f3 normalize(f3 a) { return a * (1.0f / csqrt(dot(a, a))); }
 __device__ __forceinline__ bool is_zero(f3 a) { return a.x == 0.0f && a.y == 0.0f && a.z == 0.0f; }
 __device__ __forceinline__ f3 reflect(f3 I, f3 N) { return I - (N * dot(N, I)) * 2.0f; }
-__device__ __forceinline__ f3 refract(f3 I, f3 N, float eta) {
-    float d = dot(N, I);
-    float k = 1.0f - eta * eta * (1.0f - d * d);
-    if (k >= 0.0f) return eta * I - (eta * d + csqrt(k)) * N;
+// glm::refract with the build's contractions, given d = dot(N, I)
+__device__ __forceinline__ f3 refract_f(f3 I, f3 N, float eta, float d) {
+    const float k = fma_(-(eta * eta), fma_(-d, d, 1.0f), 1.0f);
+    if (k >= 0.0f) {
+        const float c = fma_(eta, d, csqrt(k));
+        return F3(fma_(-c, N.x, eta * I.x), fma_(-c, N.y, eta * I.y), fma_(-c, N.z, eta * I.z));
+    }
     return F3(0, 0, 0);
 }
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }

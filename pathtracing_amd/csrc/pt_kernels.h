@@ -56,12 +56,28 @@ __device__ __forceinline__ uint32_t path_slot(uint32_t i, uint32_t c, uint32_t c
     return i < c ? i : cap - 1u - (i - c);
 }
 
+// A deferred NEE ray.  The unoccluded contribution is added as
+// out = fma(c, att, out), the reference's `output += att * SampleLd(...)` as
+// its build contracts it (Integrators.cpp:239), so c and att travel apart.
 struct ShadowRec {
     float4 o;  // origin, tmax
     float4 d;  // direction, target (bits): entry in next state, or DONE_BIT|entry in done list
-    float4 c;  // contribution if unoccluded
+    float4 c;  // SampleLd's value if unoccluded
+    float4 a;  // the path's attenuation
+};
+// VolPath's: SampleLd's value is ((Tr * L) * f * w) / pdf (Integrators.cpp:
+// 466-478), so its factors travel apart for Tr to multiply in first.
+struct ShadowRecV {
+    float4 o;  // origin, tmax
+    float4 d;  // direction, target | SHADOW_MLE_BIT
+    float4 L;  // light radiance, .w: the ray's medium (bits)
+    float4 f;  // scattering value, .w: MIS weight (1 for delta lights)
+    float4 a;  // the path's attenuation, .w: light pdf
 };
 #define SHADOW_DONE_BIT 0x80000000u
+// medium interaction: the medium's Le is added after SampleLd's value
+// (Integrators.cpp:356-357), occluded or not
+#define SHADOW_MLE_BIT 0x40000000u
 
 struct RenderParams {
     pt_camera_desc cam;
@@ -98,9 +114,9 @@ template <int INTEGRATOR>
 __global__ void k_shade(RenderParams R, PathSoA cur, const uint32_t* nptr, const float4* hit, PathSoA next,
                         float* sample_L, unsigned long long* next_sample, ShadowRec* sq, uint32_t* cnt);
 __global__ void k_shade_vol(RenderParams R, PathSoA cur, const uint32_t* nptr, const float4* hit, PathSoA next,
-                            float* sample_L, unsigned long long* next_sample, ShadowRec* sq, uint32_t* cnt);
+                            float* sample_L, unsigned long long* next_sample, ShadowRecV* sq, uint32_t* cnt);
 template <bool COUNT>
-__global__ void k_shadow_tr(PathSoA next, float* sample_L, const ShadowRec* sq, const uint32_t* nptr,
+__global__ void k_shadow_tr(PathSoA next, float* sample_L, const ShadowRecV* sq, const uint32_t* nptr,
                             unsigned long long* counters);
 __global__ void k_fill(RenderParams R, uint32_t n, PathSoA next, uint32_t* cnt, unsigned long long* next_sample);
 __global__ void k_resolve(const double* film, uint32_t npx, uint32_t tonemap, uint8_t* rgb);

@@ -110,7 +110,7 @@ __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, flo
             tri_glm(ro, rd, xyz(g.a), xyz(g.b), xyz(g.c), bx, by, t);
         } else if (kind == PT_PRIM_QUAD) {
             float a, b;
-            quad_hit(S.quads[pi.index], ro, rd, __int_as_float(0x7f800000), t, a, b);
+            quad_hit<false>(S.quads[pi.index], ro, rd, __int_as_float(0x7f800000), t, a, b);
         } else {
             sphere_root(S.spheres[pi.index], ro, rd, __int_as_float(0x7f800000), t);
         }
@@ -213,19 +213,19 @@ struct ShadowSrc {
         // unoccluded: add the contribution; one shadow ray per path per bounce,
         // so a plain read-modify-write
         const uint32_t tgt = __float_as_uint(sq[i].d.w);
-        const float4 c = sq[i].c;
+        const float4 c = sq[i].c, a = sq[i].a;
         if (tgt & SHADOW_DONE_BIT) {  // the path ended this bounce: its sample's radiance
             float* L = sample_L + 3ull * (tgt & ~SHADOW_DONE_BIT);
-            L[0] += c.x;
-            L[1] += c.y;
-            L[2] += c.z;
+            L[0] = fma_(c.x, a.x, L[0]);
+            L[1] = fma_(c.y, a.y, L[1]);
+            L[2] = fma_(c.z, a.z, L[2]);
             return;
         }
         float4* L = &next.L[tgt];
         float4 v = *L;
-        v.x += c.x;
-        v.y += c.y;
-        v.z += c.z;
+        v.x = fma_(c.x, a.x, v.x);
+        v.y = fma_(c.y, a.y, v.y);
+        v.z = fma_(c.z, a.z, v.z);
         *L = v;
     }
 };
@@ -496,7 +496,8 @@ __device__ __forceinline__ void camera_ray(const pt_camera_desc& c, uint32_t key
     float lx = r * cos_cr(th), ly = r * sin_cr(th);
     f3 du = c.defocus_radius * U, dv = c.defocus_radius * Vv;
     dir = dir * c.focus_distance;
-    f3 off = lx * du + ly * dv;
+    // pLens.x * du + pLens.y * dv with the second product fused (as built)
+    f3 off = F3(fma_(dv.x, ly, du.x * lx), fma_(dv.y, ly, du.y * lx), fma_(dv.z, ly, du.z * lx));
     o = org + off;
     d = normalize(dir - off);
 }
@@ -613,12 +614,13 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
             // miss: infinite lights (Integrators.cpp:140-145, 196-208)
             for (uint32_t k = 0; k < S.n_infinite_lights; k++) {
                 const pt_light& l = S.lights[S.infinite_lights[k]];
+                // as built: out += att * Le fused; lp*lp + p*p and out += (Le*att)*w fused
                 if (INTEGRATOR == PT_INTEGRATOR_SIMPLE || spec) {
-                    out = out + att * inf_le(l, rd);
+                    out = fma3(inf_le(l, rd), att, out);
                 } else if (prev > 0) {
-                    float lp = l.pmf * inf_pdf(l, rd);
-                    float w = prev * prev / (prev * prev + lp * lp);
-                    out = out + (att * inf_le(l, rd)) * w;
+                    const float lp = l.pmf * inf_pdf(l, rd), p2 = prev * prev;
+                    const float w = p2 / fma_(lp, lp, p2);
+                    out = fma3s(w, inf_le(l, rd) * att, out);
                 }
             }
             alive = false;
@@ -648,18 +650,18 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
                 f3 Le = light_L(al, si.n, si.u, si.v, rd);
                 if (!is_zero(Le)) {
                     if (INTEGRATOR == PT_INTEGRATOR_SIMPLE || spec) {
-                        out = out + att * Le;
+                        out = fma3(Le, att, out);
                     } else if (prev > 0) {
-                        float lp = al.pmf * light_pdf(al, si.p, si.n, ro, rd);
-                        float w = prev * prev / (prev * prev + lp * lp);
-                        out = out + (att * Le) * w;
+                        const float lp = al.pmf * light_pdf(al, si.p, si.n, ro, rd), p2 = prev * prev;
+                        const float w = p2 / fma_(lp, lp, p2);
+                        out = fma3s(w, Le * att, out);
                     }
                 }
             }
             if (si.mat < 0) {
                 // medium boundary: pass through (Integrators.cpp:156-159, 228-232)
                 if (INTEGRATOR == PT_INTEGRATOR_PATH) spec = true;
-                ro = ro + si.t * rd;
+                ro = at_f(ro, rd, si.t);
             } else {
                 const float us = INTEGRATOR == PT_INTEGRATOR_PATH ? r[4] : r[2];
                 const Bxdf b = mat_scatter(si.mat, ro, rd, si, us, r[0], r[1]);
@@ -685,7 +687,7 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
                                 }
                                 const f3 sd = normalize(ldir);
                                 float lpdf = l.pmf;
-                                const float dt = dot(si.ns, sd);
+                                const float dt = dot_yxz(si.ns, sd);  // as built: y, x, z order
                                 if (!(lpdf <= 0 || dt * dot(rd, si.ns) >= 0)) {
                                     const f3 f = mat_f(si.mat, rd, si, sd) * fabsf(dt);
                                     f3 c;
@@ -697,21 +699,18 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
                                         if (lpdf <= 0) {
                                             ok = false;
                                         } else {
-                                            float w2 = lpdf * lpdf;
-                                            float w1 = mat_pdf(si.mat, rd, si, sd);
-                                            w1 = w1 * w1;
-                                            float wl = w2 / (w1 + w2);
+                                            const float w2 = lpdf * lpdf;
+                                            const float w1 = mat_pdf(si.mat, rd, si, sd);
+                                            const float wl = w2 / fma_(w1, w1, w2);  // w1*w1 + w2 fused
                                             c = ((light_L(l, ls.n, ls.u, ls.v, sd) * f) * wl) / lpdf;
                                         }
                                     }
-                                    if (ok) {
-                                        f3 contrib = att * c;
-                                        if (!is_zero(contrib)) {
-                                            shadow = true;
-                                            srec.o = make_float4(si.p.x, si.p.y, si.p.z, tmax);
-                                            srec.d = make_float4(sd.x, sd.y, sd.z, 0.0f);
-                                            srec.c = make_float4(contrib.x, contrib.y, contrib.z, 0.0f);
-                                        }
+                                    if (ok && !is_zero(c)) {
+                                        shadow = true;
+                                        srec.o = make_float4(si.p.x, si.p.y, si.p.z, tmax);
+                                        srec.d = make_float4(sd.x, sd.y, sd.z, 0.0f);
+                                        srec.c = make_float4(c.x, c.y, c.z, 0.0f);
+                                        srec.a = make_float4(att.x, att.y, att.z, 0.0f);
                                     }
                                 }
                             }
@@ -792,13 +791,13 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                                                   const float4* __restrict__ hit, PathSoA next,
                                                   float* __restrict__ sample_L,
                                                   unsigned long long* __restrict__ next_sample,
-                                                  ShadowRec* __restrict__ sq, uint32_t* __restrict__ cnt) {
+                                                  ShadowRecV* __restrict__ sq, uint32_t* __restrict__ cnt) {
     const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
     if (blockIdx.x * 256 >= n) return;  // block-uniform: the grid covers the capacity
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
     const uint32_t i = (R.order && t < n) ? R.order[t] : t;  // material-sorted order, or the path order
     bool cont = false, done = false, shadow = false;
-    ShadowRec srec;
+    ShadowRecV srec;
     f3 ro = F3(0, 0, 0), rd = F3(0, 0, 0), att = F3(0, 0, 0), out = F3(0, 0, 0);
     float prev = 0;
     uint32_t key = 0, dim = 0, flags = 0, sid = 0;
@@ -825,11 +824,11 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
             for (uint32_t k = 0; k < S.n_infinite_lights; k++) {
                 const pt_light& l = S.lights[S.infinite_lights[k]];
                 if (spec) {
-                    out = out + att * inf_le(l, rd);
+                    out = fma3(inf_le(l, rd), att, out);
                 } else if (prev > 0) {
-                    float lp = l.pmf * inf_pdf(l, rd);
-                    float w = prev * prev / (prev * prev + lp * lp);
-                    out = out + (att * inf_le(l, rd)) * w;
+                    const float lp = l.pmf * inf_pdf(l, rd), p2 = prev * prev;
+                    const float w = p2 / fma_(lp, lp, p2);
+                    out = fma3s(w, inf_le(l, rd) * att, out);
                 }
             }
             alive = false;
@@ -856,7 +855,9 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                 const pt_medium& M = S.media[med];
                 nee = true;
                 nee_medium = true;
-                out = out + att * ld3(M.Le);  // output += att * Le (Integrators.cpp:357)
+                // output += att * Le (Integrators.cpp:357) comes after SampleLd's
+                // term: the shadow record carries it (SHADOW_MLE_BIT), else below
+                (void)M;
                 si.p = mp;
             } else {
                 if (si.light >= 0) {
@@ -864,11 +865,11 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                     f3 Le = light_L(al, si.n, si.u, si.v, rd);
                     if (!is_zero(Le)) {
                         if (spec) {
-                            out = out + att * Le;
+                            out = fma3(att, Le, out);
                         } else if (prev > 0) {
-                            float lp = al.pmf * light_pdf(al, si.p, si.n, ro, rd);
-                            float w = prev * prev / (prev * prev + lp * lp);
-                            out = out + (att * Le) * w;
+                            const float lp = al.pmf * light_pdf(al, si.p, si.n, ro, rd), p2 = prev * prev;
+                            const float w = p2 / fma_(lp, lp, p2);
+                            out = fma3s(w, att * Le, out);
                         }
                     }
                 }
@@ -908,33 +909,34 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                         spdf = ok ? mat_pdf(si.mat, rd, si, sd) : 0.0f;
                         f = ok ? mat_f(si.mat, rd, si, sd) * fabsf(dt) : F3(0, 0, 0);
                     }
-                    f3 c;
                     if (ok && !is_zero(f)) {
+                        // the shadow kernel forms ((Tr * L) * f * w) / pdf
+                        f3 Ll;
+                        float wl = 1.0f;
                         if (light_is_delta(l)) {
-                            c = (ls.L * f) / lpdf;
+                            Ll = ls.L;
                         } else {
                             lpdf *= light_pdf(l, ls.p, ls.n, si.p, sd);
                             if (lpdf <= 0) {
                                 ok = false;
                             } else {
-                                float w2 = lpdf * lpdf;
-                                float w1 = spdf * spdf;
-                                float wl = w2 / (w1 + w2);
-                                c = ((light_L(l, ls.n, ls.u, ls.v, sd) * f) * wl) / lpdf;
+                                const float w2 = lpdf * lpdf;
+                                wl = w2 / fma_(spdf, spdf, w2);  // spdf*spdf + w2 fused
+                                Ll = light_L(l, ls.n, ls.u, ls.v, sd);
                             }
                         }
                         if (ok) {
-                            const f3 contrib = att * c;  // the shadow kernel multiplies Tr in
-                            if (!is_zero(contrib)) {
-                                shadow = true;
-                                srec.o = make_float4(si.p.x, si.p.y, si.p.z, tmax);
-                                srec.d = make_float4(sd.x, sd.y, sd.z, 0.0f);
-                                srec.c = make_float4(contrib.x, contrib.y, contrib.z, __int_as_float(med));
-                            }
+                            shadow = true;
+                            srec.o = make_float4(si.p.x, si.p.y, si.p.z, tmax);
+                            srec.d = make_float4(sd.x, sd.y, sd.z, __uint_as_float(nee_medium ? SHADOW_MLE_BIT : 0u));
+                            srec.L = make_float4(Ll.x, Ll.y, Ll.z, __int_as_float(med));
+                            srec.f = make_float4(f.x, f.y, f.z, wl);
+                            srec.a = make_float4(att.x, att.y, att.z, lpdf);
                         }
                     }
                 }
             }
+            if (mvalid && !shadow) out = fma3(att, ld3(S.media[med].Le), out);
             if (mvalid) {
                 // phase scattering (Integrators.cpp:358-361)
                 const f3 sc = phase_sample(S.media[med].g, rd, r[6], r[7]);
@@ -947,7 +949,7 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                 spec = false;
                 if (si.mat < 0) {
                     // medium boundary: pass through, no RR (Integrators.cpp:378-382)
-                    ro = ro + si.t * rd;
+                    ro = at_f(ro, rd, si.t);
                     med = get_medium(si, smed, rd);
                     do_rr = false;
                 } else if (!b.ok) {
@@ -999,7 +1001,7 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
         store_camera_path(next, a, ns, R.cam.medium);
     }
     if (shadow) {
-        srec.d.w = __uint_as_float(cont ? a : (SHADOW_DONE_BIT | sid));
+        srec.d.w = __uint_as_float((cont ? a : (SHADOW_DONE_BIT | sid)) | (__float_as_uint(srec.d.w) & SHADOW_MLE_BIT));
         sq[c] = srec;
     }
 }
@@ -1010,7 +1012,7 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
 // material occludes.  One ray per lane (media scenes are small).
 template <bool COUNT>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow_tr(PathSoA next, float* __restrict__ sample_L,
-                                                             const ShadowRec* __restrict__ sq,
+                                                             const ShadowRecV* __restrict__ sq,
                                                              const uint32_t* __restrict__ nptr,
                                                              unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
@@ -1020,10 +1022,11 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow_tr(PathSoA next, floa
     TraceWork wk{0, 0};
     uint32_t extra = 0;
     if (i < n) {
-        const ShadowRec r = sq[i];
+        const ShadowRecV r = sq[i];
         f3 o = xyz(r.o), d = xyz(r.d);
         float max = r.o.w;
-        int med = __float_as_int(r.c.w);
+        const int med0 = __float_as_int(r.L.w);
+        int med = med0;
         f3 Tr = F3(1, 1, 1);
         bool occluded = false;
         bool first = true;
@@ -1044,25 +1047,38 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow_tr(PathSoA next, floa
             SurfInt si;
             int smed;
             hit_surface(prim, o, d, t, b1, b2, si, smed);
-            o = o + t * d;
+            o = at_f(o, d, t);
             med = get_medium(si, smed, d);
             max -= t;
         }
-        if (!occluded) {
-            const f3 c = Tr * xyz(r.c);
-            const uint32_t tgt = __float_as_uint(r.d.w);
+        const uint32_t tgt = __float_as_uint(r.d.w);
+        const bool mle = (tgt & SHADOW_MLE_BIT) != 0;
+        if (!occluded || mle) {
+            // out = fma(att, ((Tr * L) * f * w) / pdf, out), then the medium's
+            // Le (Integrators.cpp:356-357) — SampleLd's term is 0 when occluded
+            const f3 att = xyz(r.a);
+            f3 v[2];
+            int nv = 0;
+            if (!occluded) v[nv++] = (((Tr * xyz(r.L)) * xyz(r.f)) * r.f.w) / r.a.w;
+            if (mle) v[nv++] = ld3(S.media[med0].Le);
+            float* L3;
+            float4* L4 = nullptr;
+            f3 out;
             if (tgt & SHADOW_DONE_BIT) {
-                float* L = sample_L + 3ull * (tgt & ~SHADOW_DONE_BIT);
-                L[0] += c.x;
-                L[1] += c.y;
-                L[2] += c.z;
+                L3 = sample_L + 3ull * (tgt & ~(SHADOW_DONE_BIT | SHADOW_MLE_BIT));
+                out = F3(L3[0], L3[1], L3[2]);
             } else {
-                float4* L = &next.L[tgt];
-                float4 v = *L;
-                v.x += c.x;
-                v.y += c.y;
-                v.z += c.z;
-                *L = v;
+                L4 = &next.L[tgt & ~SHADOW_MLE_BIT];
+                out = xyz(*L4);
+            }
+            for (int k = 0; k < nv; k++) out = fma3(att, v[k], out);
+            if (L4) {
+                const float4 w = *L4;
+                *L4 = make_float4(out.x, out.y, out.z, w.w);
+            } else {
+                L3[0] = out.x;
+                L3[1] = out.y;
+                L3[2] = out.z;
             }
         }
     }
@@ -1626,8 +1642,8 @@ PT_INST_POOL(false, false, true)
 PT_INST_POOL(true, false, true)
 PT_INST_POOL(false, true, true)
 PT_INST_POOL(true, true, true)
-template __global__ void k_shadow_tr<false>(PathSoA, float*, const ShadowRec*, const uint32_t*, unsigned long long*);
-template __global__ void k_shadow_tr<true>(PathSoA, float*, const ShadowRec*, const uint32_t*, unsigned long long*);
+template __global__ void k_shadow_tr<false>(PathSoA, float*, const ShadowRecV*, const uint32_t*, unsigned long long*);
+template __global__ void k_shadow_tr<true>(PathSoA, float*, const ShadowRecV*, const uint32_t*, unsigned long long*);
 template __global__ void k_shade<PT_INTEGRATOR_PATH>(RenderParams, PathSoA, const uint32_t*, const float4*, PathSoA,
                                                      float*, unsigned long long*, ShadowRec*, uint32_t*);
 template __global__ void k_shade<PT_INTEGRATOR_SIMPLE>(RenderParams, PathSoA, const uint32_t*, const float4*,

@@ -18,31 +18,42 @@ __device__ __forceinline__ uint32_t medium_bits(int m) {
     return (m < 0 ? PF_MED_NONE : (uint32_t)m) << PF_MED_SHIFT;
 }
 
-// phaseHG (PhaseFunction.hpp:4-8)
+// phaseHG (PhaseFunction.hpp:4-8) as built: 1 + g*g, + 2g*cos and 1 - g*g fused
 __device__ __forceinline__ float phase_hg(float cosT, float g) {
-    const float denom = 1 + g * g + 2 * g * cosT;
-    return 0.25f * (1.0f / PT_PI) * (1.0f - g * g) / (denom * csqrt(denom));
+    const float denom = fma_(cosT, 2.0f * g, fma_(g, g, 1.0f));
+    return fma_(-g, g, 1.0f) * (0.25f * (1.0f / PT_PI)) / (denom * csqrt(denom));
 }
 
 // HenyeyGreenstein::Sample (PhaseFunction.cpp:8-25): the scattered direction
 __device__ f3 phase_sample(float g, f3 in, float u0, float u1) {
     float cosT;
-    if (fabsf(g) < 1e-3f) {
+    if (fabs((double)g) < 1e-3) {
         cosT = 1 - 2 * u0;
     } else {
-        const float sqr = (1 - g * g) / (1 - g + 2 * g * u0);
-        cosT = (1 + g * g - sqr * sqr) / (2 * g);
+        const float sqr = fma_(-g, g, 1.0f) / fma_(2.0f * g, u0, 1 - g);
+        cosT = fma_(-sqr, sqr, fma_(g, g, 1.0f)) / (2 * g);
     }
-    const float sinT = csqrt(fmaxf(0.0f, 1 - cosT * cosT));
+    const float q = fma_(-cosT, cosT, 1.0f);
+    const float sinT = q > 0 ? csqrt(q) : 0.0f;
     const float phi = 2 * PT_PI * u1;
-    const Onb b = onb_n(in);
-    return normalize(to_world(b, F3(sinT * cos_cr(phi), sinT * sin_cr(phi), cosT)));
+    const float x = cos_cr(phi) * sinT, y = sin_cr(phi) * sinT, z = cosT;
+    // onb(in).toWorld as built here: a0 = cross(a1, a2) with the x, y lanes
+    // rounded-first; x, y lanes (x*a0 fused onto y*a1) + z*a2 unfused, z lane
+    // the usual chain
+    Onb b;
+    b.a2 = in;
+    const f3 up = (fabsf(in.x) > 0.9999) ? F3(0, 1, 0) : F3(1, 0, 0);
+    b.a1 = normalize(cross(b.a2, up));
+    b.a0 = cross_v(b.a1, b.a2);
+    const f3 w = F3(fma_(b.a0.x, x, y * b.a1.x) + z * b.a2.x, fma_(b.a0.y, x, y * b.a1.y) + z * b.a2.y,
+                    fma_(z, b.a2.z, fma_(y, b.a1.z, x * b.a0.z)));
+    return normalize(w);
 }
 
 // HomogeneusMedium::Tr (Medium.hpp:21-24): exp(-sigma_t * min(t, FLT_MAX))
 __device__ __forceinline__ f3 medium_tr(const pt_medium& m, float t) {
     const float tt = fminf(t, 3.402823466e38f);
-    return F3(expf(-m.sigma_t[0] * tt), expf(-m.sigma_t[1] * tt), expf(-m.sigma_t[2] * tt));
+    return F3(exp_cr(-m.sigma_t[0] * tt), exp_cr(-m.sigma_t[1] * tt), exp_cr(-m.sigma_t[2] * tt));
 }
 
 // HomogeneusMedium::Sample (Medium.hpp:26-45): returns the attenuation
@@ -55,11 +66,11 @@ __device__ f3 medium_sample(const pt_medium& m, f3 o, f3 d, float t, float u0, f
     sampled = sd < t;
     if (sampled) p = F3(fma_(sd, d.x, o.x), fma_(sd, d.y, o.y), fma_(sd, d.z, o.z));
     const f3 tr = medium_tr(m, sd);
-    const f3 den = sampled ? ld3(m.sigma_t) * tr : tr;
-    float pdf = 0;
-    pdf += den.x;
-    pdf += den.y;
-    pdf += den.z;
+    float pdf;
+    if (sampled)  // the sum of sigma_t*tr with the products fused
+        pdf = fma_(m.sigma_t[2], tr.z, fma_(m.sigma_t[1], tr.y, tr.x * m.sigma_t[0]));
+    else
+        pdf = ((0.0f + tr.x) + tr.y) + tr.z;
     pdf = (float)((double)pdf / 3.0);
     return sampled ? (tr * ld3(m.sigma_s)) / pdf : tr / pdf;
 }

@@ -841,7 +841,7 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
     }
     AL(c->hit, n * 16);
     AL(c->qcnt, (3 * SET_WORDS + PT_POOL_WORDS) * 4);  // three counter sets, then pt_trace's pool
-    AL(c->sq, n * sizeof(ShadowRec));
+    AL(c->sq, n * sizeof(ShadowRecV));  // the larger record (VolPath's)
     AL(c->counters, (CNT_SHARDS + 1) * CNT_COUNT * 8);
     // stack entries past the LDS part: the pool kernels' resident grid x
     // (PT_POOL_STACK - their smaller LDS part); the one-ray-per-lane kernels
@@ -995,10 +995,11 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     const uint64_t max_floats = (uint64_t)PT_SAMPLE_GIB << 28;
     uint64_t per_s = 3ull * R.npix_work;
     uint32_t s_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spp_local, max_floats / per_s));
-    // a chunk's sample ids stay below SHADOW_DONE_BIT: a finished path's
-    // pending shadow record carries SHADOW_DONE_BIT | sid (pt_kernels.hip)
-    if ((uint64_t)R.npix_work >= SHADOW_DONE_BIT) return fail(c, PT_ERR_ARG, "film too large for 31-bit sample ids");
-    s_chunk = (uint32_t)std::min<uint64_t>(s_chunk, (SHADOW_DONE_BIT - 1ull) / R.npix_work);
+    // a chunk's sample ids stay below SHADOW_MLE_BIT: a finished path's
+    // pending shadow record carries [SHADOW_MLE_BIT |] SHADOW_DONE_BIT | sid
+    // (pt_kernels.hip)
+    if ((uint64_t)R.npix_work >= SHADOW_MLE_BIT) return fail(c, PT_ERR_ARG, "film too large for 30-bit sample ids");
+    s_chunk = (uint32_t)std::min<uint64_t>(s_chunk, (SHADOW_MLE_BIT - 1ull) / R.npix_work);
     pt_status st;
     // a device with less free HBM (or a second context on it) gets smaller
     // chunks instead of PT_ERR_OOM
@@ -1185,7 +1186,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                                    next_sample, c->sq, out);
             else if (rd->integrator == PT_INTEGRATOR_VOLPATH)
                 hipLaunchKernelGGL(k_shade_vol, gs, dim3(256), 0, sm, R, cur, (const uint32_t*)(in + Q_NEXT),
-                                   (const float4*)c->hit, nxt, c->sample_L, next_sample, c->sq, out);
+                                   (const float4*)c->hit, nxt, c->sample_L, next_sample, (ShadowRecV*)c->sq, out);
             else
                 hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_PATH>, gsh, dim3(PT_SHADE_BLOCK), 0, sm, R, cur,
                                    (const uint32_t*)(in + Q_NEXT), (const float4*)c->hit, nxt, c->sample_L,
@@ -1195,7 +1196,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                 // transmittance along the shadow rays: one ray per lane, the grid covers the capacity
                 hipLaunchKernelGGL(count ? k_shadow_tr<true> : k_shadow_tr<false>,
                                    dim3((nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK), dim3(PT_TRACE_BLOCK), 0, sm,
-                                   nxt, c->sample_L, (const ShadowRec*)c->sq, (const uint32_t*)(out + Q_SHADOW),
+                                   nxt, c->sample_L, (const ShadowRecV*)c->sq, (const uint32_t*)(out + Q_SHADOW),
                                    c->counters);
             } else if (rd->integrator != PT_INTEGRATOR_SIMPLE) {
                 auto ks = pick_shadow(use_pool, qn, inst, count);

@@ -207,15 +207,15 @@ __device__ f3 normal_map(int mid, const SurfInt& si) {
     return to_world_nm(onb_si(si), nn);
 }
 
-__device__ __forceinline__ void sphere_uv(f3 p, float& u, float& v) {
-    // SphereShape::GetSphereUV (Shape.hpp:35-43)
-    p = normalize(p);
-    float theta = acosf(clampf(p.y, -1.0f, 1.0f));
-    float phi = atan2f(p.z, p.x);
+// SphereShape::GetSphereUV (Shape.hpp:35-43) after its normalisation
+__device__ __forceinline__ void sphere_uv_n(f3 p, float& u, float& v) {
+    float theta = pt_acosf(clampf(p.y, -1.0f, 1.0f));
+    float phi = pt_atan2f(p.z, p.x);
     if (phi < 0) phi += 2.0f * PT_PI;
     u = PT_INV_PI * phi * 0.5f;
     v = PT_INV_PI * theta;
 }
+__device__ __forceinline__ void sphere_uv(f3 p, float& u, float& v) { sphere_uv_n(normalize(p), u, v); }
 
 // ------------------------------------------------------------------ interaction reconstruction
 // TriangleShape::Intersect shading part (Shape.cpp:206-242) from the hit's
@@ -268,19 +268,19 @@ __device__ void quad_interaction(const pt_quad& q, f3 o, f3 d, float t, float a,
     si.n = normal;
     f3 up = (fabsf(si.ns.x) > 0.9999f) ? F3(0, 1, 0) : F3(1, 0, 0);
     si.tangent = normalize(cross(up, si.ns));
-    const f3 at = F3(fma_(t, d.x, o.x), fma_(t, d.y, o.y), fma_(t, d.z, o.z));  // ray.at: fused (fixture search)
-    si.p = at + PT_EPS * nn;
+    const f3 at = at_f(o, d, t);  // as built: x, y lanes + eps*nn unfused, z lane fused
+    si.p = F3(at.x + PT_EPS * nn.x, at.y + PT_EPS * nn.y, fma_(nn.z, PT_EPS, at.z));
 }
 
 // SphereShape::Intersect (Shape.cpp:3-37) interaction part.
 __device__ void sphere_interaction(const pt_sphere& sp, f3 o, f3 d, float t, SurfInt& si) {
     si.t = t;
-    const f3 at = F3(fma_(t, d.x, o.x), fma_(t, d.y, o.y), fma_(t, d.z, o.z));  // ray.at: fused (fixture search)
+    const f3 at = at_f(o, d, t);
     si.ns = normalize(at - ld3(sp.center));
     si.n = si.ns;
     f3 up = (fabsf(si.ns.x) > 0.9999f) ? F3(0, 1, 0) : F3(1, 0, 0);
     si.tangent = normalize(cross(up, si.ns));
-    si.p = at + PT_EPS * si.n;
+    si.p = F3(fma_(si.n.x, PT_EPS, at.x), fma_(si.n.y, PT_EPS, at.y), fma_(si.n.z, PT_EPS, at.z));  // fused (as built)
     sphere_uv(si.n, si.u, si.v);
 }
 
@@ -296,7 +296,9 @@ __device__ float lambda_(const Dist& D, f3 w) {
     float sinT = csqrt(sin2);
     float cosPhi = sinT == 0 ? 1 : clampf(w.x / sinT, -1.0f, 1.0f);
     float sinPhi = sinT == 0 ? 0 : clampf(w.y / sinT, -1.0f, 1.0f);
-    float alpha2 = (cosPhi * D.ax) * (cosPhi * D.ax) + (sinPhi * D.ay) * (sinPhi * D.ay);
+    // Material.hpp:66 as built: fma(cosPhi*ax, cosPhi*ax, (sinPhi*ay)^2)
+    const float ca = cosPhi * D.ax, sa = sinPhi * D.ay;
+    float alpha2 = fma_(ca, ca, sa * sa);
     return (csqrt(1.f + alpha2 * sin2 / cos2) - 1.0f) / 2.0f;
 }
 __device__ float D_(const Dist& D, f3 wh) {
@@ -307,34 +309,50 @@ __device__ float D_(const Dist& D, f3 wh) {
     float sinT = csqrt(sin2);
     float cosPhi = sinT == 0 ? 1 : clampf(wh.x / sinT, -1.0f, 1.0f);
     float sinPhi = sinT == 0 ? 0 : clampf(wh.y / sinT, -1.0f, 1.0f);
-    float e = sin2 / cos2 * ((cosPhi / D.ax) * (cosPhi / D.ax) + (sinPhi / D.ay) * (sinPhi / D.ay));
-    float denom = PT_PI * D.ax * D.ay * cos4 * (1 + e) * (1 + e);
+    // Material.hpp:78-79 as built: the sum of squares fused and 1 + e fused
+    // into one fma(sin2/cos2, sum, 1)
+    const float cx = cosPhi / D.ax, sy = sinPhi / D.ay;
+    const float e1 = fma_(sin2 / cos2, fma_(cx, cx, sy * sy), 1.0f);
+    float denom = PT_PI * D.ax * D.ay * cos4 * e1 * e1;
     if (denom <= 0) return __int_as_float(0x7f800000);
     return 1 / denom;
 }
 __device__ __forceinline__ float G1_(const Dist& D, f3 w) { return 1 / (1 + lambda_(D, w)); }
 __device__ __forceinline__ float G_(const Dist& D, f3 wo, f3 wi) { return 1 / (1 + lambda_(D, wo) + lambda_(D, wi)); }
 __device__ __forceinline__ bool smooth_(const Dist& D) { return smax(D.ax, D.ay) < 1e-6; }
-__device__ __forceinline__ float mpdf_(const Dist& D, f3 wo, f3 wh) {
-    return D_(D, wh) * G1_(D, wo) * fabsf(dot(wo, wh) / wo.z);
+// MicrofacetDistribution::PDF with the caller's dot(wo, wh) (its order differs by call site)
+__device__ __forceinline__ float mpdf_(const Dist& D, f3 wo, f3 wh, float dwh) {
+    return D_(D, wh) * G1_(D, wo) * fabsf(dwh / wo.z);
 }
+// sampleGGXVNDF (Material.hpp:119-139) with the reference build's
+// contractions; NE_INLINE: MicrofacetDielectric::scatter's inlined final
+// normalisation (z^2 added unfused) instead of the out-of-line one
+template <bool NE_INLINE>
 __device__ f3 vndf_(float ax, float ay, f3 Ve, float U1, float U2) {
     f3 Vh = normalize(F3(ax * Ve.x, ay * Ve.y, Ve.z));
-    float lensq = Vh.x * Vh.x + Vh.y * Vh.y;
+    float lensq = fma_(Vh.x, Vh.x, Vh.y * Vh.y);
     f3 T1 = lensq > 0 ? F3(-Vh.y, Vh.x, 0) * (1.0f / csqrt(lensq)) : F3(1, 0, 0);
-    f3 T2 = cross(Vh, T1);
+    f3 T2 = cross_v(Vh, T1);
     float r = csqrt(U1);
     float phi = 2.0f * PT_PI * U2;
     float t1 = r * cos_cr(phi);
     float t2 = r * sin_cr(phi);
     float s = 0.5f * (1.0f + Vh.z);
-    t2 = (1.0f - s) * csqrt(1.0f - t1 * t1) + s * t2;
-    f3 Nh = t1 * T1 + t2 * T2 + csqrt(smax(0.0f, 1.0f - t1 * t1 - t2 * t2)) * Vh;
-    return normalize(F3(ax * Nh.x, ay * Nh.y, smax(0.0f, Nh.z)));
+    const float q1 = fma_(-t1, t1, 1.0f);  // 1 - t1*t1
+    t2 = fma_(1.0f - s, csqrt(q1), s * t2);
+    const float sq = csqrt(smax(0.0f, fma_(-t2, t2, q1)));
+    // x, y lanes: t2*T2 rounded, t1*T1 fused; z lane: t1*T1 rounded, t2*T2 fused
+    f3 Nh = F3(fma_(sq, Vh.x, fma_(t1, T1.x, t2 * T2.x)), fma_(sq, Vh.y, fma_(t1, T1.y, t2 * T2.y)),
+               fma_(sq, Vh.z, fma_(t2, T2.z, t1 * T1.z)));
+    const f3 ne = F3(ax * Nh.x, ay * Nh.y, smax(0.0f, Nh.z));
+    if (!NE_INLINE) return normalize(ne);
+    const float zz = Nh.z > 0 ? ne.z * ne.z : 0.0f;
+    return ne * (1.0f / csqrt(fma_(ne.y, ne.y, ne.x * ne.x) + zz));
 }
+template <bool NE_INLINE>
 __device__ __forceinline__ f3 sample_wh(const Dist& D, f3 wo, float u0, float u1) {
     bool flip = wo.z < 0;
-    f3 wh = vndf_(D.ax, D.ay, flip ? -wo : wo, u0, u1);
+    f3 wh = vndf_<NE_INLINE>(D.ax, D.ay, flip ? -wo : wo, u0, u1);
     return flip ? -wh : wh;
 }
 __device__ float fresnel_dielectric(float cosi, float eta) {  // Material.hpp:11-28
@@ -343,17 +361,18 @@ __device__ float fresnel_dielectric(float cosi, float eta) {  // Material.hpp:11
         eta = 1 / eta;
         cosi = -cosi;
     }
-    float sin2i = 1 - cosi * cosi;
+    // as built: 1 - cos^2, eta*cos -+ cost, cos -+ eta*cost and the sum of squares fused
+    float sin2i = fma_(-cosi, cosi, 1.0f);
     float sin2t = sin2i / (eta * eta);
     if (sin2t >= 1) return 1.f;
     float cost = csqrt(1 - sin2t);
-    float rpa = (eta * cosi - cost) / (eta * cosi + cost);
-    float rpe = (cosi - eta * cost) / (cosi + eta * cost);
-    return (rpa * rpa + rpe * rpe) / 2;
+    float rpa = fma_(cosi, eta, -cost) / fma_(cosi, eta, cost);
+    float rpe = fma_(-eta, cost, cosi) / fma_(eta, cost, cosi);
+    return fma_(rpa, rpa, rpe * rpe) * 0.5f;
 }
-__device__ __forceinline__ f3 schlick(float c, f3 F0) {  // Material.hpp:30-32
+__device__ __forceinline__ f3 schlick(float c, f3 F0) {  // Material.hpp:30-32, F0 + (1 - F0)*p fused
     float p = pow_cr(1.0f - c, 5.0f);
-    return F0 + (F3(1, 1, 1) - F0) * p;
+    return F3(fma_(p, 1.0f - F0.x, F0.x), fma_(p, 1.0f - F0.y, F0.y), fma_(p, 1.0f - F0.z, F0.z));
 }
 
 // ------------------------------------------------------------------ materials
@@ -369,7 +388,15 @@ struct Bxdf {
 __device__ __forceinline__ float diffuse_rough(const pt_material& m, const SurfInt& si) {
     return smax(tex_eval(m.rough, si.u, si.v).y, 0.0001f);
 }
-__device__ __forceinline__ f3 mixv(f3 x, f3 y, float a) { return x * (1.0f - a) + y * a; }
+// onb TBN(dot(d, ns) > 0 ? -ns : ns) and wo = TBN.toLocal(-d) as
+// MicrofacetDiffuse's three entry points are built: the sign test is the
+// unfused dot and wo.z reuses it (+-dot(d, ns))
+__device__ __forceinline__ f3 diffuse_frame(f3 d, f3 ns, Onb& tbn) {
+    const float pd = dot_p(d, ns);
+    tbn = onb_n(pd > 0 ? -ns : ns);
+    const f3 md = -d;
+    return F3(dot(md, tbn.a0), dot(md, tbn.a1), pd > 0 ? pd : -pd);
+}
 
 // MicrofacetDiffuse::scatter (Material.hpp:206-266)
 __device__ Bxdf diffuse_scatter(const pt_material& m, f3 ind, const SurfInt& si, float u,
@@ -377,13 +404,13 @@ __device__ Bxdf diffuse_scatter(const pt_material& m, f3 ind, const SurfInt& si,
     Bxdf b;
     b.ok = false;
     float rough = diffuse_rough(m, si);
-    Onb tbn = onb_n(dot(ind, si.ns) > 0 ? -si.ns : si.ns);
     Dist D = mkdist(rough);
     float prob = rough >= 0.7 ? 1.0f : 0.5f;
-    f3 wo = to_local(tbn, -ind);
+    Onb tbn;
+    f3 wo = diffuse_frame(ind, si.ns, tbn);
     f3 wi, wh;
     if (u >= prob) {
-        wh = sample_wh(D, wo, uv0, uv1);
+        wh = sample_wh<false>(D, wo, uv0, uv1);
         wi = reflect(-wo, wh);
     } else {
         float z = csqrt(1.0f - uv1);
@@ -393,20 +420,22 @@ __device__ Bxdf diffuse_scatter(const pt_material& m, f3 ind, const SurfInt& si,
         wh = normalize(wo + wi);
     }
     if (wi.z <= 0) return b;
-    float dpdf = prob * wi.z * PT_INV_PI;
-    float spdf = (1.0f - prob) * mpdf_(D, wo, wh) / (4 * fabsf(dot(wo, wh)));
-    float pdf = dpdf + spdf;
+    // as built: dot(wo, wh) in y, x, z order; prob*wi.z*inv_pi + spdf fused
+    const float dwh = dot_yxz(wo, wh);
+    float spdf = (1.0f - prob) * mpdf_(D, wo, wh, dwh) / (4 * fabsf(dwh));
+    float pdf = fma_(prob * wi.z, PT_INV_PI, spdf);
     f3 col = tex_eval(m.tex, si.u, si.v);
     float metal = tex_eval(m.metal, si.u, si.v).z;
-    f3 F0 = mixv(F3(0.04f, 0.04f, 0.04f), col, metal);
-    f3 F = schlick(dot(wi, wh), F0);
+    // glm::mix(0.04, col, metal) as built here: col*metal rounded, the other fused
+    const float om = 1.0f - metal;
+    f3 F0 = F3(fma_(om, 0.04f, col.x * metal), fma_(om, 0.04f, col.y * metal), fma_(om, 0.04f, col.z * metal));
+    f3 F = schlick(dot_yxz(wi, wh), F0);
     f3 num = (D_(D, wh) * G_(D, wo, wi)) * F;
     float den = fabsf(4.0f * wo.z * wi.z);
     if (den == 0) return b;
     f3 spec = num / den;
-    f3 kD = (F3(1, 1, 1) - F) * (1.0f - metal);
-    f3 diff = (kD * col) * PT_INV_PI;
-    b.f = diff + spec;
+    f3 kc = ((F3(1, 1, 1) - F) * om) * col;
+    b.f = fma3s(PT_INV_PI, kc, spec);
     b.pdf = pdf;
     b.flags = 0;
     b.o = si.p;
@@ -416,36 +445,42 @@ __device__ Bxdf diffuse_scatter(const pt_material& m, f3 ind, const SurfInt& si,
 }
 // MicrofacetDiffuse::calc_attenuation (Material.hpp:299-326)
 __device__ f3 diffuse_f(const pt_material& m, f3 ind, const SurfInt& si, f3 dir) {
-    Onb tbn = onb_n(dot(ind, si.ns) > 0 ? -si.ns : si.ns);
-    f3 wo = to_local(tbn, -ind);
+    Onb tbn;
+    f3 wo = diffuse_frame(ind, si.ns, tbn);
     f3 wi = to_local(tbn, dir);
     f3 wh = normalize(wo + wi);
     float rough = diffuse_rough(m, si);
     float metal = tex_eval(m.metal, si.u, si.v).z;
     Dist D = mkdist(rough);
     f3 col = tex_eval(m.tex, si.u, si.v);
-    f3 F0 = mixv(F3(0.04f, 0.04f, 0.04f), col, metal);
-    f3 F = schlick(dot(wi, wh), F0);
+    // glm::mix as built here: (1-metal)*0.04 rounded, col*metal fused
+    const float om = 1.0f - metal, c4 = om * 0.04f;
+    f3 F0 = F3(fma_(col.x, metal, c4), fma_(col.y, metal, c4), fma_(col.z, metal, c4));
+    f3 F = schlick(dot_yxz(wi, wh), F0);
     f3 num = (D_(D, wh) * G_(D, wo, wi)) * F;
     float den = fabsf(4.0f * wo.z * wi.z);
     if (den == 0) return F3(0, 0, 0);
-    f3 kD = (F3(1, 1, 1) - F) * (1.0f - metal);
-    return (kD * col) * PT_INV_PI + num / den;
+    const f3 kc = ((F3(1, 1, 1) - F) * om) * col;
+    return fma3s(PT_INV_PI, kc, num / den);
 }
 // MicrofacetDiffuse::PDF (Material.hpp:281-296): no (1-prob) on the specular term (A.7)
 __device__ float diffuse_pdf(const pt_material& m, f3 ind, const SurfInt& si, f3 dir) {
     float rough = diffuse_rough(m, si);
     Dist D = mkdist(rough);
-    Onb tbn = onb_n(dot(ind, si.ns) > 0 ? -si.ns : si.ns);
-    f3 wo = to_local(tbn, -ind);
+    Onb tbn;
+    f3 wo = diffuse_frame(ind, si.ns, tbn);
     f3 wh = to_local(tbn, normalize(dir - ind));
     float prob = rough >= 0.7 ? 1.0f : 0.5f;
     float diff = prob * fabsf(dot(si.ns, dir)) * PT_INV_PI;
-    float spec = mpdf_(D, wo, wh) / (4 * fabsf(dot(wo, wh)));
+    const float dwh = dot(wo, wh);
+    float spec = mpdf_(D, wo, wh, dwh) / (4 * fabsf(dwh));
     return diff + spec;
 }
 
-// MicrofacetDielectric::scatter (Material.hpp:392-477)
+// the out-of-line onb::toLocal (the dielectric's calls): x, y lanes in y, x, z order
+__device__ __forceinline__ f3 to_local_ool(const Onb& b, f3 v) { return F3(dot_yxz(v, b.a0), dot_yxz(v, b.a1), dot(v, b.a2)); }
+
+// MicrofacetDielectric::scatter (Material.hpp:392-477), contractions as built
 __device__ Bxdf dielectric_scatter(const pt_material& m, f3 ino, f3 ind, const SurfInt& si,
                                    float u, float uv0, float uv1) {
     Bxdf b;
@@ -453,25 +488,26 @@ __device__ Bxdf dielectric_scatter(const pt_material& m, f3 ino, f3 ind, const S
     float rough = tex_eval(m.rough, si.u, si.v).y;
     Dist D = mkdist(rough);
     Onb tbn = onb_si(si);
-    f3 wo = to_local(tbn, -ind);
+    const f3 md = -ind;
+    f3 wo = to_local_ool(tbn, md);
     float ri = m.ri;
-    float eta = dot(-ind, si.ns) > 0 ? 1 / ri : ri;
-    f3 hitp = ino + si.t * ind;
+    float eta = dot_p(md, si.ns) > 0 ? 1 / ri : ri;
+    const f3 hitp = at_f(ino, ind, si.t);
     if (ri == 1 || smooth_(D)) {
-        f3 N = dot(ind, si.ns) > 0 ? -si.ns : si.ns;
+        f3 N = dot_p(ind, si.ns) > 0 ? -si.ns : si.ns;
         f3 Ng = dot(ind, si.n) > 0 ? -si.n : si.n;
         float F = fresnel_dielectric(wo.z, ri);
         float R = F, T = 1.0f - R;
         f3 dir;
         if (u < (R / (R + T))) {
             dir = to_world(tbn, F3(-wo.x, -wo.y, wo.z));
-            b.o = hitp + PT_EPS * Ng;
+            b.o = F3(hitp.x + PT_EPS * Ng.x, hitp.y + PT_EPS * Ng.y, fma_(Ng.z, PT_EPS, hitp.z));
             b.f = (tex_eval(m.tex, si.u, si.v) * R) / fabsf(dot(si.ns, dir));
             b.pdf = R / (R + T);
         } else {
-            dir = refract(ind, N, eta);
+            dir = refract_f(ind, N, eta, dot(ind, N));
             if (is_zero(dir)) return b;
-            b.o = hitp - PT_EPS * Ng;
+            b.o = F3(hitp.x - PT_EPS * Ng.x, hitp.y - PT_EPS * Ng.y, fma_(-Ng.z, PT_EPS, hitp.z));
             b.f = (tex_eval(m.tex, si.u, si.v) * T) / fabsf(dot(si.ns, dir));
             b.pdf = T / (R + T);
         }
@@ -480,87 +516,119 @@ __device__ Bxdf dielectric_scatter(const pt_material& m, f3 ino, f3 ind, const S
         b.ok = true;
         return b;
     }
-    f3 wh = sample_wh(D, wo, uv0, uv1);
+    f3 wh = sample_wh<true>(D, wo, uv0, uv1);
     f3 Ng = dot(ind, si.n) > 0 ? -si.n : si.n;
-    float F = fresnel_dielectric(dot(wo, wh), 1 / eta);
+    const float dow = dot_p(wo, wh);  // dot(wo, wh), unfused, shared by every use below
+    float F = fresnel_dielectric(dow, 1 / eta);
     float R = F, T = 1 - R;
     uint32_t fl = FL_TRANS | (rough < 0.001f ? FL_SPEC : 0u);
     if (u < (R / (R + T))) {
-        f3 wi = reflect(-wo, wh);
+        f3 wi = -wo - (wh * (-dow)) * 2.0f;
         if (wo.z * wi.z < 0) return b;
-        b.o = hitp + PT_EPS * Ng;
+        b.o = F3(hitp.x + PT_EPS * Ng.x, hitp.y + PT_EPS * Ng.y, fma_(Ng.z, PT_EPS, hitp.z));
         b.d = to_world(tbn, wi);
-        b.pdf = mpdf_(D, wo, wh) / (4 * fabsf(dot(wo, wh))) * R / (R + T);
+        b.pdf = mpdf_(D, wo, wh, dot(wo, wh)) / (fabsf(dow) * 4) * R / (R + T);
         b.f = (((tex_eval(m.tex, si.u, si.v) * D_(D, wh)) * G_(D, wo, wi)) * R) / fabsf(4 * wi.z * wo.z);
     } else {
-        f3 wi = refract(-wo, wh, eta);
+        f3 wi = refract_f(-wo, wh, eta, -dow);
         if (wo.z * wi.z > 0 || wi.z == 0) return b;
-        b.o = hitp - PT_EPS * Ng;
+        b.o = F3(hitp.x - PT_EPS * Ng.x, hitp.y - PT_EPS * Ng.y, fma_(-Ng.z, PT_EPS, hitp.z));
         b.d = to_world(tbn, wi);
-        float denom = (dot(wi, wh) + dot(wo, wh) * eta) * (dot(wi, wh) + dot(wo, wh) * eta);
-        float dwh = fabsf(dot(wi, wh)) / denom;
-        b.pdf = mpdf_(D, wo, wh) * dwh * T / (R + T);
-        float ft = T * D_(D, wh) * G_(D, wo, wi) * fabsf(dot(wi, wh) * dot(wo, wh) / (denom * wi.z * wo.z));
+        const float diw = dot(wi, wh);
+        const float dn = fma_(eta, dow, diw);
+        float denom = dn * dn;
+        float dwh = fabsf(diw) / denom;
+        b.pdf = mpdf_(D, wo, wh, dot(wo, wh)) * dwh * T / (R + T);
+        float ft = T * D_(D, wh) * G_(D, wo, wi) * fabsf(diw * dow / (denom * wi.z * wo.z));
         b.f = tex_eval(m.tex, si.u, si.v) * ft;
     }
     b.flags = fl;
     b.ok = true;
     return b;
 }
-// MicrofacetDielectric::PDF / calc_attenuation (Material.hpp:484-564)
+// MicrofacetDielectric::PDF / calc_attenuation (Material.hpp:484-564): each
+// builds its own half vector, wi*etap + wo unfused in PDF and with the x, y
+// lanes fused in calc_attenuation
+template <bool FOR_F>
+__device__ __forceinline__ bool dielectric_frame(const pt_material& m, f3 ind, const SurfInt& si, f3 dir, Dist& D,
+                                                 f3& wo, f3& wi, f3& wh, float& etap, bool& refl) {
+    float rough = tex_eval(m.rough, si.u, si.v).y;
+    D = mkdist(rough);
+    float ri = m.ri;
+    if (ri == 1 || smooth_(D)) return false;
+    Onb tbn = onb_si(si);
+    wo = to_local_ool(tbn, -ind);
+    wi = to_local_ool(tbn, dir);
+    float co = wo.z, ci = wi.z;
+    refl = ci * co > 0;
+    etap = 1;
+    if (!refl) etap = co > 0 ? ri : (1 / ri);
+    f3 h = (FOR_F && !refl) ? F3(fma_(wi.x, etap, wo.x), fma_(wi.y, etap, wo.y), co + ci * etap) : wi * etap + wo;
+    if (dot(h, h) == 0) return false;
+    h = normalize(h);
+    if (h.z < 0) h = -h;
+    wh = h;
+    if (dot(h, wi) * ci <= 0.0 || dot(h, wo) * co <= 0.0) return false;
+    return true;
+}
 __device__ void dielectric_eval(const pt_material& m, f3 ind, const SurfInt& si, f3 dir,
                                 f3& f_out, float& pdf_out) {
     f_out = F3(0, 0, 0);
     pdf_out = 0;
-    float rough = tex_eval(m.rough, si.u, si.v).y;
-    Dist D = mkdist(rough);
-    float ri = m.ri;
-    if (ri == 1 || smooth_(D)) return;
-    Onb tbn = onb_si(si);
-    f3 wo = to_local(tbn, -ind);
-    f3 wi = to_local(tbn, dir);
-    float co = wo.z, ci = wi.z;
-    bool refl = ci * co > 0;
-    float etap = 1;
-    if (!refl) etap = co > 0 ? ri : (1 / ri);
-    f3 wh = wi * etap + wo;
-    if (dot(wh, wh) == 0) return;
-    wh = normalize(wh);
-    if (wh.z < 0) wh = -wh;
-    if (dot(wh, wi) * ci <= 0.0 || dot(wh, wo) * co <= 0.0) return;
-    float F = fresnel_dielectric(dot(wo, wh), ri);
-    float R = F, T = 1 - R;
-    float pdf = mpdf_(D, wo, wh);
-    f3 col = tex_eval(m.tex, si.u, si.v);
-    if (refl) {
-        pdf_out = pdf / (4 * fabsf(dot(wo, wh))) * R / (R + T);
-        f_out = (((col * D_(D, wh)) * G_(D, wo, wi)) * F) / fabsf(4 * ci * co);
-    } else {
-        float den = (dot(wi, wh) + dot(wo, wh) / etap) * (dot(wi, wh) + dot(wo, wh) / etap);
-        float dwh = fabsf(dot(wi, wh)) / den;
-        pdf_out = pdf * dwh * T / (R + T);
-        float den2 = (dot(wi, wh) + dot(wo, wh) / etap) * (dot(wi, wh) + dot(wo, wh) / etap) * ci * co;
-        float ft = D_(D, wh) * (1 - F) * G_(D, wo, wi) * fabsf(dot(wi, wh) * dot(wo, wh) / den2);
-        f_out = col * ft;
+    Dist D;
+    f3 wo, wi, wh;
+    float etap;
+    bool refl;
+    if (dielectric_frame<false>(m, ind, si, dir, D, wo, wi, wh, etap, refl)) {
+        const float dow = dot(wh, wo), diw = dot(wh, wi);
+        float F = fresnel_dielectric(dow, m.ri);
+        float R = F, T = 1 - R;
+        float pdf = mpdf_(D, wo, wh, dow);
+        if (refl) {
+            pdf_out = pdf / (fabsf(dow) * 4) * R / (R + T);
+        } else {
+            const float dn = dow / etap + diw;
+            float dwh = fabsf(diw) / (dn * dn);
+            pdf_out = dwh * pdf * T / (R + T);
+        }
+    }
+    if (dielectric_frame<true>(m, ind, si, dir, D, wo, wi, wh, etap, refl)) {
+        const float dow = dot(wh, wo), diw = dot(wh, wi);
+        float F = fresnel_dielectric(dow, m.ri);
+        f3 col = tex_eval(m.tex, si.u, si.v);
+        if (refl) {
+            f_out = (((col * D_(D, wh)) * G_(D, wo, wi)) * F) / fabsf(4 * wi.z * wo.z);
+        } else {
+            const float dn = dow / etap + diw;
+            float den2 = dn * dn * wi.z * wo.z;
+            float ft = (1 - F) * D_(D, wh) * G_(D, wo, wi) * fabsf(diw * dow / den2);
+            f_out = col * ft;
+        }
     }
 }
 // ThinDielectric::scatter (Material.hpp:605-644)
 __device__ Bxdf thin_scatter(const pt_material& m, f3 ino, f3 ind, const SurfInt& si, float u) {
     Bxdf b;
-    Onb tbn = onb_si(si);
-    f3 wo = to_local(tbn, -ind);
+    // as built: onb(si)'s cross rounded-first in every lane, wo.x and wo.y in
+    // y, x, z order, 1 - R*R fused, hit point fused, +-eps*Ng unfused
+    Onb tbn;
+    tbn.a2 = si.ns;
+    tbn.a0 = si.tangent;
+    tbn.a1 = cross_r(tbn.a2, tbn.a0);
+    const f3 md = -ind;
+    f3 wo = F3(dot_yxz(md, tbn.a0), dot_yxz(md, tbn.a1), dot(md, tbn.a2));
     f3 Ng = dot(ind, si.n) > 0 ? -si.n : si.n;
     float F = fresnel_dielectric(wo.z, m.ri);
     float R = F, T = 1.0f - R;
     if (R < 1.0f) {
-        R += T * T * R / (1.0f - R * R);
+        R += T * T * R / fma_(-R, R, 1.0f);
         T = 1.0f - R;
     }
-    f3 hitp = ino + si.t * ind;
+    const f3 hitp = at_f(ino, ind, si.t);
     f3 dir, f;
     if (u < (R / (R + T))) {
         dir = to_world(tbn, F3(-wo.x, -wo.y, wo.z));
-        b.o = hitp + PT_EPS * Ng;
+        b.o = PT_EPS * Ng + hitp;
         f = (F3(1, 1, 1) * R) / fabsf(dot(si.ns, dir));
         b.pdf = R / (R + T);
     } else {
@@ -680,7 +748,7 @@ __device__ __forceinline__ uint4 tri_idx(uint32_t tri) { return S.tri[tri]; }
 __device__ float shape_area(uint32_t kind, uint32_t index) {
     if (kind == PT_PRIM_QUAD) {
         const pt_quad& q = S.quads[index];
-        return length(cross_r(ld3(q.u), ld3(q.v)));  // QuadShape::Area as compiled (fixture search)
+        return length(cross(ld3(q.u), ld3(q.v)));
     }
     if (kind == PT_PRIM_SPHERE) {
         float r = S.spheres[index].radius;
@@ -696,7 +764,9 @@ __device__ void shape_sample(uint32_t kind, uint32_t index, float u0, float u1, 
     ls.v = 0;
     if (kind == PT_PRIM_QUAD) {
         const pt_quad& q = S.quads[index];
-        ls.p = ld3(q.Q) + u0 * ld3(q.u) + u1 * ld3(q.v);
+        const f3 Q = ld3(q.Q), qu = ld3(q.u), qv = ld3(q.v);  // Q + u0*u + u1*v, both fused
+        ls.p = F3(fma_(qv.x, u1, fma_(qu.x, u0, Q.x)), fma_(qv.y, u1, fma_(qu.y, u0, Q.y)),
+                  fma_(qv.z, u1, fma_(qu.z, u0, Q.z)));
         ls.n = ld3(q.normal);
     } else if (kind == PT_PRIM_SPHERE) {
         const pt_sphere& sp = S.spheres[index];
@@ -723,11 +793,13 @@ __device__ void shape_sample(uint32_t kind, uint32_t index, float u0, float u1, 
     }
 }
 // Shape::PDF(interaction, ray) (Shape.cpp:61-67, 303-315; Shape.hpp:151-158)
-__device__ float shape_pdf(uint32_t kind, uint32_t index, f3 p, f3 n, f3 ro, f3 rd) {
+// as built: dot(to, to) in y, x, z order; the quad's (inlined into
+// AreaLight::PDF) light cosine also in y, x, z order except behind the
+// one-sided test, whose dot(-d, n) it reuses
+__device__ float shape_pdf(uint32_t kind, uint32_t index, f3 p, f3 n, f3 ro, f3 rd, bool one_sided) {
     f3 to = p - ro;
-    // Shape::PDF's dot(to, to): x product fused, y rounded (fixture search)
-    float d2 = fma_(to.z, to.z, fma_(to.x, to.x, rmul(to.y, to.y)));
-    float lc = fabsf(dot(-rd, n));
+    float d2 = dot_yxz(to, to);
+    float lc = fabsf(kind == PT_PRIM_QUAD && !one_sided ? dot_yxz(-rd, n) : dot(-rd, n));
     float area = shape_area(kind, index);
     if (kind == PT_PRIM_QUAD) {
         if (area == 0) return 0;
@@ -863,19 +935,28 @@ __device__ __forceinline__ LSample light_sample(const pt_light& l, float u0, flo
         ls.v = o.v;
         return ls;
     }
+    // Distant / Uniform / Function light sample (Light.cpp:36-41, 62-67, 209-214):
+    // 1 - z*z fused except in FunctionInfiniteLight::sample, which also adds
+    // z*z unfused in its GetSphereUV normalisation
+    const bool sky = l.kind == PT_LIGHT_SKY_INF;
     float z = 2.0f * u0 - 1.0f;
     float th = 2.0f * PT_PI * u1;
-    float r = csqrt(1.0f - rmul(z, z));  // not fused here (fixture search)
-    f3 d = F3(r * cos_cr(th), r * sin_cr(th), z);
+    float r = sky ? csqrt(1.0f - z * z) : csqrt(fma_(-z, z, 1.0f));
+    const float x = cos_cr(th) * r, y = sin_cr(th) * r;
+    f3 d = F3(x, y, z);
     if (l.kind == PT_LIGHT_DISTANT) {  // Light.cpp:208-215
         ls.L = ld3(l.color);
         ls.u = u0;
         ls.v = u1;
-        ls.dir = normalize(ld3(l.vec) + d * 0.02f);
+        const f3 vv = ld3(l.vec);
+        ls.dir = normalize(F3(fma_(d.x, 0.02f, vv.x), fma_(d.y, 0.02f, vv.y), fma_(d.z, 0.02f, vv.z)));
         return ls;
     }
     ls.L = inf_le(l, d);  // Light.cpp:35-42, 61-68
-    sphere_uv(d, ls.u, ls.v);
+    if (sky)
+        sphere_uv_n(d * (1.0f / csqrt(fma_(y, y, x * x) + z * z)), ls.u, ls.v);
+    else
+        sphere_uv(d, ls.u, ls.v);
     ls.dir = d;
     return ls;
 }
@@ -894,8 +975,8 @@ __device__ __forceinline__ float light_pdf(const pt_light& l, f3 p, f3 n, f3 ro,
             ro = o.ro;
             rd = o.rd;
         }
-        if (l.one_sided) return dot(-rd, n) > 0 ? shape_pdf(kind, index, p, n, ro, rd) : 0;
-        return shape_pdf(kind, index, p, n, ro, rd);
+        if (l.one_sided) return dot(-rd, n) > 0 ? shape_pdf(kind, index, p, n, ro, rd, true) : 0;
+        return shape_pdf(kind, index, p, n, ro, rd, false);
     }
     if (l.kind == PT_LIGHT_UNIFORM_INF || l.kind == PT_LIGHT_SKY_INF) return 1.0f / (4.0f * PT_PI);
     if (l.kind == PT_LIGHT_TEX_INF) return texinf_pdf(l, rd);

@@ -57,23 +57,27 @@ __device__ __forceinline__ bool tri_pred(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float 
     return t <= tmax && t >= PT_EPS;
 }
 
-// QuadShape hit test (Shape.cpp:320-359)
+// QuadShape hit test (Shape.cpp:320-359) as built: Intersect tests and
+// divides by dot(d, nn) fused, IntersectPred (PRED) by the unfused dot; beta's
+// cross(u, ph) rounded-first with its dot in y, x, z order
+template <bool PRED>
 __device__ __forceinline__ bool quad_hit(const pt_quad& q, f3 o, f3 d, float tmax, float& t, float& a, float& b) {
     f3 normal = ld3(q.normal);
     f3 nn = normal;
     float DD = q.D;
-    if (dot(d, normal) > 0) {
+    const float dn = PRED ? dot_p(normal, d) : dot(d, normal);
+    if (dn > 0) {
         nn = -normal;
         DD = -q.D;
     }
-    float denom = dot(nn, d);
+    const float denom = PRED ? (dn > 0 ? -dn : dn) : dot(d, nn);
     if (fabsf(denom) < 1e-8f) return false;
     t = (DD - dot(nn, o)) / denom;
     if (t < PT_EPS || t > tmax) return false;
-    f3 ph = (o + t * d) - ld3(q.Q);
+    f3 ph = at_f(o, d, t) - ld3(q.Q);
     f3 w = ld3(q.w);
     a = dot(w, cross(ph, ld3(q.v)));
-    b = dot(w, cross(ld3(q.u), ph));
+    b = dot_yxz(cross_r(ld3(q.u), ph), w);
     return a >= 0 && a <= 1 && b >= 0 && b <= 1;
 }
 
@@ -124,7 +128,7 @@ __device__ __noinline__ bool other_closest(uint32_t slot, uint32_t w0, f3 o, f3 
     const DevPrimInfo pi = S.info[slot];
     float a = 0, b = 0;
     bool hit;
-    if ((w0 & GF_KIND) == PT_PRIM_QUAD) hit = quad_hit(S.quads[pi.index], o, d, tmax, t, a, b);
+    if ((w0 & GF_KIND) == PT_PRIM_QUAD) hit = quad_hit<false>(S.quads[pi.index], o, d, tmax, t, a, b);
     else {
         hit = sphere_root(S.spheres[pi.index], o, d, tmax, t);
         if (hit && (w0 & GF_ALPHA)) {
@@ -144,7 +148,11 @@ __device__ __noinline__ bool other_pred(uint32_t slot, uint32_t w0, f3 o, f3 d, 
     const DevPrimInfo pi = S.info[slot];
     float t, a = 0, b = 0;
     bool hit;
-    if ((w0 & GF_KIND) == PT_PRIM_QUAD) hit = quad_hit(S.quads[pi.index], o, d, tmax, t, a, b);
+    // GeometricPrimitive::IntersectPred: a material with alpha runs the full
+    // Intersect (GF_PRED_GLM), the others the shape's IntersectPred
+    if ((w0 & GF_KIND) == PT_PRIM_QUAD)
+        hit = (w0 & GF_PRED_GLM) ? quad_hit<false>(S.quads[pi.index], o, d, tmax, t, a, b)
+                                 : quad_hit<true>(S.quads[pi.index], o, d, tmax, t, a, b);
     else {
         hit = sphere_root(S.spheres[pi.index], o, d, tmax, t);
         if (hit && (w0 & GF_ALPHA)) {

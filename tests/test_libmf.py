@@ -1,0 +1,22 @@
+"""The device's expf / acosf / atanf / atan2f / powf
+(pathtracing_amd/csrc/pt_libmf.h) against the host libm the reference and the
+oracle call: bit-identical on a strided sample of every float, plus random
+(y, x) pairs for atan2f and powf (tools/check_libmf.c; stride 1 is the
+exhaustive run, 0 mismatches of 4.3e9 per function when last run)."""
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_libmf_matches_host_libm(tmp_path):
+    exe = tmp_path / "check_libmf"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-mfma", "-o", str(exe), str(ROOT / "tools" / "check_libmf.c"),
+                    "-lm"], check=True)
+    res = subprocess.run([str(exe), "1021", "2000000"], capture_output=True, text=True)
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert "expf table in libm: 1" in res.stdout

@@ -20,8 +20,10 @@ ROOT = Path(__file__).resolve().parents[1]
 CSRC = ROOT / "pathtracing_amd" / "csrc"
 LIBDIR = ROOT / "pathtracing_amd" / "_lib"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-# device float semantics: hipcc's default contraction (fast) for now; see DESIGN.md §4
-FP_FLAGS: list[str] = []
+# device float semantics: no implicit contraction — every fused multiply-add
+# the reference's GCC build forms is spelled out (fma_ in pt_device.h), so
+# the device rounds exactly as the reference does; see DESIGN.md §4
+FP_FLAGS: list[str] = ["-ffp-contract=off"]
 ARCH = os.environ.get("PT_OFFLOAD_ARCH", "gfx950")
 
 
