@@ -239,6 +239,58 @@ struct World {
     std::shared_ptr<Camera> camera;
 };
 
+// --- pinned estimates.  Two reference lights pre-process with unseeded
+// random jitter (Light.cpp:79-104 the sky's Power(), Light.cpp:154-200 the env
+// map's accWeights), so two runs of the same recipe differ.  A recipe may pin
+// them ("power P" after a sky, "accw FILE" after a texture light): the
+// subclasses below run the reference's own PreProcess and then replace the
+// random estimate, so the fixtures generated here and the drop-in run on the
+// GPU box see the same lights.  Private members are reached through member
+// pointers formed by explicit template instantiation (as the drop-in does).
+template <class Tag, typename Tag::type M>
+struct HarnessMember {
+    friend typename Tag::type get(Tag) { return M; }
+};
+#define H_MEMBER(NAME, CLASS, TYPE, FIELD)   \
+    struct NAME {                            \
+        using type = TYPE CLASS::*;          \
+        friend type get(NAME);               \
+    };                                       \
+    template struct HarnessMember<NAME, &CLASS::FIELD>
+H_MEMBER(HTexAcc, TextureInfiniteLight, std::vector<float>, accWeights);
+H_MEMBER(HTexTotal, TextureInfiniteLight, double, totalWeight);
+H_MEMBER(HTexPower, TextureInfiniteLight, float, cachedPower);
+H_MEMBER(HSkyPower, FunctionInfiniteLight, float, cachedPower);
+
+struct PinnedSky : FunctionInfiniteLight {
+    float pinned;
+    template <class F>
+    PinnedSky(F fn, float p) : FunctionInfiniteLight(fn), pinned(p) {}
+    void PreProcess(const AABB& bbox) override {
+        FunctionInfiniteLight::PreProcess(bbox);
+        this->*get(HSkyPower{}) = pinned;
+    }
+};
+struct PinnedTexInf : TextureInfiniteLight {
+    std::vector<float> acc;
+    PinnedTexInf(const std::shared_ptr<Texture>& t, float sc, const std::string& path) : TextureInfiniteLight(t, sc) {
+        std::ifstream f(path, std::ios::binary);
+        f.seekg(0, std::ios::end);
+        acc.resize((size_t)f.tellg() / sizeof(float));
+        f.seekg(0);
+        f.read((char*)acc.data(), acc.size() * sizeof(float));
+        if (acc.size() != (size_t)1920 * 1080) { fprintf(stderr, "accw %s: %zu entries\n", path.c_str(), acc.size()); exit(1); }
+    }
+    void PreProcess(const AABB& bbox) override {
+        TextureInfiniteLight::PreProcess(bbox);  // sceneRadius, weights (unused by sample / PDF)
+        this->*get(HTexAcc{}) = acc;
+        this->*get(HTexTotal{}) = acc.back();
+        // cachedPower = totalWeight / samples * powerFunction(sceneRadius) (Light.cpp:199),
+        // the default powerFunction sqrt
+        this->*get(HTexPower{}) = (float)((double)acc.back() / (1920 * 1080) * std::sqrt(sceneRadius));
+    }
+};
+
 static std::shared_ptr<Texture> T(World& w, int id) { return id < 0 ? nullptr : w.tex.at(id); }
 
 static glm::mat4 read_mat4(std::istringstream& s) {  // 16 floats, glm column-major
@@ -388,22 +440,30 @@ static void read_recipe(World& w, const std::string& path) {
                 w.inf.push_back(std::make_shared<UniformInfiniteLight>(glm::vec3(r, g, b)));
             } else if (kind == "texture") {
                 int id; float sc; s >> id >> sc;
-                w.inf.push_back(std::make_shared<TextureInfiniteLight>(w.tex.at(id), sc));
+                std::string opt, path;
+                if (s >> opt >> path && opt == "accw")
+                    w.inf.push_back(std::make_shared<PinnedTexInf>(w.tex.at(id), sc, path));
+                else
+                    w.inf.push_back(std::make_shared<TextureInfiniteLight>(w.tex.at(id), sc));
             } else if (kind == "sky") {
                 float c[7]; for (float& x : c) s >> x;
                 glm::vec3 c0(c[0], c[1], c[2]), c1(c[3], c[4], c[5]);
                 float sc = c[6];
+                std::string opt;
+                float pin = 0;
+                const bool pinned = (s >> opt >> pin) && opt == "power";
                 // main.cpp:292-295 gradient, parameterised
 #ifdef PT_WITH_HIP
                 // the GPU integrator recognises the gradient by its functor type
-                w.inf.push_back(std::make_shared<FunctionInfiniteLight>(pt::SkyGradient{c0, c1, sc}));
+                const pt::SkyGradient fn{c0, c1, sc};
 #else
                 auto fn = [c0, c1, sc](const Ray& ray) {
                     float a = 0.5f * (ray.dir.y + 1.0f);
                     return sc * ((1.0f - a) * c0 + a * c1);
                 };
-                w.inf.push_back(std::make_shared<FunctionInfiniteLight>(fn));
 #endif
+                if (pinned) w.inf.push_back(std::make_shared<PinnedSky>(fn, pin));
+                else w.inf.push_back(std::make_shared<FunctionInfiniteLight>(fn));
             }
             w.lightOwner[w.inf.back().get()] = "inf:" + std::to_string(w.inf.size() - 1);
         } else if (k == "extralight") {
@@ -944,7 +1004,7 @@ static void cmd_tonemap(const std::string& out, const std::string& inPath, int W
 // HipVolPathIntegrator on the
 // reference-built scene (integration/HipIntegrator.hpp), Render(gpus) into the
 // reference Film; dumps the merged accumulation like `film`.
-static void cmd_hip(World& w, const std::string& out, unsigned gpus, bool adaptive) {
+static void cmd_hip(World& w, const std::string& out, unsigned gpus, bool adaptive, bool with_ref) {
     auto sampler = std::make_shared<pt::PCGSampler>(w.spp, w.seed, w.W);
     std::vector<double> acc;
     std::vector<uint32_t> counts;
@@ -967,7 +1027,9 @@ static void cmd_hip(World& w, const std::string& out, unsigned gpus, bool adapti
     wr(out + ".hipfilm.bin", acc);
     wr(out + ".hipcounts.bin", counts);
     // the reference's own frame on the same objects (same sky power): its
-    // fixed-SPP Li splat, or its own adaptive Render
+    // fixed-SPP Li splat, or its own adaptive Render.  "noref" (the GPU box)
+    // leaves it to fixtures generated in the build container.
+    if (!with_ref) return;
     if (adaptive) cmd_adaptive(w, out);
     else cmd_film(w, out, w.spp);
 }
@@ -1005,7 +1067,14 @@ int main(int argc, char** argv) {
     else if (cmd == "lights") cmd_lights(w, out, argv[4]);
     else if (cmd == "time") cmd_time(w, atoi(argv[4]), (unsigned)atoi(argv[5]), argc > 6 ? argv[6] : "render");
 #ifdef PT_WITH_HIP
-    else if (cmd == "hip") cmd_hip(w, out, argc > 4 ? (unsigned)atoi(argv[4]) : 1u, argc > 5 && std::string(argv[5]) == "adaptive");
+    else if (cmd == "hip") {
+        bool adaptive = false, with_ref = true;
+        for (int k = 5; k < argc; k++) {
+            adaptive |= std::string(argv[k]) == "adaptive";
+            with_ref &= std::string(argv[k]) != "noref";
+        }
+        cmd_hip(w, out, argc > 4 ? (unsigned)atoi(argv[4]) : 1u, adaptive, with_ref);
+    }
 #endif
     else { fprintf(stderr, "unknown cmd %s\n", cmd.c_str()); return 2; }
     return 0;

@@ -41,8 +41,24 @@ def write_hdr(path: Path, rgbe: np.ndarray):
         f.write(np.ascontiguousarray(rgbe, np.uint8).tobytes())
 
 
+def pin_random_lights(setup) -> None:
+    """Fix the two estimates the reference draws with unseeded jitter when it
+    pre-processes lights (a sky's Power(), Light.cpp:79-104; an env map's
+    accWeights, Light.cpp:154-200) at this package's deterministic values, so
+    that a recipe written with pin=True renders the same in every run."""
+    bbox = setup.scene.BoundingBox()
+    for l in setup.scene.infiniteLights:
+        if isinstance(l, FunctionInfiniteLight) and l.power_override is None:
+            l.PreProcess(bbox)
+            l.power_override = float(l.cachedPower)
+        elif isinstance(l, TextureInfiniteLight) and l.accWeights is None:
+            l.PreProcess(bbox)
+
+
 def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: str, max_depth: int,
-                 light_sampler=None, extra_lights: Optional[list] = None) -> Path:
+                 light_sampler=None, extra_lights: Optional[list] = None, pin: bool = False) -> Path:
+    """pin: carry the sky's power and the env map's running cell sums
+    (pin_random_lights) so the harness replaces its random estimates."""
     out_dir = Path(out_dir)
     out_dir.mkdir(parents=True, exist_ok=True)
     lines: List[str] = ["ptscene 1"]
@@ -185,9 +201,15 @@ def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: 
         if isinstance(l, UniformInfiniteLight):
             lines.append(f"infinite uniform {' '.join(_f(x) for x in l.color)}")
         elif isinstance(l, FunctionInfiniteLight):
-            lines.append(f"infinite sky {' '.join(_f(x) for x in [*l.c0, *l.c1, l.scale])}")
+            pw = f" power {_f(l.power_override)}" if pin and l.power_override is not None else ""
+            lines.append(f"infinite sky {' '.join(_f(x) for x in [*l.c0, *l.c1, l.scale])}{pw}")
         elif isinstance(l, TextureInfiniteLight):
-            lines.append(f"infinite texture {tex(l.tex)} {_f(l.LeScale)}")
+            acc = ""
+            if pin and l.accWeights is not None:
+                path = out_dir / f"accw{len(lines)}.f32"
+                np.ascontiguousarray(l.accWeights, np.float32).tofile(path)
+                acc = f" accw {path.resolve()}"
+            lines.append(f"infinite texture {tex(l.tex)} {_f(l.LeScale)}{acc}")
         else:
             raise TypeError(type(l))
     for l in extra_lights or []:

@@ -290,15 +290,24 @@ STATS_SCENES = {
     "cornell_c3": lambda: scenes.cornell(W=48, H=48, spp=1024, config="c3", seed=0x5EED0052),
     "blend_box": lambda: scenes.blend_box(W=48, H=48, spp=1024, seed=0x5EED0053),
     "envmap": lambda: scenes.envmap(W=48, H=48, spp=1024, seed=0x5EED0054),
+    # the C4 recipe class (textures, alpha-masked foliage, sun + sky, lamps,
+    # glass, depth 128, PowerLightSampler, Mitchell) at 2 % detail
+    "sanmiguel_c4": lambda: scenes.sanmiguel(W=64, H=64, spp=1024, detail=0.02, tex_size=256),
 }
 
 
-def gen_stats(tmp: Path):
+def gen_stats(tmp: Path, only=None):
     """F8: the reference's own TileIntegrator::Render with main.cpp's
     StratifiedSampler(32, 32) and its unseeded random numbers (8 threads,
-    adaptive rounds): per pixel the samples traced, their mean and variance."""
+    adaptive rounds): per pixel the samples traced, their mean and variance.
+    only: regenerate these scenes and keep the others' committed entries."""
     res = {}
+    if only and (OUT / "stats.npz").exists():
+        old = np.load(OUT / "stats.npz", allow_pickle=False)
+        res = {k: old[k] for k in old.files}
     for name, make in STATS_SCENES.items():
+        if only and name not in only:
+            continue
         setup = make()
         d = tmp / f"stats_{name}"
         recipe = write_recipe(d, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
@@ -331,6 +340,8 @@ def main(names=None):
             gen_adaptive(Path(t))
         if not names or "stats" in names:
             gen_stats(Path(t))
+        elif any(n.startswith("stats:") for n in names):  # stats:NAME regenerates one stats scene
+            gen_stats(Path(t), [n[6:] for n in names if n.startswith("stats:")])
         if not names or "envmap" in names:
             gen_envmap(Path(t))
         if not names or "c4_band" in names:

@@ -2,11 +2,14 @@
 
 oracle/_ref/hip_harness (built here from the reference sources + the
 adapter, linked against libpt_hip.so; it travels to the GPU box prebuilt)
-builds each parity scene with the reference's own classes from a recipe,
-renders it with pt::HipPathIntegrator::Render into the reference Film, and
-also splats the reference's CPU Li for the same objects.  The two
-accumulations must agree like the Python-path film tests (same seeds; the
-sky's randomly estimated power is shared because both use one process).
+builds each parity scene with the reference's own classes from a recipe and
+renders it with pt::HipPathIntegrator::Render into the reference Film
+("noref": it runs no reference integrator on the box).  The reference's own
+frames of the same recipes were computed in the build container
+(tests/golden/gen_dropin.py -> dropin.npz).  The two randomly pre-processed
+light estimates (a sky's power, an env map's cell sums) are pinned in the
+recipe at this package's deterministic values (recipe.pin_random_lights), so
+both runs see the same lights.
 """
 import subprocess
 from pathlib import Path
@@ -15,47 +18,55 @@ import numpy as np
 import pytest
 
 from conftest import record_parity
-from fixtures import parity_scenes
-from pathtracing_amd.recipe import write_recipe
-from pathtracing_amd.scene import FunctionInfiniteLight
+from fixtures import GOLDEN, parity_scenes
+from pathtracing_amd.recipe import pin_random_lights, write_recipe
 
 pytestmark = pytest.mark.gpu
 
 ROOT = Path(__file__).resolve().parents[1]
 HARNESS = ROOT / "oracle" / "_ref" / "hip_harness"
-# measured bars (round 2); default 0.999
-DROPIN_FILM_MIN = {"sanmiguel": 0.99}
+# every pixel (the device rounds as the reference does: DESIGN.md §4)
+FILM_MIN = 1.0
+
+
+def _dropin(name_or_setup, tmp_path, *extra):
+    setup = parity_scenes()[name_or_setup]() if isinstance(name_or_setup, str) else name_or_setup
+    pin_random_lights(setup)
+    recipe = write_recipe(tmp_path, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
+                          setup.max_depth, setup.light_sampler, setup.extra_lights, pin=True)
+    out = tmp_path / "o"
+    subprocess.run([str(HARNESS), str(recipe), "hip", str(out), "1", "noref", *extra], check=True, timeout=300)
+    W, H = setup.camera.film.Resolution()
+    film = np.fromfile(f"{out}.hipfilm.bin", np.float64).reshape(H, W, 4)
+    counts = np.fromfile(f"{out}.hipcounts.bin", np.uint32).reshape(H, W)
+    return setup, film, counts
+
+
+def _film_frac(gpu, ref):
+    num = np.linalg.norm(gpu[..., :3] - ref[..., :3], axis=-1)
+    den = np.maximum(np.linalg.norm(ref[..., :3], axis=-1), 1e-3 * ref[..., 3])
+    return (num <= 1e-3 * den + 1e-7).mean()
 
 
 @pytest.mark.skipif(not HARNESS.exists(), reason="hip_harness not built (needs /root/reference at build time)")
 @pytest.mark.parametrize("name", ["example1", "cornell_c2", "cornell_c3", "zoo", "heightfield", "sanmiguel",
                                   "example1_volpath", "fog", "instances", "lit_instances"])
 def test_drop_in_integrator_matches_reference_film(name, tmp_path):
-    setup = parity_scenes()[name]()
-    recipe = write_recipe(tmp_path, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
-                          setup.max_depth, setup.light_sampler, setup.extra_lights)
-    out = tmp_path / "o"
-    subprocess.run([str(HARNESS), str(recipe), "hip", str(out), "1"], check=True, timeout=300)
-    W, H = setup.camera.film.Resolution()
-    gpu = np.fromfile(f"{out}.hipfilm.bin", np.float64).reshape(H, W, 4)
-    ref = np.fromfile(f"{out}.film.bin", np.float64).reshape(H, W, 4)
+    setup, gpu, _ = _dropin(name, tmp_path)
+    ref = np.load(GOLDEN / "dropin.npz", allow_pickle=False)[f"film_{name}"]
     np.testing.assert_allclose(gpu[..., 3], ref[..., 3], rtol=1e-9, atol=1e-12)
-    num = np.linalg.norm(gpu[..., :3] - ref[..., :3], axis=-1)
-    den = np.maximum(np.linalg.norm(ref[..., :3], axis=-1), 1e-3 * ref[..., 3])
-    frac = (num <= 1e-3 * den + 1e-7).mean()
+    frac = _film_frac(gpu, ref)
     record_parity(f"dropin_film_ref/{name}", "film", frac)
-    assert frac >= DROPIN_FILM_MIN.get(name, 0.999), f"{name}: {frac:.4f} of pixels within 1e-3 rel L2"
+    assert frac >= FILM_MIN, f"{name}: {frac:.4f} of pixels within 1e-3 rel L2"
     # and the drop-in renders what the Python-side API renders for the same
-    # scene (skipped with a sky: the reference estimates its power randomly)
-    if any(isinstance(l, FunctionInfiniteLight) for l in setup.scene.infiniteLights):
-        return
+    # scene (same pinned light estimates)
     integ = setup.make_integrator()
     film = setup.camera.GetFilm()
     film.Clear()
     integ.Render()
     same = np.isclose(film.accum, gpu, rtol=1e-3, atol=1e-6).mean()
     record_parity(f"dropin_vs_python/{name}", "film", same)
-    assert same >= 0.999
+    assert same == 1.0
 
 
 @pytest.mark.skipif(not HARNESS.exists(), reason="hip_harness not built (needs /root/reference at build time)")
@@ -63,46 +74,28 @@ def test_drop_in_integrator_matches_reference_film(name, tmp_path):
                                   "lit_instances"])
 def test_drop_in_adaptive_render_matches_reference_render(name, tmp_path):
     """The drop-in's default Render (adaptive, like TileIntegrator::Render)
-    against the reference's own adaptive Render of the same objects in the
-    same process (so a randomly pre-processed sky has one power): identical
+    against the reference's own adaptive Render of the same recipe: identical
     per-pixel sample counts, film within the film tolerance."""
-    setup = parity_scenes()[name]()
-    recipe = write_recipe(tmp_path, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
-                          setup.max_depth, setup.light_sampler, setup.extra_lights)
-    out = tmp_path / "o"
-    subprocess.run([str(HARNESS), str(recipe), "hip", str(out), "1", "adaptive"], check=True, timeout=300)
-    W, H = setup.camera.film.Resolution()
-    counts = np.fromfile(f"{out}.hipcounts.bin", np.uint32).reshape(H, W)
-    ref_counts = np.fromfile(f"{out}.adaptive_counts.bin", np.uint32).reshape(H, W)
-    same = (counts == ref_counts).mean()
+    _, gpu, counts = _dropin(name, tmp_path, "adaptive")
+    fx = np.load(GOLDEN / "dropin.npz", allow_pickle=False)
+    same = (counts == fx[f"adaptive_counts_{name}"]).mean()
     record_parity(f"dropin_adaptive_counts/{name}", "counts", same)
-    assert same >= DROPIN_FILM_MIN.get(name, 1.0), f"{name}: {same:.4f} of pixels with the reference's sample count"
-    gpu = np.fromfile(f"{out}.hipfilm.bin", np.float64).reshape(H, W, 4)
-    ref = np.fromfile(f"{out}.adaptive_film.bin", np.float64).reshape(H, W, 4)
-    num = np.linalg.norm(gpu[..., :3] - ref[..., :3], axis=-1)
-    den = np.maximum(np.linalg.norm(ref[..., :3], axis=-1), 1e-3 * ref[..., 3])
-    frac = (num <= 1e-3 * den + 1e-7).mean()
+    assert same == 1.0, f"{name}: {same:.4f} of pixels with the reference's sample count"
+    frac = _film_frac(gpu, fx[f"adaptive_film_{name}"])
     record_parity(f"dropin_adaptive_film/{name}", "film", frac)
-    assert frac >= DROPIN_FILM_MIN.get(name, 0.999), f"{name}: {frac:.4f} of pixels within 1e-3 rel L2"
+    assert frac >= FILM_MIN, f"{name}: {frac:.4f} of pixels within 1e-3 rel L2"
 
 
 @pytest.mark.skipif(not HARNESS.exists(), reason="hip_harness not built (needs /root/reference at build time)")
-def test_drop_in_envmap_uses_the_references_own_cell_sums(tmp_path):
-    """The drop-in with a TextureInfiniteLight over a FloatImageTexture takes
-    the reference's own PreProcess result (its accWeights from randomly
-    jittered cell estimates); the Python path computes the cell sums itself
-    (fixed-hash jitter).  The two CDFs differ by ~1e-6 of the total, about a
-    cell width (1 / 2,073,600), so some picks move to a neighbouring cell:
-    pixels agree to 1e-3 except around those samples, and the frame's mean to
-    1e-3.  The reference's jitter is seeded from std::random_device, so the
-    agreement varies from run to run (measured 98.6 %, 97.9 %)."""
+def test_drop_in_envmap_uses_the_references_cell_sums(tmp_path):
+    """The drop-in with a TextureInfiniteLight over a FloatImageTexture reads
+    the reference light's accWeights (its PreProcess result).  With the
+    recipe's cell sums pinned to the ones the Python path computes
+    (pt_texinf_weights), both sample the same CDF: the drop-in's film equals
+    the Python path's."""
     from pathtracing_amd import scenes
     setup = scenes.envmap(W=32, H=32, spp=16)
-    recipe = write_recipe(tmp_path, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
-                          setup.max_depth, setup.light_sampler, setup.extra_lights)
-    out = tmp_path / "o"
-    subprocess.run([str(HARNESS), str(recipe), "hip", str(out), "1"], check=True, timeout=300)
-    gpu = np.fromfile(f"{out}.hipfilm.bin", np.float64).reshape(32, 32, 4)
+    _, gpu, _ = _dropin(setup, tmp_path)
     integ = setup.make_integrator()
     film = setup.camera.GetFilm()
     film.Clear()
@@ -110,6 +103,4 @@ def test_drop_in_envmap_uses_the_references_own_cell_sums(tmp_path):
     np.testing.assert_allclose(gpu[..., 3], film.accum[..., 3], rtol=1e-9)
     same = np.isclose(film.accum, gpu, rtol=1e-3, atol=1e-6).all(-1).mean()
     record_parity("dropin_vs_python/envmap", "film", same)
-    assert same >= 0.95, f"{same:.4f} of pixels agree"
-    np.testing.assert_allclose(gpu[..., :3].sum() / gpu[..., 3].sum(),
-                               film.accum[..., :3].sum() / film.accum[..., 3].sum(), rtol=1e-3)
+    assert same == 1.0, f"{same:.4f} of pixels agree"

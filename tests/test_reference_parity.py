@@ -350,3 +350,20 @@ def test_oracle_c4_band_is_bit_identical_to_the_reference():
     ref = np.asarray(fx["li_L"], np.float32)
     same = _same_bits(np.asarray(L, np.float32).reshape(ref.shape), ref).all(-1)
     assert same.all(), f"{same.mean():.5f} of 3072 samples bit-identical"
+
+
+def test_oracle_c4_class_matches_reference_render_statistically():
+    """F8 for the C4 recipe class on the CPU: the oracle's per-sample Li on
+    rows 24-27 of the 64 x 64, 1024-spp, 2 %-detail San-Miguel-class scene
+    against the reference's own TileIntegrator::Render with its
+    StratifiedSampler and unseeded RNGs (tests/golden/stats.npz
+    "sanmiguel_c4"): every pixel channel within 4 standard errors (measured
+    768 / 768)."""
+    from fixtures import stats_scenes, z_test
+    setup = stats_scenes()["sanmiguel_c4"]()
+    integ = setup.make_integrator()
+    ref = np.load(GOLDEN_DIR / "stats.npz", allow_pickle=False)["sanmiguel_c4"]
+    W = ref.shape[1]
+    L = np.stack([oracle.li(integ, y * W, (y + 1) * W)[0] for y in range(24, 28)])
+    ok = z_test(L, ref[24:28])
+    assert ok.mean() >= 0.99, f"{ok.mean():.4f} of pixel channels within 4 sigma"
