@@ -121,21 +121,34 @@ def cpu_baseline(setup, config: str, target_s: float = 15.0):
     else:
         dt = pilot
     rays = cnt["closest"] + cnt["any"]
-    out = {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+    value = rays / dt / 1e6
+    per_core = value / threads
+    out = {"value": round(value, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
            "nproc": nproc, "affinity": affinity,
            "sample": f"oracle/pt_oracle.c, same scene {W}x{H} at {spp} spp ({rays} rays in {dt:.1f} s, "
-                     f"{threads} threads; the box's cpu budget is 16 threads)"}
-    ratio = _json(ROOT / "profiles" / "r02_cpu_ratio.json")
+                     f"{threads} threads; the box's cpu budget is 16 threads)",
+           "per_core": round(per_core, 4),
+           # linear in cores: an upper bound for the whole host (memory
+           # bandwidth and SMT make real scaling sub-linear)
+           "full_host_estimate": {"value": round(per_core * affinity, 3), "cores": affinity,
+                                  "method": "per-core rate x affinity (linear)"}}
+    ratio = _json(ROOT / "profiles" / "r03_cpu_ratio.json") or _json(ROOT / "profiles" / "r02_cpu_ratio.json")
     if ratio:
         out["port_vs_reference"] = ratio.get("summary")
         # the reference's own speed on this host, estimated from the port
-        # through the ratio measured on the closest scene class
+        # through the ratio measured on the closest scene class, at the
+        # measured thread count closest to the one timed here
         key = {"c4": "c4_recipe_2pct_160x90_16spp_depth128", "c1": "c1_example1_path_256x256_16spp"}.get(
             config, "c1_example1_path_256x256_16spp")
-        r = ratio.get(key, {}).get("port_over_reference")
+        ent = ratio.get(key, {})
+        by = ent.get("by_threads", {})
+        t_used = min(by, key=lambda t: abs(int(t) - threads)) if by else str(ratio.get("_meta", {}).get("threads"))
+        r = by[t_used]["port_over_reference"] if by else ent.get("port_over_reference")
         if r:
-            out["reference_estimate"] = {"value": round(out["value"] / r, 3), "port_over_reference": r,
+            out["reference_estimate"] = {"value": round(value / r, 3), "port_over_reference": r,
+                                         "ratio_threads": int(t_used) if t_used and t_used != "None" else None,
                                          "scene_class": key}
+    out["_counts"] = cnt  # traversal counts in the reference's visit order (consumed by main)
     return out
 
 
@@ -319,6 +332,9 @@ def main():
     elapsed_max = float(t.item())
     total_rays = float(rays.item())
 
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(setup, args.config, args.cpu_seconds)
     if rank == 0:
         pool = args.traversal == "pool" or (args.traversal == "auto" and args.config in HBM_CONFIGS)
         quant = pool and args.nodes != "full"
@@ -337,12 +353,27 @@ def main():
                 return None
             launch_bytes = bpr * nrays / max(1, launches)
             achieved = launch_bytes / (avg_ms * 1e-3) / 1e9
-            layout = lbpr * nrays / max(1, launches) / (avg_ms * 1e-3) / 1e9
+            layout = lbpr * nrays / max(1, launches) / (avg_ms * 1e-3) / 1e9 if lbpr else None
             return {"kernel": name, "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "bytes_per_ray": round(bpr, 1), "bytes_per_launch": round(launch_bytes),
-                    "layout_bytes_per_ray": round(lbpr, 1), "layout_achieved": round(layout, 1),
+                    "layout_bytes_per_ray": round(lbpr, 1) if lbpr else None,
+                    "layout_achieved": round(layout, 1) if layout else None,
+                    "layout_frac": round(layout / HBM_PEAK_GBS, 4) if layout else None,
                     "avg_launch_ms": round(avg_ms, 4), "launches": launches}
 
+        # the algorithmic bytes come from the reference's own
+        # visit order (the oracle's BVH4::Intersect / IntersectPred restatement,
+        # entry-distance cull included) over the cpu_baseline sample of the
+        # same frame; the GPU's instrumented count rides beside it (and stands
+        # in when no CPU sample ran, e.g. N > 1)
+        ref_counts = cpu.pop("_counts") if cpu else None
+        count_source = "gpu"
+        if ref_counts and ref_counts["closest"]:
+            bytes_closest = (128.0 * ref_counts["nodes_closest"] + 48.0 * ref_counts["tris_closest"]) / \
+                ref_counts["closest"]
+            if ref_counts["any"]:
+                bytes_any = (128.0 * ref_counts["nodes_any"] + 48.0 * ref_counts["tris_any"]) / ref_counts["any"]
+            count_source = f"oracle reference order ({ref_counts['closest']} closest / {ref_counts['any']} any rays)"
         lb_closest = lb_any = None
         if cst:
             lb_closest = (node_bytes * cst["nodes_closest"] + 48.0 * cst["tris_closest"]) / max(1, cst["rays_closest"])
@@ -360,16 +391,27 @@ def main():
                                  if traffic and rc else None),
                 "src_sha": sha, **tinfo}
         if rc:
-            roof.update({"kernel": kname, "bytes_per_ray": rc["bytes_per_ray"],
-                         "nodes_per_ray": round(cst["nodes_closest"] / max(1, cst["rays_closest"]), 2),
-                         "tris_per_ray": round(cst["tris_closest"] / max(1, cst["rays_closest"]), 2),
+            def per(c, k, n):
+                return round(c[k] / max(1, c[n]), 2) if c else None
+            roof.update({"kernel": kname, "bytes_per_ray": rc["bytes_per_ray"], "count_source": count_source,
+                         "nodes_per_ray": per(ref_counts, "nodes_closest", "closest") if ref_counts
+                         else per(cst, "nodes_closest", "rays_closest"),
+                         "tris_per_ray": per(ref_counts, "tris_closest", "closest") if ref_counts
+                         else per(cst, "tris_closest", "rays_closest"),
+                         "gpu_nodes_per_ray": per(cst, "nodes_closest", "rays_closest"),
+                         "gpu_tris_per_ray": per(cst, "tris_closest", "rays_closest"),
                          "avg_launch_ms": rc["avg_launch_ms"], "launches": rc["launches"],
                          "bytes_per_launch": rc["bytes_per_launch"], "node_layout_bytes": node_bytes,
                          "layout_bytes_per_ray": rc["layout_bytes_per_ray"],
-                         "layout_achieved": rc["layout_achieved"]})
+                         "layout_achieved": rc["layout_achieved"], "layout_frac": rc["layout_frac"]})
         if ra:
-            ra["nodes_per_ray"] = round(cst["nodes_any"] / max(1, cst["rays_any"]), 2)
-            ra["tris_per_ray"] = round(cst["tris_any"] / max(1, cst["rays_any"]), 2)
+            ra["nodes_per_ray"] = (round(ref_counts["nodes_any"] / max(1, ref_counts["any"]), 2) if ref_counts
+                                   else round(cst["nodes_any"] / max(1, cst["rays_any"]), 2))
+            ra["tris_per_ray"] = (round(ref_counts["tris_any"] / max(1, ref_counts["any"]), 2) if ref_counts
+                                  else round(cst["tris_any"] / max(1, cst["rays_any"]), 2))
+            if cst:
+                ra["gpu_nodes_per_ray"] = round(cst["nodes_any"] / max(1, cst["rays_any"]), 2)
+                ra["gpu_tris_per_ray"] = round(cst["tris_any"] / max(1, cst["rays_any"]), 2)
             roof["shadow"] = ra
         out = {
             "metric": "Mrays/s",
@@ -392,8 +434,11 @@ def main():
                        "setup_s": round(setup_s, 1)},
             "roofline": roof,
         }
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(build_setup(args.config, args.spp), args.config, args.cpu_seconds)
+        if cpu:
+            v = out["value"]
+            cpu["gpu_over_cpu"] = round(v / cpu["value"], 1)
+            cpu["gpu_over_full_host_estimate"] = round(v / cpu["full_host_estimate"]["value"], 1)
+            out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -651,22 +651,26 @@ static v3 m4_dir(const float* m, v3 v) {
 static void normal_matrix(const float* T, float* NM) {
 #define M(c, r) T[(c) * 4 + (r)]
 #define DF(a, b, c, d) fmaf(a, b, -rmul(c, d)) /* the reference build's contraction */
+#define DFN(a, b, c, d) fmaf(-(a), b, rmul(c, d))
     const float D0 = DF(M(1, 1), M(2, 2), M(2, 1), M(1, 2)), D1 = DF(M(0, 1), M(2, 2), M(2, 1), M(0, 2));
     const float D2 = DF(M(0, 1), M(1, 2), M(1, 1), M(0, 2));
     /* as GCC contracts glm's determinant: fma(m20, D2, fma(m00, D0, -(m10*D1))) */
     float od = 1.0f / fmaf(M(2, 0), D2, fmaf(M(0, 0), D0, -rmul(M(1, 0), D1)));
     float inv[3][3];
     inv[0][0] = +DF(M(1, 1), M(2, 2), M(2, 1), M(1, 2)) * od;
-    inv[1][0] = -DF(M(1, 0), M(2, 2), M(2, 0), M(1, 2)) * od;
+    /* the negated cofactors -(a*b - c*d) as the build folds them (.FNMA):
+     * -(a*b) + c*d, which is +0, not -0, where a*b == c*d */
+    inv[1][0] = DFN(M(1, 0), M(2, 2), M(2, 0), M(1, 2)) * od;
     inv[2][0] = +DF(M(1, 0), M(2, 1), M(2, 0), M(1, 1)) * od;
-    inv[0][1] = -DF(M(0, 1), M(2, 2), M(2, 1), M(0, 2)) * od;
+    inv[0][1] = DFN(M(0, 1), M(2, 2), M(2, 1), M(0, 2)) * od;
     inv[1][1] = +DF(M(0, 0), M(2, 2), M(2, 0), M(0, 2)) * od;
-    inv[2][1] = -DF(M(0, 0), M(2, 1), M(2, 0), M(0, 1)) * od;
+    inv[2][1] = DFN(M(0, 0), M(2, 1), M(2, 0), M(0, 1)) * od;
     inv[0][2] = +DF(M(0, 1), M(1, 2), M(1, 1), M(0, 2)) * od;
-    inv[1][2] = -DF(M(0, 0), M(1, 2), M(1, 0), M(0, 2)) * od;
+    inv[1][2] = DFN(M(0, 0), M(1, 2), M(1, 0), M(0, 2)) * od;
     inv[2][2] = +DF(M(0, 0), M(1, 1), M(1, 0), M(0, 1)) * od;
 #undef M
 #undef DF
+#undef DFN
     for (int c = 0; c < 3; c++)
         for (int r = 0; r < 3; r++) NM[c * 3 + r] = inv[r][c];
 }

@@ -711,20 +711,22 @@ __device__ __forceinline__ f3 m4_dir(const float* m, f3 v) {
 // transpose(inverse(mat3(T))) (glm compute_inverse<3,3>) with the reference
 // build's contraction (fixture search), NM[c*3+r]
 __device__ __forceinline__ float df_(float a, float b, float c, float d) { return fma_(a, b, -rmul(c, d)); }
+__device__ __forceinline__ float dfn_(float a, float b, float c, float d) { return fma_(-a, b, rmul(c, d)); }
 __device__ void normal_matrix(const float* T, float* NM) {
 #define M(c, r) T[(c) * 4 + (r)]
     const float D0 = df_(M(1, 1), M(2, 2), M(2, 1), M(1, 2)), D1 = df_(M(0, 1), M(2, 2), M(2, 1), M(0, 2));
     const float D2 = df_(M(0, 1), M(1, 2), M(1, 1), M(0, 2));
     const float od = 1.0f / fma_(M(2, 0), D2, fma_(M(0, 0), D0, -rmul(M(1, 0), D1)));
-    // NM[c*3 + r] = Inverse[r][c]
+    // NM[c*3 + r] = Inverse[r][c]; the negated cofactors -(a*b - c*d) as the
+    // build folds them, -(a*b) + c*d (FNMA: +0 where a*b == c*d, not -0)
     NM[0] = D0 * od;
-    NM[1] = -df_(M(1, 0), M(2, 2), M(2, 0), M(1, 2)) * od;
+    NM[1] = dfn_(M(1, 0), M(2, 2), M(2, 0), M(1, 2)) * od;
     NM[2] = df_(M(1, 0), M(2, 1), M(2, 0), M(1, 1)) * od;
-    NM[3] = -D1 * od;
+    NM[3] = dfn_(M(0, 1), M(2, 2), M(2, 1), M(0, 2)) * od;
     NM[4] = df_(M(0, 0), M(2, 2), M(2, 0), M(0, 2)) * od;
-    NM[5] = -df_(M(0, 0), M(2, 1), M(2, 0), M(0, 1)) * od;
+    NM[5] = dfn_(M(0, 0), M(2, 1), M(2, 0), M(0, 1)) * od;
     NM[6] = D2 * od;
-    NM[7] = -df_(M(0, 0), M(1, 2), M(1, 0), M(0, 2)) * od;
+    NM[7] = dfn_(M(0, 0), M(1, 2), M(1, 0), M(0, 2)) * od;
     NM[8] = df_(M(0, 0), M(1, 1), M(1, 0), M(0, 1)) * od;
 #undef M
 }

@@ -47,40 +47,51 @@ def median(xs):
     return sorted(xs)[len(xs) // 2]
 
 
-def main(out):
+def _time_ref(recipe, tmp, threads, spp, mode):
+    r = subprocess.run([str(HARNESS), str(recipe), "time", str(Path(tmp) / "o"), str(threads), str(spp), mode],
+                       capture_output=True, text=True, check=True)
+    return _rec(r.stdout)
+
+
+def _time_port(integ, threads):
     import oracle
+    t0 = time.perf_counter()
+    _, cnt = oracle.render(integ, threads=threads)
+    dt = time.perf_counter() - t0
+    return (cnt["closest"] + cnt["any"]) / dt / 1e6
+
+
+def main(out):
+    """port / reference at every thread count 1, 2, 4, ... up to this
+    container's CPUs (bench.py applies the ratio measured at the thread count
+    closest to the one it times the port at)."""
     from pathtracing_amd.recipe import write_recipe
-    threads = os.cpu_count() or 8
-    res = {"_meta": {"threads": threads, "host": "build container", "runs": 3,
+    ncpu = os.cpu_count() or 8
+    counts = sorted({1 << k for k in range(ncpu.bit_length()) if (1 << k) <= ncpu} | {ncpu})
+    res = {"_meta": {"threads": counts, "host": "build container", "runs": 3,
                      "cpu": next((l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
                                   if l.startswith("model name")), "?")}}
     for name, mk in scenes_().items():
         setup = mk()
         integ = setup.make_integrator()
+        entry = {"by_threads": {}}
         with tempfile.TemporaryDirectory() as tmp:
             recipe = write_recipe(Path(tmp), setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
                                   setup.max_depth, setup.light_sampler, setup.extra_lights)
-            ref, ren = [], []
-            for _ in range(3):
-                r = subprocess.run([str(HARNESS), str(recipe), "time", str(Path(tmp) / "o"), str(threads),
-                                    str(setup.spp), "li"], capture_output=True, text=True, check=True)
-                ref.append(_rec(r.stdout))
-                r = subprocess.run([str(HARNESS), str(recipe), "time", str(Path(tmp) / "o"), str(threads),
-                                    str(setup.spp), "render"], capture_output=True, text=True, check=True)
-                ren.append(_rec(r.stdout))
-        port = []
-        for _ in range(3):
-            t0 = time.perf_counter()
-            _, cnt = oracle.render(integ, threads=threads)
-            dt = time.perf_counter() - t0
-            port.append((cnt["closest"] + cnt["any"]) / dt / 1e6)
-        res[name] = {"reference_li_loop_mrays": round(median(ref), 3), "port_mrays": round(median(port), 3),
-                     "port_over_reference": round(median(port) / median(ref), 3),
-                     "reference_render_mrays": round(median(ren), 3)}
-        print(name, res[name], flush=True)
+            for t in counts:
+                ref = median([_time_ref(recipe, tmp, t, setup.spp, "li") for _ in range(3)])
+                port = median([_time_port(integ, t) for _ in range(3)])
+                entry["by_threads"][str(t)] = {"reference_li_loop_mrays": round(ref, 3), "port_mrays": round(port, 3),
+                                               "port_over_reference": round(port / ref, 3)}
+                print(name, t, entry["by_threads"][str(t)], flush=True)
+            entry["reference_render_mrays"] = round(
+                median([_time_ref(recipe, tmp, ncpu, setup.spp, "render") for _ in range(3)]), 3)
+        top = entry["by_threads"][str(ncpu)]
+        entry.update(top)  # the full-container figures at the top level
+        res[name] = entry
     ratios = [v["port_over_reference"] for k, v in res.items() if not k.startswith("_")]
     res["summary"] = {"port_over_reference_min": min(ratios), "port_over_reference_max": max(ratios),
-                      "threads": threads, "source": "profiles/r02_cpu_ratio.json (tools/cpu_ratio.py)"}
+                      "threads": ncpu, "source": f"{Path(out).name} (tools/cpu_ratio.py)"}
     Path(out).write_text(json.dumps(res, indent=1, sort_keys=True))
 
 

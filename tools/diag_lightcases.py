@@ -18,18 +18,21 @@ def main(name):
     cases = fx["lsample_cases"]
     got = np.asarray(ctx.light_cases(cases, integ.flat.lights.shape[0]), np.float32)
     orc = np.asarray(oracle.lights(integ.flat, cases), np.float32)
+    nc = len(cases)
     bad = np.nonzero((got.view(np.uint32) != orc.view(np.uint32)).any(1))[0]
-    print("cases", cases.dtype, len(cases), "bad", bad.tolist())
-    print("lights", integ.flat.lights.dtype.names)
-    for i in bad:
-        print("case", i, cases[i])
-        li = int(cases[i][0]) if cases.dtype.names is None else int(cases[i][cases.dtype.names[0]])
-        print(" light", integ.flat.lights[li] if 0 <= li < len(integ.flat.lights) else li)
-        print(" got", [float(x).hex() for x in got[i]])
-        print(" orc", [float(x).hex() for x in orc[i]])
-    for k, inst in enumerate(integ.flat.instances if hasattr(integ.flat, "instances") else []):
-        print("instance", k, inst)
-
+    lights = sorted({int(i) // nc for i in bad})
+    print("cases", len(cases), "bad rows", len(bad), "lights", lights)
+    for li in lights:
+        rows = [int(i) for i in bad if int(i) // nc == li]
+        print("light", li, integ.flat.lights[li], "rows", len(rows))
+        for i in rows[:3]:
+            print(" case", cases[i % nc])
+            print("  got", [float(x).hex() for x in got[i]])
+            print("  orc", [float(x).hex() for x in orc[i]])
+    inst = getattr(integ.flat, "instances", None)
+    if inst is not None:
+        for k, r in enumerate(inst):
+            print("instance", k, r)
 
 if __name__ == "__main__":
     main(sys.argv[1])
