@@ -432,6 +432,9 @@ def main():
                        "world_size": dist.get_world_size() if world > 1 else 1,
                        "film_reduce": film_reduce,
                        "setup_s": round(setup_s, 1)},
+            # rank 0's per-frame kernel time by class (HIP events on the library's stream)
+            "kernel_ms_per_step": {k[3:]: round(totals[k] / args.steps, 1)
+                                   for k in ("ms_closest", "ms_any", "ms_shade")},
             "roofline": roof,
         }
         if cpu:

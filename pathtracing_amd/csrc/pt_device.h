@@ -143,7 +143,16 @@ struct DevScene {
     uint32_t* scratch;       // SCR_WORDS x scratch_lanes (instance traversal state)
     uint32_t scratch_lanes;
     uint32_t* stack_drops;   // traversal pushes past the stack capacity (counted, rare)
+    uint32_t n_materials, n_textures, n_images;
+    uint32_t lds_tables;     // PT_LDS_TABLES: which tables the shading kernels stage (LDS_* bits)
 };
+enum { LDS_MATS = 1u, LDS_TEX = 2u, LDS_IMG = 4u, LDS_LS = 8u };
+// Caps of the shading kernels' LDS copies (PT_LDS_TABLES): 48-B materials and
+// textures, 24-B images, the light sampler's guide table and running sums
+#define PT_LDS_MATS 128
+#define PT_LDS_TEX 128
+#define PT_LDS_IMG 128
+#define PT_LDS_CDF 4096
 
 // The uploaded scene of the current context, in constant memory: every
 // device function reads it directly (no per-lane copy of the struct, and the

@@ -365,6 +365,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(const pt_ray* __r
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_interact(const pt_ray* __restrict__ rays, uint32_t n,
                                                             float* __restrict__ out) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+    stage_tables(false);
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     TraceWork wk{0, 0};
     if (i >= n) return;
@@ -386,6 +387,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_interact(const pt_ray* __res
 // Test hook: Material::scatter / calc_attenuation / PDF on given
 // interactions (pt_bsdf_cases); case and record layout of oracle_bsdf.
 __global__ void k_bsdf_cases(int mid, const float* __restrict__ in, uint32_t n, float* __restrict__ out) {
+    stage_tables(false);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float* c = in + 27ull * i;
@@ -423,6 +425,7 @@ __global__ void k_bsdf_cases(int mid, const float* __restrict__ in, uint32_t n, 
 // Test hook: LightSampler::Sample(u) picks (pt_light_picks): the light index
 // ls_sample returns (-1: no light), one per u.
 __global__ void k_light_picks(const float* __restrict__ u, uint32_t n, int32_t* __restrict__ out) {
+    stage_tables(true);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = ls_sample(u[i]);
 }
@@ -430,6 +433,7 @@ __global__ void k_light_picks(const float* __restrict__ u, uint32_t n, int32_t* 
 // Test hook: Light::sample / PDF / L per light x case (pt_light_cases);
 // case {uv[2], ref point[3]}, record layout of oracle_lights.
 __global__ void k_light_cases(const float* __restrict__ in, uint32_t n, float* __restrict__ out) {
+    stage_tables(false);
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n * S.n_lights) return;
     const uint32_t li = k / n, i = k % n;
@@ -579,6 +583,7 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
                                               ShadowRec* __restrict__ sq, uint32_t* __restrict__ cnt) {
     const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
     if (blockIdx.x * PT_SHADE_BLOCK >= n) return;  // block-uniform: the grid covers the capacity
+    stage_tables(INTEGRATOR == PT_INTEGRATOR_PATH);
     const uint32_t t = blockIdx.x * PT_SHADE_BLOCK + threadIdx.x;
     const uint32_t i = (R.order && t < n) ? R.order[t] : t;  // material-sorted order, or the path order
     bool cont = false, done = false, shadow = false;
@@ -794,6 +799,7 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                                                   ShadowRecV* __restrict__ sq, uint32_t* __restrict__ cnt) {
     const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
     if (blockIdx.x * 256 >= n) return;  // block-uniform: the grid covers the capacity
+    stage_tables(true);
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
     const uint32_t i = (R.order && t < n) ? R.order[t] : t;  // material-sorted order, or the path order
     bool cont = false, done = false, shadow = false;
@@ -1018,6 +1024,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow_tr(PathSoA next, floa
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
     const uint32_t n = *nptr;
     if (blockIdx.x * PT_TRACE_BLOCK >= n) return;
+    stage_tables(false);
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     TraceWork wk{0, 0};
     uint32_t extra = 0;

@@ -792,6 +792,18 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     DS.scratch = nullptr;
     DS.scratch_lanes = 0;
     DS.stack_drops = c->stack_drops;
+    DS.n_materials = s->n_materials;
+    DS.n_textures = s->n_textures;
+    DS.n_images = s->n_images;
+    DS.lds_tables = 0;
+#if PT_LDS_TABLES
+    // the shading kernels' LDS copies (pt_shading.h stage_tables), where the
+    // scene's tables fit their caps
+    if (s->n_materials <= PT_LDS_MATS) DS.lds_tables |= LDS_MATS;
+    if (s->n_textures <= PT_LDS_TEX) DS.lds_tables |= LDS_TEX;
+    if (s->n_images <= PT_LDS_IMG) DS.lds_tables |= LDS_IMG;
+    if (s->n_sampler_lights <= PT_LDS_CDF) DS.lds_tables |= LDS_LS;
+#endif
     c->has_scene = true;
     c->n_media = s->n_media;
     c->n_materials = s->n_materials;

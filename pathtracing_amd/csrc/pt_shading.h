@@ -12,6 +12,68 @@ struct SurfInt {  // SurfaceInteraction (Interaction.hpp:36-51)
     int32_t mat, light;
 };
 
+// ------------------------------------------------------------------ LDS-staged tables
+// PT_LDS_TABLES (A/B option): the shading kernels (k_shade, k_shade_vol and
+// the hooks that shade) copy the material, texture and image records and the
+// light sampler's guide table and running sums into LDS once per block
+// (stage_tables), and the shading path reads them there instead of through
+// L1/L2 gathers.  Tables past their caps stay in global memory (DevScene::
+// lds_tables).  The traversal kernels' alpha test keeps global reads (their
+// LDS holds the traversal stacks).
+#ifndef PT_LDS_TABLES
+#define PT_LDS_TABLES 0
+#endif
+#if PT_LDS_TABLES
+__shared__ pt_material pt_lds_mat[PT_LDS_MATS];
+__shared__ pt_texture pt_lds_tex[PT_LDS_TEX];
+__shared__ pt_image pt_lds_img[PT_LDS_IMG];
+__shared__ uint32_t pt_lds_guide[PT_LS_GUIDE + 1];
+__shared__ float pt_lds_cdf[PT_LDS_CDF];
+template <class T>
+__device__ __forceinline__ void stage_words(T* dst, const T* src, uint32_t n) {
+    static_assert(sizeof(T) % 4 == 0, "word copy");
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
+    const uint32_t w = n * (uint32_t)(sizeof(T) / 4);
+    for (uint32_t i = threadIdx.x; i < w; i += blockDim.x) d[i] = s[i];
+}
+#endif
+// Every thread of the block calls it, before any shading (barrier).
+__device__ __forceinline__ void stage_tables(bool light_sampler) {
+#if PT_LDS_TABLES
+    const uint32_t f = S.lds_tables;
+    if (f & LDS_MATS) stage_words(pt_lds_mat, S.materials, S.n_materials);
+    if (f & LDS_TEX) stage_words(pt_lds_tex, S.textures, S.n_textures);
+    if (f & LDS_IMG) stage_words(pt_lds_img, S.images, S.n_images);
+    if (light_sampler && (f & LDS_LS) && S.light_sampler != PT_LS_UNIFORM && S.n_sampler_lights) {
+        stage_words(pt_lds_guide, S.sampler_guide, PT_LS_GUIDE + 1);
+        stage_words(pt_lds_cdf, S.sampler_cdf, S.n_sampler_lights);
+    }
+    __syncthreads();
+#else
+    (void)light_sampler;
+#endif
+}
+// shading-path table reads (only from kernels that ran stage_tables)
+__device__ __forceinline__ pt_material mat_rec(int mid) {
+#if PT_LDS_TABLES
+    if (S.lds_tables & LDS_MATS) return pt_lds_mat[mid];
+#endif
+    return S.materials[mid];
+}
+__device__ __forceinline__ pt_texture tex_rec(int id) {
+#if PT_LDS_TABLES
+    if (S.lds_tables & LDS_TEX) return pt_lds_tex[id];
+#endif
+    return S.textures[id];
+}
+__device__ __forceinline__ pt_image img_rec(int id) {
+#if PT_LDS_TABLES
+    if (S.lds_tables & LDS_IMG) return pt_lds_img[id];
+#endif
+    return S.images[id];
+}
+
 // ------------------------------------------------------------------ textures
 __device__ __forceinline__ int wrap_index(int i, int n) {
     int m = i % n;
@@ -67,7 +129,8 @@ __device__ f3 tex_eval_t(int id, float u, float v) {
     f3 scale = F3(1, 1, 1);
     bool scaled = false;
     for (int guard = 0; guard < 16; guard++) {
-        const pt_texture& t = S.textures[id];
+        // PAIR: the shading kernels (staged tables); else the traversal's alpha test
+        const pt_texture t = PAIR ? tex_rec(id) : S.textures[id];
         if (t.kind == PT_TEX_SOLID) {
             f3 c = ld3(t.value);
             return scaled ? scale * c : c;
@@ -81,7 +144,7 @@ __device__ f3 tex_eval_t(int id, float u, float v) {
             id = ((ux + uy) % 2 == 0) ? t.a : t.b;
             continue;
         }
-        const pt_image& im = S.images[t.image];
+        const pt_image im = PAIR ? img_rec(t.image) : S.images[t.image];
         float x = u * im.width - 0.5f;
         float y = v * im.height - 0.5f;
         int xi = (int)floorf(x), yi = (int)floorf(y);
@@ -200,7 +263,7 @@ __device__ __forceinline__ f3 to_local(const Onb& b, f3 v) { return F3(dot(v, b.
 // sample_normalMap (Material.hpp:344-348, 580-584)
 __device__ f3 normal_map(int mid, const SurfInt& si) {
     if (mid < 0) return si.ns;
-    const pt_material& m = S.materials[mid];
+    const pt_material m = mat_rec(mid);
     if ((m.kind != PT_MAT_DIFFUSE && m.kind != PT_MAT_DIELECTRIC) || m.norm < 0) return si.ns;
     f3 t = tex_eval(m.norm, si.u, si.v);
     f3 nn = normalize(2.0f * t - F3(1, 1, 1));
@@ -664,7 +727,7 @@ __device__ Bxdf conductor_scatter(const pt_material& m, f3 ind, const SurfInt& s
 // on every path (k_shade<PATH>: 160 -> 16 B of scratch per lane).
 __device__ __forceinline__ Bxdf mat_scatter(int mid, f3 ino, f3 ind, const SurfInt& si, float u, float uv0,
                             float uv1) {
-    const pt_material& m = S.materials[mid];
+    const pt_material m = mat_rec(mid);
     switch (m.kind) {
         case PT_MAT_DIFFUSE: return diffuse_scatter(m, ind, si, u, uv0, uv1);
         case PT_MAT_DIELECTRIC: return dielectric_scatter(m, ino, ind, si, u, uv0, uv1);
@@ -673,7 +736,7 @@ __device__ __forceinline__ Bxdf mat_scatter(int mid, f3 ino, f3 ind, const SurfI
     }
 }
 __device__ __forceinline__ f3 mat_f(int mid, f3 ind, const SurfInt& si, f3 dir) {
-    const pt_material& m = S.materials[mid];
+    const pt_material m = mat_rec(mid);
     f3 f;
     float p;
     switch (m.kind) {
@@ -684,7 +747,7 @@ __device__ __forceinline__ f3 mat_f(int mid, f3 ind, const SurfInt& si, f3 dir) 
     }
 }
 __device__ __forceinline__ float mat_pdf(int mid, f3 ind, const SurfInt& si, f3 dir) {
-    const pt_material& m = S.materials[mid];
+    const pt_material m = mat_rec(mid);
     f3 f;
     float p;
     switch (m.kind) {
@@ -1013,6 +1076,18 @@ __device__ int ls_sample(float u) {
     // [guide[b], guide[b + 1]): target >= fl(b / K * total) because u >= b / K
     // and rounding is monotone, and target <= fl((b + 1) / K * total)
     const uint32_t b = min((uint32_t)(u * (float)PT_LS_GUIDE), PT_LS_GUIDE - 1u);
+#if PT_LDS_TABLES
+    if (S.lds_tables & LDS_LS) {  // staged by the calling kernel (stage_tables)
+        uint32_t lo = pt_lds_guide[b], hi = pt_lds_guide[b + 1];
+        while (lo < hi) {
+            uint32_t mid = (lo + hi) >> 1;
+            if (pt_lds_cdf[mid] >= target) hi = mid;
+            else lo = mid + 1;
+        }
+        if (lo >= n) lo = n - 1;
+        return (int)S.sampler_lights[lo];
+    }
+#endif
     uint32_t lo = S.sampler_guide[b], hi = S.sampler_guide[b + 1];
     while (lo < hi) {
         uint32_t mid = (lo + hi) >> 1;

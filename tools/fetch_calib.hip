@@ -10,6 +10,8 @@
 //                  (the BVH4 node step of k_closest_pool)
 //   k_slot_gather  one 48-B primitive slot per lane, 3 x 16-B    48 B / lane
 //                  loads, slots 128-B aligned in pairs of lines  (128-B lines)
+//   k_texel_gather two 8-B loads from two random lines per lane   16 B / lane
+//                  (k_shade's u8 bilinear texel-pair rows)
 // Lanes pick their line through an odd-multiplier bijection of the index, so
 // no line repeats and no index array is read.  Nothing is stored unless a
 // data-dependent test that never holds passes, so the only traffic is the
@@ -106,6 +108,19 @@ __global__ void k_slot_gather(const float4* __restrict__ t, unsigned long long n
     if (s == -1.0f) sink[0] = s;
 }
 
+// k_shade's bilinear lookup into a u8 image (texel_pair_u8): per lane two
+// 8-B loads, one from each of two texel rows, i.e. two random lines with 8 of
+// their 128 B used (known 16 B per lane; the lines moved are 2 x 128 B)
+__global__ void k_texel_gather(const float4* __restrict__ t, unsigned long long n, unsigned long long mask,
+                               unsigned mul, float* sink) {
+    unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint2* r0 = reinterpret_cast<const uint2*>(t + scatter(2 * i, mask, mul) * 8) + (i & 15);
+    const uint2* r1 = reinterpret_cast<const uint2*>(t + scatter(2 * i + 1, mask, mul) * 8) + (i & 15);
+    const uint2 a = *r0, b = *r1;
+    if ((a.x ^ a.y ^ b.x ^ b.y) == 0x12345678u) sink[0] = 1.0f;
+}
+
 int main(int argc, char** argv) {
     const unsigned long long bytes = 4ull << 30;
     const unsigned long long n16 = bytes / 16, lines = bytes / 128, mask = lines - 1;
@@ -149,6 +164,14 @@ int main(int argc, char** argv) {
         CHK(hipEventSynchronize(e1));
         CHK(hipEventElapsedTime(&ms, e0, e1));
         printf("{\"kernel\":\"k_qnode_gather\",\"bytes\":%llu,\"ms\":%.4f}\n", n * 64, ms);
+        CHK(hipEventRecord(e0));
+        hipLaunchKernelGGL(k_texel_gather, dim3((unsigned)((n / 2 + 255) / 256)), dim3(256), 0, 0, t, n / 2, mask,
+                           muls[rep], sink);
+        CHK(hipEventRecord(e1));
+        CHK(hipEventSynchronize(e1));
+        CHK(hipEventElapsedTime(&ms, e0, e1));
+        printf("{\"kernel\":\"k_texel_gather\",\"bytes\":%llu,\"ms\":%.4f,\"lines\":%llu}\n", n / 2 * 16, ms,
+               n / 2 * 2);
         CHK(hipEventRecord(e0));
         hipLaunchKernelGGL(k_node_gather_n<4>, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, 0, t, n / 4, mask,
                            muls[rep], sink);

@@ -67,6 +67,14 @@ def main(out_json):
     res["factor_slot_gather"] = res.get("k_slot_gather", {}).get("factor")
     res["factor_stream"] = res.get("k_stream", {}).get("factor")
     res["factor_qnode_gather"] = res.get("k_qnode_gather", {}).get("factor")
+    # texel rows: FETCH_SIZE per touched line, against the 128-B lines touched
+    tg = res.get("k_texel_gather")
+    if tg:
+        lines = tg["known_bytes"] / 16 * 2
+        tg["fetch_bytes_per_line"] = round(tg["fetch_size_kb_per_dispatch"] * 1024.0 / lines, 1)
+        if "avg_us" in tg:
+            tg["lines_per_us"] = round(lines / tg["avg_us"], 1)
+        res["factor_texel_gather"] = tg["factor"]
     Path(out_json).write_text(json.dumps(res, indent=1, sort_keys=True))
     print(json.dumps(res, indent=1, sort_keys=True))
     del trace_out
