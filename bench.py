@@ -161,9 +161,10 @@ def pmc_traffic(config: str, spp: int, world: int, kernel: str, sha: str):
     node per lane as 8 x 16-B loads, known byte count), WRITE_SIZE is exact
     for 16-B stores (MI355X_MICROARCH.md "HBM").  Returns (bytes|None, info)."""
     import glob
-    calib = _json(ROOT / "profiles" / "r02_fetch_calib.json") or {}
+    cname = "r03_fetch_calib.json" if (ROOT / "profiles" / "r03_fetch_calib.json").exists() else "r02_fetch_calib.json"
+    calib = _json(ROOT / "profiles" / cname) or {}
     factor = calib.get("factor_node_gather")
-    info = {"fetch_factor": factor, "fetch_factor_source": "r02_fetch_calib.json" if factor else None}
+    info = {"fetch_factor": factor, "fetch_factor_source": f"{cname} factor_node_gather" if factor else None}
     for path in sorted(glob.glob(str(ROOT / "profiles" / f"r*_{config}_pmc.json")), reverse=True):
         prof = _json(Path(path))
         if not prof:

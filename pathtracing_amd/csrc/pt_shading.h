@@ -27,8 +27,10 @@ struct SurfInt {  // SurfaceInteraction (Interaction.hpp:36-51)
 __shared__ pt_material pt_lds_mat[PT_LDS_MATS];
 __shared__ pt_texture pt_lds_tex[PT_LDS_TEX];
 __shared__ pt_image pt_lds_img[PT_LDS_IMG];
+#if PT_LDS_TABLES >= 2  // 2: the light sampler's tables too
 __shared__ uint32_t pt_lds_guide[PT_LS_GUIDE + 1];
 __shared__ float pt_lds_cdf[PT_LDS_CDF];
+#endif
 template <class T>
 __device__ __forceinline__ void stage_words(T* dst, const T* src, uint32_t n) {
     static_assert(sizeof(T) % 4 == 0, "word copy");
@@ -45,10 +47,14 @@ __device__ __forceinline__ void stage_tables(bool light_sampler) {
     if (f & LDS_MATS) stage_words(pt_lds_mat, S.materials, S.n_materials);
     if (f & LDS_TEX) stage_words(pt_lds_tex, S.textures, S.n_textures);
     if (f & LDS_IMG) stage_words(pt_lds_img, S.images, S.n_images);
+#if PT_LDS_TABLES >= 2
     if (light_sampler && (f & LDS_LS) && S.light_sampler != PT_LS_UNIFORM && S.n_sampler_lights) {
         stage_words(pt_lds_guide, S.sampler_guide, PT_LS_GUIDE + 1);
         stage_words(pt_lds_cdf, S.sampler_cdf, S.n_sampler_lights);
     }
+#else
+    (void)light_sampler;
+#endif
     __syncthreads();
 #else
     (void)light_sampler;
@@ -1076,7 +1082,7 @@ __device__ int ls_sample(float u) {
     // [guide[b], guide[b + 1]): target >= fl(b / K * total) because u >= b / K
     // and rounding is monotone, and target <= fl((b + 1) / K * total)
     const uint32_t b = min((uint32_t)(u * (float)PT_LS_GUIDE), PT_LS_GUIDE - 1u);
-#if PT_LDS_TABLES
+#if PT_LDS_TABLES >= 2
     if (S.lds_tables & LDS_LS) {  // staged by the calling kernel (stage_tables)
         uint32_t lo = pt_lds_guide[b], hi = pt_lds_guide[b + 1];
         while (lo < hi) {
