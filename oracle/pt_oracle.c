@@ -540,11 +540,50 @@ typedef struct { uint32_t nodes, tris; } work_t;
 static int prim_intersect(const scene_t* S, uint32_t slot, const ray_t* r, float max, si_t* si, work_t* wk);
 static int prim_pred(const scene_t* S, uint32_t slot, const ray_t* r, float max, work_t* wk);
 
+#ifdef ORACLE_WIDE_STATS
+/* Diagnostics build only (tools/wide_stats.py): how many BVH4 node visits a
+ * wide node that absorbs its children's children (greedily by surface area,
+ * up to 8 slots) would save.  A visit of a node its parent absorbed counts in
+ * g_wide[0] (closest) / g_wide[1] (any). */
+static unsigned long long g_wide[2];
+static float child_area(const pt_ref_bvh4_cluster* c, int i) {
+    float dx = c->xmax[i] - c->xmin[i], dy = c->ymax[i] - c->ymin[i], dz = c->zmax[i] - c->zmin[i];
+    return dx * dy + dy * dz + dz * dx;
+}
+static int n_valid(const pt_bvh_desc* B, pt_ref_bvh4_node nd) {
+    const pt_ref_bvh4_cluster* c = &B->clusters[nd.cluster_idx];
+    int v = 0;
+    for (int i = 0; i < 4; i++) v += !(c->children[i].active == 0 && c->children[i].count == 0);
+    return v;
+}
+/* bit i set: child i of the cluster is absorbed */
+static unsigned absorbed(const pt_bvh_desc* B, const pt_ref_bvh4_cluster* c) {
+    int slots = 0, order[4] = {0, 1, 2, 3};
+    for (int i = 0; i < 4; i++) slots += !(c->children[i].active == 0 && c->children[i].count == 0);
+    for (int a = 0; a < 4; a++)
+        for (int b = a + 1; b < 4; b++)
+            if (child_area(c, order[b]) > child_area(c, order[a])) { int t = order[a]; order[a] = order[b]; order[b] = t; }
+    unsigned m = 0;
+    for (int k = 0; k < 4; k++) {
+        int i = order[k];
+        if (c->children[i].active == 0) continue;
+        int v = n_valid(B, c->children[i]);
+        if (slots - 1 + v <= 8) { slots += v - 1; m |= 1u << i; }
+    }
+    return m;
+}
+void oracle_wide_stats(unsigned long long* out) { out[0] = g_wide[0]; out[1] = g_wide[1]; g_wide[0] = g_wide[1] = 0; }
+#endif
+
 /* BVH4::Intersect: ordered closest hit with entry-distance pruning. */
 static int bvh_intersect(const scene_t* S, const pt_bvh_desc* B, const ray_t* r, float* max, si_t* si, work_t* wk) {
     const unsigned signs = ((r->d.z < 0) << 2) | ((r->d.y < 0) << 1) | (r->d.x < 0);
     pt_ref_bvh4_node stack[64];
     float entry[64];
+#ifdef ORACLE_WIDE_STATS
+    unsigned char wflag[64];
+    wflag[0] = 0;
+#endif
     int sp = 0;
     entry[sp] = 0;
     stack[sp++] = B->root;
@@ -555,6 +594,10 @@ static int bvh_intersect(const scene_t* S, const pt_bvh_desc* B, const ray_t* r,
         if (nd.active != 0) {
             const pt_ref_bvh4_cluster* c = &B->clusters[nd.cluster_idx];
             wk->nodes++;
+#ifdef ORACLE_WIDE_STATS
+            g_wide[0] += wflag[sp];
+            const unsigned ab = absorbed(B, c);
+#endif
             float te[4];
             unsigned mask = 0;
             for (int i = 0; i < 4; i++) {
@@ -579,6 +622,9 @@ static int bvh_intersect(const scene_t* S, const pt_bvh_desc* B, const ray_t* r,
                 if (mask & (1u << idx)) {
                     if (sp >= 64) return hit;
                     entry[sp] = te[idx];
+#ifdef ORACLE_WIDE_STATS
+                    wflag[sp] = (ab >> idx) & 1u;
+#endif
                     stack[sp++] = c->children[idx];
                 }
             }
@@ -598,6 +644,10 @@ static int bvh_intersect(const scene_t* S, const pt_bvh_desc* B, const ray_t* r,
 
 static int bvh_pred(const scene_t* S, const pt_bvh_desc* B, const ray_t* r, float max, work_t* wk) {
     pt_ref_bvh4_node stack[64];
+#ifdef ORACLE_WIDE_STATS
+    unsigned char wflag[64];
+    wflag[0] = 0;
+#endif
     int sp = 0;
     stack[sp++] = B->root;
     while (sp) {
@@ -605,6 +655,10 @@ static int bvh_pred(const scene_t* S, const pt_bvh_desc* B, const ray_t* r, floa
         if (nd.active != 0) {
             const pt_ref_bvh4_cluster* c = &B->clusters[nd.cluster_idx];
             wk->nodes++;
+#ifdef ORACLE_WIDE_STATS
+            g_wide[1] += wflag[sp];
+            const unsigned ab = absorbed(B, c);
+#endif
             for (int i = 0; i < 4; i++) {
                 float tx1 = (c->xmin[i] - r->o.x) * r->inv.x, tx2 = (c->xmax[i] - r->o.x) * r->inv.x;
                 float ty1 = (c->ymin[i] - r->o.y) * r->inv.y, ty2 = (c->ymax[i] - r->o.y) * r->inv.y;
@@ -618,6 +672,9 @@ static int bvh_pred(const scene_t* S, const pt_bvh_desc* B, const ray_t* r, floa
                 float tExit = tmaxxy < tmaxz ? tmaxxy : tmaxz;
                 if (tExit >= EPS_SHADOW && tEntry < max && tEntry <= tExit) {
                     if (sp >= 64) return 0;
+#ifdef ORACLE_WIDE_STATS
+                    wflag[sp] = (ab >> i) & 1u;
+#endif
                     stack[sp++] = c->children[i];
                 }
             }

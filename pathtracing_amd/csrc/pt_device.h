@@ -45,6 +45,30 @@ struct alignas(64) DevQNode {
 };
 static_assert(sizeof(DevQNode) == 64, "qnode layout");
 
+// ---- wide node (PT_WIDE, 128 B, one line): cluster i with its largest
+// inner children absorbed (greedily by surface area while at most 8 slots
+// remain), so one step tests the children and the absorbed children's
+// children.  Index-aligned with the clusters (wnodes[i] stands for cluster
+// i; absorbed clusters' own records go unused).  Boxes quantized as DevQNode
+// with one origin / step per axis over the slots; the visit order per
+// octant is the reference's depth-first order (a cluster's LUT order with
+// each absorbed child replaced by its own LUT order): 8 x 3-bit slot indices,
+// first pushed (farthest) in the low bits.
+//   a = origin.xyz, exponents (x | y << 8 | z << 16)
+//   b0 = x lo, x hi, y lo, y hi of slots 0-3 (one byte per slot); b1 = slots 4-7
+//   z = z lo 0-3, z hi 0-3, z lo 4-7, z hi 4-7
+//   child[8] = REF_EMPTY | REF_LEAF|slot | cluster;  order[8] = octant 0..7
+struct alignas(128) DevWNode {
+    float4 a;
+    uint32_t b0[4], b1[4], z[4];
+    uint32_t child[8];
+    uint32_t order[8];
+};
+static_assert(sizeof(DevWNode) == 128, "wnode layout");
+#ifndef PT_WIDE
+#define PT_WIDE 0
+#endif
+
 // ---- primitive slot geometry (48 B): what a leaf test reads.
 // a = v0|Q|center + flags, b = e1|u|radius + index, c = e2|v
 #define GF_KIND 3u
@@ -105,7 +129,8 @@ struct DevScene {
     float bb_lo[3], bb_scale[3];  // scene box: lo and 16 / extent per axis (spatial hit sort)
     const uint32_t* ray_order;    // closest-hit claim order (PT_RENDER_SORT_RAYS), else null
     const DevCluster* nodes;
-    const DevQNode* qnodes;    // the same nodes quantized (null: the scene could not be encoded)
+    const DevQNode* qnodes;    // the same nodes quantized (null: the scene could not be encoded);
+                               // PT_WIDE: DevWNode records (reinterpreted)
     const DevGeom* geom;
     const DevPrimInfo* info;
     uint32_t root;

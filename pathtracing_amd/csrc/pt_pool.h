@@ -264,7 +264,33 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         float te[4];
         uint4 ch;
         uint32_t ow0, ow1;
-        if constexpr (QN) {
+        uint4 ch1 = make_uint4(REF_EMPTY, REF_EMPTY, REF_EMPTY, REF_EMPTY);
+        uint32_t wperm = 0;
+        if constexpr (QN && PT_WIDE) {
+            static_assert(!PT_ENTRY, "wide nodes keep no entry distances");
+            // DevWNode: 8 loads; primitive lanes re-read their slot's first 16 B
+            const float4* __restrict__ q = node_step
+                                               ? reinterpret_cast<const float4*>(
+                                                     reinterpret_cast<const DevWNode*>(S.qnodes) + idx)
+                                               : reinterpret_cast<const float4*>(S.geom + idx);
+            q0 = q[0];
+            q1 = q[1];
+            q2 = q[2];
+            const float4 qz = q[3 * nk], qc0 = q[4 * nk], qc1 = q[5 * nk], qo0 = q[6 * nk], qo1 = q[7 * nk];
+            q3 = q4 = q5 = q0;
+            uint32_t m0, m1;
+            qslab4pe(q0, q1, make_float4(qz.x, qz.y, 0.0f, 0.0f), o, inv, tmax, m0, te);
+            qslab4pe(q0, q2, make_float4(qz.z, qz.w, 0.0f, 0.0f), o, inv, tmax, m1, te);
+            mask = m0 | (m1 << 4);
+            ch = make_uint4(__float_as_uint(qc0.x), __float_as_uint(qc0.y), __float_as_uint(qc0.z),
+                            __float_as_uint(qc0.w));
+            ch1 = make_uint4(__float_as_uint(qc1.x), __float_as_uint(qc1.y), __float_as_uint(qc1.z),
+                             __float_as_uint(qc1.w));
+            const float4 qo = (oct & 4u) ? qo1 : qo0;
+            const float plo = (oct & 1u) ? qo.y : qo.x, phi = (oct & 1u) ? qo.w : qo.z;
+            wperm = __float_as_uint((oct & 2u) ? phi : plo);
+            ow0 = ow1 = 0;
+        } else if constexpr (QN) {
             const float4* __restrict__ q = node_step ? reinterpret_cast<const float4*>(S.qnodes + idx)
                                                      : reinterpret_cast<const float4*>(S.geom + idx);
             q0 = q[0];
@@ -311,8 +337,15 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 perm = (ow >> (8 * (oct & 3))) & 0xFFu;
             }
             uint32_t cand;
-            if (ENT) cand = order_children_e(mask, ch, perm, te, push);
-            else cand = order_children(mask, ch, perm, [&](uint32_t v) { push(v); });
+            if constexpr (QN && PT_WIDE) {
+                // any hit in slot order unless PT_ANY_OCT (identity: slot k at bits 3k)
+                const uint32_t wp = (!ANY || PT_ANY_OCT) ? wperm : 0xFAC688u;
+                cand = order_children8(mask, ch, ch1, wp, [&](uint32_t v) { push(v); });
+            } else if (ENT) {
+                cand = order_children_e(mask, ch, perm, te, push);
+            } else {
+                cand = order_children(mask, ch, perm, [&](uint32_t v) { push(v); });
+            }
             if (node_step) {
                 if (COUNT) wk.nodes++;
                 ref = cand;

@@ -359,18 +359,21 @@ extern "C" uint64_t pt_scene_device_bytes(const pt_ctx* c) { return c ? c->scene
 // bound up, checked with the device's own decode fma(q, step, origin) so the
 // decoded box always contains the reference's float box.  False when the
 // bounds are not finite or no step fits (the scene then keeps full nodes).
-static bool quantize_axis(const float* lo, const float* hi, uint32_t valid, float& org, uint32_t& e8, uint32_t& wlo,
-                          uint32_t& whi) {
-    wlo = 0;
-    whi = 0;
+// N children (4: DevQNode, 8: DevWNode); wlo / whi: 4 bytes per word
+static bool quantize_axis_n(int N, const float* lo, const float* hi, uint32_t valid, float& org, uint32_t& e8,
+                            uint32_t* wlo, uint32_t* whi) {
+    for (int w = 0; w < N / 4; w++) {
+        wlo[w] = 0;
+        whi[w] = 0;
+    }
     if (!valid) {
         org = 0.0f;
         e8 = 127;
-        wlo = 0xFFFFFFFFu;  // empty children: lo 255 > hi 0 (their refs are REF_EMPTY anyway)
+        for (int w = 0; w < N / 4; w++) wlo[w] = 0xFFFFFFFFu;  // empty: lo 255 > hi 0 (refs REF_EMPTY anyway)
         return true;
     }
     float mn = INFINITY, mx = -INFINITY;
-    for (int k = 0; k < 4; k++)
+    for (int k = 0; k < N; k++)
         if (valid >> k & 1) {
             if (!std::isfinite(lo[k]) || !std::isfinite(hi[k])) return false;
             mn = std::min(mn, lo[k]);
@@ -381,9 +384,9 @@ static bool quantize_axis(const float* lo, const float* hi, uint32_t valid, floa
     int k0 = ext > 0 ? (int)std::ceil(std::log2(ext / 255.0)) : -126;
     for (int k = std::max(-126, k0 - 1); k <= 127; k++) {
         const float step = std::ldexp(1.0f, k);
-        uint32_t ql[4] = {255, 255, 255, 255}, qh[4] = {0, 0, 0, 0};
+        uint32_t ql[8] = {255, 255, 255, 255, 255, 255, 255, 255}, qh[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         bool ok = true;
-        for (int c = 0; c < 4 && ok; c++) {
+        for (int c = 0; c < N && ok; c++) {
             if (!(valid >> c & 1)) continue;
             double a = std::floor(((double)lo[c] - (double)org) / step);
             a = std::min(255.0, std::max(0.0, a));
@@ -398,13 +401,117 @@ static bool quantize_axis(const float* lo, const float* hi, uint32_t valid, floa
         }
         if (!ok) continue;
         e8 = (uint32_t)(k + 127);
-        for (int c = 0; c < 4; c++) {
-            wlo |= ql[c] << (8 * c);
-            whi |= qh[c] << (8 * c);
+        for (int c = 0; c < N; c++) {
+            wlo[c / 4] |= ql[c] << (8 * (c % 4));
+            whi[c / 4] |= qh[c] << (8 * (c % 4));
         }
         return true;
     }
     return false;
+}
+static bool quantize_axis(const float* lo, const float* hi, uint32_t valid, float& org, uint32_t& e8, uint32_t& wlo,
+                          uint32_t& whi) {
+    return quantize_axis_n(4, lo, hi, valid, org, e8, &wlo, &whi);
+}
+
+// ---- wide nodes (DevWNode, PT_WIDE): cluster i plus its absorbed children's
+// children.  Slots keep the reference's depth-first visit order per octant.
+static uint32_t wide_octant_perm(const DevCluster& n, int o) {
+    return (n.order[o >> 2] >> (8 * (o & 3))) & 0xFFu;
+}
+static bool build_wnode(const std::vector<DevCluster>& nodes, size_t i, DevWNode& w) {
+    const DevCluster& n = nodes[i];
+    auto inner = [&](uint32_t r) { return r != REF_EMPTY && r < REF_LEAF && r < nodes.size(); };
+    auto nvalid = [&](const DevCluster& m) {
+        int v = 0;
+        for (int k = 0; k < 4; k++) v += m.child[k] != REF_EMPTY;
+        return v;
+    };
+    const float* nb = &n.xmin.x;  // xmin xmax ymin ymax zmin zmax, 4 floats each
+    auto area = [&](int k) {
+        const float dx = nb[4 + k] - nb[k], dy = nb[12 + k] - nb[8 + k], dz = nb[20 + k] - nb[16 + k];
+        return (double)dx * dy + (double)dy * dz + (double)dz * dx;
+    };
+    // absorb inner children, largest surface area first, while the slots fit
+    int slots = nvalid(n);
+    int ord[4] = {0, 1, 2, 3};
+    std::stable_sort(ord, ord + 4, [&](int a, int b) { return area(a) > area(b); });
+    bool absorb[4] = {false, false, false, false};
+    for (int k = 0; k < 4; k++) {
+        const int c = ord[k];
+        if (!inner(n.child[c])) continue;
+        const int v = nvalid(nodes[n.child[c]]);
+        if (slots - 1 + v <= 8) {
+            slots += v - 1;
+            absorb[c] = true;
+        }
+    }
+    // slots: (ref, box) of every kept child and every absorbed child's child
+    uint32_t ref[8];
+    float box[6][8];  // xmin xmax ymin ymax zmin zmax
+    int slot_of[4] = {-1, -1, -1, -1}, slot_of2[4][4];
+    int ns = 0;
+    for (int c = 0; c < 4; c++) {
+        if (n.child[c] == REF_EMPTY) continue;
+        if (!absorb[c]) {
+            slot_of[c] = ns;
+            ref[ns] = n.child[c];
+            for (int a = 0; a < 6; a++) box[a][ns] = nb[4 * a + c];
+            ns++;
+            continue;
+        }
+        const DevCluster& m = nodes[n.child[c]];
+        const float* mb = &m.xmin.x;
+        for (int g = 0; g < 4; g++) {
+            slot_of2[c][g] = -1;
+            if (m.child[g] == REF_EMPTY) continue;
+            slot_of2[c][g] = ns;
+            ref[ns] = m.child[g];
+            for (int a = 0; a < 6; a++) box[a][ns] = mb[4 * a + g];
+            ns++;
+        }
+    }
+    if (ns > 8) return false;
+    uint32_t valid = 0;
+    for (int k = 0; k < ns; k++) valid |= 1u << k;
+    for (int k = ns; k < 8; k++) {
+        ref[k] = REF_EMPTY;
+        for (int a = 0; a < 6; a++) box[a][k] = 0.0f;
+    }
+    float org[3];
+    uint32_t e[3], wl[3][2], wh[3][2];
+    for (int a = 0; a < 3; a++)
+        if (!quantize_axis_n(8, box[2 * a], box[2 * a + 1], valid, org[a], e[a], wl[a], wh[a])) return false;
+    w.a = make_float4(org[0], org[1], org[2], __builtin_bit_cast(float, e[0] | e[1] << 8 | e[2] << 16));
+    w.b0[0] = wl[0][0]; w.b0[1] = wh[0][0]; w.b0[2] = wl[1][0]; w.b0[3] = wh[1][0];
+    w.b1[0] = wl[0][1]; w.b1[1] = wh[0][1]; w.b1[2] = wl[1][1]; w.b1[3] = wh[1][1];
+    w.z[0] = wl[2][0]; w.z[1] = wh[2][0]; w.z[2] = wl[2][1]; w.z[3] = wh[2][1];
+    for (int k = 0; k < 8; k++) w.child[k] = ref[k];
+    // per octant: the cluster's push order (farthest first) with each absorbed
+    // child replaced by its own push order; unused positions point at an
+    // empty slot (or repeat nothing when all 8 are used)
+    for (int o = 0; o < 8; o++) {
+        const uint32_t pn = wide_octant_perm(n, o);
+        int list[8], nl = 0;
+        for (int k = 0; k < 4; k++) {
+            const int c = (pn >> (2 * k)) & 3;
+            if (n.child[c] == REF_EMPTY) continue;
+            if (!absorb[c]) {
+                list[nl++] = slot_of[c];
+                continue;
+            }
+            const uint32_t pm = wide_octant_perm(nodes[n.child[c]], o);
+            for (int j = 0; j < 4; j++) {
+                const int g = (pm >> (2 * j)) & 3;
+                if (slot_of2[c][g] >= 0) list[nl++] = slot_of2[c][g];
+            }
+        }
+        if (nl != ns) return false;
+        uint32_t p = 0;
+        for (int k = 0; k < 8; k++) p |= (uint32_t)(k < nl ? list[k] : 7) << (3 * k);
+        w.order[o] = p;
+    }
+    return true;
 }
 static bool quantize_node(const DevCluster& n, DevQNode& q) {
     uint32_t valid = 0;
@@ -705,11 +812,24 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     if ((st = upload(c, src, n, &dst)) != PT_OK) return st;
     UP(DS.nodes, nodes.data(), nodes.size());
     {
+#if PT_WIDE
+        // wide nodes take the quantized nodes' place (pt_pool.h, PT_WIDE)
+        std::vector<DevWNode> wn(nodes.size());
+        bool ok = true;
+        for (size_t k = 0; k < nodes.size() && ok; k++) ok = build_wnode(nodes, k, wn[k]);
+        c->has_qnodes = ok;
+        if (ok) {
+            const DevWNode* dw = nullptr;
+            UP(dw, wn.data(), wn.size());
+            DS.qnodes = reinterpret_cast<const DevQNode*>(dw);
+        }
+#else
         std::vector<DevQNode> qn(nodes.size());
         bool ok = true;
         for (size_t k = 0; k < nodes.size() && ok; k++) ok = quantize_node(nodes[k], qn[k]);
         c->has_qnodes = ok;
         if (ok) UP(DS.qnodes, qn.data(), qn.size());
+#endif
     }
     UP(DS.geom, geom.data(), geom.size());
     UP(DS.info, info.data(), info.size());

@@ -317,6 +317,27 @@ __device__ __forceinline__ uint32_t order_children_e(uint32_t mask, uint4 ch, ui
     return cand;
 }
 
+// The wide-node form (PT_WIDE): up to 8 slots, perm = 8 x 3-bit slot indices.
+template <class Push>
+__device__ __forceinline__ uint32_t order_children8(uint32_t mask, uint4 c0, uint4 c1, uint32_t perm, Push&& push) {
+    const uint32_t vm = mask & ((uint32_t)(c0.x != REF_EMPTY) | (uint32_t)(c0.y != REF_EMPTY) << 1 |
+                                (uint32_t)(c0.z != REF_EMPTY) << 2 | (uint32_t)(c0.w != REF_EMPTY) << 3 |
+                                (uint32_t)(c1.x != REF_EMPTY) << 4 | (uint32_t)(c1.y != REF_EMPTY) << 5 |
+                                (uint32_t)(c1.z != REF_EMPTY) << 6 | (uint32_t)(c1.w != REF_EMPTY) << 7);
+    uint32_t cand = REF_EMPTY;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint32_t ci = (perm >> (3 * k)) & 7u;
+        const uint4 h = (ci & 4u) ? c1 : c0;
+        const uint32_t lo = (ci & 1u) ? h.y : h.x, hi = (ci & 1u) ? h.w : h.z;
+        const uint32_t c = (ci & 2u) ? hi : lo;
+        const bool v = (vm >> ci) & 1u;
+        if (v && cand != REF_EMPTY) push(cand);
+        cand = v ? c : cand;
+    }
+    return cand;
+}
+
 // ---- instances: the glm matrix helpers (m4_point, m4_dir, normal_matrix,
 // m3_mul, normalize4) live in pt_shading.h (TransformedLight uses them too)
 
