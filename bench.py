@@ -154,17 +154,22 @@ def cpu_baseline(setup, config: str, target_s: float = 15.0):
 
 def pmc_traffic(config: str, spp: int, world: int, kernel: str, sha: str):
     """HBM bytes per launch of `kernel` from a committed rocprofv3 counter
-    summary of this workload AND this build (profiles/r02_<config>_pmc.json,
-    written by tools/profile_r02.sh; `_meta.src_sha` must equal the sources
+    summary of this workload AND this build (profiles/r0*_<config>_pmc.json,
+    written by tools/profile_bench.sh; `_meta.src_sha` must equal the sources
     being benched).  FETCH_SIZE is scaled by the factor calibrated on this
-    kernel's own access pattern (profiles/r02_fetch_calib.json: one 128-B
-    node per lane as 8 x 16-B loads, known byte count), WRITE_SIZE is exact
-    for 16-B stores (MI355X_MICROARCH.md "HBM").  Returns (bytes|None, info)."""
+    kernel's own access pattern (profiles/r03_fetch_calib.json, known byte
+    counts): FETCH_SIZE counts 64 B per touched 128-B line; a full-line read
+    (128-B clusters, `factor_node_gather` 2.0) moves both 64-B halves, a
+    64-B quantized node or a 48-B slot only its half (`factor_qnode_gather`
+    1.0: 1.5x the full-line gather's line rate; HBM3E bursts are 64 B).
+    WRITE_SIZE is exact for 16-B stores (MI355X_MICROARCH.md "HBM").
+    Returns (bytes|None, info)."""
     import glob
     cname = "r03_fetch_calib.json" if (ROOT / "profiles" / "r03_fetch_calib.json").exists() else "r02_fetch_calib.json"
     calib = _json(ROOT / "profiles" / cname) or {}
-    factor = calib.get("factor_node_gather")
-    info = {"fetch_factor": factor, "fetch_factor_source": f"{cname} factor_node_gather" if factor else None}
+    key = "factor_qnode_gather" if kernel.endswith(", true>") else "factor_node_gather"
+    factor = calib.get(key)
+    info = {"fetch_factor": factor, "fetch_factor_source": f"{cname} {key}" if factor else None}
     for path in sorted(glob.glob(str(ROOT / "profiles" / f"r*_{config}_pmc.json")), reverse=True):
         prof = _json(Path(path))
         if not prof:
