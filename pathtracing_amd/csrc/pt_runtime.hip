@@ -1127,11 +1127,12 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     const uint64_t max_floats = (uint64_t)PT_SAMPLE_GIB << 28;
     uint64_t per_s = 3ull * R.npix_work;
     uint32_t s_chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(spp_local, max_floats / per_s));
-    // a chunk's sample ids stay below SHADOW_MLE_BIT: a finished path's
-    // pending shadow record carries [SHADOW_MLE_BIT |] SHADOW_DONE_BIT | sid
-    // (pt_kernels.hip)
-    if ((uint64_t)R.npix_work >= SHADOW_MLE_BIT) return fail(c, PT_ERR_ARG, "film too large for 30-bit sample ids");
-    s_chunk = (uint32_t)std::min<uint64_t>(s_chunk, (SHADOW_MLE_BIT - 1ull) / R.npix_work);
+    // a chunk's sample ids stay below the shadow records' flag bits: a
+    // finished path's pending shadow record carries SHADOW_DONE_BIT | sid, and
+    // VolPath's also SHADOW_MLE_BIT (pt_kernels.hip)
+    const uint64_t sid_limit = rd->integrator == PT_INTEGRATOR_VOLPATH ? SHADOW_MLE_BIT : SHADOW_DONE_BIT;
+    if ((uint64_t)R.npix_work >= sid_limit) return fail(c, PT_ERR_ARG, "film too large for the sample ids");
+    s_chunk = (uint32_t)std::min<uint64_t>(s_chunk, (sid_limit - 1ull) / R.npix_work);
     pt_status st;
     // a device with less free HBM (or a second context on it) gets smaller
     // chunks instead of PT_ERR_OOM
