@@ -253,6 +253,8 @@ __constant__ const uint64_t pt_expf_table[32] = PT_EXPF_TABLE;
 __constant__ const double pt_powf_log2_table[32] = PT_POWF_LOG2_TABLE;
 __device__ __forceinline__ float pow_cr(float x, float y) { return pt_powf_t(x, y, pt_powf_log2_table, pt_expf_table); }
 __device__ __forceinline__ float exp_cr(float x) { return pt_expf_t(x, pt_expf_table); }
+__constant__ const double pt_log_table[256] = PT_LOG_TABLE;
+__device__ __forceinline__ double log_cr(double x) { return pt_log_t(x, pt_log_table); }
 __device__ __forceinline__ float length(f3 a) { return csqrt(dot(a, a)); }
 __device__ __forceinline__ f3 normalize(f3 a) { return a * (1.0f / csqrt(dot(a, a))); }
 __device__ __forceinline__ bool is_zero(f3 a) { return a.x == 0.0f && a.y == 0.0f && a.z == 0.0f; }

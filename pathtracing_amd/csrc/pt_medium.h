@@ -61,7 +61,7 @@ __device__ __forceinline__ f3 medium_tr(const pt_medium& m, float t) {
 __device__ f3 medium_sample(const pt_medium& m, f3 o, f3 d, float t, float u0, float u1, bool& sampled, f3& p) {
     const int ch = (int)(0.0f + 3.0f * u0);
     const float st = ch == 0 ? m.sigma_t[0] : (ch == 1 ? m.sigma_t[1] : m.sigma_t[2]);
-    float sd = (float)(-log(1.0 - (double)u1) / (double)st);
+    float sd = (float)(-log_cr(1.0 - (double)u1) / (double)st);  // glibc's log, restated (pt_libmf.h)
     if (!(sd < t)) sd = t;
     sampled = sd < t;
     if (sampled) p = F3(fma_(sd, d.x, o.x), fma_(sd, d.y, o.y), fma_(sd, d.z, o.z));

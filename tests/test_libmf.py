@@ -1,8 +1,10 @@
-"""The device's expf / acosf / atanf / atan2f / powf
+"""The device's expf / acosf / atanf / atan2f / powf and double log
 (pathtracing_amd/csrc/pt_libmf.h) against the host libm the reference and the
 oracle call: bit-identical on a strided sample of every float, plus random
-(y, x) pairs for atan2f and powf (tools/check_libmf.c; stride 1 is the
-exhaustive run, 0 mismatches of 4.3e9 per function when last run)."""
+(y, x) pairs for atan2f and powf, and log over the medium sampler's inputs
+1 - k 2^-24 and random doubles (tools/check_libmf.c; stride 1 is the
+exhaustive run: 0 mismatches of 4.3e9 per float function, and of all 2^24
+medium inputs + 1e8 random doubles for log, when last run)."""
 import shutil
 import subprocess
 from pathlib import Path

@@ -13,6 +13,7 @@
 #include "../pathtracing_amd/csrc/pt_libmf.h"
 static const uint64_t T[32] = PT_EXPF_TABLE;
 static const double PL[32] = PT_POWF_LOG2_TABLE;
+static const double LT[256] = PT_LOG_TABLE;
 
 static int same(float a, float b) { return memcmp(&a, &b, 4) == 0 || (a != a && b != b); }
 static uint64_t rng_state = 0x9e3779b97f4a7c15ull;
@@ -52,8 +53,25 @@ int main(int argc, char** argv) {
         bad[3] += !same(atan2f(y, x), pt_atan2f(y, x)), tot[3]++;
         if (y != 0.0f) bad[4] += !same(powf(fabsf(x), y), pt_powf_t(fabsf(x), y, PL, T)), tot[4]++;
     }
-    printf("expf %lu/%lu acosf %lu/%lu atanf %lu/%lu atan2f %lu/%lu powf %lu/%lu\n", bad[0], tot[0], bad[1], tot[1], bad[2],
-           tot[2], bad[3], tot[3], bad[4], tot[4]);
+    /* log(1 - u) for every u = k * 2^-24 the medium sampling can draw, and
+     * random positive normal doubles */
+    unsigned long lbad = 0, ltot = 0;
+    for (uint32_t k2 = 0; k2 < (1u << 24); k2 += (stride < 64 ? 1u : stride / 64u)) {
+        const double x = 1.0 - (double)k2 * 0x1p-24;
+        const double a = log(x), b = pt_log_t(x, LT);
+        lbad += memcmp(&a, &b, 8) != 0, ltot++;
+    }
+    for (unsigned long k2 = 0; k2 < npair; k2++) {
+        uint64_t u = ((uint64_t)rnd() << 32) | rnd();
+        u = (u & 0x000fffffffffffffull) | ((uint64_t)(1 + rnd() % 2046) << 52);
+        double x;
+        memcpy(&x, &u, 8);
+        if (k2 & 1) x = 1.0 + (x - floor(x)) * 0x1p-3 - 0x1p-4;  /* near 1 */
+        const double a = log(x), b = pt_log_t(x, LT);
+        lbad += memcmp(&a, &b, 8) != 0, ltot++;
+    }
+    printf("expf %lu/%lu acosf %lu/%lu atanf %lu/%lu atan2f %lu/%lu powf %lu/%lu log %lu/%lu\n", bad[0], tot[0], bad[1],
+           tot[1], bad[2], tot[2], bad[3], tot[3], bad[4], tot[4], lbad, ltot);
     /* the table is libm's own */
     FILE* f = fopen("/usr/lib/x86_64-linux-gnu/libm.so.6", "rb");
     int found = 0;
@@ -64,5 +82,5 @@ int main(int argc, char** argv) {
         for (size_t o = 0; o + 256 <= n && !found; o += 8) found = memcmp(buf + o, T, 256) == 0;
     }
     printf("expf table in libm: %d\n", found);
-    return (bad[0] | bad[1] | bad[2] | bad[3] | bad[4]) != 0;
+    return (bad[0] | bad[1] | bad[2] | bad[3] | bad[4] | lbad) != 0;
 }
