@@ -782,6 +782,19 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
             geom[i].b.y = __builtin_bit_cast(float, s->prims[i].index);
         }
     }
+    // A leaf holding nothing but one BLAS hop (Scene -> Model, Scene.cpp:4-6)
+    // only pushes that BLAS's root: the cluster refers to the root directly,
+    // in the leaf's place, so the traversal visits the same nodes in the same
+    // order one step sooner.
+    for (DevCluster& n : nodes)
+        for (int k = 0; k < 4; k++) {
+            const uint32_t r = n.child[k];
+            if (r == REF_EMPTY || !(r & REF_LEAF) || r >= REF_SPECIAL) continue;
+            const uint32_t slot = r & ~REF_LEAF;
+            if (slot >= s->n_prims || s->prims[slot].kind != PT_PRIM_BLAS) continue;
+            if (!(__builtin_bit_cast(uint32_t, geom[slot].a.w) & GF_LAST)) continue;
+            n.child[k] = __builtin_bit_cast(uint32_t, geom[slot].b.x);
+        }
     std::vector<DevInstance> inst(s->n_instances);
     for (uint32_t k = 0; k < s->n_instances; k++) {
         const pt_instance& I = s->instances[k];
