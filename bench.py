@@ -406,6 +406,9 @@ def main():
                          else per(cst, "tris_closest", "rays_closest"),
                          "gpu_nodes_per_ray": per(cst, "nodes_closest", "rays_closest"),
                          "gpu_tris_per_ray": per(cst, "tris_closest", "rays_closest"),
+                         "gpu_order_frac": (round(rc["frac"] * (128.0 * cst["nodes_closest"] + 48.0 *
+                                                               cst["tris_closest"]) / max(1, cst["rays_closest"])
+                                                  / rc["bytes_per_ray"], 4) if cst else None),
                          "avg_launch_ms": rc["avg_launch_ms"], "launches": rc["launches"],
                          "bytes_per_launch": rc["bytes_per_launch"], "node_layout_bytes": node_bytes,
                          "layout_bytes_per_ray": rc["layout_bytes_per_ray"],
@@ -418,6 +421,12 @@ def main():
             if cst:
                 ra["gpu_nodes_per_ray"] = round(cst["nodes_any"] / max(1, cst["rays_any"]), 2)
                 ra["gpu_tris_per_ray"] = round(cst["tris_any"] / max(1, cst["rays_any"]), 2)
+                # the same 128 B / 48 B pricing over the visits this kernel makes
+                gb = (128.0 * cst["nodes_any"] + 48.0 * cst["tris_any"]) / max(1, cst["rays_any"])
+                ra["gpu_order_frac"] = round(ra["frac"] * gb / ra["bytes_per_ray"], 4)
+                if ra["frac"] > 1.0:
+                    ra["note"] = ("frac above 1: the reference's slot order (BVH.hpp:1099-1102) visits more "
+                                  "nodes than this kernel's octant order; gpu_order_frac prices the visits it makes")
             roof["shadow"] = ra
         out = {
             "metric": "Mrays/s",

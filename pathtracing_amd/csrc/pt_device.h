@@ -18,6 +18,10 @@
 // child order (BVH.hpp:562-738) precomputed per node.  128 bytes, 128-aligned.
 #define REF_EMPTY 0xFFFFFFFFu
 #define REF_LEAF 0x80000000u
+// Quantized-node leaf refs only (DevQNode::child): the leaf holds a BLAS hop,
+// whose test pushes a traversal, so the overlapped traversal (pt_pool.h
+// PT_SPEC) pauses its node side until the leaf is done.  Slots < 2^29.
+#define REF_BLOCK 0x20000000u
 struct alignas(128) DevCluster {
     float4 xmin, xmax, ymin, ymax, zmin, zmax;  // 4 children per component
     uint32_t child[4];                          // REF_EMPTY | REF_LEAF|slot | cluster
@@ -92,6 +96,7 @@ struct alignas(16) DevGeom {
 #define OCT_MASK 7u
 #define OCT_INST 8u   // the lane's ray is in an instance's object space
 #define OCT_HIT 16u   // ... and accepted a hit there
+#define OCT_FOUND 32u // overlapped traversal (pt_pool.h trace_spec): a hit was stored
 #define OCT_SP_SHIFT 8  // ... entered at this stack depth (bits 8-13)
 #define SCR_WORDS 9   // scratch row: world o, d, tmax, length, instance
 struct DevInstance {

@@ -133,28 +133,35 @@ __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, flo
 }
 
 // ------------------------------------------------------------------ traversal kernels
-// Register budget of the pool kernels: PT_POOL_WPE waves per SIMD.  7 (72
-// VGPRs, no hot-path spills) measured +4.5 % on C4 over the unconstrained 76;
-// 8 (64 VGPRs) spills inside the step loop and loses 30 %.
+// Register budget of the pool kernels: waves per SIMD.  Step-per-iteration
+// traversal (trace_pool): 7 (72 VGPRs, no hot-path spills) measured +4.5 %
+// on C4 over the unconstrained 76; 8 (64 VGPRs) spills inside the step loop
+// and loses 30 %.  Overlapped traversal (trace_spec, quantized nodes without
+// instances): 6 (80 VGPRs, no spills); at 7 it spills and loses 3 %
+// (profiles/r03_ab_spec.txt).
 #ifndef PT_POOL_WPE
 #define PT_POOL_WPE 7
 #endif
-#if PT_POOL_WPE
-#define PT_POOL_WAVES __attribute__((amdgpu_waves_per_eu(PT_POOL_WPE, PT_POOL_WPE)))
-#else
-#define PT_POOL_WAVES
+#ifndef PT_SPEC_WPE
+#define PT_SPEC_WPE 6
 #endif
+#define PT_POOL_WAVES_FOR(SPEC_) __attribute__((amdgpu_waves_per_eu((SPEC_) ? PT_SPEC_WPE : PT_POOL_WPE, \
+                                                                    (SPEC_) ? PT_SPEC_WPE : PT_POOL_WPE)))
 // the any-hit pool kernel's own budget (it needs fewer registers: no hit
 // record): 8 waves per SIMD, C4 k_shadow_pool 10.72 -> 10.34 ms per launch
-// over 7 (6: 11.50; profiles/r02_ab_shade.txt)
+// over 7 (6: 11.50; profiles/r02_ab_shade.txt); overlapped: 7 (8 spills,
+// k_shadow_pool +17 %)
 #ifndef PT_SHADOW_WPE
 #define PT_SHADOW_WPE 8
 #endif
-#if PT_SHADOW_WPE
-#define PT_SHADOW_WAVES __attribute__((amdgpu_waves_per_eu(PT_SHADOW_WPE, PT_SHADOW_WPE)))
-#else
-#define PT_SHADOW_WAVES
+#ifndef PT_SPEC_SHADOW_WPE
+#define PT_SPEC_SHADOW_WPE 7
 #endif
+#define PT_SHADOW_WAVES_FOR(SPEC_) \
+    __attribute__((amdgpu_waves_per_eu((SPEC_) ? PT_SPEC_SHADOW_WPE : PT_SHADOW_WPE, \
+                                       (SPEC_) ? PT_SPEC_SHADOW_WPE : PT_SHADOW_WPE)))
+// which pool kernels take trace_spec (pt_pool.h trace_pool's dispatch)
+#define PT_USES_SPEC(INST_, QN_) (PT_SPEC && (QN_) && !(INST_) && !PT_ENTRY && !PT_WIDE)
 // Persistent, refilling traversal (pt_pool.h): grid = resident blocks, rays
 // claimed from the pool counters (zeroed with the queue counters).
 struct ClosestSrc {
@@ -177,7 +184,7 @@ struct ClosestSrc {
 };
 
 template <bool COUNT, bool INST, bool QN>
-__global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES void k_closest_pool(PathSoA P, const uint32_t* __restrict__ nptr,
+__global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES_FOR(PT_USES_SPEC(INST, QN)) void k_closest_pool(PathSoA P, const uint32_t* __restrict__ nptr,
                                                                 float4* __restrict__ hit, uint32_t* __restrict__ pool,
                                                                 uint32_t* __restrict__ ovf, uint32_t* __restrict__ spare,
                                                                 uint32_t* __restrict__ snap,
@@ -231,7 +238,7 @@ struct ShadowSrc {
 };
 
 template <bool COUNT, bool INST, bool QN>
-__global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SHADOW_WAVES void k_shadow_pool(PathSoA next, float* __restrict__ sample_L,
+__global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SHADOW_WAVES_FOR(PT_USES_SPEC(INST, QN)) void k_shadow_pool(PathSoA next, float* __restrict__ sample_L,
                                                                const ShadowRec* __restrict__ sq,
                                                                const uint32_t* __restrict__ nptr,
                                                                uint32_t* __restrict__ pool, uint32_t* __restrict__ ovf,

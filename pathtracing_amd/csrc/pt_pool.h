@@ -31,6 +31,16 @@
 #ifndef PT_POOL_CHECK
 #define PT_POOL_CHECK 0
 #endif
+#ifndef PT_ITER_STATS
+#define PT_ITER_STATS 0
+#endif
+#if PT_ITER_STATS
+// diagnostics builds: per-iteration wave statistics of the pool kernels,
+// [0] iterations [1] refill iterations [2] iterations reaching a step
+// [3] with a node lane [4] with a primitive lane [5] node lane-steps
+// [6] primitive lane-steps [7] lanes popping; the runtime prints them
+__device__ unsigned long long pt_iter[2][8];
+#endif
 #if PT_POOL_CHECK
 // debugging builds: [0] bad refs (popped instead), [1] shade prim out of range,
 // [2] shade saw an unwritten hit, [3] dropped stack pushes; the runtime prints
@@ -83,6 +93,12 @@ __device__ unsigned int pt_diag[4];
 #ifndef PT_QSLAB_ORDERED
 #define PT_QSLAB_ORDERED 1
 #endif
+// Overlapped traversal (trace_spec below) for the quantized-node kernels
+// without instances: C4 1280 -> 1302 Mrays/s at 6 waves per SIMD
+// (profiles/r03_ab_spec.txt)
+#ifndef PT_SPEC
+#define PT_SPEC 1
+#endif
 // overflow words per stack entry per lane (ref + entry distance)
 #define PT_OVF_WORDS 2
 // Stack capacity of the pool kernels.  The reference's stack[32] is undefined
@@ -93,6 +109,232 @@ __device__ unsigned int pt_diag[4];
 #ifndef PT_POOL_STACK
 #define PT_POOL_STACK 48
 #endif
+
+// ---- Overlapped traversal (PT_SPEC).  The pool kernels are VALU-issue bound
+// (C4 k_closest_pool: 84 % of the SIMDs' cycles issue VALU,
+// profiles/r03_valu.txt), and almost every iteration of a wave has both node
+// lanes and primitive lanes (C4: 99.9 % / 97 % of iterations), so it issues
+// the node path and the primitive path while each lane uses one of them.
+// Here a lane keeps two cursors into its own depth-first order: `leaf`, the
+// leaf whose primitives it is testing, and `ref`, the next node after that
+// leaf, and advances both in one iteration (C4: 15 % fewer iterations).
+// Primitives are still tested one at a time in the reference's order
+// (BVH4::Intersect, BVH.hpp:1111-1211); what changes is that a node after the
+// leaf can be tested before the leaf's primitives are all done, against a max
+// not yet shortened by them, so it may visit a node the reference culls (as
+// the quantized boxes already may; a hit there is accepted only if it is at
+// least as near, so the closest hit is the reference's unless two primitives
+// give the very same t).  A leaf holding a BLAS hop (REF_BLOCK) pauses the
+// node side until it is done, so the BLAS root it pushes is visited where the
+// reference visits it.  Any hit: the answer does not depend on the order.
+// In an iteration the node side runs before the primitive side, so no node
+// data is live across the primitive side's out-of-line calls (primitive side
+// first: 13 % slower, spills); a second queued leaf saved 4 % of the
+// iterations and cost 17 % (profiles/r03_ab_spec.txt).
+template <bool ANY, bool COUNT, class Src, int LN>
+__device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, uint32_t* s_ref,
+                           uint32_t* __restrict__ ovf, TraceWork& wk) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t gl = blockIdx.x * PT_TRACE_BLOCK + lane, G = gridDim.x * PT_TRACE_BLOCK;
+    const uint32_t wl = __lane_id();
+    const uint32_t cs = (n + PT_POOL_CHUNKS - 1) / PT_POOL_CHUNKS;
+    const uint32_t home = blockIdx.x % PT_POOL_CHUNKS;
+    uint32_t dead = 0;  // wave-uniform: chunks found empty
+    const uint32_t all_dead = (1u << PT_POOL_CHUNKS) - 1u;
+
+    int ri = -1;
+    f3 o = F3(0, 0, 0), d = F3(0, 0, 0), inv = F3(0, 0, 0);
+    uint32_t oct = 0, ref = REF_EMPTY, leaf = REF_EMPTY;
+    // closest hit: an accepted hit is stored at once (Src::closest), so the
+    // barycentrics and slot need no registers; OCT_FOUND marks that one was
+    float tmax = 0;
+    int sp = 0;
+#if PT_ITER_STATS
+    unsigned long long its[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    auto lead = [&]() { return wl == (uint32_t)(__ffsll((unsigned long long)__ballot(true)) - 1); };
+#define PT_IT(k, v) do { const unsigned long long v_ = (v); if (lead()) its[k] += v_; } while (0)
+#else
+#define PT_IT(k, v) do { } while (0)
+#endif
+    auto push = [&](uint32_t v) {
+        if (sp < PT_POOL_STACK) {
+            if (LN >= PT_POOL_STACK || sp < LN) s_ref[sp * PT_TRACE_BLOCK + lane] = v;
+            else ovf[(size_t)(sp - LN) * G + gl] = v;
+            ++sp;
+        } else {
+            atomicAdd(S.stack_drops, 1u);
+        }
+    };
+    auto pop = [&]() -> uint32_t {
+        --sp;
+        return (LN >= PT_POOL_STACK || sp < LN) ? s_ref[sp * PT_TRACE_BLOCK + lane] : ovf[(size_t)(sp - LN) * G + gl];
+    };
+    auto is_leaf = [](uint32_t r) { return r != REF_EMPTY && (r & REF_LEAF); };
+    for (;;) {
+        PT_IT(0, 1);
+        const uint64_t idle = __ballot(ri < 0);
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+        if (nidle >= PT_REFILL || idle == __ballot(true)) {
+            // claims as in trace_pool
+            uint32_t base = 0, got = 0;
+            PT_IT(1, 1);
+            if (dead != all_dead) {
+                if (wl == 0) {
+                    #pragma unroll 1
+                    for (uint32_t k = 0; k < PT_POOL_CHUNKS; k++) {
+                        const uint32_t c = (home + k) % PT_POOL_CHUNKS;
+                        if ((dead >> c) & 1u) continue;
+                        const uint32_t lo = c * cs, hi = min(n, lo + cs);
+                        const uint32_t old = lo < hi ? atomicAdd(&pool[c * PT_POOL_STRIDE], nidle) : hi;
+                        if (lo + old < hi) {
+                            base = lo + old;
+                            got = min(nidle, hi - base);
+                            break;
+                        }
+                        dead |= 1u << c;
+                    }
+                }
+                base = __builtin_amdgcn_readfirstlane(base);
+                got = __builtin_amdgcn_readfirstlane(got);
+                dead = __builtin_amdgcn_readfirstlane(dead);
+                if (ri < 0) {
+                    const uint32_t k = (uint32_t)__popcll(idle & ((1ull << wl) - 1ull));
+                    if (k < got) {
+                        ri = (int)(base + k);
+                        if (src.load((uint32_t)ri, o, d, tmax)) {
+                            inv = inv_dir(d);
+                            oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
+                            ref = S.root;
+                            leaf = REF_EMPTY;
+                            sp = 0;
+                        } else {
+                            ri = -1;
+                        }
+                    }
+                }
+            }
+            if (got == 0 && dead == all_dead && __ballot(ri >= 0) == 0) break;
+        }
+        if (ri < 0) continue;
+
+        // ---- feed the two cursors from the lane's depth-first order: the
+        // leaf cursor takes the next leaf once free, the node side pops unless
+        // a BLAS-hop leaf is pending (at most two pops: a leaf popped into the
+        // free leaf cursor lets the node side pop once more)
+        if (leaf == REF_EMPTY && is_leaf(ref)) {
+            leaf = ref;
+            ref = REF_EMPTY;
+        }
+        PT_IT(7, __popcll(__ballot(ref == REF_EMPTY && sp > 0)));
+        #pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (ref == REF_EMPTY && sp > 0 && !(leaf != REF_EMPTY && (leaf & REF_BLOCK))) {
+                const uint32_t r = pop();
+                if (leaf == REF_EMPTY && is_leaf(r)) leaf = r;
+                else ref = r;
+            }
+        }
+        if (ref == REF_EMPTY && leaf == REF_EMPTY) {  // sp == 0: no hit (any) / closest result
+            if (ANY) src.any((uint32_t)ri, false);
+            else if (!(oct & OCT_FOUND)) src.closest((uint32_t)ri, tmax, 0.0f, 0.0f, -1);
+            ri = -1;
+            continue;
+        }
+        const bool node_step = ref != REF_EMPTY && !(ref & REF_LEAF);
+        const bool prim_step = leaf != REF_EMPTY;
+#if PT_ITER_STATS
+        {
+            const uint32_t nn = (uint32_t)__popcll(__ballot(node_step)), np = (uint32_t)__popcll(__ballot(prim_step));
+            PT_IT(2, 1);
+            PT_IT(3, nn > 0);
+            PT_IT(4, np > 0);
+            PT_IT(5, nn);
+            PT_IT(6, np);
+        }
+#endif
+        // both cursors' loads issue before either is used: the node (64 B)
+        // and the primitive slot (48 B); a lane without one reads the root /
+        // slot 0 (shared lines, no extra traffic)
+        const uint32_t slot = prim_step ? (leaf & ~(REF_LEAF | REF_BLOCK)) : 0u;
+        const float4* __restrict__ qn = reinterpret_cast<const float4*>(S.qnodes + (node_step ? ref : 0u));
+        const float4* __restrict__ qg = reinterpret_cast<const float4*>(S.geom + slot);
+        const float4 q0 = qn[0], q1 = qn[1], q2 = qn[2], qc = qn[3];
+        const float4 g0 = qg[0], g1 = qg[1], g2 = qg[2];
+        __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink the slot loads past the node side)
+
+        // ---- node side
+        {
+            uint32_t mask;
+            float te[4];
+            qslab4pe(q0, q1, q2, o, inv, tmax, mask, te);
+            if (!node_step) mask = 0;
+            uint32_t perm = 0xE4u;
+            if (!ANY || PT_ANY_OCT) {
+                const uint32_t ow = ((oct >> 2) & 1u) ? __float_as_uint(q2.w) : __float_as_uint(q2.z);
+                perm = (ow >> (8 * (oct & 3))) & 0xFFu;
+            }
+            const uint4 ch = make_uint4(__float_as_uint(qc.x), __float_as_uint(qc.y), __float_as_uint(qc.z),
+                                        __float_as_uint(qc.w));
+            const uint32_t cand = order_children(mask, ch, perm, [&](uint32_t v) { push(v); });
+            if (node_step) {
+                if (COUNT) wk.nodes++;
+                ref = cand;
+            }
+        }
+        // ---- primitive side.  The triangle test runs on every lane (its
+        // result kept only on primitive lanes), so the slot loads are used
+        // outside the branches.
+        {
+            const uint32_t w0 = __float_as_uint(g0.w);
+            const uint32_t kind = w0 & GF_KIND;
+            const bool pred = ANY && !(w0 & GF_PRED_GLM);
+            float bx = 0, by = 0, t = 0;
+            bool tri_hit;
+            if (pred) tri_hit = tri_pred(o, d, xyz(g0), xyz(g1), xyz(g2), tmax);
+            else tri_hit = tri_glm(o, d, xyz(g0), xyz(g1), xyz(g2), bx, by, t) && !(t > tmax || t < PT_EPS);
+            if (prim_step) {
+                bool anyhit = false;
+                const uint32_t next = (w0 & GF_LAST) ? REF_EMPTY : (REF_LEAF | (leaf & REF_BLOCK) | (slot + 1));
+                if (kind == PT_PRIM_TRIANGLE) {
+                    if (COUNT) wk.tris++;
+                    if (tri_hit && (pred || !(w0 & GF_ALPHA) || tri_alpha(slot, bx, by, o, d))) {
+                        if (ANY) {
+                            anyhit = true;
+                        } else {
+                            tmax = t;
+                            oct |= OCT_FOUND;
+                            src.closest((uint32_t)ri, t, bx, by, (int)slot);
+                        }
+                    }
+                } else if (kind == PT_PRIM_BLAS) {
+                    push(__float_as_uint(g1.x));  // the node side is paused (REF_BLOCK): visited next
+                } else {
+                    if (COUNT) wk.tris++;
+                    if (ANY) {
+                        if (other_pred(slot, w0, o, d, tmax)) anyhit = true;
+                    } else {
+                        float t2, a2, b2;
+                        if (other_closest(slot, w0, o, d, tmax, t2, a2, b2)) {
+                            tmax = t2;
+                            oct |= OCT_FOUND;
+                            src.closest((uint32_t)ri, t2, a2, b2, (int)slot);
+                        }
+                    }
+                }
+                leaf = next;
+                if (ANY && anyhit) {  // early exit (BVH.hpp:1104-1105)
+                    src.any((uint32_t)ri, true);
+                    ri = -1;
+                }
+            }
+        }
+    }
+#if PT_ITER_STATS
+    for (int k = 0; k < 8; k++)
+        if (its[k]) atomicAdd(&pt_iter[ANY ? 1 : 0][k], its[k]);
+#endif
+#undef PT_IT
+}
 
 // Src interface:
 //   bool load(uint32_t ri, f3& o, f3& d, float& tmax)   (false: skip this ray)
@@ -107,6 +349,10 @@ template <bool ANY, bool COUNT, class Src, bool POOL = true, bool INST = true,
 __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, uint32_t* s_ref, uint16_t* s_ent,
                            uint32_t* __restrict__ ovf, TraceWork& wk) {
     constexpr bool ENT = PT_ENTRY && !ANY;
+    if constexpr (PT_SPEC && QN && POOL && !INST && !ENT && !PT_WIDE) {
+        trace_spec<ANY, COUNT, Src, LN>(n, pool, src, s_ref, ovf, wk);
+        return;
+    }
     const uint32_t lane = threadIdx.x;
     const uint32_t gl = blockIdx.x * PT_TRACE_BLOCK + lane, G = gridDim.x * PT_TRACE_BLOCK;
     uint32_t* __restrict__ ovf_e = ovf + (size_t)(PT_POOL_STACK - LN) * G;
@@ -122,6 +368,14 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
     int sp = 0, best = -1;
 
     const uint32_t all_dead = (1u << PT_POOL_CHUNKS) - 1u;
+#if PT_ITER_STATS
+    unsigned long long its[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // counted once per wave: by the first active lane of the counting point
+    auto lead = [&]() { return wl == (uint32_t)(__ffsll((unsigned long long)__ballot(true)) - 1); };
+#define PT_IT(k, v) do { const unsigned long long v_ = (v); if (lead()) its[k] += v_; } while (0)
+#else
+#define PT_IT(k, v) do { } while (0)
+#endif
     // pushes beyond PT_POOL_STACK are dropped and counted;
     // e < 0: never dropped at pop (BLAS roots: a fresh traversal, entry 0)
     auto push = [&](uint32_t v, float e = -1.0f) {
@@ -171,6 +425,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             if (__ballot(ri >= 0) == 0) break;
             if (ri < 0) continue;
         }
+        PT_IT(0, 1);
         const uint64_t idle = __ballot(ri < 0);
         const uint32_t nidle = (uint32_t)__popcll(idle);
         if (POOL && (nidle >= PT_REFILL || idle == __ballot(true))) {
@@ -178,6 +433,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             // home chunk or the next non-empty one; no reserve is held, so no
             // wave sits on unstarted rays while others run dry
             uint32_t base = 0, got = 0;
+            PT_IT(1, 1);
             if (dead != all_dead) {
                 if (wl == 0) {
                     #pragma unroll 1
@@ -214,6 +470,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         // (one or two primitives).  Node lanes and primitive lanes issue their
         // loads in the same pass (one memory round trip per step for the whole
         // wave); a leaf continues at ref = REF_LEAF | next slot.
+        PT_IT(7, __popcll(__ballot(ref == REF_EMPTY)));
         if (ref == REF_EMPTY) {
             bool finished = false;
             for (;;) {
@@ -243,7 +500,17 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             continue;
         }
         const bool node_step = !(ref & REF_LEAF);
-        const uint32_t idx = ref & ~REF_LEAF;
+#if PT_ITER_STATS
+        {
+            const uint32_t nn = (uint32_t)__popcll(__ballot(node_step)), np = (uint32_t)__popcll(__ballot(!node_step));
+            PT_IT(2, 1);
+            PT_IT(3, nn > 0);
+            PT_IT(4, np > 0);
+            PT_IT(5, nn);
+            PT_IT(6, np);
+        }
+#endif
+        const uint32_t idx = ref & ~(QN ? REF_LEAF | REF_BLOCK : REF_LEAF);
 #if PT_POOL_CHECK
         if (node_step ? idx >= S.n_nodes : idx >= S.n_prims) {  // debugging builds only
             atomicAdd(&pt_diag[0], 1u);
@@ -413,4 +680,9 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             }
         }
     }
+#if PT_ITER_STATS
+    for (int k = 0; k < 8; k++)
+        if (its[k]) atomicAdd(&pt_iter[ANY ? 1 : 0][k], its[k]);
+#endif
+#undef PT_IT
 }

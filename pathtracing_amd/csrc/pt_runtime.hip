@@ -838,8 +838,18 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
         }
 #else
         std::vector<DevQNode> qn(nodes.size());
-        bool ok = true;
+        bool ok = nodes.size() < REF_BLOCK && s->n_prims < REF_BLOCK;
         for (size_t k = 0; k < nodes.size() && ok; k++) ok = quantize_node(nodes[k], qn[k]);
+        // leaves holding a BLAS hop carry REF_BLOCK (pt_device.h)
+        for (size_t k = 0; k < nodes.size() && ok; k++)
+            for (uint32_t& r : qn[k].child) {
+                if (r == REF_EMPTY || !(r & REF_LEAF) || r >= REF_SPECIAL) continue;
+                for (uint32_t sl = r & ~REF_LEAF; sl < s->n_prims; sl++) {
+                    const uint32_t w = __builtin_bit_cast(uint32_t, geom[sl].a.w);
+                    if ((w & GF_KIND) == PT_PRIM_BLAS) r |= REF_BLOCK;
+                    if (w & GF_LAST) break;
+                }
+            }
         c->has_qnodes = ok;
         if (ok) UP(DS.qnodes, qn.data(), qn.size());
 #endif
@@ -1358,6 +1368,18 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         // iterations queued past the end find zero paths; let them drain
         while (read < issued)
             if ((st = consume()) != PT_OK) return st;
+#if PT_ITER_STATS
+        {
+            unsigned long long it[2][8];
+            HIPCHK(c, hipMemcpyFromSymbol(it, HIP_SYMBOL(pt_iter), sizeof(it)));
+            for (int a = 0; a < 2; a++)
+                fprintf(stderr, "pt_iter %s: iters %llu refill %llu step %llu with_node %llu with_prim %llu "
+                        "node_lanes %llu prim_lanes %llu pops %llu\n", a ? "any" : "closest", it[a][0], it[a][1],
+                        it[a][2], it[a][3], it[a][4], it[a][5], it[a][6], it[a][7]);
+            const unsigned long long z[2][8] = {};
+            HIPCHK(c, hipMemcpyToSymbol(HIP_SYMBOL(pt_iter), z, sizeof(z)));
+        }
+#endif
 #if PT_POOL_CHECK
         {
             unsigned int dg[4];
