@@ -110,11 +110,13 @@ __device__ unsigned int pt_diag[4];
 #define PT_POOL_STACK 48
 #endif
 
-// ---- Overlapped traversal (PT_SPEC).  The pool kernels are VALU-issue bound
-// (C4 k_closest_pool: 84 % of the SIMDs' cycles issue VALU,
-// profiles/r03_valu.txt), and almost every iteration of a wave has both node
-// lanes and primitive lanes (C4: 99.9 % / 97 % of iterations), so it issues
-// the node path and the primitive path while each lane uses one of them.
+// ---- Overlapped traversal (PT_SPEC).  The pool kernels wait on their loads
+// (C4 k_closest_pool: SQ_WAIT_ANY 64 % of wave cycles, VALU issue 42 % busy
+// at 2 cycles per wave64 instruction, profiles/r03_valu.txt): a ray costs
+// about one dependent memory round trip per iteration, and a lane makes one
+// node step or one primitive step per iteration.  Almost every iteration of
+// a wave has both node lanes and primitive lanes (C4: 99.9 % / 97 %), so both
+// paths are issued anyway.
 // Here a lane keeps two cursors into its own depth-first order: `leaf`, the
 // leaf whose primitives it is testing, and `ref`, the next node after that
 // leaf, and advances both in one iteration (C4: 15 % fewer iterations).
