@@ -262,6 +262,9 @@ enum { PT_FILTER_MITCHELL = 0, PT_FILTER_BOX = 1, PT_FILTER_GAUSSIAN = 2 };
                                          * the default for large scenes (pool traversal) */
 #define PT_RENDER_NO_SORT 0x200u        /* no hit sort (shade in path order) */
 #define PT_RENDER_SORT_RAYS 0x400u      /* trace closest-hit rays in origin-cell + octant order */
+#define PT_RENDER_SERIAL_SHADOW 0x800u  /* any-hit rays of a bounce after it, on one stream     */
+#define PT_RENDER_OVERLAP_SHADOW 0x1000u /* ... beside the next bounce's closest-hit rays, on a
+                                         * second stream (pool traversal, no instances)    */
 
 typedef struct pt_render_desc {
     uint32_t integrator;       /* PT_INTEGRATOR_*                               */

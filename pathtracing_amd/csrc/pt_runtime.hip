@@ -27,11 +27,22 @@
 // a chunk find zero paths and return at once)
 #define PT_LAG 4
 #define PT_RING (PT_LAG + 1)
+// Any-hit rays of bounce k on a second stream, beside bounce k+1's closest-hit
+// rays (the two only read the path state; the shading of k+1 waits for them):
+// each persistent pool kernel's draining tail leaves CUs the other fills.
+// Env PT_OVERLAP_SHADOW overrides.
+#ifndef PT_OVERLAP_SHADOW
+#define PT_OVERLAP_SHADOW 0
+#endif
 
 struct pt_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
+    // any-hit rays of bounce k traced on side_stream beside bounce k+1's
+    // closest-hit rays (PT_OVERLAP_SHADOW; see trace's loop)
+    hipStream_t side_stream = nullptr;
+    bool overlap = false;
     std::string err;
     // scene
     std::vector<void*> scene_bufs;
@@ -52,6 +63,7 @@ struct pt_ctx {
     float4* hit = nullptr;
     uint32_t* qcnt = nullptr;
     uint32_t* ovf = nullptr;  // pool traversal stack entries beyond PT_POOL_LDS
+    uint32_t* ovf_any = nullptr;  // the any-hit pool kernel's half of ovf (they may run together)
     uint32_t* scratch = nullptr;  // instance traversal state, SCR_WORDS x scratch_lanes
     uint64_t scratch_lanes = 0;
     ShadowRec* sq = nullptr;
@@ -132,6 +144,16 @@ static pt_status create_dev(pt_ctx** out, int device) {
         return PT_ERR_HIP;
     }
     c->stream = c->own_stream;
+    if (hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking) != hipSuccess) {
+        g_err = "hip init failed";
+        hipStreamDestroy(c->own_stream);
+        delete c;
+        return PT_ERR_HIP;
+    }
+    {
+        const char* ov = getenv("PT_OVERLAP_SHADOW");
+        c->overlap = ov ? atoi(ov) != 0 : PT_OVERLAP_SHADOW != 0;
+    }
     for (hipEvent_t* e = &c->ev[0]; e != &c->ev[0] + 8; ++e)
         if (hipEventCreate(e) != hipSuccess) {
             g_err = "event create failed";
@@ -309,6 +331,7 @@ static void free_work(pt_ctx* c) {
     c->sq = nullptr;
     c->counters = nullptr;
     c->ovf = nullptr;
+    c->ovf_any = nullptr;
     c->cap = 0;
 }
 
@@ -335,6 +358,7 @@ extern "C" void pt_destroy(pt_ctx* c) {
         for (auto& e : r)
             if (e) hipEventDestroy(e);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
+    if (c->side_stream) hipStreamDestroy(c->side_stream);
     delete c;
 }
 
@@ -1008,7 +1032,9 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
         constexpr int ovf_entries = PT_POOL_STACK - std::min({PT_POOL_LDS, PT_POOL_LDS_C, PT_SIMPLE_LDS});
         size_t lanes = (size_t)c->trace_blocks * PT_TRACE_BLOCK;
         if (simple_ovf) lanes = std::max<size_t>(lanes, (n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK * PT_TRACE_BLOCK);
-        AL(c->ovf, lanes * ovf_entries * PT_OVF_WORDS * 4);
+        const size_t half = lanes * ovf_entries * PT_OVF_WORDS;
+        AL(c->ovf, 2 * half * 4);
+        c->ovf_any = c->ovf + half;
     }
 #undef AL
     if (hipMemset(c->qcnt, 0, (3 * SET_WORDS + PT_POOL_WORDS) * 4) != hipSuccess) {
@@ -1246,6 +1272,9 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         HIPCHK(c, hipGetLastError());
         uint32_t issued = 0, read = 0;
         bool drained = false;
+        const bool ovl = ((c->overlap && !(rd->flags & PT_RENDER_SERIAL_SHADOW)) || (rd->flags & PT_RENDER_OVERLAP_SHADOW)) &&
+                         use_pool && !inst && rd->integrator == PT_INTEGRATOR_PATH;  // (instance scratch is per grid lane, shared)
+        hipStream_t sa = ovl ? c->side_stream : sm;  // the any-hit kernel's stream
         // Tail grids: once every camera sample of the chunk has been started
         // (read from the snapshots: the fill, then each iteration's new paths),
         // path counts can only fall, so the count entering the last iteration
@@ -1301,6 +1330,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             uint32_t* spare = set[(i + 2) % 3];
             hipEvent_t* ev = c->rev[i % PT_RING];
             if (timing) HIPCHK(c, hipEventRecord(ev[0], sm));
+            // (overlap: the previous bounce's any-hit kernel may still run on sa)
             if (sort_rays) {  // claim order of this bounce's closest-hit rays: origin cell + octant
                 constexpr int NB = PT_SORT_BINS_SPATIAL;
                 HIPCHK(c, hipMemsetAsync(c->ray_counts, 0, NB * 4, sm));
@@ -1317,6 +1347,9 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                                    c->counters);
             }
             if (timing) HIPCHK(c, hipEventRecord(ev[1], sm));
+            // the hit sort and the shading rewrite the shadow queue, the sample
+            // buffer and the path state the previous any-hit kernel updates
+            if (ovl && i > 0) HIPCHK(c, hipStreamWaitEvent(sm, c->rev[(i - 1) % PT_RING][4], 0));
             if (sort_mat) {  // bin this bounce's paths by hit material (k_sort_*), shade in that order
                 constexpr int NB = PT_SORT_BINS_MATERIAL;
                 HIPCHK(c, hipMemsetAsync(c->sort_counts, 0, NB * 4, sm));
@@ -1347,7 +1380,8 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                 hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_PATH>, gsh, dim3(PT_SHADE_BLOCK), 0, sm, R, cur,
                                    (const uint32_t*)(in + Q_NEXT), (const float4*)c->hit, nxt, c->sample_L,
                                    next_sample, c->sq, out);
-            if (timing) HIPCHK(c, hipEventRecord(ev[2], sm));
+            if (timing || ovl) HIPCHK(c, hipEventRecord(ev[2], sm));
+            if (ovl) HIPCHK(c, hipStreamWaitEvent(sa, ev[2], 0));
             if (rd->integrator == PT_INTEGRATOR_VOLPATH) {
                 // transmittance along the shadow rays: one ray per lane, the grid covers the capacity
                 hipLaunchKernelGGL(count ? k_shadow_tr<true> : k_shadow_tr<false>,
@@ -1356,18 +1390,19 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                                    c->counters);
             } else if (rd->integrator != PT_INTEGRATOR_SIMPLE) {
                 auto ks = pick_shadow(use_pool, qn, inst, count);
-                hipLaunchKernelGGL(ks, ga, dim3(PT_TRACE_BLOCK), 0, sm, nxt, c->sample_L, (const ShadowRec*)c->sq,
-                                   (const uint32_t*)(out + Q_SHADOW), out + Q_WORDS + PT_POOL_WORDS, c->ovf,
-                                   c->counters);
+                hipLaunchKernelGGL(ks, ga, dim3(PT_TRACE_BLOCK), 0, sa, nxt, c->sample_L, (const ShadowRec*)c->sq,
+                                   (const uint32_t*)(out + Q_SHADOW), out + Q_WORDS + PT_POOL_WORDS,
+                                   ovl ? c->ovf_any : c->ovf, c->counters);
             }
             HIPCHK(c, hipGetLastError());
-            HIPCHK(c, hipEventRecord(ev[4], sm));
+            HIPCHK(c, hipEventRecord(ev[4], sa));
             std::swap(cur, nxt);
             ++issued;
         }
         // iterations queued past the end find zero paths; let them drain
         while (read < issued)
             if ((st = consume()) != PT_OK) return st;
+        if (ovl && issued) HIPCHK(c, hipStreamWaitEvent(sm, c->rev[(issued - 1) % PT_RING][4], 0));
 #if PT_ITER_STATS
         {
             unsigned long long it[2][8];

@@ -224,6 +224,26 @@ def test_gpu_sanmiguel_full_size_per_sample_parity(c4_full):
     np.testing.assert_array_equal(L, Lf)
 
 
+def test_gpu_overlapped_any_hit_stream_is_bit_identical(c4_full):
+    """Bounce k's any-hit rays on a second stream beside bounce k+1's
+    closest-hit rays (PT_RENDER_OVERLAP_SHADOW) against one stream
+    (PT_RENDER_SERIAL_SHADOW): the same per-sample Li and the same film, bit
+    for bit, on the full C4 scene (pool traversal)."""
+    setup, integ = c4_full
+    b, e = 192 * 40, 192 * 48
+    Ls = integ.RenderSamples(pixel_begin=b, pixel_end=e, flags=N.PT_RENDER_SERIAL_SHADOW)
+    Lo = integ.RenderSamples(pixel_begin=b, pixel_end=e, flags=N.PT_RENDER_OVERLAP_SHADOW)
+    np.testing.assert_array_equal(Ls, Lo)
+    film = setup.camera.GetFilm()
+    films = []
+    for f in (N.PT_RENDER_SERIAL_SHADOW, N.PT_RENDER_OVERLAP_SHADOW):
+        film.Clear()
+        st = integ.Render(flags=f)
+        films.append((film.accum.copy(), st["rays_any"], st["rays_closest"]))
+    np.testing.assert_array_equal(films[0][0], films[1][0])
+    assert films[0][1:] == films[1][1:]
+
+
 def test_gpu_sanmiguel_full_size_matches_reference_band(c4_full):
     """The full ~10 M-triangle C4 scene against the reference's own per-sample
     Li (tests/golden/c4_band.npz: ref_harness li over pixel rows 40..47 at
