@@ -42,8 +42,19 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 HBM_CONFIGS = ("c4",)
 
 
-def build_setup(config: str, spp: int | None = None):
+def build_setup(config: str, spp: int | None = None, res: str | None = None):
     from pathtracing_amd import scenes
+    if res:  # tests only: the same scene at another film size
+        import inspect
+        w, h = (int(v) for v in res.lower().split("x"))
+        orig = {"c1": scenes.example_1, "c2": scenes.cornell, "c3": scenes.cornell, "c4": scenes.sanmiguel}
+        fn = orig.get(config)
+        if fn is None or "W" not in inspect.signature(fn).parameters:
+            raise SystemExit(f"bench: --res is not supported for {config}")
+        kw = {"W": w, "H": h, "spp": spp or 4}
+        if config in ("c2", "c3"):
+            kw["config"] = config
+        return fn(**kw)
     if config == "c1":
         return scenes.example_1(W=256, H=256, spp=spp or 16)
     if config == "c2":
@@ -167,7 +178,10 @@ def pmc_traffic(config: str, spp: int, world: int, kernel: str, sha: str):
     import glob
     cname = "r03_fetch_calib.json" if (ROOT / "profiles" / "r03_fetch_calib.json").exists() else "r02_fetch_calib.json"
     calib = _json(ROOT / "profiles" / cname) or {}
-    key = "factor_qnode_gather" if kernel.endswith(", true>") else "factor_node_gather"
+    # k_shade's gathers (slots, texel rows, path state) move 64-B halves like
+    # the quantized nodes: FETCH_SIZE counts each touched half once (x 1.0)
+    key = ("factor_qnode_gather" if kernel.startswith("k_shade") or kernel.endswith(", true>")
+           else "factor_node_gather")
     factor = calib.get(key)
     info = {"fetch_factor": factor, "fetch_factor_source": f"{cname} {key}" if factor else None}
     for path in sorted(glob.glob(str(ROOT / "profiles" / f"r*_{config}_pmc.json")), reverse=True):
@@ -190,6 +204,15 @@ def pmc_traffic(config: str, spp: int, world: int, kernel: str, sha: str):
             return None, info
         b = (factor * k["FETCH_SIZE_per_dispatch"] + k.get("WRITE_SIZE_per_dispatch", 0.0)) * 1024.0
         info["traffic_raw_fetch_kb"] = round(k["FETCH_SIZE_per_dispatch"], 1)
+        # what bounds the kernel besides bytes: the share of wave cycles spent
+        # waiting on memory and the L2 hit rate of the same profile
+        if k.get("SQ_WAVE_CYCLES_per_dispatch"):
+            info["wait_ratio"] = round(k["SQ_WAIT_ANY_per_dispatch"] / k["SQ_WAVE_CYCLES_per_dispatch"], 3)
+        hits, miss = k.get("TCC_HIT_sum_per_dispatch"), k.get("TCC_MISS_sum_per_dispatch")
+        if hits is not None and miss is not None and hits + miss > 0:
+            info["l2_hit_rate"] = round(hits / (hits + miss), 3)
+        if k.get("avg_us"):
+            info["profile_avg_launch_ms"] = round(k["avg_us"] / 1e3, 3)
         return round(b), info
     info["traffic_note"] = "no counter profile of this workload"
     return None, info
@@ -216,6 +239,72 @@ def log(msg: str):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+def _shard_arg(v: str | None):
+    if not v:
+        return None
+    i, _, n = v.partition("/")
+    i, n = int(i), int(n)
+    if not (n >= 1 and 0 <= i < n):
+        raise SystemExit(f"bench: bad --shard {v} (want I/N with 0 <= I < N)")
+    return i, n
+
+
+def _load_hook(path: str):
+    """--render-hook: a Python file (test infrastructure, e.g. tests/bench_cpu_hook.py)
+    defining render_shard(setup, shard_index, shard_count, film) -> stats and
+    optionally frame_samples(setup, pixels, samples) -> (n, 3) float32.  It
+    stands in for the HIP library so the CPU suite can drive this script's
+    multi-rank path end to end over gloo; its numbers are not GPU numbers."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_render_hook", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def verify_frame(setup, integ, rank: int, world: int, pairs: int, frame_samples, film=None, seed: int = 0x5EED0B0C):
+    """Untimed check of the frame just timed: per-sample Li of
+    `pairs` (pixel, sample) pairs read back from the frame's own sample buffer
+    (pt_frame_samples) must equal the oracle's Li bit for bit; half the pairs
+    take the shard's highest sample indices (the top of the 31-bit sample-id
+    range of the frame); and the film (rank 0, after the reduce) must be
+    finite with a positive filter weight on every pixel.  The oracle is the
+    checker here, never the thing timed."""
+    import numpy as np
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle
+    W, H = setup.camera.GetFilm().Resolution()
+    spp = setup.spp
+    local = list(range(rank, spp, world))
+    out = {"pairs": 0, "bit_exact": 0}
+    if pairs > 0 and local:
+        rng = np.random.default_rng(seed + rank)
+        half = max(1, pairs // 2)
+        pix = rng.integers(0, W * H, size=2 * half, dtype=np.int64).astype(np.uint32)
+        lo = rng.choice(local, size=half)
+        hi = np.asarray(local[-min(len(local), 8):])[rng.integers(0, min(len(local), 8), size=half)]
+        smp = np.concatenate([lo, hi]).astype(np.uint32)
+        t0 = time.perf_counter()
+        got = np.asarray(frame_samples(pix, smp), np.float32).reshape(-1, 3)
+        want, _ = oracle.li_pairs(integ, pix, smp)
+        same = np.all(got.view(np.uint32) == want.view(np.uint32), axis=1)
+        bad = np.nonzero(~same)[0]
+        out.update({"pairs": int(pix.size), "bit_exact": int(same.sum()), "max_sample": int(smp.max()),
+                    "check_s": round(time.perf_counter() - t0, 2),
+                    "mismatches": [{"pixel": int(pix[k]), "sample": int(smp[k]), "got": got[k].tolist(),
+                                    "want": want[k].tolist()} for k in bad[:4]]})
+    ok = out["pairs"] == out["bit_exact"]
+    if film is not None:
+        import torch
+        out["film_finite"] = bool(torch.isfinite(film).all().item())
+        out["film_weight_positive"] = bool((film[..., 3] > 0).all().item())
+        ok = ok and out["film_finite"] and out["film_weight_positive"]
+    out["ok"] = bool(ok)
+    out["method"] = ("per-sample Li of the timed frame (pt_frame_samples) vs the oracle, bit-exact; "
+                     "film finite with sum w > 0 on every pixel")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -239,6 +328,18 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the instrumented node-count pass")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--shard", default=None,
+                    help="I/N: time only rank I's sample shard of an N-GPU frame on this one GPU (no reduce): "
+                         "the per-rank work of the N-GPU run")
+    ap.add_argument("--bvh", choices=("auto", "host", "device"), default="auto",
+                    help="BVH build of the scene (auto: device build, byte-identical, for >= 1 M primitives)")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="torch.distributed backend for N > 1 (gloo: CPU rehearsal with --render-hook)")
+    ap.add_argument("--render-hook", default=None, help="test only: CPU stand-in renderer (see _load_hook)")
+    ap.add_argument("--save-film", default=None, help="rank 0 writes the reduced film (.npy)")
+    ap.add_argument("--no-verify", action="store_true", help="skip the untimed check of the timed frame")
+    ap.add_argument("--verify-pairs", type=int, default=1024)
+    ap.add_argument("--res", default=None, help="tests only: WxH film of the same scene")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -246,6 +347,7 @@ def main():
 
     import torch
     import torch.distributed as dist
+    from pathtracing_amd import flatten
     from pathtracing_amd import native as N
     from pathtracing_amd.distributed import render_frame
 
@@ -254,28 +356,54 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
+    shard = _shard_arg(args.shard)
+    if shard and world > 1:
+        raise SystemExit("bench: --shard emulates one rank on one GPU (--gpus 1)")
+    hook = _load_hook(args.render_hook) if args.render_hook else None
+    if hook is None and args.backend != "nccl":
+        raise SystemExit("bench: --backend gloo needs --render-hook (the HIP films live in device memory)")
+    cpu_run = hook is not None
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if cpu_run:
+            dist.init_process_group(args.backend)
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group(args.backend, device_id=torch.device("cuda", local))
         assert dist.get_world_size() == args.gpus
     device = local if world > 1 else 0
-    torch.cuda.set_device(device)
+    dev = torch.device("cpu") if cpu_run else torch.device("cuda", device)
+    if not cpu_run:
+        torch.cuda.set_device(device)
 
+    def sync():
+        if not cpu_run:
+            torch.cuda.synchronize(device)
+
+    # large BVHs build on this rank's GPU (byte-identical to the host build,
+    # ~60x faster): every rank builds its own replica without sharing the
+    # host's cores with the other ranks
+    if not cpu_run and args.bvh != "host":
+        flatten.set_bvh_device(device, min_prims=0 if args.bvh == "device" else 1 << 20)
     t_setup = time.perf_counter()
-    setup = build_setup(args.config, args.spp)
+    setup = build_setup(args.config, args.spp, args.res)
     integ = setup.make_integrator()
     W, H = setup.camera.GetFilm().Resolution()
-    film = torch.zeros((H, W, 4), dtype=torch.float64, device=f"cuda:{device}")
-    integ.context(device)  # scene upload
-    torch.cuda.synchronize(device)
+    film = torch.zeros((H, W, 4), dtype=torch.float64, device=dev)
+    if not cpu_run:
+        integ.context(device)  # scene upload
+    sync()
     setup_s = time.perf_counter() - t_setup
+    bvh_build = flatten.last_bvh_build()
     film_reduce = None
-    if world > 1:  # the film reduce through the library's own RCCL communicator
+    if world > 1 and not cpu_run:  # the film reduce through the library's own RCCL communicator
         from pathtracing_amd.distributed import init_film_comm
         film_reduce = ("pt_film_reduce (library RCCL communicator)" if init_film_comm(integ, device)
                        else "torch.distributed.reduce (RCCL)")
+    elif world > 1:
+        film_reduce = f"torch.distributed.reduce ({args.backend}, CPU rehearsal)"
     if rank == 0:
-        log(f"{args.config}: scene + BVH + upload {setup_s:.1f} s, {world} rank(s)")
+        log(f"{args.config}: scene + BVH ({bvh_build}) + upload {setup_s:.1f} s, {world} rank(s)"
+            + (f", emulating shard {shard[0]}/{shard[1]}" if shard else ""))
 
     tflag = {"auto": 0, "pool": N.PT_RENDER_TRAVERSAL_POOL, "simple": N.PT_RENDER_TRAVERSAL_SIMPLE}[args.traversal]
     tflag |= {"auto": 0, "full": N.PT_RENDER_NODES_FULL, "quant": N.PT_RENDER_NODES_QUANTIZED}[args.nodes]
@@ -289,8 +417,20 @@ def main():
         tflag |= N.PT_RENDER_SORT_RAYS
 
     def step(flags=0):
-        # this rank's sample shard into the device film, then the RCCL SUM
-        # reduce of the film onto rank 0 (pathtracing_amd/distributed.py)
+        # this rank's sample shard into the film, then the SUM reduce of the
+        # film onto rank 0 (pathtracing_amd/distributed.py)
+        if shard:  # one emulated rank of an N-GPU frame: its shard, no reduce
+            film.zero_()
+            ctx = integ.context(device)
+            ctx.set_stream(torch.cuda.current_stream(device).cuda_stream)
+            try:
+                return integ.Render(device=device, shard_index=shard[0], shard_count=shard[1],
+                                    film_ptr=film.data_ptr(), flags=flags | tflag,
+                                    paths_in_flight=args.paths_in_flight)
+            finally:
+                ctx.set_stream(None)
+        if cpu_run:
+            return render_frame(integ, film, render_shard=lambda i, n, f: hook.render_shard(setup, i, n, f))
         return render_frame(integ, film, flags=flags | tflag, paths_in_flight=args.paths_in_flight)
 
     for i in range(args.warmup):
@@ -300,18 +440,14 @@ def main():
             log(f"warmup {i + 1}/{args.warmup}: {time.perf_counter() - t0:.2f} s")
     # traversal work per ray (untimed, instrumented pass over the first spp/16
     # samples of every pixel: same scene, same sample stream)
-    bytes_closest = bytes_any = None
     cst = {}
-    if not args.no_count:
+    if not args.no_count and not cpu_run:
         count_spp = max(1, setup.spp // 16)
         integ.sampler.samples = count_spp
         cst = step(N.PT_RENDER_COUNT_NODES)
         integ.sampler.samples = setup.spp
-        bytes_closest = (128.0 * cst["nodes_closest"] + 48.0 * cst["tris_closest"]) / max(1, cst["rays_closest"])
-        if cst["rays_any"]:
-            bytes_any = (128.0 * cst["nodes_any"] + 48.0 * cst["tris_any"]) / cst["rays_any"]
 
-    torch.cuda.synchronize(device)
+    sync()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -321,113 +457,50 @@ def main():
         ts = time.perf_counter()
         st = step(N.PT_RENDER_TIMING)
         for k in totals:
-            totals[k] += st[k]
+            totals[k] += st.get(k, 0)
         if rank == 0:
             log(f"step {i + 1}/{args.steps}: {time.perf_counter() - ts:.2f} s")
-    torch.cuda.synchronize(device)
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
-    rays = torch.tensor([float(totals["rays_closest"] + totals["rays_any"])], dtype=torch.float64,
-                        device=f"cuda:{device}")
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    rays = torch.tensor([float(totals["rays_closest"] + totals["rays_any"])], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(rays, op=dist.ReduceOp.SUM)
     elapsed_max = float(t.item())
     total_rays = float(rays.item())
 
+    # ---- untimed: the check of the frame just timed (every rank: its shard)
+    verified = None
+    if not args.no_verify:
+        if cpu_run:
+            fs = (lambda p, s: hook.frame_samples(setup, p, s)) if hasattr(hook, "frame_samples") else None
+        else:
+            fs = integ.context(device).frame_samples
+        sh_i, sh_n = shard if shard else (rank, world)
+        verified = verify_frame(setup, integ, sh_i, sh_n, args.verify_pairs if fs else 0, fs,
+                                film if rank == 0 and not shard else None)
+        if world > 1:
+            ok = torch.tensor([1 if verified["ok"] else 0, verified["pairs"], verified["bit_exact"]],
+                              dtype=torch.int64, device=dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.SUM)
+            verified["ranks_ok"] = int(ok[0].item())
+            verified["pairs_all_ranks"] = int(ok[1].item())
+            verified["bit_exact_all_ranks"] = int(ok[2].item())
+            verified["ok"] = verified["ranks_ok"] == world
+        if rank == 0:
+            log(f"verify: {verified['bit_exact']}/{verified['pairs']} samples bit-exact, ok={verified['ok']}")
+    if args.save_film and rank == 0:
+        import numpy as np
+        np.save(args.save_film, film.cpu().numpy())
+
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not shard and not cpu_run:
         cpu = cpu_baseline(setup, args.config, args.cpu_seconds)
     if rank == 0:
-        pool = args.traversal == "pool" or (args.traversal == "auto" and args.config in HBM_CONFIGS)
-        quant = pool and args.nodes != "full"
-        q = ", true" if quant else ", false"
-        kname = f"k_closest_pool<false, false{q}>" if pool else "k_closest<false, false>"
-        sname = f"k_shadow_pool<false, false{q}>" if pool else "k_shadow<false, false>"
-        node_bytes = 64.0 if quant else 128.0  # what this kernel's node step reads
-        sha = src_sha()
-
-        def kernel_roof(name, bpr, lbpr, ms, launches, nrays):
-            # bpr: SURVEY §8(d) algorithmic bytes per ray (128 B per node visit,
-            # 48 B per primitive test: the reference's layout); lbpr: the
-            # bytes this kernel's layout reads for the same visits
-            avg_ms = ms / max(1, launches)
-            if bpr is None or avg_ms <= 0:
-                return None
-            launch_bytes = bpr * nrays / max(1, launches)
-            achieved = launch_bytes / (avg_ms * 1e-3) / 1e9
-            layout = lbpr * nrays / max(1, launches) / (avg_ms * 1e-3) / 1e9 if lbpr else None
-            return {"kernel": name, "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "bytes_per_ray": round(bpr, 1), "bytes_per_launch": round(launch_bytes),
-                    "layout_bytes_per_ray": round(lbpr, 1) if lbpr else None,
-                    "layout_achieved": round(layout, 1) if layout else None,
-                    "layout_frac": round(layout / HBM_PEAK_GBS, 4) if layout else None,
-                    "avg_launch_ms": round(avg_ms, 4), "launches": launches}
-
-        # the algorithmic bytes come from the reference's own
-        # visit order (the oracle's BVH4::Intersect / IntersectPred restatement,
-        # entry-distance cull included) over the cpu_baseline sample of the
-        # same frame; the GPU's instrumented count rides beside it (and stands
-        # in when no CPU sample ran, e.g. N > 1)
-        ref_counts = cpu.pop("_counts") if cpu else None
-        count_source = "gpu"
-        if ref_counts and ref_counts["closest"]:
-            bytes_closest = (128.0 * ref_counts["nodes_closest"] + 48.0 * ref_counts["tris_closest"]) / \
-                ref_counts["closest"]
-            if ref_counts["any"]:
-                bytes_any = (128.0 * ref_counts["nodes_any"] + 48.0 * ref_counts["tris_any"]) / ref_counts["any"]
-            count_source = f"oracle reference order ({ref_counts['closest']} closest / {ref_counts['any']} any rays)"
-        lb_closest = lb_any = None
-        if cst:
-            lb_closest = (node_bytes * cst["nodes_closest"] + 48.0 * cst["tris_closest"]) / max(1, cst["rays_closest"])
-            if cst["rays_any"]:
-                lb_any = (node_bytes * cst["nodes_any"] + 48.0 * cst["tris_any"]) / cst["rays_any"]
-
-        rc = kernel_roof(kname, bytes_closest, lb_closest, totals["ms_closest"], totals["launches_closest"],
-                         totals["rays_closest"])
-        ra = kernel_roof(sname, bytes_any, lb_any, totals["ms_any"], totals["launches_any"], totals["rays_any"])
-        traffic, tinfo = pmc_traffic(args.config, setup.spp, world, kname, sha)
-        roof = {"bound": "hbm" if args.config in HBM_CONFIGS else "l2/latency",
-                "achieved": rc["achieved"] if rc else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": rc["frac"] if rc else None, "traffic": traffic,
-                "traffic_frac": (round(traffic / (rc["avg_launch_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                                 if traffic and rc else None),
-                "src_sha": sha, **tinfo}
-        if rc:
-            def per(c, k, n):
-                return round(c[k] / max(1, c[n]), 2) if c else None
-            roof.update({"kernel": kname, "bytes_per_ray": rc["bytes_per_ray"], "count_source": count_source,
-                         "nodes_per_ray": per(ref_counts, "nodes_closest", "closest") if ref_counts
-                         else per(cst, "nodes_closest", "rays_closest"),
-                         "tris_per_ray": per(ref_counts, "tris_closest", "closest") if ref_counts
-                         else per(cst, "tris_closest", "rays_closest"),
-                         "gpu_nodes_per_ray": per(cst, "nodes_closest", "rays_closest"),
-                         "gpu_tris_per_ray": per(cst, "tris_closest", "rays_closest"),
-                         "gpu_order_frac": (round(rc["frac"] * (128.0 * cst["nodes_closest"] + 48.0 *
-                                                               cst["tris_closest"]) / max(1, cst["rays_closest"])
-                                                  / rc["bytes_per_ray"], 4) if cst else None),
-                         "avg_launch_ms": rc["avg_launch_ms"], "launches": rc["launches"],
-                         "bytes_per_launch": rc["bytes_per_launch"], "node_layout_bytes": node_bytes,
-                         "layout_bytes_per_ray": rc["layout_bytes_per_ray"],
-                         "layout_achieved": rc["layout_achieved"], "layout_frac": rc["layout_frac"]})
-        if ra:
-            ra["nodes_per_ray"] = (round(ref_counts["nodes_any"] / max(1, ref_counts["any"]), 2) if ref_counts
-                                   else round(cst["nodes_any"] / max(1, cst["rays_any"]), 2))
-            ra["tris_per_ray"] = (round(ref_counts["tris_any"] / max(1, ref_counts["any"]), 2) if ref_counts
-                                  else round(cst["tris_any"] / max(1, cst["rays_any"]), 2))
-            if cst:
-                ra["gpu_nodes_per_ray"] = round(cst["nodes_any"] / max(1, cst["rays_any"]), 2)
-                ra["gpu_tris_per_ray"] = round(cst["tris_any"] / max(1, cst["rays_any"]), 2)
-                # the same 128 B / 48 B pricing over the visits this kernel makes
-                gb = (128.0 * cst["nodes_any"] + 48.0 * cst["tris_any"]) / max(1, cst["rays_any"])
-                ra["gpu_order_frac"] = round(ra["frac"] * gb / ra["bytes_per_ray"], 4)
-                if ra["frac"] > 1.0:
-                    ra["note"] = ("frac above 1: the reference's slot order (BVH.hpp:1099-1102) visits more "
-                                  "nodes than this kernel's octant order; gpu_order_frac prices the visits it makes")
-            roof["shadow"] = ra
         out = {
             "metric": "Mrays/s",
             "value": round(total_rays / elapsed_max / 1e6, 3),
@@ -441,25 +514,169 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": WORKLOADS.get(args.config, args.config), "width": W, "height": H,
+            "config": {"workload": WORKLOADS.get(args.config, args.config) + (f" (film {args.res}: test)" if args.res else ""), "width": W, "height": H,
                        "spp": setup.spp, "max_depth": setup.max_depth, "integrator": setup.integrator,
-                       "rays_per_step": int(total_rays / args.steps), "parallelism": f"sample-shard x{world}",
+                       "rays_per_step": int(total_rays / args.steps),
+                       "parallelism": (f"one rank's shard {shard[0]}/{shard[1]} (emulated, no reduce)" if shard
+                                       else f"sample-shard x{world}"),
                        "world_size": dist.get_world_size() if world > 1 else 1,
                        "film_reduce": film_reduce,
-                       "setup_s": round(setup_s, 1)},
+                       "setup_s": round(setup_s, 1), "bvh_build": bvh_build},
             # rank 0's per-frame kernel time by class (HIP events on the library's stream)
             "kernel_ms_per_step": {k[3:]: round(totals[k] / args.steps, 1)
                                    for k in ("ms_closest", "ms_any", "ms_shade")},
-            "roofline": roof,
         }
+        if cpu_run:
+            out["renderer"] = "render hook (CPU rehearsal of the multi-rank path; not a GPU measurement)"
+            out["dtype"] = "f64 film / CPU"
+        else:
+            out["roofline"] = roofline(args, setup, world, totals, cst, cpu)
+        if verified is not None:
+            out["verified"] = verified
         if cpu:
             v = out["value"]
             cpu["gpu_over_cpu"] = round(v / cpu["value"], 1)
             cpu["gpu_over_full_host_estimate"] = round(v / cpu["full_host_estimate"]["value"], 1)
+            ref = cpu.get("reference_estimate")
+            if ref:
+                # north_star: >= 100x the reference CPU path on this box's host
+                # cores -- the reference's estimated rate scaled linearly to
+                # every core of the host (an upper bound for the CPU)
+                full = ref["value"] / cpu["cores"] * cpu["affinity"]
+                cpu["north_star_100x"] = {"target": 100.0, "reference_full_host_estimate": round(full, 2),
+                                          "gpu_over_reference_full_host": round(v / full, 1),
+                                          "met": bool(v / full >= 100.0),
+                                          "note": f"reference estimate at {cpu['cores']} threads scaled "
+                                                  f"linearly to {cpu['affinity']} cores"}
             out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def roofline(args, setup, world, totals, cst, cpu):
+    """Per-kernel roofline entries."""
+    pool = args.traversal == "pool" or (args.traversal == "auto" and args.config in HBM_CONFIGS)
+    quant = pool and args.nodes != "full"
+    q = ", true" if quant else ", false"
+    kname = f"k_closest_pool<false, false{q}>" if pool else "k_closest<false, false>"
+    sname = f"k_shadow_pool<false, false{q}>" if pool else "k_shadow<false, false>"
+    node_bytes = 64.0 if quant else 128.0  # what this kernel's node step reads
+    sha = src_sha()
+
+    def per_ray(c, n, t, r):
+        # SURVEY §8(d): 128 B per node visit, 48 B per primitive test
+        return (128.0 * c[n] + 48.0 * c[t]) / max(1, c[r]) if c and c.get(r) else None
+
+    # the reference's visit order: the oracle's BVH4::Intersect / IntersectPred
+    # restatement (entry-distance cull included) over the cpu_baseline sample
+    # of the same frame; the GPU's own instrumented count rides beside it
+    ref_counts = cpu.pop("_counts") if cpu else None
+    ref_c = per_ray(ref_counts, "nodes_closest", "tris_closest", "closest")
+    ref_a = per_ray(ref_counts, "nodes_any", "tris_any", "any")
+    own_c = per_ray(cst, "nodes_closest", "tris_closest", "rays_closest")
+    own_a = per_ray(cst, "nodes_any", "tris_any", "rays_any")
+
+    def entry(name, ref_b, own_b, layout_b, ms, launches, nrays):
+        """frac = algorithmic bytes / launch time / peak, the bytes priced on
+        the FEWER of the two visit counts (the reference's order, or the visits
+        this kernel makes), so it never credits work the kernel skips."""
+        avg_ms = ms / max(1, launches)
+        cands = [b for b in (ref_b, own_b) if b]
+        if not cands or avg_ms <= 0:
+            return None
+        bpr = min(cands)
+        per_launch = nrays / max(1, launches)
+        gbs = lambda b: b * per_launch / (avg_ms * 1e-3) / 1e9  # noqa: E731
+        e = {"kernel": name, "achieved": round(gbs(bpr), 1), "frac": round(gbs(bpr) / HBM_PEAK_GBS, 4),
+             "bytes_per_ray": round(bpr, 1), "priced_on": "reference order" if bpr == ref_b else "own visits",
+             "bytes_per_launch": round(bpr * per_launch), "avg_launch_ms": round(avg_ms, 4), "launches": launches}
+        if ref_b:
+            e["ref_order_bytes_per_ray"] = round(ref_b, 1)
+            e["ref_order_frac"] = round(gbs(ref_b) / HBM_PEAK_GBS, 4)
+        if own_b:
+            e["own_visits_bytes_per_ray"] = round(own_b, 1)
+            e["own_visits_frac"] = round(gbs(own_b) / HBM_PEAK_GBS, 4)
+        if layout_b:
+            e["layout_bytes_per_ray"] = round(layout_b, 1)
+            e["layout_achieved"] = round(gbs(layout_b), 1)
+            e["layout_frac"] = round(gbs(layout_b) / HBM_PEAK_GBS, 4)
+        traffic, info = pmc_traffic(args.config, setup.spp, world, name, sha)
+        e["traffic"] = traffic
+        e.update(info)
+        if traffic:
+            e["traffic_achieved"] = round(traffic / (avg_ms * 1e-3) / 1e9, 1)
+            e["traffic_frac"] = round(e["traffic_achieved"] / HBM_PEAK_GBS, 4)
+        # the bound the counters show: bytes from HBM far below the roofline
+        # while waves wait on memory most of their cycles = load latency
+        # through L2, not bandwidth
+        if args.config not in HBM_CONFIGS:
+            e["bound"] = "l2/latency"
+        elif traffic is None:
+            e["bound"] = "unknown (no counter profile of this build)"
+        elif e["traffic_frac"] < 0.3:
+            e["bound"] = "l2-latency"
+        else:
+            e["bound"] = "hbm"
+        return e
+
+    lb_c = (node_bytes * cst["nodes_closest"] + 48.0 * cst["tris_closest"]) / max(1, cst["rays_closest"]) if cst else None
+    lb_a = ((node_bytes * cst["nodes_any"] + 48.0 * cst["tris_any"]) / cst["rays_any"]
+            if cst and cst.get("rays_any") else None)
+    rc = entry(kname, ref_c, own_c, lb_c, totals["ms_closest"], totals["launches_closest"], totals["rays_closest"])
+    ra = entry(sname, ref_a, own_a, lb_a, totals["ms_any"], totals["launches_any"], totals["rays_any"])
+    roof = {"bound": rc["bound"] if rc else None, "achieved": rc["achieved"] if rc else None, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": rc["frac"] if rc else None, "traffic": rc["traffic"] if rc else None,
+            "src_sha": sha,
+            "count_source": (f"oracle reference order ({ref_counts['closest']} closest / {ref_counts['any']} any rays)"
+                             if ref_counts and ref_counts["closest"] else "gpu")}
+    if rc:
+        for k, v in rc.items():
+            roof.setdefault(k, v)
+        roof["nodes_per_ray"] = round(ref_counts["nodes_closest"] / max(1, ref_counts["closest"]), 2) \
+            if ref_counts else (round(cst["nodes_closest"] / max(1, cst["rays_closest"]), 2) if cst else None)
+        roof["tris_per_ray"] = round(ref_counts["tris_closest"] / max(1, ref_counts["closest"]), 2) \
+            if ref_counts else (round(cst["tris_closest"] / max(1, cst["rays_closest"]), 2) if cst else None)
+        if cst:
+            roof["gpu_nodes_per_ray"] = round(cst["nodes_closest"] / max(1, cst["rays_closest"]), 2)
+            roof["gpu_tris_per_ray"] = round(cst["tris_closest"] / max(1, cst["rays_closest"]), 2)
+        roof["node_layout_bytes"] = node_bytes
+    if ra:
+        if ref_counts:
+            ra["nodes_per_ray"] = round(ref_counts["nodes_any"] / max(1, ref_counts["any"]), 2)
+            ra["tris_per_ray"] = round(ref_counts["tris_any"] / max(1, ref_counts["any"]), 2)
+        if cst:
+            ra["gpu_nodes_per_ray"] = round(cst["nodes_any"] / max(1, cst["rays_any"]), 2)
+            ra["gpu_tris_per_ray"] = round(cst["tris_any"] / max(1, cst["rays_any"]), 2)
+        roof["shadow"] = ra
+    # k_shade: SURVEY §8(d)'s shading bytes per closest-hit ray that hits
+    # (96 B attributes + 32 B material record) + 4*C B per bilinear texel
+    # fetch, counted by the oracle over the cpu_baseline sample
+    shade_name = "k_shade<0>" if setup.integrator == "path" else None
+    if shade_name and ref_counts and ref_counts.get("closest"):
+        bpr = (128.0 * ref_counts["hits"] + ref_counts["tex_bytes"]) / ref_counts["closest"]
+        launches = totals["launches_closest"]
+        avg_ms = totals["ms_shade"] / max(1, launches)
+        if avg_ms > 0:
+            per_launch = totals["rays_closest"] / max(1, launches)
+            ach = bpr * per_launch / (avg_ms * 1e-3) / 1e9
+            sh = {"kernel": shade_name, "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                  "bytes_per_ray": round(bpr, 1),
+                  "hit_fraction": round(ref_counts["hits"] / ref_counts["closest"], 4),
+                  "texel_bytes_per_ray": round(ref_counts["tex_bytes"] / ref_counts["closest"], 1),
+                  "avg_launch_ms": round(avg_ms, 4), "launches": launches,
+                  "pricing": "SURVEY 8(d): (96 B attributes + 32 B material) per hit + 4*C B per bilinear fetch; "
+                             "avg_launch_ms includes the hit sort (HIP events bracket sort + shade)"}
+            traffic, info = pmc_traffic(args.config, setup.spp, world, shade_name, sha)
+            sh["traffic"] = traffic
+            sh.update(info)
+            if traffic:
+                prof_ms = info.get("profile_avg_launch_ms") or avg_ms
+                sh["traffic_achieved"] = round(traffic / (prof_ms * 1e-3) / 1e9, 1)
+                sh["traffic_frac"] = round(sh["traffic_achieved"] / HBM_PEAK_GBS, 4)
+                sh["bound"] = "l2-latency" if sh["traffic_frac"] < 0.3 else "hbm"
+            roof["shade"] = sh
+    return roof
 
 
 if __name__ == "__main__":

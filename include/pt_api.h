@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PT_API_VERSION 4
+#define PT_API_VERSION 5
 
 typedef int32_t pt_status;
 #define PT_OK 0
@@ -335,6 +335,12 @@ int pt_device_count(const pt_ctx* ctx);
 pt_status pt_comm_unique_id(uint8_t* id_out);
 pt_status pt_comm_init_rank(pt_ctx* ctx, int n_ranks, int rank, const uint8_t* id);
 pt_status pt_film_reduce(pt_ctx* ctx, double* film, uint64_t n, int root);
+/* pt_comm_init_rank joins without blocking past PT_COMM_TIMEOUT_S seconds
+ * (env, default 120): if the other ranks never join it aborts and returns
+ * PT_ERR_COMM.  pt_comm_destroy drops the per-process communicator
+ * (ncclCommAbort), e.g. when the ranks disagree on the reduce path, so that
+ * pt_comm_init_rank can run again.  Not for multi-device contexts. */
+pt_status pt_comm_destroy(pt_ctx* ctx);
 void pt_destroy(pt_ctx* ctx);
 const char* pt_last_error(const pt_ctx* ctx);   /* ctx may be NULL          */
 pt_status pt_set_stream(pt_ctx* ctx, void* hip_stream); /* NULL = ctx stream */
@@ -367,6 +373,15 @@ pt_status pt_render_adaptive(pt_ctx* ctx, const pt_camera_desc* cam, const pt_re
  * unfiltered Integrator::Li values behind pt_render; for parity tests. */
 pt_status pt_render_samples(pt_ctx* ctx, const pt_camera_desc* cam, const pt_render_desc* rd, float* out_L,
                             pt_stats* stats);
+/* Check hook of the last fixed-SPP pt_render on this context (first device):
+ * the per-sample radiance that frame splatted into the film, for n (pixel,
+ * sample) pairs -- pixel = y*width + x, sample = the frame's sample index s
+ * (this shard's: s % shard_count == shard_index) -- into out_L[3*i]
+ * (host pointers).  The frame's last sample chunk is kept on the device until
+ * the next render of any kind; PT_ERR_STATE when there is none, PT_ERR_ARG for
+ * a sample outside it.  The unfiltered Integrator::Li values (Integrators.cpp:
+ * 131-257) of the exact frame bench.py times. */
+pt_status pt_frame_samples(pt_ctx* ctx, const uint32_t* pixels, const uint32_t* samples, uint32_t n, float* out_L);
 /* Test hook: rays and hits are host or device pointers (detected). */
 pt_status pt_trace(pt_ctx* ctx, const pt_ray* rays, uint32_t n, int any_hit, pt_hit* hits, pt_stats* stats);
 /* Test hook: closest hit + the SurfaceInteraction the renderer reconstructs

@@ -730,11 +730,22 @@ class HipBackend {
 public:
     Flat flat;
     pt_ctx* ctx = nullptr;  // one context over the frame's GPUs (pt_create(ctx, n, ids))
+    // fallback when RCCL refuses the multi-device context (PT_ERR_COMM): one
+    // context per GPU, the films summed on the host like Film::Merge
+    std::vector<pt_ctx*> singles;
     RenderStats stats;
     std::vector<double> last;  // the reduced accumulation of the last frame
     std::vector<uint32_t> counts;  // samples per pixel of the last frame
 
-    ~HipBackend() { pt_destroy(ctx); }
+    ~HipBackend() { release(); }
+
+    void release() {
+        pt_destroy(ctx);
+        ctx = nullptr;
+        for (pt_ctx* c : singles) pt_destroy(c);
+        singles.clear();
+    }
+    int devices_in_use() const { return ctx ? pt_device_count(ctx) : (int)singles.size(); }
 
     // The scene is flattened once; the context (and its RCCL communicators)
     // is rebuilt when the requested GPU count changes.
@@ -747,12 +758,29 @@ public:
         }
         int devices = 0;
         if (hipcount(&devices) != 0 || devices <= 0) throw std::runtime_error("HipPathIntegrator: no HIP device");
-        const int want = (int)std::max(1u, std::min<unsigned>(n, (unsigned)devices));
-        if (ctx && pt_device_count(ctx) == want) return;
-        pt_destroy(ctx);
-        ctx = nullptr;
-        check(pt_create(&ctx, want, nullptr), "pt_create");
+        int want = (int)std::max(1u, std::min<unsigned>(n, (unsigned)devices));
+        // PT_FORCE_HOST_MERGE=k (tests on a one-GPU box): the fallback below
+        // with k contexts, on GPUs g % devices
+        const char* fm = getenv("PT_FORCE_HOST_MERGE");
+        const int force = fm ? atoi(fm) : 0;
+        if (force > 0) want = force;
+        if ((ctx || !singles.empty()) && devices_in_use() == want) return;
+        release();
         const pt_scene_desc d = flat.desc();
+        const pt_status st = force > 0 ? PT_ERR_COMM : pt_create(&ctx, want, nullptr);
+        if (st == PT_ERR_COMM && (want > 1 || force > 0) && !getenv("PT_NO_HOST_MERGE")) {
+            // RCCL could not join the GPUs: per-GPU contexts, host merge
+            ctx = nullptr;
+            for (int g = 0; g < want; g++) {
+                pt_ctx* c = nullptr;
+                const int id = g % devices;
+                check(pt_create(&c, 1, &id), "pt_create");
+                singles.push_back(c);
+                check(pt_scene_upload(c, &d), "pt_scene_upload", c);
+            }
+            return;
+        }
+        check(st, "pt_create");
         check(pt_scene_upload(ctx, &d), "pt_scene_upload", ctx);
     }
 
@@ -776,7 +804,9 @@ public:
         last.assign(4 * npx, 0.0);
         pt_stats st{};
         auto t0 = std::chrono::steady_clock::now();
-        if (adaptive) {
+        if (!singles.empty()) {
+            render_singles(cd, rd, npx, adaptive, st);
+        } else if (adaptive) {
             counts.assign(npx, 0u);
             check(pt_render_adaptive(ctx, &cd, &rd, last.data(), counts.data(), &st), "pt_render_adaptive", ctx);
         } else {
@@ -804,6 +834,39 @@ public:
 private:
     bool flat_built = false;
     static int hipcount(int* n);
+
+    // The per-GPU fallback: GPU g renders shard g of n (interleaved samples at
+    // fixed SPP, 32x32 tiles when adaptive) on its own host thread into its
+    // own host film; the films and sample counts are summed here.
+    void render_singles(const pt_camera_desc& cd, const pt_render_desc& rd0, size_t npx, bool adaptive,
+                        pt_stats& total) {
+        const uint32_t n = (uint32_t)singles.size();
+        std::vector<std::vector<double>> films(n, std::vector<double>(4 * npx, 0.0));
+        std::vector<std::vector<uint32_t>> cnts(n, std::vector<uint32_t>(adaptive ? npx : 0, 0u));
+        std::vector<pt_stats> st(n);
+        std::vector<pt_status> res(n, PT_OK);
+        std::vector<std::thread> th;
+        for (uint32_t g = 0; g < n; g++)
+            th.emplace_back([&, g] {
+                pt_render_desc rd = rd0;
+                rd.shard_index = g;
+                rd.shard_count = n;
+                res[g] = adaptive ? pt_render_adaptive(singles[g], &cd, &rd, films[g].data(), cnts[g].data(), &st[g])
+                                  : pt_render(singles[g], &cd, &rd, films[g].data(), &st[g]);
+            });
+        for (auto& t : th) t.join();
+        for (uint32_t g = 0; g < n; g++) check(res[g], adaptive ? "pt_render_adaptive" : "pt_render", singles[g]);
+        counts.assign(npx, adaptive ? 0u : rd0.spp);
+        for (uint32_t g = 0; g < n; g++) {
+            for (size_t i = 0; i < 4 * npx; i++) last[i] += films[g][i];
+            if (adaptive)
+                for (size_t i = 0; i < npx; i++) counts[i] += cnts[g][i];
+            total.paths += st[g].paths;
+            total.rays_closest += st[g].rays_closest;
+            total.rays_any += st[g].rays_any;
+        }
+        total.n_devices = n;
+    }
 };
 
 }  // namespace pt

@@ -21,7 +21,7 @@ HIT = np.dtype([("hit", "<i4"), ("t", "<f4"), ("p", "<f4", 3), ("n", "<f4", 3), 
 
 class Counters(C.Structure):
     _fields_ = [(k, C.c_uint64) for k in ("closest", "any", "nodes_closest", "tris_closest", "nodes_any",
-                                          "tris_any", "paths")]
+                                          "tris_any", "paths", "hits", "tex_bytes")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -39,6 +39,7 @@ def lib():
         vp = C.c_void_p
         L.oracle_trace.argtypes = [vp, vp, C.c_uint32, C.c_int, vp]
         L.oracle_li.argtypes = [vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp, C.POINTER(Counters)]
+        L.oracle_li_pairs.argtypes = [vp, vp, vp, vp, vp, C.c_uint32, vp, C.POINTER(Counters)]
         L.oracle_render.argtypes = [vp, vp, vp, vp, C.c_int, C.POINTER(Counters)]
         L.oracle_render_adaptive.argtypes = [vp, vp, vp, vp, vp, C.c_int, C.POINTER(Counters)]
         L.oracle_inf_le.argtypes = [vp, C.c_int, vp, C.c_uint32, vp]
@@ -47,7 +48,7 @@ def lib():
         L.oracle_lights.argtypes = [vp, vp, C.c_uint32, vp]
         L.oracle_filter_table.argtypes = [vp, vp]
         L.oracle_resolve.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp]
-        for f in ("oracle_trace", "oracle_li", "oracle_render", "oracle_bsdf", "oracle_lights",
+        for f in ("oracle_trace", "oracle_li", "oracle_li_pairs", "oracle_render", "oracle_bsdf", "oracle_lights",
                   "oracle_filter_table", "oracle_resolve"):
             getattr(L, f).restype = C.c_int
         _lib = L
@@ -81,6 +82,20 @@ def li(integrator, pixel_begin: int = 0, pixel_end: int = 0, spp: int | None = N
     assert lib().oracle_li(_desc(integrator.flat), C.byref(cam), C.byref(rd), pixel_begin, pixel_end,
                            L.ctypes.data, P.ctypes.data, C.byref(cnt)) == 0
     return L, P, cnt.as_dict()
+
+
+def li_pairs(integrator, pixels: np.ndarray, samples: np.ndarray):
+    """Li (n, 3) float32 of (pixel, sample) pairs, sample = the frame's global
+    sample index (pixel = y * width + x)."""
+    cam, rd = integrator.desc()
+    pix = np.ascontiguousarray(pixels, np.uint32)
+    smp = np.ascontiguousarray(samples, np.uint32)
+    assert pix.shape == smp.shape and pix.ndim == 1
+    L = np.zeros((pix.shape[0], 3), np.float32)
+    cnt = Counters()
+    assert lib().oracle_li_pairs(_desc(integrator.flat), C.byref(cam), C.byref(rd), pix.ctypes.data, smp.ctypes.data,
+                                 pix.shape[0], L.ctypes.data, C.byref(cnt)) == 0
+    return L, cnt.as_dict()
 
 
 def render(integrator, threads: int = 1, shard_index: int = 0, shard_count: int = 1, spp: int | None = None):

@@ -208,6 +208,10 @@ static inline float channel_at(const scene_t* S, const pt_image* im, int x, int 
     if (idx >= S->s->n_texel_bytes) return 0.0f;
     return S->s->texels[idx] / 255.0f;
 }
+/* SURVEY 8(d) shading bytes: 4 texels x C channels x texel size per bilinear
+ * ImageTexture::Evaluate fetch (shading only; the alpha test's fetches are
+ * traversal work).  Per thread, folded into the counters by li_one. */
+static __thread uint64_t tl_tex_bytes;
 static v3 tex_eval(const scene_t* S, int id, const float uv[2]) {
     const pt_texture* t = &S->s->textures[id];
     if (t->kind == PT_TEX_SOLID) return vl(t->value); /* colorScale*albedo, precomputed */
@@ -220,6 +224,7 @@ static v3 tex_eval(const scene_t* S, int id, const float uv[2]) {
     }
     /* ImageTexture::Evaluate (Texture.hpp:143-158) */
     const pt_image* im = &S->s->images[t->image];
+    tl_tex_bytes += 4ull * (uint64_t)im->channels * (im->format == PT_IMAGE_F32 ? 4u : 1u);
     float x = uv[0] * im->width - 0.5f;
     float y = uv[1] * im->height - 0.5f;
     int xi = (int)floorf(x), yi = (int)floorf(y);
@@ -1522,6 +1527,7 @@ static int intersect_counted(const integ_t* I, const ray_t* r, si_t* si) {
     int h = scene_intersect(I->S, r, si, &wk);
     I->cnt->nodes_closest += wk.nodes;
     I->cnt->tris_closest += wk.tris;
+    if (h) I->cnt->hits++;
     return h;
 }
 
@@ -1906,8 +1912,12 @@ static v3 li_one(const integ_t* I, const pt_camera_desc* cam, uint32_t seed, uin
     rng.dim = 0;
     ray_t r = camera_ray(cam, x, y, &rng, px, py);
     I->cnt->paths++;
-    if (I->kind == PT_INTEGRATOR_VOLPATH) return li_volpath(I, r, cam->medium, &rng);
-    return I->simple ? li_simple(I, r, &rng) : li_path(I, r, &rng);
+    tl_tex_bytes = 0;
+    v3 L;
+    if (I->kind == PT_INTEGRATOR_VOLPATH) L = li_volpath(I, r, cam->medium, &rng);
+    else L = I->simple ? li_simple(I, r, &rng) : li_path(I, r, &rng);
+    I->cnt->tex_bytes += tl_tex_bytes;
+    return L;
 }
 
 int oracle_li(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render_desc* rd, uint32_t pb, uint32_t pe,
@@ -1932,6 +1942,28 @@ int oracle_li(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render
                 out_p[2 * k + 1] = py;
             }
         }
+    }
+    return 0;
+}
+
+/* Li of n (pixel, sample) pairs, sample = the frame's global sample index
+ * (the same li_one as oracle_li; Integrators.cpp:131-257 per sample).  The
+ * checker of pt_frame_samples: the exact frame bench.py times. */
+int oracle_li_pairs(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render_desc* rd,
+                    const uint32_t* pix, const uint32_t* smp, uint32_t n, float* out_L, oracle_counters* cnt) {
+    if (!s || !cam || !rd || (n && (!pix || !smp || !out_L))) return -1;
+    scene_t S;
+    scene_init(&S, s);
+    oracle_counters local;
+    memset(&local, 0, sizeof(local));
+    integ_t I = {&S, rd->max_depth, rd->integrator == PT_INTEGRATOR_SIMPLE, cnt ? cnt : &local, rd->integrator};
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t x = pix[i] % (uint32_t)cam->width, y = pix[i] / (uint32_t)cam->width;
+        double px, py;
+        v3 L = li_one(&I, cam, rd->seed, x, y, smp[i], &px, &py);
+        out_L[3 * i] = L.x;
+        out_L[3 * i + 1] = L.y;
+        out_L[3 * i + 2] = L.z;
     }
     return 0;
 }
@@ -2143,6 +2175,8 @@ static void* render_worker(void* arg) {
     J->total.nodes_any += c.nodes_any;
     J->total.tris_any += c.tris_any;
     J->total.paths += c.paths;
+    J->total.hits += c.hits;
+    J->total.tex_bytes += c.tex_bytes;
     pthread_mutex_unlock(&J->mu);
     return NULL;
 }

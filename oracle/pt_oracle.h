@@ -27,6 +27,8 @@ typedef struct oracle_hit {
 
 typedef struct oracle_counters {
     uint64_t closest, any, nodes_closest, tris_closest, nodes_any, tris_any, paths;
+    uint64_t hits;      /* closest-hit queries that hit (shaded: SURVEY 8(d) +96 B +32 B) */
+    uint64_t tex_bytes; /* shading texel bytes: 4 texels x C channels per bilinear fetch */
 } oracle_counters;
 
 int oracle_version(void);
@@ -38,6 +40,9 @@ int oracle_trace(const pt_scene_desc* s, const pt_ray* rays, uint32_t n, int any
  * out_L[(pix*spp + s)*3], out_p[(pix*spp + s)*2] (film position, double). */
 int oracle_li(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render_desc* rd, uint32_t pixel_begin,
               uint32_t pixel_end, float* out_L, double* out_p, oracle_counters* cnt);
+/* Li of n (pixel, sample) pairs: sample = the frame's global sample index. */
+int oracle_li_pairs(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render_desc* rd, const uint32_t* pix,
+                    const uint32_t* smp, uint32_t n, float* out_L, oracle_counters* cnt);
 
 /* Whole-frame render into film_accum (W*H*4 doubles), `threads` pthreads over
  * 32x32 tiles, samples s with s % shard_count == shard_index. */

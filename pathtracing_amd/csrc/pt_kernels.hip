@@ -1307,6 +1307,19 @@ __global__ __launch_bounds__(256) void k_tri_shade(const uint4* __restrict__ tri
     out[t] = r;
 }
 
+// pt_frame_samples: per-sample radiance of the last fixed-SPP frame at the
+// given sample-buffer indices (a check of the frame bench.py timed)
+__global__ __launch_bounds__(256) void k_frame_gather(const float* __restrict__ sample_L,
+                                                     const unsigned long long* __restrict__ idx, uint32_t n,
+                                                     float* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float* L = sample_L + 3ull * idx[i];
+    out[3 * i] = L[0];
+    out[3 * i + 1] = L[1];
+    out[3 * i + 2] = L[2];
+}
+
 __global__ __launch_bounds__(256) void k_resolve(const double* __restrict__ film, uint32_t npx, uint32_t tonemap,
                                                 uint8_t* __restrict__ rgb) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;

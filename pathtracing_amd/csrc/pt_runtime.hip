@@ -98,6 +98,13 @@ struct pt_ctx {
     bool multi = false;  // renders through render_multi (n_devices > 1, or forced for tests)
     ncclComm_t comm = nullptr;
     int comm_ranks = 0, comm_rank = 0;
+    // where the last fixed-SPP frame's final sample chunk lies in sample_L
+    // (pt_frame_samples); cleared by every other use of the buffer
+    struct FrameRec {
+        bool valid = false;
+        uint32_t width = 0, npix = 0, tiled = 0, tiles_x = 0;
+        uint32_t s_lo = 0, s_hi = 0, shard_index = 0, shard_count = 1;
+    } frame;
 };
 
 static pt_status fail(pt_ctx* c, pt_status code, const char* fmt, ...) {
@@ -277,20 +284,61 @@ extern "C" pt_status pt_comm_unique_id(uint8_t* id_out) {
     return PT_OK;
 }
 
+// Non-blocking ncclCommInitRankConfig polled up to a deadline (env
+// PT_COMM_TIMEOUT_S, default 120 s): a rank whose peers never join (one failed
+// before the collective init) aborts its half-built communicator and returns
+// PT_ERR_COMM instead of blocking forever, so the caller's agreement step
+// (pathtracing_amd/distributed.py init_film_comm) is always reached.
 extern "C" pt_status pt_comm_init_rank(pt_ctx* c, int n_ranks, int rank, const uint8_t* id) {
     if (!c || !id || n_ranks < 1 || rank < 0 || rank >= n_ranks) return PT_ERR_ARG;
     if (c->multi) return fail(c, PT_ERR_STATE, "a multi-device context has its communicators");
-    if (c->comm) return fail(c, PT_ERR_STATE, "communicator already initialised");
+    if (c->comm) return fail(c, PT_ERR_STATE, "communicator already initialised (pt_comm_destroy first)");
     HIPCHK(c, hipSetDevice(c->device));
     ncclUniqueId uid;
     memcpy(&uid, id, sizeof(uid));
-    const ncclResult_t r = ncclCommInitRank(&c->comm, n_ranks, uid, rank);
+    double timeout_s = 120.0;
+    if (const char* e = getenv("PT_COMM_TIMEOUT_S")) timeout_s = std::max(1.0, atof(e));
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclComm_t comm = nullptr;
+    ncclResult_t r = ncclCommInitRankConfig(&comm, n_ranks, uid, rank, &cfg);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (r == ncclInProgress && comm) {
+        ncclResult_t a = ncclInProgress;
+        if (ncclCommGetAsyncError(comm, &a) != ncclSuccess) a = ncclInternalError;
+        r = a;
+        if (r != ncclInProgress) break;
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
+            r = ncclInternalError;
+            ncclCommAbort(comm);
+            comm = nullptr;
+            return fail(c, PT_ERR_COMM, "ncclCommInitRank(%d of %d): peers did not join within %.0f s", rank, n_ranks,
+                        timeout_s);
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
     if (r != ncclSuccess) {
-        c->comm = nullptr;
+        if (comm) ncclCommAbort(comm);
         return fail(c, PT_ERR_COMM, "ncclCommInitRank(%d of %d): %s", rank, n_ranks, ncclGetErrorString(r));
     }
+    c->comm = comm;
     c->comm_ranks = n_ranks;
     c->comm_rank = rank;
+    return PT_OK;
+}
+
+// Drops the per-process communicator (ncclCommAbort: safe when its peers are
+// gone or never finished joining), so a later pt_comm_init_rank can rejoin.
+extern "C" pt_status pt_comm_destroy(pt_ctx* c) {
+    if (!c) return PT_ERR_ARG;
+    if (c->multi) return fail(c, PT_ERR_STATE, "a multi-device context owns its communicators");
+    if (c->comm) {
+        hipSetDevice(c->device);
+        ncclCommAbort(c->comm);
+    }
+    c->comm = nullptr;
+    c->comm_ranks = 0;
+    c->comm_rank = 0;
     return PT_OK;
 }
 
@@ -342,6 +390,7 @@ extern "C" void pt_destroy(pt_ctx* c) {
     if (c->comm) ncclCommDestroy(c->comm);
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->side_stream) hipStreamSynchronize(c->side_stream);  // any-hit kernels of an overlapped frame
     free_scene(c);
     free_work(c);
     if (c->scratch) hipFree(c->scratch);
@@ -1127,6 +1176,7 @@ static ShadowFn pick_shadow(bool pool, bool qn, bool inst, bool count) {
 template <class Drive>
 static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, pt_stats* stats, Drive drive) {
     if (pt_status bs = bind_scene(c)) return bs;
+    c->frame.valid = false;  // sample_L is about to be rewritten
     const uint32_t W = (uint32_t)cam->width, H = (uint32_t)cam->height;
     RenderParams R{};
     R.cam = *cam;
@@ -1430,7 +1480,12 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         if (stats) stats->paths += R.chunk_total;
         return PT_OK;
     };
-    if ((st = drive(R, spp_local, s_chunk, trace)) != PT_OK) return st;
+    if ((st = drive(R, spp_local, s_chunk, trace)) != PT_OK) {
+        // an error inside the overlapped loop can leave any-hit kernels queued
+        // on the side stream: let them finish before the caller frees anything
+        hipStreamSynchronize(c->side_stream);
+        return st;
+    }
     HIPCHK(c, hipStreamSynchronize(sm));
     if (stats) {
         unsigned long long hs[CNT_SHARDS * CNT_COUNT], h[CNT_COUNT] = {};
@@ -1545,9 +1600,55 @@ static pt_status render_dev(pt_ctx* c, const pt_camera_desc* cam, const pt_rende
             else
                 hipLaunchKernelGGL(k_gather, dim3((npx + 255) / 256), dim3(256), 0, c->stream, R, c->sample_L, film);
             HIPCHK(c, hipGetLastError());
+            // the chunk stays in sample_L after the frame: pt_frame_samples
+            c->frame = pt_ctx::FrameRec{true, (uint32_t)cam->width, R.npix_work, R.tiled, R.tiles_x,
+                                        R.s_lo, R.s_hi, R.shard_index, R.shard_count};
             return PT_OK;
         }));
     });
+}
+
+// Per-sample radiance of the last fixed-SPP frame (pt_frame_samples): the
+// final sample chunk is still in sample_L, sample-major, pixels in the
+// chunk's work order (8x8 tiles when R.tiled, k_fill's work_pixel).
+extern "C" pt_status pt_frame_samples(pt_ctx* c, const uint32_t* pixels, const uint32_t* samples, uint32_t n,
+                                      float* out_L) {
+    if (!c || (n && (!pixels || !samples || !out_L))) return PT_ERR_ARG;
+    const pt_ctx::FrameRec& f = c->frame;
+    if (!f.valid) return fail(c, PT_ERR_STATE, "no fixed-SPP frame in the sample buffer");
+    if (n == 0) return PT_OK;
+    std::vector<unsigned long long> idx(n);
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t p = pixels[i], s = samples[i];
+        const uint32_t x = p % f.width, y = p / f.width;
+        if (p >= f.npix) return fail(c, PT_ERR_ARG, "pixel %u outside the frame", p);
+        if (s < f.shard_index || (s - f.shard_index) % f.shard_count)
+            return fail(c, PT_ERR_ARG, "sample %u belongs to another shard", s);
+        const uint32_t sl = (s - f.shard_index) / f.shard_count;
+        if (sl < f.s_lo || sl >= f.s_hi) return fail(c, PT_ERR_ARG, "sample %u is not in the last sample chunk", s);
+        const uint32_t pix_i = f.tiled ? (((y >> 3) * f.tiles_x + (x >> 3)) << 6) | ((y & 7u) << 3) | (x & 7u) : p;
+        idx[i] = (unsigned long long)(sl - f.s_lo) * f.npix + pix_i;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    unsigned long long* di = nullptr;
+    float* dout = nullptr;
+    if (hipMalloc((void**)&di, 8ull * n) != hipSuccess) return fail(c, PT_ERR_OOM, "frame samples: index buffer");
+    if (hipMalloc((void**)&dout, 12ull * n) != hipSuccess) {
+        hipFree(di);
+        return fail(c, PT_ERR_OOM, "frame samples: output buffer");
+    }
+    hipError_t e = hipMemcpyAsync(di, idx.data(), 8ull * n, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_frame_gather, dim3((n + 255) / 256), dim3(256), 0, c->stream, (const float*)c->sample_L,
+                           (const unsigned long long*)di, n, dout);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(out_L, dout, 12ull * n, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    hipFree(di);
+    hipFree(dout);
+    if (e != hipSuccess) return fail(c, PT_ERR_HIP, "frame samples: %s", hipGetErrorString(e));
+    return PT_OK;
 }
 
 // TileIntegrator::Render's adaptive loop (Integrators.cpp:55-86), round by

@@ -36,32 +36,57 @@ def local_samples(spp: int, rank: int, world_size: int) -> int:
     return (spp - rank + world_size - 1) // world_size if spp > rank else 0
 
 
+def _agree(flag: bool, device: int, group) -> bool:
+    """True iff `flag` holds on every rank of the group (MIN all-reduce)."""
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32,
+                     device=f"cuda:{device}" if dist.get_backend(group) == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
+
+
 def init_film_comm(integrator, device: int, group=None) -> bool:
     """Give this rank's library context an RCCL communicator over the group's
     ranks (rank 0 draws the id, the group broadcasts it).  Returns False, with
     the reason logged, if RCCL refuses; render_frame then reduces through
-    torch.distributed instead."""
+    torch.distributed instead.
+
+    Every decision is agreed before the next collective step, so no rank
+    enters ncclCommInitRank while another has already given up: (1) all
+    ranks already joined -> done; (2) stale or partial communicators are
+    dropped (pt_comm_destroy); (3) rank 0's id is broadcast and every rank
+    must hold one; (4) the collective init, itself bounded by
+    PT_COMM_TIMEOUT_S inside the library (a rank whose peers never join aborts
+    instead of blocking); (5) all ranks must have succeeded, else every rank
+    drops its communicator and the torch.distributed reduce is used."""
+    import sys
     from .integrator import Context
     rank, n = world() if group is None else (dist.get_rank(group), dist.get_world_size(group))
     ctx = integrator.context(device)
-    if ctx.comm_ranks == n:
+    if _agree(ctx.comm_ranks == n, device, group):
         return True
-    obj = [Context.comm_unique_id() if rank == 0 else None]
+    if ctx.comm_ranks:
+        ctx.comm_destroy()
+    uid = None
+    if rank == 0:
+        try:
+            uid = Context.comm_unique_id()
+        except RuntimeError as e:  # N.NativeError
+            print(f"[distributed] rank 0: no RCCL id ({e}); reducing through torch.distributed",
+                  file=sys.stderr, flush=True)
+    obj = [uid]
     dist.broadcast_object_list(obj, src=0, group=group)
+    if not _agree(obj[0] is not None, device, group):
+        return False
     ok = True
     try:
         ctx.comm_init_rank(n, rank, obj[0])
     except RuntimeError as e:  # N.NativeError
-        import sys
         print(f"[distributed] rank {rank}: library RCCL communicator unavailable ({e}); "
               "reducing through torch.distributed", file=sys.stderr, flush=True)
         ok = False
-    # every rank must agree on the reduce path
-    flag = torch.tensor([1 if ok else 0], dtype=torch.int32,
-                        device=f"cuda:{device}" if dist.get_backend(group) == "nccl" else "cpu")
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
-    if not int(flag.item()):
-        ctx.comm_ranks = 0  # (a communicator some ranks built stays unused)
+    if not _agree(ok, device, group):
+        if ctx.comm_ranks:
+            ctx.comm_destroy()  # a communicator some ranks built stays unusable: drop it
         return False
     return True
 

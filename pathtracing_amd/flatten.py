@@ -233,14 +233,35 @@ class _Registry:
 
 
 # Where model BLASes and the TLAS are built: the host builder (default) or the
-# device build (pt_bvh4_build_device, byte-identical output) on that GPU.
+# device build (pt_bvh4_build_device, byte-identical output) on that GPU for
+# BVHs of at least BVH_DEVICE_MIN primitives (env PT_BVH_DEVICE=<gpu>, or
+# set_bvh_device: bench.py builds C4's 10 M-triangle BLAS on each rank's own
+# GPU in ~0.1 s instead of ~5 s of host cores shared by 8 ranks).
 BVH_DEVICE: Optional[int] = (int(os.environ["PT_BVH_DEVICE"]) if os.environ.get("PT_BVH_DEVICE", "") != ""
                               else None)
+BVH_DEVICE_MIN = 0
+_last_build: list[str] = []
+
+
+def set_bvh_device(device: Optional[int], min_prims: int = 0) -> None:
+    global BVH_DEVICE, BVH_DEVICE_MIN
+    BVH_DEVICE = device
+    BVH_DEVICE_MIN = int(min_prims)
+
+
+def last_bvh_build() -> str:
+    """Where the BVHs of the last flatten were built, e.g. 'device 1 + host 1'."""
+    if not _last_build:
+        return "none"
+    return " + ".join(f"{k} {_last_build.count(k)}" for k in ("device", "host") if k in _last_build)
 
 
 def bvh_build(boxes: np.ndarray):
-    if BVH_DEVICE is None:
+    n = np.asarray(boxes).reshape(-1, 6).shape[0]
+    if BVH_DEVICE is None or n < BVH_DEVICE_MIN:
+        _last_build.append("host")
         return N.bvh4_build(boxes)
+    _last_build.append("device")
     return N.bvh4_build_device(boxes, device=BVH_DEVICE)
 
 
@@ -280,6 +301,7 @@ def instance_bbox(inner: np.ndarray, m: np.ndarray) -> np.ndarray:
 
 
 def flatten_scene(scene: Scene) -> FlatScene:
+    _last_build.clear()
     reg = _Registry()
     top = scene.primitives
     if not top:

@@ -77,6 +77,24 @@ class Context:
         """pt_film_reduce: in-place ncclReduce(SUM) of a device film onto `root`."""
         N.check(self._lib.pt_film_reduce(self.ptr, C.c_void_p(film_ptr), int(n_doubles), int(root)), self.ptr)
 
+    def comm_destroy(self):
+        """pt_comm_destroy: drop this process's film-reduce communicator."""
+        N.check(self._lib.pt_comm_destroy(self.ptr), self.ptr)
+        self.comm_ranks = 0
+
+    def frame_samples(self, pixels: np.ndarray, samples: np.ndarray) -> np.ndarray:
+        """pt_frame_samples: per-sample radiance (n, 3) float32 of the last
+        fixed-SPP frame rendered on this context, for (pixel, sample) pairs
+        (pixel = y * width + x, sample = the frame's sample index)."""
+        pix = np.ascontiguousarray(pixels, np.uint32)
+        smp = np.ascontiguousarray(samples, np.uint32)
+        if pix.shape != smp.shape or pix.ndim != 1:
+            raise ValueError("pixels and samples must be 1-D arrays of one length")
+        out = np.zeros((pix.shape[0], 3), np.float32)
+        N.check(self._lib.pt_frame_samples(self.ptr, pix.ctypes.data, smp.ctypes.data, pix.shape[0], out.ctypes.data),
+                self.ptr)
+        return out
+
     def close(self):
         if self.ptr:
             self._lib.pt_destroy(self.ptr)

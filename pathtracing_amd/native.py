@@ -140,6 +140,7 @@ EXPORTS = [
     "pt_trace", "pt_scene_device_bytes", "pt_bvh4_build", "pt_bvh4_order_table", "pt_film_resolve",
     "pt_mat4_inverse", "pt_bvh4_build_device", "pt_set_node_format", "pt_render_adaptive", "pt_render_samples",
     "pt_texinf_weights", "pt_device_count", "pt_comm_unique_id", "pt_comm_init_rank", "pt_film_reduce",
+    "pt_comm_destroy", "pt_frame_samples",
 ]
 PT_COMM_ID_BYTES = 128
 
@@ -178,6 +179,10 @@ def lib():
     L.pt_comm_init_rank.restype = C.c_int32
     L.pt_film_reduce.argtypes = [vp, vp, C.c_uint64, C.c_int]
     L.pt_film_reduce.restype = C.c_int32
+    L.pt_comm_destroy.argtypes = [vp]
+    L.pt_comm_destroy.restype = C.c_int32
+    L.pt_frame_samples.argtypes = [vp, vp, vp, C.c_uint32, vp]
+    L.pt_frame_samples.restype = C.c_int32
     L.pt_destroy.argtypes = [vp]
     L.pt_destroy.restype = None
     L.pt_last_error.argtypes = [vp]

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_version_and_error_paths_without_device():
     lib = N.lib()
-    assert lib.pt_version() == 4
+    assert lib.pt_version() == 5
     # argument validation never aborts
     assert lib.pt_scene_upload(None, None) == -1
     assert lib.pt_render(None, None, None, None, None) == -1
@@ -44,6 +44,8 @@ def test_version_and_error_paths_without_device():
     assert lib.pt_film_reduce(None, None, 0, 0) == -1
     assert lib.pt_comm_init_rank(None, 1, 0, None) == -1
     assert lib.pt_comm_unique_id(None) == -1
+    assert lib.pt_comm_destroy(None) == -1
+    assert lib.pt_frame_samples(None, None, None, 0, None) == -1
     lib.pt_destroy(None)
     assert isinstance(lib.pt_last_error(None), (bytes, type(None)))
 

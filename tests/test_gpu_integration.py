@@ -29,13 +29,14 @@ HARNESS = ROOT / "oracle" / "_ref" / "hip_harness"
 FILM_MIN = 1.0
 
 
-def _dropin(name_or_setup, tmp_path, *extra):
+def _dropin(name_or_setup, tmp_path, *extra, env=None):
     setup = parity_scenes()[name_or_setup]() if isinstance(name_or_setup, str) else name_or_setup
     pin_random_lights(setup)
     recipe = write_recipe(tmp_path, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
                           setup.max_depth, setup.light_sampler, setup.extra_lights, pin=True)
     out = tmp_path / "o"
-    subprocess.run([str(HARNESS), str(recipe), "hip", str(out), "1", "noref", *extra], check=True, timeout=300)
+    subprocess.run([str(HARNESS), str(recipe), "hip", str(out), "1", "noref", *extra], check=True, timeout=300,
+                   env=env)
     W, H = setup.camera.film.Resolution()
     film = np.fromfile(f"{out}.hipfilm.bin", np.float64).reshape(H, W, 4)
     counts = np.fromfile(f"{out}.hipcounts.bin", np.uint32).reshape(H, W)
@@ -104,3 +105,22 @@ def test_drop_in_envmap_uses_the_references_cell_sums(tmp_path):
     same = np.isclose(film.accum, gpu, rtol=1e-3, atol=1e-6).all(-1).mean()
     record_parity("dropin_vs_python/envmap", "film", same)
     assert same == 1.0, f"{same:.4f} of pixels agree"
+
+
+@pytest.mark.skipif(not HARNESS.exists(), reason="hip_harness not built (needs /root/reference at build time)")
+@pytest.mark.parametrize("mode", ["fixed", "adaptive"])
+def test_drop_in_host_merge_fallback_matches_one_context(mode, tmp_path):
+    """When RCCL refuses the multi-device context (PT_ERR_COMM) the drop-in
+    renders one context per GPU and sums the shard films on the host.  Forced
+    here with three contexts on this box's GPU(s) (PT_FORCE_HOST_MERGE=3):
+    the film equals the one-context film up to summation order, the adaptive
+    sample counts are identical."""
+    import os
+    extra = ("adaptive",) if mode == "adaptive" else ()
+    (tmp_path / "one").mkdir()
+    (tmp_path / "three").mkdir()
+    _, one, c1 = _dropin("cornell_c3", tmp_path / "one", *extra)
+    _, three, c3 = _dropin("cornell_c3", tmp_path / "three", *extra,
+                           env=dict(os.environ, PT_FORCE_HOST_MERGE="3"))
+    np.testing.assert_array_equal(c3, c1)
+    np.testing.assert_allclose(three, one, rtol=1e-9, atol=1e-12)
