@@ -249,7 +249,7 @@ typedef struct pt_camera_desc {
 
 /* PathIntegrator / SimplePathIntegrator / VolPathIntegrator (Integrators.hpp:33-67) */
 enum { PT_INTEGRATOR_PATH = 0, PT_INTEGRATOR_SIMPLE = 1, PT_INTEGRATOR_VOLPATH = 2 };
-enum { PT_FILTER_MITCHELL = 0, PT_FILTER_BOX = 1, PT_FILTER_GAUSSIAN = 2 };
+enum { PT_FILTER_MITCHELL = 0, PT_FILTER_BOX = 1, PT_FILTER_GAUSSIAN = 2, PT_FILTER_LANCZOS = 3 };
 #define PT_RENDER_COUNT_NODES 0x1u  /* instrumented traversal: node/tri counts */
 #define PT_RENDER_TIMING 0x2u       /* per-kernel HIP-event timing into stats   */
 #define PT_RENDER_TRAVERSAL_POOL 0x4u   /* force the persistent refilling traversal */
@@ -273,7 +273,10 @@ typedef struct pt_render_desc {
     uint32_t seed;             /* sample-stream base seed                       */
     uint32_t filter;           /* PT_FILTER_*                                   */
     float filter_radius[2];
-    double filter_params[2];   /* Mitchell b,c | Gaussian sigma                  */
+    double filter_params[2];   /* Mitchell b,c | Gaussian sigma | Lanczos tau and
+                                  the host filter object's Integral() (the
+                                  reference estimates it with unseeded jitter,
+                                  Filter.hpp:130-143, so the caller passes it) */
     uint32_t shard_index;      /* this call renders samples s with             */
     uint32_t shard_count;      /*   s % shard_count == shard_index              */
     uint32_t flags;            /* PT_RENDER_*                                   */

@@ -138,6 +138,7 @@ PT_MEMBER(FilmFilter, Film, std::shared_ptr<Filter>, filter);
 PT_MEMBER(MitB, MitchellFilter, double, b);
 PT_MEMBER(MitC, MitchellFilter, double, c);
 PT_MEMBER(GaussSigma, GaussianFilter, double, sigma);
+PT_MEMBER(LanczosTau, LanczosFilter, double, tau);
 #ifdef PT_WITH_MODEL
 PT_MEMBER(ModelBvh, Model, std::shared_ptr<BLASBase>, model_bvh);
 #endif
@@ -690,6 +691,13 @@ void filter_desc(const Film& film, pt_render_desc& rd) {
     } else if (auto* g = dynamic_cast<const GaussianFilter*>(f.get())) {
         rd.filter = PT_FILTER_GAUSSIAN;
         rd.filter_params[0] = PT_GET(*g, GaussSigma);
+    } else if (auto* l = dynamic_cast<const LanczosFilter*>(f.get())) {
+        // WindowedSinc x WindowedSinc (Filter.hpp:114-144); the integral is the
+        // object's own estimate (unseeded jitter: one value per call, as the
+        // reference's FilmTile takes one per tile, Film.hpp:59)
+        rd.filter = PT_FILTER_LANCZOS;
+        rd.filter_params[0] = PT_GET(*l, LanczosTau);
+        rd.filter_params[1] = f->Integral();
     } else {
         throw std::runtime_error("HipPathIntegrator: unsupported film filter");
     }

@@ -2015,8 +2015,20 @@ static double mitchell1(double x, double b, double c) {
 static double gauss1(double x, double sigma) {
     return 0.56418958354775628695 / (sigma * 1.41421356237309504880) * exp(-(x * x) / (2 * sigma * sigma));
 }
+/* Sinc / WindowedSinc (Filter.hpp:17-27): LanczosFilter::Evaluate (Filter.hpp:124-126) */
+static double sinc1(double x) {
+    if (1.0 - x * x == 1.0) return 1.0;
+    return sin(3.14159265358979323846 * x) / (3.14159265358979323846 * x);
+}
+static double wsinc1(double x, double radius, double tau) {
+    if (fabs(x) > radius) return 0.0;
+    return sinc1(x) * sinc1(x / tau);
+}
 static double filter_eval(const pt_render_desc* rd, float px, float py) {
     if (rd->filter == PT_FILTER_BOX) return fabsf(px) <= rd->filter_radius[0] && fabsf(py) <= rd->filter_radius[1];
+    if (rd->filter == PT_FILTER_LANCZOS)
+        return wsinc1(px, rd->filter_radius[0], rd->filter_params[0]) *
+               wsinc1(py, rd->filter_radius[1], rd->filter_params[0]);
     if (rd->filter == PT_FILTER_GAUSSIAN) {
         double sg = rd->filter_params[0];
         double X = gauss1(rd->filter_radius[0], sg), Y = gauss1(rd->filter_radius[1], sg);
@@ -2031,6 +2043,7 @@ static double filter_eval(const pt_render_desc* rd, float px, float py) {
 static double filter_integral(const pt_render_desc* rd) {
     float rx = rd->filter_radius[0], ry = rd->filter_radius[1];
     if (rd->filter == PT_FILTER_BOX) return 4 * rx * ry;
+    if (rd->filter == PT_FILTER_LANCZOS) return rd->filter_params[1]; /* the host object's Integral() */
     if (rd->filter == PT_FILTER_GAUSSIAN) {
         double sg = rd->filter_params[0];
         double X = gauss1(rx, sg), Y = gauss1(ry, sg);

@@ -483,6 +483,9 @@ static void read_recipe(World& w, const std::string& path) {
             std::string kind; float rx, ry; s >> kind >> rx >> ry;
             if (kind == "mitchell") { double b, c; s >> b >> c; w.filter = std::make_shared<MitchellFilter>(glm::vec2(rx, ry), b, c); }
             else if (kind == "box") w.filter = std::make_shared<BoxFilter>(glm::vec2(rx, ry));
+#ifdef PT_HARNESS_LANCZOS  // ref_harness_lanczos / hip_harness only: see oracle/Makefile
+            else if (kind == "lanczos") { double tau; s >> tau; w.filter = std::make_shared<LanczosFilter>(glm::vec2(rx, ry), tau); }
+#endif
             else { double sg; s >> sg; w.filter = std::make_shared<GaussianFilter>(glm::vec2(rx, ry), sg); }
         } else if (k == "integrator") {
             s >> w.integ >> w.maxDepth;

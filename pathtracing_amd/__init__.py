@@ -6,7 +6,7 @@ runs as hand-written HIP kernels for gfx950 behind the C ABI of
 include/pt_api.h (libpt_hip.so).  See DESIGN.md.
 """
 from .scene import (AlphaMode, AlphaTester, AreaLight, BoxFilter, Camera, CheckerTexture, DistantLight, Film,
-                    FunctionInfiniteLight, GaussianFilter, GeometricPrimitive, HenyeyGreenstein, HomogeneusMedium,
+                    FunctionInfiniteLight, GaussianFilter, LanczosFilter, GeometricPrimitive, HenyeyGreenstein, HomogeneusMedium,
                     ImageTexture,
                     MicrofacetDielectric, MicrofacetDiffuse, MitchellFilter, Mesh, Model, PointLight,
                     PowerLightSampler, QuadShape, Scene, SolidColor, SpecularConductor, SphereShape, ThinDielectric,

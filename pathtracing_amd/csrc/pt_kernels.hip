@@ -1117,8 +1117,20 @@ __device__ __forceinline__ double mitchell1(double x, double b, double c) {
 __device__ __forceinline__ double gauss1(double x, double sigma) {
     return 0.56418958354775628695 / (sigma * 1.41421356237309504880) * exp(-(x * x) / (2 * sigma * sigma));
 }
+// Sinc / WindowedSinc (Filter.hpp:17-27) in double, as LanczosFilter::Evaluate
+// calls them (Filter.hpp:124-126): x promoted from the float position.
+__device__ __forceinline__ double sinc1(double x) {
+    if (1.0 - x * x == 1.0) return 1.0;
+    return sin(3.14159265358979323846 * x) / (3.14159265358979323846 * x);
+}
+__device__ __forceinline__ double wsinc1(double x, double radius, double tau) {
+    if (fabs(x) > radius) return 0.0;
+    return sinc1(x) * sinc1(x / tau);
+}
 __device__ __forceinline__ double filter_eval(const RenderParams& R, float px, float py) {
     if (R.filter == PT_FILTER_BOX) return (fabsf(px) <= R.frad[0] && fabsf(py) <= R.frad[1]) ? 1.0 : 0.0;
+    if (R.filter == PT_FILTER_LANCZOS)
+        return wsinc1(px, R.frad[0], R.fparam[0]) * wsinc1(py, R.frad[1], R.fparam[0]);
     if (R.filter == PT_FILTER_GAUSSIAN) {
         double gx = gauss1(px, R.fparam[0]) - R.gauss_x, gy = gauss1(py, R.fparam[0]) - R.gauss_y;
         return (gx > 0 ? gx : 0) * (gy > 0 ? gy : 0);
@@ -1184,6 +1196,7 @@ __global__ __launch_bounds__(256) void k_gather(RenderParams R, const float* __r
 // neighbour-major.
 __device__ __forceinline__ double filter_1d(const RenderParams& R, float p, int axis) {
     if (R.filter == PT_FILTER_BOX) return fabsf(p) <= R.frad[axis] ? 1.0 : 0.0;
+    if (R.filter == PT_FILTER_LANCZOS) return wsinc1(p, R.frad[axis], R.fparam[0]);
     if (R.filter == PT_FILTER_GAUSSIAN) {
         const double g = gauss1(p, R.fparam[0]) - (axis ? R.gauss_y : R.gauss_x);
         return g > 0 ? g : 0;

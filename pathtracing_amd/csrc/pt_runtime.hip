@@ -1218,7 +1218,8 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         double ix = 0.5 * (std::erf(rd->filter_radius[0] / s2) - std::erf(-rd->filter_radius[0] / s2));
         double iy = 0.5 * (std::erf(rd->filter_radius[1] / s2) - std::erf(-rd->filter_radius[1] / s2));
         integral = (ix - 2 * rd->filter_radius[0] * R.gauss_x) * (iy - 2 * rd->filter_radius[1] * R.gauss_y);
-    } else integral = mitchell_int(rd->filter_radius[0], rd->filter_radius[1]);
+    } else if (rd->filter == PT_FILTER_LANCZOS) integral = rd->filter_params[1];  // the host object's Integral()
+    else integral = mitchell_int(rd->filter_radius[0], rd->filter_radius[1]);
     R.inv_integral = 1.0 / integral;
 
     const uint32_t spp_local = rd->spp > R.shard_index ? (rd->spp - R.shard_index + R.shard_count - 1) / R.shard_count : 0;
@@ -1527,8 +1528,10 @@ static pt_status check_render_args(pt_ctx* c, const pt_camera_desc* cam, const p
     if (!c->has_scene) return fail(c, PT_ERR_STATE, "no scene uploaded");
     if (cam->width <= 0 || cam->height <= 0 || (uint64_t)cam->width * cam->height > (1ull << 31))
         return fail(c, PT_ERR_ARG, "bad film size");
-    if (rd->integrator > PT_INTEGRATOR_VOLPATH || rd->filter > PT_FILTER_GAUSSIAN)
+    if (rd->integrator > PT_INTEGRATOR_VOLPATH || rd->filter > PT_FILTER_LANCZOS)
         return fail(c, PT_ERR_ARG, "bad integrator/filter");
+    if (rd->filter == PT_FILTER_LANCZOS && !(rd->filter_params[1] != 0.0 && std::isfinite(rd->filter_params[1])))
+        return fail(c, PT_ERR_ARG, "Lanczos filter: filter_params[1] must hold the filter's Integral()");
     if (cam->medium < -1 || cam->medium >= (int32_t)c->n_media) return fail(c, PT_ERR_ARG, "bad camera medium");
     if (rd->filter_radius[0] <= 0 || rd->filter_radius[1] <= 0) return fail(c, PT_ERR_ARG, "bad filter radius");
     return PT_OK;

@@ -24,7 +24,7 @@ PT_IMAGE_U8, PT_IMAGE_F32 = 0, 1
 PT_TEXINF_X, PT_TEXINF_Y = 1920, 1080
 PT_LS_UNIFORM, PT_LS_POWER = 0, 1
 PT_INTEGRATOR_PATH, PT_INTEGRATOR_SIMPLE, PT_INTEGRATOR_VOLPATH = 0, 1, 2
-PT_FILTER_MITCHELL, PT_FILTER_BOX, PT_FILTER_GAUSSIAN = 0, 1, 2
+PT_FILTER_MITCHELL, PT_FILTER_BOX, PT_FILTER_GAUSSIAN, PT_FILTER_LANCZOS = 0, 1, 2, 3
 PT_TONEMAP_REINHARD_JODIE, PT_TONEMAP_ACES = 0, 1
 PT_RENDER_COUNT_NODES = 0x1
 PT_RENDER_TIMING = 0x2

@@ -232,6 +232,8 @@ def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: 
         lines.append(f"filter mitchell {_f(flt.radius[0])} {_f(flt.radius[1])} {flt.b!r} {flt.c!r}")
     elif flt.kind == 1:
         lines.append(f"filter box {_f(flt.radius[0])} {_f(flt.radius[1])}")
+    elif flt.kind == 3:
+        lines.append(f"filter lanczos {_f(flt.radius[0])} {_f(flt.radius[1])} {flt.tau!r}")
     else:
         lines.append(f"filter gaussian {_f(flt.radius[0])} {_f(flt.radius[1])} {flt.sigma!r}")
     lines.append(f"integrator {integrator} {max_depth}")

@@ -1033,6 +1033,63 @@ class GaussianFilter(Filter):
         return (self.sigma, 0.0)
 
 
+class LanczosFilter(Filter):
+    """LanczosFilter (Filter.hpp:114-144): WindowedSinc(x, r.x, tau) *
+    WindowedSinc(y, r.y, tau), separable.  Integral() follows the reference's
+    estimator (256 x 256 jittered strata over [-r, r], times its area term
+    2 * r.x * r.y, Filter.hpp:130-143) with the unseeded random_double()
+    jitter replaced by a fixed counter-based hash, so it is reproducible; the
+    device takes the value from here (pt_render_desc.filter_params[1]), as
+    the drop-in takes the reference object's own Integral()."""
+    kind = 3
+
+    def __init__(self, radius=(1.5, 1.5), tau: float = 3.0):
+        super().__init__(radius)
+        self.tau = float(tau)
+        self._integral = None
+
+    @staticmethod
+    def _wsinc(x, radius, tau):
+        x = np.asarray(x, np.float64)
+
+        def sinc(v):
+            with np.errstate(invalid="ignore", divide="ignore"):
+                s = np.sin(np.pi * v) / (np.pi * v)
+            return np.where(1.0 - v * v == 1.0, 1.0, s)
+        return np.where(np.abs(x) > radius, 0.0, sinc(x) * sinc(x / tau))
+
+    def Evaluate(self, p) -> np.ndarray:
+        p = np.asarray(p, np.float32)
+        return (self._wsinc(p[..., 0].astype(np.float64), float(self.radius[0]), self.tau) *
+                self._wsinc(p[..., 1].astype(np.float64), float(self.radius[1]), self.tau))
+
+    def Integral(self) -> float:
+        if self._integral is None:
+            n = 256
+            ys, xs = np.meshgrid(np.arange(n, dtype=np.uint64), np.arange(n, dtype=np.uint64), indexing="ij")
+            k = (ys * n + xs).astype(np.uint64)
+            jx = (_hash_u32(k * np.uint64(2)) >> np.uint64(8)).astype(np.float64) / 16777216.0
+            jy = (_hash_u32(k * np.uint64(2) + np.uint64(1)) >> np.uint64(8)).astype(np.float64) / 16777216.0
+            u = np.stack([(xs + jx) / n, (ys + jy) / n], -1).astype(np.float32)
+            r = self.radius.astype(np.float32)
+            p = (-r + (r - -r) * u).astype(np.float32)  # glm::mix(-radius, radius, u)
+            area = 2.0 * float(r[0]) * float(r[1])
+            self._integral = area * float(self.Evaluate(p).sum()) / (n * n)
+        return self._integral
+
+    def params(self):
+        return (self.tau, self.Integral())
+
+
+def _hash_u32(v: np.ndarray) -> np.ndarray:
+    """PCG-RXS-M-XS (the sample stream's hash) over uint64-held u32."""
+    m = np.uint64(0xFFFFFFFF)
+    v = np.asarray(v, np.uint64) & m
+    s = (v * np.uint64(747796405) + np.uint64(2891336453)) & m
+    w = (((s >> ((s >> np.uint64(28)) + np.uint64(4))) ^ s) * np.uint64(277803737)) & m
+    return ((w >> np.uint64(22)) ^ w) & m
+
+
 class Film:
     """Film.hpp:112-271: accumulation buffer of {sum RGB*w, sum w} in float64."""
 

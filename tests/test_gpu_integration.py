@@ -124,3 +124,20 @@ def test_drop_in_host_merge_fallback_matches_one_context(mode, tmp_path):
                            env=dict(os.environ, PT_FORCE_HOST_MERGE="3"))
     np.testing.assert_array_equal(c3, c1)
     np.testing.assert_allclose(three, one, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.skipif(not HARNESS.exists(), reason="hip_harness not built (needs /root/reference at build time)")
+def test_drop_in_lanczos_filter_matches_reference_film(tmp_path):
+    """The drop-in with the reference's own LanczosFilter object (Filter.hpp:
+    114-144): the device evaluates WindowedSinc x WindowedSinc and takes the
+    object's Integral() (a jittered estimate, one per call), against the
+    reference FilmTile's film of the same recipe (tests/golden/lanczos.npz),
+    up to that one normalisation constant."""
+    from fixtures import rescaled_reference_film
+    _, gpu, _ = _dropin("lanczos", tmp_path)
+    fx = np.load(GOLDEN / "lanczos.npz", allow_pickle=False)
+    ref = rescaled_reference_film("lanczos", fx["film"], gpu)
+    np.testing.assert_allclose(gpu[..., 3], ref[..., 3], rtol=1e-9, atol=1e-12)
+    frac = _film_frac(gpu, ref)
+    record_parity("dropin_film_ref/lanczos", "film", frac)
+    assert frac >= FILM_MIN

