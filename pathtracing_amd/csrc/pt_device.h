@@ -49,6 +49,29 @@ struct alignas(64) DevQNode {
 };
 static_assert(sizeof(DevQNode) == 64, "qnode layout");
 
+// ---- unified 48-B records (PT_Q48, the default quantized form): node records
+// and the primitive slots of their leaf children in ONE array, each cluster's
+// children in one contiguous block (inner children 1 record, a leaf child its
+// primitives' slots), so a node names its children with one base and four
+// byte offsets and a node step is three 16-B loads instead of four.
+//   node:  a = origin.xyz, w = ex | ey << 8 | ez << 16 | perm << 24
+//              (perm: the reference's topology code, BVH4_NODE::perm; the
+//              octant order byte is BVH4::LUT[octant][perm], an LDS table)
+//          b = x lo[4], x hi[4], y lo[4], y hi[4]  (as DevQNode)
+//          c = z lo[4], z hi[4], base, desc
+//              desc = 4 x u8 per child slot: 0xFF empty, else offset (0..62)
+//              from base | 0x40 leaf | 0x80 leaf holding a BLAS hop
+//   primitive: the slot's DevGeom with c.w = the slot (hits and the shading
+//              tables stay indexed by slot)
+#ifndef PT_Q48
+#define PT_Q48 1
+#endif
+#define Q48_EMPTY 0xFFu
+#define Q48_LEAF 0x40u
+#define Q48_HOP 0x80u
+#define Q48_MAX_OFFSET 62u
+#define Q48_LUT_STRIDE 136  // bytes per octant row of the LDS order table (135 perms)
+
 // ---- wide node (PT_WIDE, 128 B, one line): cluster i with its largest
 // inner children absorbed (greedily by surface area while at most 8 slots
 // remain), so one step tests the children and the absorbed children's
@@ -102,6 +125,7 @@ struct alignas(16) DevGeom {
 struct DevInstance {
     float T[16], inv[16];  // glm column-major transform and inverse
     uint32_t root;         // BLAS root ref
+    uint32_t qroot;        // ... in the PT_Q48 records
     uint32_t prim_base;    // first slot of the BLAS
     uint32_t n_prims;
     uint32_t virt_base;    // virtual slot of the BLAS's first primitive
@@ -138,6 +162,9 @@ struct DevScene {
                                // PT_WIDE: DevWNode records (reinterpreted)
     const DevGeom* geom;
     const DevPrimInfo* info;
+    const DevGeom* qrec;       // PT_Q48 records (null: the scene could not be encoded)
+    const uint32_t* qlut;      // BVH4::LUT as 8 rows of Q48_LUT_STRIDE bytes (staged into LDS)
+    uint32_t qroot;            // TLAS root in the records
     uint32_t root;
     uint32_t n_prims;
     uint32_t n_nodes;

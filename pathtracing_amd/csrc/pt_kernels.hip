@@ -191,12 +191,14 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES_FOR(PT_USES_SPEC(INST
                                                                 unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_POOL_LDS_C * PT_TRACE_BLOCK];
     __shared__ uint16_t s_ent[PT_ENTRY ? PT_POOL_LDS_C * PT_TRACE_BLOCK : 1];
+    __shared__ __attribute__((aligned(16))) uint8_t s_lut[(QN && PT_Q48) ? 8 * Q48_LUT_STRIDE : 4];
     iteration_prologue(nptr, spare, snap);
     const uint32_t n = path_count(nptr);
     if (n == 0) return;
+    if constexpr (QN && PT_Q48) stage_q48_lut(s_lut);
     TraceWork wk{0, 0};
     ClosestSrc src{P, hit, nptr[Q_NEXT]};
-    trace_pool<false, COUNT, ClosestSrc, true, INST, PT_POOL_LDS_C, QN>(n, pool, src, s_ref, s_ent, ovf, wk);
+    trace_pool<false, COUNT, ClosestSrc, true, INST, PT_POOL_LDS_C, QN>(n, pool, src, s_ref, s_ent, ovf, wk, s_lut);
     if (COUNT) {
         count_add(counters, CNT_NODES_CLOSEST, wk.nodes);
         count_add(counters, CNT_TRIS_CLOSEST, wk.tris);
@@ -244,11 +246,13 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SHADOW_WAVES_FOR(PT_USES_SPEC(IN
                                                                uint32_t* __restrict__ pool, uint32_t* __restrict__ ovf,
                                                                unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_POOL_LDS * PT_TRACE_BLOCK];
+    __shared__ __attribute__((aligned(16))) uint8_t s_lut[(QN && PT_Q48) ? 8 * Q48_LUT_STRIDE : 4];
     TraceWork wk{0, 0};
     ShadowSrc src{sq, next, sample_L};
     const uint32_t n = *nptr;
     if (n == 0) return;
-    trace_pool<true, COUNT, ShadowSrc, true, INST, PT_POOL_LDS, QN>(n, pool, src, s_ref, nullptr, ovf, wk);
+    if constexpr (QN && PT_Q48) stage_q48_lut(s_lut);
+    trace_pool<true, COUNT, ShadowSrc, true, INST, PT_POOL_LDS, QN>(n, pool, src, s_ref, nullptr, ovf, wk, s_lut);
     if (COUNT) {
         count_add(counters, CNT_NODES_ANY, wk.nodes);
         count_add(counters, CNT_TRIS_ANY, wk.tris);
@@ -358,10 +362,12 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(const pt_ray* __r
                                                               uint32_t* __restrict__ ovf, unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_POOL_LDS * PT_TRACE_BLOCK];
     __shared__ uint16_t s_ent[PT_POOL_LDS_C * PT_TRACE_BLOCK];
+    __shared__ __attribute__((aligned(16))) uint8_t s_lut[(QN && PT_Q48) ? 8 * Q48_LUT_STRIDE : 4];
+    if constexpr (QN && PT_Q48) stage_q48_lut(s_lut);
     TraceWork wk{0, 0};
     RaysSrc src{rays, out};
-    if (any) trace_pool<true, true, RaysSrc, true, true, PT_POOL_LDS, QN>(n, pool, src, s_ref, nullptr, ovf, wk);
-    else trace_pool<false, true, RaysSrc, true, true, PT_POOL_LDS_C, QN>(n, pool, src, s_ref, s_ent, ovf, wk);
+    if (any) trace_pool<true, true, RaysSrc, true, true, PT_POOL_LDS, QN>(n, pool, src, s_ref, nullptr, ovf, wk, s_lut);
+    else trace_pool<false, true, RaysSrc, true, true, PT_POOL_LDS_C, QN>(n, pool, src, s_ref, s_ent, ovf, wk, s_lut);
     count_add(counters, any ? CNT_NODES_ANY : CNT_NODES_CLOSEST, wk.nodes);
     count_add(counters, any ? CNT_TRIS_ANY : CNT_TRIS_CLOSEST, wk.tris);
 }

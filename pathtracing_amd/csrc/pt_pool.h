@@ -99,6 +99,11 @@ __device__ unsigned int pt_diag[4];
 #ifndef PT_SPEC
 #define PT_SPEC 1
 #endif
+// PT_Q48 records in the overlapped traversal: child refs formed per pushed
+// child (order_children_q48) instead of all four up front
+#ifndef PT_Q48_LAZY
+#define PT_Q48_LAZY 1
+#endif
 // overflow words per stack entry per lane (ref + entry distance)
 #define PT_OVF_WORDS 2
 // Stack capacity of the pool kernels.  The reference's stack[32] is undefined
@@ -135,7 +140,7 @@ __device__ unsigned int pt_diag[4];
 // iterations and cost 17 % (profiles/r03_ab_spec.txt).
 template <bool ANY, bool COUNT, class Src, int LN>
 __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, uint32_t* s_ref,
-                           uint32_t* __restrict__ ovf, TraceWork& wk) {
+                           uint32_t* __restrict__ ovf, TraceWork& wk, const uint8_t* s_lut) {
     const uint32_t lane = threadIdx.x;
     const uint32_t gl = blockIdx.x * PT_TRACE_BLOCK + lane, G = gridDim.x * PT_TRACE_BLOCK;
     const uint32_t wl = __lane_id();
@@ -206,7 +211,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                         if (src.load((uint32_t)ri, o, d, tmax)) {
                             inv = inv_dir(d);
                             oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
-                            ref = S.root;
+                            ref = PT_Q48 ? S.qroot : S.root;
                             leaf = REF_EMPTY;
                             sp = 0;
                         } else {
@@ -254,13 +259,20 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             PT_IT(6, np);
         }
 #endif
-        // both cursors' loads issue before either is used: the node (64 B)
-        // and the primitive slot (48 B); a lane without one reads the root /
-        // slot 0 (shared lines, no extra traffic)
+        // both cursors' loads issue before either is used: the node (48 B
+        // record, PT_Q48; 64 B DevQNode otherwise) and the primitive slot
+        // (48 B); a lane without one reads record / slot 0 (shared lines, no
+        // extra traffic)
         const uint32_t slot = prim_step ? (leaf & ~(REF_LEAF | REF_BLOCK)) : 0u;
+#if PT_Q48
+        const float4* __restrict__ qn = reinterpret_cast<const float4*>(S.qrec + (node_step ? ref : 0u));
+        const float4* __restrict__ qg = reinterpret_cast<const float4*>(S.qrec + slot);
+        const float4 q0 = qn[0], q1 = qn[1], q2 = qn[2];
+#else
         const float4* __restrict__ qn = reinterpret_cast<const float4*>(S.qnodes + (node_step ? ref : 0u));
         const float4* __restrict__ qg = reinterpret_cast<const float4*>(S.geom + slot);
         const float4 q0 = qn[0], q1 = qn[1], q2 = qn[2], qc = qn[3];
+#endif
         const float4 g0 = qg[0], g1 = qg[1], g2 = qg[2];
         __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink the slot loads past the node side)
 
@@ -271,13 +283,24 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             qslab4pe(q0, q1, q2, o, inv, tmax, mask, te);
             if (!node_step) mask = 0;
             uint32_t perm = 0xE4u;
+#if PT_Q48
+            if (!ANY || PT_ANY_OCT) perm = q48_perm(s_lut, oct, q0.w);
+#if PT_Q48_LAZY
+            const uint32_t cand = order_children_q48(mask, q2.z, q2.w, perm, [&](uint32_t v) { push(v); });
+#else
+            const uint4 ch = q48_children(q2.z, q2.w);
+#endif
+#else
             if (!ANY || PT_ANY_OCT) {
                 const uint32_t ow = ((oct >> 2) & 1u) ? __float_as_uint(q2.w) : __float_as_uint(q2.z);
                 perm = (ow >> (8 * (oct & 3))) & 0xFFu;
             }
             const uint4 ch = make_uint4(__float_as_uint(qc.x), __float_as_uint(qc.y), __float_as_uint(qc.z),
                                         __float_as_uint(qc.w));
+#endif
+#if !(PT_Q48 && PT_Q48_LAZY)
             const uint32_t cand = order_children(mask, ch, perm, [&](uint32_t v) { push(v); });
+#endif
             if (node_step) {
                 if (COUNT) wk.nodes++;
                 ref = cand;
@@ -297,15 +320,17 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             if (prim_step) {
                 bool anyhit = false;
                 const uint32_t next = (w0 & GF_LAST) ? REF_EMPTY : (REF_LEAF | (leaf & REF_BLOCK) | (slot + 1));
+                // the primitive's slot (PT_Q48: the record keeps it in c.w)
+                const uint32_t ps = PT_Q48 ? __float_as_uint(g2.w) : slot;
                 if (kind == PT_PRIM_TRIANGLE) {
                     if (COUNT) wk.tris++;
-                    if (tri_hit && (pred || !(w0 & GF_ALPHA) || tri_alpha(slot, bx, by, o, d))) {
+                    if (tri_hit && (pred || !(w0 & GF_ALPHA) || tri_alpha(ps, bx, by, o, d))) {
                         if (ANY) {
                             anyhit = true;
                         } else {
                             tmax = t;
                             oct |= OCT_FOUND;
-                            src.closest((uint32_t)ri, t, bx, by, (int)slot);
+                            src.closest((uint32_t)ri, t, bx, by, (int)ps);
                         }
                     }
                 } else if (kind == PT_PRIM_BLAS) {
@@ -313,13 +338,13 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 } else {
                     if (COUNT) wk.tris++;
                     if (ANY) {
-                        if (other_pred(slot, w0, o, d, tmax)) anyhit = true;
+                        if (other_pred(ps, w0, o, d, tmax)) anyhit = true;
                     } else {
                         float t2, a2, b2;
-                        if (other_closest(slot, w0, o, d, tmax, t2, a2, b2)) {
+                        if (other_closest(ps, w0, o, d, tmax, t2, a2, b2)) {
                             tmax = t2;
                             oct |= OCT_FOUND;
-                            src.closest((uint32_t)ri, t2, a2, b2, (int)slot);
+                            src.closest((uint32_t)ri, t2, a2, b2, (int)ps);
                         }
                     }
                 }
@@ -349,10 +374,12 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
 template <bool ANY, bool COUNT, class Src, bool POOL = true, bool INST = true,
           int LN = (ANY ? PT_POOL_LDS : PT_POOL_LDS_C), bool QN = false>
 __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, uint32_t* s_ref, uint16_t* s_ent,
-                           uint32_t* __restrict__ ovf, TraceWork& wk) {
+                           uint32_t* __restrict__ ovf, TraceWork& wk, const uint8_t* s_lut = nullptr) {
     constexpr bool ENT = PT_ENTRY && !ANY;
+    static_assert(!(PT_Q48 && (PT_WIDE || PT_ENTRY)), "PT_WIDE / PT_ENTRY read the 64-B DevQNode form (PT_Q48=0)");
+    constexpr bool Q48 = QN && PT_Q48;  // nodes and leaf slots in the 48-B records
     if constexpr (PT_SPEC && QN && POOL && !INST && !ENT && !PT_WIDE) {
-        trace_spec<ANY, COUNT, Src, LN>(n, pool, src, s_ref, ovf, wk);
+        trace_spec<ANY, COUNT, Src, LN>(n, pool, src, s_ref, ovf, wk, s_lut);
         return;
     }
     const uint32_t lane = threadIdx.x;
@@ -410,7 +437,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
     auto start = [&]() {
         inv = inv_dir(d);
         oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
-        ref = S.root;
+        ref = Q48 ? S.qroot : S.root;
         sp = 0;
         best = -1;
         bb1 = bb2 = 0;
@@ -514,7 +541,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
 #endif
         const uint32_t idx = ref & ~(QN ? REF_LEAF | REF_BLOCK : REF_LEAF);
 #if PT_POOL_CHECK
-        if (node_step ? idx >= S.n_nodes : idx >= S.n_prims) {  // debugging builds only
+        if (!Q48 && (node_step ? idx >= S.n_nodes : idx >= S.n_prims)) {  // debugging builds only
             atomicAdd(&pt_diag[0], 1u);
             ref = REF_EMPTY;
             continue;
@@ -559,6 +586,16 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             const float plo = (oct & 1u) ? qo.y : qo.x, phi = (oct & 1u) ? qo.w : qo.z;
             wperm = __float_as_uint((oct & 2u) ? phi : plo);
             ow0 = ow1 = 0;
+        } else if constexpr (Q48) {
+            // node records and leaf slots share the array: three loads either way
+            const float4* __restrict__ q = reinterpret_cast<const float4*>(S.qrec + idx);
+            q0 = q[0];
+            q1 = q[1];
+            q2 = q[2];
+            q3 = q4 = q5 = q0;
+            qslab4pe(q0, q1, q2, o, inv, tmax, mask, te);
+            ch = q48_children(q2.z, q2.w);
+            ow0 = ow1 = 0;  // the order byte comes from s_lut below
         } else if constexpr (QN) {
             const float4* __restrict__ q = node_step ? reinterpret_cast<const float4*>(S.qnodes + idx)
                                                      : reinterpret_cast<const float4*>(S.geom + idx);
@@ -602,8 +639,12 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             // order far -> near for closest hit (BVH4::LUT, BVH.hpp:1195-1204)
             uint32_t perm = 0xE4u;
             if (!ANY || PT_ANY_OCT) {
-                const uint32_t ow = ((oct >> 2) & 1u) ? ow1 : ow0;
-                perm = (ow >> (8 * (oct & 3))) & 0xFFu;
+                if constexpr (Q48) {
+                    perm = q48_perm(s_lut, oct, q0.w);
+                } else {
+                    const uint32_t ow = ((oct >> 2) & 1u) ? ow1 : ow0;
+                    perm = (ow >> (8 * (oct & 3))) & 0xFFu;
+                }
             }
             uint32_t cand;
             if constexpr (QN && PT_WIDE) {
@@ -621,9 +662,10 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 continue;
             }
         }
-        // leaf primitives at slot idx (and idx + 1)
+        // leaf primitives at slot idx (and idx + 1); PT_Q48: record idx,
+        // whose c.w is the slot
         {
-            const uint32_t slot = idx;
+            const uint32_t slot = Q48 ? __float_as_uint(q2.w) : idx;
             const uint32_t w0 = __float_as_uint(q0.w);
             const uint32_t kind = w0 & GF_KIND;
             bool anyhit = false;
@@ -650,7 +692,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                     }
                 }
             };
-            uint32_t next = (w0 & GF_LAST) ? REF_EMPTY : (REF_LEAF | (slot + 1));
+            uint32_t next = (w0 & GF_LAST) ? REF_EMPTY : (REF_LEAF | (idx + 1));
             if (kind == PT_PRIM_TRIANGLE) {
                 tri(slot, w0, q0, q1, q2);
                 const uint32_t w1 = __float_as_uint(q3.w);

@@ -699,7 +699,8 @@ struct Conv {
         uint32_t perm = desc.perm < 135 ? desc.perm : 0;
         dc.order[0] = dc.order[1] = 0;
         for (int o = 0; o < 8; o++) dc.order[o >> 2] |= (uint32_t)lut[o][perm] << (8 * (o & 3));
-        dc.pad[0] = dc.pad[1] = 0;
+        dc.pad[0] = perm;  // the topology code itself (PT_Q48 records look the order up)
+        dc.pad[1] = 0;
         for (int k = 0; k < 4; k++) dc.child[k] = REF_EMPTY;
         for (int k = 0; k < 4; k++) {
             pt_ref_bvh4_node ch = rc.children[k];
@@ -711,6 +712,132 @@ struct Conv {
 };
 
 extern "C" pt_status pt_bvh4_order_table(uint8_t* out);
+
+// ---- PT_Q48 records (pt_device.h): every BVH's root gets a record first;
+// then, depth first from each root, a node's children get one contiguous
+// block (an inner child one record, a leaf child a copy of its slots in leaf
+// order, c.w = the slot) and the node record names them by base + offsets.
+// A child that is another BVH's root (a lone BLAS hop resolved at upload) is
+// a copy of that root's record.  BLAS-hop slots push the BLAS root's record.
+// False (the scene keeps 64-B nodes) when a block offset or the record count
+// does not fit.
+static bool build_q48(const std::vector<DevCluster>& nodes, const std::vector<DevGeom>& geom,
+                      const std::vector<uint32_t>& roots, uint32_t n_prims, std::vector<DevGeom>& rec,
+                      std::vector<uint32_t>& qroots) {
+    rec.clear();
+    rec.reserve(nodes.size() + n_prims + 16);
+    std::vector<uint32_t> node_rec(nodes.size(), REF_EMPTY);
+    std::vector<std::pair<uint32_t, uint32_t>> copies;  // (record, cluster whose record it repeats)
+    std::vector<std::pair<uint32_t, uint32_t>> work;    // (cluster, its record)
+    auto alloc = [&](uint32_t n) {
+        const uint32_t b = (uint32_t)rec.size();
+        rec.resize(rec.size() + n);
+        return b;
+    };
+    auto leaf_len = [&](uint32_t slot) {
+        uint32_t n = 0;
+        for (uint32_t s = slot; s < n_prims; s++) {
+            n++;
+            if (__builtin_bit_cast(uint32_t, geom[s].a.w) & GF_LAST) break;
+        }
+        return n;
+    };
+    auto is_hop = [&](uint32_t slot, uint32_t len) {
+        for (uint32_t s = slot; s < slot + len; s++)
+            if ((__builtin_bit_cast(uint32_t, geom[s].a.w) & GF_KIND) == PT_PRIM_BLAS) return true;
+        return false;
+    };
+    // cluster-space root refs -> record-space (BLAS-hop slots carry them)
+    std::vector<std::pair<uint32_t, uint32_t>> root_map;
+    std::vector<uint32_t> hops;  // records of BLAS-hop slots
+    auto copy_leaf = [&](uint32_t slot, uint32_t len, uint32_t at) {
+        for (uint32_t k = 0; k < len; k++) {
+            DevGeom g = geom[slot + k];
+            g.c.w = __builtin_bit_cast(float, slot + k);
+            rec[at + k] = g;  // BLAS-hop roots patched below, once every root has its record
+            if ((__builtin_bit_cast(uint32_t, g.a.w) & GF_KIND) == PT_PRIM_BLAS) hops.push_back(at + k);
+        }
+    };
+    qroots.assign(roots.size(), REF_EMPTY);
+    for (size_t b = 0; b < roots.size(); b++) {
+        const uint32_t r = roots[b];
+        if (r == REF_EMPTY || r >= REF_SPECIAL) continue;
+        if (r & REF_LEAF) {
+            const uint32_t slot = r & ~REF_LEAF, len = leaf_len(slot), at = alloc(len);
+            copy_leaf(slot, len, at);
+            qroots[b] = REF_LEAF | (is_hop(slot, len) ? REF_BLOCK : 0u) | at;
+        } else {
+            if (r >= nodes.size()) return false;
+            if (node_rec[r] == REF_EMPTY) {
+                node_rec[r] = alloc(1);
+                work.push_back({r, node_rec[r]});
+            }
+            qroots[b] = node_rec[r];
+        }
+        root_map.push_back({r, qroots[b]});
+    }
+    while (!work.empty()) {
+        const auto [gi, r] = work.back();
+        work.pop_back();
+        const DevCluster& n = nodes[gi];
+        uint32_t size[4] = {0, 0, 0, 0};
+        for (int k = 0; k < 4; k++) {
+            const uint32_t ch = n.child[k];
+            if (ch == REF_EMPTY) continue;
+            if (ch >= REF_SPECIAL) return false;
+            size[k] = (ch & REF_LEAF) ? leaf_len(ch & ~REF_LEAF) : 1u;
+        }
+        const uint32_t total = size[0] + size[1] + size[2] + size[3];
+        const uint32_t base = alloc(total);
+        uint32_t desc = 0, off = 0;
+        for (int k = 0; k < 4; k++) {
+            const uint32_t ch = n.child[k];
+            uint32_t d = Q48_EMPTY;
+            if (ch != REF_EMPTY) {
+                if (off > Q48_MAX_OFFSET) return false;
+                d = off;
+                if (ch & REF_LEAF) {
+                    const uint32_t slot = ch & ~REF_LEAF;
+                    copy_leaf(slot, size[k], base + off);
+                    d |= Q48_LEAF | (is_hop(slot, size[k]) ? Q48_HOP : 0u);
+                } else if (node_rec[ch] != REF_EMPTY) {  // another BVH's root: a copy of its record
+                    copies.push_back({base + off, ch});
+                } else {
+                    node_rec[ch] = base + off;
+                    work.push_back({ch, base + off});
+                }
+                off += size[k];
+            }
+            desc |= d << (8 * k);
+        }
+        // the node record: the cluster's quantized boxes, perm, base, desc
+        DevQNode q;
+        if (!quantize_node(n, q)) return false;
+        DevGeom& o = rec[r];
+        o.a = q.a;
+        o.a.w = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, q.a.w) | (n.pad[0] & 0xFFu) << 24);
+        o.b = make_float4(__builtin_bit_cast(float, q.b[0]), __builtin_bit_cast(float, q.b[1]),
+                          __builtin_bit_cast(float, q.b[2]), __builtin_bit_cast(float, q.b[3]));
+        o.c = make_float4(__builtin_bit_cast(float, q.c[0]), __builtin_bit_cast(float, q.c[1]),
+                          __builtin_bit_cast(float, base), __builtin_bit_cast(float, desc));
+        if (rec.size() >= REF_BLOCK) return false;
+    }
+    for (const auto& [at, ci] : copies) rec[at] = rec[node_rec[ci]];
+    // BLAS-hop slots push the BLAS root's record (instance hops keep REF_INST_ENTER | slot)
+    for (uint32_t h : hops) {
+        DevGeom& g = rec[h];
+        const uint32_t tgt = __builtin_bit_cast(uint32_t, g.b.x);
+        if (tgt >= REF_SPECIAL) continue;
+        uint32_t q = REF_EMPTY;
+        for (const auto& [cr, qr] : root_map)
+            if (cr == tgt) q = qr;
+        if (q == REF_EMPTY) return false;
+        g.b.x = __builtin_bit_cast(float, q);
+    }
+    // one pad record: leaf steps may read the record after the last one
+    rec.push_back(DevGeom{});
+    return !rec.empty() && rec.size() < REF_BLOCK;
+}
 
 static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s);
 extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
@@ -875,6 +1002,7 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
         std::memcpy(D.T, I.transform, sizeof(D.T));
         std::memcpy(D.inv, I.inv, sizeof(D.inv));
         D.root = roots[I.bvh];
+        D.qroot = REF_EMPTY;  // PT_Q48 records: set with them
         D.prim_base = s->bvhs[I.bvh].prim_base;
         D.n_prims = s->bvhs[I.bvh].n_prims;
         D.virt_base = I.virt_base;
@@ -908,6 +1036,23 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
             const DevWNode* dw = nullptr;
             UP(dw, wn.data(), wn.size());
             DS.qnodes = reinterpret_cast<const DevQNode*>(dw);
+        }
+#elif PT_Q48
+        // nodes and leaf slots in one array of 48-B records (pt_device.h)
+        std::vector<DevGeom> rec;
+        std::vector<uint32_t> qroots;
+        const bool ok = nodes.size() < REF_BLOCK && s->n_prims < REF_BLOCK &&
+                        build_q48(nodes, geom, roots, s->n_prims, rec, qroots);
+        c->has_qnodes = ok;
+        if (ok) {
+            UP(DS.qrec, rec.data(), rec.size());
+            DS.qroot = qroots[0];
+            for (uint32_t k = 0; k < s->n_instances; k++) inst[k].qroot = qroots[s->instances[k].bvh];
+            std::vector<uint32_t> lut(8 * Q48_LUT_STRIDE / 4, 0u);
+            for (int o = 0; o < 8; o++)
+                for (int p = 0; p < 135; p++)
+                    reinterpret_cast<uint8_t*>(lut.data())[o * Q48_LUT_STRIDE + p] = cv.lut[o][p];
+            UP(DS.qlut, lut.data(), lut.size());
         }
 #else
         std::vector<DevQNode> qn(nodes.size());

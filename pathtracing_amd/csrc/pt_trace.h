@@ -270,6 +270,53 @@ __device__ __forceinline__ void qslab4pe(float4 a, float4 b, float4 c, f3 o, f3 
     }
 }
 
+// PT_Q48 node record (pt_device.h): child refs from the block base and the
+// per-child descriptor bytes (offset | Q48_LEAF -> REF_LEAF | Q48_HOP ->
+// REF_BLOCK), and the octant order byte BVH4::LUT[octant][perm] from the
+// block's LDS copy of the table (s_lut, staged by stage_q48_lut).
+__device__ __forceinline__ uint4 q48_children(float cz, float cw) {
+    const uint32_t base = __float_as_uint(cz), desc = __float_as_uint(cw);
+    uint32_t r[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t d = (desc >> (8 * k)) & 0xFFu;
+        const uint32_t ref = (base + (d & 63u)) | ((d & Q48_LEAF) << 25) | ((d & Q48_HOP) << 22);
+        r[k] = d == Q48_EMPTY ? REF_EMPTY : ref;
+    }
+    return make_uint4(r[0], r[1], r[2], r[3]);
+}
+// order_children over a PT_Q48 record's base + descriptors: the ref of a
+// child is formed only when it is pushed or kept (fewer live registers than
+// four decoded refs)
+template <class Push>
+__device__ __forceinline__ uint32_t order_children_q48(uint32_t mask, float cz, float cw, uint32_t perm, Push&& push) {
+    const uint32_t base = __float_as_uint(cz), desc = __float_as_uint(cw);
+    uint32_t vm = mask;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (((desc >> (8 * k)) & 0xFFu) == Q48_EMPTY) vm &= ~(1u << k);
+    uint32_t cand = REF_EMPTY;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t ci = (perm >> (2 * k)) & 3u;
+        const uint32_t d = (desc >> (8 * ci)) & 0xFFu;
+        const uint32_t c = (base + (d & 63u)) | ((d & Q48_LEAF) << 25) | ((d & Q48_HOP) << 22);
+        const bool v = (vm >> ci) & 1u;
+        if (v && cand != REF_EMPTY) push(cand);
+        cand = v ? c : cand;
+    }
+    return cand;
+}
+__device__ __forceinline__ uint32_t q48_perm(const uint8_t* s_lut, uint32_t oct, float aw) {
+    return s_lut[(oct & OCT_MASK) * Q48_LUT_STRIDE + (__float_as_uint(aw) >> 24)];
+}
+// every thread of the block takes part (one barrier)
+__device__ __forceinline__ void stage_q48_lut(uint8_t* s_lut) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(s_lut);
+    for (uint32_t i = threadIdx.x; i < 8 * Q48_LUT_STRIDE / 4; i += blockDim.x) w[i] = S.qlut[i];
+    __syncthreads();
+}
+
 // Children of a cluster in visit order: every valid child (passes the slab
 // test, exists) but the last is pushed, the last becomes the next ref.  perm
 // holds the visit order as 2-bit slot indices from the low end (0xE4 = slot
@@ -356,7 +403,7 @@ struct InstState {
     int best;
     uint32_t ref;
 };
-template <bool ANY>
+template <bool ANY, bool QN = false>
 __device__ __forceinline__ InstState instance_step_inl(InstState s) {
     const uint32_t L = S.scratch_lanes;
     uint32_t* sc = S.scratch + blockIdx.x * blockDim.x + threadIdx.x;
@@ -390,14 +437,14 @@ __device__ __forceinline__ InstState instance_step_inl(InstState s) {
     s.inv = inv_dir(s.d);
     s.oct = octant(s.d) | OCT_INST;
     s.tmax = s.tmax * len;
-    s.ref = I.root;
+    s.ref = (QN && PT_Q48) ? I.qroot : I.root;  // the BLAS root in the traversal's node form
     return s;
 }
 // The pool kernels (7 waves per SIMD, 72 VGPRs) call it out of line; the
 // one-ray-per-lane kernels (5 waves) inline it (+4 % on the instanced scene).
-template <bool ANY>
+template <bool ANY, bool QN>
 __device__ __noinline__ InstState instance_step(InstState s) {
-    return instance_step_inl<ANY>(s);
+    return instance_step_inl<ANY, QN>(s);
 }
 // Entering records the stack depth in oct (OCT_SP_SHIFT); the instance is
 // left when the traversal is back at that depth with nothing to visit
@@ -406,7 +453,7 @@ __device__ __noinline__ InstState instance_step(InstState s) {
 #define PT_INSTANCE_STEP_FN(ANY_, FN_)                                                          \
     do {                                                                                \
         const bool enter_ = ref != REF_INST_EXIT;                                       \
-        const InstState st_ = FN_<ANY_>(InstState{o, d, inv, tmax, oct, best, ref});          \
+        const InstState st_ = FN_(InstState{o, d, inv, tmax, oct, best, ref});               \
         o = st_.o;                                                                      \
         d = st_.d;                                                                      \
         inv = st_.inv;                                                                  \
@@ -417,8 +464,9 @@ __device__ __noinline__ InstState instance_step(InstState s) {
     } while (0)
 // true when the lane's ray is inside an instance whose BLAS is exhausted
 #define PT_INSTANCE_DONE() ((oct & OCT_INST) && (uint32_t)sp == (oct >> OCT_SP_SHIFT))
-#define PT_INSTANCE_STEP(ANY_) PT_INSTANCE_STEP_FN(ANY_, instance_step)
-#define PT_INSTANCE_STEP_INL(ANY_) PT_INSTANCE_STEP_FN(ANY_, instance_step_inl)
+// (PT_INSTANCE_STEP: inside trace_pool, whose QN names the node form)
+#define PT_INSTANCE_STEP(ANY_) PT_INSTANCE_STEP_FN(ANY_, (instance_step<ANY_, QN>))
+#define PT_INSTANCE_STEP_INL(ANY_) PT_INSTANCE_STEP_FN(ANY_, instance_step_inl<ANY_>)
 
 // Closest hit.  Returns prim slot or -1; t, b1, b2 of the accepted hit.
 // LN: stack entries kept in LDS; entries [LN, PT_STACK) go to ovf
