@@ -583,8 +583,11 @@ def roofline(args, setup, world, totals, cst, cpu):
         this kernel makes), so it never credits work the kernel skips."""
         avg_ms = ms / max(1, launches)
         cands = [b for b in (ref_b, own_b) if b]
-        if not cands or avg_ms <= 0:
+        if avg_ms <= 0:
             return None
+        if not cands:  # no visit counts (--no-count, no CPU sample): timing only
+            return {"kernel": name, "avg_launch_ms": round(avg_ms, 4), "launches": launches, "achieved": None,
+                    "frac": None, "traffic": None, "bound": None}
         bpr = min(cands)
         per_launch = nrays / max(1, launches)
         gbs = lambda b: b * per_launch / (avg_ms * 1e-3) / 1e9  # noqa: E731

@@ -104,6 +104,11 @@ __device__ unsigned int pt_diag[4];
 #ifndef PT_Q48_LAZY
 #define PT_Q48_LAZY 1
 #endif
+// overlapped traversal: node and slot loads only on the lanes that take that
+// step (exec-masked) instead of every lane reading record / slot 0
+#ifndef PT_MASKED_LOADS
+#define PT_MASKED_LOADS 0
+#endif
 // overflow words per stack entry per lane (ref + entry distance)
 #define PT_OVF_WORDS 2
 // Stack capacity of the pool kernels.  The reference's stack[32] is undefined
@@ -264,7 +269,24 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         // (48 B); a lane without one reads record / slot 0 (shared lines, no
         // extra traffic)
         const uint32_t slot = prim_step ? (leaf & ~(REF_LEAF | REF_BLOCK)) : 0u;
-#if PT_Q48
+#if PT_Q48 && PT_MASKED_LOADS
+        // each side's loads under its own exec mask: a lane without a node
+        // (primitive) step issues no node (slot) loads, so the vector memory
+        // pipe processes only the lanes that step (its rate is per lane)
+        float4 q0, q1, q2, g0, g1, g2;  // (lanes without the step: unused values)
+        if (node_step) {
+            const float4* __restrict__ qn = reinterpret_cast<const float4*>(S.qrec + ref);
+            q0 = qn[0];
+            q1 = qn[1];
+            q2 = qn[2];
+        }
+        if (prim_step) {
+            const float4* __restrict__ qg = reinterpret_cast<const float4*>(S.qrec + slot);
+            g0 = qg[0];
+            g1 = qg[1];
+            g2 = qg[2];
+        }
+#elif PT_Q48
         const float4* __restrict__ qn = reinterpret_cast<const float4*>(S.qrec + (node_step ? ref : 0u));
         const float4* __restrict__ qg = reinterpret_cast<const float4*>(S.qrec + slot);
         const float4 q0 = qn[0], q1 = qn[1], q2 = qn[2];
@@ -273,7 +295,9 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         const float4* __restrict__ qg = reinterpret_cast<const float4*>(S.geom + slot);
         const float4 q0 = qn[0], q1 = qn[1], q2 = qn[2], qc = qn[3];
 #endif
+#if !(PT_Q48 && PT_MASKED_LOADS)
         const float4 g0 = qg[0], g1 = qg[1], g2 = qg[2];
+#endif
         __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink the slot loads past the node side)
 
         // ---- node side

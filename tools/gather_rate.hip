@@ -72,6 +72,36 @@ __global__ __launch_bounds__(256) void k_chase(const uint4* __restrict__ t, uint
             a = (q0.x ^ q1.y ^ q2.z ^ q3.w) % granules;
             b = (r0.x ^ r1.y ^ r2.z) % granules;
             acc ^= q3.x ^ r2.x;
+        } else if constexpr (P >= 100) {  // P4 with only (P - 100)% of the lanes stepping
+            // 1xx: the idle lanes are masked off (exec); 2xx: they load granule 0
+            // (what the traversal's unconditional loads do)
+            const uint32_t pct = P % 100;
+            const bool on = (hash(gid * 31u + s) % 100u) < pct;
+            if constexpr (P >= 300) {  // 3xx: buffer loads, idle lanes out of the buffer's range (no fetch)
+                const __amdgpu_buffer_rsrc_t rs =
+                    __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(t), (short)0, (int)(granules * 64u), 0x00020000);
+                const uint32_t off = on ? a * 64u : 0xFFFFFFF0u;
+                const uint4 q0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+                const uint4 q1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16u, 0, 0));
+                const uint4 q2 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 32u, 0, 0));
+                const uint4 q3 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 48u, 0, 0));
+                const uint32_t na = (q0.x ^ q1.y ^ q2.z ^ q3.w) % granules;
+                a = on ? na : a;
+                acc ^= on ? q3.x : 0u;
+            } else if constexpr (P < 200) {
+                if (on) {
+                    const uint4* g = t + 4 * a;
+                    const uint4 q0 = g[0], q1 = g[1], q2 = g[2], q3 = g[3];
+                    a = (q0.x ^ q1.y ^ q2.z ^ q3.w) % granules;
+                    acc ^= q3.x;
+                }
+            } else {
+                const uint4* g = t + 4 * (on ? a : 0u);
+                const uint4 q0 = g[0], q1 = g[1], q2 = g[2], q3 = g[3];
+                const uint32_t na = (q0.x ^ q1.y ^ q2.z ^ q3.w) % granules;
+                a = on ? na : a;
+                acc ^= on ? q3.x : 0u;
+            }
         } else {  // C4: cooperative node loads
             const uint32_t lane = __lane_id(), wbase = threadIdx.x & ~63u;
             uint4 v[4];
@@ -109,7 +139,7 @@ static void run(const uint4* t, uint32_t granules, int cus, int waves_per_simd, 
     CHK(hipEventSynchronize(e1));
     float ms = 0;
     CHK(hipEventElapsedTime(&ms, e0, e1));
-    const int loads = P == 1 ? 1 : P == 3 ? 3 : P == 4 ? 4 : P == 7 ? 7 : 4;
+    const int loads = P == 1 ? 1 : P == 3 ? 3 : P == 4 ? 4 : P == 7 ? 7 : 4;  // lane-loads counted for every lane
     const double wave_steps = (double)blocks * 4 * steps;
     const double lane_loads = wave_steps * 64 * loads;
     const double cycles = ms * 1e-3 * clock_ghz * 1e9;
@@ -130,6 +160,24 @@ int main(int argc, char** argv) {
     CHK(hipMalloc(&sink, 64));
     const struct { const char* name; size_t bytes; uint32_t steps; } tabs[] = {
         {"L2", 2ull << 20, 4096}, {"MALL", 64ull << 20, 2048}, {"HBM", 2ull << 30, 1024}};
+    if (argc > 2 && atoi(argv[2]) == 1) {  // masked vs dummy loads at 30 / 70 / 100 % active lanes
+        const uint32_t granules = (uint32_t)((2ull << 20) / 64);
+        uint4* t;
+        CHK(hipMalloc(&t, 2ull << 20));
+        hipLaunchKernelGGL(k_init, dim3(4096), dim3(256), 0, 0, t, granules);
+        CHK(hipDeviceSynchronize());
+        for (int w : {4, 6}) {
+            run<130>(t, granules, cus, w, 4096, sink, ghz, "L2m30");
+            run<230>(t, granules, cus, w, 4096, sink, ghz, "L2d30");
+            run<170>(t, granules, cus, w, 4096, sink, ghz, "L2m70");
+            run<270>(t, granules, cus, w, 4096, sink, ghz, "L2d70");
+            run<330>(t, granules, cus, w, 4096, sink, ghz, "L2b30");
+            run<370>(t, granules, cus, w, 4096, sink, ghz, "L2b70");
+            run<4>(t, granules, cus, w, 4096, sink, ghz, "L2all");
+        }
+        CHK(hipFree(t));
+        return 0;
+    }
     for (const auto& tb : tabs) {
         const uint32_t granules = (uint32_t)(tb.bytes / 64);
         uint4* t;
