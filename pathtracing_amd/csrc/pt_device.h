@@ -120,6 +120,7 @@ struct alignas(16) DevGeom {
 #define OCT_INST 8u   // the lane's ray is in an instance's object space
 #define OCT_HIT 16u   // ... and accepted a hit there
 #define OCT_FOUND 32u // overlapped traversal (pt_pool.h trace_spec): a hit was stored
+#define OCT_TIE 64u   // pool traversal: this ray met a hit at exactly t == max (listed once for the exact re-trace)
 #define OCT_SP_SHIFT 8  // ... entered at this stack depth (bits 8-13)
 #define SCR_WORDS 9   // scratch row: world o, d, tmax, length, instance
 struct DevInstance {
@@ -164,6 +165,7 @@ struct DevScene {
     const DevPrimInfo* info;
     const DevGeom* qrec;       // PT_Q48 records (null: the scene could not be encoded)
     const uint32_t* qlut;      // BVH4::LUT as 8 rows of Q48_LUT_STRIDE bytes (staged into LDS)
+    uint32_t qrec_bytes;       // bytes of qrec (< 2^32 - 256; PT_BUFFER_LOADS addresses it with 32-bit offsets)
     uint32_t qroot;            // TLAS root in the records
     uint32_t root;
     uint32_t n_prims;

@@ -20,7 +20,8 @@
 // two traversals claim rays from.  The runtime rotates three sets: iteration i
 // reads its input count from set i % 3 (written by iteration i - 1), appends
 // into set (i + 1) % 3 and zeroes set (i + 2) % 3 for iteration i + 1.
-#define SET_WORDS (Q_WORDS + 2 * PT_POOL_WORDS)
+#define Q_TIES (Q_WORDS + 2 * PT_POOL_WORDS)  // closest-hit rays met an exact-t tie (k_closest_ties)
+#define SET_WORDS (Q_TIES + Q_STRIDE)
 // host snapshot slot (pinned, written by the iteration prologue)
 #define SNAP_PATHS 0        // paths entering the iteration
 #define SNAP_SHADOW_PREV 1  // shadow rays of the previous iteration
@@ -100,10 +101,13 @@ struct RenderParams {
 
 template <bool COUNT, bool INST>
 __global__ void k_closest(PathSoA P, const uint32_t* in, float4* hit, uint32_t* pool, uint32_t* ovf, uint32_t* spare,
-                          uint32_t* snap, unsigned long long* counters);
+                          uint32_t* snap, unsigned long long* counters, uint32_t* ties);
 template <bool COUNT, bool INST, bool QN>
 __global__ void k_closest_pool(PathSoA P, const uint32_t* in, float4* hit, uint32_t* pool, uint32_t* ovf,
-                               uint32_t* spare, uint32_t* snap, unsigned long long* counters);
+                               uint32_t* spare, uint32_t* snap, unsigned long long* counters, uint32_t* ties);
+// exact re-trace of the rays a pool kernel listed for exact-t ties (pt_pool.h)
+template <bool INST>
+__global__ void k_closest_ties(PathSoA P, const uint32_t* in, float4* hit, const uint32_t* pool, const uint32_t* ties);
 template <bool COUNT, bool INST>
 __global__ void k_shadow(PathSoA next, float* sample_L, const ShadowRec* sq, const uint32_t* nptr, uint32_t* pool,
                          uint32_t* ovf, unsigned long long* counters);
@@ -170,4 +174,5 @@ __global__ void k_light_cases(const float* in, uint32_t n, float* out);
 __global__ void k_light_picks(const float* u, uint32_t n, int32_t* out);
 template <bool QN>
 __global__ void k_trace_rays(const pt_ray* rays, uint32_t n, int any, pt_hit* out, uint32_t* pool, uint32_t* ovf,
-                             unsigned long long* counters);
+                             unsigned long long* counters, uint32_t* ties, uint32_t* n_ties);
+__global__ void k_trace_rays_ties(const pt_ray* rays, pt_hit* out, const uint32_t* ties, const uint32_t* n_ties);

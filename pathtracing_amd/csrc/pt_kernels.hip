@@ -168,6 +168,8 @@ struct ClosestSrc {
     PathSoA P;
     float4* hit;
     uint32_t front;  // continuing paths at the front of P
+    uint32_t* ties;      // rays to re-trace exactly (k_closest_ties), and their count
+    uint32_t* n_ties;
     // S.ray_order (PT_RENDER_SORT_RAYS): claim i traces path ray_order[i]
     __device__ __forceinline__ bool load(uint32_t i, f3& o, f3& d, float& tmax) {
         const uint32_t j = S.ray_order ? S.ray_order[i] : i;
@@ -181,6 +183,7 @@ struct ClosestSrc {
         hit[S.ray_order ? S.ray_order[i] : i] = make_float4(t, b1, b2, __int_as_float(prim));
     }
     __device__ __forceinline__ void any(uint32_t, bool) {}
+    __device__ __forceinline__ void tie(uint32_t i) { ties[atomicAdd(n_ties, 1u)] = i; }
 };
 
 template <bool COUNT, bool INST, bool QN>
@@ -188,7 +191,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES_FOR(PT_USES_SPEC(INST
                                                                 float4* __restrict__ hit, uint32_t* __restrict__ pool,
                                                                 uint32_t* __restrict__ ovf, uint32_t* __restrict__ spare,
                                                                 uint32_t* __restrict__ snap,
-                                                                unsigned long long* counters) {
+                                                                unsigned long long* counters, uint32_t* __restrict__ ties) {
     __shared__ uint32_t s_ref[PT_POOL_LDS_C * PT_TRACE_BLOCK];
     __shared__ uint16_t s_ent[PT_ENTRY ? PT_POOL_LDS_C * PT_TRACE_BLOCK : 1];
     __shared__ __attribute__((aligned(16))) uint8_t s_lut[(QN && PT_Q48) ? 8 * Q48_LUT_STRIDE : 4];
@@ -197,11 +200,34 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES_FOR(PT_USES_SPEC(INST
     if (n == 0) return;
     if constexpr (QN && PT_Q48) stage_q48_lut(s_lut);
     TraceWork wk{0, 0};
-    ClosestSrc src{P, hit, nptr[Q_NEXT]};
+    ClosestSrc src{P, hit, nptr[Q_NEXT], ties, pool + (Q_TIES - Q_WORDS)};
     trace_pool<false, COUNT, ClosestSrc, true, INST, PT_POOL_LDS_C, QN>(n, pool, src, s_ref, s_ent, ovf, wk, s_lut);
     if (COUNT) {
         count_add(counters, CNT_NODES_CLOSEST, wk.nodes);
         count_add(counters, CNT_TRIS_CLOSEST, wk.tris);
+    }
+}
+
+// Exact re-trace of the rays the pool kernel listed for an exact-t tie
+// (pt_pool.h "Exact-t ties"): trace_closest over the reference's clusters
+// in the reference's order; the listed count sits in the pool's counter set.
+template <bool INST>
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest_ties(PathSoA P, const uint32_t* __restrict__ nptr,
+                                                                float4* __restrict__ hit,
+                                                                const uint32_t* __restrict__ pool,
+                                                                const uint32_t* __restrict__ ties) {
+    __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+    const uint32_t n = pool[Q_TIES - Q_WORDS];
+    if (n == 0) return;
+    ClosestSrc src{P, hit, nptr[Q_NEXT], nullptr, nullptr};
+    TraceWork wk{0, 0};
+    for (uint32_t k = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x; k < n; k += gridDim.x * PT_TRACE_BLOCK) {
+        const uint32_t i = ties[k];
+        f3 o, d;
+        float tmax, t, b1, b2;
+        src.load(i, o, d, tmax);
+        const int prim = trace_closest<false, INST, PT_STACK>(o, d, tmax, t, b1, b2, s_ref, wk);
+        src.closest(i, t, b1, b2, prim);
     }
 }
 
@@ -217,6 +243,7 @@ struct ShadowSrc {
         return true;
     }
     __device__ __forceinline__ void closest(uint32_t, float, float, float, int) {}
+    __device__ __forceinline__ void tie(uint32_t) {}
     __device__ __forceinline__ void any(uint32_t i, bool hit) {
         if (hit) return;
         // unoccluded: add the contribution; one shadow ray per path per bounce,
@@ -286,7 +313,8 @@ template <bool COUNT, bool INST>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SIMPLE_WAVES void k_closest(PathSoA P, const uint32_t* __restrict__ nptr,
                                                            float4* __restrict__ hit, uint32_t* __restrict__,
                                                            uint32_t* __restrict__ ovf, uint32_t* __restrict__ spare,
-                                                           uint32_t* __restrict__ snap, unsigned long long* counters) {
+                                                           uint32_t* __restrict__ snap, unsigned long long* counters,
+                                                           uint32_t* __restrict__) {
     __shared__ uint32_t s_ref[PT_SIMPLE_LDS * PT_TRACE_BLOCK];
     iteration_prologue(nptr, spare, snap);
     const uint32_t n = path_count(nptr);  // the grid covers the wavefront's capacity
@@ -343,6 +371,8 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SIMPLE_WAVES void k_shadow(PathS
 struct RaysSrc {
     const pt_ray* rays;
     pt_hit* out;
+    uint32_t* ties;  // exact-t ties (pt_pool.h), re-traced by k_trace_rays_ties
+    uint32_t* n_ties;
     __device__ __forceinline__ bool load(uint32_t i, f3& o, f3& d, float& tmax) {
         const pt_ray r = rays[i];
         o = F3(r.o[0], r.o[1], r.o[2]);
@@ -354,22 +384,41 @@ struct RaysSrc {
         out[i] = pt_hit{t, b1, b2, prim};
     }
     __device__ __forceinline__ void any(uint32_t i, bool hit) { out[i] = pt_hit{0, 0, 0, hit ? 1 : 0}; }
+    __device__ __forceinline__ void tie(uint32_t i) { ties[atomicAdd(n_ties, 1u)] = i; }
 };
 
 template <bool QN>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(const pt_ray* __restrict__ rays, uint32_t n, int any,
                                                               pt_hit* __restrict__ out, uint32_t* __restrict__ pool,
-                                                              uint32_t* __restrict__ ovf, unsigned long long* counters) {
+                                                              uint32_t* __restrict__ ovf, unsigned long long* counters,
+                                                              uint32_t* __restrict__ ties, uint32_t* __restrict__ n_ties) {
     __shared__ uint32_t s_ref[PT_POOL_LDS * PT_TRACE_BLOCK];
     __shared__ uint16_t s_ent[PT_POOL_LDS_C * PT_TRACE_BLOCK];
     __shared__ __attribute__((aligned(16))) uint8_t s_lut[(QN && PT_Q48) ? 8 * Q48_LUT_STRIDE : 4];
     if constexpr (QN && PT_Q48) stage_q48_lut(s_lut);
     TraceWork wk{0, 0};
-    RaysSrc src{rays, out};
+    RaysSrc src{rays, out, ties, n_ties};
     if (any) trace_pool<true, true, RaysSrc, true, true, PT_POOL_LDS, QN>(n, pool, src, s_ref, nullptr, ovf, wk, s_lut);
     else trace_pool<false, true, RaysSrc, true, true, PT_POOL_LDS_C, QN>(n, pool, src, s_ref, s_ent, ovf, wk, s_lut);
     count_add(counters, any ? CNT_NODES_ANY : CNT_NODES_CLOSEST, wk.nodes);
     count_add(counters, any ? CNT_TRIS_ANY : CNT_TRIS_CLOSEST, wk.tris);
+}
+
+// pt_trace's exact re-trace of the rays k_trace_rays listed for an exact-t tie
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays_ties(const pt_ray* __restrict__ rays,
+                                                                   pt_hit* __restrict__ out,
+                                                                   const uint32_t* __restrict__ ties,
+                                                                   const uint32_t* __restrict__ n_ties) {
+    __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+    const uint32_t n = *n_ties;
+    TraceWork wk{0, 0};
+    for (uint32_t k = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x; k < n; k += gridDim.x * PT_TRACE_BLOCK) {
+        const pt_ray r = rays[ties[k]];
+        float t, b1, b2;
+        const int prim = trace_closest<false, true, PT_STACK>(F3(r.o[0], r.o[1], r.o[2]), F3(r.d[0], r.d[1], r.d[2]),
+                                                             r.tmax, t, b1, b2, s_ref, wk);
+        out[ties[k]] = pt_hit{t, b1, b2, prim};
+    }
 }
 
 // Test hook: closest hit + the full SurfaceInteraction the shade kernel
@@ -1668,14 +1717,16 @@ __global__ __launch_bounds__(256) void k_adapt_decide(const uint32_t* __restrict
 // instances (it costs the pool kernels registers: see DESIGN.md).
 #define PT_INST_TRACE(B, I)                                                                                         \
     template __global__ void k_closest<B, I>(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*, uint32_t*,     \
-                                             uint32_t*, unsigned long long*);                                        \
+                                             uint32_t*, unsigned long long*, uint32_t*);                             \
     template __global__ void k_shadow<B, I>(PathSoA, float*, const ShadowRec*, const uint32_t*, uint32_t*,           \
                                             uint32_t*, unsigned long long*);
 #define PT_INST_POOL(B, I, Q)                                                                                       \
     template __global__ void k_closest_pool<B, I, Q>(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*,        \
-                                                     uint32_t*, uint32_t*, unsigned long long*);                     \
+                                                     uint32_t*, uint32_t*, unsigned long long*, uint32_t*);          \
     template __global__ void k_shadow_pool<B, I, Q>(PathSoA, float*, const ShadowRec*, const uint32_t*, uint32_t*,   \
                                                     uint32_t*, unsigned long long*);
+template __global__ void k_closest_ties<false>(PathSoA, const uint32_t*, float4*, const uint32_t*, const uint32_t*);
+template __global__ void k_closest_ties<true>(PathSoA, const uint32_t*, float4*, const uint32_t*, const uint32_t*);
 PT_INST_TRACE(false, false)
 PT_INST_TRACE(true, false)
 PT_INST_TRACE(false, true)

@@ -109,6 +109,14 @@ __device__ unsigned int pt_diag[4];
 #ifndef PT_MASKED_LOADS
 #define PT_MASKED_LOADS 0
 #endif
+// ... or through a buffer resource, lanes without the step out of its range
+#ifndef PT_BUFFER_LOADS
+#define PT_BUFFER_LOADS 0
+#endif
+#define Q48_OOB_OFFSET 0xFFFFFF00u  // + 32 stays below 2^32: never wraps into range
+__device__ __forceinline__ float4 q48_buf_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+}
 // overflow words per stack entry per lane (ref + entry distance)
 #define PT_OVF_WORDS 2
 // Stack capacity of the pool kernels.  The reference's stack[32] is undefined
@@ -157,6 +165,10 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
     int ri = -1;
     f3 o = F3(0, 0, 0), d = F3(0, 0, 0), inv = F3(0, 0, 0);
     uint32_t oct = 0, ref = REF_EMPTY, leaf = REF_EMPTY;
+#if PT_Q48 && PT_BUFFER_LOADS
+    const __amdgpu_buffer_rsrc_t qrs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<DevGeom*>(S.qrec), (short)0, (int)S.qrec_bytes, 0x00020000);
+#endif
     // closest hit: an accepted hit is stored at once (Src::closest), so the
     // barycentrics and slot need no registers; OCT_FOUND marks that one was
     float tmax = 0;
@@ -269,7 +281,15 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         // (48 B); a lane without one reads record / slot 0 (shared lines, no
         // extra traffic)
         const uint32_t slot = prim_step ? (leaf & ~(REF_LEAF | REF_BLOCK)) : 0u;
-#if PT_Q48 && PT_MASKED_LOADS
+#if PT_Q48 && PT_BUFFER_LOADS
+        // raw buffer loads over the record array: a lane without the step
+        // reads past the buffer's end, which returns zeros without a fetch
+        // (the runtime keeps the array below 4 GiB in this build)
+        const uint32_t noff = node_step ? ref * 48u : Q48_OOB_OFFSET;
+        const uint32_t poff = prim_step ? slot * 48u : Q48_OOB_OFFSET;
+        const float4 q0 = q48_buf_load(qrs, noff), q1 = q48_buf_load(qrs, noff + 16u), q2 = q48_buf_load(qrs, noff + 32u);
+        const float4 g0 = q48_buf_load(qrs, poff), g1 = q48_buf_load(qrs, poff + 16u), g2 = q48_buf_load(qrs, poff + 32u);
+#elif PT_Q48 && PT_MASKED_LOADS
         // each side's loads under its own exec mask: a lane without a node
         // (primitive) step issues no node (slot) loads, so the vector memory
         // pipe processes only the lanes that step (its rate is per lane)
@@ -295,7 +315,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         const float4* __restrict__ qg = reinterpret_cast<const float4*>(S.geom + slot);
         const float4 q0 = qn[0], q1 = qn[1], q2 = qn[2], qc = qn[3];
 #endif
-#if !(PT_Q48 && PT_MASKED_LOADS)
+#if !(PT_Q48 && (PT_MASKED_LOADS || PT_BUFFER_LOADS))
         const float4 g0 = qg[0], g1 = qg[1], g2 = qg[2];
 #endif
         __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink the slot loads past the node side)
@@ -343,7 +363,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             else tri_hit = tri_glm(o, d, xyz(g0), xyz(g1), xyz(g2), bx, by, t) && !(t > tmax || t < PT_EPS);
             if (prim_step) {
                 bool anyhit = false;
-                const uint32_t next = (w0 & GF_LAST) ? REF_EMPTY : (REF_LEAF | (leaf & REF_BLOCK) | (slot + 1));
+                uint32_t next = (w0 & GF_LAST) ? REF_EMPTY : (REF_LEAF | (leaf & REF_BLOCK) | (slot + 1));
                 // the primitive's slot (PT_Q48: the record keeps it in c.w)
                 const uint32_t ps = PT_Q48 ? __float_as_uint(g2.w) : slot;
                 if (kind == PT_PRIM_TRIANGLE) {
@@ -352,13 +372,23 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                         if (ANY) {
                             anyhit = true;
                         } else {
+                            if ((oct & (OCT_FOUND | OCT_TIE)) == OCT_FOUND && t == tmax) {
+                                oct |= OCT_TIE;  // an exact tie: the reference's culling decides (pt_pool.h top)
+                                src.tie((uint32_t)ri);
+                            }
                             tmax = t;
                             oct |= OCT_FOUND;
                             src.closest((uint32_t)ri, t, bx, by, (int)ps);
                         }
                     }
                 } else if (kind == PT_PRIM_BLAS) {
-                    push(__float_as_uint(g1.x));  // the node side is paused (REF_BLOCK): visited next
+                    // the reference recurses into the BLAS inside the leaf loop
+                    // (Model::Intersect, BVH.hpp:1206): the rest of the leaf
+                    // waits on the stack under the BLAS root, which the
+                    // (paused) node side visits next
+                    if (next != REF_EMPTY) push(next);
+                    push(__float_as_uint(g1.x));
+                    next = REF_EMPTY;
                 } else {
                     if (COUNT) wk.tris++;
                     if (ANY) {
@@ -366,6 +396,10 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                     } else {
                         float t2, a2, b2;
                         if (other_closest(ps, w0, o, d, tmax, t2, a2, b2)) {
+                            if ((oct & (OCT_FOUND | OCT_TIE)) == OCT_FOUND && t2 == tmax) {
+                                oct |= OCT_TIE;
+                                src.tie((uint32_t)ri);
+                            }
                             tmax = t2;
                             oct |= OCT_FOUND;
                             src.closest((uint32_t)ri, t2, a2, b2, (int)ps);
@@ -391,6 +425,19 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
 //   bool load(uint32_t ri, f3& o, f3& d, float& tmax)   (false: skip this ray)
 //   void closest(uint32_t ri, float t, float b1, float b2, int prim)
 //   void any(uint32_t ri, bool hit)
+//   void tie(uint32_t ri)   (closest hit: the ray met an exact-t tie, see below)
+//
+// Exact-t ties.  A hit at t == max replaces the current one, in the
+// reference as here (Shape.cpp:204 rejects only t > max).  The pool
+// traversals visit a superset of the reference's nodes (quantized boxes
+// enclose the float boxes; the overlapped form tests nodes ahead of the
+// pending leaf, against a max that leaf may still shorten), and the only
+// primitive such an extra visit can change the result with is one at exactly
+// t == max in a node the reference culled (its float box entry == max).  So
+// a ray that meets t == max once a hit exists is listed (Src::tie), and
+// k_closest_ties re-traces the listed rays with trace_closest over the
+// reference's own clusters in the reference's order, which decides ties as
+// the reference does (tests/golden tie_models: three coincident Models).
 // POOL = false: no refill, lane i of the grid traces ray i (small scenes,
 // where traversal lengths are uniform and the claims would only cost).
 // LN: stack entries in LDS (s_ref, and s_ent for closest hit with PT_ENTRY);
@@ -706,6 +753,10 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                             if (ANY) {
                                 anyhit = true;
                             } else {
+                                if (POOL && best >= 0 && t == tmax && !(oct & OCT_TIE)) {
+                                    oct |= OCT_TIE;
+                                    src.tie((uint32_t)ri);
+                                }
                                 tmax = t;
                                 best = (int)sl;
                                 bb1 = bx;
@@ -725,7 +776,11 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                     next = (w1 & GF_LAST) ? REF_EMPTY : (REF_LEAF | (slot + 2));
                 }
             } else if (kind == PT_PRIM_BLAS) {
+                // BLAS (or instance) first, the rest of the leaf after it, as
+                // the reference's recursion inside the leaf loop (BVH.hpp:1206)
+                if (next != REF_EMPTY) push(next);
                 push(__float_as_uint(q1.x));
+                next = REF_EMPTY;
             } else {
                 if (COUNT) wk.tris++;
                 if (ANY) {
@@ -733,6 +788,10 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 } else {
                     float t, a, b;
                     if (other_closest(slot, w0, o, d, tmax, t, a, b)) {
+                        if (POOL && best >= 0 && t == tmax && !(oct & OCT_TIE)) {
+                            oct |= OCT_TIE;
+                            src.tie((uint32_t)ri);
+                        }
                         tmax = t;
                         best = (int)slot;
                         bb1 = a;

@@ -64,6 +64,7 @@ struct pt_ctx {
     uint32_t* qcnt = nullptr;
     uint32_t* ovf = nullptr;  // pool traversal stack entries beyond PT_POOL_LDS
     uint32_t* ovf_any = nullptr;  // the any-hit pool kernel's half of ovf (they may run together)
+    uint32_t* ties = nullptr;     // closest-hit rays listed for the exact re-trace (k_closest_ties)
     uint32_t* scratch = nullptr;  // instance traversal state, SCR_WORDS x scratch_lanes
     uint64_t scratch_lanes = 0;
     ShadowRec* sq = nullptr;
@@ -369,7 +370,7 @@ static void free_scene(pt_ctx* c) {
 }
 static void free_work(pt_ctx* c) {
     void* bufs[] = {c->PA.o, c->PA.d, c->PA.beta, c->PA.L, c->PA.sid, c->PB.o, c->PB.d, c->PB.beta, c->PB.L,
-                    c->PB.sid, c->hit, c->qcnt, c->sq, c->counters, c->ovf};
+                    c->PB.sid, c->hit, c->qcnt, c->sq, c->counters, c->ovf, c->ties};
     for (void* p : bufs)
         if (p) hipFree(p);
     c->PA = PathSoA{};
@@ -380,6 +381,7 @@ static void free_work(pt_ctx* c) {
     c->counters = nullptr;
     c->ovf = nullptr;
     c->ovf_any = nullptr;
+    c->ties = nullptr;
     c->cap = 0;
 }
 
@@ -1041,8 +1043,11 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
         // nodes and leaf slots in one array of 48-B records (pt_device.h)
         std::vector<DevGeom> rec;
         std::vector<uint32_t> qroots;
-        const bool ok = nodes.size() < REF_BLOCK && s->n_prims < REF_BLOCK &&
-                        build_q48(nodes, geom, roots, s->n_prims, rec, qroots);
+        bool ok = nodes.size() < REF_BLOCK && s->n_prims < REF_BLOCK &&
+                  build_q48(nodes, geom, roots, s->n_prims, rec, qroots);
+        // 32-bit buffer offsets (PT_BUFFER_LOADS) below the out-of-range marker
+        if (PT_BUFFER_LOADS && ok && rec.size() * sizeof(DevGeom) >= (uint64_t)Q48_OOB_OFFSET) ok = false;
+        DS.qrec_bytes = ok ? (uint32_t)(rec.size() * sizeof(DevGeom)) : 0u;
         c->has_qnodes = ok;
         if (ok) {
             UP(DS.qrec, rec.data(), rec.size());
@@ -1213,7 +1218,9 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
         AL(P->sid, n * 4);
     }
     AL(c->hit, n * 16);
-    AL(c->qcnt, (3 * SET_WORDS + PT_POOL_WORDS) * 4);  // three counter sets, then pt_trace's pool
+    AL(c->ties, n * 4);  // a ray is listed at most once per launch
+    // three counter sets, then pt_trace's pool and its tie count
+    AL(c->qcnt, (3 * SET_WORDS + PT_POOL_WORDS + Q_STRIDE) * 4);
     AL(c->sq, n * sizeof(ShadowRecV));  // the larger record (VolPath's)
     AL(c->counters, (CNT_SHARDS + 1) * CNT_COUNT * 8);
     // stack entries past the LDS part: the pool kernels' resident grid x
@@ -1231,7 +1238,7 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
         c->ovf_any = c->ovf + half;
     }
 #undef AL
-    if (hipMemset(c->qcnt, 0, (3 * SET_WORDS + PT_POOL_WORDS) * 4) != hipSuccess) {
+    if (hipMemset(c->qcnt, 0, (3 * SET_WORDS + PT_POOL_WORDS + Q_STRIDE) * 4) != hipSuccess) {
         free_work(c);
         return fail(c, PT_ERR_HIP, "hipMemset of the queue counters failed");
     }
@@ -1295,7 +1302,7 @@ static pt_status bind_scene(pt_ctx* c, uint64_t lanes = 0) {
 
 // traversal kernel of one wavefront iteration
 using ClosestFn = void (*)(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*, uint32_t*, uint32_t*,
-                           unsigned long long*);
+                           unsigned long long*, uint32_t*);
 using ShadowFn = void (*)(PathSoA, float*, const ShadowRec*, const uint32_t*, uint32_t*, uint32_t*,
                           unsigned long long*);
 template <bool C, bool I>
@@ -1540,7 +1547,12 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                 auto kc = pick_closest(use_pool, qn, inst, count);
                 hipLaunchKernelGGL(kc, gt, dim3(PT_TRACE_BLOCK), 0, sm, cur, (const uint32_t*)in, c->hit,
                                    out + Q_WORDS, c->ovf, spare, c->host_cnt_dev + (i % PT_RING) * SNAP_WORDS,
-                                   c->counters);
+                                   c->counters, c->ties);
+                if (use_pool)  // the rays that met an exact-t tie, re-traced in the reference's order
+                    hipLaunchKernelGGL(inst ? k_closest_ties<true> : k_closest_ties<false>,
+                                       dim3(std::min(64u, gt.x)), dim3(PT_TRACE_BLOCK), 0, sm, cur,
+                                       (const uint32_t*)in, c->hit, (const uint32_t*)(out + Q_WORDS),
+                                       (const uint32_t*)c->ties);
             }
             if (timing) HIPCHK(c, hipEventRecord(ev[1], sm));
             // the hit sort and the shading rewrite the shadow queue, the sample
@@ -2088,14 +2100,22 @@ extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
     uint32_t* pool = c->qcnt + 3 * SET_WORDS;
-    HIPCHK(c, hipMemsetAsync(pool, 0, PT_POOL_WORDS * 4, c->stream));
+    uint32_t* n_ties = pool + PT_POOL_WORDS;
+    HIPCHK(c, hipMemsetAsync(pool, 0, (PT_POOL_WORDS + Q_STRIDE) * 4, c->stream));
+    uint32_t* tl = nullptr;  // rays listed for the exact re-trace (at most each once)
+    HIPCHK(c, hipMalloc((void**)&tl, (size_t)n * 4));
+    tmp.push_back(tl);
     // the pool traversal of the renderer: quantized nodes where the renderer
     // would use them (large scenes), unless pt_set_node_format says otherwise
     const bool qn = c->has_qnodes && (c->node_format == PT_NODES_QUANTIZED ||
                                       (c->node_format == PT_NODES_AUTO && c->n_clusters >= PT_POOL_MIN_CLUSTERS));
-    hipLaunchKernelGGL(qn ? k_trace_rays<true> : k_trace_rays<false>,
-                       dim3(std::max(1u, std::min((n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK, c->trace_blocks))),
-                       dim3(PT_TRACE_BLOCK), 0, c->stream, dr, n, any_hit, dh, pool, c->ovf, c->counters);
+    const uint32_t tb = std::max(1u, std::min((n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK, c->trace_blocks));
+    hipLaunchKernelGGL(qn ? k_trace_rays<true> : k_trace_rays<false>, dim3(tb), dim3(PT_TRACE_BLOCK), 0, c->stream, dr,
+                       n, any_hit, dh, pool, c->ovf, c->counters, tl, n_ties);
+    HIPCHK(c, hipGetLastError());
+    if (!any_hit)
+        hipLaunchKernelGGL(k_trace_rays_ties, dim3(std::min(64u, tb)), dim3(PT_TRACE_BLOCK), 0, c->stream,
+                           (const pt_ray*)dr, dh, (const uint32_t*)tl, (const uint32_t*)n_ties);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
     if (!hdev) HIPCHK(c, hipMemcpyAsync(hits, dh, (size_t)n * sizeof(pt_hit), hipMemcpyDeviceToHost, c->stream));

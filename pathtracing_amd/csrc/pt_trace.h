@@ -543,8 +543,12 @@ __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out
                     }
                 }
             } else if (kind == PT_PRIM_BLAS) {  // a Model's BLAS root, or REF_INST_ENTER | slot
+                // the BLAS first, the rest of the leaf after it: the
+                // reference recurses inside its leaf loop (BVH.hpp:1206)
                 if (COUNT) wk.tris--;
+                if (!(w0 & GF_LAST)) push(REF_LEAF | (slot + 1));
                 push(__float_as_uint(g.b.x));
+                break;
             } else {
                 float t, a, b;
                 if (other_closest(slot, w0, o, d, tmax, t, a, b)) {

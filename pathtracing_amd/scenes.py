@@ -134,6 +134,32 @@ def _box(center, size, angle):
     return _merge([_quad_tris(*f) for f in faces])
 
 
+def tie_models(W: int = 32, H: int = 32, spp: int = 4, max_depth: int = 8, seed: int = 0x5EED0035) -> SceneSetup:
+    """Exact-t ties across BLAS hops: the Cornell walls as two identical
+    Models with different materials, plus a third copy of the floor beside a
+    quad light in the TLAS.  Identical boxes cannot be split, so the TLAS
+    holds the Models in one leaf; every wall hit is a tie, which the
+    reference breaks by visit order: it recurses into each Model inside its
+    leaf loop (Model::Intersect, BVH.hpp:1206) and a tie accepts the later
+    hit (Primitive.cpp:6-26).  A traversal that visits a leaf's BLAS after
+    the rest of the leaf picks the other Model."""
+    scene = Scene()
+    walls = [
+        _quad_tris((-1, -1, 1), (1, -1, 1), (1, -1, -1), (-1, -1, -1)),   # floor
+        _quad_tris((-1, -1, -1), (1, -1, -1), (1, 1, -1), (-1, 1, -1)),   # back
+        _quad_tris((-1, -1, 1), (-1, -1, -1), (-1, 1, -1), (-1, 1, 1)),   # left
+        _quad_tris((1, -1, -1), (1, -1, 1), (1, 1, 1), (1, 1, -1)),       # right
+    ]
+    mats = [MicrofacetDiffuse((0.73, 0.73, 0.73)), MicrofacetDiffuse((0.65, 0.05, 0.05)),
+            MicrofacetDiffuse((0.12, 0.45, 0.15))]
+    for m in mats:
+        scene.Add(Model([Mesh(i, v, None, n, uv, m) for (i, v, n, uv) in walls]))
+    light = AreaLight(QuadShape((-0.25, 0.999, -0.25), (0.5, 0, 0), (0, 0, 0.5)), (17.0, 12.0, 4.0), False)
+    scene.Add(GeometricPrimitive(light.getShape(), MicrofacetDiffuse((0.78, 0.78, 0.78)), light))
+    camera = Camera((0, 0, 3.7), (0, 0, 0), 0.75, Film((W, H), MitchellFilter()))
+    return SceneSetup(scene, camera, "path", UniformLightSampler(), max_depth, seed, spp).finish()
+
+
 def cornell(W: int = 1024, H: int = 1024, spp: int = 256, config: str = "c2", max_depth: int = 8,
             seed: Optional[int] = None, fog: bool = False, filt=None, lens=None) -> SceneSetup:
     """C2/C3 Cornell box: 5 walls + 2 boxes as one triangle Model (34 tris) and

@@ -51,6 +51,9 @@ def parity_scenes():
         # the host's Integral() (the reference's is a jittered estimate)
         "lanczos": lambda: scenes.cornell(W=32, H=32, spp=4, config="c3", seed=0x5EED0034,
                                           filt=LanczosFilter((1.5, 1.5), 3.0)),
+        # exact-t ties across BLAS hops in one TLAS leaf (three identical
+        # Models): the reference's recursion order decides which one is hit
+        "tie_models": lambda: scenes.tie_models(W=32, H=32, spp=4),
         # emitters inside instances: TransformedLight / AnimatedLight
         # (Light.cpp:300-364) for an emissive Model, a quad and a sphere light
         "lit_instances": lambda: scenes.lit_instances(W=32, H=32, spp=4),

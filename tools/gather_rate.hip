@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256) void k_chase(const uint4* __restrict__ t, uint
             if constexpr (P >= 300) {  // 3xx: buffer loads, idle lanes out of the buffer's range (no fetch)
                 const __amdgpu_buffer_rsrc_t rs =
                     __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(t), (short)0, (int)(granules * 64u), 0x00020000);
-                const uint32_t off = on ? a * 64u : 0xFFFFFFF0u;
+                const uint32_t off = on ? a * 64u : 0xFFFFFF00u;  // (+48 must not wrap into range)
                 const uint4 q0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
                 const uint4 q1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16u, 0, 0));
                 const uint4 q2 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 32u, 0, 0));
