@@ -466,7 +466,8 @@ __global__ void k_bsdf_cases(int mid, const float* __restrict__ in, uint32_t n, 
     si.t = c[20];
     si.mat = mid;
     si.light = -1;
-    const Bxdf b = mat_scatter(mid, ro, rd, si, c[21], c[22], c[23]);
+    const MatTex mt = mat_tex(mid, si);
+    const Bxdf b = mat_scatter(mt, ro, rd, si, c[21], c[22], c[23]);
     if (b.ok) {
         o[0] = 1.0f;
         o[1] = b.f.x; o[2] = b.f.y; o[3] = b.f.z;
@@ -474,14 +475,14 @@ __global__ void k_bsdf_cases(int mid, const float* __restrict__ in, uint32_t n, 
         o[5] = (float)b.flags;
         o[6] = b.o.x; o[7] = b.o.y; o[8] = b.o.z;
         o[9] = b.d.x; o[10] = b.d.y; o[11] = b.d.z;
-        const f3 a = mat_f(mid, rd, si, b.d);
+        const f3 a = mat_f(mt, rd, si, b.d);
         o[12] = a.x; o[13] = a.y; o[14] = a.z;
-        o[15] = mat_pdf(mid, rd, si, b.d);
+        o[15] = mat_pdf(mt, rd, si, b.d);
     }
     const f3 other = F3(c[24], c[25], c[26]);
-    const f3 a2 = mat_f(mid, rd, si, other);
+    const f3 a2 = mat_f(mt, rd, si, other);
     o[16] = a2.x; o[17] = a2.y; o[18] = a2.z;
-    o[19] = mat_pdf(mid, rd, si, other);
+    o[19] = mat_pdf(mt, rd, si, other);
 }
 
 // Test hook: LightSampler::Sample(u) picks (pt_light_picks): the light index
@@ -731,7 +732,8 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
                 ro = at_f(ro, rd, si.t);
             } else {
                 const float us = INTEGRATOR == PT_INTEGRATOR_PATH ? r[4] : r[2];
-                const Bxdf b = mat_scatter(si.mat, ro, rd, si, us, r[0], r[1]);
+                const MatTex mt = mat_tex(si.mat, si);  // the hit's textures, read once
+                const Bxdf b = mat_scatter(mt, ro, rd, si, us, r[0], r[1]);
                 if (!b.ok) {
                     alive = false;  // absorbed
                 } else {
@@ -756,7 +758,7 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
                                 float lpdf = l.pmf;
                                 const float dt = dot_yxz(si.ns, sd);  // as built: y, x, z order
                                 if (!(lpdf <= 0 || dt * dot(rd, si.ns) >= 0)) {
-                                    const f3 f = mat_f(si.mat, rd, si, sd) * fabsf(dt);
+                                    const f3 f = mat_f(mt, rd, si, sd) * fabsf(dt);
                                     f3 c;
                                     bool ok = true;
                                     if (light_is_delta(l)) {
@@ -767,7 +769,7 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
                                             ok = false;
                                         } else {
                                             const float w2 = lpdf * lpdf;
-                                            const float w1 = mat_pdf(si.mat, rd, si, sd);
+                                            const float w1 = mat_pdf(mt, rd, si, sd);
                                             const float wl = w2 / fma_(w1, w1, w2);  // w1*w1 + w2 fused
                                             c = ((light_L(l, ls.n, ls.u, ls.v, sd) * f) * wl) / lpdf;
                                         }
@@ -781,7 +783,7 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
                                     }
                                 }
                             }
-                            prev = mat_pdf(si.mat, rd, si, b.d);
+                            prev = mat_pdf(mt, rd, si, b.d);
 #ifdef PT_DEBUG_KEY
                             if (key == PT_DEBUG_KEY)
                                 printf("G  nee c %a %a %a (light %d) shadow %d\n", srec.c.x, srec.c.y, srec.c.z, li,
@@ -944,8 +946,10 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
             }
             Bxdf b;
             b.ok = false;
+            MatTex mt{};
             if (!mvalid && si.mat >= 0) {
-                b = mat_scatter(si.mat, ro, rd, si, r[4], r[0], r[1]);
+                mt = mat_tex(si.mat, si);  // the hit's textures, read once
+                b = mat_scatter(mt, ro, rd, si, r[4], r[0], r[1]);
                 if (b.ok && !(b.flags & FL_SPEC)) nee = true;
             }
             if (nee) {
@@ -974,8 +978,8 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                     } else {
                         const float dt = dot(si.ns, sd);
                         ok = !(dt * dot(rd, si.ns) >= 0);
-                        spdf = ok ? mat_pdf(si.mat, rd, si, sd) : 0.0f;
-                        f = ok ? mat_f(si.mat, rd, si, sd) * fabsf(dt) : F3(0, 0, 0);
+                        spdf = ok ? mat_pdf(mt, rd, si, sd) : 0.0f;
+                        f = ok ? mat_f(mt, rd, si, sd) * fabsf(dt) : F3(0, 0, 0);
                     }
                     if (ok && !is_zero(f)) {
                         // the shadow kernel forms ((Tr * L) * f * w) / pdf
@@ -1026,7 +1030,7 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                     int nm = get_medium(si, smed, b.d);
                     if (!(b.flags & FL_TRANS) && dot(rd, si.ns) <= 0) nm = med;
                     spec = (b.flags & FL_SPEC) != 0;
-                    if (!spec) prev = mat_pdf(si.mat, rd, si, b.d);
+                    if (!spec) prev = mat_pdf(mt, rd, si, b.d);
                     att = att * ((b.f * fabsf(dot(si.ns, b.d))) / b.pdf);
                     ro = b.o;
                     rd = b.d;

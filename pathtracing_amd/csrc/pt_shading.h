@@ -48,7 +48,10 @@ __device__ __forceinline__ void stage_tables(bool light_sampler) {
     if (f & LDS_TEX) stage_words(pt_lds_tex, S.textures, S.n_textures);
     if (f & LDS_IMG) stage_words(pt_lds_img, S.images, S.n_images);
 #if PT_LDS_TABLES >= 2
-    if (light_sampler && (f & LDS_LS) && S.light_sampler != PT_LS_UNIFORM && S.n_sampler_lights) {
+    // staged by every staging kernel, whatever it says it samples: ls_sample
+    // reads them whenever LDS_LS is set (light_sampler only documents)
+    (void)light_sampler;
+    if ((f & LDS_LS) && S.light_sampler != PT_LS_UNIFORM && S.n_sampler_lights) {
         stage_words(pt_lds_guide, S.sampler_guide, PT_LS_GUIDE + 1);
         stage_words(pt_lds_cdf, S.sampler_cdf, S.n_sampler_lights);
     }
@@ -454,8 +457,38 @@ struct Bxdf {
     bool ok;
 };
 
-__device__ __forceinline__ float diffuse_rough(const pt_material& m, const SurfInt& si) {
-    return smax(tex_eval(m.rough, si.u, si.v).y, 0.0001f);
+// A hit's material record and texture values, read once per hit: the
+// reference evaluates the same textures again in scatter, calc_attenuation
+// and PDF (Material.hpp:206-348, 392-564); the values are the same, so one
+// evaluation serves all three and its texel loads are issued together.
+struct MatTex {
+    uint32_t kind;
+    f3 col;       // tex (DIFFUSE / DIELECTRIC / THIN) or albedo (CONDUCTOR)
+    float rough;  // DIFFUSE: max(rough.y, 0.0001) (GetRoughness); DIELECTRIC: rough.y
+    float metal;  // DIFFUSE: metal.z
+    float ri;
+};
+__device__ __forceinline__ MatTex mat_tex(int mid, const SurfInt& si) {
+    const pt_material m = mat_rec(mid);
+    MatTex t;
+    t.kind = m.kind;
+    t.ri = m.ri;
+    t.rough = 0.0f;
+    t.metal = 0.0f;
+    switch (m.kind) {
+        case PT_MAT_DIFFUSE:
+            t.rough = smax(tex_eval(m.rough, si.u, si.v).y, 0.0001f);
+            t.metal = tex_eval(m.metal, si.u, si.v).z;
+            t.col = tex_eval(m.tex, si.u, si.v);
+            break;
+        case PT_MAT_DIELECTRIC:
+            t.rough = tex_eval(m.rough, si.u, si.v).y;
+            t.col = tex_eval(m.tex, si.u, si.v);
+            break;
+        case PT_MAT_THIN: t.col = tex_eval(m.tex, si.u, si.v); break;
+        default: t.col = ld3(m.albedo);
+    }
+    return t;
 }
 // onb TBN(dot(d, ns) > 0 ? -ns : ns) and wo = TBN.toLocal(-d) as
 // MicrofacetDiffuse's three entry points are built: the sign test is the
@@ -468,11 +501,11 @@ __device__ __forceinline__ f3 diffuse_frame(f3 d, f3 ns, Onb& tbn) {
 }
 
 // MicrofacetDiffuse::scatter (Material.hpp:206-266)
-__device__ Bxdf diffuse_scatter(const pt_material& m, f3 ind, const SurfInt& si, float u,
+__device__ Bxdf diffuse_scatter(const MatTex& m, f3 ind, const SurfInt& si, float u,
                                 float uv0, float uv1) {
     Bxdf b;
     b.ok = false;
-    float rough = diffuse_rough(m, si);
+    float rough = m.rough;
     Dist D = mkdist(rough);
     float prob = rough >= 0.7 ? 1.0f : 0.5f;
     Onb tbn;
@@ -493,8 +526,8 @@ __device__ Bxdf diffuse_scatter(const pt_material& m, f3 ind, const SurfInt& si,
     const float dwh = dot_yxz(wo, wh);
     float spdf = (1.0f - prob) * mpdf_(D, wo, wh, dwh) / (4 * fabsf(dwh));
     float pdf = fma_(prob * wi.z, PT_INV_PI, spdf);
-    f3 col = tex_eval(m.tex, si.u, si.v);
-    float metal = tex_eval(m.metal, si.u, si.v).z;
+    const f3 col = m.col;
+    const float metal = m.metal;
     // glm::mix(0.04, col, metal) as built here: col*metal rounded, the other fused
     const float om = 1.0f - metal;
     f3 F0 = F3(fma_(om, 0.04f, col.x * metal), fma_(om, 0.04f, col.y * metal), fma_(om, 0.04f, col.z * metal));
@@ -513,15 +546,15 @@ __device__ Bxdf diffuse_scatter(const pt_material& m, f3 ind, const SurfInt& si,
     return b;
 }
 // MicrofacetDiffuse::calc_attenuation (Material.hpp:299-326)
-__device__ f3 diffuse_f(const pt_material& m, f3 ind, const SurfInt& si, f3 dir) {
+__device__ f3 diffuse_f(const MatTex& m, f3 ind, const SurfInt& si, f3 dir) {
     Onb tbn;
     f3 wo = diffuse_frame(ind, si.ns, tbn);
     f3 wi = to_local(tbn, dir);
     f3 wh = normalize(wo + wi);
-    float rough = diffuse_rough(m, si);
-    float metal = tex_eval(m.metal, si.u, si.v).z;
+    const float rough = m.rough;
+    const float metal = m.metal;
     Dist D = mkdist(rough);
-    f3 col = tex_eval(m.tex, si.u, si.v);
+    const f3 col = m.col;
     // glm::mix as built here: (1-metal)*0.04 rounded, col*metal fused
     const float om = 1.0f - metal, c4 = om * 0.04f;
     f3 F0 = F3(fma_(col.x, metal, c4), fma_(col.y, metal, c4), fma_(col.z, metal, c4));
@@ -533,8 +566,8 @@ __device__ f3 diffuse_f(const pt_material& m, f3 ind, const SurfInt& si, f3 dir)
     return fma3s(PT_INV_PI, kc, num / den);
 }
 // MicrofacetDiffuse::PDF (Material.hpp:281-296): no (1-prob) on the specular term (A.7)
-__device__ float diffuse_pdf(const pt_material& m, f3 ind, const SurfInt& si, f3 dir) {
-    float rough = diffuse_rough(m, si);
+__device__ float diffuse_pdf(const MatTex& m, f3 ind, const SurfInt& si, f3 dir) {
+    const float rough = m.rough;
     Dist D = mkdist(rough);
     Onb tbn;
     f3 wo = diffuse_frame(ind, si.ns, tbn);
@@ -550,11 +583,11 @@ __device__ float diffuse_pdf(const pt_material& m, f3 ind, const SurfInt& si, f3
 __device__ __forceinline__ f3 to_local_ool(const Onb& b, f3 v) { return F3(dot_yxz(v, b.a0), dot_yxz(v, b.a1), dot(v, b.a2)); }
 
 // MicrofacetDielectric::scatter (Material.hpp:392-477), contractions as built
-__device__ Bxdf dielectric_scatter(const pt_material& m, f3 ino, f3 ind, const SurfInt& si,
+__device__ Bxdf dielectric_scatter(const MatTex& m, f3 ino, f3 ind, const SurfInt& si,
                                    float u, float uv0, float uv1) {
     Bxdf b;
     b.ok = false;
-    float rough = tex_eval(m.rough, si.u, si.v).y;
+    const float rough = m.rough;
     Dist D = mkdist(rough);
     Onb tbn = onb_si(si);
     const f3 md = -ind;
@@ -571,13 +604,13 @@ __device__ Bxdf dielectric_scatter(const pt_material& m, f3 ino, f3 ind, const S
         if (u < (R / (R + T))) {
             dir = to_world(tbn, F3(-wo.x, -wo.y, wo.z));
             b.o = F3(hitp.x + PT_EPS * Ng.x, hitp.y + PT_EPS * Ng.y, fma_(Ng.z, PT_EPS, hitp.z));
-            b.f = (tex_eval(m.tex, si.u, si.v) * R) / fabsf(dot(si.ns, dir));
+            b.f = (m.col * R) / fabsf(dot(si.ns, dir));
             b.pdf = R / (R + T);
         } else {
             dir = refract_f(ind, N, eta, dot(ind, N));
             if (is_zero(dir)) return b;
             b.o = F3(hitp.x - PT_EPS * Ng.x, hitp.y - PT_EPS * Ng.y, fma_(-Ng.z, PT_EPS, hitp.z));
-            b.f = (tex_eval(m.tex, si.u, si.v) * T) / fabsf(dot(si.ns, dir));
+            b.f = (m.col * T) / fabsf(dot(si.ns, dir));
             b.pdf = T / (R + T);
         }
         b.d = dir;
@@ -597,7 +630,7 @@ __device__ Bxdf dielectric_scatter(const pt_material& m, f3 ino, f3 ind, const S
         b.o = F3(hitp.x + PT_EPS * Ng.x, hitp.y + PT_EPS * Ng.y, fma_(Ng.z, PT_EPS, hitp.z));
         b.d = to_world(tbn, wi);
         b.pdf = mpdf_(D, wo, wh, dot(wo, wh)) / (fabsf(dow) * 4) * R / (R + T);
-        b.f = (((tex_eval(m.tex, si.u, si.v) * D_(D, wh)) * G_(D, wo, wi)) * R) / fabsf(4 * wi.z * wo.z);
+        b.f = (((m.col * D_(D, wh)) * G_(D, wo, wi)) * R) / fabsf(4 * wi.z * wo.z);
     } else {
         f3 wi = refract_f(-wo, wh, eta, -dow);
         if (wo.z * wi.z > 0 || wi.z == 0) return b;
@@ -609,7 +642,7 @@ __device__ Bxdf dielectric_scatter(const pt_material& m, f3 ino, f3 ind, const S
         float dwh = fabsf(diw) / denom;
         b.pdf = mpdf_(D, wo, wh, dot(wo, wh)) * dwh * T / (R + T);
         float ft = T * D_(D, wh) * G_(D, wo, wi) * fabsf(diw * dow / (denom * wi.z * wo.z));
-        b.f = tex_eval(m.tex, si.u, si.v) * ft;
+        b.f = m.col * ft;
     }
     b.flags = fl;
     b.ok = true;
@@ -619,9 +652,9 @@ __device__ Bxdf dielectric_scatter(const pt_material& m, f3 ino, f3 ind, const S
 // builds its own half vector, wi*etap + wo unfused in PDF and with the x, y
 // lanes fused in calc_attenuation
 template <bool FOR_F>
-__device__ __forceinline__ bool dielectric_frame(const pt_material& m, f3 ind, const SurfInt& si, f3 dir, Dist& D,
+__device__ __forceinline__ bool dielectric_frame(const MatTex& m, f3 ind, const SurfInt& si, f3 dir, Dist& D,
                                                  f3& wo, f3& wi, f3& wh, float& etap, bool& refl) {
-    float rough = tex_eval(m.rough, si.u, si.v).y;
+    const float rough = m.rough;
     D = mkdist(rough);
     float ri = m.ri;
     if (ri == 1 || smooth_(D)) return false;
@@ -640,7 +673,7 @@ __device__ __forceinline__ bool dielectric_frame(const pt_material& m, f3 ind, c
     if (dot(h, wi) * ci <= 0.0 || dot(h, wo) * co <= 0.0) return false;
     return true;
 }
-__device__ void dielectric_eval(const pt_material& m, f3 ind, const SurfInt& si, f3 dir,
+__device__ void dielectric_eval(const MatTex& m, f3 ind, const SurfInt& si, f3 dir,
                                 f3& f_out, float& pdf_out) {
     f_out = F3(0, 0, 0);
     pdf_out = 0;
@@ -664,7 +697,7 @@ __device__ void dielectric_eval(const pt_material& m, f3 ind, const SurfInt& si,
     if (dielectric_frame<true>(m, ind, si, dir, D, wo, wi, wh, etap, refl)) {
         const float dow = dot(wh, wo), diw = dot(wh, wi);
         float F = fresnel_dielectric(dow, m.ri);
-        f3 col = tex_eval(m.tex, si.u, si.v);
+        const f3 col = m.col;
         if (refl) {
             f_out = (((col * D_(D, wh)) * G_(D, wo, wi)) * F) / fabsf(4 * wi.z * wo.z);
         } else {
@@ -676,7 +709,7 @@ __device__ void dielectric_eval(const pt_material& m, f3 ind, const SurfInt& si,
     }
 }
 // ThinDielectric::scatter (Material.hpp:605-644)
-__device__ Bxdf thin_scatter(const pt_material& m, f3 ino, f3 ind, const SurfInt& si, float u) {
+__device__ Bxdf thin_scatter(const MatTex& m, f3 ino, f3 ind, const SurfInt& si, float u) {
     Bxdf b;
     // as built: onb(si)'s cross rounded-first in every lane, wo.x and wo.y in
     // y, x, z order, 1 - R*R fused, hit point fused, +-eps*Ng unfused
@@ -706,20 +739,20 @@ __device__ Bxdf thin_scatter(const pt_material& m, f3 ino, f3 ind, const SurfInt
         f = (F3(1, 1, 1) * T) / fabsf(dot(si.ns, dir));
         b.pdf = T / (R + T);
     }
-    b.f = f * tex_eval(m.tex, si.u, si.v);
+    b.f = f * m.col;
     b.d = dir;
     b.flags = FL_TRANS | FL_SPEC;
     b.ok = true;
     return b;
 }
 // SpecularConductor::scatter (Material.hpp:664-669)
-__device__ Bxdf conductor_scatter(const pt_material& m, f3 ind, const SurfInt& si) {
+__device__ Bxdf conductor_scatter(const MatTex& m, f3 ind, const SurfInt& si) {
     Bxdf b;
     b.ok = false;
     f3 d = reflect(ind, si.ns);
     float dt = dot(d, si.ns);
     if (dt <= 0) return b;
-    b.f = schlick(dot(si.ns, -ind), ld3(m.albedo)) / dt;
+    b.f = schlick(dot(si.ns, -ind), m.col) / dt;
     b.pdf = 1;
     b.flags = FL_SPEC;
     b.o = si.p;
@@ -731,9 +764,8 @@ __device__ Bxdf conductor_scatter(const pt_material& m, f3 ind, const SurfInt& s
 // The material and light entry points are inlined into k_shade: taken out of
 // line, their `const SurfInt&` argument kept the interaction in scratch memory
 // on every path (k_shade<PATH>: 160 -> 16 B of scratch per lane).
-__device__ __forceinline__ Bxdf mat_scatter(int mid, f3 ino, f3 ind, const SurfInt& si, float u, float uv0,
+__device__ __forceinline__ Bxdf mat_scatter(const MatTex& m, f3 ino, f3 ind, const SurfInt& si, float u, float uv0,
                             float uv1) {
-    const pt_material m = mat_rec(mid);
     switch (m.kind) {
         case PT_MAT_DIFFUSE: return diffuse_scatter(m, ind, si, u, uv0, uv1);
         case PT_MAT_DIELECTRIC: return dielectric_scatter(m, ino, ind, si, u, uv0, uv1);
@@ -741,8 +773,7 @@ __device__ __forceinline__ Bxdf mat_scatter(int mid, f3 ino, f3 ind, const SurfI
         default: return conductor_scatter(m, ind, si);
     }
 }
-__device__ __forceinline__ f3 mat_f(int mid, f3 ind, const SurfInt& si, f3 dir) {
-    const pt_material m = mat_rec(mid);
+__device__ __forceinline__ f3 mat_f(const MatTex& m, f3 ind, const SurfInt& si, f3 dir) {
     f3 f;
     float p;
     switch (m.kind) {
@@ -752,8 +783,7 @@ __device__ __forceinline__ f3 mat_f(int mid, f3 ind, const SurfInt& si, f3 dir) 
         default: return F3(1, 1, 1);  // base Material::calc_attenuation
     }
 }
-__device__ __forceinline__ float mat_pdf(int mid, f3 ind, const SurfInt& si, f3 dir) {
-    const pt_material m = mat_rec(mid);
+__device__ __forceinline__ float mat_pdf(const MatTex& m, f3 ind, const SurfInt& si, f3 dir) {
     f3 f;
     float p;
     switch (m.kind) {
