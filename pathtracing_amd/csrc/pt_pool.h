@@ -111,7 +111,7 @@ __device__ unsigned int pt_diag[4];
 #endif
 // ... or through a buffer resource, lanes without the step out of its range
 #ifndef PT_BUFFER_LOADS
-#define PT_BUFFER_LOADS 0
+#define PT_BUFFER_LOADS 1
 #endif
 #define Q48_OOB_OFFSET 0xFFFFFF00u  // + 32 stays below 2^32: never wraps into range
 __device__ __forceinline__ float4 q48_buf_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {

@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -106,6 +107,16 @@ struct pt_ctx {
         uint32_t width = 0, npix = 0, tiled = 0, tiles_x = 0;
         uint32_t s_lo = 0, s_hi = 0, shard_index = 0, shard_count = 1;
     } frame;
+};
+
+// The uploaded scene lives in the device's __constant__ DevScene S (one per
+// device, not per context): calls that bind a context's scene and launch are
+// serialized per device, so two contexts on one GPU used from two host
+// threads cannot run kernels against each other's scene record.
+static std::mutex g_device_mu[64];
+struct DeviceLock {
+    std::unique_lock<std::mutex> lk;
+    explicit DeviceLock(int device) : lk(g_device_mu[(unsigned)device & 63u]) {}
 };
 
 static pt_status fail(pt_ctx* c, pt_status code, const char* fmt, ...) {
@@ -852,6 +863,7 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
 }
 static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     if (!c || !s) return PT_ERR_ARG;
+    DeviceLock dl(c->device);
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     free_scene(c);
@@ -1742,6 +1754,7 @@ extern "C" pt_status pt_render(pt_ctx* c, const pt_camera_desc* cam, const pt_re
 // One device's fixed-SPP frame (shard rd->shard_index of rd->shard_count).
 static pt_status render_dev(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, double* film_accum,
                             pt_stats* stats) {
+    DeviceLock dl(c->device);
     pt_status st;
     if (!film_accum) return fail(c, PT_ERR_ARG, "film_accum is null");
     if (!(rd->pixel_begin == 0 && rd->pixel_end == 0)) return fail(c, PT_ERR_ARG, "pt_render renders whole films");
@@ -1929,6 +1942,7 @@ static pt_status render_multi(pt_ctx* c, const pt_camera_desc* cam, const pt_ren
 // One device's adaptive frame (pt_render_adaptive on a one-device context).
 static pt_status render_adaptive_dev(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd,
                                      double* film_accum, uint32_t* sample_counts, pt_stats* stats) {
+    DeviceLock dl(c->device);
     pt_status st;
     HIPCHK(c, hipSetDevice(c->device));
     const uint32_t npx = (uint32_t)cam->width * cam->height;
@@ -1997,6 +2011,8 @@ static pt_status render_adaptive_dev(pt_ctx* c, const pt_camera_desc* cam, const
 
 extern "C" pt_status pt_render_samples(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc* rd, float* out_L,
                                        pt_stats* stats) {
+    if (!c) return PT_ERR_ARG;
+    DeviceLock dl(c->device);
     pt_status st = check_render_args(c, cam, rd);
     if (st) return st;
     if (!out_L) return fail(c, PT_ERR_ARG, "out_L is null");
@@ -2076,6 +2092,8 @@ extern "C" pt_status pt_film_resolve(pt_ctx* c, const double* film, int32_t widt
 }
 
 extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any_hit, pt_hit* hits, pt_stats* stats) {
+    if (!c) return PT_ERR_ARG;
+    DeviceLock dl(c->device);
     if (!c || (n && (!rays || !hits))) return PT_ERR_ARG;
     if (!c->has_scene) return fail(c, PT_ERR_STATE, "no scene uploaded");
     HIPCHK(c, hipSetDevice(c->device));
@@ -2176,6 +2194,8 @@ static pt_status run_hook(pt_ctx* c, const void* in, size_t in_bytes, float* out
 }
 
 extern "C" pt_status pt_interact(pt_ctx* c, const pt_ray* rays, uint32_t n, float* out) {
+    if (!c) return PT_ERR_ARG;
+    DeviceLock dl(c->device);
     if (!c || (n && (!rays || !out))) return PT_ERR_ARG;
     if (!c->has_scene) return fail(c, PT_ERR_STATE, "no scene uploaded");
     HIPCHK(c, hipSetDevice(c->device));
@@ -2190,6 +2210,8 @@ extern "C" pt_status pt_interact(pt_ctx* c, const pt_ray* rays, uint32_t n, floa
 }
 
 extern "C" pt_status pt_bsdf_cases(pt_ctx* c, int32_t material, const float* cases, uint32_t n, float* out) {
+    if (!c) return PT_ERR_ARG;
+    DeviceLock dl(c->device);
     if (!c || (n && (!cases || !out))) return PT_ERR_ARG;
     if (!c->has_scene) return fail(c, PT_ERR_STATE, "no scene uploaded");
     if (material < 0 || (uint32_t)material >= c->n_materials) return fail(c, PT_ERR_ARG, "bad material id");
@@ -2203,6 +2225,8 @@ extern "C" pt_status pt_bsdf_cases(pt_ctx* c, int32_t material, const float* cas
 }
 
 extern "C" pt_status pt_light_cases(pt_ctx* c, const float* cases, uint32_t n, float* out) {
+    if (!c) return PT_ERR_ARG;
+    DeviceLock dl(c->device);
     if (!c || (n && (!cases || !out))) return PT_ERR_ARG;
     if (!c->has_scene) return fail(c, PT_ERR_STATE, "no scene uploaded");
     HIPCHK(c, hipSetDevice(c->device));
@@ -2217,6 +2241,8 @@ extern "C" pt_status pt_light_cases(pt_ctx* c, const float* cases, uint32_t n, f
 }
 
 extern "C" pt_status pt_light_picks(pt_ctx* c, const float* u, uint32_t n, int32_t* out) {
+    if (!c) return PT_ERR_ARG;
+    DeviceLock dl(c->device);
     if (!c || (n && (!u || !out))) return PT_ERR_ARG;
     if (!c->has_scene) return fail(c, PT_ERR_STATE, "no scene uploaded");
     HIPCHK(c, hipSetDevice(c->device));
