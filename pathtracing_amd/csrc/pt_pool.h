@@ -113,6 +113,19 @@ __device__ unsigned int pt_diag[4];
 #ifndef PT_BUFFER_LOADS
 #define PT_BUFFER_LOADS 1
 #endif
+// overlapped traversal: the primitive side's triangle test before the node
+// side (only its result live across the node side), its hit handling after
+// overlapped traversal: a leaf step tests the leaf's next primitive too when
+// both are triangles (three more 16-B loads on primitive lanes)
+#ifndef PT_SPEC_LEAF2
+#define PT_SPEC_LEAF2 0
+#endif
+#if PT_SPEC_LEAF2 && !(PT_Q48 && PT_BUFFER_LOADS)
+#error "PT_SPEC_LEAF2 needs the buffer-load PT_Q48 form"
+#endif
+#ifndef PT_TRI_FIRST
+#define PT_TRI_FIRST 0
+#endif
 #define Q48_OOB_OFFSET 0xFFFFFF00u  // + 32 stays below 2^32: never wraps into range
 __device__ __forceinline__ float4 q48_buf_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
@@ -289,6 +302,11 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         const uint32_t poff = prim_step ? slot * 48u : Q48_OOB_OFFSET;
         const float4 q0 = q48_buf_load(qrs, noff), q1 = q48_buf_load(qrs, noff + 16u), q2 = q48_buf_load(qrs, noff + 32u);
         const float4 g0 = q48_buf_load(qrs, poff), g1 = q48_buf_load(qrs, poff + 16u), g2 = q48_buf_load(qrs, poff + 32u);
+#if PT_SPEC_LEAF2
+        const uint32_t poff2 = prim_step ? poff + 48u : Q48_OOB_OFFSET;
+        const float4 h0 = q48_buf_load(qrs, poff2), h1 = q48_buf_load(qrs, poff2 + 16u),
+                     h2 = q48_buf_load(qrs, poff2 + 32u);
+#endif
 #elif PT_Q48 && PT_MASKED_LOADS
         // each side's loads under its own exec mask: a lane without a node
         // (primitive) step issues no node (slot) loads, so the vector memory
@@ -319,6 +337,18 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         const float4 g0 = qg[0], g1 = qg[1], g2 = qg[2];
 #endif
         __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink the slot loads past the node side)
+#if PT_TRI_FIRST
+        // the triangle test first: its 12 slot words die before the node side,
+        // and only its result (t, barycentrics, flags) stays live across it
+        const uint32_t w0 = __float_as_uint(g0.w);
+        const bool pred = ANY && !(w0 & GF_PRED_GLM);
+        float bx = 0, by = 0, t = 0;
+        bool tri_hit;
+        if (pred) tri_hit = tri_pred(o, d, xyz(g0), xyz(g1), xyz(g2), tmax);
+        else tri_hit = tri_glm(o, d, xyz(g0), xyz(g1), xyz(g2), bx, by, t) && !(t > tmax || t < PT_EPS);
+        const uint32_t blas_root = __float_as_uint(g1.x), g2w = __float_as_uint(g2.w);
+        __builtin_amdgcn_sched_barrier(0);
+#endif
 
         // ---- node side
         {
@@ -354,18 +384,30 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         // result kept only on primitive lanes), so the slot loads are used
         // outside the branches.
         {
+#if !PT_TRI_FIRST
             const uint32_t w0 = __float_as_uint(g0.w);
-            const uint32_t kind = w0 & GF_KIND;
             const bool pred = ANY && !(w0 & GF_PRED_GLM);
             float bx = 0, by = 0, t = 0;
             bool tri_hit;
             if (pred) tri_hit = tri_pred(o, d, xyz(g0), xyz(g1), xyz(g2), tmax);
             else tri_hit = tri_glm(o, d, xyz(g0), xyz(g1), xyz(g2), bx, by, t) && !(t > tmax || t < PT_EPS);
+            const uint32_t blas_root = __float_as_uint(g1.x), g2w = __float_as_uint(g2.w);
+#endif
+            const uint32_t kind = w0 & GF_KIND;
+#if PT_SPEC_LEAF2
+            const uint32_t w1 = __float_as_uint(h0.w);
+            const bool pred2 = ANY && !(w1 & GF_PRED_GLM);
+            float bx2 = 0, by2 = 0, t2r = 0;
+            bool tri_hit2;
+            if (pred2) tri_hit2 = tri_pred(o, d, xyz(h0), xyz(h1), xyz(h2), tmax);
+            else tri_hit2 = tri_glm(o, d, xyz(h0), xyz(h1), xyz(h2), bx2, by2, t2r);
+            const uint32_t ps2 = __float_as_uint(h2.w);
+#endif
             if (prim_step) {
                 bool anyhit = false;
                 uint32_t next = (w0 & GF_LAST) ? REF_EMPTY : (REF_LEAF | (leaf & REF_BLOCK) | (slot + 1));
                 // the primitive's slot (PT_Q48: the record keeps it in c.w)
-                const uint32_t ps = PT_Q48 ? __float_as_uint(g2.w) : slot;
+                const uint32_t ps = PT_Q48 ? g2w : slot;
                 if (kind == PT_PRIM_TRIANGLE) {
                     if (COUNT) wk.tris++;
                     if (tri_hit && (pred || !(w0 & GF_ALPHA) || tri_alpha(ps, bx, by, o, d))) {
@@ -381,13 +423,35 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                             src.closest((uint32_t)ri, t, bx, by, (int)ps);
                         }
                     }
+#if PT_SPEC_LEAF2
+                    // the leaf's next primitive in the same step when it is a
+                    // triangle too (tested after the first, against its max)
+                    if (!(w0 & GF_LAST) && !(ANY && anyhit) && (w1 & GF_KIND) == PT_PRIM_TRIANGLE) {
+                        if (COUNT) wk.tris++;
+                        if (!pred2) tri_hit2 = tri_hit2 && !(t2r > tmax || t2r < PT_EPS);
+                        if (tri_hit2 && (pred2 || !(w1 & GF_ALPHA) || tri_alpha(ps2, bx2, by2, o, d))) {
+                            if (ANY) {
+                                anyhit = true;
+                            } else {
+                                if ((oct & (OCT_FOUND | OCT_TIE)) == OCT_FOUND && t2r == tmax) {
+                                    oct |= OCT_TIE;
+                                    src.tie((uint32_t)ri);
+                                }
+                                tmax = t2r;
+                                oct |= OCT_FOUND;
+                                src.closest((uint32_t)ri, t2r, bx2, by2, (int)ps2);
+                            }
+                        }
+                        next = (w1 & GF_LAST) ? REF_EMPTY : (REF_LEAF | (leaf & REF_BLOCK) | (slot + 2));
+                    }
+#endif
                 } else if (kind == PT_PRIM_BLAS) {
                     // the reference recurses into the BLAS inside the leaf loop
                     // (Model::Intersect, BVH.hpp:1206): the rest of the leaf
                     // waits on the stack under the BLAS root, which the
                     // (paused) node side visits next
                     if (next != REF_EMPTY) push(next);
-                    push(__float_as_uint(g1.x));
+                    push(blas_root);
                     next = REF_EMPTY;
                 } else {
                     if (COUNT) wk.tris++;
