@@ -106,6 +106,44 @@ struct alignas(16) DevGeom {
     float4 a, b, c;
 };
 
+// ---- alpha records: what tri_alpha reads for an alpha-tested triangle, in
+// one 48-B record (its slot's b.w holds the record index; ALPHA_NONE: the
+// general path).  tri_alpha otherwise walks prim info -> shading record ->
+// material -> texture -> image -> texels, six dependent reads inside the
+// traversal loop; here it is the record, then the texels.
+//   su / sv   the triangle's uv components in lerp3f order (uv1, uv2, uv0)
+//   off       the image's byte offset in the texel buffer (ALPHA_SRC_CONST:
+//             word 0 = the constant alpha)
+//   wh        width | height << 16;  mode = alpha mode | source << 2 |
+//             channels << 8;  cut = MASK cutoff;  scale = the alpha
+//             texture's colorScale.x (ALPHA_SRC_CH1)
+#define ALPHA_NONE 0xFFFFFFFFu
+#define ALPHA_SRC_CH4 0u    // Texture::alpha of the material's texture: channel 4 (Texture.cpp:47-62)
+#define ALPHA_SRC_CH1 1u    // the material's alpha texture: Evaluate(uv).x (Material.hpp:181-198)
+#define ALPHA_SRC_CONST 2u  // a constant alpha (solid texture, or an image without a 4th channel)
+struct alignas(16) DevAlpha {
+    float su[3], sv[3];
+    uint32_t off_lo, off_hi;
+    uint32_t wh, mode;
+    float cut, scale;
+};
+static_assert(sizeof(DevAlpha) == 48, "alpha record layout");
+// ---- texture records for the shading path: a texture with its image's
+// fields in one 32-B record (Texture::Evaluate reads the texture, then its
+// image, then texels: one dependent read fewer)
+//   kfc = kind | image format << 8 | image channels << 16;  scale = colorScale
+//   u   SOLID: value[3];  CHECKER: a, b, inv_scale[2] (as bits);
+//       IMAGE: offset lo, hi, width, height
+struct alignas(16) DevTex {
+    uint32_t kfc;
+    float scale[3];
+    uint32_t u[4];
+};
+static_assert(sizeof(DevTex) == 32, "texture record layout");
+#ifndef PT_ALPHA_RECORDS
+#define PT_ALPHA_RECORDS 1
+#endif
+
 // Instances (TransformedPrimitive, Primitive.cpp:32-72).  A TLAS leaf slot of
 // an instance is encoded like a BLAS hop whose pushed ref is
 // REF_INST_ENTER | slot; popping it takes the lane's ray to object space
@@ -176,11 +214,13 @@ struct DevScene {
     const float* uvs;          // 2 per vertex
     const float* tangents;
     const DevTriShade* tshade;  // per-triangle shading records (vertex order x, y, z of tri)
+    const DevAlpha* alpha;      // alpha records of the alpha-tested triangles (slot b.w)
     const pt_quad* quads;
     const pt_sphere* spheres;
     const pt_material* materials;
     const pt_texture* textures;
     const pt_image* images;
+    const DevTex* texrec;      // DevTex per texture (the shading path's reads)
     const uint8_t* texels;
     uint64_t n_texel_bytes;
     const pt_light* lights;

@@ -346,7 +346,9 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         bool tri_hit;
         if (pred) tri_hit = tri_pred(o, d, xyz(g0), xyz(g1), xyz(g2), tmax);
         else tri_hit = tri_glm(o, d, xyz(g0), xyz(g1), xyz(g2), bx, by, t) && !(t > tmax || t < PT_EPS);
-        const uint32_t blas_root = __float_as_uint(g1.x), g2w = __float_as_uint(g2.w);
+        // BLAS hop: its root ref (b.x); triangle: its alpha record (b.w)
+        const uint32_t g1v = (w0 & GF_KIND) == PT_PRIM_BLAS ? __float_as_uint(g1.x) : __float_as_uint(g1.w);
+        const uint32_t g2w = __float_as_uint(g2.w);
         __builtin_amdgcn_sched_barrier(0);
 #endif
 
@@ -391,7 +393,8 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             bool tri_hit;
             if (pred) tri_hit = tri_pred(o, d, xyz(g0), xyz(g1), xyz(g2), tmax);
             else tri_hit = tri_glm(o, d, xyz(g0), xyz(g1), xyz(g2), bx, by, t) && !(t > tmax || t < PT_EPS);
-            const uint32_t blas_root = __float_as_uint(g1.x), g2w = __float_as_uint(g2.w);
+            const uint32_t g1v = (w0 & GF_KIND) == PT_PRIM_BLAS ? __float_as_uint(g1.x) : __float_as_uint(g1.w);
+            const uint32_t g2w = __float_as_uint(g2.w);
 #endif
             const uint32_t kind = w0 & GF_KIND;
 #if PT_SPEC_LEAF2
@@ -410,7 +413,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 const uint32_t ps = PT_Q48 ? g2w : slot;
                 if (kind == PT_PRIM_TRIANGLE) {
                     if (COUNT) wk.tris++;
-                    if (tri_hit && (pred || !(w0 & GF_ALPHA) || tri_alpha(ps, bx, by, o, d))) {
+                    if (tri_hit && (pred || !(w0 & GF_ALPHA) || tri_alpha(g1v, ps, bx, by, o, d))) {
                         if (ANY) {
                             anyhit = true;
                         } else {
@@ -429,7 +432,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                     if (!(w0 & GF_LAST) && !(ANY && anyhit) && (w1 & GF_KIND) == PT_PRIM_TRIANGLE) {
                         if (COUNT) wk.tris++;
                         if (!pred2) tri_hit2 = tri_hit2 && !(t2r > tmax || t2r < PT_EPS);
-                        if (tri_hit2 && (pred2 || !(w1 & GF_ALPHA) || tri_alpha(ps2, bx2, by2, o, d))) {
+                        if (tri_hit2 && (pred2 || !(w1 & GF_ALPHA) || tri_alpha(__float_as_uint(h1.w), ps2, bx2, by2, o, d))) {
                             if (ANY) {
                                 anyhit = true;
                             } else {
@@ -451,7 +454,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                     // waits on the stack under the BLAS root, which the
                     // (paused) node side visits next
                     if (next != REF_EMPTY) push(next);
-                    push(blas_root);
+                    push(g1v);  // the BLAS root
                     next = REF_EMPTY;
                 } else {
                     if (COUNT) wk.tris++;
@@ -813,7 +816,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 } else {
                     float bx, by, t;
                     if (tri_glm(o, d, xyz(a), xyz(b), xyz(c), bx, by, t) && !(t > tmax || t < PT_EPS)) {
-                        if (!(w & GF_ALPHA) || tri_alpha(sl, bx, by, o, d)) {
+                        if (!(w & GF_ALPHA) || tri_alpha(__float_as_uint(b.w), sl, bx, by, o, d)) {
                             if (ANY) {
                                 anyhit = true;
                             } else {

@@ -674,6 +674,49 @@ static void material_alpha_flags(const pt_scene_desc* s, int mid, uint32_t& flag
     if (!always_true) flags |= GF_ALPHA;
 }
 
+// DevAlpha record of an alpha-tested triangle (pt_device.h): mat_alpha's
+// source resolved here (Material.hpp:181-198, Texture.cpp:47-62); false where
+// only the general path handles it (checker sources, float images, images
+// wider or taller than 65535)
+static bool alpha_record(const pt_scene_desc* s, const pt_prim& p, DevAlpha& r) {
+    if (!s->uvs || p.material < 0) return false;
+    const pt_material& m = s->materials[p.material];
+    const uint32_t* v = s->tri_vidx + 3 * (size_t)p.index;
+    const float* u0 = s->uvs + 2 * (size_t)v[0];
+    const float* u1 = s->uvs + 2 * (size_t)v[1];
+    const float* u2 = s->uvs + 2 * (size_t)v[2];
+    r = DevAlpha{{u1[0], u2[0], u0[0]}, {u1[1], u2[1], u0[1]}, 0, 0, 0, 0, m.alpha_cutoff, 1.0f};
+    uint32_t src;
+    const pt_image* im = nullptr;
+    const pt_texture& t = s->textures[m.alpha >= 0 ? m.alpha : m.tex];
+    if (t.kind == PT_TEX_SOLID) {
+        src = ALPHA_SRC_CONST;  // Evaluate(uv).x of a solid alpha texture; Texture::alpha of a solid is 1
+        r.off_lo = __builtin_bit_cast(uint32_t, m.alpha >= 0 ? t.value[0] : 1.0f);
+    } else if (t.kind == PT_TEX_IMAGE) {
+        im = &s->images[t.image];
+        if (m.alpha < 0 && im->channels != 4) {  // ImageTexture::alpha without an alpha channel: 1
+            src = ALPHA_SRC_CONST;
+            r.off_lo = __builtin_bit_cast(uint32_t, 1.0f);
+            im = nullptr;
+        } else {
+            if (im->format != PT_IMAGE_U8 || im->width <= 0 || im->height <= 0 || im->width > 0xFFFF ||
+                im->height > 0xFFFF || im->channels <= 0 || im->channels > 0xFF)
+                return false;
+            src = m.alpha >= 0 ? ALPHA_SRC_CH1 : ALPHA_SRC_CH4;
+            r.scale = t.scale[0];
+        }
+    } else {
+        return false;
+    }
+    if (im) {
+        r.off_lo = (uint32_t)im->offset;
+        r.off_hi = (uint32_t)(im->offset >> 32);
+        r.wh = (uint32_t)im->width | (uint32_t)im->height << 16;
+    }
+    r.mode = (m.alpha_mode & 3u) | src << 2 | (im ? (uint32_t)im->channels : 0u) << 8;
+    return true;
+}
+
 struct Conv {
     const pt_scene_desc* s;
     std::vector<DevCluster>& nodes;
@@ -900,6 +943,14 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
                                         (L.instance >= 0 && (uint32_t)L.instance >= s->n_instances)))
             return fail(c, PT_ERR_ARG, "light %u: bad area light", l);
     }
+    for (uint32_t k = 0; k < s->n_textures; k++) {
+        const pt_texture& T = s->textures[k];
+        if (T.kind == PT_TEX_IMAGE && (T.image < 0 || (uint32_t)T.image >= s->n_images))
+            return fail(c, PT_ERR_ARG, "texture %u: bad image", k);
+        if (T.kind == PT_TEX_CHECKER && (T.a < 0 || T.b < 0 || (uint32_t)T.a >= s->n_textures ||
+                                         (uint32_t)T.b >= s->n_textures))
+            return fail(c, PT_ERR_ARG, "texture %u: bad checker child", k);
+    }
     for (uint32_t m = 0; m < s->n_materials; m++) {
         const pt_material& M = s->materials[m];
         int ids[5] = {M.tex, M.norm, M.rough, M.metal, M.alpha};
@@ -967,6 +1018,16 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
         g.a.w = __builtin_bit_cast(float, flags);
         geom[i] = g;
         info[i] = DevPrimInfo{p.material, p.light, p.medium, p.index};
+    }
+    // ---- alpha records of the alpha-tested triangles (the slot's b.w names one)
+    std::vector<DevAlpha> alpha;
+    for (uint32_t i = 0; i < s->n_prims; i++) {
+        const uint32_t fl = __builtin_bit_cast(uint32_t, geom[i].a.w);
+        if ((fl & GF_KIND) != PT_PRIM_TRIANGLE || !(fl & GF_ALPHA)) continue;
+        DevAlpha r;
+        const bool fast = PT_ALPHA_RECORDS && alpha_record(s, s->prims[i], r);
+        geom[i].b.w = __builtin_bit_cast(float, fast ? (uint32_t)alpha.size() : ALPHA_NONE);
+        if (fast) alpha.push_back(r);
     }
     // ---- nodes: TLAS then every BLAS, converted from the root descriptors
     std::vector<uint32_t> cbase(s->n_bvhs);
@@ -1097,6 +1158,7 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     UP(DS.uvs, s->uvs, 2 * (size_t)s->n_vertices);
     UP(DS.tangents, s->tangents, s->tangents ? 3 * (size_t)s->n_vertices : 0);
     UP(DS.tshade, (const DevTriShade*)nullptr, s->n_triangles);
+    UP(DS.alpha, alpha.data(), alpha.size());
     if (s->n_triangles) {
         hipLaunchKernelGGL(k_tri_shade, dim3((s->n_triangles + 255) / 256), dim3(256), 0, c->stream, DS.tri,
                            DS.normals, DS.uvs, s->tangents ? DS.tangents : nullptr, s->n_triangles,
@@ -1109,6 +1171,33 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     UP(DS.materials, s->materials, s->n_materials);
     UP(DS.textures, s->textures, s->n_textures);
     UP(DS.images, s->images, s->n_images);
+    {
+        std::vector<DevTex> tr(s->n_textures);
+        for (uint32_t k = 0; k < s->n_textures; k++) {
+            const pt_texture& t = s->textures[k];
+            DevTex& r = tr[k];
+            r = DevTex{};
+            r.kfc = t.kind;
+            std::memcpy(r.scale, t.scale, sizeof(r.scale));
+            if (t.kind == PT_TEX_SOLID) {
+                std::memcpy(r.u, t.value, sizeof(t.value));
+            } else if (t.kind == PT_TEX_CHECKER) {
+                r.u[0] = (uint32_t)t.a;
+                r.u[1] = (uint32_t)t.b;
+                std::memcpy(&r.u[2], t.inv_scale, sizeof(t.inv_scale));
+            } else {
+                const pt_image& im = s->images[t.image];  // (validated above)
+                if (im.channels < 0 || im.channels > 0xFFFF || im.format < 0 || im.format > 0xFF)
+                    return fail(c, PT_ERR_ARG, "image %d: bad channels / format", t.image);
+                r.kfc |= (uint32_t)im.format << 8 | (uint32_t)im.channels << 16;
+                r.u[0] = (uint32_t)im.offset;
+                r.u[1] = (uint32_t)(im.offset >> 32);
+                r.u[2] = (uint32_t)im.width;
+                r.u[3] = (uint32_t)im.height;
+            }
+        }
+        UP(DS.texrec, tr.data(), tr.size());
+    }
     // texels: 16 bytes of padding for the word loads of texel_pair_u8
     if ((st = upload(c, s->texels, s->n_texel_bytes, &DS.texels, 16)) != PT_OK) return st;
     UP(DS.lights, s->lights, s->n_lights);

@@ -178,7 +178,80 @@ __device__ f3 tex_eval_t(int id, float u, float v) {
     return F3(0, 0, 0);
 }
 
-__device__ __forceinline__ f3 tex_eval(int id, float u, float v) { return tex_eval_t<true>(id, u, v); }
+// PT_TEXREC (A/B option, default on): the shading path reads DevTex records
+#ifndef PT_TEXREC
+#define PT_TEXREC 1
+#endif
+// The same over DevTex records (shading path without LDS tables): the
+// texture's record is its image's too, and a caller may load the records of
+// a material's textures together before evaluating any of them.
+__device__ __forceinline__ DevTex tex_full(int id) {
+    const float4* p = reinterpret_cast<const float4*>(S.texrec + id);
+    const float4 a = p[0], b = p[1];
+    DevTex t;
+    t.kfc = __float_as_uint(a.x);
+    t.scale[0] = a.y;
+    t.scale[1] = a.z;
+    t.scale[2] = a.w;
+    t.u[0] = __float_as_uint(b.x);
+    t.u[1] = __float_as_uint(b.y);
+    t.u[2] = __float_as_uint(b.z);
+    t.u[3] = __float_as_uint(b.w);
+    return t;
+}
+__device__ __forceinline__ f3 tex_eval_r(DevTex t, float u, float v) {
+    f3 scale = F3(1, 1, 1);
+    bool scaled = false;
+    for (int guard = 0; guard < 16; guard++) {
+        const uint32_t kind = t.kfc & 0xFFu;
+        if (kind == PT_TEX_SOLID) {
+            f3 c = F3(__uint_as_float(t.u[0]), __uint_as_float(t.u[1]), __uint_as_float(t.u[2]));
+            return scaled ? scale * c : c;
+        }
+        if (kind == PT_TEX_CHECKER) {
+            int ux = (int)floorf(u * __uint_as_float(t.u[2]));
+            int uy = (int)floorf(v * __uint_as_float(t.u[3]));
+            scale = scaled ? scale * ld3(t.scale) : ld3(t.scale);
+            scaled = true;
+            t = tex_full(((ux + uy) % 2 == 0) ? (int)t.u[0] : (int)t.u[1]);
+            continue;
+        }
+        pt_image im;
+        im.offset = (uint64_t)t.u[0] | (uint64_t)t.u[1] << 32;
+        im.width = (int32_t)t.u[2];
+        im.height = (int32_t)t.u[3];
+        im.channels = (int32_t)(t.kfc >> 16);
+        im.format = (int32_t)((t.kfc >> 8) & 0xFFu);
+        float x = u * im.width - 0.5f;
+        float y = v * im.height - 0.5f;
+        int xi = (int)floorf(x), yi = (int)floorf(y);
+        float dx = x - xi, dy = y - yi;
+        f3 a, b, c, d;
+        if (!texel_pair_u8(im, xi, yi, a, b)) {
+            a = texel3(im, xi, yi);
+            b = texel3(im, xi + 1, yi);
+        }
+        if (!texel_pair_u8(im, xi, yi + 1, c, d)) {
+            c = texel3(im, xi, yi + 1);
+            d = texel3(im, xi + 1, yi + 1);
+        }
+        float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
+        f3 r = F3(fma_(wd, d.x, fma_(wc, c.x, fma_(wb, b.x, rmul(wa, a.x)))),
+                  fma_(wd, d.y, fma_(wc, c.y, fma_(wb, b.y, rmul(wa, a.y)))),
+                  fma_(wd, d.z, fma_(wc, c.z, fma_(wb, b.z, rmul(wa, a.z)))));
+        r = ld3(t.scale) * r;
+        return scaled ? scale * r : r;
+    }
+    return F3(0, 0, 0);
+}
+
+__device__ __forceinline__ f3 tex_eval(int id, float u, float v) {
+#if PT_LDS_TABLES || !PT_TEXREC
+    return tex_eval_t<true>(id, u, v);
+#else
+    return tex_eval_r(tex_full(id), u, v);
+#endif
+}
 
 // Texture::alpha (Texture.hpp:112-114, Texture.cpp:47-62, 41-45)
 __device__ float tex_alpha(int id, float u, float v) {
@@ -476,15 +549,31 @@ __device__ __forceinline__ MatTex mat_tex(int mid, const SurfInt& si) {
     t.rough = 0.0f;
     t.metal = 0.0f;
     switch (m.kind) {
-        case PT_MAT_DIFFUSE:
+        case PT_MAT_DIFFUSE: {
+#if PT_LDS_TABLES || !PT_TEXREC
             t.rough = smax(tex_eval(m.rough, si.u, si.v).y, 0.0001f);
             t.metal = tex_eval(m.metal, si.u, si.v).z;
             t.col = tex_eval(m.tex, si.u, si.v);
+#else
+            // the three records read together, then evaluated
+            const DevTex tr = tex_full(m.rough), tm = tex_full(m.metal), tc = tex_full(m.tex);
+            t.rough = smax(tex_eval_r(tr, si.u, si.v).y, 0.0001f);
+            t.metal = tex_eval_r(tm, si.u, si.v).z;
+            t.col = tex_eval_r(tc, si.u, si.v);
+#endif
             break;
-        case PT_MAT_DIELECTRIC:
+        }
+        case PT_MAT_DIELECTRIC: {
+#if PT_LDS_TABLES || !PT_TEXREC
             t.rough = tex_eval(m.rough, si.u, si.v).y;
             t.col = tex_eval(m.tex, si.u, si.v);
+#else
+            const DevTex tr = tex_full(m.rough), tc = tex_full(m.tex);
+            t.rough = tex_eval_r(tr, si.u, si.v).y;
+            t.col = tex_eval_r(tc, si.u, si.v);
+#endif
             break;
+        }
         case PT_MAT_THIN: t.col = tex_eval(m.tex, si.u, si.v); break;
         default: t.col = ld3(m.albedo);
     }

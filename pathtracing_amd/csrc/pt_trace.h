@@ -110,8 +110,50 @@ __device__ __forceinline__ f3 inv_dir(f3 d) {  // Ray ctor (Ray.hpp:32-35)
               fabsf(d.z) < 1e-32f ? 1e32f : 1.0f / d.z);
 }
 
-// Candidate uv for the alpha test on an alpha-tested triangle (rare path).
-__device__ __noinline__ bool tri_alpha(uint32_t slot, float bu, float bv, f3 o, f3 d) {
+// A u8 texel channel as channel_at reads it (wrapped coordinates, 0 past
+// the texel buffer)
+__device__ __forceinline__ float alpha_texel(uint64_t off, int w, int h, int C, int x, int y, int ch0) {
+    const int xi = wrap_index(x, w), yi = wrap_index(y, h);
+    const uint64_t idx = off + ((uint64_t)yi * (uint64_t)w + (uint64_t)xi) * (uint64_t)C + (uint64_t)ch0;
+    if (idx >= S.n_texel_bytes) return 0.0f;
+    return S.texels[idx] / 255.0f;
+}
+// The material alpha test of an alpha-tested triangle at its candidate hit
+// (GeometricPrimitive::Intersect -> Material::Alpha, Primitive.cpp:6-26,
+// Material.hpp:181-198).  ai: the slot's alpha record (DevAlpha, slot b.w):
+// the record, then the four texels; ALPHA_NONE: prim info -> shading record
+// -> material -> texture -> image.  Same values either way.
+__device__ __noinline__ bool tri_alpha(uint32_t ai, uint32_t slot, float bu, float bv, f3 o, f3 d) {
+    if (ai != ALPHA_NONE) {
+        const DevAlpha r = S.alpha[ai];
+        const float u = bu, v = bv, w = 1.0f - u - v;
+        const float tu = lerp3f(u, r.su[0], v, r.su[1], w, r.su[2]);
+        const float tv = lerp3f(u, r.sv[0], v, r.sv[1], w, r.sv[2]);
+        const uint32_t src = (r.mode >> 2) & 3u;
+        float a;
+        if (src == ALPHA_SRC_CONST) {
+            a = __uint_as_float(r.off_lo);
+        } else {
+            const int W = (int)(r.wh & 0xFFFFu), H = (int)(r.wh >> 16), C = (int)((r.mode >> 8) & 0xFFu);
+            const uint64_t off = (uint64_t)r.off_lo | (uint64_t)r.off_hi << 32;
+            const float x = tu * W - 0.5f, y = tv * H - 0.5f;
+            const int xi = (int)floorf(x), yi = (int)floorf(y);
+            const float dx = x - xi, dy = y - yi;
+            const int ch0 = src == ALPHA_SRC_CH4 ? 3 : 0;
+            const float ta = alpha_texel(off, W, H, C, xi, yi, ch0), tb = alpha_texel(off, W, H, C, xi + 1, yi, ch0);
+            const float tc = alpha_texel(off, W, H, C, xi, yi + 1, ch0),
+                        td = alpha_texel(off, W, H, C, xi + 1, yi + 1, ch0);
+            const float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
+            // the two contractions as built: ImageTexture::alpha (tex_alpha) and
+            // Evaluate(uv).x * colorScale.x (tex_eval_t)
+            a = src == ALPHA_SRC_CH4 ? fma_(wd, td, fma_(wc, tc, fma_(wa, ta, rmul(wb, tb))))
+                                     : r.scale * fma_(wd, td, fma_(wc, tc, fma_(wb, tb, rmul(wa, ta))));
+        }
+        const uint32_t mode = r.mode & 3u;
+        if (mode == PT_ALPHA_OPAQUE) return true;
+        if (mode == PT_ALPHA_MASK) return a > r.cut;
+        return a >= 1.0f ? true : (blend_random(o, d, (int)slot) < a);
+    }
     const DevPrimInfo pi = S.info[slot];
     const DevTriShade* R = S.tshade + pi.index;
     const float4 rc = R->c, rd = R->d;
@@ -534,7 +576,7 @@ __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out
             if (kind == PT_PRIM_TRIANGLE) {
                 float bx, by, t;
                 if (tri_glm(o, d, xyz(g.a), xyz(g.b), xyz(g.c), bx, by, t) && !(t > tmax || t < PT_EPS)) {
-                    if (!(w0 & GF_ALPHA) || tri_alpha(slot, bx, by, o, d)) {
+                    if (!(w0 & GF_ALPHA) || tri_alpha(__float_as_uint(g.b.w), slot, bx, by, o, d)) {
                         tmax = t;
                         best = (int)slot;
                         bb1 = bx;
@@ -629,7 +671,7 @@ __device__ bool trace_any(f3 o, f3 d, float tmax, uint32_t* s_ref, TraceWork& wk
                     // material HasAlpha(): full Intersect + Alpha (Primitive.cpp:7-10)
                     float bx, by, t;
                     if (tri_glm(o, d, xyz(g.a), xyz(g.b), xyz(g.c), bx, by, t) && !(t > tmax || t < PT_EPS)) {
-                        if (!(w0 & GF_ALPHA) || tri_alpha(slot, bx, by, o, d)) return true;
+                        if (!(w0 & GF_ALPHA) || tri_alpha(__float_as_uint(g.b.w), slot, bx, by, o, d)) return true;
                     }
                 } else if (tri_pred(o, d, xyz(g.a), xyz(g.b), xyz(g.c), tmax)) {
                     return true;
