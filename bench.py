@@ -37,6 +37,10 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+# chip-wide rate of random row gathers served by the XCDs' L2s
+# (MI355X_MICROARCH.md "Indexed rows": 16.8-18.8 TB/s, lower bounds): the
+# ceiling of a kernel whose reads are L2 hits (its "l2-latency" bound)
+L2_GATHER_PEAK_GBS = 18800.0
 # configurations whose BVH + primitive slots exceed the 256 MiB Infinity Cache:
 # their traversal bytes stream from HBM.  The small scenes live in L2/MALL.
 HBM_CONFIGS = ("c4",)
@@ -554,6 +558,32 @@ def main():
         dist.destroy_process_group()
 
 
+def bound_peak(e: dict, large: bool, counted: bool) -> None:
+    """The bound a kernel's counters show and the ceiling its fraction is
+    priced against (a hierarchical roofline: the memory level that serves its
+    reads).  HBM bytes near the HBM peak: "hbm" (8 TB/s).  Far below it, with
+    most reads L2 hits: "l2-latency", priced against the L2 gather rate
+    (L2_GATHER_PEAK_GBS) — each ray's loads form a dependent chain, one round
+    trip per step, and the waves wait on it.  Far below it with a low L2 hit
+    rate: "memory-latency" (misses served by the Infinity Cache / HBM,
+    priced against HBM).  No counter profile of this build: HBM, label
+    unknown."""
+    tf, hit = e.get("traffic_frac"), e.get("l2_hit_rate")
+    if not large:
+        e["bound"], peak = "l2/latency", L2_GATHER_PEAK_GBS
+    elif not counted or tf is None:
+        e["bound"], peak = "unknown (no counter profile of this build)", HBM_PEAK_GBS
+    elif tf >= 0.6:
+        e["bound"], peak = "hbm", HBM_PEAK_GBS
+    elif hit is not None and hit >= 0.7:
+        e["bound"], peak = "l2-latency", L2_GATHER_PEAK_GBS
+    else:
+        e["bound"], peak = "memory-latency", HBM_PEAK_GBS
+    e["peak"] = peak
+    e["peak_source"] = ("MI355X_MICROARCH.md 'Indexed rows' L2-served gather, chip-wide"
+                        if peak == L2_GATHER_PEAK_GBS else "MI355X_MICROARCH.md HBM3E peak")
+
+
 def roofline(args, setup, world, totals, cst, cpu):
     """Per-kernel roofline entries."""
     pool = args.traversal == "pool" or (args.traversal == "auto" and args.config in HBM_CONFIGS)
@@ -591,36 +621,31 @@ def roofline(args, setup, world, totals, cst, cpu):
         bpr = min(cands)
         per_launch = nrays / max(1, launches)
         gbs = lambda b: b * per_launch / (avg_ms * 1e-3) / 1e9  # noqa: E731
-        e = {"kernel": name, "achieved": round(gbs(bpr), 1), "frac": round(gbs(bpr) / HBM_PEAK_GBS, 4),
+        e = {"kernel": name, "achieved": round(gbs(bpr), 1),
              "bytes_per_ray": round(bpr, 1), "priced_on": "reference order" if bpr == ref_b else "own visits",
              "bytes_per_launch": round(bpr * per_launch), "avg_launch_ms": round(avg_ms, 4), "launches": launches}
-        if ref_b:
-            e["ref_order_bytes_per_ray"] = round(ref_b, 1)
-            e["ref_order_frac"] = round(gbs(ref_b) / HBM_PEAK_GBS, 4)
-        if own_b:
-            e["own_visits_bytes_per_ray"] = round(own_b, 1)
-            e["own_visits_frac"] = round(gbs(own_b) / HBM_PEAK_GBS, 4)
-        if layout_b:
-            e["layout_bytes_per_ray"] = round(layout_b, 1)
-            e["layout_achieved"] = round(gbs(layout_b), 1)
-            e["layout_frac"] = round(gbs(layout_b) / HBM_PEAK_GBS, 4)
         traffic, info = pmc_traffic(args.config, setup.spp, world, name, sha)
         e["traffic"] = traffic
         e.update(info)
         if traffic:
             e["traffic_achieved"] = round(traffic / (avg_ms * 1e-3) / 1e9, 1)
             e["traffic_frac"] = round(e["traffic_achieved"] / HBM_PEAK_GBS, 4)
-        # the bound the counters show: bytes from HBM far below the roofline
-        # while waves wait on memory most of their cycles = load latency
-        # through L2, not bandwidth
-        if args.config not in HBM_CONFIGS:
-            e["bound"] = "l2/latency"
-        elif traffic is None:
-            e["bound"] = "unknown (no counter profile of this build)"
-        elif e["traffic_frac"] < 0.3:
-            e["bound"] = "l2-latency"
-        else:
-            e["bound"] = "hbm"
+        bound_peak(e, args.config in HBM_CONFIGS, traffic is not None)
+        peak = e["peak"]
+        e["frac"] = round(gbs(bpr) / peak, 4)
+        # SURVEY §8(d)'s own fraction: the algorithmic bytes over the HBM peak
+        # (above 1 when caches serve what HBM could not: reuse, not skipped work)
+        e["hbm_frac"] = round(gbs(bpr) / HBM_PEAK_GBS, 4)
+        if ref_b:
+            e["ref_order_bytes_per_ray"] = round(ref_b, 1)
+            e["ref_order_frac"] = round(gbs(ref_b) / peak, 4)
+        if own_b:
+            e["own_visits_bytes_per_ray"] = round(own_b, 1)
+            e["own_visits_frac"] = round(gbs(own_b) / peak, 4)
+        if layout_b:
+            e["layout_bytes_per_ray"] = round(layout_b, 1)
+            e["layout_achieved"] = round(gbs(layout_b), 1)
+            e["layout_frac"] = round(gbs(layout_b) / peak, 4)
         return e
 
     lb_c = (node_bytes * cst["nodes_closest"] + 48.0 * cst["tris_closest"]) / max(1, cst["rays_closest"]) if cst else None
@@ -628,7 +653,8 @@ def roofline(args, setup, world, totals, cst, cpu):
             if cst and cst.get("rays_any") else None)
     rc = entry(kname, ref_c, own_c, lb_c, totals["ms_closest"], totals["launches_closest"], totals["rays_closest"])
     ra = entry(sname, ref_a, own_a, lb_a, totals["ms_any"], totals["launches_any"], totals["rays_any"])
-    roof = {"bound": rc["bound"] if rc else None, "achieved": rc["achieved"] if rc else None, "peak": HBM_PEAK_GBS,
+    roof = {"bound": rc["bound"] if rc else None, "achieved": rc["achieved"] if rc else None,
+            "peak": rc["peak"] if rc and rc.get("peak") else HBM_PEAK_GBS,
             "unit": "GB/s", "frac": rc["frac"] if rc else None, "traffic": rc["traffic"] if rc else None,
             "src_sha": sha,
             "count_source": (f"oracle reference order ({ref_counts['closest']} closest / {ref_counts['any']} any rays)"
@@ -663,7 +689,7 @@ def roofline(args, setup, world, totals, cst, cpu):
         if avg_ms > 0:
             per_launch = totals["rays_closest"] / max(1, launches)
             ach = bpr * per_launch / (avg_ms * 1e-3) / 1e9
-            sh = {"kernel": shade_name, "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+            sh = {"kernel": shade_name, "achieved": round(ach, 1),
                   "bytes_per_ray": round(bpr, 1),
                   "hit_fraction": round(ref_counts["hits"] / ref_counts["closest"], 4),
                   "texel_bytes_per_ray": round(ref_counts["tex_bytes"] / ref_counts["closest"], 1),
@@ -677,7 +703,9 @@ def roofline(args, setup, world, totals, cst, cpu):
                 prof_ms = info.get("profile_avg_launch_ms") or avg_ms
                 sh["traffic_achieved"] = round(traffic / (prof_ms * 1e-3) / 1e9, 1)
                 sh["traffic_frac"] = round(sh["traffic_achieved"] / HBM_PEAK_GBS, 4)
-                sh["bound"] = "l2-latency" if sh["traffic_frac"] < 0.3 else "hbm"
+            bound_peak(sh, True, traffic is not None)
+            sh["frac"] = round(ach / sh["peak"], 4)
+            sh["hbm_frac"] = round(ach / HBM_PEAK_GBS, 4)
             roof["shade"] = sh
     return roof
 
