@@ -633,6 +633,12 @@ __global__ __launch_bounds__(256) void k_fill(RenderParams R, uint32_t n, PathSo
 }
 
 // ------------------------------------------------------------------ shading
+// k_shade (Path): the NEE light sample (LightSampler::Sample + Light::sample)
+// drawn before the hit's interaction is rebuilt (it depends only on the
+// sample's draws), so its reads overlap the hit's; same values
+#ifndef PT_SHADE_EARLY_LS
+#define PT_SHADE_EARLY_LS 0
+#endif
 template <int INTEGRATOR>
 #ifdef PT_SHADE_WPE  // tuning: a waves-per-SIMD budget for k_shade
 #define PT_SHADE_WAVES __attribute__((amdgpu_waves_per_eu(PT_SHADE_WPE, PT_SHADE_WPE)))
@@ -703,6 +709,16 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
                 for (int k = 0; k < 4; k++) r[k] = draw(key, dim + k);
                 dim += 4;
             }
+#if PT_SHADE_EARLY_LS
+            // the light sample needs no hit: its chain of reads (guide table,
+            // running sums, light record, shape) runs beside the hit's
+            int li = -1;
+            LSample ls_e;
+            if (INTEGRATOR == PT_INTEGRATOR_PATH) {
+                li = ls_sample(r[5]);
+                if (li >= 0) ls_e = light_sample(S.lights[li], r[2], r[3], texinf_uc(key, dim));
+            }
+#endif
             SurfInt si;
             int smed;
             hit_surface(prim, ro, rd, h.x, h.y, h.z, si, smed);
@@ -741,10 +757,16 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
                         spec = (b.flags & FL_SPEC) != 0;
                         if (!spec) {
                             // PathIntegrator::SampleLd (Integrators.cpp:260-294); occlusion deferred
+#if !PT_SHADE_EARLY_LS
                             const int li = ls_sample(r[5]);
+#endif
                             if (li >= 0) {
                                 const pt_light& l = S.lights[li];
+#if PT_SHADE_EARLY_LS
+                                const LSample ls = ls_e;
+#else
                                 LSample ls = light_sample(l, r[2], r[3], texinf_uc(key, dim));
+#endif
                                 f3 ldir;
                                 float tmax;
                                 if (is_zero(ls.n)) {
