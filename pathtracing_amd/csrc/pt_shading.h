@@ -178,9 +178,12 @@ __device__ f3 tex_eval_t(int id, float u, float v) {
     return F3(0, 0, 0);
 }
 
-// PT_TEXREC (A/B option, default on): the shading path reads DevTex records
+// PT_TEXREC (A/B option, off): the shading path reads DevTex records.  C4:
+// k_shade 1362 -> 1370 ms per frame with them (profiles/r04_ab_alpha.txt):
+// the texture and image records are L1/L2 hits, the hop they save is not
+// what the shading waits on
 #ifndef PT_TEXREC
-#define PT_TEXREC 1
+#define PT_TEXREC 0
 #endif
 // The same over DevTex records (shading path without LDS tables): the
 // texture's record is its image's too, and a caller may load the records of
