@@ -76,6 +76,12 @@ struct ShadowRecV {
     float4 a;  // the path's attenuation, .w: light pdf
 };
 #define SHADOW_DONE_BIT 0x80000000u
+// ShadowRec::c.w of an unoccluded ray whose contribution k_shadow_apply adds
+// (PT_SHADOW_DEFER; the shading writes 0)
+#define SHADOW_VISIBLE 1.0f
+#ifndef PT_SHADOW_DEFER
+#define PT_SHADOW_DEFER 1
+#endif
 // medium interaction: the medium's Le is added after SampleLd's value
 // (Integrators.cpp:356-357), occluded or not
 #define SHADOW_MLE_BIT 0x40000000u
@@ -109,10 +115,10 @@ __global__ void k_closest_pool(PathSoA P, const uint32_t* in, float4* hit, uint3
 template <bool INST>
 __global__ void k_closest_ties(PathSoA P, const uint32_t* in, float4* hit, const uint32_t* pool, const uint32_t* ties);
 template <bool COUNT, bool INST>
-__global__ void k_shadow(PathSoA next, float* sample_L, const ShadowRec* sq, const uint32_t* nptr, uint32_t* pool,
+__global__ void k_shadow(PathSoA next, float* sample_L, ShadowRec* sq, const uint32_t* nptr, uint32_t* pool,
                          uint32_t* ovf, unsigned long long* counters);
 template <bool COUNT, bool INST, bool QN>
-__global__ void k_shadow_pool(PathSoA next, float* sample_L, const ShadowRec* sq, const uint32_t* nptr,
+__global__ void k_shadow_pool(PathSoA next, float* sample_L, ShadowRec* sq, const uint32_t* nptr,
                               uint32_t* pool, uint32_t* ovf, unsigned long long* counters);
 template <int INTEGRATOR>
 __global__ void k_shade(RenderParams R, PathSoA cur, const uint32_t* nptr, const float4* hit, PathSoA next,

@@ -231,8 +231,33 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest_ties(PathSoA P, cons
     }
 }
 
-struct ShadowSrc {
-    const ShadowRec* sq;
+// The unoccluded shadow ray's contribution: fma(c, att, L) into its path's
+// radiance, or into its sample's when the path ended this bounce; one shadow
+// ray per path per bounce, so a plain read-modify-write
+__device__ __forceinline__ void shadow_add(PathSoA& next, float* __restrict__ sample_L, uint32_t tgt, float4 c,
+                                           float4 a) {
+    if (tgt & SHADOW_DONE_BIT) {  // the path ended this bounce: its sample's radiance
+        float* L = sample_L + 3ull * (tgt & ~SHADOW_DONE_BIT);
+        L[0] = fma_(c.x, a.x, L[0]);
+        L[1] = fma_(c.y, a.y, L[1]);
+        L[2] = fma_(c.z, a.z, L[2]);
+        return;
+    }
+    float4* L = &next.L[tgt];
+    float4 v = *L;
+    v.x = fma_(c.x, a.x, v.x);
+    v.y = fma_(c.y, a.y, v.y);
+    v.z = fma_(c.z, a.z, v.z);
+    *L = v;
+}
+// Shadow-ray source of the any-hit kernels.  DEFER (the pool kernel,
+// PT_SHADOW_DEFER): an unoccluded ray only flags its record (c.w = 1, a
+// store) and k_shadow_apply adds the contributions after the traversal; in
+// the loop the add is two dependent reads (record, then the path's radiance)
+// that hold up the whole wave whenever one of its lanes finishes unoccluded.
+template <bool DEFER>
+struct ShadowSrcT {
+    ShadowRec* sq;
     PathSoA next;
     float* sample_L;
     __device__ __forceinline__ bool load(uint32_t i, f3& o, f3& d, float& tmax) {
@@ -246,43 +271,47 @@ struct ShadowSrc {
     __device__ __forceinline__ void tie(uint32_t) {}
     __device__ __forceinline__ void any(uint32_t i, bool hit) {
         if (hit) return;
-        // unoccluded: add the contribution; one shadow ray per path per bounce,
-        // so a plain read-modify-write
-        const uint32_t tgt = __float_as_uint(sq[i].d.w);
-        const float4 c = sq[i].c, a = sq[i].a;
-        if (tgt & SHADOW_DONE_BIT) {  // the path ended this bounce: its sample's radiance
-            float* L = sample_L + 3ull * (tgt & ~SHADOW_DONE_BIT);
-            L[0] = fma_(c.x, a.x, L[0]);
-            L[1] = fma_(c.y, a.y, L[1]);
-            L[2] = fma_(c.z, a.z, L[2]);
+        if (DEFER) {
+            sq[i].c.w = SHADOW_VISIBLE;
             return;
         }
-        float4* L = &next.L[tgt];
-        float4 v = *L;
-        v.x = fma_(c.x, a.x, v.x);
-        v.y = fma_(c.y, a.y, v.y);
-        v.z = fma_(c.z, a.z, v.z);
-        *L = v;
+        shadow_add(next, sample_L, __float_as_uint(sq[i].d.w), sq[i].c, sq[i].a);
     }
 };
+using ShadowSrc = ShadowSrcT<false>;
 
 template <bool COUNT, bool INST, bool QN>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SHADOW_WAVES_FOR(PT_USES_SPEC(INST, QN)) void k_shadow_pool(PathSoA next, float* __restrict__ sample_L,
-                                                               const ShadowRec* __restrict__ sq,
+                                                               ShadowRec* __restrict__ sq,
                                                                const uint32_t* __restrict__ nptr,
                                                                uint32_t* __restrict__ pool, uint32_t* __restrict__ ovf,
                                                                unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_POOL_LDS * PT_TRACE_BLOCK];
     __shared__ __attribute__((aligned(16))) uint8_t s_lut[(QN && PT_Q48) ? 8 * Q48_LUT_STRIDE : 4];
     TraceWork wk{0, 0};
-    ShadowSrc src{sq, next, sample_L};
+    using Src = ShadowSrcT<PT_SHADOW_DEFER != 0>;
+    Src src{sq, next, sample_L};
     const uint32_t n = *nptr;
     if (n == 0) return;
     if constexpr (QN && PT_Q48) stage_q48_lut(s_lut);
-    trace_pool<true, COUNT, ShadowSrc, true, INST, PT_POOL_LDS, QN>(n, pool, src, s_ref, nullptr, ovf, wk, s_lut);
+    trace_pool<true, COUNT, Src, true, INST, PT_POOL_LDS, QN>(n, pool, src, s_ref, nullptr, ovf, wk, s_lut);
     if (COUNT) {
         count_add(counters, CNT_NODES_ANY, wk.nodes);
         count_add(counters, CNT_TRIS_ANY, wk.tris);
+    }
+}
+
+// The deferred contributions of k_shadow_pool (PT_SHADOW_DEFER): the rays it
+// found unoccluded (c.w flagged) add fma(c, att, L) exactly as ShadowSrc::any
+// does in place
+__global__ __launch_bounds__(256) void k_shadow_apply(PathSoA next, float* __restrict__ sample_L,
+                                                      const ShadowRec* __restrict__ sq,
+                                                      const uint32_t* __restrict__ nptr) {
+    const uint32_t n = *nptr;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const float4 c = sq[i].c;
+        if (c.w != SHADOW_VISIBLE) continue;
+        shadow_add(next, sample_L, __float_as_uint(sq[i].d.w), c, sq[i].a);
     }
 }
 
@@ -343,7 +372,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SIMPLE_WAVES void k_closest(Path
 
 template <bool COUNT, bool INST>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SIMPLE_WAVES void k_shadow(PathSoA next, float* __restrict__ sample_L,
-                                                          const ShadowRec* __restrict__ sq,
+                                                          ShadowRec* __restrict__ sq,
                                                           const uint32_t* __restrict__ nptr, uint32_t* __restrict__,
                                                           uint32_t* __restrict__ ovf, unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_SIMPLE_LDS * PT_TRACE_BLOCK];
@@ -1744,12 +1773,12 @@ __global__ __launch_bounds__(256) void k_adapt_decide(const uint32_t* __restrict
 #define PT_INST_TRACE(B, I)                                                                                         \
     template __global__ void k_closest<B, I>(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*, uint32_t*,     \
                                              uint32_t*, unsigned long long*, uint32_t*);                             \
-    template __global__ void k_shadow<B, I>(PathSoA, float*, const ShadowRec*, const uint32_t*, uint32_t*,           \
+    template __global__ void k_shadow<B, I>(PathSoA, float*, ShadowRec*, const uint32_t*, uint32_t*,           \
                                             uint32_t*, unsigned long long*);
 #define PT_INST_POOL(B, I, Q)                                                                                       \
     template __global__ void k_closest_pool<B, I, Q>(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*,        \
                                                      uint32_t*, uint32_t*, unsigned long long*, uint32_t*);          \
-    template __global__ void k_shadow_pool<B, I, Q>(PathSoA, float*, const ShadowRec*, const uint32_t*, uint32_t*,   \
+    template __global__ void k_shadow_pool<B, I, Q>(PathSoA, float*, ShadowRec*, const uint32_t*, uint32_t*,   \
                                                     uint32_t*, unsigned long long*);
 template __global__ void k_closest_ties<false>(PathSoA, const uint32_t*, float4*, const uint32_t*, const uint32_t*);
 template __global__ void k_closest_ties<true>(PathSoA, const uint32_t*, float4*, const uint32_t*, const uint32_t*);

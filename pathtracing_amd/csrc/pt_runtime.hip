@@ -1404,7 +1404,7 @@ static pt_status bind_scene(pt_ctx* c, uint64_t lanes = 0) {
 // traversal kernel of one wavefront iteration
 using ClosestFn = void (*)(PathSoA, const uint32_t*, float4*, uint32_t*, uint32_t*, uint32_t*, uint32_t*,
                            unsigned long long*, uint32_t*);
-using ShadowFn = void (*)(PathSoA, float*, const ShadowRec*, const uint32_t*, uint32_t*, uint32_t*,
+using ShadowFn = void (*)(PathSoA, float*, ShadowRec*, const uint32_t*, uint32_t*, uint32_t*,
                           unsigned long long*);
 template <bool C, bool I>
 static ClosestFn closest_fn(bool pool, bool qn) {
@@ -1699,9 +1699,13 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                                    c->counters);
             } else if (rd->integrator != PT_INTEGRATOR_SIMPLE) {
                 auto ks = pick_shadow(use_pool, qn, inst, count);
-                hipLaunchKernelGGL(ks, ga, dim3(PT_TRACE_BLOCK), 0, sa, nxt, c->sample_L, (const ShadowRec*)c->sq,
+                hipLaunchKernelGGL(ks, ga, dim3(PT_TRACE_BLOCK), 0, sa, nxt, c->sample_L, c->sq,
                                    (const uint32_t*)(out + Q_SHADOW), out + Q_WORDS + PT_POOL_WORDS,
                                    ovl ? c->ovf_any : c->ovf, c->counters);
+                if (use_pool && PT_SHADOW_DEFER)  // the unoccluded rays' contributions (k_shadow_pool defers them)
+                    hipLaunchKernelGGL(k_shadow_apply, dim3(std::max(1u, std::min(2048u, (nb + 255) / 256))),
+                                       dim3(256), 0, sa, nxt, c->sample_L, (const ShadowRec*)c->sq,
+                                       (const uint32_t*)(out + Q_SHADOW));
             }
             HIPCHK(c, hipGetLastError());
             HIPCHK(c, hipEventRecord(ev[4], sa));
