@@ -77,10 +77,11 @@ struct ShadowRecV {
 };
 #define SHADOW_DONE_BIT 0x80000000u
 // ShadowRec::c.w of an unoccluded ray whose contribution k_shadow_apply adds
-// (PT_SHADOW_DEFER; the shading writes 0)
+// (PT_SHADOW_DEFER; the shading writes 0).  Off: C4 any-hit 1178 -> 1192 ms
+// per frame deferred, apply kernel included (profiles/r04_ab_traversal.txt)
 #define SHADOW_VISIBLE 1.0f
 #ifndef PT_SHADOW_DEFER
-#define PT_SHADOW_DEFER 1
+#define PT_SHADOW_DEFER 0
 #endif
 // medium interaction: the medium's Le is added after SampleLd's value
 // (Integrators.cpp:356-357), occluded or not

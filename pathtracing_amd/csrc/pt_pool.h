@@ -25,6 +25,8 @@
 // live in a global overflow array ([entry][grid lane], written and read back by
 // the same lane only).  Deep stacks are rare, and a 20-entry LDS stack (10 KB
 // per block) lets 32 waves per CU fit instead of 20 with all 32 in LDS.
+// C4 r04: 16 / 20 / 24 (closest-hit kernel) -> 1596 / 1613 / 1577 Mrays/s
+// (profiles/r04_ab_traversal.txt)
 #ifndef PT_POOL_LDS
 #define PT_POOL_LDS 20
 #endif
@@ -116,7 +118,9 @@ __device__ unsigned int pt_diag[4];
 // overlapped traversal: the primitive side's triangle test before the node
 // side (only its result live across the node side), its hit handling after
 // overlapped traversal: a leaf step tests the leaf's next primitive too when
-// both are triangles (three more 16-B loads on primitive lanes)
+// both are triangles (three more 16-B loads on primitive lanes).  Off: C4
+// 1613 -> 1100 Mrays/s at 6 waves (spills), 1346 at 5 waves without spills
+// (profiles/r04_ab_traversal.txt)
 #ifndef PT_SPEC_LEAF2
 #define PT_SPEC_LEAF2 0
 #endif
