@@ -156,10 +156,10 @@ enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1, PT_SORT_RAYS = 2 };
 #ifndef PT_SHADE_BLOCK
 // k_shade threads per block (its appends aggregate per block): C4 64 / 128 /
 // 256 / 512 / 1024 -> 1206 / 1236 / 1270 / 1205 / 1278 Mrays/s
-// (profiles/r02_ab_shade.txt).  r04: 256-thread blocks at 3 waves per SIMD
-// (up to 168 VGPRs; 1024-thread blocks force 4 waves, 128 VGPRs): k_shade
-// 1370 -> 1350 ms per frame (profiles/r04_ab_alpha.txt)
-#define PT_SHADE_BLOCK 256
+// (profiles/r02_ab_shade.txt).  r04, k_shade ms per frame on one box
+// (gpurun_out/r4h): 1024 x 4 waves per SIMD 1372, 256 x 3 waves 1374,
+// 512 x 3 waves 1713 (one block per CU: 2 waves per SIMD)
+#define PT_SHADE_BLOCK 1024
 #endif
 #ifndef PT_SORT_PER
 #define PT_SORT_PER 16u  // paths per thread of k_sort_count / k_sort_scatter

@@ -665,13 +665,14 @@ __global__ __launch_bounds__(256) void k_fill(RenderParams R, uint32_t n, PathSo
 // k_shade (Path): the NEE light sample (LightSampler::Sample + Light::sample)
 // drawn before the hit's interaction is rebuilt (it depends only on the
 // sample's draws), so its reads overlap the hit's; same values.  Off: C4
-// k_shade 1350 -> 1354 ms per frame at the same 3 waves (r04_ab_alpha.txt)
+// k_shade 1350 -> 1354 ms per frame (256-thread blocks at 3 waves, where it
+// fits without spills; profiles/r04_ab_alpha.txt)
 #ifndef PT_SHADE_EARLY_LS
 #define PT_SHADE_EARLY_LS 0
 #endif
 template <int INTEGRATOR>
 #ifndef PT_SHADE_WPE  // waves-per-SIMD budget for k_shade (pt_kernels.h PT_SHADE_BLOCK)
-#define PT_SHADE_WPE 3
+#define PT_SHADE_WPE (PT_SHADE_BLOCK >= 1024 ? 4 : 3)
 #endif
 #define PT_SHADE_WAVES __attribute__((amdgpu_waves_per_eu(PT_SHADE_WPE, PT_SHADE_WPE)))
 __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderParams R, PathSoA cur, const uint32_t* __restrict__ nptr,
