@@ -123,7 +123,22 @@ __device__ __forceinline__ float alpha_texel(uint64_t off, int w, int h, int C, 
 // Material.hpp:181-198).  ai: the slot's alpha record (DevAlpha, slot b.w):
 // the record, then the four texels; ALPHA_NONE: prim info -> shading record
 // -> material -> texture -> image.  Same values either way.
-__device__ __noinline__ bool tri_alpha(uint32_t ai, uint32_t slot, float bu, float bv, f3 o, f3 d) {
+__device__ __forceinline__ bool tri_alpha_general(uint32_t slot, float bu, float bv, f3 o, f3 d);
+__device__ __noinline__ bool tri_alpha_slow(uint32_t slot, float bu, float bv, f3 o, f3 d) {
+    return tri_alpha_general(slot, bu, bv, o, d);
+}
+#ifndef PT_ALPHA_INLINE  // the alpha-record path inline in the traversal loop (the general one stays a call)
+#define PT_ALPHA_INLINE 0
+#endif
+#if PT_ALPHA_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+bool tri_alpha(uint32_t ai, uint32_t slot, float bu, float bv, f3 o, f3 d) {
+#ifdef PT_DIAG_NO_ALPHA  // diagnostics builds only (timing of the test's cost; wrong results)
+    return true;
+#endif
     if (ai != ALPHA_NONE) {
         const DevAlpha r = S.alpha[ai];
         const float u = bu, v = bv, w = 1.0f - u - v;
@@ -154,6 +169,10 @@ __device__ __noinline__ bool tri_alpha(uint32_t ai, uint32_t slot, float bu, flo
         if (mode == PT_ALPHA_MASK) return a > r.cut;
         return a >= 1.0f ? true : (blend_random(o, d, (int)slot) < a);
     }
+    return PT_ALPHA_INLINE ? tri_alpha_slow(slot, bu, bv, o, d) : tri_alpha_general(slot, bu, bv, o, d);
+}
+// the general path: prim info -> shading record -> material -> texture -> image
+__device__ __forceinline__ bool tri_alpha_general(uint32_t slot, float bu, float bv, f3 o, f3 d) {
     const DevPrimInfo pi = S.info[slot];
     const DevTriShade* R = S.tshade + pi.index;
     const float4 rc = R->c, rd = R->d;
