@@ -340,6 +340,46 @@ def blend_box(W: int = 64, H: int = 64, spp: int = 16, max_depth: int = 8, alpha
     return SceneSetup(scene, setup.camera, setup.integrator, UniformLightSampler(), max_depth, seed, spp).finish()
 
 
+def alpha_maps(W: int = 32, H: int = 32, spp: int = 4, max_depth: int = 8, seed: int = 0x5EED0042) -> SceneSetup:
+    """C3 Cornell box behind panels cut by every deterministic alpha source
+    (AlphaTester Mask, Material.hpp:181-198): an RGB alpha texture with a
+    colorScale (Evaluate(uv).x * scale), a one-channel alpha texture, a solid
+    alpha below the cutoff (never passes), an RGBA albedo's fourth channel
+    (Texture::alpha), and a rough dielectric with an alpha texture."""
+    rng = np.random.default_rng(4242)
+    setup = cornell(W=W, H=H, spp=spp, config="c3", max_depth=max_depth, seed=seed)
+    scene = setup.scene
+    Mask = AlphaTester(AlphaMode.Mask, 0.5)
+    rgb_alpha = ImageTexture(_noise_img(rng, 24, 24, 3, 0, 255, smooth=3), colorScale=(1.25, 1, 1))
+    one_alpha = ImageTexture(_noise_img(rng, 16, 16, 1, 0, 255, smooth=2))
+    rgba = ImageTexture(_noise_img(rng, 16, 16, 4, 0, 255, smooth=2), gammaCorrection=True)
+    mats = []
+    m = MicrofacetDiffuse(SolidColor((0.2, 0.5, 0.8)), None, None, None, rgb_alpha)
+    m.setAlphaTester(Mask)
+    mats.append(m)
+    m = MicrofacetDiffuse(SolidColor((0.8, 0.3, 0.2)), None, None, None, one_alpha)
+    m.setAlphaTester(AlphaTester(AlphaMode.Mask, 0.4))
+    mats.append(m)
+    m = MicrofacetDiffuse(SolidColor((0.9, 0.9, 0.1)), None, None, None, SolidColor((0.3, 0.3, 0.3)))
+    m.setAlphaTester(Mask)
+    mats.append(m)
+    m = MicrofacetDiffuse(rgba)
+    m.setAlphaTester(AlphaTester(AlphaMode.Mask, 0.55))
+    mats.append(m)
+    m = MicrofacetDielectric(1.5, SolidColor((1, 1, 1)), None, SolidColor((0.3, 0.3, 0.3)), one_alpha)
+    m.setAlphaTester(Mask)
+    mats.append(m)
+    meshes = []
+    for k, mat in enumerate(mats):
+        x0 = -0.9 + 0.36 * k
+        z = 0.9 - 0.25 * (k % 2)
+        idx, v, n, uv = _quad_tris((x0, -0.8, z), (x0 + 0.34, -0.8, z), (x0 + 0.34, 0.3, z + 0.1),
+                                   (x0, 0.3, z + 0.1))
+        meshes.append(Mesh(idx, v, None, n, uv * 1.7, mat))
+    scene.Add(Model(meshes))
+    return SceneSetup(scene, setup.camera, setup.integrator, UniformLightSampler(), max_depth, seed, spp).finish()
+
+
 # --------------------------------------------------------------------------
 def _grid_mesh(nx: int, nz: int, size: float, y_fn, rng, tangents: bool, uv_scale: float = 1.0):
     xs = np.linspace(-size, size, nx + 1, dtype=np.float32)

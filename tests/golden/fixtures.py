@@ -57,6 +57,9 @@ def parity_scenes():
         # emitters inside instances: TransformedLight / AnimatedLight
         # (Light.cpp:300-364) for an emissive Model, a quad and a sphere light
         "lit_instances": lambda: scenes.lit_instances(W=32, H=32, spp=4),
+        # every deterministic alpha source (the traversal's alpha records):
+        # RGB / one-channel / solid alpha textures, an RGBA albedo's alpha
+        "alpha_maps": lambda: scenes.alpha_maps(W=32, H=32, spp=4),
     }
 
 
