@@ -158,6 +158,7 @@ static_assert(sizeof(DevTex) == 32, "texture record layout");
 #define OCT_INST 8u   // the lane's ray is in an instance's object space
 #define OCT_HIT 16u   // ... and accepted a hit there
 #define OCT_FOUND 32u // overlapped traversal (pt_pool.h trace_spec): a hit was stored
+#define OCT_FRESH 128u // overlapped traversal with PT_PRECLAIM: the ray was claimed this iteration (set up after the loads)
 #define OCT_TIE 64u   // pool traversal: this ray met a hit at exactly t == max (listed once for the exact re-trace)
 #define OCT_SP_SHIFT 8  // ... entered at this stack depth (bits 8-13)
 #define SCR_WORDS 9   // scratch row: world o, d, tmax, length, instance

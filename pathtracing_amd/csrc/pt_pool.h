@@ -115,6 +115,17 @@ __device__ unsigned int pt_diag[4];
 #ifndef PT_BUFFER_LOADS
 #define PT_BUFFER_LOADS 1
 #endif
+// overlapped traversal: each refill claims the next refill's rays (the claim's
+// atomic returns while the wave traverses), and a claimed ray's origin and
+// direction load beside its first node load instead of before it
+#ifndef PT_PRECLAIM
+#define PT_PRECLAIM 1
+#endif
+// overlapped traversal: the stack's LDS and overflow parts through separate
+// ds / buffer ops (no flat pops waiting on all vector memory)
+#ifndef PT_STACK_SPLIT
+#define PT_STACK_SPLIT 1
+#endif
 // overlapped traversal: the primitive side's triangle test before the node
 // side (only its result live across the node side), its hit handling after
 // overlapped traversal: a leaf step tests the leaf's next primitive too when
@@ -197,6 +208,36 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
 #else
 #define PT_IT(k, v) do { } while (0)
 #endif
+#if PT_STACK_SPLIT
+    // the overflow entries through a buffer resource and the LDS ones through
+    // ds ops, in separate branches: a pointer select of the two becomes a flat
+    // access, and a flat pop waits for every outstanding vector memory op of
+    // the wave (the previous iteration's hit stores, a fresh ray's loads)
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(ovf, (short)0, 0x7FFFFFFF, 0x00020000);
+    auto push = [&](uint32_t v) {
+        if (sp < PT_POOL_STACK) {
+            if (LN >= PT_POOL_STACK || sp < LN) {
+                s_ref[sp * PT_TRACE_BLOCK + lane] = v;
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b32(v, ors, (uint32_t)((sp - LN) * G + gl) * 4u, 0, 0);
+            }
+            ++sp;
+        } else {
+            atomicAdd(S.stack_drops, 1u);
+        }
+    };
+    auto pop = [&]() -> uint32_t {
+        --sp;
+        uint32_t v;
+        if (LN >= PT_POOL_STACK || sp < LN) {
+            v = s_ref[sp * PT_TRACE_BLOCK + lane];
+        } else {
+            v = __builtin_amdgcn_raw_buffer_load_b32(ors, (uint32_t)((sp - LN) * G + gl) * 4u, 0, 0);
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) here, on the rare overflow path only
+        }
+        return v;
+    };
+#else
     auto push = [&](uint32_t v) {
         if (sp < PT_POOL_STACK) {
             if (LN >= PT_POOL_STACK || sp < LN) s_ref[sp * PT_TRACE_BLOCK + lane] = v;
@@ -210,7 +251,14 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         --sp;
         return (LN >= PT_POOL_STACK || sp < LN) ? s_ref[sp * PT_TRACE_BLOCK + lane] : ovf[(size_t)(sp - LN) * G + gl];
     };
+#endif
     auto is_leaf = [](uint32_t r) { return r != REF_EMPTY && (r & REF_LEAF); };
+#if PT_PRECLAIM
+    // the next refill's rays, claimed at this refill (PT_REFILL of them from
+    // chunk pc_chunk; lane 0 holds the atomic's return until then)
+    bool pc_valid = false;
+    uint32_t pc_chunk = home, pc_old = 0;
+#endif
     for (;;) {
         PT_IT(0, 1);
         const uint64_t idle = __ballot(ri < 0);
@@ -219,7 +267,23 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             // claims as in trace_pool
             uint32_t base = 0, got = 0;
             PT_IT(1, 1);
+#if PT_PRECLAIM
+            if (pc_valid) {  // the batch claimed at the previous refill
+                const uint32_t old = __builtin_amdgcn_readfirstlane(pc_old);
+                const uint32_t lo = pc_chunk * cs, hi = min(n, lo + cs);
+                if (lo + old < hi) {
+                    base = lo + old;
+                    got = min((uint32_t)PT_REFILL, hi - base);
+                } else {
+                    dead |= 1u << pc_chunk;
+                }
+                pc_valid = false;
+            }
+            if (got == 0 && dead != all_dead) {
+#else
             if (dead != all_dead) {
+#endif
+                uint32_t cc = 0;
                 if (wl == 0) {
                     #pragma unroll 1
                     for (uint32_t k = 0; k < PT_POOL_CHUNKS; k++) {
@@ -230,6 +294,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                         if (lo + old < hi) {
                             base = lo + old;
                             got = min(nidle, hi - base);
+                            cc = c;
                             break;
                         }
                         dead |= 1u << c;
@@ -238,23 +303,49 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 base = __builtin_amdgcn_readfirstlane(base);
                 got = __builtin_amdgcn_readfirstlane(got);
                 dead = __builtin_amdgcn_readfirstlane(dead);
-                if (ri < 0) {
-                    const uint32_t k = (uint32_t)__popcll(idle & ((1ull << wl) - 1ull));
-                    if (k < got) {
-                        ri = (int)(base + k);
-                        if (src.load((uint32_t)ri, o, d, tmax)) {
-                            inv = inv_dir(d);
-                            oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
-                            ref = PT_Q48 ? S.qroot : S.root;
-                            leaf = REF_EMPTY;
-                            sp = 0;
-                        } else {
-                            ri = -1;
-                        }
-                    }
+#if PT_PRECLAIM
+                pc_chunk = __builtin_amdgcn_readfirstlane(cc);
+#else
+                (void)cc;
+#endif
+            }
+            if (ri < 0) {
+                const uint32_t k = (uint32_t)__popcll(idle & ((1ull << wl) - 1ull));
+                if (k < got) {
+                    ri = (int)(base + k);
+#if PT_PRECLAIM
+                    // only the loads here: the ray is set up (1/d, octant) once
+                    // this iteration's node loads are in flight too, so the
+                    // two round trips overlap (trace_spec's sources never skip
+                    // a ray: ClosestSrc / ShadowSrcT::load return true)
+                    src.load((uint32_t)ri, o, d, tmax);
+                    oct = OCT_FRESH;
+#else
+                    if (!src.load((uint32_t)ri, o, d, tmax)) __builtin_trap();
+                    inv = inv_dir(d);
+                    oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
+#endif
+                    ref = PT_Q48 ? S.qroot : S.root;
+                    leaf = REF_EMPTY;
+                    sp = 0;
                 }
             }
+#if PT_PRECLAIM
+            // claim the next refill's rays now: the atomic returns while the
+            // wave traverses instead of on the refill's critical path
+            if (dead != all_dead) {
+                #pragma unroll 1
+                for (uint32_t k = 0; k < PT_POOL_CHUNKS; k++) {
+                    if (!((dead >> pc_chunk) & 1u)) break;
+                    pc_chunk = (pc_chunk + 1) % PT_POOL_CHUNKS;
+                }
+                if (wl == 0) pc_old = atomicAdd(&pool[pc_chunk * PT_POOL_STRIDE], (uint32_t)PT_REFILL);
+                pc_valid = true;
+            }
+            if (got == 0 && dead == all_dead && !pc_valid && __ballot(ri >= 0) == 0) break;
+#else
             if (got == 0 && dead == all_dead && __ballot(ri >= 0) == 0) break;
+#endif
         }
         if (ri < 0) continue;
 
@@ -341,6 +432,12 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         const float4 g0 = qg[0], g1 = qg[1], g2 = qg[2];
 #endif
         __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink the slot loads past the node side)
+#if PT_PRECLAIM
+        if (oct & OCT_FRESH) {  // a ray claimed this iteration: its origin and direction are in
+            inv = inv_dir(d);
+            oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
+        }
+#endif
 #if PT_TRI_FIRST
         // the triangle test first: its 12 slot words die before the node side,
         // and only its result (t, barycentrics, flags) stays live across it
