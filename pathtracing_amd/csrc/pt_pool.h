@@ -117,12 +117,15 @@ __device__ unsigned int pt_diag[4];
 #endif
 // overlapped traversal: each refill claims the next refill's rays (the claim's
 // atomic returns while the wave traverses), and a claimed ray's origin and
-// direction load beside its first node load instead of before it
+// direction load beside its first node load instead of before it.  Off: C4
+// closest-hit 3641 -> 3699 ms per frame (a refill then starts PT_REFILL rays,
+// not every idle lane; profiles/r04_ab_traversal.txt)
 #ifndef PT_PRECLAIM
-#define PT_PRECLAIM 1
+#define PT_PRECLAIM 0
 #endif
 // overlapped traversal: the stack's LDS and overflow parts through separate
-// ds / buffer ops (no flat pops waiting on all vector memory)
+// ds / buffer ops (no flat pops waiting on all vector memory; C4: neutral,
+// 3640 vs 3641 ms per frame)
 #ifndef PT_STACK_SPLIT
 #define PT_STACK_SPLIT 1
 #endif

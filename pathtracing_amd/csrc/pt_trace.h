@@ -127,8 +127,11 @@ __device__ __forceinline__ bool tri_alpha_general(uint32_t slot, float bu, float
 __device__ __noinline__ bool tri_alpha_slow(uint32_t slot, float bu, float bv, f3 o, f3 d) {
     return tri_alpha_general(slot, bu, bv, o, d);
 }
-#ifndef PT_ALPHA_INLINE  // the alpha-record path inline in the traversal loop (the general one stays a call)
-#define PT_ALPHA_INLINE 0
+// the alpha-record path inline in the traversal loop (the general one stays a
+// call): C4 1615 -> 1633 Mrays/s (closest-hit 20.58 -> 20.29 ms per launch,
+// profiles/r04_ab_traversal.txt)
+#ifndef PT_ALPHA_INLINE
+#define PT_ALPHA_INLINE 1
 #endif
 #if PT_ALPHA_INLINE
 __device__ __forceinline__
