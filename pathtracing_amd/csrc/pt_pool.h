@@ -123,6 +123,12 @@ __device__ unsigned int pt_diag[4];
 #ifndef PT_PRECLAIM
 #define PT_PRECLAIM 0
 #endif
+// overlapped traversal: a claimed ray's origin / direction load beside its
+// first node load and the ray is set up (1/d, octant) after both arrive:
+// C4 1636.7 -> 1641.9 Mrays/s (profiles/r04_ab_traversal.txt)
+#ifndef PT_DEFER_SETUP
+#define PT_DEFER_SETUP 1
+#endif
 // overlapped traversal: the stack's LDS and overflow parts through separate
 // ds / buffer ops (no flat pops waiting on all vector memory; C4: neutral,
 // 3640 vs 3641 ms per frame)
@@ -316,7 +322,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 const uint32_t k = (uint32_t)__popcll(idle & ((1ull << wl) - 1ull));
                 if (k < got) {
                     ri = (int)(base + k);
-#if PT_PRECLAIM
+#if PT_DEFER_SETUP
                     // only the loads here: the ray is set up (1/d, octant) once
                     // this iteration's node loads are in flight too, so the
                     // two round trips overlap (trace_spec's sources never skip
@@ -435,7 +441,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         const float4 g0 = qg[0], g1 = qg[1], g2 = qg[2];
 #endif
         __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink the slot loads past the node side)
-#if PT_PRECLAIM
+#if PT_DEFER_SETUP
         if (oct & OCT_FRESH) {  // a ray claimed this iteration: its origin and direction are in
             inv = inv_dir(d);
             oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
