@@ -265,6 +265,9 @@ enum { PT_FILTER_MITCHELL = 0, PT_FILTER_BOX = 1, PT_FILTER_GAUSSIAN = 2, PT_FIL
 #define PT_RENDER_SERIAL_SHADOW 0x800u  /* any-hit rays of a bounce after it, on one stream     */
 #define PT_RENDER_OVERLAP_SHADOW 0x1000u /* ... beside the next bounce's closest-hit rays, on a
                                          * second stream (pool traversal, no instances)    */
+#define PT_RENDER_NO_TAIL 0x2000u       /* no tail kernel: every bounce a wavefront iteration
+                                          (default: the last bounces of a fixed-SPP Path /
+                                          SimplePath chunk finish in one launch, k_tail) */
 
 typedef struct pt_render_desc {
     uint32_t integrator;       /* PT_INTEGRATOR_*                               */

@@ -35,6 +35,8 @@
 #define CNT_TRIS_ANY 3
 #define CNT_NEXT_SAMPLE 4
 #define CNT_EXTRA_ANY 5  // VolPath: shadow-ray continuations past medium boundaries
+#define CNT_TAIL_CLOSEST 6  // k_tail: closest-hit queries (Scene::Intersect) it traced
+#define CNT_TAIL_ANY 7      // k_tail: NEE queries (Scene::IntersectPred) it traced
 #define CNT_COUNT 8
 #define CNT_SHARDS 64  // work counters are sharded by block to avoid a hot line
 
@@ -121,6 +123,9 @@ __global__ void k_shadow(PathSoA next, float* sample_L, ShadowRec* sq, const uin
 template <bool COUNT, bool INST, bool QN>
 __global__ void k_shadow_pool(PathSoA next, float* sample_L, ShadowRec* sq, const uint32_t* nptr,
                               uint32_t* pool, uint32_t* ovf, unsigned long long* counters);
+template <int INTEGRATOR, bool INST, bool COUNT>
+__global__ void k_tail(RenderParams R, PathSoA cur, const uint32_t* nptr, float* sample_L,
+                       unsigned long long* counters);
 template <int INTEGRATOR>
 __global__ void k_shade(RenderParams R, PathSoA cur, const uint32_t* nptr, const float4* hit, PathSoA next,
                         float* sample_L, unsigned long long* next_sample, ShadowRec* sq, uint32_t* cnt);

@@ -670,6 +670,183 @@ __global__ __launch_bounds__(256) void k_fill(RenderParams R, uint32_t n, PathSo
 #ifndef PT_SHADE_EARLY_LS
 #define PT_SHADE_EARLY_LS 0
 #endif
+// One bounce of PathIntegrator::Li / SimplePathIntegrator::Li for one path
+// (Integrators.cpp:131-294): the closest hit h = (t, b1, b2, prim) of the ray
+// (ro, rd) is shaded, emission and the NEE sample drawn, the next ray sampled.
+// In: the path's state (f0 = depth | rr | spec flags); out: the next state,
+// cont / done, and the NEE shadow record when `shadow`.  k_shade runs it over
+// the wavefront, k_tail per lane in a loop.
+template <int INTEGRATOR>
+__device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, uint32_t f0, f3& ro, f3& rd, f3& att,
+                                             f3& out, float& prev, uint32_t key, uint32_t& dim, uint32_t& flags,
+                                             bool& cont, bool& done, bool& shadow, ShadowRec& srec) {
+    uint32_t depth = f0 & PF_DEPTH_MASK, rr = (f0 >> PF_RR_SHIFT) & PF_DEPTH_MASK;
+    bool spec = (f0 & PF_SPEC) != 0;
+    int prim = __float_as_int(h.w);
+#if PT_POOL_CHECK
+    if (__float_as_uint(h.x) == 0xFFFFFFFFu) atomicAdd(&pt_diag[2], 1u);  // debugging builds only
+    if (prim >= (int)S.n_prims) {
+        atomicAdd(&pt_diag[1], 1u);
+        prim = -1;
+    }
+#endif
+    bool alive = true;
+    if (prim < 0) {
+        // miss: infinite lights (Integrators.cpp:140-145, 196-208)
+        for (uint32_t k = 0; k < S.n_infinite_lights; k++) {
+            const pt_light& l = S.lights[S.infinite_lights[k]];
+            // as built: out += att * Le fused; lp*lp + p*p and out += (Le*att)*w fused
+            if (INTEGRATOR == PT_INTEGRATOR_SIMPLE || spec) {
+                out = fma3(inf_le(l, rd), att, out);
+            } else if (prev > 0) {
+                const float lp = l.pmf * inf_pdf(l, rd), p2 = prev * prev;
+                const float w = p2 / fma_(lp, lp, p2);
+                out = fma3s(w, inf_le(l, rd) * att, out);
+            }
+        }
+        alive = false;
+    } else {
+        float r[8];
+        if (INTEGRATOR == PT_INTEGRATOR_PATH) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) r[k] = draw(key, dim + k);
+            dim += 8;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++) r[k] = draw(key, dim + k);
+            dim += 4;
+        }
+#if PT_SHADE_EARLY_LS
+        // the light sample needs no hit: its chain of reads (guide table,
+        // running sums, light record, shape) runs beside the hit's
+        int li = -1;
+        LSample ls_e;
+        if (INTEGRATOR == PT_INTEGRATOR_PATH) {
+            li = ls_sample(r[5]);
+            if (li >= 0) ls_e = light_sample(S.lights[li], r[2], r[3], texinf_uc(key, dim));
+        }
+#endif
+        SurfInt si;
+        int smed;
+        hit_surface(prim, ro, rd, h.x, h.y, h.z, si, smed);
+#ifdef PT_DEBUG_KEY
+        if (key == PT_DEBUG_KEY)
+            printf("G d%u prim %d t %a p %a %a %a ns %a %a %a uv %a %a mat %d light %d out %a %a %a att %a %a %a\n",
+                   depth, prim, si.t, si.p.x, si.p.y, si.p.z, si.ns.x, si.ns.y, si.ns.z, si.u, si.v, si.mat,
+                   si.light, out.x, out.y, out.z, att.x, att.y, att.z);
+#endif
+        // emission (Integrators.cpp:151-154, 217-226)
+        if (si.light >= 0) {
+            const pt_light& al = S.lights[si.light];
+            f3 Le = light_L(al, si.n, si.u, si.v, rd);
+            if (!is_zero(Le)) {
+                if (INTEGRATOR == PT_INTEGRATOR_SIMPLE || spec) {
+                    out = fma3(Le, att, out);
+                } else if (prev > 0) {
+                    const float lp = al.pmf * light_pdf(al, si.p, si.n, ro, rd), p2 = prev * prev;
+                    const float w = p2 / fma_(lp, lp, p2);
+                    out = fma3s(w, Le * att, out);
+                }
+            }
+        }
+        if (si.mat < 0) {
+            // medium boundary: pass through (Integrators.cpp:156-159, 228-232)
+            if (INTEGRATOR == PT_INTEGRATOR_PATH) spec = true;
+            ro = at_f(ro, rd, si.t);
+        } else {
+            const float us = INTEGRATOR == PT_INTEGRATOR_PATH ? r[4] : r[2];
+            const MatTex mt = mat_tex(si.mat, si);  // the hit's textures, read once
+            const Bxdf b = mat_scatter(mt, ro, rd, si, us, r[0], r[1]);
+            if (!b.ok) {
+                alive = false;  // absorbed
+            } else {
+                if (INTEGRATOR == PT_INTEGRATOR_PATH) {
+                    spec = (b.flags & FL_SPEC) != 0;
+                    if (!spec) {
+                        // PathIntegrator::SampleLd (Integrators.cpp:260-294); occlusion deferred
+#if !PT_SHADE_EARLY_LS
+                        const int li = ls_sample(r[5]);
+#endif
+                        if (li >= 0) {
+                            const pt_light& l = S.lights[li];
+#if PT_SHADE_EARLY_LS
+                            const LSample ls = ls_e;
+#else
+                            LSample ls = light_sample(l, r[2], r[3], texinf_uc(key, dim));
+#endif
+                            f3 ldir;
+                            float tmax;
+                            if (is_zero(ls.n)) {
+                                ldir = ls.dir;
+                                tmax = __int_as_float(0x7f800000);
+                            } else {
+                                ldir = ls.p - si.p;
+                                tmax = length(ldir) - PT_EPS;
+                            }
+                            const f3 sd = normalize(ldir);
+                            float lpdf = l.pmf;
+                            const float dt = dot_yxz(si.ns, sd);  // as built: y, x, z order
+                            if (!(lpdf <= 0 || dt * dot(rd, si.ns) >= 0)) {
+                                const f3 f = mat_f(mt, rd, si, sd) * fabsf(dt);
+                                f3 c;
+                                bool ok = true;
+                                if (light_is_delta(l)) {
+                                    c = (ls.L * f) / lpdf;
+                                } else {
+                                    lpdf *= light_pdf(l, ls.p, ls.n, si.p, sd);
+                                    if (lpdf <= 0) {
+                                        ok = false;
+                                    } else {
+                                        const float w2 = lpdf * lpdf;
+                                        const float w1 = mat_pdf(mt, rd, si, sd);
+                                        const float wl = w2 / fma_(w1, w1, w2);  // w1*w1 + w2 fused
+                                        c = ((light_L(l, ls.n, ls.u, ls.v, sd) * f) * wl) / lpdf;
+                                    }
+                                }
+                                if (ok && !is_zero(c)) {
+                                    shadow = true;
+                                    srec.o = make_float4(si.p.x, si.p.y, si.p.z, tmax);
+                                    srec.d = make_float4(sd.x, sd.y, sd.z, 0.0f);
+                                    srec.c = make_float4(c.x, c.y, c.z, 0.0f);
+                                    srec.a = make_float4(att.x, att.y, att.z, 0.0f);
+                                }
+                            }
+                        }
+                        prev = mat_pdf(mt, rd, si, b.d);
+#ifdef PT_DEBUG_KEY
+                        if (key == PT_DEBUG_KEY)
+                            printf("G  nee c %a %a %a (light %d) shadow %d\n", srec.c.x, srec.c.y, srec.c.z, li,
+                                   (int)shadow);
+#endif
+                    }
+                }
+#ifdef PT_DEBUG_KEY
+                if (key == PT_DEBUG_KEY)
+                    printf("G  scatter d %a %a %a f %a %a %a pdf %a prev %a\n", b.d.x, b.d.y, b.d.z, b.f.x, b.f.y,
+                           b.f.z, b.pdf, prev);
+#endif
+                att = att * ((b.f * fabsf(dot(si.ns, b.d))) / b.pdf);
+                const float urr = INTEGRATOR == PT_INTEGRATOR_PATH ? r[6] : r[3];
+                if (rr++ > 3) {
+                    float qq = fminf(0.95f, fmaxf(fmaxf(att.x, att.y), att.z));
+                    if (urr >= qq) alive = false;
+                    else att = att / qq;
+                }
+                ro = b.o;
+                rd = b.d;
+            }
+        }
+    }
+    // loop test `depth++ < maxDepth && sum(att) > 0` (Integrators.cpp:138, 193)
+    if (alive && depth < R.max_depth && (att.x + att.y + att.z) > 0.0f) {
+        depth++;
+        cont = true;
+    } else {
+        done = true;
+    }
+    flags = depth | (rr << PF_RR_SHIFT) | (spec ? PF_SPEC : 0u);
+}
+
 template <int INTEGRATOR>
 #ifndef PT_SHADE_WPE  // waves-per-SIMD budget for k_shade (pt_kernels.h PT_SHADE_BLOCK)
 #define PT_SHADE_WPE (PT_SHADE_BLOCK >= 1024 ? 4 : 3)
@@ -702,172 +879,8 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
         prev = b4.w;
         key = __float_as_uint(o4.w);
         dim = __float_as_uint(L4.w);
-        const uint32_t f0 = __float_as_uint(d4.w);
-        uint32_t depth = f0 & PF_DEPTH_MASK, rr = (f0 >> PF_RR_SHIFT) & PF_DEPTH_MASK;
-        bool spec = (f0 & PF_SPEC) != 0;
-        int prim = __float_as_int(h.w);
-#if PT_POOL_CHECK
-        if (__float_as_uint(h.x) == 0xFFFFFFFFu) atomicAdd(&pt_diag[2], 1u);  // debugging builds only
-        if (prim >= (int)S.n_prims) {
-            atomicAdd(&pt_diag[1], 1u);
-            prim = -1;
-        }
-#endif
-        bool alive = true;
-        if (prim < 0) {
-            // miss: infinite lights (Integrators.cpp:140-145, 196-208)
-            for (uint32_t k = 0; k < S.n_infinite_lights; k++) {
-                const pt_light& l = S.lights[S.infinite_lights[k]];
-                // as built: out += att * Le fused; lp*lp + p*p and out += (Le*att)*w fused
-                if (INTEGRATOR == PT_INTEGRATOR_SIMPLE || spec) {
-                    out = fma3(inf_le(l, rd), att, out);
-                } else if (prev > 0) {
-                    const float lp = l.pmf * inf_pdf(l, rd), p2 = prev * prev;
-                    const float w = p2 / fma_(lp, lp, p2);
-                    out = fma3s(w, inf_le(l, rd) * att, out);
-                }
-            }
-            alive = false;
-        } else {
-            float r[8];
-            if (INTEGRATOR == PT_INTEGRATOR_PATH) {
-#pragma unroll
-                for (int k = 0; k < 8; k++) r[k] = draw(key, dim + k);
-                dim += 8;
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; k++) r[k] = draw(key, dim + k);
-                dim += 4;
-            }
-#if PT_SHADE_EARLY_LS
-            // the light sample needs no hit: its chain of reads (guide table,
-            // running sums, light record, shape) runs beside the hit's
-            int li = -1;
-            LSample ls_e;
-            if (INTEGRATOR == PT_INTEGRATOR_PATH) {
-                li = ls_sample(r[5]);
-                if (li >= 0) ls_e = light_sample(S.lights[li], r[2], r[3], texinf_uc(key, dim));
-            }
-#endif
-            SurfInt si;
-            int smed;
-            hit_surface(prim, ro, rd, h.x, h.y, h.z, si, smed);
-#ifdef PT_DEBUG_KEY
-            if (key == PT_DEBUG_KEY)
-                printf("G d%u prim %d t %a p %a %a %a ns %a %a %a uv %a %a mat %d light %d out %a %a %a att %a %a %a\n",
-                       depth, prim, si.t, si.p.x, si.p.y, si.p.z, si.ns.x, si.ns.y, si.ns.z, si.u, si.v, si.mat,
-                       si.light, out.x, out.y, out.z, att.x, att.y, att.z);
-#endif
-            // emission (Integrators.cpp:151-154, 217-226)
-            if (si.light >= 0) {
-                const pt_light& al = S.lights[si.light];
-                f3 Le = light_L(al, si.n, si.u, si.v, rd);
-                if (!is_zero(Le)) {
-                    if (INTEGRATOR == PT_INTEGRATOR_SIMPLE || spec) {
-                        out = fma3(Le, att, out);
-                    } else if (prev > 0) {
-                        const float lp = al.pmf * light_pdf(al, si.p, si.n, ro, rd), p2 = prev * prev;
-                        const float w = p2 / fma_(lp, lp, p2);
-                        out = fma3s(w, Le * att, out);
-                    }
-                }
-            }
-            if (si.mat < 0) {
-                // medium boundary: pass through (Integrators.cpp:156-159, 228-232)
-                if (INTEGRATOR == PT_INTEGRATOR_PATH) spec = true;
-                ro = at_f(ro, rd, si.t);
-            } else {
-                const float us = INTEGRATOR == PT_INTEGRATOR_PATH ? r[4] : r[2];
-                const MatTex mt = mat_tex(si.mat, si);  // the hit's textures, read once
-                const Bxdf b = mat_scatter(mt, ro, rd, si, us, r[0], r[1]);
-                if (!b.ok) {
-                    alive = false;  // absorbed
-                } else {
-                    if (INTEGRATOR == PT_INTEGRATOR_PATH) {
-                        spec = (b.flags & FL_SPEC) != 0;
-                        if (!spec) {
-                            // PathIntegrator::SampleLd (Integrators.cpp:260-294); occlusion deferred
-#if !PT_SHADE_EARLY_LS
-                            const int li = ls_sample(r[5]);
-#endif
-                            if (li >= 0) {
-                                const pt_light& l = S.lights[li];
-#if PT_SHADE_EARLY_LS
-                                const LSample ls = ls_e;
-#else
-                                LSample ls = light_sample(l, r[2], r[3], texinf_uc(key, dim));
-#endif
-                                f3 ldir;
-                                float tmax;
-                                if (is_zero(ls.n)) {
-                                    ldir = ls.dir;
-                                    tmax = __int_as_float(0x7f800000);
-                                } else {
-                                    ldir = ls.p - si.p;
-                                    tmax = length(ldir) - PT_EPS;
-                                }
-                                const f3 sd = normalize(ldir);
-                                float lpdf = l.pmf;
-                                const float dt = dot_yxz(si.ns, sd);  // as built: y, x, z order
-                                if (!(lpdf <= 0 || dt * dot(rd, si.ns) >= 0)) {
-                                    const f3 f = mat_f(mt, rd, si, sd) * fabsf(dt);
-                                    f3 c;
-                                    bool ok = true;
-                                    if (light_is_delta(l)) {
-                                        c = (ls.L * f) / lpdf;
-                                    } else {
-                                        lpdf *= light_pdf(l, ls.p, ls.n, si.p, sd);
-                                        if (lpdf <= 0) {
-                                            ok = false;
-                                        } else {
-                                            const float w2 = lpdf * lpdf;
-                                            const float w1 = mat_pdf(mt, rd, si, sd);
-                                            const float wl = w2 / fma_(w1, w1, w2);  // w1*w1 + w2 fused
-                                            c = ((light_L(l, ls.n, ls.u, ls.v, sd) * f) * wl) / lpdf;
-                                        }
-                                    }
-                                    if (ok && !is_zero(c)) {
-                                        shadow = true;
-                                        srec.o = make_float4(si.p.x, si.p.y, si.p.z, tmax);
-                                        srec.d = make_float4(sd.x, sd.y, sd.z, 0.0f);
-                                        srec.c = make_float4(c.x, c.y, c.z, 0.0f);
-                                        srec.a = make_float4(att.x, att.y, att.z, 0.0f);
-                                    }
-                                }
-                            }
-                            prev = mat_pdf(mt, rd, si, b.d);
-#ifdef PT_DEBUG_KEY
-                            if (key == PT_DEBUG_KEY)
-                                printf("G  nee c %a %a %a (light %d) shadow %d\n", srec.c.x, srec.c.y, srec.c.z, li,
-                                       (int)shadow);
-#endif
-                        }
-                    }
-#ifdef PT_DEBUG_KEY
-                    if (key == PT_DEBUG_KEY)
-                        printf("G  scatter d %a %a %a f %a %a %a pdf %a prev %a\n", b.d.x, b.d.y, b.d.z, b.f.x, b.f.y,
-                               b.f.z, b.pdf, prev);
-#endif
-                    att = att * ((b.f * fabsf(dot(si.ns, b.d))) / b.pdf);
-                    const float urr = INTEGRATOR == PT_INTEGRATOR_PATH ? r[6] : r[3];
-                    if (rr++ > 3) {
-                        float qq = fminf(0.95f, fmaxf(fmaxf(att.x, att.y), att.z));
-                        if (urr >= qq) alive = false;
-                        else att = att / qq;
-                    }
-                    ro = b.o;
-                    rd = b.d;
-                }
-            }
-        }
-        // loop test `depth++ < maxDepth && sum(att) > 0` (Integrators.cpp:138, 193)
-        if (alive && depth < R.max_depth && (att.x + att.y + att.z) > 0.0f) {
-            depth++;
-            cont = true;
-        } else {
-            done = true;
-        }
-        flags = depth | (rr << PF_RR_SHIFT) | (spec ? PF_SPEC : 0u);
+        shade_bounce<INTEGRATOR>(R, h, __float_as_uint(d4.w), ro, rd, att, out, prev, key, dim, flags, cont, done,
+                                 shadow, srec);
     }
     // a finished path stores its sample's radiance (the pending NEE ray, if
     // any, adds to it later) and its entry takes the next camera sample
@@ -895,6 +908,63 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
     if (shadow) {
         srec.d.w = __uint_as_float(cont ? a : (SHADOW_DONE_BIT | sid));
         sq[c] = srec;
+    }
+}
+
+// The wavefront's tail (Path / SimplePath, fixed SPP): once every camera
+// sample of the chunk has started and few paths remain, one launch finishes
+// them, each lane looping over its own path's bounces -- the closest hit
+// (trace_closest over the reference's clusters, its own order and ties), the
+// bounce (shade_bounce, as k_shade), the NEE ray (trace_any) and its
+// contribution fma(c, att, out) right after the bounce that drew it, as
+// k_shadow_pool adds it.  A wavefront iteration per bounce would cost a
+// handful of launches and a bounce-wide wait for the slowest ray each (C4:
+// the last ~127 bounces took ~97 ms of a 6.2 s frame).
+template <int INTEGRATOR, bool INST, bool COUNT>
+__global__ __launch_bounds__(PT_TRACE_BLOCK) void k_tail(RenderParams R, PathSoA cur,
+                                                         const uint32_t* __restrict__ nptr,
+                                                         float* __restrict__ sample_L,
+                                                         unsigned long long* counters) {
+    __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
+    const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
+    TraceWork wc{0, 0}, wa{0, 0};
+    uint64_t n_cl = 0, n_any = 0;
+    for (uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x; i < n; i += gridDim.x * PT_TRACE_BLOCK) {
+        const uint32_t e = path_slot(i, front, cur.cap);
+        const float4 o4 = cur.o[e], d4 = cur.d[e], b4 = cur.beta[e], L4 = cur.L[e];
+        const uint32_t sid = cur.sid[e];
+        f3 ro = xyz(o4), rd = xyz(d4), att = xyz(b4), out = xyz(L4);
+        float prev = b4.w;
+        const uint32_t key = __float_as_uint(o4.w);
+        uint32_t dim = __float_as_uint(L4.w), flags = __float_as_uint(d4.w);
+        for (;;) {
+            float t = 0, b1 = 0, b2 = 0;
+            const int prim = trace_closest<COUNT, INST>(ro, rd, __int_as_float(0x7f800000), t, b1, b2, s_ref, wc);
+            ++n_cl;
+            bool cont = false, done = false, shadow = false;
+            ShadowRec srec;
+            shade_bounce<INTEGRATOR>(R, make_float4(t, b1, b2, __int_as_float(prim)), flags, ro, rd, att, out, prev,
+                                     key, dim, flags, cont, done, shadow, srec);
+            if (shadow) {
+                ++n_any;
+                if (!trace_any<COUNT, INST>(xyz(srec.o), xyz(srec.d), srec.o.w, s_ref, wa))
+                    out = F3(fma_(srec.c.x, srec.a.x, out.x), fma_(srec.c.y, srec.a.y, out.y),
+                             fma_(srec.c.z, srec.a.z, out.z));
+            }
+            if (!cont) break;
+        }
+        float* o = sample_L + 3ull * sid;
+        o[0] = out.x;
+        o[1] = out.y;
+        o[2] = out.z;
+    }
+    count_add(counters, CNT_TAIL_CLOSEST, n_cl);
+    count_add(counters, CNT_TAIL_ANY, n_any);
+    if (COUNT) {
+        count_add(counters, CNT_NODES_CLOSEST, wc.nodes);
+        count_add(counters, CNT_TRIS_CLOSEST, wc.tris);
+        count_add(counters, CNT_NODES_ANY, wa.nodes);
+        count_add(counters, CNT_TRIS_ANY, wa.tris);
     }
 }
 
@@ -1781,6 +1851,13 @@ __global__ __launch_bounds__(256) void k_adapt_decide(const uint32_t* __restrict
                                                      uint32_t*, uint32_t*, unsigned long long*, uint32_t*);          \
     template __global__ void k_shadow_pool<B, I, Q>(PathSoA, float*, ShadowRec*, const uint32_t*, uint32_t*,   \
                                                     uint32_t*, unsigned long long*);
+#define PT_INST_TAIL(G, I, C)                                                                              \
+    template __global__ void k_tail<G, I, C>(RenderParams, PathSoA, const uint32_t*, float*, unsigned long long*);
+PT_INST_TAIL(PT_INTEGRATOR_PATH, false, false)
+PT_INST_TAIL(PT_INTEGRATOR_PATH, false, true)
+PT_INST_TAIL(PT_INTEGRATOR_SIMPLE, false, false)
+PT_INST_TAIL(PT_INTEGRATOR_SIMPLE, false, true)
+#undef PT_INST_TAIL
 template __global__ void k_closest_ties<false>(PathSoA, const uint32_t*, float4*, const uint32_t*, const uint32_t*);
 template __global__ void k_closest_ties<true>(PathSoA, const uint32_t*, float4*, const uint32_t*, const uint32_t*);
 PT_INST_TRACE(false, false)

@@ -28,6 +28,14 @@
 // a chunk find zero paths and return at once)
 #define PT_LAG 4
 #define PT_RING (PT_LAG + 1)
+// The tail (k_tail): at most this many live paths, and at most 1/PT_TAIL_SHARE
+// of the wavefront, once every camera sample of the chunk has started
+#ifndef PT_TAIL_PATHS
+#define PT_TAIL_PATHS 65536u
+#endif
+#ifndef PT_TAIL_SHARE
+#define PT_TAIL_SHARE 16u
+#endif
 // Any-hit rays of bounce k on a second stream, beside bounce k+1's closest-hit
 // rays (the two only read the path state; the shading of k+1 waits for them):
 // each persistent pool kernel's draining tail leaves CUs the other fills.
@@ -93,6 +101,7 @@ struct pt_ctx {
     uint64_t ray_order_cap = 0, ray_counts_cap = 0;
     hipEvent_t ev[8] = {};
     hipEvent_t rev[PT_RING][5] = {};  // per in-flight iteration: kernel boundaries [0..2], end [4] ([3] unused)
+    hipEvent_t tail_ev[2] = {};       // around the tail launch (k_tail)
     uint32_t* stack_drops = nullptr;  // device word: traversal pushes beyond the stack (DevScene::stack_drops)
     // multi-device context (pt_create with n_devices > 1): the other devices'
     // contexts (owned) and, per device, an RCCL communicator for the film reduce
@@ -174,6 +183,12 @@ static pt_status create_dev(pt_ctx** out, int device) {
         c->overlap = ov ? atoi(ov) != 0 : PT_OVERLAP_SHADOW != 0;
     }
     for (hipEvent_t* e = &c->ev[0]; e != &c->ev[0] + 8; ++e)
+        if (hipEventCreate(e) != hipSuccess) {
+            g_err = "event create failed";
+            delete c;
+            return PT_ERR_HIP;
+        }
+    for (hipEvent_t* e : {&c->tail_ev[0], &c->tail_ev[1]})
         if (hipEventCreate(e) != hipSuccess) {
             g_err = "event create failed";
             delete c;
@@ -415,6 +430,8 @@ extern "C" void pt_destroy(pt_ctx* c) {
     if (c->host_cnt) hipHostFree(c->host_cnt);
     if (c->stack_drops) hipFree(c->stack_drops);
     for (auto& e : c->ev)
+        if (e) hipEventDestroy(e);
+    for (auto& e : c->tail_ev)
         if (e) hipEventDestroy(e);
     for (auto& r : c->rev)
         for (auto& e : r)
@@ -1616,10 +1633,20 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             ++read;
             return PT_OK;
         };
+        // the tail (k_tail): once every sample has started and the live paths
+        // have fallen to a small share of the wavefront, one launch finishes them
+        const bool tail_ok = PT_TAIL_PATHS > 0 && !inst && !(rd->flags & PT_RENDER_NO_TAIL) &&
+                             (rd->integrator == PT_INTEGRATOR_PATH || rd->integrator == PT_INTEGRATOR_SIMPLE);
+        const uint32_t tail_max = std::min<uint32_t>(PT_TAIL_PATHS, paths / PT_TAIL_SHARE);
+        bool tail = false;
         while (!drained) {
             if (issued - read >= PT_LAG) {
                 if ((st = consume()) != PT_OK) return st;
                 continue;
+            }
+            if (tail_ok && read > 0 && started >= R.chunk_total && bound <= tail_max) {
+                tail = true;
+                break;
             }
             const uint32_t i = issued;
             const uint32_t nb = std::max(bound, 1u);
@@ -1713,9 +1740,29 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             ++issued;
         }
         // iterations queued past the end find zero paths; let them drain
+        if (tail) {
+            if (ovl && issued) HIPCHK(c, hipStreamWaitEvent(sm, c->rev[(issued - 1) % PT_RING][4], 0));
+            uint32_t* in = set[issued % 3];  // the paths entering the next bounce
+            const dim3 gt(std::max(1u, std::min(c->blocks_closest, (bound + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK)));
+            if (timing) HIPCHK(c, hipEventRecord(c->tail_ev[0], sm));
+            using TailFn = void (*)(RenderParams, PathSoA, const uint32_t*, float*, unsigned long long*);
+            const TailFn kt = rd->integrator == PT_INTEGRATOR_SIMPLE
+                                  ? (count ? k_tail<PT_INTEGRATOR_SIMPLE, false, true> : k_tail<PT_INTEGRATOR_SIMPLE, false, false>)
+                                  : (count ? k_tail<PT_INTEGRATOR_PATH, false, true> : k_tail<PT_INTEGRATOR_PATH, false, false>);
+            hipLaunchKernelGGL(kt, gt, dim3(PT_TRACE_BLOCK), 0, sm, R, cur, (const uint32_t*)in, c->sample_L, c->counters);
+            HIPCHK(c, hipGetLastError());
+            if (timing) HIPCHK(c, hipEventRecord(c->tail_ev[1], sm));
+            if (stats) stats->launches_closest++;
+        }
         while (read < issued)
             if ((st = consume()) != PT_OK) return st;
         if (ovl && issued) HIPCHK(c, hipStreamWaitEvent(sm, c->rev[(issued - 1) % PT_RING][4], 0));
+        if (tail && timing) {  // (the tail is mostly traversal: its time counts as closest-hit time)
+            float a;
+            HIPCHK(c, hipEventSynchronize(c->tail_ev[1]));
+            HIPCHK(c, hipEventElapsedTime(&a, c->tail_ev[0], c->tail_ev[1]));
+            t_cl += a;
+        }
 #if PT_ITER_STATS
         {
             unsigned long long it[2][8];
@@ -1759,6 +1806,9 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         stats->tris_closest += h[CNT_TRIS_CLOSEST];
         stats->nodes_any += h[CNT_NODES_ANY];
         stats->rays_any += h[CNT_EXTRA_ANY];
+        stats->rays_closest += h[CNT_TAIL_CLOSEST];  // the tail's queries (k_tail)
+        stats->shade_hits += h[CNT_TAIL_CLOSEST];
+        stats->rays_any += h[CNT_TAIL_ANY];
         stats->tris_any += h[CNT_TRIS_ANY];
         stats->ms_closest += t_cl;
         stats->ms_shade += t_sh;

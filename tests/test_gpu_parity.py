@@ -256,6 +256,42 @@ def test_gpu_overlapped_any_hit_stream_is_bit_identical(c4_full):
     assert films[0][1:] == films[1][1:]
 
 
+def test_gpu_tail_kernel_is_bit_identical(c4_full):
+    """The last bounces of a fixed-SPP chunk in one launch (k_tail: each lane
+    loops over its path's bounces) against a wavefront iteration per bounce
+    (PT_RENDER_NO_TAIL): the same per-sample Li and film bit for bit, and the
+    same closest-hit / NEE query counts, on the full C4 scene."""
+    setup, integ = c4_full
+    b, e = 192 * 40, 192 * 48
+    Lt = integ.RenderSamples(pixel_begin=b, pixel_end=e)
+    Ln = integ.RenderSamples(pixel_begin=b, pixel_end=e, flags=N.PT_RENDER_NO_TAIL)
+    np.testing.assert_array_equal(Lt, Ln)
+    film = setup.camera.GetFilm()
+    films = []
+    for f in (0, N.PT_RENDER_NO_TAIL):
+        film.Clear()
+        st = integ.Render(flags=f)
+        films.append((film.accum.copy(), st["rays_any"], st["rays_closest"], st["paths"]))
+    np.testing.assert_array_equal(films[0][0], films[1][0])
+    assert films[0][1:] == films[1][1:]
+
+
+@pytest.mark.parametrize("name", ["zoo", "sanmiguel", "cornell_c2", "alpha_maps", "example1"])
+def test_gpu_tail_kernel_matches_the_wavefront_on_parity_scenes(name):
+    """Small scenes reach the tail after a few bounces (a sixteenth of the
+    wavefront left): with and without it, the same Li and query counts."""
+    setup, integ, fx = load(name)
+    Lt = integ.RenderSamples()
+    Ln = integ.RenderSamples(flags=N.PT_RENDER_NO_TAIL)
+    np.testing.assert_array_equal(Lt, Ln)
+    sts = []
+    for f in (0, N.PT_RENDER_NO_TAIL):
+        setup.camera.GetFilm().Clear()
+        st = integ.Render(flags=f)
+        sts.append((st["rays_closest"], st["rays_any"], st["paths"]))
+    assert sts[0] == sts[1]
+
+
 def test_gpu_sanmiguel_full_size_matches_reference_band(c4_full):
     """The full ~10 M-triangle C4 scene against the reference's own per-sample
     Li (tests/golden/c4_band.npz: ref_harness li over pixel rows 40..47 at
