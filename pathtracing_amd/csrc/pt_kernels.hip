@@ -960,6 +960,9 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_tail(RenderParams R, PathSoA
     }
     count_add(counters, CNT_TAIL_CLOSEST, n_cl);
     count_add(counters, CNT_TAIL_ANY, n_any);
+    // the previous bounce's NEE rays: its any-hit kernel traced them, and the
+    // next iteration's snapshot (which the tail replaces) would have counted them
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&counters[CNT_TAIL_ANY], (unsigned long long)nptr[Q_SHADOW]);
     if (COUNT) {
         count_add(counters, CNT_NODES_CLOSEST, wc.nodes);
         count_add(counters, CNT_TRIS_CLOSEST, wc.tris);
