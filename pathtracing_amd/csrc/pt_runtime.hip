@@ -101,7 +101,6 @@ struct pt_ctx {
     uint64_t ray_order_cap = 0, ray_counts_cap = 0;
     hipEvent_t ev[8] = {};
     hipEvent_t rev[PT_RING][5] = {};  // per in-flight iteration: kernel boundaries [0..2], end [4] ([3] unused)
-    hipEvent_t tail_ev[2] = {};       // around the tail launch (k_tail)
     uint32_t* stack_drops = nullptr;  // device word: traversal pushes beyond the stack (DevScene::stack_drops)
     // multi-device context (pt_create with n_devices > 1): the other devices'
     // contexts (owned) and, per device, an RCCL communicator for the film reduce
@@ -183,12 +182,6 @@ static pt_status create_dev(pt_ctx** out, int device) {
         c->overlap = ov ? atoi(ov) != 0 : PT_OVERLAP_SHADOW != 0;
     }
     for (hipEvent_t* e = &c->ev[0]; e != &c->ev[0] + 8; ++e)
-        if (hipEventCreate(e) != hipSuccess) {
-            g_err = "event create failed";
-            delete c;
-            return PT_ERR_HIP;
-        }
-    for (hipEvent_t* e : {&c->tail_ev[0], &c->tail_ev[1]})
         if (hipEventCreate(e) != hipSuccess) {
             g_err = "event create failed";
             delete c;
@@ -430,8 +423,6 @@ extern "C" void pt_destroy(pt_ctx* c) {
     if (c->host_cnt) hipHostFree(c->host_cnt);
     if (c->stack_drops) hipFree(c->stack_drops);
     for (auto& e : c->ev)
-        if (e) hipEventDestroy(e);
-    for (auto& e : c->tail_ev)
         if (e) hipEventDestroy(e);
     for (auto& r : c->rev)
         for (auto& e : r)
@@ -1744,25 +1735,20 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             if (ovl && issued) HIPCHK(c, hipStreamWaitEvent(sm, c->rev[(issued - 1) % PT_RING][4], 0));
             uint32_t* in = set[issued % 3];  // the paths entering the next bounce
             const dim3 gt(std::max(1u, std::min(c->blocks_closest, (bound + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK)));
-            if (timing) HIPCHK(c, hipEventRecord(c->tail_ev[0], sm));
             using TailFn = void (*)(RenderParams, PathSoA, const uint32_t*, float*, unsigned long long*);
             const TailFn kt = rd->integrator == PT_INTEGRATOR_SIMPLE
                                   ? (count ? k_tail<PT_INTEGRATOR_SIMPLE, false, true> : k_tail<PT_INTEGRATOR_SIMPLE, false, false>)
                                   : (count ? k_tail<PT_INTEGRATOR_PATH, false, true> : k_tail<PT_INTEGRATOR_PATH, false, false>);
             hipLaunchKernelGGL(kt, gt, dim3(PT_TRACE_BLOCK), 0, sm, R, cur, (const uint32_t*)in, c->sample_L, c->counters);
             HIPCHK(c, hipGetLastError());
-            if (timing) HIPCHK(c, hipEventRecord(c->tail_ev[1], sm));
-            if (stats) stats->launches_closest++;
+            // its queries join rays_closest / rays_any (CNT_TAIL_*); its time only
+            // the wall clock: the per-kernel times and launch counts stay the
+            // wavefront kernels' own (what the roofline entries divide)
         }
         while (read < issued)
             if ((st = consume()) != PT_OK) return st;
         if (ovl && issued) HIPCHK(c, hipStreamWaitEvent(sm, c->rev[(issued - 1) % PT_RING][4], 0));
-        if (tail && timing) {  // (the tail is mostly traversal: its time counts as closest-hit time)
-            float a;
-            HIPCHK(c, hipEventSynchronize(c->tail_ev[1]));
-            HIPCHK(c, hipEventElapsedTime(&a, c->tail_ev[0], c->tail_ev[1]));
-            t_cl += a;
-        }
+
 #if PT_ITER_STATS
         {
             unsigned long long it[2][8];
