@@ -838,12 +838,12 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
         }
     }
     // loop test `depth++ < maxDepth && sum(att) > 0` (Integrators.cpp:138, 193)
-    if (alive && depth < R.max_depth && (att.x + att.y + att.z) > 0.0f) {
-        depth++;
-        cont = true;
-    } else {
-        done = true;
-    }
+    // (both flags assigned: a store to one of the two through a selected
+    // pointer would keep them in scratch memory)
+    const bool go = alive && depth < R.max_depth && (att.x + att.y + att.z) > 0.0f;
+    depth += go ? 1u : 0u;
+    cont = go;
+    done = !go;
     flags = depth | (rr << PF_RR_SHIFT) | (spec ? PF_SPEC : 0u);
 }
 
