@@ -558,7 +558,7 @@ def main():
         dist.destroy_process_group()
 
 
-def bound_peak(e: dict, large: bool, counted: bool) -> None:
+def bound_peak(e: dict, large: bool, counted: bool, achieved: float = 0.0) -> None:
     """The bound a kernel's counters show and the ceiling its fraction is
     priced against (a hierarchical roofline: the memory level that serves its
     reads).  HBM bytes near the HBM peak: "hbm" (8 TB/s).  Far below it, with
@@ -571,6 +571,11 @@ def bound_peak(e: dict, large: bool, counted: bool) -> None:
     tf, hit = e.get("traffic_frac"), e.get("l2_hit_rate")
     if not large:
         e["bound"], peak = "l2/latency", L2_GATHER_PEAK_GBS
+    elif (not counted or tf is None) and achieved > HBM_PEAK_GBS:
+        # no counters, but more algorithmic bytes than HBM could deliver:
+        # caches serve at least part of them
+        e["bound"], peak = "l2-latency (no counter profile of this build; algorithmic bytes above the HBM peak)", \
+            L2_GATHER_PEAK_GBS
     elif not counted or tf is None:
         e["bound"], peak = "unknown (no counter profile of this build)", HBM_PEAK_GBS
     elif tf >= 0.6:
@@ -630,7 +635,7 @@ def roofline(args, setup, world, totals, cst, cpu):
         if traffic:
             e["traffic_achieved"] = round(traffic / (avg_ms * 1e-3) / 1e9, 1)
             e["traffic_frac"] = round(e["traffic_achieved"] / HBM_PEAK_GBS, 4)
-        bound_peak(e, args.config in HBM_CONFIGS, traffic is not None)
+        bound_peak(e, args.config in HBM_CONFIGS, traffic is not None, gbs(bpr))
         peak = e["peak"]
         e["frac"] = round(gbs(bpr) / peak, 4)
         # SURVEY §8(d)'s own fraction: the algorithmic bytes over the HBM peak
@@ -703,7 +708,7 @@ def roofline(args, setup, world, totals, cst, cpu):
                 prof_ms = info.get("profile_avg_launch_ms") or avg_ms
                 sh["traffic_achieved"] = round(traffic / (prof_ms * 1e-3) / 1e9, 1)
                 sh["traffic_frac"] = round(sh["traffic_achieved"] / HBM_PEAK_GBS, 4)
-            bound_peak(sh, True, traffic is not None)
+            bound_peak(sh, True, traffic is not None, ach)
             sh["frac"] = round(ach / sh["peak"], 4)
             sh["hbm_frac"] = round(ach / HBM_PEAK_GBS, 4)
             roof["shade"] = sh
