@@ -129,6 +129,11 @@ __device__ unsigned int pt_diag[4];
 #ifndef PT_DEFER_SETUP
 #define PT_DEFER_SETUP 1
 #endif
+// overlapped traversal: the two pops of an iteration (a leaf into the free leaf
+// cursor, then a node) read the top two stack entries together
+#ifndef PT_POP2
+#define PT_POP2 0
+#endif
 // overlapped traversal: the stack's LDS and overflow parts through separate
 // ds / buffer ops (no flat pops waiting on all vector memory; C4: neutral,
 // 3640 vs 3641 ms per frame)
@@ -367,6 +372,34 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             ref = REF_EMPTY;
         }
         PT_IT(7, __popcll(__ballot(ref == REF_EMPTY && sp > 0)));
+#if PT_POP2
+        // the top two entries read together (one LDS round trip where the
+        // second pop follows a leaf taken by the free leaf cursor)
+        if (ref == REF_EMPTY && sp > 0 && !(leaf != REF_EMPTY && (leaf & REF_BLOCK))) {
+            uint32_t v1, v2 = REF_EMPTY;
+            const bool lds2 = LN >= PT_POOL_STACK || sp <= LN;  // entries sp - 1 and sp - 2 in LDS
+            if (lds2) {
+                v1 = s_ref[(sp - 1) * PT_TRACE_BLOCK + lane];
+                v2 = s_ref[max(sp - 2, 0) * PT_TRACE_BLOCK + lane];  // (unused when sp == 1)
+                --sp;
+            } else {
+                v1 = pop();
+            }
+            if (leaf == REF_EMPTY && is_leaf(v1)) {
+                leaf = v1;
+                if (sp > 0 && !(leaf & REF_BLOCK)) {
+                    if (lds2) {
+                        ref = v2;
+                        --sp;
+                    } else {
+                        ref = pop();
+                    }
+                }
+            } else {
+                ref = v1;
+            }
+        }
+#else
         #pragma unroll
         for (int k = 0; k < 2; k++) {
             if (ref == REF_EMPTY && sp > 0 && !(leaf != REF_EMPTY && (leaf & REF_BLOCK))) {
@@ -375,6 +408,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 else ref = r;
             }
         }
+#endif
         if (ref == REF_EMPTY && leaf == REF_EMPTY) {  // sp == 0: no hit (any) / closest result
             if (ANY) src.any((uint32_t)ri, false);
             else if (!(oct & OCT_FOUND)) src.closest((uint32_t)ri, tmax, 0.0f, 0.0f, -1);
