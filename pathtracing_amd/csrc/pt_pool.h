@@ -132,7 +132,7 @@ __device__ unsigned int pt_diag[4];
 // overlapped traversal: the two pops of an iteration (a leaf into the free leaf
 // cursor, then a node) read the top two stack entries together
 #ifndef PT_POP2
-#define PT_POP2 0
+#define PT_POP2 0  // C4: +0.07 %, noise (profiles/r04_ab_traversal.txt)
 #endif
 // overlapped traversal: the stack's LDS and overflow parts through separate
 // ds / buffer ops (no flat pops waiting on all vector memory; C4: neutral,
