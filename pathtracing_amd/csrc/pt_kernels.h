@@ -158,6 +158,11 @@ enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1, PT_SORT_RAYS = 2 };
 #define PT_SORT_CELL_BITS 4  // spatial sort: 2^bits cells per axis of the scene box
 #endif
 #define PT_SORT_BINS_SPATIAL (1 << (3 * PT_SORT_CELL_BITS))
+// spatial sort key: the hit primitive's slot range (leaf order) instead of
+// the hit point's Morton cell (reads the hit record only)
+#ifndef PT_SORT_BY_SLOT
+#define PT_SORT_BY_SLOT 0  // off: C4 -1.5 % (profiles/r04_ab_traversal.txt)
+#endif
 #ifndef PT_SHADE_BLOCK
 // k_shade threads per block (its appends aggregate per block): C4 64 / 128 /
 // 256 / 512 / 1024 -> 1206 / 1236 / 1270 / 1205 / 1278 Mrays/s

@@ -1572,6 +1572,13 @@ __device__ __forceinline__ uint32_t sort_bin(const PathSoA& cur, uint32_t front,
     const float4 h = hit[i];
     const int prim = __float_as_int(h.w);
     if (prim < 0) return 0u;
+    if (KEY == PT_SORT_SPATIAL && PT_SORT_BY_SLOT) {
+        // the hit primitive's slot: slots are in the BVH's leaf order, so a
+        // range of them is a compact patch of geometry (and of its materials);
+        // only the hit record is read
+        if ((uint32_t)prim >= S.n_prims) return PT_SORT_BINS_SPATIAL - 1u;  // a virtual slot inside an instance
+        return 1u + (uint32_t)(((uint64_t)(uint32_t)prim * (PT_SORT_BINS_SPATIAL - 2u)) / S.n_prims);
+    }
     if (KEY == PT_SORT_MATERIAL) {
         if ((uint32_t)prim >= S.n_prims) return PT_SORT_BINS_MATERIAL - 1u;  // a virtual slot inside an instance
         const int mat = S.info[prim].material;
