@@ -175,11 +175,17 @@ enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1, PT_SORT_RAYS = 2 };
 #define PT_SORT_PER 16u  // paths per thread of k_sort_count / k_sort_scatter
 #endif
 template <int KEY, int NB>
-__global__ void k_sort_count(PathSoA cur, const uint32_t* nptr, const float4* hit, uint32_t* counts);
+__global__ void k_sort_count(PathSoA cur, const uint32_t* nptr, const float4* hit, uint32_t* counts, uint16_t* bins);
 template <int NB>
 __global__ void k_sort_scan(uint32_t* counts);
 template <int KEY, int NB>
-__global__ void k_sort_scatter(PathSoA cur, const uint32_t* nptr, const float4* hit, uint32_t* offsets, uint32_t* order);
+__global__ void k_sort_scatter(PathSoA cur, const uint32_t* nptr, const float4* hit, uint32_t* offsets, uint32_t* order,
+                               const uint16_t* bins);
+// k_sort_count keeps each path's bin for k_sort_scatter (2 B read instead of
+// the 48 B of path and hit records the bin is computed from)
+#ifndef PT_SORT_KEEP_BINS
+#define PT_SORT_KEEP_BINS 1
+#endif
 __global__ void k_adapt_init(RenderParams R, uint32_t shard_index, uint32_t shard_count, uint32_t* list,
                              uint32_t* cnt, AdaptEst* est, uint32_t* counts);
 __global__ void k_adapt_map(const uint32_t* list, const uint32_t* n, int32_t* map);

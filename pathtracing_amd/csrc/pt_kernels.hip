@@ -1601,9 +1601,12 @@ __device__ __forceinline__ uint32_t sort_bin(const PathSoA& cur, uint32_t front,
 // Each block bins PT_SORT_PER paths per thread (PT_SORT_PER x 256
 // consecutive paths), so clearing and folding the block's 4096-bin LDS
 // histogram is paid once per 4096 paths rather than once per 256.
+// bins (PT_SORT_KEEP_BINS, or null): each path's bin, for k_sort_scatter to
+// read (2 B) instead of recomputing it from the path and hit records (48 B)
 template <int KEY, int NB>
 __global__ __launch_bounds__(256) void k_sort_count(PathSoA cur, const uint32_t* __restrict__ nptr,
-                                                   const float4* __restrict__ hit, uint32_t* __restrict__ counts) {
+                                                   const float4* __restrict__ hit, uint32_t* __restrict__ counts,
+                                                   uint16_t* __restrict__ bins) {
     __shared__ uint32_t h[NB];
     const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
     const uint32_t t0 = blockIdx.x * (256u * PT_SORT_PER);
@@ -1613,7 +1616,11 @@ __global__ __launch_bounds__(256) void k_sort_count(PathSoA cur, const uint32_t*
 #pragma unroll 4
     for (uint32_t k = 0; k < PT_SORT_PER; k++) {
         const uint32_t t = t0 + k * 256u + threadIdx.x;
-        if (t < n) atomicAdd(&h[sort_bin<KEY>(cur, front, hit, t)], 1u);
+        if (t < n) {
+            const uint32_t b = sort_bin<KEY>(cur, front, hit, t);
+            atomicAdd(&h[b], 1u);
+            if (bins) bins[t] = (uint16_t)b;
+        }
     }
     __syncthreads();
     for (int b = threadIdx.x; b < NB; b += 256)
@@ -1653,7 +1660,7 @@ __global__ __launch_bounds__(256) void k_sort_scan(uint32_t* __restrict__ counts
 template <int KEY, int NB>
 __global__ __launch_bounds__(256) void k_sort_scatter(PathSoA cur, const uint32_t* __restrict__ nptr,
                                                      const float4* __restrict__ hit, uint32_t* __restrict__ offsets,
-                                                     uint32_t* __restrict__ order) {
+                                                     uint32_t* __restrict__ order, const uint16_t* __restrict__ bins) {
     __shared__ uint32_t h[NB];
     const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
     const uint32_t t0 = blockIdx.x * (256u * PT_SORT_PER);
@@ -1664,7 +1671,7 @@ __global__ __launch_bounds__(256) void k_sort_scatter(PathSoA cur, const uint32_
 #pragma unroll
     for (uint32_t k = 0; k < PT_SORT_PER; k++) {
         const uint32_t t = t0 + k * 256u + threadIdx.x;
-        bin[k] = t < n ? sort_bin<KEY>(cur, front, hit, t) : 0u;
+        bin[k] = t < n ? (bins ? (uint32_t)bins[t] : sort_bin<KEY>(cur, front, hit, t)) : 0u;
         if (t < n) atomicAdd(&h[bin[k]], 1u);
     }
     __syncthreads();
@@ -1678,19 +1685,20 @@ __global__ __launch_bounds__(256) void k_sort_scatter(PathSoA cur, const uint32_
     }
 }
 template __global__ void k_sort_count<PT_SORT_MATERIAL, PT_SORT_BINS_MATERIAL>(PathSoA, const uint32_t*, const float4*,
-                                                                             uint32_t*);
+                                                                             uint32_t*, uint16_t*);
 template __global__ void k_sort_count<PT_SORT_SPATIAL, PT_SORT_BINS_SPATIAL>(PathSoA, const uint32_t*, const float4*,
-                                                                           uint32_t*);
+                                                                           uint32_t*, uint16_t*);
 template __global__ void k_sort_count<PT_SORT_RAYS, PT_SORT_BINS_SPATIAL>(PathSoA, const uint32_t*, const float4*,
-                                                                        uint32_t*);
+                                                                        uint32_t*, uint16_t*);
 template __global__ void k_sort_scatter<PT_SORT_RAYS, PT_SORT_BINS_SPATIAL>(PathSoA, const uint32_t*, const float4*,
-                                                                          uint32_t*, uint32_t*);
+                                                                          uint32_t*, uint32_t*, const uint16_t*);
 template __global__ void k_sort_scan<PT_SORT_BINS_MATERIAL>(uint32_t*);
 template __global__ void k_sort_scan<PT_SORT_BINS_SPATIAL>(uint32_t*);
 template __global__ void k_sort_scatter<PT_SORT_MATERIAL, PT_SORT_BINS_MATERIAL>(PathSoA, const uint32_t*,
-                                                                               const float4*, uint32_t*, uint32_t*);
+                                                                               const float4*, uint32_t*, uint32_t*,
+                                                                               const uint16_t*);
 template __global__ void k_sort_scatter<PT_SORT_SPATIAL, PT_SORT_BINS_SPATIAL>(PathSoA, const uint32_t*, const float4*,
-                                                                             uint32_t*, uint32_t*);
+                                                                             uint32_t*, uint32_t*, const uint16_t*);
 
 // ------------------------------------------------------------------ adaptive sampling
 // TileIntegrator::Render (Integrators.cpp:55-86): each pixel takes rounds of

@@ -96,6 +96,8 @@ struct pt_ctx {
     uint32_t* sort_order = nullptr;
     uint32_t* sort_counts = nullptr;
     uint64_t sort_order_cap = 0, sort_counts_cap = 0;
+    uint16_t* sort_bins = nullptr;  // each path's bin between k_sort_count and k_sort_scatter
+    uint64_t sort_bins_cap = 0;
     uint32_t* ray_order = nullptr;  // PT_RENDER_SORT_RAYS: closest-hit claim order
     uint32_t* ray_counts = nullptr;
     uint64_t ray_order_cap = 0, ray_counts_cap = 0;
@@ -418,7 +420,8 @@ extern "C" void pt_destroy(pt_ctx* c) {
     if (c->sample_L) hipFree(c->sample_L);
     if (c->film) hipFree(c->film);
     for (void* p : {(void*)c->a_est, (void*)c->a_counts, (void*)c->a_map, (void*)c->a_list, (void*)c->a_cnt,
-                    (void*)c->sort_order, (void*)c->sort_counts, (void*)c->ray_order, (void*)c->ray_counts})
+                    (void*)c->sort_order, (void*)c->sort_counts, (void*)c->ray_order, (void*)c->ray_counts,
+                    (void*)c->sort_bins})
         if (p) hipFree(p);
     if (c->host_cnt) hipHostFree(c->host_cnt);
     if (c->stack_drops) hipFree(c->stack_drops);
@@ -1550,6 +1553,11 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         if ((st = ensure(c, &c->sort_order, c->sort_order_cap, paths)) != PT_OK) return st;
         if ((st = ensure(c, &c->sort_counts, c->sort_counts_cap, PT_SORT_BINS_SPATIAL)) != PT_OK) return st;
     }
+    uint16_t* bins = nullptr;  // (shared by the claim-order and hit sorts: each pass pair runs in turn on sm)
+    if (PT_SORT_KEEP_BINS && (sort_mat || sort_sp || sort_rays)) {
+        if ((st = ensure(c, &c->sort_bins, c->sort_bins_cap, paths)) != PT_OK) return st;
+        bins = c->sort_bins;
+    }
     hipStream_t sm = c->stream;
     HIPCHK(c, hipMemsetAsync(c->counters, 0, (CNT_SHARDS + 1) * CNT_COUNT * 8, sm));
     HIPCHK(c, hipMemsetAsync(c->stack_drops, 0, 4, sm));
@@ -1657,10 +1665,10 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                 constexpr int NB = PT_SORT_BINS_SPATIAL;
                 HIPCHK(c, hipMemsetAsync(c->ray_counts, 0, NB * 4, sm));
                 hipLaunchKernelGGL((k_sort_count<PT_SORT_RAYS, NB>), gsort, dim3(256), 0, sm, cur, (const uint32_t*)in,
-                                   (const float4*)c->hit, c->ray_counts);
+                                   (const float4*)c->hit, c->ray_counts, bins);
                 hipLaunchKernelGGL((k_sort_scan<NB>), dim3(1), dim3(256), 0, sm, c->ray_counts);
                 hipLaunchKernelGGL((k_sort_scatter<PT_SORT_RAYS, NB>), gsort, dim3(256), 0, sm, cur, (const uint32_t*)in,
-                                   (const float4*)c->hit, c->ray_counts, c->ray_order);
+                                   (const float4*)c->hit, c->ray_counts, c->ray_order, bins);
             }
             {
                 auto kc = pick_closest(use_pool, qn, inst, count);
@@ -1681,19 +1689,19 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                 constexpr int NB = PT_SORT_BINS_MATERIAL;
                 HIPCHK(c, hipMemsetAsync(c->sort_counts, 0, NB * 4, sm));
                 hipLaunchKernelGGL((k_sort_count<PT_SORT_MATERIAL, NB>), gsort, dim3(256), 0, sm, cur, (const uint32_t*)in,
-                                   (const float4*)c->hit, c->sort_counts);
+                                   (const float4*)c->hit, c->sort_counts, bins);
                 hipLaunchKernelGGL((k_sort_scan<NB>), dim3(1), dim3(256), 0, sm, c->sort_counts);
                 hipLaunchKernelGGL((k_sort_scatter<PT_SORT_MATERIAL, NB>), gsort, dim3(256), 0, sm, cur,
-                                   (const uint32_t*)in, (const float4*)c->hit, c->sort_counts, c->sort_order);
+                                   (const uint32_t*)in, (const float4*)c->hit, c->sort_counts, c->sort_order, bins);
                 R.order = c->sort_order;
             } else if (sort_sp) {  // ... by the hit point's Morton cell
                 constexpr int NB = PT_SORT_BINS_SPATIAL;
                 HIPCHK(c, hipMemsetAsync(c->sort_counts, 0, NB * 4, sm));
                 hipLaunchKernelGGL((k_sort_count<PT_SORT_SPATIAL, NB>), gsort, dim3(256), 0, sm, cur, (const uint32_t*)in,
-                                   (const float4*)c->hit, c->sort_counts);
+                                   (const float4*)c->hit, c->sort_counts, bins);
                 hipLaunchKernelGGL((k_sort_scan<NB>), dim3(1), dim3(256), 0, sm, c->sort_counts);
                 hipLaunchKernelGGL((k_sort_scatter<PT_SORT_SPATIAL, NB>), gsort, dim3(256), 0, sm, cur,
-                                   (const uint32_t*)in, (const float4*)c->hit, c->sort_counts, c->sort_order);
+                                   (const uint32_t*)in, (const float4*)c->hit, c->sort_counts, c->sort_order, bins);
                 R.order = c->sort_order;
             }
             if (rd->integrator == PT_INTEGRATOR_SIMPLE)
