@@ -266,20 +266,25 @@ def _load_hook(path: str):
     return mod
 
 
-def verify_frame(setup, integ, rank: int, world: int, pairs: int, frame_samples, film=None, seed: int = 0x5EED0B0C):
+def verify_frame(setup, integ, rank: int, world: int, pairs: int, frame_samples, film=None, seed: int = 0x5EED0B0C,
+                 sample_range=None):
     """Untimed check of the frame just timed: per-sample Li of
     `pairs` (pixel, sample) pairs read back from the frame's own sample buffer
     (pt_frame_samples) must equal the oracle's Li bit for bit; half the pairs
     take the shard's highest sample indices (the top of the 31-bit sample-id
     range of the frame); and the film (rank 0, after the reduce) must be
     finite with a positive filter weight on every pixel.  The oracle is the
-    checker here, never the thing timed."""
+    checker here, never the thing timed.  sample_range = (first, last): the
+    frame samples the sample buffer still holds (its last chunk,
+    pt_frame_sample_range); the pairs are drawn from those."""
     import numpy as np
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle
     W, H = setup.camera.GetFilm().Resolution()
     spp = setup.spp
     local = list(range(rank, spp, world))
+    if sample_range is not None:
+        local = [s for s in local if sample_range[0] <= s <= sample_range[1]]
     out = {"pairs": 0, "bit_exact": 0}
     if pairs > 0 and local:
         rng = np.random.default_rng(seed + rank)
@@ -480,13 +485,15 @@ def main():
     # ---- untimed: the check of the frame just timed (every rank: its shard)
     verified = None
     if not args.no_verify:
+        srange = None
         if cpu_run:
             fs = (lambda p, s: hook.frame_samples(setup, p, s)) if hasattr(hook, "frame_samples") else None
         else:
             fs = integ.context(device).frame_samples
+            srange = integ.context(device).frame_sample_range()
         sh_i, sh_n = shard if shard else (rank, world)
         verified = verify_frame(setup, integ, sh_i, sh_n, args.verify_pairs if fs else 0, fs,
-                                film if rank == 0 and not shard else None)
+                                film if rank == 0 and not shard else None, sample_range=srange)
         if world > 1:
             ok = torch.tensor([1 if verified["ok"] else 0, verified["pairs"], verified["bit_exact"]],
                               dtype=torch.int64, device=dev)

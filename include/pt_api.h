@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PT_API_VERSION 5
+#define PT_API_VERSION 6
 
 typedef int32_t pt_status;
 #define PT_OK 0
@@ -101,6 +101,13 @@ typedef struct pt_instance {
     float inv[16];
     uint32_t bvh;
     uint32_t virt_base;
+    /* AnimatedPrimitive (Primitive.hpp:52-66, Primitive.cpp:76-96): animated
+     * != 0 translates by motion * t, t = clamp(time - t0, t0, t1) / (t1 - t0),
+     * per ray at the ray's time; transform / inv hold the time-0 translation
+     * (what a camera without a shutter sees) */
+    float motion[3];
+    float time_bounds[2];
+    uint32_t animated;
 } pt_instance;
 
 typedef struct pt_bvh_desc {
@@ -245,6 +252,12 @@ typedef struct pt_camera_desc {
     float defocus_radius, focus_distance, focus_angle;
     int32_t width, height;
     int32_t medium;      /* Camera::GetMedium() (Camera.hpp:41-47), or -1   */
+    /* Camera(..., glm::vec2 shutterBounds) (Camera.hpp:16-19): rays carry
+     * time = mix(shutter[0], shutter[1], u) with the sample's time draw
+     * (Camera.hpp:25); has_shutter 0: time 0 (the other ctors leave the
+     * bounds uninitialised) */
+    float shutter[2];
+    int32_t has_shutter;
 } pt_camera_desc;
 
 /* PathIntegrator / SimplePathIntegrator / VolPathIntegrator (Integrators.hpp:33-67) */
@@ -309,6 +322,7 @@ typedef struct pt_stats {
 /* Rays for the pt_trace test hook (Scene::Intersect / IntersectPred). */
 typedef struct pt_ray {
     float o[3], d[3], tmax;
+    float time;          /* Ray::time (Ray.hpp:30): AnimatedPrimitive's      */
 } pt_ray;
 
 typedef struct pt_hit {
@@ -388,6 +402,10 @@ pt_status pt_render_samples(pt_ctx* ctx, const pt_camera_desc* cam, const pt_ren
  * a sample outside it.  The unfiltered Integrator::Li values (Integrators.cpp:
  * 131-257) of the exact frame bench.py times. */
 pt_status pt_frame_samples(pt_ctx* ctx, const uint32_t* pixels, const uint32_t* samples, uint32_t n, float* out_L);
+/* The frame sample indices pt_frame_samples can serve: this shard's samples
+ * s with first <= s <= last (s % shard_count == shard_index), the frame's last
+ * sample chunk; PT_ERR_STATE when there is no fixed-SPP frame. */
+pt_status pt_frame_sample_range(const pt_ctx* ctx, uint32_t* first, uint32_t* last);
 /* Test hook: rays and hits are host or device pointers (detected). */
 pt_status pt_trace(pt_ctx* ctx, const pt_ray* rays, uint32_t n, int any_hit, pt_hit* hits, pt_stats* stats);
 /* Test hook: closest hit + the SurfaceInteraction the renderer reconstructs

@@ -134,6 +134,8 @@ PT_MEMBER(CamHH, Camera, float, halfHeight);
 PT_MEMBER(CamDefocus, Camera, float, defocusRadius);
 PT_MEMBER(CamFocusDist, Camera, float, FocusDistance);
 PT_MEMBER(CamFocusAngle, Camera, float, FocusAngle);
+PT_MEMBER(CamShutterStart, Camera, float, shutterStart);
+PT_MEMBER(CamShutterEnd, Camera, float, shutterEnd);
 PT_MEMBER(FilmFilter, Film, std::shared_ptr<Filter>, filter);
 PT_MEMBER(MitB, MitchellFilter, double, b);
 PT_MEMBER(MitC, MitchellFilter, double, c);
@@ -404,6 +406,9 @@ struct Flat {
         struct Inst {
             uint32_t blas;
             glm::mat4 xf, inv;
+            bool animated = false;  // AnimatedPrimitive: translated per ray at its time
+            glm::vec3 dir{0};
+            glm::vec2 tb{0};
         };
         std::vector<Inst> inst;
         std::vector<uint32_t> blas_of_slot(n_top, UINT32_MAX), inst_of_slot(n_top, UINT32_MAX);
@@ -415,18 +420,23 @@ struct Flat {
             if (dynamic_cast<const GeometricPrimitive*>(p)) continue;
             const Primitive* inner = nullptr;
             glm::mat4 xf, inv;
+            Inst anim{};
             if (auto* tp = dynamic_cast<const TransformedPrimitive*>(p)) {
                 inner = PT_GET(*tp, TpPrim).get();
                 xf = PT_GET(*tp, TpXf);
                 inv = PT_GET(*tp, TpInv);
             } else if (auto* ap = dynamic_cast<const AnimatedPrimitive*>(p)) {
-                // AnimatedPrimitive::Intersect (Primitive.cpp:86-89) at the
-                // rays' time 0 (the shutter is not sampled)
+                // AnimatedPrimitive::Intersect (Primitive.cpp:86-89): the
+                // device translates by dir * t at each ray's time; the time-0
+                // matrix keys its AnimatedLights below
                 inner = PT_GET(*ap, ApPrim).get();
                 const glm::vec2 tb = PT_GET(*ap, ApTb);
                 const float t = glm::clamp(0.0f - tb.x, tb.x, tb.y) / (tb.y - tb.x);
                 xf = glm::translate(glm::mat4(1), PT_GET(*ap, ApDir) * t);
                 inv = glm::inverse(xf);
+                anim.animated = true;
+                anim.dir = PT_GET(*ap, ApDir);
+                anim.tb = tb;
             } else {
                 blas_of_slot[i] = blas_of(p);
                 if (blas_of_slot[i] == UINT32_MAX) throw std::runtime_error("HipPathIntegrator: unsupported TLAS primitive");
@@ -442,7 +452,7 @@ struct Flat {
             const uint32_t b = blas_of(inner);
             if (b == UINT32_MAX) throw std::runtime_error("HipPathIntegrator: unsupported instanced primitive");
             inst_of_slot[i] = (uint32_t)inst.size();
-            inst.push_back(Inst{b, xf, inv});
+            inst.push_back(Inst{b, xf, inv, anim.animated, anim.dir, anim.tb});
         }
         auto blas_count = [&](const Blas& b) -> uint32_t {
             return b.gp ? 1u : (uint32_t)PT_GET(*static_cast<const BLASBase*>(b.b), BlasPrims).size();
@@ -470,6 +480,12 @@ struct Flat {
                 std::memcpy(r.inv, &in.inv[0][0], sizeof(r.inv));
                 r.bvh = 1 + in.blas;
                 r.virt_base = virt;
+                if (in.animated) {
+                    r.animated = 1;
+                    put3(r.motion, in.dir);
+                    r.time_bounds[0] = in.tb.x;
+                    r.time_bounds[1] = in.tb.y;
+                }
                 virt += blas_count(blas[in.blas]);
                 prims[i] = pt_prim{PT_PRIM_INSTANCE, (uint32_t)instances.size(), -1, -1, -1};
                 instances.push_back(r);
@@ -549,7 +565,9 @@ struct Flat {
                 const Light* inner = PT_GET(*t, TlLight).get();
                 area(r, inner, wrapped(inner, PT_GET(*t, TlXf)));
             } else if (auto* an = dynamic_cast<const AnimatedLight*>(l.get())) {
-                // AnimatedLight at the rays' time 0: the AnimatedPrimitive's matrix
+                // AnimatedLight (Light.cpp:338-364): the light of the
+                // AnimatedPrimitive whose time-0 matrix this is; the device
+                // moves it with that instance at each ray's time
                 const Light* inner = PT_GET(*an, AlLight).get();
                 const glm::vec2 tb = PT_GET(*an, AlTb);
                 const float tt = glm::clamp(0.0f - tb.x, tb.x, tb.y) / (tb.y - tb.x);
@@ -667,6 +685,12 @@ pt_camera_desc camera_desc(const Camera& cam, const Flat& flat) {
     c.defocus_radius = PT_GET(cam, CamDefocus);
     c.focus_distance = PT_GET(cam, CamFocusDist);
     c.focus_angle = PT_GET(cam, CamFocusAngle);
+    // rays carry time = glm::mix(shutterStart, shutterEnd, u) (Camera.hpp:25)
+    // for every camera, as the reference's Render does: the bounds of a camera
+    // built without a shutter are whatever its ctor left
+    c.has_shutter = 1;
+    c.shutter[0] = PT_GET(cam, CamShutterStart);
+    c.shutter[1] = PT_GET(cam, CamShutterEnd);
     glm::ivec2 res = cam.GetFilm()->Resolution();
     c.width = res.x;
     c.height = res.y;

@@ -115,8 +115,9 @@ static inline float blend_random(v3 o, v3 d, int prim) { /* the device's draw (p
 }
 
 /* ------------------------------------------------------------------ ray / interaction */
-typedef struct { v3 o, inv, d; } ray_t;
-static inline ray_t mkray(v3 o, v3 d) {
+/* Ray (Ray.hpp:14-41): time is what AnimatedPrimitive / AnimatedLight read */
+typedef struct { v3 o, inv, d; float time; } ray_t;
+static inline ray_t mkray_t(v3 o, v3 d, float time) {
     /* Ray ctor (Ray.hpp:32-35) */
     ray_t r;
     r.o = o;
@@ -124,8 +125,10 @@ static inline ray_t mkray(v3 o, v3 d) {
     r.inv.x = fabsf(d.x) < 1e-32f ? 1e32f : 1.0f / d.x;
     r.inv.y = fabsf(d.y) < 1e-32f ? 1e32f : 1.0f / d.y;
     r.inv.z = fabsf(d.z) < 1e-32f ? 1e32f : 1.0f / d.z;
+    r.time = time;
     return r;
 }
+static inline ray_t mkray(v3 o, v3 d) { return mkray_t(o, d, 0.0f); }
 static inline v3 at(const ray_t* r, float t) { return add(r->o, smul(t, r->d)); }
 
 typedef struct {
@@ -748,10 +751,75 @@ static v3 normalize4(v3 v) {
     const float d = fmaf(v.y, v.y, rmul(v.x, v.x)) + rmul(v.z, v.z); /* fixture search */
     return muls(v, 1.0f / sqrtf(d));
 }
+/* glm::inverse(mat4) (glm/detail/func_matrix.inl compute_inverse<4,4>),
+ * each operation rounded: used on translations only, whose cofactor products
+ * are all exact (one translation component times ones and zeros), so any
+ * contraction of the reference build rounds them alike, zero signs included */
+static void mat4_inverse_(const float* mm, float* out) {
+#define M(c, r) mm[(c) * 4 + (r)]
+#define D2(a, b, c, d) (rmul(a, b) - rmul(c, d))
+    const float C00 = D2(M(2, 2), M(3, 3), M(3, 2), M(2, 3)), C02 = D2(M(1, 2), M(3, 3), M(3, 2), M(1, 3));
+    const float C03 = D2(M(1, 2), M(2, 3), M(2, 2), M(1, 3)), C04 = D2(M(2, 1), M(3, 3), M(3, 1), M(2, 3));
+    const float C06 = D2(M(1, 1), M(3, 3), M(3, 1), M(1, 3)), C07 = D2(M(1, 1), M(2, 3), M(2, 1), M(1, 3));
+    const float C08 = D2(M(2, 1), M(3, 2), M(3, 1), M(2, 2)), C10 = D2(M(1, 1), M(3, 2), M(3, 1), M(1, 2));
+    const float C11 = D2(M(1, 1), M(2, 2), M(2, 1), M(1, 2)), C12 = D2(M(2, 0), M(3, 3), M(3, 0), M(2, 3));
+    const float C14 = D2(M(1, 0), M(3, 3), M(3, 0), M(1, 3)), C15 = D2(M(1, 0), M(2, 3), M(2, 0), M(1, 3));
+    const float C16 = D2(M(2, 0), M(3, 2), M(3, 0), M(2, 2)), C18 = D2(M(1, 0), M(3, 2), M(3, 0), M(1, 2));
+    const float C19 = D2(M(1, 0), M(2, 2), M(2, 0), M(1, 2)), C20 = D2(M(2, 0), M(3, 1), M(3, 0), M(2, 1));
+    const float C22 = D2(M(1, 0), M(3, 1), M(3, 0), M(1, 1)), C23 = D2(M(1, 0), M(2, 1), M(2, 0), M(1, 1));
+    const float F[6][4] = {{C00, C00, C02, C03}, {C04, C04, C06, C07}, {C08, C08, C10, C11},
+                           {C12, C12, C14, C15}, {C16, C16, C18, C19}, {C20, C20, C22, C23}};
+    float Vv[4][4];
+    for (int k = 0; k < 4; k++) {
+        Vv[k][0] = M(1, k);
+        Vv[k][1] = Vv[k][2] = Vv[k][3] = M(0, k);
+    }
+    /* Inv_i = (Va * Fa - Vb * Fb) + Vc * Fc, lane by lane */
+    static const int comb[4][6] = {{1, 0, 2, 1, 3, 2}, {0, 0, 2, 3, 3, 4}, {0, 1, 1, 3, 3, 5}, {0, 2, 1, 4, 2, 5}};
+    float inv[4][4];
+    for (int i = 0; i < 4; i++) {
+        const int* c = comb[i];
+        const float sg = (i & 1) ? -1.0f : 1.0f; /* SignA = (+,-,+,-), SignB = -SignA */
+        for (int k = 0; k < 4; k++) {
+            const float v = (rmul(Vv[c[0]][k], F[c[1]][k]) - rmul(Vv[c[2]][k], F[c[3]][k])) + rmul(Vv[c[4]][k], F[c[5]][k]);
+            inv[i][k] = v * ((k & 1) ? -sg : sg);
+        }
+    }
+    float d0[4];
+    for (int k = 0; k < 4; k++) d0[k] = rmul(M(0, k), inv[k][0]);
+    const float od = 1.0f / ((d0[0] + d0[1]) + (d0[2] + d0[3]));
+    for (int c = 0; c < 4; c++)
+        for (int r = 0; r < 4; r++) out[c * 4 + r] = inv[c][r] * od;
+#undef M
+#undef D2
+}
+
+/* AnimatedPrimitive / AnimatedLight at a ray's time (Primitive.cpp:82-89,
+ * Light.cpp:341-356): TransformedPrimitive / TransformedLight over
+ * glm::translate(mat4(1), dir * t), t = glm::clamp(time - t0, t0, t1) /
+ * (t1 - t0); tmp receives the instance with that transform and its inverse.
+ * A static instance is returned as is. */
+static const pt_instance* inst_at(const pt_instance* I, float time, pt_instance* tmp) {
+    if (!I || !I->animated) return I;
+    *tmp = *I;
+    const float t0 = I->time_bounds[0], t1 = I->time_bounds[1];
+    float x = time - t0;
+    x = t0 > x ? t0 : x; /* glm::max (func_common.inl:29) */
+    x = t1 < x ? t1 : x; /* glm::min (func_common.inl:20) */
+    const float t = x / (t1 - t0);
+    float* T = tmp->transform;
+    for (int k = 0; k < 16; k++) T[k] = (k % 5 == 0) ? 1.0f : 0.0f;
+    /* column 3 = m[0]*v.x + m[1]*v.y + m[2]*v.z + m[3] over the identity:
+     * the products are exact, so v, with a zero made +0 by the final add */
+    for (int k = 0; k < 3; k++) T[12 + k] = rmul(I->motion[k], t) + 0.0f;
+    mat4_inverse_(T, tmp->inv);
+    return tmp;
+}
+
 static ray_t instance_ray(const pt_instance* I, const ray_t* r, float* len) {
     v3 dir = m4_dir(I->inv, r->d);
     *len = length3(dir);
-    return mkray(m4_point(I->inv, r->o), divs(dir, *len));
+    return mkray_t(m4_point(I->inv, r->o), divs(dir, *len), r->time);
 }
 
 /* GeometricPrimitive::Intersect (Primitive.cpp:15-26) / Model::Intersect (Model.hpp:25-27) */
@@ -759,7 +827,8 @@ static int prim_intersect(const scene_t* S, uint32_t slot, const ray_t* r, float
     const pt_prim* p = &S->s->prims[slot];
     if (p->kind == PT_PRIM_BLAS) return bvh_intersect(S, &S->s->bvhs[p->index], r, &max, si, wk);
     if (p->kind == PT_PRIM_INSTANCE) {
-        const pt_instance* I = &S->s->instances[p->index];
+        pt_instance at_time;
+        const pt_instance* I = inst_at(&S->s->instances[p->index], r->time, &at_time);
         const pt_bvh_desc* B = &S->s->bvhs[I->bvh];
         float len;
         ray_t tr = instance_ray(I, r, &len);
@@ -799,7 +868,8 @@ static int prim_pred(const scene_t* S, uint32_t slot, const ray_t* r, float max,
     const pt_prim* p = &S->s->prims[slot];
     if (p->kind == PT_PRIM_BLAS) return bvh_pred(S, &S->s->bvhs[p->index], r, max, wk);
     if (p->kind == PT_PRIM_INSTANCE) { /* TransformedPrimitive::IntersectPred (Primitive.cpp:42-47) */
-        const pt_instance* I = &S->s->instances[p->index];
+        pt_instance at_time;
+        const pt_instance* I = inst_at(&S->s->instances[p->index], r->time, &at_time);
         float len;
         ray_t tr = instance_ray(I, r, &len);
         return bvh_pred(S, &S->s->bvhs[I->bvh], &tr, max * len, wk);
@@ -1346,10 +1416,11 @@ static float texinf_uc(const rng_t* r) {
 
 /* TransformedLight / AnimatedLight (Light.cpp:300-364): the inner
  * AreaLight's shape in the instance's object space */
-static const pt_instance* light_instance(const scene_t* S, const pt_light* l) {
-    return (l->kind == PT_LIGHT_AREA && l->instance >= 0) ? &S->s->instances[l->instance] : NULL;
+static const pt_instance* light_instance(const scene_t* S, const pt_light* l, float time, pt_instance* tmp) {
+    return (l->kind == PT_LIGHT_AREA && l->instance >= 0) ? inst_at(&S->s->instances[l->instance], time, tmp) : NULL;
 }
-static lsample_t light_sample(const scene_t* S, const pt_light* l, float u0, float u1, float uc) {
+/* Light::sample(uv, time) (Light.hpp:21): the time moves an AnimatedLight */
+static lsample_t light_sample(const scene_t* S, const pt_light* l, float u0, float u1, float uc, float time) {
     lsample_t ls;
     memset(&ls, 0, sizeof(ls));
     if (l->kind == PT_LIGHT_TEX_INF) { /* TextureInfiniteLight::sample (Light.cpp:118-144) */
@@ -1374,7 +1445,8 @@ static lsample_t light_sample(const scene_t* S, const pt_light* l, float u0, flo
     }
     if (l->kind == PT_LIGHT_AREA) {
         ls.si = shape_sample(S, &S->s->prims[l->prim], u0, u1);
-        const pt_instance* I = light_instance(S, l);
+        pt_instance at_time;
+        const pt_instance* I = light_instance(S, l, time, &at_time);
         if (I) { /* TransformedLight::sample: p by the transform, n by the normal matrix */
             float NM[9];
             normal_matrix(I->transform, NM);
@@ -1420,7 +1492,8 @@ static inline int light_is_delta(const pt_light* l) { return l->kind == PT_LIGHT
 static float light_pdf(const scene_t* S, const pt_light* l, const si_t* si, const ray_t* r) {
     if (l->kind == PT_LIGHT_AREA) {
         const pt_prim* p = &S->s->prims[l->prim];
-        const pt_instance* I = light_instance(S, l);
+        pt_instance at_time;
+        const pt_instance* I = light_instance(S, l, r->time, &at_time);
         if (I) { /* TransformedLight::PDF: point, normal and ray to object space */
             si_t lo = *si;
             lo.p = m4_point(I->inv, si->p);
@@ -1440,7 +1513,8 @@ static float light_pdf(const scene_t* S, const pt_light* l, const si_t* si, cons
 }
 static v3 light_L(const scene_t* S, const pt_light* l, const si_t* si, const ray_t* r) {
     if (l->kind == PT_LIGHT_AREA) {
-        const pt_instance* I = light_instance(S, l);
+        pt_instance at_time;
+        const pt_instance* I = light_instance(S, l, r->time, &at_time);
         if (I) { /* TransformedLight::L: a fresh interaction, n by the normal matrix, uv (0, 0) */
             float NM[9];
             normal_matrix(I->transform, NM);
@@ -1491,7 +1565,7 @@ static v3 sample_ld(const integ_t* I, const ray_t* ray, const si_t* si, float u,
     int li = ls_sample(S, u);
     if (li < 0) return V(0, 0, 0);
     const pt_light* l = &S->s->lights[li];
-    lsample_t ls = light_sample(S, l, uv0, uv1, uc);
+    lsample_t ls = light_sample(S, l, uv0, uv1, uc, ray->time);
     v3 ldir;
     float t;
     if (is_zero(ls.si.n)) {
@@ -1501,7 +1575,7 @@ static v3 sample_ld(const integ_t* I, const ray_t* ray, const si_t* si, float u,
         ldir = sub(ls.si.p, si->p);
         t = length3(ldir) - EPS_SHADOW;
     }
-    ray_t sh = mkray(si->p, normalize(ldir));
+    ray_t sh = mkray_t(si->p, normalize(ldir), ray->time);
     float lpdf = l->pmf;
     float dt = dot_yxz(si->ns, sh.d); /* as built: y, x, z order */
     if (lpdf <= 0 || dt * dot(ray->d, si->ns) >= 0) return V(0, 0, 0);
@@ -1598,7 +1672,7 @@ static v3 li_path(const integ_t* I, ray_t ray, rng_t* rng) {
         }
         bxdf_t b = mat_scatter(S, si.mat, &ray, &si, r[4], r[0], r[1]);
         if (!b.ok) return out;
-        ray_t nr = mkray(b.o, b.d);
+        ray_t nr = mkray_t(b.o, b.d, ray.time); /* scatter: Ray(..., incoming.time) */
         spec = (b.flags & FL_SPEC) != 0;
         if (!spec) {
             v3 ld = sample_ld(I, &ray, &si, r[5], r[2], r[3], texinf_uc(rng));
@@ -1646,7 +1720,7 @@ static v3 li_simple(const integ_t* I, ray_t ray, rng_t* rng) {
         }
         bxdf_t b = mat_scatter(S, si.mat, &ray, &si, us, u0, u1);
         if (!b.ok) return out;
-        ray_t nr = mkray(b.o, b.d);
+        ray_t nr = mkray_t(b.o, b.d, ray.time); /* scatter: Ray(..., incoming.time) */
         att = mul(att, divs(muls(b.f, fabsf(dot(si.ns, nr.d))), b.pdf));
         if (rr++ > 3) {
             float q = fminf(0.95f, fmaxf(fmaxf(att.x, att.y), att.z));
@@ -1735,7 +1809,7 @@ static int intersect_tr(const integ_t* I, ray_t ray, int med, float max, v3* Tr)
         }
         if (med >= 0) *Tr = mul(*Tr, medium_tr(&S->s->media[med], si.t));
         if (si.mat >= 0) return 1;
-        ray = mkray(at_f(&ray, si.t), ray.d);
+        ray = mkray_t(at_f(&ray, si.t), ray.d, ray.time); /* Scene.cpp:25 */
         med = get_medium(&si, ray.d);
         max -= si.t;
     }
@@ -1750,7 +1824,7 @@ static v3 sample_ld_vol(const integ_t* I, const ray_t* ray, int ray_med, const s
     int li = ls_sample(S, u);
     if (li < 0) return V(0, 0, 0);
     const pt_light* l = &S->s->lights[li];
-    lsample_t ls = light_sample(S, l, uv0, uv1, uc);
+    lsample_t ls = light_sample(S, l, uv0, uv1, uc, ray->time);
     v3 ldir;
     float t;
     if (is_zero(ls.si.n)) {
@@ -1761,7 +1835,7 @@ static v3 sample_ld_vol(const integ_t* I, const ray_t* ray, int ray_med, const s
         t = length3(ldir) - EPS_SHADOW;
         t -= EPS_SHADOW;
     }
-    ray_t sh = mkray(si->p, normalize(ldir));
+    ray_t sh = mkray_t(si->p, normalize(ldir), ray->time);
     float lpdf = l->pmf;
     if (lpdf <= 0) return V(0, 0, 0);
     v3 f;
@@ -1827,7 +1901,7 @@ static v3 li_volpath(const integ_t* I, ray_t ray, int med, rng_t* rng) {
             out = fma3(att, vl(M->Le), out);
             v3 sc = phase_sample(M->g, ray.d, r[6], r[7]);
             int nm = get_medium(&si, sc);
-            ray = mkray(mp, sc);
+            ray = mkray_t(mp, sc, ray.time); /* Integrators.cpp:314, 361 */
             med = nm;
             spec = 0;
         } else {
@@ -1853,7 +1927,7 @@ static v3 li_volpath(const integ_t* I, ray_t ray, int med, rng_t* rng) {
             }
             bxdf_t b = mat_scatter(S, si.mat, &ray, &si, r[4], r[0], r[1]);
             if (!b.ok) return out;
-            ray_t nr = mkray(b.o, b.d);
+            ray_t nr = mkray_t(b.o, b.d, ray.time); /* scatter: Ray(..., incoming.time) */
             int nm = get_medium(&si, nr.d);
             if (!(b.flags & FL_TRANS) && dot(ray.d, si.ns) <= 0) nm = med;
             spec = (b.flags & FL_SPEC) != 0;
@@ -1877,8 +1951,12 @@ static v3 li_volpath(const integ_t* I, ray_t ray, int med, rng_t* rng) {
 /* Camera::GenerateRay (Camera.hpp:21-35) + camera draws (Integrators.cpp:61-64) */
 static ray_t camera_ray(const pt_camera_desc* c, uint32_t x, uint32_t y, rng_t* rng, double* px, double* py) {
     float ja = next1(rng), jb = next1(rng);
-    (void)next1(rng); /* time */
+    const float tu = next1(rng); /* time */
     float l0 = next1(rng), l1 = next1(rng);
+    /* t = glm::mix(shutterStart, shutterEnd, time) (Camera.hpp:25) as the
+     * reference build contracts it: fma(start, 1 - time, time * end); 0 for
+     * the cameras without a shutter (their bounds are uninitialised, A.14) */
+    const float tm = c->has_shutter ? fmaf(c->shutter[0], 1.0f - tu, rmul(tu, c->shutter[1])) : 0.0f;
     *px = (double)x + (double)ja;
     *py = (double)y + (double)jb;
     float pxf = (float)*px, pyf = (float)*py;
@@ -1888,7 +1966,7 @@ static ray_t camera_ray(const pt_camera_desc* c, uint32_t x, uint32_t y, rng_t* 
     float a = (2.0f * uc - 1.0f) * c->half_width, b = (2.0f * vc - 1.0f) * c->half_height;
     v3 dir = normalize(V(fmaf(b, c->v[0], fmaf(a, c->u[0], -c->w[0])), fmaf(b, c->v[1], fmaf(a, c->u[1], -c->w[1])),
                          fmaf(b, c->v[2], fmaf(a, c->u[2], -c->w[2]))));
-    if (c->focus_distance == 0 || c->focus_angle == 0) return mkray(vl(c->origin), dir);
+    if (c->focus_distance == 0 || c->focus_angle == 0) return mkray_t(vl(c->origin), dir, tm);
     float r = sqrtf(l0);
     float th = 2 * PI_F * l1;
     float lx = r * cosf(th), ly = r * sinf(th);
@@ -1897,7 +1975,7 @@ static ray_t camera_ray(const pt_camera_desc* c, uint32_t x, uint32_t y, rng_t* 
     dir = muls(dir, c->focus_distance);
     /* offset = pLens.x*du + pLens.y*dv with the second product fused (as built) */
     v3 off = V(fmaf(dv.x, ly, du.x * lx), fmaf(dv.y, ly, du.y * lx), fmaf(dv.z, ly, du.z * lx));
-    return mkray(add(off, vl(c->origin)), normalize(sub(dir, off)));
+    return mkray_t(add(off, vl(c->origin)), normalize(sub(dir, off)), tm);
 }
 
 static void scene_init(scene_t* S, const pt_scene_desc* s) {
@@ -1972,7 +2050,7 @@ int oracle_trace(const pt_scene_desc* s, const pt_ray* rays, uint32_t n, int any
     scene_t S;
     scene_init(&S, s);
     for (uint32_t i = 0; i < n; i++) {
-        ray_t r = mkray(vl(rays[i].o), vl(rays[i].d));
+        ray_t r = mkray_t(vl(rays[i].o), vl(rays[i].d), rays[i].time);
         oracle_hit* h = &out[i];
         memset(h, 0, sizeof(*h));
         h->prim = h->material = h->light = -1;
@@ -2324,7 +2402,7 @@ int oracle_lights(const pt_scene_desc* s, const float* in, uint32_t n, float* ou
             memcpy(&h0, &c[0], 4);
             memcpy(&h1, &c[1], 4);
             const float uc = (float)(pcg_hash(pcg_hash(h0 ^ pcg_hash(h1))) >> 8) * (1.0f / 16777216.0f);
-            lsample_t ls = light_sample(&S, l, c[0], c[1], uc);
+            lsample_t ls = light_sample(&S, l, c[0], c[1], uc, 0.0f);
             o[0] = ls.L.x; o[1] = ls.L.y; o[2] = ls.L.z;
             o[3] = ls.si.p.x; o[4] = ls.si.p.y; o[5] = ls.si.p.z;
             o[6] = ls.si.n.x; o[7] = ls.si.n.y; o[8] = ls.si.n.z;

@@ -225,6 +225,8 @@ struct World {
     std::shared_ptr<Medium> sceneMedium, cameraMedium;
     glm::vec3 camFrom{0}, camAt{0, 0, -1};
     float fov = 1.0f, focusAngle = 0, focusDist = 0;
+    bool shutter = false;  // Camera(..., glm::vec2 shutterBounds) (Camera.hpp:16-19)
+    glm::vec2 shutterBounds{0, 0};
     int W = 64, H = 64;
     std::shared_ptr<Filter> filter = std::make_shared<MitchellFilter>();
     std::string integ = "path";
@@ -261,6 +263,8 @@ H_MEMBER(HTexAcc, TextureInfiniteLight, std::vector<float>, accWeights);
 H_MEMBER(HTexTotal, TextureInfiniteLight, double, totalWeight);
 H_MEMBER(HTexPower, TextureInfiniteLight, float, cachedPower);
 H_MEMBER(HSkyPower, FunctionInfiniteLight, float, cachedPower);
+H_MEMBER(HCamShutterStart, Camera, float, shutterStart);
+H_MEMBER(HCamShutterEnd, Camera, float, shutterEnd);
 
 struct PinnedSky : FunctionInfiniteLight {
     float pinned;
@@ -479,6 +483,9 @@ static void read_recipe(World& w, const std::string& path) {
             s >> w.samplerKind;
         } else if (k == "camera") {
             s >> w.camFrom.x >> w.camFrom.y >> w.camFrom.z >> w.camAt.x >> w.camAt.y >> w.camAt.z >> w.fov >> w.W >> w.H >> w.focusAngle >> w.focusDist;
+        } else if (k == "shutter") {
+            s >> w.shutterBounds.x >> w.shutterBounds.y;
+            w.shutter = true;
         } else if (k == "filter") {
             std::string kind; float rx, ry; s >> kind >> rx >> ry;
             if (kind == "mitchell") { double b, c; s >> b >> c; w.filter = std::make_shared<MitchellFilter>(glm::vec2(rx, ry), b, c); }
@@ -494,6 +501,26 @@ static void read_recipe(World& w, const std::string& path) {
         }
     }
 }
+
+// A camera without a shutter leaves Camera::shutterStart/End uninitialised
+// (Camera.hpp:7-14), so its rays' time is garbage: the harness
+// sets it to 0.  A shutter camera's rays carry glm::mix(start, end, u)
+// (Camera.hpp:25) as TileIntegrator::Render's inlined copy of GenerateRay
+// rounds it, fma(start, 1 - u, u * end) (its optimized GIMPLE,
+// tools/refgimple.py): this TU's own inlined copy contracts the other way
+// round, so the loops below that stand in for Render's camera draws
+// (Integrators.cpp:61-64) set the time Render would give the ray.  Inside
+// Render itself (Recording / StatRec) the ray comes from Render: kept.
+static bool g_shutter = false;
+static glm::vec2 g_shutter_bounds{0, 0};
+__attribute__((optimize("fp-contract=off"))) static float render_time(float u) {
+    const float e = u * g_shutter_bounds.y;  // rounded: the FMA takes start * (1 - u)
+    return std::fma(g_shutter_bounds.x, 1.0f - u, e);
+}
+static inline void fix_time(Ray& ray) {
+    if (!g_shutter) ray.time = 0;
+}
+static inline void fix_time(Ray& ray, float u) { ray.time = g_shutter ? render_time(u) : 0.0f; }
 
 static void build_world(World& w, bool counting = false) {
     w.scene = std::make_shared<Scene>();
@@ -513,11 +540,22 @@ static void build_world(World& w, bool counting = false) {
     for (auto& l : w.extra) w.ls->Add(l);
     w.ls->PreProcess(w.scene->BoundingBox());
     w.film = std::make_shared<Film>(glm::ivec2{w.W, w.H}, w.filter);
-    if (w.focusAngle != 0 && w.focusDist != 0)
+    if (w.shutter)
+        w.camera = std::make_shared<Camera>(w.camFrom, w.camAt, w.fov, w.film, w.shutterBounds);
+    else if (w.focusAngle != 0 && w.focusDist != 0)
         w.camera = std::make_shared<Camera>(w.camFrom, w.camAt, w.fov, w.film, w.focusAngle, w.focusDist);
     else
         w.camera = std::make_shared<Camera>(w.camFrom, w.camAt, w.fov, w.film);
     if (w.cameraMedium) w.camera->SetMedium(w.cameraMedium);
+    if (!w.shutter) {
+        // the other ctors leave the bounds uninitialised (Camera.hpp:7-14,
+        // SURVEY A.14); the harness defines them as 0, which is the time its
+        // loops and the drop-in (which reads them, as Render does) then use
+        (*w.camera).*get(HCamShutterStart{}) = 0.0f;
+        (*w.camera).*get(HCamShutterEnd{}) = 0.0f;
+    }
+    g_shutter = w.shutter;
+    g_shutter_bounds = w.shutterBounds;
 }
 
 static std::shared_ptr<Integrator> make_integrator(World& w, std::shared_ptr<Sampler> s) {
@@ -614,9 +652,11 @@ static void cmd_info(World& w, const std::string& out) {
 }
 
 // --- trace: rays file f32 [n][7] (o.xyz, d.xyz, tmax) -> closest-hit + any-hit
-static void cmd_trace(World& w, const std::string& out, const std::string& raysPath) {
+// timesPath (optional): one Ray::time per ray (a shutter scene's rays)
+static void cmd_trace(World& w, const std::string& out, const std::string& raysPath, const std::string& timesPath = "") {
     auto raw = rd<float>(raysPath);
     size_t n = raw.size() / 7;
+    std::vector<float> times = timesPath.empty() ? std::vector<float>(n, 0.0f) : rd<float>(timesPath);
     std::vector<float> rec(n * 16, 0.0f);
     std::vector<int32_t> ids(n * 3, -1);
     std::vector<uint8_t> anyhit(n, 0);
@@ -627,7 +667,7 @@ static void cmd_trace(World& w, const std::string& out, const std::string& raysP
     }
     for (size_t i = 0; i < n; i++) {
         const float* r = &raw[i * 7];
-        Ray ray(glm::vec3(r[0], r[1], r[2]), glm::vec3(r[3], r[4], r[5]));
+        Ray ray(glm::vec3(r[0], r[1], r[2]), glm::vec3(r[3], r[4], r[5]), times[i]);
         SurfaceInteraction si;
         bool hit = w.scene->Intersect(ray, si, r[6]);
         float* o = &rec[i * 16];
@@ -668,7 +708,7 @@ static std::vector<SampleRec> run_li(World& w, int x0, int y0, int x1, int y1, u
                 float time = (float)sampler->get1D();
                 glm::dvec2 lens = sampler->get2D();
                 Ray ray = w.camera->GenerateRay(p, time, lens);
-                ray.time = 0;  // shutter is uninitialised in the reference
+                fix_time(ray, time);
                 glm::vec3 L = integ->Li(ray);
                 out.push_back({p.x, p.y, {L.x, L.y, L.z}, sampler->dims()});
             }
@@ -830,7 +870,7 @@ static void cmd_time(World& w, int threads, unsigned spp, const std::string& mod
                                 glm::dvec2 p = glm::dvec2{x, y} + sampler->getPixel2D();
                                 float time = (float)sampler->get1D();
                                 Ray ray = w.camera->GenerateRay(p, time, sampler->get2D());
-                                ray.time = 0;
+                                fix_time(ray, time);
                                 volatile glm::vec3 L = integ->Li(ray);
                                 (void)L;
                             }
@@ -857,7 +897,7 @@ template <class Base>
 struct Recording : Base {
     using Base::Base;
     glm::vec3 Li(Ray ray) const override {
-        ray.time = 0;  // shutter is uninitialised in the reference
+        fix_time(ray);
         glm::vec3 L = Base::Li(ray);
         g_adapt.push_back({g_stream->pixel(), g_stream->sample(), {L.x, L.y, L.z}});
         return L;
@@ -925,7 +965,7 @@ template <class Base>
 struct StatRec : Base {
     using Base::Base;
     glm::vec3 Li(Ray ray) const override {
-        ray.time = 0;
+        fix_time(ray);
         glm::vec3 L = Base::Li(ray);
         PixStat& s = g_stat[t_pixel];  // a pixel is rendered by one thread
         s.n += 1;
@@ -1049,13 +1089,23 @@ int main(int argc, char** argv) {
         return 0;
     }
     std::cout.setstate(std::ios::failbit);  // silence the reference's progress/log prints
+    // The reference runs inside TileIntegrator::Render's worker threads
+    // (Integrators.cpp:25-118), where libstdc++'s __libc_single_threaded is
+    // false.  GCC compiles some reference functions into two copies keyed on
+    // that flag (shared_ptr's atomic vs plain refcount), and folds their
+    // arithmetic differently: AnimatedLight's inlined TransformedLight ctor
+    // builds its normal matrix (Light.cpp:338-356) with +0 entries on the
+    // threaded path and constant-folded -0 entries on the single-threaded one.
+    // One thread started and joined makes this process take Render's path
+    // (glibc never sets the flag back).
+    std::thread([] {}).join();
     World w;
     read_recipe(w, argv[1]);
     std::string cmd = argv[2], out = argv[3];
     build_world(w, cmd == "time");
     if (cmd == "bvh") cmd_bvh(w, out);
     else if (cmd == "info") cmd_info(w, out);
-    else if (cmd == "trace") cmd_trace(w, out, argv[4]);
+    else if (cmd == "trace") cmd_trace(w, out, argv[4], argc > 5 ? argv[5] : "");
     else if (cmd == "li") {
         int x0 = 0, y0 = 0, x1 = w.W, y1 = w.H;
         unsigned spp = w.spp;

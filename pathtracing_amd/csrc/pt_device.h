@@ -169,6 +169,11 @@ struct DevInstance {
     uint32_t prim_base;    // first slot of the BLAS
     uint32_t n_prims;
     uint32_t virt_base;    // virtual slot of the BLAS's first primitive
+    // AnimatedPrimitive (Primitive.cpp:76-96): anim != 0 translates by mdir * t
+    // at each ray's time (pt_shading.h anim_transform); T / inv: time 0
+    float mdir[3];
+    float t0, t1;
+    uint32_t anim;
 };
 
 // ---- per-triangle shading record (128 B, one cache line): the three
@@ -240,6 +245,11 @@ struct DevScene {
     int32_t scene_medium;
     const DevInstance* instances;
     uint32_t n_instances;
+    // motion blur (a shutter camera's frame over a scene with an
+    // AnimatedPrimitive): rays carry a time (PathSoA::time, sq_time[shadow
+    // record]) and animated instances are rebuilt at it; else 0 / null
+    uint32_t motion;
+    float* sq_time;
     uint32_t* scratch;       // SCR_WORDS x scratch_lanes (instance traversal state)
     uint32_t scratch_lanes;
     uint32_t* stack_drops;   // traversal pushes past the stack capacity (counted, rare)

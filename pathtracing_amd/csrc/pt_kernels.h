@@ -53,6 +53,8 @@ struct PathSoA {
     float4* L;    // radiance so far .xyz, next draw dimension (bits)
     uint32_t* sid;// sample id within the chunk
     uint32_t cap; // entries
+    float* time;  // the path's ray time (Ray::time, constant along a path: every
+                  // scatter copies it, Material.hpp:264 ...); only with S.motion
 };
 __device__ __forceinline__ uint32_t path_count(const uint32_t* set) { return set[Q_NEXT] + set[Q_NEW]; }
 __device__ __forceinline__ uint32_t path_slot(uint32_t i, uint32_t c, uint32_t cap) {
@@ -200,4 +202,5 @@ __global__ void k_light_picks(const float* u, uint32_t n, int32_t* out);
 template <bool QN>
 __global__ void k_trace_rays(const pt_ray* rays, uint32_t n, int any, pt_hit* out, uint32_t* pool, uint32_t* ovf,
                              unsigned long long* counters, uint32_t* ties, uint32_t* n_ties);
-__global__ void k_trace_rays_ties(const pt_ray* rays, pt_hit* out, const uint32_t* ties, const uint32_t* n_ties);
+__global__ void k_trace_rays_ties(const pt_ray* rays, pt_hit* out, const uint32_t* ties, const uint32_t* n_ties,
+                                  uint32_t n_rays);

@@ -86,20 +86,53 @@ __device__ __forceinline__ void iteration_prologue(const uint32_t* __restrict__ 
 // Primitive.cpp:48-64): the object-space ray is rebuilt, the primitive test
 // re-run for t (the traversal kept the world t) and the object-space
 // interaction carried back with the transform and its normal matrix.
+// AnimatedPrimitive hits (S.motion): the ray to object space and the
+// interaction back at the ray's time, out of line (the rare path keeps
+// k_shade's registers) with values in and out
+struct ObjRay {
+    f3 o, d;
+    float len;
+};
+__device__ __noinline__ ObjRay anim_object_ray(const DevInstance* I, float time, f3 ro, f3 rd) {
+    float T[16], inv[16];
+    anim_transform(*I, time, T);
+    m4_inverse(T, inv);
+    const f3 dir = m4_dir(inv, rd);
+    const float len = length(dir);
+    return ObjRay{m4_point(inv, ro), dir / len, len};
+}
+struct SurfXf {
+    f3 p, n, ns, tangent;
+};
+__device__ __noinline__ SurfXf anim_world_surface(const DevInstance* I, float time, f3 p, f3 n, f3 ns, f3 tangent) {
+    float T[16], NM[9];
+    anim_transform(*I, time, T);
+    normal_matrix(T, NM);
+    return SurfXf{m4_point(T, p), normalize(m3_mul(NM, n)), normalize(m3_mul(NM, ns)), normalize4(m4_dir(T, tangent))};
+}
 __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, float b1, float b2, SurfInt& si,
-                                         int& medium) {
+                                         int& medium, float time = 0.0f) {
     float len = 1.0f;
     const DevInstance* I = nullptr;
+    bool anim = false;
     if ((uint32_t)prim >= S.n_prims) {
         for (uint32_t k = 0; k < S.n_instances; k++) {
             const DevInstance& c = S.instances[k];
             if ((uint32_t)prim >= c.virt_base && (uint32_t)prim < c.virt_base + c.n_prims) I = &c;
         }
         prim = (int)(I->prim_base + ((uint32_t)prim - I->virt_base));
-        const f3 dir = m4_dir(I->inv, rd);
-        len = length(dir);
-        ro = m4_point(I->inv, ro);
-        rd = dir / len;
+        anim = S.motion && I->anim;
+        if (anim) {  // AnimatedPrimitive::Intersect at the ray's time (Primitive.cpp:86-89)
+            const ObjRay r = anim_object_ray(I, time, ro, rd);
+            ro = r.o;
+            rd = r.d;
+            len = r.len;
+        } else {
+            const f3 dir = m4_dir(I->inv, rd);
+            len = length(dir);
+            ro = m4_point(I->inv, ro);
+            rd = dir / len;
+        }
     }
     const DevGeom g = S.geom[prim];
     const DevPrimInfo pi = S.info[prim];
@@ -121,7 +154,14 @@ __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, flo
     si.mat = pi.material;
     si.light = pi.light;
     medium = pi.medium;
-    if (I) {
+    if (anim) {
+        const SurfXf w = anim_world_surface(I, time, si.p, si.n, si.ns, si.tangent);
+        si.p = w.p;
+        si.n = w.n;
+        si.ns = w.ns;
+        si.t = si.t / len;
+        si.tangent = w.tangent;
+    } else if (I) {
         float NM[9];
         normal_matrix(I->T, NM);
         si.p = m4_point(I->T, si.p);
@@ -182,8 +222,16 @@ struct ClosestSrc {
     __device__ __forceinline__ void closest(uint32_t i, float t, float b1, float b2, int prim) {
         hit[S.ray_order ? S.ray_order[i] : i] = make_float4(t, b1, b2, __int_as_float(prim));
     }
+    __device__ __forceinline__ float time(uint32_t i) const {
+        return P.time[path_slot(S.ray_order ? S.ray_order[i] : i, front, P.cap)];
+    }
     __device__ __forceinline__ void any(uint32_t, bool) {}
-    __device__ __forceinline__ void tie(uint32_t i) { ties[atomicAdd(n_ties, 1u)] = i; }
+    // the list holds P.cap entries (a ray is listed at most once per launch:
+    // OCT_TIE survives instance enter / exit); the bound keeps a miscount in bounds
+    __device__ __forceinline__ void tie(uint32_t i) {
+        const uint32_t k = atomicAdd(n_ties, 1u);
+        if (k < P.cap) ties[k] = i;
+    }
 };
 
 template <bool COUNT, bool INST, bool QN>
@@ -217,7 +265,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest_ties(PathSoA P, cons
                                                                 const uint32_t* __restrict__ pool,
                                                                 const uint32_t* __restrict__ ties) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
-    const uint32_t n = pool[Q_TIES - Q_WORDS];
+    const uint32_t n = min(pool[Q_TIES - Q_WORDS], P.cap);
     if (n == 0) return;
     ClosestSrc src{P, hit, nptr[Q_NEXT], nullptr, nullptr};
     TraceWork wk{0, 0};
@@ -226,7 +274,8 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_closest_ties(PathSoA P, cons
         f3 o, d;
         float tmax, t, b1, b2;
         src.load(i, o, d, tmax);
-        const int prim = trace_closest<false, INST, PT_STACK>(o, d, tmax, t, b1, b2, s_ref, wk);
+        const int prim = trace_closest<false, INST, PT_STACK>(o, d, tmax, t, b1, b2, s_ref, wk, nullptr,
+                                                              (INST && S.motion) ? src.time(i) : 0.0f);
         src.closest(i, t, b1, b2, prim);
     }
 }
@@ -269,6 +318,7 @@ struct ShadowSrcT {
     }
     __device__ __forceinline__ void closest(uint32_t, float, float, float, int) {}
     __device__ __forceinline__ void tie(uint32_t) {}
+    __device__ __forceinline__ float time(uint32_t i) const { return S.sq_time[i]; }
     __device__ __forceinline__ void any(uint32_t i, bool hit) {
         if (hit) return;
         if (DEFER) {
@@ -360,7 +410,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SIMPLE_WAVES void k_closest(Path
         const float4 o = P.o[e], d = P.d[e];
         float t, b1, b2;
         int prim = trace_closest<COUNT, INST, PT_SIMPLE_LN>(xyz(o), xyz(d), __int_as_float(0x7f800000), t, b1, b2,
-                                                            s_ref, wk, ovf);
+                                                            s_ref, wk, ovf, (INST && S.motion) ? P.time[e] : 0.0f);
         hit[i] = make_float4(t, b1, b2, __int_as_float(prim));
     }
 #endif
@@ -387,7 +437,8 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SIMPLE_WAVES void k_shadow(PathS
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     if (i < n) {
         const ShadowRec r = sq[i];
-        src.any(i, trace_any<COUNT, INST, PT_SIMPLE_LN>(xyz(r.o), xyz(r.d), r.o.w, s_ref, wk, ovf));
+        src.any(i, trace_any<COUNT, INST, PT_SIMPLE_LN>(xyz(r.o), xyz(r.d), r.o.w, s_ref, wk, ovf,
+                                                        (INST && S.motion) ? S.sq_time[i] : 0.0f));
     }
 #endif
     if (COUNT) {
@@ -402,6 +453,7 @@ struct RaysSrc {
     pt_hit* out;
     uint32_t* ties;  // exact-t ties (pt_pool.h), re-traced by k_trace_rays_ties
     uint32_t* n_ties;
+    uint32_t n;      // rays, and entries of the tie list
     __device__ __forceinline__ bool load(uint32_t i, f3& o, f3& d, float& tmax) {
         const pt_ray r = rays[i];
         o = F3(r.o[0], r.o[1], r.o[2]);
@@ -413,7 +465,11 @@ struct RaysSrc {
         out[i] = pt_hit{t, b1, b2, prim};
     }
     __device__ __forceinline__ void any(uint32_t i, bool hit) { out[i] = pt_hit{0, 0, 0, hit ? 1 : 0}; }
-    __device__ __forceinline__ void tie(uint32_t i) { ties[atomicAdd(n_ties, 1u)] = i; }
+    __device__ __forceinline__ float time(uint32_t i) const { return rays[i].time; }
+    __device__ __forceinline__ void tie(uint32_t i) {
+        const uint32_t k = atomicAdd(n_ties, 1u);
+        if (k < n) ties[k] = i;
+    }
 };
 
 template <bool QN>
@@ -426,7 +482,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(const pt_ray* __r
     __shared__ __attribute__((aligned(16))) uint8_t s_lut[(QN && PT_Q48) ? 8 * Q48_LUT_STRIDE : 4];
     if constexpr (QN && PT_Q48) stage_q48_lut(s_lut);
     TraceWork wk{0, 0};
-    RaysSrc src{rays, out, ties, n_ties};
+    RaysSrc src{rays, out, ties, n_ties, n};
     if (any) trace_pool<true, true, RaysSrc, true, true, PT_POOL_LDS, QN>(n, pool, src, s_ref, nullptr, ovf, wk, s_lut);
     else trace_pool<false, true, RaysSrc, true, true, PT_POOL_LDS_C, QN>(n, pool, src, s_ref, s_ent, ovf, wk, s_lut);
     count_add(counters, any ? CNT_NODES_ANY : CNT_NODES_CLOSEST, wk.nodes);
@@ -437,15 +493,16 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(const pt_ray* __r
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays_ties(const pt_ray* __restrict__ rays,
                                                                    pt_hit* __restrict__ out,
                                                                    const uint32_t* __restrict__ ties,
-                                                                   const uint32_t* __restrict__ n_ties) {
+                                                                   const uint32_t* __restrict__ n_ties,
+                                                                   uint32_t n_rays) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
-    const uint32_t n = *n_ties;
+    const uint32_t n = min(*n_ties, n_rays);
     TraceWork wk{0, 0};
     for (uint32_t k = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x; k < n; k += gridDim.x * PT_TRACE_BLOCK) {
         const pt_ray r = rays[ties[k]];
         float t, b1, b2;
         const int prim = trace_closest<false, true, PT_STACK>(F3(r.o[0], r.o[1], r.o[2]), F3(r.d[0], r.d[1], r.d[2]),
-                                                             r.tmax, t, b1, b2, s_ref, wk);
+                                                             r.tmax, t, b1, b2, s_ref, wk, nullptr, r.time);
         out[ties[k]] = pt_hit{t, b1, b2, prim};
     }
 }
@@ -463,13 +520,13 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_interact(const pt_ray* __res
     const pt_ray r = rays[i];
     f3 o = F3(r.o[0], r.o[1], r.o[2]), d = F3(r.d[0], r.d[1], r.d[2]);
     float t, b1, b2;
-    const int prim = trace_closest<false>(o, d, r.tmax, t, b1, b2, s_ref, wk);
+    const int prim = trace_closest<false>(o, d, r.tmax, t, b1, b2, s_ref, wk, nullptr, r.time);
     float* w = out + 16ull * i;
     for (int k = 0; k < 16; k++) w[k] = 0.0f;
     if (prim < 0) return;
     SurfInt si;
     int medium;
-    hit_surface(prim, o, d, t, b1, b2, si, medium);
+    hit_surface(prim, o, d, t, b1, b2, si, medium, r.time);
     const float rec[16] = {1.0f, si.t, si.p.x, si.p.y, si.p.z, si.n.x, si.n.y, si.n.z, si.ns.x, si.ns.y, si.ns.z,
                            si.u, si.v, si.tangent.x, si.tangent.y, si.tangent.z};
     for (int k = 0; k < 16; k++) w[k] = rec[k];
@@ -570,8 +627,18 @@ __device__ __forceinline__ void work_pixel(const RenderParams& R, uint32_t pix_i
 
 // Camera::GenerateRay (Camera.hpp:21-35) with the camera draws of
 // TileIntegrator::Render (Integrators.cpp:61-64): pixel2D, time, lens2D.
-__device__ __forceinline__ void camera_ray(const pt_camera_desc& c, uint32_t key, uint32_t x, uint32_t y, f3& o, f3& d) {
+__device__ __forceinline__ void camera_ray(const pt_camera_desc& c, uint32_t key, uint32_t x, uint32_t y, f3& o, f3& d,
+                                           float& time) {
     float a = draw(key, 0), b = draw(key, 1);
+    // t = glm::mix(shutterStart, shutterEnd, time) (Camera.hpp:25) as
+    // TileIntegrator::Render's copy rounds it, fma(start, 1 - u, u * end); a
+    // camera without a shutter: 0
+    if (c.has_shutter) {
+        const float u = draw(key, 2);
+        time = fma_(c.shutter[0], 1.0f - u, rmul(u, c.shutter[1]));
+    } else {
+        time = 0.0f;
+    }
     float pxf = (float)x + a, pyf = (float)y + b;  // == float(double(x) + a): both round the exact sum
     float uc = pxf / (float)c.width;
     float vc = pyf / (float)c.height;
@@ -606,6 +673,7 @@ struct NewSample {
     bool enq;
     uint32_t sid, key;
     f3 o, d;
+    float time;
 };
 __device__ __forceinline__ NewSample claim_camera_sample(const RenderParams& R, bool want,
                                                          unsigned long long* __restrict__ next_sample) {
@@ -626,14 +694,14 @@ __device__ __forceinline__ NewSample claim_camera_sample(const RenderParams& R, 
     }
     __syncthreads();
     const unsigned long long g = s_base + s_w[wave] + lanemask_lt_count(m);
-    NewSample ns{want && g < R.chunk_total, (uint32_t)g, 0u, F3(0, 0, 0), F3(0, 0, 0)};
+    NewSample ns{want && g < R.chunk_total, (uint32_t)g, 0u, F3(0, 0, 0), F3(0, 0, 0), 0.0f};
     if (ns.enq) {
         const uint32_t s_rel = (uint32_t)(g / R.npix_work), pix_i = (uint32_t)(g % R.npix_work);
         uint32_t x, y;
         work_pixel(R, pix_i, x, y);
         const uint32_t s = R.shard_index + (R.s_lo + s_rel) * R.shard_count;
         ns.key = stream_key(R.seed, y * (uint32_t)R.cam.width + x, s);
-        camera_ray(R.cam, ns.key, x, y, ns.o, ns.d);
+        camera_ray(R.cam, ns.key, x, y, ns.o, ns.d, ns.time);
     }
     return ns;
 }
@@ -644,6 +712,7 @@ __device__ __forceinline__ void store_camera_path(PathSoA& next, uint32_t at, co
     next.beta[at] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);  // attenuation, prevPDF = 1
     next.L[at] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(5u));  // camera used dims 0..4
     next.sid[at] = ns.sid;
+    if (S.motion) next.time[at] = ns.time;
 }
 
 // Initial fill of a chunk's wavefront: one camera sample per entry.  Later
@@ -679,7 +748,7 @@ __global__ __launch_bounds__(256) void k_fill(RenderParams R, uint32_t n, PathSo
 template <int INTEGRATOR>
 __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, uint32_t f0, f3& ro, f3& rd, f3& att,
                                              f3& out, float& prev, uint32_t key, uint32_t& dim, uint32_t& flags,
-                                             bool& cont, bool& done, bool& shadow, ShadowRec& srec) {
+                                             bool& cont, bool& done, bool& shadow, ShadowRec& srec, float tm) {
     uint32_t depth = f0 & PF_DEPTH_MASK, rr = (f0 >> PF_RR_SHIFT) & PF_DEPTH_MASK;
     bool spec = (f0 & PF_SPEC) != 0;
     int prim = __float_as_int(h.w);
@@ -723,12 +792,12 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
         LSample ls_e;
         if (INTEGRATOR == PT_INTEGRATOR_PATH) {
             li = ls_sample(r[5]);
-            if (li >= 0) ls_e = light_sample(S.lights[li], r[2], r[3], texinf_uc(key, dim));
+            if (li >= 0) ls_e = light_sample(S.lights[li], r[2], r[3], texinf_uc(key, dim), tm);
         }
 #endif
         SurfInt si;
         int smed;
-        hit_surface(prim, ro, rd, h.x, h.y, h.z, si, smed);
+        hit_surface(prim, ro, rd, h.x, h.y, h.z, si, smed, tm);
 #ifdef PT_DEBUG_KEY
         if (key == PT_DEBUG_KEY)
             printf("G d%u prim %d t %a p %a %a %a ns %a %a %a uv %a %a mat %d light %d out %a %a %a att %a %a %a\n",
@@ -738,12 +807,12 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
         // emission (Integrators.cpp:151-154, 217-226)
         if (si.light >= 0) {
             const pt_light& al = S.lights[si.light];
-            f3 Le = light_L(al, si.n, si.u, si.v, rd);
+            f3 Le = light_L(al, si.n, si.u, si.v, rd, tm);
             if (!is_zero(Le)) {
                 if (INTEGRATOR == PT_INTEGRATOR_SIMPLE || spec) {
                     out = fma3(Le, att, out);
                 } else if (prev > 0) {
-                    const float lp = al.pmf * light_pdf(al, si.p, si.n, ro, rd), p2 = prev * prev;
+                    const float lp = al.pmf * light_pdf(al, si.p, si.n, ro, rd, tm), p2 = prev * prev;
                     const float w = p2 / fma_(lp, lp, p2);
                     out = fma3s(w, Le * att, out);
                 }
@@ -772,7 +841,7 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
 #if PT_SHADE_EARLY_LS
                             const LSample ls = ls_e;
 #else
-                            LSample ls = light_sample(l, r[2], r[3], texinf_uc(key, dim));
+                            LSample ls = light_sample(l, r[2], r[3], texinf_uc(key, dim), tm);
 #endif
                             f3 ldir;
                             float tmax;
@@ -793,14 +862,14 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
                                 if (light_is_delta(l)) {
                                     c = (ls.L * f) / lpdf;
                                 } else {
-                                    lpdf *= light_pdf(l, ls.p, ls.n, si.p, sd);
+                                    lpdf *= light_pdf(l, ls.p, ls.n, si.p, sd, tm);
                                     if (lpdf <= 0) {
                                         ok = false;
                                     } else {
                                         const float w2 = lpdf * lpdf;
                                         const float w1 = mat_pdf(mt, rd, si, sd);
                                         const float wl = w2 / fma_(w1, w1, w2);  // w1*w1 + w2 fused
-                                        c = ((light_L(l, ls.n, ls.u, ls.v, sd) * f) * wl) / lpdf;
+                                        c = ((light_L(l, ls.n, ls.u, ls.v, sd, tm) * f) * wl) / lpdf;
                                     }
                                 }
                                 if (ok && !is_zero(c)) {
@@ -865,13 +934,14 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
     bool cont = false, done = false, shadow = false;
     ShadowRec srec;
     f3 ro = F3(0, 0, 0), rd = F3(0, 0, 0), att = F3(0, 0, 0), out = F3(0, 0, 0);
-    float prev = 0;
+    float prev = 0, tm = 0;
     uint32_t key = 0, dim = 0, flags = 0, sid = 0;
     if (i < n) {
         const uint32_t e = path_slot(i, front, cur.cap);
         const float4 o4 = cur.o[e], d4 = cur.d[e], b4 = cur.beta[e], L4 = cur.L[e];
         const float4 h = hit[i];
         sid = cur.sid[e];
+        if (S.motion) tm = cur.time[e];
         ro = xyz(o4);
         rd = xyz(d4);
         att = xyz(b4);
@@ -880,7 +950,7 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
         key = __float_as_uint(o4.w);
         dim = __float_as_uint(L4.w);
         shade_bounce<INTEGRATOR>(R, h, __float_as_uint(d4.w), ro, rd, att, out, prev, key, dim, flags, cont, done,
-                                 shadow, srec);
+                                 shadow, srec, tm);
     }
     // a finished path stores its sample's radiance (the pending NEE ray, if
     // any, adds to it later) and its entry takes the next camera sample
@@ -902,12 +972,14 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
         next.beta[a] = make_float4(att.x, att.y, att.z, prev);
         next.L[a] = make_float4(out.x, out.y, out.z, __uint_as_float(dim));
         next.sid[a] = sid;
+        if (S.motion) next.time[a] = tm;
     } else if (ns.enq) {
         store_camera_path(next, a, ns, R.cam.medium);
     }
     if (shadow) {
         srec.d.w = __uint_as_float(cont ? a : (SHADOW_DONE_BIT | sid));
         sq[c] = srec;
+        if (S.motion) S.sq_time[c] = tm;  // the shadow ray's time (Integrators.cpp:274)
     }
 }
 
@@ -937,17 +1009,19 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_tail(RenderParams R, PathSoA
         float prev = b4.w;
         const uint32_t key = __float_as_uint(o4.w);
         uint32_t dim = __float_as_uint(L4.w), flags = __float_as_uint(d4.w);
+        const float tm = S.motion ? cur.time[e] : 0.0f;
         for (;;) {
             float t = 0, b1 = 0, b2 = 0;
-            const int prim = trace_closest<COUNT, INST>(ro, rd, __int_as_float(0x7f800000), t, b1, b2, s_ref, wc);
+            const int prim = trace_closest<COUNT, INST>(ro, rd, __int_as_float(0x7f800000), t, b1, b2, s_ref, wc,
+                                                        nullptr, tm);
             ++n_cl;
             bool cont = false, done = false, shadow = false;
             ShadowRec srec;
             shade_bounce<INTEGRATOR>(R, make_float4(t, b1, b2, __int_as_float(prim)), flags, ro, rd, att, out, prev,
-                                     key, dim, flags, cont, done, shadow, srec);
+                                     key, dim, flags, cont, done, shadow, srec, tm);
             if (shadow) {
                 ++n_any;
-                if (!trace_any<COUNT, INST>(xyz(srec.o), xyz(srec.d), srec.o.w, s_ref, wa))
+                if (!trace_any<COUNT, INST>(xyz(srec.o), xyz(srec.d), srec.o.w, s_ref, wa, nullptr, tm))
                     out = F3(fma_(srec.c.x, srec.a.x, out.x), fma_(srec.c.y, srec.a.y, out.y),
                              fma_(srec.c.z, srec.a.z, out.z));
             }
@@ -994,13 +1068,14 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
     bool cont = false, done = false, shadow = false;
     ShadowRecV srec;
     f3 ro = F3(0, 0, 0), rd = F3(0, 0, 0), att = F3(0, 0, 0), out = F3(0, 0, 0);
-    float prev = 0;
+    float prev = 0, tm = 0;
     uint32_t key = 0, dim = 0, flags = 0, sid = 0;
     if (i < n) {
         const uint32_t e = path_slot(i, front, cur.cap);
         const float4 o4 = cur.o[e], d4 = cur.d[e], b4 = cur.beta[e], L4 = cur.L[e];
         const float4 h = hit[i];
         sid = cur.sid[e];
+        if (S.motion) tm = cur.time[e];
         ro = xyz(o4);
         rd = xyz(d4);
         att = xyz(b4);
@@ -1030,7 +1105,7 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
         } else {
             SurfInt si;
             int smed;
-            hit_surface(prim, ro, rd, h.x, h.y, h.z, si, smed);
+            hit_surface(prim, ro, rd, h.x, h.y, h.z, si, smed, tm);
             if (med < 0) med = S.scene_medium;
             bool mvalid = false;
             f3 mp = F3(0, 0, 0);
@@ -1057,12 +1132,12 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
             } else {
                 if (si.light >= 0) {
                     const pt_light& al = S.lights[si.light];
-                    f3 Le = light_L(al, si.n, si.u, si.v, rd);
+                    f3 Le = light_L(al, si.n, si.u, si.v, rd, tm);
                     if (!is_zero(Le)) {
                         if (spec) {
                             out = fma3(att, Le, out);
                         } else if (prev > 0) {
-                            const float lp = al.pmf * light_pdf(al, si.p, si.n, ro, rd), p2 = prev * prev;
+                            const float lp = al.pmf * light_pdf(al, si.p, si.n, ro, rd, tm), p2 = prev * prev;
                             const float w = p2 / fma_(lp, lp, p2);
                             out = fma3s(w, att * Le, out);
                         }
@@ -1081,7 +1156,7 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                 const int li = ls_sample(r[5]);
                 if (li >= 0 && S.lights[li].pmf > 0) {
                     const pt_light& l = S.lights[li];
-                    LSample ls = light_sample(l, r[2], r[3], texinf_uc(key, dim));
+                    LSample ls = light_sample(l, r[2], r[3], texinf_uc(key, dim), tm);
                     f3 ldir;
                     float tmax;
                     if (is_zero(ls.n)) {
@@ -1113,13 +1188,13 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                         if (light_is_delta(l)) {
                             Ll = ls.L;
                         } else {
-                            lpdf *= light_pdf(l, ls.p, ls.n, si.p, sd);
+                            lpdf *= light_pdf(l, ls.p, ls.n, si.p, sd, tm);
                             if (lpdf <= 0) {
                                 ok = false;
                             } else {
                                 const float w2 = lpdf * lpdf;
                                 wl = w2 / fma_(spdf, spdf, w2);  // spdf*spdf + w2 fused
-                                Ll = light_L(l, ls.n, ls.u, ls.v, sd);
+                                Ll = light_L(l, ls.n, ls.u, ls.v, sd, tm);
                             }
                         }
                         if (ok) {
@@ -1194,12 +1269,14 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
         next.beta[a] = make_float4(att.x, att.y, att.z, prev);
         next.L[a] = make_float4(out.x, out.y, out.z, __uint_as_float(dim));
         next.sid[a] = sid;
+        if (S.motion) next.time[a] = tm;
     } else if (ns.enq) {
         store_camera_path(next, a, ns, R.cam.medium);
     }
     if (shadow) {
         srec.d.w = __uint_as_float((cont ? a : (SHADOW_DONE_BIT | sid)) | (__float_as_uint(srec.d.w) & SHADOW_MLE_BIT));
         sq[c] = srec;
+        if (S.motion) S.sq_time[c] = tm;  // the shadow ray's time (Integrators.cpp:447)
     }
 }
 
@@ -1223,6 +1300,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow_tr(PathSoA next, floa
         const ShadowRecV r = sq[i];
         f3 o = xyz(r.o), d = xyz(r.d);
         float max = r.o.w;
+        const float tm = S.motion ? S.sq_time[i] : 0.0f;
         const int med0 = __float_as_int(r.L.w);
         int med = med0;
         f3 Tr = F3(1, 1, 1);
@@ -1232,7 +1310,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow_tr(PathSoA next, floa
             if (!first) extra++;
             first = false;
             float t, b1, b2;
-            const int prim = trace_closest<COUNT>(o, d, max, t, b1, b2, s_ref, wk);
+            const int prim = trace_closest<COUNT>(o, d, max, t, b1, b2, s_ref, wk, nullptr, tm);
             if (prim < 0) {
                 if (med >= 0) Tr = Tr * medium_tr(S.media[med], max);
                 break;
@@ -1244,7 +1322,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow_tr(PathSoA next, floa
             }
             SurfInt si;
             int smed;
-            hit_surface(prim, o, d, t, b1, b2, si, smed);
+            hit_surface(prim, o, d, t, b1, b2, si, smed, tm);
             o = at_f(o, d, t);
             med = get_medium(si, smed, d);
             max -= t;

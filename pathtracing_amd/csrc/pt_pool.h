@@ -634,6 +634,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
 
 // Src interface:
 //   bool load(uint32_t ri, f3& o, f3& d, float& tmax)   (false: skip this ray)
+//   float time(uint32_t ri)   the ray's time (instanced scenes with S.motion)
 //   void closest(uint32_t ri, float t, float b1, float b2, int prim)
 //   void any(uint32_t ri, bool hit)
 //   void tie(uint32_t ri)   (closest hit: the ray met an exact-t tie, see below)
@@ -806,9 +807,11 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 continue;
             }
         }
-        if (INST && ref >= REF_SPECIAL) {  // instance enter / exit (pt_trace.h instance_step)
-            PT_INSTANCE_STEP(ANY);
-            continue;
+        if constexpr (INST) {
+            if (ref >= REF_SPECIAL) {  // instance enter / exit (pt_trace.h instance_step)
+                PT_INSTANCE_STEP(ANY, S.motion ? src.time((uint32_t)ri) : 0.0f);
+                continue;
+            }
         }
         const bool node_step = !(ref & REF_LEAF);
 #if PT_ITER_STATS

@@ -74,6 +74,7 @@ struct pt_ctx {
     uint32_t* ovf = nullptr;  // pool traversal stack entries beyond PT_POOL_LDS
     uint32_t* ovf_any = nullptr;  // the any-hit pool kernel's half of ovf (they may run together)
     uint32_t* ties = nullptr;     // closest-hit rays listed for the exact re-trace (k_closest_ties)
+    float* sq_time = nullptr;     // motion blur: each queued shadow ray's time (with PA/PB.time)
     uint32_t* scratch = nullptr;  // instance traversal state, SCR_WORDS x scratch_lanes
     uint64_t scratch_lanes = 0;
     ShadowRec* sq = nullptr;
@@ -116,6 +117,7 @@ struct pt_ctx {
         bool valid = false;
         uint32_t width = 0, npix = 0, tiled = 0, tiles_x = 0;
         uint32_t s_lo = 0, s_hi = 0, shard_index = 0, shard_count = 1;
+        uint32_t height = 0;  // the film's: npix counts the padded 8x8 tiles when tiled
     } frame;
 };
 
@@ -306,6 +308,41 @@ extern "C" pt_status pt_comm_unique_id(uint8_t* id_out) {
     return PT_OK;
 }
 
+static double comm_timeout_s() {
+    double timeout_s = 120.0;
+    if (const char* e = getenv("PT_COMM_TIMEOUT_S")) timeout_s = std::max(1.0, atof(e));
+    return timeout_s;
+}
+
+// A per-rank communicator is built non-blocking (pt_comm_init_rank), and that
+// mode stays with it: any later call on it (init, the reduce that sets up the
+// connections, finalize) may return ncclInProgress while the work completes
+// in the background.  Polls ncclCommGetAsyncError until the state leaves
+// ncclInProgress or the deadline passes (then ncclInternalError: the caller
+// aborts the communicator).  Test hook: PT_COMM_FAKE_INPROGRESS=n makes a
+// reduce's enqueue report ncclInProgress and the first n polls after it too,
+// as a real non-blocking communicator may (tests/test_gpu_distributed.py).
+static int fake_inprogress() {
+    const char* e = getenv("PT_COMM_FAKE_INPROGRESS");
+    return e ? std::max(0, atoi(e)) : 0;
+}
+static ncclResult_t comm_wait(ncclComm_t comm, ncclResult_t r, double timeout_s, int fake_polls = 0) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (r == ncclInProgress && comm) {
+        if (fake_polls > 0) {
+            fake_polls--;
+            r = ncclInProgress;
+        } else if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) {
+            r = ncclInternalError;
+        }
+        if (r != ncclInProgress) break;
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+            return ncclInternalError;
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    return r;
+}
+
 // Non-blocking ncclCommInitRankConfig polled up to a deadline (env
 // PT_COMM_TIMEOUT_S, default 120 s): a rank whose peers never join (one failed
 // before the collective init) aborts its half-built communicator and returns
@@ -318,29 +355,18 @@ extern "C" pt_status pt_comm_init_rank(pt_ctx* c, int n_ranks, int rank, const u
     HIPCHK(c, hipSetDevice(c->device));
     ncclUniqueId uid;
     memcpy(&uid, id, sizeof(uid));
-    double timeout_s = 120.0;
-    if (const char* e = getenv("PT_COMM_TIMEOUT_S")) timeout_s = std::max(1.0, atof(e));
+    const double timeout_s = comm_timeout_s();
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
     cfg.blocking = 0;
     ncclComm_t comm = nullptr;
     ncclResult_t r = ncclCommInitRankConfig(&comm, n_ranks, uid, rank, &cfg);
-    const auto t0 = std::chrono::steady_clock::now();
-    while (r == ncclInProgress && comm) {
-        ncclResult_t a = ncclInProgress;
-        if (ncclCommGetAsyncError(comm, &a) != ncclSuccess) a = ncclInternalError;
-        r = a;
-        if (r != ncclInProgress) break;
-        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s) {
-            r = ncclInternalError;
-            ncclCommAbort(comm);
-            comm = nullptr;
-            return fail(c, PT_ERR_COMM, "ncclCommInitRank(%d of %d): peers did not join within %.0f s", rank, n_ranks,
-                        timeout_s);
-        }
-        std::this_thread::sleep_for(std::chrono::milliseconds(1));
-    }
+    const bool pending = r == ncclInProgress && comm;
+    r = comm_wait(comm, r, timeout_s);
     if (r != ncclSuccess) {
         if (comm) ncclCommAbort(comm);
+        if (pending && r == ncclInternalError)
+            return fail(c, PT_ERR_COMM, "ncclCommInitRank(%d of %d): peers did not join within %.0f s", rank,
+                        n_ranks, timeout_s);
         return fail(c, PT_ERR_COMM, "ncclCommInitRank(%d of %d): %s", rank, n_ranks, ncclGetErrorString(r));
     }
     c->comm = comm;
@@ -364,10 +390,33 @@ extern "C" pt_status pt_comm_destroy(pt_ctx* c) {
     return PT_OK;
 }
 
+// Orderly teardown of a per-rank (non-blocking) communicator: finalize (which
+// may report ncclInProgress while it flushes), wait, then destroy; a finalize
+// that fails or does not finish in time aborts instead.
+static void comm_release(ncclComm_t comm, bool nonblocking) {
+    if (!comm) return;
+    if (!nonblocking) {
+        ncclCommDestroy(comm);
+        return;
+    }
+    ncclResult_t r = ncclCommFinalize(comm);
+    r = comm_wait(comm, r, comm_timeout_s());
+    if (r == ncclSuccess)
+        ncclCommDestroy(comm);
+    else
+        ncclCommAbort(comm);
+}
+
 // In-place SUM reduce of n doubles onto `root` over the context's communicator,
 // on its stream (replaces Film::Merge's atomic<double> adds, Film.hpp:125-132).
+// On a non-blocking communicator the enqueue itself may report ncclInProgress
+// (the first reduce sets up the connections): it is waited for, not treated as
+// a failure, so this rank does not raise while its peers' reduce is queued.
 static pt_status film_reduce_async(pt_ctx* c, double* film, uint64_t n, int root) {
-    const ncclResult_t r = ncclReduce(film, film, n, ncclDouble, ncclSum, root, c->comm, c->stream);
+    ncclResult_t r = ncclReduce(film, film, n, ncclDouble, ncclSum, root, c->comm, c->stream);
+    const int fake = c->multi ? 0 : fake_inprogress();
+    if (fake && r == ncclSuccess) r = ncclInProgress;
+    if (r == ncclInProgress && !c->multi) r = comm_wait(c->comm, r, comm_timeout_s(), fake);
     if (r != ncclSuccess) return fail(c, PT_ERR_COMM, "ncclReduce: %s", ncclGetErrorString(r));
     return PT_OK;
 }
@@ -390,8 +439,9 @@ static void free_scene(pt_ctx* c) {
     c->has_scene = false;
 }
 static void free_work(pt_ctx* c) {
-    void* bufs[] = {c->PA.o, c->PA.d, c->PA.beta, c->PA.L, c->PA.sid, c->PB.o, c->PB.d, c->PB.beta, c->PB.L,
-                    c->PB.sid, c->hit, c->qcnt, c->sq, c->counters, c->ovf, c->ties};
+    void* bufs[] = {c->PA.o, c->PA.d, c->PA.beta, c->PA.L, c->PA.sid, c->PA.time, c->PB.o, c->PB.d, c->PB.beta,
+                    c->PB.L, c->PB.sid, c->PB.time, c->hit, c->qcnt, c->sq, c->counters, c->ovf, c->ties,
+                    c->sq_time};
     for (void* p : bufs)
         if (p) hipFree(p);
     c->PA = PathSoA{};
@@ -403,6 +453,7 @@ static void free_work(pt_ctx* c) {
     c->ovf = nullptr;
     c->ovf_any = nullptr;
     c->ties = nullptr;
+    c->sq_time = nullptr;
     c->cap = 0;
 }
 
@@ -410,8 +461,9 @@ extern "C" void pt_destroy(pt_ctx* c) {
     if (!c) return;
     for (pt_ctx* p : c->peers) pt_destroy(p);
     c->peers.clear();
-    if (c->comm) ncclCommDestroy(c->comm);
     hipSetDevice(c->device);
+    if (c->comm) comm_release(c->comm, !c->multi);  // per-rank communicators are non-blocking
+    c->comm = nullptr;
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->side_stream) hipStreamSynchronize(c->side_stream);  // any-hit kernels of an overlapped frame
     free_scene(c);
@@ -1092,6 +1144,10 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
         D.prim_base = s->bvhs[I.bvh].prim_base;
         D.n_prims = s->bvhs[I.bvh].n_prims;
         D.virt_base = I.virt_base;
+        D.anim = I.animated ? 1u : 0u;
+        for (int j = 0; j < 3; j++) D.mdir[j] = I.motion[j];
+        D.t0 = I.time_bounds[0];
+        D.t1 = I.time_bounds[1];
     }
     // ---- triangles: vertex indices + flags as uint4
     std::vector<uint4> tri(s->n_triangles);
@@ -1267,6 +1323,9 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     DS.n_media = s->n_media;
     DS.scene_medium = s->scene_medium;
     DS.n_instances = s->n_instances;
+    DS.motion = 0;  // an AnimatedPrimitive: rays carry their time (DevScene::motion)
+    for (uint32_t k = 0; k < s->n_instances; k++)
+        if (s->instances[k].animated) DS.motion = 1;
     DS.scratch = nullptr;
     DS.scratch_lanes = 0;
     DS.stack_drops = c->stack_drops;
@@ -1358,6 +1417,36 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
     return PT_OK;
 }
 
+// Ray-time buffers of a scene with an AnimatedPrimitive (DevScene::motion):
+// each path's time (PA / PB.time, ping-pong with the path state) and each
+// queued shadow ray's (sq_time), sized with the wavefront; none otherwise.
+static pt_status ensure_motion(pt_ctx* c) {
+    if (c->scene.motion && c->cap && !(c->PA.time && c->PB.time && c->sq_time)) {
+        for (float** p : {&c->PA.time, &c->PB.time, &c->sq_time})
+            if (!*p && hipMalloc((void**)p, (size_t)c->cap * sizeof(float)) != hipSuccess) {
+                (void)hipGetLastError();
+                return fail(c, PT_ERR_OOM, "ray-time buffers of %u paths", c->cap);
+            }
+    }
+    c->scene.sq_time = c->scene.motion ? c->sq_time : nullptr;
+    return PT_OK;
+}
+
+// Frees every buffer sized by the wavefront's path count (alloc_paths' OOM retry).
+static void free_paths(pt_ctx* c) {
+    free_work(c);
+    struct Buf {
+        void** p;
+        uint64_t* cap;
+    } bufs[] = {{(void**)&c->sort_order, &c->sort_order_cap}, {(void**)&c->sort_bins, &c->sort_bins_cap},
+                {(void**)&c->ray_order, &c->ray_order_cap}};
+    for (const Buf& b : bufs) {
+        if (*b.p) hipFree(*b.p);
+        *b.p = nullptr;
+        *b.cap = 0;
+    }
+}
+
 static double mitchell_int(float rx, float ry) { return rx * ry / 4.0; }
 static double gauss_h(double x, double sigma) {
     return 0.56418958354775628695 / (sigma * 1.41421356237309504880) * std::exp(-(x * x) / (2 * sigma * sigma));
@@ -1407,8 +1496,10 @@ static pt_status ensure_scratch(pt_ctx* c, uint64_t lanes) {
     return PT_OK;
 }
 
+static pt_status ensure_motion(pt_ctx* c);
 static pt_status bind_scene(pt_ctx* c, uint64_t lanes = 0) {
     if (pt_status st = ensure_scratch(c, lanes)) return st;
+    if (pt_status st = ensure_motion(c)) return st;
     c->scene.scratch = c->scratch;
     c->scene.scratch_lanes = (uint32_t)c->scratch_lanes;
     HIPCHK(c, hipMemcpyToSymbolAsync(HIP_SYMBOL(S), &c->scene, sizeof(DevScene), 0, hipMemcpyHostToDevice, c->stream));
@@ -1500,6 +1591,8 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     const uint64_t sid_limit = rd->integrator == PT_INTEGRATOR_VOLPATH ? SHADOW_MLE_BIT : SHADOW_DONE_BIT;
     if ((uint64_t)R.npix_work >= sid_limit) return fail(c, PT_ERR_ARG, "film too large for the sample ids");
     s_chunk = (uint32_t)std::min<uint64_t>(s_chunk, (sid_limit - 1ull) / R.npix_work);
+    // test hook: a smaller chunk (a frame in several chunks at test sizes)
+    if (const char* e = getenv("PT_SAMPLE_CHUNK")) s_chunk = std::max(1u, std::min<uint32_t>(s_chunk, (uint32_t)atoi(e)));
     pt_status st;
     // a device with less free HBM (or a second context on it) gets smaller
     // chunks instead of PT_ERR_OOM
@@ -1516,14 +1609,6 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     uint32_t paths = rd->paths_in_flight ? rd->paths_in_flight : (big_scene ? PT_PATHS_POOL : PT_PATHS_SIMPLE);
     paths = (uint32_t)std::min<uint64_t>(paths, std::max<uint64_t>(1, (uint64_t)R.npix_work * s_chunk));
     paths = (paths + 255) & ~255u;
-    // ... and a smaller wavefront
-    while ((st = ensure_work(c, paths)) == PT_ERR_OOM && paths > (1u << 20)) {
-        (void)hipGetLastError();
-        paths = ((paths >> 1) + 255) & ~255u;
-    }
-    if (st) return st;
-    if ((st = bind_scene(c)) != PT_OK) return st;  // instance scratch sized for this wavefront
-
     const bool count = (rd->flags & PT_RENDER_COUNT_NODES) != 0;
     // traversal variant: pool (persistent, refilling) for deep trees where ray
     // lengths diverge, one ray per lane for small ones; flags override
@@ -1539,28 +1624,41 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     // spp: 897 -> 949 Mrays/s, profiles/r02_ab_sort.txt), off for small ones
     // (the three passes cost ~0.1 ms a bounce, more than a small scene gains)
     const bool sort_rays = (rd->flags & PT_RENDER_SORT_RAYS) != 0;
-    if (sort_rays) {
-        if ((st = ensure(c, &c->ray_order, c->ray_order_cap, paths)) != PT_OK) return st;
-        if ((st = ensure(c, &c->ray_counts, c->ray_counts_cap, PT_SORT_BINS_SPATIAL)) != PT_OK) return st;
+    const bool sort_mat = (rd->flags & PT_RENDER_SORT_MATERIAL) != 0;
+    const bool sort_sp = !sort_mat && !(rd->flags & PT_RENDER_NO_SORT) &&
+                         ((rd->flags & PT_RENDER_SORT_SPATIAL) || big_scene);
+    const bool keep_bins = PT_SORT_KEEP_BINS && (sort_mat || sort_sp || sort_rays);
+    // every buffer sized by the path count — the wavefront, the claim / hit
+    // orders and bins, the instance scratch — is allocated in one step, and a
+    // device short of HBM (or a second context on it) retries the whole step
+    // with half the paths instead of failing the frame with PT_ERR_OOM
+    auto alloc_paths = [&](uint32_t p) -> pt_status {
+        pt_status s;
+        if ((s = ensure_work(c, p)) != PT_OK) return s;
+        if (sort_rays) {
+            if ((s = ensure(c, &c->ray_order, c->ray_order_cap, p)) != PT_OK) return s;
+            if ((s = ensure(c, &c->ray_counts, c->ray_counts_cap, PT_SORT_BINS_SPATIAL)) != PT_OK) return s;
+        }
+        if (sort_mat || sort_sp) {
+            if ((s = ensure(c, &c->sort_order, c->sort_order_cap, p)) != PT_OK) return s;
+            if ((s = ensure(c, &c->sort_counts, c->sort_counts_cap, PT_SORT_BINS_SPATIAL)) != PT_OK) return s;
+        }
+        if (keep_bins && (s = ensure(c, &c->sort_bins, c->sort_bins_cap, p)) != PT_OK) return s;
+        return bind_scene(c);  // instance scratch and ray-time buffers sized for this wavefront
+    };
+    while ((st = alloc_paths(paths)) == PT_ERR_OOM && paths > (1u << 20)) {
+        (void)hipGetLastError();
+        free_paths(c);  // the larger buffers that did fit make room for the retry
+        paths = ((paths >> 1) + 255) & ~255u;
     }
+    if (st) return st;
     c->scene.ray_order = sort_rays ? c->ray_order : nullptr;
     struct ResetOrder {  // other entry points bind the scene without a claim order
         pt_ctx* c;
         ~ResetOrder() { c->scene.ray_order = nullptr; }
     } reset_order{c};
     if ((st = bind_scene(c)) != PT_OK) return st;
-    const bool sort_mat = (rd->flags & PT_RENDER_SORT_MATERIAL) != 0;
-    const bool sort_sp = !sort_mat && !(rd->flags & PT_RENDER_NO_SORT) &&
-                         ((rd->flags & PT_RENDER_SORT_SPATIAL) || big_scene);
-    if (sort_mat || sort_sp) {
-        if ((st = ensure(c, &c->sort_order, c->sort_order_cap, paths)) != PT_OK) return st;
-        if ((st = ensure(c, &c->sort_counts, c->sort_counts_cap, PT_SORT_BINS_SPATIAL)) != PT_OK) return st;
-    }
-    uint16_t* bins = nullptr;  // (shared by the claim-order and hit sorts: each pass pair runs in turn on sm)
-    if (PT_SORT_KEEP_BINS && (sort_mat || sort_sp || sort_rays)) {
-        if ((st = ensure(c, &c->sort_bins, c->sort_bins_cap, paths)) != PT_OK) return st;
-        bins = c->sort_bins;
-    }
+    uint16_t* bins = keep_bins ? c->sort_bins : nullptr;  // (shared by the claim-order and hit sorts: each pass pair runs in turn on sm)
     hipStream_t sm = c->stream;
     HIPCHK(c, hipMemsetAsync(c->counters, 0, (CNT_SHARDS + 1) * CNT_COUNT * 8, sm));
     HIPCHK(c, hipMemsetAsync(c->stack_drops, 0, 4, sm));
@@ -1915,7 +2013,7 @@ static pt_status render_dev(pt_ctx* c, const pt_camera_desc* cam, const pt_rende
             HIPCHK(c, hipGetLastError());
             // the chunk stays in sample_L after the frame: pt_frame_samples
             c->frame = pt_ctx::FrameRec{true, (uint32_t)cam->width, R.npix_work, R.tiled, R.tiles_x,
-                                        R.s_lo, R.s_hi, R.shard_index, R.shard_count};
+                                        R.s_lo, R.s_hi, R.shard_index, R.shard_count, (uint32_t)cam->height};
             return PT_OK;
         }));
     });
@@ -1933,8 +2031,8 @@ extern "C" pt_status pt_frame_samples(pt_ctx* c, const uint32_t* pixels, const u
     std::vector<unsigned long long> idx(n);
     for (uint32_t i = 0; i < n; i++) {
         const uint32_t p = pixels[i], s = samples[i];
+        if ((uint64_t)p >= (uint64_t)f.width * f.height) return fail(c, PT_ERR_ARG, "pixel %u outside the frame", p);
         const uint32_t x = p % f.width, y = p / f.width;
-        if (p >= f.npix) return fail(c, PT_ERR_ARG, "pixel %u outside the frame", p);
         if (s < f.shard_index || (s - f.shard_index) % f.shard_count)
             return fail(c, PT_ERR_ARG, "sample %u belongs to another shard", s);
         const uint32_t sl = (s - f.shard_index) / f.shard_count;
@@ -1961,6 +2059,15 @@ extern "C" pt_status pt_frame_samples(pt_ctx* c, const uint32_t* pixels, const u
     hipFree(di);
     hipFree(dout);
     if (e != hipSuccess) return fail(c, PT_ERR_HIP, "frame samples: %s", hipGetErrorString(e));
+    return PT_OK;
+}
+
+extern "C" pt_status pt_frame_sample_range(const pt_ctx* c, uint32_t* first, uint32_t* last) {
+    if (!c || !first || !last) return PT_ERR_ARG;
+    const pt_ctx::FrameRec& f = c->frame;
+    if (!f.valid || f.s_hi <= f.s_lo) return PT_ERR_STATE;
+    *first = f.s_lo * f.shard_count + f.shard_index;
+    *last = (f.s_hi - 1) * f.shard_count + f.shard_index;
     return PT_OK;
 }
 
@@ -2273,7 +2380,7 @@ extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any
     HIPCHK(c, hipGetLastError());
     if (!any_hit)
         hipLaunchKernelGGL(k_trace_rays_ties, dim3(std::min(64u, tb)), dim3(PT_TRACE_BLOCK), 0, c->stream,
-                           (const pt_ray*)dr, dh, (const uint32_t*)tl, (const uint32_t*)n_ties);
+                           (const pt_ray*)dr, dh, (const uint32_t*)tl, (const uint32_t*)n_ties, (uint32_t)n);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev[5], c->stream));
     if (!hdev) HIPCHK(c, hipMemcpyAsync(hits, dh, (size_t)n * sizeof(pt_hit), hipMemcpyDeviceToHost, c->stream));

@@ -932,6 +932,85 @@ __device__ __forceinline__ f3 normalize4(f3 v) {
     return v * (1.0f / csqrt(d));
 }
 
+// ---- AnimatedPrimitive / AnimatedLight (Primitive.cpp:76-96, Light.cpp:338-364):
+// a TransformedPrimitive / TransformedLight over glm::translate(mat4(1),
+// dir * t), t = glm::clamp(time - t0, t0, t1) / (t1 - t0), rebuilt per ray at
+// the ray's time (the reference builds the temporary per call).  glm::inverse
+// (compute_inverse<4,4>) is restated op by op: on a translation every
+// cofactor product is exact, so the reference build's contractions round it
+// alike, zero signs included (pt_mat4_inverse, the oracle's mat4_inverse_).
+__device__ __forceinline__ void anim_transform(const DevInstance& I, float time, float* T) {
+    const float t0 = I.t0, t1 = I.t1;
+    float x = time - t0;
+    x = t0 > x ? t0 : x;  // glm::max (func_common.inl:29)
+    x = t1 < x ? t1 : x;  // glm::min (func_common.inl:20)
+    const float t = x / (t1 - t0);
+#pragma unroll
+    for (int k = 0; k < 16; k++) T[k] = (k % 5 == 0) ? 1.0f : 0.0f;
+    // column 3 = m[0]*v.x + m[1]*v.y + m[2]*v.z + m[3] over the identity: the
+    // products are exact, so v itself, a zero made +0 by the final add
+#pragma unroll
+    for (int k = 0; k < 3; k++) T[12 + k] = rmul(I.mdir[k], t) + 0.0f;
+}
+__device__ __forceinline__ void m4_inverse(const float* m, float* out) {
+#define M(c, r) m[(c) * 4 + (r)]
+#define D2(a, b, c, d) (rmul(a, b) - rmul(c, d))
+    const float C00 = D2(M(2, 2), M(3, 3), M(3, 2), M(2, 3)), C02 = D2(M(1, 2), M(3, 3), M(3, 2), M(1, 3));
+    const float C03 = D2(M(1, 2), M(2, 3), M(2, 2), M(1, 3)), C04 = D2(M(2, 1), M(3, 3), M(3, 1), M(2, 3));
+    const float C06 = D2(M(1, 1), M(3, 3), M(3, 1), M(1, 3)), C07 = D2(M(1, 1), M(2, 3), M(2, 1), M(1, 3));
+    const float C08 = D2(M(2, 1), M(3, 2), M(3, 1), M(2, 2)), C10 = D2(M(1, 1), M(3, 2), M(3, 1), M(1, 2));
+    const float C11 = D2(M(1, 1), M(2, 2), M(2, 1), M(1, 2)), C12 = D2(M(2, 0), M(3, 3), M(3, 0), M(2, 3));
+    const float C14 = D2(M(1, 0), M(3, 3), M(3, 0), M(1, 3)), C15 = D2(M(1, 0), M(2, 3), M(2, 0), M(1, 3));
+    const float C16 = D2(M(2, 0), M(3, 2), M(3, 0), M(2, 2)), C18 = D2(M(1, 0), M(3, 2), M(3, 0), M(1, 2));
+    const float C19 = D2(M(1, 0), M(2, 2), M(2, 0), M(1, 2)), C20 = D2(M(2, 0), M(3, 1), M(3, 0), M(2, 1));
+    const float C22 = D2(M(1, 0), M(3, 1), M(3, 0), M(1, 1)), C23 = D2(M(1, 0), M(2, 1), M(2, 0), M(1, 1));
+    const float F[6][4] = {{C00, C00, C02, C03}, {C04, C04, C06, C07}, {C08, C08, C10, C11},
+                           {C12, C12, C14, C15}, {C16, C16, C18, C19}, {C20, C20, C22, C23}};
+    float V[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        V[k][0] = M(1, k);
+        V[k][1] = V[k][2] = V[k][3] = M(0, k);
+    }
+    // Inv_i = (Va * Fa - Vb * Fb) + Vc * Fc lane by lane, times SignA / SignB
+    constexpr int comb[4][6] = {{1, 0, 2, 1, 3, 2}, {0, 0, 2, 3, 3, 4}, {0, 1, 1, 3, 3, 5}, {0, 2, 1, 4, 2, 5}};
+    float inv[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const float sg = (i & 1) ? -1.0f : 1.0f;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int* c = comb[i];
+            const float v = (rmul(V[c[0]][k], F[c[1]][k]) - rmul(V[c[2]][k], F[c[3]][k])) + rmul(V[c[4]][k], F[c[5]][k]);
+            inv[i][k] = v * ((k & 1) ? -sg : sg);
+        }
+    }
+    float d0[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) d0[k] = rmul(M(0, k), inv[k][0]);
+    const float od = 1.0f / ((d0[0] + d0[1]) + (d0[2] + d0[3]));
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) out[c * 4 + r] = inv[c][r] * od;
+#undef M
+#undef D2
+}
+// An instance's transform and inverse at a ray's time: the uploaded pair, or
+// an AnimatedPrimitive's rebuilt at `time` (S.motion: the scene has one)
+__device__ __forceinline__ void inst_matrices(const DevInstance& I, float time, float* T, float* inv) {
+    if (S.motion && I.anim) {
+        anim_transform(I, time, T);
+        m4_inverse(T, inv);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            T[k] = I.T[k];
+            inv[k] = I.inv[k];
+        }
+    }
+}
+
 struct LSample {
     f3 L, p, n, dir;
     float u, v;
@@ -1027,22 +1106,25 @@ __device__ __forceinline__ f3 inf_le(const pt_light& l, f3 d) {
 struct PN {
     f3 p, n;
 };
-__device__ __noinline__ PN tlight_to_world(int inst, f3 p, f3 n) {  // TransformedLight::sample
-    const DevInstance& I = S.instances[inst];
-    float NM[9];
-    normal_matrix(I.T, NM);
-    return PN{m4_point(I.T, p), m3_mul(NM, n)};
+// The time moves an AnimatedLight (its instance's translation at the ray's time).
+__device__ __noinline__ PN tlight_to_world(int inst, f3 p, f3 n, float time) {  // TransformedLight::sample
+    float T[16], inv[16], NM[9];
+    inst_matrices(S.instances[inst], time, T, inv);
+    normal_matrix(T, NM);
+    return PN{m4_point(T, p), m3_mul(NM, n)};
 }
 struct TLObj {
     f3 p, n, ro, rd;
 };
-__device__ __noinline__ TLObj tlight_to_object(int inst, f3 p, f3 n, f3 ro, f3 rd) {  // TransformedLight::PDF
-    const DevInstance& I = S.instances[inst];
-    return TLObj{m4_point(I.inv, p), normalize(m4_dir(I.inv, n)), m4_point(I.inv, ro), normalize(m4_dir(I.inv, rd))};
+__device__ __noinline__ TLObj tlight_to_object(int inst, f3 p, f3 n, f3 ro, f3 rd, float time) {  // TransformedLight::PDF
+    float T[16], inv[16];
+    inst_matrices(S.instances[inst], time, T, inv);
+    return TLObj{m4_point(inv, p), normalize(m4_dir(inv, n)), m4_point(inv, ro), normalize(m4_dir(inv, rd))};
 }
-__device__ __noinline__ f3 tlight_normal(int inst, f3 n) {  // TransformedLight::L's temp.n
-    float NM[9];
-    normal_matrix(S.instances[inst].T, NM);
+__device__ __noinline__ f3 tlight_normal(int inst, f3 n, float time) {  // TransformedLight::L's temp.n
+    float T[16], inv[16], NM[9];
+    inst_matrices(S.instances[inst], time, T, inv);
+    normal_matrix(T, NM);
     return m3_mul(NM, n);
 }
 
@@ -1095,7 +1177,9 @@ __device__ __forceinline__ float inf_pdf(const pt_light& l, f3 rd) {
     return l.kind == PT_LIGHT_TEX_INF ? texinf_pdf(l, rd) : 1.0f / (4.0f * PT_PI);
 }
 
-__device__ __forceinline__ LSample light_sample(const pt_light& l, float u0, float u1, float uc = 0.0f) {
+// time: the ray's (Light::sample(uv, time), Light.hpp:21) -- an AnimatedLight's
+__device__ __forceinline__ LSample light_sample(const pt_light& l, float u0, float u1, float uc = 0.0f,
+                                                float time = 0.0f) {
     LSample ls;
     ls.L = F3(0, 0, 0);
     ls.p = F3(0, 0, 0);
@@ -1107,7 +1191,7 @@ __device__ __forceinline__ LSample light_sample(const pt_light& l, float u0, flo
         uint32_t kind = __float_as_uint(S.geom[l.prim].a.w) & GF_KIND;
         shape_sample(kind, pi.index, u0, u1, ls);
         if (l.instance >= 0) {
-            const PN w = tlight_to_world(l.instance, ls.p, ls.n);
+            const PN w = tlight_to_world(l.instance, ls.p, ls.n, time);
             ls.p = w.p;
             ls.n = w.n;
         }
@@ -1157,12 +1241,12 @@ __device__ __forceinline__ bool light_is_delta(const pt_light& l) {
     return l.kind == PT_LIGHT_DISTANT || l.kind == PT_LIGHT_POINT;
 }
 // Light::PDF(interaction, ray)
-__device__ __forceinline__ float light_pdf(const pt_light& l, f3 p, f3 n, f3 ro, f3 rd) {
+__device__ __forceinline__ float light_pdf(const pt_light& l, f3 p, f3 n, f3 ro, f3 rd, float time = 0.0f) {
     if (l.kind == PT_LIGHT_AREA) {  // Light.cpp:267-272
         uint32_t kind = __float_as_uint(S.geom[l.prim].a.w) & GF_KIND;
         uint32_t index = S.info[l.prim].index;
         if (l.instance >= 0) {
-            const TLObj o = tlight_to_object(l.instance, p, n, ro, rd);
+            const TLObj o = tlight_to_object(l.instance, p, n, ro, rd, time);
             p = o.p;
             n = o.n;
             ro = o.ro;
@@ -1176,10 +1260,10 @@ __device__ __forceinline__ float light_pdf(const pt_light& l, f3 p, f3 n, f3 ro,
     return 0;
 }
 // Light::L(interaction, ray)
-__device__ __forceinline__ f3 light_L(const pt_light& l, f3 n, float u, float v, f3 rd) {
+__device__ __forceinline__ f3 light_L(const pt_light& l, f3 n, float u, float v, f3 rd, float time = 0.0f) {
     if (l.kind == PT_LIGHT_AREA) {  // Light.cpp:257-260
         if (l.instance >= 0) {  // TransformedLight::L: fresh interaction, uv (0, 0)
-            n = tlight_normal(l.instance, n);
+            n = tlight_normal(l.instance, n, time);
             u = v = 0;
         }
         if (l.one_sided && dot(rd, n) > 0) return F3(0, 0, 0);

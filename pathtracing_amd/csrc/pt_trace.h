@@ -466,6 +466,7 @@ struct InstState {
     uint32_t oct;
     int best;
     uint32_t ref;
+    float time;  // the ray's (an AnimatedPrimitive is entered at its translation then)
 };
 template <bool ANY, bool QN = false>
 __device__ __forceinline__ InstState instance_step_inl(InstState s) {
@@ -483,7 +484,9 @@ __device__ __forceinline__ InstState instance_step_inl(InstState s) {
         s.o = F3(__uint_as_float(sc[0]), __uint_as_float(sc[L]), __uint_as_float(sc[2 * L]));
         s.d = F3(__uint_as_float(sc[3 * L]), __uint_as_float(sc[4 * L]), __uint_as_float(sc[5 * L]));
         s.inv = inv_dir(s.d);
-        s.oct = octant(s.d);
+        // the per-ray flags survive the exit: a ray already listed for the
+        // exact-tie re-trace (OCT_TIE) must not be listed again
+        s.oct = octant(s.d) | (s.oct & (OCT_TIE | OCT_FOUND));
         s.ref = REF_EMPTY;
         return s;
     }
@@ -492,14 +495,24 @@ __device__ __forceinline__ InstState instance_step_inl(InstState s) {
     const DevInstance& I = S.instances[inst];
     const float w[7] = {s.o.x, s.o.y, s.o.z, s.d.x, s.d.y, s.d.z, s.tmax};
     for (int k = 0; k < 7; k++) sc[k * L] = __float_as_uint(w[k]);
-    const f3 dir = m4_dir(I.inv, s.d);
+    f3 dir, org;
+    if (S.motion && I.anim) {  // AnimatedPrimitive::Intersect(Pred) at the ray's time (Primitive.cpp:82-89)
+        float T[16], inv[16];
+        anim_transform(I, s.time, T);
+        m4_inverse(T, inv);
+        dir = m4_dir(inv, s.d);
+        org = m4_point(inv, s.o);
+    } else {
+        dir = m4_dir(I.inv, s.d);
+        org = m4_point(I.inv, s.o);
+    }
     const float len = length(dir);
     sc[7 * L] = __float_as_uint(len);
     sc[8 * L] = inst;
-    s.o = m4_point(I.inv, s.o);
+    s.o = org;
     s.d = dir / len;
     s.inv = inv_dir(s.d);
-    s.oct = octant(s.d) | OCT_INST;
+    s.oct = octant(s.d) | OCT_INST | (s.oct & (OCT_TIE | OCT_FOUND));
     s.tmax = s.tmax * len;
     s.ref = (QN && PT_Q48) ? I.qroot : I.root;  // the BLAS root in the traversal's node form
     return s;
@@ -514,10 +527,10 @@ __device__ __noinline__ InstState instance_step(InstState s) {
 // left when the traversal is back at that depth with nothing to visit
 // (PT_INSTANCE_LEAVE), so no marker takes a stack entry that a full stack
 // could drop.
-#define PT_INSTANCE_STEP_FN(ANY_, FN_)                                                          \
+#define PT_INSTANCE_STEP_FN(ANY_, FN_, TIME_)                                                   \
     do {                                                                                \
         const bool enter_ = ref != REF_INST_EXIT;                                       \
-        const InstState st_ = FN_(InstState{o, d, inv, tmax, oct, best, ref});               \
+        const InstState st_ = FN_(InstState{o, d, inv, tmax, oct, best, ref, (TIME_)});      \
         o = st_.o;                                                                      \
         d = st_.d;                                                                      \
         inv = st_.inv;                                                                  \
@@ -529,15 +542,16 @@ __device__ __noinline__ InstState instance_step(InstState s) {
 // true when the lane's ray is inside an instance whose BLAS is exhausted
 #define PT_INSTANCE_DONE() ((oct & OCT_INST) && (uint32_t)sp == (oct >> OCT_SP_SHIFT))
 // (PT_INSTANCE_STEP: inside trace_pool, whose QN names the node form)
-#define PT_INSTANCE_STEP(ANY_) PT_INSTANCE_STEP_FN(ANY_, (instance_step<ANY_, QN>))
-#define PT_INSTANCE_STEP_INL(ANY_) PT_INSTANCE_STEP_FN(ANY_, instance_step_inl<ANY_>)
+// TIME_: the lane's ray time (0 unless the scene has an AnimatedPrimitive)
+#define PT_INSTANCE_STEP(ANY_, TIME_) PT_INSTANCE_STEP_FN(ANY_, (instance_step<ANY_, QN>), TIME_)
+#define PT_INSTANCE_STEP_INL(ANY_) PT_INSTANCE_STEP_FN(ANY_, instance_step_inl<ANY_>, time)
 
 // Closest hit.  Returns prim slot or -1; t, b1, b2 of the accepted hit.
 // LN: stack entries kept in LDS; entries [LN, PT_STACK) go to ovf
 // ([entry][grid lane], sized by the runtime for the one-ray-per-lane grid).
 template <bool COUNT, bool INST = true, int LN = PT_STACK>
 __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out, float& b2_out,
-                             uint32_t* s_ref, TraceWork& wk, uint32_t* __restrict__ ovf = nullptr) {
+                             uint32_t* s_ref, TraceWork& wk, uint32_t* __restrict__ ovf = nullptr, float time = 0.0f) {
     const uint32_t lane = threadIdx.x;
     f3 inv = inv_dir(d);
     uint32_t oct = octant(d);
@@ -637,7 +651,7 @@ __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out
 // reference (BVH.hpp:1099-1102); the last one is visited next without a push.
 template <bool COUNT, bool INST = true, int LN = PT_STACK>
 __device__ bool trace_any(f3 o, f3 d, float tmax, uint32_t* s_ref, TraceWork& wk,
-                          uint32_t* __restrict__ ovf = nullptr) {
+                          uint32_t* __restrict__ ovf = nullptr, float time = 0.0f) {
     const uint32_t lane = threadIdx.x;
     f3 inv = inv_dir(d);
     uint32_t oct = 0;

@@ -410,6 +410,10 @@ def flatten_scene(scene: Scene) -> FlatScene:
             ins["inv"] = p.invTransform.reshape(16)
             ins["bvh"] = b
             ins["virt_base"] = virt_base
+            if isinstance(p, AnimatedPrimitive):  # per-ray translation (Primitive.cpp:82-89)
+                ins["motion"] = p.direction
+                ins["time_bounds"] = p.timeBounds
+                ins["animated"] = 1
             virt_base += int((model_blas + gp_blas)[b - 1][2].shape[0])
             rec["kind"] = N.PT_PRIM_INSTANCE
             rec["index"] = len(instances)
@@ -635,6 +639,10 @@ def camera_desc(cam, flat: Optional[FlatScene] = None) -> N.CameraDesc:
     d.defocus_radius = float(cam.defocusRadius)
     d.focus_distance = float(cam.FocusDistance)
     d.focus_angle = float(cam.FocusAngle)
+    sh = getattr(cam, "shutter", None)
+    d.has_shutter = 0 if sh is None else 1
+    if sh is not None:
+        d.shutter[:] = [float(sh[0]), float(sh[1])]
     W, H = cam.film.Resolution()
     d.width = W
     d.height = H

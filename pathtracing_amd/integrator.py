@@ -82,6 +82,13 @@ class Context:
         N.check(self._lib.pt_comm_destroy(self.ptr), self.ptr)
         self.comm_ranks = 0
 
+    def frame_sample_range(self) -> tuple[int, int]:
+        """pt_frame_sample_range: (first, last) frame sample indices of this
+        shard that frame_samples can serve (the last sample chunk)."""
+        a, b = C.c_uint32(0), C.c_uint32(0)
+        N.check(self._lib.pt_frame_sample_range(self.ptr, C.byref(a), C.byref(b)), self.ptr)
+        return int(a.value), int(b.value)
+
     def frame_samples(self, pixels: np.ndarray, samples: np.ndarray) -> np.ndarray:
         """pt_frame_samples: per-sample radiance (n, 3) float32 of the last
         fixed-SPP frame rendered on this context, for (pixel, sample) pairs

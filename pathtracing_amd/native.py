@@ -58,15 +58,16 @@ MATERIAL = np.dtype([("kind", "<u4"), ("tex", "<i4"), ("norm", "<i4"), ("rough",
                      ("albedo", "<f4", 3)])
 LIGHT = np.dtype([("kind", "<u4"), ("prim", "<i4"), ("tex", "<i4"), ("one_sided", "<u4"), ("power", "<f4"),
                   ("pmf", "<f4"), ("color", "<f4", 3), ("vec", "<f4", 3), ("scale", "<f4"), ("instance", "<i4")])
-INSTANCE = np.dtype([("transform", "<f4", 16), ("inv", "<f4", 16), ("bvh", "<u4"), ("virt_base", "<u4")])
+INSTANCE = np.dtype([("transform", "<f4", 16), ("inv", "<f4", 16), ("bvh", "<u4"), ("virt_base", "<u4"),
+                     ("motion", "<f4", 3), ("time_bounds", "<f4", 2), ("animated", "<u4")])
 MEDIUM = np.dtype([("sigma_a", "<f4", 3), ("sigma_s", "<f4", 3), ("sigma_t", "<f4", 3), ("Le", "<f4", 3),
                    ("g", "<f4")])
-RAY = np.dtype([("o", "<f4", 3), ("d", "<f4", 3), ("tmax", "<f4")])
+RAY = np.dtype([("o", "<f4", 3), ("d", "<f4", 3), ("tmax", "<f4"), ("time", "<f4")])
 HIT = np.dtype([("t", "<f4"), ("b1", "<f4"), ("b2", "<f4"), ("prim", "<i4")])
 
 assert REF_NODE.itemsize == 8 and REF_CLUSTER.itemsize == 128 and PRIM.itemsize == 20
 assert QUAD.itemsize == 64 and SPHERE.itemsize == 16 and TEXTURE.itemsize == 48 and IMAGE.itemsize == 24
-assert MATERIAL.itemsize == 48 and LIGHT.itemsize == 56 and RAY.itemsize == 28 and HIT.itemsize == 16
+assert MATERIAL.itemsize == 48 and LIGHT.itemsize == 56 and RAY.itemsize == 32 and INSTANCE.itemsize == 160 and HIT.itemsize == 16
 
 
 class RefNode(C.Structure):
@@ -106,7 +107,7 @@ class CameraDesc(C.Structure):
     _fields_ = [("origin", C.c_float * 3), ("u", C.c_float * 3), ("v", C.c_float * 3), ("w", C.c_float * 3),
                 ("half_width", C.c_float), ("half_height", C.c_float), ("defocus_radius", C.c_float),
                 ("focus_distance", C.c_float), ("focus_angle", C.c_float), ("width", C.c_int32),
-                ("height", C.c_int32), ("medium", C.c_int32)]
+                ("height", C.c_int32), ("medium", C.c_int32), ("shutter", C.c_float * 2), ("has_shutter", C.c_int32)]
 
 
 class RenderDesc(C.Structure):
@@ -141,7 +142,7 @@ EXPORTS = [
     "pt_trace", "pt_scene_device_bytes", "pt_bvh4_build", "pt_bvh4_order_table", "pt_film_resolve",
     "pt_mat4_inverse", "pt_bvh4_build_device", "pt_set_node_format", "pt_render_adaptive", "pt_render_samples",
     "pt_texinf_weights", "pt_device_count", "pt_comm_unique_id", "pt_comm_init_rank", "pt_film_reduce",
-    "pt_comm_destroy", "pt_frame_samples",
+    "pt_comm_destroy", "pt_frame_samples", "pt_frame_sample_range",
 ]
 PT_COMM_ID_BYTES = 128
 
@@ -184,6 +185,8 @@ def lib():
     L.pt_comm_destroy.restype = C.c_int32
     L.pt_frame_samples.argtypes = [vp, vp, vp, C.c_uint32, vp]
     L.pt_frame_samples.restype = C.c_int32
+    L.pt_frame_sample_range.argtypes = [vp, vp, vp]
+    L.pt_frame_sample_range.restype = C.c_int32
     L.pt_destroy.argtypes = [vp]
     L.pt_destroy.restype = None
     L.pt_last_error.argtypes = [vp]

@@ -227,6 +227,8 @@ def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: 
     W, H = camera.film.Resolution()
     lines.append(f"camera {' '.join(_f(x) for x in [*camera.lookFrom, *camera.lookAt])} {_f(camera.fov)} {W} {H} "
                  f"{_f(camera.FocusAngle)} {_f(camera.FocusDistance)}")
+    if camera.shutter is not None:  # Camera(..., glm::vec2 shutterBounds) (Camera.hpp:16-19)
+        lines.append(f"shutter {_f(camera.shutter[0])} {_f(camera.shutter[1])}")
     flt = camera.film.filter
     if flt.kind == 0:
         lines.append(f"filter mitchell {_f(flt.radius[0])} {_f(flt.radius[1])} {flt.b!r} {flt.c!r}")

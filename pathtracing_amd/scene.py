@@ -912,9 +912,11 @@ class TransformedPrimitive(Primitive):
 
 class AnimatedPrimitive(TransformedPrimitive):
     """AnimatedPrimitive (Primitive.hpp:52-66, Primitive.cpp:76-96): a
-    translation by direction * t, t = clamp(time - t0, t0, t1) / (t1 - t0).
-    Camera rays carry time 0 (the reference's shutter is uninitialised, SURVEY
-    A.14), so the instance is the translation at time 0."""
+    translation by direction * t, t = clamp(time - t0, t0, t1) / (t1 - t0),
+    evaluated per ray at the ray's time (the device and the oracle rebuild
+    the translation and its glm::inverse per ray).  `transform` holds the
+    time-0 translation: what rays see under a camera without a shutter (time
+    0)."""
 
     def __init__(self, primitive: Primitive, direction, timeBounds):
         self.direction = _v3(direction)
@@ -1159,8 +1161,21 @@ class Film:
 class Camera:
     """Camera.hpp:7-35.  The basis is built in float32 like the reference ctor."""
 
-    def __init__(self, lookFrom, lookAt, fov: float, film: Film, FocusAngle: float = 0.0, FocusDistance: float = 0.0,
-                 medium: Optional[HomogeneusMedium] = None):
+    def __init__(self, lookFrom, lookAt, fov: float, film: Film, FocusAngle=0.0, FocusDistance: float = 0.0,
+                 medium: Optional[HomogeneusMedium] = None, shutterBounds=None):
+        # Camera(lookFrom, lookAt, fov, film, glm::vec2 shutterBounds)
+        # (Camera.hpp:16-19): a 2-sequence in FocusAngle's place, or the
+        # keyword, is the shutter; that ctor has no lens (FocusAngle 0).
+        # Rays carry time = mix(shutterStart, shutterEnd, u) (Camera.hpp:25);
+        # without a shutter the reference's bounds are uninitialised (SURVEY
+        # A.14) and rays carry time 0.
+        if not np.isscalar(FocusAngle):
+            if shutterBounds is not None or FocusDistance or medium is not None:
+                raise TypeError("Camera(lookFrom, lookAt, fov, film, shutterBounds) takes no lens or medium")
+            shutterBounds, FocusAngle = FocusAngle, 0.0
+        self.shutter = None if shutterBounds is None else np.asarray(shutterBounds, np.float32).reshape(2)
+        if self.shutter is not None and (FocusAngle or FocusDistance):
+            raise TypeError("the reference's shutter camera has no thin lens (Camera.hpp:16-19)")
         self.cameraMedium = medium
         self.lookFrom = _v3(lookFrom)
         self.lookAt = _v3(lookAt)

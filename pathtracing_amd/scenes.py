@@ -160,6 +160,34 @@ def tie_models(W: int = 32, H: int = 32, spp: int = 4, max_depth: int = 8, seed:
     return SceneSetup(scene, camera, "path", UniformLightSampler(), max_depth, seed, spp).finish()
 
 
+def tie_instances(W: int = 32, H: int = 32, spp: int = 4, max_depth: int = 8,
+                  seed: int = 0x5EED0036) -> SceneSetup:
+    """Exact-t ties inside instances: tie_models' three wall Models (same
+    geometry, three materials), each instanced under the same rotation and
+    scale (TransformedPrimitive, Primitive.cpp:42-64).  The three instances
+    have identical boxes, so the TLAS holds them in one leaf, and every wall
+    hit is a tie met again inside each instance: the exact re-trace must list
+    such a ray once (pt_pool.h OCT_TIE across instance enter / exit) and pick
+    the instance the reference's recursion order picks."""
+    from .scene import TransformedPrimitive, mat4_identity, mat4_rotate, mat4_scale
+    scene = Scene()
+    walls = [
+        _quad_tris((-1, -1, 1), (1, -1, 1), (1, -1, -1), (-1, -1, -1)),   # floor
+        _quad_tris((-1, -1, -1), (1, -1, -1), (1, 1, -1), (-1, 1, -1)),   # back
+        _quad_tris((-1, -1, 1), (-1, -1, -1), (-1, 1, -1), (-1, 1, 1)),   # left
+        _quad_tris((1, -1, -1), (1, -1, 1), (1, 1, 1), (1, 1, -1)),       # right
+    ]
+    mats = [MicrofacetDiffuse((0.73, 0.73, 0.73)), MicrofacetDiffuse((0.65, 0.05, 0.05)),
+            MicrofacetDiffuse((0.12, 0.45, 0.15))]
+    xf = mat4_scale(mat4_rotate(mat4_identity(), 0.15, (0, 1, 0)), (1.05, 1.0, 0.95))
+    for m in mats:
+        scene.Add(TransformedPrimitive(Model([Mesh(i, v, None, n, uv, m) for (i, v, n, uv) in walls]), xf))
+    light = AreaLight(QuadShape((-0.25, 0.95, -0.25), (0.5, 0, 0), (0, 0, 0.5)), (17.0, 12.0, 4.0), False)
+    scene.Add(GeometricPrimitive(light.getShape(), MicrofacetDiffuse((0.78, 0.78, 0.78)), light))
+    camera = Camera((0, 0, 3.7), (0, 0, 0), 0.75, Film((W, H), MitchellFilter()))
+    return SceneSetup(scene, camera, "path", UniformLightSampler(), max_depth, seed, spp).finish()
+
+
 def cornell(W: int = 1024, H: int = 1024, spp: int = 256, config: str = "c2", max_depth: int = 8,
             seed: Optional[int] = None, fog: bool = False, filt=None, lens=None) -> SceneSetup:
     """C2/C3 Cornell box: 5 walls + 2 boxes as one triangle Model (34 tris) and
@@ -893,3 +921,80 @@ def instances(W: int = 1024, H: int = 1024, spp: int = 256, max_depth: int = 8,
     film = Film((W, H), MitchellFilter())
     camera = Camera((0, 0, 3.7), (0, 0, 0), 0.75, film)
     return SceneSetup(scene, camera, "path", PowerLightSampler(), max_depth, seed, spp).finish()
+
+
+# --------------------------------------------------------------------------
+def motion_blur(W: int = 32, H: int = 32, spp: int = 4, max_depth: int = 16,
+                seed: int = 0x5EED0071) -> SceneSetup:
+    """Motion blur, NoModel-lite (main.cpp:164-270): a shutter camera
+    Camera(lookFrom, lookAt, fov, film, vec2(0, 1)) (Camera.hpp:16-19) inside
+    a thin forward-scattering medium (camera and scene medium), the animated
+    sphere of main.cpp:186-190 (AnimatedPrimitive, direction (0, 0.2, 0),
+    time bounds (0, 1)), an emissive sphere under an AnimatedPrimitive (its
+    AnimatedLight, Light.cpp:338-364), the quad light, the rough glass and
+    metallic spheres, a medium-only sphere and the checker floor and dome;
+    VolPathIntegrator with the PowerLightSampler.  Every ray carries the time
+    its camera sample drew (Camera.hpp:25), through scatter (Material.hpp:264),
+    shadow rays (Integrators.cpp:433, 447) and medium steps (314, 361)."""
+    from .scene import AnimatedPrimitive
+    outside = HomogeneusMedium((0.01, 0.9, 0.9), (1.0, 0.1, 0.1), HenyeyGreenstein(0.75), 0.1)
+    scene = Scene(outside)
+    white = SolidColor((0.9, 0.9, 0.9))
+    green = SolidColor((0.2, 0.3, 0.1))
+    area = AreaLight(QuadShape((0.3, 2.5, 0), (-0.15, 0, 0), (0, 0, -0.15)), (1000.0, 1000.0, 1000.0), False)
+    scene.Add(GeometricPrimitive(area.getShape(), MicrofacetDiffuse((0, 0, 0)), area, None))
+    scene.Add(GeometricPrimitive(QuadShape((-100, -0.3, -100), (1000, 0, 0), (0, 0, 1000)),
+                                 MicrofacetDiffuse(CheckerTexture(white, green, (0.001, 0.001))), None, None))
+    ball = GeometricPrimitive(SphereShape((0, 0.1, -1.2), 0.5), MicrofacetDiffuse((0.1, 0.2, 0.5)), None)
+    scene.Add(AnimatedPrimitive(ball, (0, 0.2, 0), (0, 1)))
+    lamp = AreaLight(SphereShape((0.55, 0.45, -0.5), 0.12), (10.0, 6.0, 3.0), False)
+    scene.Add(AnimatedPrimitive(GeometricPrimitive(lamp.getShape(), MicrofacetDiffuse((0.8, 0.8, 0.8)), lamp),
+                                (-0.6, 0.1, 0.3), (0, 1)))
+    scene.Add(GeometricPrimitive(SphereShape((-1, 0.3, -1), 0.5), MicrofacetDielectric(1.5, 0.15, (1, 1, 1)), None))
+    met = MicrofacetDiffuse(SolidColor((0.8, 0.6, 0.2)), None, SolidColor((0, 0, 0)), SolidColor((1, 1, 1)))
+    scene.Add(GeometricPrimitive(SphereShape((-1, 0, 0.2), 0.5), met, None))
+    scene.Add(GeometricPrimitive(SphereShape((1, 0, -1), 0.5), None, None,
+                                 HomogeneusMedium((0.01, 0.9, 0.9), (1.0, 0.1, 0.1), HenyeyGreenstein(0.8), 5.0)))
+    scene.Add(GeometricPrimitive(SphereShape((0, 0, 0), 10),
+                                 MicrofacetDiffuse(CheckerTexture(white, green, (0.02, 0.02))), None))
+    camera = Camera((0.3, 0.4, 1), (0, 0, 0), 1.7, Film((W, H), MitchellFilter()), (0.0, 1.0))
+    camera.SetMedium(outside)
+    return SceneSetup(scene, camera, "volpath", PowerLightSampler(), max_depth, seed, spp).finish()
+
+
+def motion_path(W: int = 32, H: int = 32, spp: int = 4, max_depth: int = 8, integrator: str = "path",
+                seed: int = 0x5EED0072, shutter=(0.1, 0.9)) -> SceneSetup:
+    """Motion blur on triangles and the pool of lights (PathIntegrator / SimplePathIntegrator):
+    the C2 room, an AnimatedPrimitive Model (a box mesh whose BLAS the rays
+    enter at their own translation), an emissive box Model under an
+    AnimatedPrimitive (one AnimatedLight per emissive triangle), an animated
+    metal sphere whose time bounds (0.25, 1) exercise the clamp of
+    Primitive.cpp:83 (clamp(time - t0, t0, t1)), under a shutter (0.1, 0.9)
+    camera."""
+    from .scene import AnimatedPrimitive
+    scene = Scene()
+    white = MicrofacetDiffuse((0.73, 0.73, 0.73))
+    red = MicrofacetDiffuse((0.65, 0.05, 0.05))
+    green = MicrofacetDiffuse((0.12, 0.45, 0.15))
+    walls = [
+        (_quad_tris((-1, -1, 1), (1, -1, 1), (1, -1, -1), (-1, -1, -1)), white),
+        (_quad_tris((-1, 1, -1), (1, 1, -1), (1, 1, 1), (-1, 1, 1)), white),
+        (_quad_tris((-1, -1, -1), (1, -1, -1), (1, 1, -1), (-1, 1, -1)), white),
+        (_quad_tris((-1, -1, 1), (-1, -1, -1), (-1, 1, -1), (-1, 1, 1)), red),
+        (_quad_tris((1, -1, -1), (1, -1, 1), (1, 1, 1), (1, 1, -1)), green),
+    ]
+    scene.Add(Model([Mesh(i, v, None, n, uv, m) for (i, v, n, uv), m in walls]))
+    light = AreaLight(QuadShape((-0.25, 0.999, -0.25), (0.5, 0, 0), (0, 0, 0.5)), (12.0, 10.0, 8.0), False)
+    scene.Add(GeometricPrimitive(light.getShape(), MicrofacetDiffuse((0.78, 0.78, 0.78)), light))
+    bi, bv, bn, buv = _box((-0.35, -0.55, -0.2), (0.4, 0.9, 0.4), 0.3)
+    crate = Model([Mesh(bi, bv, None, bn, buv, MicrofacetDiffuse(SolidColor((0.9, 0.5, 0.2)), None,
+                                                                 SolidColor((0.4, 0.4, 0.4)), SolidColor((0, 0, 0))))])
+    scene.Add(AnimatedPrimitive(crate, (0.5, 0.0, 0.15), (0, 1)))
+    li, lv, ln, luv = _box((0.4, 0.3, -0.3), (0.12, 0.12, 0.12), -0.4)
+    lamp = Model([Mesh(li, lv, None, ln, luv, MicrofacetDiffuse((0.8, 0.8, 0.8)), SolidColor((4.0, 3.0, 1.5)))])
+    scene.Add(AnimatedPrimitive(lamp, (-0.3, -0.5, 0.2), (0, 1)))
+    ball = GeometricPrimitive(SphereShape((0.35, -0.8, 0.4), 0.2), SpecularConductor((0.9, 0.85, 0.8)))
+    scene.Add(AnimatedPrimitive(ball, (0, 0.35, -0.2), (0.25, 1.0)))
+    camera = Camera((0, 0, 3.7), (0, 0, 0), 0.75, Film((W, H), MitchellFilter()), shutterBounds=shutter)
+    ls = None if integrator == "simple" else PowerLightSampler()
+    return SceneSetup(scene, camera, integrator, ls, max_depth, seed, spp).finish()

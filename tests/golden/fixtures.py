@@ -54,12 +54,22 @@ def parity_scenes():
         # exact-t ties across BLAS hops in one TLAS leaf (three identical
         # Models): the reference's recursion order decides which one is hit
         "tie_models": lambda: scenes.tie_models(W=32, H=32, spp=4),
+        # ... inside three coincident instances (TransformedPrimitive): a ray
+        # meets the tie again in each instance it enters
+        "tie_instances": lambda: scenes.tie_instances(W=32, H=32, spp=4),
         # emitters inside instances: TransformedLight / AnimatedLight
         # (Light.cpp:300-364) for an emissive Model, a quad and a sphere light
         "lit_instances": lambda: scenes.lit_instances(W=32, H=32, spp=4),
         # every deterministic alpha source (the traversal's alpha records):
         # RGB / one-channel / solid alpha textures, an RGBA albedo's alpha
         "alpha_maps": lambda: scenes.alpha_maps(W=32, H=32, spp=4),
+        # motion blur: a shutter camera's ray time (Camera.hpp:16-25) through
+        # AnimatedPrimitive / AnimatedLight (Primitive.cpp:76-96,
+        # Light.cpp:338-364): NoModel-lite under VolPath, and a triangle /
+        # light-pool variant under Path and SimplePath
+        "motion_blur": lambda: scenes.motion_blur(W=32, H=32, spp=4),
+        "motion_path": lambda: scenes.motion_path(W=32, H=32, spp=4),
+        "motion_simple": lambda: scenes.motion_path(W=32, H=32, spp=4, integrator="simple", seed=0x5EED0073),
     }
 
 

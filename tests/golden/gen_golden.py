@@ -139,7 +139,14 @@ def gen(name, setup, rng, tmp: Path):
     res["pick_owner"] = np.array(picks)
     rays = random_rays(setup, 2048, rng)
     rays.tofile(d / "rays.bin")
-    harness(recipe, "trace", out, d / "rays.bin")
+    sh = getattr(setup.camera, "shutter", None)
+    if sh is not None:  # a shutter scene: each ray at its own time in the shutter (and past it)
+        times = (float(sh[0]) + (rng.random(rays.shape[0]) * 1.2 - 0.1) * float(sh[1] - sh[0])).astype(np.float32)
+        times.tofile(d / "times.bin")
+        harness(recipe, "trace", out, d / "rays.bin", d / "times.bin")
+        res["ray_times"] = times
+    else:
+        harness(recipe, "trace", out, d / "rays.bin")
     res["rays"] = rays
     res["hits"] = np.fromfile(f"{out}.hits.bin", np.float32).reshape(-1, 16)
     res["hit_ids"] = np.fromfile(f"{out}.ids.bin", np.int32).reshape(-1, 3)

@@ -102,3 +102,105 @@ def test_render_frame_validates_the_film():
         render_frame(integ, torch.zeros((16, 24, 4), dtype=torch.float32), render_shard=lambda i, n, f: {})
     with pytest.raises(ValueError):  # the HIP path needs device memory
         render_frame(integ, torch.zeros((16, 24, 4), dtype=torch.float64))
+
+
+# ---------------------------------------------------------------- init_film_comm's agreement steps
+class _StubCtx:
+    """Stands in for the library context: records the calls init_film_comm
+    makes, fails comm_init_rank on the ranks told to."""
+
+    def __init__(self, fail: bool, joined: int = 0):
+        self.fail = fail
+        self.comm_ranks = joined
+        self.calls = []
+
+    def comm_init_rank(self, n, rank, uid):
+        self.calls.append(("init", n, rank, uid))
+        if self.fail:
+            raise RuntimeError("stub: RCCL refused")
+        self.comm_ranks = n
+
+    def comm_destroy(self):
+        self.calls.append(("destroy",))
+        self.comm_ranks = 0
+
+
+class _StubIntegrator:
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def context(self, device):
+        return self.ctx
+
+
+def _comm_worker(rank, world, port, fail_ranks, joined, q):
+    import torch.distributed as dist
+    from pathtracing_amd import distributed
+    from pathtracing_amd.integrator import Context
+
+    # rank 0's id comes from the stub, not from RCCL (no GPU here)
+    Context.comm_unique_id = staticmethod(lambda: bytes(range(128)))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ctx = _StubCtx(rank in fail_ranks, joined)
+        ok = distributed.init_film_comm(_StubIntegrator(ctx), 0)
+        q.put((rank, ok, ctx.calls, ctx.comm_ranks))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_comm(world, fail_ranks, joined=0):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, world, port, fail_ranks, joined, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        got = sorted(q.get(timeout=120) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    return got
+
+
+@pytest.mark.timeout(180)
+def test_init_film_comm_falls_back_on_every_rank_when_one_rank_fails():
+    """Rank 1's comm_init_rank fails: neither rank hangs, both return False,
+    and the rank whose init succeeded drops its communicator so the frame
+    reduces through torch.distributed on both."""
+    got = _run_comm(2, fail_ranks=(1,))
+    for rank, ok, calls, comm_ranks in got:
+        assert ok is False
+        assert comm_ranks == 0
+        assert calls[0][:3] == ("init", 2, rank) and calls[0][3] == bytes(range(128))
+    assert got[0][2][-1] == ("destroy",)      # rank 0 had joined: dropped
+    assert ("destroy",) not in got[1][2]      # rank 1 never joined
+
+
+@pytest.mark.timeout(180)
+def test_init_film_comm_joins_every_rank_with_rank0s_id():
+    got = _run_comm(2, fail_ranks=())
+    for rank, ok, calls, comm_ranks in got:
+        assert ok is True and comm_ranks == 2
+        assert calls == [("init", 2, rank, bytes(range(128)))]
+
+
+@pytest.mark.timeout(180)
+def test_init_film_comm_all_already_joined_is_a_no_op():
+    got = _run_comm(2, fail_ranks=(0, 1), joined=2)
+    for rank, ok, calls, comm_ranks in got:
+        assert ok is True and comm_ranks == 2 and calls == []
+
+
+@pytest.mark.timeout(180)
+def test_init_film_comm_drops_a_stale_communicator_before_rejoining():
+    """Every rank holds a communicator of another size (a stale one): it is
+    destroyed first, then the ranks join afresh."""
+    got = _run_comm(2, fail_ranks=(), joined=3)
+    for rank, ok, calls, comm_ranks in got:
+        assert ok is True and comm_ranks == 2
+        assert calls == [("destroy",), ("init", 2, rank, bytes(range(128)))]

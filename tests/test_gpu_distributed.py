@@ -133,3 +133,62 @@ def test_multi_device_context_path_on_one_gpu(monkeypatch, adaptive):
         assert st1["n_devices"] == 1 and st1["paths"] == st0["paths"] and st1["stack_overflows"] == 0
     finally:
         ctx.close()
+
+
+# ---------------------------------------------------------------- bench's nccl path at N = 1
+def _nccl_worker(port, fake_polls, q):
+    import torch.distributed as dist
+    from pathtracing_amd.distributed import init_film_comm, render_frame
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        setup = _setup()
+        integ = setup.make_integrator()
+        W, H = setup.camera.GetFilm().Resolution()
+        # rank 0's id, broadcast_object_list, _agree on CUDA tensors, pt_comm_init_rank
+        ok = init_film_comm(integ, 0)
+        ctx = integ.context(0)
+        joined = ctx.comm_ranks
+        film = torch.zeros((H, W, 4), dtype=torch.float64, device="cuda:0")
+        st = render_frame(integ, film)
+        before = film.clone()
+        # the reduce on the library's own communicator; PT_COMM_FAKE_INPROGRESS
+        # makes its enqueue and the first polls report ncclInProgress (what a
+        # non-blocking communicator may return): waited for, not an error
+        os.environ["PT_COMM_FAKE_INPROGRESS"] = str(fake_polls)
+        ctx.film_reduce(film.data_ptr(), film.numel(), 0)
+        torch.cuda.synchronize()
+        q.put((ok, joined, st["paths"], torch.equal(film, before), film.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("fake_polls", [0, 25])
+def test_init_film_comm_over_nccl_one_rank(fake_polls):
+    """bench.py's nccl path at N = 1: init_process_group("nccl", device_id=...),
+    init_film_comm (id broadcast, agreement on CUDA tensors, the library's
+    non-blocking communicator), render_frame into a device film, then the
+    library's film reduce; the film equals the one-process render."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), fake_polls, q))
+    p.start()
+    try:
+        ok, joined, paths, unchanged, film = q.get(timeout=200)
+    finally:
+        p.join(timeout=60)
+    assert p.exitcode == 0
+    assert ok is True and joined == 1 and unchanged
+    setup = _setup()
+    integ = setup.make_integrator()
+    W, H = setup.camera.GetFilm().Resolution()
+    one = torch.zeros((H, W, 4), dtype=torch.float64, device="cuda:0")
+    torch.cuda.synchronize()
+    st = integ.Render(film_ptr=one.data_ptr())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(film, one.cpu().numpy())
+    assert paths == st["paths"] == W * H * setup.spp

@@ -38,6 +38,8 @@ def case(request):
 def _rays(fx):
     rays = np.zeros(fx["rays"].shape[0], dtype=N.RAY)
     rays["o"], rays["d"], rays["tmax"] = fx["rays"][:, :3], fx["rays"][:, 3:6], fx["rays"][:, 6]
+    if "ray_times" in fx:  # a shutter scene's rays, each at its own time
+        rays["time"] = fx["ray_times"]
     return rays
 
 
@@ -339,6 +341,11 @@ def test_gpu_frame_samples_are_the_oracle_li(W, H, shard):
     got = ctx.frame_samples(pix, smp)
     want, _ = oracle.li_pairs(integ, pix, smp)
     _li_bits(got, want, f"frame_samples/{W}x{H}_{shard[0]}of{shard[1]}")
+    # one chunk holds the whole frame here: the range is the shard's samples
+    own = np.arange(shard[0], 7, shard[1])
+    assert ctx.frame_sample_range() == (int(own[0]), int(own[-1]))
+    with pytest.raises(N.NativeError):  # a pixel past the film (the tiled work order pads it)
+        ctx.frame_samples(np.array([W * H], np.uint32), np.array([shard[0]], np.uint32))
     if shard[1] > 1:
         with pytest.raises(N.NativeError):
             ctx.frame_samples(np.array([0], np.uint32), np.array([shard[0] + 1], np.uint32))
@@ -665,3 +672,23 @@ def test_gpu_envmap_matches_oracle(integrator):
     integ.Render()
     ref, _ = oracle.render(integ, threads=4)
     _film_close(film.accum, ref, 1.0, f"film_oracle/envmap_{integrator}")
+
+
+def test_gpu_frame_sample_range_of_a_multi_chunk_frame(monkeypatch):
+    """A frame rendered in several sample chunks keeps only the last one:
+    pt_frame_sample_range names it, frame_samples serves it (bit-exact against
+    the oracle) and refuses the earlier chunks' samples (bench.py's check draws
+    its pairs from the range)."""
+    monkeypatch.setenv("PT_SAMPLE_CHUNK", "2")
+    setup = scenes.cornell(W=24, H=16, spp=9, config="c3")
+    integ = setup.make_integrator()
+    setup.camera.GetFilm().Clear()
+    integ.Render(shard_index=1, shard_count=2)  # local samples 1, 3 | 5, 7
+    ctx = integ.context()
+    assert ctx.frame_sample_range() == (5, 7)
+    pix = np.arange(0, 24 * 16, 7, dtype=np.uint32)
+    smp = np.where(np.arange(pix.size) % 2 == 0, 5, 7).astype(np.uint32)
+    want, _ = oracle.li_pairs(integ, pix, smp)
+    _li_bits(ctx.frame_samples(pix, smp), want, "frame_samples/multi_chunk")
+    with pytest.raises(N.NativeError):
+        ctx.frame_samples(pix[:1], np.array([3], np.uint32))

@@ -15,6 +15,7 @@ import pytest
 
 import oracle
 from fixtures import GOLDEN as GOLDEN_DIR, NAMES, RANDOM_INTEGRAL, load, rescaled_reference_film
+from pathtracing_amd import native as N
 from pathtracing_amd.scene import (AreaLight, DistantLight, FunctionInfiniteLight, PointLight, TransformedLight,
                                    TransformedPrimitive, UniformInfiniteLight)
 
@@ -115,8 +116,10 @@ def test_light_sampler_picks(case):
 def test_oracle_trace_matches_reference(case):
     name, setup, integ, fx = case
     flat = integ.flat
-    rays = np.zeros(fx["rays"].shape[0], dtype=[("o", "<f4", 3), ("d", "<f4", 3), ("tmax", "<f4")])
+    rays = np.zeros(fx["rays"].shape[0], dtype=N.RAY)
     rays["o"], rays["d"], rays["tmax"] = fx["rays"][:, :3], fx["rays"][:, 3:6], fx["rays"][:, 6]
+    if "ray_times" in fx:  # a shutter scene's rays, each at its own time
+        rays["time"] = fx["ray_times"]
     got = oracle.trace(flat, rays, any_hit=False)
     ref = fx["hits"]
     hit_ref = ref[:, 0] > 0
