@@ -37,13 +37,38 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
-# chip-wide rate of random row gathers served by the XCDs' L2s
-# (MI355X_MICROARCH.md "Indexed rows": 16.8-18.8 TB/s, lower bounds): the
-# ceiling of a kernel whose reads are L2 hits (its "l2-latency" bound)
-L2_GATHER_PEAK_GBS = 18800.0
+MI355X_CUS = 256
+CLOCK_GHZ = 2.4  # the engine clock GRBM_GUI_ACTIVE shows under load
+
+
+def gather_ceiling(pattern: str = "P3", level: str = "L2") -> dict:
+    """The measured ceiling of the traversal's access pattern: a dependent
+    random gather per lane, three 16-B loads of one 48-B record per step (P3,
+    the PT_Q48 node / slot read), on an L2-resident table -- tools/gather_rate.hip
+    on one MI355X, committed as profiles/r05_gather_rate.json.  The vector
+    memory pipe takes about one lane address per clock per CU whatever the
+    occupancy; in GB/s at 16 B per lane-load."""
+    path = ROOT / "profiles" / "r05_gather_rate.json"
+    prof = json.loads(path.read_text()) if path.exists() else {}
+    rates = [r["lane_loads_per_clk_cu"] for r in prof.get("rows", [])
+             if r.get("pattern") == pattern and r.get("level") == level]
+    if not rates:
+        return {}
+    lpc = max(rates)
+    return {"pattern": f"{pattern} {level}", "lane_loads_per_clk_cu": lpc,
+            "gbs_at_16B": round(lpc * 16 * MI355X_CUS * CLOCK_GHZ, 1), "source": "profiles/r05_gather_rate.json"}
+
+
+# the chip-wide ceiling of a kernel whose reads are L2 hits (its "l2-latency"
+# bound): the measured gather rate of the traversal's own access pattern
+L2_GATHER_PEAK_GBS = (lambda g: g.get("gbs_at_16B") or 14150.0)(gather_ceiling())
 # configurations whose BVH + primitive slots exceed the 256 MiB Infinity Cache:
 # their traversal bytes stream from HBM.  The small scenes live in L2/MALL.
 HBM_CONFIGS = ("c4",)
+# bytes a node step reads: the PT_Q48 record (the default pool traversal,
+# pt_device.h), the 64-B quantized node (PT_Q48=0 builds), the reference's
+# 128-B cluster (full nodes)
+NODE_BYTES = {"q48": 48.0, "q64": 64.0, "full": 128.0}
 
 
 def build_setup(config: str, spp: int | None = None, res: str | None = None):
@@ -217,6 +242,12 @@ def pmc_traffic(config: str, spp: int, world: int, kernel: str, sha: str):
             info["l2_hit_rate"] = round(hits / (hits + miss), 3)
         if k.get("avg_us"):
             info["profile_avg_launch_ms"] = round(k["avg_us"] / 1e3, 3)
+            if k.get("SQ_INSTS_VMEM_RD_per_dispatch"):
+                # issued vector-memory lane addresses per clock per CU (every
+                # lane of each wave instruction counted)
+                clk = k["avg_us"] * 1e-6 * CLOCK_GHZ * 1e9 * MI355X_CUS
+                info["issued_lane_loads_per_clk_cu"] = round(64.0 * k["SQ_INSTS_VMEM_RD_per_dispatch"] / clk, 3)
+                info["vmem_rd_insts_per_dispatch"] = round(k["SQ_INSTS_VMEM_RD_per_dispatch"])
         return round(b), info
     info["traffic_note"] = "no counter profile of this workload"
     return None, info
@@ -603,7 +634,9 @@ def roofline(args, setup, world, totals, cst, cpu):
     q = ", true" if quant else ", false"
     kname = f"k_closest_pool<false, false{q}>" if pool else "k_closest<false, false>"
     sname = f"k_shadow_pool<false, false{q}>" if pool else "k_shadow<false, false>"
-    node_bytes = 64.0 if quant else 128.0  # what this kernel's node step reads
+    # the default library reads PT_Q48 records (pt_device.h); PT_Q48=0 tuning
+    # builds (64-B nodes) are A/B variants only
+    node_bytes = NODE_BYTES["q48"] if quant else NODE_BYTES["full"]
     sha = src_sha()
 
     def per_ray(c, n, t, r):
@@ -619,7 +652,7 @@ def roofline(args, setup, world, totals, cst, cpu):
     own_c = per_ray(cst, "nodes_closest", "tris_closest", "rays_closest")
     own_a = per_ray(cst, "nodes_any", "tris_any", "rays_any")
 
-    def entry(name, ref_b, own_b, layout_b, ms, launches, nrays):
+    def entry(name, ref_b, own_b, layout_b, ms, launches, nrays, own_visits=None):
         """frac = algorithmic bytes / launch time / peak, the bytes priced on
         the FEWER of the two visit counts (the reference's order, or the visits
         this kernel makes), so it never credits work the kernel skips."""
@@ -658,16 +691,45 @@ def roofline(args, setup, world, totals, cst, cpu):
             e["layout_bytes_per_ray"] = round(layout_b, 1)
             e["layout_achieved"] = round(gbs(layout_b), 1)
             e["layout_frac"] = round(gbs(layout_b) / peak, 4)
+        # the gather ceiling of this access pattern (measured): the loads the
+        # visits need (three 16-B loads per 48-B record) and the loads the
+        # kernel issues, in lane addresses per clock per CU
+        gc = gather_ceiling()
+        if gc and own_visits and quant:
+            clk = avg_ms * 1e-3 * CLOCK_GHZ * 1e9 * MI355X_CUS
+            useful = 3.0 * own_visits * per_launch / clk
+            e["gather"] = dict(gc, useful_lane_loads_per_clk_cu=round(useful, 3),
+                               useful_frac_of_ceiling=round(useful / gc["lane_loads_per_clk_cu"], 4))
+            if e.get("issued_lane_loads_per_clk_cu"):
+                e["gather"]["issued_lane_loads_per_clk_cu"] = e["issued_lane_loads_per_clk_cu"]
+                e["gather"]["useful_over_issued"] = round(useful / e["issued_lane_loads_per_clk_cu"], 4)
         return e
 
     lb_c = (node_bytes * cst["nodes_closest"] + 48.0 * cst["tris_closest"]) / max(1, cst["rays_closest"]) if cst else None
     lb_a = ((node_bytes * cst["nodes_any"] + 48.0 * cst["tris_any"]) / cst["rays_any"]
             if cst and cst.get("rays_any") else None)
-    rc = entry(kname, ref_c, own_c, lb_c, totals["ms_closest"], totals["launches_closest"], totals["rays_closest"])
-    ra = entry(sname, ref_a, own_a, lb_a, totals["ms_any"], totals["launches_any"], totals["rays_any"])
-    roof = {"bound": rc["bound"] if rc else None, "achieved": rc["achieved"] if rc else None,
-            "peak": rc["peak"] if rc and rc.get("peak") else HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": rc["frac"] if rc else None, "traffic": rc["traffic"] if rc else None,
+    vis_c = (cst["nodes_closest"] + cst["tris_closest"]) / max(1, cst["rays_closest"]) if cst else None
+    vis_a = (cst["nodes_any"] + cst["tris_any"]) / cst["rays_any"] if cst and cst.get("rays_any") else None
+    rc = entry(kname, ref_c, own_c, lb_c, totals["ms_closest"], totals["launches_closest"], totals["rays_closest"],
+               vis_c)
+    ra = entry(sname, ref_a, own_a, lb_a, totals["ms_any"], totals["launches_any"], totals["rays_any"], vis_a)
+    # the headline is north_star's measure: HBM bytes the counters measured per
+    # launch over the HBM peak.  SURVEY 8(d)'s algorithmic bytes stay beside
+    # it (frac_algorithmic, above 1 where the L2 serves what HBM could not),
+    # and the measured gather ceiling of the access pattern under "gather".
+    measured = bool(rc and rc.get("traffic_achieved"))
+    roof = {"bound": rc["bound"] if rc else None,
+            "achieved": (rc["traffic_achieved"] if measured else rc["achieved"]) if rc else None,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": (rc["traffic_frac"] if measured else rc["hbm_frac"]) if rc else None,
+            "traffic": rc["traffic"] if rc else None,
+            "frac_basis": ("rocprofv3 HBM bytes (FETCH_SIZE x calibration + WRITE_SIZE) per launch of this build "
+                           "/ the kernel's average launch time / 8 TB/s" if measured else
+                           "SURVEY 8(d) algorithmic bytes / 8 TB/s (no counter profile of this build)"),
+            "achieved_algorithmic": rc["achieved"] if rc else None,
+            "frac_algorithmic": rc["hbm_frac"] if rc else None,
+            "frac_algorithmic_note": "SURVEY 8(d) bytes (128 B per node, 48 B per primitive) over the HBM peak; "
+                                     "> 1 = served by L2, not skipped work",
             "src_sha": sha,
             "count_source": (f"oracle reference order ({ref_counts['closest']} closest / {ref_counts['any']} any rays)"
                              if ref_counts and ref_counts["closest"] else "gpu")}

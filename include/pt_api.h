@@ -299,6 +299,13 @@ typedef struct pt_render_desc {
     uint32_t paths_in_flight;  /* wavefront size; 0 = library default           */
     uint32_t pixel_begin;      /* render pixels [pixel_begin, pixel_end) only;  */
     uint32_t pixel_end;        /*   0,0 = whole film                            */
+    /* A StratifiedSampler(xSamples, ySamples) host (Sampler.hpp:73-151):
+     * strata[0] * strata[1] == spp stratifies the camera draws of Render's
+     * per-thread clone (pixel, time, lens; Integrators.cpp:39, 61-64) --
+     * stratum PermutationElement(i, spp, Hash(px, py, dimension)) of sample
+     * index i within the pixel's round (Util.hpp:45-73, 160-168), jittered
+     * by the stream's draw; 0,0 = the plain stream */
+    uint32_t strata[2];
 } pt_render_desc;
 
 typedef struct pt_stats {

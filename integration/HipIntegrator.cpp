@@ -135,6 +135,8 @@ PT_MEMBER(CamDefocus, Camera, float, defocusRadius);
 PT_MEMBER(CamFocusDist, Camera, float, FocusDistance);
 PT_MEMBER(CamFocusAngle, Camera, float, FocusAngle);
 PT_MEMBER(CamShutterStart, Camera, float, shutterStart);
+PT_MEMBER(StratX, StratifiedSampler, unsigned int, xSamples);
+PT_MEMBER(StratY, StratifiedSampler, unsigned int, ySamples);
 PT_MEMBER(CamShutterEnd, Camera, float, shutterEnd);
 PT_MEMBER(FilmFilter, Film, std::shared_ptr<Filter>, filter);
 PT_MEMBER(MitB, MitchellFilter, double, b);
@@ -821,7 +823,8 @@ public:
     // one host thread per GPU and reduces the per-GPU films with ncclReduce
     // onto the first GPU; the result is merged into the Film once
     // (Film::Merge, Film.hpp:125-132).
-    void render(const Camera& cam, uint32_t integrator, uint32_t spp, uint32_t depth, uint32_t seed, bool adaptive) {
+    void render(const Camera& cam, uint32_t integrator, uint32_t spp, uint32_t depth, uint32_t seed, bool adaptive,
+                std::array<uint32_t, 2> strata = {0u, 0u}) {
         const pt_camera_desc cd = camera_desc(cam, flat);
         const auto film = cam.GetFilm();
         const glm::ivec2 res = film->Resolution();
@@ -833,6 +836,8 @@ public:
         rd.seed = seed;
         filter_desc(*film, rd);
         rd.shard_count = 1;
+        rd.strata[0] = strata[0];
+        rd.strata[1] = strata[1];
         last.assign(4 * npx, 0.0);
         pt_stats st{};
         auto t0 = std::chrono::steady_clock::now();
@@ -912,6 +917,13 @@ static uint32_t seed_of(const std::shared_ptr<Sampler>& s) {
     if (auto* p = dynamic_cast<const PCGSampler*>(s.get())) return p->Seed();
     return 0x5EED0001u;
 }
+// the camera strata of a StratifiedSampler host (Sampler.hpp:73-151), or of a
+// PCGSampler given strata; {0, 0}: the plain stream
+static std::array<uint32_t, 2> strata_of(const std::shared_ptr<Sampler>& s) {
+    if (auto* st = dynamic_cast<const StratifiedSampler*>(s.get())) return {PT_GET(*st, StratX), PT_GET(*st, StratY)};
+    if (auto* p = dynamic_cast<const PCGSampler*>(s.get())) return {p->StrataX(), p->StrataY()};
+    return {0u, 0u};
+}
 
 HipPathIntegrator::HipPathIntegrator(const std::shared_ptr<Scene>& scene, const std::shared_ptr<Camera>& camera,
                                      const std::shared_ptr<Sampler>& sampler,
@@ -924,7 +936,7 @@ void HipPathIntegrator::Render(unsigned int n) const {
     if (!be_) be_ = std::make_unique<HipBackend>();
     be_->ensure(*scene, ls_, n);
     be_->render(*camera, PT_INTEGRATOR_PATH, sampler->SamplesPerPixel(), depth_, seed_of(sampler),
-                adaptive_);
+                adaptive_, strata_of(sampler));
 }
 RenderStats HipPathIntegrator::LastStats() const { return be_ ? be_->stats : RenderStats{}; }
 static const std::vector<double> kEmpty;
@@ -941,7 +953,7 @@ void HipSimplePathIntegrator::Render(unsigned int n) const {
     if (!be_) be_ = std::make_unique<HipBackend>();
     be_->ensure(*scene, nullptr, n);
     be_->render(*camera, PT_INTEGRATOR_SIMPLE, sampler->SamplesPerPixel(), depth_, seed_of(sampler),
-                adaptive_);
+                adaptive_, strata_of(sampler));
 }
 RenderStats HipSimplePathIntegrator::LastStats() const { return be_ ? be_->stats : RenderStats{}; }
 
@@ -956,7 +968,7 @@ void HipVolPathIntegrator::Render(unsigned int n) const {
     if (!be_) be_ = std::make_unique<HipBackend>();
     be_->ensure(*scene, ls_, n, camera->GetMedium());
     be_->render(*camera, PT_INTEGRATOR_VOLPATH, sampler->SamplesPerPixel(), depth_, seed_of(sampler),
-                adaptive_);
+                adaptive_, strata_of(sampler));
 }
 RenderStats HipVolPathIntegrator::LastStats() const { return be_ ? be_->stats : RenderStats{}; }
 const std::vector<double>& HipVolPathIntegrator::LastAccumulation() const { return be_ ? be_->last : kEmpty; }

@@ -20,7 +20,10 @@
 //
 // The sample stream is the counter-based PCG stream of DESIGN.md; use
 // pt::PCGSampler to choose its seed (any other Sampler supplies only its
-// SamplesPerPixel(); the reference's own samplers are unseeded).
+// SamplesPerPixel(); the reference's own samplers are unseeded).  A
+// StratifiedSampler(xSamples, ySamples) -- or a PCGSampler given strata --
+// stratifies the camera draws as Render's per-thread clone of it does
+// (Sampler.hpp:73-151), the stream supplying the jitter.
 // FunctionInfiniteLight is supported when its function is a pt::SkyGradient
 // (the gradient of main.cpp:292-295).  See INTEGRATION.md.
 #pragma once
@@ -52,21 +55,27 @@ struct SkyGradient {
 // key = h(h(seed ^ h(pixel)) + sample), draw = (h(key + 0x9E3779B9*dim) >> 8) * 2^-24
 class PCGSampler : public Sampler {
 public:
-    PCGSampler(unsigned spp, uint32_t seed, int width) : spp_(spp), seed_(seed), width_(width) {}
+    PCGSampler(unsigned spp, uint32_t seed, int width, unsigned strata_x = 0, unsigned strata_y = 0)
+        : spp_(spp), seed_(seed), width_(width), strata_x_(strata_x), strata_y_(strata_y) {}
     unsigned int SamplesPerPixel() const override { return spp_; }
     void StartPixelSample(const glm::ivec2& p, int index) override;
     double get1D() override { return next(); }
     glm::dvec2 get2D() override;
     glm::dvec2 getPixel2D() override { return get2D(); }
     std::array<glm::vec2, 4> get2Dx4f() override;
-    std::shared_ptr<Sampler> Clone() const override { return std::make_shared<PCGSampler>(spp_, seed_, width_); }
+    std::shared_ptr<Sampler> Clone() const override {
+        return std::make_shared<PCGSampler>(spp_, seed_, width_, strata_x_, strata_y_);
+    }
     uint32_t Seed() const { return seed_; }
+    unsigned StrataX() const { return strata_x_; }
+    unsigned StrataY() const { return strata_y_; }
 
 private:
     float next();
     unsigned spp_;
     uint32_t seed_;
     int width_;
+    unsigned strata_x_, strata_y_;  // camera strata (0: the plain stream)
     uint32_t key_ = 0, dim_ = 0;
 };
 

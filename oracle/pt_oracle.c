@@ -1557,6 +1557,7 @@ typedef struct {
     int simple;
     oracle_counters* cnt;
     uint32_t kind; /* PT_INTEGRATOR_* */
+    uint32_t strata_x, strata_y; /* a StratifiedSampler host's camera strata (0: none) */
 } integ_t;
 
 /* PathIntegrator::SampleLd (Integrators.cpp:260-294) */
@@ -1948,17 +1949,93 @@ static v3 li_volpath(const integ_t* I, ray_t ray, int med, rng_t* rng) {
     return out;
 }
 
-/* Camera::GenerateRay (Camera.hpp:21-35) + camera draws (Integrators.cpp:61-64) */
-static ray_t camera_ray(const pt_camera_desc* c, uint32_t x, uint32_t y, rng_t* rng, double* px, double* py) {
+/* StratifiedSampler's camera draws (Sampler.hpp:73-151) on Render's
+ * per-thread clone (Integrators.cpp:39, 61-64): the stratum of sample index i
+ * of the pixel in dimension d is PermutationElement(i, spp, Hash(px, py, d))
+ * (Util.hpp:45-73) with Hash = MurmurHash64A over the 16 bytes {px, py, d}
+ * (Util.hpp:75-168), jittered by the stream's draw of that dimension (the
+ * reference's random_float()). */
+static uint64_t murmur_pxd(uint32_t px, uint32_t py, uint64_t d) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    uint64_t h = 0 ^ (16ull * m);
+    const uint64_t ks[2] = {(uint64_t)px | ((uint64_t)py << 32), d};
+    for (int j = 0; j < 2; j++) {
+        uint64_t k = ks[j];
+        k *= m;
+        k ^= k >> 47;
+        k *= m;
+        h ^= k;
+        h *= m;
+    }
+    h ^= h >> 47;
+    h *= m;
+    h ^= h >> 47;
+    return h;
+}
+static uint32_t permutation_element(uint32_t i, uint32_t l, uint32_t p) {
+    uint32_t w = l - 1;
+    w |= w >> 1;
+    w |= w >> 2;
+    w |= w >> 4;
+    w |= w >> 8;
+    w |= w >> 16;
+    do {
+        i ^= p;
+        i *= 0xe170893du;
+        i ^= p >> 16;
+        i ^= (i & w) >> 4;
+        i ^= p >> 8;
+        i *= 0x0929eb3fu;
+        i ^= p >> 23;
+        i ^= (i & w) >> 1;
+        i *= 1u | p >> 27;
+        i *= 0x6935fa69u;
+        i ^= (i & w) >> 11;
+        i *= 0x74dcb303u;
+        i ^= (i & w) >> 2;
+        i *= 0x9e501cc3u;
+        i ^= (i & w) >> 2;
+        i *= 0xc860a3dfu;
+        i &= w;
+        i ^= i >> 5;
+    } while (i >= l);
+    return (i + p) % l;
+}
+static uint32_t stratum_of(uint32_t x, uint32_t y, uint32_t d, uint32_t idx, uint32_t spp) {
+    return permutation_element(idx, spp, (uint32_t)murmur_pxd(x, y, d));
+}
+
+/* Camera::GenerateRay (Camera.hpp:21-35) + camera draws (Integrators.cpp:61-64);
+ * strata_x > 0: a StratifiedSampler(strata_x, strata_y) host, sample index idx
+ * of the pixel's round */
+static ray_t camera_ray(const pt_camera_desc* c, uint32_t x, uint32_t y, rng_t* rng, double* px, double* py,
+                        uint32_t strata_x, uint32_t strata_y, uint32_t idx) {
     float ja = next1(rng), jb = next1(rng);
-    const float tu = next1(rng); /* time */
+    float tu = next1(rng); /* time */
     float l0 = next1(rng), l1 = next1(rng);
+    if (strata_x) {
+        const uint32_t spp = strata_x * strata_y;
+        /* getPixel2D = get2D at dimension 0: (sx + dx) / double(xSamples), in double */
+        uint32_t st = stratum_of(x, y, 0, idx, spp);
+        const double fx = ((int)(st % strata_x) + (double)ja) / (double)strata_x;
+        const double fy = ((int)(st / strata_x) + (double)jb) / (double)strata_y;
+        /* get1D at dimension 2: (stratum + random_float()) / spp, in float */
+        st = stratum_of(x, y, 2, idx, spp);
+        tu = ((float)st + tu) / (float)spp;
+        /* get2D at dimension 3, handed to GenerateRay as a glm::vec2 */
+        st = stratum_of(x, y, 3, idx, spp);
+        l0 = (float)(((int)(st % strata_x) + (double)l0) / (double)strata_x);
+        l1 = (float)(((int)(st / strata_x) + (double)l1) / (double)strata_y);
+        *px = (double)x + fx;
+        *py = (double)y + fy;
+    } else {
+        *px = (double)x + (double)ja;
+        *py = (double)y + (double)jb;
+    }
     /* t = glm::mix(shutterStart, shutterEnd, time) (Camera.hpp:25) as the
      * reference build contracts it: fma(start, 1 - time, time * end); 0 for
      * the cameras without a shutter (their bounds are uninitialised, A.14) */
     const float tm = c->has_shutter ? fmaf(c->shutter[0], 1.0f - tu, rmul(tu, c->shutter[1])) : 0.0f;
-    *px = (double)x + (double)ja;
-    *py = (double)y + (double)jb;
     float pxf = (float)*px, pyf = (float)*py;
     float uc = pxf / (float)c->width;
     float vc = pyf / (float)c->height;
@@ -1988,7 +2065,8 @@ static v3 li_one(const integ_t* I, const pt_camera_desc* cam, uint32_t seed, uin
     rng_t rng;
     rng.key = stream_key(seed, y * (uint32_t)cam->width + x, s);
     rng.dim = 0;
-    ray_t r = camera_ray(cam, x, y, &rng, px, py);
+    ray_t r = camera_ray(cam, x, y, &rng, px, py, I->strata_x, I->strata_y,
+                         I->strata_x ? s % (I->strata_x * I->strata_y) : 0u);
     I->cnt->paths++;
     tl_tex_bytes = 0;
     v3 L;
@@ -2005,7 +2083,8 @@ int oracle_li(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_render
     scene_init(&S, s);
     oracle_counters local;
     memset(&local, 0, sizeof(local));
-    integ_t I = {&S, rd->max_depth, rd->integrator == PT_INTEGRATOR_SIMPLE, cnt ? cnt : &local, rd->integrator};
+    integ_t I = {&S, rd->max_depth, rd->integrator == PT_INTEGRATOR_SIMPLE, cnt ? cnt : &local, rd->integrator,
+                 rd->strata[0], rd->strata[1]};
     size_t k = 0;
     for (uint32_t pix = pb; pix < pe; pix++) {
         uint32_t x = pix % (uint32_t)cam->width, y = pix / (uint32_t)cam->width;
@@ -2034,7 +2113,8 @@ int oracle_li_pairs(const pt_scene_desc* s, const pt_camera_desc* cam, const pt_
     scene_init(&S, s);
     oracle_counters local;
     memset(&local, 0, sizeof(local));
-    integ_t I = {&S, rd->max_depth, rd->integrator == PT_INTEGRATOR_SIMPLE, cnt ? cnt : &local, rd->integrator};
+    integ_t I = {&S, rd->max_depth, rd->integrator == PT_INTEGRATOR_SIMPLE, cnt ? cnt : &local, rd->integrator,
+                 rd->strata[0], rd->strata[1]};
     for (uint32_t i = 0; i < n; i++) {
         const uint32_t x = pix[i] % (uint32_t)cam->width, y = pix[i] / (uint32_t)cam->width;
         double px, py;
@@ -2219,7 +2299,8 @@ static void* render_worker(void* arg) {
     scene_init(&S, J->s);
     oracle_counters c;
     memset(&c, 0, sizeof(c));
-    integ_t I = {&S, J->rd->max_depth, J->rd->integrator == PT_INTEGRATOR_SIMPLE, &c, J->rd->integrator};
+    integ_t I = {&S, J->rd->max_depth, J->rd->integrator == PT_INTEGRATOR_SIMPLE, &c, J->rd->integrator,
+                 J->rd->strata[0], J->rd->strata[1]};
     int W = J->cam->width, H = J->cam->height;
     double inv_int = 1.0 / filter_integral(J->rd);
     int rx = (int)ceilf(J->rd->filter_radius[0] - 0.5f), ry = (int)ceilf(J->rd->filter_radius[1] - 0.5f);

@@ -74,6 +74,12 @@ static inline float draw_float(uint32_t key, uint32_t dim) {
 // fresh random state each round).
 class DetSampler;
 static thread_local DetSampler* g_stream = nullptr;  // the sampler of the sample being traced on this thread
+// "strata XS YS" in the recipe: a StratifiedSampler(XS, YS) host.  Its camera
+// draws (Integrators.cpp:61-64 on Render's per-thread clone) are the
+// reference's strata -- PermutationElement(sampleIndex, spp, Hash(px, py,
+// dimension)), Sampler.hpp:93-139, Util.hpp:45-73, 160-168 -- with the stream's
+// draws as the jitter (the reference's is random_float()).
+static unsigned g_strata_x = 0, g_strata_y = 0;
 class DetSampler : public Sampler, public std::enable_shared_from_this<DetSampler> {
 public:
     DetSampler(unsigned spp, uint32_t seed, int width, bool rounds = false)
@@ -93,10 +99,29 @@ public:
         }
         key = stream_key(seed, pix, smp);
         dim = 0;
+        spx = (unsigned)p.x;
+        spy = (unsigned)p.y;
+        sidx = (uint64_t)index;
         g_stream = this;
     }
-    double get1D() override { return next(); }
+    double get1D() override {
+        if (g_strata_x && dim == 2) {  // the camera's time draw: StratifiedSampler::get1D (Sampler.hpp:93-97)
+            const uint64_t sd = Hash(spx, spy, (uint64_t)dim);
+            const uint64_t stratum = PermutationElement(sidx, SamplesPerPixel(), sd);
+            return (stratum + next()) / (SamplesPerPixel());
+        }
+        return next();
+    }
     glm::dvec2 get2D() override {
+        if (g_strata_x && (dim == 0 || dim == 3)) {  // pixel / lens: StratifiedSampler::get2D (Sampler.hpp:99-112)
+            const uint64_t sd = Hash(spx, spy, (uint64_t)dim);
+            const uint64_t stratum = PermutationElement(sidx, SamplesPerPixel(), sd);
+            const int sx = stratum % g_strata_x;
+            const int sy = stratum / g_strata_x;
+            const double dx = next();
+            const double dy = next();
+            return {(sx + dx) / double(g_strata_x), (sy + dy) / double(g_strata_y)};
+        }
         double a = next();
         double b = next();
         return {a, b};
@@ -133,6 +158,8 @@ private:
     uint32_t round = 0, pix = 0, smp = 0;
     uint32_t key = 0;
     uint32_t dim = 0;
+    unsigned spx = 0, spy = 0;  // StratifiedSampler's px, py, sampleIndex
+    uint64_t sidx = 0;
 };
 
 
@@ -498,6 +525,8 @@ static void read_recipe(World& w, const std::string& path) {
             s >> w.integ >> w.maxDepth;
         } else if (k == "sampler") {
             s >> w.seed >> w.spp;
+        } else if (k == "strata") {
+            s >> g_strata_x >> g_strata_y;
         }
     }
 }
@@ -1048,7 +1077,7 @@ static void cmd_tonemap(const std::string& out, const std::string& inPath, int W
 // reference-built scene (integration/HipIntegrator.hpp), Render(gpus) into the
 // reference Film; dumps the merged accumulation like `film`.
 static void cmd_hip(World& w, const std::string& out, unsigned gpus, bool adaptive, bool with_ref) {
-    auto sampler = std::make_shared<pt::PCGSampler>(w.spp, w.seed, w.W);
+    auto sampler = std::make_shared<pt::PCGSampler>(w.spp, w.seed, w.W, g_strata_x, g_strata_y);
     std::vector<double> acc;
     std::vector<uint32_t> counts;
     auto go = [&](auto& integ) {

@@ -108,6 +108,7 @@ struct RenderParams {
     double fparam[2];
     double inv_integral;
     double gauss_x, gauss_y;
+    uint32_t strata_x, strata_y;    // a StratifiedSampler host's camera strata (pt_render_desc::strata)
 };
 
 template <bool COUNT, bool INST>

@@ -625,21 +625,101 @@ __device__ __forceinline__ void work_pixel(const RenderParams& R, uint32_t pix_i
     }
 }
 
+// StratifiedSampler's camera draws (Sampler.hpp:73-151) on Render's
+// per-thread clone (Integrators.cpp:39, 61-64): the stratum of the pixel's
+// sample index i in dimension d is PermutationElement(i, spp, Hash(px, py, d))
+// (Util.hpp:45-73; Hash = MurmurHash64A over the 16 bytes {px, py, d},
+// Util.hpp:75-168), jittered by the stream's draw (the reference's
+// random_float()).  Three per camera sample; the integer work is negligible
+// beside the traversal.
+__device__ __forceinline__ uint64_t murmur_pxd(uint32_t px, uint32_t py, uint64_t d) {
+    const uint64_t m = 0xc6a4a7935bd1e995ull;
+    uint64_t h = 16ull * m;
+    const uint64_t ks[2] = {(uint64_t)px | ((uint64_t)py << 32), d};
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        uint64_t k = ks[j] * m;
+        k ^= k >> 47;
+        k *= m;
+        h ^= k;
+        h *= m;
+    }
+    h ^= h >> 47;
+    h *= m;
+    h ^= h >> 47;
+    return h;
+}
+__device__ __forceinline__ uint32_t permutation_element(uint32_t i, uint32_t l, uint32_t p) {
+    uint32_t w = l - 1;
+    w |= w >> 1;
+    w |= w >> 2;
+    w |= w >> 4;
+    w |= w >> 8;
+    w |= w >> 16;
+    do {
+        i ^= p;
+        i *= 0xe170893du;
+        i ^= p >> 16;
+        i ^= (i & w) >> 4;
+        i ^= p >> 8;
+        i *= 0x0929eb3fu;
+        i ^= p >> 23;
+        i ^= (i & w) >> 1;
+        i *= 1u | p >> 27;
+        i *= 0x6935fa69u;
+        i ^= (i & w) >> 11;
+        i *= 0x74dcb303u;
+        i ^= (i & w) >> 2;
+        i *= 0x9e501cc3u;
+        i ^= (i & w) >> 2;
+        i *= 0xc860a3dfu;
+        i &= w;
+        i ^= i >> 5;
+    } while (i >= l);
+    return (i + p) % l;
+}
+__device__ __forceinline__ uint32_t stratum_of(uint32_t x, uint32_t y, uint32_t d, uint32_t idx, uint32_t spp) {
+    return permutation_element(idx, spp, (uint32_t)murmur_pxd(x, y, d));
+}
+
 // Camera::GenerateRay (Camera.hpp:21-35) with the camera draws of
-// TileIntegrator::Render (Integrators.cpp:61-64): pixel2D, time, lens2D.
+// TileIntegrator::Render (Integrators.cpp:61-64): pixel2D, time, lens2D;
+// sx > 0: a StratifiedSampler(sx, sy) host, idx the sample's index in its
+// pixel's round.
 __device__ __forceinline__ void camera_ray(const pt_camera_desc& c, uint32_t key, uint32_t x, uint32_t y, f3& o, f3& d,
-                                           float& time) {
+                                           float& time, uint32_t sx = 0, uint32_t sy = 0, uint32_t idx = 0) {
     float a = draw(key, 0), b = draw(key, 1);
+    float pxf, pyf;
+    float tu = 0.0f, l0 = 0.0f, l1 = 0.0f;
+    const bool lens = !(c.focus_distance == 0 || c.focus_angle == 0);
+    if (sx) {
+        const uint32_t spp = sx * sy;
+        // getPixel2D at dimension 0: x + (stratum x + dx) / xSamples, in double
+        uint32_t st = stratum_of(x, y, 0, idx, spp);
+        pxf = (float)((double)x + ((double)(int)(st % sx) + (double)a) / (double)sx);
+        pyf = (float)((double)y + ((double)(int)(st / sx) + (double)b) / (double)sy);
+        if (c.has_shutter) {  // get1D at dimension 2: (stratum + u) / spp, in float
+            st = stratum_of(x, y, 2, idx, spp);
+            tu = ((float)st + draw(key, 2)) / (float)spp;
+        }
+        if (lens) {  // get2D at dimension 3, handed over as a glm::vec2
+            st = stratum_of(x, y, 3, idx, spp);
+            l0 = (float)(((double)(int)(st % sx) + (double)draw(key, 3)) / (double)sx);
+            l1 = (float)(((double)(int)(st / sx) + (double)draw(key, 4)) / (double)sy);
+        }
+    } else {
+        pxf = (float)x + a;  // == float(double(x) + a): both round the exact sum
+        pyf = (float)y + b;
+        if (c.has_shutter) tu = draw(key, 2);
+        if (lens) {
+            l0 = draw(key, 3);
+            l1 = draw(key, 4);
+        }
+    }
     // t = glm::mix(shutterStart, shutterEnd, time) (Camera.hpp:25) as
     // TileIntegrator::Render's copy rounds it, fma(start, 1 - u, u * end); a
     // camera without a shutter: 0
-    if (c.has_shutter) {
-        const float u = draw(key, 2);
-        time = fma_(c.shutter[0], 1.0f - u, rmul(u, c.shutter[1]));
-    } else {
-        time = 0.0f;
-    }
-    float pxf = (float)x + a, pyf = (float)y + b;  // == float(double(x) + a): both round the exact sum
+    time = c.has_shutter ? fma_(c.shutter[0], 1.0f - tu, rmul(tu, c.shutter[1])) : 0.0f;
     float uc = pxf / (float)c.width;
     float vc = pyf / (float)c.height;
     f3 U = F3(c.u[0], c.u[1], c.u[2]), Vv = F3(c.v[0], c.v[1], c.v[2]), W = F3(c.w[0], c.w[1], c.w[2]);
@@ -648,12 +728,11 @@ __device__ __forceinline__ void camera_ray(const pt_camera_desc& c, uint32_t key
     f3 dir = normalize(F3(fma_(cb, Vv.x, fma_(ca, U.x, -W.x)), fma_(cb, Vv.y, fma_(ca, U.y, -W.y)),
                           fma_(cb, Vv.z, fma_(ca, U.z, -W.z))));
     f3 org = F3(c.origin[0], c.origin[1], c.origin[2]);
-    if (c.focus_distance == 0 || c.focus_angle == 0) {
+    if (!lens) {
         o = org;
         d = dir;
         return;
     }
-    float l0 = draw(key, 3), l1 = draw(key, 4);
     float r = csqrt(l0);
     float th = 2 * PT_PI * l1;
     float lx = r * cos_cr(th), ly = r * sin_cr(th);
@@ -701,7 +780,8 @@ __device__ __forceinline__ NewSample claim_camera_sample(const RenderParams& R, 
         work_pixel(R, pix_i, x, y);
         const uint32_t s = R.shard_index + (R.s_lo + s_rel) * R.shard_count;
         ns.key = stream_key(R.seed, y * (uint32_t)R.cam.width + x, s);
-        camera_ray(R.cam, ns.key, x, y, ns.o, ns.d, ns.time);
+        camera_ray(R.cam, ns.key, x, y, ns.o, ns.d, ns.time, R.strata_x, R.strata_y,
+                   R.strata_x ? s % (R.strata_x * R.strata_y) : 0u);
     }
     return ns;
 }

@@ -1540,6 +1540,8 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     R.cam = *cam;
     R.seed = rd->seed;
     R.max_depth = rd->max_depth;
+    R.strata_x = rd->strata[0];
+    R.strata_y = rd->strata[1];
     R.shard_count = rd->shard_count ? rd->shard_count : 1;
     R.shard_index = rd->shard_index;
     if (R.shard_index >= R.shard_count) return fail(c, PT_ERR_ARG, "shard_index >= shard_count");
@@ -1941,6 +1943,9 @@ static pt_status check_render_args(pt_ctx* c, const pt_camera_desc* cam, const p
         return fail(c, PT_ERR_ARG, "Lanczos filter: filter_params[1] must hold the filter's Integral()");
     if (cam->medium < -1 || cam->medium >= (int32_t)c->n_media) return fail(c, PT_ERR_ARG, "bad camera medium");
     if (rd->filter_radius[0] <= 0 || rd->filter_radius[1] <= 0) return fail(c, PT_ERR_ARG, "bad filter radius");
+    if ((rd->strata[0] || rd->strata[1]) && (uint64_t)rd->strata[0] * rd->strata[1] != rd->spp)
+        return fail(c, PT_ERR_ARG, "strata %u x %u do not make the %u samples per pixel", rd->strata[0],
+                    rd->strata[1], rd->spp);
     return PT_OK;
 }
 

@@ -6,9 +6,12 @@ SimplePathIntegrator(scene, camera, sampler, maxDepth); Render() fills the
 camera's Film (sum RGB*w, sum w per pixel, Film.hpp:227-253).
 
 The sample stream is the deterministic counter-based PCG stream of DESIGN.md
-(`PCGSampler`); the reference's `UniformSampler` / `StratifiedSampler` names are
-accepted for their samples-per-pixel count (their RNG is unseeded, so no frame
-of theirs is reproducible anyway: SURVEY.md §0.4).
+(`PCGSampler`); the reference's `UniformSampler` name is accepted for its
+samples-per-pixel count (its RNG is unseeded, so no frame of it is
+reproducible anyway: SURVEY.md §0.4).  `StratifiedSampler(xSamples,
+ySamples)` stratifies the camera draws as the reference's does on Render's
+per-thread clone (Sampler.hpp:73-151): pixel, time and lens strata from
+PermutationElement / Hash, the stream as the jitter.
 """
 from __future__ import annotations
 
@@ -40,8 +43,22 @@ class UniformSampler(Sampler):
 
 
 class StratifiedSampler(Sampler):
+    """StratifiedSampler(xSamples, ySamples) (Sampler.hpp:73-151).  Render's
+    camera draws go through its per-thread clone (Integrators.cpp:39, 61-64):
+    sample index i of pixel (px, py) takes the stratum
+    PermutationElement(i, spp, Hash(px, py, dimension)) (Util.hpp:45-73,
+    160-168) of the pixel (dimension 0), time (2) and lens (3) draws, jittered
+    by the stream's draw of that dimension (the reference's random_float()).
+    The path's own draws come from the stream (the reference's Li draws from
+    the integrator's shared sampler)."""
+
     def __init__(self, xSamples: int, ySamples: int, seed: int = 0x5EED0001):
         super().__init__(int(xSamples) * int(ySamples), seed)
+        self.xSamples, self.ySamples = int(xSamples), int(ySamples)
+
+    @property
+    def strata(self) -> tuple[int, int]:
+        return self.xSamples, self.ySamples
 
 
 class Context:
@@ -199,7 +216,7 @@ def get_context(device: int = 0) -> Context:
 
 def render_desc(integrator: int, spp: int, max_depth: int, seed: int, film_filter, shard_index: int = 0,
                 shard_count: int = 1, flags: int = 0, paths_in_flight: int = 0, pixel_begin: int = 0,
-                pixel_end: int = 0) -> N.RenderDesc:
+                pixel_end: int = 0, strata=(0, 0)) -> N.RenderDesc:
     rd = N.RenderDesc()
     rd.integrator = integrator
     rd.spp = int(spp)
@@ -217,6 +234,7 @@ def render_desc(integrator: int, spp: int, max_depth: int, seed: int, film_filte
     rd.paths_in_flight = int(paths_in_flight)
     rd.pixel_begin = int(pixel_begin)
     rd.pixel_end = int(pixel_end)
+    rd.strata[0], rd.strata[1] = int(strata[0]), int(strata[1])
     return rd
 
 
@@ -245,8 +263,13 @@ class Integrator:
 
     def desc(self, **kw) -> tuple[N.CameraDesc, N.RenderDesc]:
         film = self.camera.GetFilm()
-        rd = render_desc(self.kind, kw.pop("spp", self.sampler.SamplesPerPixel()), self.maxDepth,
-                         kw.pop("seed", self.sampler.seed), film.filter, **kw)
+        spp = kw.pop("spp", self.sampler.SamplesPerPixel())
+        # a StratifiedSampler's strata, while its own sample count is rendered
+        strata = getattr(self.sampler, "strata", (0, 0))
+        if strata[0] * strata[1] != spp:
+            strata = (0, 0)
+        rd = render_desc(self.kind, spp, self.maxDepth, kw.pop("seed", self.sampler.seed), film.filter,
+                         strata=kw.pop("strata", strata), **kw)
         return camera_desc(self.camera, self.flat), rd
 
     def Render(self, device: int = 0, shard_index: int = 0, shard_count: int = 1, flags: int = 0,

@@ -114,7 +114,8 @@ class RenderDesc(C.Structure):
     _fields_ = [("integrator", C.c_uint32), ("spp", C.c_uint32), ("max_depth", C.c_uint32), ("seed", C.c_uint32),
                 ("filter", C.c_uint32), ("filter_radius", C.c_float * 2), ("filter_params", C.c_double * 2),
                 ("shard_index", C.c_uint32), ("shard_count", C.c_uint32), ("flags", C.c_uint32),
-                ("paths_in_flight", C.c_uint32), ("pixel_begin", C.c_uint32), ("pixel_end", C.c_uint32)]
+                ("paths_in_flight", C.c_uint32), ("pixel_begin", C.c_uint32), ("pixel_end", C.c_uint32),
+                ("strata", C.c_uint32 * 2)]
 
 
 class Stats(C.Structure):

@@ -56,7 +56,7 @@ def pin_random_lights(setup) -> None:
 
 
 def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: str, max_depth: int,
-                 light_sampler=None, extra_lights: Optional[list] = None, pin: bool = False) -> Path:
+                 light_sampler=None, extra_lights: Optional[list] = None, pin: bool = False, strata=None) -> Path:
     """pin: carry the sky's power and the env map's running cell sums
     (pin_random_lights) so the harness replaces its random estimates."""
     out_dir = Path(out_dir)
@@ -240,6 +240,8 @@ def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: 
         lines.append(f"filter gaussian {_f(flt.radius[0])} {_f(flt.radius[1])} {flt.sigma!r}")
     lines.append(f"integrator {integrator} {max_depth}")
     lines.append(f"sampler {seed} {spp}")
+    if strata:  # a StratifiedSampler(xSamples, ySamples) host (Sampler.hpp:73-151)
+        lines.append(f"strata {int(strata[0])} {int(strata[1])}")
     path = out_dir / "recipe.txt"
     path.write_text("\n".join(lines) + "\n")
     # recipe material index -> object, for mapping fixtures onto flat scenes

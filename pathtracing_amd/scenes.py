@@ -39,6 +39,7 @@ class SceneSetup:
     seed: int
     spp: int
     extra_lights: list = field(default_factory=list)
+    strata: Optional[tuple] = None  # (xSamples, ySamples): a StratifiedSampler host
 
     def finish(self):
         """BuildTlas + LightSampler::Add/PreProcess, as main.cpp:300-306."""
@@ -51,8 +52,12 @@ class SceneSetup:
         return self
 
     def make_integrator(self):
-        from .integrator import PathIntegrator, PCGSampler, SimplePathIntegrator, VolPathIntegrator
-        sampler = PCGSampler(self.spp, self.seed)
+        from .integrator import PathIntegrator, PCGSampler, SimplePathIntegrator, StratifiedSampler, VolPathIntegrator
+        if self.strata:
+            sampler = StratifiedSampler(self.strata[0], self.strata[1], self.seed)
+            assert sampler.SamplesPerPixel() == self.spp
+        else:
+            sampler = PCGSampler(self.spp, self.seed)
         if self.integrator == "simple":
             return SimplePathIntegrator(self.scene, self.camera, sampler, self.max_depth)
         if self.integrator == "volpath":

@@ -70,7 +70,18 @@ def parity_scenes():
         "motion_blur": lambda: scenes.motion_blur(W=32, H=32, spp=4),
         "motion_path": lambda: scenes.motion_path(W=32, H=32, spp=4),
         "motion_simple": lambda: scenes.motion_path(W=32, H=32, spp=4, integrator="simple", seed=0x5EED0073),
+        # a StratifiedSampler host (Sampler.hpp:73-151): the camera's pixel,
+        # lens and time draws stratified as on Render's per-thread clone, the
+        # stream as the jitter -- the thin-lens C3 box, and the shutter scene
+        "stratified": lambda: _strat(scenes.cornell(W=32, H=32, spp=4, config="c3", seed=0x5EED0081,
+                                                    lens=(0.12, 3.2)), (2, 2)),
+        "stratified_motion": lambda: _strat(scenes.motion_path(W=32, H=24, spp=6, seed=0x5EED0082), (3, 2)),
     }
+
+
+def _strat(setup, strata):
+    setup.strata = strata
+    return setup
 
 
 NAMES = list(parity_scenes().keys())

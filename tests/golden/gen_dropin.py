@@ -40,7 +40,7 @@ ADAPTIVE_SCENES = ["example1", "cornell_c3", "zoo", "fog", "instances", "sanmigu
 def pinned_recipe(tmp: Path, setup) -> Path:
     pin_random_lights(setup)
     return write_recipe(tmp, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator, setup.max_depth,
-                        setup.light_sampler, setup.extra_lights, pin=True)
+                        setup.light_sampler, setup.extra_lights, pin=True, strata=setup.strata)
 
 
 def main() -> None:

@@ -105,7 +105,7 @@ def bsdf_cases(n, rng):
 def gen(name, setup, rng, tmp: Path):
     d = tmp / name
     recipe = write_recipe(d, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
-                          setup.max_depth, setup.light_sampler, setup.extra_lights)
+                          setup.max_depth, setup.light_sampler, setup.extra_lights, strata=setup.strata)
     out = d / "o"
     res = {}
     harness(recipe, "bvh", out)
@@ -222,7 +222,8 @@ def gen_resolve(rng, tmp: Path):
     print(f"film_resolve: {(OUT / 'film_resolve.npz').stat().st_size / 1024:.0f} KiB")
 
 
-ADAPTIVE_SCENES = ("cornell_c3", "example1", "example1_simple", "zoo", "fog", "lens_box", "instances", "mitchell2")
+ADAPTIVE_SCENES = ("cornell_c3", "example1", "example1_simple", "zoo", "fog", "lens_box", "instances", "mitchell2",
+                   "stratified", "motion_path")
 
 
 def gen_adaptive(tmp: Path):
@@ -236,7 +237,7 @@ def gen_adaptive(tmp: Path):
         setup, _, _ = load(name)
         d = tmp / f"adaptive_{name}"
         recipe = write_recipe(d, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
-                              setup.max_depth, setup.light_sampler, setup.extra_lights)
+                              setup.max_depth, setup.light_sampler, setup.extra_lights, strata=setup.strata)
         out = d / "o"
         subprocess.run([str(HARNESS), str(recipe), "adaptive", str(out)], check=True, stdout=subprocess.DEVNULL)
         W, H = setup.camera.film.Resolution()

@@ -44,3 +44,71 @@ def test_small_scenes_are_labelled_cache_resident():
     e = _entry(tf=0.01, hit=0.99)
     bench.bound_peak(e, False, True, 20000.0)
     assert e["bound"] == "l2/latency" and e["peak"] == bench.L2_GATHER_PEAK_GBS
+
+
+def test_q48_records_are_priced_at_48_bytes_per_node_step():
+    """The default pool traversal reads PT_Q48 records (pt_device.h): 48 B per
+    node step, as per primitive slot."""
+    assert bench.NODE_BYTES["q48"] == 48.0
+    assert bench.NODE_BYTES["full"] == 128.0
+
+
+def test_gather_ceiling_comes_from_the_committed_microbenchmark(tmp_path, monkeypatch):
+    """bench.gather_ceiling reads profiles/r05_gather_rate.json (tools/gather_rate.hip,
+    parsed by tools/gather_rate_json.py): the best P3 L2 rate in lane-loads per
+    clock per CU, in GB/s at 16 B per lane-load over 256 CUs at 2.4 GHz."""
+    import sys
+    sys.path.insert(0, str(bench.ROOT / "tools"))
+    import gather_rate_json
+    text = ("L2     P3  waves/SIMD 2      1.87 ms     4.48 G wave-steps/s   1.399 lane-loads/clk/CU     1098 clk/step/wave\n"
+            "L2     P3  waves/SIMD 4      3.64 ms     4.61 G wave-steps/s   1.441 lane-loads/clk/CU     2131 clk/step/wave\n"
+            "HBM    P3  waves/SIMD 4      3.23 ms     1.30 G wave-steps/s   0.405 lane-loads/clk/CU     7578 clk/step/wave\n")
+    prof = gather_rate_json.parse(text)
+    assert len(prof["rows"]) == 3
+    (tmp_path / "profiles").mkdir()
+    (tmp_path / "profiles" / "r05_gather_rate.json").write_text(__import__("json").dumps(prof))
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    g = bench.gather_ceiling()
+    assert g["lane_loads_per_clk_cu"] == 1.441
+    assert abs(g["gbs_at_16B"] - 1.441 * 16 * 256 * 2.4) < 0.1
+    assert bench.gather_ceiling("P3", "HBM")["lane_loads_per_clk_cu"] == 0.405
+
+
+def _roof(monkeypatch, traffic_bytes):
+    import types
+    args = types.SimpleNamespace(traversal="auto", config="c4", nodes="auto")
+    setup = types.SimpleNamespace(spp=1024, integrator="path")
+    totals = {"ms_closest": 29 * 121.0, "launches_closest": 29, "rays_closest": 6_857_000_000,
+              "ms_any": 29 * 38.0, "launches_any": 29, "rays_any": 2_000_000_000, "ms_shade": 1205.0}
+    cst = {"nodes_closest": 33.86e9, "tris_closest": 15.57e9, "rays_closest": 1e9,
+           "nodes_any": 21.6e9, "tris_any": 9.0e9, "rays_any": 1e9}
+
+    def fake_pmc(config, spp, world, kernel, sha):
+        if traffic_bytes is None:
+            return None, {"traffic_note": "none"}
+        return traffic_bytes, {"l2_hit_rate": 0.82, "issued_lane_loads_per_clk_cu": 1.9}
+    monkeypatch.setattr(bench, "pmc_traffic", fake_pmc)
+    monkeypatch.setattr(bench, "gather_ceiling", lambda *a: {"pattern": "P3 L2", "lane_loads_per_clk_cu": 1.441,
+                                                             "gbs_at_16B": 14165.0, "source": "test"})
+    return bench.roofline(args, setup, 1, totals, cst, None)
+
+
+def test_headline_frac_is_the_counted_hbm_fraction(monkeypatch):
+    """With a counter profile of the build the headline is north_star's
+    measure (HBM bytes per launch / launch time / 8 TB/s); SURVEY 8(d)'s
+    algorithmic figure stays beside it as frac_algorithmic."""
+    per_launch = 103.6e9
+    roof = _roof(monkeypatch, per_launch)
+    assert roof["peak"] == bench.HBM_PEAK_GBS and roof["unit"] == "GB/s"
+    assert abs(roof["achieved"] - per_launch / 0.121 / 1e9) < 1.0
+    assert abs(roof["frac"] - roof["achieved"] / bench.HBM_PEAK_GBS) < 1e-3
+    assert roof["frac_algorithmic"] > 1.0 and roof["frac"] < 0.2
+    assert roof["node_layout_bytes"] == 48.0
+    g = roof["gather"]
+    assert g["useful_lane_loads_per_clk_cu"] > 0 and g["issued_lane_loads_per_clk_cu"] == 1.9
+
+
+def test_without_counters_the_headline_is_algorithmic_and_says_so(monkeypatch):
+    roof = _roof(monkeypatch, None)
+    assert roof["frac"] == roof["frac_algorithmic"]
+    assert roof["frac_basis"].startswith("SURVEY 8(d) algorithmic")

@@ -33,7 +33,7 @@ def _dropin(name_or_setup, tmp_path, *extra, env=None):
     setup = parity_scenes()[name_or_setup]() if isinstance(name_or_setup, str) else name_or_setup
     pin_random_lights(setup)
     recipe = write_recipe(tmp_path, setup.scene, setup.camera, setup.spp, setup.seed, setup.integrator,
-                          setup.max_depth, setup.light_sampler, setup.extra_lights, pin=True)
+                          setup.max_depth, setup.light_sampler, setup.extra_lights, pin=True, strata=setup.strata)
     out = tmp_path / "o"
     subprocess.run([str(HARNESS), str(recipe), "hip", str(out), "1", "noref", *extra], check=True, timeout=300,
                    env=env)

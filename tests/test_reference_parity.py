@@ -376,3 +376,28 @@ def test_oracle_c4_class_matches_reference_render_statistically():
     L = np.stack([oracle.li(integ, y * W, (y + 1) * W)[0] for y in range(24, 28)])
     ok = z_test(L, ref[24:28])
     assert ok.mean() >= 0.99, f"{ok.mean():.4f} of pixel channels within 4 sigma"
+
+
+@pytest.mark.parametrize("name", ["stratified", "stratified_motion"])
+def test_stratified_camera_draws_fill_every_stratum(name):
+    """A StratifiedSampler(xs, ys) host: each pixel's spp camera samples fall
+    one per pixel stratum (Sampler.hpp:99-112), in the reference's own
+    positions (its getPixel2D, recorded by the harness) and the oracle's, and
+    the unstratified stream does not (a check that the strata take effect)."""
+    setup, integ, fx = load(name)
+    xs, ys = setup.strata
+    W, H = setup.camera.GetFilm().Resolution()
+    _, P, _ = oracle.li(integ)
+    np.testing.assert_array_equal(P.reshape(fx["li_p"].shape), fx["li_p"])
+    x = np.arange(W * H) % W
+    y = np.arange(W * H) // W
+    cx = np.floor((P[..., 0] - x[:, None]) * xs).astype(int)
+    cy = np.floor((P[..., 1] - y[:, None]) * ys).astype(int)
+    cells = np.sort(cy * xs + cx, axis=1)
+    assert (cells == np.arange(xs * ys)[None, :]).all()
+    setup.strata = None
+    _, P0, _ = oracle.li(setup.make_integrator())
+    cx0 = np.floor((P0[..., 0] - x[:, None]) * xs).astype(int)
+    cy0 = np.floor((P0[..., 1] - y[:, None]) * ys).astype(int)
+    full = (np.sort(cy0 * xs + cx0, axis=1) == np.arange(xs * ys)[None, :]).all(1)
+    assert full.mean() < 0.5

@@ -74,12 +74,15 @@ def build_product(force: bool = False, variant: str = "", defines=()) -> Path:
 
 
 def build_tools() -> None:
-    """Measurement helpers run on the GPU box (tools/_bin/, git-ignored)."""
-    src = ROOT / "tools" / "fetch_calib.hip"
-    out = ROOT / "tools" / "_bin" / "fetch_calib"
-    out.parent.mkdir(parents=True, exist_ok=True)
-    if _stale(out, [src]):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", src, "-o", out])
+    """Measurement helpers run on the GPU box (tools/_bin/, git-ignored):
+    the FETCH_SIZE calibration and the gather-rate ceiling of the traversal's
+    access pattern (profiles/r05_gather_rate.json)."""
+    for name in ("fetch_calib", "gather_rate"):
+        src = ROOT / "tools" / f"{name}.hip"
+        out = ROOT / "tools" / "_bin" / name
+        out.parent.mkdir(parents=True, exist_ok=True)
+        if _stale(out, [src]):
+            _run([HIPCC, f"--offload-arch={ARCH}", "-O3", src, "-o", out])
 
 
 def build_oracle() -> Path:
