@@ -744,6 +744,26 @@ __device__ __forceinline__ void camera_ray(const pt_camera_desc& c, uint32_t key
     d = normalize(dir - off);
 }
 
+// FilmTile::Add's pixelSample = glm::fract(p) of a camera sample (Film.hpp:
+// 65-67), recomputed by the film gathers from the sample's stream: the jitter
+// itself (x + a is exact in double), or a StratifiedSampler's stratum +
+// jitter, p = x + (sx + a) / xSamples rounded in double as camera_ray forms it
+__device__ __forceinline__ void sample_fract(const RenderParams& R, uint32_t key, uint32_t x, uint32_t y, uint32_t s,
+                                             double& fx, double& fy) {
+    const float a = draw(key, 0), b = draw(key, 1);
+    if (R.strata_x) {
+        const uint32_t spp = R.strata_x * R.strata_y;
+        const uint32_t st = stratum_of(x, y, 0, s % spp, spp);
+        const double px = (double)x + ((double)(int)(st % R.strata_x) + (double)a) / (double)R.strata_x;
+        const double py = (double)y + ((double)(int)(st / R.strata_x) + (double)b) / (double)R.strata_y;
+        fx = px - floor(px);
+        fy = py - floor(py);
+    } else {
+        fx = (double)a;  // fract(x + a) = a, a in [0,1)
+        fy = (double)b;
+    }
+}
+
 // One new camera sample per `want` lane: a block-aggregated claim of
 // consecutive sample ids (one returning atomic per block: coherent primary
 // rays), then Camera::GenerateRay for the claimed ids below the chunk's end.
@@ -1506,9 +1526,9 @@ __global__ __launch_bounds__(256) void k_gather(RenderParams R, const float* __r
             for (uint32_t k = 0; k < ns; k++) {
                 const uint32_t s = R.shard_index + (R.s_lo + k) * R.shard_count;
                 const uint32_t key = stream_key(R.seed, spix, s);
-                const float a = draw(key, 0), b = draw(key, 1);
                 // FilmTile::Add: pixelSample = fract(p), sample_pos = (o + 0.5) - fract
-                const double fx = (double)a, fy = (double)b;  // fract(x + a) = a, a in [0,1)
+                double fx, fy;
+                sample_fract(R, key, (uint32_t)sx, (uint32_t)sy, s, fx, fy);
                 const double spx = (double)ox + 0.5 - fx, spy = (double)oy + 0.5 - fy;
                 const double w = filter_eval(R, (float)spx, (float)spy) * R.inv_integral;
                 if (w <= 0) continue;
@@ -1578,7 +1598,8 @@ __global__ __launch_bounds__(256) void k_gather_tile(RenderParams R, const float
                 const uint32_t spix = (uint32_t)sy * (uint32_t)W + (uint32_t)sx;
                 const uint32_t s = R.shard_index + (R.s_lo + k) * R.shard_count;
                 const uint32_t key = stream_key(R.seed, spix, s);
-                const double fx = (double)draw(key, 0), fy = (double)draw(key, 1);
+                double fx, fy;
+                sample_fract(R, key, (uint32_t)sx, (uint32_t)sy, s, fx, fy);
 #pragma unroll
                 for (int o = -RAD; o <= RAD; o++) {
                     if (o >= -rx && o <= rx) wx[o + RAD] = filter_1d(R, (float)((double)o + 0.5 - fx), 0);
@@ -1957,7 +1978,8 @@ __global__ __launch_bounds__(256) void k_adapt_gather(RenderParams R, const int3
             any = true;
             for (uint32_t k = 0; k < ns; k++) {
                 const uint32_t key = stream_key(R.seed, spix, R.s_lo + k);
-                const double fx = (double)draw(key, 0), fy = (double)draw(key, 1);
+                double fx, fy;
+                sample_fract(R, key, (uint32_t)sx, (uint32_t)sy, R.s_lo + k, fx, fy);
                 const double spx = (double)ox + 0.5 - fx, spy = (double)oy + 0.5 - fy;
                 const double w = filter_eval(R, (float)spx, (float)spy) * R.inv_integral;
                 if (w <= 0) continue;
