@@ -521,7 +521,8 @@ def main():
             fs = (lambda p, s: hook.frame_samples(setup, p, s)) if hasattr(hook, "frame_samples") else None
         else:
             fs = integ.context(device).frame_samples
-            srange = integ.context(device).frame_sample_range()
+            ctx = integ.context(device)
+            srange = ctx.frame_sample_range() if hasattr(ctx._lib, "pt_frame_sample_range") else None
         sh_i, sh_n = shard if shard else (rank, world)
         verified = verify_frame(setup, integ, sh_i, sh_n, args.verify_pairs if fs else 0, fs,
                                 film if rank == 0 and not shard else None, sample_range=srange)
@@ -719,15 +720,15 @@ def roofline(args, setup, world, totals, cst, cpu):
     # and the measured gather ceiling of the access pattern under "gather".
     measured = bool(rc and rc.get("traffic_achieved"))
     roof = {"bound": rc["bound"] if rc else None,
-            "achieved": (rc["traffic_achieved"] if measured else rc["achieved"]) if rc else None,
+            "achieved": (rc["traffic_achieved"] if measured else rc.get("achieved")) if rc else None,
             "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": (rc["traffic_frac"] if measured else rc["hbm_frac"]) if rc else None,
+            "frac": (rc["traffic_frac"] if measured else rc.get("hbm_frac")) if rc else None,
             "traffic": rc["traffic"] if rc else None,
             "frac_basis": ("rocprofv3 HBM bytes (FETCH_SIZE x calibration + WRITE_SIZE) per launch of this build "
                            "/ the kernel's average launch time / 8 TB/s" if measured else
                            "SURVEY 8(d) algorithmic bytes / 8 TB/s (no counter profile of this build)"),
-            "achieved_algorithmic": rc["achieved"] if rc else None,
-            "frac_algorithmic": rc["hbm_frac"] if rc else None,
+            "achieved_algorithmic": rc.get("achieved") if rc else None,
+            "frac_algorithmic": rc.get("hbm_frac") if rc else None,
             "frac_algorithmic_note": "SURVEY 8(d) bytes (128 B per node, 48 B per primitive) over the HBM peak; "
                                      "> 1 = served by L2, not skipped work",
             "src_sha": sha,

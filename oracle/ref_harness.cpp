@@ -947,8 +947,14 @@ static void cmd_adaptive(World& w, const std::string& out) {
     for (const auto& r : g_adapt) {
         counts[r.pixel]++;
         const uint32_t key = stream_key(w.seed, r.pixel, r.sample);
-        const glm::dvec2 jit{(double)draw_float(key, 0), (double)draw_float(key, 1)};
-        const glm::dvec2 p = glm::dvec2{(double)(r.pixel % w.W), (double)(r.pixel / w.W)} + jit;
+        const unsigned x = r.pixel % w.W, y = r.pixel / w.W;
+        glm::dvec2 jit{(double)draw_float(key, 0), (double)draw_float(key, 1)};
+        if (g_strata_x) {  // the sample's getPixel2D as DetSampler::get2D drew it (round r's index r.sample % spp)
+            const uint64_t stratum = PermutationElement((uint64_t)(r.sample % w.spp), w.spp, Hash(x, y, (uint64_t)0));
+            jit = {((int)(stratum % g_strata_x) + jit.x) / double(g_strata_x),
+                   ((int)(stratum / g_strata_x) + jit.y) / double(g_strata_y)};
+        }
+        const glm::dvec2 p = glm::dvec2{(double)x, (double)y} + jit;
         tile.Add(p, glm::dvec3(r.L[0], r.L[1], r.L[2]));
     }
     std::vector<double> acc((size_t)w.W * w.H * 4);

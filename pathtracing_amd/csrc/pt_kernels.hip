@@ -96,7 +96,7 @@ struct ObjRay {
 __device__ __noinline__ ObjRay anim_object_ray(const DevInstance* I, float time, f3 ro, f3 rd) {
     float T[16], inv[16];
     anim_transform(*I, time, T);
-    m4_inverse(T, inv);
+    anim_inverse(T, inv);
     const f3 dir = m4_dir(inv, rd);
     const float len = length(dir);
     return ObjRay{m4_point(inv, ro), dir / len, len};
@@ -242,11 +242,12 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES_FOR(PT_USES_SPEC(INST
                                                                 unsigned long long* counters, uint32_t* __restrict__ ties) {
     __shared__ uint32_t s_ref[PT_POOL_LDS_C * PT_TRACE_BLOCK];
     __shared__ uint16_t s_ent[PT_ENTRY ? PT_POOL_LDS_C * PT_TRACE_BLOCK : 1];
-    __shared__ __attribute__((aligned(16))) uint8_t s_lut[(QN && PT_Q48) ? 8 * Q48_LUT_STRIDE : 4];
+    constexpr int TREE = PT_USES_SPEC(INST, QN) ? PT_TREELET : 0;
+    __shared__ __attribute__((aligned(16))) uint8_t s_lut[(QN && PT_Q48) ? Q48_LDS_BYTES(TREE) : 4];
     iteration_prologue(nptr, spare, snap);
     const uint32_t n = path_count(nptr);
     if (n == 0) return;
-    if constexpr (QN && PT_Q48) stage_q48_lut(s_lut);
+    if constexpr (QN && PT_Q48) stage_q48_lut<TREE>(s_lut);
     TraceWork wk{0, 0};
     ClosestSrc src{P, hit, nptr[Q_NEXT], ties, pool + (Q_TIES - Q_WORDS)};
     trace_pool<false, COUNT, ClosestSrc, true, INST, PT_POOL_LDS_C, QN>(n, pool, src, s_ref, s_ent, ovf, wk, s_lut);
@@ -337,13 +338,14 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SHADOW_WAVES_FOR(PT_USES_SPEC(IN
                                                                uint32_t* __restrict__ pool, uint32_t* __restrict__ ovf,
                                                                unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_POOL_LDS * PT_TRACE_BLOCK];
-    __shared__ __attribute__((aligned(16))) uint8_t s_lut[(QN && PT_Q48) ? 8 * Q48_LUT_STRIDE : 4];
+    constexpr int TREE = PT_USES_SPEC(INST, QN) ? PT_TREELET_ANY : 0;
+    __shared__ __attribute__((aligned(16))) uint8_t s_lut[(QN && PT_Q48) ? Q48_LDS_BYTES(TREE) : 4];
     TraceWork wk{0, 0};
     using Src = ShadowSrcT<PT_SHADOW_DEFER != 0>;
     Src src{sq, next, sample_L};
     const uint32_t n = *nptr;
     if (n == 0) return;
-    if constexpr (QN && PT_Q48) stage_q48_lut(s_lut);
+    if constexpr (QN && PT_Q48) stage_q48_lut<TREE>(s_lut);
     trace_pool<true, COUNT, Src, true, INST, PT_POOL_LDS, QN>(n, pool, src, s_ref, nullptr, ovf, wk, s_lut);
     if (COUNT) {
         count_add(counters, CNT_NODES_ANY, wk.nodes);

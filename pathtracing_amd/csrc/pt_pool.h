@@ -193,7 +193,7 @@ __device__ __forceinline__ float4 q48_buf_load(__amdgpu_buffer_rsrc_t rs, uint32
 // data is live across the primitive side's out-of-line calls (primitive side
 // first: 13 % slower, spills); a second queued leaf saved 4 % of the
 // iterations and cost 17 % (profiles/r03_ab_spec.txt).
-template <bool ANY, bool COUNT, class Src, int LN>
+template <bool ANY, bool COUNT, class Src, int LN, int TREE = (ANY ? PT_TREELET_ANY : PT_TREELET)>
 __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, uint32_t* s_ref,
                            uint32_t* __restrict__ ovf, TraceWork& wk, const uint8_t* s_lut) {
     const uint32_t lane = threadIdx.x;
@@ -436,10 +436,21 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         // raw buffer loads over the record array: a lane without the step
         // reads past the buffer's end, which returns zeros without a fetch
         // (the runtime keeps the array below 4 GiB in this build)
-        const uint32_t noff = node_step ? ref * 48u : Q48_OOB_OFFSET;
+        // (PT_TREELET: a node in the block's LDS copy of the top records is
+        // read there, its buffer load out of range)
+        const bool tnode = TREE > 0 && node_step && ref < (uint32_t)TREE;
+        const uint32_t noff = (node_step && !tnode) ? ref * 48u : Q48_OOB_OFFSET;
         const uint32_t poff = prim_step ? slot * 48u : Q48_OOB_OFFSET;
-        const float4 q0 = q48_buf_load(qrs, noff), q1 = q48_buf_load(qrs, noff + 16u), q2 = q48_buf_load(qrs, noff + 32u);
+        float4 q0 = q48_buf_load(qrs, noff), q1 = q48_buf_load(qrs, noff + 16u), q2 = q48_buf_load(qrs, noff + 32u);
         const float4 g0 = q48_buf_load(qrs, poff), g1 = q48_buf_load(qrs, poff + 16u), g2 = q48_buf_load(qrs, poff + 32u);
+        if constexpr (TREE > 0) {
+            if (tnode) {
+                const float4* tr = reinterpret_cast<const float4*>(s_lut + Q48_LUT_BYTES) + 3u * ref;
+                q0 = tr[0];
+                q1 = tr[1];
+                q2 = tr[2];
+            }
+        }
 #if PT_SPEC_LEAF2
         const uint32_t poff2 = prim_step ? poff + 48u : Q48_OOB_OFFSET;
         const float4 h0 = q48_buf_load(qrs, poff2), h1 = q48_buf_load(qrs, poff2 + 16u),

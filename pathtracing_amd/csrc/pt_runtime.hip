@@ -61,7 +61,7 @@ struct pt_ctx {
     uint32_t n_materials = 0;
     uint32_t n_media = 0;
     uint32_t trace_blocks = 0;  // resident traversal blocks on this device (persistent grid), max of the two
-    uint32_t blocks_closest = 0, blocks_any = 0;  // per pool kernel
+    uint32_t pool_blocks[2][2][2] = {};  // [any hit][instanced][quantized]: each pool kernel's resident blocks
     uint64_t n_clusters = 0;    // BVH clusters of the uploaded scene (traversal choice)
     bool has_qnodes = false;    // the scene's nodes have a quantized copy (DevQNode)
     int node_format = PT_NODES_AUTO;  // pt_set_node_format
@@ -200,32 +200,36 @@ static pt_status create_dev(pt_ctx** out, int device) {
         }
     }
     {
-        // the persistent (pool) traversal grid: the blocks of the pool kernels
-        // that are resident together (the fewer of closest / any hit)
-        // (instanced variants included)
-        int cus = 0, per_cu[2] = {1 << 30, 1 << 30};
-        const void* pool_kernels[8] = {reinterpret_cast<const void*>(&k_closest_pool<false, false, false>),
-                                       reinterpret_cast<const void*>(&k_shadow_pool<false, false, false>),
-                                       reinterpret_cast<const void*>(&k_closest_pool<false, true, false>),
-                                       reinterpret_cast<const void*>(&k_shadow_pool<false, true, false>),
-                                       reinterpret_cast<const void*>(&k_closest_pool<false, false, true>),
-                                       reinterpret_cast<const void*>(&k_shadow_pool<false, false, true>),
-                                       reinterpret_cast<const void*>(&k_closest_pool<false, true, true>),
-                                       reinterpret_cast<const void*>(&k_shadow_pool<false, true, true>)};
+        // the persistent (pool) traversal grid of each pool kernel: its blocks
+        // that are resident together (a variant's own figure: the instanced
+        // kernels' registers must not shrink the grid of the others); the
+        // overflow stack array covers the largest
+        int cus = 0;
+        const void* pool_kernels[2][2][2] = {
+            {{reinterpret_cast<const void*>(&k_closest_pool<false, false, false>),
+              reinterpret_cast<const void*>(&k_closest_pool<false, false, true>)},
+             {reinterpret_cast<const void*>(&k_closest_pool<false, true, false>),
+              reinterpret_cast<const void*>(&k_closest_pool<false, true, true>)}},
+            {{reinterpret_cast<const void*>(&k_shadow_pool<false, false, false>),
+              reinterpret_cast<const void*>(&k_shadow_pool<false, false, true>)},
+             {reinterpret_cast<const void*>(&k_shadow_pool<false, true, false>),
+              reinterpret_cast<const void*>(&k_shadow_pool<false, true, true>)}}};
         bool ok = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess;
-        for (int k = 0; ok && k < 8; k++) {
-            int b = 0;
-            ok = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, pool_kernels[k], PT_TRACE_BLOCK, 0) == hipSuccess;
-            per_cu[k & 1] = std::min(per_cu[k & 1], b);
-        }
+        c->trace_blocks = 1;
+        for (int a = 0; a < 2; a++)
+            for (int i = 0; i < 2; i++)
+                for (int q = 0; ok && q < 2; q++) {
+                    int b = 0;
+                    ok = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, pool_kernels[a][i][q], PT_TRACE_BLOCK, 0) ==
+                         hipSuccess;
+                    c->pool_blocks[a][i][q] = (uint32_t)std::max(1, cus * std::max(1, b));
+                    c->trace_blocks = std::max(c->trace_blocks, c->pool_blocks[a][i][q]);
+                }
         if (!ok) {
             g_err = "occupancy query failed";
             delete c;
             return PT_ERR_HIP;
         }
-        c->blocks_closest = (uint32_t)std::max(1, cus * std::max(1, per_cu[0]));
-        c->blocks_any = (uint32_t)std::max(1, cus * std::max(1, per_cu[1]));
-        c->trace_blocks = std::max(c->blocks_closest, c->blocks_any);
     }
     if (hipHostMalloc((void**)&c->host_cnt, PT_RING * SNAP_WORDS * 4, hipHostMallocCoherent | hipHostMallocMapped) !=
             hipSuccess ||
@@ -895,9 +899,21 @@ static bool build_q48(const std::vector<DevCluster>& nodes, const std::vector<De
         }
         root_map.push_back({r, qroots[b]});
     }
-    while (!work.empty()) {
-        const auto [gi, r] = work.back();
-        work.pop_back();
+    // depth-first (each node's subtree contiguous), except with a treelet
+    // (PT_TREELET, pt_trace.h): breadth-first from the roots until the first
+    // treelet-size records are laid out, so those are the top levels the
+    // pool kernels keep in LDS
+    constexpr uint32_t tree_recs = (uint32_t)std::max(PT_TREELET, PT_TREELET_ANY);
+    size_t head = 0;  // breadth-first cursor into `work`
+    while (head < work.size()) {
+        std::pair<uint32_t, uint32_t> item;
+        if (tree_recs && rec.size() < tree_recs) {
+            item = work[head++];
+        } else {
+            item = work.back();
+            work.pop_back();
+        }
+        const auto [gi, r] = item;
         const DevCluster& n = nodes[gi];
         uint32_t size[4] = {0, 0, 0, 0};
         for (int k = 0; k < 4; k++) {
@@ -1752,9 +1768,9 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             }
             const uint32_t i = issued;
             const uint32_t nb = std::max(bound, 1u);
-            const dim3 gt(use_pool ? std::min(c->blocks_closest, (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK)
+            const dim3 gt(use_pool ? std::min(c->pool_blocks[0][inst][qn], (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK)
                                    : (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK);
-            const dim3 ga(use_pool ? std::min(c->blocks_any, (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK)
+            const dim3 ga(use_pool ? std::min(c->pool_blocks[1][inst][qn], (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK)
                                    : (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK);
             const dim3 gs((nb + 255) / 256), gsh((nb + PT_SHADE_BLOCK - 1) / PT_SHADE_BLOCK);
             const dim3 gsort((nb + 256 * PT_SORT_PER - 1) / (256 * PT_SORT_PER));  // k_sort_count / k_sort_scatter
@@ -1845,7 +1861,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         if (tail) {
             if (ovl && issued) HIPCHK(c, hipStreamWaitEvent(sm, c->rev[(issued - 1) % PT_RING][4], 0));
             uint32_t* in = set[issued % 3];  // the paths entering the next bounce
-            const dim3 gt(std::max(1u, std::min(c->blocks_closest, (bound + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK)));
+            const dim3 gt(std::max(1u, std::min(c->pool_blocks[0][inst][qn], (bound + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK)));
             using TailFn = void (*)(RenderParams, PathSoA, const uint32_t*, float*, unsigned long long*);
             const TailFn kt = rd->integrator == PT_INTEGRATOR_SIMPLE
                                   ? (count ? k_tail<PT_INTEGRATOR_SIMPLE, false, true> : k_tail<PT_INTEGRATOR_SIMPLE, false, false>)

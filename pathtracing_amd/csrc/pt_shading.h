@@ -935,10 +935,8 @@ __device__ __forceinline__ f3 normalize4(f3 v) {
 // ---- AnimatedPrimitive / AnimatedLight (Primitive.cpp:76-96, Light.cpp:338-364):
 // a TransformedPrimitive / TransformedLight over glm::translate(mat4(1),
 // dir * t), t = glm::clamp(time - t0, t0, t1) / (t1 - t0), rebuilt per ray at
-// the ray's time (the reference builds the temporary per call).  glm::inverse
-// (compute_inverse<4,4>) is restated op by op: on a translation every
-// cofactor product is exact, so the reference build's contractions round it
-// alike, zero signs included (pt_mat4_inverse, the oracle's mat4_inverse_).
+// the ray's time (the reference builds the temporary per call); its
+// glm::inverse in closed form (anim_inverse below).
 __device__ __forceinline__ void anim_transform(const DevInstance& I, float time, float* T) {
     const float t0 = I.t0, t1 = I.t1;
     float x = time - t0;
@@ -952,56 +950,32 @@ __device__ __forceinline__ void anim_transform(const DevInstance& I, float time,
 #pragma unroll
     for (int k = 0; k < 3; k++) T[12 + k] = rmul(I.mdir[k], t) + 0.0f;
 }
-__device__ __forceinline__ void m4_inverse(const float* m, float* out) {
-#define M(c, r) m[(c) * 4 + (r)]
-#define D2(a, b, c, d) (rmul(a, b) - rmul(c, d))
-    const float C00 = D2(M(2, 2), M(3, 3), M(3, 2), M(2, 3)), C02 = D2(M(1, 2), M(3, 3), M(3, 2), M(1, 3));
-    const float C03 = D2(M(1, 2), M(2, 3), M(2, 2), M(1, 3)), C04 = D2(M(2, 1), M(3, 3), M(3, 1), M(2, 3));
-    const float C06 = D2(M(1, 1), M(3, 3), M(3, 1), M(1, 3)), C07 = D2(M(1, 1), M(2, 3), M(2, 1), M(1, 3));
-    const float C08 = D2(M(2, 1), M(3, 2), M(3, 1), M(2, 2)), C10 = D2(M(1, 1), M(3, 2), M(3, 1), M(1, 2));
-    const float C11 = D2(M(1, 1), M(2, 2), M(2, 1), M(1, 2)), C12 = D2(M(2, 0), M(3, 3), M(3, 0), M(2, 3));
-    const float C14 = D2(M(1, 0), M(3, 3), M(3, 0), M(1, 3)), C15 = D2(M(1, 0), M(2, 3), M(2, 0), M(1, 3));
-    const float C16 = D2(M(2, 0), M(3, 2), M(3, 0), M(2, 2)), C18 = D2(M(1, 0), M(3, 2), M(3, 0), M(1, 2));
-    const float C19 = D2(M(1, 0), M(2, 2), M(2, 0), M(1, 2)), C20 = D2(M(2, 0), M(3, 1), M(3, 0), M(2, 1));
-    const float C22 = D2(M(1, 0), M(3, 1), M(3, 0), M(1, 1)), C23 = D2(M(1, 0), M(2, 1), M(2, 0), M(1, 1));
-    const float F[6][4] = {{C00, C00, C02, C03}, {C04, C04, C06, C07}, {C08, C08, C10, C11},
-                           {C12, C12, C14, C15}, {C16, C16, C18, C19}, {C20, C20, C22, C23}};
-    float V[4][4];
+// glm::inverse of anim_transform's matrix.  Every cofactor product of the
+// general formula (compute_inverse<4,4>) is a translation component times a
+// one or a zero, the determinant is 1, and v is finite and never -0, so the
+// formula reduces exactly to constants and -v -- zero signs included: the
+// upper 3x4 block keeps the formula's signed zeros, and column 3's y entry is
+// 0 - v.y (+0 for v.y = +0) where x and z are -v (-0).  Checked against the
+// general formula over 2e7 random bit patterns (tests/test_anim_inverse.py
+// keeps that check); the oracle keeps the general formula,
+// so the motion parity scenes check it on the device.  As a closed form it
+// needs no cofactor registers in the traversal's instance step.
+__device__ __forceinline__ void anim_inverse(const float* T, float* out) {
+    constexpr float z = 0.0f, nz = -0.0f;
+    const float c[12] = {1.0f, nz, z, nz, nz, 1.0f, nz, z, z, nz, 1.0f, nz};
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        V[k][0] = M(1, k);
-        V[k][1] = V[k][2] = V[k][3] = M(0, k);
-    }
-    // Inv_i = (Va * Fa - Vb * Fb) + Vc * Fc lane by lane, times SignA / SignB
-    constexpr int comb[4][6] = {{1, 0, 2, 1, 3, 2}, {0, 0, 2, 3, 3, 4}, {0, 1, 1, 3, 3, 5}, {0, 2, 1, 4, 2, 5}};
-    float inv[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const float sg = (i & 1) ? -1.0f : 1.0f;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int* c = comb[i];
-            const float v = (rmul(V[c[0]][k], F[c[1]][k]) - rmul(V[c[2]][k], F[c[3]][k])) + rmul(V[c[4]][k], F[c[5]][k]);
-            inv[i][k] = v * ((k & 1) ? -sg : sg);
-        }
-    }
-    float d0[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) d0[k] = rmul(M(0, k), inv[k][0]);
-    const float od = 1.0f / ((d0[0] + d0[1]) + (d0[2] + d0[3]));
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) out[c * 4 + r] = inv[c][r] * od;
-#undef M
-#undef D2
+    for (int k = 0; k < 12; k++) out[k] = c[k];
+    out[12] = -T[12];
+    out[13] = 0.0f - T[13];
+    out[14] = -T[14];
+    out[15] = 1.0f;
 }
 // An instance's transform and inverse at a ray's time: the uploaded pair, or
 // an AnimatedPrimitive's rebuilt at `time` (S.motion: the scene has one)
 __device__ __forceinline__ void inst_matrices(const DevInstance& I, float time, float* T, float* inv) {
     if (S.motion && I.anim) {
         anim_transform(I, time, T);
-        m4_inverse(T, inv);
+        anim_inverse(T, inv);
     } else {
 #pragma unroll
         for (int k = 0; k < 16; k++) {

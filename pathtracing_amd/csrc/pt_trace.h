@@ -374,10 +374,31 @@ __device__ __forceinline__ uint32_t order_children_q48(uint32_t mask, float cz, 
 __device__ __forceinline__ uint32_t q48_perm(const uint8_t* s_lut, uint32_t oct, float aw) {
     return s_lut[(oct & OCT_MASK) * Q48_LUT_STRIDE + (__float_as_uint(aw) >> 24)];
 }
-// every thread of the block takes part (one barrier)
+// The top of the BVH in LDS (A/B option): the first PT_TREELET records of the
+// PT_Q48 array -- laid out breadth-first from the roots by the runtime, so
+// they are the TLAS and the first levels of the BLASes every ray descends --
+// sit after the order table in the same LDS block; node steps on them read
+// LDS instead of the vector memory pipe.  PT_TREELET_ANY: the any-hit
+// kernels' count.  0 = off.
+#ifndef PT_TREELET
+#define PT_TREELET 0
+#endif
+#ifndef PT_TREELET_ANY
+#define PT_TREELET_ANY 0
+#endif
+#define Q48_LUT_BYTES (8 * Q48_LUT_STRIDE)  // a multiple of 16
+#define Q48_LDS_BYTES(T_) (Q48_LUT_BYTES + 48 * (T_))
+// every thread of the block takes part (one barrier); T: treelet records
+template <int T = 0>
 __device__ __forceinline__ void stage_q48_lut(uint8_t* s_lut) {
     uint32_t* w = reinterpret_cast<uint32_t*>(s_lut);
     for (uint32_t i = threadIdx.x; i < 8 * Q48_LUT_STRIDE / 4; i += blockDim.x) w[i] = S.qlut[i];
+    if constexpr (T > 0) {
+        float4* tr = reinterpret_cast<float4*>(s_lut + Q48_LUT_BYTES);
+        const uint32_t n = 3u * min((uint32_t)T, S.qrec_bytes / 48u);
+        const float4* src = reinterpret_cast<const float4*>(S.qrec);
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) tr[i] = src[i];
+    }
     __syncthreads();
 }
 
@@ -499,7 +520,7 @@ __device__ __forceinline__ InstState instance_step_inl(InstState s) {
     if (S.motion && I.anim) {  // AnimatedPrimitive::Intersect(Pred) at the ray's time (Primitive.cpp:82-89)
         float T[16], inv[16];
         anim_transform(I, s.time, T);
-        m4_inverse(T, inv);
+        anim_inverse(T, inv);
         dir = m4_dir(inv, s.d);
         org = m4_point(inv, s.o);
     } else {

@@ -186,8 +186,9 @@ def lib():
     L.pt_comm_destroy.restype = C.c_int32
     L.pt_frame_samples.argtypes = [vp, vp, vp, C.c_uint32, vp]
     L.pt_frame_samples.restype = C.c_int32
-    L.pt_frame_sample_range.argtypes = [vp, vp, vp]
-    L.pt_frame_sample_range.restype = C.c_int32
+    if hasattr(L, "pt_frame_sample_range"):  # an API-5 build loaded for a timing A/B lacks it
+        L.pt_frame_sample_range.argtypes = [vp, vp, vp]
+        L.pt_frame_sample_range.restype = C.c_int32
     L.pt_destroy.argtypes = [vp]
     L.pt_destroy.restype = None
     L.pt_last_error.argtypes = [vp]

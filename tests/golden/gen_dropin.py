@@ -32,9 +32,9 @@ from pathtracing_amd.recipe import pin_random_lights, write_recipe  # noqa: E402
 
 HARNESS = ROOT / "oracle" / "_ref" / "ref_harness"
 FILM_SCENES = ["example1", "cornell_c2", "cornell_c3", "zoo", "heightfield", "sanmiguel", "example1_volpath", "fog",
-               "instances", "lit_instances", "motion_blur", "motion_path"]
+               "instances", "lit_instances", "motion_blur", "motion_path", "stratified"]
 ADAPTIVE_SCENES = ["example1", "cornell_c3", "zoo", "fog", "instances", "sanmiguel", "lens_box", "lit_instances",
-                   "motion_blur", "motion_path"]
+                   "motion_blur", "motion_path", "stratified", "stratified_motion"]
 
 
 def pinned_recipe(tmp: Path, setup) -> Path:

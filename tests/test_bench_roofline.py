@@ -112,3 +112,17 @@ def test_without_counters_the_headline_is_algorithmic_and_says_so(monkeypatch):
     roof = _roof(monkeypatch, None)
     assert roof["frac"] == roof["frac_algorithmic"]
     assert roof["frac_basis"].startswith("SURVEY 8(d) algorithmic")
+
+
+def test_timing_only_runs_keep_a_headline_without_fractions(monkeypatch):
+    """--no-count with no CPU sample (the A/B runs): no visit counts, so the
+    entries carry launch times only and the headline's fractions are null."""
+    import types
+    monkeypatch.setattr(bench, "pmc_traffic", lambda *a: (None, {}))
+    args = types.SimpleNamespace(traversal="auto", config="c4", nodes="auto")
+    setup = types.SimpleNamespace(spp=1024, integrator="path")
+    totals = {"ms_closest": 29 * 121.0, "launches_closest": 29, "rays_closest": 6_857_000_000,
+              "ms_any": 29 * 38.0, "launches_any": 29, "rays_any": 2_000_000_000, "ms_shade": 1205.0}
+    roof = bench.roofline(args, setup, 1, totals, None, None)
+    assert roof["frac"] is None and roof["achieved"] is None and roof["frac_algorithmic"] is None
+    assert abs(roof["avg_launch_ms"] - 121.0) < 1e-6

@@ -542,7 +542,8 @@ def test_gpu_film_resolve_full_size_matches_oracle():
 
 
 # ---------------------------------------------------------------- adaptive sampling (pt_render_adaptive)
-ADAPTIVE = ["cornell_c3", "example1", "example1_simple", "zoo", "fog", "lens_box", "instances", "mitchell2"]
+ADAPTIVE = ["cornell_c3", "example1", "example1_simple", "zoo", "fog", "lens_box", "instances", "mitchell2",
+            "stratified", "motion_path"]
 
 
 @pytest.mark.parametrize("name", ADAPTIVE)

@@ -231,7 +231,8 @@ def test_oracle_resolve_matches_reference(film, tonemap, key):
 
 
 # ---------------------------------------------------------------- adaptive sampling (a25)
-ADAPTIVE = ["cornell_c3", "example1", "example1_simple", "zoo", "fog", "lens_box", "instances", "mitchell2"]
+ADAPTIVE = ["cornell_c3", "example1", "example1_simple", "zoo", "fog", "lens_box", "instances", "mitchell2",
+            "stratified", "motion_path"]
 
 
 @pytest.mark.parametrize("name", ADAPTIVE)
