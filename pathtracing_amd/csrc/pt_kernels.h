@@ -46,11 +46,23 @@
 // Continuing paths fill entries [0, c) from the front and new camera paths
 // [cap - r, cap) from the back, so camera rays stay in coherent waves of their
 // own; path i of an iteration (i < c + r) lives at path_slot(i).
+// PT_PATH_AOS (default): the four float4 fields of a path are one 64-B
+// record, so the shading kernel's reads through the hit sort's permutation
+// fetch one 64-B sector per path instead of four (random 16-B reads fetch
+// 64 B each: profiles/r03_fetch_calib.json); 0: one array per field.
+#ifndef PT_PATH_AOS
+#define PT_PATH_AOS 1
+#endif
+#define PT_PATH_STRIDE (PT_PATH_AOS ? 4u : 1u)
+struct PField {  // one float4 field of the path state, indexed by entry
+    float4* p;
+    __device__ __forceinline__ float4& operator[](uint32_t e) const { return p[(size_t)e * PT_PATH_STRIDE]; }
+};
 struct PathSoA {
-    float4* o;    // origin.xyz, stream key (bits)
-    float4* d;    // direction.xyz, flags (bits): depth | rr << 12 | spec
-    float4* beta; // attenuation.xyz, prevPDF
-    float4* L;    // radiance so far .xyz, next draw dimension (bits)
+    PField o;     // origin.xyz, stream key (bits)
+    PField d;     // direction.xyz, flags (bits): depth | rr << 12 | spec
+    PField beta;  // attenuation.xyz, prevPDF
+    PField L;     // radiance so far .xyz, next draw dimension (bits)
     uint32_t* sid;// sample id within the chunk
     uint32_t cap; // entries
     float* time;  // the path's ray time (Ray::time, constant along a path: every

@@ -40,8 +40,11 @@
 // diagnostics builds: per-iteration wave statistics of the pool kernels,
 // [0] iterations [1] refill iterations [2] iterations reaching a step
 // [3] with a node lane [4] with a primitive lane [5] node lane-steps
-// [6] primitive lane-steps [7] lanes popping; the runtime prints them
-__device__ unsigned long long pt_iter[2][8];
+// [6] primitive lane-steps [7] lanes popping [8] with node lanes all on one
+// record [9] with primitive lanes all on one slot [10] with a fresh ray's
+// setup [11] with an alpha test [12] alpha-testing lanes [13] with a
+// non-triangle primitive; the runtime prints them
+__device__ unsigned long long pt_iter[2][14];
 #endif
 #if PT_POOL_CHECK
 // debugging builds: [0] bad refs (popped instead), [1] shade prim out of range,
@@ -216,7 +219,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
     float tmax = 0;
     int sp = 0;
 #if PT_ITER_STATS
-    unsigned long long its[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long its[14] = {};
     auto lead = [&]() { return wl == (uint32_t)(__ffsll((unsigned long long)__ballot(true)) - 1); };
 #define PT_IT(k, v) do { const unsigned long long v_ = (v); if (lead()) its[k] += v_; } while (0)
 #else
@@ -425,6 +428,11 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             PT_IT(4, np > 0);
             PT_IT(5, nn);
             PT_IT(6, np);
+            const uint64_t nb = __ballot(node_step), pb = __ballot(prim_step);
+            const uint32_t r0 = __builtin_amdgcn_readlane(ref, nb ? __ffsll((unsigned long long)nb) - 1 : 0);
+            const uint32_t l0 = __builtin_amdgcn_readlane(leaf, pb ? __ffsll((unsigned long long)pb) - 1 : 0);
+            PT_IT(8, nb && __ballot(node_step && ref != r0) == 0);
+            PT_IT(9, pb && __ballot(prim_step && leaf != l0) == 0);
         }
 #endif
         // both cursors' loads issue before either is used: the node (48 B
@@ -487,6 +495,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
 #endif
         __builtin_amdgcn_sched_barrier(0);  // (the scheduler would sink the slot loads past the node side)
 #if PT_DEFER_SETUP
+        PT_IT(10, __ballot(oct & OCT_FRESH) != 0);
         if (oct & OCT_FRESH) {  // a ray claimed this iteration: its origin and direction are in
             inv = inv_dir(d);
             oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
@@ -552,6 +561,15 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             const uint32_t g2w = __float_as_uint(g2.w);
 #endif
             const uint32_t kind = w0 & GF_KIND;
+#if PT_ITER_STATS
+            {
+                const uint64_t ab = __ballot(prim_step && kind == PT_PRIM_TRIANGLE && tri_hit && !pred &&
+                                             (w0 & GF_ALPHA));
+                PT_IT(11, ab != 0);
+                PT_IT(12, __popcll(ab));
+                PT_IT(13, __ballot(prim_step && kind != PT_PRIM_TRIANGLE && kind != PT_PRIM_BLAS) != 0);
+            }
+#endif
 #if PT_SPEC_LEAF2
             const uint32_t w1 = __float_as_uint(h0.w);
             const bool pred2 = ANY && !(w1 & GF_PRED_GLM);
@@ -637,7 +655,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         }
     }
 #if PT_ITER_STATS
-    for (int k = 0; k < 8; k++)
+    for (int k = 0; k < 14; k++)
         if (its[k]) atomicAdd(&pt_iter[ANY ? 1 : 0][k], its[k]);
 #endif
 #undef PT_IT
@@ -692,7 +710,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
 
     const uint32_t all_dead = (1u << PT_POOL_CHUNKS) - 1u;
 #if PT_ITER_STATS
-    unsigned long long its[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long its[14] = {};
     // counted once per wave: by the first active lane of the counting point
     auto lead = [&]() { return wl == (uint32_t)(__ffsll((unsigned long long)__ballot(true)) - 1); };
 #define PT_IT(k, v) do { const unsigned long long v_ = (v); if (lead()) its[k] += v_; } while (0)
@@ -1033,7 +1051,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         }
     }
 #if PT_ITER_STATS
-    for (int k = 0; k < 8; k++)
+    for (int k = 0; k < 14; k++)
         if (its[k]) atomicAdd(&pt_iter[ANY ? 1 : 0][k], its[k]);
 #endif
 #undef PT_IT

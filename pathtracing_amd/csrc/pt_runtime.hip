@@ -443,9 +443,12 @@ static void free_scene(pt_ctx* c) {
     c->has_scene = false;
 }
 static void free_work(pt_ctx* c) {
-    void* bufs[] = {c->PA.o, c->PA.d, c->PA.beta, c->PA.L, c->PA.sid, c->PA.time, c->PB.o, c->PB.d, c->PB.beta,
-                    c->PB.L, c->PB.sid, c->PB.time, c->hit, c->qcnt, c->sq, c->counters, c->ovf, c->ties,
-                    c->sq_time};
+    // (PT_PATH_AOS: the four fields share the o allocation)
+    void* bufs[] = {c->PA.o.p, PT_PATH_AOS ? nullptr : c->PA.d.p, PT_PATH_AOS ? nullptr : c->PA.beta.p,
+                    PT_PATH_AOS ? nullptr : c->PA.L.p, c->PA.sid, c->PA.time, c->PB.o.p,
+                    PT_PATH_AOS ? nullptr : c->PB.d.p, PT_PATH_AOS ? nullptr : c->PB.beta.p,
+                    PT_PATH_AOS ? nullptr : c->PB.L.p, c->PB.sid, c->PB.time, c->hit, c->qcnt, c->sq, c->counters,
+                    c->ovf, c->ties, c->sq_time};
     for (void* p : bufs)
         if (p) hipFree(p);
     c->PA = PathSoA{};
@@ -1398,10 +1401,17 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
     }
     for (PathSoA* P : {&c->PA, &c->PB}) {
         P->cap = (uint32_t)n;
-        AL(P->o, n * 16);
-        AL(P->d, n * 16);
-        AL(P->beta, n * 16);
-        AL(P->L, n * 16);
+        if (PT_PATH_AOS) {  // one 64-B record per path (pt_kernels.h PathSoA)
+            AL(P->o.p, n * 64);
+            P->d.p = P->o.p + 1;
+            P->beta.p = P->o.p + 2;
+            P->L.p = P->o.p + 3;
+        } else {
+            AL(P->o.p, n * 16);
+            AL(P->d.p, n * 16);
+            AL(P->beta.p, n * 16);
+            AL(P->L.p, n * 16);
+        }
         AL(P->sid, n * 4);
     }
     AL(c->hit, n * 16);
@@ -1878,13 +1888,15 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
 
 #if PT_ITER_STATS
         {
-            unsigned long long it[2][8];
+            unsigned long long it[2][14];
             HIPCHK(c, hipMemcpyFromSymbol(it, HIP_SYMBOL(pt_iter), sizeof(it)));
             for (int a = 0; a < 2; a++)
                 fprintf(stderr, "pt_iter %s: iters %llu refill %llu step %llu with_node %llu with_prim %llu "
-                        "node_lanes %llu prim_lanes %llu pops %llu\n", a ? "any" : "closest", it[a][0], it[a][1],
-                        it[a][2], it[a][3], it[a][4], it[a][5], it[a][6], it[a][7]);
-            const unsigned long long z[2][8] = {};
+                        "node_lanes %llu prim_lanes %llu pops %llu uniform_node %llu uniform_prim %llu "
+                        "fresh %llu with_alpha %llu alpha_lanes %llu with_other %llu\n",
+                        a ? "any" : "closest", it[a][0], it[a][1], it[a][2], it[a][3], it[a][4], it[a][5], it[a][6],
+                        it[a][7], it[a][8], it[a][9], it[a][10], it[a][11], it[a][12], it[a][13]);
+            const unsigned long long z[2][14] = {};
             HIPCHK(c, hipMemcpyToSymbol(HIP_SYMBOL(pt_iter), z, sizeof(z)));
         }
 #endif

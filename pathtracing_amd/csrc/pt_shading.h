@@ -85,13 +85,34 @@ __device__ __forceinline__ pt_image img_rec(int id) {
 
 // ------------------------------------------------------------------ textures
 __device__ __forceinline__ int wrap_index(int i, int n) {
+    // a power-of-two size: the low bits are the non-negative remainder (two's
+    // complement), no integer division
+#ifndef PT_WRAP_POW2
+#define PT_WRAP_POW2 0
+#endif
+    if (PT_WRAP_POW2 && (n & (n - 1)) == 0) return i & (n - 1);
     int m = i % n;
     if (m < 0) m += n;
     return m;
 }
+// byte / 255.0f exactly as the IEEE division rounds it: the product with the
+// rounded reciprocal and one fma correction give the correctly rounded
+// quotient for every byte 0..255 (tools/check_u8unit.c, run by
+// tests/test_libmf.py) in 3 VALU instead of a division's ~11
+__device__ __forceinline__ float u8_unit(uint32_t b) {
+    const float x = (float)b, r = 1.0f / 255.0f;
+#ifdef PT_U8_DIV  // A/B builds: the division itself
+    return x / 255.0f;
+#endif
+    const float q = x * r;
+    return fma_(fma_(-q, 255.0f, x), r, q);
+}
 // Image::GetChannelAt (Texture.hpp:43-48): byte ch-1 of the pixel, any channel count.
-__device__ __forceinline__ float channel_at(const pt_image& im, int x, int y, int ch) {
-    int xi = wrap_index(x, im.width), yi = wrap_index(y, im.height);
+// wrap_index(x + 1, n) from w = wrap_index(x, n): a bilinear footprint wraps
+// each axis once (one integer remainder per axis instead of one per texel)
+__device__ __forceinline__ int wrap_next(int w, int n) { return w + 1 == n ? 0 : w + 1; }
+// (xi, yi: wrapped coordinates)
+__device__ __forceinline__ float channel_w(const pt_image& im, int xi, int yi, int ch) {
     uint64_t idx = im.offset + ((uint64_t)yi * (uint64_t)im.width + (uint64_t)xi) * (uint64_t)im.channels +
                    (uint64_t)(ch - 1);
     if (im.format == PT_IMAGE_F32) {  // FloatImage::GetChannelAt (Texture.hpp:78-83): floats, no /255
@@ -100,10 +121,13 @@ __device__ __forceinline__ float channel_at(const pt_image& im, int x, int y, in
         return *reinterpret_cast<const float*>(S.texels + fi);
     }
     if (idx >= S.n_texel_bytes) return 0.0f;
-    return S.texels[idx] / 255.0f;
+    return u8_unit(S.texels[idx]);
 }
-__device__ __forceinline__ f3 texel3(const pt_image& im, int x, int y) {
-    return F3(channel_at(im, x, y, 1), channel_at(im, x, y, 2), channel_at(im, x, y, 3));
+__device__ __forceinline__ float channel_at(const pt_image& im, int x, int y, int ch) {
+    return channel_w(im, wrap_index(x, im.width), wrap_index(y, im.height), ch);
+}
+__device__ __forceinline__ f3 texel3_w(const pt_image& im, int xi, int yi) {
+    return F3(channel_w(im, xi, yi, 1), channel_w(im, xi, yi, 2), channel_w(im, xi, yi, 3));
 }
 
 // The two texels (x, y), (x + 1, y) of a bilinear row of a u8 RGB / RGBA image
@@ -112,10 +136,10 @@ __device__ __forceinline__ f3 texel3(const pt_image& im, int x, int y) {
 // texel3 (byte / 255); false (caller falls back to texel3) when x + 1 wraps,
 // for other formats, or near the end of the texel buffer (the upload pads it
 // by 16 bytes, so the word loads stay inside the allocation).
-__device__ __forceinline__ bool texel_pair_u8(const pt_image& im, int x, int y, f3& a, f3& b) {
+__device__ __forceinline__ bool texel_pair_u8(const pt_image& im, int xi, int yi, f3& a, f3& b) {
+    // (xi, yi: wrapped coordinates)
     const int C = im.channels;
     if (im.format != PT_IMAGE_U8 || (C != 3 && C != 4)) return false;
-    const int xi = wrap_index(x, im.width), yi = wrap_index(y, im.height);
     if (xi + 1 >= im.width) return false;
     const uint64_t idx = im.offset + ((uint64_t)yi * (uint64_t)im.width + (uint64_t)xi) * (uint64_t)C;
     if (idx + 2u * (uint64_t)C > S.n_texel_bytes) return false;
@@ -124,7 +148,7 @@ __device__ __forceinline__ bool texel_pair_u8(const pt_image& im, int x, int y, 
     const uint32_t sh = (uint32_t)(idx & 3u);
     const uint32_t q0 = __builtin_amdgcn_alignbyte(w1, w0, sh), q1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
     const uint32_t qb = C == 4 ? q1 : __builtin_amdgcn_alignbyte(q1, q0, 3u);  // second texel's bytes
-    auto ch = [](uint32_t q, int k) { return (float)((q >> (8 * k)) & 0xFFu) / 255.0f; };
+    auto ch = [](uint32_t q, int k) { return u8_unit((q >> (8 * k)) & 0xFFu); };
     a = F3(ch(q0, 0), ch(q0, 1), ch(q0, 2));
     b = F3(ch(qb, 0), ch(qb, 1), ch(qb, 2));
     return true;
@@ -158,14 +182,16 @@ __device__ f3 tex_eval_t(int id, float u, float v) {
         float y = v * im.height - 0.5f;
         int xi = (int)floorf(x), yi = (int)floorf(y);
         float dx = x - xi, dy = y - yi;
+        const int x0 = wrap_index(xi, im.width), x1 = wrap_next(x0, im.width);
+        const int y0 = wrap_index(yi, im.height), y1 = wrap_next(y0, im.height);
         f3 a, b, c, d;
-        if (!PAIR || !texel_pair_u8(im, xi, yi, a, b)) {
-            a = texel3(im, xi, yi);
-            b = texel3(im, xi + 1, yi);
+        if (!PAIR || !texel_pair_u8(im, x0, y0, a, b)) {
+            a = texel3_w(im, x0, y0);
+            b = texel3_w(im, x1, y0);
         }
-        if (!PAIR || !texel_pair_u8(im, xi, yi + 1, c, d)) {
-            c = texel3(im, xi, yi + 1);
-            d = texel3(im, xi + 1, yi + 1);
+        if (!PAIR || !texel_pair_u8(im, x0, y1, c, d)) {
+            c = texel3_w(im, x0, y1);
+            d = texel3_w(im, x1, y1);
         }
         // contraction of the reference build: w_a*a rounded, then fma(w_b, b), fma(w_c, c), fma(w_d, d)
         float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
@@ -229,14 +255,16 @@ __device__ __forceinline__ f3 tex_eval_r(DevTex t, float u, float v) {
         float y = v * im.height - 0.5f;
         int xi = (int)floorf(x), yi = (int)floorf(y);
         float dx = x - xi, dy = y - yi;
+        const int x0 = wrap_index(xi, im.width), x1 = wrap_next(x0, im.width);
+        const int y0 = wrap_index(yi, im.height), y1 = wrap_next(y0, im.height);
         f3 a, b, c, d;
-        if (!texel_pair_u8(im, xi, yi, a, b)) {
-            a = texel3(im, xi, yi);
-            b = texel3(im, xi + 1, yi);
+        if (!texel_pair_u8(im, x0, y0, a, b)) {
+            a = texel3_w(im, x0, y0);
+            b = texel3_w(im, x1, y0);
         }
-        if (!texel_pair_u8(im, xi, yi + 1, c, d)) {
-            c = texel3(im, xi, yi + 1);
-            d = texel3(im, xi + 1, yi + 1);
+        if (!texel_pair_u8(im, x0, y1, c, d)) {
+            c = texel3_w(im, x0, y1);
+            d = texel3_w(im, x1, y1);
         }
         float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
         f3 r = F3(fma_(wd, d.x, fma_(wc, c.x, fma_(wb, b.x, rmul(wa, a.x)))),
@@ -273,8 +301,10 @@ __device__ float tex_alpha(int id, float u, float v) {
         float y = v * im.height - 0.5f;
         int xi = (int)floorf(x), yi = (int)floorf(y);
         float dx = x - xi, dy = y - yi;
-        float a = channel_at(im, xi, yi, 4), b = channel_at(im, xi + 1, yi, 4);
-        float c = channel_at(im, xi, yi + 1, 4), d = channel_at(im, xi + 1, yi + 1, 4);
+        const int x0 = wrap_index(xi, im.width), x1 = wrap_next(x0, im.width);
+        const int y0 = wrap_index(yi, im.height), y1 = wrap_next(y0, im.height);
+        float a = channel_w(im, x0, y0, 4), b = channel_w(im, x1, y0, 4);
+        float c = channel_w(im, x0, y1, 4), d = channel_w(im, x1, y1, 4);
         // ImageTexture::alpha as compiled in the reference: w_b*b rounded, then fma(w_a, a), fma(w_c, c), fma(w_d, d)
         float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
         return fma_(wd, d, fma_(wc, c, fma_(wa, a, rmul(wb, b))));

@@ -112,11 +112,11 @@ __device__ __forceinline__ f3 inv_dir(f3 d) {  // Ray ctor (Ray.hpp:32-35)
 
 // A u8 texel channel as channel_at reads it (wrapped coordinates, 0 past
 // the texel buffer)
-__device__ __forceinline__ float alpha_texel(uint64_t off, int w, int h, int C, int x, int y, int ch0) {
-    const int xi = wrap_index(x, w), yi = wrap_index(y, h);
+// (xi, yi: wrapped coordinates)
+__device__ __forceinline__ float alpha_texel(uint64_t off, int w, int C, int xi, int yi, int ch0) {
     const uint64_t idx = off + ((uint64_t)yi * (uint64_t)w + (uint64_t)xi) * (uint64_t)C + (uint64_t)ch0;
     if (idx >= S.n_texel_bytes) return 0.0f;
-    return S.texels[idx] / 255.0f;
+    return u8_unit(S.texels[idx]);
 }
 // The material alpha test of an alpha-tested triangle at its candidate hit
 // (GeometricPrimitive::Intersect -> Material::Alpha, Primitive.cpp:6-26,
@@ -158,9 +158,9 @@ bool tri_alpha(uint32_t ai, uint32_t slot, float bu, float bv, f3 o, f3 d) {
             const int xi = (int)floorf(x), yi = (int)floorf(y);
             const float dx = x - xi, dy = y - yi;
             const int ch0 = src == ALPHA_SRC_CH4 ? 3 : 0;
-            const float ta = alpha_texel(off, W, H, C, xi, yi, ch0), tb = alpha_texel(off, W, H, C, xi + 1, yi, ch0);
-            const float tc = alpha_texel(off, W, H, C, xi, yi + 1, ch0),
-                        td = alpha_texel(off, W, H, C, xi + 1, yi + 1, ch0);
+            const int x0 = wrap_index(xi, W), x1 = wrap_next(x0, W), y0 = wrap_index(yi, H), y1 = wrap_next(y0, H);
+            const float ta = alpha_texel(off, W, C, x0, y0, ch0), tb = alpha_texel(off, W, C, x1, y0, ch0);
+            const float tc = alpha_texel(off, W, C, x0, y1, ch0), td = alpha_texel(off, W, C, x1, y1, ch0);
             const float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
             // the two contractions as built: ImageTexture::alpha (tex_alpha) and
             // Evaluate(uv).x * colorScale.x (tex_eval_t)

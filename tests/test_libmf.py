@@ -22,3 +22,15 @@ def test_libmf_matches_host_libm(tmp_path):
     res = subprocess.run([str(exe), "1021", "2000000"], capture_output=True, text=True)
     assert res.returncode == 0, res.stdout + res.stderr
     assert "expf table in libm: 1" in res.stdout
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="needs gcc")
+def test_u8_unit_is_the_division_for_every_byte(tmp_path):
+    """pt_shading.h u8_unit (texel byte / 255 as mul + fma correction) equals
+    the IEEE division for all 256 bytes."""
+    exe = tmp_path / "check_u8unit"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-mfma", "-o", str(exe), str(ROOT / "tools" / "check_u8unit.c"),
+                    "-lm"], check=True)
+    res = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert "mismatches: 0 of 256" in res.stdout
