@@ -1025,6 +1025,14 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
                                         (L.instance >= 0 && (uint32_t)L.instance >= s->n_instances)))
             return fail(c, PT_ERR_ARG, "light %u: bad area light", l);
     }
+    // (the texel lookups index an image's elements in 32 bits)
+    for (uint32_t k = 0; k < s->n_images; k++) {
+        const pt_image& im = s->images[k];
+        if (im.width <= 0 || im.height <= 0 || im.channels <= 0 ||
+            (uint64_t)im.width * (uint64_t)im.height * (uint64_t)im.channels >= (1ull << 32))
+            return fail(c, PT_ERR_ARG, "image %u: bad size (%d x %d x %d channels; below 2^32 elements)", k,
+                        im.width, im.height, im.channels);
+    }
     for (uint32_t k = 0; k < s->n_textures; k++) {
         const pt_texture& T = s->textures[k];
         if (T.kind == PT_TEX_IMAGE && (T.image < 0 || (uint32_t)T.image >= s->n_images))

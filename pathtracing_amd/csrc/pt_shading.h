@@ -112,11 +112,12 @@ __device__ __forceinline__ float u8_unit(uint32_t b) {
 // each axis once (one integer remainder per axis instead of one per texel)
 __device__ __forceinline__ int wrap_next(int w, int n) { return w + 1 == n ? 0 : w + 1; }
 // (xi, yi: wrapped coordinates)
+// (an image's element index fits 32 bits: pt_scene_upload checks its size)
 __device__ __forceinline__ float channel_w(const pt_image& im, int xi, int yi, int ch) {
-    uint64_t idx = im.offset + ((uint64_t)yi * (uint64_t)im.width + (uint64_t)xi) * (uint64_t)im.channels +
-                   (uint64_t)(ch - 1);
+    const uint32_t local = ((uint32_t)yi * (uint32_t)im.width + (uint32_t)xi) * (uint32_t)im.channels + (uint32_t)(ch - 1);
+    const uint64_t idx = im.offset + local;
     if (im.format == PT_IMAGE_F32) {  // FloatImage::GetChannelAt (Texture.hpp:78-83): floats, no /255
-        const uint64_t fi = im.offset + 4ull * (idx - im.offset);
+        const uint64_t fi = im.offset + 4ull * local;
         if (fi + 4 > S.n_texel_bytes) return 0.0f;
         return *reinterpret_cast<const float*>(S.texels + fi);
     }

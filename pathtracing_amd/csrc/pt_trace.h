@@ -113,10 +113,16 @@ __device__ __forceinline__ f3 inv_dir(f3 d) {  // Ray ctor (Ray.hpp:32-35)
 // A u8 texel channel as channel_at reads it (wrapped coordinates, 0 past
 // the texel buffer)
 // (xi, yi: wrapped coordinates)
-__device__ __forceinline__ float alpha_texel(uint64_t off, int w, int C, int xi, int yi, int ch0) {
-    const uint64_t idx = off + ((uint64_t)yi * (uint64_t)w + (uint64_t)xi) * (uint64_t)C + (uint64_t)ch0;
-    if (idx >= S.n_texel_bytes) return 0.0f;
-    return u8_unit(S.texels[idx]);
+// (an image's element index fits 32 bits: pt_scene_upload checks its size;
+// lim = the texel bytes from the image's offset on).  Branch-free: a texel
+// past the buffer reads the buffer's first byte instead (an image texel
+// exists, so the buffer does) and is replaced by 0, so the four loads of a
+// footprint issue back to back instead of one branch (and one memory round
+// trip) each.
+__device__ __forceinline__ uint32_t alpha_texel_byte(const uint8_t* base, uint64_t lim, uint32_t local) {
+    const bool in = (uint64_t)local < lim;
+    const uint32_t b = *(in ? base + local : S.texels);
+    return in ? b : 0u;
 }
 // The material alpha test of an alpha-tested triangle at its candidate hit
 // (GeometricPrimitive::Intersect -> Material::Alpha, Primitive.cpp:6-26,
@@ -159,8 +165,13 @@ bool tri_alpha(uint32_t ai, uint32_t slot, float bu, float bv, f3 o, f3 d) {
             const float dx = x - xi, dy = y - yi;
             const int ch0 = src == ALPHA_SRC_CH4 ? 3 : 0;
             const int x0 = wrap_index(xi, W), x1 = wrap_next(x0, W), y0 = wrap_index(yi, H), y1 = wrap_next(y0, H);
-            const float ta = alpha_texel(off, W, C, x0, y0, ch0), tb = alpha_texel(off, W, C, x1, y0, ch0);
-            const float tc = alpha_texel(off, W, C, x0, y1, ch0), td = alpha_texel(off, W, C, x1, y1, ch0);
+            const uint8_t* base = S.texels + off;
+            const uint64_t lim = S.n_texel_bytes > off ? S.n_texel_bytes - off : 0ull;
+            const uint32_t r0 = (uint32_t)y0 * (uint32_t)W, r1 = (uint32_t)y1 * (uint32_t)W;
+            auto at = [&](uint32_t r, int x) { return (r + (uint32_t)x) * (uint32_t)C + (uint32_t)ch0; };
+            const uint32_t ba = alpha_texel_byte(base, lim, at(r0, x0)), bb = alpha_texel_byte(base, lim, at(r0, x1));
+            const uint32_t bc = alpha_texel_byte(base, lim, at(r1, x0)), bd = alpha_texel_byte(base, lim, at(r1, x1));
+            const float ta = u8_unit(ba), tb = u8_unit(bb), tc = u8_unit(bc), td = u8_unit(bd);
             const float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
             // the two contractions as built: ImageTexture::alpha (tex_alpha) and
             // Evaluate(uv).x * colorScale.x (tex_eval_t)
