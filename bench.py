@@ -236,7 +236,20 @@ def pmc_traffic(config: str, spp: int, world: int, kernel: str, sha: str):
         # what bounds the kernel besides bytes: the share of wave cycles spent
         # waiting on memory and the L2 hit rate of the same profile
         if k.get("SQ_WAVE_CYCLES_per_dispatch"):
-            info["wait_ratio"] = round(k["SQ_WAIT_ANY_per_dispatch"] / k["SQ_WAVE_CYCLES_per_dispatch"], 3)
+            wc = k["SQ_WAVE_CYCLES_per_dispatch"]
+            info["wait_ratio"] = round(k["SQ_WAIT_ANY_per_dispatch"] / wc, 3)
+            # issue-stalled (an instruction ready but not issued) and active shares
+            if k.get("SQ_WAIT_INST_ANY_per_dispatch") is not None:
+                info["issue_stall_ratio"] = round(k["SQ_WAIT_INST_ANY_per_dispatch"] / wc, 3)
+            if k.get("SQ_ACTIVE_INST_ANY_per_dispatch") is not None:
+                info["active_ratio"] = round(k["SQ_ACTIVE_INST_ANY_per_dispatch"] / wc, 3)
+            # resident waves per SIMD, time-averaged over the launch: the wave
+            # quad-cycles (SQ_WAVE_CYCLES counts quad-cycles, MI355X_MICROARCH.md
+            # "SQ PMC units") x 4 over the launch's cycles x 1024 SIMDs, the
+            # launch's cycles being SQ_BUSY_CYCLES over its 32 SQ instances
+            # (8 XCDs x 4 shader engines; = avg_us x 2.4 GHz within 2 %)
+            if k.get("SQ_BUSY_CYCLES_per_dispatch"):
+                info["waves_per_simd"] = round(4.0 * wc * 32.0 / (k["SQ_BUSY_CYCLES_per_dispatch"] * 4.0 * MI355X_CUS), 2)
         hits, miss = k.get("TCC_HIT_sum_per_dispatch"), k.get("TCC_MISS_sum_per_dispatch")
         if hits is not None and miss is not None and hits + miss > 0:
             info["l2_hit_rate"] = round(hits / (hits + miss), 3)

@@ -110,8 +110,11 @@ __device__ __noinline__ SurfXf anim_world_surface(const DevInstance* I, float ti
     normal_matrix(T, NM);
     return SurfXf{m4_point(T, p), normalize(m3_mul(NM, n)), normalize(m3_mul(NM, ns)), normalize4(m4_dir(T, tangent))};
 }
+// defer_nm (PT_TEX_JOINT shading): a triangle's normal map is left to
+// mat_tex unless the hit is in an instance (whose transform follows it)
 __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, float b1, float b2, SurfInt& si,
-                                         int& medium, float time = 0.0f) {
+                                         int& medium, float time = 0.0f, bool defer_nm = false) {
+    si.nm_pending = false;
     float len = 1.0f;
     const DevInstance* I = nullptr;
     bool anim = false;
@@ -148,7 +151,7 @@ __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, flo
             sphere_root(S.spheres[pi.index], ro, rd, __int_as_float(0x7f800000), t);
         }
     }
-    if (kind == PT_PRIM_TRIANGLE) tri_interaction(g, pi.index, pi.material, ro, rd, t, b1, b2, si);
+    if (kind == PT_PRIM_TRIANGLE) tri_interaction(g, pi.index, pi.material, ro, rd, t, b1, b2, si, !(defer_nm && !I));
     else if (kind == PT_PRIM_QUAD) quad_interaction(S.quads[pi.index], ro, rd, t, b1, b2, si);
     else sphere_interaction(S.spheres[pi.index], ro, rd, t, si);
     si.mat = pi.material;
@@ -899,7 +902,7 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
 #endif
         SurfInt si;
         int smed;
-        hit_surface(prim, ro, rd, h.x, h.y, h.z, si, smed, tm);
+        hit_surface(prim, ro, rd, h.x, h.y, h.z, si, smed, tm, PT_TEX_JOINT && PT_NM_DEFER);
 #ifdef PT_DEBUG_KEY
         if (key == PT_DEBUG_KEY)
             printf("G d%u prim %d t %a p %a %a %a ns %a %a %a uv %a %a mat %d light %d out %a %a %a att %a %a %a\n",

@@ -43,8 +43,9 @@
 // [6] primitive lane-steps [7] lanes popping [8] with node lanes all on one
 // record [9] with primitive lanes all on one slot [10] with a fresh ray's
 // setup [11] with an alpha test [12] alpha-testing lanes [13] with a
-// non-triangle primitive; the runtime prints them
-__device__ unsigned long long pt_iter[2][14];
+// non-triangle primitive [14] alpha-testing lanes on their leaf's first slot;
+// the runtime prints them
+__device__ unsigned long long pt_iter[2][15];
 #endif
 #if PT_POOL_CHECK
 // debugging builds: [0] bad refs (popped instead), [1] shade prim out of range,
@@ -158,6 +159,12 @@ __device__ unsigned int pt_diag[4];
 #ifndef PT_TRI_FIRST
 #define PT_TRI_FIRST 0
 #endif
+#ifndef PT_ALPHA_PREFETCH  // A/B option: an alpha record read before its triangle's test
+#define PT_ALPHA_PREFETCH 0
+#endif
+#ifndef PT_PUSH_FAST  // A/B option: branch-light child pushes while the LDS stack has room
+#define PT_PUSH_FAST 1
+#endif
 #define Q48_OOB_OFFSET 0xFFFFFF00u  // + 32 stays below 2^32: never wraps into range
 __device__ __forceinline__ float4 q48_buf_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
@@ -219,11 +226,14 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
     float tmax = 0;
     int sp = 0;
 #if PT_ITER_STATS
-    unsigned long long its[14] = {};
+    unsigned long long its[15] = {};
+    uint32_t lfirst = 0;  // the leaf cursor is on its leaf's first slot
     auto lead = [&]() { return wl == (uint32_t)(__ffsll((unsigned long long)__ballot(true)) - 1); };
 #define PT_IT(k, v) do { const unsigned long long v_ = (v); if (lead()) its[k] += v_; } while (0)
+#define PT_LF(v) (lfirst = (v))
 #else
 #define PT_IT(k, v) do { } while (0)
+#define PT_LF(v) ((void)0)
 #endif
 #if PT_STACK_SPLIT
     // the overflow entries through a buffer resource and the LDS ones through
@@ -372,6 +382,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         // free leaf cursor lets the node side pop once more)
         if (leaf == REF_EMPTY && is_leaf(ref)) {
             leaf = ref;
+            PT_LF(1u);
             ref = REF_EMPTY;
         }
         PT_IT(7, __popcll(__ballot(ref == REF_EMPTY && sp > 0)));
@@ -390,6 +401,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
             }
             if (leaf == REF_EMPTY && is_leaf(v1)) {
                 leaf = v1;
+                PT_LF(1u);
                 if (sp > 0 && !(leaf & REF_BLOCK)) {
                     if (lds2) {
                         ref = v2;
@@ -407,7 +419,10 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         for (int k = 0; k < 2; k++) {
             if (ref == REF_EMPTY && sp > 0 && !(leaf != REF_EMPTY && (leaf & REF_BLOCK))) {
                 const uint32_t r = pop();
-                if (leaf == REF_EMPTY && is_leaf(r)) leaf = r;
+                if (leaf == REF_EMPTY && is_leaf(r)) {
+                    leaf = r;
+                    PT_LF(1u);
+                }
                 else ref = r;
             }
         }
@@ -526,7 +541,35 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
 #if PT_Q48
             if (!ANY || PT_ANY_OCT) perm = q48_perm(s_lut, oct, q0.w);
 #if PT_Q48_LAZY
+#if PT_PUSH_FAST
+            // a lane with room for three more LDS entries pushes without the
+            // capacity / overflow branches of push(): one masked LDS store per
+            // pushed child (the other lanes take the general path)
+            uint32_t cand;
+            if ((LN >= PT_POOL_STACK ? PT_POOL_STACK : LN) - sp >= 3) {
+                const uint32_t base = __float_as_uint(q2.z), desc = __float_as_uint(q2.w);
+                uint32_t vm = mask;
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (((desc >> (8 * k)) & 0xFFu) == Q48_EMPTY) vm &= ~(1u << k);
+                cand = REF_EMPTY;
+                int np = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t ci = (perm >> (2 * k)) & 3u;
+                    const uint32_t dd = (desc >> (8 * ci)) & 0xFFu;
+                    const uint32_t c = (base + (dd & 63u)) | ((dd & Q48_LEAF) << 25) | ((dd & Q48_HOP) << 22);
+                    const bool v = (vm >> ci) & 1u;
+                    if (v && cand != REF_EMPTY) s_ref[(sp + np++) * PT_TRACE_BLOCK + lane] = cand;
+                    cand = v ? c : cand;
+                }
+                sp += np;
+            } else {
+                cand = order_children_q48(mask, q2.z, q2.w, perm, [&](uint32_t v) { push(v); });
+            }
+#else
             const uint32_t cand = order_children_q48(mask, q2.z, q2.w, perm, [&](uint32_t v) { push(v); });
+#endif
 #else
             const uint4 ch = q48_children(q2.z, q2.w);
 #endif
@@ -553,6 +596,19 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
 #if !PT_TRI_FIRST
             const uint32_t w0 = __float_as_uint(g0.w);
             const bool pred = ANY && !(w0 & GF_PRED_GLM);
+#if PT_ALPHA_PREFETCH
+            // an alpha-tested triangle's record (slot b.w), read before its
+            // test so the load's latency overlaps the test
+            const uint32_t ai = __float_as_uint(g1.w);
+            const bool alane = prim_step && (w0 & GF_KIND) == PT_PRIM_TRIANGLE && (w0 & GF_ALPHA) && !pred &&
+                               ai != ALPHA_NONE;
+            DevAlpha arec;
+            if (__ballot(alane)) {
+                const float4* ap = reinterpret_cast<const float4*>(S.alpha + (alane ? ai : 0u));
+                const float4 a0 = ap[0], a1 = ap[1], a2 = ap[2];
+                arec = __builtin_bit_cast(DevAlpha, (DevGeom{a0, a1, a2}));
+            }
+#endif
             float bx = 0, by = 0, t = 0;
             bool tri_hit;
             if (pred) tri_hit = tri_pred(o, d, xyz(g0), xyz(g1), xyz(g2), tmax);
@@ -568,6 +624,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 PT_IT(11, ab != 0);
                 PT_IT(12, __popcll(ab));
                 PT_IT(13, __ballot(prim_step && kind != PT_PRIM_TRIANGLE && kind != PT_PRIM_BLAS) != 0);
+                PT_IT(14, __popcll(ab & __ballot(lfirst != 0)));
             }
 #endif
 #if PT_SPEC_LEAF2
@@ -586,7 +643,12 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 const uint32_t ps = PT_Q48 ? g2w : slot;
                 if (kind == PT_PRIM_TRIANGLE) {
                     if (COUNT) wk.tris++;
+#if PT_ALPHA_PREFETCH
+                    if (tri_hit && (pred || !(w0 & GF_ALPHA) ||
+                                    (alane ? tri_alpha_rec(arec, ps, bx, by, o, d) : tri_alpha(g1v, ps, bx, by, o, d)))) {
+#else
                     if (tri_hit && (pred || !(w0 & GF_ALPHA) || tri_alpha(g1v, ps, bx, by, o, d))) {
+#endif
                         if (ANY) {
                             anyhit = true;
                         } else {
@@ -647,6 +709,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                     }
                 }
                 leaf = next;
+                PT_LF(0u);
                 if (ANY && anyhit) {  // early exit (BVH.hpp:1104-1105)
                     src.any((uint32_t)ri, true);
                     ri = -1;
@@ -655,7 +718,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         }
     }
 #if PT_ITER_STATS
-    for (int k = 0; k < 14; k++)
+    for (int k = 0; k < 15; k++)
         if (its[k]) atomicAdd(&pt_iter[ANY ? 1 : 0][k], its[k]);
 #endif
 #undef PT_IT
@@ -710,7 +773,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
 
     const uint32_t all_dead = (1u << PT_POOL_CHUNKS) - 1u;
 #if PT_ITER_STATS
-    unsigned long long its[14] = {};
+    unsigned long long its[15] = {};
     // counted once per wave: by the first active lane of the counting point
     auto lead = [&]() { return wl == (uint32_t)(__ffsll((unsigned long long)__ballot(true)) - 1); };
 #define PT_IT(k, v) do { const unsigned long long v_ = (v); if (lead()) its[k] += v_; } while (0)
@@ -1051,7 +1114,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         }
     }
 #if PT_ITER_STATS
-    for (int k = 0; k < 14; k++)
+    for (int k = 0; k < 15; k++)
         if (its[k]) atomicAdd(&pt_iter[ANY ? 1 : 0][k], its[k]);
 #endif
 #undef PT_IT

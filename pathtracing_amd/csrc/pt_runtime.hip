@@ -1896,15 +1896,15 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
 
 #if PT_ITER_STATS
         {
-            unsigned long long it[2][14];
+            unsigned long long it[2][15];
             HIPCHK(c, hipMemcpyFromSymbol(it, HIP_SYMBOL(pt_iter), sizeof(it)));
             for (int a = 0; a < 2; a++)
                 fprintf(stderr, "pt_iter %s: iters %llu refill %llu step %llu with_node %llu with_prim %llu "
                         "node_lanes %llu prim_lanes %llu pops %llu uniform_node %llu uniform_prim %llu "
-                        "fresh %llu with_alpha %llu alpha_lanes %llu with_other %llu\n",
+                        "fresh %llu with_alpha %llu alpha_lanes %llu with_other %llu alpha_first_slot %llu\n",
                         a ? "any" : "closest", it[a][0], it[a][1], it[a][2], it[a][3], it[a][4], it[a][5], it[a][6],
-                        it[a][7], it[a][8], it[a][9], it[a][10], it[a][11], it[a][12], it[a][13]);
-            const unsigned long long z[2][14] = {};
+                        it[a][7], it[a][8], it[a][9], it[a][10], it[a][11], it[a][12], it[a][13], it[a][14]);
+            const unsigned long long z[2][15] = {};
             HIPCHK(c, hipMemcpyToSymbol(HIP_SYMBOL(pt_iter), z, sizeof(z)));
         }
 #endif

@@ -10,6 +10,7 @@ struct SurfInt {  // SurfaceInteraction (Interaction.hpp:36-51)
     float u, v;  // uv
     float t;
     int32_t mat, light;
+    bool nm_pending = false;  // the material's normal map not applied yet (mat_tex applies it)
 };
 
 // ------------------------------------------------------------------ LDS-staged tables
@@ -155,6 +156,33 @@ __device__ __forceinline__ bool texel_pair_u8(const pt_image& im, int xi, int yi
     return true;
 }
 
+// Both rows of a bilinear footprint of a u8 RGB / RGBA image (texel_pair_u8
+// per row): the checks of both rows first, then the six word loads together,
+// then the decode -- one memory round trip per lookup instead of one per row.
+// false: the caller falls back to the texels one by one.
+__device__ __forceinline__ bool texel_quad_u8(const pt_image& im, int x0, int y0, int y1, f3& a, f3& b, f3& c,
+                                              f3& d) {
+    const int C = im.channels;
+    if (im.format != PT_IMAGE_U8 || (C != 3 && C != 4)) return false;
+    if (x0 + 1 >= im.width) return false;
+    const uint64_t i0 = im.offset + ((uint64_t)y0 * (uint64_t)im.width + (uint64_t)x0) * (uint64_t)C;
+    const uint64_t i1 = im.offset + ((uint64_t)y1 * (uint64_t)im.width + (uint64_t)x0) * (uint64_t)C;
+    if (i0 + 2u * (uint64_t)C > S.n_texel_bytes || i1 + 2u * (uint64_t)C > S.n_texel_bytes) return false;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(S.texels + (i0 & ~3ull));
+    const uint32_t* v = reinterpret_cast<const uint32_t*>(S.texels + (i1 & ~3ull));
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], v0 = v[0], v1 = v[1], v2 = v[2];
+    auto row = [C](uint32_t r0, uint32_t r1, uint32_t r2, uint32_t sh, f3& p, f3& q) {
+        const uint32_t q0 = __builtin_amdgcn_alignbyte(r1, r0, sh), q1 = __builtin_amdgcn_alignbyte(r2, r1, sh);
+        const uint32_t qb = C == 4 ? q1 : __builtin_amdgcn_alignbyte(q1, q0, 3u);  // second texel's bytes
+        auto ch = [](uint32_t x, int k) { return u8_unit((x >> (8 * k)) & 0xFFu); };
+        p = F3(ch(q0, 0), ch(q0, 1), ch(q0, 2));
+        q = F3(ch(qb, 0), ch(qb, 1), ch(qb, 2));
+    };
+    row(w0, w1, w2, (uint32_t)(i0 & 3u), a, b);
+    row(v0, v1, v2, (uint32_t)(i1 & 3u), c, d);
+    return true;
+}
+
 // Texture::Evaluate for SolidColor / CheckerTexture / ImageTexture (Texture.hpp:128-207).
 // PAIR: texel_pair_u8 row loads (shading); the alpha test inside the traversal
 // kernels keeps the byte loads (its callee registers count toward theirs).
@@ -186,11 +214,9 @@ __device__ f3 tex_eval_t(int id, float u, float v) {
         const int x0 = wrap_index(xi, im.width), x1 = wrap_next(x0, im.width);
         const int y0 = wrap_index(yi, im.height), y1 = wrap_next(y0, im.height);
         f3 a, b, c, d;
-        if (!PAIR || !texel_pair_u8(im, x0, y0, a, b)) {
+        if (!PAIR || !texel_quad_u8(im, x0, y0, y1, a, b, c, d)) {
             a = texel3_w(im, x0, y0);
             b = texel3_w(im, x1, y0);
-        }
-        if (!PAIR || !texel_pair_u8(im, x0, y1, c, d)) {
             c = texel3_w(im, x0, y1);
             d = texel3_w(im, x1, y1);
         }
@@ -203,6 +229,150 @@ __device__ f3 tex_eval_t(int id, float u, float v) {
         return scaled ? scale * r : r;
     }
     return F3(0, 0, 0);
+}
+
+// Two textures of one hit evaluated together (PT_TEX_JOINT): each chain is
+// resolved to its leaf (records only), then the u8 RGB / RGBA image leaves'
+// footprints are read with all their word loads in flight at once, then
+// decoded -- one memory round trip for both lookups instead of one each.
+// Values are tex_eval's: the same texels, the same arithmetic.
+#ifndef PT_TEX_JOINT
+#define PT_TEX_JOINT 0
+#endif
+#ifndef PT_NM_DEFER  // the normal map joins the material's textures in mat_tex
+#define PT_NM_DEFER 1
+#endif
+struct TexLeaf {
+    bool image;  // else a solid value in `val`
+    bool scaled;
+    f3 scale;    // the checkers' colorScales, multiplied outward-in
+    f3 val;      // SOLID: the value; IMAGE: the texture's colorScale
+    int image_id;
+};
+__device__ __forceinline__ TexLeaf tex_resolve(int id, float u, float v) {
+    TexLeaf r;
+    r.image = false;
+    r.scaled = false;
+    r.scale = F3(1, 1, 1);
+    r.val = F3(0, 0, 0);
+    r.image_id = -1;
+    for (int guard = 0; guard < 16; guard++) {
+        const pt_texture t = tex_rec(id);
+        if (t.kind == PT_TEX_SOLID) {
+            r.val = ld3(t.value);
+            return r;
+        }
+        if (t.kind == PT_TEX_CHECKER) {
+            int ux = (int)floorf(u * t.inv_scale[0]);
+            int uy = (int)floorf(v * t.inv_scale[1]);
+            r.scale = r.scaled ? r.scale * ld3(t.scale) : ld3(t.scale);
+            r.scaled = true;
+            id = ((ux + uy) % 2 == 0) ? t.a : t.b;
+            continue;
+        }
+        r.image = true;
+        r.val = ld3(t.scale);
+        r.image_id = t.image;
+        return r;
+    }
+    r.val = F3(0, 0, 0);  // (a chain deeper than the guard: tex_eval's zero)
+    r.scaled = false;
+    return r;
+}
+// an image leaf's bilinear footprint: coordinates, and the quad's six words
+// once issued (ok: the u8 RGB / RGBA fast form applies)
+struct TexQuad {
+    float dx, dy;
+    int x0, x1, y0, y1;
+    bool ok;
+    uint32_t sh0, sh1;
+    const uint32_t* w;
+    const uint32_t* vrow;
+};
+__device__ __forceinline__ TexQuad tex_quad_addr(const pt_image& im, float u, float v) {
+    TexQuad q;
+    const float x = u * im.width - 0.5f, y = v * im.height - 0.5f;
+    const int xi = (int)floorf(x), yi = (int)floorf(y);
+    q.dx = x - xi;
+    q.dy = y - yi;
+    q.x0 = wrap_index(xi, im.width);
+    q.x1 = wrap_next(q.x0, im.width);
+    q.y0 = wrap_index(yi, im.height);
+    q.y1 = wrap_next(q.y0, im.height);
+    const int C = im.channels;
+    q.ok = im.format == PT_IMAGE_U8 && (C == 3 || C == 4) && q.x0 + 1 < im.width;
+    const uint64_t i0 = im.offset + ((uint64_t)q.y0 * (uint64_t)im.width + (uint64_t)q.x0) * (uint64_t)C;
+    const uint64_t i1 = im.offset + ((uint64_t)q.y1 * (uint64_t)im.width + (uint64_t)q.x0) * (uint64_t)C;
+    q.ok = q.ok && i0 + 2u * (uint64_t)C <= S.n_texel_bytes && i1 + 2u * (uint64_t)C <= S.n_texel_bytes;
+    // (a lane off the fast form reads the buffer's first words; unused)
+    q.w = reinterpret_cast<const uint32_t*>(S.texels + (q.ok ? (i0 & ~3ull) : 0ull));
+    q.vrow = reinterpret_cast<const uint32_t*>(S.texels + (q.ok ? (i1 & ~3ull) : 0ull));
+    q.sh0 = (uint32_t)(i0 & 3u);
+    q.sh1 = (uint32_t)(i1 & 3u);
+    return q;
+}
+__device__ __forceinline__ void tex_quad_decode(int C, uint32_t r0, uint32_t r1, uint32_t r2, uint32_t sh, f3& p,
+                                                f3& q) {
+    const uint32_t q0 = __builtin_amdgcn_alignbyte(r1, r0, sh), q1 = __builtin_amdgcn_alignbyte(r2, r1, sh);
+    const uint32_t qb = C == 4 ? q1 : __builtin_amdgcn_alignbyte(q1, q0, 3u);
+    auto ch = [](uint32_t x, int k) { return u8_unit((x >> (8 * k)) & 0xFFu); };
+    p = F3(ch(q0, 0), ch(q0, 1), ch(q0, 2));
+    q = F3(ch(qb, 0), ch(qb, 1), ch(qb, 2));
+}
+__device__ __forceinline__ f3 tex_bilerp(const TexLeaf& L, float dx, float dy, f3 a, f3 b, f3 c, f3 d) {
+    // contraction of the reference build: w_a*a rounded, then fma(w_b, b), fma(w_c, c), fma(w_d, d)
+    float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
+    f3 r = F3(fma_(wd, d.x, fma_(wc, c.x, fma_(wb, b.x, rmul(wa, a.x)))),
+              fma_(wd, d.y, fma_(wc, c.y, fma_(wb, b.y, rmul(wa, a.y)))),
+              fma_(wd, d.z, fma_(wc, c.z, fma_(wb, b.z, rmul(wa, a.z)))));
+    r = L.val * r;
+    return L.scaled ? L.scale * r : r;
+}
+__device__ __forceinline__ f3 tex_leaf_slow(const TexLeaf& L, const TexQuad& q) {
+    const pt_image im = img_rec(L.image_id);
+    const f3 a = texel3_w(im, q.x0, q.y0), b = texel3_w(im, q.x1, q.y0);
+    const f3 c = texel3_w(im, q.x0, q.y1), d = texel3_w(im, q.x1, q.y1);
+    return tex_bilerp(L, q.dx, q.dy, a, b, c, d);
+}
+template <int N>
+__device__ __forceinline__ void tex_eval_n(const int (&ids)[N], float u, float v, f3 (&out)[N]) {
+    TexLeaf L[N];
+    TexQuad q[N];
+    int ch[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        L[k] = tex_resolve(ids[k], u, v);
+        q[k].ok = false;
+        ch[k] = 0;
+        if (L[k].image) {
+            const pt_image im = img_rec(L[k].image_id);
+            q[k] = tex_quad_addr(im, u, v);
+            ch[k] = im.channels;
+        }
+    }
+    // every footprint's words in flight together
+    uint32_t w[N][6];
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        w[k][0] = w[k][1] = w[k][2] = w[k][3] = w[k][4] = w[k][5] = 0u;
+        if (q[k].ok) {
+            w[k][0] = q[k].w[0], w[k][1] = q[k].w[1], w[k][2] = q[k].w[2];
+            w[k][3] = q[k].vrow[0], w[k][4] = q[k].vrow[1], w[k][5] = q[k].vrow[2];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+        if (!L[k].image) {
+            out[k] = L[k].scaled ? L[k].scale * L[k].val : L[k].val;
+        } else if (q[k].ok) {
+            f3 a, b, c, d;
+            tex_quad_decode(ch[k], w[k][0], w[k][1], w[k][2], q[k].sh0, a, b);
+            tex_quad_decode(ch[k], w[k][3], w[k][4], w[k][5], q[k].sh1, c, d);
+            out[k] = tex_bilerp(L[k], q[k].dx, q[k].dy, a, b, c, d);
+        } else {
+            out[k] = tex_leaf_slow(L[k], q[k]);
+        }
+    }
 }
 
 // PT_TEXREC (A/B option, off): the shading path reads DevTex records.  C4:
@@ -259,11 +429,9 @@ __device__ __forceinline__ f3 tex_eval_r(DevTex t, float u, float v) {
         const int x0 = wrap_index(xi, im.width), x1 = wrap_next(x0, im.width);
         const int y0 = wrap_index(yi, im.height), y1 = wrap_next(y0, im.height);
         f3 a, b, c, d;
-        if (!texel_pair_u8(im, x0, y0, a, b)) {
+        if (!texel_quad_u8(im, x0, y0, y1, a, b, c, d)) {
             a = texel3_w(im, x0, y0);
             b = texel3_w(im, x1, y0);
-        }
-        if (!texel_pair_u8(im, x0, y1, c, d)) {
             c = texel3_w(im, x0, y1);
             d = texel3_w(im, x1, y1);
         }
@@ -401,7 +569,7 @@ __device__ __forceinline__ void sphere_uv(f3 p, float& u, float& v) { sphere_uv_
 // barycentrics; identical to computing it at the candidate (the reference does
 // it per candidate, only the last accepted survives).
 __device__ void tri_interaction(const DevGeom& g, uint32_t tri, int mid, f3 o, f3 d, float t,
-                                float bu, float bv, SurfInt& si) {
+                                float bu, float bv, SurfInt& si, bool nm = true) {
     // one shading record (DevTriShade) instead of S.tri + the indexed
     // normals / uvs / tangents: the same values, the same arithmetic
     const DevTriShade* R = S.tshade + tri;
@@ -433,7 +601,10 @@ __device__ void tri_interaction(const DevGeom& g, uint32_t tri, int mid, f3 o, f
         f3 up = (fabsf(si.ns.x) > 0.9999f) ? F3(0, 1, 0) : F3(1, 0, 0);
         si.tangent = normalize(cross(up, si.ns));
     }
-    si.ns = normal_map(mid, si);
+    // (nm false: mat_tex applies the normal map with the material's other
+    // textures, their texel loads in flight together)
+    if (nm) si.ns = normal_map(mid, si);
+    else si.nm_pending = true;
 }
 
 // QuadShape::Intersect (Shape.cpp:320-343) interaction part.
@@ -575,8 +746,10 @@ struct MatTex {
     float metal;  // DIFFUSE: metal.z
     float ri;
 };
-__device__ __forceinline__ MatTex mat_tex(int mid, const SurfInt& si) {
+__device__ __forceinline__ MatTex mat_tex(int mid, SurfInt& si) {
     const pt_material m = mat_rec(mid);
+    const bool nm = si.nm_pending;
+    si.nm_pending = false;
     MatTex t;
     t.kind = m.kind;
     t.ri = m.ri;
@@ -584,7 +757,21 @@ __device__ __forceinline__ MatTex mat_tex(int mid, const SurfInt& si) {
     t.metal = 0.0f;
     switch (m.kind) {
         case PT_MAT_DIFFUSE: {
-#if PT_LDS_TABLES || !PT_TEXREC
+#if PT_TEX_JOINT && (PT_LDS_TABLES || !PT_TEXREC)
+            if (nm && m.norm >= 0) {  // sample_normalMap (Material.hpp:344-348) with the others
+                f3 r[3];
+                tex_eval_n<3>({m.tex, m.rough, m.norm}, si.u, si.v, r);
+                t.col = r[0];
+                t.rough = smax(r[1].y, 0.0001f);
+                si.ns = to_world_nm(onb_si(si), normalize(2.0f * r[2] - F3(1, 1, 1)));
+            } else {
+                f3 r[2];
+                tex_eval_n<2>({m.tex, m.rough}, si.u, si.v, r);
+                t.col = r[0];
+                t.rough = smax(r[1].y, 0.0001f);
+            }
+            t.metal = tex_eval(m.metal, si.u, si.v).z;
+#elif PT_LDS_TABLES || !PT_TEXREC
             t.rough = smax(tex_eval(m.rough, si.u, si.v).y, 0.0001f);
             t.metal = tex_eval(m.metal, si.u, si.v).z;
             t.col = tex_eval(m.tex, si.u, si.v);
@@ -598,7 +785,20 @@ __device__ __forceinline__ MatTex mat_tex(int mid, const SurfInt& si) {
             break;
         }
         case PT_MAT_DIELECTRIC: {
-#if PT_LDS_TABLES || !PT_TEXREC
+#if PT_TEX_JOINT && (PT_LDS_TABLES || !PT_TEXREC)
+            if (nm && m.norm >= 0) {
+                f3 r[3];
+                tex_eval_n<3>({m.tex, m.rough, m.norm}, si.u, si.v, r);
+                t.col = r[0];
+                t.rough = r[1].y;
+                si.ns = to_world_nm(onb_si(si), normalize(2.0f * r[2] - F3(1, 1, 1)));
+            } else {
+                f3 r[2];
+                tex_eval_n<2>({m.tex, m.rough}, si.u, si.v, r);
+                t.col = r[0];
+                t.rough = r[1].y;
+            }
+#elif PT_LDS_TABLES || !PT_TEXREC
             t.rough = tex_eval(m.rough, si.u, si.v).y;
             t.col = tex_eval(m.tex, si.u, si.v);
 #else

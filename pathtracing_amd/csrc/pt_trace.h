@@ -139,6 +139,7 @@ __device__ __noinline__ bool tri_alpha_slow(uint32_t slot, float bu, float bv, f
 #ifndef PT_ALPHA_INLINE
 #define PT_ALPHA_INLINE 1
 #endif
+__device__ __forceinline__ bool tri_alpha_rec(const DevAlpha& r, uint32_t slot, float bu, float bv, f3 o, f3 d);
 #if PT_ALPHA_INLINE
 __device__ __forceinline__
 #else
@@ -149,7 +150,20 @@ bool tri_alpha(uint32_t ai, uint32_t slot, float bu, float bv, f3 o, f3 d) {
     return true;
 #endif
     if (ai != ALPHA_NONE) {
-        const DevAlpha r = S.alpha[ai];
+        // the whole record in three 16-B loads issued together (a reference
+        // into S.alpha would let the compiler read its fields where they are
+        // used, in branches, one round trip each)
+        const float4* ap = reinterpret_cast<const float4*>(S.alpha + ai);
+        const float4 a0 = ap[0], a1 = ap[1], a2 = ap[2];
+        const DevAlpha r = __builtin_bit_cast(DevAlpha, (DevGeom{a0, a1, a2}));
+        return tri_alpha_rec(r, slot, bu, bv, o, d);
+    }
+    return PT_ALPHA_INLINE ? tri_alpha_slow(slot, bu, bv, o, d) : tri_alpha_general(slot, bu, bv, o, d);
+}
+// the test over an alpha record already read (PT_ALPHA_PREFETCH: the
+// traversal loads it with the triangle test still running)
+__device__ __forceinline__ bool tri_alpha_rec(const DevAlpha& r, uint32_t slot, float bu, float bv, f3 o, f3 d) {
+    {
         const float u = bu, v = bv, w = 1.0f - u - v;
         const float tu = lerp3f(u, r.su[0], v, r.su[1], w, r.su[2]);
         const float tv = lerp3f(u, r.sv[0], v, r.sv[1], w, r.sv[2]);
@@ -183,7 +197,6 @@ bool tri_alpha(uint32_t ai, uint32_t slot, float bu, float bv, f3 o, f3 d) {
         if (mode == PT_ALPHA_MASK) return a > r.cut;
         return a >= 1.0f ? true : (blend_random(o, d, (int)slot) < a);
     }
-    return PT_ALPHA_INLINE ? tri_alpha_slow(slot, bu, bv, o, d) : tri_alpha_general(slot, bu, bv, o, d);
 }
 // the general path: prim info -> shading record -> material -> texture -> image
 __device__ __forceinline__ bool tri_alpha_general(uint32_t slot, float bu, float bv, f3 o, f3 d) {
