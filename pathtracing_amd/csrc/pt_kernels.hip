@@ -180,13 +180,14 @@ __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, flo
 // traversal (trace_pool): 7 (72 VGPRs, no hot-path spills) measured +4.5 %
 // on C4 over the unconstrained 76; 8 (64 VGPRs) spills inside the step loop
 // and loses 30 %.  Overlapped traversal (trace_spec, quantized nodes without
-// instances): 6 (80 VGPRs, no spills); at 7 it spills and loses 3 %
-// (profiles/r03_ab_spec.txt).
+// instances): 7 (72 VGPRs, 1 spilled) since round 5's cheaper pushes and
+// alpha path, closest-hit -2.1 % over 6 (profiles/r05_ab_traversal.txt; in
+// round 3 it spilled and lost 3 %, profiles/r03_ab_spec.txt).
 #ifndef PT_POOL_WPE
 #define PT_POOL_WPE 7
 #endif
 #ifndef PT_SPEC_WPE
-#define PT_SPEC_WPE 6
+#define PT_SPEC_WPE 7
 #endif
 #define PT_POOL_WAVES_FOR(SPEC_) __attribute__((amdgpu_waves_per_eu((SPEC_) ? PT_SPEC_WPE : PT_POOL_WPE, \
                                                                     (SPEC_) ? PT_SPEC_WPE : PT_POOL_WPE)))

@@ -85,6 +85,28 @@ __device__ __forceinline__ pt_image img_rec(int id) {
 }
 
 // ------------------------------------------------------------------ textures
+// The non-negative remainder by the float reciprocal (PT_WRAP_RCP, A/B): for
+// |i| < 2^20 the product i * rcp(n) (rcp within 1 ulp) is within 1/4 of i / n,
+// so floor() is off by at most one and one correction each way gives the
+// exact remainder; other lanes take the integer division.
+#ifndef PT_WRAP_RCP
+#define PT_WRAP_RCP 1
+#endif
+__device__ __forceinline__ int wrap_rcp(int i, int n) {
+    const float q = floorf((float)i * __builtin_amdgcn_rcpf((float)n));
+    int m = i - (int)q * n;
+    m += m < 0 ? n : 0;
+    m -= m >= n ? n : 0;
+    return m;
+}
+// the traversal's alpha test (PT_WRAP_RCP): the reciprocal form where it is exact
+__device__ __forceinline__ int wrap_index(int i, int n);
+__device__ __forceinline__ int wrap_index_t(int i, int n) {
+#if PT_WRAP_RCP
+    if ((uint32_t)i + (1u << 20) < (2u << 20)) return wrap_rcp(i, n);
+#endif
+    return wrap_index(i, n);
+}
 __device__ __forceinline__ int wrap_index(int i, int n) {
     // a power-of-two size: the low bits are the non-negative remainder (two's
     // complement), no integer division

@@ -178,7 +178,7 @@ __device__ __forceinline__ bool tri_alpha_rec(const DevAlpha& r, uint32_t slot, 
             const int xi = (int)floorf(x), yi = (int)floorf(y);
             const float dx = x - xi, dy = y - yi;
             const int ch0 = src == ALPHA_SRC_CH4 ? 3 : 0;
-            const int x0 = wrap_index(xi, W), x1 = wrap_next(x0, W), y0 = wrap_index(yi, H), y1 = wrap_next(y0, H);
+            const int x0 = wrap_index_t(xi, W), x1 = wrap_next(x0, W), y0 = wrap_index_t(yi, H), y1 = wrap_next(y0, H);
             const uint8_t* base = S.texels + off;
             const uint64_t lim = S.n_texel_bytes > off ? S.n_texel_bytes - off : 0ull;
             const uint32_t r0 = (uint32_t)y0 * (uint32_t)W, r1 = (uint32_t)y1 * (uint32_t)W;
