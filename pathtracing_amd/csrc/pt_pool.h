@@ -165,6 +165,9 @@ __device__ unsigned int pt_diag[4];
 #ifndef PT_PUSH_FAST  // A/B option: branch-light child pushes while the LDS stack has room
 #define PT_PUSH_FAST 1
 #endif
+#ifndef PT_SPHERE_INLINE  // spheres without an alpha test tested inline from their slot
+#define PT_SPHERE_INLINE 1
+#endif
 #define Q48_OOB_OFFSET 0xFFFFFF00u  // + 32 stays below 2^32: never wraps into range
 __device__ __forceinline__ float4 q48_buf_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
@@ -693,11 +696,24 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                     next = REF_EMPTY;
                 } else {
                     if (COUNT) wk.tris++;
-                    if (ANY) {
-                        if (other_pred(ps, w0, o, d, tmax)) anyhit = true;
+                    // a sphere without an alpha test inline: its slot holds the
+                    // center (a.xyz) and radius (b.x), so no record read and no
+                    // call (other_closest / other_pred: the same root, uv 0)
+                    const bool sph = PT_SPHERE_INLINE && kind == PT_PRIM_SPHERE && !(w0 & GF_ALPHA);
+                    float t2, a2 = 0.0f, b2 = 0.0f;
+                    bool oh;
+                    if (sph) {
+                        const pt_sphere sp{{g0.x, g0.y, g0.z}, g1.x};
+                        oh = sphere_root(sp, o, d, tmax, t2);
+                    } else if (ANY) {
+                        oh = other_pred(ps, w0, o, d, tmax);
                     } else {
-                        float t2, a2, b2;
-                        if (other_closest(ps, w0, o, d, tmax, t2, a2, b2)) {
+                        oh = other_closest(ps, w0, o, d, tmax, t2, a2, b2);
+                    }
+                    if (ANY) {
+                        if (oh) anyhit = true;
+                    } else {
+                        if (oh) {
                             if ((oct & (OCT_FOUND | OCT_TIE)) == OCT_FOUND && t2 == tmax) {
                                 oct |= OCT_TIE;
                                 src.tie((uint32_t)ri);
