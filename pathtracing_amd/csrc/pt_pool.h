@@ -526,8 +526,11 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         const bool pred = ANY && !(w0 & GF_PRED_GLM);
         float bx = 0, by = 0, t = 0;
         bool tri_hit;
-        if (pred) tri_hit = tri_pred(o, d, xyz(g0), xyz(g1), xyz(g2), tmax);
-        else tri_hit = tri_glm(o, d, xyz(g0), xyz(g1), xyz(g2), bx, by, t) && !(t > tmax || t < PT_EPS);
+        if (pred) tri_hit = PT_TRI_PK ? tri_pred_pk(o, d, xyz(g0), xyz(g1), xyz(g2), tmax)
+                                      : tri_pred(o, d, xyz(g0), xyz(g1), xyz(g2), tmax);
+        else tri_hit = (PT_TRI_PK ? tri_glm_pk(o, d, xyz(g0), xyz(g1), xyz(g2), bx, by, t)
+                                  : tri_glm(o, d, xyz(g0), xyz(g1), xyz(g2), bx, by, t)) &&
+                       !(t > tmax || t < PT_EPS);
         // BLAS hop: its root ref (b.x); triangle: its alpha record (b.w)
         const uint32_t g1v = (w0 & GF_KIND) == PT_PRIM_BLAS ? __float_as_uint(g1.x) : __float_as_uint(g1.w);
         const uint32_t g2w = __float_as_uint(g2.w);
@@ -614,8 +617,11 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
 #endif
             float bx = 0, by = 0, t = 0;
             bool tri_hit;
-            if (pred) tri_hit = tri_pred(o, d, xyz(g0), xyz(g1), xyz(g2), tmax);
-            else tri_hit = tri_glm(o, d, xyz(g0), xyz(g1), xyz(g2), bx, by, t) && !(t > tmax || t < PT_EPS);
+            if (pred) tri_hit = PT_TRI_PK ? tri_pred_pk(o, d, xyz(g0), xyz(g1), xyz(g2), tmax)
+                                          : tri_pred(o, d, xyz(g0), xyz(g1), xyz(g2), tmax);
+            else tri_hit = (PT_TRI_PK ? tri_glm_pk(o, d, xyz(g0), xyz(g1), xyz(g2), bx, by, t)
+                                      : tri_glm(o, d, xyz(g0), xyz(g1), xyz(g2), bx, by, t)) &&
+                           !(t > tmax || t < PT_EPS);
             const uint32_t g1v = (w0 & GF_KIND) == PT_PRIM_BLAS ? __float_as_uint(g1.x) : __float_as_uint(g1.w);
             const uint32_t g2w = __float_as_uint(g2.w);
 #endif

@@ -57,6 +57,70 @@ __device__ __forceinline__ bool tri_pred(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float 
     return t <= tmax && t >= PT_EPS;
 }
 
+// The same two tests on the packed-FP32 ALU (PT_TRI_PK): the x / y lanes of
+// each cross product and each pair of dot products sharing a vector run as
+// one v_pk_mul / v_pk_fma, every lane rounding as the scalar form does
+// (cross: fma(a.y, b.z, -round(b.y * a.z)) ...; dot: fma(z, z, fma(y, y,
+// round(x * x)))), so the results are bit-identical.  Off: the operand pairs
+// need moves into adjacent registers, and the packed build ran the closest-hit
+// kernel 13 % slower (profiles/r05_ab_traversal.txt).
+#ifndef PT_TRI_PK
+#define PT_TRI_PK 0
+#endif
+typedef float tv2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ tv2 pk_fma(tv2 a, tv2 b, tv2 c) { return __builtin_elementwise_fma(a, b, c); }
+// cross(a, b)
+__device__ __forceinline__ f3 cross_pk(f3 a, f3 b) {
+    const tv2 m = tv2{b.y, b.z} * tv2{a.z, a.x};
+    const tv2 xy = pk_fma(tv2{a.y, a.z}, tv2{b.z, b.x}, -m);
+    return F3(xy.x, xy.y, fma_(a.x, b.y, -rmul(b.x, a.y)));
+}
+// (dot(a, c), dot(b, c))
+__device__ __forceinline__ tv2 dot2_pk(f3 a, f3 b, f3 c) {
+    tv2 r = tv2{a.x, b.x} * tv2{c.x, c.x};
+    r = pk_fma(tv2{a.y, b.y}, tv2{c.y, c.y}, r);
+    return pk_fma(tv2{a.z, b.z}, tv2{c.z, c.z}, r);
+}
+__device__ __forceinline__ bool tri_glm_pk(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& bx, float& by, float& t) {
+    const f3 p = cross_pk(d, e2);
+    const tv2 dxy = tv2{o.x, o.y} - tv2{v0.x, v0.y};
+    const f3 dist = F3(dxy.x, dxy.y, o.z - v0.z);
+    const tv2 db = dot2_pk(e1, dist, p);  // det, bx
+    const float det = db.x;
+    bx = db.y;
+    const f3 perp = cross_pk(dist, e1);
+    const tv2 bt = dot2_pk(d, e2, perp);  // by, dot(e2, perp)
+    by = bt.x;
+    bool ok;
+    if (det > 0.0f) ok = !(bx < 0.0f || bx > det) && !(by < 0.0f || bx + by > det);
+    else if (det < 0.0f) ok = !(bx > 0.0f || bx < det) && !(by > 0.0f || bx + by < det);
+    else ok = false;
+    if (!ok) return false;
+    const float inv = 1.0f / det;
+    t = bt.y * inv;
+    const tv2 b2 = tv2{bx, by} * tv2{inv, inv};
+    bx = b2.x;
+    by = b2.y;
+    return true;
+}
+__device__ __forceinline__ bool tri_pred_pk(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float tmax) {
+    const f3 h = cross_pk(d, e2);
+    const tv2 sxy = tv2{o.x, o.y} - tv2{v0.x, v0.y};
+    const f3 s = F3(sxy.x, sxy.y, o.z - v0.z);
+    const tv2 du = dot2_pk(e1, s, h);  // det, dot(s, h)
+    const float det = du.x;
+    if (det > -PT_FLT_EPS && det < PT_FLT_EPS) return false;
+    const float inv = 1.0f / det;
+    const float u = du.y * inv;
+    if (u < 0 || u > 1) return false;
+    const f3 q = cross_pk(s, e1);
+    const tv2 vt = dot2_pk(d, e2, q) * tv2{inv, inv};  // v, t
+    const float v = vt.x;
+    if (v < 0 || u + v > 1) return false;
+    return vt.y <= tmax && vt.y >= PT_EPS;
+}
+
+
 // QuadShape hit test (Shape.cpp:320-359) as built: Intersect tests and
 // divides by dot(d, nn) fused, IntersectPred (PRED) by the unfused dot; beta's
 // cross(u, ph) rounded-first with its dot in y, x, z order
