@@ -46,14 +46,17 @@
 // Continuing paths fill entries [0, c) from the front and new camera paths
 // [cap - r, cap) from the back, so camera rays stay in coherent waves of their
 // own; path i of an iteration (i < c + r) lives at path_slot(i).
-// PT_PATH_AOS (default): the four float4 fields of a path are one 64-B
-// record, so the shading kernel's reads through the hit sort's permutation
-// fetch one 64-B sector per path instead of four (random 16-B reads fetch
-// 64 B each: profiles/r03_fetch_calib.json); 0: one array per field.
+// PT_PATH_AOS 1: the four float4 fields of a path are one 64-B record, so
+// the shading kernel's reads through the hit sort's permutation fetch one
+// 64-B sector per path instead of four (random 16-B reads fetch 64 B each:
+// profiles/r03_fetch_calib.json), but the sequential readers of the ray
+// alone (the traversal's claim, the hit sort's count) fetch 64 B for 32;
+// 2 (default): {o, d} and {beta, L} as two 32-B records -- the ray readers
+// read their 32 B, the shading two sectors per path; 0: one array per field.
 #ifndef PT_PATH_AOS
-#define PT_PATH_AOS 1
+#define PT_PATH_AOS 2
 #endif
-#define PT_PATH_STRIDE (PT_PATH_AOS ? 4u : 1u)
+#define PT_PATH_STRIDE (PT_PATH_AOS == 1 ? 4u : PT_PATH_AOS == 2 ? 2u : 1u)
 struct PField {  // one float4 field of the path state, indexed by entry
     float4* p;
     __device__ __forceinline__ float4& operator[](uint32_t e) const { return p[(size_t)e * PT_PATH_STRIDE]; }

@@ -443,11 +443,13 @@ static void free_scene(pt_ctx* c) {
     c->has_scene = false;
 }
 static void free_work(pt_ctx* c) {
-    // (PT_PATH_AOS: the four fields share the o allocation)
-    void* bufs[] = {c->PA.o.p, PT_PATH_AOS ? nullptr : c->PA.d.p, PT_PATH_AOS ? nullptr : c->PA.beta.p,
-                    PT_PATH_AOS ? nullptr : c->PA.L.p, c->PA.sid, c->PA.time, c->PB.o.p,
-                    PT_PATH_AOS ? nullptr : c->PB.d.p, PT_PATH_AOS ? nullptr : c->PB.beta.p,
-                    PT_PATH_AOS ? nullptr : c->PB.L.p, c->PB.sid, c->PB.time, c->hit, c->qcnt, c->sq, c->counters,
+    // (PT_PATH_AOS 1: the four fields share the o allocation; 2: d shares o's,
+    // L beta's)
+    constexpr bool own_d = PT_PATH_AOS == 0, own_beta = PT_PATH_AOS != 1, own_L = PT_PATH_AOS == 0;
+    void* bufs[] = {c->PA.o.p, own_d ? c->PA.d.p : nullptr, own_beta ? c->PA.beta.p : nullptr,
+                    own_L ? c->PA.L.p : nullptr, c->PA.sid, c->PA.time, c->PB.o.p,
+                    own_d ? c->PB.d.p : nullptr, own_beta ? c->PB.beta.p : nullptr,
+                    own_L ? c->PB.L.p : nullptr, c->PB.sid, c->PB.time, c->hit, c->qcnt, c->sq, c->counters,
                     c->ovf, c->ties, c->sq_time};
     for (void* p : bufs)
         if (p) hipFree(p);
@@ -1409,11 +1411,16 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
     }
     for (PathSoA* P : {&c->PA, &c->PB}) {
         P->cap = (uint32_t)n;
-        if (PT_PATH_AOS) {  // one 64-B record per path (pt_kernels.h PathSoA)
+        if (PT_PATH_AOS == 1) {  // one 64-B record per path (pt_kernels.h PathSoA)
             AL(P->o.p, n * 64);
             P->d.p = P->o.p + 1;
             P->beta.p = P->o.p + 2;
             P->L.p = P->o.p + 3;
+        } else if (PT_PATH_AOS == 2) {  // {o, d} and {beta, L}: two 32-B records per path
+            AL(P->o.p, n * 32);
+            P->d.p = P->o.p + 1;
+            AL(P->beta.p, n * 32);
+            P->L.p = P->beta.p + 1;
         } else {
             AL(P->o.p, n * 16);
             AL(P->d.p, n * 16);
