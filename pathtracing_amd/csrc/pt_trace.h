@@ -200,6 +200,9 @@ __device__ __noinline__ bool tri_alpha_slow(uint32_t slot, float bu, float bv, f
 // the alpha-record path inline in the traversal loop (the general one stays a
 // call): C4 1615 -> 1633 Mrays/s (closest-hit 20.58 -> 20.29 ms per launch,
 // profiles/r04_ab_traversal.txt)
+#ifndef PT_ALPHA_INB  // the alpha test's no-wrap fast path (uniform branch)
+#define PT_ALPHA_INB 1
+#endif
 #ifndef PT_ALPHA_INLINE
 #define PT_ALPHA_INLINE 1
 #endif
@@ -242,7 +245,16 @@ __device__ __forceinline__ bool tri_alpha_rec(const DevAlpha& r, uint32_t slot, 
             const int xi = (int)floorf(x), yi = (int)floorf(y);
             const float dx = x - xi, dy = y - yi;
             const int ch0 = src == ALPHA_SRC_CH4 ? 3 : 0;
-            const int x0 = wrap_index_t(xi, W), x1 = wrap_next(x0, W), y0 = wrap_index_t(yi, H), y1 = wrap_next(y0, H);
+            // a footprint inside the image needs no wrap; when every active
+            // lane's is (a leaf card's uvs in [0, 1]: all but its edge texels),
+            // the wave skips the remainders (a uniform branch)
+            int x0, x1, y0, y1;
+            const bool inb = (uint32_t)xi < (uint32_t)(W - 1) && (uint32_t)yi < (uint32_t)(H - 1);
+            if (PT_ALPHA_INB && __ballot(!inb) == 0) {
+                x0 = xi, x1 = xi + 1, y0 = yi, y1 = yi + 1;
+            } else {
+                x0 = wrap_index_t(xi, W), x1 = wrap_next(x0, W), y0 = wrap_index_t(yi, H), y1 = wrap_next(y0, H);
+            }
             const uint8_t* base = S.texels + off;
             const uint64_t lim = S.n_texel_bytes > off ? S.n_texel_bytes - off : 0ull;
             const uint32_t r0 = (uint32_t)y0 * (uint32_t)W, r1 = (uint32_t)y1 * (uint32_t)W;
