@@ -1027,13 +1027,19 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
                                         (L.instance >= 0 && (uint32_t)L.instance >= s->n_instances)))
             return fail(c, PT_ERR_ARG, "light %u: bad area light", l);
     }
-    // (the texel lookups index an image's elements in 32 bits)
+    // (the texel lookups index an image's elements in 32 bits, and the alpha
+    // test reads an image's texels without a bound check: each image must lie
+    // inside the texel buffer)
     for (uint32_t k = 0; k < s->n_images; k++) {
         const pt_image& im = s->images[k];
-        if (im.width <= 0 || im.height <= 0 || im.channels <= 0 ||
-            (uint64_t)im.width * (uint64_t)im.height * (uint64_t)im.channels >= (1ull << 32))
+        const uint64_t elems = (uint64_t)std::max(im.width, 0) * (uint64_t)std::max(im.height, 0) *
+                               (uint64_t)std::max(im.channels, 0);
+        if (im.width <= 0 || im.height <= 0 || im.channels <= 0 || elems >= (1ull << 32))
             return fail(c, PT_ERR_ARG, "image %u: bad size (%d x %d x %d channels; below 2^32 elements)", k,
                         im.width, im.height, im.channels);
+        const uint64_t bytes = elems * (im.format == PT_IMAGE_F32 ? 4ull : 1ull);
+        if (im.offset > s->n_texel_bytes || bytes > s->n_texel_bytes - im.offset)
+            return fail(c, PT_ERR_ARG, "image %u: texels past the texel buffer", k);
     }
     for (uint32_t k = 0; k < s->n_textures; k++) {
         const pt_texture& T = s->textures[k];

@@ -719,3 +719,21 @@ def test_gpu_stratified_camera_lowers_the_pixel_variance():
     v_strat = frames((4, 4)).var(0).mean(-1)
     edge = v_plain > np.percentile(v_plain, 75)  # pixels whose estimate the camera draws move most
     assert v_strat[edge].mean() < 0.7 * v_plain[edge].mean(), (v_strat[edge].mean(), v_plain[edge].mean())
+
+
+def test_gpu_upload_rejects_an_image_past_the_texel_buffer():
+    """pt_scene_upload checks every image lies inside the texel buffer (the
+    alpha test reads an image's texels without a bound check): an image whose
+    texels run past the buffer is PT_ERR_ARG, the unmodified scene uploads."""
+    import copy
+    setup = scenes.alpha_maps(W=16, H=16, spp=1)
+    integ = setup.make_integrator()
+    ctx = integ.context()
+    flat = integ.flat
+    assert flat.images.shape[0] > 0
+    bad = copy.copy(flat)
+    bad.images = flat.images.copy()
+    bad.images["offset"][0] = flat.texels.size  # its texels start at the buffer's end
+    with pytest.raises(N.NativeError):
+        ctx.upload(bad)
+    ctx.upload(flat)  # and the real one again
