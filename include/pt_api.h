@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define PT_API_VERSION 6
+#define PT_API_VERSION 7
 
 typedef int32_t pt_status;
 #define PT_OK 0
@@ -94,8 +94,18 @@ typedef struct pt_prim {
  * (bvhs[bvh], a Model or a one-primitive BVH) under a glm::mat4 transform,
  * column-major m[col][row], and its glm::inverse.  A hit inside the instance
  * is reported as the virtual slot virt_base + (BLAS slot - prim_base); virtual
- * slots start at n_prims and the instances' ranges are ascending.  One level:
- * no instance inside an instance, no area light inside an instance. */
+ * slots start at n_prims and the instances' ranges are ascending.
+ *
+ * Nested wrappers (a TransformedPrimitive / AnimatedPrimitive whose primitive
+ * is itself one, Primitive.cpp:48-64, 86-89): `inner` chains the levels, the
+ * outermost first.  inner = -1 ends the chain at bvhs[bvh]; otherwise it names
+ * the next level down, an instance record with a larger index that no TLAS
+ * slot references (a level record), at most PT_MAX_INSTANCE_DEPTH levels in
+ * all.  Every record of a chain names the same bvh; a level record's
+ * virt_base is unused.  Rays enter the levels outermost first (each level's
+ * inverse, length and max * length in turn); hits leave innermost first
+ * (t / length per level). */
+#define PT_MAX_INSTANCE_DEPTH 4
 typedef struct pt_instance {
     float transform[16];
     float inv[16];
@@ -108,6 +118,7 @@ typedef struct pt_instance {
     float motion[3];
     float time_bounds[2];
     uint32_t animated;
+    int32_t inner;       /* the next level down, or -1 (API v7)             */
 } pt_instance;
 
 typedef struct pt_bvh_desc {

@@ -405,56 +405,73 @@ struct Flat {
             blas.push_back(Blas{b, gp});
             return blas_index[key] = (uint32_t)blas.size() - 1;
         };
-        struct Inst {
-            uint32_t blas;
+        // one wrapper level: TransformedPrimitive / AnimatedPrimitive
+        struct Level {
             glm::mat4 xf, inv;
             bool animated = false;  // AnimatedPrimitive: translated per ray at its time
             glm::vec3 dir{0};
             glm::vec2 tb{0};
         };
+        struct Inst {
+            uint32_t blas;
+            std::vector<Level> levels;  // nested wrappers, the outermost first (pt_instance.inner)
+        };
         std::vector<Inst> inst;
         std::vector<uint32_t> blas_of_slot(n_top, UINT32_MAX), inst_of_slot(n_top, UINT32_MAX);
         auto mat_key = [](const glm::mat4& m) { return std::string((const char*)&m[0][0], sizeof(glm::mat4)); };
-        std::map<std::pair<const Light*, std::string>, int32_t> inst_light;  // (inner light, matrix) -> instance
+        // (inner AreaLight, the wrappers' matrices outermost first) -> instance
+        std::map<std::pair<const Light*, std::string>, int32_t> inst_light;
         std::vector<std::shared_ptr<Light>> inner_lights;
-        for (uint32_t i = 0; i < n_top; i++) {
-            const Primitive* p = top[i].get();
-            if (dynamic_cast<const GeometricPrimitive*>(p)) continue;
-            const Primitive* inner = nullptr;
-            glm::mat4 xf, inv;
-            Inst anim{};
+        // a wrapper level, or false for anything else
+        auto level_of = [&](const Primitive* p, Level& lv, const Primitive*& inner) {
             if (auto* tp = dynamic_cast<const TransformedPrimitive*>(p)) {
                 inner = PT_GET(*tp, TpPrim).get();
-                xf = PT_GET(*tp, TpXf);
-                inv = PT_GET(*tp, TpInv);
-            } else if (auto* ap = dynamic_cast<const AnimatedPrimitive*>(p)) {
+                lv.xf = PT_GET(*tp, TpXf);
+                lv.inv = PT_GET(*tp, TpInv);
+                return true;
+            }
+            if (auto* ap = dynamic_cast<const AnimatedPrimitive*>(p)) {
                 // AnimatedPrimitive::Intersect (Primitive.cpp:86-89): the
                 // device translates by dir * t at each ray's time; the time-0
                 // matrix keys its AnimatedLights below
                 inner = PT_GET(*ap, ApPrim).get();
                 const glm::vec2 tb = PT_GET(*ap, ApTb);
                 const float t = glm::clamp(0.0f - tb.x, tb.x, tb.y) / (tb.y - tb.x);
-                xf = glm::translate(glm::mat4(1), PT_GET(*ap, ApDir) * t);
-                inv = glm::inverse(xf);
-                anim.animated = true;
-                anim.dir = PT_GET(*ap, ApDir);
-                anim.tb = tb;
-            } else {
+                lv.xf = glm::translate(glm::mat4(1), PT_GET(*ap, ApDir) * t);
+                lv.inv = glm::inverse(lv.xf);
+                lv.animated = true;
+                lv.dir = PT_GET(*ap, ApDir);
+                lv.tb = tb;
+                return true;
+            }
+            return false;
+        };
+        for (uint32_t i = 0; i < n_top; i++) {
+            const Primitive* p = top[i].get();
+            if (dynamic_cast<const GeometricPrimitive*>(p)) continue;
+            Inst in{};
+            const Primitive* inner = p;
+            for (Level lv; level_of(inner, lv, inner); lv = Level{}) in.levels.push_back(lv);
+            if (in.levels.empty()) {
                 blas_of_slot[i] = blas_of(p);
                 if (blas_of_slot[i] == UINT32_MAX) throw std::runtime_error("HipPathIntegrator: unsupported TLAS primitive");
                 continue;
             }
-            // emitters inside the instance: TransformedPrimitive / AnimatedPrimitive
-            // ::GetLights wrap its inner AreaLights with this very matrix
-            // (Primitive.cpp:66-73, 91-96; Light.cpp:338-364)
+            if (in.levels.size() > PT_MAX_INSTANCE_DEPTH)
+                throw std::runtime_error("HipPathIntegrator: instances nested deeper than PT_MAX_INSTANCE_DEPTH");
+            // emitters inside the instance: each wrapper's GetLights wraps its
+            // inner primitive's lights with its own matrix (Primitive.cpp:66-73,
+            // 91-96; Light.cpp:338-364), keyed here by the whole chain
+            std::string key;
+            for (const Level& lv : in.levels) key += mat_key(lv.xf);
             for (const auto& l : inner->GetLights()) {
-                inst_light[{l.get(), mat_key(xf)}] = (int32_t)inst.size();
+                inst_light[{l.get(), key}] = (int32_t)inst.size();
                 inner_lights.push_back(l);
             }
-            const uint32_t b = blas_of(inner);
-            if (b == UINT32_MAX) throw std::runtime_error("HipPathIntegrator: unsupported instanced primitive");
+            in.blas = blas_of(inner);
+            if (in.blas == UINT32_MAX) throw std::runtime_error("HipPathIntegrator: unsupported instanced primitive");
             inst_of_slot[i] = (uint32_t)inst.size();
-            inst.push_back(Inst{b, xf, inv, anim.animated, anim.dir, anim.tb});
+            inst.push_back(std::move(in));
         }
         auto blas_count = [&](const Blas& b) -> uint32_t {
             return b.gp ? 1u : (uint32_t)PT_GET(*static_cast<const BLASBase*>(b.b), BlasPrims).size();
@@ -474,19 +491,33 @@ struct Flat {
         t.n_prims = n_top;
         bvhs.push_back(t);
         uint32_t virt = total;  // virtual slots of the instances' primitives, ascending
+        auto record = [&](const Level& lv, uint32_t b) {
+            pt_instance r{};
+            std::memcpy(r.transform, &lv.xf[0][0], sizeof(r.transform));
+            std::memcpy(r.inv, &lv.inv[0][0], sizeof(r.inv));
+            r.bvh = 1 + b;
+            r.inner = -1;
+            if (lv.animated) {
+                r.animated = 1;
+                put3(r.motion, lv.dir);
+                r.time_bounds[0] = lv.tb.x;
+                r.time_bounds[1] = lv.tb.y;
+            }
+            return r;
+        };
+        // the inner levels of nested wrappers follow every record a TLAS slot names
+        uint32_t n_top_inst = 0;
+        for (uint32_t i = 0; i < n_top; i++) n_top_inst += inst_of_slot[i] != UINT32_MAX;
+        std::vector<pt_instance> level_records;
         for (uint32_t i = 0; i < n_top; i++) {
             if (inst_of_slot[i] != UINT32_MAX) {
                 const Inst& in = inst[inst_of_slot[i]];
-                pt_instance r{};
-                std::memcpy(r.transform, &in.xf[0][0], sizeof(r.transform));
-                std::memcpy(r.inv, &in.inv[0][0], sizeof(r.inv));
-                r.bvh = 1 + in.blas;
+                pt_instance r = record(in.levels[0], in.blas);
                 r.virt_base = virt;
-                if (in.animated) {
-                    r.animated = 1;
-                    put3(r.motion, in.dir);
-                    r.time_bounds[0] = in.tb.x;
-                    r.time_bounds[1] = in.tb.y;
+                for (size_t k = 1; k < in.levels.size(); k++) {  // linked outermost first
+                    const int32_t at = (int32_t)(n_top_inst + level_records.size());
+                    (k == 1 ? r : level_records.back()).inner = at;
+                    level_records.push_back(record(in.levels[k], in.blas));
                 }
                 virt += blas_count(blas[in.blas]);
                 prims[i] = pt_prim{PT_PRIM_INSTANCE, (uint32_t)instances.size(), -1, -1, -1};
@@ -497,6 +528,7 @@ struct Flat {
                 geometric(*static_cast<const GeometricPrimitive*>(top[i].get()), i);
             }
         }
+        instances.insert(instances.end(), level_records.begin(), level_records.end());
         own_clusters.reserve(blas.size());
         for (size_t k = 0; k < blas.size(); k++) {
             pt_bvh_desc d{};
@@ -552,10 +584,33 @@ struct Flat {
             r.instance = instance;
             return it->second;
         };
-        auto wrapped = [&](const Light* inner, const glm::mat4& xf) {
-            auto it = inst_light.find({inner, mat_key(xf)});
+        // a TransformedLight / AnimatedLight, possibly wrapping another (a nested
+        // wrapper's light): its AreaLight and the instance its chain of matrices names
+        struct Unwrapped {
+            const Light* area;
+            int32_t instance;
+        };
+        auto unwrap = [&](const Light* l) {
+            std::string key;
+            for (;;) {
+                if (auto* t = dynamic_cast<const TransformedLight*>(l)) {
+                    key += mat_key(PT_GET(*t, TlXf));
+                    l = PT_GET(*t, TlLight).get();
+                } else if (auto* an = dynamic_cast<const AnimatedLight*>(l)) {
+                    // AnimatedLight (Light.cpp:338-364): the light of the
+                    // AnimatedPrimitive whose time-0 matrix this is; the device
+                    // moves it with that instance at each ray's time
+                    const glm::vec2 tb = PT_GET(*an, AlTb);
+                    const float tt = glm::clamp(0.0f - tb.x, tb.x, tb.y) / (tb.y - tb.x);
+                    key += mat_key(glm::translate(glm::mat4(1), PT_GET(*an, AlDir) * tt));
+                    l = PT_GET(*an, AlLight).get();
+                } else {
+                    break;
+                }
+            }
+            auto it = inst_light.find({l, key});
             if (it == inst_light.end()) throw std::runtime_error("HipPathIntegrator: light of an unknown instance");
-            return it->second;
+            return Unwrapped{l, it->second};
         };
         for (const auto& l : all) {
             pt_light r{};
@@ -563,17 +618,9 @@ struct Flat {
             r.instance = -1;
             r.power = l->Power();
             r.pmf = ls ? ls->PMF(l) : 0.0f;
-            if (auto* t = dynamic_cast<const TransformedLight*>(l.get())) {
-                const Light* inner = PT_GET(*t, TlLight).get();
-                area(r, inner, wrapped(inner, PT_GET(*t, TlXf)));
-            } else if (auto* an = dynamic_cast<const AnimatedLight*>(l.get())) {
-                // AnimatedLight (Light.cpp:338-364): the light of the
-                // AnimatedPrimitive whose time-0 matrix this is; the device
-                // moves it with that instance at each ray's time
-                const Light* inner = PT_GET(*an, AlLight).get();
-                const glm::vec2 tb = PT_GET(*an, AlTb);
-                const float tt = glm::clamp(0.0f - tb.x, tb.x, tb.y) / (tb.y - tb.x);
-                area(r, inner, wrapped(inner, glm::translate(glm::mat4(1), PT_GET(*an, AlDir) * tt)));
+            if (dynamic_cast<const TransformedLight*>(l.get()) || dynamic_cast<const AnimatedLight*>(l.get())) {
+                const Unwrapped u = unwrap(l.get());
+                area(r, u.area, u.instance);
             } else if (auto* a = dynamic_cast<const AreaLight*>(l.get())) {
                 auto it = light_slot.find(a);
                 if (it == light_slot.end()) throw std::runtime_error("HipPathIntegrator: area light without a primitive");

@@ -822,29 +822,49 @@ static ray_t instance_ray(const pt_instance* I, const ray_t* r, float* len) {
     return mkray_t(m4_point(I->inv, r->o), divs(dir, *len), r->time);
 }
 
+/* TransformedPrimitive::Intersect (Primitive.cpp:48-64) of instance record k:
+ * its primitive is the next level down (pt_instance.inner, a nested wrapper)
+ * or the BLAS; tmp.prim stays the BLAS slot */
+static int inst_intersect(const scene_t* S, int32_t k, const ray_t* r, float max, si_t* si, work_t* wk) {
+    pt_instance at_time;
+    const pt_instance* I = inst_at(&S->s->instances[k], r->time, &at_time);
+    float len;
+    ray_t tr = instance_ray(I, r, &len);
+    float m = max * len;
+    si_t tmp;
+    memset(&tmp, 0, sizeof(tmp));
+    if (I->inner >= 0) {
+        if (!inst_intersect(S, I->inner, &tr, m, &tmp, wk)) return 0;
+    } else if (!bvh_intersect(S, &S->s->bvhs[I->bvh], &tr, &m, &tmp, wk)) {
+        return 0;
+    }
+    float NM[9];
+    normal_matrix(I->transform, NM);
+    *si = tmp;
+    si->p = m4_point(I->transform, tmp.p);
+    si->n = normalize(m3_mul(NM, tmp.n));
+    si->ns = normalize(m3_mul(NM, tmp.ns));
+    si->t = tmp.t / len;
+    si->tangent = normalize4(m4_dir(I->transform, tmp.tangent));
+    return 1;
+}
+static int inst_pred(const scene_t* S, int32_t k, const ray_t* r, float max, work_t* wk) {
+    pt_instance at_time;
+    const pt_instance* I = inst_at(&S->s->instances[k], r->time, &at_time);
+    float len;
+    ray_t tr = instance_ray(I, r, &len);
+    if (I->inner >= 0) return inst_pred(S, I->inner, &tr, max * len, wk);
+    return bvh_pred(S, &S->s->bvhs[I->bvh], &tr, max * len, wk);
+}
+
 /* GeometricPrimitive::Intersect (Primitive.cpp:15-26) / Model::Intersect (Model.hpp:25-27) */
 static int prim_intersect(const scene_t* S, uint32_t slot, const ray_t* r, float max, si_t* si, work_t* wk) {
     const pt_prim* p = &S->s->prims[slot];
     if (p->kind == PT_PRIM_BLAS) return bvh_intersect(S, &S->s->bvhs[p->index], r, &max, si, wk);
     if (p->kind == PT_PRIM_INSTANCE) {
-        pt_instance at_time;
-        const pt_instance* I = inst_at(&S->s->instances[p->index], r->time, &at_time);
-        const pt_bvh_desc* B = &S->s->bvhs[I->bvh];
-        float len;
-        ray_t tr = instance_ray(I, r, &len);
-        float m = max * len;
-        si_t tmp;
-        memset(&tmp, 0, sizeof(tmp));
-        if (!bvh_intersect(S, B, &tr, &m, &tmp, wk)) return 0;
-        float NM[9];
-        normal_matrix(I->transform, NM);
-        *si = tmp;
-        si->p = m4_point(I->transform, tmp.p);
-        si->n = normalize(m3_mul(NM, tmp.n));
-        si->ns = normalize(m3_mul(NM, tmp.ns));
-        si->t = tmp.t / len;
-        si->tangent = normalize4(m4_dir(I->transform, tmp.tangent));
-        si->prim = (int)(I->virt_base + ((uint32_t)tmp.prim - B->prim_base));
+        const pt_instance* I = &S->s->instances[p->index];
+        if (!inst_intersect(S, (int32_t)p->index, r, max, si, wk)) return 0;
+        si->prim = (int)(I->virt_base + ((uint32_t)si->prim - S->s->bvhs[I->bvh].prim_base));
         return 1;
     }
     si_t tmp;
@@ -867,13 +887,8 @@ static int prim_intersect(const scene_t* S, uint32_t slot, const ray_t* r, float
 static int prim_pred(const scene_t* S, uint32_t slot, const ray_t* r, float max, work_t* wk) {
     const pt_prim* p = &S->s->prims[slot];
     if (p->kind == PT_PRIM_BLAS) return bvh_pred(S, &S->s->bvhs[p->index], r, max, wk);
-    if (p->kind == PT_PRIM_INSTANCE) { /* TransformedPrimitive::IntersectPred (Primitive.cpp:42-47) */
-        pt_instance at_time;
-        const pt_instance* I = inst_at(&S->s->instances[p->index], r->time, &at_time);
-        float len;
-        ray_t tr = instance_ray(I, r, &len);
-        return bvh_pred(S, &S->s->bvhs[I->bvh], &tr, max * len, wk);
-    }
+    if (p->kind == PT_PRIM_INSTANCE) /* TransformedPrimitive::IntersectPred (Primitive.cpp:42-47) */
+        return inst_pred(S, (int32_t)p->index, r, max, wk);
     wk->tris++;
     if (mat_has_alpha(S, p->material)) {
         si_t tmp;
@@ -1415,9 +1430,16 @@ static float texinf_uc(const rng_t* r) {
 }
 
 /* TransformedLight / AnimatedLight (Light.cpp:300-364): the inner
- * AreaLight's shape in the instance's object space */
-static const pt_instance* light_instance(const scene_t* S, const pt_light* l, float time, pt_instance* tmp) {
-    return (l->kind == PT_LIGHT_AREA && l->instance >= 0) ? inst_at(&S->s->instances[l->instance], time, tmp) : NULL;
+ * AreaLight's shape in the instance's object space.  A nested wrapper's
+ * light is a TransformedLight of a TransformedLight: lv receives the levels
+ * at the time, the outermost first (tmp holds their storage); returns the
+ * count, 0 for a light outside any instance */
+static int light_levels(const scene_t* S, const pt_light* l, float time, pt_instance* tmp, const pt_instance** lv) {
+    if (l->kind != PT_LIGHT_AREA || l->instance < 0) return 0;
+    int k = 0;
+    for (int32_t i = l->instance; i >= 0 && k < PT_MAX_INSTANCE_DEPTH; i = S->s->instances[i].inner, k++)
+        lv[k] = inst_at(&S->s->instances[i], time, &tmp[k]);
+    return k;
 }
 /* Light::sample(uv, time) (Light.hpp:21): the time moves an AnimatedLight */
 static lsample_t light_sample(const scene_t* S, const pt_light* l, float u0, float u1, float uc, float time) {
@@ -1445,12 +1467,14 @@ static lsample_t light_sample(const scene_t* S, const pt_light* l, float u0, flo
     }
     if (l->kind == PT_LIGHT_AREA) {
         ls.si = shape_sample(S, &S->s->prims[l->prim], u0, u1);
-        pt_instance at_time;
-        const pt_instance* I = light_instance(S, l, time, &at_time);
-        if (I) { /* TransformedLight::sample: p by the transform, n by the normal matrix */
+        pt_instance tmp[PT_MAX_INSTANCE_DEPTH];
+        const pt_instance* lv[PT_MAX_INSTANCE_DEPTH];
+        /* TransformedLight::sample: p by the transform, n by the normal
+         * matrix, of the inner light's sample (the innermost level first) */
+        for (int k = light_levels(S, l, time, tmp, lv) - 1; k >= 0; k--) {
             float NM[9];
-            normal_matrix(I->transform, NM);
-            ls.si.p = m4_point(I->transform, ls.si.p);
+            normal_matrix(lv[k]->transform, NM);
+            ls.si.p = m4_point(lv[k]->transform, ls.si.p);
             ls.si.n = m3_mul(NM, ls.si.n);
         }
         return ls;
@@ -1492,15 +1516,19 @@ static inline int light_is_delta(const pt_light* l) { return l->kind == PT_LIGHT
 static float light_pdf(const scene_t* S, const pt_light* l, const si_t* si, const ray_t* r) {
     if (l->kind == PT_LIGHT_AREA) {
         const pt_prim* p = &S->s->prims[l->prim];
-        pt_instance at_time;
-        const pt_instance* I = light_instance(S, l, r->time, &at_time);
-        if (I) { /* TransformedLight::PDF: point, normal and ray to object space */
+        pt_instance tmp[PT_MAX_INSTANCE_DEPTH];
+        const pt_instance* lv[PT_MAX_INSTANCE_DEPTH];
+        const int nl = light_levels(S, l, r->time, tmp, lv);
+        if (nl) { /* TransformedLight::PDF: point, normal and ray to object space, the outermost level first */
             si_t lo = *si;
-            lo.p = m4_point(I->inv, si->p);
-            lo.n = normalize(m4_dir(I->inv, si->n));
             ray_t lr = *r;
-            lr.o = m4_point(I->inv, r->o);
-            lr.d = normalize(m4_dir(I->inv, r->d));
+            for (int k = 0; k < nl; k++) {
+                const float* inv = lv[k]->inv;
+                lo.p = m4_point(inv, lo.p);
+                lo.n = normalize(m4_dir(inv, lo.n));
+                lr.o = m4_point(inv, lr.o);
+                lr.d = normalize(m4_dir(inv, lr.d));
+            }
             if (l->one_sided) return dot(neg(lr.d), lo.n) > 0 ? shape_pdf(S, p, &lo, &lr, 1) : 0;
             return shape_pdf(S, p, &lo, &lr, 0);
         }
@@ -1513,12 +1541,17 @@ static float light_pdf(const scene_t* S, const pt_light* l, const si_t* si, cons
 }
 static v3 light_L(const scene_t* S, const pt_light* l, const si_t* si, const ray_t* r) {
     if (l->kind == PT_LIGHT_AREA) {
-        pt_instance at_time;
-        const pt_instance* I = light_instance(S, l, r->time, &at_time);
-        if (I) { /* TransformedLight::L: a fresh interaction, n by the normal matrix, uv (0, 0) */
-            float NM[9];
-            normal_matrix(I->transform, NM);
-            const v3 n = m3_mul(NM, si->n);
+        pt_instance tmp[PT_MAX_INSTANCE_DEPTH];
+        const pt_instance* lv[PT_MAX_INSTANCE_DEPTH];
+        const int nl = light_levels(S, l, r->time, tmp, lv);
+        if (nl) { /* TransformedLight::L: a fresh interaction, n by the normal matrix
+                   * (the outermost level first), uv (0, 0) */
+            v3 n = si->n;
+            for (int k = 0; k < nl; k++) {
+                float NM[9];
+                normal_matrix(lv[k]->transform, NM);
+                n = m3_mul(NM, n);
+            }
             const float uv0[2] = {0, 0};
             if (l->one_sided && dot(r->d, n) > 0) return V(0, 0, 0);
             return tex_eval(S, l->tex, uv0);

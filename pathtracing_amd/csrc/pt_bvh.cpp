@@ -382,62 +382,54 @@ extern "C" pt_status pt_bvh4_build(const float* boxes, uint32_t n, pt_ref_bvh4_c
 
 // ---------------------------------------------------------------------------
 // Instance matrices (host).  glm::inverse(mat4) (glm/detail/func_matrix.inl,
-// compute_inverse<4,4>) with glm's expression structure, compiled like the
-// reference (GNU dialect, FMA contraction) so that TransformedPrimitive's
-// invTransform (Primitive.hpp:37) comes out the same.  m, out: column-major
-// m[c*4+r].
-namespace {
-struct V4 {
-    float v[4];
-};
-inline V4 operator*(const V4& a, const V4& b) { return {{a.v[0] * b.v[0], a.v[1] * b.v[1], a.v[2] * b.v[2], a.v[3] * b.v[3]}}; }
-inline V4 operator-(const V4& a, const V4& b) { return {{a.v[0] - b.v[0], a.v[1] - b.v[1], a.v[2] - b.v[2], a.v[3] - b.v[3]}}; }
-inline V4 operator+(const V4& a, const V4& b) { return {{a.v[0] + b.v[0], a.v[1] + b.v[1], a.v[2] + b.v[2], a.v[3] + b.v[3]}}; }
-inline V4 operator*(const V4& a, float s) { return {{a.v[0] * s, a.v[1] * s, a.v[2] * s, a.v[3] * s}}; }
-}  // namespace
-
+// compute_inverse<4,4>) with every fused multiply-add the reference build
+// (g++ -O3 -march=native) forms in it spelled out, so that
+// TransformedPrimitive's invTransform (Primitive.hpp:37) comes out bit for
+// bit: the cofactors as fused a*b minus a rounded c*d, each lane of Inv0..3
+// as a rounded first product with the second and third fused in turn, the
+// determinant's pairs fused once (read from GCC's GIMPLE of that function;
+// oracle/glm_inverse_probe.cpp computes the reference the two over random affine and
+// general matrices).  Explicit, so this file's own contraction cannot change
+// it.  m, out: column-major m[c*4+r].
 extern "C" pt_status pt_mat4_inverse(const float* mm, float* out) {
     if (!mm || !out) return PT_ERR_ARG;
-    float m[4][4];
-    for (int c = 0; c < 4; c++)
-        for (int r = 0; r < 4; r++) m[c][r] = mm[c * 4 + r];
-    const float Coef00 = m[2][2] * m[3][3] - m[3][2] * m[2][3];
-    const float Coef02 = m[1][2] * m[3][3] - m[3][2] * m[1][3];
-    const float Coef03 = m[1][2] * m[2][3] - m[2][2] * m[1][3];
-    const float Coef04 = m[2][1] * m[3][3] - m[3][1] * m[2][3];
-    const float Coef06 = m[1][1] * m[3][3] - m[3][1] * m[1][3];
-    const float Coef07 = m[1][1] * m[2][3] - m[2][1] * m[1][3];
-    const float Coef08 = m[2][1] * m[3][2] - m[3][1] * m[2][2];
-    const float Coef10 = m[1][1] * m[3][2] - m[3][1] * m[1][2];
-    const float Coef11 = m[1][1] * m[2][2] - m[2][1] * m[1][2];
-    const float Coef12 = m[2][0] * m[3][3] - m[3][0] * m[2][3];
-    const float Coef14 = m[1][0] * m[3][3] - m[3][0] * m[1][3];
-    const float Coef15 = m[1][0] * m[2][3] - m[2][0] * m[1][3];
-    const float Coef16 = m[2][0] * m[3][2] - m[3][0] * m[2][2];
-    const float Coef18 = m[1][0] * m[3][2] - m[3][0] * m[1][2];
-    const float Coef19 = m[1][0] * m[2][2] - m[2][0] * m[1][2];
-    const float Coef20 = m[2][0] * m[3][1] - m[3][0] * m[2][1];
-    const float Coef22 = m[1][0] * m[3][1] - m[3][0] * m[1][1];
-    const float Coef23 = m[1][0] * m[2][1] - m[2][0] * m[1][1];
-    const V4 Fac0{{Coef00, Coef00, Coef02, Coef03}}, Fac1{{Coef04, Coef04, Coef06, Coef07}};
-    const V4 Fac2{{Coef08, Coef08, Coef10, Coef11}}, Fac3{{Coef12, Coef12, Coef14, Coef15}};
-    const V4 Fac4{{Coef16, Coef16, Coef18, Coef19}}, Fac5{{Coef20, Coef20, Coef22, Coef23}};
-    const V4 Vec0{{m[1][0], m[0][0], m[0][0], m[0][0]}}, Vec1{{m[1][1], m[0][1], m[0][1], m[0][1]}};
-    const V4 Vec2{{m[1][2], m[0][2], m[0][2], m[0][2]}}, Vec3{{m[1][3], m[0][3], m[0][3], m[0][3]}};
-    const V4 Inv0 = Vec1 * Fac0 - Vec2 * Fac1 + Vec3 * Fac2;
-    const V4 Inv1 = Vec0 * Fac0 - Vec2 * Fac3 + Vec3 * Fac4;
-    const V4 Inv2 = Vec0 * Fac1 - Vec1 * Fac3 + Vec3 * Fac5;
-    const V4 Inv3 = Vec0 * Fac2 - Vec1 * Fac4 + Vec2 * Fac5;
-    const V4 SignA{{+1, -1, +1, -1}}, SignB{{-1, +1, -1, +1}};
-    const V4 I[4] = {Inv0 * SignA, Inv1 * SignB, Inv2 * SignA, Inv3 * SignB};
-    const V4 Row0{{I[0].v[0], I[1].v[0], I[2].v[0], I[3].v[0]}};
-    const V4 M0{{m[0][0], m[0][1], m[0][2], m[0][3]}};
-    const V4 Dot0 = M0 * Row0;
-    const float Dot1 = (Dot0.v[0] + Dot0.v[1]) + (Dot0.v[2] + Dot0.v[3]);
-    const float OneOverDeterminant = 1.0f / Dot1;
-    for (int c = 0; c < 4; c++) {
-        const V4 r = I[c] * OneOverDeterminant;
-        for (int k = 0; k < 4; k++) out[c * 4 + k] = r.v[k];
-    }
+    // m[c][r]
+    const float m00 = mm[0], m01 = mm[1], m02 = mm[2], m03 = mm[3];
+    const float m10 = mm[4], m11 = mm[5], m12 = mm[6], m13 = mm[7];
+    const float m20 = mm[8], m21 = mm[9], m22 = mm[10], m23 = mm[11];
+    const float m30 = mm[12], m31 = mm[13], m32 = mm[14], m33 = mm[15];
+    // Coef = a*b - c*d: the first product fused, the second rounded (FMS)
+    auto fms = [](float a, float b, float c) { return std::fma(a, b, -c); };
+    const float C00 = fms(m22, m33, m32 * m23), C02 = fms(m33, m12, m32 * m13), C03 = fms(m23, m12, m22 * m13);
+    const float C04 = fms(m33, m21, m23 * m31), C06 = fms(m33, m11, m13 * m31), C07 = fms(m23, m11, m13 * m21);
+    const float C08 = fms(m32, m21, m22 * m31), C10 = fms(m32, m11, m12 * m31), C11 = fms(m22, m11, m12 * m21);
+    const float C12 = fms(m33, m20, m23 * m30), C14 = fms(m33, m10, m13 * m30), C15 = fms(m23, m10, m13 * m20);
+    const float C16 = fms(m32, m20, m22 * m30), C18 = fms(m32, m10, m12 * m30), C19 = fms(m22, m10, m12 * m20);
+    const float C20 = fms(m31, m20, m21 * m30), C22 = fms(m31, m10, m11 * m30), C23 = fms(m21, m10, m11 * m20);
+    // Inv_i lane = (Va*Fa - Vb*Fb) + Vc*Fc: Va*Fa rounded, the other two fused in turn
+    auto lane = [](float va, float fa, float vb, float fb, float vc, float fc) {
+        return std::fma(vc, fc, std::fma(-vb, fb, va * fa));
+    };
+    float I[16];
+    I[0] = lane(m11, C00, m12, C04, m13, C08);
+    I[1] = -lane(m01, C00, m02, C04, m03, C08);
+    I[2] = lane(m01, C02, m02, C06, m03, C10);
+    I[3] = -lane(m01, C03, m02, C07, m03, C11);
+    I[4] = -lane(m10, C00, m12, C12, m13, C16);
+    I[5] = lane(m00, C00, m02, C12, m03, C16);
+    I[6] = -lane(m00, C02, m02, C14, m03, C18);
+    I[7] = lane(m00, C03, m02, C15, m03, C19);
+    I[8] = lane(m10, C04, m11, C12, m13, C20);
+    I[9] = -lane(m00, C04, m01, C12, m03, C20);
+    I[10] = lane(m00, C06, m01, C14, m03, C22);
+    I[11] = -lane(m00, C07, m01, C15, m03, C23);
+    I[12] = -lane(m10, C08, m11, C16, m12, C20);
+    I[13] = lane(m00, C08, m01, C16, m02, C20);
+    I[14] = -lane(m00, C10, m01, C18, m02, C22);
+    I[15] = lane(m00, C11, m01, C19, m02, C23);
+    // Dot1 = (m00*Row0.x + m01*Row0.y) + (m02*Row0.z + m03*Row0.w), each pair fused once
+    const float dot = std::fma(m01, I[4], m00 * I[0]) + std::fma(m03, I[12], m02 * I[8]);
+    const float od = 1.0f / dot;
+    for (int k = 0; k < 16; k++) out[k] = I[k] * od;
     return PT_OK;
 }

@@ -161,7 +161,9 @@ static_assert(sizeof(DevTex) == 32, "texture record layout");
 #define OCT_FRESH 128u // overlapped traversal with PT_PRECLAIM: the ray was claimed this iteration (set up after the loads)
 #define OCT_TIE 64u   // pool traversal: this ray met a hit at exactly t == max (listed once for the exact re-trace)
 #define OCT_SP_SHIFT 8  // ... entered at this stack depth (bits 8-13)
-#define SCR_WORDS 9   // scratch row: world o, d, tmax, length, instance
+// scratch row: world o, d, tmax, the outermost level's length, instance, the
+// inner levels' lengths (nested wrappers, pt_api.h PT_MAX_INSTANCE_DEPTH)
+#define SCR_WORDS (9 + PT_MAX_INSTANCE_DEPTH - 1)
 struct DevInstance {
     float T[16], inv[16];  // glm column-major transform and inverse
     uint32_t root;         // BLAS root ref
@@ -174,6 +176,7 @@ struct DevInstance {
     float mdir[3];
     float t0, t1;
     uint32_t anim;
+    int32_t inner;         // the next level down (nested wrappers), or -1
 };
 
 // ---- per-triangle shading record (128 B, one cache line): the three

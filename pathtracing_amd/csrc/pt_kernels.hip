@@ -86,29 +86,45 @@ __device__ __forceinline__ void iteration_prologue(const uint32_t* __restrict__ 
 // Primitive.cpp:48-64): the object-space ray is rebuilt, the primitive test
 // re-run for t (the traversal kept the world t) and the object-space
 // interaction carried back with the transform and its normal matrix.
-// AnimatedPrimitive hits (S.motion): the ray to object space and the
-// interaction back at the ray's time, out of line (the rare path keeps
-// k_shade's registers) with values in and out
-struct ObjRay {
+// AnimatedPrimitive hits (S.motion) and nested wrappers (pt_instance.inner)
+// go out of line (the rare path keeps k_shade's registers), values in and
+// out: the object-space ray through every level at the ray's time, the
+// outermost first; the interaction back through them, the innermost first
+// (TransformedPrimitive::Intersect called by the wrapper around it).  Their
+// world t is the traversal's, which divided the object-space t by each
+// level's length in that same order.
+struct ChainRay {
     f3 o, d;
-    float len;
 };
-__device__ __noinline__ ObjRay anim_object_ray(const DevInstance* I, float time, f3 ro, f3 rd) {
-    float T[16], inv[16];
-    anim_transform(*I, time, T);
-    anim_inverse(T, inv);
-    const f3 dir = m4_dir(inv, rd);
-    const float len = length(dir);
-    return ObjRay{m4_point(inv, ro), dir / len, len};
+__device__ __noinline__ ChainRay chain_object_ray(const DevInstance* I, float time, f3 ro, f3 rd) {
+    const DevInstance* lv[PT_MAX_INSTANCE_DEPTH];
+    const int k = inst_chain(I, lv);
+    for (int j = 0; j < k; j++) {
+        float T[16], inv[16];
+        inst_matrices(*lv[j], time, T, inv);
+        const f3 dir = m4_dir(inv, rd);
+        const float len = length(dir);
+        ro = m4_point(inv, ro);
+        rd = dir / len;
+    }
+    return ChainRay{ro, rd};
 }
 struct SurfXf {
     f3 p, n, ns, tangent;
 };
-__device__ __noinline__ SurfXf anim_world_surface(const DevInstance* I, float time, f3 p, f3 n, f3 ns, f3 tangent) {
-    float T[16], NM[9];
-    anim_transform(*I, time, T);
-    normal_matrix(T, NM);
-    return SurfXf{m4_point(T, p), normalize(m3_mul(NM, n)), normalize(m3_mul(NM, ns)), normalize4(m4_dir(T, tangent))};
+__device__ __noinline__ SurfXf chain_world_surface(const DevInstance* I, float time, f3 p, f3 n, f3 ns, f3 tangent) {
+    const DevInstance* lv[PT_MAX_INSTANCE_DEPTH];
+    const int k = inst_chain(I, lv);
+    for (int j = k - 1; j >= 0; j--) {
+        float T[16], inv[16], NM[9];
+        inst_matrices(*lv[j], time, T, inv);
+        normal_matrix(T, NM);
+        p = m4_point(T, p);
+        n = normalize(m3_mul(NM, n));
+        ns = normalize(m3_mul(NM, ns));
+        tangent = normalize4(m4_dir(T, tangent));
+    }
+    return SurfXf{p, n, ns, tangent};
 }
 // defer_nm (PT_TEX_JOINT shading): a triangle's normal map is left to
 // mat_tex unless the hit is in an instance (whose transform follows it)
@@ -117,19 +133,19 @@ __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, flo
     si.nm_pending = false;
     float len = 1.0f;
     const DevInstance* I = nullptr;
-    bool anim = false;
+    bool xf = false;  // the hit's levels go out of line (an AnimatedPrimitive, nested wrappers)
     if ((uint32_t)prim >= S.n_prims) {
         for (uint32_t k = 0; k < S.n_instances; k++) {
             const DevInstance& c = S.instances[k];
             if ((uint32_t)prim >= c.virt_base && (uint32_t)prim < c.virt_base + c.n_prims) I = &c;
         }
         prim = (int)(I->prim_base + ((uint32_t)prim - I->virt_base));
-        anim = S.motion && I->anim;
-        if (anim) {  // AnimatedPrimitive::Intersect at the ray's time (Primitive.cpp:86-89)
-            const ObjRay r = anim_object_ray(I, time, ro, rd);
+        xf = (S.motion && I->anim) || I->inner >= 0;
+        if (xf) {  // AnimatedPrimitive::Intersect at the ray's time (Primitive.cpp:86-89), level by level
+            const ChainRay r = chain_object_ray(I, time, ro, rd);
             ro = r.o;
             rd = r.d;
-            len = r.len;
+            len = t;  // (the world t, kept for si.t)
         } else {
             const f3 dir = m4_dir(I->inv, rd);
             len = length(dir);
@@ -157,12 +173,12 @@ __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, flo
     si.mat = pi.material;
     si.light = pi.light;
     medium = pi.medium;
-    if (anim) {
-        const SurfXf w = anim_world_surface(I, time, si.p, si.n, si.ns, si.tangent);
+    if (xf) {
+        const SurfXf w = chain_world_surface(I, time, si.p, si.n, si.ns, si.tangent);
         si.p = w.p;
         si.n = w.n;
         si.ns = w.ns;
-        si.t = si.t / len;
+        si.t = len;
         si.tangent = w.tangent;
     } else if (I) {
         float NM[9];

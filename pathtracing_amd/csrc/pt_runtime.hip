@@ -1065,8 +1065,21 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     if (s->n_media && !s->media) return fail(c, PT_ERR_ARG, "media array missing");
     if (s->n_media > PT_MAX_MEDIA) return fail(c, PT_ERR_ARG, "more than %d media", PT_MAX_MEDIA);
     if (s->n_prims > REF_SLOT_MASK) return fail(c, PT_ERR_ARG, "too many primitives");
-    {  // instances: one level, BLAS targets without instances / nested BLAS,
-       // ascending virtual ranges past the real slots
+    {  // instances: chains of levels (pt_instance.inner) ending at a BLAS
+       // without instances / nested BLAS; the records the TLAS names take
+       // ascending virtual ranges past the real slots, level records none
+        if (s->n_instances && !s->instances) return fail(c, PT_ERR_ARG, "instances array missing");
+        std::vector<uint8_t> is_level(s->n_instances, 0);
+        for (uint32_t k = 0; k < s->n_instances; k++) {
+            const int32_t in = s->instances[k].inner;
+            if (in < -1 || (in >= 0 && ((uint32_t)in <= k || (uint32_t)in >= s->n_instances)))
+                return fail(c, PT_ERR_ARG, "instance %u: bad inner level %d", k, in);
+            if (in >= 0) is_level[in] = 1;
+        }
+        for (uint32_t i = 0; i < s->n_prims; i++)
+            if (s->prims[i].kind == PT_PRIM_INSTANCE &&
+                (s->prims[i].index >= s->n_instances || is_level[s->prims[i].index]))
+                return fail(c, PT_ERR_ARG, "prim %u: bad instance %u", i, s->prims[i].index);
         uint64_t next = s->n_prims;
         for (uint32_t k = 0; k < s->n_instances; k++) {
             const pt_instance& I = s->instances[k];
@@ -1076,6 +1089,13 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
             for (uint32_t j = B.prim_base; j < B.prim_base + B.n_prims; j++)
                 if (s->prims[j].kind == PT_PRIM_BLAS || s->prims[j].kind == PT_PRIM_INSTANCE)
                     return fail(c, PT_ERR_ARG, "instance %u: nested instance", k);
+            int depth = 1;
+            for (int32_t in = I.inner; in >= 0; in = s->instances[in].inner, depth++)
+                if (s->instances[in].bvh != I.bvh)
+                    return fail(c, PT_ERR_ARG, "instance %u: level %d names another bvh", k, in);
+            if (depth > PT_MAX_INSTANCE_DEPTH)
+                return fail(c, PT_ERR_ARG, "instance %u: %d levels (at most %d)", k, depth, PT_MAX_INSTANCE_DEPTH);
+            if (is_level[k]) continue;
             if (I.virt_base < next || (uint64_t)I.virt_base + B.n_prims > REF_SLOT_MASK)
                 return fail(c, PT_ERR_ARG, "instance %u: bad virtual slot range", k);
             next = (uint64_t)I.virt_base + B.n_prims;
@@ -1179,11 +1199,16 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
         D.prim_base = s->bvhs[I.bvh].prim_base;
         D.n_prims = s->bvhs[I.bvh].n_prims;
         D.virt_base = I.virt_base;
+        D.inner = I.inner;
         D.anim = I.animated ? 1u : 0u;
         for (int j = 0; j < 3; j++) D.mdir[j] = I.motion[j];
         D.t0 = I.time_bounds[0];
         D.t1 = I.time_bounds[1];
     }
+    // level records own no virtual slots: the hit's instance lookup
+    // (hit_surface) finds the chain's outermost record
+    for (uint32_t k = 0; k < s->n_instances; k++)
+        if (s->instances[k].inner >= 0) inst[s->instances[k].inner].n_prims = 0;
     // ---- triangles: vertex indices + flags as uint4
     std::vector<uint4> tri(s->n_triangles);
     for (uint32_t t = 0; t < s->n_triangles; t++)

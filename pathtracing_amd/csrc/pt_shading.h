@@ -1329,30 +1329,62 @@ __device__ __forceinline__ f3 inf_le(const pt_light& l, f3 d) {
 // instance; its AreaLight's shape stays in object space (l.prim is the BLAS
 // slot).  Out of line: the rare path keeps k_shade's registers.  Values in and
 // out (returned in registers): a reference argument would keep the caller's
-// variables in scratch memory on every path.
+// variables in scratch memory on every path.  Nested wrappers (a
+// TransformedLight of a TransformedLight, what GetLights of a nested
+// TransformedPrimitive returns, Primitive.cpp:66-73) apply their levels in the
+// reference's call order: sample() transforms the inner light's sample, so
+// the innermost level first; PDF() and L() transform the query before the
+// inner light sees it, so the outermost first.
 struct PN {
     f3 p, n;
 };
+// the levels of a chain from its outermost record, the outermost first; returns the count
+__device__ __forceinline__ int inst_chain(const DevInstance* c, const DevInstance** lv) {
+    int k = 0;
+    for (;; c = &S.instances[c->inner]) {
+        lv[k++] = c;
+        if (c->inner < 0 || k == PT_MAX_INSTANCE_DEPTH) return k;
+    }
+}
 // The time moves an AnimatedLight (its instance's translation at the ray's time).
 __device__ __noinline__ PN tlight_to_world(int inst, f3 p, f3 n, float time) {  // TransformedLight::sample
-    float T[16], inv[16], NM[9];
-    inst_matrices(S.instances[inst], time, T, inv);
-    normal_matrix(T, NM);
-    return PN{m4_point(T, p), m3_mul(NM, n)};
+    const DevInstance* lv[PT_MAX_INSTANCE_DEPTH];
+    const int k = inst_chain(&S.instances[inst], lv);
+    for (int j = k - 1; j >= 0; j--) {
+        float T[16], inv[16], NM[9];
+        inst_matrices(*lv[j], time, T, inv);
+        normal_matrix(T, NM);
+        p = m4_point(T, p);
+        n = m3_mul(NM, n);
+    }
+    return PN{p, n};
 }
 struct TLObj {
     f3 p, n, ro, rd;
 };
 __device__ __noinline__ TLObj tlight_to_object(int inst, f3 p, f3 n, f3 ro, f3 rd, float time) {  // TransformedLight::PDF
-    float T[16], inv[16];
-    inst_matrices(S.instances[inst], time, T, inv);
-    return TLObj{m4_point(inv, p), normalize(m4_dir(inv, n)), m4_point(inv, ro), normalize(m4_dir(inv, rd))};
+    const DevInstance* lv[PT_MAX_INSTANCE_DEPTH];
+    const int k = inst_chain(&S.instances[inst], lv);
+    for (int j = 0; j < k; j++) {
+        float T[16], inv[16];
+        inst_matrices(*lv[j], time, T, inv);
+        p = m4_point(inv, p);
+        n = normalize(m4_dir(inv, n));
+        ro = m4_point(inv, ro);
+        rd = normalize(m4_dir(inv, rd));
+    }
+    return TLObj{p, n, ro, rd};
 }
 __device__ __noinline__ f3 tlight_normal(int inst, f3 n, float time) {  // TransformedLight::L's temp.n
-    float T[16], inv[16], NM[9];
-    inst_matrices(S.instances[inst], time, T, inv);
-    normal_matrix(T, NM);
-    return m3_mul(NM, n);
+    const DevInstance* lv[PT_MAX_INSTANCE_DEPTH];
+    const int k = inst_chain(&S.instances[inst], lv);
+    for (int j = 0; j < k; j++) {
+        float T[16], inv[16], NM[9];
+        inst_matrices(*lv[j], time, T, inv);
+        normal_matrix(T, NM);
+        n = m3_mul(NM, n);
+    }
+    return n;
 }
 
 // TextureInfiniteLight::sample (Light.cpp:118-144): the cell whose running

@@ -576,11 +576,14 @@ __device__ __forceinline__ uint32_t order_children8(uint32_t mask, uint4 c0, uin
 __device__ __forceinline__ uint32_t octant(f3 d) { return ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0); }
 
 // Pops of REF_INST_ENTER, and the instance exit (ref = REF_INST_EXIT, not a
-// stack entry).  Enter: save the world ray, take it to object space (dir =
-// inv*d, length, origin = inv*o, d = dir/length, max*length); the caller
-// records its stack depth and continues at the BLAS root.  Exit: restore; a
-// hit accepted inside becomes t/length and its virtual slot.  Out of line and by value, so the traversal loop's registers
-// are untouched by this rare path.
+// stack entry).  Enter: save the world ray, take it to object space level by
+// level, the outermost first (TransformedPrimitive::Intersect / IntersectPred,
+// Primitive.cpp:42-64, once per nested wrapper: dir = inv*d, length, origin =
+// inv*o, d = dir/length, max*length); the caller records its stack depth and
+// continues at the BLAS root.  Exit: restore; a hit accepted inside becomes
+// t/length per level, the innermost first, and its virtual slot.  Out of line
+// and by value, so the traversal loop's registers are untouched by this rare
+// path.
 struct InstState {
     f3 o, d, inv;
     float tmax;
@@ -589,6 +592,8 @@ struct InstState {
     uint32_t ref;
     float time;  // the ray's (an AnimatedPrimitive is entered at its translation then)
 };
+// scratch word of level k's length: the outermost at 7, inner levels past the instance id
+__device__ __forceinline__ uint32_t scr_len_word(int k) { return k == 0 ? 7u : 8u + (uint32_t)k; }
 template <bool ANY, bool QN = false>
 __device__ __forceinline__ InstState instance_step_inl(InstState s) {
     const uint32_t L = S.scratch_lanes;
@@ -597,7 +602,11 @@ __device__ __forceinline__ InstState instance_step_inl(InstState s) {
         const uint32_t inst = sc[8 * L];
         if (!ANY && (s.oct & OCT_HIT)) {
             const DevInstance& I = S.instances[inst];
-            s.tmax = s.tmax / __uint_as_float(sc[7 * L]);
+            int levels = 1;
+            for (int32_t in = I.inner; in >= 0 && levels < PT_MAX_INSTANCE_DEPTH; in = S.instances[in].inner) levels++;
+            float t = s.tmax;
+            for (int k = levels - 1; k >= 0; k--) t = t / __uint_as_float(sc[scr_len_word(k) * L]);
+            s.tmax = t;
             s.best = (int)(I.virt_base + ((uint32_t)s.best - I.prim_base));
         } else {
             s.tmax = __uint_as_float(sc[6 * L]);
@@ -613,29 +622,33 @@ __device__ __forceinline__ InstState instance_step_inl(InstState s) {
     }
     const uint32_t slot = s.ref & REF_SLOT_MASK;
     const uint32_t inst = __float_as_uint(S.geom[slot].b.y);
-    const DevInstance& I = S.instances[inst];
     const float w[7] = {s.o.x, s.o.y, s.o.z, s.d.x, s.d.y, s.d.z, s.tmax};
     for (int k = 0; k < 7; k++) sc[k * L] = __float_as_uint(w[k]);
-    f3 dir, org;
-    if (S.motion && I.anim) {  // AnimatedPrimitive::Intersect(Pred) at the ray's time (Primitive.cpp:82-89)
-        float T[16], inv[16];
-        anim_transform(I, s.time, T);
-        anim_inverse(T, inv);
-        dir = m4_dir(inv, s.d);
-        org = m4_point(inv, s.o);
-    } else {
-        dir = m4_dir(I.inv, s.d);
-        org = m4_point(I.inv, s.o);
-    }
-    const float len = length(dir);
-    sc[7 * L] = __float_as_uint(len);
     sc[8 * L] = inst;
-    s.o = org;
-    s.d = dir / len;
+    const DevInstance* I = &S.instances[inst];
+    for (int k = 0;; k++) {
+        f3 dir, org;
+        if (S.motion && I->anim) {  // AnimatedPrimitive::Intersect(Pred) at the ray's time (Primitive.cpp:82-89)
+            float T[16], inv[16];
+            anim_transform(*I, s.time, T);
+            anim_inverse(T, inv);
+            dir = m4_dir(inv, s.d);
+            org = m4_point(inv, s.o);
+        } else {
+            dir = m4_dir(I->inv, s.d);
+            org = m4_point(I->inv, s.o);
+        }
+        const float len = length(dir);
+        sc[scr_len_word(k) * L] = __float_as_uint(len);
+        s.o = org;
+        s.d = dir / len;
+        s.tmax = s.tmax * len;
+        if (I->inner < 0 || k + 1 == PT_MAX_INSTANCE_DEPTH) break;  // (the upload bounds the depth)
+        I = &S.instances[I->inner];
+    }
     s.inv = inv_dir(s.d);
     s.oct = octant(s.d) | OCT_INST | (s.oct & (OCT_TIE | OCT_FOUND));
-    s.tmax = s.tmax * len;
-    s.ref = (QN && PT_Q48) ? I.qroot : I.root;  // the BLAS root in the traversal's node form
+    s.ref = (QN && PT_Q48) ? I->qroot : I->root;  // the BLAS root in the traversal's node form
     return s;
 }
 // The pool kernels (7 waves per SIMD, 72 VGPRs) call it out of line; the

@@ -300,6 +300,17 @@ def instance_bbox(inner: np.ndarray, m: np.ndarray) -> np.ndarray:
     return _expand_seq(pts)
 
 
+def _chain(p):
+    """(wrapper levels outermost first, the Model / GeometricPrimitive they
+    wrap) of a TransformedPrimitive / AnimatedPrimitive, possibly nested
+    (Primitive.cpp:32-96); ([], p) for anything else."""
+    levels = []
+    while isinstance(p, TransformedPrimitive):
+        levels.append(p)
+        p = p.primitive
+    return levels, p
+
+
 def flatten_scene(scene: Scene) -> FlatScene:
     _last_build.clear()
     reg = _Registry()
@@ -310,17 +321,18 @@ def flatten_scene(scene: Scene) -> FlatScene:
     # ---- models: BLAS over their triangles (top-level and instanced, once each) ----
     models, model_index = [], {}
     for p in top:
-        m = p.primitive if isinstance(p, TransformedPrimitive) else p
+        m = _chain(p)[1]
         if isinstance(m, Model) and id(m) not in model_index:
             model_index[id(m)] = len(models)
             models.append(m)
     # instanced GeometricPrimitives: a one-primitive BLAS each
     gp_inst, gp_index = [], {}
     for p in top:
-        if isinstance(p, TransformedPrimitive) and isinstance(p.primitive, GeometricPrimitive):
-            if id(p.primitive) not in gp_index:
-                gp_index[id(p.primitive)] = len(gp_inst)
-                gp_inst.append(p.primitive)
+        m = _chain(p)[1]
+        if isinstance(p, TransformedPrimitive) and isinstance(m, GeometricPrimitive):
+            if id(m) not in gp_index:
+                gp_index[id(m)] = len(gp_inst)
+                gp_inst.append(m)
     pos, nrm, uvs, tan, vidx, tflags = [], [], [], [], [], []
     vbase = 0
     tri_base = 0
@@ -367,15 +379,17 @@ def flatten_scene(scene: Scene) -> FlatScene:
         elif isinstance(p, GeometricPrimitive):
             top_boxes[i] = p.shape.bbox()
         elif isinstance(p, TransformedPrimitive):
-            m = p.primitive
-            inner = model_blas[model_index[id(m)]][3] if isinstance(m, Model) else m.shape.bbox()
-            if isinstance(p, AnimatedPrimitive):
-                # AnimatedPrimitive::BoundingBox (Primitive.cpp:76-80): the box at
-                # rest expanded by the box translated by the whole direction
-                moved = instance_bbox(inner, mat4_translate(mat4_identity(), p.direction))
-                top_boxes[i] = _expand_seq([inner[:3], inner[3:], moved[:3], moved[3:]])
-            else:
-                top_boxes[i] = instance_bbox(inner, p.transform)
+            levels, m = _chain(p)
+            box = model_blas[model_index[id(m)]][3] if isinstance(m, Model) else m.shape.bbox()
+            for lv in reversed(levels):  # each wrapper boxes the box of what it wraps
+                if isinstance(lv, AnimatedPrimitive):
+                    # AnimatedPrimitive::BoundingBox (Primitive.cpp:76-80): the box at
+                    # rest expanded by the box translated by the whole direction
+                    moved = instance_bbox(box, mat4_translate(mat4_identity(), lv.direction))
+                    box = _expand_seq([box[:3], box[3:], moved[:3], moved[3:]])
+                else:
+                    box = instance_bbox(box, lv.transform)
+            top_boxes[i] = box
         else:
             raise TypeError(f"unsupported primitive {type(p).__name__}")
     tl_clusters, tl_root, tl_order, tl_bbox = bvh_build(top_boxes)
@@ -397,23 +411,37 @@ def flatten_scene(scene: Scene) -> FlatScene:
         blas_base.append(base)
         base += int(b[2].shape[0])
     instances = []  # pt_instance records, TLAS slot order
+    # the inner levels of nested wrappers, after every record a TLAS slot names
+    level_records = []
+    n_top_inst = sum(1 for p in top if isinstance(p, TransformedPrimitive))
     virt_base = n_top + n_blas_prims
+
+    def level_record(lv, b):
+        ins = np.zeros(1, dtype=N.INSTANCE)[0]
+        ins["transform"] = lv.transform.reshape(16)
+        ins["inv"] = lv.invTransform.reshape(16)
+        ins["bvh"] = b
+        ins["inner"] = -1
+        if isinstance(lv, AnimatedPrimitive):  # per-ray translation (Primitive.cpp:82-89)
+            ins["motion"] = lv.direction
+            ins["time_bounds"] = lv.timeBounds
+            ins["animated"] = 1
+        return ins
+
     # TLAS slots
     for slot in range(n_top):
         p = top[int(tl_order[slot])]
         rec = prims[slot]
         if isinstance(p, TransformedPrimitive):
-            m = p.primitive
+            levels, m = _chain(p)
             b = 1 + (model_index[id(m)] if isinstance(m, Model) else len(model_blas) + gp_index[id(m)])
-            ins = np.zeros(1, dtype=N.INSTANCE)[0]
-            ins["transform"] = p.transform.reshape(16)
-            ins["inv"] = p.invTransform.reshape(16)
-            ins["bvh"] = b
+            ins = level_record(p, b)
             ins["virt_base"] = virt_base
-            if isinstance(p, AnimatedPrimitive):  # per-ray translation (Primitive.cpp:82-89)
-                ins["motion"] = p.direction
-                ins["time_bounds"] = p.timeBounds
-                ins["animated"] = 1
+            prev = ins
+            for lv in levels[1:]:  # nested wrappers: a level record each, linked outermost first
+                prev["inner"] = n_top_inst + len(level_records)
+                prev = level_record(lv, b)
+                level_records.append(prev)
             virt_base += int((model_blas + gp_blas)[b - 1][2].shape[0])
             rec["kind"] = N.PT_PRIM_INSTANCE
             rec["index"] = len(instances)
@@ -431,7 +459,9 @@ def flatten_scene(scene: Scene) -> FlatScene:
             elif isinstance(m, GeometricPrimitive) and m.areaLight is not None:
                 inner_lights = [(m.areaLight, blas_base[len(model_blas) + gp_index[id(m)]])]
             for al, bslot in inner_lights:
-                tl = TransformedLight(al, p)
+                tl = al
+                for lv in reversed(levels):  # GetLights of each wrapper wraps the inner one's
+                    tl = TransformedLight(tl, lv)
                 light_slot[id(tl)] = bslot
                 light_instance[id(tl)] = len(instances)
                 light_slot[id(al)] = bslot
@@ -525,7 +555,7 @@ def flatten_scene(scene: Scene) -> FlatScene:
         top_order=tl_order, blas_orders=[b[2] for b in model_blas], model_tri_base=model_tri_base,
         texture_ids=dict(reg.tex_ids))
     flat._reg = reg
-    flat.instances = _stack(instances, N.INSTANCE)
+    flat.instances = _stack(instances + level_records, N.INSTANCE)
     flat.light_instance = light_instance
     flat.inner_area_lights = inner_area_lights
     # media: the scene's first, then primitives in slot order, then meshes
@@ -570,8 +600,8 @@ def bind_lights(flat: FlatScene, scene: Scene, sampler: Optional[LightSampler]):
         if isinstance(l, TransformedLight):
             r["kind"] = N.PT_LIGHT_AREA
             r["prim"] = flat.light_slot[id(l)]
-            r["tex"] = reg.texture(l.light.emissiveTexture)
-            r["one_sided"] = 1 if l.light.oneSided else 0
+            r["tex"] = reg.texture(l.area.emissiveTexture)
+            r["one_sided"] = 1 if l.area.oneSided else 0
             r["instance"] = flat.light_instance[id(l)]
         elif isinstance(l, AreaLight):
             r["kind"] = N.PT_LIGHT_AREA

@@ -59,7 +59,7 @@ MATERIAL = np.dtype([("kind", "<u4"), ("tex", "<i4"), ("norm", "<i4"), ("rough",
 LIGHT = np.dtype([("kind", "<u4"), ("prim", "<i4"), ("tex", "<i4"), ("one_sided", "<u4"), ("power", "<f4"),
                   ("pmf", "<f4"), ("color", "<f4", 3), ("vec", "<f4", 3), ("scale", "<f4"), ("instance", "<i4")])
 INSTANCE = np.dtype([("transform", "<f4", 16), ("inv", "<f4", 16), ("bvh", "<u4"), ("virt_base", "<u4"),
-                     ("motion", "<f4", 3), ("time_bounds", "<f4", 2), ("animated", "<u4")])
+                     ("motion", "<f4", 3), ("time_bounds", "<f4", 2), ("animated", "<u4"), ("inner", "<i4")])
 MEDIUM = np.dtype([("sigma_a", "<f4", 3), ("sigma_s", "<f4", 3), ("sigma_t", "<f4", 3), ("Le", "<f4", 3),
                    ("g", "<f4")])
 RAY = np.dtype([("o", "<f4", 3), ("d", "<f4", 3), ("tmax", "<f4"), ("time", "<f4")])
@@ -67,7 +67,7 @@ HIT = np.dtype([("t", "<f4"), ("b1", "<f4"), ("b2", "<f4"), ("prim", "<i4")])
 
 assert REF_NODE.itemsize == 8 and REF_CLUSTER.itemsize == 128 and PRIM.itemsize == 20
 assert QUAD.itemsize == 64 and SPHERE.itemsize == 16 and TEXTURE.itemsize == 48 and IMAGE.itemsize == 24
-assert MATERIAL.itemsize == 48 and LIGHT.itemsize == 56 and RAY.itemsize == 32 and INSTANCE.itemsize == 160 and HIT.itemsize == 16
+assert MATERIAL.itemsize == 48 and LIGHT.itemsize == 56 and RAY.itemsize == 32 and INSTANCE.itemsize == 164 and HIT.itemsize == 16
 
 
 class RefNode(C.Structure):

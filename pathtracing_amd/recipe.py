@@ -157,22 +157,34 @@ def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: 
             raise ValueError("recipes do not carry Model material overrides")
         return [mesh(me) for me in p.meshes]
 
+    def level(lv):  # (matrix, animation) operands of one wrapper level
+        m16 = " ".join(_f(x) for x in lv.transform.reshape(16))
+        anim = (f"{' '.join(_f(x) for x in lv.direction)} {_f(lv.timeBounds[0])} {_f(lv.timeBounds[1])}"
+                if isinstance(lv, AnimatedPrimitive) else None)
+        return m16, anim
+
+    def wrap_line(lv):  # the harness wraps its last top primitive
+        m16, anim = level(lv)
+        return f"wrapanim {anim}" if anim else f"wrapprim {m16}"
+
     for k, p in enumerate(scene.primitives):
-        wrap = None
+        wraps = []
         if isinstance(p, TransformedPrimitive):
-            m16 = " ".join(_f(x) for x in p.transform.reshape(16))
-            anim = (f"{' '.join(_f(x) for x in p.direction)} {_f(p.timeBounds[0])} {_f(p.timeBounds[1])}"
-                    if isinstance(p, AnimatedPrimitive) else None)
-            if isinstance(p.primitive, Model):
-                if id(p.primitive) not in blas_ids:
-                    ids = model_ids(p.primitive)
-                    blas_ids[id(p.primitive)] = len(blas_ids)
-                    lines.append(f"blasdef {blas_ids[id(p.primitive)]} {len(ids)} {' '.join(map(str, ids))}")
-                b = blas_ids[id(p.primitive)]
+            levels = []  # nested wrappers, outermost first
+            while isinstance(p, TransformedPrimitive):
+                levels.append(p)
+                p = p.primitive
+            if isinstance(p, Model):
+                if id(p) not in blas_ids:
+                    ids = model_ids(p)
+                    blas_ids[id(p)] = len(blas_ids)
+                    lines.append(f"blasdef {blas_ids[id(p)]} {len(ids)} {' '.join(map(str, ids))}")
+                b = blas_ids[id(p)]
+                m16, anim = level(levels[-1])
                 lines.append(f"animinstance {k} {b} {anim}" if anim else f"instance {k} {b} {m16}")
+                lines.extend(wrap_line(lv) for lv in reversed(levels[:-1]))
                 continue
-            wrap = f"wrapanim {anim}" if anim else f"wrapprim {m16}"
-            p = p.primitive
+            wraps = [wrap_line(lv) for lv in reversed(levels)]
         if isinstance(p, Model):
             if id(p) in blas_ids:
                 lines.append(f"topblas {k} {blas_ids[id(p)]}")
@@ -195,8 +207,7 @@ def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: 
                 lines.append(f"sphere {k} {g} {m} {em} {one} {md}")
             else:
                 raise TypeError(type(sh))
-            if wrap:
-                lines.append(wrap)
+            lines.extend(wraps)
     for l in scene.infiniteLights:
         if isinstance(l, UniformInfiniteLight):
             lines.append(f"infinite uniform {' '.join(_f(x) for x in l.color)}")

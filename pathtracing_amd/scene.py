@@ -712,12 +712,20 @@ class TransformedLight(Light):
     a fresh interaction (normal matrix applied, uv = (0, 0)).  Power() is the
     inner power times det(transform) (TransformedLight) or the inner power
     (AnimatedLight).  A path that hits the emitter sees the inner AreaLight
-    itself (Primitive.cpp:58)."""
+    itself (Primitive.cpp:58).  Nested wrappers wrap the inner wrapper's
+    light: `light` is then a TransformedLight, `area` the AreaLight inside."""
 
-    def __init__(self, light: "AreaLight", instance: "TransformedPrimitive"):
+    def __init__(self, light: Light, instance: "TransformedPrimitive"):
         self.light = light
         self.instance = instance
         self.animated = isinstance(instance, AnimatedPrimitive)
+
+    @property
+    def area(self) -> "AreaLight":
+        l = self.light
+        while isinstance(l, TransformedLight):
+            l = l.light
+        return l
 
     def isDelta(self) -> bool:
         return self.light.isDelta()
@@ -892,15 +900,25 @@ def mat4_inverse(m) -> np.ndarray:
     return (inv * f(f(1) / det)).astype(np.float32)
 
 
+MAX_INSTANCE_DEPTH = 4  # pt_api.h PT_MAX_INSTANCE_DEPTH
+
+
 class TransformedPrimitive(Primitive):
     """TransformedPrimitive (Primitive.hpp:34-48, Primitive.cpp:32-72): an
-    instance of a Model (BLAS) or of a GeometricPrimitive under an affine
-    glm::mat4 (float32 [col][row]).  Rays are taken to object space with the
-    inverse, the hit back with the transform and its normal matrix."""
+    instance of a Model (BLAS), of a GeometricPrimitive, or of another
+    TransformedPrimitive / AnimatedPrimitive (nested, up to
+    MAX_INSTANCE_DEPTH levels) under an affine glm::mat4 (float32
+    [col][row]).  Rays are taken to object space with the inverse, the hit
+    back with the transform and its normal matrix, level by level."""
 
     def __init__(self, primitive: Primitive, transform):
-        if not isinstance(primitive, (Model, GeometricPrimitive)):
-            raise TypeError("instances of a Model or a GeometricPrimitive only (no nested instances)")
+        depth, base = 1, primitive
+        while isinstance(base, TransformedPrimitive):
+            depth, base = depth + 1, base.primitive
+        if not isinstance(base, (Model, GeometricPrimitive)):
+            raise TypeError("instances of a Model, a GeometricPrimitive or another instance only")
+        if depth > MAX_INSTANCE_DEPTH:
+            raise ValueError(f"{depth} nested instance levels (at most {MAX_INSTANCE_DEPTH})")
         self.primitive = primitive
         self.transform = np.ascontiguousarray(transform, np.float32).reshape(4, 4)
         # glm::inverse as the reference build contracts it: the native host

@@ -1003,3 +1003,58 @@ def motion_path(W: int = 32, H: int = 32, spp: int = 4, max_depth: int = 8, inte
     camera = Camera((0, 0, 3.7), (0, 0, 0), 0.75, Film((W, H), MitchellFilter()), shutterBounds=shutter)
     ls = None if integrator == "simple" else PowerLightSampler()
     return SceneSetup(scene, camera, integrator, ls, max_depth, seed, spp).finish()
+
+
+def nested_instances(W: int = 32, H: int = 32, spp: int = 4, max_depth: int = 8, integrator: str = "path",
+                     seed: int = 0x5EED0091, shutter=(0.0, 1.0)) -> SceneSetup:
+    """Nested wrappers (TransformedPrimitive of a TransformedPrimitive,
+    Primitive.cpp:32-96; their lights TransformedLight of a TransformedLight,
+    Light.cpp:300-364): a crate Model under two and under three static
+    levels (rotate / non-uniform scale / translate), an emissive lamp Model
+    under a TransformedPrimitive of an AnimatedPrimitive (a moving emitter
+    inside a static frame), an emissive sphere under an AnimatedPrimitive of
+    a TransformedPrimitive, and a glass quad under four levels, in the C2 room
+    with its ceiling light; shutter camera, PowerLightSampler."""
+    from .scene import (AnimatedPrimitive, TransformedPrimitive, mat4_identity, mat4_rotate, mat4_scale,
+                        mat4_translate)
+    I = mat4_identity()
+    scene = Scene()
+    white = MicrofacetDiffuse((0.73, 0.73, 0.73))
+    red = MicrofacetDiffuse((0.65, 0.05, 0.05))
+    green = MicrofacetDiffuse((0.12, 0.45, 0.15))
+    walls = [
+        (_quad_tris((-1, -1, 1), (1, -1, 1), (1, -1, -1), (-1, -1, -1)), white),
+        (_quad_tris((-1, 1, -1), (1, 1, -1), (1, 1, 1), (-1, 1, 1)), white),
+        (_quad_tris((-1, -1, -1), (1, -1, -1), (1, 1, -1), (-1, 1, -1)), white),
+        (_quad_tris((-1, -1, 1), (-1, -1, -1), (-1, 1, -1), (-1, 1, 1)), red),
+        (_quad_tris((1, -1, -1), (1, -1, 1), (1, 1, 1), (1, 1, -1)), green),
+    ]
+    scene.Add(Model([Mesh(i, v, None, n, uv, m) for (i, v, n, uv), m in walls]))
+    light = AreaLight(QuadShape((-0.25, 0.999, -0.25), (0.5, 0, 0), (0, 0, 0.5)), (8.0, 7.0, 6.0), False)
+    scene.Add(GeometricPrimitive(light.getShape(), MicrofacetDiffuse((0.78, 0.78, 0.78)), light))
+    bi, bv, bn, buv = _box((0, 0, 0), (0.3, 0.3, 0.3), 0.0)
+    crate = Model([Mesh(bi, bv, None, bn, buv, MicrofacetDiffuse(SolidColor((0.9, 0.5, 0.2)), None,
+                                                                 SolidColor((0.4, 0.4, 0.4)), SolidColor((0, 0, 0))))])
+    inner = TransformedPrimitive(crate, mat4_scale(mat4_rotate(I, 0.6, (0, 1, 0)), (1.4, 0.7, 1.1)))
+    scene.Add(TransformedPrimitive(inner, mat4_translate(I, (-0.45, -0.75, -0.25))))
+    mid = TransformedPrimitive(TransformedPrimitive(crate, mat4_rotate(I, -0.4, (1, 0, 0))),
+                               mat4_scale(I, (0.8, 1.3, 0.8)))
+    scene.Add(TransformedPrimitive(mid, mat4_rotate(mat4_translate(I, (0.45, -0.6, 0.2)), 0.3, (0, 0, 1))))
+    li, lv, ln, luv = _box((0, 0, 0), (0.1, 0.1, 0.1), -0.4)
+    lamp = Model([Mesh(li, lv, None, ln, luv, MicrofacetDiffuse((0.8, 0.8, 0.8)), SolidColor((4.0, 3.0, 1.5)))])
+    scene.Add(TransformedPrimitive(AnimatedPrimitive(lamp, (0.0, -0.3, 0.2), (0, 1)),
+                                   mat4_scale(mat4_translate(I, (0.3, 0.4, -0.3)), (1.5, 1.0, 1.2))))
+    sl = AreaLight(SphereShape((0, 0, 0), 0.08), (5.0, 1.5, 1.0), False)
+    ball = GeometricPrimitive(sl.getShape(), MicrofacetDiffuse((0.9, 0.9, 0.9)), sl)
+    scene.Add(AnimatedPrimitive(TransformedPrimitive(ball, mat4_scale(mat4_translate(I, (-0.5, 0.3, 0.3)),
+                                                                       (1.2, 0.9, 1.0))),
+                                (0.25, -0.1, 0.0), (0.25, 1.0)))
+    pane = GeometricPrimitive(QuadShape((-0.5, 0, -0.5), (1, 0, 0), (0, 0, 1)), MicrofacetDielectric(1.5, 0.1, (1, 1, 1)))
+    chain = pane
+    for m in (mat4_scale(I, (0.5, 1, 0.4)), mat4_rotate(I, 1.2, (1, 0, 0)), mat4_rotate(I, 0.5, (0, 1, 0)),
+              mat4_translate(I, (0.1, -0.1, 0.5))):
+        chain = TransformedPrimitive(chain, m)
+    scene.Add(chain)
+    camera = Camera((0, 0, 3.7), (0, 0, 0), 0.75, Film((W, H), MitchellFilter()), shutterBounds=shutter)
+    ls = None if integrator == "simple" else PowerLightSampler()
+    return SceneSetup(scene, camera, integrator, ls, max_depth, seed, spp).finish()

@@ -76,6 +76,10 @@ def parity_scenes():
         "stratified": lambda: _strat(scenes.cornell(W=32, H=32, spp=4, config="c3", seed=0x5EED0081,
                                                     lens=(0.12, 3.2)), (2, 2)),
         "stratified_motion": lambda: _strat(scenes.motion_path(W=32, H=24, spp=6, seed=0x5EED0082), (3, 2)),
+        # nested wrappers (TransformedPrimitive of a TransformedPrimitive, up
+        # to four levels, static and animated levels mixed) and their lights
+        # (TransformedLight of a TransformedLight), under a shutter camera
+        "nested_instances": lambda: scenes.nested_instances(W=32, H=32, spp=4),
     }
 
 

@@ -32,9 +32,9 @@ from pathtracing_amd.recipe import pin_random_lights, write_recipe  # noqa: E402
 
 HARNESS = ROOT / "oracle" / "_ref" / "ref_harness"
 FILM_SCENES = ["example1", "cornell_c2", "cornell_c3", "zoo", "heightfield", "sanmiguel", "example1_volpath", "fog",
-               "instances", "lit_instances", "motion_blur", "motion_path", "stratified"]
+               "instances", "lit_instances", "motion_blur", "motion_path", "stratified", "nested_instances"]
 ADAPTIVE_SCENES = ["example1", "cornell_c3", "zoo", "fog", "instances", "sanmiguel", "lens_box", "lit_instances",
-                   "motion_blur", "motion_path", "stratified", "stratified_motion"]
+                   "motion_blur", "motion_path", "stratified", "stratified_motion", "nested_instances"]
 
 
 def pinned_recipe(tmp: Path, setup) -> Path:

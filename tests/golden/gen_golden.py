@@ -339,6 +339,39 @@ def gen_stats(tmp: Path, only=None):
     print(f"stats: {(OUT / 'stats.npz').stat().st_size / 1024:.0f} KiB, {len(res)} scenes")
 
 
+def gen_mat4_inverse(rng, tmp: Path):
+    """glm::inverse(mat4) by the reference's own build of glm
+    (oracle/glm_inverse_probe.cpp): what TransformedPrimitive's ctor stores
+    as invTransform (Primitive.hpp:37), for pt_mat4_inverse.  Instance-like
+    matrices (rotate / non-uniform scale / translate in every order, axis
+    rotations with exact zeros) and general ones."""
+    from pathtracing_amd.scene import mat4_identity, mat4_rotate, mat4_scale, mat4_translate
+    I = mat4_identity()
+    ms = []
+    for k in range(3000):
+        ops = [lambda m: mat4_translate(m, rng.normal(size=3)),
+               lambda m: mat4_rotate(m, rng.uniform(-3.2, 3.2), rng.normal(size=3)),
+               lambda m: mat4_scale(m, rng.uniform(0.2, 3.0, 3))]
+        m = I
+        for j in rng.permutation(3)[:1 + k % 3]:
+            m = ops[j](m)
+        ms.append(m)
+    for k in range(1500):
+        m = mat4_rotate(I, rng.uniform(-3.2, 3.2), [(1, 0, 0), (0, 1, 0), (0, 0, 1)][k % 3])
+        if k % 2:
+            m = mat4_translate(m, rng.normal(size=3))
+        if k % 5 == 0:
+            m = mat4_scale(m, rng.uniform(0.2, 3.0, 3))
+        ms.append(m)
+    ms += [rng.normal(size=(4, 4)) for _ in range(1500)]
+    A = np.stack([np.ascontiguousarray(m, np.float32).reshape(16) for m in ms])
+    A.tofile(tmp / "m.bin")
+    subprocess.run([str(HARNESS.parent / "glm_inverse_probe"), str(tmp / "m.bin"), str(tmp / "inv.bin")], check=True)
+    inv = np.fromfile(tmp / "inv.bin", np.float32).reshape(-1, 16)
+    np.savez_compressed(OUT / "mat4_inverse.npz", m=A, inv=inv)
+    print(f"mat4_inverse: {(OUT / 'mat4_inverse.npz').stat().st_size / 1024:.0f} KiB, {len(A)} matrices")
+
+
 def main(names=None):
     """All scenes share one rng stream (the committed round-1 fixtures); a
     scene regenerated alone (`gen_golden.py NAME...`) uses its own stream
@@ -367,6 +400,8 @@ def main(names=None):
             gen_c4_band(Path(t))
         if not names or "emission_power" in names:
             gen_emission_power(Path(t))
+        if not names or "mat4_inverse" in names:
+            gen_mat4_inverse(np.random.default_rng([20261018, 4]), Path(t))
 
 
 if __name__ == "__main__":

@@ -478,7 +478,7 @@ def test_gpu_light_samples_match_oracle_and_reference(case):
     assert same.all(), f"{same.mean():.4f} of light cases bit-identical to the reference"
 
 
-@pytest.mark.parametrize("name", ["cornell_c3", "zoo", "sanmiguel", "instances"])
+@pytest.mark.parametrize("name", ["cornell_c3", "zoo", "sanmiguel", "instances", "nested_instances"])
 @pytest.mark.parametrize("nodes", [N.PT_RENDER_NODES_FULL, N.PT_RENDER_NODES_QUANTIZED])
 def test_gpu_pool_and_simple_traversal_agree_bit_for_bit(name, nodes):
     """The persistent refilling traversal (pt_pool.h) and the one-ray-per-lane
@@ -491,7 +491,7 @@ def test_gpu_pool_and_simple_traversal_agree_bit_for_bit(name, nodes):
     np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("name", ["zoo", "sanmiguel", "lit_instances", "fog"])
+@pytest.mark.parametrize("name", ["zoo", "sanmiguel", "lit_instances", "fog", "nested_instances"])
 @pytest.mark.parametrize("flag", [N.PT_RENDER_SORT_MATERIAL, N.PT_RENDER_SORT_SPATIAL,
                                   N.PT_RENDER_SORT_RAYS | N.PT_RENDER_TRAVERSAL_POOL])
 def test_gpu_hit_sorted_shading_is_identical(name, flag):

@@ -64,7 +64,10 @@ def _owner(setup, flat, l):
         if slot < len(flat.top_order):
             return f"top:{int(flat.top_order[slot])}"
         for i, p in enumerate(setup.scene.primitives):  # a GeometricPrimitive's light inside an instance
-            if isinstance(p, TransformedPrimitive) and getattr(p.primitive, "areaLight", None) is l:
+            base = p
+            while isinstance(base, TransformedPrimitive):  # (nested wrappers)
+                base = base.primitive
+            if base is not p and getattr(base, "areaLight", None) is l:
                 return f"top:{i}"
         for k, base in enumerate(flat.bvh_prim_base[1:]):
             if base <= slot < base + flat.bvh_n_prims[1 + k]:
