@@ -786,16 +786,28 @@ __device__ __forceinline__ void sample_fract(const RenderParams& R, uint32_t key
     }
 }
 
-// One new camera sample per `want` lane: a block-aggregated claim of
-// consecutive sample ids (one returning atomic per block: coherent primary
-// rays), then Camera::GenerateRay for the claimed ids below the chunk's end.
-// Every thread of the block calls it (barriers).
 struct NewSample {
     bool enq;
     uint32_t sid, key;
     f3 o, d;
     float time;
 };
+// Camera::GenerateRay for chunk sample ns.sid (its pixel in the chunk's work
+// order, its stream key)
+__device__ __forceinline__ void camera_sample(const RenderParams& R, NewSample& ns) {
+    const unsigned long long g = ns.sid;
+    const uint32_t s_rel = (uint32_t)(g / R.npix_work), pix_i = (uint32_t)(g % R.npix_work);
+    uint32_t x, y;
+    work_pixel(R, pix_i, x, y);
+    const uint32_t s = R.shard_index + (R.s_lo + s_rel) * R.shard_count;
+    ns.key = stream_key(R.seed, y * (uint32_t)R.cam.width + x, s);
+    camera_ray(R.cam, ns.key, x, y, ns.o, ns.d, ns.time, R.strata_x, R.strata_y,
+               R.strata_x ? s % (R.strata_x * R.strata_y) : 0u);
+}
+// One new camera sample per `want` lane: a block-aggregated claim of
+// consecutive sample ids (one returning atomic per block: coherent primary
+// rays), then Camera::GenerateRay for the claimed ids below the chunk's end.
+// Every thread of the block calls it (barriers).
 __device__ __forceinline__ NewSample claim_camera_sample(const RenderParams& R, bool want,
                                                          unsigned long long* __restrict__ next_sample) {
     __shared__ uint32_t s_w[17];  // up to 1024 threads per block
@@ -816,15 +828,7 @@ __device__ __forceinline__ NewSample claim_camera_sample(const RenderParams& R, 
     __syncthreads();
     const unsigned long long g = s_base + s_w[wave] + lanemask_lt_count(m);
     NewSample ns{want && g < R.chunk_total, (uint32_t)g, 0u, F3(0, 0, 0), F3(0, 0, 0), 0.0f};
-    if (ns.enq) {
-        const uint32_t s_rel = (uint32_t)(g / R.npix_work), pix_i = (uint32_t)(g % R.npix_work);
-        uint32_t x, y;
-        work_pixel(R, pix_i, x, y);
-        const uint32_t s = R.shard_index + (R.s_lo + s_rel) * R.shard_count;
-        ns.key = stream_key(R.seed, y * (uint32_t)R.cam.width + x, s);
-        camera_ray(R.cam, ns.key, x, y, ns.o, ns.d, ns.time, R.strata_x, R.strata_y,
-                   R.strata_x ? s % (R.strata_x * R.strata_y) : 0u);
-    }
+    if (ns.enq) camera_sample(R, ns);
     return ns;
 }
 __device__ __forceinline__ void store_camera_path(PathSoA& next, uint32_t at, const NewSample& ns, int cam_medium) {
@@ -840,16 +844,23 @@ __device__ __forceinline__ void store_camera_path(PathSoA& next, uint32_t at, co
 // Initial fill of a chunk's wavefront: one camera sample per entry.  Later
 // refills happen in k_shade, where paths finish.  maxDepth 0 never gets here:
 // the runtime zero-fills.
+// The chunk's initial fill.  Both counters start at zero (the runtime clears
+// them), so path slot i takes chunk sample i directly and one thread books
+// the whole fill: the block-aggregated claims and appends the refills use
+// would be two returning atomics per block on one address each (4 M for
+// 512 M paths, which was the launch's whole cost: C4 k_fill 25 ms).
 __global__ __launch_bounds__(256) void k_fill(RenderParams R, uint32_t n, PathSoA next, uint32_t* __restrict__ cnt,
                                              unsigned long long* __restrict__ next_sample) {
-    if (blockIdx.x * 256 >= n) return;
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    const NewSample ns = claim_camera_sample(R, i < n, next_sample);
-    const int qoff[1] = {Q_NEXT};
-    const bool pred[1] = {ns.enq};
-    uint32_t at[1];
-    block_append<1, 256>(cnt, qoff, pred, at);
-    if (ns.enq) store_camera_path(next, at[0], ns, R.cam.medium);
+    const uint32_t m = (uint32_t)min((unsigned long long)n, R.chunk_total);
+    if (i == 0) {
+        atomicAdd(next_sample, (unsigned long long)m);
+        atomicAdd(&cnt[Q_NEXT], m);
+    }
+    if (i >= m) return;
+    NewSample ns{true, i, 0u, F3(0, 0, 0), F3(0, 0, 0), 0.0f};
+    camera_sample(R, ns);
+    store_camera_path(next, i, ns, R.cam.medium);
 }
 
 // ------------------------------------------------------------------ shading

@@ -100,11 +100,14 @@ RANDOM_INTEGRAL = ("lanczos",)
 def rescaled_reference_film(name: str, ref: np.ndarray, film: np.ndarray) -> np.ndarray:
     """The reference's film on this package's filter integral: identity,
     except for RANDOM_INTEGRAL scenes, where the one tile constant is taken
-    from the weight sums and bounded by the estimator's spread (2e-4)."""
+    from the weight sums and bounded by the estimators' spread: the ratio of
+    two of LanczosFilter::Integral()'s jittered 256x256 estimates has a
+    relative standard deviation of 1.0e-4 (300 simulated estimates), so 5e-4
+    is five of them (2e-4, two, failed a drop-in run at 2.55e-4)."""
     if name not in RANDOM_INTEGRAL:
         return ref
     s = float(film[..., 3].sum() / ref[..., 3].sum())
-    assert abs(s - 1.0) < 2e-4, f"{name}: filter integral estimates differ by {s - 1.0:.2e}"
+    assert abs(s - 1.0) < 5e-4, f"{name}: filter integral estimates differ by {s - 1.0:.2e}"
     return ref * s
 
 
