@@ -205,6 +205,7 @@ struct DevPrimInfo {
 struct DevScene {
     float bb_lo[3], bb_scale[3];  // scene box: lo and 16 / extent per axis (spatial hit sort)
     const uint32_t* ray_order;    // closest-hit claim order (PT_RENDER_SORT_RAYS), else null
+    uint16_t* hit_bins;           // the pool kernels write each closest hit's spatial sort bin here, else null
     const DevCluster* nodes;
     const DevQNode* qnodes;    // the same nodes quantized (null: the scene could not be encoded);
                                // PT_WIDE: DevWNode records (reinterpreted)

@@ -178,6 +178,15 @@ enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1, PT_SORT_RAYS = 2 };
 #define PT_SORT_BINS_SPATIAL (1 << (3 * PT_SORT_CELL_BITS))
 // spatial sort key: the hit primitive's slot range (leaf order) instead of
 // the hit point's Morton cell (reads the hit record only)
+// PT_HIT_BINS: the closest-hit pool kernel writes each path's spatial sort
+// bin when its ray is done (ClosestSrc::done), k_sort_count reads 2 B per
+// path instead of 48.  Off: C4 k_sort_count 63.7 -> 27.9 ms per frame, but
+// k_closest_pool 2947 -> 3341 (the bin's code on the overlapped loop's
+// ray-done path, which a wave runs whenever one lane finishes; 3 -> 6 VGPR
+// spills): -6.5 % (profiles/r05_ab_hitbins.txt)
+#ifndef PT_HIT_BINS
+#define PT_HIT_BINS 0
+#endif
 #ifndef PT_SORT_BY_SLOT
 #define PT_SORT_BY_SLOT 0  // off: C4 -1.5 % (profiles/r04_ab_traversal.txt)
 #endif

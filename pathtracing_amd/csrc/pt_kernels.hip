@@ -222,6 +222,20 @@ __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, flo
                                        (SPEC_) ? PT_SPEC_SHADOW_WPE : PT_SHADOW_WPE)))
 // which pool kernels take trace_spec (pt_pool.h trace_pool's dispatch)
 #define PT_USES_SPEC(INST_, QN_) (PT_SPEC && (QN_) && !(INST_) && !PT_ENTRY && !PT_WIDE)
+// The spatial hit sort's bin of a hit at o + t d: the Morton code of its
+// cell in a 2^PT_SORT_CELL_BITS grid over the scene box (0 for a miss too)
+__device__ __forceinline__ uint32_t hit_cell(f3 o, f3 d, float t) {
+    uint32_t code = 0;
+    const float p[3] = {fmaf(t, d.x, o.x), fmaf(t, d.y, o.y), fmaf(t, d.z, o.z)};
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const float q = (p[a] - S.bb_lo[a]) * S.bb_scale[a];  // [0, 2^bits)
+        const uint32_t c = (uint32_t)fminf(fmaxf(q, 0.0f), (float)((1 << PT_SORT_CELL_BITS) - 1));
+#pragma unroll
+        for (int b = 0; b < PT_SORT_CELL_BITS; b++) code |= ((c >> b) & 1u) << (3 * b + a);
+    }
+    return code;
+}
 // Persistent, refilling traversal (pt_pool.h): grid = resident blocks, rays
 // claimed from the pool counters (zeroed with the queue counters).
 struct ClosestSrc {
@@ -246,6 +260,12 @@ struct ClosestSrc {
         return P.time[path_slot(S.ray_order ? S.ray_order[i] : i, front, P.cap)];
     }
     __device__ __forceinline__ void any(uint32_t, bool) {}
+    // the ray is done (world o, d; t of its closest hit when found): its
+    // spatial sort bin, while the ray is still in registers, so the hit sort
+    // reads 2 B per path instead of the hit and the ray (48 B)
+    __device__ __forceinline__ void done(uint32_t i, f3 o, f3 d, float t, bool found) {
+        if (PT_HIT_BINS && S.hit_bins) S.hit_bins[S.ray_order ? S.ray_order[i] : i] = (uint16_t)(found ? hit_cell(o, d, t) : 0u);
+    }
     // the list holds P.cap entries (a ray is listed at most once per launch:
     // OCT_TIE survives instance enter / exit); the bound keeps a miscount in bounds
     __device__ __forceinline__ void tie(uint32_t i) {
@@ -330,6 +350,7 @@ struct ShadowSrcT {
     ShadowRec* sq;
     PathSoA next;
     float* sample_L;
+    __device__ __forceinline__ void done(uint32_t, f3, f3, float, bool) {}
     __device__ __forceinline__ bool load(uint32_t i, f3& o, f3& d, float& tmax) {
         const float4 ro = sq[i].o, rd = sq[i].d;
         o = xyz(ro);
@@ -476,6 +497,7 @@ struct RaysSrc {
     uint32_t* ties;  // exact-t ties (pt_pool.h), re-traced by k_trace_rays_ties
     uint32_t* n_ties;
     uint32_t n;      // rays, and entries of the tie list
+    __device__ __forceinline__ void done(uint32_t, f3, f3, float, bool) {}
     __device__ __forceinline__ bool load(uint32_t i, f3& o, f3& d, float& tmax) {
         const pt_ray r = rays[i];
         o = F3(r.o[0], r.o[1], r.o[2]);
@@ -1797,18 +1819,7 @@ __device__ __forceinline__ uint32_t sort_bin(const PathSoA& cur, uint32_t front,
         return mat < 0 ? 0u : 1u + (uint32_t)mat % (PT_SORT_BINS_MATERIAL - 2u);
     }
     const uint32_t e = path_slot(i, front, cur.cap);
-    const f3 o = xyz(cur.o[e]), d = xyz(cur.d[e]);
-    const float t = h.x;
-    uint32_t code = 0;
-    const float p[3] = {fmaf(t, d.x, o.x), fmaf(t, d.y, o.y), fmaf(t, d.z, o.z)};
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-        const float q = (p[a] - S.bb_lo[a]) * S.bb_scale[a];  // [0, 2^bits)
-        const uint32_t c = (uint32_t)fminf(fmaxf(q, 0.0f), (float)((1 << PT_SORT_CELL_BITS) - 1));
-#pragma unroll
-        for (int b = 0; b < PT_SORT_CELL_BITS; b++) code |= ((c >> b) & 1u) << (3 * b + a);
-    }
-    return code;
+    return hit_cell(xyz(cur.o[e]), xyz(cur.d[e]), h.x);
 }
 // Each block bins PT_SORT_PER paths per thread (PT_SORT_PER x 256
 // consecutive paths), so clearing and folding the block's 4096-bin LDS
@@ -1829,9 +1840,14 @@ __global__ __launch_bounds__(256) void k_sort_count(PathSoA cur, const uint32_t*
     for (uint32_t k = 0; k < PT_SORT_PER; k++) {
         const uint32_t t = t0 + k * 256u + threadIdx.x;
         if (t < n) {
-            const uint32_t b = sort_bin<KEY>(cur, front, hit, t);
+            uint32_t b;
+            if (KEY == PT_SORT_SPATIAL && S.hit_bins) {  // written by the closest-hit pool kernel
+                b = S.hit_bins[t];
+            } else {
+                b = sort_bin<KEY>(cur, front, hit, t);
+                if (bins) bins[t] = (uint16_t)b;
+            }
             atomicAdd(&h[b], 1u);
-            if (bins) bins[t] = (uint16_t)b;
         }
     }
     __syncthreads();

@@ -431,8 +431,12 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         }
 #endif
         if (ref == REF_EMPTY && leaf == REF_EMPTY) {  // sp == 0: no hit (any) / closest result
-            if (ANY) src.any((uint32_t)ri, false);
-            else if (!(oct & OCT_FOUND)) src.closest((uint32_t)ri, tmax, 0.0f, 0.0f, -1);
+            if (ANY) {
+                src.any((uint32_t)ri, false);
+            } else {
+                if (!(oct & OCT_FOUND)) src.closest((uint32_t)ri, tmax, 0.0f, 0.0f, -1);
+                src.done((uint32_t)ri, o, d, tmax, (oct & OCT_FOUND) != 0);
+            }
             ri = -1;
             continue;
         }
@@ -915,8 +919,12 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 }
             }
             if (finished) {  // no hit (any) / closest result
-                if (ANY) src.any((uint32_t)ri, false);
-                else src.closest((uint32_t)ri, tmax, bb1, bb2, best);
+                if (ANY) {
+                    src.any((uint32_t)ri, false);
+                } else {
+                    src.closest((uint32_t)ri, tmax, bb1, bb2, best);
+                    src.done((uint32_t)ri, o, d, tmax, best >= 0);
+                }
                 ri = -1;
                 continue;
             }

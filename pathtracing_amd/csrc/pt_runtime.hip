@@ -1727,9 +1727,14 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     }
     if (st) return st;
     c->scene.ray_order = sort_rays ? c->ray_order : nullptr;
-    struct ResetOrder {  // other entry points bind the scene without a claim order
+    // the spatial hit sort's bins come from the closest-hit pool kernel
+    c->scene.hit_bins = (PT_HIT_BINS && sort_sp && keep_bins && use_pool) ? c->sort_bins : nullptr;
+    struct ResetOrder {  // other entry points bind the scene without a claim order or hit bins
         pt_ctx* c;
-        ~ResetOrder() { c->scene.ray_order = nullptr; }
+        ~ResetOrder() {
+            c->scene.ray_order = nullptr;
+            c->scene.hit_bins = nullptr;
+        }
     } reset_order{c};
     if ((st = bind_scene(c)) != PT_OK) return st;
     uint16_t* bins = keep_bins ? c->sort_bins : nullptr;  // (shared by the claim-order and hit sorts: each pass pair runs in turn on sm)
