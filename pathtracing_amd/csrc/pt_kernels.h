@@ -56,6 +56,15 @@
 #ifndef PT_PATH_AOS
 #define PT_PATH_AOS 2
 #endif
+// PT_PATH_INV: the path state carries the ray's 1/d (PathSoA.inv), written by
+// the kernels that write the ray; the overlapped closest-hit traversal loads
+// it with the ray instead of dividing on its ray-setup path.  Off: the
+// traversal's loop loses 43 static VALU but not time (102.2 -> 102.3 ms per
+// launch), and the shading's extra 16-B writes cost more: C4 -0.4 %
+// (profiles/r05_ab_path_inv.txt)
+#ifndef PT_PATH_INV
+#define PT_PATH_INV 0
+#endif
 #define PT_PATH_STRIDE (PT_PATH_AOS == 1 ? 4u : PT_PATH_AOS == 2 ? 2u : 1u)
 struct PField {  // one float4 field of the path state, indexed by entry
     float4* p;
@@ -70,6 +79,8 @@ struct PathSoA {
     uint32_t cap; // entries
     float* time;  // the path's ray time (Ray::time, constant along a path: every
                   // scatter copies it, Material.hpp:264 ...); only with S.motion
+    float4* inv;  // PT_PATH_INV: 1/d.xyz (the Ray ctor's invDir, Ray.hpp:32-35), written
+                  // with the ray, so the closest-hit pool kernel's ray setup loads it
 };
 __device__ __forceinline__ uint32_t path_count(const uint32_t* set) { return set[Q_NEXT] + set[Q_NEW]; }
 __device__ __forceinline__ uint32_t path_slot(uint32_t i, uint32_t c, uint32_t cap) {

@@ -253,6 +253,15 @@ struct ClosestSrc {
         tmax = __int_as_float(0x7f800000);
         return true;
     }
+    static constexpr bool kInv = PT_PATH_INV;  // the ray's 1/d comes with it (PathSoA.inv)
+    __device__ __forceinline__ void load_inv(uint32_t i, f3& o, f3& d, f3& inv, float& tmax) {
+        const uint32_t j = S.ray_order ? S.ray_order[i] : i;
+        const uint32_t e = path_slot(j, front, P.cap);
+        o = xyz(P.o[e]);
+        d = xyz(P.d[e]);
+        inv = xyz(P.inv[e]);
+        tmax = __int_as_float(0x7f800000);
+    }
     __device__ __forceinline__ void closest(uint32_t i, float t, float b1, float b2, int prim) {
         hit[S.ray_order ? S.ray_order[i] : i] = make_float4(t, b1, b2, __int_as_float(prim));
     }
@@ -350,6 +359,8 @@ struct ShadowSrcT {
     ShadowRec* sq;
     PathSoA next;
     float* sample_L;
+    static constexpr bool kInv = false;
+    __device__ __forceinline__ void load_inv(uint32_t, f3&, f3&, f3&, float&) {}
     __device__ __forceinline__ void done(uint32_t, f3, f3, float, bool) {}
     __device__ __forceinline__ bool load(uint32_t i, f3& o, f3& d, float& tmax) {
         const float4 ro = sq[i].o, rd = sq[i].d;
@@ -497,6 +508,8 @@ struct RaysSrc {
     uint32_t* ties;  // exact-t ties (pt_pool.h), re-traced by k_trace_rays_ties
     uint32_t* n_ties;
     uint32_t n;      // rays, and entries of the tie list
+    static constexpr bool kInv = false;
+    __device__ __forceinline__ void load_inv(uint32_t, f3&, f3&, f3&, float&) {}
     __device__ __forceinline__ void done(uint32_t, f3, f3, float, bool) {}
     __device__ __forceinline__ bool load(uint32_t i, f3& o, f3& d, float& tmax) {
         const pt_ray r = rays[i];
@@ -853,10 +866,12 @@ __device__ __forceinline__ NewSample claim_camera_sample(const RenderParams& R, 
     if (ns.enq) camera_sample(R, ns);
     return ns;
 }
+__device__ __forceinline__ float4 f4_of(f3 v) { return make_float4(v.x, v.y, v.z, 0.0f); }
 __device__ __forceinline__ void store_camera_path(PathSoA& next, uint32_t at, const NewSample& ns, int cam_medium) {
     next.o[at] = make_float4(ns.o.x, ns.o.y, ns.o.z, __uint_as_float(ns.key));
     // depth 1 (first loop test passed), spec = true, the camera's medium (Camera.hpp:27, 34)
     next.d[at] = make_float4(ns.d.x, ns.d.y, ns.d.z, __uint_as_float(1u | PF_SPEC | medium_bits(cam_medium)));
+    if (PT_PATH_INV) next.inv[at] = f4_of(inv_dir(ns.d));
     next.beta[at] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);  // attenuation, prevPDF = 1
     next.L[at] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(5u));  // camera used dims 0..4
     next.sid[at] = ns.sid;
@@ -1124,6 +1139,7 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
     if (cont) {
         next.o[a] = make_float4(ro.x, ro.y, ro.z, __uint_as_float(key));
         next.d[a] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(flags));
+        if (PT_PATH_INV) next.inv[a] = f4_of(inv_dir(rd));
         next.beta[a] = make_float4(att.x, att.y, att.z, prev);
         next.L[a] = make_float4(out.x, out.y, out.z, __uint_as_float(dim));
         next.sid[a] = sid;
@@ -1421,6 +1437,7 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
     if (cont) {
         next.o[a] = make_float4(ro.x, ro.y, ro.z, __uint_as_float(key));
         next.d[a] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(flags));
+        if (PT_PATH_INV) next.inv[a] = f4_of(inv_dir(rd));
         next.beta[a] = make_float4(att.x, att.y, att.z, prev);
         next.L[a] = make_float4(out.x, out.y, out.z, __uint_as_float(dim));
         next.sid[a] = sid;

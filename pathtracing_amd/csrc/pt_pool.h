@@ -348,7 +348,8 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                     // this iteration's node loads are in flight too, so the
                     // two round trips overlap (trace_spec's sources never skip
                     // a ray: ClosestSrc / ShadowSrcT::load return true)
-                    src.load((uint32_t)ri, o, d, tmax);
+                    if constexpr (Src::kInv) src.load_inv((uint32_t)ri, o, d, inv, tmax);
+                    else src.load((uint32_t)ri, o, d, tmax);
                     oct = OCT_FRESH;
 #else
                     if (!src.load((uint32_t)ri, o, d, tmax)) __builtin_trap();
@@ -519,7 +520,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
 #if PT_DEFER_SETUP
         PT_IT(10, __ballot(oct & OCT_FRESH) != 0);
         if (oct & OCT_FRESH) {  // a ray claimed this iteration: its origin and direction are in
-            inv = inv_dir(d);
+            if constexpr (!Src::kInv) inv = inv_dir(d);
             oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
         }
 #endif

@@ -447,9 +447,9 @@ static void free_work(pt_ctx* c) {
     // L beta's)
     constexpr bool own_d = PT_PATH_AOS == 0, own_beta = PT_PATH_AOS != 1, own_L = PT_PATH_AOS == 0;
     void* bufs[] = {c->PA.o.p, own_d ? c->PA.d.p : nullptr, own_beta ? c->PA.beta.p : nullptr,
-                    own_L ? c->PA.L.p : nullptr, c->PA.sid, c->PA.time, c->PB.o.p,
+                    own_L ? c->PA.L.p : nullptr, c->PA.sid, c->PA.time, c->PA.inv, c->PB.o.p,
                     own_d ? c->PB.d.p : nullptr, own_beta ? c->PB.beta.p : nullptr,
-                    own_L ? c->PB.L.p : nullptr, c->PB.sid, c->PB.time, c->hit, c->qcnt, c->sq, c->counters,
+                    own_L ? c->PB.L.p : nullptr, c->PB.sid, c->PB.time, c->PB.inv, c->hit, c->qcnt, c->sq, c->counters,
                     c->ovf, c->ties, c->sq_time};
     for (void* p : bufs)
         if (p) hipFree(p);
@@ -1459,6 +1459,7 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
             AL(P->L.p, n * 16);
         }
         AL(P->sid, n * 4);
+        if (PT_PATH_INV) AL(P->inv, n * 16);
     }
     AL(c->hit, n * 16);
     AL(c->ties, n * 4);  // a ray is listed at most once per launch
