@@ -204,6 +204,7 @@ struct DevPrimInfo {
 
 struct DevScene {
     float bb_lo[3], bb_scale[3];  // scene box: lo and 16 / extent per axis (spatial hit sort)
+    const uint16_t* prim_cell;    // PT_SORT_PRIM_CELL: each primitive slot's centroid cell (spatial hit sort), else null
     const uint32_t* ray_order;    // closest-hit claim order (PT_RENDER_SORT_RAYS), else null
     uint16_t* hit_bins;           // the pool kernels write each closest hit's spatial sort bin here, else null
     const DevCluster* nodes;

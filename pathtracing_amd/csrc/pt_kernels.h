@@ -198,6 +198,12 @@ enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1, PT_SORT_RAYS = 2 };
 #ifndef PT_HIT_BINS
 #define PT_HIT_BINS 0
 #endif
+// PT_SORT_PRIM_CELL: the spatial hit sort bins a hit by its primitive's
+// centroid cell (a 2-B table built at upload) instead of the hit point's, so
+// k_sort_count reads the hit record alone (16 B per path instead of 48)
+#ifndef PT_SORT_PRIM_CELL
+#define PT_SORT_PRIM_CELL 1
+#endif
 #ifndef PT_SORT_BY_SLOT
 #define PT_SORT_BY_SLOT 0  // off: C4 -1.5 % (profiles/r04_ab_traversal.txt)
 #endif

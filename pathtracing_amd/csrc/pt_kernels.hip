@@ -1823,6 +1823,10 @@ __device__ __forceinline__ uint32_t sort_bin(const PathSoA& cur, uint32_t front,
     const float4 h = hit[i];
     const int prim = __float_as_int(h.w);
     if (prim < 0) return 0u;
+    if (KEY == PT_SORT_SPATIAL && PT_SORT_PRIM_CELL && S.prim_cell) {
+        if ((uint32_t)prim >= S.n_prims) return PT_SORT_BINS_SPATIAL - 1u;  // a virtual slot inside an instance
+        return S.prim_cell[prim];
+    }
     if (KEY == PT_SORT_SPATIAL && PT_SORT_BY_SLOT) {
         // the hit primitive's slot: slots are in the BVH's leaf order, so a
         // range of them is a compact patch of geometry (and of its materials);

@@ -1373,6 +1373,38 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
             DS.bb_scale[a] = hi[a] > lo[a] ? (float)(1 << PT_SORT_CELL_BITS) / (hi[a] - lo[a]) : 0.0f;
         }
     }
+    DS.prim_cell = nullptr;
+    if (PT_SORT_PRIM_CELL && s->n_prims) {  // each primitive's centroid cell, hit_cell's Morton code
+        std::vector<uint16_t> cell(s->n_prims, 0);
+        auto code = [&](const float* p) {
+            uint32_t m = 0;
+            for (int a = 0; a < 3; a++) {
+                const float q = (p[a] - DS.bb_lo[a]) * DS.bb_scale[a];
+                const uint32_t c = (uint32_t)std::min(std::max(q, 0.0f), (float)((1 << PT_SORT_CELL_BITS) - 1));
+                for (int b = 0; b < PT_SORT_CELL_BITS; b++) m |= ((c >> b) & 1u) << (3 * b + a);
+            }
+            return (uint16_t)m;
+        };
+        for (uint32_t i = 0; i < s->n_prims; i++) {
+            const pt_prim& pr = s->prims[i];
+            float c[3];
+            if (pr.kind == PT_PRIM_TRIANGLE) {
+                const uint32_t* v = s->tri_vidx + 3 * (size_t)pr.index;
+                for (int a = 0; a < 3; a++)
+                    c[a] = (s->positions[3 * (size_t)v[0] + a] + s->positions[3 * (size_t)v[1] + a] +
+                            s->positions[3 * (size_t)v[2] + a]) * (1.0f / 3.0f);
+            } else if (pr.kind == PT_PRIM_QUAD) {
+                const pt_quad& q = s->quads[pr.index];
+                for (int a = 0; a < 3; a++) c[a] = q.Q[a] + 0.5f * (q.u[a] + q.v[a]);
+            } else if (pr.kind == PT_PRIM_SPHERE) {
+                for (int a = 0; a < 3; a++) c[a] = s->spheres[pr.index].center[a];
+            } else {
+                continue;  // a hop or an instance: never a hit's slot
+            }
+            cell[i] = code(c);
+        }
+        if ((st = upload(c, cell.data(), cell.size(), &DS.prim_cell)) != PT_OK) return st;
+    }
     DS.n_nodes = (uint32_t)nodes.size();
     DS.n_texel_bytes = s->n_texel_bytes;
     DS.n_lights = s->n_lights;
