@@ -187,8 +187,19 @@ enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1, PT_SORT_RAYS = 2 };
 #define PT_SORT_CELL_BITS 4  // spatial sort: 2^bits cells per axis of the scene box
 #endif
 #define PT_SORT_BINS_SPATIAL (1 << (3 * PT_SORT_CELL_BITS))
+// Hit-state binning of a bounce's paths before shading: the spatial key
+// (default) is the hit primitive's centroid cell (PT_SORT_PRIM_CELL: a 2-B
+// table built at upload, so k_sort_count reads the hit record alone, 16 B per
+// path instead of the hit and the ray's 48: C4 +0.4 %,
+// profiles/r05_ab_prim_cell.txt); 0: the hit point's cell
+#ifndef PT_SORT_PRIM_CELL
+#define PT_SORT_PRIM_CELL 1
+#endif
 // spatial sort key: the hit primitive's slot range (leaf order) instead of
 // the hit point's Morton cell (reads the hit record only)
+#ifndef PT_SORT_BY_SLOT
+#define PT_SORT_BY_SLOT 0  // off: C4 -1.5 % (profiles/r04_ab_traversal.txt)
+#endif
 // PT_HIT_BINS: the closest-hit pool kernel writes each path's spatial sort
 // bin when its ray is done (ClosestSrc::done), k_sort_count reads 2 B per
 // path instead of 48.  Off: C4 k_sort_count 63.7 -> 27.9 ms per frame, but
@@ -198,14 +209,10 @@ enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1, PT_SORT_RAYS = 2 };
 #ifndef PT_HIT_BINS
 #define PT_HIT_BINS 0
 #endif
-// PT_SORT_PRIM_CELL: the spatial hit sort bins a hit by its primitive's
-// centroid cell (a 2-B table built at upload) instead of the hit point's, so
-// k_sort_count reads the hit record alone (16 B per path instead of 48)
-#ifndef PT_SORT_PRIM_CELL
-#define PT_SORT_PRIM_CELL 1
-#endif
-#ifndef PT_SORT_BY_SLOT
-#define PT_SORT_BY_SLOT 0  // off: C4 -1.5 % (profiles/r04_ab_traversal.txt)
+// blocks of the exact-tie re-trace (k_closest_ties, grid-stride over the
+// listed rays): with 64 (a quarter of the CUs) it took 0.66 ms per C4 launch
+#ifndef PT_TIE_BLOCKS
+#define PT_TIE_BLOCKS 1024u
 #endif
 #ifndef PT_SHADE_BLOCK
 // k_shade threads per block (its appends aggregate per block): C4 64 / 128 /
@@ -216,7 +223,7 @@ enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1, PT_SORT_RAYS = 2 };
 #define PT_SHADE_BLOCK 1024
 #endif
 #ifndef PT_SORT_PER
-#define PT_SORT_PER 16u  // paths per thread of k_sort_count / k_sort_scatter
+#define PT_SORT_PER 32u  // paths per thread of k_sort_count / k_sort_scatter (16: -0.07 %, profiles/r05_ab_ties_sort.txt)
 #endif
 template <int KEY, int NB>
 __global__ void k_sort_count(PathSoA cur, const uint32_t* nptr, const float4* hit, uint32_t* counts, uint16_t* bins);

@@ -1890,7 +1890,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                                    c->counters, c->ties);
                 if (use_pool)  // the rays that met an exact-t tie, re-traced in the reference's order
                     hipLaunchKernelGGL(inst ? k_closest_ties<true> : k_closest_ties<false>,
-                                       dim3(std::min(64u, gt.x)), dim3(PT_TRACE_BLOCK), 0, sm, cur,
+                                       dim3(std::min(PT_TIE_BLOCKS, gt.x)), dim3(PT_TRACE_BLOCK), 0, sm, cur,
                                        (const uint32_t*)in, c->hit, (const uint32_t*)(out + Q_WORDS),
                                        (const uint32_t*)c->ties);
             }
