@@ -1628,17 +1628,21 @@ __global__ __launch_bounds__(256) void k_gather(RenderParams R, const float* __r
 // re-hashing and re-evaluating the filter per (source, target).  Weights are
 // bit-identical to k_gather's; the f64 sums run sample-major instead of
 // neighbour-major.
+// FILT: the filter the tile kernel is built for (-1: any, chosen per call),
+// so a launch carries only its own filter's code and registers
+template <int FILT = -1>
 __device__ __forceinline__ double filter_1d(const RenderParams& R, float p, int axis) {
-    if (R.filter == PT_FILTER_BOX) return fabsf(p) <= R.frad[axis] ? 1.0 : 0.0;
-    if (R.filter == PT_FILTER_LANCZOS) return wsinc1(p, R.frad[axis], R.fparam[0]);
-    if (R.filter == PT_FILTER_GAUSSIAN) {
+    const uint32_t f = FILT < 0 ? R.filter : (uint32_t)FILT;
+    if (f == PT_FILTER_BOX) return fabsf(p) <= R.frad[axis] ? 1.0 : 0.0;
+    if (f == PT_FILTER_LANCZOS) return wsinc1(p, R.frad[axis], R.fparam[0]);
+    if (f == PT_FILTER_GAUSSIAN) {
         const double g = gauss1(p, R.fparam[0]) - (axis ? R.gauss_y : R.gauss_x);
         return g > 0 ? g : 0;
     }
     return mitchell1(2 * p / R.frad[axis], R.fparam[0], R.fparam[1]);
 }
 
-template <int RAD>
+template <int RAD, int FILT>
 __global__ __launch_bounds__(256) void k_gather_tile(RenderParams R, const float* __restrict__ sample_L,
                                                      double* __restrict__ film) {
     constexpr int T = 16, SW = T + 2 * RAD, NS = SW * SW, NW = 2 * RAD + 1;
@@ -1674,8 +1678,8 @@ __global__ __launch_bounds__(256) void k_gather_tile(RenderParams R, const float
                 sample_fract(R, key, (uint32_t)sx, (uint32_t)sy, s, fx, fy);
 #pragma unroll
                 for (int o = -RAD; o <= RAD; o++) {
-                    if (o >= -rx && o <= rx) wx[o + RAD] = filter_1d(R, (float)((double)o + 0.5 - fx), 0);
-                    if (o >= -ry && o <= ry) wy[o + RAD] = filter_1d(R, (float)((double)o + 0.5 - fy), 1);
+                    if (o >= -rx && o <= rx) wx[o + RAD] = filter_1d<FILT>(R, (float)((double)o + 0.5 - fx), 0);
+                    if (o >= -ry && o <= ry) wy[o + RAD] = filter_1d<FILT>(R, (float)((double)o + 0.5 - fy), 1);
                 }
                 const float* L = sample_L + 3ull * ((uint64_t)k * R.npix_work + pix_i);
                 L0 = L[0], L1 = L[1], L2 = L[2];

@@ -2121,10 +2121,19 @@ static pt_status render_dev(pt_ctx* c, const pt_camera_desc* cam, const pt_rende
             const uint32_t npx = (uint32_t)cam->width * cam->height;
             const int rad = std::max(R.rad_x, R.rad_y);
             const dim3 tiles((cam->width + 15) / 16, (cam->height + 15) / 16);
+            // the tile gather built for the film's filter (its own code and registers only)
+            auto tile = [&](auto rad_c) {
+                constexpr int RAD = decltype(rad_c)::value;
+                auto k = R.filter == PT_FILTER_MITCHELL ? k_gather_tile<RAD, PT_FILTER_MITCHELL>
+                         : R.filter == PT_FILTER_BOX    ? k_gather_tile<RAD, PT_FILTER_BOX>
+                         : R.filter == PT_FILTER_GAUSSIAN ? k_gather_tile<RAD, PT_FILTER_GAUSSIAN>
+                                                          : k_gather_tile<RAD, PT_FILTER_LANCZOS>;
+                hipLaunchKernelGGL(k, tiles, dim3(256), 0, c->stream, R, c->sample_L, film);
+            };
             if (R.npix_work == npx && rad <= 1 && !getenv("PT_GATHER_PIXEL"))
-                hipLaunchKernelGGL(k_gather_tile<1>, tiles, dim3(256), 0, c->stream, R, c->sample_L, film);
+                tile(std::integral_constant<int, 1>{});
             else if (R.npix_work == npx && rad == 2 && !getenv("PT_GATHER_PIXEL"))
-                hipLaunchKernelGGL(k_gather_tile<2>, tiles, dim3(256), 0, c->stream, R, c->sample_L, film);
+                tile(std::integral_constant<int, 2>{});
             else
                 hipLaunchKernelGGL(k_gather, dim3((npx + 255) / 256), dim3(256), 0, c->stream, R, c->sample_L, film);
             HIPCHK(c, hipGetLastError());
