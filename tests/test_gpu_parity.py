@@ -737,3 +737,58 @@ def test_gpu_upload_rejects_an_image_past_the_texel_buffer():
     with pytest.raises(N.NativeError):
         ctx.upload(bad)
     ctx.upload(flat)  # and the real one again
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("defect", ["cycle", "backward", "other_bvh", "tlas_names_level", "too_deep"])
+def test_gpu_upload_rejects_a_malformed_instance_chain(defect):
+    """pt_scene_upload validates nested wrappers (pt_instance.inner): a level
+    record must come after the record that names it (no cycles), share its
+    chain's bvh, never be a TLAS slot's instance, and a chain holds at most
+    PT_MAX_INSTANCE_DEPTH levels; each defect is PT_ERR_ARG and the
+    unmodified scene uploads afterwards."""
+    import copy
+    setup = scenes.nested_instances(W=16, H=16, spp=1)
+    integ = setup.make_integrator()
+    ctx = integ.context()
+    flat = integ.flat
+    ins = flat.instances
+    top = np.nonzero(np.isin(np.arange(len(ins)), flat.prims["index"][flat.prims["kind"] == N.PT_PRIM_INSTANCE]))[0]
+    deep = max(top, key=lambda k: _chain_len(ins, k))  # the four-level pane
+    assert _chain_len(ins, deep) == 4
+    bad = copy.copy(flat)
+    bad.instances = ins.copy()
+    first = int(ins["inner"][deep])
+    if defect == "cycle":  # the innermost level points back at the chain's second record
+        last = first
+        while bad.instances["inner"][last] >= 0:
+            last = int(bad.instances["inner"][last])
+        bad.instances["inner"][last] = first
+    elif defect == "backward":  # a level record before the record that names it
+        bad.instances["inner"][first] = deep
+    elif defect == "other_bvh":
+        other = next(int(b) for b in np.unique(ins["bvh"]) if b != ins["bvh"][deep])
+        bad.instances["bvh"][first] = other
+    elif defect == "tlas_names_level":
+        bad.prims = flat.prims.copy()
+        slot = int(np.nonzero((flat.prims["kind"] == N.PT_PRIM_INSTANCE))[0][0])
+        bad.prims["index"][slot] = first
+    else:  # a fifth level: the innermost record chains to a copy of itself
+        extra = bad.instances[first:first + 1].copy()
+        last = first
+        while bad.instances["inner"][last] >= 0:
+            last = int(bad.instances["inner"][last])
+        extra["inner"] = -1
+        bad.instances["inner"][last] = len(bad.instances)
+        bad.instances = np.concatenate([bad.instances, extra])
+    with pytest.raises(N.NativeError):
+        ctx.upload(bad)
+    ctx.upload(flat)
+
+
+def _chain_len(ins, k):
+    n = 1
+    while ins["inner"][k] >= 0:
+        k = int(ins["inner"][k])
+        n += 1
+    return n
