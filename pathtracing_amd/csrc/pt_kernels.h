@@ -219,8 +219,12 @@ enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1, PT_SORT_RAYS = 2 };
 // 256 / 512 / 1024 -> 1206 / 1236 / 1270 / 1205 / 1278 Mrays/s
 // (profiles/r02_ab_shade.txt).  r04, k_shade ms per frame on one box
 // (gpurun_out/r4h): 1024 x 4 waves per SIMD 1372, 256 x 3 waves 1374,
-// 512 x 3 waves 1713 (one block per CU: 2 waves per SIMD)
-#define PT_SHADE_BLOCK 1024
+// 512 x 3 waves 1713 (one block per CU: 2 waves per SIMD).  r05, every size
+// at 4 waves per SIMD (128 VGPRs): 64 / 128 / 256 / 512 / 1024 -> 1846 /
+// 1982 / 2015 / 2004 / 1970 Mrays/s (profiles/r05_ab_shade_block.txt): a
+// 1024-thread block fills its CU alone, so each of its barriers (the sample
+// claim, the queue appends) idles the whole CU
+#define PT_SHADE_BLOCK 256
 #endif
 #ifndef PT_SORT_PER
 #define PT_SORT_PER 32u  // paths per thread of k_sort_count / k_sort_scatter (16: -0.07 %, profiles/r05_ab_ties_sort.txt)

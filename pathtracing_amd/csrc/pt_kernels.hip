@@ -1088,7 +1088,7 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
 
 template <int INTEGRATOR>
 #ifndef PT_SHADE_WPE  // waves-per-SIMD budget for k_shade (pt_kernels.h PT_SHADE_BLOCK)
-#define PT_SHADE_WPE (PT_SHADE_BLOCK >= 1024 ? 4 : 3)
+#define PT_SHADE_WPE 4
 #endif
 #define PT_SHADE_WAVES __attribute__((amdgpu_waves_per_eu(PT_SHADE_WPE, PT_SHADE_WPE)))
 __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderParams R, PathSoA cur, const uint32_t* __restrict__ nptr,
