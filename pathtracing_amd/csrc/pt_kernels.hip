@@ -1086,6 +1086,58 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
     flags = depth | (rr << PF_RR_SHIFT) | (spec ? PF_SPEC : 0u);
 }
 
+// k_shade's block-wide bookkeeping in one step: the finished paths' camera
+// sample claim (their rank among the block's finished lanes, as
+// claim_camera_sample numbers them) and the three queue appends share one
+// count / atomics / barrier round instead of two.  The claimed ids below the
+// chunk's end are the first ranks, so the block books min(claimed, left) new
+// paths right after its claim returns.  Off: measured equal (C4 2009.8 /
+// 2013.5 vs 2016.2 / 2012.6 Mrays/s, profiles/r05_ab_shade_block.txt).
+#ifndef PT_SHADE_ONE_STEP
+#define PT_SHADE_ONE_STEP 0
+#endif
+__device__ __forceinline__ NewSample shade_slots(const RenderParams& R, bool done, bool cont, bool shadow,
+                                                 unsigned long long* __restrict__ next_sample,
+                                                 uint32_t* __restrict__ cnt, uint32_t (&at)[3]) {
+    constexpr int NW = PT_SHADE_BLOCK / 64;
+    __shared__ uint32_t s_c[3][NW + 1];
+    __shared__ unsigned long long s_base;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint64_t m[3] = {__ballot(done), __ballot(cont), __ballot(shadow)};
+    if (__lane_id() == 0) {
+#pragma unroll
+        for (int q = 0; q < 3; q++) s_c[q][wave] = (uint32_t)__popcll(m[q]);
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const int q = threadIdx.x;
+        uint32_t tot = 0;
+        for (int w = 0; w < NW; w++) {
+            const uint32_t c = s_c[q][w];
+            s_c[q][w] = tot;
+            tot += c;
+        }
+        if (q == 0) {  // sample ids for the finished paths, then the new paths among them
+            const unsigned long long base = tot ? atomicAdd(next_sample, (unsigned long long)tot) : 0ull;
+            const unsigned long long left = base < R.chunk_total ? R.chunk_total - base : 0ull;
+            const uint32_t nn = (uint32_t)min((unsigned long long)tot, left);
+            s_base = base;
+            s_c[0][NW] = nn ? atomicAdd(&cnt[Q_NEW], nn) : 0u;
+        } else {
+            s_c[q][NW] = tot ? atomicAdd(&cnt[q == 1 ? Q_NEXT : Q_SHADOW], tot) : 0u;
+        }
+    }
+    __syncthreads();
+    const uint32_t r0 = s_c[0][wave] + lanemask_lt_count(m[0]);
+    const unsigned long long g = s_base + r0;
+    at[0] = s_c[1][NW] + s_c[1][wave] + lanemask_lt_count(m[1]);
+    at[1] = s_c[2][NW] + s_c[2][wave] + lanemask_lt_count(m[2]);
+    at[2] = s_c[0][NW] + r0;
+    NewSample ns{done && g < R.chunk_total, (uint32_t)g, 0u, F3(0, 0, 0), F3(0, 0, 0), 0.0f};
+    if (ns.enq) camera_sample(R, ns);
+    return ns;
+}
+
 template <int INTEGRATOR>
 #ifndef PT_SHADE_WPE  // waves-per-SIMD budget for k_shade (pt_kernels.h PT_SHADE_BLOCK)
 #define PT_SHADE_WPE 4
@@ -1130,11 +1182,15 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
         o[1] = out.y;
         o[2] = out.z;
     }
+    uint32_t at[3];
+#if PT_SHADE_ONE_STEP
+    const NewSample ns = shade_slots(R, done, cont, shadow, next_sample, cnt, at);
+#else
     const NewSample ns = claim_camera_sample(R, done, next_sample);
     const int qoff[3] = {Q_NEXT, Q_SHADOW, Q_NEW};
     const bool pred[3] = {cont, shadow, ns.enq};
-    uint32_t at[3];
     block_append<3, PT_SHADE_BLOCK>(cnt, qoff, pred, at);
+#endif
     const uint32_t a = cont ? at[0] : next.cap - 1u - at[2], c = at[1];
     if (cont) {
         next.o[a] = make_float4(ro.x, ro.y, ro.z, __uint_as_float(key));

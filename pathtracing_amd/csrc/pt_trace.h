@@ -15,7 +15,9 @@
 #include "pt_shading.h"
 
 #define PT_STACK 32
+#ifndef PT_TRACE_BLOCK
 #define PT_TRACE_BLOCK 128
+#endif
 
 struct TraceWork {
     uint32_t nodes, tris;
