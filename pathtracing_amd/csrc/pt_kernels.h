@@ -227,7 +227,7 @@ enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1, PT_SORT_RAYS = 2 };
 #define PT_SHADE_BLOCK 256
 #endif
 #ifndef PT_SORT_PER
-#define PT_SORT_PER 32u  // paths per thread of k_sort_count / k_sort_scatter (16: -0.07 %, profiles/r05_ab_ties_sort.txt)
+#define PT_SORT_PER 64u  // paths per thread of k_sort_count / k_sort_scatter (16: -0.07 %, 32: -0.3 %; profiles/r05_ab_ties_sort.txt)
 #endif
 template <int KEY, int NB>
 __global__ void k_sort_count(PathSoA cur, const uint32_t* nptr, const float4* hit, uint32_t* counts, uint16_t* bins);
