@@ -751,48 +751,53 @@ static v3 normalize4(v3 v) {
     const float d = fmaf(v.y, v.y, rmul(v.x, v.x)) + rmul(v.z, v.z); /* fixture search */
     return muls(v, 1.0f / sqrtf(d));
 }
-/* glm::inverse(mat4) (glm/detail/func_matrix.inl compute_inverse<4,4>),
- * each operation rounded: used on translations only, whose cofactor products
- * are all exact (one translation component times ones and zeros), so any
- * contraction of the reference build rounds them alike, zero signs included */
-static void mat4_inverse_(const float* mm, float* out) {
-#define M(c, r) mm[(c) * 4 + (r)]
-#define D2(a, b, c, d) (rmul(a, b) - rmul(c, d))
-    const float C00 = D2(M(2, 2), M(3, 3), M(3, 2), M(2, 3)), C02 = D2(M(1, 2), M(3, 3), M(3, 2), M(1, 3));
-    const float C03 = D2(M(1, 2), M(2, 3), M(2, 2), M(1, 3)), C04 = D2(M(2, 1), M(3, 3), M(3, 1), M(2, 3));
-    const float C06 = D2(M(1, 1), M(3, 3), M(3, 1), M(1, 3)), C07 = D2(M(1, 1), M(2, 3), M(2, 1), M(1, 3));
-    const float C08 = D2(M(2, 1), M(3, 2), M(3, 1), M(2, 2)), C10 = D2(M(1, 1), M(3, 2), M(3, 1), M(1, 2));
-    const float C11 = D2(M(1, 1), M(2, 2), M(2, 1), M(1, 2)), C12 = D2(M(2, 0), M(3, 3), M(3, 0), M(2, 3));
-    const float C14 = D2(M(1, 0), M(3, 3), M(3, 0), M(1, 3)), C15 = D2(M(1, 0), M(2, 3), M(2, 0), M(1, 3));
-    const float C16 = D2(M(2, 0), M(3, 2), M(3, 0), M(2, 2)), C18 = D2(M(1, 0), M(3, 2), M(3, 0), M(1, 2));
-    const float C19 = D2(M(1, 0), M(2, 2), M(2, 0), M(1, 2)), C20 = D2(M(2, 0), M(3, 1), M(3, 0), M(2, 1));
-    const float C22 = D2(M(1, 0), M(3, 1), M(3, 0), M(1, 1)), C23 = D2(M(1, 0), M(2, 1), M(2, 0), M(1, 1));
-    const float F[6][4] = {{C00, C00, C02, C03}, {C04, C04, C06, C07}, {C08, C08, C10, C11},
-                           {C12, C12, C14, C15}, {C16, C16, C18, C19}, {C20, C20, C22, C23}};
-    float Vv[4][4];
-    for (int k = 0; k < 4; k++) {
-        Vv[k][0] = M(1, k);
-        Vv[k][1] = Vv[k][2] = Vv[k][3] = M(0, k);
-    }
-    /* Inv_i = (Va * Fa - Vb * Fb) + Vc * Fc, lane by lane */
-    static const int comb[4][6] = {{1, 0, 2, 1, 3, 2}, {0, 0, 2, 3, 3, 4}, {0, 1, 1, 3, 3, 5}, {0, 2, 1, 4, 2, 5}};
-    float inv[4][4];
-    for (int i = 0; i < 4; i++) {
-        const int* c = comb[i];
-        const float sg = (i & 1) ? -1.0f : 1.0f; /* SignA = (+,-,+,-), SignB = -SignA */
-        for (int k = 0; k < 4; k++) {
-            const float v = (rmul(Vv[c[0]][k], F[c[1]][k]) - rmul(Vv[c[2]][k], F[c[3]][k])) + rmul(Vv[c[4]][k], F[c[5]][k]);
-            inv[i][k] = v * ((k & 1) ? -sg : sg);
-        }
-    }
-    float d0[4];
-    for (int k = 0; k < 4; k++) d0[k] = rmul(M(0, k), inv[k][0]);
-    const float od = 1.0f / ((d0[0] + d0[1]) + (d0[2] + d0[3]));
-    for (int c = 0; c < 4; c++)
-        for (int r = 0; r < 4; r++) out[c * 4 + r] = inv[c][r] * od;
-#undef M
-#undef D2
+/* glm::inverse(mat4) (glm/detail/func_matrix.inl compute_inverse<4,4>) as
+ * the reference build (g++ -O3 -march=native) contracts it: the cofactors a
+ * fused first product minus a rounded second, each lane a rounded first
+ * product with the other two fused in turn, the negated lanes negated after,
+ * the determinant's pairs fused once (GCC's GIMPLE of that function; the
+ * host's pt_mat4_inverse is the same).  Exported as oracle_mat4_inverse for
+ * tests/test_mat4_inverse.py, which checks it against the reference build's
+ * own glm. */
+static inline float fms_(float a, float b, float c) { return fmaf(a, b, -c); }
+static inline float inv_lane(float va, float fa, float vb, float fb, float vc, float fc) {
+    return fmaf(vc, fc, fmaf(-vb, fb, rmul(va, fa)));
 }
+static void mat4_inverse_(const float* mm, float* out) {
+    const float m00 = mm[0], m01 = mm[1], m02 = mm[2], m03 = mm[3];
+    const float m10 = mm[4], m11 = mm[5], m12 = mm[6], m13 = mm[7];
+    const float m20 = mm[8], m21 = mm[9], m22 = mm[10], m23 = mm[11];
+    const float m30 = mm[12], m31 = mm[13], m32 = mm[14], m33 = mm[15];
+    const float C00 = fms_(m22, m33, rmul(m32, m23)), C02 = fms_(m33, m12, rmul(m32, m13));
+    const float C03 = fms_(m23, m12, rmul(m22, m13)), C04 = fms_(m33, m21, rmul(m23, m31));
+    const float C06 = fms_(m33, m11, rmul(m13, m31)), C07 = fms_(m23, m11, rmul(m13, m21));
+    const float C08 = fms_(m32, m21, rmul(m22, m31)), C10 = fms_(m32, m11, rmul(m12, m31));
+    const float C11 = fms_(m22, m11, rmul(m12, m21)), C12 = fms_(m33, m20, rmul(m23, m30));
+    const float C14 = fms_(m33, m10, rmul(m13, m30)), C15 = fms_(m23, m10, rmul(m13, m20));
+    const float C16 = fms_(m32, m20, rmul(m22, m30)), C18 = fms_(m32, m10, rmul(m12, m30));
+    const float C19 = fms_(m22, m10, rmul(m12, m20)), C20 = fms_(m31, m20, rmul(m21, m30));
+    const float C22 = fms_(m31, m10, rmul(m11, m30)), C23 = fms_(m21, m10, rmul(m11, m20));
+    float I[16];
+    I[0] = inv_lane(m11, C00, m12, C04, m13, C08);
+    I[1] = -inv_lane(m01, C00, m02, C04, m03, C08);
+    I[2] = inv_lane(m01, C02, m02, C06, m03, C10);
+    I[3] = -inv_lane(m01, C03, m02, C07, m03, C11);
+    I[4] = -inv_lane(m10, C00, m12, C12, m13, C16);
+    I[5] = inv_lane(m00, C00, m02, C12, m03, C16);
+    I[6] = -inv_lane(m00, C02, m02, C14, m03, C18);
+    I[7] = inv_lane(m00, C03, m02, C15, m03, C19);
+    I[8] = inv_lane(m10, C04, m11, C12, m13, C20);
+    I[9] = -inv_lane(m00, C04, m01, C12, m03, C20);
+    I[10] = inv_lane(m00, C06, m01, C14, m03, C22);
+    I[11] = -inv_lane(m00, C07, m01, C15, m03, C23);
+    I[12] = -inv_lane(m10, C08, m11, C16, m12, C20);
+    I[13] = inv_lane(m00, C08, m01, C16, m02, C20);
+    I[14] = -inv_lane(m00, C10, m01, C18, m02, C22);
+    I[15] = inv_lane(m00, C11, m01, C19, m02, C23);
+    const float od = 1.0f / (fmaf(m01, I[4], rmul(m00, I[0])) + fmaf(m03, I[12], rmul(m02, I[8])));
+    for (int k = 0; k < 16; k++) out[k] = rmul(I[k], od);
+}
+void oracle_mat4_inverse(const float* m, float* out) { mat4_inverse_(m, out); }
 
 /* AnimatedPrimitive / AnimatedLight at a ray's time (Primitive.cpp:82-89,
  * Light.cpp:341-356): TransformedPrimitive / TransformedLight over

@@ -70,6 +70,9 @@ int oracle_resolve(const double* film, int W, int H, int tonemap, uint8_t* out);
 /* Filter weight table (33x33 grid on [-2,2]^2 + integral), as ref_harness cmd_film. */
 int oracle_filter_table(const pt_render_desc* rd, double* out);
 
+/* glm::inverse(mat4) as the reference build contracts it (tests/test_mat4_inverse.py) */
+void oracle_mat4_inverse(const float* m, float* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1203,24 +1203,29 @@ __device__ __forceinline__ void anim_transform(const DevInstance& I, float time,
 #pragma unroll
     for (int k = 0; k < 3; k++) T[12 + k] = rmul(I.mdir[k], t) + 0.0f;
 }
-// glm::inverse of anim_transform's matrix.  Every cofactor product of the
-// general formula (compute_inverse<4,4>) is a translation component times a
-// one or a zero, the determinant is 1, and v is finite and never -0, so the
-// formula reduces exactly to constants and -v -- zero signs included: the
-// upper 3x4 block keeps the formula's signed zeros, and column 3's y entry is
-// 0 - v.y (+0 for v.y = +0) where x and z are -v (-0).  Checked against the
-// general formula over 2e7 random bit patterns (tests/test_anim_inverse.py
-// keeps that check); the oracle keeps the general formula,
-// so the motion parity scenes check it on the device.  As a closed form it
-// needs no cofactor registers in the traversal's instance step.
+// glm::inverse of anim_transform's matrix as the reference build computes it
+// (AnimatedPrimitive::Intersect builds a TransformedPrimitive, whose ctor
+// calls glm::inverse, Primitive.hpp:37), in closed form: compute_inverse<4,4>
+// with g++'s contractions (pt_bvh.cpp pt_mat4_inverse; the oracle's
+// mat4_inverse_) on identity + translation t (finite, never -0) gives 1 on the
+// diagonal, -t in column 3 and zeros whose signs follow t's signs through the
+// fused cofactors.  The rules below were read off that formula and checked
+// against it on 60 000 translations from 1e-40 to 1e38 of every sign pattern;
+// the motion parity scenes pin them against the reference harness.  As a
+// closed form it needs no cofactor registers in the traversal's instance step.
 __device__ __forceinline__ void anim_inverse(const float* T, float* out) {
+    const float tx = T[12], ty = T[13], tz = T[14];
     constexpr float z = 0.0f, nz = -0.0f;
-    const float c[12] = {1.0f, nz, z, nz, nz, 1.0f, nz, z, z, nz, 1.0f, nz};
-#pragma unroll
-    for (int k = 0; k < 12; k++) out[k] = c[k];
-    out[12] = -T[12];
-    out[13] = 0.0f - T[13];
-    out[14] = -T[14];
+    out[0] = 1.0f, out[2] = z, out[3] = nz;
+    out[5] = 1.0f, out[7] = z;
+    out[8] = z, out[10] = 1.0f, out[11] = nz;
+    out[1] = (ty > 0.0f || (ty == 0.0f && tz < 0.0f)) ? z : nz;
+    out[4] = (tx > 0.0f || (tx == 0.0f && tz < 0.0f)) ? z : nz;
+    out[6] = (tz < 0.0f && tx >= 0.0f) ? z : nz;
+    out[9] = (ty < 0.0f && tx >= 0.0f) ? z : nz;
+    out[12] = tx != 0.0f ? -tx : ((ty < 0.0f || (ty > 0.0f && tz >= 0.0f)) ? z : nz);
+    out[13] = 0.0f - ty;
+    out[14] = tz != 0.0f ? -tz : ((tx > 0.0f || (tx == 0.0f && ty < 0.0f)) ? z : nz);
     out[15] = 1.0f;
 }
 // An instance's transform and inverse at a ray's time: the uploaded pair, or

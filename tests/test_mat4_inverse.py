@@ -26,3 +26,24 @@ def test_mat4_inverse_fixture_kinds(k):
     assert np.isfinite(fx["inv"][k]).all()
     if k < 4500:
         np.testing.assert_array_equal(m[:, 3][:3], 0)  # affine: glm column-major, row 3 = (0, 0, 0, 1)
+
+
+def test_oracle_and_device_inverse_formula_bit_exact_vs_reference_glm():
+    """The oracle's mat4_inverse_ -- the operations the device's anim_inverse
+    (pt_shading.h) runs for an AnimatedPrimitive at each ray's time -- against
+    the reference build's own glm::inverse on all 6000 fixture matrices,
+    pure translations included (their zero signs follow the contractions)."""
+    import ctypes as C
+    import sys
+    sys.path.insert(0, str(GOLDEN.parents[1] / "oracle"))
+    import oracle
+    L = oracle.lib()
+    L.oracle_mat4_inverse.argtypes = [C.c_void_p, C.c_void_p]
+    L.oracle_mat4_inverse.restype = None
+    fx = np.load(GOLDEN / "mat4_inverse.npz", allow_pickle=False)
+    A, want = np.ascontiguousarray(fx["m"], np.float32), fx["inv"]
+    got = np.zeros_like(A)
+    for k in range(A.shape[0]):
+        L.oracle_mat4_inverse(A[k].ctypes.data, got[k].ctypes.data)
+    bad = np.nonzero((got.view(np.uint32) != want.view(np.uint32)).any(1))[0]
+    assert bad.size == 0, f"{bad.size} of {len(A)} matrices differ, first {bad[:8].tolist()}"
