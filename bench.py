@@ -311,29 +311,33 @@ def _load_hook(path: str):
 
 
 def _nonfinite_vs_oracle(setup, integ, film, frame_samples, sample_range, oracle, max_pixels: int = 64) -> dict:
-    """The film's non-finite pixels traced to their samples: the samples the
-    sample buffer still holds (its last chunk) of every pixel within the
-    filter radius of each non-finite pixel are read back; a non-finite one
-    must be non-finite in the same channels in the oracle's Li (the reference
-    itself produces it).  explained: every non-finite pixel (up to
-    max_pixels) has such a sample within its footprint."""
+    """The film's non-finite pixels traced to their samples.  Every sample of
+    every pixel within the filter radius of each non-finite pixel is read back
+    from the frame's sample buffer; each non-finite one must be non-finite in
+    the same channels (and equal in the others) in the oracle's Li -- the
+    reference itself produces it.  explained: the sample buffer holds the
+    whole frame (a multi-chunk frame keeps only its last chunk, so a NaN could
+    come from a sample no longer there: not explained), at most max_pixels
+    pixels are non-finite, every one of them has a non-finite sample in its
+    footprint, and every non-finite sample in every footprint is the oracle's."""
     import numpy as np
     W, H = setup.camera.GetFilm().Resolution()
     f = film.detach().cpu().numpy()
     bad = np.argwhere(~np.isfinite(f).all(-1))
     lo, hi = sample_range if sample_range is not None else (0, setup.spp - 1)
+    whole = lo == 0 and hi >= setup.spp - 1
     smp = np.arange(lo, hi + 1, dtype=np.uint32)
     rad = int(np.ceil(float(np.max(setup.camera.GetFilm().filter.radius)) - 0.5))
     checked, matched, seen, explained = 0, 0, {}, 0
     for y, x in bad[:max_pixels]:
-        hit = False
+        found, all_ok = False, True
         for yy in range(max(0, y - rad), min(H, y + rad + 1)):
             for xx in range(max(0, x - rad), min(W, x + rad + 1)):
                 p = yy * W + xx
                 if p not in seen:
                     L = np.asarray(frame_samples(np.full(smp.shape, p, np.uint32), smp), np.float32).reshape(-1, 3)
-                    nf = np.nonzero(~np.isfinite(L).all(1))[0][:4]
-                    ok_p = False
+                    nf = np.nonzero(~np.isfinite(L).all(1))[0]  # every non-finite sample of the pixel
+                    ok_p = True
                     if nf.size:
                         want, _ = oracle.li_pairs(integ, np.full(nf.size, p, np.uint32), smp[nf])
                         want = np.asarray(want, np.float32).reshape(-1, 3)
@@ -342,17 +346,18 @@ def _nonfinite_vs_oracle(setup, integ, film, frame_samples, sample_range, oracle
                         checked += int(nf.size)
                         matched += int(same.sum())
                         ok_p = bool(same.all())
-                    seen[p] = ok_p
-                hit = hit or seen[p]
-        explained += int(hit)
+                    seen[p] = (int(nf.size), ok_p)
+                found = found or seen[p][0] > 0
+                all_ok = all_ok and seen[p][1]
+        explained += int(found and all_ok)
     n = int(min(bad.shape[0], max_pixels))
     return {"pixels": int(bad.shape[0]), "pixels_checked": n, "pixels_explained": explained,
-            "samples_checked": checked, "samples_as_oracle": matched,
-            "explained": bool(n > 0 and explained == n and checked == matched)}
+            "samples_checked": checked, "samples_as_oracle": matched, "whole_frame_in_buffer": bool(whole),
+            "explained": bool(whole and 0 < bad.shape[0] <= max_pixels and explained == n and checked == matched)}
 
 
 def verify_frame(setup, integ, rank: int, world: int, pairs: int, frame_samples, film=None, seed: int = 0x5EED0B0C,
-                 sample_range=None):
+                 sample_range=None, overflows=None):
     """Untimed check of the frame just timed: per-sample Li of
     `pairs` (pixel, sample) pairs read back from the frame's own sample buffer
     (pt_frame_samples) must equal the oracle's Li bit for bit; half the pairs
@@ -361,7 +366,9 @@ def verify_frame(setup, integ, rank: int, world: int, pairs: int, frame_samples,
     finite with a positive filter weight on every pixel.  The oracle is the
     checker here, never the thing timed.  sample_range = (first, last): the
     frame samples the sample buffer still holds (its last chunk,
-    pt_frame_sample_range); the pairs are drawn from those."""
+    pt_frame_sample_range); the pairs are drawn from those.  overflows: the
+    timed steps' summed pt_stats stack_overflows / tie_overflows, both 0 for
+    a frame whose traversal dropped nothing."""
     import numpy as np
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle
@@ -388,6 +395,9 @@ def verify_frame(setup, integ, rank: int, world: int, pairs: int, frame_samples,
                     "mismatches": [{"pixel": int(pix[k]), "sample": int(smp[k]), "got": got[k].tolist(),
                                     "want": want[k].tolist()} for k in bad[:4]]})
     ok = out["pairs"] == out["bit_exact"]
+    if overflows is not None:
+        out.update({k: int(v) for k, v in overflows.items()})
+        ok = ok and not any(overflows.values())
     if film is not None:
         import torch
         out["film_finite"] = bool(torch.isfinite(film).all().item())
@@ -402,8 +412,9 @@ def verify_frame(setup, integ, rank: int, world: int, pairs: int, frame_samples,
         ok = ok and film_ok and out["film_weight_positive"]
     out["ok"] = bool(ok)
     out["method"] = ("per-sample Li of the timed frame (pt_frame_samples) vs the oracle, bit-exact; "
-                     "film finite with sum w > 0 on every pixel, a non-finite pixel only where the oracle's "
-                     "Li of a sample in its footprint is non-finite too")
+                     "no traversal stack push or exact-tie entry dropped in the timed steps; "
+                     "film finite with sum w > 0 on every pixel, a non-finite pixel only where every "
+                     "non-finite sample in its footprint is the oracle's too")
     return out
 
 
@@ -554,7 +565,7 @@ def main():
         dist.barrier()
     t0 = time.perf_counter()
     totals = {"rays_closest": 0, "rays_any": 0, "ms_closest": 0.0, "ms_any": 0.0, "ms_shade": 0.0,
-              "launches_closest": 0, "launches_any": 0, "paths": 0}
+              "launches_closest": 0, "launches_any": 0, "paths": 0, "stack_overflows": 0, "tie_overflows": 0}
     for i in range(args.steps):
         ts = time.perf_counter()
         st = step(N.PT_RENDER_TIMING)
@@ -587,7 +598,9 @@ def main():
             srange = ctx.frame_sample_range() if hasattr(ctx._lib, "pt_frame_sample_range") else None
         sh_i, sh_n = shard if shard else (rank, world)
         verified = verify_frame(setup, integ, sh_i, sh_n, args.verify_pairs if fs else 0, fs,
-                                film if rank == 0 and not shard else None, sample_range=srange)
+                                film if rank == 0 and not shard else None, sample_range=srange,
+                                overflows=None if cpu_run else {k: totals[k] for k in ("stack_overflows",
+                                                                                       "tie_overflows")})
         if world > 1:
             ok = torch.tensor([1 if verified["ok"] else 0, verified["pairs"], verified["bit_exact"]],
                               dtype=torch.int64, device=dev)

@@ -25,7 +25,8 @@
 extern "C" {
 #endif
 
-#define PT_API_VERSION 7
+/* v8: pt_stats.tie_overflows (was padding), pt_anim_inverse_cases */
+#define PT_API_VERSION 8
 
 typedef int32_t pt_status;
 #define PT_OK 0
@@ -334,7 +335,10 @@ typedef struct pt_stats {
     uint64_t stack_overflows;  /* traversal stack pushes beyond the stack's
                                   capacity (dropped; the test suite asserts 0) */
     uint32_t n_devices;        /* devices that rendered                         */
-    uint32_t pad;
+    uint32_t tie_overflows;    /* exact-t tie re-trace list entries dropped past
+                                  its capacity (a dropped tie could change which
+                                  primitive wins, Shape.cpp:204; the test suite
+                                  and bench's frame check assert 0)            */
 } pt_stats;
 
 /* Rays for the pt_trace test hook (Scene::Intersect / IntersectPred). */
@@ -446,6 +450,13 @@ pt_status pt_light_cases(pt_ctx* ctx, const float* cases, uint32_t n, float* out
  * the picked light's index into pt_scene_desc.lights, -1 when the sampler
  * is empty.  Host pointers. */
 pt_status pt_light_picks(pt_ctx* ctx, const float* u, uint32_t n, int32_t* out);
+/* Test hook: the device's inverse of an AnimatedPrimitive's matrix at a ray's
+ * time (AnimatedPrimitive::Intersect -> TransformedPrimitive's ctor ->
+ * glm::inverse, Primitive.cpp:82-89, Primitive.hpp:37), for n translations
+ * (3 floats each; the matrix is identity + that translation, as the device
+ * builds it: components never -0) -> n glm column-major 4x4 matrices (16
+ * floats).  Host pointers.  Needs a context, not a scene. */
+pt_status pt_anim_inverse_cases(pt_ctx* ctx, const float* translations, uint32_t n, float* out);
 /* Film resolve (Film::WritePNG / WritePPM, Film.hpp:154-217): per pixel
  * color = sum RGB*w / sum w, the tone mapper (through the writers'
  * std::function<vec3(vec3)>, i.e. in float around a double body),

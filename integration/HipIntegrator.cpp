@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -734,12 +735,23 @@ pt_camera_desc camera_desc(const Camera& cam, const Flat& flat) {
     c.defocus_radius = PT_GET(cam, CamDefocus);
     c.focus_distance = PT_GET(cam, CamFocusDist);
     c.focus_angle = PT_GET(cam, CamFocusAngle);
-    // rays carry time = glm::mix(shutterStart, shutterEnd, u) (Camera.hpp:25)
-    // for every camera, as the reference's Render does: the bounds of a camera
-    // built without a shutter are whatever its ctor left
-    c.has_shutter = 1;
-    c.shutter[0] = PT_GET(cam, CamShutterStart);
-    c.shutter[1] = PT_GET(cam, CamShutterEnd);
+    // rays carry time = glm::mix(shutterStart, shutterEnd, u) (Camera.hpp:25).
+    // Only the shutter ctor (Camera.hpp:16-19) sets those bounds; the others
+    // leave them uninitialised, and a ray's time matters only to
+    // AnimatedPrimitive / AnimatedLight.  So a scene without them renders at
+    // time 0, whatever the camera (the same images: no primitive or light
+    // depends on it; the Python front end does the same), and a scene with
+    // them takes the camera's bounds, which must then be finite.
+    bool motion = false;
+    for (const pt_instance& r : flat.instances) motion = motion || r.animated;
+    c.has_shutter = motion ? 1 : 0;
+    if (motion) {
+        c.shutter[0] = PT_GET(cam, CamShutterStart);
+        c.shutter[1] = PT_GET(cam, CamShutterEnd);
+        if (!std::isfinite(c.shutter[0]) || !std::isfinite(c.shutter[1]))
+            throw std::runtime_error("HipIntegrator: a scene with an AnimatedPrimitive needs a camera built with "
+                                     "shutter bounds (Camera.hpp:16-19)");
+    }
     glm::ivec2 res = cam.GetFilm()->Resolution();
     c.width = res.x;
     c.height = res.y;

@@ -18,9 +18,9 @@
 // child order (BVH.hpp:562-738) precomputed per node.  128 bytes, 128-aligned.
 #define REF_EMPTY 0xFFFFFFFFu
 #define REF_LEAF 0x80000000u
-// Quantized-node leaf refs only (DevQNode::child): the leaf holds a BLAS hop,
-// whose test pushes a traversal, so the overlapped traversal (pt_pool.h
-// PT_SPEC) pauses its node side until the leaf is done.  Slots < 2^29.
+// Quantized-record leaf refs only: the leaf holds a BLAS hop, whose test
+// pushes a traversal, so the overlapped traversal (pt_pool.h trace_spec)
+// pauses its node side until the leaf is done.  Slots < 2^29.
 #define REF_BLOCK 0x20000000u
 struct alignas(128) DevCluster {
     float4 xmin, xmax, ymin, ymax, zmin, zmax;  // 4 children per component
@@ -30,7 +30,8 @@ struct alignas(128) DevCluster {
 };
 static_assert(sizeof(DevCluster) == 128, "cluster layout");
 
-// ---- quantized BVH4 node (64 B, 64-aligned): the same cluster with its four
+// ---- quantized BVH4 node (the upload's intermediate form of a 48-B node
+// record below): the same cluster with its four
 // child boxes stored as 8-bit offsets from a per-node origin in power-of-two
 // steps per axis (scale 2^(e-127)).  Encoded on the host so that every
 // decoded bound fma(q, scale, origin) lies outside the reference's float
@@ -49,7 +50,7 @@ struct alignas(64) DevQNode {
 };
 static_assert(sizeof(DevQNode) == 64, "qnode layout");
 
-// ---- unified 48-B records (PT_Q48, the default quantized form): node records
+// ---- unified 48-B records (the quantized node form): node records
 // and the primitive slots of their leaf children in ONE array, each cluster's
 // children in one contiguous block (inner children 1 record, a leaf child its
 // primitives' slots), so a node names its children with one base and four
@@ -63,38 +64,11 @@ static_assert(sizeof(DevQNode) == 64, "qnode layout");
 //              from base | 0x40 leaf | 0x80 leaf holding a BLAS hop
 //   primitive: the slot's DevGeom with c.w = the slot (hits and the shading
 //              tables stay indexed by slot)
-#ifndef PT_Q48
-#define PT_Q48 1
-#endif
 #define Q48_EMPTY 0xFFu
 #define Q48_LEAF 0x40u
 #define Q48_HOP 0x80u
 #define Q48_MAX_OFFSET 62u
 #define Q48_LUT_STRIDE 136  // bytes per octant row of the LDS order table (135 perms)
-
-// ---- wide node (PT_WIDE, 128 B, one line): cluster i with its largest
-// inner children absorbed (greedily by surface area while at most 8 slots
-// remain), so one step tests the children and the absorbed children's
-// children.  Index-aligned with the clusters (wnodes[i] stands for cluster
-// i; absorbed clusters' own records go unused).  Boxes quantized as DevQNode
-// with one origin / step per axis over the slots; the visit order per
-// octant is the reference's depth-first order (a cluster's LUT order with
-// each absorbed child replaced by its own LUT order): 8 x 3-bit slot indices,
-// first pushed (farthest) in the low bits.
-//   a = origin.xyz, exponents (x | y << 8 | z << 16)
-//   b0 = x lo, x hi, y lo, y hi of slots 0-3 (one byte per slot); b1 = slots 4-7
-//   z = z lo 0-3, z hi 0-3, z lo 4-7, z hi 4-7
-//   child[8] = REF_EMPTY | REF_LEAF|slot | cluster;  order[8] = octant 0..7
-struct alignas(128) DevWNode {
-    float4 a;
-    uint32_t b0[4], b1[4], z[4];
-    uint32_t child[8];
-    uint32_t order[8];
-};
-static_assert(sizeof(DevWNode) == 128, "wnode layout");
-#ifndef PT_WIDE
-#define PT_WIDE 0
-#endif
 
 // ---- primitive slot geometry (48 B): what a leaf test reads.
 // a = v0|Q|center + flags, b = e1|u|radius + index, c = e2|v
@@ -128,22 +102,6 @@ struct alignas(16) DevAlpha {
     float cut, scale;
 };
 static_assert(sizeof(DevAlpha) == 48, "alpha record layout");
-// ---- texture records for the shading path: a texture with its image's
-// fields in one 32-B record (Texture::Evaluate reads the texture, then its
-// image, then texels: one dependent read fewer)
-//   kfc = kind | image format << 8 | image channels << 16;  scale = colorScale
-//   u   SOLID: value[3];  CHECKER: a, b, inv_scale[2] (as bits);
-//       IMAGE: offset lo, hi, width, height
-struct alignas(16) DevTex {
-    uint32_t kfc;
-    float scale[3];
-    uint32_t u[4];
-};
-static_assert(sizeof(DevTex) == 32, "texture record layout");
-#ifndef PT_ALPHA_RECORDS
-#define PT_ALPHA_RECORDS 1
-#endif
-
 // Instances (TransformedPrimitive, Primitive.cpp:32-72).  A TLAS leaf slot of
 // an instance is encoded like a BLAS hop whose pushed ref is
 // REF_INST_ENTER | slot; popping it takes the lane's ray to object space
@@ -158,7 +116,7 @@ static_assert(sizeof(DevTex) == 32, "texture record layout");
 #define OCT_INST 8u   // the lane's ray is in an instance's object space
 #define OCT_HIT 16u   // ... and accepted a hit there
 #define OCT_FOUND 32u // overlapped traversal (pt_pool.h trace_spec): a hit was stored
-#define OCT_FRESH 128u // overlapped traversal with PT_PRECLAIM: the ray was claimed this iteration (set up after the loads)
+#define OCT_FRESH 128u // overlapped traversal: the ray was claimed this iteration (set up after the loads)
 #define OCT_TIE 64u   // pool traversal: this ray met a hit at exactly t == max (listed once for the exact re-trace)
 #define OCT_SP_SHIFT 8  // ... entered at this stack depth (bits 8-13)
 // scratch row: world o, d, tmax, the outermost level's length, instance, the
@@ -167,7 +125,7 @@ static_assert(sizeof(DevTex) == 32, "texture record layout");
 struct DevInstance {
     float T[16], inv[16];  // glm column-major transform and inverse
     uint32_t root;         // BLAS root ref
-    uint32_t qroot;        // ... in the PT_Q48 records
+    uint32_t qroot;        // ... in the quantized records
     uint32_t prim_base;    // first slot of the BLAS
     uint32_t n_prims;
     uint32_t virt_base;    // virtual slot of the BLAS's first primitive
@@ -204,17 +162,14 @@ struct DevPrimInfo {
 
 struct DevScene {
     float bb_lo[3], bb_scale[3];  // scene box: lo and 16 / extent per axis (spatial hit sort)
-    const uint16_t* prim_cell;    // PT_SORT_PRIM_CELL: each primitive slot's centroid cell (spatial hit sort), else null
+    const uint16_t* prim_cell;    // each primitive slot's centroid cell (spatial hit sort), else null
     const uint32_t* ray_order;    // closest-hit claim order (PT_RENDER_SORT_RAYS), else null
-    uint16_t* hit_bins;           // the pool kernels write each closest hit's spatial sort bin here, else null
     const DevCluster* nodes;
-    const DevQNode* qnodes;    // the same nodes quantized (null: the scene could not be encoded);
-                               // PT_WIDE: DevWNode records (reinterpreted)
     const DevGeom* geom;
     const DevPrimInfo* info;
-    const DevGeom* qrec;       // PT_Q48 records (null: the scene could not be encoded)
+    const DevGeom* qrec;       // the quantized records (null: the scene could not be encoded)
     const uint32_t* qlut;      // BVH4::LUT as 8 rows of Q48_LUT_STRIDE bytes (staged into LDS)
-    uint32_t qrec_bytes;       // bytes of qrec (< 2^32 - 256; PT_BUFFER_LOADS addresses it with 32-bit offsets)
+    uint32_t qrec_bytes;       // bytes of qrec (< 2^32 - 256: the traversal's buffer loads address it with 32-bit offsets)
     uint32_t qroot;            // TLAS root in the records
     uint32_t root;
     uint32_t n_prims;
@@ -231,7 +186,6 @@ struct DevScene {
     const pt_material* materials;
     const pt_texture* textures;
     const pt_image* images;
-    const DevTex* texrec;      // DevTex per texture (the shading path's reads)
     const uint8_t* texels;
     uint64_t n_texel_bytes;
     const pt_light* lights;
@@ -258,16 +212,9 @@ struct DevScene {
     uint32_t* scratch;       // SCR_WORDS x scratch_lanes (instance traversal state)
     uint32_t scratch_lanes;
     uint32_t* stack_drops;   // traversal pushes past the stack capacity (counted, rare)
+    uint32_t* tie_drops;     // exact-tie list entries past its capacity (counted; none expected)
     uint32_t n_materials, n_textures, n_images;
-    uint32_t lds_tables;     // PT_LDS_TABLES: which tables the shading kernels stage (LDS_* bits)
 };
-enum { LDS_MATS = 1u, LDS_TEX = 2u, LDS_IMG = 4u, LDS_LS = 8u };
-// Caps of the shading kernels' LDS copies (PT_LDS_TABLES): 48-B materials and
-// textures, 24-B images, the light sampler's guide table and running sums
-#define PT_LDS_MATS 128
-#define PT_LDS_TEX 128
-#define PT_LDS_IMG 128
-#define PT_LDS_CDF 4096
 
 // The uploaded scene of the current context, in constant memory: every
 // device function reads it directly (no per-lane copy of the struct, and the

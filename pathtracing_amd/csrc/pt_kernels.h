@@ -46,26 +46,13 @@
 // Continuing paths fill entries [0, c) from the front and new camera paths
 // [cap - r, cap) from the back, so camera rays stay in coherent waves of their
 // own; path i of an iteration (i < c + r) lives at path_slot(i).
-// PT_PATH_AOS 1: the four float4 fields of a path are one 64-B record, so
-// the shading kernel's reads through the hit sort's permutation fetch one
-// 64-B sector per path instead of four (random 16-B reads fetch 64 B each:
-// profiles/r03_fetch_calib.json), but the sequential readers of the ray
-// alone (the traversal's claim, the hit sort's count) fetch 64 B for 32;
-// 2 (default): {o, d} and {beta, L} as two 32-B records -- the ray readers
-// read their 32 B, the shading two sectors per path; 0: one array per field.
-#ifndef PT_PATH_AOS
-#define PT_PATH_AOS 2
-#endif
-// PT_PATH_INV: the path state carries the ray's 1/d (PathSoA.inv), written by
-// the kernels that write the ray; the overlapped closest-hit traversal loads
-// it with the ray instead of dividing on its ray-setup path.  Off: the
-// traversal's loop loses 43 static VALU but not time (102.2 -> 102.3 ms per
-// launch), and the shading's extra 16-B writes cost more: C4 -0.4 %
-// (profiles/r05_ab_path_inv.txt)
-#ifndef PT_PATH_INV
-#define PT_PATH_INV 0
-#endif
-#define PT_PATH_STRIDE (PT_PATH_AOS == 1 ? 4u : PT_PATH_AOS == 2 ? 2u : 1u)
+// {o, d} and {beta, L} are two 32-B records per path: the ray's readers (the
+// traversal's claim) read their 32 B, the shading two sectors per path
+// (random 16-B reads fetch 64 B each: profiles/r03_fetch_calib.json).  One
+// 64-B record or one array per field measured slower
+// (profiles/r05_ab_path_aos.txt); so did 1/d carried with the ray (C4 -0.4 %,
+// profiles/r05_ab_path_inv.txt).
+#define PT_PATH_STRIDE 2u
 struct PField {  // one float4 field of the path state, indexed by entry
     float4* p;
     __device__ __forceinline__ float4& operator[](uint32_t e) const { return p[(size_t)e * PT_PATH_STRIDE]; }
@@ -79,8 +66,6 @@ struct PathSoA {
     uint32_t cap; // entries
     float* time;  // the path's ray time (Ray::time, constant along a path: every
                   // scatter copies it, Material.hpp:264 ...); only with S.motion
-    float4* inv;  // PT_PATH_INV: 1/d.xyz (the Ray ctor's invDir, Ray.hpp:32-35), written
-                  // with the ray, so the closest-hit pool kernel's ray setup loads it
 };
 __device__ __forceinline__ uint32_t path_count(const uint32_t* set) { return set[Q_NEXT] + set[Q_NEW]; }
 __device__ __forceinline__ uint32_t path_slot(uint32_t i, uint32_t c, uint32_t cap) {
@@ -106,13 +91,6 @@ struct ShadowRecV {
     float4 a;  // the path's attenuation, .w: light pdf
 };
 #define SHADOW_DONE_BIT 0x80000000u
-// ShadowRec::c.w of an unoccluded ray whose contribution k_shadow_apply adds
-// (PT_SHADOW_DEFER; the shading writes 0).  Off: C4 any-hit 1178 -> 1192 ms
-// per frame deferred, apply kernel included (profiles/r04_ab_traversal.txt)
-#define SHADOW_VISIBLE 1.0f
-#ifndef PT_SHADOW_DEFER
-#define PT_SHADOW_DEFER 0
-#endif
 // medium interaction: the medium's Le is added after SampleLd's value
 // (Integrators.cpp:356-357), occluded or not
 #define SHADOW_MLE_BIT 0x40000000u
@@ -187,28 +165,12 @@ enum { PT_SORT_MATERIAL = 0, PT_SORT_SPATIAL = 1, PT_SORT_RAYS = 2 };
 #define PT_SORT_CELL_BITS 4  // spatial sort: 2^bits cells per axis of the scene box
 #endif
 #define PT_SORT_BINS_SPATIAL (1 << (3 * PT_SORT_CELL_BITS))
-// Hit-state binning of a bounce's paths before shading: the spatial key
-// (default) is the hit primitive's centroid cell (PT_SORT_PRIM_CELL: a 2-B
-// table built at upload, so k_sort_count reads the hit record alone, 16 B per
-// path instead of the hit and the ray's 48: C4 +0.4 %,
-// profiles/r05_ab_prim_cell.txt); 0: the hit point's cell
-#ifndef PT_SORT_PRIM_CELL
-#define PT_SORT_PRIM_CELL 1
-#endif
-// spatial sort key: the hit primitive's slot range (leaf order) instead of
-// the hit point's Morton cell (reads the hit record only)
-#ifndef PT_SORT_BY_SLOT
-#define PT_SORT_BY_SLOT 0  // off: C4 -1.5 % (profiles/r04_ab_traversal.txt)
-#endif
-// PT_HIT_BINS: the closest-hit pool kernel writes each path's spatial sort
-// bin when its ray is done (ClosestSrc::done), k_sort_count reads 2 B per
-// path instead of 48.  Off: C4 k_sort_count 63.7 -> 27.9 ms per frame, but
-// k_closest_pool 2947 -> 3341 (the bin's code on the overlapped loop's
-// ray-done path, which a wave runs whenever one lane finishes; 3 -> 6 VGPR
-// spills): -6.5 % (profiles/r05_ab_hitbins.txt)
-#ifndef PT_HIT_BINS
-#define PT_HIT_BINS 0
-#endif
+// The spatial key is the hit primitive's centroid cell (a 2-B table built at
+// upload, so k_sort_count reads the hit record alone, 16 B per path instead of
+// the hit and the ray's 48: C4 +0.4 %, profiles/r05_ab_prim_cell.txt).  The
+// hit point's cell (the key of scenes without the table), the hit slot's leaf
+// range (-1.5 %, profiles/r04_ab_traversal.txt) and bins written by the
+// traversal (-6.5 %, profiles/r05_ab_hitbins.txt) measured slower.
 // blocks of the exact-tie re-trace (k_closest_ties, grid-stride over the
 // listed rays): with 64 (a quarter of the CUs) it took 0.66 ms per C4 launch
 #ifndef PT_TIE_BLOCKS
@@ -236,11 +198,8 @@ __global__ void k_sort_scan(uint32_t* counts);
 template <int KEY, int NB>
 __global__ void k_sort_scatter(PathSoA cur, const uint32_t* nptr, const float4* hit, uint32_t* offsets, uint32_t* order,
                                const uint16_t* bins);
-// k_sort_count keeps each path's bin for k_sort_scatter (2 B read instead of
+// (k_sort_count keeps each path's bin for k_sort_scatter: 2 B read instead of
 // the 48 B of path and hit records the bin is computed from)
-#ifndef PT_SORT_KEEP_BINS
-#define PT_SORT_KEEP_BINS 1
-#endif
 __global__ void k_adapt_init(RenderParams R, uint32_t shard_index, uint32_t shard_count, uint32_t* list,
                              uint32_t* cnt, AdaptEst* est, uint32_t* counts);
 __global__ void k_adapt_map(const uint32_t* list, const uint32_t* n, int32_t* map);
@@ -252,6 +211,7 @@ __global__ void k_interact(const pt_ray* rays, uint32_t n, float* out);
 __global__ void k_bsdf_cases(int mid, const float* in, uint32_t n, float* out);
 __global__ void k_light_cases(const float* in, uint32_t n, float* out);
 __global__ void k_light_picks(const float* u, uint32_t n, int32_t* out);
+__global__ void k_anim_inverse(const float* t, uint32_t n, float* out);
 template <bool QN>
 __global__ void k_trace_rays(const pt_ray* rays, uint32_t n, int any, pt_hit* out, uint32_t* pool, uint32_t* ovf,
                              unsigned long long* counters, uint32_t* ties, uint32_t* n_ties);

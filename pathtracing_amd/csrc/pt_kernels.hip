@@ -126,11 +126,8 @@ __device__ __noinline__ SurfXf chain_world_surface(const DevInstance* I, float t
     }
     return SurfXf{p, n, ns, tangent};
 }
-// defer_nm (PT_TEX_JOINT shading): a triangle's normal map is left to
-// mat_tex unless the hit is in an instance (whose transform follows it)
 __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, float b1, float b2, SurfInt& si,
-                                         int& medium, float time = 0.0f, bool defer_nm = false) {
-    si.nm_pending = false;
+                                         int& medium, float time = 0.0f) {
     float len = 1.0f;
     const DevInstance* I = nullptr;
     bool xf = false;  // the hit's levels go out of line (an AnimatedPrimitive, nested wrappers)
@@ -167,7 +164,7 @@ __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, flo
             sphere_root(S.spheres[pi.index], ro, rd, __int_as_float(0x7f800000), t);
         }
     }
-    if (kind == PT_PRIM_TRIANGLE) tri_interaction(g, pi.index, pi.material, ro, rd, t, b1, b2, si, !(defer_nm && !I));
+    if (kind == PT_PRIM_TRIANGLE) tri_interaction(g, pi.index, pi.material, ro, rd, t, b1, b2, si);
     else if (kind == PT_PRIM_QUAD) quad_interaction(S.quads[pi.index], ro, rd, t, b1, b2, si);
     else sphere_interaction(S.spheres[pi.index], ro, rd, t, si);
     si.mat = pi.material;
@@ -221,7 +218,7 @@ __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, flo
     __attribute__((amdgpu_waves_per_eu((SPEC_) ? PT_SPEC_SHADOW_WPE : PT_SHADOW_WPE, \
                                        (SPEC_) ? PT_SPEC_SHADOW_WPE : PT_SHADOW_WPE)))
 // which pool kernels take trace_spec (pt_pool.h trace_pool's dispatch)
-#define PT_USES_SPEC(INST_, QN_) (PT_SPEC && (QN_) && !(INST_) && !PT_ENTRY && !PT_WIDE)
+#define PT_USES_SPEC(INST_, QN_) ((QN_) && !(INST_))
 // The spatial hit sort's bin of a hit at o + t d: the Morton code of its
 // cell in a 2^PT_SORT_CELL_BITS grid over the scene box (0 for a miss too)
 __device__ __forceinline__ uint32_t hit_cell(f3 o, f3 d, float t) {
@@ -253,15 +250,6 @@ struct ClosestSrc {
         tmax = __int_as_float(0x7f800000);
         return true;
     }
-    static constexpr bool kInv = PT_PATH_INV;  // the ray's 1/d comes with it (PathSoA.inv)
-    __device__ __forceinline__ void load_inv(uint32_t i, f3& o, f3& d, f3& inv, float& tmax) {
-        const uint32_t j = S.ray_order ? S.ray_order[i] : i;
-        const uint32_t e = path_slot(j, front, P.cap);
-        o = xyz(P.o[e]);
-        d = xyz(P.d[e]);
-        inv = xyz(P.inv[e]);
-        tmax = __int_as_float(0x7f800000);
-    }
     __device__ __forceinline__ void closest(uint32_t i, float t, float b1, float b2, int prim) {
         hit[S.ray_order ? S.ray_order[i] : i] = make_float4(t, b1, b2, __int_as_float(prim));
     }
@@ -269,17 +257,14 @@ struct ClosestSrc {
         return P.time[path_slot(S.ray_order ? S.ray_order[i] : i, front, P.cap)];
     }
     __device__ __forceinline__ void any(uint32_t, bool) {}
-    // the ray is done (world o, d; t of its closest hit when found): its
-    // spatial sort bin, while the ray is still in registers, so the hit sort
-    // reads 2 B per path instead of the hit and the ray (48 B)
-    __device__ __forceinline__ void done(uint32_t i, f3 o, f3 d, float t, bool found) {
-        if (PT_HIT_BINS && S.hit_bins) S.hit_bins[S.ray_order ? S.ray_order[i] : i] = (uint16_t)(found ? hit_cell(o, d, t) : 0u);
-    }
     // the list holds P.cap entries (a ray is listed at most once per launch:
-    // OCT_TIE survives instance enter / exit); the bound keeps a miscount in bounds
+    // OCT_TIE survives instance enter / exit, so it cannot fill); an entry
+    // past it would be a dropped tie, which could change a hit
+    // (Shape.cpp:204): counted as pt_stats::tie_overflows, asserted 0
     __device__ __forceinline__ void tie(uint32_t i) {
         const uint32_t k = atomicAdd(n_ties, 1u);
         if (k < P.cap) ties[k] = i;
+        else atomicAdd(S.tie_drops, 1u);
     }
 };
 
@@ -289,17 +274,15 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_POOL_WAVES_FOR(PT_USES_SPEC(INST
                                                                 uint32_t* __restrict__ ovf, uint32_t* __restrict__ spare,
                                                                 uint32_t* __restrict__ snap,
                                                                 unsigned long long* counters, uint32_t* __restrict__ ties) {
-    __shared__ uint32_t s_ref[PT_POOL_LDS_C * PT_TRACE_BLOCK];
-    __shared__ uint16_t s_ent[PT_ENTRY ? PT_POOL_LDS_C * PT_TRACE_BLOCK : 1];
-    constexpr int TREE = PT_USES_SPEC(INST, QN) ? PT_TREELET : 0;
-    __shared__ __attribute__((aligned(16))) uint8_t s_lut[(QN && PT_Q48) ? Q48_LDS_BYTES(TREE) : 4];
+    __shared__ uint32_t s_ref[PT_POOL_LDS * PT_TRACE_BLOCK];
+    __shared__ __attribute__((aligned(16))) uint8_t s_lut[QN ? Q48_LUT_BYTES : 4];
     iteration_prologue(nptr, spare, snap);
     const uint32_t n = path_count(nptr);
     if (n == 0) return;
-    if constexpr (QN && PT_Q48) stage_q48_lut<TREE>(s_lut);
+    if constexpr (QN) stage_q48_lut(s_lut);
     TraceWork wk{0, 0};
     ClosestSrc src{P, hit, nptr[Q_NEXT], ties, pool + (Q_TIES - Q_WORDS)};
-    trace_pool<false, COUNT, ClosestSrc, true, INST, PT_POOL_LDS_C, QN>(n, pool, src, s_ref, s_ent, ovf, wk, s_lut);
+    trace_pool<false, COUNT, ClosestSrc, INST, PT_POOL_LDS, QN>(n, pool, src, s_ref, ovf, wk, s_lut);
     if (COUNT) {
         count_add(counters, CNT_NODES_CLOSEST, wk.nodes);
         count_add(counters, CNT_TRIS_CLOSEST, wk.tris);
@@ -349,19 +332,14 @@ __device__ __forceinline__ void shadow_add(PathSoA& next, float* __restrict__ sa
     v.z = fma_(c.z, a.z, v.z);
     *L = v;
 }
-// Shadow-ray source of the any-hit kernels.  DEFER (the pool kernel,
-// PT_SHADOW_DEFER): an unoccluded ray only flags its record (c.w = 1, a
-// store) and k_shadow_apply adds the contributions after the traversal; in
-// the loop the add is two dependent reads (record, then the path's radiance)
-// that hold up the whole wave whenever one of its lanes finishes unoccluded.
-template <bool DEFER>
-struct ShadowSrcT {
+// Shadow-ray source of the any-hit kernels: an unoccluded ray adds its
+// contribution in place (deferring the add to a kernel after the traversal
+// measured slower: C4 any-hit 1178 -> 1192 ms per frame,
+// profiles/r04_ab_traversal.txt)
+struct ShadowSrc {
     ShadowRec* sq;
     PathSoA next;
     float* sample_L;
-    static constexpr bool kInv = false;
-    __device__ __forceinline__ void load_inv(uint32_t, f3&, f3&, f3&, float&) {}
-    __device__ __forceinline__ void done(uint32_t, f3, f3, float, bool) {}
     __device__ __forceinline__ bool load(uint32_t i, f3& o, f3& d, float& tmax) {
         const float4 ro = sq[i].o, rd = sq[i].d;
         o = xyz(ro);
@@ -374,14 +352,9 @@ struct ShadowSrcT {
     __device__ __forceinline__ float time(uint32_t i) const { return S.sq_time[i]; }
     __device__ __forceinline__ void any(uint32_t i, bool hit) {
         if (hit) return;
-        if (DEFER) {
-            sq[i].c.w = SHADOW_VISIBLE;
-            return;
-        }
         shadow_add(next, sample_L, __float_as_uint(sq[i].d.w), sq[i].c, sq[i].a);
     }
 };
-using ShadowSrc = ShadowSrcT<false>;
 
 template <bool COUNT, bool INST, bool QN>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SHADOW_WAVES_FOR(PT_USES_SPEC(INST, QN)) void k_shadow_pool(PathSoA next, float* __restrict__ sample_L,
@@ -390,74 +363,40 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SHADOW_WAVES_FOR(PT_USES_SPEC(IN
                                                                uint32_t* __restrict__ pool, uint32_t* __restrict__ ovf,
                                                                unsigned long long* counters) {
     __shared__ uint32_t s_ref[PT_POOL_LDS * PT_TRACE_BLOCK];
-    constexpr int TREE = PT_USES_SPEC(INST, QN) ? PT_TREELET_ANY : 0;
-    __shared__ __attribute__((aligned(16))) uint8_t s_lut[(QN && PT_Q48) ? Q48_LDS_BYTES(TREE) : 4];
+    __shared__ __attribute__((aligned(16))) uint8_t s_lut[QN ? Q48_LUT_BYTES : 4];
     TraceWork wk{0, 0};
-    using Src = ShadowSrcT<PT_SHADOW_DEFER != 0>;
-    Src src{sq, next, sample_L};
+    ShadowSrc src{sq, next, sample_L};
     const uint32_t n = *nptr;
     if (n == 0) return;
-    if constexpr (QN && PT_Q48) stage_q48_lut<TREE>(s_lut);
-    trace_pool<true, COUNT, Src, true, INST, PT_POOL_LDS, QN>(n, pool, src, s_ref, nullptr, ovf, wk, s_lut);
+    if constexpr (QN) stage_q48_lut(s_lut);
+    trace_pool<true, COUNT, ShadowSrc, INST, PT_POOL_LDS, QN>(n, pool, src, s_ref, ovf, wk, s_lut);
     if (COUNT) {
         count_add(counters, CNT_NODES_ANY, wk.nodes);
         count_add(counters, CNT_TRIS_ANY, wk.tris);
     }
 }
 
-// The deferred contributions of k_shadow_pool (PT_SHADOW_DEFER): the rays it
-// found unoccluded (c.w flagged) add fma(c, att, L) exactly as ShadowSrc::any
-// does in place
-__global__ __launch_bounds__(256) void k_shadow_apply(PathSoA next, float* __restrict__ sample_L,
-                                                      const ShadowRec* __restrict__ sq,
-                                                      const uint32_t* __restrict__ nptr) {
-    const uint32_t n = *nptr;
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-        const float4 c = sq[i].c;
-        if (c.w != SHADOW_VISIBLE) continue;
-        shadow_add(next, sample_L, __float_as_uint(sq[i].d.w), c, sq[i].a);
-    }
-}
-
 // One ray per lane (grid covers all rays): lower overhead where traversal
 // lengths are uniform (small scenes); the runtime picks per scene.  The
 // whole-leaf inner loop of trace_closest / trace_any measures faster here than
-// the one-primitive-per-step loop of pt_pool.h (C2: 171 vs 191 us per launch),
-// PT_SIMPLE_STEP=1 selects the latter.
-#ifndef PT_SIMPLE_STEP
-#define PT_SIMPLE_STEP 0
-#endif
-// PT_SIMPLE_LN: stack entries the one-ray-per-lane kernels keep in LDS (the
-// rest in the global overflow array); PT_SIMPLE_WPE: their waves-per-SIMD budget.
+// the one-primitive-per-step loop of pt_pool.h (C2: 171 vs 191 us per launch).
+// PT_SIMPLE_LN: stack entries these kernels keep in LDS (the rest in the
+// global overflow array).
 #ifndef PT_SIMPLE_LN
 #define PT_SIMPLE_LN PT_STACK
 #endif
-#if PT_SIMPLE_STEP
-#define PT_SIMPLE_LDS PT_POOL_LDS  // split stack, as the pool kernels
-#else
-#define PT_SIMPLE_LDS PT_SIMPLE_LN
-#endif
-#ifdef PT_SIMPLE_WPE
-#define PT_SIMPLE_WAVES __attribute__((amdgpu_waves_per_eu(PT_SIMPLE_WPE, PT_SIMPLE_WPE)))
-#else
 #define PT_SIMPLE_WAVES
-#endif
 template <bool COUNT, bool INST>
 __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SIMPLE_WAVES void k_closest(PathSoA P, const uint32_t* __restrict__ nptr,
                                                            float4* __restrict__ hit, uint32_t* __restrict__,
                                                            uint32_t* __restrict__ ovf, uint32_t* __restrict__ spare,
                                                            uint32_t* __restrict__ snap, unsigned long long* counters,
                                                            uint32_t* __restrict__) {
-    __shared__ uint32_t s_ref[PT_SIMPLE_LDS * PT_TRACE_BLOCK];
+    __shared__ uint32_t s_ref[PT_SIMPLE_LN * PT_TRACE_BLOCK];
     iteration_prologue(nptr, spare, snap);
     const uint32_t n = path_count(nptr);  // the grid covers the wavefront's capacity
     if (blockIdx.x * PT_TRACE_BLOCK >= n) return;
     TraceWork wk{0, 0};
-#if PT_SIMPLE_STEP
-    __shared__ uint16_t s_ent[PT_SIMPLE_LDS * PT_TRACE_BLOCK];
-    ClosestSrc src{P, hit, nptr[Q_NEXT]};
-    trace_pool<false, COUNT, ClosestSrc, false, INST, PT_SIMPLE_LDS>(n, nullptr, src, s_ref, s_ent, ovf, wk);
-#else
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     if (i < n) {
         const uint32_t e = path_slot(i, nptr[Q_NEXT], P.cap);
@@ -467,7 +406,6 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SIMPLE_WAVES void k_closest(Path
                                                             s_ref, wk, ovf, (INST && S.motion) ? P.time[e] : 0.0f);
         hit[i] = make_float4(t, b1, b2, __int_as_float(prim));
     }
-#endif
     if (COUNT) {
         count_add(counters, CNT_NODES_CLOSEST, wk.nodes);
         count_add(counters, CNT_TRIS_CLOSEST, wk.tris);
@@ -479,22 +417,17 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SIMPLE_WAVES void k_shadow(PathS
                                                           ShadowRec* __restrict__ sq,
                                                           const uint32_t* __restrict__ nptr, uint32_t* __restrict__,
                                                           uint32_t* __restrict__ ovf, unsigned long long* counters) {
-    __shared__ uint32_t s_ref[PT_SIMPLE_LDS * PT_TRACE_BLOCK];
+    __shared__ uint32_t s_ref[PT_SIMPLE_LN * PT_TRACE_BLOCK];
     const uint32_t n = *nptr;
     if (blockIdx.x * PT_TRACE_BLOCK >= n) return;
     TraceWork wk{0, 0};
     ShadowSrc src{sq, next, sample_L};
-#if PT_SIMPLE_STEP
-    if (blockIdx.x * PT_TRACE_BLOCK < n)
-        trace_pool<true, COUNT, ShadowSrc, false, INST, PT_SIMPLE_LDS>(n, nullptr, src, s_ref, nullptr, ovf, wk);
-#else
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     if (i < n) {
         const ShadowRec r = sq[i];
         src.any(i, trace_any<COUNT, INST, PT_SIMPLE_LN>(xyz(r.o), xyz(r.d), r.o.w, s_ref, wk, ovf,
                                                         (INST && S.motion) ? S.sq_time[i] : 0.0f));
     }
-#endif
     if (COUNT) {
         count_add(counters, CNT_NODES_ANY, wk.nodes);
         count_add(counters, CNT_TRIS_ANY, wk.tris);
@@ -508,9 +441,6 @@ struct RaysSrc {
     uint32_t* ties;  // exact-t ties (pt_pool.h), re-traced by k_trace_rays_ties
     uint32_t* n_ties;
     uint32_t n;      // rays, and entries of the tie list
-    static constexpr bool kInv = false;
-    __device__ __forceinline__ void load_inv(uint32_t, f3&, f3&, f3&, float&) {}
-    __device__ __forceinline__ void done(uint32_t, f3, f3, float, bool) {}
     __device__ __forceinline__ bool load(uint32_t i, f3& o, f3& d, float& tmax) {
         const pt_ray r = rays[i];
         o = F3(r.o[0], r.o[1], r.o[2]);
@@ -526,6 +456,7 @@ struct RaysSrc {
     __device__ __forceinline__ void tie(uint32_t i) {
         const uint32_t k = atomicAdd(n_ties, 1u);
         if (k < n) ties[k] = i;
+        else atomicAdd(S.tie_drops, 1u);  // (as ClosestSrc::tie)
     }
 };
 
@@ -535,13 +466,12 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(const pt_ray* __r
                                                               uint32_t* __restrict__ ovf, unsigned long long* counters,
                                                               uint32_t* __restrict__ ties, uint32_t* __restrict__ n_ties) {
     __shared__ uint32_t s_ref[PT_POOL_LDS * PT_TRACE_BLOCK];
-    __shared__ uint16_t s_ent[PT_POOL_LDS_C * PT_TRACE_BLOCK];
-    __shared__ __attribute__((aligned(16))) uint8_t s_lut[(QN && PT_Q48) ? 8 * Q48_LUT_STRIDE : 4];
-    if constexpr (QN && PT_Q48) stage_q48_lut(s_lut);
+    __shared__ __attribute__((aligned(16))) uint8_t s_lut[QN ? Q48_LUT_BYTES : 4];
+    if constexpr (QN) stage_q48_lut(s_lut);
     TraceWork wk{0, 0};
     RaysSrc src{rays, out, ties, n_ties, n};
-    if (any) trace_pool<true, true, RaysSrc, true, true, PT_POOL_LDS, QN>(n, pool, src, s_ref, nullptr, ovf, wk, s_lut);
-    else trace_pool<false, true, RaysSrc, true, true, PT_POOL_LDS_C, QN>(n, pool, src, s_ref, s_ent, ovf, wk, s_lut);
+    if (any) trace_pool<true, true, RaysSrc, true, PT_POOL_LDS, QN>(n, pool, src, s_ref, ovf, wk, s_lut);
+    else trace_pool<false, true, RaysSrc, true, PT_POOL_LDS, QN>(n, pool, src, s_ref, ovf, wk, s_lut);
     count_add(counters, any ? CNT_NODES_ANY : CNT_NODES_CLOSEST, wk.nodes);
     count_add(counters, any ? CNT_TRIS_ANY : CNT_TRIS_CLOSEST, wk.tris);
 }
@@ -570,7 +500,6 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays_ties(const pt_ray
 __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_interact(const pt_ray* __restrict__ rays, uint32_t n,
                                                             float* __restrict__ out) {
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
-    stage_tables(false);
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     TraceWork wk{0, 0};
     if (i >= n) return;
@@ -592,7 +521,6 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_interact(const pt_ray* __res
 // Test hook: Material::scatter / calc_attenuation / PDF on given
 // interactions (pt_bsdf_cases); case and record layout of oracle_bsdf.
 __global__ void k_bsdf_cases(int mid, const float* __restrict__ in, uint32_t n, float* __restrict__ out) {
-    stage_tables(false);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float* c = in + 27ull * i;
@@ -628,10 +556,25 @@ __global__ void k_bsdf_cases(int mid, const float* __restrict__ in, uint32_t n, 
     o[19] = mat_pdf(mt, rd, si, other);
 }
 
+// Test hook: anim_inverse (pt_shading.h) on the matrix identity + t
+// (pt_anim_inverse_cases), as inst_matrices forms it for an AnimatedPrimitive
+__global__ void k_anim_inverse(const float* __restrict__ t, uint32_t n, float* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float T[16], inv[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) T[k] = (k % 5 == 0) ? 1.0f : 0.0f;
+    T[12] = t[3 * i];
+    T[13] = t[3 * i + 1];
+    T[14] = t[3 * i + 2];
+    anim_inverse(T, inv);
+#pragma unroll
+    for (int k = 0; k < 16; k++) out[16ull * i + k] = inv[k];
+}
+
 // Test hook: LightSampler::Sample(u) picks (pt_light_picks): the light index
 // ls_sample returns (-1: no light), one per u.
 __global__ void k_light_picks(const float* __restrict__ u, uint32_t n, int32_t* __restrict__ out) {
-    stage_tables(true);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = ls_sample(u[i]);
 }
@@ -639,7 +582,6 @@ __global__ void k_light_picks(const float* __restrict__ u, uint32_t n, int32_t* 
 // Test hook: Light::sample / PDF / L per light x case (pt_light_cases);
 // case {uv[2], ref point[3]}, record layout of oracle_lights.
 __global__ void k_light_cases(const float* __restrict__ in, uint32_t n, float* __restrict__ out) {
-    stage_tables(false);
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n * S.n_lights) return;
     const uint32_t li = k / n, i = k % n;
@@ -871,7 +813,6 @@ __device__ __forceinline__ void store_camera_path(PathSoA& next, uint32_t at, co
     next.o[at] = make_float4(ns.o.x, ns.o.y, ns.o.z, __uint_as_float(ns.key));
     // depth 1 (first loop test passed), spec = true, the camera's medium (Camera.hpp:27, 34)
     next.d[at] = make_float4(ns.d.x, ns.d.y, ns.d.z, __uint_as_float(1u | PF_SPEC | medium_bits(cam_medium)));
-    if (PT_PATH_INV) next.inv[at] = f4_of(inv_dir(ns.d));
     next.beta[at] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);  // attenuation, prevPDF = 1
     next.L[at] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(5u));  // camera used dims 0..4
     next.sid[at] = ns.sid;
@@ -901,14 +842,6 @@ __global__ __launch_bounds__(256) void k_fill(RenderParams R, uint32_t n, PathSo
 }
 
 // ------------------------------------------------------------------ shading
-// k_shade (Path): the NEE light sample (LightSampler::Sample + Light::sample)
-// drawn before the hit's interaction is rebuilt (it depends only on the
-// sample's draws), so its reads overlap the hit's; same values.  Off: C4
-// k_shade 1350 -> 1354 ms per frame (256-thread blocks at 3 waves, where it
-// fits without spills; profiles/r04_ab_alpha.txt)
-#ifndef PT_SHADE_EARLY_LS
-#define PT_SHADE_EARLY_LS 0
-#endif
 // One bounce of PathIntegrator::Li / SimplePathIntegrator::Li for one path
 // (Integrators.cpp:131-294): the closest hit h = (t, b1, b2, prim) of the ray
 // (ro, rd) is shaded, emission and the NEE sample drawn, the next ray sampled.
@@ -921,14 +854,7 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
                                              bool& cont, bool& done, bool& shadow, ShadowRec& srec, float tm) {
     uint32_t depth = f0 & PF_DEPTH_MASK, rr = (f0 >> PF_RR_SHIFT) & PF_DEPTH_MASK;
     bool spec = (f0 & PF_SPEC) != 0;
-    int prim = __float_as_int(h.w);
-#if PT_POOL_CHECK
-    if (__float_as_uint(h.x) == 0xFFFFFFFFu) atomicAdd(&pt_diag[2], 1u);  // debugging builds only
-    if (prim >= (int)S.n_prims) {
-        atomicAdd(&pt_diag[1], 1u);
-        prim = -1;
-    }
-#endif
+    const int prim = __float_as_int(h.w);
     bool alive = true;
     if (prim < 0) {
         // miss: infinite lights (Integrators.cpp:140-145, 196-208)
@@ -955,25 +881,9 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
             for (int k = 0; k < 4; k++) r[k] = draw(key, dim + k);
             dim += 4;
         }
-#if PT_SHADE_EARLY_LS
-        // the light sample needs no hit: its chain of reads (guide table,
-        // running sums, light record, shape) runs beside the hit's
-        int li = -1;
-        LSample ls_e;
-        if (INTEGRATOR == PT_INTEGRATOR_PATH) {
-            li = ls_sample(r[5]);
-            if (li >= 0) ls_e = light_sample(S.lights[li], r[2], r[3], texinf_uc(key, dim), tm);
-        }
-#endif
         SurfInt si;
         int smed;
-        hit_surface(prim, ro, rd, h.x, h.y, h.z, si, smed, tm, PT_TEX_JOINT && PT_NM_DEFER);
-#ifdef PT_DEBUG_KEY
-        if (key == PT_DEBUG_KEY)
-            printf("G d%u prim %d t %a p %a %a %a ns %a %a %a uv %a %a mat %d light %d out %a %a %a att %a %a %a\n",
-                   depth, prim, si.t, si.p.x, si.p.y, si.p.z, si.ns.x, si.ns.y, si.ns.z, si.u, si.v, si.mat,
-                   si.light, out.x, out.y, out.z, att.x, att.y, att.z);
-#endif
+        hit_surface(prim, ro, rd, h.x, h.y, h.z, si, smed, tm);
         // emission (Integrators.cpp:151-154, 217-226)
         if (si.light >= 0) {
             const pt_light& al = S.lights[si.light];
@@ -1003,16 +913,10 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
                     spec = (b.flags & FL_SPEC) != 0;
                     if (!spec) {
                         // PathIntegrator::SampleLd (Integrators.cpp:260-294); occlusion deferred
-#if !PT_SHADE_EARLY_LS
                         const int li = ls_sample(r[5]);
-#endif
                         if (li >= 0) {
                             const pt_light& l = S.lights[li];
-#if PT_SHADE_EARLY_LS
-                            const LSample ls = ls_e;
-#else
-                            LSample ls = light_sample(l, r[2], r[3], texinf_uc(key, dim), tm);
-#endif
+                            const LSample ls = light_sample(l, r[2], r[3], texinf_uc(key, dim), tm);
                             f3 ldir;
                             float tmax;
                             if (is_zero(ls.n)) {
@@ -1052,18 +956,8 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
                             }
                         }
                         prev = mat_pdf(mt, rd, si, b.d);
-#ifdef PT_DEBUG_KEY
-                        if (key == PT_DEBUG_KEY)
-                            printf("G  nee c %a %a %a (light %d) shadow %d\n", srec.c.x, srec.c.y, srec.c.z, li,
-                                   (int)shadow);
-#endif
                     }
                 }
-#ifdef PT_DEBUG_KEY
-                if (key == PT_DEBUG_KEY)
-                    printf("G  scatter d %a %a %a f %a %a %a pdf %a prev %a\n", b.d.x, b.d.y, b.d.z, b.f.x, b.f.y,
-                           b.f.z, b.pdf, prev);
-#endif
                 att = att * ((b.f * fabsf(dot(si.ns, b.d))) / b.pdf);
                 const float urr = INTEGRATOR == PT_INTEGRATOR_PATH ? r[6] : r[3];
                 if (rr++ > 3) {
@@ -1086,58 +980,6 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
     flags = depth | (rr << PF_RR_SHIFT) | (spec ? PF_SPEC : 0u);
 }
 
-// k_shade's block-wide bookkeeping in one step: the finished paths' camera
-// sample claim (their rank among the block's finished lanes, as
-// claim_camera_sample numbers them) and the three queue appends share one
-// count / atomics / barrier round instead of two.  The claimed ids below the
-// chunk's end are the first ranks, so the block books min(claimed, left) new
-// paths right after its claim returns.  Off: measured equal (C4 2009.8 /
-// 2013.5 vs 2016.2 / 2012.6 Mrays/s, profiles/r05_ab_shade_block.txt).
-#ifndef PT_SHADE_ONE_STEP
-#define PT_SHADE_ONE_STEP 0
-#endif
-__device__ __forceinline__ NewSample shade_slots(const RenderParams& R, bool done, bool cont, bool shadow,
-                                                 unsigned long long* __restrict__ next_sample,
-                                                 uint32_t* __restrict__ cnt, uint32_t (&at)[3]) {
-    constexpr int NW = PT_SHADE_BLOCK / 64;
-    __shared__ uint32_t s_c[3][NW + 1];
-    __shared__ unsigned long long s_base;
-    const uint32_t wave = threadIdx.x >> 6;
-    const uint64_t m[3] = {__ballot(done), __ballot(cont), __ballot(shadow)};
-    if (__lane_id() == 0) {
-#pragma unroll
-        for (int q = 0; q < 3; q++) s_c[q][wave] = (uint32_t)__popcll(m[q]);
-    }
-    __syncthreads();
-    if (threadIdx.x < 3) {
-        const int q = threadIdx.x;
-        uint32_t tot = 0;
-        for (int w = 0; w < NW; w++) {
-            const uint32_t c = s_c[q][w];
-            s_c[q][w] = tot;
-            tot += c;
-        }
-        if (q == 0) {  // sample ids for the finished paths, then the new paths among them
-            const unsigned long long base = tot ? atomicAdd(next_sample, (unsigned long long)tot) : 0ull;
-            const unsigned long long left = base < R.chunk_total ? R.chunk_total - base : 0ull;
-            const uint32_t nn = (uint32_t)min((unsigned long long)tot, left);
-            s_base = base;
-            s_c[0][NW] = nn ? atomicAdd(&cnt[Q_NEW], nn) : 0u;
-        } else {
-            s_c[q][NW] = tot ? atomicAdd(&cnt[q == 1 ? Q_NEXT : Q_SHADOW], tot) : 0u;
-        }
-    }
-    __syncthreads();
-    const uint32_t r0 = s_c[0][wave] + lanemask_lt_count(m[0]);
-    const unsigned long long g = s_base + r0;
-    at[0] = s_c[1][NW] + s_c[1][wave] + lanemask_lt_count(m[1]);
-    at[1] = s_c[2][NW] + s_c[2][wave] + lanemask_lt_count(m[2]);
-    at[2] = s_c[0][NW] + r0;
-    NewSample ns{done && g < R.chunk_total, (uint32_t)g, 0u, F3(0, 0, 0), F3(0, 0, 0), 0.0f};
-    if (ns.enq) camera_sample(R, ns);
-    return ns;
-}
-
 template <int INTEGRATOR>
 #ifndef PT_SHADE_WPE  // waves-per-SIMD budget for k_shade (pt_kernels.h PT_SHADE_BLOCK)
 #define PT_SHADE_WPE 4
@@ -1150,7 +992,6 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
                                               ShadowRec* __restrict__ sq, uint32_t* __restrict__ cnt) {
     const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
     if (blockIdx.x * PT_SHADE_BLOCK >= n) return;  // block-uniform: the grid covers the capacity
-    stage_tables(INTEGRATOR == PT_INTEGRATOR_PATH);
     const uint32_t t = blockIdx.x * PT_SHADE_BLOCK + threadIdx.x;
     const uint32_t i = (R.order && t < n) ? R.order[t] : t;  // material-sorted order, or the path order
     bool cont = false, done = false, shadow = false;
@@ -1182,20 +1023,17 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
         o[1] = out.y;
         o[2] = out.z;
     }
+    // (the claim and the appends in one barrier round measured equal,
+    // profiles/r05_ab_shade_block.txt)
     uint32_t at[3];
-#if PT_SHADE_ONE_STEP
-    const NewSample ns = shade_slots(R, done, cont, shadow, next_sample, cnt, at);
-#else
     const NewSample ns = claim_camera_sample(R, done, next_sample);
     const int qoff[3] = {Q_NEXT, Q_SHADOW, Q_NEW};
     const bool pred[3] = {cont, shadow, ns.enq};
     block_append<3, PT_SHADE_BLOCK>(cnt, qoff, pred, at);
-#endif
     const uint32_t a = cont ? at[0] : next.cap - 1u - at[2], c = at[1];
     if (cont) {
         next.o[a] = make_float4(ro.x, ro.y, ro.z, __uint_as_float(key));
         next.d[a] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(flags));
-        if (PT_PATH_INV) next.inv[a] = f4_of(inv_dir(rd));
         next.beta[a] = make_float4(att.x, att.y, att.z, prev);
         next.L[a] = make_float4(out.x, out.y, out.z, __uint_as_float(dim));
         next.sid[a] = sid;
@@ -1289,7 +1127,6 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                                                   ShadowRecV* __restrict__ sq, uint32_t* __restrict__ cnt) {
     const uint32_t n = path_count(nptr), front = nptr[Q_NEXT];
     if (blockIdx.x * 256 >= n) return;  // block-uniform: the grid covers the capacity
-    stage_tables(true);
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
     const uint32_t i = (R.order && t < n) ? R.order[t] : t;  // material-sorted order, or the path order
     bool cont = false, done = false, shadow = false;
@@ -1493,7 +1330,6 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
     if (cont) {
         next.o[a] = make_float4(ro.x, ro.y, ro.z, __uint_as_float(key));
         next.d[a] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(flags));
-        if (PT_PATH_INV) next.inv[a] = f4_of(inv_dir(rd));
         next.beta[a] = make_float4(att.x, att.y, att.z, prev);
         next.L[a] = make_float4(out.x, out.y, out.z, __uint_as_float(dim));
         next.sid[a] = sid;
@@ -1520,7 +1356,6 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow_tr(PathSoA next, floa
     __shared__ uint32_t s_ref[PT_STACK * PT_TRACE_BLOCK];
     const uint32_t n = *nptr;
     if (blockIdx.x * PT_TRACE_BLOCK >= n) return;
-    stage_tables(false);
     const uint32_t i = blockIdx.x * PT_TRACE_BLOCK + threadIdx.x;
     TraceWork wk{0, 0};
     uint32_t extra = 0;
@@ -1883,16 +1718,9 @@ __device__ __forceinline__ uint32_t sort_bin(const PathSoA& cur, uint32_t front,
     const float4 h = hit[i];
     const int prim = __float_as_int(h.w);
     if (prim < 0) return 0u;
-    if (KEY == PT_SORT_SPATIAL && PT_SORT_PRIM_CELL && S.prim_cell) {
+    if (KEY == PT_SORT_SPATIAL && S.prim_cell) {
         if ((uint32_t)prim >= S.n_prims) return PT_SORT_BINS_SPATIAL - 1u;  // a virtual slot inside an instance
         return S.prim_cell[prim];
-    }
-    if (KEY == PT_SORT_SPATIAL && PT_SORT_BY_SLOT) {
-        // the hit primitive's slot: slots are in the BVH's leaf order, so a
-        // range of them is a compact patch of geometry (and of its materials);
-        // only the hit record is read
-        if ((uint32_t)prim >= S.n_prims) return PT_SORT_BINS_SPATIAL - 1u;  // a virtual slot inside an instance
-        return 1u + (uint32_t)(((uint64_t)(uint32_t)prim * (PT_SORT_BINS_SPATIAL - 2u)) / S.n_prims);
     }
     if (KEY == PT_SORT_MATERIAL) {
         if ((uint32_t)prim >= S.n_prims) return PT_SORT_BINS_MATERIAL - 1u;  // a virtual slot inside an instance
@@ -1905,8 +1733,8 @@ __device__ __forceinline__ uint32_t sort_bin(const PathSoA& cur, uint32_t front,
 // Each block bins PT_SORT_PER paths per thread (PT_SORT_PER x 256
 // consecutive paths), so clearing and folding the block's 4096-bin LDS
 // histogram is paid once per 4096 paths rather than once per 256.
-// bins (PT_SORT_KEEP_BINS, or null): each path's bin, for k_sort_scatter to
-// read (2 B) instead of recomputing it from the path and hit records (48 B)
+// bins (or null): each path's bin, for k_sort_scatter to read (2 B) instead
+// of recomputing it from the path and hit records (48 B)
 template <int KEY, int NB>
 __global__ __launch_bounds__(256) void k_sort_count(PathSoA cur, const uint32_t* __restrict__ nptr,
                                                    const float4* __restrict__ hit, uint32_t* __restrict__ counts,
@@ -1921,13 +1749,8 @@ __global__ __launch_bounds__(256) void k_sort_count(PathSoA cur, const uint32_t*
     for (uint32_t k = 0; k < PT_SORT_PER; k++) {
         const uint32_t t = t0 + k * 256u + threadIdx.x;
         if (t < n) {
-            uint32_t b;
-            if (KEY == PT_SORT_SPATIAL && S.hit_bins) {  // written by the closest-hit pool kernel
-                b = S.hit_bins[t];
-            } else {
-                b = sort_bin<KEY>(cur, front, hit, t);
-                if (bins) bins[t] = (uint16_t)b;
-            }
+            const uint32_t b = sort_bin<KEY>(cur, front, hit, t);
+            if (bins) bins[t] = (uint16_t)b;
             atomicAdd(&h[b], 1u);
         }
     }

@@ -39,17 +39,15 @@
 // Any-hit rays of bounce k on a second stream, beside bounce k+1's closest-hit
 // rays (the two only read the path state; the shading of k+1 waits for them):
 // each persistent pool kernel's draining tail leaves CUs the other fills.
-// Env PT_OVERLAP_SHADOW overrides.
-#ifndef PT_OVERLAP_SHADOW
-#define PT_OVERLAP_SHADOW 0
-#endif
+// Off by default (C4 -6.8 %, profiles/r03_ab_streams_shade.txt); the render
+// flags or env PT_OVERLAP_SHADOW=1 turn it on.
 
 struct pt_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     // any-hit rays of bounce k traced on side_stream beside bounce k+1's
-    // closest-hit rays (PT_OVERLAP_SHADOW; see trace's loop)
+    // closest-hit rays (PT_RENDER_OVERLAP_SHADOW; see trace's loop)
     hipStream_t side_stream = nullptr;
     bool overlap = false;
     std::string err;
@@ -63,7 +61,7 @@ struct pt_ctx {
     uint32_t trace_blocks = 0;  // resident traversal blocks on this device (persistent grid), max of the two
     uint32_t pool_blocks[2][2][2] = {};  // [any hit][instanced][quantized]: each pool kernel's resident blocks
     uint64_t n_clusters = 0;    // BVH clusters of the uploaded scene (traversal choice)
-    bool has_qnodes = false;    // the scene's nodes have a quantized copy (DevQNode)
+    bool has_qnodes = false;    // the scene's nodes have a quantized copy (48-B records)
     int node_format = PT_NODES_AUTO;  // pt_set_node_format
     // wavefront buffers: two compacted path states (ping-pong), per-bounce hits,
     // the finished-path list and the shadow-ray queue
@@ -104,12 +102,14 @@ struct pt_ctx {
     uint64_t ray_order_cap = 0, ray_counts_cap = 0;
     hipEvent_t ev[8] = {};
     hipEvent_t rev[PT_RING][5] = {};  // per in-flight iteration: kernel boundaries [0..2], end [4] ([3] unused)
-    uint32_t* stack_drops = nullptr;  // device word: traversal pushes beyond the stack (DevScene::stack_drops)
+    uint32_t* stack_drops = nullptr;  // device words: traversal pushes beyond the stack, exact-tie list drops
+                                      // (DevScene::stack_drops / tie_drops)
     // multi-device context (pt_create with n_devices > 1): the other devices'
     // contexts (owned) and, per device, an RCCL communicator for the film reduce
     std::vector<pt_ctx*> peers;
     bool multi = false;  // renders through render_multi (n_devices > 1, or forced for tests)
     ncclComm_t comm = nullptr;
+    bool comm_nonblocking = false;  // built by pt_comm_init_rank (non-blocking); else ncclCommInitAll's
     int comm_ranks = 0, comm_rank = 0;
     // where the last fixed-SPP frame's final sample chunk lies in sample_L
     // (pt_frame_samples); cleared by every other use of the buffer
@@ -183,7 +183,7 @@ static pt_status create_dev(pt_ctx** out, int device) {
     }
     {
         const char* ov = getenv("PT_OVERLAP_SHADOW");
-        c->overlap = ov ? atoi(ov) != 0 : PT_OVERLAP_SHADOW != 0;
+        c->overlap = ov && atoi(ov) != 0;
     }
     for (hipEvent_t* e = &c->ev[0]; e != &c->ev[0] + 8; ++e)
         if (hipEventCreate(e) != hipSuccess) {
@@ -374,6 +374,7 @@ extern "C" pt_status pt_comm_init_rank(pt_ctx* c, int n_ranks, int rank, const u
         return fail(c, PT_ERR_COMM, "ncclCommInitRank(%d of %d): %s", rank, n_ranks, ncclGetErrorString(r));
     }
     c->comm = comm;
+    c->comm_nonblocking = true;
     c->comm_ranks = n_ranks;
     c->comm_rank = rank;
     return PT_OK;
@@ -389,6 +390,7 @@ extern "C" pt_status pt_comm_destroy(pt_ctx* c) {
         ncclCommAbort(c->comm);
     }
     c->comm = nullptr;
+    c->comm_nonblocking = false;
     c->comm_ranks = 0;
     c->comm_rank = 0;
     return PT_OK;
@@ -443,14 +445,9 @@ static void free_scene(pt_ctx* c) {
     c->has_scene = false;
 }
 static void free_work(pt_ctx* c) {
-    // (PT_PATH_AOS 1: the four fields share the o allocation; 2: d shares o's,
-    // L beta's)
-    constexpr bool own_d = PT_PATH_AOS == 0, own_beta = PT_PATH_AOS != 1, own_L = PT_PATH_AOS == 0;
-    void* bufs[] = {c->PA.o.p, own_d ? c->PA.d.p : nullptr, own_beta ? c->PA.beta.p : nullptr,
-                    own_L ? c->PA.L.p : nullptr, c->PA.sid, c->PA.time, c->PA.inv, c->PB.o.p,
-                    own_d ? c->PB.d.p : nullptr, own_beta ? c->PB.beta.p : nullptr,
-                    own_L ? c->PB.L.p : nullptr, c->PB.sid, c->PB.time, c->PB.inv, c->hit, c->qcnt, c->sq, c->counters,
-                    c->ovf, c->ties, c->sq_time};
+    // (d shares o's allocation, L beta's: pt_kernels.h PathSoA)
+    void* bufs[] = {c->PA.o.p, c->PA.beta.p, c->PA.sid, c->PA.time, c->PB.o.p, c->PB.beta.p, c->PB.sid,
+                    c->PB.time, c->hit, c->qcnt, c->sq, c->counters, c->ovf, c->ties, c->sq_time};
     for (void* p : bufs)
         if (p) hipFree(p);
     c->PA = PathSoA{};
@@ -468,10 +465,28 @@ static void free_work(pt_ctx* c) {
 
 extern "C" void pt_destroy(pt_ctx* c) {
     if (!c) return;
+    if (c->multi) {
+        // the multi-device context's communicators (ncclCommInitAll: blocking,
+        // one per device, every one owned by this thread) are finalized
+        // together in one group -- one at a time, each finalize would wait for
+        // peers that are not being finalized -- then destroyed
+        std::vector<ncclComm_t> comms;
+        for (size_t i = 0; i <= c->peers.size(); i++) {
+            pt_ctx* d = i ? c->peers[i - 1] : c;
+            if (d->comm) comms.push_back(d->comm);
+            d->comm = nullptr;
+        }
+        if (!comms.empty()) {
+            ncclGroupStart();
+            for (ncclComm_t m : comms) ncclCommFinalize(m);
+            ncclGroupEnd();
+            for (ncclComm_t m : comms) ncclCommDestroy(m);
+        }
+    }
     for (pt_ctx* p : c->peers) pt_destroy(p);
     c->peers.clear();
     hipSetDevice(c->device);
-    if (c->comm) comm_release(c->comm, !c->multi);  // per-rank communicators are non-blocking
+    if (c->comm) comm_release(c->comm, c->comm_nonblocking);  // a per-rank communicator (pt_comm_init_rank)
     c->comm = nullptr;
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->side_stream) hipStreamSynchronize(c->side_stream);  // any-hit kernels of an overlapped frame
@@ -517,7 +532,7 @@ extern "C" uint64_t pt_scene_device_bytes(const pt_ctx* c) { return c ? c->scene
 // bound up, checked with the device's own decode fma(q, step, origin) so the
 // decoded box always contains the reference's float box.  False when the
 // bounds are not finite or no step fits (the scene then keeps full nodes).
-// N children (4: DevQNode, 8: DevWNode); wlo / whi: 4 bytes per word
+// N children (4 per node); wlo / whi: 4 bytes per word
 static bool quantize_axis_n(int N, const float* lo, const float* hi, uint32_t valid, float& org, uint32_t& e8,
                             uint32_t* wlo, uint32_t* whi) {
     for (int w = 0; w < N / 4; w++) {
@@ -572,105 +587,6 @@ static bool quantize_axis(const float* lo, const float* hi, uint32_t valid, floa
     return quantize_axis_n(4, lo, hi, valid, org, e8, &wlo, &whi);
 }
 
-// ---- wide nodes (DevWNode, PT_WIDE): cluster i plus its absorbed children's
-// children.  Slots keep the reference's depth-first visit order per octant.
-static uint32_t wide_octant_perm(const DevCluster& n, int o) {
-    return (n.order[o >> 2] >> (8 * (o & 3))) & 0xFFu;
-}
-static bool build_wnode(const std::vector<DevCluster>& nodes, size_t i, DevWNode& w) {
-    const DevCluster& n = nodes[i];
-    auto inner = [&](uint32_t r) { return r != REF_EMPTY && r < REF_LEAF && r < nodes.size(); };
-    auto nvalid = [&](const DevCluster& m) {
-        int v = 0;
-        for (int k = 0; k < 4; k++) v += m.child[k] != REF_EMPTY;
-        return v;
-    };
-    const float* nb = &n.xmin.x;  // xmin xmax ymin ymax zmin zmax, 4 floats each
-    auto area = [&](int k) {
-        const float dx = nb[4 + k] - nb[k], dy = nb[12 + k] - nb[8 + k], dz = nb[20 + k] - nb[16 + k];
-        return (double)dx * dy + (double)dy * dz + (double)dz * dx;
-    };
-    // absorb inner children, largest surface area first, while the slots fit
-    int slots = nvalid(n);
-    int ord[4] = {0, 1, 2, 3};
-    std::stable_sort(ord, ord + 4, [&](int a, int b) { return area(a) > area(b); });
-    bool absorb[4] = {false, false, false, false};
-    for (int k = 0; k < 4; k++) {
-        const int c = ord[k];
-        if (!inner(n.child[c])) continue;
-        const int v = nvalid(nodes[n.child[c]]);
-        if (slots - 1 + v <= 8) {
-            slots += v - 1;
-            absorb[c] = true;
-        }
-    }
-    // slots: (ref, box) of every kept child and every absorbed child's child
-    uint32_t ref[8];
-    float box[6][8];  // xmin xmax ymin ymax zmin zmax
-    int slot_of[4] = {-1, -1, -1, -1}, slot_of2[4][4];
-    int ns = 0;
-    for (int c = 0; c < 4; c++) {
-        if (n.child[c] == REF_EMPTY) continue;
-        if (!absorb[c]) {
-            slot_of[c] = ns;
-            ref[ns] = n.child[c];
-            for (int a = 0; a < 6; a++) box[a][ns] = nb[4 * a + c];
-            ns++;
-            continue;
-        }
-        const DevCluster& m = nodes[n.child[c]];
-        const float* mb = &m.xmin.x;
-        for (int g = 0; g < 4; g++) {
-            slot_of2[c][g] = -1;
-            if (m.child[g] == REF_EMPTY) continue;
-            slot_of2[c][g] = ns;
-            ref[ns] = m.child[g];
-            for (int a = 0; a < 6; a++) box[a][ns] = mb[4 * a + g];
-            ns++;
-        }
-    }
-    if (ns > 8) return false;
-    uint32_t valid = 0;
-    for (int k = 0; k < ns; k++) valid |= 1u << k;
-    for (int k = ns; k < 8; k++) {
-        ref[k] = REF_EMPTY;
-        for (int a = 0; a < 6; a++) box[a][k] = 0.0f;
-    }
-    float org[3];
-    uint32_t e[3], wl[3][2], wh[3][2];
-    for (int a = 0; a < 3; a++)
-        if (!quantize_axis_n(8, box[2 * a], box[2 * a + 1], valid, org[a], e[a], wl[a], wh[a])) return false;
-    w.a = make_float4(org[0], org[1], org[2], __builtin_bit_cast(float, e[0] | e[1] << 8 | e[2] << 16));
-    w.b0[0] = wl[0][0]; w.b0[1] = wh[0][0]; w.b0[2] = wl[1][0]; w.b0[3] = wh[1][0];
-    w.b1[0] = wl[0][1]; w.b1[1] = wh[0][1]; w.b1[2] = wl[1][1]; w.b1[3] = wh[1][1];
-    w.z[0] = wl[2][0]; w.z[1] = wh[2][0]; w.z[2] = wl[2][1]; w.z[3] = wh[2][1];
-    for (int k = 0; k < 8; k++) w.child[k] = ref[k];
-    // per octant: the cluster's push order (farthest first) with each absorbed
-    // child replaced by its own push order; unused positions point at an
-    // empty slot (or repeat nothing when all 8 are used)
-    for (int o = 0; o < 8; o++) {
-        const uint32_t pn = wide_octant_perm(n, o);
-        int list[8], nl = 0;
-        for (int k = 0; k < 4; k++) {
-            const int c = (pn >> (2 * k)) & 3;
-            if (n.child[c] == REF_EMPTY) continue;
-            if (!absorb[c]) {
-                list[nl++] = slot_of[c];
-                continue;
-            }
-            const uint32_t pm = wide_octant_perm(nodes[n.child[c]], o);
-            for (int j = 0; j < 4; j++) {
-                const int g = (pm >> (2 * j)) & 3;
-                if (slot_of2[c][g] >= 0) list[nl++] = slot_of2[c][g];
-            }
-        }
-        if (nl != ns) return false;
-        uint32_t p = 0;
-        for (int k = 0; k < 8; k++) p |= (uint32_t)(k < nl ? list[k] : 7) << (3 * k);
-        w.order[o] = p;
-    }
-    return true;
-}
 static bool quantize_node(const DevCluster& n, DevQNode& q) {
     uint32_t valid = 0;
     for (int k = 0; k < 4; k++)
@@ -827,7 +743,7 @@ struct Conv {
         uint32_t perm = desc.perm < 135 ? desc.perm : 0;
         dc.order[0] = dc.order[1] = 0;
         for (int o = 0; o < 8; o++) dc.order[o >> 2] |= (uint32_t)lut[o][perm] << (8 * (o & 3));
-        dc.pad[0] = perm;  // the topology code itself (PT_Q48 records look the order up)
+        dc.pad[0] = perm;  // the topology code itself (the quantized records look the order up)
         dc.pad[1] = 0;
         for (int k = 0; k < 4; k++) dc.child[k] = REF_EMPTY;
         for (int k = 0; k < 4; k++) {
@@ -841,7 +757,7 @@ struct Conv {
 
 extern "C" pt_status pt_bvh4_order_table(uint8_t* out);
 
-// ---- PT_Q48 records (pt_device.h): every BVH's root gets a record first;
+// ---- quantized 48-B records (pt_device.h): every BVH's root gets a record first;
 // then, depth first from each root, a node's children get one contiguous
 // block (an inner child one record, a leaf child a copy of its slots in leaf
 // order, c.w = the slot) and the node record names them by base + offsets.
@@ -904,21 +820,10 @@ static bool build_q48(const std::vector<DevCluster>& nodes, const std::vector<De
         }
         root_map.push_back({r, qroots[b]});
     }
-    // depth-first (each node's subtree contiguous), except with a treelet
-    // (PT_TREELET, pt_trace.h): breadth-first from the roots until the first
-    // treelet-size records are laid out, so those are the top levels the
-    // pool kernels keep in LDS
-    constexpr uint32_t tree_recs = (uint32_t)std::max(PT_TREELET, PT_TREELET_ANY);
-    size_t head = 0;  // breadth-first cursor into `work`
-    while (head < work.size()) {
-        std::pair<uint32_t, uint32_t> item;
-        if (tree_recs && rec.size() < tree_recs) {
-            item = work[head++];
-        } else {
-            item = work.back();
-            work.pop_back();
-        }
-        const auto [gi, r] = item;
+    // depth-first: each node's subtree contiguous
+    while (!work.empty()) {
+        const auto [gi, r] = work.back();
+        work.pop_back();
         const DevCluster& n = nodes[gi];
         uint32_t size[4] = {0, 0, 0, 0};
         for (int k = 0; k < 4; k++) {
@@ -1143,7 +1048,7 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
         const uint32_t fl = __builtin_bit_cast(uint32_t, geom[i].a.w);
         if ((fl & GF_KIND) != PT_PRIM_TRIANGLE || !(fl & GF_ALPHA)) continue;
         DevAlpha r;
-        const bool fast = PT_ALPHA_RECORDS && alpha_record(s, s->prims[i], r);
+        const bool fast = alpha_record(s, s->prims[i], r);
         geom[i].b.w = __builtin_bit_cast(float, fast ? (uint32_t)alpha.size() : ALPHA_NONE);
         if (fast) alpha.push_back(r);
     }
@@ -1195,7 +1100,7 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
         std::memcpy(D.T, I.transform, sizeof(D.T));
         std::memcpy(D.inv, I.inv, sizeof(D.inv));
         D.root = roots[I.bvh];
-        D.qroot = REF_EMPTY;  // PT_Q48 records: set with them
+        D.qroot = REF_EMPTY;  // the quantized records: set with them
         D.prim_base = s->bvhs[I.bvh].prim_base;
         D.n_prims = s->bvhs[I.bvh].n_prims;
         D.virt_base = I.virt_base;
@@ -1228,25 +1133,13 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     if ((st = upload(c, src, n, &dst)) != PT_OK) return st;
     UP(DS.nodes, nodes.data(), nodes.size());
     {
-#if PT_WIDE
-        // wide nodes take the quantized nodes' place (pt_pool.h, PT_WIDE)
-        std::vector<DevWNode> wn(nodes.size());
-        bool ok = true;
-        for (size_t k = 0; k < nodes.size() && ok; k++) ok = build_wnode(nodes, k, wn[k]);
-        c->has_qnodes = ok;
-        if (ok) {
-            const DevWNode* dw = nullptr;
-            UP(dw, wn.data(), wn.size());
-            DS.qnodes = reinterpret_cast<const DevQNode*>(dw);
-        }
-#elif PT_Q48
         // nodes and leaf slots in one array of 48-B records (pt_device.h)
         std::vector<DevGeom> rec;
         std::vector<uint32_t> qroots;
         bool ok = nodes.size() < REF_BLOCK && s->n_prims < REF_BLOCK &&
                   build_q48(nodes, geom, roots, s->n_prims, rec, qroots);
-        // 32-bit buffer offsets (PT_BUFFER_LOADS) below the out-of-range marker
-        if (PT_BUFFER_LOADS && ok && rec.size() * sizeof(DevGeom) >= (uint64_t)Q48_OOB_OFFSET) ok = false;
+        // 32-bit buffer offsets (pt_pool.h q48_buf_load) below the out-of-range marker
+        if (ok && rec.size() * sizeof(DevGeom) >= (uint64_t)Q48_OOB_OFFSET) ok = false;
         DS.qrec_bytes = ok ? (uint32_t)(rec.size() * sizeof(DevGeom)) : 0u;
         c->has_qnodes = ok;
         if (ok) {
@@ -1259,23 +1152,6 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
                     reinterpret_cast<uint8_t*>(lut.data())[o * Q48_LUT_STRIDE + p] = cv.lut[o][p];
             UP(DS.qlut, lut.data(), lut.size());
         }
-#else
-        std::vector<DevQNode> qn(nodes.size());
-        bool ok = nodes.size() < REF_BLOCK && s->n_prims < REF_BLOCK;
-        for (size_t k = 0; k < nodes.size() && ok; k++) ok = quantize_node(nodes[k], qn[k]);
-        // leaves holding a BLAS hop carry REF_BLOCK (pt_device.h)
-        for (size_t k = 0; k < nodes.size() && ok; k++)
-            for (uint32_t& r : qn[k].child) {
-                if (r == REF_EMPTY || !(r & REF_LEAF) || r >= REF_SPECIAL) continue;
-                for (uint32_t sl = r & ~REF_LEAF; sl < s->n_prims; sl++) {
-                    const uint32_t w = __builtin_bit_cast(uint32_t, geom[sl].a.w);
-                    if ((w & GF_KIND) == PT_PRIM_BLAS) r |= REF_BLOCK;
-                    if (w & GF_LAST) break;
-                }
-            }
-        c->has_qnodes = ok;
-        if (ok) UP(DS.qnodes, qn.data(), qn.size());
-#endif
     }
     UP(DS.geom, geom.data(), geom.size());
     UP(DS.info, info.data(), info.size());
@@ -1298,32 +1174,13 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     UP(DS.materials, s->materials, s->n_materials);
     UP(DS.textures, s->textures, s->n_textures);
     UP(DS.images, s->images, s->n_images);
-    {
-        std::vector<DevTex> tr(s->n_textures);
-        for (uint32_t k = 0; k < s->n_textures; k++) {
-            const pt_texture& t = s->textures[k];
-            DevTex& r = tr[k];
-            r = DevTex{};
-            r.kfc = t.kind;
-            std::memcpy(r.scale, t.scale, sizeof(r.scale));
-            if (t.kind == PT_TEX_SOLID) {
-                std::memcpy(r.u, t.value, sizeof(t.value));
-            } else if (t.kind == PT_TEX_CHECKER) {
-                r.u[0] = (uint32_t)t.a;
-                r.u[1] = (uint32_t)t.b;
-                std::memcpy(&r.u[2], t.inv_scale, sizeof(t.inv_scale));
-            } else {
-                const pt_image& im = s->images[t.image];  // (validated above)
-                if (im.channels < 0 || im.channels > 0xFFFF || im.format < 0 || im.format > 0xFF)
-                    return fail(c, PT_ERR_ARG, "image %d: bad channels / format", t.image);
-                r.kfc |= (uint32_t)im.format << 8 | (uint32_t)im.channels << 16;
-                r.u[0] = (uint32_t)im.offset;
-                r.u[1] = (uint32_t)(im.offset >> 32);
-                r.u[2] = (uint32_t)im.width;
-                r.u[3] = (uint32_t)im.height;
-            }
+    for (uint32_t k = 0; k < s->n_textures; k++) {
+        const pt_texture& t = s->textures[k];
+        if (t.kind != PT_TEX_SOLID && t.kind != PT_TEX_CHECKER) {
+            const pt_image& im = s->images[t.image];  // (validated above)
+            if (im.channels < 0 || im.channels > 0xFFFF || im.format < 0 || im.format > 0xFF)
+                return fail(c, PT_ERR_ARG, "image %d: bad channels / format", t.image);
         }
-        UP(DS.texrec, tr.data(), tr.size());
     }
     // texels: 16 bytes of padding for the word loads of texel_pair_u8
     if ((st = upload(c, s->texels, s->n_texel_bytes, &DS.texels, 16)) != PT_OK) return st;
@@ -1374,7 +1231,7 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
         }
     }
     DS.prim_cell = nullptr;
-    if (PT_SORT_PRIM_CELL && s->n_prims) {  // each primitive's centroid cell, hit_cell's Morton code
+    if (s->n_prims) {  // each primitive's centroid cell, hit_cell's Morton code
         std::vector<uint16_t> cell(s->n_prims, 0);
         auto code = [&](const float* p) {
             uint32_t m = 0;
@@ -1421,18 +1278,10 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     DS.scratch = nullptr;
     DS.scratch_lanes = 0;
     DS.stack_drops = c->stack_drops;
+    DS.tie_drops = c->stack_drops + 1;
     DS.n_materials = s->n_materials;
     DS.n_textures = s->n_textures;
     DS.n_images = s->n_images;
-    DS.lds_tables = 0;
-#if PT_LDS_TABLES
-    // the shading kernels' LDS copies (pt_shading.h stage_tables), where the
-    // scene's tables fit their caps
-    if (s->n_materials <= PT_LDS_MATS) DS.lds_tables |= LDS_MATS;
-    if (s->n_textures <= PT_LDS_TEX) DS.lds_tables |= LDS_TEX;
-    if (s->n_images <= PT_LDS_IMG) DS.lds_tables |= LDS_IMG;
-    if (s->n_sampler_lights <= PT_LDS_CDF) DS.lds_tables |= LDS_LS;
-#endif
     c->has_scene = true;
     c->n_media = s->n_media;
     c->n_materials = s->n_materials;
@@ -1474,24 +1323,12 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
     }
     for (PathSoA* P : {&c->PA, &c->PB}) {
         P->cap = (uint32_t)n;
-        if (PT_PATH_AOS == 1) {  // one 64-B record per path (pt_kernels.h PathSoA)
-            AL(P->o.p, n * 64);
-            P->d.p = P->o.p + 1;
-            P->beta.p = P->o.p + 2;
-            P->L.p = P->o.p + 3;
-        } else if (PT_PATH_AOS == 2) {  // {o, d} and {beta, L}: two 32-B records per path
-            AL(P->o.p, n * 32);
-            P->d.p = P->o.p + 1;
-            AL(P->beta.p, n * 32);
-            P->L.p = P->beta.p + 1;
-        } else {
-            AL(P->o.p, n * 16);
-            AL(P->d.p, n * 16);
-            AL(P->beta.p, n * 16);
-            AL(P->L.p, n * 16);
-        }
+        // {o, d} and {beta, L}: two 32-B records per path (pt_kernels.h PathSoA)
+        AL(P->o.p, n * 32);
+        P->d.p = P->o.p + 1;
+        AL(P->beta.p, n * 32);
+        P->L.p = P->beta.p + 1;
         AL(P->sid, n * 4);
-        if (PT_PATH_INV) AL(P->inv, n * 16);
     }
     AL(c->hit, n * 16);
     AL(c->ties, n * 4);  // a ray is listed at most once per launch
@@ -1501,15 +1338,14 @@ static pt_status ensure_work(pt_ctx* c, uint32_t cap) {
     AL(c->counters, (CNT_SHARDS + 1) * CNT_COUNT * 8);
     // stack entries past the LDS part: the pool kernels' resident grid x
     // (PT_POOL_STACK - their smaller LDS part); the one-ray-per-lane kernels
-    // keep their whole stack in LDS unless a tuning build splits it, and then
+    // keep their whole stack in LDS unless PT_SIMPLE_LN splits it, and then
     // the array covers their grid (the capacity) too
-    // (refs, then as many entry distances: PT_OVF_WORDS words per entry)
     {
-        constexpr bool simple_ovf = PT_SIMPLE_STEP || PT_SIMPLE_LN < PT_STACK;
-        constexpr int ovf_entries = PT_POOL_STACK - std::min({PT_POOL_LDS, PT_POOL_LDS_C, PT_SIMPLE_LDS});
+        constexpr bool simple_ovf = PT_SIMPLE_LN < PT_STACK;
+        constexpr int ovf_entries = PT_POOL_STACK - std::min(PT_POOL_LDS, PT_SIMPLE_LN);
         size_t lanes = (size_t)c->trace_blocks * PT_TRACE_BLOCK;
         if (simple_ovf) lanes = std::max<size_t>(lanes, (n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK * PT_TRACE_BLOCK);
-        const size_t half = lanes * ovf_entries * PT_OVF_WORDS;
+        const size_t half = lanes * ovf_entries;
         AL(c->ovf, 2 * half * 4);
         c->ovf_any = c->ovf + half;
     }
@@ -1734,7 +1570,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     const bool sort_mat = (rd->flags & PT_RENDER_SORT_MATERIAL) != 0;
     const bool sort_sp = !sort_mat && !(rd->flags & PT_RENDER_NO_SORT) &&
                          ((rd->flags & PT_RENDER_SORT_SPATIAL) || big_scene);
-    const bool keep_bins = PT_SORT_KEEP_BINS && (sort_mat || sort_sp || sort_rays);
+    const bool keep_bins = sort_mat || sort_sp || sort_rays;
     // every buffer sized by the path count — the wavefront, the claim / hit
     // orders and bins, the instance scratch — is allocated in one step, and a
     // device short of HBM (or a second context on it) retries the whole step
@@ -1760,20 +1596,15 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     }
     if (st) return st;
     c->scene.ray_order = sort_rays ? c->ray_order : nullptr;
-    // the spatial hit sort's bins come from the closest-hit pool kernel
-    c->scene.hit_bins = (PT_HIT_BINS && sort_sp && keep_bins && use_pool) ? c->sort_bins : nullptr;
-    struct ResetOrder {  // other entry points bind the scene without a claim order or hit bins
+    struct ResetOrder {  // other entry points bind the scene without a claim order
         pt_ctx* c;
-        ~ResetOrder() {
-            c->scene.ray_order = nullptr;
-            c->scene.hit_bins = nullptr;
-        }
+        ~ResetOrder() { c->scene.ray_order = nullptr; }
     } reset_order{c};
     if ((st = bind_scene(c)) != PT_OK) return st;
     uint16_t* bins = keep_bins ? c->sort_bins : nullptr;  // (shared by the claim-order and hit sorts: each pass pair runs in turn on sm)
     hipStream_t sm = c->stream;
     HIPCHK(c, hipMemsetAsync(c->counters, 0, (CNT_SHARDS + 1) * CNT_COUNT * 8, sm));
-    HIPCHK(c, hipMemsetAsync(c->stack_drops, 0, 4, sm));
+    HIPCHK(c, hipMemsetAsync(c->stack_drops, 0, 8, sm));  // stack and tie drops
     // the sample-id counter sits on its own line after the work-counter shards
     unsigned long long* next_sample = c->counters + CNT_SHARDS * CNT_COUNT + CNT_NEXT_SAMPLE;
     float t_cl = 0, t_sh = 0, t_an = 0;
@@ -1941,10 +1772,6 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                 hipLaunchKernelGGL(ks, ga, dim3(PT_TRACE_BLOCK), 0, sa, nxt, c->sample_L, c->sq,
                                    (const uint32_t*)(out + Q_SHADOW), out + Q_WORDS + PT_POOL_WORDS,
                                    ovl ? c->ovf_any : c->ovf, c->counters);
-                if (use_pool && PT_SHADOW_DEFER)  // the unoccluded rays' contributions (k_shadow_pool defers them)
-                    hipLaunchKernelGGL(k_shadow_apply, dim3(std::max(1u, std::min(2048u, (nb + 255) / 256))),
-                                       dim3(256), 0, sa, nxt, c->sample_L, (const ShadowRec*)c->sq,
-                                       (const uint32_t*)(out + Q_SHADOW));
             }
             HIPCHK(c, hipGetLastError());
             HIPCHK(c, hipEventRecord(ev[4], sa));
@@ -1970,32 +1797,6 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             if ((st = consume()) != PT_OK) return st;
         if (ovl && issued) HIPCHK(c, hipStreamWaitEvent(sm, c->rev[(issued - 1) % PT_RING][4], 0));
 
-#if PT_ITER_STATS
-        {
-            unsigned long long it[2][15];
-            HIPCHK(c, hipMemcpyFromSymbol(it, HIP_SYMBOL(pt_iter), sizeof(it)));
-            for (int a = 0; a < 2; a++)
-                fprintf(stderr, "pt_iter %s: iters %llu refill %llu step %llu with_node %llu with_prim %llu "
-                        "node_lanes %llu prim_lanes %llu pops %llu uniform_node %llu uniform_prim %llu "
-                        "fresh %llu with_alpha %llu alpha_lanes %llu with_other %llu alpha_first_slot %llu\n",
-                        a ? "any" : "closest", it[a][0], it[a][1], it[a][2], it[a][3], it[a][4], it[a][5], it[a][6],
-                        it[a][7], it[a][8], it[a][9], it[a][10], it[a][11], it[a][12], it[a][13], it[a][14]);
-            const unsigned long long z[2][15] = {};
-            HIPCHK(c, hipMemcpyToSymbol(HIP_SYMBOL(pt_iter), z, sizeof(z)));
-        }
-#endif
-#if PT_POOL_CHECK
-        {
-            unsigned int dg[4];
-            HIPCHK(c, hipMemcpyFromSymbol(dg, HIP_SYMBOL(pt_diag), sizeof(dg)));
-            if (dg[0] | dg[1] | dg[2] | dg[3]) {
-                fprintf(stderr, "pt_diag: use_pool %d bad_ref %u bad_prim %u unwritten_hit %u dropped_push %u\n",
-                        (int)use_pool, dg[0], dg[1], dg[2], dg[3]);
-                const unsigned int z[4] = {0, 0, 0, 0};
-                HIPCHK(c, hipMemcpyToSymbol(HIP_SYMBOL(pt_diag), z, sizeof(z)));
-            }
-        }
-#endif
         if (stats) stats->paths += R.chunk_total;
         return PT_OK;
     };
@@ -2022,9 +1823,10 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
         stats->ms_closest += t_cl;
         stats->ms_shade += t_sh;
         stats->ms_any += t_an;
-        uint32_t drops = 0;
-        HIPCHK(c, hipMemcpy(&drops, c->stack_drops, 4, hipMemcpyDeviceToHost));
-        stats->stack_overflows += drops;
+        uint32_t drops[2] = {0, 0};
+        HIPCHK(c, hipMemcpy(drops, c->stack_drops, 8, hipMemcpyDeviceToHost));
+        stats->stack_overflows += drops[0];
+        stats->tie_overflows += drops[1];
         stats->n_devices = 1;
     }
     return PT_OK;
@@ -2301,6 +2103,7 @@ static pt_status render_multi(pt_ctx* c, const pt_camera_desc* cam, const pt_ren
             S.launches_closest += x.launches_closest;
             S.launches_any += x.launches_any;
             S.stack_overflows += x.stack_overflows;
+            S.tie_overflows += x.tie_overflows;
             S.ms_closest = std::max(S.ms_closest, x.ms_closest);
             S.ms_any = std::max(S.ms_any, x.ms_any);
             S.ms_shade = std::max(S.ms_shade, x.ms_shade);
@@ -2487,7 +2290,7 @@ extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any
     if (c->cap == 0 && ensure_work(c, 256) != PT_OK) return PT_ERR_OOM;
     if (pt_status bs = bind_scene(c)) return bs;
     HIPCHK(c, hipMemsetAsync(c->counters, 0, CNT_SHARDS * CNT_COUNT * 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->stack_drops, 0, 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->stack_drops, 0, 8, c->stream));  // stack and tie drops
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(c, hipEventRecord(c->ev[4], c->stream));
     uint32_t* pool = c->qcnt + 3 * SET_WORDS;
@@ -2530,9 +2333,10 @@ extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any
             stats->tris_closest = h[CNT_TRIS_CLOSEST];
             stats->ms_closest = ms;
         }
-        uint32_t drops = 0;
-        HIPCHK(c, hipMemcpy(&drops, c->stack_drops, 4, hipMemcpyDeviceToHost));
-        stats->stack_overflows = drops;
+        uint32_t drops[2] = {0, 0};
+        HIPCHK(c, hipMemcpy(drops, c->stack_drops, 8, hipMemcpyDeviceToHost));
+        stats->stack_overflows = drops[0];
+        stats->tie_overflows = drops[1];
         stats->n_devices = 1;
         stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
@@ -2625,6 +2429,32 @@ extern "C" pt_status pt_light_picks(pt_ctx* c, const float* u, uint32_t n, int32
                         hipLaunchKernelGGL(k_light_picks, dim3((n + 255) / 256), dim3(256), 0, c->stream,
                                            (const float*)din, n, reinterpret_cast<int32_t*>(dout));
                     });
+}
+
+extern "C" pt_status pt_anim_inverse_cases(pt_ctx* c, const float* t, uint32_t n, float* out) {
+    if (!c) return PT_ERR_ARG;
+    DeviceLock dl(c->device);
+    if (n && (!t || !out)) return PT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (n == 0) return PT_OK;
+    float *dt = nullptr, *dout = nullptr;
+    if (hipMalloc((void**)&dt, (size_t)n * 12) != hipSuccess) return fail(c, PT_ERR_OOM, "hook input");
+    if (hipMalloc((void**)&dout, (size_t)n * 64) != hipSuccess) {
+        hipFree(dt);
+        return fail(c, PT_ERR_OOM, "hook output");
+    }
+    pt_status st = PT_OK;
+    if (hipMemcpyAsync(dt, t, (size_t)n * 12, hipMemcpyHostToDevice, c->stream) != hipSuccess) st = PT_ERR_HIP;
+    if (st == PT_OK) {
+        hipLaunchKernelGGL(k_anim_inverse, dim3((n + 255) / 256), dim3(256), 0, c->stream, (const float*)dt, n, dout);
+        if (hipGetLastError() != hipSuccess) st = PT_ERR_HIP;
+    }
+    if (st == PT_OK && hipMemcpyAsync(out, dout, (size_t)n * 64, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        st = PT_ERR_HIP;
+    if (st == PT_OK && hipStreamSynchronize(c->stream) != hipSuccess) st = PT_ERR_HIP;
+    hipFree(dt);
+    hipFree(dout);
+    return st == PT_OK ? PT_OK : fail(c, st, "anim_inverse hook failed");
 }
 
 // Device BVH build (pt_bvh4_build_device)

@@ -10,88 +10,21 @@ struct SurfInt {  // SurfaceInteraction (Interaction.hpp:36-51)
     float u, v;  // uv
     float t;
     int32_t mat, light;
-    bool nm_pending = false;  // the material's normal map not applied yet (mat_tex applies it)
 };
 
-// ------------------------------------------------------------------ LDS-staged tables
-// PT_LDS_TABLES (A/B option): the shading kernels (k_shade, k_shade_vol and
-// the hooks that shade) copy the material, texture and image records and the
-// light sampler's guide table and running sums into LDS once per block
-// (stage_tables), and the shading path reads them there instead of through
-// L1/L2 gathers.  Tables past their caps stay in global memory (DevScene::
-// lds_tables).  The traversal kernels' alpha test keeps global reads (their
-// LDS holds the traversal stacks).
-#ifndef PT_LDS_TABLES
-#define PT_LDS_TABLES 0
-#endif
-#if PT_LDS_TABLES
-__shared__ pt_material pt_lds_mat[PT_LDS_MATS];
-__shared__ pt_texture pt_lds_tex[PT_LDS_TEX];
-__shared__ pt_image pt_lds_img[PT_LDS_IMG];
-#if PT_LDS_TABLES >= 2  // 2: the light sampler's tables too
-__shared__ uint32_t pt_lds_guide[PT_LS_GUIDE + 1];
-__shared__ float pt_lds_cdf[PT_LDS_CDF];
-#endif
-template <class T>
-__device__ __forceinline__ void stage_words(T* dst, const T* src, uint32_t n) {
-    static_assert(sizeof(T) % 4 == 0, "word copy");
-    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
-    const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
-    const uint32_t w = n * (uint32_t)(sizeof(T) / 4);
-    for (uint32_t i = threadIdx.x; i < w; i += blockDim.x) d[i] = s[i];
-}
-#endif
-// Every thread of the block calls it, before any shading (barrier).
-__device__ __forceinline__ void stage_tables(bool light_sampler) {
-#if PT_LDS_TABLES
-    const uint32_t f = S.lds_tables;
-    if (f & LDS_MATS) stage_words(pt_lds_mat, S.materials, S.n_materials);
-    if (f & LDS_TEX) stage_words(pt_lds_tex, S.textures, S.n_textures);
-    if (f & LDS_IMG) stage_words(pt_lds_img, S.images, S.n_images);
-#if PT_LDS_TABLES >= 2
-    // staged by every staging kernel, whatever it says it samples: ls_sample
-    // reads them whenever LDS_LS is set (light_sampler only documents)
-    (void)light_sampler;
-    if ((f & LDS_LS) && S.light_sampler != PT_LS_UNIFORM && S.n_sampler_lights) {
-        stage_words(pt_lds_guide, S.sampler_guide, PT_LS_GUIDE + 1);
-        stage_words(pt_lds_cdf, S.sampler_cdf, S.n_sampler_lights);
-    }
-#else
-    (void)light_sampler;
-#endif
-    __syncthreads();
-#else
-    (void)light_sampler;
-#endif
-}
-// shading-path table reads (only from kernels that ran stage_tables)
-__device__ __forceinline__ pt_material mat_rec(int mid) {
-#if PT_LDS_TABLES
-    if (S.lds_tables & LDS_MATS) return pt_lds_mat[mid];
-#endif
-    return S.materials[mid];
-}
-__device__ __forceinline__ pt_texture tex_rec(int id) {
-#if PT_LDS_TABLES
-    if (S.lds_tables & LDS_TEX) return pt_lds_tex[id];
-#endif
-    return S.textures[id];
-}
-__device__ __forceinline__ pt_image img_rec(int id) {
-#if PT_LDS_TABLES
-    if (S.lds_tables & LDS_IMG) return pt_lds_img[id];
-#endif
-    return S.images[id];
-}
+// ------------------------------------------------------------------ table reads
+// (LDS copies of the material / texture / image / light-sampler tables were
+// measured slower: the reads are L1/L2 hits and each block waits for its
+// staging behind a barrier, profiles/r03_ab_lds_tables.txt)
+__device__ __forceinline__ pt_material mat_rec(int mid) { return S.materials[mid]; }
+__device__ __forceinline__ pt_texture tex_rec(int id) { return S.textures[id]; }
+__device__ __forceinline__ pt_image img_rec(int id) { return S.images[id]; }
 
 // ------------------------------------------------------------------ textures
-// The non-negative remainder by the float reciprocal (PT_WRAP_RCP, A/B): for
+// The non-negative remainder by the float reciprocal: for
 // |i| < 2^20 the product i * rcp(n) (rcp within 1 ulp) is within 1/4 of i / n,
 // so floor() is off by at most one and one correction each way gives the
 // exact remainder; other lanes take the integer division.
-#ifndef PT_WRAP_RCP
-#define PT_WRAP_RCP 1
-#endif
 __device__ __forceinline__ int wrap_rcp(int i, int n) {
     const float q = floorf((float)i * __builtin_amdgcn_rcpf((float)n));
     int m = i - (int)q * n;
@@ -99,21 +32,13 @@ __device__ __forceinline__ int wrap_rcp(int i, int n) {
     m -= m >= n ? n : 0;
     return m;
 }
-// the traversal's alpha test (PT_WRAP_RCP): the reciprocal form where it is exact
+// the traversal's alpha test: the reciprocal form where it is exact
 __device__ __forceinline__ int wrap_index(int i, int n);
 __device__ __forceinline__ int wrap_index_t(int i, int n) {
-#if PT_WRAP_RCP
     if ((uint32_t)i + (1u << 20) < (2u << 20)) return wrap_rcp(i, n);
-#endif
     return wrap_index(i, n);
 }
 __device__ __forceinline__ int wrap_index(int i, int n) {
-    // a power-of-two size: the low bits are the non-negative remainder (two's
-    // complement), no integer division
-#ifndef PT_WRAP_POW2
-#define PT_WRAP_POW2 0
-#endif
-    if (PT_WRAP_POW2 && (n & (n - 1)) == 0) return i & (n - 1);
     int m = i % n;
     if (m < 0) m += n;
     return m;
@@ -124,9 +49,6 @@ __device__ __forceinline__ int wrap_index(int i, int n) {
 // tests/test_libmf.py) in 3 VALU instead of a division's ~11
 __device__ __forceinline__ float u8_unit(uint32_t b) {
     const float x = (float)b, r = 1.0f / 255.0f;
-#ifdef PT_U8_DIV  // A/B builds: the division itself
-    return x / 255.0f;
-#endif
     const float q = x * r;
     return fma_(fma_(-q, 255.0f, x), r, q);
 }
@@ -253,227 +175,7 @@ __device__ f3 tex_eval_t(int id, float u, float v) {
     return F3(0, 0, 0);
 }
 
-// Two textures of one hit evaluated together (PT_TEX_JOINT): each chain is
-// resolved to its leaf (records only), then the u8 RGB / RGBA image leaves'
-// footprints are read with all their word loads in flight at once, then
-// decoded -- one memory round trip for both lookups instead of one each.
-// Values are tex_eval's: the same texels, the same arithmetic.
-#ifndef PT_TEX_JOINT
-#define PT_TEX_JOINT 0
-#endif
-#ifndef PT_NM_DEFER  // the normal map joins the material's textures in mat_tex
-#define PT_NM_DEFER 1
-#endif
-struct TexLeaf {
-    bool image;  // else a solid value in `val`
-    bool scaled;
-    f3 scale;    // the checkers' colorScales, multiplied outward-in
-    f3 val;      // SOLID: the value; IMAGE: the texture's colorScale
-    int image_id;
-};
-__device__ __forceinline__ TexLeaf tex_resolve(int id, float u, float v) {
-    TexLeaf r;
-    r.image = false;
-    r.scaled = false;
-    r.scale = F3(1, 1, 1);
-    r.val = F3(0, 0, 0);
-    r.image_id = -1;
-    for (int guard = 0; guard < 16; guard++) {
-        const pt_texture t = tex_rec(id);
-        if (t.kind == PT_TEX_SOLID) {
-            r.val = ld3(t.value);
-            return r;
-        }
-        if (t.kind == PT_TEX_CHECKER) {
-            int ux = (int)floorf(u * t.inv_scale[0]);
-            int uy = (int)floorf(v * t.inv_scale[1]);
-            r.scale = r.scaled ? r.scale * ld3(t.scale) : ld3(t.scale);
-            r.scaled = true;
-            id = ((ux + uy) % 2 == 0) ? t.a : t.b;
-            continue;
-        }
-        r.image = true;
-        r.val = ld3(t.scale);
-        r.image_id = t.image;
-        return r;
-    }
-    r.val = F3(0, 0, 0);  // (a chain deeper than the guard: tex_eval's zero)
-    r.scaled = false;
-    return r;
-}
-// an image leaf's bilinear footprint: coordinates, and the quad's six words
-// once issued (ok: the u8 RGB / RGBA fast form applies)
-struct TexQuad {
-    float dx, dy;
-    int x0, x1, y0, y1;
-    bool ok;
-    uint32_t sh0, sh1;
-    const uint32_t* w;
-    const uint32_t* vrow;
-};
-__device__ __forceinline__ TexQuad tex_quad_addr(const pt_image& im, float u, float v) {
-    TexQuad q;
-    const float x = u * im.width - 0.5f, y = v * im.height - 0.5f;
-    const int xi = (int)floorf(x), yi = (int)floorf(y);
-    q.dx = x - xi;
-    q.dy = y - yi;
-    q.x0 = wrap_index(xi, im.width);
-    q.x1 = wrap_next(q.x0, im.width);
-    q.y0 = wrap_index(yi, im.height);
-    q.y1 = wrap_next(q.y0, im.height);
-    const int C = im.channels;
-    q.ok = im.format == PT_IMAGE_U8 && (C == 3 || C == 4) && q.x0 + 1 < im.width;
-    const uint64_t i0 = im.offset + ((uint64_t)q.y0 * (uint64_t)im.width + (uint64_t)q.x0) * (uint64_t)C;
-    const uint64_t i1 = im.offset + ((uint64_t)q.y1 * (uint64_t)im.width + (uint64_t)q.x0) * (uint64_t)C;
-    q.ok = q.ok && i0 + 2u * (uint64_t)C <= S.n_texel_bytes && i1 + 2u * (uint64_t)C <= S.n_texel_bytes;
-    // (a lane off the fast form reads the buffer's first words; unused)
-    q.w = reinterpret_cast<const uint32_t*>(S.texels + (q.ok ? (i0 & ~3ull) : 0ull));
-    q.vrow = reinterpret_cast<const uint32_t*>(S.texels + (q.ok ? (i1 & ~3ull) : 0ull));
-    q.sh0 = (uint32_t)(i0 & 3u);
-    q.sh1 = (uint32_t)(i1 & 3u);
-    return q;
-}
-__device__ __forceinline__ void tex_quad_decode(int C, uint32_t r0, uint32_t r1, uint32_t r2, uint32_t sh, f3& p,
-                                                f3& q) {
-    const uint32_t q0 = __builtin_amdgcn_alignbyte(r1, r0, sh), q1 = __builtin_amdgcn_alignbyte(r2, r1, sh);
-    const uint32_t qb = C == 4 ? q1 : __builtin_amdgcn_alignbyte(q1, q0, 3u);
-    auto ch = [](uint32_t x, int k) { return u8_unit((x >> (8 * k)) & 0xFFu); };
-    p = F3(ch(q0, 0), ch(q0, 1), ch(q0, 2));
-    q = F3(ch(qb, 0), ch(qb, 1), ch(qb, 2));
-}
-__device__ __forceinline__ f3 tex_bilerp(const TexLeaf& L, float dx, float dy, f3 a, f3 b, f3 c, f3 d) {
-    // contraction of the reference build: w_a*a rounded, then fma(w_b, b), fma(w_c, c), fma(w_d, d)
-    float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
-    f3 r = F3(fma_(wd, d.x, fma_(wc, c.x, fma_(wb, b.x, rmul(wa, a.x)))),
-              fma_(wd, d.y, fma_(wc, c.y, fma_(wb, b.y, rmul(wa, a.y)))),
-              fma_(wd, d.z, fma_(wc, c.z, fma_(wb, b.z, rmul(wa, a.z)))));
-    r = L.val * r;
-    return L.scaled ? L.scale * r : r;
-}
-__device__ __forceinline__ f3 tex_leaf_slow(const TexLeaf& L, const TexQuad& q) {
-    const pt_image im = img_rec(L.image_id);
-    const f3 a = texel3_w(im, q.x0, q.y0), b = texel3_w(im, q.x1, q.y0);
-    const f3 c = texel3_w(im, q.x0, q.y1), d = texel3_w(im, q.x1, q.y1);
-    return tex_bilerp(L, q.dx, q.dy, a, b, c, d);
-}
-template <int N>
-__device__ __forceinline__ void tex_eval_n(const int (&ids)[N], float u, float v, f3 (&out)[N]) {
-    TexLeaf L[N];
-    TexQuad q[N];
-    int ch[N];
-#pragma unroll
-    for (int k = 0; k < N; k++) {
-        L[k] = tex_resolve(ids[k], u, v);
-        q[k].ok = false;
-        ch[k] = 0;
-        if (L[k].image) {
-            const pt_image im = img_rec(L[k].image_id);
-            q[k] = tex_quad_addr(im, u, v);
-            ch[k] = im.channels;
-        }
-    }
-    // every footprint's words in flight together
-    uint32_t w[N][6];
-#pragma unroll
-    for (int k = 0; k < N; k++) {
-        w[k][0] = w[k][1] = w[k][2] = w[k][3] = w[k][4] = w[k][5] = 0u;
-        if (q[k].ok) {
-            w[k][0] = q[k].w[0], w[k][1] = q[k].w[1], w[k][2] = q[k].w[2];
-            w[k][3] = q[k].vrow[0], w[k][4] = q[k].vrow[1], w[k][5] = q[k].vrow[2];
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < N; k++) {
-        if (!L[k].image) {
-            out[k] = L[k].scaled ? L[k].scale * L[k].val : L[k].val;
-        } else if (q[k].ok) {
-            f3 a, b, c, d;
-            tex_quad_decode(ch[k], w[k][0], w[k][1], w[k][2], q[k].sh0, a, b);
-            tex_quad_decode(ch[k], w[k][3], w[k][4], w[k][5], q[k].sh1, c, d);
-            out[k] = tex_bilerp(L[k], q[k].dx, q[k].dy, a, b, c, d);
-        } else {
-            out[k] = tex_leaf_slow(L[k], q[k]);
-        }
-    }
-}
-
-// PT_TEXREC (A/B option, off): the shading path reads DevTex records.  C4:
-// k_shade 1362 -> 1370 ms per frame with them (profiles/r04_ab_alpha.txt):
-// the texture and image records are L1/L2 hits, the hop they save is not
-// what the shading waits on
-#ifndef PT_TEXREC
-#define PT_TEXREC 0
-#endif
-// The same over DevTex records (shading path without LDS tables): the
-// texture's record is its image's too, and a caller may load the records of
-// a material's textures together before evaluating any of them.
-__device__ __forceinline__ DevTex tex_full(int id) {
-    const float4* p = reinterpret_cast<const float4*>(S.texrec + id);
-    const float4 a = p[0], b = p[1];
-    DevTex t;
-    t.kfc = __float_as_uint(a.x);
-    t.scale[0] = a.y;
-    t.scale[1] = a.z;
-    t.scale[2] = a.w;
-    t.u[0] = __float_as_uint(b.x);
-    t.u[1] = __float_as_uint(b.y);
-    t.u[2] = __float_as_uint(b.z);
-    t.u[3] = __float_as_uint(b.w);
-    return t;
-}
-__device__ __forceinline__ f3 tex_eval_r(DevTex t, float u, float v) {
-    f3 scale = F3(1, 1, 1);
-    bool scaled = false;
-    for (int guard = 0; guard < 16; guard++) {
-        const uint32_t kind = t.kfc & 0xFFu;
-        if (kind == PT_TEX_SOLID) {
-            f3 c = F3(__uint_as_float(t.u[0]), __uint_as_float(t.u[1]), __uint_as_float(t.u[2]));
-            return scaled ? scale * c : c;
-        }
-        if (kind == PT_TEX_CHECKER) {
-            int ux = (int)floorf(u * __uint_as_float(t.u[2]));
-            int uy = (int)floorf(v * __uint_as_float(t.u[3]));
-            scale = scaled ? scale * ld3(t.scale) : ld3(t.scale);
-            scaled = true;
-            t = tex_full(((ux + uy) % 2 == 0) ? (int)t.u[0] : (int)t.u[1]);
-            continue;
-        }
-        pt_image im;
-        im.offset = (uint64_t)t.u[0] | (uint64_t)t.u[1] << 32;
-        im.width = (int32_t)t.u[2];
-        im.height = (int32_t)t.u[3];
-        im.channels = (int32_t)(t.kfc >> 16);
-        im.format = (int32_t)((t.kfc >> 8) & 0xFFu);
-        float x = u * im.width - 0.5f;
-        float y = v * im.height - 0.5f;
-        int xi = (int)floorf(x), yi = (int)floorf(y);
-        float dx = x - xi, dy = y - yi;
-        const int x0 = wrap_index(xi, im.width), x1 = wrap_next(x0, im.width);
-        const int y0 = wrap_index(yi, im.height), y1 = wrap_next(y0, im.height);
-        f3 a, b, c, d;
-        if (!texel_quad_u8(im, x0, y0, y1, a, b, c, d)) {
-            a = texel3_w(im, x0, y0);
-            b = texel3_w(im, x1, y0);
-            c = texel3_w(im, x0, y1);
-            d = texel3_w(im, x1, y1);
-        }
-        float wa = (1 - dx) * (1 - dy), wb = dx * (1 - dy), wc = (1 - dx) * dy, wd = dx * dy;
-        f3 r = F3(fma_(wd, d.x, fma_(wc, c.x, fma_(wb, b.x, rmul(wa, a.x)))),
-                  fma_(wd, d.y, fma_(wc, c.y, fma_(wb, b.y, rmul(wa, a.y)))),
-                  fma_(wd, d.z, fma_(wc, c.z, fma_(wb, b.z, rmul(wa, a.z)))));
-        r = ld3(t.scale) * r;
-        return scaled ? scale * r : r;
-    }
-    return F3(0, 0, 0);
-}
-
-__device__ __forceinline__ f3 tex_eval(int id, float u, float v) {
-#if PT_LDS_TABLES || !PT_TEXREC
-    return tex_eval_t<true>(id, u, v);
-#else
-    return tex_eval_r(tex_full(id), u, v);
-#endif
-}
+__device__ __forceinline__ f3 tex_eval(int id, float u, float v) { return tex_eval_t<true>(id, u, v); }
 
 // Texture::alpha (Texture.hpp:112-114, Texture.cpp:47-62, 41-45)
 __device__ float tex_alpha(int id, float u, float v) {
@@ -591,7 +293,7 @@ __device__ __forceinline__ void sphere_uv(f3 p, float& u, float& v) { sphere_uv_
 // barycentrics; identical to computing it at the candidate (the reference does
 // it per candidate, only the last accepted survives).
 __device__ void tri_interaction(const DevGeom& g, uint32_t tri, int mid, f3 o, f3 d, float t,
-                                float bu, float bv, SurfInt& si, bool nm = true) {
+                                float bu, float bv, SurfInt& si) {
     // one shading record (DevTriShade) instead of S.tri + the indexed
     // normals / uvs / tangents: the same values, the same arithmetic
     const DevTriShade* R = S.tshade + tri;
@@ -623,10 +325,7 @@ __device__ void tri_interaction(const DevGeom& g, uint32_t tri, int mid, f3 o, f
         f3 up = (fabsf(si.ns.x) > 0.9999f) ? F3(0, 1, 0) : F3(1, 0, 0);
         si.tangent = normalize(cross(up, si.ns));
     }
-    // (nm false: mat_tex applies the normal map with the material's other
-    // textures, their texel loads in flight together)
-    if (nm) si.ns = normal_map(mid, si);
-    else si.nm_pending = true;
+    si.ns = normal_map(mid, si);
 }
 
 // QuadShape::Intersect (Shape.cpp:320-343) interaction part.
@@ -770,8 +469,6 @@ struct MatTex {
 };
 __device__ __forceinline__ MatTex mat_tex(int mid, SurfInt& si) {
     const pt_material m = mat_rec(mid);
-    const bool nm = si.nm_pending;
-    si.nm_pending = false;
     MatTex t;
     t.kind = m.kind;
     t.ri = m.ri;
@@ -779,55 +476,14 @@ __device__ __forceinline__ MatTex mat_tex(int mid, SurfInt& si) {
     t.metal = 0.0f;
     switch (m.kind) {
         case PT_MAT_DIFFUSE: {
-#if PT_TEX_JOINT && (PT_LDS_TABLES || !PT_TEXREC)
-            if (nm && m.norm >= 0) {  // sample_normalMap (Material.hpp:344-348) with the others
-                f3 r[3];
-                tex_eval_n<3>({m.tex, m.rough, m.norm}, si.u, si.v, r);
-                t.col = r[0];
-                t.rough = smax(r[1].y, 0.0001f);
-                si.ns = to_world_nm(onb_si(si), normalize(2.0f * r[2] - F3(1, 1, 1)));
-            } else {
-                f3 r[2];
-                tex_eval_n<2>({m.tex, m.rough}, si.u, si.v, r);
-                t.col = r[0];
-                t.rough = smax(r[1].y, 0.0001f);
-            }
-            t.metal = tex_eval(m.metal, si.u, si.v).z;
-#elif PT_LDS_TABLES || !PT_TEXREC
             t.rough = smax(tex_eval(m.rough, si.u, si.v).y, 0.0001f);
             t.metal = tex_eval(m.metal, si.u, si.v).z;
             t.col = tex_eval(m.tex, si.u, si.v);
-#else
-            // the three records read together, then evaluated
-            const DevTex tr = tex_full(m.rough), tm = tex_full(m.metal), tc = tex_full(m.tex);
-            t.rough = smax(tex_eval_r(tr, si.u, si.v).y, 0.0001f);
-            t.metal = tex_eval_r(tm, si.u, si.v).z;
-            t.col = tex_eval_r(tc, si.u, si.v);
-#endif
             break;
         }
         case PT_MAT_DIELECTRIC: {
-#if PT_TEX_JOINT && (PT_LDS_TABLES || !PT_TEXREC)
-            if (nm && m.norm >= 0) {
-                f3 r[3];
-                tex_eval_n<3>({m.tex, m.rough, m.norm}, si.u, si.v, r);
-                t.col = r[0];
-                t.rough = r[1].y;
-                si.ns = to_world_nm(onb_si(si), normalize(2.0f * r[2] - F3(1, 1, 1)));
-            } else {
-                f3 r[2];
-                tex_eval_n<2>({m.tex, m.rough}, si.u, si.v, r);
-                t.col = r[0];
-                t.rough = r[1].y;
-            }
-#elif PT_LDS_TABLES || !PT_TEXREC
             t.rough = tex_eval(m.rough, si.u, si.v).y;
             t.col = tex_eval(m.tex, si.u, si.v);
-#else
-            const DevTex tr = tex_full(m.rough), tc = tex_full(m.tex);
-            t.rough = tex_eval_r(tr, si.u, si.v).y;
-            t.col = tex_eval_r(tc, si.u, si.v);
-#endif
             break;
         }
         case PT_MAT_THIN: t.col = tex_eval(m.tex, si.u, si.v); break;
@@ -1552,18 +1208,6 @@ __device__ int ls_sample(float u) {
     // [guide[b], guide[b + 1]): target >= fl(b / K * total) because u >= b / K
     // and rounding is monotone, and target <= fl((b + 1) / K * total)
     const uint32_t b = min((uint32_t)(u * (float)PT_LS_GUIDE), PT_LS_GUIDE - 1u);
-#if PT_LDS_TABLES >= 2
-    if (S.lds_tables & LDS_LS) {  // staged by the calling kernel (stage_tables)
-        uint32_t lo = pt_lds_guide[b], hi = pt_lds_guide[b + 1];
-        while (lo < hi) {
-            uint32_t mid = (lo + hi) >> 1;
-            if (pt_lds_cdf[mid] >= target) hi = mid;
-            else lo = mid + 1;
-        }
-        if (lo >= n) lo = n - 1;
-        return (int)S.sampler_lights[lo];
-    }
-#endif
     uint32_t lo = S.sampler_guide[b], hi = S.sampler_guide[b + 1];
     while (lo < hi) {
         uint32_t mid = (lo + hi) >> 1;

@@ -59,70 +59,6 @@ __device__ __forceinline__ bool tri_pred(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float 
     return t <= tmax && t >= PT_EPS;
 }
 
-// The same two tests on the packed-FP32 ALU (PT_TRI_PK): the x / y lanes of
-// each cross product and each pair of dot products sharing a vector run as
-// one v_pk_mul / v_pk_fma, every lane rounding as the scalar form does
-// (cross: fma(a.y, b.z, -round(b.y * a.z)) ...; dot: fma(z, z, fma(y, y,
-// round(x * x)))), so the results are bit-identical.  Off: the operand pairs
-// need moves into adjacent registers, and the packed build ran the closest-hit
-// kernel 13 % slower (profiles/r05_ab_traversal.txt).
-#ifndef PT_TRI_PK
-#define PT_TRI_PK 0
-#endif
-typedef float tv2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ tv2 pk_fma(tv2 a, tv2 b, tv2 c) { return __builtin_elementwise_fma(a, b, c); }
-// cross(a, b)
-__device__ __forceinline__ f3 cross_pk(f3 a, f3 b) {
-    const tv2 m = tv2{b.y, b.z} * tv2{a.z, a.x};
-    const tv2 xy = pk_fma(tv2{a.y, a.z}, tv2{b.z, b.x}, -m);
-    return F3(xy.x, xy.y, fma_(a.x, b.y, -rmul(b.x, a.y)));
-}
-// (dot(a, c), dot(b, c))
-__device__ __forceinline__ tv2 dot2_pk(f3 a, f3 b, f3 c) {
-    tv2 r = tv2{a.x, b.x} * tv2{c.x, c.x};
-    r = pk_fma(tv2{a.y, b.y}, tv2{c.y, c.y}, r);
-    return pk_fma(tv2{a.z, b.z}, tv2{c.z, c.z}, r);
-}
-__device__ __forceinline__ bool tri_glm_pk(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& bx, float& by, float& t) {
-    const f3 p = cross_pk(d, e2);
-    const tv2 dxy = tv2{o.x, o.y} - tv2{v0.x, v0.y};
-    const f3 dist = F3(dxy.x, dxy.y, o.z - v0.z);
-    const tv2 db = dot2_pk(e1, dist, p);  // det, bx
-    const float det = db.x;
-    bx = db.y;
-    const f3 perp = cross_pk(dist, e1);
-    const tv2 bt = dot2_pk(d, e2, perp);  // by, dot(e2, perp)
-    by = bt.x;
-    bool ok;
-    if (det > 0.0f) ok = !(bx < 0.0f || bx > det) && !(by < 0.0f || bx + by > det);
-    else if (det < 0.0f) ok = !(bx > 0.0f || bx < det) && !(by > 0.0f || bx + by < det);
-    else ok = false;
-    if (!ok) return false;
-    const float inv = 1.0f / det;
-    t = bt.y * inv;
-    const tv2 b2 = tv2{bx, by} * tv2{inv, inv};
-    bx = b2.x;
-    by = b2.y;
-    return true;
-}
-__device__ __forceinline__ bool tri_pred_pk(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float tmax) {
-    const f3 h = cross_pk(d, e2);
-    const tv2 sxy = tv2{o.x, o.y} - tv2{v0.x, v0.y};
-    const f3 s = F3(sxy.x, sxy.y, o.z - v0.z);
-    const tv2 du = dot2_pk(e1, s, h);  // det, dot(s, h)
-    const float det = du.x;
-    if (det > -PT_FLT_EPS && det < PT_FLT_EPS) return false;
-    const float inv = 1.0f / det;
-    const float u = du.y * inv;
-    if (u < 0 || u > 1) return false;
-    const f3 q = cross_pk(s, e1);
-    const tv2 vt = dot2_pk(d, e2, q) * tv2{inv, inv};  // v, t
-    const float v = vt.x;
-    if (v < 0 || u + v > 1) return false;
-    return vt.y <= tmax && vt.y >= PT_EPS;
-}
-
-
 // QuadShape hit test (Shape.cpp:320-359) as built: Intersect tests and
 // divides by dot(d, nn) fused, IntersectPred (PRED) by the unfused dot; beta's
 // cross(u, ph) rounded-first with its dot in y, x, z order
@@ -202,22 +138,9 @@ __device__ __noinline__ bool tri_alpha_slow(uint32_t slot, float bu, float bv, f
 // the alpha-record path inline in the traversal loop (the general one stays a
 // call): C4 1615 -> 1633 Mrays/s (closest-hit 20.58 -> 20.29 ms per launch,
 // profiles/r04_ab_traversal.txt)
-#ifndef PT_ALPHA_INB  // the alpha test's no-wrap fast path (uniform branch)
-#define PT_ALPHA_INB 1
-#endif
-#ifndef PT_ALPHA_INLINE
-#define PT_ALPHA_INLINE 1
-#endif
 __device__ __forceinline__ bool tri_alpha_rec(const DevAlpha& r, uint32_t slot, float bu, float bv, f3 o, f3 d);
-#if PT_ALPHA_INLINE
 __device__ __forceinline__
-#else
-__device__ __noinline__
-#endif
 bool tri_alpha(uint32_t ai, uint32_t slot, float bu, float bv, f3 o, f3 d) {
-#ifdef PT_DIAG_NO_ALPHA  // diagnostics builds only (timing of the test's cost; wrong results)
-    return true;
-#endif
     if (ai != ALPHA_NONE) {
         // the whole record in three 16-B loads issued together (a reference
         // into S.alpha would let the compiler read its fields where they are
@@ -227,10 +150,9 @@ bool tri_alpha(uint32_t ai, uint32_t slot, float bu, float bv, f3 o, f3 d) {
         const DevAlpha r = __builtin_bit_cast(DevAlpha, (DevGeom{a0, a1, a2}));
         return tri_alpha_rec(r, slot, bu, bv, o, d);
     }
-    return PT_ALPHA_INLINE ? tri_alpha_slow(slot, bu, bv, o, d) : tri_alpha_general(slot, bu, bv, o, d);
+    return tri_alpha_slow(slot, bu, bv, o, d);
 }
-// the test over an alpha record already read (PT_ALPHA_PREFETCH: the
-// traversal loads it with the triangle test still running)
+// the test over an alpha record already read
 __device__ __forceinline__ bool tri_alpha_rec(const DevAlpha& r, uint32_t slot, float bu, float bv, f3 o, f3 d) {
     {
         const float u = bu, v = bv, w = 1.0f - u - v;
@@ -252,7 +174,7 @@ __device__ __forceinline__ bool tri_alpha_rec(const DevAlpha& r, uint32_t slot, 
             // the wave skips the remainders (a uniform branch)
             int x0, x1, y0, y1;
             const bool inb = (uint32_t)xi < (uint32_t)(W - 1) && (uint32_t)yi < (uint32_t)(H - 1);
-            if (PT_ALPHA_INB && __ballot(!inb) == 0) {
+            if (__ballot(!inb) == 0) {
                 x0 = xi, x1 = xi + 1, y0 = yi, y1 = yi + 1;
             } else {
                 x0 = wrap_index_t(xi, W), x1 = wrap_next(x0, W), y0 = wrap_index_t(yi, H), y1 = wrap_next(y0, H);
@@ -372,28 +294,14 @@ __device__ __forceinline__ void slab4p(float4 xmn, float4 xmx, float4 ymn, float
     slab4pe(xmn, xmx, ymn, ymx, zmn, zmx, o, inv, tmax, mask, te);
 }
 
-// The child boxes of a quantized node (DevQNode), as the 4-wide SoA float4s
-// slab4p takes: bound = fma(byte, 2^(e-127), origin) per axis.
+// bound = fma(byte, 2^(e-127), origin) per axis of a quantized record
 __device__ __forceinline__ float qdec(uint32_t w, int k, float sc, float org) {
     return fma_((float)((w >> (8 * k)) & 0xFFu), sc, org);
 }
 __device__ __forceinline__ float4 qdec4(uint32_t w, float sc, float org) {
     return make_float4(qdec(w, 0, sc, org), qdec(w, 1, sc, org), qdec(w, 2, sc, org), qdec(w, 3, sc, org));
 }
-__device__ __forceinline__ void qnode_boxes(float4 a, float4 b, float4 c, float4& xmn, float4& xmx, float4& ymn,
-                                            float4& ymx, float4& zmn, float4& zmx) {
-    const uint32_t ex = __float_as_uint(a.w);
-    const float sx = __uint_as_float((ex & 0xFFu) << 23), sy = __uint_as_float(((ex >> 8) & 0xFFu) << 23),
-                sz = __uint_as_float(((ex >> 16) & 0xFFu) << 23);
-    xmn = qdec4(__float_as_uint(b.x), sx, a.x);
-    xmx = qdec4(__float_as_uint(b.y), sx, a.x);
-    ymn = qdec4(__float_as_uint(b.z), sy, a.y);
-    ymx = qdec4(__float_as_uint(b.w), sy, a.y);
-    zmn = qdec4(__float_as_uint(c.x), sz, a.z);
-    zmx = qdec4(__float_as_uint(c.y), sz, a.z);
-}
-
-// The same test on a quantized node with each axis's bounds pre-ordered by
+// The slab test on a quantized node with each axis's bounds pre-ordered by
 // the sign of inv (near bound first): then min(t1, t2) is the near plane's t
 // and max(t1, t2) the far plane's exactly (rounding is monotone, lo' <= hi'),
 // so tEntry / tExit are one max3 / min3 per child instead of six min/max, and
@@ -436,7 +344,7 @@ __device__ __forceinline__ void qslab4pe(float4 a, float4 b, float4 c, f3 o, f3 
     }
 }
 
-// PT_Q48 node record (pt_device.h): child refs from the block base and the
+// Quantized node record (pt_device.h): child refs from the block base and the
 // per-child descriptor bytes (offset | Q48_LEAF -> REF_LEAF | Q48_HOP ->
 // REF_BLOCK), and the octant order byte BVH4::LUT[octant][perm] from the
 // block's LDS copy of the table (s_lut, staged by stage_q48_lut).
@@ -451,7 +359,7 @@ __device__ __forceinline__ uint4 q48_children(float cz, float cw) {
     }
     return make_uint4(r[0], r[1], r[2], r[3]);
 }
-// order_children over a PT_Q48 record's base + descriptors: the ref of a
+// order_children over a quantized record's base + descriptors: the ref of a
 // child is formed only when it is pushed or kept (fewer live registers than
 // four decoded refs)
 template <class Push>
@@ -476,31 +384,11 @@ __device__ __forceinline__ uint32_t order_children_q48(uint32_t mask, float cz, 
 __device__ __forceinline__ uint32_t q48_perm(const uint8_t* s_lut, uint32_t oct, float aw) {
     return s_lut[(oct & OCT_MASK) * Q48_LUT_STRIDE + (__float_as_uint(aw) >> 24)];
 }
-// The top of the BVH in LDS (A/B option): the first PT_TREELET records of the
-// PT_Q48 array -- laid out breadth-first from the roots by the runtime, so
-// they are the TLAS and the first levels of the BLASes every ray descends --
-// sit after the order table in the same LDS block; node steps on them read
-// LDS instead of the vector memory pipe.  PT_TREELET_ANY: the any-hit
-// kernels' count.  0 = off.
-#ifndef PT_TREELET
-#define PT_TREELET 0
-#endif
-#ifndef PT_TREELET_ANY
-#define PT_TREELET_ANY 0
-#endif
 #define Q48_LUT_BYTES (8 * Q48_LUT_STRIDE)  // a multiple of 16
-#define Q48_LDS_BYTES(T_) (Q48_LUT_BYTES + 48 * (T_))
-// every thread of the block takes part (one barrier); T: treelet records
-template <int T = 0>
+// every thread of the block takes part (one barrier)
 __device__ __forceinline__ void stage_q48_lut(uint8_t* s_lut) {
     uint32_t* w = reinterpret_cast<uint32_t*>(s_lut);
     for (uint32_t i = threadIdx.x; i < 8 * Q48_LUT_STRIDE / 4; i += blockDim.x) w[i] = S.qlut[i];
-    if constexpr (T > 0) {
-        float4* tr = reinterpret_cast<float4*>(s_lut + Q48_LUT_BYTES);
-        const uint32_t n = 3u * min((uint32_t)T, S.qrec_bytes / 48u);
-        const float4* src = reinterpret_cast<const float4*>(S.qrec);
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) tr[i] = src[i];
-    }
     __syncthreads();
 }
 
@@ -518,52 +406,6 @@ __device__ __forceinline__ uint32_t order_children(uint32_t mask, uint4 ch, uint
     for (int k = 0; k < 4; k++) {
         const uint32_t ci = (perm >> (2 * k)) & 3u;
         const uint32_t lo = (ci & 1u) ? ch.y : ch.x, hi = (ci & 1u) ? ch.w : ch.z;
-        const uint32_t c = (ci & 2u) ? hi : lo;
-        const bool v = (vm >> ci) & 1u;
-        if (v && cand != REF_EMPTY) push(cand);
-        cand = v ? c : cand;
-    }
-    return cand;
-}
-
-// The same with each pushed child's entry distance (BVH4::Intersect keeps
-// entryDist[] beside the stack and skips a popped node whose entry exceeds
-// the current max, BVH.hpp:1134-1135, 1200-1203): push(ref, tEntry).
-template <class Push>
-__device__ __forceinline__ uint32_t order_children_e(uint32_t mask, uint4 ch, uint32_t perm, const float (&te)[4],
-                                                     Push&& push) {
-    const uint32_t vm = mask & ((uint32_t)(ch.x != REF_EMPTY) | (uint32_t)(ch.y != REF_EMPTY) << 1 |
-                                (uint32_t)(ch.z != REF_EMPTY) << 2 | (uint32_t)(ch.w != REF_EMPTY) << 3);
-    uint32_t cand = REF_EMPTY;
-    float ce = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t ci = (perm >> (2 * k)) & 3u;
-        const uint32_t lo = (ci & 1u) ? ch.y : ch.x, hi = (ci & 1u) ? ch.w : ch.z;
-        const uint32_t c = (ci & 2u) ? hi : lo;
-        const float elo = (ci & 1u) ? te[1] : te[0], ehi = (ci & 1u) ? te[3] : te[2];
-        const float e = (ci & 2u) ? ehi : elo;
-        const bool v = (vm >> ci) & 1u;
-        if (v && cand != REF_EMPTY) push(cand, ce);
-        cand = v ? c : cand;
-        ce = v ? e : ce;
-    }
-    return cand;
-}
-
-// The wide-node form (PT_WIDE): up to 8 slots, perm = 8 x 3-bit slot indices.
-template <class Push>
-__device__ __forceinline__ uint32_t order_children8(uint32_t mask, uint4 c0, uint4 c1, uint32_t perm, Push&& push) {
-    const uint32_t vm = mask & ((uint32_t)(c0.x != REF_EMPTY) | (uint32_t)(c0.y != REF_EMPTY) << 1 |
-                                (uint32_t)(c0.z != REF_EMPTY) << 2 | (uint32_t)(c0.w != REF_EMPTY) << 3 |
-                                (uint32_t)(c1.x != REF_EMPTY) << 4 | (uint32_t)(c1.y != REF_EMPTY) << 5 |
-                                (uint32_t)(c1.z != REF_EMPTY) << 6 | (uint32_t)(c1.w != REF_EMPTY) << 7);
-    uint32_t cand = REF_EMPTY;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const uint32_t ci = (perm >> (3 * k)) & 7u;
-        const uint4 h = (ci & 4u) ? c1 : c0;
-        const uint32_t lo = (ci & 1u) ? h.y : h.x, hi = (ci & 1u) ? h.w : h.z;
         const uint32_t c = (ci & 2u) ? hi : lo;
         const bool v = (vm >> ci) & 1u;
         if (v && cand != REF_EMPTY) push(cand);
@@ -650,7 +492,7 @@ __device__ __forceinline__ InstState instance_step_inl(InstState s) {
     }
     s.inv = inv_dir(s.d);
     s.oct = octant(s.d) | OCT_INST | (s.oct & (OCT_TIE | OCT_FOUND));
-    s.ref = (QN && PT_Q48) ? I->qroot : I->root;  // the BLAS root in the traversal's node form
+    s.ref = QN ? I->qroot : I->root;  // the BLAS root in the traversal's node form
     return s;
 }
 // The pool kernels (7 waves per SIMD, 72 VGPRs) call it out of line; the

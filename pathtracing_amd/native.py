@@ -124,7 +124,7 @@ class Stats(C.Structure):
                 ("tris_any", C.c_uint64), ("shade_hits", C.c_uint64), ("ms_total", C.c_double),
                 ("ms_closest", C.c_double), ("ms_any", C.c_double), ("ms_shade", C.c_double),
                 ("launches_closest", C.c_uint64), ("launches_any", C.c_uint64),
-                ("stack_overflows", C.c_uint64), ("n_devices", C.c_uint32), ("pad", C.c_uint32)]
+                ("stack_overflows", C.c_uint64), ("n_devices", C.c_uint32), ("tie_overflows", C.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
@@ -217,6 +217,8 @@ def lib():
     L.pt_light_cases.restype = C.c_int32
     L.pt_light_picks.argtypes = [vp, vp, C.c_uint32, vp]
     L.pt_light_picks.restype = C.c_int32
+    L.pt_anim_inverse_cases.argtypes = [vp, vp, C.c_uint32, vp]
+    L.pt_anim_inverse_cases.restype = C.c_int32
     L.pt_scene_device_bytes.argtypes = [vp]
     L.pt_scene_device_bytes.restype = C.c_uint64
     L.pt_bvh4_build.argtypes = [vp, C.c_uint32, vp, C.POINTER(C.c_uint32), C.POINTER(RefNode), vp, vp]
