@@ -200,16 +200,9 @@ private:
     std::shared_ptr<PhaseFunction> phase;
 };
 
-// Expose protected BVH4 arrays (BVH.hpp:1214-1216, 392-394) — API use only.
-template <class T>
-struct Peek : BVH4<T> {
-    using BVH4<T>::BVH4;
-    const std::vector<BVH4_CLUSTER>& Nodes() const { return this->nodes; }
-    BVH4_NODE Root() const { return this->rootNode; }
-    const std::vector<T>& Prims() const { return this->primitives; }
-};
-using PeekTLAS = Peek<std::shared_ptr<Primitive>>;
-using PeekBLAS = Peek<GeometricPrimitive>;
+// Peek (protected BVH4 arrays) and the reference's own Model without Assimp
+#include "ref_peek.hpp"
+#include "ref_model.hpp"
 
 // Ray-counting wrapper used only by the `time` command.
 static std::atomic<uint64_t> g_closest{0}, g_any{0};
@@ -241,6 +234,8 @@ struct World {
     std::map<int, std::shared_ptr<Mesh>> mesh;
     std::vector<std::shared_ptr<Primitive>> top;          // Add order
     std::vector<std::shared_ptr<PeekBLAS>> blas;          // per model, in order
+    std::vector<std::shared_ptr<Primitive>> blasPrim;     // what the TLAS / instances hold per model
+    bool refModels = false;  // "refmodels": models are the reference's Model (ref_model.cpp)
     std::vector<std::shared_ptr<PeekTLAS>> blasPtr;       // pointer twin (prim order)
     std::vector<std::vector<std::shared_ptr<Primitive>>> blasItems;  // originals, per model
     std::vector<int> blasTop;                              // top index of each model
@@ -418,7 +413,7 @@ static void read_recipe(World& w, const std::string& path) {
         } else if (k == "instance" || k == "animinstance") {
             // TransformedPrimitive / AnimatedPrimitive over a defined BLAS
             int pid, bid; s >> pid >> bid;
-            std::shared_ptr<Primitive> inner = w.blas.at(bid);
+            std::shared_ptr<Primitive> inner = w.blasPrim.at(bid);
             if (k == "instance") w.top.push_back(std::make_shared<TransformedPrimitive>(inner, read_mat4(s)));
             else {
                 float dx, dy, dz, t0, t1; s >> dx >> dy >> dz >> t0 >> t1;
@@ -431,19 +426,37 @@ static void read_recipe(World& w, const std::string& path) {
             w.top.back() = std::make_shared<AnimatedPrimitive>(w.top.back(), glm::vec3(dx, dy, dz), glm::vec2(t0, t1));
         } else if (k == "topblas") {
             int pid, bid; s >> pid >> bid;
-            w.top.push_back(w.blas.at(bid));
+            w.top.push_back(w.blasPrim.at(bid));
         } else if (k == "model" || k == "blasdef") {
             // Model::BuildBlas<BLAS4> (Model.hpp:43-60) without Assimp: one
             // GeometricPrimitive per triangle, an AreaLight per emissive one.
             // blasdef: the BLAS of a model that is only instanced (not in the TLAS).
+            // "override M MD" after the mesh ids: BuildBlas(material, medium)
+            // (Model.hpp:62-80), every triangle with that material / medium.
+            // refmodels: the TLAS holds the reference's own Model, built by
+            // ResourceManager::CacheModel<BLAS4> (ref_model.cpp); the BLAS
+            // built here is then only the pointer twin's order.
             const bool top = k == "model";
             int pid, nm; s >> pid >> nm;
             std::vector<GeometricPrimitive> prims;
             std::vector<std::shared_ptr<Primitive>> ptrs;
-            int tri = 0;
+            std::vector<std::shared_ptr<Mesh>> meshes;
             for (int i = 0; i < nm; i++) {
                 int mid; s >> mid;
-                auto& me = w.mesh.at(mid);
+                meshes.push_back(w.mesh.at(mid));
+            }
+            std::string ov;
+            bool override_mat = false;
+            std::shared_ptr<Material> omat;
+            std::shared_ptr<Medium> omed;
+            if (s >> ov && ov == "override") {
+                int om, omd; s >> om >> omd;
+                override_mat = true;
+                omat = om < 0 ? nullptr : w.mat.at(om);
+                omed = omd < 0 ? nullptr : w.med.at(omd);
+            }
+            int tri = 0;
+            for (auto& me : meshes) {
                 for (uint32_t j = 0; j < me->GetTriangleCount(); j++, tri++) {
                     std::shared_ptr<Shape> shape(me->GetControlPtr(), me->GetShape(j));
                     std::shared_ptr<AreaLight> area = me->GetEmissiveTexture() != nullptr
@@ -453,17 +466,32 @@ static void read_recipe(World& w, const std::string& path) {
                         area->PreProcess({});
                         if (area->Power() <= std::numeric_limits<float>::epsilon()) area = nullptr;
                     }
-                    if (area) w.lightOwner[area.get()] = "tri:" + std::to_string(w.blas.size()) + ":" + std::to_string(tri);
-                    prims.emplace_back(shape, me->GetMaterial(), area, me->GetMedium());
+                    if (area && !w.refModels)
+                        w.lightOwner[area.get()] = "tri:" + std::to_string(w.blas.size()) + ":" + std::to_string(tri);
+                    prims.emplace_back(shape, override_mat ? omat : me->GetMaterial(), area,
+                                       override_mat ? omed : me->GetMedium());
                     ptrs.push_back(std::make_shared<GeometricPrimitive>(prims.back()));
                 }
             }
-            auto b = std::make_shared<PeekBLAS>(prims);
+            std::shared_ptr<PeekBLAS> b;
+            std::shared_ptr<Primitive> held;
+            if (w.refModels) {
+                HarnessModel hm = pt_harness_model("harness model " + std::to_string(w.blas.size()), meshes,
+                                                   override_mat, omat, omed);
+                for (const auto& [l, t] : hm.lights)
+                    w.lightOwner[l] = "tri:" + std::to_string(w.blas.size()) + ":" + std::to_string(t);
+                b = hm.blas;
+                held = hm.model;
+            } else {
+                b = std::make_shared<PeekBLAS>(prims);
+                held = b;
+            }
             w.blas.push_back(b);
+            w.blasPrim.push_back(held);
             w.blasPtr.push_back(std::make_shared<PeekTLAS>(ptrs));
             w.blasItems.push_back(ptrs);
             w.blasTop.push_back(top ? (int)w.top.size() : -1);
-            if (top) w.top.push_back(b);
+            if (top) w.top.push_back(held);
         } else if (k == "infinite") {
             std::string kind; s >> kind;
             if (kind == "uniform") {
@@ -525,6 +553,8 @@ static void read_recipe(World& w, const std::string& path) {
             s >> w.integ >> w.maxDepth;
         } else if (k == "sampler") {
             s >> w.seed >> w.spp;
+        } else if (k == "refmodels") {
+            w.refModels = true;
         } else if (k == "strata") {
             s >> g_strata_x >> g_strata_y;
         }

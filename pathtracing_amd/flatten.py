@@ -354,9 +354,12 @@ def flatten_scene(scene: Scene) -> FlatScene:
             nt = mesh.GetTriangleCount()
             tflags.append(np.full(nt, 1 if mesh.tangents is not None else 0, dtype=np.uint32))
             boxes.append(mesh.tri_bboxes())
-            mat = m.override_material if m.override_material is not None else mesh.material
+            # Model::BuildBlas(material, medium) (Model.hpp:62-80) takes both
+            # overrides, a null one included; BuildBlas() the meshes' own
+            override = m.override_material is not None or m.override_medium is not None
+            mat = m.override_material if override else mesh.material
             mats.append(np.full(nt, reg.material(mat), dtype=np.int32))
-            med = m.override_medium if m.override_medium is not None else mesh.medium
+            med = m.override_medium if override else mesh.medium
             meds.append(np.full(nt, -1, dtype=np.int32))
             med_objs.append((len(meds) - 1, med))
             vbase += nv

@@ -197,6 +197,14 @@ class Context:
         N.check(self._lib.pt_light_picks(self.ptr, u.ctypes.data, u.shape[0], out.ctypes.data), self.ptr)
         return out
 
+    def anim_inverse(self, t: np.ndarray) -> np.ndarray:
+        """The device's inverse of identity + translation t (AnimatedPrimitive's
+        glm::inverse at a ray's time), (n, 3) -> (n, 16) column-major (test hook)."""
+        t = np.ascontiguousarray(t, np.float32).reshape(-1, 3)
+        out = np.zeros((t.shape[0], 16), np.float32)
+        N.check(self._lib.pt_anim_inverse_cases(self.ptr, t.ctypes.data, t.shape[0], out.ctypes.data), self.ptr)
+        return out
+
     def light_cases(self, cases: np.ndarray, n_lights: int) -> np.ndarray:
         """Light sample / PDF / L for every light x case: (n_lights*n, 18) (test hook)."""
         cases = np.ascontiguousarray(cases, np.float32)

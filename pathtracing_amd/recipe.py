@@ -62,6 +62,11 @@ def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: 
     out_dir = Path(out_dir)
     out_dir.mkdir(parents=True, exist_ok=True)
     lines: List[str] = ["ptscene 1"]
+    if getattr(scene, "ref_models", False):
+        # the harness holds the reference's own Model objects
+        # (ResourceManager::CacheModel<BLAS4>, oracle/ref_model.cpp), not a
+        # BLAS4 it builds over the same GeometricPrimitives
+        lines.append("refmodels")
     tex_ids: Dict[int, int] = {}
     mat_ids: Dict[int, int] = {}
     med_ids: Dict[int, int] = {}
@@ -153,9 +158,13 @@ def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: 
     blas_ids: Dict[int, int] = {}  # id(Model) -> BLAS index (model / blasdef line order)
 
     def model_ids(p):
-        if p.override_material is not None or p.override_medium is not None:
-            raise ValueError("recipes do not carry Model material overrides")
         return [mesh(me) for me in p.meshes]
+
+    def model_override(p):  # Model::BuildBlas(material, medium) (Model.hpp:62-80)
+        if p.override_material is None and p.override_medium is None:
+            return ""
+        return f" override {mat(p.override_material)} {med(p.override_medium)}"
+
 
     def level(lv):  # (matrix, animation) operands of one wrapper level
         m16 = " ".join(_f(x) for x in lv.transform.reshape(16))
@@ -178,7 +187,7 @@ def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: 
                 if id(p) not in blas_ids:
                     ids = model_ids(p)
                     blas_ids[id(p)] = len(blas_ids)
-                    lines.append(f"blasdef {blas_ids[id(p)]} {len(ids)} {' '.join(map(str, ids))}")
+                    lines.append(f"blasdef {blas_ids[id(p)]} {len(ids)} {' '.join(map(str, ids))}{model_override(p)}")
                 b = blas_ids[id(p)]
                 m16, anim = level(levels[-1])
                 lines.append(f"animinstance {k} {b} {anim}" if anim else f"instance {k} {b} {m16}")
@@ -191,7 +200,7 @@ def write_recipe(out_dir: Path, scene, camera, spp: int, seed: int, integrator: 
                 continue
             ids = model_ids(p)
             blas_ids[id(p)] = len(blas_ids)
-            lines.append(f"model {k} {len(ids)} {' '.join(map(str, ids))}")
+            lines.append(f"model {k} {len(ids)} {' '.join(map(str, ids))}{model_override(p)}")
         else:
             sh = p.shape
             m, md = mat(p.material), med(p.medium)

@@ -946,7 +946,10 @@ class AnimatedPrimitive(TransformedPrimitive):
 
 class Model(Primitive):
     """A BLAS4 over meshes: Model::BuildBlas<BLAS4> (Model.hpp:43-60) without Assimp.
-    Emissive meshes get one AreaLight per triangle, culled if Power <= FLT_EPSILON."""
+    Emissive meshes get one AreaLight per triangle, culled if Power <= FLT_EPSILON.
+    material / medium: BuildBlas<BLAS4>(material, medium) (Model.hpp:62-80,
+    ResourceManager::CacheModel's extra arguments, main.cpp:376): every
+    triangle takes both, a None one included."""
 
     def __init__(self, meshes: Sequence[Mesh], material: Optional[Material] = None, medium=None):
         self.meshes = list(meshes)
@@ -977,6 +980,9 @@ class Scene:
         self.infiniteLights: List[InfiniteLight] = []
         self.sceneMedium = medium
         self.flat = None  # set by BuildTlas
+        # test recipes only (pathtracing_amd.recipe): the reference harness
+        # builds this scene's Models as the reference's own Model objects
+        self.ref_models = False
 
     def GetMedium(self) -> Optional[HomogeneusMedium]:
         return self.sceneMedium

@@ -1058,3 +1058,85 @@ def nested_instances(W: int = 32, H: int = 32, spp: int = 4, max_depth: int = 8,
     camera = Camera((0, 0, 3.7), (0, 0, 0), 0.75, Film((W, H), MitchellFilter()), shutterBounds=shutter)
     ls = None if integrator == "simple" else PowerLightSampler()
     return SceneSetup(scene, camera, integrator, ls, max_depth, seed, spp).finish()
+
+
+# --------------------------------------------------------------------------
+def ref_models(W: int = 32, H: int = 32, spp: int = 4, max_depth: int = 8, seed: int = 0x5EED0091) -> SceneSetup:
+    """What every main.cpp scene holds: ResourceManager::CacheModel<BLAS4>
+    results in the TLAS (main.cpp:290) -- the C2 room as one Model, an
+    emissive lamp Model (its BuildBlas makes one AreaLight per triangle,
+    Model.hpp:43-60) and a sphere mesh Model built with a material override,
+    BuildBlas<BLAS4>(glass, nullptr) (Model.hpp:62-80, the extra CacheModel
+    arguments of main.cpp:376), beside a quad light; PathIntegrator,
+    PowerLightSampler.  The reference harness builds these as the reference's
+    own Model objects (scene.ref_models, oracle/ref_model.cpp), so the
+    drop-in's Model unwrap (integration/HipIntegrator.cpp, PT_WITH_MODEL)
+    runs on them."""
+    scene = Scene()
+    scene.ref_models = True
+    white = MicrofacetDiffuse((0.73, 0.73, 0.73))
+    red = MicrofacetDiffuse((0.65, 0.05, 0.05))
+    green = MicrofacetDiffuse((0.12, 0.45, 0.15))
+    walls = [
+        (_quad_tris((-1, -1, 1), (1, -1, 1), (1, -1, -1), (-1, -1, -1)), white),
+        (_quad_tris((-1, 1, -1), (1, 1, -1), (1, 1, 1), (-1, 1, 1)), white),
+        (_quad_tris((-1, -1, -1), (1, -1, -1), (1, 1, -1), (-1, 1, -1)), white),
+        (_quad_tris((-1, -1, 1), (-1, -1, -1), (-1, 1, -1), (-1, 1, 1)), red),
+        (_quad_tris((1, -1, -1), (1, -1, 1), (1, 1, 1), (1, 1, -1)), green),
+    ]
+    scene.Add(Model([Mesh(i, v, None, n, uv, m) for (i, v, n, uv), m in walls]))
+    light = AreaLight(QuadShape((-0.25, 0.999, -0.25), (0.5, 0, 0), (0, 0, 0.5)), (9.0, 7.0, 4.0), False)
+    scene.Add(GeometricPrimitive(light.getShape(), MicrofacetDiffuse((0.78, 0.78, 0.78)), light))
+    bi, bv, bn, buv = _box((0.45, -0.85, -0.35), (0.3, 0.3, 0.3), 0.4)
+    scene.Add(Model([Mesh(bi, bv, None, bn, buv, MicrofacetDiffuse((0.8, 0.8, 0.8)), SolidColor((2.5, 1.8, 1.0)))]))
+    idx, v, t, n, uv = _smooth_sphere(20, 10)
+    v = v * np.float32(0.3) + np.asarray((-0.3, -0.55, 0.2), np.float32)
+    scene.Add(Model([Mesh(idx, v, t, n, uv, white)], material=MicrofacetDielectric(1.5, 0.1, (1, 1, 1))))
+    camera = Camera((0, 0, 3.7), (0, 0, 0), 0.75, Film((W, H), MitchellFilter()))
+    return SceneSetup(scene, camera, "path", PowerLightSampler(), max_depth, seed, spp).finish()
+
+
+def ref_transformed_models(W: int = 32, H: int = 32, spp: int = 4, max_depth: int = 16,
+                           seed: int = 0x5EED0092) -> SceneSetup:
+    """TransformedPrimitive of a Model, as main.cpp:376 / 483 place their
+    models: a glass "dragon" (a sphere mesh) built by
+    CacheModel<BLAS4>(name, path, glass, HomogeneusMedium) -- the
+    BuildBlas(material, medium) form -- placed twice under rotate / scale /
+    translate (the cache returns the same Model), a plain Model under one
+    transform and an emissive lamp Model under another (its lights become
+    TransformedLights, Primitive.cpp:66-73), in the C2 room (itself a Model);
+    VolPathIntegrator (the dragon's medium), UniformLightSampler.  The harness
+    holds the reference's own Model objects (scene.ref_models)."""
+    from .scene import TransformedPrimitive, mat4_identity, mat4_rotate, mat4_scale, mat4_translate
+    scene = Scene()
+    scene.ref_models = True
+    white = MicrofacetDiffuse((0.73, 0.73, 0.73))
+    red = MicrofacetDiffuse((0.65, 0.05, 0.05))
+    green = MicrofacetDiffuse((0.12, 0.45, 0.15))
+    walls = [
+        (_quad_tris((-1, -1, 1), (1, -1, 1), (1, -1, -1), (-1, -1, -1)), white),
+        (_quad_tris((-1, 1, -1), (1, 1, -1), (1, 1, 1), (-1, 1, 1)), white),
+        (_quad_tris((-1, -1, -1), (1, -1, -1), (1, 1, -1), (-1, 1, -1)), white),
+        (_quad_tris((-1, -1, 1), (-1, -1, -1), (-1, 1, -1), (-1, 1, 1)), red),
+        (_quad_tris((1, -1, -1), (1, -1, 1), (1, 1, 1), (1, 1, -1)), green),
+    ]
+    scene.Add(Model([Mesh(i, v, None, n, uv, m) for (i, v, n, uv), m in walls]))
+    light = AreaLight(QuadShape((-0.25, 0.999, -0.25), (0.5, 0, 0), (0, 0, 0.5)), (12.0, 9.0, 5.0), False)
+    scene.Add(GeometricPrimitive(light.getShape(), MicrofacetDiffuse((0.78, 0.78, 0.78)), light))
+    idx, v, t, n, uv = _smooth_sphere(20, 10)
+    fill = HomogeneusMedium((0.01, 0.9, 0.9), (1.0, 0.1, 0.1), HenyeyGreenstein(0.8), 5.0)
+    dragon = Model([Mesh(idx, v, t, n, uv, white)], material=MicrofacetDielectric(1.5, 0.05, (1, 1, 1)),
+                   medium=fill)
+    for pos, ang, ax, sc in [((-0.45, -0.6, 0.1), 0.5, (0, 1, 0), (0.3, 0.35, 0.3)),
+                             ((0.35, -0.1, -0.4), -0.8, (1, 0, 1), (0.25, 0.2, 0.3))]:
+        scene.Add(TransformedPrimitive(dragon, mat4_scale(mat4_rotate(mat4_translate(mat4_identity(), pos), ang, ax),
+                                                          sc)))
+    rock = Model([Mesh(idx, v, t, n, uv, MicrofacetDiffuse((0.3, 0.5, 0.8)))])
+    scene.Add(TransformedPrimitive(rock, mat4_scale(mat4_translate(mat4_identity(), (0.5, -0.8, 0.5)),
+                                                    (0.18, 0.18, 0.18))))
+    bi, bv, bn, buv = _box((0, 0, 0), (0.2, 0.12, 0.2), 0.0)
+    lamp = Model([Mesh(bi, bv, None, bn, buv, MicrofacetDiffuse((0.8, 0.8, 0.8)), SolidColor((3.0, 2.0, 1.2)))])
+    scene.Add(TransformedPrimitive(lamp, mat4_rotate(mat4_translate(mat4_identity(), (-0.55, 0.55, -0.5)), 0.7,
+                                                     (1, 1, 0))))
+    camera = Camera((0, 0, 3.7), (0, 0, 0), 0.75, Film((W, H), MitchellFilter()))
+    return SceneSetup(scene, camera, "volpath", UniformLightSampler(), max_depth, seed, spp).finish()

@@ -80,6 +80,13 @@ def parity_scenes():
         # to four levels, static and animated levels mixed) and their lights
         # (TransformedLight of a TransformedLight), under a shutter camera
         "nested_instances": lambda: scenes.nested_instances(W=32, H=32, spp=4),
+        # the reference's own Model objects (ResourceManager::CacheModel<BLAS4>,
+        # Model::BuildBlas, oracle/ref_model.cpp): Models in the TLAS
+        # (main.cpp:290), one with a material override; and TransformedPrimitive
+        # of a Model (main.cpp:376, 483), a glass + medium override, an
+        # emissive Model under a transform, under VolPath
+        "ref_models": lambda: scenes.ref_models(W=32, H=32, spp=4),
+        "ref_transformed_models": lambda: scenes.ref_transformed_models(W=32, H=32, spp=4),
     }
 
 

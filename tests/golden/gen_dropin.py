@@ -32,9 +32,11 @@ from pathtracing_amd.recipe import pin_random_lights, write_recipe  # noqa: E402
 
 HARNESS = ROOT / "oracle" / "_ref" / "ref_harness"
 FILM_SCENES = ["example1", "cornell_c2", "cornell_c3", "zoo", "heightfield", "sanmiguel", "example1_volpath", "fog",
-               "instances", "lit_instances", "motion_blur", "motion_path", "stratified", "nested_instances"]
+               "instances", "lit_instances", "motion_blur", "motion_path", "stratified", "nested_instances",
+               "ref_models", "ref_transformed_models"]
 ADAPTIVE_SCENES = ["example1", "cornell_c3", "zoo", "fog", "instances", "sanmiguel", "lens_box", "lit_instances",
-                   "motion_blur", "motion_path", "stratified", "stratified_motion", "nested_instances"]
+                   "motion_blur", "motion_path", "stratified", "stratified_motion", "nested_instances",
+                   "ref_models", "ref_transformed_models"]
 
 
 def pinned_recipe(tmp: Path, setup) -> Path:
@@ -43,11 +45,18 @@ def pinned_recipe(tmp: Path, setup) -> Path:
                         setup.light_sampler, setup.extra_lights, pin=True, strata=setup.strata)
 
 
-def main() -> None:
+def main(names=None) -> None:
+    """names: regenerate only these scenes' entries, keeping the others"""
     from fixtures import parity_scenes
     ps = parity_scenes()
+    path = ROOT / "tests" / "golden" / "dropin.npz"
     out = {}
+    if names and path.exists():
+        with np.load(path, allow_pickle=False) as old:
+            out = {k: old[k] for k in old.files}
     for name in sorted(set(FILM_SCENES) | set(ADAPTIVE_SCENES)):
+        if names and name not in names:
+            continue
         setup = ps[name]()
         W, H = setup.camera.film.Resolution()
         with tempfile.TemporaryDirectory() as td:
@@ -62,8 +71,8 @@ def main() -> None:
                 out[f"adaptive_film_{name}"] = np.fromfile(f"{o}.adaptive_film.bin", np.float64).reshape(H, W, 4)
                 out[f"adaptive_counts_{name}"] = np.fromfile(f"{o}.adaptive_counts.bin", np.uint32).reshape(H, W)
         print(name, flush=True)
-    np.savez_compressed(ROOT / "tests" / "golden" / "dropin.npz", **out)
+    np.savez_compressed(path, **out)
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or None)

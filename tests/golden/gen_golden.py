@@ -372,6 +372,31 @@ def gen_mat4_inverse(rng, tmp: Path):
     print(f"mat4_inverse: {(OUT / 'mat4_inverse.npz').stat().st_size / 1024:.0f} KiB, {len(A)} matrices")
 
 
+def gen_anim_inverse(rng, tmp: Path):
+    """glm::inverse of identity + translation t by the reference's own build
+    of glm (oracle/glm_inverse_probe.cpp): the matrix AnimatedPrimitive
+    inverts at each ray's time (Primitive.cpp:82-89), for the device's closed
+    form (pt_shading.h anim_inverse, test hook pt_anim_inverse_cases).  Every
+    sign pattern of +0 and +-{denormal, tiny, unit, large, near-max} per axis,
+    and random translations over 20 decades.  No -0 component: the device
+    builds the column as v + 0 (anim_transform), as glm's matrix product
+    rounds it."""
+    mags = [1e-40, 1e-30, 0.3, 1.0, 7.5, 1e20, 3e38]
+    vals = [0.0] + [s * m for m in mags for s in (1.0, -1.0)]
+    t = [(a, b, c) for a in vals for b in vals for c in vals]
+    r = rng.normal(size=(2000, 3)) * 10.0 ** rng.uniform(-10, 10, (2000, 1))
+    r[rng.random((2000, 3)) < 0.2] = 0.0
+    t = np.concatenate([np.asarray(t, np.float64), r]).astype(np.float32) + np.float32(0.0)  # (-0 -> +0)
+    A = np.tile(np.eye(4, dtype=np.float32).reshape(16), (t.shape[0], 1))
+    A[:, 12:15] = t
+    A.tofile(tmp / "anim.bin")
+    subprocess.run([str(HARNESS.parent / "glm_inverse_probe"), str(tmp / "anim.bin"), str(tmp / "anim_inv.bin")],
+                   check=True)
+    inv = np.fromfile(tmp / "anim_inv.bin", np.float32).reshape(-1, 16)
+    np.savez_compressed(OUT / "anim_inverse.npz", t=t, inv=inv)
+    print(f"anim_inverse: {(OUT / 'anim_inverse.npz').stat().st_size / 1024:.0f} KiB, {len(t)} translations")
+
+
 def main(names=None):
     """All scenes share one rng stream (the committed round-1 fixtures); a
     scene regenerated alone (`gen_golden.py NAME...`) uses its own stream
@@ -402,6 +427,8 @@ def main(names=None):
             gen_emission_power(Path(t))
         if not names or "mat4_inverse" in names:
             gen_mat4_inverse(np.random.default_rng([20261018, 4]), Path(t))
+        if not names or "anim_inverse" in names:
+            gen_anim_inverse(np.random.default_rng([20261019, 6]), Path(t))
 
 
 if __name__ == "__main__":

@@ -52,8 +52,12 @@ def _film_frac(gpu, ref):
 @pytest.mark.skipif(not HARNESS.exists(), reason="hip_harness not built (needs /root/reference at build time)")
 @pytest.mark.parametrize("name", ["example1", "cornell_c2", "cornell_c3", "zoo", "heightfield", "sanmiguel",
                                   "example1_volpath", "fog", "instances", "lit_instances", "motion_blur",
-                                  "motion_path", "stratified", "nested_instances"])
+                                  "motion_path", "stratified", "nested_instances", "ref_models",
+                                  "ref_transformed_models"])
 def test_drop_in_integrator_matches_reference_film(name, tmp_path):
+    """ref_models / ref_transformed_models: the reference's own Model objects
+    (ResourceManager::CacheModel<BLAS4>) in the TLAS and inside
+    TransformedPrimitives, unwrapped by the exporter's PT_WITH_MODEL path."""
     setup, gpu, _ = _dropin(name, tmp_path)
     ref = np.load(GOLDEN / "dropin.npz", allow_pickle=False)[f"film_{name}"]
     np.testing.assert_allclose(gpu[..., 3], ref[..., 3], rtol=1e-9, atol=1e-12)
@@ -74,7 +78,7 @@ def test_drop_in_integrator_matches_reference_film(name, tmp_path):
 @pytest.mark.skipif(not HARNESS.exists(), reason="hip_harness not built (needs /root/reference at build time)")
 @pytest.mark.parametrize("name", ["example1", "cornell_c3", "zoo", "fog", "instances", "sanmiguel", "lens_box",
                                   "lit_instances", "motion_blur", "motion_path", "stratified",
-                                  "stratified_motion", "nested_instances"])
+                                  "stratified_motion", "nested_instances", "ref_models", "ref_transformed_models"])
 def test_drop_in_adaptive_render_matches_reference_render(name, tmp_path):
     """The drop-in's default Render (adaptive, like TileIntegrator::Render)
     against the reference's own adaptive Render of the same recipe: identical

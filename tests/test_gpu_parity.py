@@ -106,6 +106,9 @@ def test_gpu_trace_matches_oracle_and_reference(case, nodes):
         bad = np.nonzero((anyh["prim"] > 0) != (fx["any"] > 0))[0]
         assert bad.size == 0, f"any-hit differs from the reference on rays {bad[:8].tolist()}"
         assert st["rays_closest"] == len(rays) and st["nodes_closest"] > 0
+        # no exact-t tie was dropped from the re-trace list (pt_stats::
+        # tie_overflows; tie_models / tie_instances put ties on every wall hit)
+        assert st["tie_overflows"] == 0 and st["stack_overflows"] == 0
     finally:
         ctx.set_node_format(N.PT_NODES_AUTO)
 
@@ -132,6 +135,7 @@ def test_gpu_film_matches_oracle_and_reference(case):
     # NEE rays whose contribution is already zero are not traced, so never
     # more than the reference's
     assert st["rays_any"] <= cnt["any"]
+    assert st["tie_overflows"] == 0 and st["stack_overflows"] == 0
 
 
 @pytest.mark.parametrize("name", ["lens_box", "lens_gauss", "mitchell2", "cornell_c3"])
@@ -377,6 +381,9 @@ def test_gpu_sanmiguel_full_size_shards_sum(c4_full):
     # no traversal stack push was dropped (pt_stats::stack_overflows: the
     # pool kernels' 48-entry stack, LDS + HBM)
     assert st["stack_overflows"] == 0
+    # ... and no exact-t tie was dropped from the re-trace list
+    # (pt_stats::tie_overflows, Shape.cpp:204)
+    assert st["tie_overflows"] == 0
     parts = []
     for r in range(2):
         film.Clear()
@@ -792,3 +799,21 @@ def _chain_len(ins, k):
         k = int(ins["inner"][k])
         n += 1
     return n
+
+
+# ---------------------------------------------------------------- AnimatedPrimitive inverse (anim_inverse)
+def test_gpu_anim_inverse_bit_exact_vs_reference_glm():
+    """The device's closed-form inverse of an AnimatedPrimitive's matrix at a
+    ray's time (pt_shading.h anim_inverse, through pt_anim_inverse_cases)
+    against glm::inverse as the reference's own build computes it
+    (tests/golden/anim_inverse.npz): every sign pattern of +0 and
+    +-{denormal, tiny, unit, large, near-max} translations, and random ones
+    over 20 decades -- all 16 entries bit for bit, the zeros' signs included."""
+    from fixtures import GOLDEN
+    from pathtracing_amd.integrator import Context
+    fx = np.load(GOLDEN / "anim_inverse.npz", allow_pickle=False)
+    ctx = Context(0)
+    got = ctx.anim_inverse(fx["t"])
+    want = fx["inv"]
+    bad = np.nonzero((got.view(np.uint32) != want.view(np.uint32)).any(1))[0]
+    assert bad.size == 0, f"{bad.size} of {len(want)} differ; first t {fx['t'][bad[:4]].tolist()}"
