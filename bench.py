@@ -172,14 +172,18 @@ def cpu_baseline(setup, config: str, target_s: float = 15.0):
            # bandwidth and SMT make real scaling sub-linear)
            "full_host_estimate": {"value": round(per_core * affinity, 3), "cores": affinity,
                                   "method": "per-core rate x affinity (linear)"}}
-    ratio = _json(ROOT / "profiles" / "r03_cpu_ratio.json") or _json(ROOT / "profiles" / "r02_cpu_ratio.json")
+    ratio = (_json(ROOT / "profiles" / "r06_cpu_ratio.json") or _json(ROOT / "profiles" / "r03_cpu_ratio.json") or
+             _json(ROOT / "profiles" / "r02_cpu_ratio.json"))
     if ratio:
         out["port_vs_reference"] = ratio.get("summary")
         # the reference's own speed on this host, estimated from the port
         # through the ratio measured on the closest scene class, at the
         # measured thread count closest to the one timed here
-        key = {"c4": "c4_recipe_2pct_160x90_16spp_depth128", "c1": "c1_example1_path_256x256_16spp"}.get(
+        # C4: the full-detail scene itself (r06; the 2 %-detail recipe before)
+        key = {"c4": "c4_full_192x108_32spp_depth128", "c1": "c1_example1_path_256x256_16spp"}.get(
             config, "c1_example1_path_256x256_16spp")
+        if key not in ratio:
+            key = {"c4": "c4_recipe_2pct_160x90_16spp_depth128"}.get(config, "c1_example1_path_256x256_16spp")
         ent = ratio.get(key, {})
         by = ent.get("by_threads", {})
         t_used = min(by, key=lambda t: abs(int(t) - threads)) if by else str(ratio.get("_meta", {}).get("threads"))
@@ -438,6 +442,8 @@ def main():
     ap.add_argument("--no-sort", action="store_true", help="no hit sort before shading (PT_RENDER_NO_SORT)")
     ap.add_argument("--sort-rays", action="store_true",
                     help="trace closest-hit rays in origin-cell + octant order (PT_RENDER_SORT_RAYS)")
+    ap.add_argument("--any-stackless", action="store_true",
+                    help="NEE any-hit rays through the stackless traversal (PT_RENDER_ANY_STACKLESS)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the instrumented node-count pass")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -528,6 +534,8 @@ def main():
         tflag |= N.PT_RENDER_NO_SORT
     if args.sort_rays:
         tflag |= N.PT_RENDER_SORT_RAYS
+    if args.any_stackless:
+        tflag |= N.PT_RENDER_ANY_STACKLESS
 
     def step(flags=0):
         # this rank's sample shard into the film, then the SUM reduce of the
@@ -709,7 +717,8 @@ def roofline(args, setup, world, totals, cst, cpu):
     quant = pool and args.nodes != "full"
     q = ", true" if quant else ", false"
     kname = f"k_closest_pool<false, false{q}>" if pool else "k_closest<false, false>"
-    sname = f"k_shadow_pool<false, false{q}>" if pool else "k_shadow<false, false>"
+    sname = ("k_shadow_sl<false>" if getattr(args, "any_stackless", False) and quant else
+             f"k_shadow_pool<false, false{q}>" if pool else "k_shadow<false, false>")
     # the default library reads PT_Q48 records (pt_device.h); PT_Q48=0 tuning
     # builds (64-B nodes) are A/B variants only
     node_bytes = NODE_BYTES["q48"] if quant else NODE_BYTES["full"]

@@ -293,6 +293,9 @@ enum { PT_FILTER_MITCHELL = 0, PT_FILTER_BOX = 1, PT_FILTER_GAUSSIAN = 2, PT_FIL
 #define PT_RENDER_NO_TAIL 0x2000u       /* no tail kernel: every bounce a wavefront iteration
                                           (default: the last bounces of a fixed-SPP Path /
                                           SimplePath chunk finish in one launch, k_tail) */
+#define PT_RENDER_ANY_STACKLESS 0x4000u /* NEE any-hit rays through the stackless traversal
+                                          (escape links, no stack; quantized records
+                                          without instances, else ignored) */
 
 typedef struct pt_render_desc {
     uint32_t integrator;       /* PT_INTEGRATOR_*                               */
@@ -428,7 +431,10 @@ pt_status pt_frame_samples(pt_ctx* ctx, const uint32_t* pixels, const uint32_t* 
  * s with first <= s <= last (s % shard_count == shard_index), the frame's last
  * sample chunk; PT_ERR_STATE when there is no fixed-SPP frame. */
 pt_status pt_frame_sample_range(const pt_ctx* ctx, uint32_t* first, uint32_t* last);
-/* Test hook: rays and hits are host or device pointers (detected). */
+/* Test hook: rays and hits are host or device pointers (detected).  any_hit:
+ * 0 closest hit, 1 any hit, 2 any hit through the stackless traversal
+ * (PT_RENDER_ANY_STACKLESS; PT_ERR_ARG on a scene without quantized records
+ * or with instances). */
 pt_status pt_trace(pt_ctx* ctx, const pt_ray* rays, uint32_t n, int any_hit, pt_hit* hits, pt_stats* stats);
 /* Test hook: closest hit + the SurfaceInteraction the renderer reconstructs
  * (TriangleShape/QuadShape/SphereShape::Intersect incl. sample_normalMap,

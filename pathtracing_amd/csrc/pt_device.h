@@ -68,6 +68,11 @@ static_assert(sizeof(DevQNode) == 64, "qnode layout");
 #define Q48_LEAF 0x40u
 #define Q48_HOP 0x80u
 #define Q48_MAX_OFFSET 62u
+// escape links (DevScene::qesc, one per record): a node record's parent record
+// and its child slot there, parent << 2 | k (records < 2^29); ESC_EXIT at each
+// BVH's root record; ESC_BLAS marks a copy of a BLAS root in a TLAS block
+#define ESC_EXIT 0xFFFFFFFFu
+#define ESC_BLAS 0x80000000u
 #define Q48_LUT_STRIDE 136  // bytes per octant row of the LDS order table (135 perms)
 
 // ---- primitive slot geometry (48 B): what a leaf test reads.
@@ -169,6 +174,7 @@ struct DevScene {
     const DevPrimInfo* info;
     const DevGeom* qrec;       // the quantized records (null: the scene could not be encoded)
     const uint32_t* qlut;      // BVH4::LUT as 8 rows of Q48_LUT_STRIDE bytes (staged into LDS)
+    const uint32_t* qesc;      // per record: escape link of the stackless any-hit traversal (ESC_*)
     uint32_t qrec_bytes;       // bytes of qrec (< 2^32 - 256: the traversal's buffer loads address it with 32-bit offsets)
     uint32_t qroot;            // TLAS root in the records
     uint32_t root;

@@ -130,6 +130,11 @@ __global__ void k_shadow(PathSoA next, float* sample_L, ShadowRec* sq, const uin
 template <bool COUNT, bool INST, bool QN>
 __global__ void k_shadow_pool(PathSoA next, float* sample_L, ShadowRec* sq, const uint32_t* nptr,
                               uint32_t* pool, uint32_t* ovf, unsigned long long* counters);
+template <bool COUNT>
+__global__ void k_shadow_sl(PathSoA next, float* sample_L, ShadowRec* sq, const uint32_t* nptr, uint32_t* pool,
+                            uint32_t* ovf, unsigned long long* counters);
+__global__ void k_trace_rays_sl(const pt_ray* rays, uint32_t n, pt_hit* out, uint32_t* pool,
+                                unsigned long long* counters);
 template <int INTEGRATOR, bool INST, bool COUNT>
 __global__ void k_tail(RenderParams R, PathSoA cur, const uint32_t* nptr, float* sample_L,
                        unsigned long long* counters);

@@ -126,6 +126,19 @@ __device__ __noinline__ SurfXf chain_world_surface(const DevInstance* I, float t
     }
     return SurfXf{p, n, ns, tangent};
 }
+// The slot of a hit's primitive: a virtual slot (a primitive inside an
+// instance, past S.n_prims) maps to its slot in the instance's BLAS
+__device__ __forceinline__ uint32_t hit_slot(int prim) {
+    uint32_t slot = (uint32_t)prim;
+    if (slot >= S.n_prims) {
+        for (uint32_t k = 0; k < S.n_instances; k++) {
+            const DevInstance& c = S.instances[k];
+            if ((uint32_t)prim >= c.virt_base && (uint32_t)prim < c.virt_base + c.n_prims)
+                slot = c.prim_base + ((uint32_t)prim - c.virt_base);
+        }
+    }
+    return slot;
+}
 __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, float b1, float b2, SurfInt& si,
                                          int& medium, float time = 0.0f) {
     float len = 1.0f;
@@ -376,6 +389,30 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) PT_SHADOW_WAVES_FOR(PT_USES_SPEC(IN
     }
 }
 
+// The stackless any-hit traversal (pt_pool.h trace_any_stackless,
+// PT_RENDER_ANY_STACKLESS): quantized records without instances.  Its LDS
+// holds only the octant table, so registers alone set its occupancy
+#ifndef PT_SL_WPE
+#define PT_SL_WPE 8
+#endif
+template <bool COUNT>
+__global__ __launch_bounds__(PT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(PT_SL_WPE, PT_SL_WPE)))
+void k_shadow_sl(PathSoA next, float* __restrict__ sample_L, ShadowRec* __restrict__ sq,
+                 const uint32_t* __restrict__ nptr, uint32_t* __restrict__ pool, uint32_t* __restrict__,
+                 unsigned long long* counters) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_lut[Q48_LUT_BYTES];
+    TraceWork wk{0, 0};
+    ShadowSrc src{sq, next, sample_L};
+    const uint32_t n = *nptr;
+    if (n == 0) return;
+    stage_q48_lut(s_lut);
+    trace_any_stackless<COUNT, ShadowSrc>(n, pool, src, wk, s_lut);
+    if (COUNT) {
+        count_add(counters, CNT_NODES_ANY, wk.nodes);
+        count_add(counters, CNT_TRIS_ANY, wk.tris);
+    }
+}
+
 // One ray per lane (grid covers all rays): lower overhead where traversal
 // lengths are uniform (small scenes); the runtime picks per scene.  The
 // whole-leaf inner loop of trace_closest / trace_any measures faster here than
@@ -474,6 +511,19 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_trace_rays(const pt_ray* __r
     else trace_pool<false, true, RaysSrc, true, PT_POOL_LDS, QN>(n, pool, src, s_ref, ovf, wk, s_lut);
     count_add(counters, any ? CNT_NODES_ANY : CNT_NODES_CLOSEST, wk.nodes);
     count_add(counters, any ? CNT_TRIS_ANY : CNT_TRIS_CLOSEST, wk.tris);
+}
+
+// pt_trace with any_hit 2: the stackless any-hit traversal on arbitrary rays
+__global__ __launch_bounds__(PT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(PT_SL_WPE, PT_SL_WPE)))
+void k_trace_rays_sl(const pt_ray* __restrict__ rays, uint32_t n, pt_hit* __restrict__ out,
+                     uint32_t* __restrict__ pool, unsigned long long* counters) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_lut[Q48_LUT_BYTES];
+    stage_q48_lut(s_lut);
+    TraceWork wk{0, 0};
+    RaysSrc src{rays, out, nullptr, nullptr, n};
+    trace_any_stackless<true, RaysSrc>(n, pool, src, wk, s_lut);
+    count_add(counters, CNT_NODES_ANY, wk.nodes);
+    count_add(counters, CNT_TRIS_ANY, wk.tris);
 }
 
 // pt_trace's exact re-trace of the rays k_trace_rays listed for an exact-t tie
@@ -1379,7 +1429,7 @@ __global__ __launch_bounds__(PT_TRACE_BLOCK) void k_shadow_tr(PathSoA next, floa
                 break;
             }
             if (med >= 0) Tr = Tr * medium_tr(S.media[med], t);
-            if (S.info[prim].material >= 0) {
+            if (S.info[hit_slot(prim)].material >= 0) {  // (an instance's hit: a virtual slot)
                 occluded = true;
                 break;
             }
@@ -2023,6 +2073,10 @@ PT_INST_POOL(false, false, true)
 PT_INST_POOL(true, false, true)
 PT_INST_POOL(false, true, true)
 PT_INST_POOL(true, true, true)
+template __global__ void k_shadow_sl<false>(PathSoA, float*, ShadowRec*, const uint32_t*, uint32_t*, uint32_t*,
+                                           unsigned long long*);
+template __global__ void k_shadow_sl<true>(PathSoA, float*, ShadowRec*, const uint32_t*, uint32_t*, uint32_t*,
+                                          unsigned long long*);
 template __global__ void k_shadow_tr<false>(PathSoA, float*, const ShadowRecV*, const uint32_t*, unsigned long long*);
 template __global__ void k_shadow_tr<true>(PathSoA, float*, const ShadowRecV*, const uint32_t*, unsigned long long*);
 template __global__ void k_shade<PT_INTEGRATOR_PATH>(RenderParams, PathSoA, const uint32_t*, const float4*, PathSoA,

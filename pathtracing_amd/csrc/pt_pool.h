@@ -589,3 +589,260 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
         }
     }
 }
+
+// ---- Stackless any hit (north_star "stackless BVH4 traversal"; the runtime
+// option PT_RENDER_ANY_STACKLESS).  No traversal stack: a lane keeps the node
+// it is at in registers -- the record's child block (base, descriptors), the
+// octant order and the visit positions still to take among the children its
+// slab test hit -- and, when they run out, follows escape links
+// (DevScene::qesc, built with the 48-B records) up the tree: the parent
+// record is fetched again and its slab test rerun, resuming after the child
+// the lane came from.  A descent into a node's last remaining child hands that
+// node's own continuation down instead (a tail call), so only nodes with
+// hits left are fetched again.  An occlusion answer does not depend on the
+// visit order (BVH4::IntersectPred, BVH.hpp:1019-1109), so children go in
+// the octant order nearest first, as the stack kernels visit them.  BLAS
+// hops and BLAS root copies enter the BLAS with one saved continuation
+// (the rest of the TLAS leaf, then the TLAS node), restored at the BLAS
+// root's ESC_EXIT.  One node record or one primitive slot per lane per
+// iteration; LDS holds only the octant table, so occupancy is set by
+// registers alone.
+//   continuation words: (record << 2 | k) resume `record` after its child
+//   slot k; CONT_FRESH | record << 2: enter `record` (its escape applies);
+//   ESC_EXIT: leave the BLAS (or finish, at the TLAS root); SL_DONE: finish
+#define CONT_FRESH 0x80000000u
+#define SL_DONE 0xFFFFFFFEu
+#define SL_NORET 0xFFFFFFFDu  // ret_cont: no BLAS entered (ESC_EXIT is a continuation too)
+#ifndef PT_SL_MAX_STEPS
+#define PT_SL_MAX_STEPS (1u << 26)  // > 5 x the C4 records: a node is fetched at most once per child, a slot once
+#endif
+template <bool COUNT, class Src>
+__device__ void trace_any_stackless(uint32_t n, uint32_t* __restrict__ pool, Src& src, TraceWork& wk,
+                                    const uint8_t* s_lut) {
+    const uint32_t wl = __lane_id();
+    const uint32_t cs = (n + PT_POOL_CHUNKS - 1) / PT_POOL_CHUNKS;
+    const uint32_t home = blockIdx.x % PT_POOL_CHUNKS;
+    uint32_t dead = 0;  // wave-uniform: chunks found empty
+    const uint32_t all_dead = (1u << PT_POOL_CHUNKS) - 1u;
+    const __amdgpu_buffer_rsrc_t qrs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<DevGeom*>(S.qrec), (short)0, (int)S.qrec_bytes, 0x00020000);
+    // the escape links through a buffer resource too: a record index out of
+    // range reads 0 instead of faulting
+    const __amdgpu_buffer_rsrc_t ers = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t*>(S.qesc), (short)0, (int)(S.qrec_bytes / 48u * 4u), 0x00020000);
+
+    int ri = -1;
+    f3 o = F3(0, 0, 0), d = F3(0, 0, 0), inv = F3(0, 0, 0);
+    uint32_t oct = 0;
+    float tmax = 0;
+    // steps of the lane's ray: a ray past PT_SL_MAX_STEPS is abandoned and
+    // counted with the stack overflows (a traversal must end whatever the links)
+    uint32_t steps = 0;
+    // the node context: record nrec (REF_EMPTY: none), its child block and
+    // descriptors, npk = octant order byte | positions left << 8 (position p
+    // = the p-th nearest, perm index 3 - p), nup = its continuation
+    uint32_t nrec = REF_EMPTY, nbase = 0, ndesc = 0, npk = 0, nup = SL_DONE;
+    uint32_t leaf = REF_EMPTY, lk = 0;  // the primitive slot being tested; its child slot k in nrec
+    uint32_t cont = SL_DONE;            // what follows when there is neither a leaf nor a context
+    uint32_t ret_leaf = REF_EMPTY, ret_cont = SL_NORET;  // the TLAS continuation of an entered BLAS
+    for (;;) {
+        const uint64_t idle = __ballot(ri < 0);
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+        if (nidle >= PT_REFILL || idle == __ballot(true)) {
+            uint32_t base = 0, got = 0;
+            if (dead != all_dead) {
+                if (wl == 0) {
+                    #pragma unroll 1
+                    for (uint32_t k = 0; k < PT_POOL_CHUNKS; k++) {
+                        const uint32_t c = (home + k) % PT_POOL_CHUNKS;
+                        if ((dead >> c) & 1u) continue;
+                        const uint32_t lo = c * cs, hi = min(n, lo + cs);
+                        const uint32_t old = lo < hi ? atomicAdd(&pool[c * PT_POOL_STRIDE], nidle) : hi;
+                        if (lo + old < hi) {
+                            base = lo + old;
+                            got = min(nidle, hi - base);
+                            break;
+                        }
+                        dead |= 1u << c;
+                    }
+                }
+                base = __builtin_amdgcn_readfirstlane(base);
+                got = __builtin_amdgcn_readfirstlane(got);
+                dead = __builtin_amdgcn_readfirstlane(dead);
+            }
+            if (ri < 0) {
+                const uint32_t k = (uint32_t)__popcll(idle & ((1ull << wl) - 1ull));
+                if (k < got) {
+                    ri = (int)(base + k);
+                    src.load((uint32_t)ri, o, d, tmax);
+                    oct = OCT_FRESH;
+                    steps = 0;
+                    nrec = REF_EMPTY;
+                    ret_leaf = REF_EMPTY;
+                    ret_cont = SL_NORET;
+                    const uint32_t r = S.qroot;
+                    if (r & REF_LEAF) {  // a one-leaf TLAS
+                        leaf = r & ~(REF_LEAF | REF_BLOCK);
+                        cont = SL_DONE;
+                    } else {
+                        leaf = REF_EMPTY;
+                        cont = CONT_FRESH | (r << 2);
+                    }
+                }
+            }
+            if (got == 0 && dead == all_dead && __ballot(ri >= 0) == 0) break;
+        }
+        if (ri < 0) continue;
+
+        // ---- what this iteration loads: the leaf's next slot, the context's
+        // next child, or the record a continuation names (registers only)
+        uint32_t lrec = REF_EMPTY;  // node record to load
+        bool resume = false;        // ... resuming it after child slot rk (else a descent with up = lup)
+        uint32_t rk = 0, lup = SL_DONE;
+        bool finished = false;
+#pragma unroll 1
+        for (int guard = 0; guard < 4; guard++) {
+            if (leaf != REF_EMPTY || lrec != REF_EMPTY || finished) break;
+            if (nrec != REF_EMPTY) {
+                const uint32_t rem = npk >> 8;
+                if (rem == 0) {  // the context is exhausted
+                    cont = nup;
+                    nrec = REF_EMPTY;
+                    continue;
+                }
+                const uint32_t p = (uint32_t)__builtin_ctz(rem);  // the nearest child left
+                const uint32_t ci = (npk >> (2 * (3 - p))) & 3u;
+                const uint32_t dd = (ndesc >> (8 * ci)) & 0xFFu;
+                const uint32_t c = nbase + (dd & 63u);
+                const uint32_t rem2 = rem & ~(1u << p);
+                npk = (npk & 0xFFu) | rem2 << 8;
+                if (dd & Q48_LEAF) {  // a leaf: its slots in turn, the context kept
+                    leaf = c;
+                    lk = ci;
+                } else {  // descend; come back here only if children are left
+                    lrec = c;
+                    lup = rem2 ? ((nrec << 2) | ci) : nup;
+                    nrec = REF_EMPTY;
+                }
+            } else if (cont == SL_DONE) {
+                finished = true;
+            } else if (cont == ESC_EXIT) {  // out of a BLAS, or out of the TLAS root
+                if (ret_cont == SL_NORET) {
+                    finished = true;
+                } else {
+                    leaf = ret_leaf;
+                    cont = ret_cont;
+                    ret_leaf = REF_EMPTY;
+                    ret_cont = SL_NORET;
+                }
+            } else {  // a record to (re-)enter
+                lrec = (cont >> 2) & (REF_BLOCK - 1u);
+                resume = true;
+                rk = (cont & CONT_FRESH) ? 4u : (cont & 3u);
+                cont = SL_DONE;
+            }
+        }
+        if (++steps > PT_SL_MAX_STEPS) {
+            atomicAdd(S.stack_drops, 1u);
+            finished = true;
+        }
+        if (finished) {  // no occluder (BVH.hpp:1108)
+            src.any((uint32_t)ri, false);
+            ri = -1;
+            continue;
+        }
+        const bool node_step = lrec != REF_EMPTY;
+        // one 48-B record either way (three 16-B buffer loads), and a node's
+        // escape link beside it
+        const uint32_t off = (node_step ? lrec : leaf) * 48u;
+        const float4 q0 = q48_buf_load(qrs, off), q1 = q48_buf_load(qrs, off + 16u), q2 = q48_buf_load(qrs, off + 32u);
+        const uint32_t e = __builtin_amdgcn_raw_buffer_load_b32(ers, node_step ? lrec * 4u : Q48_OOB_OFFSET, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (oct & OCT_FRESH) {  // a ray claimed this iteration: its origin and direction are in
+            inv = inv_dir(d);
+            oct = ((d.z < 0) << 2) | ((d.y < 0) << 1) | (d.x < 0);
+        }
+        if (node_step) {
+            if (COUNT) wk.nodes++;
+            uint32_t mask;
+            float te[4];
+            qslab4pe(q0, q1, q2, o, inv, tmax, mask, te);
+            const uint32_t perm = q48_perm(s_lut, oct, q0.w);
+            const uint32_t desc = __float_as_uint(q2.w);
+            uint32_t rem = 0, rpos = 0;
+#pragma unroll
+            for (int p = 0; p < 4; p++) {
+                const uint32_t ci = (perm >> (2 * (3 - p))) & 3u;
+                if (((mask >> ci) & 1u) && ((desc >> (8 * ci)) & 0xFFu) != Q48_EMPTY) rem |= 1u << p;
+                if (ci == rk) rpos = (uint32_t)p;
+            }
+            uint32_t up;
+            if (resume) {
+                // after child slot rk: the positions up to it are done (rk 4:
+                // entering afresh); a root's escape (ESC_EXIT) or a BLAS copy's
+                // (its TLAS continuation is in ret_cont) leaves the BLAS
+                if (rk < 4u) rem &= ~((2u << rpos) - 1u);
+                up = (e & ESC_BLAS) ? ESC_EXIT : e;
+            } else {
+                up = lup;
+                if (e != ESC_EXIT && (e & ESC_BLAS)) {  // a copy of a BLAS root: entering the BLAS
+                    ret_leaf = REF_EMPTY;
+                    ret_cont = lup;
+                    up = ESC_EXIT;
+                }
+            }
+            nrec = lrec;
+            nbase = __float_as_uint(q2.z);
+            ndesc = desc;
+            npk = perm | rem << 8;
+            nup = up;
+        } else {
+            // ---- one primitive of the leaf: GeometricPrimitive::IntersectPred
+            // (Primitive.cpp:6-26), as trace_spec's primitive side
+            const uint32_t w0 = __float_as_uint(q0.w);
+            const uint32_t kind = w0 & GF_KIND;
+            const uint32_t ps = __float_as_uint(q2.w);  // the primitive's slot
+            const uint32_t next = (w0 & GF_LAST) ? REF_EMPTY : leaf + 1u;
+            bool anyhit = false;
+            if (kind == PT_PRIM_TRIANGLE) {
+                if (COUNT) wk.tris++;
+                if (!(w0 & GF_PRED_GLM)) {
+                    anyhit = tri_pred(o, d, xyz(q0), xyz(q1), xyz(q2), tmax);
+                } else {
+                    float bx, by, t;
+                    anyhit = tri_glm(o, d, xyz(q0), xyz(q1), xyz(q2), bx, by, t) && !(t > tmax || t < PT_EPS) &&
+                             (!(w0 & GF_ALPHA) || tri_alpha(__float_as_uint(q1.w), ps, bx, by, o, d));
+                }
+                leaf = next;
+            } else if (kind == PT_PRIM_BLAS) {
+                // into the BLAS (Model::IntersectPred, Model.hpp:29-31): the rest
+                // of this leaf and of its node wait in ret_leaf / ret_cont
+                ret_leaf = next;
+                ret_cont = nrec != REF_EMPTY ? ((npk >> 8) ? ((nrec << 2) | lk) : nup) : cont;
+                nrec = REF_EMPTY;
+                const uint32_t r = __float_as_uint(q1.x);  // the BLAS root (record, or a leaf ref)
+                if (r & REF_LEAF) {
+                    leaf = r & ~(REF_LEAF | REF_BLOCK);
+                    cont = ESC_EXIT;
+                } else {
+                    leaf = REF_EMPTY;
+                    cont = CONT_FRESH | (r << 2);
+                }
+            } else {
+                if (COUNT) wk.tris++;
+                if (kind == PT_PRIM_SPHERE && !(w0 & GF_ALPHA)) {
+                    const pt_sphere sp{{q0.x, q0.y, q0.z}, q1.x};
+                    float t2;
+                    anyhit = sphere_root(sp, o, d, tmax, t2);
+                } else {
+                    anyhit = other_pred(ps, w0, o, d, tmax);
+                }
+                leaf = next;
+            }
+            if (anyhit) {  // early exit (BVH.hpp:1104-1105)
+                src.any((uint32_t)ri, true);
+                ri = -1;
+            }
+        }
+    }
+}

@@ -60,6 +60,7 @@ struct pt_ctx {
     uint32_t n_media = 0;
     uint32_t trace_blocks = 0;  // resident traversal blocks on this device (persistent grid), max of the two
     uint32_t pool_blocks[2][2][2] = {};  // [any hit][instanced][quantized]: each pool kernel's resident blocks
+    uint32_t sl_blocks = 0;              // ... of the stackless any-hit kernel (k_shadow_sl)
     uint64_t n_clusters = 0;    // BVH clusters of the uploaded scene (traversal choice)
     bool has_qnodes = false;    // the scene's nodes have a quantized copy (48-B records)
     int node_format = PT_NODES_AUTO;  // pt_set_node_format
@@ -225,6 +226,12 @@ static pt_status create_dev(pt_ctx** out, int device) {
                     c->pool_blocks[a][i][q] = (uint32_t)std::max(1, cus * std::max(1, b));
                     c->trace_blocks = std::max(c->trace_blocks, c->pool_blocks[a][i][q]);
                 }
+        if (ok) {
+            int b = 0;
+            ok = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_shadow_sl<false>),
+                                                              PT_TRACE_BLOCK, 0) == hipSuccess;
+            c->sl_blocks = (uint32_t)std::max(1, cus * std::max(1, b));
+        }
         if (!ok) {
             g_err = "occupancy query failed";
             delete c;
@@ -244,6 +251,7 @@ static pt_status create_dev(pt_ctx** out, int device) {
         return PT_ERR_OOM;
     }
     c->scene.stack_drops = c->stack_drops;
+    c->scene.tie_drops = c->stack_drops + 1;
     *out = c;
     return PT_OK;
 }
@@ -765,17 +773,24 @@ extern "C" pt_status pt_bvh4_order_table(uint8_t* out);
 // a copy of that root's record.  BLAS-hop slots push the BLAS root's record.
 // False (the scene keeps 64-B nodes) when a block offset or the record count
 // does not fit.
+// esc (the stackless any-hit traversal's escape links, pt_pool.h
+// trace_any_stackless): per record, its node's parent record and child slot,
+// (parent << 2 | k); ESC_EXIT for every BVH's root record; a copy of a BLAS
+// root in a TLAS child block also carries ESC_BLAS (entering it enters the
+// BLAS, whose shared children escape to the original root record).
 static bool build_q48(const std::vector<DevCluster>& nodes, const std::vector<DevGeom>& geom,
                       const std::vector<uint32_t>& roots, uint32_t n_prims, std::vector<DevGeom>& rec,
-                      std::vector<uint32_t>& qroots) {
+                      std::vector<uint32_t>& qroots, std::vector<uint32_t>& esc) {
     rec.clear();
     rec.reserve(nodes.size() + n_prims + 16);
+    esc.clear();
     std::vector<uint32_t> node_rec(nodes.size(), REF_EMPTY);
     std::vector<std::pair<uint32_t, uint32_t>> copies;  // (record, cluster whose record it repeats)
     std::vector<std::pair<uint32_t, uint32_t>> work;    // (cluster, its record)
     auto alloc = [&](uint32_t n) {
         const uint32_t b = (uint32_t)rec.size();
         rec.resize(rec.size() + n);
+        esc.resize(rec.size(), 0u);
         return b;
     };
     auto leaf_len = [&](uint32_t slot) {
@@ -814,6 +829,7 @@ static bool build_q48(const std::vector<DevCluster>& nodes, const std::vector<De
             if (r >= nodes.size()) return false;
             if (node_rec[r] == REF_EMPTY) {
                 node_rec[r] = alloc(1);
+                esc[node_rec[r]] = ESC_EXIT;
                 work.push_back({r, node_rec[r]});
             }
             qroots[b] = node_rec[r];
@@ -847,8 +863,10 @@ static bool build_q48(const std::vector<DevCluster>& nodes, const std::vector<De
                     d |= Q48_LEAF | (is_hop(slot, size[k]) ? Q48_HOP : 0u);
                 } else if (node_rec[ch] != REF_EMPTY) {  // another BVH's root: a copy of its record
                     copies.push_back({base + off, ch});
+                    esc[base + off] = (r << 2) | (uint32_t)k | ESC_BLAS;
                 } else {
                     node_rec[ch] = base + off;
+                    esc[base + off] = (r << 2) | (uint32_t)k;
                     work.push_back({ch, base + off});
                 }
                 off += size[k];
@@ -881,6 +899,7 @@ static bool build_q48(const std::vector<DevCluster>& nodes, const std::vector<De
     }
     // one pad record: leaf steps may read the record after the last one
     rec.push_back(DevGeom{});
+    esc.push_back(0u);
     return !rec.empty() && rec.size() < REF_BLOCK;
 }
 
@@ -1135,15 +1154,16 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     {
         // nodes and leaf slots in one array of 48-B records (pt_device.h)
         std::vector<DevGeom> rec;
-        std::vector<uint32_t> qroots;
+        std::vector<uint32_t> qroots, esc;
         bool ok = nodes.size() < REF_BLOCK && s->n_prims < REF_BLOCK &&
-                  build_q48(nodes, geom, roots, s->n_prims, rec, qroots);
+                  build_q48(nodes, geom, roots, s->n_prims, rec, qroots, esc);
         // 32-bit buffer offsets (pt_pool.h q48_buf_load) below the out-of-range marker
         if (ok && rec.size() * sizeof(DevGeom) >= (uint64_t)Q48_OOB_OFFSET) ok = false;
         DS.qrec_bytes = ok ? (uint32_t)(rec.size() * sizeof(DevGeom)) : 0u;
         c->has_qnodes = ok;
         if (ok) {
             UP(DS.qrec, rec.data(), rec.size());
+            UP(DS.qesc, esc.data(), esc.size());
             DS.qroot = qroots[0];
             for (uint32_t k = 0; k < s->n_instances; k++) inst[k].qroot = qroots[s->instances[k].bvh];
             std::vector<uint32_t> lut(8 * Q48_LUT_STRIDE / 4, 0u);
@@ -1563,6 +1583,9 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
     const bool qn = use_pool && c->has_qnodes && !(rd->flags & PT_RENDER_NODES_FULL) &&
                     ((rd->flags & PT_RENDER_NODES_QUANTIZED) || c->node_format != PT_NODES_FULL);
     const bool timing = (rd->flags & PT_RENDER_TIMING) != 0;
+    // NEE rays through the stackless any-hit traversal (pt_pool.h
+    // trace_any_stackless): quantized records without instances
+    const bool sl = qn && !inst && (rd->flags & PT_RENDER_ANY_STACKLESS);
     // hit sort before shading: spatial by default for large scenes (C4 at 256
     // spp: 897 -> 949 Mrays/s, profiles/r02_ab_sort.txt), off for small ones
     // (the three passes cost ~0.1 ms a bounce, more than a small scene gains)
@@ -1695,7 +1718,8 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             const uint32_t nb = std::max(bound, 1u);
             const dim3 gt(use_pool ? std::min(c->pool_blocks[0][inst][qn], (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK)
                                    : (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK);
-            const dim3 ga(use_pool ? std::min(c->pool_blocks[1][inst][qn], (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK)
+            const dim3 ga(use_pool ? std::min(sl ? c->sl_blocks : c->pool_blocks[1][inst][qn],
+                                              (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK)
                                    : (nb + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK);
             const dim3 gs((nb + 255) / 256), gsh((nb + PT_SHADE_BLOCK - 1) / PT_SHADE_BLOCK);
             const dim3 gsort((nb + 256 * PT_SORT_PER - 1) / (256 * PT_SORT_PER));  // k_sort_count / k_sort_scatter
@@ -1768,7 +1792,7 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
                                    nxt, c->sample_L, (const ShadowRecV*)c->sq, (const uint32_t*)(out + Q_SHADOW),
                                    c->counters);
             } else if (rd->integrator != PT_INTEGRATOR_SIMPLE) {
-                auto ks = pick_shadow(use_pool, qn, inst, count);
+                auto ks = sl ? (count ? k_shadow_sl<true> : k_shadow_sl<false>) : pick_shadow(use_pool, qn, inst, count);
                 hipLaunchKernelGGL(ks, ga, dim3(PT_TRACE_BLOCK), 0, sa, nxt, c->sample_L, c->sq,
                                    (const uint32_t*)(out + Q_SHADOW), out + Q_WORDS + PT_POOL_WORDS,
                                    ovl ? c->ovf_any : c->ovf, c->counters);
@@ -2304,8 +2328,18 @@ extern "C" pt_status pt_trace(pt_ctx* c, const pt_ray* rays, uint32_t n, int any
     const bool qn = c->has_qnodes && (c->node_format == PT_NODES_QUANTIZED ||
                                       (c->node_format == PT_NODES_AUTO && c->n_clusters >= PT_POOL_MIN_CLUSTERS));
     const uint32_t tb = std::max(1u, std::min((n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK, c->trace_blocks));
-    hipLaunchKernelGGL(qn ? k_trace_rays<true> : k_trace_rays<false>, dim3(tb), dim3(PT_TRACE_BLOCK), 0, c->stream, dr,
-                       n, any_hit, dh, pool, c->ovf, c->counters, tl, n_ties);
+    if (any_hit == 2) {  // the stackless any-hit traversal
+        if (!qn || c->scene.n_instances) {
+            for (void* p : tmp) hipFree(p);
+            return fail(c, PT_ERR_ARG, "the stackless any-hit traversal needs quantized records and no instances");
+        }
+        hipLaunchKernelGGL(k_trace_rays_sl, dim3(std::max(1u, std::min((n + PT_TRACE_BLOCK - 1) / PT_TRACE_BLOCK,
+                                                                        c->sl_blocks))),
+                           dim3(PT_TRACE_BLOCK), 0, c->stream, (const pt_ray*)dr, n, dh, pool, c->counters);
+    } else {
+        hipLaunchKernelGGL(qn ? k_trace_rays<true> : k_trace_rays<false>, dim3(tb), dim3(PT_TRACE_BLOCK), 0, c->stream,
+                           dr, n, any_hit, dh, pool, c->ovf, c->counters, tl, n_ties);
+    }
     HIPCHK(c, hipGetLastError());
     if (!any_hit)
         hipLaunchKernelGGL(k_trace_rays_ties, dim3(std::min(64u, tb)), dim3(PT_TRACE_BLOCK), 0, c->stream,

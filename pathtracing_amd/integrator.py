@@ -165,11 +165,14 @@ class Context:
         N.check(L.pt_render_samples(self.ptr, C.byref(cam), C.byref(rd), out.ctypes.data, C.byref(st)), self.ptr)
         return out, st.as_dict()
 
-    def trace(self, rays: np.ndarray, any_hit: bool) -> tuple[np.ndarray, dict]:
+    def trace(self, rays: np.ndarray, any_hit: bool, stackless: bool = False) -> tuple[np.ndarray, dict]:
+        """pt_trace: closest or any hit per ray (test hook); stackless: any hit
+        through the stackless traversal (pt_trace any_hit 2)."""
         rays = np.ascontiguousarray(rays, dtype=N.RAY)
         hits = np.zeros(rays.shape[0], dtype=N.HIT)
         st = N.Stats()
-        N.check(self._lib.pt_trace(self.ptr, rays.ctypes.data, rays.shape[0], 1 if any_hit else 0, hits.ctypes.data,
+        mode = (2 if stackless else 1) if any_hit else 0
+        N.check(self._lib.pt_trace(self.ptr, rays.ctypes.data, rays.shape[0], mode, hits.ctypes.data,
                                    C.byref(st)), self.ptr)
         return hits, st.as_dict()
 

@@ -39,6 +39,7 @@ PT_RENDER_NO_SORT = 0x200
 PT_RENDER_SORT_RAYS = 0x400
 PT_RENDER_SERIAL_SHADOW = 0x800
 PT_RENDER_OVERLAP_SHADOW = 0x1000
+PT_RENDER_ANY_STACKLESS = 0x4000
 PT_RENDER_NO_TAIL = 0x2000
 PT_NODES_AUTO, PT_NODES_FULL, PT_NODES_QUANTIZED = 0, 1, 2
 

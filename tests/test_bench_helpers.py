@@ -44,3 +44,15 @@ def test_cpu_ratio_table_covers_the_thread_counts():
         assert set(by) >= {"1", "2", "4", "8"}
         for t, e in by.items():
             assert abs(e["port_mrays"] / e["reference_li_loop_mrays"] - e["port_over_reference"]) < 0.01
+
+
+def test_cpu_ratio_r06_full_detail_c4():
+    """r06: the port / reference ratio on the full-detail C4 scene itself
+    (tools/cpu_ratio.py), which bench.py's cpu_baseline now prefers."""
+    r = json.loads((ROOT / "profiles" / "r06_cpu_ratio.json").read_text())
+    e = r["c4_full_192x108_32spp_depth128"]
+    assert set(e["by_threads"]) >= {"1", "8"}
+    for t, v in e["by_threads"].items():
+        assert abs(v["port_mrays"] / v["reference_li_loop_mrays"] - v["port_over_reference"]) < 0.01
+    # the r03 entries merged in, so c1 keeps its ratio
+    assert "c1_example1_path_256x256_16spp" in r

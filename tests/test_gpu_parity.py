@@ -817,3 +817,54 @@ def test_gpu_anim_inverse_bit_exact_vs_reference_glm():
     want = fx["inv"]
     bad = np.nonzero((got.view(np.uint32) != want.view(np.uint32)).any(1))[0]
     assert bad.size == 0, f"{bad.size} of {len(want)} differ; first t {fx['t'][bad[:4]].tolist()}"
+
+
+# ---------------------------------------------------------------- stackless any hit (PT_RENDER_ANY_STACKLESS)
+STACKLESS_SCENES = [n for n in NAMES if n not in ("instances", "tie_instances", "lit_instances", "motion_blur",
+                                                  "motion_path", "motion_simple", "stratified_motion",
+                                                  "nested_instances", "ref_transformed_models")]
+
+
+@pytest.mark.parametrize("name", STACKLESS_SCENES)
+def test_gpu_stackless_any_hit_matches_the_reference(name):
+    """The stackless any-hit traversal (escape links, no stack; pt_trace
+    any_hit 2) answers every fixture ray as the reference's IntersectPred does
+    (BVH.hpp:1019-1109), over the quantized records of the scenes without
+    instances (the traversal's domain): TLAS leaves with BLAS hops, BLAS-root
+    copies, one-leaf BVHs, alpha-tested triangles, quads and spheres."""
+    setup, integ, fx = load(name)
+    ctx = integ.context()
+    ctx.set_node_format(N.PT_NODES_QUANTIZED)
+    try:
+        rays = _rays(fx)
+        sl, st = ctx.trace(rays, any_hit=True, stackless=True)
+        bad = np.nonzero((sl["prim"] > 0) != (fx["any"] > 0))[0]
+        assert bad.size == 0, f"any-hit differs from the reference on rays {bad[:8].tolist()}"
+        stack, _ = ctx.trace(rays, any_hit=True)
+        np.testing.assert_array_equal(sl["prim"], stack["prim"])
+        assert st["stack_overflows"] == 0 and st["nodes_any"] > 0
+    finally:
+        ctx.set_node_format(N.PT_NODES_AUTO)
+
+
+@pytest.mark.parametrize("name", ["sanmiguel", "cornell_c3", "tie_models", "ref_models", "alpha_maps"])
+def test_gpu_stackless_any_hit_li_bit_identical(name):
+    """Per-sample Li with the NEE rays through the stackless traversal, over
+    the pool kernels and quantized records: bit for bit the oracle's."""
+    setup, integ, fx = load(name)
+    L = integ.RenderSamples(flags=N.PT_RENDER_ANY_STACKLESS | N.PT_RENDER_TRAVERSAL_POOL |
+                            N.PT_RENDER_NODES_QUANTIZED)
+    Lo, _, _ = oracle.li(integ)
+    _li_bits(L, Lo, f"li_stackless/{name}")
+
+
+def test_gpu_stackless_any_hit_full_size_c4(c4_full):
+    """The full ~10 M-triangle C4 band with the stackless any-hit kernel
+    (the benched scene): every sample bit-exact against the oracle, no ray
+    abandoned (the kernel's step bound counts into stack_overflows)."""
+    setup, integ = c4_full
+    b, e = 192 * 40, 192 * 48
+    L = integ.RenderSamples(pixel_begin=b, pixel_end=e, flags=N.PT_RENDER_ANY_STACKLESS)
+    assert integ.last_stats["stack_overflows"] == 0
+    Lo, _, _ = oracle.li(integ, pixel_begin=b, pixel_end=e)
+    _li_bits(L, Lo, "li_stackless/c4_band")

@@ -5,6 +5,9 @@ scenes, sample stream and thread count, in this container (BASELINE.md §3,
 SURVEY.md §8(d) "CPU baseline timing").  TEST INFRASTRUCTURE.
 
     python tools/cpu_ratio.py profiles/r02_cpu_ratio.json
+    python tools/cpu_ratio.py OUT --scenes NAME[,NAME] --threads 1,8 --merge OLD.json
+
+(--scenes / --threads: a subset; --merge: keep OLD.json's other scenes)
 
 Both sides run a fixed-SPP tile loop over Li with the counter-based sample
 stream (ref_harness `time ... li`; oracle.render); Mrays/s counts every
@@ -34,6 +37,9 @@ def scenes_():
         "heightfield_1M_tris_256x256_16spp": lambda: scenes.heightfield(n=700, W=256, H=256, spp=16),
         "c4_recipe_2pct_160x90_16spp_depth128": lambda: scenes.sanmiguel(W=160, H=90, spp=16, detail=0.02,
                                                                        tex_size=64),
+        # the full-detail C4 scene (~10 M triangles, the benched one) on a
+        # small film: what bench.py's cpu_baseline times the port on
+        "c4_full_192x108_32spp_depth128": lambda: scenes.sanmiguel(W=192, H=108, spp=32),
     }
 
 
@@ -61,17 +67,23 @@ def _time_port(integ, threads):
     return (cnt["closest"] + cnt["any"]) / dt / 1e6
 
 
-def main(out):
+def main(out, names=None, threads=None, merge=None):
     """port / reference at every thread count 1, 2, 4, ... up to this
     container's CPUs (bench.py applies the ratio measured at the thread count
     closest to the one it times the port at)."""
     from pathtracing_amd.recipe import write_recipe
     ncpu = os.cpu_count() or 8
-    counts = sorted({1 << k for k in range(ncpu.bit_length()) if (1 << k) <= ncpu} | {ncpu})
+    counts = threads or sorted({1 << k for k in range(ncpu.bit_length()) if (1 << k) <= ncpu} | {ncpu})
     res = {"_meta": {"threads": counts, "host": "build container", "runs": 3,
                      "cpu": next((l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
                                   if l.startswith("model name")), "?")}}
+    if merge:
+        old = json.loads(Path(merge).read_text())
+        res.update({k: v for k, v in old.items() if k not in ("_meta", "summary")})
+        res["_meta"]["merged_from"] = Path(merge).name
     for name, mk in scenes_().items():
+        if names and name not in names:
+            continue
         setup = mk()
         integ = setup.make_integrator()
         entry = {"by_threads": {}}
@@ -85,15 +97,23 @@ def main(out):
                                                "port_over_reference": round(port / ref, 3)}
                 print(name, t, entry["by_threads"][str(t)], flush=True)
             entry["reference_render_mrays"] = round(
-                median([_time_ref(recipe, tmp, ncpu, setup.spp, "render") for _ in range(3)]), 3)
-        top = entry["by_threads"][str(ncpu)]
+                median([_time_ref(recipe, tmp, max(counts), setup.spp, "render") for _ in range(3)]), 3)
+        top = entry["by_threads"][str(max(counts))]
         entry.update(top)  # the full-container figures at the top level
         res[name] = entry
     ratios = [v["port_over_reference"] for k, v in res.items() if not k.startswith("_")]
     res["summary"] = {"port_over_reference_min": min(ratios), "port_over_reference_max": max(ratios),
-                      "threads": ncpu, "source": f"{Path(out).name} (tools/cpu_ratio.py)"}
+                      "threads": max(counts), "source": f"{Path(out).name} (tools/cpu_ratio.py)"}
     Path(out).write_text(json.dumps(res, indent=1, sort_keys=True))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out")
+    ap.add_argument("--scenes", default=None)
+    ap.add_argument("--threads", default=None)
+    ap.add_argument("--merge", default=None)
+    a = ap.parse_args()
+    main(a.out, a.scenes.split(",") if a.scenes else None,
+         [int(t) for t in a.threads.split(",")] if a.threads else None, a.merge)
