@@ -25,8 +25,9 @@
 extern "C" {
 #endif
 
-/* v8: pt_stats.tie_overflows (was padding), pt_anim_inverse_cases */
-#define PT_API_VERSION 8
+/* v8: pt_stats.tie_overflows (was padding), pt_anim_inverse_cases
+ * v9: pt_alpha_coverage */
+#define PT_API_VERSION 9
 
 typedef int32_t pt_status;
 #define PT_OK 0
@@ -463,6 +464,16 @@ pt_status pt_light_picks(pt_ctx* ctx, const float* u, uint32_t n, int32_t* out);
  * builds it: components never -0) -> n glm column-major 4x4 matrices (16
  * floats).  Host pointers.  Needs a context, not a scene. */
 pt_status pt_anim_inverse_cases(pt_ctx* ctx, const float* translations, uint32_t n, float* out);
+/* Check hook, host code (no device): the conservative alpha coverage masks
+ * pt_scene_upload stores with each alpha-tested triangle, replacing no
+ * reference interface (the reference runs Material::Alpha, Material.hpp:
+ * 181-198, on every candidate hit).  A cell of the triangle's N x N
+ * barycentric subdivision is "accept" when every hit in it passes the alpha
+ * test and "reject" when every hit fails.  Per primitive slot: masks4 = the
+ * 4 x 4 accept cells | reject cells << 16 (n_prims words); masks8 = the
+ * 8 x 8 accept and reject masks (2 * n_prims words); 0 for slots without an
+ * alpha test. */
+pt_status pt_alpha_coverage(const pt_scene_desc* scene, uint32_t* masks4, uint64_t* masks8);
 /* Film resolve (Film::WritePNG / WritePPM, Film.hpp:154-217): per pixel
  * color = sum RGB*w / sum w, the tone mapper (through the writers'
  * std::function<vec3(vec3)>, i.e. in float around a double body),

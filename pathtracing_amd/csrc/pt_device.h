@@ -86,8 +86,8 @@ struct alignas(16) DevGeom {
 };
 
 // ---- alpha records: what tri_alpha reads for an alpha-tested triangle, in
-// one 48-B record (its slot's b.w holds the record index; ALPHA_NONE: the
-// general path).  tri_alpha otherwise walks prim info -> shading record ->
+// one 48-B record (its slot names the record index, alpha_index below;
+// ALPHA_IDX_NONE: the general path).  tri_alpha otherwise walks prim info -> shading record ->
 // material -> texture -> image -> texels, six dependent reads inside the
 // traversal loop; here it is the record, then the texels.
 //   su / sv   the triangle's uv components in lerp3f order (uv1, uv2, uv0)
@@ -96,7 +96,10 @@ struct alignas(16) DevGeom {
 //   wh        width | height << 16;  mode = alpha mode | source << 2 |
 //             channels << 8;  cut = MASK cutoff;  scale = the alpha
 //             texture's colorScale.x (ALPHA_SRC_CH1)
-#define ALPHA_NONE 0xFFFFFFFFu
+//   acc / rej the coverage masks over the 8 x 8 subdivision (alpha_cell<8>,
+//             64 bits each, low word first): cells where every hit passes /
+//             fails the test (pt_alpha_cov.h)
+#define ALPHA_IDX_NONE 0x7FFFFFFu
 #define ALPHA_SRC_CH4 0u    // Texture::alpha of the material's texture: channel 4 (Texture.cpp:47-62)
 #define ALPHA_SRC_CH1 1u    // the material's alpha texture: Evaluate(uv).x (Material.hpp:181-198)
 #define ALPHA_SRC_CONST 2u  // a constant alpha (solid texture, or an image without a 4th channel)
@@ -105,8 +108,34 @@ struct alignas(16) DevAlpha {
     uint32_t off_lo, off_hi;
     uint32_t wh, mode;
     float cut, scale;
+    uint32_t acc[2], rej[2];
 };
-static_assert(sizeof(DevAlpha) == 48, "alpha record layout");
+static_assert(sizeof(DevAlpha) == 64, "alpha record layout");
+// ---- alpha coverage (pt_alpha_cov.h): an alpha-tested triangle's slot holds
+// the accept mask of its 4 x 4 subdivision in a.w bits 16-31 and the reject
+// mask in b.w bits 16-31 (its alpha record holds the 8 x 8 masks); the alpha
+// record index (27 bits) is split over a.w bits 5-15 (high) and b.w bits 0-15
+// (low).  The cell of a hit's barycentrics (u, v) (weights of vertices 1 and
+// 2) in the N x N subdivision: row j = floor(N v) has N - j lower and N-1-j
+// upper sub-triangles; cell j (2N - j) + 2 i + upper.  N u and N v are exact;
+// a point past the hypotenuse (by rounding only) goes to the diagonal's lower
+// cell, whose footprint margin covers it.
+// PT_ALPHA_COV: 0 no masks, 1 the record's 8 x 8 masks, 2 + the slot's 4 x 4
+#ifndef PT_ALPHA_COV
+#define PT_ALPHA_COV 1
+#endif
+__device__ __forceinline__ uint32_t alpha_index(uint32_t w0, uint32_t w1) {
+    return ((w0 >> 5) & 0x7FFu) << 16 | (w1 & 0xFFFFu);
+}
+template <int N>
+__device__ __forceinline__ uint32_t alpha_cell(float u, float v) {
+    const float a = (float)N * u, b = (float)N * v;
+    const float fi = __builtin_amdgcn_fmed3f(floorf(a), 0.0f, (float)(N - 1));
+    const float fj = __builtin_amdgcn_fmed3f(floorf(b), 0.0f, (float)(N - 1));
+    const int i = (int)fi, j = (int)fj, im = N - 1 - j;
+    const bool up = (a - fi) + (b - fj) > 1.0f && i < im;
+    return (uint32_t)(j * (2 * N - j) + 2 * min(i, im) + (up ? 1 : 0));
+}
 // Instances (TransformedPrimitive, Primitive.cpp:32-72).  A TLAS leaf slot of
 // an instance is encoded like a BLAS hop whose pushed ref is
 // REF_INST_ENTER | slot; popping it takes the lane's ray to object space

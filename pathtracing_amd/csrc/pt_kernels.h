@@ -21,7 +21,8 @@
 // reads its input count from set i % 3 (written by iteration i - 1), appends
 // into set (i + 1) % 3 and zeroes set (i + 2) % 3 for iteration i + 1.
 #define Q_TIES (Q_WORDS + 2 * PT_POOL_WORDS)  // closest-hit rays met an exact-t tie (k_closest_ties)
-#define SET_WORDS (Q_TIES + Q_STRIDE)
+#define Q_NEE (Q_TIES + Q_STRIDE)  // NEE jobs of a split bounce (PT_SHADE_SPLIT: k_shade -> k_shade_nee)
+#define SET_WORDS (Q_NEE + Q_STRIDE)
 // host snapshot slot (pinned, written by the iteration prologue)
 #define SNAP_PATHS 0        // paths entering the iteration
 #define SNAP_SHADOW_PREV 1  // shadow rays of the previous iteration
@@ -113,7 +114,14 @@ struct RenderParams {
     double inv_integral;
     double gauss_x, gauss_y;
     uint32_t strata_x, strata_y;    // a StratifiedSampler host's camera strata (pt_render_desc::strata)
+    uint2* nee_jobs;                // split bounce (PT_SHADE_SPLIT): {path index, shadow target} per NEE job
 };
+// PT_SHADE_SPLIT 1: PathIntegrator's bounce in two kernels, k_shade
+// (interaction, emission, scatter, RR -> path state, + a NEE job) and
+// k_shade_nee (the interaction again, SampleLd -> shadow record)
+#ifndef PT_SHADE_SPLIT
+#define PT_SHADE_SPLIT 0
+#endif
 
 template <bool COUNT, bool INST>
 __global__ void k_closest(PathSoA P, const uint32_t* in, float4* hit, uint32_t* pool, uint32_t* ovf, uint32_t* spare,
@@ -141,6 +149,8 @@ __global__ void k_tail(RenderParams R, PathSoA cur, const uint32_t* nptr, float*
 template <int INTEGRATOR>
 __global__ void k_shade(RenderParams R, PathSoA cur, const uint32_t* nptr, const float4* hit, PathSoA next,
                         float* sample_L, unsigned long long* next_sample, ShadowRec* sq, uint32_t* cnt);
+__global__ void k_shade_nee(RenderParams R, PathSoA cur, const uint32_t* nptr, const float4* hit, ShadowRec* sq,
+                            uint32_t* cnt);
 __global__ void k_shade_vol(RenderParams R, PathSoA cur, const uint32_t* nptr, const float4* hit, PathSoA next,
                             float* sample_L, unsigned long long* next_sample, ShadowRecV* sq, uint32_t* cnt);
 template <bool COUNT>

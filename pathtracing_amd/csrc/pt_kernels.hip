@@ -892,13 +892,57 @@ __global__ __launch_bounds__(256) void k_fill(RenderParams R, uint32_t n, PathSo
 }
 
 // ------------------------------------------------------------------ shading
+// PathIntegrator::SampleLd (Integrators.cpp:260-294) at the interaction si
+// with the hit's textures mt: the light pick (r5), its sample (r2, r3), the
+// BSDF value and MIS weight -> the shadow record (occlusion deferred).  False
+// when it contributes nothing.  dim: the bounce's dimension after its 8 draws.
+__device__ __forceinline__ bool sample_ld(const MatTex& mt, const SurfInt& si, f3 rd, f3 att, float r2, float r3,
+                                          float r5, uint32_t key, uint32_t dim, float tm, ShadowRec& srec) {
+    const int li = ls_sample(r5);
+    if (li < 0) return false;
+    const pt_light& l = S.lights[li];
+    const LSample ls = light_sample(l, r2, r3, texinf_uc(key, dim), tm);
+    f3 ldir;
+    float tmax;
+    if (is_zero(ls.n)) {
+        ldir = ls.dir;
+        tmax = __int_as_float(0x7f800000);
+    } else {
+        ldir = ls.p - si.p;
+        tmax = length(ldir) - PT_EPS;
+    }
+    const f3 sd = normalize(ldir);
+    float lpdf = l.pmf;
+    const float dt = dot_yxz(si.ns, sd);  // as built: y, x, z order
+    if (lpdf <= 0 || dt * dot(rd, si.ns) >= 0) return false;
+    const f3 f = mat_f(mt, rd, si, sd) * fabsf(dt);
+    f3 c;
+    if (light_is_delta(l)) {
+        c = (ls.L * f) / lpdf;
+    } else {
+        lpdf *= light_pdf(l, ls.p, ls.n, si.p, sd, tm);
+        if (lpdf <= 0) return false;
+        const float w2 = lpdf * lpdf;
+        const float w1 = mat_pdf(mt, rd, si, sd);
+        const float wl = w2 / fma_(w1, w1, w2);  // w1*w1 + w2 fused
+        c = ((light_L(l, ls.n, ls.u, ls.v, sd, tm) * f) * wl) / lpdf;
+    }
+    if (is_zero(c)) return false;
+    srec.o = make_float4(si.p.x, si.p.y, si.p.z, tmax);
+    srec.d = make_float4(sd.x, sd.y, sd.z, 0.0f);
+    srec.c = make_float4(c.x, c.y, c.z, 0.0f);
+    srec.a = make_float4(att.x, att.y, att.z, 0.0f);
+    return true;
+}
+
 // One bounce of PathIntegrator::Li / SimplePathIntegrator::Li for one path
 // (Integrators.cpp:131-294): the closest hit h = (t, b1, b2, prim) of the ray
 // (ro, rd) is shaded, emission and the NEE sample drawn, the next ray sampled.
 // In: the path's state (f0 = depth | rr | spec flags); out: the next state,
 // cont / done, and the NEE shadow record when `shadow`.  k_shade runs it over
-// the wavefront, k_tail per lane in a loop.
-template <int INTEGRATOR>
+// the wavefront, k_tail per lane in a loop.  NEE false (PT_SHADE_SPLIT): no
+// SampleLd here, `shadow` marks the bounces k_shade_nee samples it for.
+template <int INTEGRATOR, bool NEE = true>
 __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, uint32_t f0, f3& ro, f3& rd, f3& att,
                                              f3& out, float& prev, uint32_t key, uint32_t& dim, uint32_t& flags,
                                              bool& cont, bool& done, bool& shadow, ShadowRec& srec, float tm) {
@@ -962,49 +1006,11 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
                 if (INTEGRATOR == PT_INTEGRATOR_PATH) {
                     spec = (b.flags & FL_SPEC) != 0;
                     if (!spec) {
-                        // PathIntegrator::SampleLd (Integrators.cpp:260-294); occlusion deferred
-                        const int li = ls_sample(r[5]);
-                        if (li >= 0) {
-                            const pt_light& l = S.lights[li];
-                            const LSample ls = light_sample(l, r[2], r[3], texinf_uc(key, dim), tm);
-                            f3 ldir;
-                            float tmax;
-                            if (is_zero(ls.n)) {
-                                ldir = ls.dir;
-                                tmax = __int_as_float(0x7f800000);
-                            } else {
-                                ldir = ls.p - si.p;
-                                tmax = length(ldir) - PT_EPS;
-                            }
-                            const f3 sd = normalize(ldir);
-                            float lpdf = l.pmf;
-                            const float dt = dot_yxz(si.ns, sd);  // as built: y, x, z order
-                            if (!(lpdf <= 0 || dt * dot(rd, si.ns) >= 0)) {
-                                const f3 f = mat_f(mt, rd, si, sd) * fabsf(dt);
-                                f3 c;
-                                bool ok = true;
-                                if (light_is_delta(l)) {
-                                    c = (ls.L * f) / lpdf;
-                                } else {
-                                    lpdf *= light_pdf(l, ls.p, ls.n, si.p, sd, tm);
-                                    if (lpdf <= 0) {
-                                        ok = false;
-                                    } else {
-                                        const float w2 = lpdf * lpdf;
-                                        const float w1 = mat_pdf(mt, rd, si, sd);
-                                        const float wl = w2 / fma_(w1, w1, w2);  // w1*w1 + w2 fused
-                                        c = ((light_L(l, ls.n, ls.u, ls.v, sd, tm) * f) * wl) / lpdf;
-                                    }
-                                }
-                                if (ok && !is_zero(c)) {
-                                    shadow = true;
-                                    srec.o = make_float4(si.p.x, si.p.y, si.p.z, tmax);
-                                    srec.d = make_float4(sd.x, sd.y, sd.z, 0.0f);
-                                    srec.c = make_float4(c.x, c.y, c.z, 0.0f);
-                                    srec.a = make_float4(att.x, att.y, att.z, 0.0f);
-                                }
-                            }
-                        }
+                        // PathIntegrator::SampleLd (Integrators.cpp:260-294); occlusion
+                        // deferred.  A split bounce (NEE false) leaves it to
+                        // k_shade_nee: `shadow` then marks a NEE job.
+                        if (NEE) shadow = sample_ld(mt, si, rd, att, r[2], r[3], r[5], key, dim, tm, srec);
+                        else shadow = true;
                         prev = mat_pdf(mt, rd, si, b.d);
                     }
                 }
@@ -1062,9 +1068,10 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
         prev = b4.w;
         key = __float_as_uint(o4.w);
         dim = __float_as_uint(L4.w);
-        shade_bounce<INTEGRATOR>(R, h, __float_as_uint(d4.w), ro, rd, att, out, prev, key, dim, flags, cont, done,
-                                 shadow, srec, tm);
+        shade_bounce<INTEGRATOR, !(PT_SHADE_SPLIT && INTEGRATOR == PT_INTEGRATOR_PATH)>(
+            R, h, __float_as_uint(d4.w), ro, rd, att, out, prev, key, dim, flags, cont, done, shadow, srec, tm);
     }
+    constexpr bool split = PT_SHADE_SPLIT && INTEGRATOR == PT_INTEGRATOR_PATH;
     // a finished path stores its sample's radiance (the pending NEE ray, if
     // any, adds to it later) and its entry takes the next camera sample
     if (done) {
@@ -1077,7 +1084,7 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
     // profiles/r05_ab_shade_block.txt)
     uint32_t at[3];
     const NewSample ns = claim_camera_sample(R, done, next_sample);
-    const int qoff[3] = {Q_NEXT, Q_SHADOW, Q_NEW};
+    const int qoff[3] = {Q_NEXT, split ? Q_NEE : Q_SHADOW, Q_NEW};
     const bool pred[3] = {cont, shadow, ns.enq};
     block_append<3, PT_SHADE_BLOCK>(cnt, qoff, pred, at);
     const uint32_t a = cont ? at[0] : next.cap - 1u - at[2], c = at[1];
@@ -1091,10 +1098,56 @@ __global__ __launch_bounds__(PT_SHADE_BLOCK) PT_SHADE_WAVES void k_shade(RenderP
     } else if (ns.enq) {
         store_camera_path(next, a, ns, R.cam.medium);
     }
-    if (shadow) {
+    if (shadow && split) {
+        R.nee_jobs[c] = make_uint2(i, cont ? a : (SHADOW_DONE_BIT | sid));
+    } else if (shadow) {
         srec.d.w = __uint_as_float(cont ? a : (SHADOW_DONE_BIT | sid));
         sq[c] = srec;
         if (S.motion) S.sq_time[c] = tm;  // the shadow ray's time (Integrators.cpp:274)
+    }
+}
+
+// The NEE half of a split PathIntegrator bounce (PT_SHADE_SPLIT): per job
+// {path index in cur, shadow target} that k_shade appended, the hit's
+// interaction and textures again (hit_surface, mat_tex: the same values) and
+// SampleLd (sample_ld) with the bounce's draws 2, 3, 5 -> the shadow record.
+// cur, hit and the path's attenuation are those k_shade read (it writes the
+// next state elsewhere).
+#ifndef PT_NEE_WPE
+#define PT_NEE_WPE 4
+#endif
+__global__ __launch_bounds__(PT_SHADE_BLOCK) __attribute__((amdgpu_waves_per_eu(PT_NEE_WPE, PT_NEE_WPE)))
+void k_shade_nee(RenderParams R, PathSoA cur, const uint32_t* __restrict__ nptr, const float4* __restrict__ hit,
+                 ShadowRec* __restrict__ sq, uint32_t* __restrict__ cnt) {
+    const uint32_t n = cnt[Q_NEE], front = nptr[Q_NEXT];
+    if (blockIdx.x * PT_SHADE_BLOCK >= n) return;  // block-uniform: the grid covers the capacity
+    const uint32_t t = blockIdx.x * PT_SHADE_BLOCK + threadIdx.x;
+    bool shadow = false;
+    ShadowRec srec;
+    float tm = 0;
+    if (t < n) {
+        const uint2 job = R.nee_jobs[t];
+        const uint32_t i = job.x, e = path_slot(i, front, cur.cap);
+        const float4 o4 = cur.o[e], d4 = cur.d[e], b4 = cur.beta[e], L4 = cur.L[e];
+        const float4 h = hit[i];
+        if (S.motion) tm = cur.time[e];
+        const f3 ro = xyz(o4), rd = xyz(d4);
+        const uint32_t key = __float_as_uint(o4.w), dim0 = __float_as_uint(L4.w);
+        SurfInt si;
+        int smed;
+        hit_surface(__float_as_int(h.w), ro, rd, h.x, h.y, h.z, si, smed, tm);
+        const MatTex mt = mat_tex(si.mat, si);
+        shadow = sample_ld(mt, si, rd, xyz(b4), draw(key, dim0 + 2), draw(key, dim0 + 3), draw(key, dim0 + 5), key,
+                           dim0 + 8, tm, srec);
+        srec.d.w = __uint_as_float(job.y);
+    }
+    uint32_t c[1];
+    const int qoff[1] = {Q_SHADOW};
+    const bool pred[1] = {shadow};
+    block_append<1, PT_SHADE_BLOCK>(cnt, qoff, pred, c);
+    if (shadow) {
+        sq[c[0]] = srec;
+        if (S.motion) S.sq_time[c[0]] = tm;
     }
 }
 

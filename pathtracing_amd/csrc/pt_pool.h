@@ -283,7 +283,7 @@ __device__ void trace_spec(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 const uint32_t ps = g2w;
                 if (kind == PT_PRIM_TRIANGLE) {
                     if (COUNT) wk.tris++;
-                    if (tri_hit && (pred || !(w0 & GF_ALPHA) || tri_alpha(g1v, ps, bx, by, o, d))) {
+                    if (tri_hit && (pred || !(w0 & GF_ALPHA) || tri_alpha_cov(w0, g1v, ps, bx, by, o, d))) {
                         if (ANY) {
                             anyhit = true;
                         } else {
@@ -539,7 +539,7 @@ __device__ void trace_pool(uint32_t n, uint32_t* __restrict__ pool, Src& src, ui
                 } else {
                     float bx, by, t;
                     if (tri_glm(o, d, xyz(q0), xyz(q1), xyz(q2), bx, by, t) && !(t > tmax || t < PT_EPS)) {
-                        if (!(w0 & GF_ALPHA) || tri_alpha(__float_as_uint(q1.w), slot, bx, by, o, d)) {
+                        if (!(w0 & GF_ALPHA) || tri_alpha_cov(w0, __float_as_uint(q1.w), slot, bx, by, o, d)) {
                             if (ANY) {
                                 anyhit = true;
                             } else {
@@ -811,7 +811,7 @@ __device__ void trace_any_stackless(uint32_t n, uint32_t* __restrict__ pool, Src
                 } else {
                     float bx, by, t;
                     anyhit = tri_glm(o, d, xyz(q0), xyz(q1), xyz(q2), bx, by, t) && !(t > tmax || t < PT_EPS) &&
-                             (!(w0 & GF_ALPHA) || tri_alpha(__float_as_uint(q1.w), ps, bx, by, o, d));
+                             (!(w0 & GF_ALPHA) || tri_alpha_cov(w0, __float_as_uint(q1.w), ps, bx, by, o, d));
                 }
                 leaf = next;
             } else if (kind == PT_PRIM_BLAS) {

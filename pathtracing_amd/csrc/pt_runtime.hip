@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "pt_kernels.hip"
+#include "pt_alpha_cov.h"
 
 // The host keeps up to PT_LAG wavefront iterations queued ahead of the one
 // whose counts it reads (no per-bounce round trip; iterations past the end of
@@ -101,6 +102,8 @@ struct pt_ctx {
     uint32_t* ray_order = nullptr;  // PT_RENDER_SORT_RAYS: closest-hit claim order
     uint32_t* ray_counts = nullptr;
     uint64_t ray_order_cap = 0, ray_counts_cap = 0;
+    uint2* nee_jobs = nullptr;  // PT_SHADE_SPLIT: k_shade's NEE jobs for k_shade_nee
+    uint64_t nee_jobs_cap = 0;
     hipEvent_t ev[8] = {};
     hipEvent_t rev[PT_RING][5] = {};  // per in-flight iteration: kernel boundaries [0..2], end [4] ([3] unused)
     uint32_t* stack_drops = nullptr;  // device words: traversal pushes beyond the stack, exact-tie list drops
@@ -505,7 +508,7 @@ extern "C" void pt_destroy(pt_ctx* c) {
     if (c->film) hipFree(c->film);
     for (void* p : {(void*)c->a_est, (void*)c->a_counts, (void*)c->a_map, (void*)c->a_list, (void*)c->a_cnt,
                     (void*)c->sort_order, (void*)c->sort_counts, (void*)c->ray_order, (void*)c->ray_counts,
-                    (void*)c->sort_bins})
+                    (void*)c->sort_bins, (void*)c->nee_jobs})
         if (p) hipFree(p);
     if (c->host_cnt) hipHostFree(c->host_cnt);
     if (c->stack_drops) hipFree(c->stack_drops);
@@ -713,6 +716,56 @@ static bool alpha_record(const pt_scene_desc* s, const pt_prim& p, DevAlpha& r) 
     return true;
 }
 
+static PtAlphaRecord alpha_cov_record(const DevAlpha& r) {
+    PtAlphaRecord a;
+    std::memset(&a, 0, sizeof a);  // the coverage memo keys on the bytes
+    for (int k = 0; k < 3; k++) a.su[k] = r.su[k], a.sv[k] = r.sv[k];
+    a.src = (r.mode >> 2) & 3u;
+    a.mode = r.mode & 3u;
+    a.cut = r.cut;
+    a.scale = r.scale;
+    if (a.src == ALPHA_SRC_CONST) {
+        a.constant = __builtin_bit_cast(float, r.off_lo);
+    } else {
+        a.off = (uint64_t)r.off_lo | (uint64_t)r.off_hi << 32;
+        a.W = r.wh & 0xFFFFu, a.H = r.wh >> 16, a.C = (r.mode >> 8) & 0xFFu;
+    }
+    return a;
+}
+
+// The alpha records of the alpha-tested triangles among the slots `geom`
+// (flags in a.w already set) with their 8 x 8 coverage masks, and each slot's
+// 4 x 4 masks + record index (pt_device.h).  Test hook outputs (may be null):
+// masks4 accept | reject << 16 per slot, masks8 {accept, reject} per slot.
+static void alpha_records(const pt_scene_desc* s, std::vector<DevGeom>& geom, std::vector<DevAlpha>* alpha,
+                          uint32_t* masks4, uint64_t* masks8) {
+    PtAlphaCoverage cov(s->texels, s->texels ? s->n_texel_bytes : 0);
+    uint32_t n = 0;
+    for (uint32_t i = 0; i < s->n_prims; i++) {
+        if (masks4) masks4[i] = 0;
+        if (masks8) masks8[2 * i] = masks8[2 * i + 1] = 0;
+        const uint32_t fl = __builtin_bit_cast(uint32_t, geom[i].a.w);
+        if ((fl & GF_KIND) != PT_PRIM_TRIANGLE || !(fl & GF_ALPHA)) continue;
+        DevAlpha r;
+        const bool fast = n < ALPHA_IDX_NONE && alpha_record(s, s->prims[i], r);
+        const uint32_t idx = fast ? n++ : ALPHA_IDX_NONE;
+        PtAlphaMasks m4{0, 0}, m8{0, 0};
+        if (fast) {
+            const PtAlphaRecord a = alpha_cov_record(r);
+            m4 = cov.masks(a, 4);
+            m8 = cov.masks(a, 8);
+        }
+        const uint32_t m = (uint32_t)m4.acc | (uint32_t)m4.rej << 16;
+        r.acc[0] = (uint32_t)m8.acc, r.acc[1] = (uint32_t)(m8.acc >> 32);
+        r.rej[0] = (uint32_t)m8.rej, r.rej[1] = (uint32_t)(m8.rej >> 32);
+        geom[i].a.w = __builtin_bit_cast(float, (fl & 0x1Fu) | (idx >> 16) << 5 | (m & 0xFFFFu) << 16);
+        geom[i].b.w = __builtin_bit_cast(float, (idx & 0xFFFFu) | (m >> 16) << 16);
+        if (masks4) masks4[i] = m;
+        if (masks8) masks8[2 * i] = m8.acc, masks8[2 * i + 1] = m8.rej;
+        if (fast && alpha) alpha->push_back(r);
+    }
+}
+
 struct Conv {
     const pt_scene_desc* s;
     std::vector<DevCluster>& nodes;
@@ -912,12 +965,9 @@ extern "C" pt_status pt_scene_upload(pt_ctx* c, const pt_scene_desc* s) {
         if (pt_status st = upload_dev(p, s)) return fail(c, st, "device %d: %s", p->device, p->err.c_str());
     return PT_OK;
 }
-static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
-    if (!c || !s) return PT_ERR_ARG;
-    DeviceLock dl(c->device);
-    HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    free_scene(c);
+// Validate a scene description (pt_scene_upload's checks, also the host
+// hooks' that read it)
+static pt_status validate_scene(pt_ctx* c, const pt_scene_desc* s) {
     if (s->n_bvhs == 0 || !s->bvhs || s->n_prims == 0 || !s->prims)
         return fail(c, PT_ERR_ARG, "scene needs a TLAS and primitives");
     // ---- validate
@@ -1028,11 +1078,11 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     if (s->scene_medium < -1 || s->scene_medium >= (int32_t)s->n_media) return fail(c, PT_ERR_ARG, "bad scene medium");
     for (uint32_t i = 0; i < s->n_infinite_lights; i++)
         if (s->infinite_lights[i] >= s->n_lights) return fail(c, PT_ERR_ARG, "infinite light %u out of range", i);
+    return PT_OK;
+}
 
-    // ---- geometry slots
-    // one zero pad slot past the end: pool leaf steps read slot + 1 unconditionally
-    std::vector<DevGeom> geom(s->n_prims + 1);
-    std::vector<DevPrimInfo> info(s->n_prims);
+// The primitive slots' geometry and flags (DevGeom, pt_device.h) and info
+static void slot_geometry(const pt_scene_desc* s, std::vector<DevGeom>& geom, std::vector<DevPrimInfo>& info) {
     for (uint32_t i = 0; i < s->n_prims; i++) {
         const pt_prim& p = s->prims[i];
         uint32_t flags = p.kind;
@@ -1061,16 +1111,25 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
         geom[i] = g;
         info[i] = DevPrimInfo{p.material, p.light, p.medium, p.index};
     }
-    // ---- alpha records of the alpha-tested triangles (the slot's b.w names one)
+}
+
+static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
+    if (!c || !s) return PT_ERR_ARG;
+    DeviceLock dl(c->device);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    free_scene(c);
+    if (pt_status st = validate_scene(c, s)) return st;
+
+    // ---- geometry slots
+    // one zero pad slot past the end: pool leaf steps read slot + 1 unconditionally
+    std::vector<DevGeom> geom(s->n_prims + 1);
+    std::vector<DevPrimInfo> info(s->n_prims);
+    slot_geometry(s, geom, info);
+    // ---- alpha records of the alpha-tested triangles and their coverage
+    // masks (pt_device.h alpha_index / alpha_cell, pt_alpha_cov.h)
     std::vector<DevAlpha> alpha;
-    for (uint32_t i = 0; i < s->n_prims; i++) {
-        const uint32_t fl = __builtin_bit_cast(uint32_t, geom[i].a.w);
-        if ((fl & GF_KIND) != PT_PRIM_TRIANGLE || !(fl & GF_ALPHA)) continue;
-        DevAlpha r;
-        const bool fast = alpha_record(s, s->prims[i], r);
-        geom[i].b.w = __builtin_bit_cast(float, fast ? (uint32_t)alpha.size() : ALPHA_NONE);
-        if (fast) alpha.push_back(r);
-    }
+    alpha_records(s, geom, &alpha, nullptr, nullptr);
     // ---- nodes: TLAS then every BLAS, converted from the root descriptors
     std::vector<uint32_t> cbase(s->n_bvhs);
     uint64_t total = 0;
@@ -1400,7 +1459,7 @@ static void free_paths(pt_ctx* c) {
         void** p;
         uint64_t* cap;
     } bufs[] = {{(void**)&c->sort_order, &c->sort_order_cap}, {(void**)&c->sort_bins, &c->sort_bins_cap},
-                {(void**)&c->ray_order, &c->ray_order_cap}};
+                {(void**)&c->ray_order, &c->ray_order_cap}, {(void**)&c->nee_jobs, &c->nee_jobs_cap}};
     for (const Buf& b : bufs) {
         if (*b.p) hipFree(*b.p);
         *b.p = nullptr;
@@ -1610,6 +1669,9 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             if ((s = ensure(c, &c->sort_counts, c->sort_counts_cap, PT_SORT_BINS_SPATIAL)) != PT_OK) return s;
         }
         if (keep_bins && (s = ensure(c, &c->sort_bins, c->sort_bins_cap, p)) != PT_OK) return s;
+        if (PT_SHADE_SPLIT && rd->integrator == PT_INTEGRATOR_PATH &&
+            (s = ensure(c, &c->nee_jobs, c->nee_jobs_cap, p)) != PT_OK)
+            return s;
         return bind_scene(c);  // instance scratch and ray-time buffers sized for this wavefront
     };
     while ((st = alloc_paths(paths)) == PT_ERR_OOM && paths > (1u << 20)) {
@@ -1779,10 +1841,15 @@ static pt_status run(pt_ctx* c, const pt_camera_desc* cam, const pt_render_desc*
             else if (rd->integrator == PT_INTEGRATOR_VOLPATH)
                 hipLaunchKernelGGL(k_shade_vol, gs, dim3(256), 0, sm, R, cur, (const uint32_t*)(in + Q_NEXT),
                                    (const float4*)c->hit, nxt, c->sample_L, next_sample, (ShadowRecV*)c->sq, out);
-            else
+            else {
+                R.nee_jobs = c->nee_jobs;
                 hipLaunchKernelGGL(k_shade<PT_INTEGRATOR_PATH>, gsh, dim3(PT_SHADE_BLOCK), 0, sm, R, cur,
                                    (const uint32_t*)(in + Q_NEXT), (const float4*)c->hit, nxt, c->sample_L,
                                    next_sample, c->sq, out);
+                if (PT_SHADE_SPLIT)  // the bounce's NEE half (pt_kernels.h)
+                    hipLaunchKernelGGL(k_shade_nee, gsh, dim3(PT_SHADE_BLOCK), 0, sm, R, cur,
+                                       (const uint32_t*)(in + Q_NEXT), (const float4*)c->hit, c->sq, out);
+            }
             if (timing || ovl) HIPCHK(c, hipEventRecord(ev[2], sm));
             if (ovl) HIPCHK(c, hipStreamWaitEvent(sa, ev[2], 0));
             if (rd->integrator == PT_INTEGRATOR_VOLPATH) {
@@ -2463,6 +2530,18 @@ extern "C" pt_status pt_light_picks(pt_ctx* c, const float* u, uint32_t n, int32
                         hipLaunchKernelGGL(k_light_picks, dim3((n + 255) / 256), dim3(256), 0, c->stream,
                                            (const float*)din, n, reinterpret_cast<int32_t*>(dout));
                     });
+}
+
+// Test hook (host code, no device): the coverage masks pt_scene_upload stores
+// for the alpha-tested triangles (pt_alpha_cov.h), 0 for the other slots.
+extern "C" pt_status pt_alpha_coverage(const pt_scene_desc* s, uint32_t* masks4, uint64_t* masks8) {
+    if (!s || !masks4 || !masks8) return PT_ERR_ARG;
+    if (pt_status st = validate_scene(nullptr, s)) return st;
+    std::vector<DevGeom> geom(s->n_prims + 1);
+    std::vector<DevPrimInfo> info(s->n_prims);
+    slot_geometry(s, geom, info);
+    alpha_records(s, geom, nullptr, masks4, masks8);
+    return PT_OK;
 }
 
 extern "C" pt_status pt_anim_inverse_cases(pt_ctx* c, const float* t, uint32_t n, float* out) {

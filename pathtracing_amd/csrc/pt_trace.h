@@ -129,7 +129,7 @@ __device__ __forceinline__ uint32_t alpha_texel_byte(const uint8_t* base, uint64
 // The material alpha test of an alpha-tested triangle at its candidate hit
 // (GeometricPrimitive::Intersect -> Material::Alpha, Primitive.cpp:6-26,
 // Material.hpp:181-198).  ai: the slot's alpha record (DevAlpha, slot b.w):
-// the record, then the four texels; ALPHA_NONE: prim info -> shading record
+// the record, then the four texels; ALPHA_IDX_NONE: prim info -> shading record
 // -> material -> texture -> image.  Same values either way.
 __device__ __forceinline__ bool tri_alpha_general(uint32_t slot, float bu, float bv, f3 o, f3 d);
 __device__ __noinline__ bool tri_alpha_slow(uint32_t slot, float bu, float bv, f3 o, f3 d) {
@@ -141,16 +141,34 @@ __device__ __noinline__ bool tri_alpha_slow(uint32_t slot, float bu, float bv, f
 __device__ __forceinline__ bool tri_alpha_rec(const DevAlpha& r, uint32_t slot, float bu, float bv, f3 o, f3 d);
 __device__ __forceinline__
 bool tri_alpha(uint32_t ai, uint32_t slot, float bu, float bv, f3 o, f3 d) {
-    if (ai != ALPHA_NONE) {
-        // the whole record in three 16-B loads issued together (a reference
+    if (ai != ALPHA_IDX_NONE) {
+        // the whole record in four 16-B loads issued together (a reference
         // into S.alpha would let the compiler read its fields where they are
         // used, in branches, one round trip each)
         const float4* ap = reinterpret_cast<const float4*>(S.alpha + ai);
-        const float4 a0 = ap[0], a1 = ap[1], a2 = ap[2];
-        const DevAlpha r = __builtin_bit_cast(DevAlpha, (DevGeom{a0, a1, a2}));
+        const float4 a0 = ap[0], a1 = ap[1], a2 = ap[2], a3 = ap[3];
+        if (PT_ALPHA_COV >= 1) {  // a cell the 8 x 8 masks decide: no texel read
+            const uint32_t c = alpha_cell<8>(bu, bv);
+            const uint32_t acc = __float_as_uint(c < 32 ? a3.x : a3.y), rej = __float_as_uint(c < 32 ? a3.z : a3.w);
+            if ((acc >> (c & 31)) & 1u) return true;
+            if ((rej >> (c & 31)) & 1u) return false;
+        }
+        struct Rec { float4 a, b, c, d; };
+        const DevAlpha r = __builtin_bit_cast(DevAlpha, (Rec{a0, a1, a2, a3}));
         return tri_alpha_rec(r, slot, bu, bv, o, d);
     }
     return tri_alpha_slow(slot, bu, bv, o, d);
+}
+// the test from a slot's words w0 = a.w, w1 = b.w: a cell its coverage masks
+// decide (pt_alpha_cov.h) answers without a read; the others run the exact test
+__device__ __forceinline__
+bool tri_alpha_cov(uint32_t w0, uint32_t w1, uint32_t slot, float bu, float bv, f3 o, f3 d) {
+    if (PT_ALPHA_COV >= 2) {
+        const uint32_t c = alpha_cell<4>(bu, bv);
+        if ((w0 >> 16 >> c) & 1u) return true;
+        if ((w1 >> 16 >> c) & 1u) return false;
+    }
+    return tri_alpha(alpha_index(w0, w1), slot, bu, bv, o, d);
 }
 // the test over an alpha record already read
 __device__ __forceinline__ bool tri_alpha_rec(const DevAlpha& r, uint32_t slot, float bu, float bv, f3 o, f3 d) {
@@ -590,7 +608,7 @@ __device__ int trace_closest(f3 o, f3 d, float tmax, float& t_out, float& b1_out
             if (kind == PT_PRIM_TRIANGLE) {
                 float bx, by, t;
                 if (tri_glm(o, d, xyz(g.a), xyz(g.b), xyz(g.c), bx, by, t) && !(t > tmax || t < PT_EPS)) {
-                    if (!(w0 & GF_ALPHA) || tri_alpha(__float_as_uint(g.b.w), slot, bx, by, o, d)) {
+                    if (!(w0 & GF_ALPHA) || tri_alpha_cov(w0, __float_as_uint(g.b.w), slot, bx, by, o, d)) {
                         tmax = t;
                         best = (int)slot;
                         bb1 = bx;
@@ -685,7 +703,7 @@ __device__ bool trace_any(f3 o, f3 d, float tmax, uint32_t* s_ref, TraceWork& wk
                     // material HasAlpha(): full Intersect + Alpha (Primitive.cpp:7-10)
                     float bx, by, t;
                     if (tri_glm(o, d, xyz(g.a), xyz(g.b), xyz(g.c), bx, by, t) && !(t > tmax || t < PT_EPS)) {
-                        if (!(w0 & GF_ALPHA) || tri_alpha(__float_as_uint(g.b.w), slot, bx, by, o, d)) return true;
+                        if (!(w0 & GF_ALPHA) || tri_alpha_cov(w0, __float_as_uint(g.b.w), slot, bx, by, o, d)) return true;
                     }
                 } else if (tri_pred(o, d, xyz(g.a), xyz(g.b), xyz(g.c), tmax)) {
                     return true;

@@ -220,6 +220,8 @@ def lib():
     L.pt_light_picks.restype = C.c_int32
     L.pt_anim_inverse_cases.argtypes = [vp, vp, C.c_uint32, vp]
     L.pt_anim_inverse_cases.restype = C.c_int32
+    L.pt_alpha_coverage.argtypes = [C.POINTER(SceneDesc), vp, vp]
+    L.pt_alpha_coverage.restype = C.c_int32
     L.pt_scene_device_bytes.argtypes = [vp]
     L.pt_scene_device_bytes.restype = C.c_uint64
     L.pt_bvh4_build.argtypes = [vp, C.c_uint32, vp, C.POINTER(C.c_uint32), C.POINTER(RefNode), vp, vp]

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_version_and_error_paths_without_device():
     lib = N.lib()
-    assert lib.pt_version() == 8
+    assert lib.pt_version() == 9
     # argument validation never aborts
     assert lib.pt_scene_upload(None, None) == -1
     assert lib.pt_render(None, None, None, None, None) == -1

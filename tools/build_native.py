@@ -61,6 +61,10 @@ def build_product(force: bool = False, variant: str = "", defines=()) -> Path:
     env_o = build / "pt_envmap.o"
     _run(["g++", "-std=gnu++20", "-O3", "-march=x86-64-v3", "-ffp-contract=off", "-fPIC", "-c",
           CSRC / "pt_envmap.cpp", "-o", env_o, *inc])
+    # alpha coverage masks (host, upload time; pt_alpha_cov.h)
+    cov_o = build / "pt_alpha_cov.o"
+    _run(["g++", "-std=gnu++20", "-O2", "-march=x86-64-v3", "-ffp-contract=off", "-fPIC", "-c",
+          CSRC / "pt_alpha_cov.cpp", "-o", cov_o, *inc])
     rt_o = build / "pt_runtime.o"
     extra = [d for d in defines if d.startswith("-")]  # raw compiler flags of a tuning variant
     defs = [f"-D{d}" for d in defines if not d.startswith("-")]
@@ -68,7 +72,7 @@ def build_product(force: bool = False, variant: str = "", defines=()) -> Path:
           "-Wno-unused-result", "-Wno-unused-value", *FP_FLAGS, *extra, *defs,
           "-c", CSRC / "pt_runtime.hip", "-o", rt_o, *inc])
     tmp = out.with_suffix(".so.tmp")
-    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", rt_o, bvh_o, env_o, "-o", tmp, "-lrccl", "-lpthread"])
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", rt_o, bvh_o, env_o, cov_o, "-o", tmp, "-lrccl", "-lpthread"])
     os.replace(tmp, out)
     return out
 
