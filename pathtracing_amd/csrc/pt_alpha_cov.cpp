@@ -55,23 +55,26 @@ int wrap_ranges(int64_t X0, int64_t X1, int n, int r[2][2]) {
 }
 }  // namespace
 
-void PtAlphaCoverage::Pyramid::query(int x0, int x1, int y0, int y1, uint8_t& lo, uint8_t& hi) const {
+uint64_t PtAlphaCoverage::Pyramid::query(int x0, int x1, int y0, int y1, uint8_t& lo, uint8_t& hi) const {
     const int w = x1 - x0 + 1, h = y1 - y0 + 1;
     int k = 0;
     while (k + 1 < (int)mn.size() && (2 << k) <= std::min(w, h)) k++;
     const int s = 1 << k;
     const std::vector<uint8_t>& A = mn[k];
     const std::vector<uint8_t>& B = mx[k];
+    uint64_t n = 0;
     for (int y = y0;; y += s) {
         const int yy = std::min(y, y1 - s + 1);
         for (int x = x0;; x += s) {
             const size_t i = (size_t)yy * W + std::min(x, x1 - s + 1);
             lo = std::min(lo, A[i]);
             hi = std::max(hi, B[i]);
+            n++;
             if (x + s > x1) break;
         }
         if (y + s > y1) break;
     }
+    return n;
 }
 
 const PtAlphaCoverage::Pyramid* PtAlphaCoverage::pyramid(uint64_t off, uint32_t W, uint32_t H, uint32_t C,
@@ -111,7 +114,7 @@ const PtAlphaCoverage::Pyramid* PtAlphaCoverage::pyramid(uint64_t off, uint32_t 
 // over the band (widened), so the footprint follows the triangle's shape, not
 // its bounding box.  False when the coordinates are too large to reason about.
 bool PtAlphaCoverage::footprint(const Pyramid& P, const double px[3], const double py[3], double mx, double my,
-                                uint8_t& blo, uint8_t& bhi) const {
+                                uint8_t& blo, uint8_t& bhi) {
     double ylo = std::min({py[0], py[1], py[2]}) - my, yhi = std::max({py[0], py[1], py[2]}) + my;
     double xlo = std::min({px[0], px[1], px[2]}) - mx, xhi = std::max({px[0], px[1], px[2]}) + mx;
     if (!(std::fabs(ylo) < MAX_COORD && std::fabs(yhi) < MAX_COORD && std::fabs(xlo) < MAX_COORD &&
@@ -146,33 +149,51 @@ bool PtAlphaCoverage::footprint(const Pyramid& P, const double px[3], const doub
         int rx[2][2], ry[2][2];
         const int nx = wrap_ranges(X0, X1, P.W, rx), ny = wrap_ranges(r0, r0 + s, P.H, ry);
         for (int a = 0; a < nx; a++)
-            for (int b = 0; b < ny; b++) P.query(rx[a][0], rx[a][1], ry[b][0], ry[b][1], blo, bhi);
+            for (int b = 0; b < ny; b++) lookups_ += P.query(rx[a][0], rx[a][1], ry[b][0], ry[b][1], blo, bhi);
     }
     return true;
 }
 
-PtAlphaMasks PtAlphaCoverage::masks(const PtAlphaRecord& r, int n) {
-    const uint64_t all = n >= 8 ? ~0ull : (1ull << (n * n)) - 1;
-    if (r.mode == M_OPAQUE) return {all, 0};  // tri_alpha_rec returns true whatever a is
-    if (r.src == SRC_CONST) {
-        const double a = r.constant;
-        const int k = decide(r.mode, a, a, r.cut);
-        return {k == 1 ? all : 0, k == 2 ? all : 0};
+// the subdivision for a triangle spanning `ext` texels: cells of ~8 texels, 4 .. 32 per side
+static int cells_per_side(double ext) {
+    int n = 4;
+    while (n < 32 && ext > 8.0 * n) n *= 2;
+    return n;
+}
+
+uint32_t PtAlphaCoverage::set(const PtAlphaRecord& rec) {
+    PtAlphaRecord r = rec;
+    const bool whole = r.mode == M_OPAQUE || r.src == SRC_CONST;  // one verdict for every cell
+    if (!whole && r.src != SRC_CH4 && r.src != SRC_CH1) return PT_ALPHA_SET_NONE;
+    if (whole) {  // the verdict does not depend on the uvs: one shared set
+        for (int k = 0; k < 3; k++) r.su[k] = r.sv[k] = 0.0f;
+        r.off = 0, r.W = r.H = r.C = 0;
     }
-    PtAlphaMasks out{0, 0};
-    if ((r.src != SRC_CH4 && r.src != SRC_CH1) || n < 1 || n > 8) return out;
     std::string key(reinterpret_cast<const char*>(&r), sizeof r);
-    key.push_back((char)n);
     if (auto it = memo_.find(key); it != memo_.end()) return it->second;
-    const Pyramid* P = pyramid(r.off, r.W, r.H, r.C, r.src == SRC_CH4 ? 3u : 0u);
-    double maxu = 0, maxv = 0;
+    uint32_t out = PT_ALPHA_SET_NONE;
+    const Pyramid* P = whole ? nullptr : pyramid(r.off, r.W, r.H, r.C, r.src == SRC_CH4 ? 3u : 0u);
+    double maxu = 0, maxv = 0, ext = 0;
     bool finite = std::isfinite(r.scale);
     for (int k = 0; k < 3; k++) {
         finite = finite && std::isfinite(r.su[k]) && std::isfinite(r.sv[k]);
         maxu = std::max(maxu, std::fabs((double)r.su[k]));
         maxv = std::max(maxv, std::fabs((double)r.sv[k]));
+        const int m = (k + 1) % 3;
+        ext = std::max({ext, std::fabs((double)r.su[m] - r.su[k]) * r.W, std::fabs((double)r.sv[m] - r.sv[k]) * r.H});
     }
-    if (P && finite) {
+    const int n = whole ? 4 : cells_per_side(ext);
+    const uint32_t wpm = std::max(1, n * n / 32);  // words per mask
+    std::vector<uint32_t> acc(wpm, 0), rej(wpm, 0);
+    bool any = false;
+    if (whole) {
+        const double a = r.mode == M_OPAQUE ? 1.0 : (double)r.constant;
+        const int k = decide(r.mode, a, a, r.cut);
+        if (k) {
+            (k == 1 ? acc : rej)[0] = 0xFFFFu;
+            any = true;
+        }
+    } else if (P && finite && lookups_ < PT_ALPHA_LOOKUP_BUDGET && words_.size() + 2 * wpm < (1u << 30)) {
         // texel-space margins: far above the float error of the computed
         // barycentrics' lerp and of u W - 0.5 (a few ulp of max|u| W)
         const double mx = 1e-4 + 1e-5 * (maxu * r.W + 1.0), my = 1e-4 + 1e-5 * (maxv * r.H + 1.0);
@@ -203,9 +224,18 @@ PtAlphaMasks PtAlphaCoverage::masks(const PtAlphaRecord& r, int n) {
                         hi = std::max(s * tlo, s * thi) + e;
                     }
                     const int dcs = decide(r.mode, lo, hi, r.cut);
-                    if (dcs == 1) out.acc |= 1ull << cell;
-                    if (dcs == 2) out.rej |= 1ull << cell;
+                    if (dcs) {
+                        (dcs == 1 ? acc : rej)[cell >> 5] |= 1u << (cell & 31);
+                        any = true;
+                    }
                 }
+    }
+    if (any) {
+        int ln = 0;
+        while ((4 << ln) < n) ln++;
+        out = (uint32_t)words_.size() | (uint32_t)ln << 30;
+        words_.insert(words_.end(), acc.begin(), acc.end());
+        words_.insert(words_.end(), rej.begin(), rej.end());
     }
     memo_.emplace(std::move(key), out);
     return out;

@@ -33,15 +33,22 @@ struct PtAlphaRecord {
     float cut, scale, constant;
 };
 
-struct PtAlphaMasks {
-    uint64_t acc, rej;  // bit c: cell c decided accept / reject
-};
+// A mask set (the upload's word array words()): accept mask then reject
+// mask over the n x n cells (cell c: bit c & 31 of word c >> 5), each
+// max(1, n n / 32) words.  Its handle = word offset | log2(n / 4) << 30;
+// PT_ALPHA_SET_NONE: no cell decided (or no set computed).
+#define PT_ALPHA_SET_NONE 0xFFFFFFFFu
+// square-table lookups the masks of one upload may spend (host time); the
+// records past it get no set
+#define PT_ALPHA_LOOKUP_BUDGET (1ull << 31)
 
 class PtAlphaCoverage {
 public:
     PtAlphaCoverage(const uint8_t* texels, uint64_t n_texel_bytes) : texels_(texels), n_(n_texel_bytes) {}
-    // the masks over the n x n subdivision (n * n cells, n <= 8)
-    PtAlphaMasks masks(const PtAlphaRecord& r, int n);
+    // the mask set of a record (n from the triangle's texel extent: cells of
+    // ~8 texels, 4 .. 32 per side); identical records share one set
+    uint32_t set(const PtAlphaRecord& r);
+    const std::vector<uint32_t>& words() const { return words_; }
 
 private:
     // min / max of one channel over every 2^k x 2^k square (k <= 6): any
@@ -49,13 +56,15 @@ private:
     struct Pyramid {
         int W, H;
         std::vector<std::vector<uint8_t>> mn, mx;  // [k][y W + x]: square at (x, y)
-        void query(int x0, int x1, int y0, int y1, uint8_t& lo, uint8_t& hi) const;
+        uint64_t query(int x0, int x1, int y0, int y1, uint8_t& lo, uint8_t& hi) const;  // -> squares read
     };
     bool footprint(const Pyramid& P, const double px[3], const double py[3], double mx, double my, uint8_t& blo,
-                   uint8_t& bhi) const;
+                   uint8_t& bhi);
     const Pyramid* pyramid(uint64_t off, uint32_t W, uint32_t H, uint32_t C, uint32_t ch);
     const uint8_t* texels_;
     uint64_t n_;
     std::map<std::tuple<uint64_t, uint32_t, uint32_t, uint32_t, uint32_t>, std::unique_ptr<Pyramid>> pyr_;
-    std::unordered_map<std::string, PtAlphaMasks> memo_;  // identical records (leaf cards share uvs)
+    std::unordered_map<std::string, uint32_t> memo_;  // identical records (leaf cards share uvs)
+    std::vector<uint32_t> words_;
+    uint64_t lookups_ = 0;
 };

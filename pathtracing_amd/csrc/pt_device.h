@@ -96,9 +96,6 @@ struct alignas(16) DevGeom {
 //   wh        width | height << 16;  mode = alpha mode | source << 2 |
 //             channels << 8;  cut = MASK cutoff;  scale = the alpha
 //             texture's colorScale.x (ALPHA_SRC_CH1)
-//   acc / rej the coverage masks over the 8 x 8 subdivision (alpha_cell<8>,
-//             64 bits each, low word first): cells where every hit passes /
-//             fails the test (pt_alpha_cov.h)
 #define ALPHA_IDX_NONE 0x7FFFFFFu
 #define ALPHA_SRC_CH4 0u    // Texture::alpha of the material's texture: channel 4 (Texture.cpp:47-62)
 #define ALPHA_SRC_CH1 1u    // the material's alpha texture: Evaluate(uv).x (Material.hpp:181-198)
@@ -108,33 +105,33 @@ struct alignas(16) DevAlpha {
     uint32_t off_lo, off_hi;
     uint32_t wh, mode;
     float cut, scale;
-    uint32_t acc[2], rej[2];
 };
-static_assert(sizeof(DevAlpha) == 64, "alpha record layout");
+static_assert(sizeof(DevAlpha) == 48, "alpha record layout");
 // ---- alpha coverage (pt_alpha_cov.h): an alpha-tested triangle's slot holds
-// the accept mask of its 4 x 4 subdivision in a.w bits 16-31 and the reject
-// mask in b.w bits 16-31 (its alpha record holds the 8 x 8 masks); the alpha
-// record index (27 bits) is split over a.w bits 5-15 (high) and b.w bits 0-15
-// (low).  The cell of a hit's barycentrics (u, v) (weights of vertices 1 and
-// 2) in the N x N subdivision: row j = floor(N v) has N - j lower and N-1-j
-// upper sub-triangles; cell j (2N - j) + 2 i + upper.  N u and N v are exact;
-// a point past the hypotenuse (by rounding only) goes to the diagonal's lower
-// cell, whose footprint margin covers it.
-// PT_ALPHA_COV: 0 no masks, 1 the record's 8 x 8 masks, 2 + the slot's 4 x 4
+// the handle of its coverage mask set (DevScene::amask word offset | log2(n /
+// 4) << 30, PT_ALPHA_SET_NONE: none) in a.w bits 16-31 (low half) and b.w
+// bits 16-31 (high half); the alpha record index (27 bits) is split over a.w
+// bits 5-15 (high) and b.w bits 0-15 (low).  The cell of a hit's barycentrics
+// (u, v) (weights of vertices 1 and 2) in the n x n subdivision: row j =
+// floor(n v) has n - j lower and n-1-j upper sub-triangles; cell j (2n - j) +
+// 2 i + upper.  n u and n v are exact (n a power of two); a point past the
+// hypotenuse (by rounding only) goes to the diagonal's lower cell, whose
+// footprint margin covers it.
+// PT_ALPHA_COV: 0 no masks (the exact test always), 1 the mask sets
 #ifndef PT_ALPHA_COV
 #define PT_ALPHA_COV 1
 #endif
+#define PT_ALPHA_SET_NONE 0xFFFFFFFFu
 __device__ __forceinline__ uint32_t alpha_index(uint32_t w0, uint32_t w1) {
     return ((w0 >> 5) & 0x7FFu) << 16 | (w1 & 0xFFFFu);
 }
-template <int N>
-__device__ __forceinline__ uint32_t alpha_cell(float u, float v) {
-    const float a = (float)N * u, b = (float)N * v;
-    const float fi = __builtin_amdgcn_fmed3f(floorf(a), 0.0f, (float)(N - 1));
-    const float fj = __builtin_amdgcn_fmed3f(floorf(b), 0.0f, (float)(N - 1));
-    const int i = (int)fi, j = (int)fj, im = N - 1 - j;
+__device__ __forceinline__ uint32_t alpha_cell(float u, float v, int n) {
+    const float fn = (float)n, a = fn * u, b = fn * v;
+    const float fi = __builtin_amdgcn_fmed3f(floorf(a), 0.0f, fn - 1.0f);
+    const float fj = __builtin_amdgcn_fmed3f(floorf(b), 0.0f, fn - 1.0f);
+    const int i = (int)fi, j = (int)fj, im = n - 1 - j;
     const bool up = (a - fi) + (b - fj) > 1.0f && i < im;
-    return (uint32_t)(j * (2 * N - j) + 2 * min(i, im) + (up ? 1 : 0));
+    return (uint32_t)(j * (2 * n - j) + 2 * min(i, im) + (up ? 1 : 0));
 }
 // Instances (TransformedPrimitive, Primitive.cpp:32-72).  A TLAS leaf slot of
 // an instance is encoded like a BLAS hop whose pushed ref is
@@ -215,7 +212,8 @@ struct DevScene {
     const float* uvs;          // 2 per vertex
     const float* tangents;
     const DevTriShade* tshade;  // per-triangle shading records (vertex order x, y, z of tri)
-    const DevAlpha* alpha;      // alpha records of the alpha-tested triangles (slot b.w)
+    const DevAlpha* alpha;      // alpha records of the alpha-tested triangles (alpha_index)
+    const uint32_t* amask;      // their coverage mask sets (pt_alpha_cov.h)
     const pt_quad* quads;
     const pt_sphere* spheres;
     const pt_material* materials;

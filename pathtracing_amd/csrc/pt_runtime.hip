@@ -734,36 +734,36 @@ static PtAlphaRecord alpha_cov_record(const DevAlpha& r) {
 }
 
 // The alpha records of the alpha-tested triangles among the slots `geom`
-// (flags in a.w already set) with their 8 x 8 coverage masks, and each slot's
-// 4 x 4 masks + record index (pt_device.h).  Test hook outputs (may be null):
-// masks4 accept | reject << 16 per slot, masks8 {accept, reject} per slot.
+// (flags in a.w already set), each slot's record index and coverage mask set
+// (pt_device.h) and the mask words (amask).  Test hook output (may be null):
+// per slot PT_ALPHA_HOOK_WORDS words: the set handle, then its accept and
+// reject masks (each max(1, n n / 32) words, padded to 32).
+#define PT_ALPHA_HOOK_WORDS 65
 static void alpha_records(const pt_scene_desc* s, std::vector<DevGeom>& geom, std::vector<DevAlpha>* alpha,
-                          uint32_t* masks4, uint64_t* masks8) {
+                          std::vector<uint32_t>* amask, uint32_t* hook) {
     PtAlphaCoverage cov(s->texels, s->texels ? s->n_texel_bytes : 0);
     uint32_t n = 0;
     for (uint32_t i = 0; i < s->n_prims; i++) {
-        if (masks4) masks4[i] = 0;
-        if (masks8) masks8[2 * i] = masks8[2 * i + 1] = 0;
+        uint32_t* h = hook ? hook + (size_t)PT_ALPHA_HOOK_WORDS * i : nullptr;
+        if (h) std::fill(h, h + PT_ALPHA_HOOK_WORDS, 0u), h[0] = PT_ALPHA_SET_NONE;
         const uint32_t fl = __builtin_bit_cast(uint32_t, geom[i].a.w);
         if ((fl & GF_KIND) != PT_PRIM_TRIANGLE || !(fl & GF_ALPHA)) continue;
         DevAlpha r;
         const bool fast = n < ALPHA_IDX_NONE && alpha_record(s, s->prims[i], r);
         const uint32_t idx = fast ? n++ : ALPHA_IDX_NONE;
-        PtAlphaMasks m4{0, 0}, m8{0, 0};
-        if (fast) {
-            const PtAlphaRecord a = alpha_cov_record(r);
-            m4 = cov.masks(a, 4);
-            m8 = cov.masks(a, 8);
+        const uint32_t set = PT_ALPHA_COV && fast ? cov.set(alpha_cov_record(r)) : PT_ALPHA_SET_NONE;
+        geom[i].a.w = __builtin_bit_cast(float, (fl & 0x1Fu) | (idx >> 16) << 5 | (set & 0xFFFFu) << 16);
+        geom[i].b.w = __builtin_bit_cast(float, (idx & 0xFFFFu) | (set & 0xFFFF0000u));
+        if (h && set != PT_ALPHA_SET_NONE) {
+            const int cn = 4 << (set >> 30), wpm = std::max(1, cn * cn / 32);
+            const uint32_t* w = cov.words().data() + (set & 0x3FFFFFFFu);
+            h[0] = set;
+            std::copy(w, w + wpm, h + 1);
+            std::copy(w + wpm, w + 2 * wpm, h + 33);
         }
-        const uint32_t m = (uint32_t)m4.acc | (uint32_t)m4.rej << 16;
-        r.acc[0] = (uint32_t)m8.acc, r.acc[1] = (uint32_t)(m8.acc >> 32);
-        r.rej[0] = (uint32_t)m8.rej, r.rej[1] = (uint32_t)(m8.rej >> 32);
-        geom[i].a.w = __builtin_bit_cast(float, (fl & 0x1Fu) | (idx >> 16) << 5 | (m & 0xFFFFu) << 16);
-        geom[i].b.w = __builtin_bit_cast(float, (idx & 0xFFFFu) | (m >> 16) << 16);
-        if (masks4) masks4[i] = m;
-        if (masks8) masks8[2 * i] = m8.acc, masks8[2 * i + 1] = m8.rej;
         if (fast && alpha) alpha->push_back(r);
     }
+    if (amask) *amask = cov.words();
 }
 
 struct Conv {
@@ -1129,7 +1129,9 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     // ---- alpha records of the alpha-tested triangles and their coverage
     // masks (pt_device.h alpha_index / alpha_cell, pt_alpha_cov.h)
     std::vector<DevAlpha> alpha;
-    alpha_records(s, geom, &alpha, nullptr, nullptr);
+    std::vector<uint32_t> amask;
+    alpha_records(s, geom, &alpha, &amask, nullptr);
+    if (amask.empty()) amask.push_back(0);
     // ---- nodes: TLAS then every BLAS, converted from the root descriptors
     std::vector<uint32_t> cbase(s->n_bvhs);
     uint64_t total = 0;
@@ -1241,6 +1243,7 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     UP(DS.tangents, s->tangents, s->tangents ? 3 * (size_t)s->n_vertices : 0);
     UP(DS.tshade, (const DevTriShade*)nullptr, s->n_triangles);
     UP(DS.alpha, alpha.data(), alpha.size());
+    UP(DS.amask, amask.data(), amask.size());
     if (s->n_triangles) {
         hipLaunchKernelGGL(k_tri_shade, dim3((s->n_triangles + 255) / 256), dim3(256), 0, c->stream, DS.tri,
                            DS.normals, DS.uvs, s->tangents ? DS.tangents : nullptr, s->n_triangles,
@@ -2532,15 +2535,15 @@ extern "C" pt_status pt_light_picks(pt_ctx* c, const float* u, uint32_t n, int32
                     });
 }
 
-// Test hook (host code, no device): the coverage masks pt_scene_upload stores
-// for the alpha-tested triangles (pt_alpha_cov.h), 0 for the other slots.
-extern "C" pt_status pt_alpha_coverage(const pt_scene_desc* s, uint32_t* masks4, uint64_t* masks8) {
-    if (!s || !masks4 || !masks8) return PT_ERR_ARG;
+// Test hook (host code, no device): the coverage mask sets pt_scene_upload
+// stores for the alpha-tested triangles (pt_alpha_cov.h), per slot.
+extern "C" pt_status pt_alpha_coverage(const pt_scene_desc* s, uint32_t* out) {
+    if (!s || !out) return PT_ERR_ARG;
     if (pt_status st = validate_scene(nullptr, s)) return st;
     std::vector<DevGeom> geom(s->n_prims + 1);
     std::vector<DevPrimInfo> info(s->n_prims);
     slot_geometry(s, geom, info);
-    alpha_records(s, geom, nullptr, masks4, masks8);
+    alpha_records(s, geom, nullptr, nullptr, out);
     return PT_OK;
 }
 

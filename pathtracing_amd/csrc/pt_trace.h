@@ -139,36 +139,34 @@ __device__ __noinline__ bool tri_alpha_slow(uint32_t slot, float bu, float bv, f
 // call): C4 1615 -> 1633 Mrays/s (closest-hit 20.58 -> 20.29 ms per launch,
 // profiles/r04_ab_traversal.txt)
 __device__ __forceinline__ bool tri_alpha_rec(const DevAlpha& r, uint32_t slot, float bu, float bv, f3 o, f3 d);
+// ai: the alpha record index, set: its coverage mask set (pt_device.h)
 __device__ __forceinline__
-bool tri_alpha(uint32_t ai, uint32_t slot, float bu, float bv, f3 o, f3 d) {
+bool tri_alpha(uint32_t ai, uint32_t set, uint32_t slot, float bu, float bv, f3 o, f3 d) {
     if (ai != ALPHA_IDX_NONE) {
-        // the whole record in four 16-B loads issued together (a reference
+        // the whole record in three 16-B loads issued together (a reference
         // into S.alpha would let the compiler read its fields where they are
         // used, in branches, one round trip each)
         const float4* ap = reinterpret_cast<const float4*>(S.alpha + ai);
-        const float4 a0 = ap[0], a1 = ap[1], a2 = ap[2], a3 = ap[3];
-        if (PT_ALPHA_COV >= 1) {  // a cell the 8 x 8 masks decide: no texel read
-            const uint32_t c = alpha_cell<8>(bu, bv);
-            const uint32_t acc = __float_as_uint(c < 32 ? a3.x : a3.y), rej = __float_as_uint(c < 32 ? a3.z : a3.w);
+        const float4 a0 = ap[0], a1 = ap[1], a2 = ap[2];
+        if (PT_ALPHA_COV && set != PT_ALPHA_SET_NONE) {
+            // the hit's cell in the two masks, read beside the record: a
+            // decided cell answers without the texel reads
+            const int n = 4 << (set >> 30);
+            const uint32_t c = alpha_cell(bu, bv, n);
+            const uint32_t* m = S.amask + (set & 0x3FFFFFFFu) + (c >> 5);
+            const uint32_t acc = m[0], rej = m[max(1, (n * n) >> 5)];
             if ((acc >> (c & 31)) & 1u) return true;
             if ((rej >> (c & 31)) & 1u) return false;
         }
-        struct Rec { float4 a, b, c, d; };
-        const DevAlpha r = __builtin_bit_cast(DevAlpha, (Rec{a0, a1, a2, a3}));
+        const DevAlpha r = __builtin_bit_cast(DevAlpha, (DevGeom{a0, a1, a2}));
         return tri_alpha_rec(r, slot, bu, bv, o, d);
     }
     return tri_alpha_slow(slot, bu, bv, o, d);
 }
-// the test from a slot's words w0 = a.w, w1 = b.w: a cell its coverage masks
-// decide (pt_alpha_cov.h) answers without a read; the others run the exact test
+// the test from a slot's words w0 = a.w, w1 = b.w (record index and mask set)
 __device__ __forceinline__
 bool tri_alpha_cov(uint32_t w0, uint32_t w1, uint32_t slot, float bu, float bv, f3 o, f3 d) {
-    if (PT_ALPHA_COV >= 2) {
-        const uint32_t c = alpha_cell<4>(bu, bv);
-        if ((w0 >> 16 >> c) & 1u) return true;
-        if ((w1 >> 16 >> c) & 1u) return false;
-    }
-    return tri_alpha(alpha_index(w0, w1), slot, bu, bv, o, d);
+    return tri_alpha(alpha_index(w0, w1), (w0 >> 16) | (w1 & 0xFFFF0000u), slot, bu, bv, o, d);
 }
 // the test over an alpha record already read
 __device__ __forceinline__ bool tri_alpha_rec(const DevAlpha& r, uint32_t slot, float bu, float bv, f3 o, f3 d) {

@@ -220,7 +220,7 @@ def lib():
     L.pt_light_picks.restype = C.c_int32
     L.pt_anim_inverse_cases.argtypes = [vp, vp, C.c_uint32, vp]
     L.pt_anim_inverse_cases.restype = C.c_int32
-    L.pt_alpha_coverage.argtypes = [C.POINTER(SceneDesc), vp, vp]
+    L.pt_alpha_coverage.argtypes = [C.POINTER(SceneDesc), vp]
     L.pt_alpha_coverage.restype = C.c_int32
     L.pt_scene_device_bytes.argtypes = [vp]
     L.pt_scene_device_bytes.restype = C.c_uint64

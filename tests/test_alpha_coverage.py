@@ -37,11 +37,22 @@ def coverage(setup):
     flat = sc.flat if sc.flat is not None else sc.BuildTlas()
     flat = bind_lights(flat, sc, setup.light_sampler)
     d = flat.desc()
-    m4 = np.zeros(flat.n_prims, np.uint32)
-    m8 = np.zeros((flat.n_prims, 2), np.uint64)
-    assert _lib().pt_alpha_coverage(C.byref(d), N.ptr(m4), N.ptr(m8)) == 0
-    # {n: (accept, reject) per slot}
-    return flat, {4: (m4 & 0xFFFF, m4 >> 16), 8: (m8[:, 0], m8[:, 1])}
+    out = np.zeros((flat.n_prims, 65), np.uint32)
+    assert _lib().pt_alpha_coverage(C.byref(d), N.ptr(out)) == 0
+    return flat, out
+
+
+NONE = 0xFFFFFFFF
+
+
+def set_n(handle) -> int:
+    return 4 << (int(handle) >> 30)
+
+
+def cell_bits(row, cell):
+    """(accept, reject) bits of cells `cell` in a hook row."""
+    w, b = cell >> 5, (cell & 31).astype(np.uint32)
+    return (row[1 + w] >> b) & 1, (row[33 + w] >> b) & 1
 
 
 def alpha_cell(u, v, n=4):
@@ -89,59 +100,59 @@ def exact_alpha(flat, slot, u, v):
     return a >= 1.0, a <= 0.0  # Blend: certainly true / certainly false
 
 
-def sample_points(rng, n):
+def sample_points(rng, n, k=4):
     """Random barycentrics in the triangle plus every cell corner and edge
-    midpoint of the 4 x 4 subdivision."""
+    midpoint of the k x k subdivision."""
     r1, r2 = rng.random(n), rng.random(n)
     s = np.sqrt(r1)
     u, v = s * (1 - r2), s * r2
-    g = np.array([(a / 8, b / 8) for a in range(9) for b in range(9 - a)])
+    m = 2 * k
+    g = np.array([(a / m, b / m) for a in range(m + 1) for b in range(m + 1 - a)])
     return np.concatenate([u, g[:, 0]]), np.concatenate([v, g[:, 1]])
 
 
 def check_scene(setup, rng, min_decided=None, n=400):
-    """Every decided cell of both subdivisions agrees with the exact test at
-    every sampled point; returns the decided fraction of the points per n."""
+    """Every decided cell agrees with the exact test at every sampled point;
+    returns the decided fraction of the points."""
     flat, masks = coverage(setup)
-    decided = {4: 0, 8: 0}
-    total = 0
+    decided = total = 0
     for slot in range(flat.n_prims):
-        if flat.prims[slot]["kind"] != 0 or flat.prims[slot]["material"] < 0:
-            continue
-        if not any(int(masks[k][w][slot]) for k in (4, 8) for w in (0, 1)):
+        if flat.prims[slot]["kind"] != 0 or flat.prims[slot]["material"] < 0 or masks[slot, 0] == NONE:
             continue
         mat = flat.materials[flat.prims[slot]["material"]]
         tid = mat["alpha"] if mat["alpha"] >= 0 else mat["tex"]
         if flat.textures[tid]["kind"] != ALPHA_IMAGE_TEX:
             continue  # constant alpha: decided whole (test_alpha_maps_masks_hold)
-        u, v = sample_points(rng, n)
+        k = set_n(masks[slot, 0])
+        u, v = sample_points(rng, n, k)
         sure_pass, sure_fail = exact_alpha(flat, slot, u, v)
         total += u.size
-        for k in (4, 8):
-            cell = alpha_cell(u, v, k).astype(np.uint64)
-            acc = (np.uint64(masks[k][0][slot]) >> cell) & np.uint64(1)
-            rej = (np.uint64(masks[k][1][slot]) >> cell) & np.uint64(1)
-            assert not np.any(acc & rej), f"slot {slot}: a {k}x{k} cell both accepted and rejected"
-            bad = (acc == 1) & ~sure_pass | (rej == 1) & ~sure_fail
-            assert not bad.any(), f"slot {slot} {k}x{k}: wrong at {u[bad][:4]}, {v[bad][:4]}"
-            decided[k] += int(((acc | rej) == 1).sum())
-    frac = {k: decided[k] / total for k in decided} if total else None
+        acc, rej = cell_bits(masks[slot], alpha_cell(u, v, k))
+        assert not np.any(acc & rej), f"slot {slot}: a {k}x{k} cell both accepted and rejected"
+        bad = (acc == 1) & ~sure_pass | (rej == 1) & ~sure_fail
+        assert not bad.any(), f"slot {slot} {k}x{k}: wrong at {u[bad][:4]}, {v[bad][:4]}"
+        decided += int(((acc | rej) == 1).sum())
+    frac = decided / total if total else None
     if min_decided is not None:
-        assert frac is not None and frac[8] >= min_decided, frac
+        assert frac is not None and frac >= min_decided, frac
     return flat, masks, frac
 
 
-def test_alpha_cell_covers_the_16_cells_once():
-    # the sub-triangle centroids land in 16 distinct cells, in the row order
+@pytest.mark.parametrize("k", [4, 8, 16, 32])
+def test_alpha_cell_covers_the_cells_once(k):
+    # the sub-triangle centroids land in k * k distinct cells, in the row order
     cents = []
-    for j in range(4):
-        for i in range(4 - j):
-            cents.append(((i + 1 / 3) / 4, (j + 1 / 3) / 4))
-            if i < 3 - j:
-                cents.append(((i + 2 / 3) / 4, (j + 2 / 3) / 4))
+    for j in range(k):
+        for i in range(k - j):
+            cents.append(((i + 1 / 3) / k, (j + 1 / 3) / k))
+            if i < k - 1 - j:
+                cents.append(((i + 2 / 3) / k, (j + 2 / 3) / k))
     c = np.array(cents)
-    cells = alpha_cell(c[:, 0], c[:, 1])
-    assert sorted(cells.tolist()) == list(range(16))
+    cells = alpha_cell(c[:, 0], c[:, 1], k)
+    assert sorted(cells.tolist()) == list(range(k * k))
+
+
+def test_alpha_cell_stays_in_range():
     # vertices and points past the hypotenuse (rounding) stay in range
     u = np.array([0, 1, 0, 0.5000001, 0.25, 1.0000001, -1e-9])
     v = np.array([0, 0, 1, 0.5, 0.7500001, 0, 0.3])
@@ -157,9 +168,9 @@ def test_alpha_maps_masks_hold():
              flat.materials[flat.prims[s]["material"]]["alpha"] >= 0 and
              flat.textures[flat.materials[flat.prims[s]["material"]]["alpha"]]["kind"] == 0]
     assert solid
-    for s in solid:
-        assert masks[4][0][s] == 0 and masks[4][1][s] == 0xFFFF
-        assert masks[8][0][s] == 0 and masks[8][1][s] == np.uint64(0xFFFFFFFFFFFFFFFF)
+    for s in solid:  # one shared 4 x 4 set, all cells rejected
+        assert set_n(masks[s, 0]) == 4 and masks[s, 1] == 0 and masks[s, 33] == 0xFFFF
+    assert len({int(masks[s, 0]) for s in solid}) == 1
 
 
 def leaf_scene(uv_scale=1.0, uv_offset=(0.0, 0.0), mode=AlphaMode.Mask, cutoff=0.5, size=256, n=60, seed=7):
@@ -177,8 +188,10 @@ def leaf_scene(uv_scale=1.0, uv_offset=(0.0, 0.0), mode=AlphaMode.Mask, cutoff=0
 def test_leaf_card_masks_hold_and_decide_most_hits():
     """C4's leaf cards (the ellipse mask of scenes._leaf_image): most of the
     area is decided -- what saves the traversal its texel reads."""
-    _, _, frac = check_scene(leaf_scene(), np.random.default_rng(2), min_decided=0.5)
-    assert frac[8] > frac[4]
+    flat, masks, frac = check_scene(leaf_scene(size=1024), np.random.default_rng(2), min_decided=0.85)
+    # the cards share two uv layouts: two mask sets, 32 x 32 cells each
+    sets = {int(h) for h in masks[:, 0] if h != NONE}
+    assert len(sets) == 2 and all(set_n(h) == 32 for h in sets)
 
 
 @pytest.mark.parametrize("scale,offset", [(2.5, (-0.3, 0.7)), (0.3, (3.9, -2.2)), (40.0, (0.0, 0.0))])
@@ -196,6 +209,4 @@ def test_blend_masks_hold():
 def test_masks_are_deterministic_and_memoised_identically():
     a = coverage(leaf_scene(seed=9))[1]
     b = coverage(leaf_scene(seed=9))[1]
-    for k in (4, 8):
-        for w in (0, 1):
-            assert np.array_equal(a[k][w], b[k][w])
+    assert np.array_equal(a, b)
