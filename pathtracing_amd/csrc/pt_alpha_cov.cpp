@@ -154,10 +154,10 @@ bool PtAlphaCoverage::footprint(const Pyramid& P, const double px[3], const doub
     return true;
 }
 
-// the subdivision for a triangle spanning `ext` texels: cells of ~8 texels, 4 .. 32 per side
-static int cells_per_side(double ext) {
+// the subdivision for a triangle spanning `ext` texels: cells of ~8 texels, 4 .. max_n per side
+static int cells_per_side(double ext, int max_n) {
     int n = 4;
-    while (n < 32 && ext > 8.0 * n) n *= 2;
+    while (n < max_n && ext > 8.0 * n) n *= 2;
     return n;
 }
 
@@ -182,7 +182,7 @@ uint32_t PtAlphaCoverage::set(const PtAlphaRecord& rec) {
         const int m = (k + 1) % 3;
         ext = std::max({ext, std::fabs((double)r.su[m] - r.su[k]) * r.W, std::fabs((double)r.sv[m] - r.sv[k]) * r.H});
     }
-    const int n = whole ? 4 : cells_per_side(ext);
+    const int n = whole ? 4 : cells_per_side(ext, std::min(256, std::max(4, max_n_)));
     const uint32_t wpm = std::max(1, n * n / 32);  // words per mask
     std::vector<uint32_t> acc(wpm, 0), rej(wpm, 0);
     bool any = false;
@@ -193,7 +193,7 @@ uint32_t PtAlphaCoverage::set(const PtAlphaRecord& rec) {
             (k == 1 ? acc : rej)[0] = 0xFFFFu;
             any = true;
         }
-    } else if (P && finite && lookups_ < PT_ALPHA_LOOKUP_BUDGET && words_.size() + 2 * wpm < (1u << 30)) {
+    } else if (P && finite && lookups_ < PT_ALPHA_LOOKUP_BUDGET && words_.size() + 2 * wpm < (1u << 29)) {
         // texel-space margins: far above the float error of the computed
         // barycentrics' lerp and of u W - 0.5 (a few ulp of max|u| W)
         const double mx = 1e-4 + 1e-5 * (maxu * r.W + 1.0), my = 1e-4 + 1e-5 * (maxv * r.H + 1.0);
@@ -233,7 +233,7 @@ uint32_t PtAlphaCoverage::set(const PtAlphaRecord& rec) {
     if (any) {
         int ln = 0;
         while ((4 << ln) < n) ln++;
-        out = (uint32_t)words_.size() | (uint32_t)ln << 30;
+        out = (uint32_t)words_.size() | (uint32_t)ln << 29;
         words_.insert(words_.end(), acc.begin(), acc.end());
         words_.insert(words_.end(), rej.begin(), rej.end());
     }

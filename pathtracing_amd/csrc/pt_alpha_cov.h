@@ -35,7 +35,7 @@ struct PtAlphaRecord {
 
 // A mask set (the upload's word array words()): accept mask then reject
 // mask over the n x n cells (cell c: bit c & 31 of word c >> 5), each
-// max(1, n n / 32) words.  Its handle = word offset | log2(n / 4) << 30;
+// max(1, n n / 32) words.  Its handle = word offset | log2(n / 4) << 29;
 // PT_ALPHA_SET_NONE: no cell decided (or no set computed).
 #define PT_ALPHA_SET_NONE 0xFFFFFFFFu
 // square-table lookups the masks of one upload may spend (host time); the
@@ -44,9 +44,11 @@ struct PtAlphaRecord {
 
 class PtAlphaCoverage {
 public:
-    PtAlphaCoverage(const uint8_t* texels, uint64_t n_texel_bytes) : texels_(texels), n_(n_texel_bytes) {}
+    // max_n: the finest subdivision (a power of two, 4 .. 64)
+    PtAlphaCoverage(const uint8_t* texels, uint64_t n_texel_bytes, int max_n = 64)
+        : texels_(texels), n_(n_texel_bytes), max_n_(max_n) {}
     // the mask set of a record (n from the triangle's texel extent: cells of
-    // ~8 texels, 4 .. 32 per side); identical records share one set
+    // ~8 texels, 4 .. max_n per side); identical records share one set
     uint32_t set(const PtAlphaRecord& r);
     const std::vector<uint32_t>& words() const { return words_; }
 
@@ -63,6 +65,7 @@ private:
     const Pyramid* pyramid(uint64_t off, uint32_t W, uint32_t H, uint32_t C, uint32_t ch);
     const uint8_t* texels_;
     uint64_t n_;
+    int max_n_;
     std::map<std::tuple<uint64_t, uint32_t, uint32_t, uint32_t, uint32_t>, std::unique_ptr<Pyramid>> pyr_;
     std::unordered_map<std::string, uint32_t> memo_;  // identical records (leaf cards share uvs)
     std::vector<uint32_t> words_;

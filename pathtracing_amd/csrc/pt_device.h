@@ -109,7 +109,7 @@ struct alignas(16) DevAlpha {
 static_assert(sizeof(DevAlpha) == 48, "alpha record layout");
 // ---- alpha coverage (pt_alpha_cov.h): an alpha-tested triangle's slot holds
 // the handle of its coverage mask set (DevScene::amask word offset | log2(n /
-// 4) << 30, PT_ALPHA_SET_NONE: none) in a.w bits 16-31 (low half) and b.w
+// 4) << 29, PT_ALPHA_SET_NONE: none) in a.w bits 16-31 (low half) and b.w
 // bits 16-31 (high half); the alpha record index (27 bits) is split over a.w
 // bits 5-15 (high) and b.w bits 0-15 (low).  The cell of a hit's barycentrics
 // (u, v) (weights of vertices 1 and 2) in the n x n subdivision: row j =

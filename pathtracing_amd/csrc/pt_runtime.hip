@@ -737,11 +737,14 @@ static PtAlphaRecord alpha_cov_record(const DevAlpha& r) {
 // (flags in a.w already set), each slot's record index and coverage mask set
 // (pt_device.h) and the mask words (amask).  Test hook output (may be null):
 // per slot PT_ALPHA_HOOK_WORDS words: the set handle, then its accept and
-// reject masks (each max(1, n n / 32) words, padded to 32).
-#define PT_ALPHA_HOOK_WORDS 65
+// reject masks (each max(1, n n / 32) words, padded to 128).
+#define PT_ALPHA_HOOK_WORDS 257
 static void alpha_records(const pt_scene_desc* s, std::vector<DevGeom>& geom, std::vector<DevAlpha>* alpha,
                           std::vector<uint32_t>* amask, uint32_t* hook) {
-    PtAlphaCoverage cov(s->texels, s->texels ? s->n_texel_bytes : 0);
+#ifndef PT_ALPHA_MAXN  // the finest coverage subdivision (pt_alpha_cov.h)
+#define PT_ALPHA_MAXN 64
+#endif
+    PtAlphaCoverage cov(s->texels, s->texels ? s->n_texel_bytes : 0, PT_ALPHA_MAXN);
     uint32_t n = 0;
     for (uint32_t i = 0; i < s->n_prims; i++) {
         uint32_t* h = hook ? hook + (size_t)PT_ALPHA_HOOK_WORDS * i : nullptr;
@@ -755,11 +758,11 @@ static void alpha_records(const pt_scene_desc* s, std::vector<DevGeom>& geom, st
         geom[i].a.w = __builtin_bit_cast(float, (fl & 0x1Fu) | (idx >> 16) << 5 | (set & 0xFFFFu) << 16);
         geom[i].b.w = __builtin_bit_cast(float, (idx & 0xFFFFu) | (set & 0xFFFF0000u));
         if (h && set != PT_ALPHA_SET_NONE) {
-            const int cn = 4 << (set >> 30), wpm = std::max(1, cn * cn / 32);
-            const uint32_t* w = cov.words().data() + (set & 0x3FFFFFFFu);
+            const int cn = 4 << (set >> 29), wpm = std::max(1, cn * cn / 32);
+            const uint32_t* w = cov.words().data() + (set & 0x1FFFFFFFu);
             h[0] = set;
-            std::copy(w, w + wpm, h + 1);
-            std::copy(w + wpm, w + 2 * wpm, h + 33);
+            std::copy(w, w + std::min(wpm, 128), h + 1);  // (the hook's rows hold n <= 64)
+            std::copy(w + wpm, w + wpm + std::min(wpm, 128), h + 129);
         }
         if (fast && alpha) alpha->push_back(r);
     }
