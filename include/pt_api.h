@@ -468,12 +468,12 @@ pt_status pt_anim_inverse_cases(pt_ctx* ctx, const float* translations, uint32_t
  * pt_scene_upload stores with each alpha-tested triangle, replacing no
  * reference interface (the reference runs Material::Alpha, Material.hpp:
  * 181-198, on every candidate hit).  A cell of the triangle's n x n
- * barycentric subdivision (n = 4 ... 64 from its texel extent) is "accept"
+ * barycentric subdivision (n = 4 ... 128 from its texel extent) is "accept"
  * when every hit in it passes the alpha test and "reject" when every hit
- * fails.  Per primitive slot, 257 words: the set handle (word offset |
+ * fails.  Per primitive slot, 1025 words: the set handle (word offset |
  * log2(n / 4) << 29; 0xFFFFFFFF: no set -- no alpha test, or nothing
- * decided), 128 words of accept mask, 128 of reject mask (cell c: bit c % 32
- * of word c / 32; max(1, n n / 32) words used).  out: 257 * n_prims words. */
+ * decided), 512 words of accept mask, 512 of reject mask (cell c: bit c % 32
+ * of word c / 32; max(1, n n / 32) words used).  out: 1025 * n_prims words. */
 pt_status pt_alpha_coverage(const pt_scene_desc* scene, uint32_t* out);
 /* Film resolve (Film::WritePNG / WritePPM, Film.hpp:154-217): per pixel
  * color = sum RGB*w / sum w, the tone mapper (through the writers'

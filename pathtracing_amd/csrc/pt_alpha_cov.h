@@ -44,8 +44,8 @@ struct PtAlphaRecord {
 
 class PtAlphaCoverage {
 public:
-    // max_n: the finest subdivision (a power of two, 4 .. 64)
-    PtAlphaCoverage(const uint8_t* texels, uint64_t n_texel_bytes, int max_n = 64)
+    // max_n: the finest subdivision (a power of two, 4 .. 256)
+    PtAlphaCoverage(const uint8_t* texels, uint64_t n_texel_bytes, int max_n = 128)
         : texels_(texels), n_(n_texel_bytes), max_n_(max_n) {}
     // the mask set of a record (n from the triangle's texel extent: cells of
     // ~8 texels, 4 .. max_n per side); identical records share one set

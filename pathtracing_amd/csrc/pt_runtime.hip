@@ -737,12 +737,12 @@ static PtAlphaRecord alpha_cov_record(const DevAlpha& r) {
 // (flags in a.w already set), each slot's record index and coverage mask set
 // (pt_device.h) and the mask words (amask).  Test hook output (may be null):
 // per slot PT_ALPHA_HOOK_WORDS words: the set handle, then its accept and
-// reject masks (each max(1, n n / 32) words, padded to 128).
-#define PT_ALPHA_HOOK_WORDS 257
+// reject masks (each max(1, n n / 32) words, padded to 512).
+#define PT_ALPHA_HOOK_WORDS 1025
 static void alpha_records(const pt_scene_desc* s, std::vector<DevGeom>& geom, std::vector<DevAlpha>* alpha,
                           std::vector<uint32_t>* amask, uint32_t* hook) {
 #ifndef PT_ALPHA_MAXN  // the finest coverage subdivision (pt_alpha_cov.h)
-#define PT_ALPHA_MAXN 64
+#define PT_ALPHA_MAXN 128
 #endif
     PtAlphaCoverage cov(s->texels, s->texels ? s->n_texel_bytes : 0, PT_ALPHA_MAXN);
     uint32_t n = 0;
@@ -761,8 +761,8 @@ static void alpha_records(const pt_scene_desc* s, std::vector<DevGeom>& geom, st
             const int cn = 4 << (set >> 29), wpm = std::max(1, cn * cn / 32);
             const uint32_t* w = cov.words().data() + (set & 0x1FFFFFFFu);
             h[0] = set;
-            std::copy(w, w + std::min(wpm, 128), h + 1);  // (the hook's rows hold n <= 64)
-            std::copy(w + wpm, w + wpm + std::min(wpm, 128), h + 129);
+            std::copy(w, w + std::min(wpm, 512), h + 1);  // (the hook's rows hold n <= 128)
+            std::copy(w + wpm, w + wpm + std::min(wpm, 512), h + 513);
         }
         if (fast && alpha) alpha->push_back(r);
     }

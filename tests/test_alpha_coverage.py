@@ -37,7 +37,7 @@ def coverage(setup):
     flat = sc.flat if sc.flat is not None else sc.BuildTlas()
     flat = bind_lights(flat, sc, setup.light_sampler)
     d = flat.desc()
-    out = np.zeros((flat.n_prims, 257), np.uint32)
+    out = np.zeros((flat.n_prims, 1025), np.uint32)
     assert _lib().pt_alpha_coverage(C.byref(d), N.ptr(out)) == 0
     return flat, out
 
@@ -52,7 +52,7 @@ def set_n(handle) -> int:
 def cell_bits(row, cell):
     """(accept, reject) bits of cells `cell` in a hook row."""
     w, b = cell >> 5, (cell & 31).astype(np.uint32)
-    return (row[1 + w] >> b) & 1, (row[129 + w] >> b) & 1
+    return (row[1 + w] >> b) & 1, (row[513 + w] >> b) & 1
 
 
 def alpha_cell(u, v, n=4):
@@ -138,7 +138,7 @@ def check_scene(setup, rng, min_decided=None, n=400):
     return flat, masks, frac
 
 
-@pytest.mark.parametrize("k", [4, 8, 16, 32, 64])
+@pytest.mark.parametrize("k", [4, 8, 16, 32, 64, 128])
 def test_alpha_cell_covers_the_cells_once(k):
     # the sub-triangle centroids land in k * k distinct cells, in the row order
     cents = []
@@ -169,7 +169,7 @@ def test_alpha_maps_masks_hold():
              flat.textures[flat.materials[flat.prims[s]["material"]]["alpha"]]["kind"] == 0]
     assert solid
     for s in solid:  # one shared 4 x 4 set, all cells rejected
-        assert set_n(masks[s, 0]) == 4 and masks[s, 1] == 0 and masks[s, 129] == 0xFFFF
+        assert set_n(masks[s, 0]) == 4 and masks[s, 1] == 0 and masks[s, 513] == 0xFFFF
     assert len({int(masks[s, 0]) for s in solid}) == 1
 
 
@@ -188,10 +188,10 @@ def leaf_scene(uv_scale=1.0, uv_offset=(0.0, 0.0), mode=AlphaMode.Mask, cutoff=0
 def test_leaf_card_masks_hold_and_decide_most_hits():
     """C4's leaf cards (the ellipse mask of scenes._leaf_image): most of the
     area is decided -- what saves the traversal its texel reads."""
-    flat, masks, frac = check_scene(leaf_scene(size=1024), np.random.default_rng(2), min_decided=0.9)
-    # the cards share two uv layouts: two mask sets, 64 x 64 cells each
+    flat, masks, frac = check_scene(leaf_scene(size=1024), np.random.default_rng(2), min_decided=0.95)
+    # the cards share two uv layouts: two mask sets, 128 x 128 cells each
     sets = {int(h) for h in masks[:, 0] if h != NONE}
-    assert len(sets) == 2 and all(set_n(h) == 64 for h in sets)
+    assert len(sets) == 2 and all(set_n(h) == 128 for h in sets)
 
 
 @pytest.mark.parametrize("scale,offset", [(2.5, (-0.3, 0.7)), (0.3, (3.9, -2.2)), (40.0, (0.0, 0.0))])
