@@ -180,6 +180,18 @@ struct alignas(128) DevTriShade {
 };
 static_assert(sizeof(DevTriShade) == 128, "shading record layout");
 
+// An area light's triangle, gathered per light at upload (what AreaLight::
+// sample / PDF read through its shape: the vertices and uvs), so NEE reads it
+// beside the light instead of prim info -> triangle -> vertices:
+//   a = v0.xyz, uv0.x   b = v1.xyz, uv1.x   c = v2.xyz, uv2.x
+//   d = uv0.y, uv1.y, uv2.y, valid (bits: 1 = a triangle area light)
+struct alignas(16) DevLightTri {
+    float4 a, b, c, d;
+};
+#ifndef PT_LIGHT_TRI  // 0: AreaLight::sample / PDF read the triangle through prim info -> S.tri -> vertices
+#define PT_LIGHT_TRI 1
+#endif
+
 struct DevPrimInfo {
     int32_t material, light, medium;
     uint32_t index;  // triangle / quad / sphere id, BLAS root ref
@@ -211,7 +223,7 @@ struct DevScene {
     const float* normals;
     const float* uvs;          // 2 per vertex
     const float* tangents;
-    const DevTriShade* tshade;  // per-triangle shading records (vertex order x, y, z of tri)
+    const DevTriShade* tshade;  // shading records per primitive slot (a triangle slot: its vertices x, y, z)
     const DevAlpha* alpha;      // alpha records of the alpha-tested triangles (alpha_index)
     const uint32_t* amask;      // their coverage mask sets (pt_alpha_cov.h)
     const pt_quad* quads;
@@ -222,6 +234,7 @@ struct DevScene {
     const uint8_t* texels;
     uint64_t n_texel_bytes;
     const pt_light* lights;
+    const DevLightTri* ltri;    // per light: its triangle (DevLightTri), valid for triangle area lights
     uint32_t n_lights;
     uint32_t light_sampler;
     const uint32_t* sampler_lights;

@@ -159,7 +159,8 @@ __global__ void k_shadow_tr(PathSoA next, float* sample_L, const ShadowRecV* sq,
 __global__ void k_fill(RenderParams R, uint32_t n, PathSoA next, uint32_t* cnt, unsigned long long* next_sample);
 __global__ void k_resolve(const double* film, uint32_t npx, uint32_t tonemap, uint8_t* rgb);
 __global__ void k_frame_gather(const float* sample_L, const unsigned long long* idx, uint32_t n, float* out);
-__global__ void k_tri_shade(const uint4* tri, const float* normals, const float* uvs, const float* tangents,
+__global__ void k_tri_shade(const DevGeom* geom, const DevPrimInfo* info, const uint4* tri, const float* normals,
+                            const float* uvs, const float* tangents,
                             uint32_t n, DevTriShade* out);
 __global__ void k_gather(RenderParams R, const float* sample_L, double* film);
 

@@ -165,6 +165,9 @@ __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, flo
     }
     const DevGeom g = S.geom[prim];
     const DevPrimInfo pi = S.info[prim];
+    // the slot's shading record (one 128-B line) with its geometry and info:
+    // three independent reads instead of info -> record
+    const DevTriShade R = S.tshade[prim];
     const uint32_t kind = __float_as_uint(g.a.w) & GF_KIND;
     if (I) {  // the object-space t of the accepted hit
         if (kind == PT_PRIM_TRIANGLE) {
@@ -177,7 +180,7 @@ __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, flo
             sphere_root(S.spheres[pi.index], ro, rd, __int_as_float(0x7f800000), t);
         }
     }
-    if (kind == PT_PRIM_TRIANGLE) tri_interaction(g, pi.index, pi.material, ro, rd, t, b1, b2, si);
+    if (kind == PT_PRIM_TRIANGLE) tri_interaction(g, R, pi.material, ro, rd, t, b1, b2, si);
     else if (kind == PT_PRIM_QUAD) quad_interaction(S.quads[pi.index], ro, rd, t, b1, b2, si);
     else sphere_interaction(S.spheres[pi.index], ro, rd, t, si);
     si.mat = pi.material;
@@ -1723,13 +1726,22 @@ __device__ __forceinline__ double linear_to_srgb(double v) {
 }
 // Per-triangle shading records (DevTriShade) from the indexed mesh arrays,
 // once per scene upload.
-__global__ __launch_bounds__(256) void k_tri_shade(const uint4* __restrict__ tri, const float* __restrict__ normals,
+// one shading record per primitive SLOT (triangle slots; the others zero), so
+// the shading reads it beside the slot's geometry and info, not after them
+__global__ __launch_bounds__(256) void k_tri_shade(const DevGeom* __restrict__ geom,
+                                                   const DevPrimInfo* __restrict__ info,
+                                                   const uint4* __restrict__ tri, const float* __restrict__ normals,
                                                    const float* __restrict__ uvs,
                                                    const float* __restrict__ tangents, uint32_t n,
                                                    DevTriShade* __restrict__ out) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    const uint4 T = tri[t];
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    if ((__float_as_uint(geom[s].a.w) & GF_KIND) != PT_PRIM_TRIANGLE) {
+        const float4 z = make_float4(0, 0, 0, 0);
+        out[s] = DevTriShade{z, z, z, z, z, z, z, z};
+        return;
+    }
+    const uint4 T = tri[info[s].index];
     const float* n0 = normals + 3 * (size_t)T.x;
     const float* n1 = normals + 3 * (size_t)T.y;
     const float* n2 = normals + 3 * (size_t)T.z;
@@ -1750,7 +1762,7 @@ __global__ __launch_bounds__(256) void k_tri_shade(const uint4* __restrict__ tri
         r.f = make_float4(t1[1], t1[2], t2[0], t2[1]);
         r.g = make_float4(t2[2], 0, 0, 0);
     }
-    out[t] = r;
+    out[s] = r;
 }
 
 // pt_frame_samples: per-sample radiance of the last fixed-SPP frame at the

@@ -1244,12 +1244,12 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     UP(DS.normals, s->normals, 3 * (size_t)s->n_vertices);
     UP(DS.uvs, s->uvs, 2 * (size_t)s->n_vertices);
     UP(DS.tangents, s->tangents, s->tangents ? 3 * (size_t)s->n_vertices : 0);
-    UP(DS.tshade, (const DevTriShade*)nullptr, s->n_triangles);
+    UP(DS.tshade, (const DevTriShade*)nullptr, s->n_prims);  // per slot (k_tri_shade)
     UP(DS.alpha, alpha.data(), alpha.size());
     UP(DS.amask, amask.data(), amask.size());
     if (s->n_triangles) {
-        hipLaunchKernelGGL(k_tri_shade, dim3((s->n_triangles + 255) / 256), dim3(256), 0, c->stream, DS.tri,
-                           DS.normals, DS.uvs, s->tangents ? DS.tangents : nullptr, s->n_triangles,
+        hipLaunchKernelGGL(k_tri_shade, dim3((s->n_prims + 255) / 256), dim3(256), 0, c->stream, DS.geom, DS.info,
+                           DS.tri, DS.normals, DS.uvs, s->tangents ? DS.tangents : nullptr, s->n_prims,
                            const_cast<DevTriShade*>(DS.tshade));
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1270,6 +1270,28 @@ static pt_status upload_dev(pt_ctx* c, const pt_scene_desc* s) {
     // texels: 16 bytes of padding for the word loads of texel_pair_u8
     if ((st = upload(c, s->texels, s->n_texel_bytes, &DS.texels, 16)) != PT_OK) return st;
     UP(DS.lights, s->lights, s->n_lights);
+    {  // each triangle area light's vertices and uvs (DevLightTri), beside its light record
+        std::vector<DevLightTri> lt(std::max<uint32_t>(s->n_lights, 1));
+        for (uint32_t k = 0; k < s->n_lights; k++) {
+            const pt_light& L = s->lights[k];
+            lt[k] = DevLightTri{};
+            if (L.kind != PT_LIGHT_AREA || !s->uvs) continue;
+            const pt_prim& p = s->prims[L.prim];
+            if (p.kind != PT_PRIM_TRIANGLE) continue;
+            const uint32_t* v = s->tri_vidx + 3 * (size_t)p.index;
+            const float* P0 = s->positions + 3 * (size_t)v[0];
+            const float* P1 = s->positions + 3 * (size_t)v[1];
+            const float* P2 = s->positions + 3 * (size_t)v[2];
+            const float* U0 = s->uvs + 2 * (size_t)v[0];
+            const float* U1 = s->uvs + 2 * (size_t)v[1];
+            const float* U2 = s->uvs + 2 * (size_t)v[2];
+            lt[k].a = make_float4(P0[0], P0[1], P0[2], U0[0]);
+            lt[k].b = make_float4(P1[0], P1[1], P1[2], U1[0]);
+            lt[k].c = make_float4(P2[0], P2[1], P2[2], U2[0]);
+            lt[k].d = make_float4(U0[1], U1[1], U2[1], __builtin_bit_cast(float, 1u));
+        }
+        UP(DS.ltri, lt.data(), lt.size());
+    }
     UP(DS.sampler_lights, s->sampler_lights, s->n_sampler_lights);
     UP(DS.sampler_cdf, cdf.data(), cdf.size());
     {  // guide table (pt_device.h PT_LS_GUIDE): bucket b starts at the first

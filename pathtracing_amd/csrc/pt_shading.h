@@ -292,12 +292,11 @@ __device__ __forceinline__ void sphere_uv(f3 p, float& u, float& v) { sphere_uv_
 // TriangleShape::Intersect shading part (Shape.cpp:206-242) from the hit's
 // barycentrics; identical to computing it at the candidate (the reference does
 // it per candidate, only the last accepted survives).
-__device__ void tri_interaction(const DevGeom& g, uint32_t tri, int mid, f3 o, f3 d, float t,
+__device__ void tri_interaction(const DevGeom& g, const DevTriShade& R, int mid, f3 o, f3 d, float t,
                                 float bu, float bv, SurfInt& si) {
-    // one shading record (DevTriShade) instead of S.tri + the indexed
-    // normals / uvs / tangents: the same values, the same arithmetic
-    const DevTriShade* R = S.tshade + tri;
-    const float4 ra = R->a, rb = R->b, rc = R->c, rd = R->d;
+    // one shading record (DevTriShade, the slot's) instead of S.tri + the
+    // indexed normals / uvs / tangents: the same values, the same arithmetic
+    const float4 ra = R.a, rb = R.b, rc = R.c, rd = R.d;
     float u = bu, v = bv, w = 1.0f - u - v;
     si.u = lerp3f(u, rc.w, v, rd.y, w, rc.y);
     si.v = lerp3f(u, rd.x, v, rd.z, w, rc.z);
@@ -315,7 +314,7 @@ __device__ void tri_interaction(const DevGeom& g, uint32_t tri, int mid, f3 o, f
     si.p = F3(fma_(rmul(PT_EPS, N.x), sg, o.x + rmul(t, d.x)), fma_(rmul(PT_EPS, N.y), sg, o.y + rmul(t, d.y)),
               fma_(rmul(PT_EPS, N.z), sg, fma_(t, d.z, o.z)));
     if (__float_as_uint(rd.w) & 1u) {
-        const float4 re = R->e, rf = R->f, rg = R->g;
+        const float4 re = R.e, rf = R.f, rg = R.g;
         // t0 = (e.x e.y e.z), t1 = (e.w f.x f.y), t2 = (f.z f.w g.x)
         f3 tv = F3(lerp3f(u, re.w, v, rf.z, w, re.x), lerp3f(u, rf.x, v, rf.w, w, re.y),
                    lerp3f(u, rf.y, v, rg.x, w, re.z));
@@ -905,6 +904,21 @@ struct LSample {
 };
 __device__ __forceinline__ uint4 tri_idx(uint32_t tri) { return S.tri[tri]; }
 
+// the triangle parts of Shape::Area / Sample (Shape.cpp:277-315) over the
+// vertices and uvs themselves (shape_area / shape_sample, or a light's
+// DevLightTri: the same values, the same arithmetic)
+__device__ __forceinline__ float tri_area(f3 v0, f3 v1, f3 v2) { return length(cross(v0 - v2, v1 - v2)) * 0.5f; }
+__device__ __forceinline__ void tri_sample(f3 v0, f3 v1, f3 v2, float a0, float a1, float a2, float b0, float b1,
+                                           float b2, float u0, float u1, LSample& ls) {
+    float w = 1.0f - u0 - u1;  // not folded
+    f3 n = normalize(cross(v1 - v0, v2 - v0));
+    if (n.x != n.x) n = F3(0, 0, 0);
+    ls.p = F3(lerp3f(u0, v1.x, u1, v2.x, w, v0.x), lerp3f(u0, v1.y, u1, v2.y, w, v0.y),
+              lerp3f(u0, v1.z, u1, v2.z, w, v0.z));
+    ls.u = lerp3f(u0, a1, u1, a2, w, a0);
+    ls.v = lerp3f(u0, b1, u1, b2, w, b0);
+    ls.n = n;
+}
 __device__ float shape_area(uint32_t kind, uint32_t index) {
     if (kind == PT_PRIM_QUAD) {
         const pt_quad& q = S.quads[index];
@@ -916,7 +930,7 @@ __device__ float shape_area(uint32_t kind, uint32_t index) {
     }
     uint4 T = tri_idx(index);
     f3 v0 = ld3(S.positions + 3 * T.x), v1 = ld3(S.positions + 3 * T.y), v2 = ld3(S.positions + 3 * T.z);
-    return length(cross(v0 - v2, v1 - v2)) * 0.5f;
+    return tri_area(v0, v1, v2);
 }
 // Shape::Sample (Shape.cpp:74-81, 277-297; Shape.hpp:139-141)
 __device__ void shape_sample(uint32_t kind, uint32_t index, float u0, float u1, LSample& ls) {
@@ -939,28 +953,21 @@ __device__ void shape_sample(uint32_t kind, uint32_t index, float u0, float u1, 
         ls.n = normalize(ls.p - c);
         sphere_uv(ls.p, ls.u, ls.v);
     } else {
-        float w = 1.0f - u0 - u1;  // not folded
         uint4 T = tri_idx(index);
         f3 v0 = ld3(S.positions + 3 * T.x), v1 = ld3(S.positions + 3 * T.y), v2 = ld3(S.positions + 3 * T.z);
-        f3 n = normalize(cross(v1 - v0, v2 - v0));
-        if (n.x != n.x) n = F3(0, 0, 0);
-        ls.p = F3(lerp3f(u0, v1.x, u1, v2.x, w, v0.x), lerp3f(u0, v1.y, u1, v2.y, w, v0.y),
-                  lerp3f(u0, v1.z, u1, v2.z, w, v0.z));
         const float* uvs = S.uvs;
-        ls.u = lerp3f(u0, uvs[2 * T.y], u1, uvs[2 * T.z], w, uvs[2 * T.x]);
-        ls.v = lerp3f(u0, uvs[2 * T.y + 1], u1, uvs[2 * T.z + 1], w, uvs[2 * T.x + 1]);
-        ls.n = n;
+        tri_sample(v0, v1, v2, uvs[2 * T.x], uvs[2 * T.y], uvs[2 * T.z], uvs[2 * T.x + 1], uvs[2 * T.y + 1],
+                   uvs[2 * T.z + 1], u0, u1, ls);
     }
 }
 // Shape::PDF(interaction, ray) (Shape.cpp:61-67, 303-315; Shape.hpp:151-158)
 // as built: dot(to, to) in y, x, z order; the quad's (inlined into
 // AreaLight::PDF) light cosine also in y, x, z order except behind the
 // one-sided test, whose dot(-d, n) it reuses
-__device__ float shape_pdf(uint32_t kind, uint32_t index, f3 p, f3 n, f3 ro, f3 rd, bool one_sided) {
+__device__ float shape_pdf_a(uint32_t kind, float area, f3 p, f3 n, f3 ro, f3 rd, bool one_sided) {
     f3 to = p - ro;
     float d2 = dot_yxz(to, to);
     float lc = fabsf(kind == PT_PRIM_QUAD && !one_sided ? dot_yxz(-rd, n) : dot(-rd, n));
-    float area = shape_area(kind, index);
     if (kind == PT_PRIM_QUAD) {
         if (area == 0) return 0;
     } else if (kind == PT_PRIM_SPHERE) {
@@ -969,6 +976,9 @@ __device__ float shape_pdf(uint32_t kind, uint32_t index, f3 p, f3 n, f3 ro, f3 
         if (area == 0 || lc == 0 || n.x != n.x) return 0;
     }
     return d2 / (lc * area);
+}
+__device__ __forceinline__ float shape_pdf(uint32_t kind, uint32_t index, f3 p, f3 n, f3 ro, f3 rd, bool one_sided) {
+    return shape_pdf_a(kind, shape_area(kind, index), p, n, ro, rd, one_sided);
 }
 // TextureInfiniteLight::Le (Light.cpp:110-112): LeScale * tex(GetSphereUV(dir))
 __device__ __noinline__ f3 texinf_le(const pt_light& l, f3 d) {
@@ -1107,9 +1117,16 @@ __device__ __forceinline__ LSample light_sample(const pt_light& l, float u0, flo
     ls.dir = F3(0, 0, 0);
     ls.u = ls.v = 0;
     if (l.kind == PT_LIGHT_AREA) {  // AreaLight::sample (Light.cpp:261-263)
-        const DevPrimInfo& pi = S.info[l.prim];
-        uint32_t kind = __float_as_uint(S.geom[l.prim].a.w) & GF_KIND;
-        shape_sample(kind, pi.index, u0, u1, ls);
+        const DevLightTri* R = S.ltri + (&l - S.lights);  // (l: a reference into S.lights)
+        float4 ra = make_float4(0, 0, 0, 0), rb = ra, rc = ra, rd = ra;
+        if (PT_LIGHT_TRI) ra = R->a, rb = R->b, rc = R->c, rd = R->d;
+        if (PT_LIGHT_TRI && __float_as_uint(rd.w)) {  // a triangle: its vertices and uvs gathered at upload
+            tri_sample(xyz(ra), xyz(rb), xyz(rc), ra.w, rb.w, rc.w, rd.x, rd.y, rd.z, u0, u1, ls);
+        } else {
+            const DevPrimInfo& pi = S.info[l.prim];
+            uint32_t kind = __float_as_uint(S.geom[l.prim].a.w) & GF_KIND;
+            shape_sample(kind, pi.index, u0, u1, ls);
+        }
         if (l.instance >= 0) {
             const PN w = tlight_to_world(l.instance, ls.p, ls.n, time);
             ls.p = w.p;
@@ -1163,8 +1180,10 @@ __device__ __forceinline__ bool light_is_delta(const pt_light& l) {
 // Light::PDF(interaction, ray)
 __device__ __forceinline__ float light_pdf(const pt_light& l, f3 p, f3 n, f3 ro, f3 rd, float time = 0.0f) {
     if (l.kind == PT_LIGHT_AREA) {  // Light.cpp:267-272
-        uint32_t kind = __float_as_uint(S.geom[l.prim].a.w) & GF_KIND;
-        uint32_t index = S.info[l.prim].index;
+        const DevLightTri* R = S.ltri + (&l - S.lights);  // (l: a reference into S.lights)
+        float4 ra = make_float4(0, 0, 0, 0), rb = ra, rc = ra;
+        bool tri = false;
+        if (PT_LIGHT_TRI) ra = R->a, rb = R->b, rc = R->c, tri = __float_as_uint(R->d.w) != 0u;
         if (l.instance >= 0) {
             const TLObj o = tlight_to_object(l.instance, p, n, ro, rd, time);
             p = o.p;
@@ -1172,8 +1191,16 @@ __device__ __forceinline__ float light_pdf(const pt_light& l, f3 p, f3 n, f3 ro,
             ro = o.ro;
             rd = o.rd;
         }
-        if (l.one_sided) return dot(-rd, n) > 0 ? shape_pdf(kind, index, p, n, ro, rd, true) : 0;
-        return shape_pdf(kind, index, p, n, ro, rd, false);
+        uint32_t kind = PT_PRIM_TRIANGLE;
+        float area;
+        if (tri) {
+            area = tri_area(xyz(ra), xyz(rb), xyz(rc));
+        } else {
+            kind = __float_as_uint(S.geom[l.prim].a.w) & GF_KIND;
+            area = shape_area(kind, S.info[l.prim].index);
+        }
+        if (l.one_sided) return dot(-rd, n) > 0 ? shape_pdf_a(kind, area, p, n, ro, rd, true) : 0;
+        return shape_pdf_a(kind, area, p, n, ro, rd, false);
     }
     if (l.kind == PT_LIGHT_UNIFORM_INF || l.kind == PT_LIGHT_SKY_INF) return 1.0f / (4.0f * PT_PI);
     if (l.kind == PT_LIGHT_TEX_INF) return texinf_pdf(l, rd);

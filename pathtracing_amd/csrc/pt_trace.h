@@ -222,7 +222,7 @@ __device__ __forceinline__ bool tri_alpha_rec(const DevAlpha& r, uint32_t slot, 
 // the general path: prim info -> shading record -> material -> texture -> image
 __device__ __forceinline__ bool tri_alpha_general(uint32_t slot, float bu, float bv, f3 o, f3 d) {
     const DevPrimInfo pi = S.info[slot];
-    const DevTriShade* R = S.tshade + pi.index;
+    const DevTriShade* R = S.tshade + slot;
     const float4 rc = R->c, rd = R->d;
     float u = bu, v = bv, w = 1.0f - u - v;
     // the uv TriangleShape::Intersect computes (same contraction as tri_interaction)
