@@ -644,7 +644,7 @@ __global__ void k_light_cases(const float* __restrict__ in, uint32_t n, float* _
     for (int j = 0; j < 18; j++) o[j] = 0.0f;
     // a TextureInfiniteLight's hidden cell draw: a hash of the case
     const float uc = draw(pcg_hash(__float_as_uint(c[0]) ^ pcg_hash(__float_as_uint(c[1]))), 0);
-    const LSample ls = light_sample(l, c[0], c[1], uc);
+    const LSample ls = light_sample(li, c[0], c[1], uc);
     o[0] = ls.L.x; o[1] = ls.L.y; o[2] = ls.L.z;
     o[3] = ls.p.x; o[4] = ls.p.y; o[5] = ls.p.z;
     o[6] = ls.n.x; o[7] = ls.n.y; o[8] = ls.n.z;
@@ -653,7 +653,7 @@ __global__ void k_light_cases(const float* __restrict__ in, uint32_t n, float* _
     if (!is_zero(ls.n)) {
         const f3 ref = F3(c[2], c[3], c[4]);
         const f3 rd = normalize(ls.p - ref);
-        o[14] = light_pdf(l, ls.p, ls.n, ref, rd);
+        o[14] = light_pdf(li, ls.p, ls.n, ref, rd);
         const f3 L = light_L(l, ls.n, ls.u, ls.v, rd);
         o[15] = L.x; o[16] = L.y; o[17] = L.z;
     }
@@ -904,7 +904,7 @@ __device__ __forceinline__ bool sample_ld(const MatTex& mt, const SurfInt& si, f
     const int li = ls_sample(r5);
     if (li < 0) return false;
     const pt_light& l = S.lights[li];
-    const LSample ls = light_sample(l, r2, r3, texinf_uc(key, dim), tm);
+    const LSample ls = light_sample(li, r2, r3, texinf_uc(key, dim), tm);
     f3 ldir;
     float tmax;
     if (is_zero(ls.n)) {
@@ -923,7 +923,7 @@ __device__ __forceinline__ bool sample_ld(const MatTex& mt, const SurfInt& si, f
     if (light_is_delta(l)) {
         c = (ls.L * f) / lpdf;
     } else {
-        lpdf *= light_pdf(l, ls.p, ls.n, si.p, sd, tm);
+        lpdf *= light_pdf(li, ls.p, ls.n, si.p, sd, tm);
         if (lpdf <= 0) return false;
         const float w2 = lpdf * lpdf;
         const float w1 = mat_pdf(mt, rd, si, sd);
@@ -989,7 +989,7 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
                 if (INTEGRATOR == PT_INTEGRATOR_SIMPLE || spec) {
                     out = fma3(Le, att, out);
                 } else if (prev > 0) {
-                    const float lp = al.pmf * light_pdf(al, si.p, si.n, ro, rd, tm), p2 = prev * prev;
+                    const float lp = al.pmf * light_pdf(si.light, si.p, si.n, ro, rd, tm), p2 = prev * prev;
                     const float w = p2 / fma_(lp, lp, p2);
                     out = fma3s(w, Le * att, out);
                 }
@@ -1307,7 +1307,7 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                         if (spec) {
                             out = fma3(att, Le, out);
                         } else if (prev > 0) {
-                            const float lp = al.pmf * light_pdf(al, si.p, si.n, ro, rd, tm), p2 = prev * prev;
+                            const float lp = al.pmf * light_pdf(si.light, si.p, si.n, ro, rd, tm), p2 = prev * prev;
                             const float w = p2 / fma_(lp, lp, p2);
                             out = fma3s(w, att * Le, out);
                         }
@@ -1326,7 +1326,7 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                 const int li = ls_sample(r[5]);
                 if (li >= 0 && S.lights[li].pmf > 0) {
                     const pt_light& l = S.lights[li];
-                    LSample ls = light_sample(l, r[2], r[3], texinf_uc(key, dim), tm);
+                    LSample ls = light_sample(li, r[2], r[3], texinf_uc(key, dim), tm);
                     f3 ldir;
                     float tmax;
                     if (is_zero(ls.n)) {
@@ -1358,7 +1358,7 @@ __global__ __launch_bounds__(256) void k_shade_vol(RenderParams R, PathSoA cur, 
                         if (light_is_delta(l)) {
                             Ll = ls.L;
                         } else {
-                            lpdf *= light_pdf(l, ls.p, ls.n, si.p, sd, tm);
+                            lpdf *= light_pdf(li, ls.p, ls.n, si.p, sd, tm);
                             if (lpdf <= 0) {
                                 ok = false;
                             } else {

@@ -1108,8 +1108,9 @@ __device__ __forceinline__ float inf_pdf(const pt_light& l, f3 rd) {
 }
 
 // time: the ray's (Light::sample(uv, time), Light.hpp:21) -- an AnimatedLight's
-__device__ __forceinline__ LSample light_sample(const pt_light& l, float u0, float u1, float uc = 0.0f,
-                                                float time = 0.0f) {
+// (li: the light's index in S.lights; its DevLightTri is S.ltri[li])
+__device__ __forceinline__ LSample light_sample(int li, float u0, float u1, float uc = 0.0f, float time = 0.0f) {
+    const pt_light& l = S.lights[li];
     LSample ls;
     ls.L = F3(0, 0, 0);
     ls.p = F3(0, 0, 0);
@@ -1117,7 +1118,7 @@ __device__ __forceinline__ LSample light_sample(const pt_light& l, float u0, flo
     ls.dir = F3(0, 0, 0);
     ls.u = ls.v = 0;
     if (l.kind == PT_LIGHT_AREA) {  // AreaLight::sample (Light.cpp:261-263)
-        const DevLightTri* R = S.ltri + (&l - S.lights);  // (l: a reference into S.lights)
+        const DevLightTri* R = S.ltri + li;
         float4 ra = make_float4(0, 0, 0, 0), rb = ra, rc = ra, rd = ra;
         if (PT_LIGHT_TRI) ra = R->a, rb = R->b, rc = R->c, rd = R->d;
         if (PT_LIGHT_TRI && __float_as_uint(rd.w)) {  // a triangle: its vertices and uvs gathered at upload
@@ -1178,9 +1179,10 @@ __device__ __forceinline__ bool light_is_delta(const pt_light& l) {
     return l.kind == PT_LIGHT_DISTANT || l.kind == PT_LIGHT_POINT;
 }
 // Light::PDF(interaction, ray)
-__device__ __forceinline__ float light_pdf(const pt_light& l, f3 p, f3 n, f3 ro, f3 rd, float time = 0.0f) {
+__device__ __forceinline__ float light_pdf(int li, f3 p, f3 n, f3 ro, f3 rd, float time = 0.0f) {
+    const pt_light& l = S.lights[li];
     if (l.kind == PT_LIGHT_AREA) {  // Light.cpp:267-272
-        const DevLightTri* R = S.ltri + (&l - S.lights);  // (l: a reference into S.lights)
+        const DevLightTri* R = S.ltri + li;
         float4 ra = make_float4(0, 0, 0, 0), rb = ra, rc = ra;
         bool tri = false;
         if (PT_LIGHT_TRI) ra = R->a, rb = R->b, rc = R->c, tri = __float_as_uint(R->d.w) != 0u;
