@@ -210,3 +210,32 @@ def test_masks_are_deterministic_and_memoised_identically():
     a = coverage(leaf_scene(seed=9))[1]
     b = coverage(leaf_scene(seed=9))[1]
     assert np.array_equal(a, b)
+
+
+def alpha_tex_scene(scale, cutoff, mode=AlphaMode.Mask, size=48, seed=11):
+    """Cards whose alpha is a separate one-channel texture with a colorScale
+    (Evaluate(uv).x * colorScale.x, the CH1 source), random uvs per card."""
+    rng = np.random.default_rng(seed)
+    setup = scenes.cornell(W=16, H=16, spp=1, config="c3", max_depth=2, seed=seed)
+    a = scenes._noise_img(rng, size, size, 1, 0, 255, smooth=12)
+    a = np.where(a > 140, 255, np.where(a < 110, 0, a)).astype(np.uint8)  # large flat regions
+    alpha = ImageTexture(a, colorScale=(scale, 1, 1))
+    m = MicrofacetDiffuse(SolidColor((0.3, 0.6, 0.2)), None, None, None, alpha)
+    m.setAlphaTester(AlphaTester(mode, cutoff))
+    idx, v, _, nr, uv = scenes._leaf_cards(rng, (0.0, 0.0, 0.0), 0.8, 40, 0.15)
+    uv = uv * rng.uniform(0.3, 2.5, (uv.shape[0], 1)).astype(np.float32) + rng.uniform(-2, 2, (1, 2)).astype(
+        np.float32)
+    setup.scene.Add(Model([Mesh(idx, v, None, nr, uv.astype(np.float32), m)]))
+    return setup.finish()
+
+
+@pytest.mark.parametrize("scale,cutoff", [(1.25, 0.5), (-0.8, -0.3), (0.7, 0.0)])
+def test_scaled_alpha_texture_masks_hold(scale, cutoff):
+    """The CH1 source with positive and negative colorScale: the value range
+    is scaled (and flipped) before the cutoff decision."""
+    _, masks, frac = check_scene(alpha_tex_scene(scale, cutoff), np.random.default_rng(5))
+    assert frac is not None and frac > 0.05  # the flat regions decide cells
+
+
+def test_blend_scaled_alpha_texture_masks_hold():
+    check_scene(alpha_tex_scene(1.0, 0.5, mode=AlphaMode.Blend), np.random.default_rng(6))
