@@ -120,6 +120,17 @@ bool PtAlphaCoverage::footprint(const Pyramid& P, const double px[3], const doub
     if (!(std::fabs(ylo) < MAX_COORD && std::fabs(yhi) < MAX_COORD && std::fabs(xlo) < MAX_COORD &&
           std::fabs(xhi) < MAX_COORD))
         return false;
+    // a footprint spanning a whole axis of the image: its bounding rectangle
+    // (every row or every column, wrapped) -- conservative, and bounded work
+    // for triangles whose uvs tile the image many times
+    if (yhi - ylo + 2.0 >= (double)P.H || xhi - xlo + 2.0 >= (double)P.W) {
+        int rx[2][2], ry[2][2];
+        const int nx = wrap_ranges((int64_t)std::floor(xlo), (int64_t)std::floor(xhi) + 1, P.W, rx);
+        const int ny = wrap_ranges((int64_t)std::floor(ylo), (int64_t)std::floor(yhi) + 1, P.H, ry);
+        for (int a = 0; a < nx; a++)
+            for (int b = 0; b < ny; b++) lookups_ += P.query(rx[a][0], rx[a][1], ry[b][0], ry[b][1], blo, bhi);
+        return true;
+    }
     // band height: ~16 bands over the triangle, a power of two
     int s = 1;
     while (s < 64 && (double)(2 * s) * 16.0 <= yhi - ylo) s *= 2;

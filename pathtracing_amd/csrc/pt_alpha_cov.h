@@ -32,6 +32,7 @@ struct PtAlphaRecord {
     uint32_t mode;        // PT_ALPHA_OPAQUE / BLEND / MASK
     float cut, scale, constant;
 };
+static_assert(sizeof(PtAlphaRecord) == 64, "no padding: the coverage memo keys on the bytes");
 
 // A mask set (the upload's word array words()): accept mask then reject
 // mask over the n x n cells (cell c: bit c & 31 of word c >> 5), each
