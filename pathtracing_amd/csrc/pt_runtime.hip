@@ -1515,9 +1515,10 @@ static double gauss_h(double x, double sigma) {
 #endif
 // r04 (alpha records, tail kernel): 128 M 1655 -> 256 M 1671 -> 384 M 1673
 // -> 512 M 1678 Mrays/s (≈ 150 GB of HBM with the sample chunk; 64 M 1619;
-// profiles/r04_ab_traversal.txt); a device short of memory halves it
+// profiles/r04_ab_traversal.txt); r06: 768 M 2145.4 vs 512 M 2136.3
+// (≈ 210 GB; profiles/r06_ab_misc.txt).  A device short of memory halves it
 #ifndef PT_PATHS_POOL
-#define PT_PATHS_POOL (1u << 29)
+#define PT_PATHS_POOL (3u << 28)
 #endif
 #ifndef PT_PATHS_SIMPLE
 #define PT_PATHS_SIMPLE (1u << 21)
