@@ -139,8 +139,15 @@ __device__ __forceinline__ uint32_t hit_slot(int prim) {
     }
     return slot;
 }
+// mt (PT_MT_EARLY): the hit material's textures (mat_tex), evaluated next to
+// the normal map's texture -- both need only the hit's uv -- so their reads
+// overlap; the same values as mat_tex after hit_surface (C4 shade -2.3 %,
+// +0.4 %; profiles/r06_ab_shade_chain.txt)
+#ifndef PT_MT_EARLY
+#define PT_MT_EARLY 1
+#endif
 __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, float b1, float b2, SurfInt& si,
-                                         int& medium, float time = 0.0f) {
+                                         int& medium, float time = 0.0f, MatTex* mt = nullptr) {
     float len = 1.0f;
     const DevInstance* I = nullptr;
     bool xf = false;  // the hit's levels go out of line (an AnimatedPrimitive, nested wrappers)
@@ -180,9 +187,17 @@ __device__ __forceinline__ void hit_surface(int prim, f3 ro, f3 rd, float t, flo
             sphere_root(S.spheres[pi.index], ro, rd, __int_as_float(0x7f800000), t);
         }
     }
-    if (kind == PT_PRIM_TRIANGLE) tri_interaction(g, R, pi.material, ro, rd, t, b1, b2, si);
-    else if (kind == PT_PRIM_QUAD) quad_interaction(S.quads[pi.index], ro, rd, t, b1, b2, si);
-    else sphere_interaction(S.spheres[pi.index], ro, rd, t, si);
+    if (kind == PT_PRIM_TRIANGLE) {
+        tri_interaction(g, R, pi.material, ro, rd, t, b1, b2, si, !mt);
+        if (mt) {  // the textures and the normal map's texture side by side
+            if (pi.material >= 0) *mt = mat_tex(pi.material, si);
+            si.ns = normal_map(pi.material, si);
+        }
+    } else {
+        if (kind == PT_PRIM_QUAD) quad_interaction(S.quads[pi.index], ro, rd, t, b1, b2, si);
+        else sphere_interaction(S.spheres[pi.index], ro, rd, t, si);
+        if (mt && pi.material >= 0) *mt = mat_tex(pi.material, si);
+    }
     si.mat = pi.material;
     si.light = pi.light;
     medium = pi.medium;
@@ -980,7 +995,8 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
         }
         SurfInt si;
         int smed;
-        hit_surface(prim, ro, rd, h.x, h.y, h.z, si, smed, tm);
+        MatTex mte;
+        hit_surface(prim, ro, rd, h.x, h.y, h.z, si, smed, tm, PT_MT_EARLY ? &mte : nullptr);
         // emission (Integrators.cpp:151-154, 217-226)
         if (si.light >= 0) {
             const pt_light& al = S.lights[si.light];
@@ -1001,7 +1017,7 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
             ro = at_f(ro, rd, si.t);
         } else {
             const float us = INTEGRATOR == PT_INTEGRATOR_PATH ? r[4] : r[2];
-            const MatTex mt = mat_tex(si.mat, si);  // the hit's textures, read once
+            const MatTex mt = PT_MT_EARLY ? mte : mat_tex(si.mat, si);  // the hit's textures, read once
             const Bxdf b = mat_scatter(mt, ro, rd, si, us, r[0], r[1]);
             if (!b.ok) {
                 alive = false;  // absorbed

@@ -293,7 +293,7 @@ __device__ __forceinline__ void sphere_uv(f3 p, float& u, float& v) { sphere_uv_
 // barycentrics; identical to computing it at the candidate (the reference does
 // it per candidate, only the last accepted survives).
 __device__ void tri_interaction(const DevGeom& g, const DevTriShade& R, int mid, f3 o, f3 d, float t,
-                                float bu, float bv, SurfInt& si) {
+                                float bu, float bv, SurfInt& si, bool nm = true) {
     // one shading record (DevTriShade, the slot's) instead of S.tri + the
     // indexed normals / uvs / tangents: the same values, the same arithmetic
     const float4 ra = R.a, rb = R.b, rc = R.c, rd = R.d;
@@ -324,7 +324,7 @@ __device__ void tri_interaction(const DevGeom& g, const DevTriShade& R, int mid,
         f3 up = (fabsf(si.ns.x) > 0.9999f) ? F3(0, 1, 0) : F3(1, 0, 0);
         si.tangent = normalize(cross(up, si.ns));
     }
-    si.ns = normal_map(mid, si);
+    if (nm) si.ns = normal_map(mid, si);
 }
 
 // QuadShape::Intersect (Shape.cpp:320-343) interaction part.
