@@ -914,9 +914,9 @@ __global__ __launch_bounds__(256) void k_fill(RenderParams R, uint32_t n, PathSo
 // with the hit's textures mt: the light pick (r5), its sample (r2, r3), the
 // BSDF value and MIS weight -> the shadow record (occlusion deferred).  False
 // when it contributes nothing.  dim: the bounce's dimension after its 8 draws.
+// li: the light LightSampler::Sample(r5) picked (ls_sample)
 __device__ __forceinline__ bool sample_ld(const MatTex& mt, const SurfInt& si, f3 rd, f3 att, float r2, float r3,
-                                          float r5, uint32_t key, uint32_t dim, float tm, ShadowRec& srec) {
-    const int li = ls_sample(r5);
+                                          int li, uint32_t key, uint32_t dim, float tm, ShadowRec& srec) {
     if (li < 0) return false;
     const pt_light& l = S.lights[li];
     const LSample ls = light_sample(li, r2, r3, texinf_uc(key, dim), tm);
@@ -1028,7 +1028,10 @@ __device__ __forceinline__ void shade_bounce(const RenderParams& R, float4 h, ui
                         // PathIntegrator::SampleLd (Integrators.cpp:260-294); occlusion
                         // deferred.  A split bounce (NEE false) leaves it to
                         // k_shade_nee: `shadow` then marks a NEE job.
-                        if (NEE) shadow = sample_ld(mt, si, rd, att, r[2], r[3], r[5], key, dim, tm, srec);
+                        // (the light pick drawn at the start of the bounce instead, so
+                        // its reads overlap the interaction's: -1.4 %, 12 spilled
+                        // VGPRs; profiles/r06_ab_shade_chain.txt)
+                        if (NEE) shadow = sample_ld(mt, si, rd, att, r[2], r[3], ls_sample(r[5]), key, dim, tm, srec);
                         else shadow = true;
                         prev = mat_pdf(mt, rd, si, b.d);
                     }
@@ -1156,8 +1159,8 @@ void k_shade_nee(RenderParams R, PathSoA cur, const uint32_t* __restrict__ nptr,
         int smed;
         hit_surface(__float_as_int(h.w), ro, rd, h.x, h.y, h.z, si, smed, tm);
         const MatTex mt = mat_tex(si.mat, si);
-        shadow = sample_ld(mt, si, rd, xyz(b4), draw(key, dim0 + 2), draw(key, dim0 + 3), draw(key, dim0 + 5), key,
-                           dim0 + 8, tm, srec);
+        shadow = sample_ld(mt, si, rd, xyz(b4), draw(key, dim0 + 2), draw(key, dim0 + 3), ls_sample(draw(key, dim0 + 5)),
+                           key, dim0 + 8, tm, srec);
         srec.d.w = __uint_as_float(job.y);
     }
     uint32_t c[1];
