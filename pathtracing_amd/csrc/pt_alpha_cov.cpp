@@ -244,9 +244,14 @@ uint32_t PtAlphaCoverage::set(const PtAlphaRecord& rec) {
     if (any) {
         int ln = 0;
         while ((4 << ln) < n) ln++;
+        if (il_ && (words_.size() & 1)) words_.push_back(0);  // 8-B aligned pairs
         out = (uint32_t)words_.size() | (uint32_t)ln << 29;
-        words_.insert(words_.end(), acc.begin(), acc.end());
-        words_.insert(words_.end(), rej.begin(), rej.end());
+        if (il_) {
+            for (uint32_t k = 0; k < wpm; k++) words_.push_back(acc[k]), words_.push_back(rej[k]);
+        } else {
+            words_.insert(words_.end(), acc.begin(), acc.end());
+            words_.insert(words_.end(), rej.begin(), rej.end());
+        }
     }
     memo_.emplace(std::move(key), out);
     return out;

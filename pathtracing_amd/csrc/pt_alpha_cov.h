@@ -34,9 +34,11 @@ struct PtAlphaRecord {
 };
 static_assert(sizeof(PtAlphaRecord) == 64, "no padding: the coverage memo keys on the bytes");
 
-// A mask set (the upload's word array words()): accept mask then reject
-// mask over the n x n cells (cell c: bit c & 31 of word c >> 5), each
-// max(1, n n / 32) words.  Its handle = word offset | log2(n / 4) << 29;
+// A mask set (the upload's word array words()): an accept and a reject mask
+// over the n x n cells (cell c: bit c & 31 of word c >> 5), each max(1, n n /
+// 32) words, stored either one after the other or interleaved (accept word k,
+// reject word k, ...; 8-B aligned: one 64-bit read gives a cell's two bits).
+// Its handle = word offset | log2(n / 4) << 29;
 // PT_ALPHA_SET_NONE: no cell decided (or no set computed).
 #define PT_ALPHA_SET_NONE 0xFFFFFFFFu
 // square-table lookups the masks of one upload may spend (host time); the
@@ -46,8 +48,8 @@ static_assert(sizeof(PtAlphaRecord) == 64, "no padding: the coverage memo keys o
 class PtAlphaCoverage {
 public:
     // max_n: the finest subdivision (a power of two, 4 .. 256)
-    PtAlphaCoverage(const uint8_t* texels, uint64_t n_texel_bytes, int max_n = 128)
-        : texels_(texels), n_(n_texel_bytes), max_n_(max_n) {}
+    PtAlphaCoverage(const uint8_t* texels, uint64_t n_texel_bytes, int max_n = 128, bool interleave = false)
+        : texels_(texels), n_(n_texel_bytes), max_n_(max_n), il_(interleave) {}
     // the mask set of a record (n from the triangle's texel extent: cells of
     // ~8 texels, 4 .. max_n per side); identical records share one set
     uint32_t set(const PtAlphaRecord& r);
@@ -67,6 +69,7 @@ private:
     const uint8_t* texels_;
     uint64_t n_;
     int max_n_;
+    bool il_;
     std::map<std::tuple<uint64_t, uint32_t, uint32_t, uint32_t, uint32_t>, std::unique_ptr<Pyramid>> pyr_;
     std::unordered_map<std::string, uint32_t> memo_;  // identical records (leaf cards share uvs)
     std::vector<uint32_t> words_;

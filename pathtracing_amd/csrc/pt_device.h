@@ -122,6 +122,9 @@ static_assert(sizeof(DevAlpha) == 48, "alpha record layout");
 #define PT_ALPHA_COV 1
 #endif
 #define PT_ALPHA_SET_NONE 0xFFFFFFFFu
+#ifndef PT_ALPHA_IL  // mask words interleaved (accept, reject) per 32 cells (pt_alpha_cov.h): +0.5 %, r06
+#define PT_ALPHA_IL 1
+#endif
 __device__ __forceinline__ uint32_t alpha_index(uint32_t w0, uint32_t w1) {
     return ((w0 >> 5) & 0x7FFu) << 16 | (w1 & 0xFFFFu);
 }

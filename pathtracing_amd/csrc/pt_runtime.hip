@@ -744,7 +744,7 @@ static void alpha_records(const pt_scene_desc* s, std::vector<DevGeom>& geom, st
 #ifndef PT_ALPHA_MAXN  // the finest coverage subdivision (pt_alpha_cov.h)
 #define PT_ALPHA_MAXN 128
 #endif
-    PtAlphaCoverage cov(s->texels, s->texels ? s->n_texel_bytes : 0, PT_ALPHA_MAXN);
+    PtAlphaCoverage cov(s->texels, s->texels ? s->n_texel_bytes : 0, PT_ALPHA_MAXN, PT_ALPHA_IL != 0);
     uint32_t n = 0;
     for (uint32_t i = 0; i < s->n_prims; i++) {
         uint32_t* h = hook ? hook + (size_t)PT_ALPHA_HOOK_WORDS * i : nullptr;
@@ -761,8 +761,10 @@ static void alpha_records(const pt_scene_desc* s, std::vector<DevGeom>& geom, st
             const int cn = 4 << (set >> 29), wpm = std::max(1, cn * cn / 32);
             const uint32_t* w = cov.words().data() + (set & 0x1FFFFFFFu);
             h[0] = set;
-            std::copy(w, w + std::min(wpm, 512), h + 1);  // (the hook's rows hold n <= 128)
-            std::copy(w + wpm, w + wpm + std::min(wpm, 512), h + 513);
+            for (int k = 0; k < std::min(wpm, 512); k++) {  // (the hook's rows hold n <= 128)
+                h[1 + k] = PT_ALPHA_IL ? w[2 * k] : w[k];
+                h[513 + k] = PT_ALPHA_IL ? w[2 * k + 1] : w[wpm + k];
+            }
         }
         if (fast && alpha) alpha->push_back(r);
     }

@@ -157,8 +157,14 @@ bool tri_alpha(uint32_t ai, uint32_t set, uint32_t slot, float bu, float bv, f3 
             // decided cell answers without the texel reads
             const int n = 4 << (set >> 29);
             const uint32_t c = alpha_cell(bu, bv, n);
-            const uint32_t* m = S.amask + (set & 0x1FFFFFFFu) + (c >> 5);
-            const uint32_t acc = m[0], rej = m[max(1, (n * n) >> 5)];
+            uint32_t acc, rej;
+            if (PT_ALPHA_IL) {  // the cell's accept and reject words side by side: one 8-B read
+                const uint2 w = *reinterpret_cast<const uint2*>(S.amask + (set & 0x1FFFFFFFu) + 2u * (c >> 5));
+                acc = w.x, rej = w.y;
+            } else {
+                const uint32_t* m = S.amask + (set & 0x1FFFFFFFu) + (c >> 5);
+                acc = m[0], rej = m[max(1, (n * n) >> 5)];
+            }
             if ((acc >> (c & 31)) & 1u) return true;
             if ((rej >> (c & 31)) & 1u) return false;
         }
